@@ -1,0 +1,233 @@
+/*
+ * qf_fec.h -- C ABI of the MI355X-native GF(2^8) RLNC FEC library
+ *             (libqf_fec.so, hand-written HIP kernels for gfx950).
+ *
+ * This is the drop-in boundary for QuicFuscate's src/fec hot path.  Every
+ * entry point names the reference interface it replaces (paths relative to
+ * the reference repository, Christopher-Schulze/QuicFuscate @ 2025-07-18).
+ * INTEGRATION.md shows the Rust FFI a maintainer would add on the reference
+ * side.
+ *
+ * Conventions
+ *  - All functions return int status: QF_OK (0) or a negative QF_E* code.
+ *    Nothing panics or aborts; the reference's panics (gf_inv(0), k + r > 256)
+ *    become QF_ERANGE.
+ *  - Buffers are caller-owned.  The library never frees or zeroes caller
+ *    memory.  "_dev" pointers are device (HBM) pointers; "_host" pointers are
+ *    host memory (pinned for full PCIe rate).
+ *  - Work is enqueued asynchronously on the context's stream; qf_sync()
+ *    waits.  One context per host thread; distinct contexts are independent.
+ *  - Arithmetic is GF(2^8) with polynomial 0x11D and generator 2, table
+ *    semantics (gf_tables.rs:47-57, 384-408).
+ */
+#ifndef QF_FEC_H
+#define QF_FEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QF_OK 0
+#define QF_EINVAL (-1)     /* bad argument / shape                               */
+#define QF_ERANGE (-2)     /* gf_inv(0): k + r > 256, Cauchy undefined (F5)      */
+#define QF_ENOTREADY (-3)  /* window not full / fewer than k rows received       */
+#define QF_ERANK (-4)      /* decode matrix singular                             */
+#define QF_EDEVICE (-5)    /* HIP runtime error                                  */
+#define QF_ENOMEM (-6)     /* allocation failed                                  */
+#define QF_ETOOSMALL (-7)  /* output buffer too short (quiche BufferTooShort)    */
+
+#define QF_ABI_VERSION 1
+int qf_abi_version(void);
+const char *qf_strerror(int status);
+
+/* ---------------------------------------------------------------------------
+ * GF(2^8) scalar helpers (host).  These mirror the reference's public GF API
+ * for callers and parity tests; the hot path never calls them.
+ * ------------------------------------------------------------------------- */
+/* replaces gf_tables.rs:392 init_gf_tables (idempotent) */
+int qf_gf256_init(void);
+/* replaces gf_tables.rs:283 gf_mul and :47 gf_mul_table (same result) */
+uint8_t qf_gf256_mul(uint8_t a, uint8_t b);
+/* replaces gf_tables.rs:327 gf_mul_add: a*b ^ c */
+uint8_t qf_gf256_mul_add(uint8_t a, uint8_t b, uint8_t c);
+/* replaces gf_tables.rs:304 gf_inv / :312 gf_inv_prefetch; QF_ERANGE for 0 */
+int qf_gf256_inv(uint8_t a, uint8_t *out);
+/* replaces decoder.rs:280-298 Encoder::generate_cauchy_coefficients for
+ * repairs 0..r-1: out[j*k + i] = inv((u8)i ^ (u8)(k + j)).  QF_ERANGE where
+ * the reference panics (k + r > 256). */
+int qf_cauchy_coeffs(uint32_t k, uint32_t r, uint8_t *out_rxk);
+
+/* ---------------------------------------------------------------------------
+ * Context
+ * ------------------------------------------------------------------------- */
+typedef struct qf_ctx qf_ctx;
+/* device: HIP device ordinal.  stream: hipStream_t to enqueue on (NULL = the
+ * context creates its own non-blocking stream). */
+int qf_ctx_create(int device, void *stream, qf_ctx **out);
+int qf_ctx_destroy(qf_ctx *ctx);
+int qf_ctx_set_stream(qf_ctx *ctx, void *stream);
+void *qf_ctx_stream(qf_ctx *ctx);
+int qf_sync(qf_ctx *ctx);
+
+/* ---------------------------------------------------------------------------
+ * Element-wise slice multiply on the device.
+ * replaces gf_tables.rs:255-274 gf_mul_slice (benches/gf_mul_slice_bench.rs)
+ * out[i] = a[i] * b[i] for i < n (device pointers).
+ * ------------------------------------------------------------------------- */
+int qf_gf256_mul_slice_dev(qf_ctx *ctx, const uint8_t *a_dev, const uint8_t *b_dev,
+                           uint8_t *out_dev, size_t n);
+
+/* ---------------------------------------------------------------------------
+ * Batched block encode (device resident).
+ * replaces decoder.rs:172-275 Encoder::generate_repair_packet, for r repairs
+ * of G independent generations in one launch:
+ *   rep[g][j][t] = XOR_{i<k} C[j][i] * src[g][i][t]      (t < L, j < r)
+ * Row i of generation g starts at src_dev + g*src_gen_stride + i*src_row_stride;
+ * repair j at rep_dev + g*rep_gen_stride + j*rep_row_stride.  Exactly L bytes
+ * per repair row are written.  coeff_rxk (host, r*k bytes, row-major) or NULL
+ * for the reference's Cauchy matrix (decoder.rs:280-298).
+ * Sliding windows (adaptive.rs:519-562, one window per source packet) are the
+ * special case src_gen_stride == src_row_stride.
+ * Fast path: src/rep pointers and strides 16-byte aligned (any L).
+ * ------------------------------------------------------------------------- */
+typedef struct qf_encode_shape {
+    uint32_t k;              /* generation (window) size, 1..255 */
+    uint32_t r;              /* repairs per generation, k + r <= 256 for Cauchy */
+    uint32_t L;              /* payload bytes per packet */
+    uint32_t reserved;
+    uint64_t src_row_stride;
+    uint64_t src_gen_stride;
+    uint64_t rep_row_stride;
+    uint64_t rep_gen_stride;
+} qf_encode_shape;
+
+int qf_encode_batch(qf_ctx *ctx, const qf_encode_shape *shape, uint32_t G,
+                    const uint8_t *src_dev, uint8_t *rep_dev, const uint8_t *coeff_rxk);
+
+/* Same, host-resident src/rep (pinned memory recommended).  Chunks of
+ * generations are streamed H2D -> encode -> D2H on several HIP streams with
+ * device staging owned by the context.  Synchronous on return. */
+int qf_encode_batch_host(qf_ctx *ctx, const qf_encode_shape *shape, uint32_t G,
+                         const uint8_t *src_host, uint8_t *rep_host,
+                         const uint8_t *coeff_rxk);
+
+/* ---------------------------------------------------------------------------
+ * Batched decode (device resident).
+ * replaces decoder.rs:658-791 Decoder::{add_packet, try_decode,
+ * gaussian_elimination, get_decoded_packets} for G independent generations:
+ *  - rows: the received packets of generation g in arrival order,
+ *    rows_dev + g*rows_gen_stride + slot*row_stride, slot < n_rows[g]
+ *  - row_index_dev[g*max_rows + slot]: < k = systematic source index
+ *    (the reference's id % k, decoder.rs:684); >= k = repair j = value - k
+ *  - row_coeffs_dev: NULL (repair coefficients are the Cauchy row of j) or
+ *    k coefficient bytes per slot at row_coeffs_dev + (g*max_rows + slot)*k
+ *    (the packet's coefficient block, decoder.rs:694-696)
+ *  - n_rows_dev: per-generation slot count, or NULL (= max_rows)
+ * Acceptance follows decoder.rs:678-701: the first k rows win, duplicate
+ * systematic rows are ignored.  For each generation the erased source rows
+ * are recovered (ascending source index) into
+ *   rec_dev + g*rec_gen_stride + m*rec_row_stride,  m < n_rec[g] <= min(k, r)
+ * with rec_index_dev[g*min(k,r) + m] = source index of recovered row m and
+ * status_dev[g] = QF_OK / QF_ENOTREADY / QF_ERANK / QF_ERANGE / QF_EINVAL.
+ * Received systematic rows are not copied (they are already the payload).
+ * Deviation from the reference: systematic rows carry their
+ * payloads, so the recovered bytes are the original bytes.
+ * ------------------------------------------------------------------------- */
+typedef struct qf_decode_shape {
+    uint32_t k;
+    uint32_t r;              /* max repairs that may arrive (bounds n_rec) */
+    uint32_t L;
+    uint32_t max_rows;       /* slots per generation in row_index / rows   */
+    uint64_t row_stride;
+    uint64_t rows_gen_stride;
+    uint64_t rec_row_stride;
+    uint64_t rec_gen_stride;
+} qf_decode_shape;
+
+int qf_decode_batch(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G,
+                    const uint8_t *rows_dev, const uint16_t *row_index_dev,
+                    const uint32_t *n_rows_dev, const uint8_t *row_coeffs_dev,
+                    uint8_t *rec_dev, uint16_t *rec_index_dev, uint32_t *n_rec_dev,
+                    int32_t *status_dev);
+
+/* ---------------------------------------------------------------------------
+ * Per-connection objects mirroring the reference's Rust API one call at a
+ * time (what core.rs drives).  Payload state lives in HBM.
+ * ------------------------------------------------------------------------- */
+typedef struct qf_encoder qf_encoder;
+/* replaces decoder.rs:156 Encoder::new(k, n); max_len bounds packet length */
+int qf_encoder_new(qf_ctx *ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_encoder **out);
+int qf_encoder_free(qf_encoder *enc);
+/* replaces decoder.rs:164 Encoder::add_source_packet (slides the window) */
+int qf_encoder_add_source_packet(qf_encoder *enc, uint64_t id, const uint8_t *data,
+                                 uint32_t len);
+/* replaces decoder.rs:172 Encoder::generate_repair_packet(j).  QF_ENOTREADY
+ * while the window holds fewer than k packets (the reference's None).
+ * out_data receives len = window[0].len bytes, out_coeffs k bytes,
+ * *out_id = last.id + 1 + j. */
+int qf_encoder_generate_repair_packet(qf_encoder *enc, uint32_t repair_index,
+                                      uint8_t *out_data, uint32_t out_cap,
+                                      uint32_t *out_len, uint8_t *out_coeffs,
+                                      uint64_t *out_id);
+/* All repairs first..first+count-1 of the current window in one launch
+ * (adaptive.rs:546-562 emit_repairs). out_data rows are out_stride apart. */
+int qf_encoder_generate_repairs(qf_encoder *enc, uint32_t first, uint32_t count,
+                                uint8_t *out_data, uint32_t out_stride, uint32_t *out_len,
+                                uint8_t *out_coeffs, uint64_t *out_ids);
+int qf_encoder_window_len(const qf_encoder *enc);
+
+typedef struct qf_decoder qf_decoder;
+/* replaces decoder.rs:659 Decoder::new(k, pool) */
+int qf_decoder_new(qf_ctx *ctx, uint32_t k, uint32_t max_len, qf_decoder **out);
+int qf_decoder_free(qf_decoder *dec);
+/* replaces decoder.rs:678 Decoder::add_packet.  Returns 1 when the generation
+ * is decoded, 0 when more packets are needed, QF_EINVAL for a repair packet
+ * without coefficients ("Repair packet missing coefficients.").  A singular
+ * matrix leaves the decoder undecoded, as in the reference. */
+int qf_decoder_add_packet(qf_decoder *dec, uint64_t id, int is_systematic,
+                          const uint8_t *data, uint32_t len, const uint8_t *coeffs,
+                          uint32_t coeff_len);
+/* replaces the decoder.rs:532 field is_decoded */
+int qf_decoder_is_decoded(const qf_decoder *dec);
+/* replaces decoder.rs:785 get_decoded_packets: drains the k source packets in
+ * index order.  out_data holds k rows of out_stride bytes; out_len[i] and
+ * out_ids[i] describe row i; *count = number of packets returned (k, or 0 if
+ * not decoded or already drained). */
+int qf_decoder_get_decoded_packets(qf_decoder *dec, uint8_t *out_data, uint32_t out_stride,
+                                   uint32_t *out_len, uint64_t *out_ids, uint32_t *count);
+
+/* ---------------------------------------------------------------------------
+ * Wire framing, byte-compatible with encoder.rs:124-152 (to_raw) and
+ * encoder.rs:18-68 (from_raw): [u8 sys(1/0)] [u16 BE coeff_len][coeffs] payload
+ * (the coefficient header is present only when coeffs != NULL).
+ * ------------------------------------------------------------------------- */
+int qf_packet_to_raw(int is_systematic, const uint8_t *coeffs, uint32_t coeff_len,
+                     const uint8_t *payload, uint32_t len, uint8_t *out, uint32_t out_cap,
+                     uint32_t *out_len);
+/* Parses a frame; pointers returned point into raw.  coeffs is NULL for
+ * systematic frames. */
+int qf_packet_from_raw(const uint8_t *raw, uint32_t raw_len, int *is_systematic,
+                       const uint8_t **coeffs, uint32_t *coeff_len,
+                       const uint8_t **payload, uint32_t *len);
+
+/* ---------------------------------------------------------------------------
+ * Synthetic payload (bench / tests): byte t of the region is byte (t & 7) of
+ * splitmix64(seed + word_offset + t/8), little endian.  Device kernel.
+ * ------------------------------------------------------------------------- */
+int qf_fill_splitmix_dev(qf_ctx *ctx, uint8_t *dst_dev, size_t n, uint64_t seed,
+                         uint64_t word_offset);
+
+/* ---------------------------------------------------------------------------
+ * Host self-test of the split-index v_perm tables the kernels use: checks
+ * T0[x&7]^T1[x>>3&7]^T2[x>>6] == gf_mul_table(c, x) for all 65,536 (c, x)
+ * with a host emulation of v_perm_b32.  Returns QF_OK or QF_EINVAL.
+ * ------------------------------------------------------------------------- */
+int qf_selftest_split_tables(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QF_FEC_H */

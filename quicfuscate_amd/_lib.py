@@ -1,0 +1,125 @@
+"""ctypes binding of libqf_fec.so (the C ABI declared in include/qf_fec.h).
+
+The product path has no fallback: if the library is missing this raises.
+torch is imported first so that the process holds one HIP runtime (the
+library is linked against the runtime bundled with torch).
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "lib" / "libqf_fec.so"
+HEADER = PKG.parent / "include" / "qf_fec.h"
+
+QF_OK = 0
+QF_EINVAL = -1
+QF_ERANGE = -2
+QF_ENOTREADY = -3
+QF_ERANK = -4
+QF_EDEVICE = -5
+QF_ENOMEM = -6
+QF_ETOOSMALL = -7
+
+_P = ctypes.c_void_p
+_U8 = ctypes.c_uint8
+_U16 = ctypes.c_uint16
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+_SZ = ctypes.c_size_t
+
+
+class QfError(RuntimeError):
+    """A negative status returned by libqf_fec."""
+
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = _lib().qf_strerror(status).decode() if _LIB is not None else str(status)
+        super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
+
+
+class EncodeShape(ctypes.Structure):
+    _fields_ = [
+        ("k", _U32), ("r", _U32), ("L", _U32), ("reserved", _U32),
+        ("src_row_stride", _U64), ("src_gen_stride", _U64),
+        ("rep_row_stride", _U64), ("rep_gen_stride", _U64),
+    ]
+
+
+class DecodeShape(ctypes.Structure):
+    _fields_ = [
+        ("k", _U32), ("r", _U32), ("L", _U32), ("max_rows", _U32),
+        ("row_stride", _U64), ("rows_gen_stride", _U64),
+        ("rec_row_stride", _U64), ("rec_gen_stride", _U64),
+    ]
+
+
+_SIGS = {
+    "qf_abi_version": (_I, []),
+    "qf_strerror": (ctypes.c_char_p, [_I]),
+    "qf_gf256_init": (_I, []),
+    "qf_gf256_mul": (_U8, [_U8, _U8]),
+    "qf_gf256_mul_add": (_U8, [_U8, _U8, _U8]),
+    "qf_gf256_inv": (_I, [_U8, _P]),
+    "qf_cauchy_coeffs": (_I, [_U32, _U32, _P]),
+    "qf_ctx_create": (_I, [_I, _P, ctypes.POINTER(_P)]),
+    "qf_ctx_destroy": (_I, [_P]),
+    "qf_ctx_set_stream": (_I, [_P, _P]),
+    "qf_ctx_stream": (_P, [_P]),
+    "qf_sync": (_I, [_P]),
+    "qf_gf256_mul_slice_dev": (_I, [_P, _P, _P, _P, _SZ]),
+    "qf_encode_batch": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
+    "qf_encode_batch_host": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
+    "qf_decode_batch": (_I, [_P, ctypes.POINTER(DecodeShape), _U32, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "qf_encoder_new": (_I, [_P, _U32, _U32, _U32, ctypes.POINTER(_P)]),
+    "qf_encoder_free": (_I, [_P]),
+    "qf_encoder_add_source_packet": (_I, [_P, _U64, _P, _U32]),
+    "qf_encoder_generate_repair_packet": (_I, [_P, _U32, _P, _U32, _P, _P, _P]),
+    "qf_encoder_generate_repairs": (_I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
+    "qf_encoder_window_len": (_I, [_P]),
+    "qf_decoder_new": (_I, [_P, _U32, _U32, ctypes.POINTER(_P)]),
+    "qf_decoder_free": (_I, [_P]),
+    "qf_decoder_add_packet": (_I, [_P, _U64, _I, _P, _U32, _P, _U32]),
+    "qf_decoder_is_decoded": (_I, [_P]),
+    "qf_decoder_get_decoded_packets": (_I, [_P, _P, _U32, _P, _P, _P]),
+    "qf_packet_to_raw": (_I, [_I, _P, _U32, _P, _U32, _P, _U32, _P]),
+    "qf_packet_from_raw": (_I, [_P, _U32, _P, _P, _P, _P, _P]),
+    "qf_fill_splitmix_dev": (_I, [_P, _P, _SZ, _U64, _U64]),
+    "qf_selftest_split_tables": (_I, []),
+}
+
+_LIB: ctypes.CDLL | None = None
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/qf_fec.h."""
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(qf_[a-z0-9_]+)\s*\(", text)))
+
+
+def _lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  (one HIP runtime per process)
+
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is not built; run `python -m quicfuscate_amd.build_lib` "
+            "(there is no CPU fallback for the FEC path)")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> int:
+    if status < 0:
+        raise QfError(status, what)
+    return status

@@ -1,0 +1,122 @@
+"""Build libqf_fec.so (gfx950) in-tree.
+
+    python -m quicfuscate_amd.build_lib
+
+Compiles quicfuscate_amd/csrc/*.hip with hipcc for gfx950 and links the
+shared library against the HIP runtime that ships with PyTorch (same soname
+as /opt/rocm's, so a process that imports torch holds exactly one HIP
+runtime).  The asm-pipelined kernels keep in-flight load destinations in
+registers; a register spill would copy them before the data lands, so the
+build fails if any k_combine_* kernel reports scratch usage.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import re
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parent
+CSRC = PKG / "csrc"
+OUT_DIR = PKG / "lib"
+LIB = OUT_DIR / "libqf_fec.so"
+SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip"]
+ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libqf_fec.so)")
+
+
+def _clangxx() -> str:
+    for cand in ("/opt/rocm/llvm/bin/clang++", shutil.which("clang++")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("clang++ not found")
+
+
+def _torch_hip_runtime() -> Path:
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or spec.origin is None:
+        raise RuntimeError("torch is required (its HIP runtime is the one linked)")
+    lib = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+    if not lib.exists():
+        raise RuntimeError(f"{lib} missing: need a ROCm build of torch")
+    return lib
+
+
+def _compile(src: str, build_dir: Path, extra: list[str]) -> tuple[Path, str]:
+    obj = build_dir / (Path(src).stem + ".o")
+    cmd = [
+        _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+        "-Wno-unused-value", "-Wno-unused-result",
+        f"-I{REPO / 'include'}", f"-I{CSRC}",
+        "-c", str(CSRC / src), "-o", str(obj),
+    ] + extra
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{res.stderr[-4000:]}")
+    return obj, res.stderr
+
+
+def _check_no_scratch(remarks: str) -> dict[str, dict[str, int]]:
+    usage: dict[str, dict[str, int]] = {}
+    cur = None
+    for line in remarks.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            usage[cur] = {}
+            continue
+        m = re.search(r"(VGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)", line)
+        if m and cur:
+            usage[cur][m.group(1).split(" ")[0]] = int(m.group(2))
+    bad = [n for n, u in usage.items() if "combine" in n and u.get("ScratchSize", 0) > 0]
+    if bad:
+        raise RuntimeError(f"register spill in asm-pipelined kernels (unsafe): {bad}")
+    return usage
+
+
+def build(verbose: bool = False) -> Path:
+    build_dir = PKG / "build"
+    build_dir.mkdir(exist_ok=True)
+    OUT_DIR.mkdir(exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=3) as ex:
+        futs = {
+            s: ex.submit(_compile, s, build_dir,
+                         ["-Rpass-analysis=kernel-resource-usage"] if s == "qf_kernels.hip" else [])
+            for s in SOURCES
+        }
+        objs = []
+        for s in SOURCES:
+            obj, err = futs[s].result()
+            objs.append(obj)
+            if s == "qf_kernels.hip":
+                usage = _check_no_scratch(err)
+                if verbose:
+                    for n, u in sorted(usage.items()):
+                        print(f"  {n}: {u}")
+    hip = _torch_hip_runtime()
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [_clangxx(), "-shared", "-o", str(tmp)] + [str(o) for o in objs] + [
+        str(hip), f"-Wl,-rpath,{hip.parent}", "-Wl,--no-undefined", "-lstdc++",
+    ]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed:\n{res.stderr[-4000:]}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    p = build(verbose="-v" in sys.argv)
+    print(p)

@@ -1,0 +1,565 @@
+// qf_api.hip -- C ABI of libqf_fec.so (see include/qf_fec.h).
+//
+// Host-side orchestration only: argument validation, split-table
+// construction, workspace management and kernel launches.  All payload
+// arithmetic runs in the kernels of qf_kernels.hip; there is no CPU compute
+// path for encode or decode.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "gf256_tables.h"
+#include "qf_fec.h"
+#include "qf_kernels.h"
+
+namespace qf {
+const Gf256& gf() {
+    static Gf256 g;
+    return g;
+}
+}  // namespace qf
+
+using qf::gf;
+
+#define QF_CHECK_HIP(expr)                         \
+    do {                                           \
+        hipError_t _e = (expr);                    \
+        if (_e != hipSuccess) return QF_EDEVICE;   \
+    } while (0)
+
+static inline uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+struct EncTab {
+    uint32_t* dev = nullptr;
+    uint32_t k_pad = 0;
+    uint32_t R = 0;
+};
+
+struct qf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 256;
+    uint32_t* d_tab256 = nullptr;  // 256 split-table records (8 dwords each)
+    uint8_t* d_explog = nullptr;   // exp[512] | log[256]
+    // Cauchy split tables, keyed by (k, r, pass)
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, EncTab> cauchy;
+    // custom coefficient tables: pinned host staging + device buffer
+    uint32_t* h_custom = nullptr;
+    uint32_t* d_custom = nullptr;
+    size_t custom_words = 0;
+    hipEvent_t custom_done = nullptr;
+    // decode workspace
+    uint8_t* d_work = nullptr;
+    size_t work_bytes = 0;
+    // host-memory pipeline
+    static const int kPipe = 3;
+    hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
+    uint8_t* d_stage_src[kPipe] = {nullptr, nullptr, nullptr};
+    uint8_t* d_stage_rep[kPipe] = {nullptr, nullptr, nullptr};
+    size_t stage_src_bytes = 0, stage_rep_bytes = 0;
+    std::mutex mu;
+};
+
+namespace {
+
+int ensure_device(qf_ctx* ctx) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return QF_EDEVICE;
+    if (cur != ctx->device && hipSetDevice(ctx->device) != hipSuccess) return QF_EDEVICE;
+    return QF_OK;
+}
+
+// r x k coefficient matrix (row-major) of the reference's Cauchy
+// construction, decoder.rs:280-298.
+int cauchy_matrix(uint32_t k, uint32_t r, std::vector<uint8_t>& out) {
+    out.assign((size_t)k * r, 0);
+    const auto& f = gf();
+    for (uint32_t j = 0; j < r; ++j) {
+        const uint8_t y = (uint8_t)(k + j);
+        for (uint32_t i = 0; i < k; ++i) {
+            uint8_t c;
+            if (!f.inv((uint8_t)((uint8_t)i ^ y), &c)) return QF_ERANGE;
+            out[(size_t)j * k + i] = c;
+        }
+    }
+    return QF_OK;
+}
+
+// Split tables for repairs [j0, j0 + ra) of a coefficient matrix: records
+// (i, jj) at (i*R + jj)*8 for i < k_pad, zero for i >= k or jj >= ra.
+void build_tabs(const uint8_t* coeff_rxk, uint32_t k, uint32_t j0, uint32_t ra, uint32_t R,
+                uint32_t k_pad, std::vector<uint32_t>& out) {
+    out.assign((size_t)k_pad * R * 8, 0);
+    for (uint32_t i = 0; i < k; ++i)
+        for (uint32_t jj = 0; jj < ra; ++jj)
+            qf::perm_record(coeff_rxk[(size_t)(j0 + jj) * k + i], &out[((size_t)i * R + jj) * 8]);
+}
+
+uint32_t pick_R(uint32_t ra) {
+    if (ra <= 1) return 1;
+    if (ra <= 2) return 2;
+    if (ra <= 4) return 4;
+    if (ra <= 8) return 8;
+    return 16;
+}
+
+// Units (16 B) per lane in the encode kernel; QF_ENCODE_V=2 selects the
+// two-unit variant (read per call so tests and benches can compare both).
+int pick_V() {
+    const char* e = getenv("QF_ENCODE_V");
+    return (e && atoi(e) == 2) ? 2 : 1;
+}
+
+int grow_work(qf_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->work_bytes) return QF_OK;
+    if (ctx->d_work) {
+        QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        QF_CHECK_HIP(hipFree(ctx->d_work));
+        ctx->d_work = nullptr;
+        ctx->work_bytes = 0;
+    }
+    const size_t b = round_up(bytes, 1 << 20);
+    if (hipMalloc(&ctx->d_work, b) != hipSuccess) return QF_ENOMEM;
+    ctx->work_bytes = b;
+    return QF_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
+                uint8_t* rep, const uint8_t* coeff, hipStream_t st) {
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    if (k == 0 || k > 256) return QF_EINVAL;
+    if (G == 0 || r == 0 || L == 0) return QF_OK;
+    if (!src || !rep) return QF_EINVAL;
+    if (!aligned16(src) || !aligned16(rep) || (sh->src_row_stride & 15) || (sh->src_gen_stride & 15) ||
+        (sh->rep_row_stride & 15) || (sh->rep_gen_stride & 15))
+        return QF_EINVAL;
+    if (sh->src_row_stride < L && k > 1) return QF_EINVAL;
+    if (sh->rep_row_stride < L && r > 1) return QF_EINVAL;
+    const uint32_t Lu = (L + 15) / 16;
+    const uint32_t k_pad = (uint32_t)round_up(k, 4);
+    const uint32_t passes = (r + 15) / 16;
+    std::vector<uint8_t> cm;
+    if (!coeff) {
+        int s = cauchy_matrix(k, r, cm);
+        if (s != QF_OK) return s;
+    }
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint32_t j0 = p * 16;
+        const uint32_t ra = std::min<uint32_t>(16, r - j0);
+        const uint32_t R = pick_R(ra);
+        if ((size_t)k_pad * R * 32 > 160 * 1024) return QF_EINVAL;
+        const uint32_t* d_tabs = nullptr;
+        if (!coeff) {
+            auto key = std::make_tuple(k, r, p);
+            auto it = ctx->cauchy.find(key);
+            if (it == ctx->cauchy.end()) {
+                std::vector<uint32_t> h;
+                build_tabs(cm.data(), k, j0, ra, R, k_pad, h);
+                EncTab t;
+                t.k_pad = k_pad;
+                t.R = R;
+                if (hipMalloc(&t.dev, h.size() * 4) != hipSuccess) return QF_ENOMEM;
+                QF_CHECK_HIP(hipMemcpy(t.dev, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+                it = ctx->cauchy.emplace(key, t).first;
+            }
+            d_tabs = it->second.dev;
+        } else {
+            std::vector<uint32_t> h;
+            build_tabs(coeff, k, j0, ra, R, k_pad, h);
+            if (h.size() > ctx->custom_words) {
+                QF_CHECK_HIP(hipStreamSynchronize(st));
+                if (ctx->h_custom) hipHostFree(ctx->h_custom);
+                if (ctx->d_custom) hipFree(ctx->d_custom);
+                ctx->h_custom = nullptr;
+                ctx->d_custom = nullptr;
+                const size_t w = round_up(h.size(), 4096);
+                if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_custom), w * 4) != hipSuccess) return QF_ENOMEM;
+                if (hipMalloc(&ctx->d_custom, w * 4) != hipSuccess) return QF_ENOMEM;
+                ctx->custom_words = w;
+            } else {
+                // the previous upload / kernel may still read the staging
+                QF_CHECK_HIP(hipEventSynchronize(ctx->custom_done));
+            }
+            memcpy(ctx->h_custom, h.data(), h.size() * 4);
+            QF_CHECK_HIP(hipMemcpyAsync(ctx->d_custom, ctx->h_custom, h.size() * 4,
+                                        hipMemcpyHostToDevice, st));
+            d_tabs = ctx->d_custom;
+        }
+        qf::CombineUniformArgs a{};
+        a.src = src;
+        a.src_gen_stride = sh->src_gen_stride;
+        a.src_row_stride = sh->src_row_stride;
+        a.dst = rep + (uint64_t)j0 * sh->rep_row_stride;
+        a.dst_gen_stride = sh->rep_gen_stride;
+        a.dst_row_stride = sh->rep_row_stride;
+        a.tabs = d_tabs;
+        a.k = k;
+        a.k_pad = k_pad;
+        a.r_active = ra;
+        a.L = L;
+        a.Lu = Lu;
+        a.total_units = (uint64_t)G * Lu;
+        QF_CHECK_HIP(qf::launch_combine_uniform(a, (int)R, pick_V(), ctx->num_cus, st));
+        if (coeff) {
+            QF_CHECK_HIP(hipEventRecord(ctx->custom_done, st));
+            // a second pass rewrites the staging: wait for this pass first
+            if (p + 1 < passes) QF_CHECK_HIP(hipEventSynchronize(ctx->custom_done));
+        }
+    }
+    return QF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qf_abi_version(void) { return QF_ABI_VERSION; }
+
+const char* qf_strerror(int s) {
+    switch (s) {
+        case QF_OK: return "ok";
+        case QF_EINVAL: return "invalid argument";
+        case QF_ERANGE: return "coefficient undefined (gf_inv(0): k + r > 256)";
+        case QF_ENOTREADY: return "not ready (window not full / fewer than k rows)";
+        case QF_ERANK: return "decode matrix singular";
+        case QF_EDEVICE: return "HIP device error";
+        case QF_ENOMEM: return "out of memory";
+        case QF_ETOOSMALL: return "buffer too short";
+        default: return "unknown status";
+    }
+}
+
+int qf_gf256_init(void) {
+    (void)gf();
+    return QF_OK;
+}
+
+uint8_t qf_gf256_mul(uint8_t a, uint8_t b) { return gf().mul(a, b); }
+
+uint8_t qf_gf256_mul_add(uint8_t a, uint8_t b, uint8_t c) { return (uint8_t)(gf().mul(a, b) ^ c); }
+
+int qf_gf256_inv(uint8_t a, uint8_t* out) {
+    if (!out) return QF_EINVAL;
+    return gf().inv(a, out) ? QF_OK : QF_ERANGE;
+}
+
+int qf_cauchy_coeffs(uint32_t k, uint32_t r, uint8_t* out_rxk) {
+    if (!out_rxk && k && r) return QF_EINVAL;
+    std::vector<uint8_t> m;
+    int s = cauchy_matrix(k, r, m);
+    if (s != QF_OK) return s;
+    if (!m.empty()) memcpy(out_rxk, m.data(), m.size());
+    return QF_OK;
+}
+
+int qf_ctx_create(int device, void* stream, qf_ctx** out) {
+    if (!out) return QF_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return QF_EDEVICE;
+    QF_CHECK_HIP(hipSetDevice(device));
+    qf_ctx* c = new qf_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+    if (stream) {
+        c->stream = reinterpret_cast<hipStream_t>(stream);
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete c;
+            return QF_EDEVICE;
+        }
+        c->own_stream = true;
+    }
+    // value-indexed split tables and exp/log tables
+    std::vector<uint32_t> tab(256 * 8);
+    for (int v = 0; v < 256; ++v) qf::perm_record((uint8_t)v, &tab[v * 8]);
+    std::vector<uint8_t> el(768);
+    memcpy(el.data(), gf().exp, 512);
+    memcpy(el.data() + 512, gf().log, 256);
+    bool ok = hipMalloc(&c->d_tab256, tab.size() * 4) == hipSuccess &&
+              hipMalloc(&c->d_explog, 768) == hipSuccess &&
+              hipMemcpy(c->d_tab256, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(c->d_explog, el.data(), 768, hipMemcpyHostToDevice) == hipSuccess &&
+              hipEventCreateWithFlags(&c->custom_done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        qf_ctx_destroy(c);
+        return QF_EDEVICE;
+    }
+    *out = c;
+    return QF_OK;
+}
+
+int qf_ctx_destroy(qf_ctx* c) {
+    if (!c) return QF_OK;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (auto& kv : c->cauchy) hipFree(kv.second.dev);
+    if (c->d_tab256) hipFree(c->d_tab256);
+    if (c->d_explog) hipFree(c->d_explog);
+    if (c->h_custom) hipHostFree(c->h_custom);
+    if (c->d_custom) hipFree(c->d_custom);
+    if (c->custom_done) hipEventDestroy(c->custom_done);
+    if (c->d_work) hipFree(c->d_work);
+    for (int i = 0; i < qf_ctx::kPipe; ++i) {
+        if (c->pstream[i]) {
+            hipStreamSynchronize(c->pstream[i]);
+            hipStreamDestroy(c->pstream[i]);
+        }
+        if (c->d_stage_src[i]) hipFree(c->d_stage_src[i]);
+        if (c->d_stage_rep[i]) hipFree(c->d_stage_rep[i]);
+    }
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return QF_OK;
+}
+
+int qf_ctx_set_stream(qf_ctx* ctx, void* stream) {
+    if (!ctx) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (ctx->own_stream && ctx->stream) {
+        hipStreamSynchronize(ctx->stream);
+        hipStreamDestroy(ctx->stream);
+        ctx->own_stream = false;
+    }
+    if (stream) {
+        ctx->stream = reinterpret_cast<hipStream_t>(stream);
+    } else {
+        QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+    }
+    return QF_OK;
+}
+
+void* qf_ctx_stream(qf_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
+
+int qf_sync(qf_ctx* ctx) {
+    if (!ctx) return QF_EINVAL;
+    QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return QF_OK;
+}
+
+int qf_gf256_mul_slice_dev(qf_ctx* ctx, const uint8_t* a, const uint8_t* b, uint8_t* out, size_t n) {
+    if (!ctx || (n && (!a || !b || !out))) return QF_EINVAL;
+    if (n == 0) return QF_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    if (!aligned16(a) || !aligned16(b) || !aligned16(out)) return QF_EINVAL;
+    QF_CHECK_HIP(qf::launch_mul_slice(a, b, out, n, ctx->d_explog, ctx->num_cus, ctx->stream));
+    return QF_OK;
+}
+
+int qf_fill_splitmix_dev(qf_ctx* ctx, uint8_t* dst, size_t n, uint64_t seed, uint64_t word_offset) {
+    if (!ctx || (n && !dst)) return QF_EINVAL;
+    if (n == 0) return QF_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    QF_CHECK_HIP(qf::launch_fill_splitmix(dst, n, seed, word_offset, ctx->num_cus, ctx->stream));
+    return QF_OK;
+}
+
+int qf_encode_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
+                    uint8_t* rep, const uint8_t* coeff) {
+    if (!ctx || !sh) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    return encode_impl(ctx, sh, G, src, rep, coeff, ctx->stream);
+}
+
+int qf_encode_batch_host(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
+                         uint8_t* rep, const uint8_t* coeff) {
+    if (!ctx || !sh) return QF_EINVAL;
+    if (G == 0 || sh->r == 0 || sh->L == 0) return QF_OK;
+    if (!src || !rep) return QF_EINVAL;
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    // dense generations only: rows back to back inside a generation
+    if (sh->src_gen_stride != (uint64_t)k * sh->src_row_stride ||
+        sh->rep_gen_stride != (uint64_t)r * sh->rep_row_stride)
+        return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    // ~64 MiB of source per chunk
+    uint64_t per = std::max<uint64_t>(1, (64ull << 20) / std::max<uint64_t>(1, sh->src_gen_stride));
+    per = std::min<uint64_t>(per, G);
+    const size_t sb = per * sh->src_gen_stride, rb = per * sh->rep_gen_stride;
+    if (sb > ctx->stage_src_bytes || rb > ctx->stage_rep_bytes) {
+        for (int i = 0; i < qf_ctx::kPipe; ++i) {
+            if (ctx->pstream[i]) QF_CHECK_HIP(hipStreamSynchronize(ctx->pstream[i]));
+            if (ctx->d_stage_src[i]) hipFree(ctx->d_stage_src[i]);
+            if (ctx->d_stage_rep[i]) hipFree(ctx->d_stage_rep[i]);
+            ctx->d_stage_src[i] = ctx->d_stage_rep[i] = nullptr;
+        }
+        for (int i = 0; i < qf_ctx::kPipe; ++i) {
+            if (hipMalloc(&ctx->d_stage_src[i], sb) != hipSuccess) return QF_ENOMEM;
+            if (hipMalloc(&ctx->d_stage_rep[i], rb) != hipSuccess) return QF_ENOMEM;
+        }
+        ctx->stage_src_bytes = sb;
+        ctx->stage_rep_bytes = rb;
+    }
+    for (int i = 0; i < qf_ctx::kPipe; ++i)
+        if (!ctx->pstream[i]) QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->pstream[i], hipStreamNonBlocking));
+    // Chunk c on stream c % kPipe: H2D -> encode -> D2H; chunks on different
+    // streams overlap copies in both directions with the kernels.
+    uint32_t c = 0;
+    for (uint64_t g0 = 0; g0 < G; g0 += per, ++c) {
+        const uint64_t n = std::min<uint64_t>(per, G - g0);
+        hipStream_t st = ctx->pstream[c % qf_ctx::kPipe];
+        uint8_t* ds = ctx->d_stage_src[c % qf_ctx::kPipe];
+        uint8_t* dr = ctx->d_stage_rep[c % qf_ctx::kPipe];
+        QF_CHECK_HIP(hipMemcpyAsync(ds, src + g0 * sh->src_gen_stride, n * sh->src_gen_stride,
+                                    hipMemcpyHostToDevice, st));
+        qf_encode_shape s2 = *sh;
+        int e = encode_impl(ctx, &s2, (uint32_t)n, ds, dr, coeff, st);
+        if (e != QF_OK) return e;
+        QF_CHECK_HIP(hipMemcpy2DAsync(rep + g0 * sh->rep_gen_stride, sh->rep_row_stride, dr,
+                                      sh->rep_row_stride, L, n * r, hipMemcpyDeviceToHost, st));
+    }
+    for (int i = 0; i < qf_ctx::kPipe; ++i) QF_CHECK_HIP(hipStreamSynchronize(ctx->pstream[i]));
+    return QF_OK;
+}
+
+int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                    const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
+                    uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    if (!ctx || !sh) return QF_EINVAL;
+    const uint32_t k = sh->k, r = sh->r, L = sh->L, max_rows = sh->max_rows;
+    if (k == 0 || k > 256 || max_rows == 0 || max_rows > 4096 || L == 0) return QF_EINVAL;
+    if (G == 0) return QF_OK;
+    if (!rows || !row_index || !n_rec || !status) return QF_EINVAL;
+    const uint32_t e_max = std::min(k, r);
+    if (e_max > 128) return QF_EINVAL;
+    if (e_max && (!rec || !rec_index)) return QF_EINVAL;
+    if (!aligned16(rows) || (sh->row_stride & 15) || (sh->rows_gen_stride & 15)) return QF_EINVAL;
+    if (e_max && (!aligned16(rec) || (sh->rec_row_stride & 15) || (sh->rec_gen_stride & 15)))
+        return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    const uint32_t passes = (e_max + 15) / 16;
+    const uint64_t coef_gen_stride = ((uint64_t)max_rows + 1) * 16;
+    const size_t coef_bytes = (size_t)std::max<uint32_t>(passes, 1) * G * coef_gen_stride;
+    const size_t bound_off = round_up(coef_bytes, 256);
+    s = grow_work(ctx, bound_off + (size_t)G * 4);
+    if (s) return s;
+    uint8_t* d_coef = ctx->d_work;
+    uint32_t* d_bound = reinterpret_cast<uint32_t*>(ctx->d_work + bound_off);
+    qf::PrepareArgs pa{};
+    pa.row_index = row_index;
+    pa.n_rows = n_rows;
+    pa.row_coeffs = row_coeffs;
+    pa.explog = ctx->d_explog;
+    pa.coef_out = d_coef;
+    pa.coef_gen_stride = coef_gen_stride;
+    pa.n_out = n_rec;
+    pa.bound = d_bound;
+    pa.rec_index = rec_index;
+    pa.status = status;
+    pa.k = k;
+    pa.e_max = e_max;
+    pa.max_rows = max_rows;
+    pa.max_rows_pad = (max_rows + 7) & ~7u;
+    pa.passes = passes;
+    pa.G = G;
+    if (qf::prepare_lds_bytes(k, e_max, max_rows) > 160 * 1024) return QF_EINVAL;
+    QF_CHECK_HIP(qf::launch_decode_prepare(pa, ctx->stream));
+    const uint32_t Lu = (L + 15) / 16;
+    for (uint32_t p = 0; p < passes; ++p) {
+        qf::CombineSlotsArgs a{};
+        a.rows = rows;
+        a.rows_gen_stride = sh->rows_gen_stride;
+        a.row_stride = sh->row_stride;
+        a.dst = rec + (uint64_t)p * 16 * sh->rec_row_stride;
+        a.dst_gen_stride = sh->rec_gen_stride;
+        a.dst_row_stride = sh->rec_row_stride;
+        a.coef = d_coef + (uint64_t)p * G * coef_gen_stride;
+        a.coef_gen_stride = coef_gen_stride;
+        a.n_out = n_rec;
+        a.bound = d_bound;
+        a.tab256 = ctx->d_tab256;
+        a.pass = p;
+        a.L = L;
+        a.Lu = Lu;
+        a.zero_slot = max_rows;
+        a.total_units = (uint64_t)G * Lu;
+        QF_CHECK_HIP(qf::launch_combine_slots(a, ctx->num_cus, ctx->stream));
+    }
+    return QF_OK;
+}
+
+int qf_selftest_split_tables(void) {
+    const auto& f = gf();
+    uint32_t rec[8];
+    for (int c = 0; c < 256; ++c) {
+        qf::perm_record((uint8_t)c, rec);
+        for (int x = 0; x < 256; x += 4) {
+            const uint32_t packed = qf::pack4((uint8_t)x, (uint8_t)(x + 1), (uint8_t)(x + 2), (uint8_t)(x + 3));
+            const uint32_t got = qf::perm_mul4_emul(rec, packed);
+            for (int b = 0; b < 4; ++b)
+                if (((got >> (8 * b)) & 0xFF) != f.mul((uint8_t)c, (uint8_t)(x + b))) return QF_EINVAL;
+        }
+    }
+    return QF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Wire framing (encoder.rs:18-152)
+// ---------------------------------------------------------------------------
+int qf_packet_to_raw(int is_systematic, const uint8_t* coeffs, uint32_t coeff_len,
+                     const uint8_t* payload, uint32_t len, uint8_t* out, uint32_t out_cap,
+                     uint32_t* out_len) {
+    if (!out || !out_len || (len && !payload) || coeff_len > 0xFFFF) return QF_EINVAL;
+    uint64_t need = (uint64_t)len + 1 + (coeffs ? 2 + (uint64_t)coeff_len : 0);
+    if (need > out_cap) return QF_ETOOSMALL;
+    uint32_t o = 0;
+    out[o++] = is_systematic ? 1 : 0;
+    if (coeffs) {
+        out[o++] = (uint8_t)(coeff_len >> 8);
+        out[o++] = (uint8_t)(coeff_len & 0xFF);
+        memcpy(out + o, coeffs, coeff_len);
+        o += coeff_len;
+    }
+    if (len) memcpy(out + o, payload, len);
+    o += len;
+    *out_len = o;
+    return QF_OK;
+}
+
+int qf_packet_from_raw(const uint8_t* raw, uint32_t raw_len, int* is_systematic,
+                       const uint8_t** coeffs, uint32_t* coeff_len, const uint8_t** payload,
+                       uint32_t* len) {
+    if (!is_systematic || !coeffs || !coeff_len || !payload || !len) return QF_EINVAL;
+    if (!raw || raw_len == 0) return QF_EINVAL;  // "Raw data is empty"
+    const int sys = raw[0] == 1;
+    uint32_t off = 1;
+    *coeffs = nullptr;
+    *coeff_len = 0;
+    if (!sys) {
+        if (raw_len < 3) return QF_ETOOSMALL;  // coefficient length missing
+        const uint32_t cl = ((uint32_t)raw[1] << 8) | raw[2];
+        off = 3;
+        if (raw_len < off + cl) return QF_ETOOSMALL;  // coefficients truncated
+        *coeffs = raw + off;
+        *coeff_len = cl;
+        off += cl;
+    }
+    *is_systematic = sys;
+    *payload = raw + off;
+    *len = raw_len - off;
+    return QF_OK;
+}
+
+}  // extern "C"

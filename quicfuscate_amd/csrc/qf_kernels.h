@@ -1,0 +1,81 @@
+// qf_kernels.h -- kernel argument blocks and launch wrappers (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qf {
+
+// Encode / uniform combination:
+//   dst[g][j] = XOR_i C[j][i] * src[g][i]   for j < r_active, i < k
+// tabs: k_pad * R records of 8 dwords, record (i, j) at (i*R + j)*8, zero
+// records for i >= k.  Lanes map over units f = g*Lu + u (16 bytes each).
+struct CombineUniformArgs {
+    const uint8_t* src;
+    uint64_t src_gen_stride;
+    uint64_t src_row_stride;
+    uint8_t* dst;
+    uint64_t dst_gen_stride;
+    uint64_t dst_row_stride;
+    const uint32_t* tabs;
+    uint32_t k;
+    uint32_t k_pad;
+    uint32_t r_active;
+    uint32_t L;
+    uint32_t Lu;
+    uint32_t pad0;
+    uint64_t total_units;
+};
+
+// Decode payload pass (one 16-output pass):
+//   dst[g][j] = XOR_s coef[g][s][j] * rows[g][s]   for j < n_out[g]-16*pass
+// coef: 16 coefficient bytes per slot, slot s of generation g at
+// coef + g*coef_gen_stride + s*16.  Slots >= bound[g] are not read.
+struct CombineSlotsArgs {
+    const uint8_t* rows;
+    uint64_t rows_gen_stride;
+    uint64_t row_stride;
+    uint8_t* dst;
+    uint64_t dst_gen_stride;
+    uint64_t dst_row_stride;
+    const uint8_t* coef;
+    uint64_t coef_gen_stride;
+    const uint32_t* n_out;
+    const uint32_t* bound;
+    const uint32_t* tab256;
+    uint32_t pass;
+    uint32_t L;
+    uint32_t Lu;
+    uint32_t zero_slot;  // index of an all-zero coefficient record
+    uint64_t total_units;
+};
+
+struct PrepareArgs {
+    const uint16_t* row_index;
+    const uint32_t* n_rows;
+    const uint8_t* row_coeffs;
+    const uint8_t* explog;  // exp[512] then log[256]
+    uint8_t* coef_out;      // [pass][G][coef_gen_stride]
+    uint64_t coef_gen_stride;
+    uint32_t* n_out;
+    uint32_t* bound;
+    uint16_t* rec_index;    // [G][e_max]
+    int32_t* status;
+    uint32_t k;
+    uint32_t e_max;
+    uint32_t max_rows;
+    uint32_t max_rows_pad;
+    uint32_t passes;
+    uint32_t G;
+};
+
+hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int num_cus,
+                                  hipStream_t st);
+hipError_t launch_combine_slots(const CombineSlotsArgs& a, int num_cus, hipStream_t st);
+hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st);
+size_t prepare_lds_bytes(uint32_t k, uint32_t e_max, uint32_t max_rows);
+hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n,
+                            const uint8_t* explog, int num_cus, hipStream_t st);
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t word_offset,
+                                int num_cus, hipStream_t st);
+
+}  // namespace qf

@@ -1,0 +1,830 @@
+// qf_kernels.hip -- hand-written CDNA4 (gfx950) kernels for GF(2^8) RLNC.
+//
+// Arithmetic core: split-index table multiply on v_perm_b32 (see
+// gf256_tables.h).  One v_perm performs four 8-entry byte lookups, so a
+// product c*x of four packed bytes is three v_perm (bits 0-2, 3-5, 6-7); two
+// source rows are folded per step so that six products accumulate with three
+// v_bitop3_b32 (3-input XOR, truth table 0x96).  That is 4.5 VALU ops per
+// dword-coefficient (1.125 per byte multiply-add), no MFMA, no LDS lookups in
+// the inner loop for encode.  The selectors (x & 7, x>>3 & 7, x>>6 & 3) of a
+// source dword are computed once and reused by all r repairs.
+//
+// Kernels
+//  k_combine_uniform<R,V,TAIL>  encode: out[g][j] = sum_i C[j][i] * in[g][i]
+//                               with one coefficient matrix for the batch;
+//                               its split tables live in LDS, [i][j] order,
+//                               read by broadcast ds_read with immediate
+//                               offsets.  Lanes map flat over (generation,
+//                               16-byte unit) so a 1200-B row costs no lane
+//                               waste.  Persistent grid.
+//  k_combine_slots<R,TAIL>      decode payload pass: per-generation
+//                               coefficient records (one 16-byte record per
+//                               received slot), value-indexed split tables in
+//                               LDS.
+//  k_decode_prepare             decode control: row acceptance
+//                               (decoder.rs:678-701), erasure bookkeeping and
+//                               Gauss-Jordan over [A_E | A_S | I] in LDS
+//                               (decoder.rs:720-783, F4 fixed) producing the
+//                               e x k recovery matrix; one wave per generation,
+//                               ballot pivot search.
+//  k_mul_slice                  element-wise a[i]*b[i] (gf_tables.rs:255-274).
+//  k_fill_splitmix              synthetic payload generator.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "qf_kernels.h"
+
+namespace qf {
+
+#define QF_DEV __device__ __forceinline__
+#ifndef QF_SLOTS_WAVES
+#define QF_SLOTS_WAVES 3
+#endif
+
+QF_DEV uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+QF_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+QF_DEV uint32_t comp(const uint4& v, int c) {
+    return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+QF_DEV void set_comp(uint4& v, int c, uint32_t x) {
+    if (c == 0) v.x = x;
+    else if (c == 1) v.y = x;
+    else if (c == 2) v.z = x;
+    else v.w = x;
+}
+
+// Load 16 bytes (nb valid, the rest zero).  nb == 16 is the fast path.
+QF_DEV uint4 load_unit(const uint8_t* p, uint32_t nb) {
+    if (nb >= 16) return *reinterpret_cast<const uint4*>(p);
+    uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        if ((uint32_t)b < nb) {
+            uint32_t w = comp(r, b >> 2) | ((uint32_t)p[b] << (8 * (b & 3)));
+            set_comp(r, b >> 2, w);
+        }
+    }
+    return r;
+}
+
+QF_DEV void store_unit(uint8_t* p, const uint4& v, uint32_t nb) {
+    if (nb >= 16) {
+        *reinterpret_cast<uint4*>(p) = v;
+        return;
+    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if ((uint32_t)b < nb) p[b] = (uint8_t)(comp(v, b >> 2) >> (8 * (b & 3)));
+}
+
+// ---------------------------------------------------------------------------
+// Explicitly pipelined streaming loads.  hipcc sinks loop-carried loads down
+// to their first use (exposing the whole HBM latency per step), so the hot
+// loops issue global_load_dwordx4 through inline asm and wait with a counted
+// s_waitcnt vmcnt(N) whose asm operands are the destination registers: the
+// data dependency orders every use after the wait, and hipcc's own counters
+// never see these loads (the loops contain no other vector-memory ops).
+// ---------------------------------------------------------------------------
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+QF_DEV void aload16(v4u& r, const uint8_t* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+}
+
+template <int N>
+QF_DEV void vm_wait2(v4u& a, v4u& b);
+#define QF_VM_WAIT2(N)                                                           \
+    template <>                                                                  \
+    QF_DEV void vm_wait2<N>(v4u & a, v4u & b) {                                  \
+        asm volatile("s_waitcnt vmcnt(" #N ")" : "+v"(a), "+v"(b)::"memory");   \
+    }
+QF_VM_WAIT2(0)
+QF_VM_WAIT2(2)
+QF_VM_WAIT2(4)
+QF_VM_WAIT2(6)
+QF_VM_WAIT2(8)
+
+QF_DEV uint4 to_u4(const v4u& v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
+struct Sel {
+    uint4 s0, s1, s2;
+};
+QF_DEV Sel selectors(const uint4& x) {
+    Sel s;
+    s.s0 = make_uint4(x.x & 0x07070707u, x.y & 0x07070707u, x.z & 0x07070707u, x.w & 0x07070707u);
+    s.s1 = make_uint4((x.x >> 3) & 0x07070707u, (x.y >> 3) & 0x07070707u,
+                      (x.z >> 3) & 0x07070707u, (x.w >> 3) & 0x07070707u);
+    s.s2 = make_uint4((x.x >> 6) & 0x03030303u, (x.y >> 6) & 0x03030303u,
+                      (x.z >> 6) & 0x03030303u, (x.w >> 6) & 0x03030303u);
+    return s;
+}
+
+// acc ^= ca * xa ^ cb * xb  for the four dwords of one unit.
+// A = {T0lo,T0hi,T1lo,T1hi} of ca, a2 = T2 of ca; same for cb.
+QF_DEV void fma_pair(uint4& acc, const uint4& A, uint32_t a2, const Sel& sa, const uint4& B,
+                     uint32_t b2, const Sel& sb) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        uint32_t t = comp(acc, c);
+        t = xor3(t, vperm(A.y, A.x, comp(sa.s0, c)), vperm(A.w, A.z, comp(sa.s1, c)));
+        t = xor3(t, vperm(a2, a2, comp(sa.s2, c)), vperm(B.y, B.x, comp(sb.s0, c)));
+        t = xor3(t, vperm(B.w, B.z, comp(sb.s1, c)), vperm(b2, b2, comp(sb.s2, c)));
+        set_comp(acc, c, t);
+    }
+}
+
+QF_DEV uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        uint32_t o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// ---------------------------------------------------------------------------
+// Encode: one coefficient matrix for the whole batch.
+// ---------------------------------------------------------------------------
+template <int R, int V>
+QF_DEV void fma_rows(uint4 (&acc)[R][V], const uint32_t* __restrict__ t, const uint4 (&xa)[V],
+                     const uint4 (&xb)[V]) {
+    Sel sa[V], sb[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        sa[v] = selectors(xa[v]);
+        sb[v] = selectors(xb[v]);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const uint4 A = *reinterpret_cast<const uint4*>(t + j * 8);
+        const uint32_t a2 = t[j * 8 + 4];
+        const uint4 B = *reinterpret_cast<const uint4*>(t + R * 8 + j * 8);
+        const uint32_t b2 = t[R * 8 + j * 8 + 4];
+#pragma unroll
+        for (int v = 0; v < V; ++v) fma_pair(acc[j][v], A, a2, sa[v], B, b2, sb[v]);
+    }
+}
+
+template <int V>
+QF_DEV void load_pair(uint4 (&xa)[V], uint4 (&xb)[V], const uint8_t* const (&sp)[V],
+                      uint64_t offa, uint64_t offb, const uint32_t (&nbytes)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        xa[v] = load_unit(sp[v] + offa, nbytes[v]);
+        xb[v] = load_unit(sp[v] + offb, nbytes[v]);
+    }
+}
+
+template <int V>
+QF_DEV void aload_pair(v4u (&xa)[V], v4u (&xb)[V], const uint8_t* const (&sp)[V], uint64_t offa,
+                       uint64_t offb) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        aload16(xa[v], sp[v] + offa);
+        aload16(xb[v], sp[v] + offb);
+    }
+}
+
+// Wait for the older pair while the 2V loads of the newer pair stay in flight.
+template <int V>
+QF_DEV void wait_pair(v4u (&xa)[V], v4u (&xb)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) vm_wait2<2 * V>(xa[v], xb[v]);
+}
+
+template <int V>
+QF_DEV void to_u4v(uint4 (&o)[V], const v4u (&x)[V]) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) o[v] = to_u4(x[v]);
+}
+
+// One work item: V units per lane, all k rows, R outputs.  The row loop is a
+// two-buffer ping-pong unrolled by four rows; the loads of pair i+2 are in
+// flight while pair i is computed.  Rows past k-1 are clamped to row k-1;
+// their split tables are zero records (k_pad = round_up(k, 4)), so the
+// clamped data contributes nothing and every load is unconditional.
+template <int R, int V, bool TAIL>
+QF_DEV void combine_uniform_item(const CombineUniformArgs& a, const uint32_t* __restrict__ tabs,
+                                 const uint8_t* const (&sp)[V], uint8_t* const (&dp)[V],
+                                 const uint32_t (&nbytes)[V]) {
+    const uint64_t rs = a.src_row_stride;
+    const uint32_t k = a.k;
+    const uint32_t klast = k - 1;
+    auto off = [&](uint32_t i) -> uint64_t { return (uint64_t)(i < klast ? i : klast) * rs; };
+    uint4 acc[R][V];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[j][v] = make_uint4(0, 0, 0, 0);
+
+    if (TAIL) {
+        // Partial units (rows shorter than a whole 16-byte unit): plain loads.
+        uint4 xa[V], xb[V];
+        for (uint32_t i = 0; i < k; i += 2) {
+            load_pair<V>(xa, xb, sp, off(i), off(i + 1), nbytes);
+            fma_rows<R, V>(acc, tabs + (size_t)i * R * 8, xa, xb);
+        }
+    } else {
+        v4u p0a[V], p0b[V], p1a[V], p1b[V];
+        aload_pair<V>(p0a, p0b, sp, off(0), off(1));
+        for (uint32_t i = 0; i < k; i += 4) {
+            aload_pair<V>(p1a, p1b, sp, off(i + 2), off(i + 3));
+            wait_pair<V>(p0a, p0b);
+            {
+                uint4 xa[V], xb[V];
+                to_u4v<V>(xa, p0a);
+                to_u4v<V>(xb, p0b);
+                fma_rows<R, V>(acc, tabs + (size_t)i * R * 8, xa, xb);
+            }
+            aload_pair<V>(p0a, p0b, sp, off(i + 4), off(i + 5));
+            wait_pair<V>(p1a, p1b);
+            {
+                uint4 xa[V], xb[V];
+                to_u4v<V>(xa, p1a);
+                to_u4v<V>(xb, p1b);
+                fma_rows<R, V>(acc, tabs + (size_t)(i + 2) * R * 8, xa, xb);
+            }
+        }
+        // Drain the last (unused) prefetch before the stores / next item.
+#pragma unroll
+        for (int v = 0; v < V; ++v) vm_wait2<0>(p0a[v], p0b[v]);
+    }
+    const uint32_t ra = a.r_active;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        if ((uint32_t)j < ra) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                if (TAIL) {
+                    if (nbytes[v]) store_unit(dp[v] + (uint64_t)j * a.dst_row_stride, acc[j][v], nbytes[v]);
+                } else {
+                    store_unit(dp[v] + (uint64_t)j * a.dst_row_stride, acc[j][v], 16);
+                }
+            }
+        }
+    }
+}
+
+template <int R, int V>
+__global__ void __launch_bounds__(256, (V == 1 ? 3 : 2)) k_combine_uniform(CombineUniformArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_tabs[];
+    {
+        const uint32_t n4 = a.k_pad * R * 2;  // uint4 count (8 words per record)
+        const uint4* g = reinterpret_cast<const uint4*>(a.tabs);
+        uint4* l = reinterpret_cast<uint4*>(lds_tabs);
+        for (uint32_t w = threadIdx.x; w < n4; w += blockDim.x) l[w] = g[w];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wave = blockIdx.x * wpb + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * wpb;
+    const uint32_t per_wave = 64u * V;
+    for (uint64_t base = (uint64_t)wave * per_wave; base < a.total_units;
+         base += (uint64_t)nwaves * per_wave) {
+        const uint8_t* sp[V];
+        uint8_t* dp[V];
+        uint32_t nbytes[V];
+        bool all_full = true;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const uint64_t f = base + (uint64_t)v * 64 + lane;
+            sp[v] = a.src;
+            dp[v] = a.dst;
+            nbytes[v] = 0;
+            if (f < a.total_units) {
+                const uint64_t g = f / a.Lu;
+                const uint32_t u = (uint32_t)(f - g * a.Lu);
+                sp[v] = a.src + g * a.src_gen_stride + (uint64_t)u * 16;
+                dp[v] = a.dst + g * a.dst_gen_stride + (uint64_t)u * 16;
+                const uint32_t rem = a.L - u * 16;
+                nbytes[v] = rem < 16 ? rem : 16;
+            }
+            all_full = all_full && nbytes[v] == 16;
+        }
+        if (__all(all_full)) combine_uniform_item<R, V, false>(a, lds_tabs, sp, dp, nbytes);
+        else combine_uniform_item<R, V, true>(a, lds_tabs, sp, dp, nbytes);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decode payload pass: per-generation coefficient records over slots.
+// ---------------------------------------------------------------------------
+
+template <int R>
+QF_DEV void fma_rows_slots(uint4 (&acc)[R], const uint32_t* __restrict__ tab256, const uint4& xa,
+                           const uint4& xb, const uint4& ca, const uint4& cb) {
+    const Sel sa = selectors(xa), sb = selectors(xb);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const uint32_t wa = comp(ca, j >> 2), wb = comp(cb, j >> 2);
+        // record address = coefficient * 32 bytes
+        const uint32_t oa = ((wa >> (8 * (j & 3))) & 0xFF) << 5;
+        const uint32_t ob = ((wb >> (8 * (j & 3))) & 0xFF) << 5;
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(tab256);
+        const uint4 A = *reinterpret_cast<const uint4*>(base + oa);
+        const uint32_t a2 = *reinterpret_cast<const uint32_t*>(base + oa + 16);
+        const uint4 B = *reinterpret_cast<const uint4*>(base + ob);
+        const uint32_t b2 = *reinterpret_cast<const uint32_t*>(base + ob + 16);
+        fma_pair(acc[j], A, a2, sa, B, b2, sb);
+    }
+}
+
+// Coefficient records: slot s of a lane's generation, or the all-zero record
+// at index a.zero_slot for slots at/after the lane's bound.  Data rows past
+// the bound are clamped to the last valid slot (multiplied by zero).
+template <int R, bool TAIL>
+QF_DEV void combine_slots_item(const CombineSlotsArgs& a, const uint32_t* __restrict__ tab256,
+                               const uint8_t* rowp, uint8_t* outp, const uint8_t* coefp,
+                               uint32_t nbytes, uint32_t e_lane, uint32_t bound_lane,
+                               uint32_t smax) {
+    const uint64_t rs = a.row_stride;
+    const uint32_t zs = a.zero_slot;
+    uint4 acc[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = make_uint4(0, 0, 0, 0);
+    const uint32_t blast = bound_lane ? bound_lane - 1 : 0;
+#define QF_ROW(s) (rowp + (uint64_t)((s) < blast ? (s) : blast) * rs)
+#define QF_COEF(s) (coefp + (uint64_t)((s) < bound_lane ? (s) : zs) * 16)
+    if (TAIL) {
+        for (uint32_t s = 0; s < smax; s += 2) {
+            const uint4 xa = load_unit(QF_ROW(s), nbytes);
+            const uint4 xb = load_unit(QF_ROW(s + 1), nbytes);
+            const uint4 ca = *reinterpret_cast<const uint4*>(QF_COEF(s));
+            const uint4 cb = *reinterpret_cast<const uint4*>(QF_COEF(s + 1));
+            fma_rows_slots<R>(acc, tab256, xa, xb, ca, cb);
+        }
+    } else {
+        // Ping-pong as in combine_uniform_item: four loads per slot pair (two
+        // rows, two coefficient records) stay in flight one step ahead.
+        v4u p0a, p0b, q0a, q0b, p1a, p1b, q1a, q1b;
+        aload16(p0a, QF_ROW(0u));
+        aload16(p0b, QF_ROW(1u));
+        aload16(q0a, QF_COEF(0u));
+        aload16(q0b, QF_COEF(1u));
+        for (uint32_t s = 0; s < smax; s += 4) {
+            aload16(p1a, QF_ROW(s + 2));
+            aload16(p1b, QF_ROW(s + 3));
+            aload16(q1a, QF_COEF(s + 2));
+            aload16(q1b, QF_COEF(s + 3));
+            vm_wait2<4>(p0a, p0b);
+            vm_wait2<4>(q0a, q0b);
+            fma_rows_slots<R>(acc, tab256, to_u4(p0a), to_u4(p0b), to_u4(q0a), to_u4(q0b));
+            aload16(p0a, QF_ROW(s + 4));
+            aload16(p0b, QF_ROW(s + 5));
+            aload16(q0a, QF_COEF(s + 4));
+            aload16(q0b, QF_COEF(s + 5));
+            vm_wait2<4>(p1a, p1b);
+            vm_wait2<4>(q1a, q1b);
+            fma_rows_slots<R>(acc, tab256, to_u4(p1a), to_u4(p1b), to_u4(q1a), to_u4(q1b));
+        }
+        vm_wait2<0>(p0a, p0b);
+        vm_wait2<0>(q0a, q0b);
+    }
+#undef QF_ROW
+#undef QF_COEF
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        if ((uint32_t)j < e_lane) {
+            if (TAIL) store_unit(outp + (uint64_t)j * a.dst_row_stride, acc[j], nbytes);
+            else store_unit(outp + (uint64_t)j * a.dst_row_stride, acc[j], 16);
+        }
+    }
+}
+
+template <int R>
+QF_DEV void combine_slots_dispatch(const CombineSlotsArgs& a, const uint32_t* tab256,
+                                   const uint8_t* rowp, uint8_t* outp, const uint8_t* coefp,
+                                   uint32_t nbytes, uint32_t e_lane, uint32_t bound_lane,
+                                   uint32_t smax, bool full) {
+    if (full) combine_slots_item<R, false>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax);
+    else combine_slots_item<R, true>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax);
+}
+
+__global__ void __launch_bounds__(256, QF_SLOTS_WAVES) k_combine_slots(CombineSlotsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab256[256 * 8];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.tab256);
+        uint4* l = reinterpret_cast<uint4*>(tab256);
+        for (uint32_t w = threadIdx.x; w < 512; w += blockDim.x) l[w] = g[w];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wave = blockIdx.x * wpb + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * wpb;
+    for (uint64_t base = (uint64_t)wave * 64; base < a.total_units; base += (uint64_t)nwaves * 64) {
+        const uint64_t f = base + lane;
+        const uint8_t* rowp = a.rows;
+        uint8_t* outp = a.dst;
+        const uint8_t* coefp = a.coef;
+        uint32_t nbytes = 0, e_lane = 0, bound_lane = 0;
+        if (f < a.total_units) {
+            const uint64_t g = f / a.Lu;
+            const uint32_t u = (uint32_t)(f - g * a.Lu);
+            rowp = a.rows + g * a.rows_gen_stride + (uint64_t)u * 16;
+            outp = a.dst + g * a.dst_gen_stride + (uint64_t)u * 16;
+            coefp = a.coef + g * a.coef_gen_stride;
+            const uint32_t rem = a.L - u * 16;
+            nbytes = rem < 16 ? rem : 16;
+            const uint32_t e = a.n_out[g];
+            const uint32_t lo = a.pass * 16;
+            e_lane = e > lo ? (e - lo < 16 ? e - lo : 16) : 0;
+            bound_lane = e_lane ? a.bound[g] : 0;
+        }
+        const uint32_t jmax = wave_max_u32(e_lane);
+        if (jmax == 0) continue;
+        const uint32_t smax = wave_max_u32(bound_lane);
+        const bool full = __all(nbytes == 16);
+        // Output rows per wave pick the unrolled width (zero coefficients
+        // beyond a generation's e make the extra rows harmless).
+        if (jmax <= 4) combine_slots_dispatch<4>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 8) combine_slots_dispatch<8>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 12) combine_slots_dispatch<12>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 14) combine_slots_dispatch<14>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else combine_slots_dispatch<16>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decode control: one wave (64 lanes) per generation.
+// ---------------------------------------------------------------------------
+struct PrepLds {
+    uint8_t* exp;     // 512
+    uint8_t* log;     // 256
+    uint32_t* first;  // k    : first slot of systematic index
+    uint16_t* sys_slot;  // k : accepted slot of systematic i (0xFFFF none)
+    uint16_t* col;    // k    : matrix column of source i
+    uint16_t* rep_slot;  // e_max
+    uint16_t* emap;   // e_max: erased source indices
+    uint16_t* slot_col;  // max_rows: D column of slot (0xFFFF = unused)
+    uint16_t* lf;     // e_max: log of elimination factors (0xFFFF = zero)
+    uint8_t* M;       // e_max x W
+};
+
+QF_DEV uint8_t gmul(const PrepLds& L, uint32_t a, uint32_t b) {
+    if (a == 0 || b == 0) return 0;
+    return L.exp[(uint32_t)L.log[a] + (uint32_t)L.log[b]];
+}
+
+__global__ void __launch_bounds__(64) k_decode_prepare(PrepareArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t g = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k = a.k, emax = a.e_max;
+    PrepLds L;
+    {
+        uint8_t* p = lds;
+        L.exp = p; p += 512;
+        L.log = p; p += 256;
+        L.first = reinterpret_cast<uint32_t*>(p); p += 4 * 256;
+        L.sys_slot = reinterpret_cast<uint16_t*>(p); p += 2 * 256;
+        L.col = reinterpret_cast<uint16_t*>(p); p += 2 * 256;
+        L.rep_slot = reinterpret_cast<uint16_t*>(p); p += 2 * 256;
+        L.emap = reinterpret_cast<uint16_t*>(p); p += 2 * 256;
+        L.lf = reinterpret_cast<uint16_t*>(p); p += 2 * 256;
+        L.slot_col = reinterpret_cast<uint16_t*>(p); p += 2 * a.max_rows_pad;
+        L.M = p;
+    }
+    for (uint32_t i = lane; i < 768; i += 64) lds[i] = a.explog[i];
+    for (uint32_t i = lane; i < 256; i += 64) {
+        L.first[i] = 0xFFFFFFFFu;
+        L.sys_slot[i] = 0xFFFF;
+    }
+    __syncthreads();
+    const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
+    const uint16_t* ridx = a.row_index + (uint64_t)g * a.max_rows;
+    bool bad = false;
+    for (uint32_t s = lane; s < n; s += 64) {
+        const uint32_t idx = ridx[s];
+        if (idx < k) atomicMin(&L.first[idx], s);
+        else if (idx - k >= 256) bad = true;
+    }
+    for (uint32_t s = lane; s < a.max_rows; s += 64) L.slot_col[s] = 0xFFFF;
+    __syncthreads();
+    int32_t status = 0;
+    if (__any(bad)) status = -1;  // QF_EINVAL
+    // Acceptance scan (first k candidate rows win).
+    uint32_t accepted = 0, nrep = 0, bound = 0;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t s0 = 0; s0 < n && accepted < k; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        uint32_t idx = 0;
+        bool cand = false;
+        if (s < n) {
+            idx = ridx[s];
+            cand = idx >= k ? (idx - k < 256) : (L.first[idx] == s);
+        }
+        const uint64_t bc = __ballot(cand);
+        const uint32_t pos = accepted + __popcll(bc & lt_mask);
+        const bool acc = cand && pos < k;
+        const bool isrep = acc && idx >= k;
+        const uint64_t br = __ballot(isrep);
+        const uint32_t rpos = nrep + __popcll(br & lt_mask);
+        if (acc) {
+            if (idx < k) L.sys_slot[idx] = (uint16_t)s;
+            else if (rpos < 256) L.rep_slot[rpos] = (uint16_t)s;
+        }
+        const uint64_t ba = __ballot(acc);
+        if (ba) bound = s0 + 64 - __builtin_clzll(ba);
+        accepted += __popcll(ba);
+        nrep += __popcll(br);
+    }
+    __syncthreads();
+    const uint32_t e = nrep;
+    if (status == 0 && accepted < k) status = -3;  // QF_ENOTREADY
+    if (status == 0 && e > emax) status = -1;      // more erasures than capacity
+    uint32_t W = k + e;
+    if (status == 0 && e > 0) {
+        // Erased list (ascending source index) and column map.
+        uint32_t ne = 0, np = 0;
+        for (uint32_t i0 = 0; i0 < k; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool miss = i < k && L.sys_slot[i] == 0xFFFF;
+            const bool pres = i < k && !miss;
+            const uint64_t bm = __ballot(miss), bp = __ballot(pres);
+            if (miss) {
+                const uint32_t p = ne + __popcll(bm & lt_mask);
+                L.emap[p] = (uint16_t)i;
+                L.col[i] = (uint16_t)p;
+            }
+            if (pres) {
+                const uint32_t p = np + __popcll(bp & lt_mask);
+                L.col[i] = (uint16_t)(e + p);
+                L.slot_col[L.sys_slot[i]] = (uint16_t)(e + p);
+            }
+            ne += __popcll(bm);
+            np += __popcll(bp);
+        }
+        for (uint32_t m = lane; m < e; m += 64) L.slot_col[L.rep_slot[m]] = (uint16_t)(k + m);
+        __syncthreads();
+        // Build M = [A_E | A_S | I_e].
+        bool erange = false;
+        for (uint32_t m = 0; m < e; ++m) {
+            const uint32_t s = L.rep_slot[m];
+            const uint32_t j = ridx[s] - k;
+            const uint8_t* rc = a.row_coeffs ? a.row_coeffs + ((uint64_t)g * a.max_rows + s) * k : nullptr;
+            const uint32_t y = (k + j) & 0xFF;
+            for (uint32_t i = lane; i < k; i += 64) {
+                uint8_t c;
+                if (rc) c = rc[i];
+                else {
+                    const uint32_t d = (i & 0xFF) ^ y;
+                    if (d == 0) { erange = true; c = 0; }
+                    else c = L.exp[255 - L.log[d]];
+                }
+                L.M[m * W + L.col[i]] = c;
+            }
+            for (uint32_t q = lane; q < e; q += 64) L.M[m * W + k + q] = (q == m) ? 1 : 0;
+        }
+        __syncthreads();
+        if (__any(erange)) status = -2;  // QF_ERANGE
+        // Gauss-Jordan on the first e columns.
+        for (uint32_t c = 0; c < e && status == 0; ++c) {
+            int32_t p = -1;
+            for (uint32_t r0 = c; r0 < e; r0 += 64) {
+                const uint32_t rr = r0 + lane;
+                const uint64_t b = __ballot(rr < e && L.M[rr * W + c] != 0);
+                if (b) { p = (int32_t)(r0 + __builtin_ctzll(b)); break; }
+            }
+            if (p < 0) { status = -4; break; }  // QF_ERANK
+            if ((uint32_t)p != c) {
+                for (uint32_t col = lane; col < W; col += 64) {
+                    const uint8_t t = L.M[c * W + col];
+                    L.M[c * W + col] = L.M[p * W + col];
+                    L.M[p * W + col] = t;
+                }
+                __syncthreads();
+            }
+            const uint8_t piv = L.M[c * W + c];
+            const uint8_t inv = L.exp[255 - L.log[piv]];
+            __syncthreads();
+            for (uint32_t col = lane; col < W; col += 64) L.M[c * W + col] = gmul(L, L.M[c * W + col], inv);
+            for (uint32_t m = lane; m < e; m += 64) {
+                const uint8_t f = L.M[m * W + c];
+                L.lf[m] = (m == c || f == 0) ? 0xFFFF : L.log[f];
+            }
+            __syncthreads();
+            for (uint32_t col = lane; col < W; col += 64) {
+                const uint8_t pv = L.M[c * W + col];
+                if (pv == 0) continue;
+                const uint32_t lp = L.log[pv];
+                for (uint32_t m = 0; m < e; ++m) {
+                    const uint32_t lfm = L.lf[m];
+                    if (lfm == 0xFFFF) continue;
+                    L.M[m * W + col] ^= L.exp[lfm + lp];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // Outputs.  Record layout per (pass, generation): max_rows slot records
+    // of 16 coefficient bytes, then one all-zero record (slot max_rows) that
+    // the payload pass reads for slots past a lane's bound.
+    if (lane < a.passes) {
+        uint8_t* out = a.coef_out + ((uint64_t)lane * a.G + g) * a.coef_gen_stride;
+        *reinterpret_cast<uint4*>(out + (uint64_t)a.max_rows * 16) = make_uint4(0, 0, 0, 0);
+    }
+    if (status == 0 && e > 0) {
+        for (uint32_t pass = 0; pass < a.passes; ++pass) {
+            uint8_t* out = a.coef_out + ((uint64_t)pass * a.G + g) * a.coef_gen_stride;
+            for (uint32_t s = lane; s < bound; s += 64) {
+                const uint32_t cl = L.slot_col[s];
+                uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const uint32_t m = pass * 16 + q;
+                    uint32_t v = 0;
+                    if (cl != 0xFFFF && m < e) v = L.M[m * W + cl];
+                    w[q >> 2] |= v << (8 * (q & 3));
+                }
+                *reinterpret_cast<uint4*>(out + (uint64_t)s * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+        for (uint32_t m = lane; m < e; m += 64) a.rec_index[(uint64_t)g * emax + m] = L.emap[m];
+    }
+    if (lane == 0) {
+        a.status[g] = status;
+        a.n_out[g] = status == 0 ? e : 0;
+        a.bound[g] = status == 0 ? bound : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Element-wise slice multiply and synthetic fill.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_mul_slice(const uint8_t* __restrict__ a,
+                                                   const uint8_t* __restrict__ b,
+                                                   uint8_t* __restrict__ out, uint64_t n,
+                                                   const uint8_t* __restrict__ explog) {
+    __shared__ uint8_t sexp[512];
+    __shared__ uint8_t slog[256];
+    for (uint32_t i = threadIdx.x; i < 768; i += blockDim.x) {
+        if (i < 512) sexp[i] = explog[i];
+        else slog[i - 512] = explog[i];
+    }
+    __syncthreads();
+    const uint64_t nvec = n / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nvec; w += stride) {
+        const uint4 va = reinterpret_cast<const uint4*>(a)[w];
+        const uint4 vb = reinterpret_cast<const uint4*>(b)[w];
+        uint4 r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t x = comp(va, c), y = comp(vb, c);
+            uint32_t o = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t xa = (x >> (8 * q)) & 0xFF, yb = (y >> (8 * q)) & 0xFF;
+                const uint32_t p = (xa && yb) ? sexp[(uint32_t)slog[xa] + slog[yb]] : 0u;
+                o |= p << (8 * q);
+            }
+            set_comp(r, c, o);
+        }
+        reinterpret_cast<uint4*>(out)[w] = r;
+    }
+    // tail bytes
+    const uint64_t t0 = nvec * 16;
+    for (uint64_t t = t0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        const uint32_t xa = a[t], yb = b[t];
+        out[t] = (xa && yb) ? sexp[(uint32_t)slog[xa] + slog[yb]] : 0;
+    }
+}
+
+QF_DEV uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_fill_splitmix(uint8_t* __restrict__ dst, uint64_t n,
+                                                       uint64_t seed, uint64_t word_offset) {
+    const uint64_t nw = n / 8;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const bool aligned = (reinterpret_cast<uintptr_t>(dst) & 7) == 0;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+        const uint64_t v = splitmix64(seed + word_offset + w);
+        if (aligned) {
+            reinterpret_cast<uint64_t*>(dst)[w] = v;
+        } else {
+            for (int q = 0; q < 8; ++q) dst[w * 8 + q] = (uint8_t)(v >> (8 * q));
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nw * 8 < n) {
+        const uint64_t v = splitmix64(seed + word_offset + nw);
+        for (uint64_t t = nw * 8; t < n; ++t) dst[t] = (uint8_t)(v >> (8 * (t - nw * 8)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launch wrappers (host).
+// ---------------------------------------------------------------------------
+template <int R, int V>
+static hipError_t launch_uniform_rv(const CombineUniformArgs& a, int num_cus, hipStream_t st) {
+    const size_t lds = (size_t)a.k_pad * R * 32;
+    auto kern = k_combine_uniform<R, V>;
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_done = true;
+    }
+    int occ = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lds);
+    if (e != hipSuccess) return e;
+    if (occ < 1) return hipErrorInvalidConfiguration;
+    const uint64_t waves = (a.total_units + 64 * V - 1) / (64 * V);
+    uint64_t blocks = (waves + 3) / 4;
+    const uint64_t cap = (uint64_t)num_cus * occ;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int num_cus,
+                                  hipStream_t st) {
+    if (V == 2) {
+        switch (R) {
+            case 1: return launch_uniform_rv<1, 2>(a, num_cus, st);
+            case 2: return launch_uniform_rv<2, 2>(a, num_cus, st);
+            case 4: return launch_uniform_rv<4, 2>(a, num_cus, st);
+            case 8: return launch_uniform_rv<8, 2>(a, num_cus, st);
+            case 16: return launch_uniform_rv<16, 2>(a, num_cus, st);
+        }
+    } else {
+        switch (R) {
+            case 1: return launch_uniform_rv<1, 1>(a, num_cus, st);
+            case 2: return launch_uniform_rv<2, 1>(a, num_cus, st);
+            case 4: return launch_uniform_rv<4, 1>(a, num_cus, st);
+            case 8: return launch_uniform_rv<8, 1>(a, num_cus, st);
+            case 16: return launch_uniform_rv<16, 1>(a, num_cus, st);
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_combine_slots(const CombineSlotsArgs& a, int num_cus, hipStream_t st) {
+    auto kern = k_combine_slots;
+    int occ = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0);
+    if (e != hipSuccess) return e;
+    if (occ < 1) occ = 1;
+    const uint64_t waves = (a.total_units + 63) / 64;
+    uint64_t blocks = (waves + 3) / 4;
+    const uint64_t cap = (uint64_t)num_cus * occ;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+size_t prepare_lds_bytes(uint32_t k, uint32_t e_max, uint32_t max_rows) {
+    const uint32_t max_rows_pad = (max_rows + 7) & ~7u;
+    return 768 + 4 * 256 + 2 * 256 * 5 + 2 * (size_t)max_rows_pad + (size_t)e_max * (k + e_max) + 16;
+}
+
+hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st) {
+    const size_t lds = prepare_lds_bytes(a.k, a.e_max, a.max_rows);
+    static bool attr_done = false;
+    if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_prepare),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr_done = true;
+    }
+    if (a.G == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_prepare, dim3(a.G), dim3(64), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n,
+                            const uint8_t* explog, int num_cus, hipStream_t st) {
+    uint64_t blocks = (n / 16 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    const uint64_t cap = (uint64_t)num_cus * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_mul_slice, dim3((uint32_t)blocks), dim3(256), 0, st, a, b, out, n, explog);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t word_offset,
+                                int num_cus, hipStream_t st) {
+    uint64_t blocks = (n / 8 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    const uint64_t cap = (uint64_t)num_cus * 8;
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL(k_fill_splitmix, dim3((uint32_t)blocks), dim3(256), 0, st, dst, n, seed,
+                       word_offset);
+    return hipGetLastError();
+}
+
+}  // namespace qf

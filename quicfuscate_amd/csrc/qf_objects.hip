@@ -1,0 +1,309 @@
+// qf_objects.hip -- per-connection Encoder / Decoder objects of the C ABI,
+// mirroring the reference's Rust API call for call (decoder.rs:155-299,
+// 658-791).  Payload state lives in HBM; each call is one batch launch of
+// the same kernels the batch API uses (G = 1 generation).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "gf256_tables.h"
+#include "qf_fec.h"
+
+#define QF_CHECK_HIP(expr)                         \
+    do {                                           \
+        hipError_t _e = (expr);                    \
+        if (_e != hipSuccess) return QF_EDEVICE;   \
+    } while (0)
+
+static inline uint32_t round16(uint32_t x) { return (x + 15) & ~15u; }
+
+struct qf_encoder {
+    qf_ctx* ctx = nullptr;
+    uint32_t k = 0, n = 0, max_len = 0, stride = 0;
+    uint8_t* d_ring = nullptr;  // k slots of `stride` bytes (zero padded)
+    uint8_t* d_out = nullptr;   // up to 256 repair rows
+    std::vector<uint32_t> lens;
+    std::vector<uint64_t> ids;
+    uint32_t count = 0;  // packets in the window (<= k)
+    uint32_t head = 0;   // next slot to write (== oldest slot once full)
+    std::vector<uint8_t> stage;
+};
+
+struct qf_decoder {
+    qf_ctx* ctx = nullptr;
+    uint32_t k = 0, max_len = 0, stride = 0;
+    bool decoded = false, drained = false;
+    // accepted rows, in arrival order (the first k win)
+    std::vector<uint8_t> rows;     // k * stride
+    std::vector<uint32_t> lens;    // k
+    std::vector<uint16_t> index;   // k: source index (< k) or k (repair)
+    std::vector<uint8_t> coeffs;   // k * k (repair rows)
+    std::vector<int32_t> sys_slot; // per source index: accepted slot or -1
+    uint32_t accepted = 0;
+    // decoded output, source index order
+    std::vector<uint8_t> out;      // k * stride
+    std::vector<uint32_t> out_len;
+    // device buffers for one generation
+    uint8_t* d_rows = nullptr;
+    uint8_t* d_coeffs = nullptr;
+    uint16_t* d_index = nullptr;
+    uint8_t* d_rec = nullptr;
+    uint16_t* d_rec_index = nullptr;
+    uint32_t* d_nrec = nullptr;
+    int32_t* d_status = nullptr;
+};
+
+extern "C" {
+
+int qf_encoder_new(qf_ctx* ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_encoder** out) {
+    if (!ctx || !out || k == 0 || k > 256 || n < k || max_len == 0) return QF_EINVAL;
+    qf_encoder* e = new qf_encoder();
+    e->ctx = ctx;
+    e->k = k;
+    e->n = n;
+    e->max_len = max_len;
+    e->stride = round16(max_len);
+    e->lens.assign(k, 0);
+    e->ids.assign(k, 0);
+    e->stage.assign(e->stride, 0);
+    if (hipMalloc(&e->d_ring, (size_t)k * e->stride) != hipSuccess ||
+        hipMalloc(&e->d_out, (size_t)256 * e->stride) != hipSuccess ||
+        hipMemset(e->d_ring, 0, (size_t)k * e->stride) != hipSuccess) {
+        qf_encoder_free(e);
+        return QF_ENOMEM;
+    }
+    *out = e;
+    return QF_OK;
+}
+
+int qf_encoder_free(qf_encoder* e) {
+    if (!e) return QF_OK;
+    if (e->d_ring) hipFree(e->d_ring);
+    if (e->d_out) hipFree(e->d_out);
+    delete e;
+    return QF_OK;
+}
+
+int qf_encoder_window_len(const qf_encoder* e) { return e ? (int)e->count : QF_EINVAL; }
+
+// decoder.rs:164-169: when the window holds k packets the oldest is dropped.
+int qf_encoder_add_source_packet(qf_encoder* e, uint64_t id, const uint8_t* data, uint32_t len) {
+    if (!e || (len && !data) || len > e->max_len) return QF_EINVAL;
+    memset(e->stage.data(), 0, e->stride);
+    if (len) memcpy(e->stage.data(), data, len);
+    const uint32_t slot = e->head;
+    QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)slot * e->stride, e->stage.data(), e->stride,
+                                hipMemcpyHostToDevice, (hipStream_t)qf_ctx_stream(e->ctx)));
+    QF_CHECK_HIP(hipStreamSynchronize((hipStream_t)qf_ctx_stream(e->ctx)));
+    e->lens[slot] = len;
+    e->ids[slot] = id;
+    e->head = (e->head + 1) % e->k;
+    if (e->count < e->k) e->count++;
+    return QF_OK;
+}
+
+int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, uint8_t* out_data,
+                                uint32_t out_stride, uint32_t* out_len, uint8_t* out_coeffs,
+                                uint64_t* out_ids) {
+    if (!e || count == 0 || count > 256) return QF_EINVAL;
+    if (e->count < e->k) return QF_ENOTREADY;  // decoder.rs:177-179 (None)
+    const uint32_t k = e->k;
+    const uint32_t oldest = e->head;  // window full: head is the oldest slot
+    const uint32_t L = e->lens[oldest];  // packet_len = window[0].len
+    const uint32_t newest = (e->head + k - 1) % k;
+    if (out_data && out_stride < L) return QF_ETOOSMALL;
+    // Cauchy rows first..first+count-1 in window order (decoder.rs:280-298)
+    std::vector<uint8_t> win((size_t)count * k), slotc((size_t)count * k);
+    const auto& f = qf::gf();
+    for (uint32_t q = 0; q < count; ++q) {
+        const uint8_t y = (uint8_t)(k + first + q);
+        for (uint32_t i = 0; i < k; ++i) {
+            uint8_t c;
+            if (!f.inv((uint8_t)((uint8_t)i ^ y), &c)) return QF_ERANGE;
+            win[(size_t)q * k + i] = c;
+            slotc[(size_t)q * k + (oldest + i) % k] = c;  // ring slot of window position i
+        }
+    }
+    if (L > 0) {
+        qf_encode_shape sh{};
+        sh.k = k;
+        sh.r = count;
+        sh.L = L;
+        sh.src_row_stride = e->stride;
+        sh.src_gen_stride = (uint64_t)k * e->stride;
+        sh.rep_row_stride = e->stride;
+        sh.rep_gen_stride = (uint64_t)count * e->stride;
+        int s = qf_encode_batch(e->ctx, &sh, 1, e->d_ring, e->d_out, slotc.data());
+        if (s != QF_OK) return s;
+        if (out_data) {
+            QF_CHECK_HIP(hipMemcpy2DAsync(out_data, out_stride, e->d_out, e->stride, L, count,
+                                          hipMemcpyDeviceToHost, (hipStream_t)qf_ctx_stream(e->ctx)));
+        }
+        QF_CHECK_HIP(hipStreamSynchronize((hipStream_t)qf_ctx_stream(e->ctx)));
+    }
+    for (uint32_t q = 0; q < count; ++q) {
+        if (out_len) out_len[q] = L;
+        if (out_ids) out_ids[q] = e->ids[newest] + 1 + first + q;  // decoder.rs:267
+        if (out_coeffs) memcpy(out_coeffs + (size_t)q * k, win.data() + (size_t)q * k, k);
+    }
+    return QF_OK;
+}
+
+int qf_encoder_generate_repair_packet(qf_encoder* e, uint32_t j, uint8_t* out_data, uint32_t out_cap,
+                                      uint32_t* out_len, uint8_t* out_coeffs, uint64_t* out_id) {
+    if (!e) return QF_EINVAL;
+    if (e->count < e->k) return QF_ENOTREADY;
+    const uint32_t L = e->lens[e->head];
+    if (out_data && out_cap < L) return QF_ETOOSMALL;
+    return qf_encoder_generate_repairs(e, j, 1, out_data, out_cap, out_len, out_coeffs, out_id);
+}
+
+int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) {
+    if (!ctx || !out || k == 0 || k > 256 || max_len == 0) return QF_EINVAL;
+    qf_decoder* d = new qf_decoder();
+    d->ctx = ctx;
+    d->k = k;
+    d->max_len = max_len;
+    d->stride = round16(max_len);
+    d->rows.assign((size_t)k * d->stride, 0);
+    d->lens.assign(k, 0);
+    d->index.assign(k, 0);
+    d->coeffs.assign((size_t)k * k, 0);
+    d->sys_slot.assign(k, -1);
+    const uint32_t emax = k < 128 ? k : 128;
+    bool ok = hipMalloc(&d->d_rows, (size_t)k * d->stride) == hipSuccess &&
+              hipMalloc(&d->d_coeffs, (size_t)k * k) == hipSuccess &&
+              hipMalloc(&d->d_index, (size_t)k * 2) == hipSuccess &&
+              hipMalloc(&d->d_rec, (size_t)emax * d->stride) == hipSuccess &&
+              hipMalloc(&d->d_rec_index, (size_t)emax * 2) == hipSuccess &&
+              hipMalloc(&d->d_nrec, 4) == hipSuccess && hipMalloc(&d->d_status, 4) == hipSuccess;
+    if (!ok) {
+        qf_decoder_free(d);
+        return QF_ENOMEM;
+    }
+    *out = d;
+    return QF_OK;
+}
+
+int qf_decoder_free(qf_decoder* d) {
+    if (!d) return QF_OK;
+    hipFree(d->d_rows);
+    hipFree(d->d_coeffs);
+    hipFree(d->d_index);
+    hipFree(d->d_rec);
+    hipFree(d->d_rec_index);
+    hipFree(d->d_nrec);
+    hipFree(d->d_status);
+    delete d;
+    return QF_OK;
+}
+
+int qf_decoder_is_decoded(const qf_decoder* d) { return d ? (d->decoded ? 1 : 0) : QF_EINVAL; }
+
+// decoder.rs:704-783 for the k accepted rows, on the device.
+static int decoder_try_decode(qf_decoder* d) {
+    const uint32_t k = d->k;
+    uint32_t L = 0;
+    for (uint32_t q = 0; q < k; ++q) L = d->lens[q] > L ? d->lens[q] : L;
+    if (L == 0) L = 1;
+    hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows, d->rows.data(), (size_t)k * d->stride, hipMemcpyHostToDevice, st));
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_index, d->index.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
+    const uint32_t emax = k < 128 ? k : 128;
+    qf_decode_shape sh{};
+    sh.k = k;
+    sh.r = emax;
+    sh.L = L;
+    sh.max_rows = k;
+    sh.row_stride = d->stride;
+    sh.rows_gen_stride = (uint64_t)k * d->stride;
+    sh.rec_row_stride = d->stride;
+    sh.rec_gen_stride = (uint64_t)emax * d->stride;
+    int s = qf_decode_batch(d->ctx, &sh, 1, d->d_rows, d->d_index, nullptr, d->d_coeffs, d->d_rec,
+                            d->d_rec_index, d->d_nrec, d->d_status);
+    if (s != QF_OK) return s;
+    int32_t status = 0;
+    uint32_t nrec = 0;
+    QF_CHECK_HIP(hipMemcpyAsync(&status, d->d_status, 4, hipMemcpyDeviceToHost, st));
+    QF_CHECK_HIP(hipMemcpyAsync(&nrec, d->d_nrec, 4, hipMemcpyDeviceToHost, st));
+    QF_CHECK_HIP(hipStreamSynchronize(st));
+    if (status != QF_OK) return status;  // singular: stays undecoded (decoder.rs:756-758)
+    std::vector<uint16_t> ridx(nrec);
+    std::vector<uint8_t> rec((size_t)nrec * d->stride);
+    if (nrec) {
+        QF_CHECK_HIP(hipMemcpyAsync(ridx.data(), d->d_rec_index, (size_t)nrec * 2, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipMemcpyAsync(rec.data(), d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipStreamSynchronize(st));
+    }
+    d->out.assign((size_t)k * d->stride, 0);
+    d->out_len.assign(k, 0);
+    for (uint32_t i = 0; i < k; ++i) {
+        const int32_t q = d->sys_slot[i];
+        if (q >= 0) {
+            memcpy(&d->out[(size_t)i * d->stride], &d->rows[(size_t)q * d->stride], d->stride);
+            d->out_len[i] = d->lens[q];
+        }
+    }
+    for (uint32_t m = 0; m < nrec; ++m) {
+        const uint32_t i = ridx[m];
+        memcpy(&d->out[(size_t)i * d->stride], &rec[(size_t)m * d->stride], L);
+        d->out_len[i] = L;
+    }
+    d->decoded = true;
+    return QF_OK;
+}
+
+int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const uint8_t* data,
+                          uint32_t len, const uint8_t* coeffs, uint32_t coeff_len) {
+    if (!d || (len && !data)) return QF_EINVAL;
+    if (len > d->max_len) return QF_EINVAL;
+    // decoder.rs:679-681
+    if (d->decoded || d->accepted >= d->k) return d->decoded ? 1 : 0;
+    const uint32_t k = d->k;
+    const uint32_t q = d->accepted;
+    if (is_systematic) {
+        const uint32_t idx = (uint32_t)(id % k);  // decoder.rs:684
+        if (d->sys_slot[idx] >= 0) return d->decoded ? 1 : 0;  // duplicate (687-691)
+        d->sys_slot[idx] = (int32_t)q;
+        d->index[q] = (uint16_t)idx;
+        memset(&d->coeffs[(size_t)q * k], 0, k);
+    } else {
+        if (!coeffs) return QF_EINVAL;  // "Repair packet missing coefficients."
+        d->index[q] = (uint16_t)k;
+        memset(&d->coeffs[(size_t)q * k], 0, k);
+        memcpy(&d->coeffs[(size_t)q * k], coeffs, coeff_len < k ? coeff_len : k);
+    }
+    memset(&d->rows[(size_t)q * d->stride], 0, d->stride);
+    if (len) memcpy(&d->rows[(size_t)q * d->stride], data, len);
+    d->lens[q] = len;
+    d->accepted++;
+    if (d->accepted == k) {
+        int s = decoder_try_decode(d);
+        if (s == QF_ERANK) return 0;
+        if (s != QF_OK) return s;
+    }
+    return d->decoded ? 1 : 0;
+}
+
+int qf_decoder_get_decoded_packets(qf_decoder* d, uint8_t* out_data, uint32_t out_stride,
+                                   uint32_t* out_len, uint64_t* out_ids, uint32_t* count) {
+    if (!d || !count) return QF_EINVAL;
+    *count = 0;
+    if (!d->decoded || d->drained) return QF_OK;
+    uint32_t need = 0;
+    for (uint32_t i = 0; i < d->k; ++i) need = d->out_len[i] > need ? d->out_len[i] : need;
+    if (out_data && out_stride < need) return QF_ETOOSMALL;
+    for (uint32_t i = 0; i < d->k; ++i) {
+        if (out_data) memcpy(out_data + (size_t)i * out_stride, &d->out[(size_t)i * d->stride], d->out_len[i]);
+        if (out_len) out_len[i] = d->out_len[i];
+        if (out_ids) out_ids[i] = i;  // decoder.rs:771
+    }
+    *count = d->k;
+    d->drained = true;  // get_decoded_packets take()s the packets
+    return QF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""ctypes wrapper of oracle/build/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of src/fec (oracle/qf_oracle.c) used as the parity
+checker.  Never imported by the product package.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "oracle" / "build" / "liboracle.so"
+_lib = ctypes.CDLL(str(_LIB_PATH))
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_SZ = ctypes.c_size_t
+_lib.oracle_gf_mul.restype = ctypes.c_uint8
+_lib.oracle_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+_lib.oracle_gf_mul_shift.restype = ctypes.c_uint8
+_lib.oracle_gf_mul_shift.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+_lib.oracle_gf_mul_clmul_fold.restype = ctypes.c_uint8
+_lib.oracle_gf_mul_clmul_fold.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+_lib.oracle_gf_inv.argtypes = [ctypes.c_uint8, _P]
+_lib.oracle_gf_tables.argtypes = [_P, _P]
+_lib.oracle_gf_mul_slice.argtypes = [_P, _P, _P, _SZ]
+_lib.oracle_cauchy_coeffs.argtypes = [_U32, _U32, _P]
+_lib.oracle_encode_window.argtypes = [_U32, _U32, _U32, _P, _SZ, _P, _P, _SZ]
+_lib.oracle_encode_window_clmul_fold.argtypes = [_U32, _U32, _U32, _P, _SZ, _P, _P, _SZ]
+_lib.oracle_decode_generation.argtypes = [_U32, _U32, _U32, _P, _P, _SZ, _P, _P, _SZ, _P]
+_lib.oracle_decode_generation_as_written.argtypes = [_U32, _U32, _U32, _P, _P, _SZ, _P, _P, _SZ]
+_lib.oracle_fill_splitmix.argtypes = [_P, _SZ, ctypes.c_uint64, ctypes.c_uint64]
+_lib.oracle_gf_init()
+
+OK, ENOTREADY, ERANK, EINVAL, ERANGE = 0, -3, -4, -1, -2
+
+
+def _p(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data
+
+
+def tables() -> tuple[np.ndarray, np.ndarray]:
+    e = np.zeros(512, np.uint8)
+    lg = np.zeros(256, np.uint8)
+    _lib.oracle_gf_tables(_p(e), _p(lg))
+    return e, lg
+
+
+def mul(a: int, b: int) -> int:
+    return int(_lib.oracle_gf_mul(a, b))
+
+
+def mul_shift(a: int, b: int) -> int:
+    return int(_lib.oracle_gf_mul_shift(a, b))
+
+
+def mul_clmul_fold(a: int, b: int) -> int:
+    return int(_lib.oracle_gf_mul_clmul_fold(a, b))
+
+
+def mul_table_full() -> np.ndarray:
+    """256 x 256 product table via oracle_gf_mul_slice."""
+    a = np.repeat(np.arange(256, dtype=np.uint8), 256)
+    b = np.tile(np.arange(256, dtype=np.uint8), 256)
+    out = np.zeros(65536, np.uint8)
+    _lib.oracle_gf_mul_slice(_p(a), _p(b), _p(out), 65536)
+    return out.reshape(256, 256)
+
+
+def inv(a: int) -> int | None:
+    o = ctypes.c_uint8(0)
+    return None if _lib.oracle_gf_inv(a, ctypes.byref(o)) else int(o.value)
+
+
+def cauchy(k: int, r: int) -> np.ndarray | None:
+    out = np.zeros((r, k), np.uint8)
+    return None if _lib.oracle_cauchy_coeffs(k, r, _p(out)) else out
+
+
+def encode(src: np.ndarray, r: int, coeff: np.ndarray | None = None, L: int | None = None) -> np.ndarray:
+    """src: (k, stride) uint8 rows -> (r, L) repairs (decoder.rs:172-275)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    k, stride = src.shape
+    L = stride if L is None else L
+    rep = np.zeros((r, max(L, 1)), np.uint8)
+    c = None if coeff is None else np.ascontiguousarray(coeff, dtype=np.uint8)
+    s = _lib.oracle_encode_window(k, r, L, _p(src), stride, _p(c), _p(rep), rep.shape[1])
+    if s != 0:
+        raise ValueError(f"oracle encode status {s}")
+    return rep[:, :L]
+
+
+def encode_clmul_fold(src: np.ndarray, r: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    k, L = src.shape
+    rep = np.zeros((r, L), np.uint8)
+    _lib.oracle_encode_window_clmul_fold(k, r, L, _p(src), L, None, _p(rep), L)
+    return rep
+
+
+def decode(k: int, row_index, rows: np.ndarray, row_coeffs: np.ndarray | None = None):
+    """rows: (n, L) in arrival order -> (status, out (k, L), received mask)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    n, L = rows.shape
+    ri = np.ascontiguousarray(row_index, dtype=np.uint16)
+    out = np.zeros((k, max(L, 1)), np.uint8)
+    mask = np.zeros(k, np.uint8)
+    rc = None if row_coeffs is None else np.ascontiguousarray(row_coeffs, dtype=np.uint8)
+    s = _lib.oracle_decode_generation(k, L, n, _p(ri), _p(rows), L, _p(rc), _p(out), out.shape[1], _p(mask))
+    return s, out[:, :L], mask
+
+
+def decode_as_written(k: int, row_index, rows: np.ndarray):
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    n, L = rows.shape
+    ri = np.ascontiguousarray(row_index, dtype=np.uint16)
+    out = np.zeros((k, L), np.uint8)
+    s = _lib.oracle_decode_generation_as_written(k, L, n, _p(ri), _p(rows), L, None, _p(out), L)
+    return s, out
+
+
+def fill_splitmix(n: int, seed: int, word_offset: int = 0) -> np.ndarray:
+    out = np.zeros(n, np.uint8)
+    _lib.oracle_fill_splitmix(_p(out), n, seed, word_offset)
+    return out

@@ -1,0 +1,160 @@
+"""Decode parity on the MI355X: k_decode_prepare + k_combine_slots vs the
+CPU oracle (decoder.rs:658-791 with the F4 fix).  Recovered rows must be the
+original source bytes and equal the oracle's solution; statuses must match
+(ENOTREADY, ERANK)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _r16(x):
+    return (x + 15) // 16 * 16
+
+
+def make_batch(oracle, rng, k, r, L, G, max_rows, *, dup_prob=0.0, shuffle=True, erase=None,
+               coeff_mode="cauchy"):
+    """Per generation: source rows, repairs, an arrival list (row index per slot)."""
+    src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
+    gens = []
+    for g in range(G):
+        if coeff_mode == "cauchy":
+            C = oracle.cauchy(k, r)
+        else:
+            C = rng.integers(0, 256, (r, k), dtype=np.uint8)
+        rep = oracle.encode(src[g], r, C)
+        e = rng.integers(0, min(k, r) + 1) if erase is None else erase
+        erased = set(rng.choice(k, size=e, replace=False).tolist())
+        arr = [i for i in range(k) if i not in erased] + [k + j for j in range(r)]
+        if shuffle:
+            rng.shuffle(arr)
+        if dup_prob:
+            extra = [a for a in arr if rng.random() < dup_prob]
+            for a in extra:
+                arr.insert(int(rng.integers(0, len(arr) + 1)), a)
+        arr = arr[:max_rows]
+        rows = np.stack([src[g, a] if a < k else rep[a - k] for a in arr]) if arr else np.zeros((0, L), np.uint8)
+        rc = np.stack([np.zeros(k, np.uint8) if a < k else C[a - k] for a in arr]) if arr else None
+        gens.append((arr, rows, rc))
+    return src, gens
+
+
+def run_decode(qf, k, r, L, G, max_rows, gens, with_coeffs):
+    import torch
+
+    rs = _r16(L) + 16
+    rgs = max_rows * rs
+    emax = min(k, r)
+    rrs = _r16(L) + 16
+    rec_gs = emax * rrs + 32
+    rows = np.zeros(G * rgs, np.uint8)
+    ridx = np.zeros((G, max_rows), np.uint16)
+    nrows = np.zeros(G, np.uint32)
+    rcoef = np.zeros((G, max_rows, k), np.uint8)
+    for g, (arr, rw, rc) in enumerate(gens):
+        nrows[g] = len(arr)
+        ridx[g, : len(arr)] = arr
+        for s in range(len(arr)):
+            rows[g * rgs + s * rs: g * rgs + s * rs + L] = rw[s]
+            if rc is not None:
+                rcoef[g, s] = rc[s]
+    dev = "cuda"
+    t_rows = torch.from_numpy(rows).to(dev)
+    t_idx = torch.from_numpy(ridx.view(np.int16)).to(dev)
+    t_n = torch.from_numpy(nrows.view(np.int32)).to(dev)
+    t_coef = torch.from_numpy(rcoef.reshape(-1)).to(dev) if with_coeffs else None
+    t_rec = torch.full((G * rec_gs + 64,), 0x5A, dtype=torch.uint8, device=dev)
+    t_recidx = torch.zeros(G * max(emax, 1), dtype=torch.int16, device=dev)
+    t_nrec = torch.zeros(G, dtype=torch.int32, device=dev)
+    t_status = torch.full((G,), 77, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    qf.decode_batch(t_rows, t_idx, t_rec, t_recidx, t_nrec, t_status, k, r, L, max_rows=max_rows,
+                    row_stride=rs, rows_gen_stride=rgs, rec_row_stride=rrs, rec_gen_stride=rec_gs,
+                    G=G, n_rows=t_n, row_coeffs=t_coef)
+    qf.default_context().sync()
+    return (t_rec.cpu().numpy(), t_recidx.cpu().numpy().view(np.uint16).reshape(G, -1),
+            t_nrec.cpu().numpy(), t_status.cpu().numpy(), rrs, rec_gs)
+
+
+def check(oracle, k, L, src, gens, out, with_coeffs):
+    rec, recidx, nrec, status, rrs, rec_gs = out
+    for g, (arr, rw, rc) in enumerate(gens):
+        st, sol, mask = oracle.decode(k, arr, rw if len(arr) else np.zeros((0, L), np.uint8),
+                                      rc if with_coeffs else None)
+        assert status[g] == st, (g, status[g], st)
+        if st != 0:
+            assert nrec[g] == 0
+            continue
+        erased = [i for i in range(k) if not mask[i]]
+        assert nrec[g] == len(erased)
+        assert list(recidx[g, : nrec[g]]) == erased
+        for m, i in enumerate(erased):
+            got = rec[g * rec_gs + m * rrs: g * rec_gs + m * rrs + L]
+            assert (got == sol[i]).all(), (g, i)
+            assert (got == src[g, i]).all(), (g, i)
+            assert (rec[g * rec_gs + m * rrs + L: g * rec_gs + (m + 1) * rrs] == 0x5A).all()
+
+
+@pytest.mark.parametrize("k,r,L,G", [(64, 16, 1200, 40), (16, 16, 100, 30), (4, 2, 8, 20),
+                                     (10, 2, 8, 20), (33, 7, 37, 25), (1, 3, 16, 10)])
+def test_decode_matches_oracle_random_erasures(qf, oracle, gpu_ctx, k, r, L, G):
+    rng = np.random.default_rng(k + r + L)
+    max_rows = k + r
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows)
+    out = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+
+
+def test_decode_bench_shape_fixed_13_erasures(qf, oracle, gpu_ctx):
+    # k=64, 13 erased sources, arrival = surviving sources then repairs
+    rng = np.random.default_rng(2024)
+    k, r, L, G = 64, 16, 1200, 24
+    src, gens = make_batch(oracle, rng, k, r, L, G, k - 13 + r, shuffle=False, erase=13)
+    out = run_decode(qf, k, r, L, G, k - 13 + r, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+
+
+def test_decode_explicit_coefficients_and_duplicates(qf, oracle, gpu_ctx):
+    # random coefficient matrices (some singular) + duplicate arrivals
+    rng = np.random.default_rng(7)
+    k, r, L, G = 12, 8, 64, 60
+    max_rows = 40
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, dup_prob=0.15, coeff_mode="random")
+    out = run_decode(qf, k, r, L, G, max_rows, gens, True)
+    check(oracle, k, L, src, gens, out, True)
+    assert set(out[3].tolist()) >= {0}
+
+
+def test_decode_not_enough_rows_and_singular(qf, oracle, gpu_ctx):
+    rng = np.random.default_rng(3)
+    k, r, L = 8, 4, 48
+    src = rng.integers(0, 256, (3, k, L), dtype=np.uint8)
+    C = oracle.cauchy(k, r)
+    gens = []
+    rep0 = oracle.encode(src[0], r)
+    gens.append(([0, 1, 2, 8], np.vstack([src[0, :3], rep0[:1]]), None))             # ENOTREADY
+    rep1 = oracle.encode(src[1], r)
+    gens.append(([0, 1, 2, 3, 4, 5, 8, 8, 9], np.vstack([src[1, :6], rep1[0], rep1[0], rep1[1]]), None))  # ERANK
+    rep2 = oracle.encode(src[2], r)
+    gens.append(([8, 9, 10, 11, 0, 1, 2, 3, 4, 5], np.vstack([rep2, src[2, :6]]), None))  # OK, e = 4
+    out = run_decode(qf, k, r, L, 3, 12, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+    assert list(out[3]) == [-3, -4, 0]
+
+
+def test_decode_many_erasures_multi_pass(qf, oracle, gpu_ctx):
+    # e > 16 -> several 16-row payload passes
+    rng = np.random.default_rng(11)
+    k, r, L, G = 40, 40, 80, 12
+    src, gens = make_batch(oracle, rng, k, r, L, G, k + r, erase=33)
+    out = run_decode(qf, k, r, L, G, k + r, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+
+
+def test_decode_no_erasures(qf, oracle, gpu_ctx):
+    rng = np.random.default_rng(12)
+    k, r, L, G = 16, 4, 32, 5
+    src, gens = make_batch(oracle, rng, k, r, L, G, k + r, erase=0)
+    out = run_decode(qf, k, r, L, G, k + r, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+    assert (out[2] == 0).all()

@@ -1,0 +1,139 @@
+"""Encode parity on the MI355X: k_combine_uniform vs the CPU oracle.
+
+Bit-exact comparison of every repair byte, plus the bytes around each repair
+row (the library must write exactly L bytes per row)."""
+import hashlib
+import json
+import os
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.loads((Path(__file__).parent / "golden" / "golden.json").read_text())
+
+
+def _r16(x):
+    return (x + 15) // 16 * 16
+
+
+def run_encode(qf, src_np, k, r, L, G, rs, gs, rrs, rgs, coeff=None):
+    import torch
+
+    dev = torch.device("cuda")
+    src = torch.from_numpy(src_np).to(dev)
+    rep = torch.full((G * rgs + 64,), 0xA5, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    qf.encode_batch(src, rep, k, r, L, src_row_stride=rs, src_gen_stride=gs, rep_row_stride=rrs,
+                    rep_gen_stride=rgs, G=G, coeff=coeff)
+    qf.default_context().sync()
+    return rep.cpu().numpy()
+
+
+CASES = [
+    # k, r, L, G
+    (64, 16, 1200, 37),    # the benchmark shape
+    (16, 16, 1200, 5),
+    (16, 1, 1200, 9),      # Light mode params_for(Light,16) = (16,17)
+    (4, 2, 8, 3),          # tests/fec.rs make_packet shape
+    (7, 5, 33, 11),        # odd k, odd r, tail unit
+    (1, 1, 16, 2),
+    (3, 3, 1, 130),        # 1-byte packets, many generations per wave
+    (255, 1, 64, 2),       # largest k
+    (200, 56, 48, 1),      # k + r = 256 (largest valid), 4 passes
+    (64, 40, 100, 3),      # r > 16 -> passes of 16
+    (96, 15, 9000, 2),     # jumbo payload (Normal ratio 1.15: r = 15 at k = 96)
+    (63, 16, 1201, 7),     # k % 4 = 3, L % 16 = 1
+]
+
+
+@pytest.mark.parametrize("k,r,L,G", CASES)
+@pytest.mark.parametrize("V", ["1", "2"])
+def test_encode_matches_oracle(qf, oracle, gpu_ctx, k, r, L, G, V, monkeypatch):
+    monkeypatch.setenv("QF_ENCODE_V", V)
+    rng = np.random.default_rng(k * 1000 + r * 10 + L)
+    rs = _r16(L) + (16 if k % 2 else 0)
+    gs = k * rs + 32
+    rrs = _r16(L) + 16
+    rgs = r * rrs + 48
+    src = rng.integers(0, 256, G * gs, dtype=np.uint8)
+    rep = run_encode(qf, src, k, r, L, G, rs, gs, rrs, rgs)
+    for g in range(G):
+        rows = np.stack([src[g * gs + i * rs: g * gs + i * rs + L] for i in range(k)])
+        want = oracle.encode(rows, r)
+        for j in range(r):
+            off = g * rgs + j * rrs
+            assert (rep[off: off + L] == want[j]).all(), (g, j)
+            assert (rep[off + L: off + rrs] == 0xA5).all(), "bytes past L written"
+        assert (rep[g * rgs + r * rrs: (g + 1) * rgs] == 0xA5).all()
+
+
+def test_encode_custom_coefficients(qf, oracle, gpu_ctx):
+    rng = np.random.default_rng(5)
+    k, r, L, G = 20, 9, 200, 6
+    coeff = rng.integers(0, 256, (r, k), dtype=np.uint8)
+    coeff[0, :] = 0
+    coeff[1, 3] = 1
+    rs = _r16(L)
+    src = rng.integers(0, 256, G * k * rs, dtype=np.uint8)
+    rep = run_encode(qf, src, k, r, L, G, rs, k * rs, rs, r * rs, coeff=coeff.tobytes())
+    for g in range(G):
+        rows = src[g * k * rs:(g + 1) * k * rs].reshape(k, rs)[:, :L]
+        want = oracle.encode(rows, r, coeff)
+        got = rep[g * r * rs:(g + 1) * r * rs].reshape(r, rs)[:, :L]
+        assert (got == want).all()
+
+
+def test_encode_golden_pattern_hashes(qf, gpu_ctx):
+    for k in (16, 64):
+        L = 1200
+        i = np.arange(k)[:, None]
+        t = np.arange(L)[None, :]
+        src = ((7 * i + 13 * t + 1) & 255).astype(np.uint8).reshape(-1)
+        rep = run_encode(qf, src, k, 16, L, 1, L, k * L, L, 16 * L)
+        h = hashlib.sha256(rep[: 16 * L].tobytes()).hexdigest()[:32]
+        assert h == GOLDEN["encode"][f"k{k}_r16_L1200_pattern"]["rep_sha"]
+
+
+def test_encode_sliding_window_layout(qf, oracle, gpu_ctx):
+    # adaptive.rs:519-562: after every source packet, n-k repairs over the
+    # last k packets -> overlapping generations (gen stride = row stride).
+    rng = np.random.default_rng(9)
+    k, r, L, P = 16, 3, 96, 40
+    rs = _r16(L)
+    stream = rng.integers(0, 256, P * rs, dtype=np.uint8)
+    G = P - k + 1
+    rep = run_encode(qf, stream, k, r, L, G, rs, rs, rs, r * rs)
+    for p in range(G):
+        rows = stream[p * rs:(p + k) * rs].reshape(k, rs)[:, :L]
+        want = oracle.encode(rows, r)
+        got = rep[p * r * rs:(p + 1) * r * rs].reshape(r, rs)[:, :L]
+        assert (got == want).all(), p
+
+
+def test_encode_errors(qf, gpu_ctx):
+    import torch
+
+    buf = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(qf.QfError) as e:  # Cauchy undefined: k + r > 256
+        qf.encode_batch(buf, buf, 250, 10, 16, src_row_stride=16, src_gen_stride=4000,
+                        rep_row_stride=16, rep_gen_stride=160, G=1)
+    assert e.value.status == -2
+    with pytest.raises(qf.QfError):  # misaligned stride
+        qf.encode_batch(buf, buf, 4, 2, 16, src_row_stride=17, src_gen_stride=68,
+                        rep_row_stride=16, rep_gen_stride=32, G=1)
+
+
+def test_gf_mul_slice_exhaustive_matches_table(qf, oracle, gpu_ctx):
+    # tests/fec.rs:262-307 bitsliced_mul_matches_table / *_kernel_matches_table:
+    # the device multiply equals gf_mul_table for all 65,536 pairs.
+    a = np.repeat(np.arange(256, dtype=np.uint8), 256)
+    b = np.tile(np.arange(256, dtype=np.uint8), 256)
+    got = np.frombuffer(qf.gf_mul_slice(a.tobytes(), b.tobytes()), np.uint8).reshape(256, 256)
+    assert (got == oracle.mul_table_full()).all()
+    # benches/gf_mul_slice_bench.rs inputs (1024 bytes, a=i, b=255-i) and a ragged length
+    a = (np.arange(1029) & 255).astype(np.uint8)
+    b = (255 - np.arange(1029)).astype(np.uint8)
+    got = np.frombuffer(qf.gf_mul_slice(a.tobytes(), b.tobytes()), np.uint8)
+    assert all(int(got[i]) == oracle.mul(int(a[i]), int(b[i])) for i in range(1029))

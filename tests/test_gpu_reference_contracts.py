@@ -1,0 +1,132 @@
+"""The reference's own FEC tests, restated through the Python mirror of its
+API (quicfuscate_amd.fec), running on the MI355X library.
+
+tests/fec.rs and src/fec/mod.rs build packets with make_packet(id, val):
+8 bytes of `val` in a pool block (tests/fec.rs:5-18) and assert that
+out[i].data[0] == i after encode/erase/decode."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def make_packet(qf, pid, val, pool):
+    buf = pool.alloc()
+    buf[:8] = bytes([val & 0xFF]) * 8
+    return qf.Packet(pid, buf, 8, True)
+
+
+def _roundtrip(qf, k, n, keep_src, keep_rep, val=lambda i: i):
+    qf.init_gf_tables()
+    pool = qf.MemoryPool(64, 64)
+    enc = qf.Encoder(k, n, max_len=64)
+    packets = []
+    for i in range(k):
+        p = make_packet(qf, i, val(i), pool)
+        enc.add_source_packet(p.clone())
+        packets.append(p)
+    repairs = [enc.generate_repair_packet(i, pool) for i in range(n - k)]
+    assert all(r is not None for r in repairs)
+    dec = qf.Decoder(k, pool)
+    for i, p in enumerate(packets):
+        if keep_src(i):
+            dec.add_packet(p.clone())
+    for j, r in enumerate(repairs):
+        if keep_rep(j):
+            dec.add_packet(r)
+    return dec, packets, repairs
+
+
+def test_gf8_encode_decode(qf, gpu_ctx):
+    # tests/fec.rs:20-50
+    dec, _, _ = _roundtrip(qf, 4, 6, lambda i: i != 1, lambda j: True)
+    assert dec.is_decoded
+    out = dec.get_decoded_packets()
+    assert len(out) == 4
+    for i in range(4):
+        assert out[i].data[0] == i
+        assert bytes(out[i].data[:8]) == bytes([i]) * 8
+
+
+def test_gaussian_path_decodes(qf, gpu_ctx):
+    # src/fec/mod.rs:107-139 (drop packet 2)
+    dec, _, _ = _roundtrip(qf, 4, 6, lambda i: i != 2, lambda j: True)
+    assert dec.is_decoded
+    out = dec.get_decoded_packets()
+    assert [p.data[0] for p in out] == [0, 1, 2, 3]
+
+
+def test_repair_known_answer(qf, gpu_ctx):
+    # SURVEY 8(c) KAT: repairs of the k=4 make_packet window are [128]*8, [160]*8
+    _, _, repairs = _roundtrip(qf, 4, 6, lambda i: True, lambda j: False)
+    assert bytes(repairs[0].data[:8]) == bytes([128]) * 8
+    assert bytes(repairs[1].data[:8]) == bytes([160]) * 8
+    assert repairs[0].coefficients == bytes([71, 167, 122, 186])
+    assert repairs[0].id == 3 + 1 + 0 and repairs[1].id == 3 + 1 + 1   # decoder.rs:267
+
+
+def test_recovery_low_loss(qf, gpu_ctx):
+    # src/fec/mod.rs:295-322
+    dec, _, _ = _roundtrip(qf, 10, 12, lambda i: i != 3, lambda j: True)
+    assert dec.is_decoded
+
+
+def test_recovery_high_loss(qf, gpu_ctx):
+    # src/fec/mod.rs:324-353
+    dec, _, _ = _roundtrip(qf, 16, 32, lambda i: i % 2 == 0, lambda j: j % 3 != 0, val=lambda i: i % 255)
+    assert dec.is_decoded
+    out = dec.get_decoded_packets()
+    assert [p.data[0] for p in out] == list(range(16))
+    assert dec.get_decoded_packets() == []  # drained (take())
+
+
+def test_window_not_full_returns_none(qf, gpu_ctx):
+    # decoder.rs:177-179
+    pool = qf.MemoryPool(8, 64)
+    enc = qf.Encoder(4, 6, max_len=64)
+    enc.add_source_packet(make_packet(qf, 0, 0, pool))
+    assert enc.generate_repair_packet(0, pool) is None
+
+
+def test_sliding_window_slides(qf, oracle, gpu_ctx):
+    # decoder.rs:164-169: the oldest packet leaves once k are held
+    import numpy as np
+
+    pool = qf.MemoryPool(8, 64)
+    enc = qf.Encoder(4, 5, max_len=64)
+    for i in range(7):
+        enc.add_source_packet(make_packet(qf, i, 10 + i, pool))
+    rep = enc.generate_repair_packet(0, pool)
+    window = np.stack([np.full(8, 10 + i, np.uint8) for i in range(3, 7)])
+    assert bytes(rep.data[:8]) == oracle.encode(window, 1)[0].tobytes()
+    assert rep.id == 6 + 1
+
+
+def test_repair_without_coefficients_is_an_error(qf, gpu_ctx):
+    # decoder.rs:699 Err("Repair packet missing coefficients.")
+    dec = qf.Decoder(4, qf.MemoryPool(8, 64))
+    with pytest.raises(qf.QfError):
+        dec.add_packet(qf.Packet(9, bytearray(8), 8, False))
+
+
+def test_duplicate_systematic_ignored(qf, gpu_ctx):
+    # decoder.rs:687-691
+    pool = qf.MemoryPool(16, 64)
+    dec = qf.Decoder(4, pool)
+    p = make_packet(qf, 1, 1, pool)
+    assert not dec.add_packet(p.clone())
+    assert not dec.add_packet(p.clone())
+    for i in (0, 2, 3):
+        dec.add_packet(make_packet(qf, i, i, pool))
+    assert dec.is_decoded
+
+
+@pytest.mark.parametrize("k,n", [(1024, 1032), (512, 516), (260, 264)])
+def test_large_windows_error_where_reference_panics(qf, gpu_ctx, k, n):
+    # tests/fec.rs:94-126, 162-194; mod.rs:141-175: k + r > 256 panics in
+    # gf_inv(0) -> QF_ERANGE (or EINVAL for k > 256 windows).
+    with pytest.raises(qf.QfError):
+        enc = qf.Encoder(k, n, max_len=16)
+        pool = qf.MemoryPool(k, 16)
+        for i in range(k):
+            enc.add_source_packet(qf.Packet(i, bytearray(8), 8, True))
+        enc.generate_repair_packet(0, pool)
