@@ -89,7 +89,11 @@ def main(argv=None):
     lib = L._lib()
     k, r, Lb, G, e = args.k, args.r, args.L, args.G, args.erase
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    # A dedicated stream for the library AND torch: torch's default stream is
+    # handle 0, which the C ABI would replace by a private stream, and the
+    # timing events must be recorded on the stream the kernels run on.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx = fec.Context(local, stream.cuda_stream)
 
     # --- inputs (resident in HBM before timing) ---------------------------

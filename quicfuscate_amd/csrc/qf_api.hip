@@ -49,8 +49,8 @@ struct qf_ctx {
     int num_cus = 256;
     uint32_t* d_tab256 = nullptr;  // 256 split-table records (8 dwords each)
     uint8_t* d_explog = nullptr;   // exp[512] | log[256]
-    // Cauchy split tables, keyed by (k, r, pass)
-    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, EncTab> cauchy;
+    // Cauchy split tables, keyed by (k, r, pass, k_pad)
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, EncTab> cauchy;
     // custom coefficient tables: pinned host staging + device buffer
     uint32_t* h_custom = nullptr;
     uint32_t* d_custom = nullptr;
@@ -118,6 +118,16 @@ int pick_V() {
     return (e && atoi(e) == 2) ? 2 : 1;
 }
 
+// Prefetch depth (row pairs in flight per wave) of the combine kernels.
+int pick_PD(const char* var, int V, int dflt) {
+    const char* e = getenv(var);
+    int pd = e ? atoi(e) : dflt;
+    const int maxpd = V == 2 ? 2 : 3;
+    if (pd < 1) pd = 1;
+    if (pd > maxpd) pd = maxpd;
+    return pd;
+}
+
 int grow_work(qf_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->work_bytes) return QF_OK;
     if (ctx->d_work) {
@@ -146,7 +156,9 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     if (sh->src_row_stride < L && k > 1) return QF_EINVAL;
     if (sh->rep_row_stride < L && r > 1) return QF_EINVAL;
     const uint32_t Lu = (L + 15) / 16;
-    const uint32_t k_pad = (uint32_t)round_up(k, 4);
+    const int V = (r >= 9) ? 1 : pick_V();  // R = 16 tiles run V = 1 (see launcher)
+    const int PD = pick_PD("QF_ENCODE_PD", V, 2);
+    const uint32_t k_pad = (uint32_t)round_up(k, 2 * (PD + 1));
     const uint32_t passes = (r + 15) / 16;
     std::vector<uint8_t> cm;
     if (!coeff) {
@@ -160,7 +172,7 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         if ((size_t)k_pad * R * 32 > 160 * 1024) return QF_EINVAL;
         const uint32_t* d_tabs = nullptr;
         if (!coeff) {
-            auto key = std::make_tuple(k, r, p);
+            auto key = std::make_tuple(k, r, p, k_pad);
             auto it = ctx->cauchy.find(key);
             if (it == ctx->cauchy.end()) {
                 std::vector<uint32_t> h;
@@ -209,7 +221,7 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         a.L = L;
         a.Lu = Lu;
         a.total_units = (uint64_t)G * Lu;
-        QF_CHECK_HIP(qf::launch_combine_uniform(a, (int)R, pick_V(), ctx->num_cus, st));
+        QF_CHECK_HIP(qf::launch_combine_uniform(a, (int)R, V, PD, ctx->num_cus, st));
         if (coeff) {
             QF_CHECK_HIP(hipEventRecord(ctx->custom_done, st));
             // a second pass rewrites the staging: wait for this pass first
@@ -470,11 +482,12 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     pa.status = status;
     pa.k = k;
     pa.e_max = e_max;
+    pa.e_lds = std::min<uint32_t>(k, 128);
     pa.max_rows = max_rows;
     pa.max_rows_pad = (max_rows + 7) & ~7u;
     pa.passes = passes;
     pa.G = G;
-    if (qf::prepare_lds_bytes(k, e_max, max_rows) > 160 * 1024) return QF_EINVAL;
+    if (qf::prepare_lds_bytes(k, pa.e_lds, max_rows) > 160 * 1024) return QF_EINVAL;
     QF_CHECK_HIP(qf::launch_decode_prepare(pa, ctx->stream));
     const uint32_t Lu = (L + 15) / 16;
     for (uint32_t p = 0; p < passes; ++p) {
@@ -495,7 +508,7 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
         a.Lu = Lu;
         a.zero_slot = max_rows;
         a.total_units = (uint64_t)G * Lu;
-        QF_CHECK_HIP(qf::launch_combine_slots(a, ctx->num_cus, ctx->stream));
+        QF_CHECK_HIP(qf::launch_combine_slots(a, pick_PD("QF_DECODE_PD", 1, 2), ctx->num_cus, ctx->stream));
     }
     return QF_OK;
 }

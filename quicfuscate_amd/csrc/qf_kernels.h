@@ -61,16 +61,19 @@ struct PrepareArgs {
     uint16_t* rec_index;    // [G][e_max]
     int32_t* status;
     uint32_t k;
-    uint32_t e_max;
+    uint32_t e_max;   // output capacity min(k, r)
+    uint32_t e_lds;   // matrix rows held in LDS, min(k, 128)
     uint32_t max_rows;
     uint32_t max_rows_pad;
     uint32_t passes;
     uint32_t G;
 };
 
-hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int num_cus,
+// PD: prefetch depth in row pairs (V=1: 1..3, V=2: 1..2); k_pad must be a
+// multiple of 2*(PD+1).
+hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int PD, int num_cus,
                                   hipStream_t st);
-hipError_t launch_combine_slots(const CombineSlotsArgs& a, int num_cus, hipStream_t st);
+hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st);
 hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st);
 size_t prepare_lds_bytes(uint32_t k, uint32_t e_max, uint32_t max_rows);
 hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n,

@@ -37,9 +37,6 @@
 namespace qf {
 
 #define QF_DEV __device__ __forceinline__
-#ifndef QF_SLOTS_WAVES
-#define QF_SLOTS_WAVES 3
-#endif
 
 QF_DEV uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
@@ -108,6 +105,12 @@ QF_VM_WAIT2(2)
 QF_VM_WAIT2(4)
 QF_VM_WAIT2(6)
 QF_VM_WAIT2(8)
+QF_VM_WAIT2(10)
+QF_VM_WAIT2(12)
+QF_VM_WAIT2(14)
+QF_VM_WAIT2(16)
+QF_VM_WAIT2(20)
+QF_VM_WAIT2(24)
 
 QF_DEV uint4 to_u4(const v4u& v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
@@ -190,25 +193,21 @@ QF_DEV void aload_pair(v4u (&xa)[V], v4u (&xb)[V], const uint8_t* const (&sp)[V]
     }
 }
 
-// Wait for the older pair while the 2V loads of the newer pair stay in flight.
-template <int V>
-QF_DEV void wait_pair(v4u (&xa)[V], v4u (&xb)[V]) {
-#pragma unroll
-    for (int v = 0; v < V; ++v) vm_wait2<2 * V>(xa[v], xb[v]);
-}
-
 template <int V>
 QF_DEV void to_u4v(uint4 (&o)[V], const v4u (&x)[V]) {
 #pragma unroll
     for (int v = 0; v < V; ++v) o[v] = to_u4(x[v]);
 }
 
-// One work item: V units per lane, all k rows, R outputs.  The row loop is a
-// two-buffer ping-pong unrolled by four rows; the loads of pair i+2 are in
-// flight while pair i is computed.  Rows past k-1 are clamped to row k-1;
-// their split tables are zero records (k_pad = round_up(k, 4)), so the
-// clamped data contributes nothing and every load is unconditional.
-template <int R, int V, bool TAIL>
+// One work item: V units per lane, all k rows, R outputs.
+//
+// Row pairs stream through a ring of PD+1 register buffers: the loads of
+// pair p+PD are issued before pair p is computed, so 2*V*PD loads (PD pairs)
+// stay in flight per wave while it computes.  Rows past k-1 are clamped to
+// row k-1; their split tables are zero records (k_pad = round_up(k,
+// 2*(PD+1))), so the clamped data contributes nothing and every load is
+// unconditional.
+template <int R, int V, int PD, bool TAIL>
 QF_DEV void combine_uniform_item(const CombineUniformArgs& a, const uint32_t* __restrict__ tabs,
                                  const uint8_t* const (&sp)[V], uint8_t* const (&dp)[V],
                                  const uint32_t (&nbytes)[V]) {
@@ -230,29 +229,28 @@ QF_DEV void combine_uniform_item(const CombineUniformArgs& a, const uint32_t* __
             fma_rows<R, V>(acc, tabs + (size_t)i * R * 8, xa, xb);
         }
     } else {
-        v4u p0a[V], p0b[V], p1a[V], p1b[V];
-        aload_pair<V>(p0a, p0b, sp, off(0), off(1));
-        for (uint32_t i = 0; i < k; i += 4) {
-            aload_pair<V>(p1a, p1b, sp, off(i + 2), off(i + 3));
-            wait_pair<V>(p0a, p0b);
-            {
+        constexpr int NB = PD + 1;
+        v4u ba[NB][V], bb[NB][V];
+#pragma unroll
+        for (int q = 0; q < PD; ++q) aload_pair<V>(ba[q], bb[q], sp, off(2 * q), off(2 * q + 1));
+        for (uint32_t i = 0; i < k; i += 2 * NB) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const int nbuf = (q + PD) % NB;
+                aload_pair<V>(ba[nbuf], bb[nbuf], sp, off(i + 2 * (q + PD)), off(i + 2 * (q + PD) + 1));
+#pragma unroll
+                for (int v = 0; v < V; ++v) vm_wait2<2 * V * PD>(ba[q][v], bb[q][v]);
                 uint4 xa[V], xb[V];
-                to_u4v<V>(xa, p0a);
-                to_u4v<V>(xb, p0b);
-                fma_rows<R, V>(acc, tabs + (size_t)i * R * 8, xa, xb);
-            }
-            aload_pair<V>(p0a, p0b, sp, off(i + 4), off(i + 5));
-            wait_pair<V>(p1a, p1b);
-            {
-                uint4 xa[V], xb[V];
-                to_u4v<V>(xa, p1a);
-                to_u4v<V>(xb, p1b);
-                fma_rows<R, V>(acc, tabs + (size_t)(i + 2) * R * 8, xa, xb);
+                to_u4v<V>(xa, ba[q]);
+                to_u4v<V>(xb, bb[q]);
+                fma_rows<R, V>(acc, tabs + (size_t)(i + 2 * q) * R * 8, xa, xb);
             }
         }
-        // Drain the last (unused) prefetch before the stores / next item.
+        // Drain the prefetches of the (unused) pairs past the end.
 #pragma unroll
-        for (int v = 0; v < V; ++v) vm_wait2<0>(p0a[v], p0b[v]);
+        for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int v = 0; v < V; ++v) vm_wait2<0>(ba[q][v], bb[q][v]);
     }
     const uint32_t ra = a.r_active;
 #pragma unroll
@@ -270,8 +268,8 @@ QF_DEV void combine_uniform_item(const CombineUniformArgs& a, const uint32_t* __
     }
 }
 
-template <int R, int V>
-__global__ void __launch_bounds__(256, (V == 1 ? 3 : 2)) k_combine_uniform(CombineUniformArgs a) {
+template <int R, int V, int PD>
+__global__ void __launch_bounds__(256, (V == 1 && PD == 1 ? 3 : 2)) k_combine_uniform(CombineUniformArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_tabs[];
     {
         const uint32_t n4 = a.k_pad * R * 2;  // uint4 count (8 words per record)
@@ -307,8 +305,8 @@ __global__ void __launch_bounds__(256, (V == 1 ? 3 : 2)) k_combine_uniform(Combi
             }
             all_full = all_full && nbytes[v] == 16;
         }
-        if (__all(all_full)) combine_uniform_item<R, V, false>(a, lds_tabs, sp, dp, nbytes);
-        else combine_uniform_item<R, V, true>(a, lds_tabs, sp, dp, nbytes);
+        if (__all(all_full)) combine_uniform_item<R, V, PD, false>(a, lds_tabs, sp, dp, nbytes);
+        else combine_uniform_item<R, V, PD, true>(a, lds_tabs, sp, dp, nbytes);
     }
 }
 
@@ -338,7 +336,7 @@ QF_DEV void fma_rows_slots(uint4 (&acc)[R], const uint32_t* __restrict__ tab256,
 // Coefficient records: slot s of a lane's generation, or the all-zero record
 // at index a.zero_slot for slots at/after the lane's bound.  Data rows past
 // the bound are clamped to the last valid slot (multiplied by zero).
-template <int R, bool TAIL>
+template <int R, int PD, bool TAIL>
 QF_DEV void combine_slots_item(const CombineSlotsArgs& a, const uint32_t* __restrict__ tab256,
                                const uint8_t* rowp, uint8_t* outp, const uint8_t* coefp,
                                uint32_t nbytes, uint32_t e_lane, uint32_t bound_lane,
@@ -360,31 +358,36 @@ QF_DEV void combine_slots_item(const CombineSlotsArgs& a, const uint32_t* __rest
             fma_rows_slots<R>(acc, tab256, xa, xb, ca, cb);
         }
     } else {
-        // Ping-pong as in combine_uniform_item: four loads per slot pair (two
-        // rows, two coefficient records) stay in flight one step ahead.
-        v4u p0a, p0b, q0a, q0b, p1a, p1b, q1a, q1b;
-        aload16(p0a, QF_ROW(0u));
-        aload16(p0b, QF_ROW(1u));
-        aload16(q0a, QF_COEF(0u));
-        aload16(q0b, QF_COEF(1u));
-        for (uint32_t s = 0; s < smax; s += 4) {
-            aload16(p1a, QF_ROW(s + 2));
-            aload16(p1b, QF_ROW(s + 3));
-            aload16(q1a, QF_COEF(s + 2));
-            aload16(q1b, QF_COEF(s + 3));
-            vm_wait2<4>(p0a, p0b);
-            vm_wait2<4>(q0a, q0b);
-            fma_rows_slots<R>(acc, tab256, to_u4(p0a), to_u4(p0b), to_u4(q0a), to_u4(q0b));
-            aload16(p0a, QF_ROW(s + 4));
-            aload16(p0b, QF_ROW(s + 5));
-            aload16(q0a, QF_COEF(s + 4));
-            aload16(q0b, QF_COEF(s + 5));
-            vm_wait2<4>(p1a, p1b);
-            vm_wait2<4>(q1a, q1b);
-            fma_rows_slots<R>(acc, tab256, to_u4(p1a), to_u4(p1b), to_u4(q1a), to_u4(q1b));
+        // Ring of PD+1 slot pairs as in combine_uniform_item: four loads per
+        // pair (two rows, two coefficient records), PD pairs in flight.
+        constexpr int NB = PD + 1;
+        v4u pa[NB], pb[NB], qa[NB], qb[NB];
+#pragma unroll
+        for (int q = 0; q < PD; ++q) {
+            aload16(pa[q], QF_ROW(2u * q));
+            aload16(pb[q], QF_ROW(2u * q + 1));
+            aload16(qa[q], QF_COEF(2u * q));
+            aload16(qb[q], QF_COEF(2u * q + 1));
         }
-        vm_wait2<0>(p0a, p0b);
-        vm_wait2<0>(q0a, q0b);
+        for (uint32_t s = 0; s < smax; s += 2 * NB) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const int nb = (q + PD) % NB;
+                const uint32_t sn = s + 2 * (q + PD);
+                aload16(pa[nb], QF_ROW(sn));
+                aload16(pb[nb], QF_ROW(sn + 1));
+                aload16(qa[nb], QF_COEF(sn));
+                aload16(qb[nb], QF_COEF(sn + 1));
+                vm_wait2<4 * PD>(pa[q], pb[q]);
+                vm_wait2<4 * PD>(qa[q], qb[q]);
+                fma_rows_slots<R>(acc, tab256, to_u4(pa[q]), to_u4(pb[q]), to_u4(qa[q]), to_u4(qb[q]));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            vm_wait2<0>(pa[q], pb[q]);
+            vm_wait2<0>(qa[q], qb[q]);
+        }
     }
 #undef QF_ROW
 #undef QF_COEF
@@ -397,16 +400,17 @@ QF_DEV void combine_slots_item(const CombineSlotsArgs& a, const uint32_t* __rest
     }
 }
 
-template <int R>
+template <int R, int PD>
 QF_DEV void combine_slots_dispatch(const CombineSlotsArgs& a, const uint32_t* tab256,
                                    const uint8_t* rowp, uint8_t* outp, const uint8_t* coefp,
                                    uint32_t nbytes, uint32_t e_lane, uint32_t bound_lane,
                                    uint32_t smax, bool full) {
-    if (full) combine_slots_item<R, false>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax);
-    else combine_slots_item<R, true>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax);
+    if (full) combine_slots_item<R, PD, false>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax);
+    else combine_slots_item<R, PD, true>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax);
 }
 
-__global__ void __launch_bounds__(256, QF_SLOTS_WAVES) k_combine_slots(CombineSlotsArgs a) {
+template <int PD>
+__global__ void __launch_bounds__(256, (PD == 1 ? 3 : 2)) k_combine_slots(CombineSlotsArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab256[256 * 8];
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.tab256);
@@ -443,11 +447,11 @@ __global__ void __launch_bounds__(256, QF_SLOTS_WAVES) k_combine_slots(CombineSl
         const bool full = __all(nbytes == 16);
         // Output rows per wave pick the unrolled width (zero coefficients
         // beyond a generation's e make the extra rows harmless).
-        if (jmax <= 4) combine_slots_dispatch<4>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
-        else if (jmax <= 8) combine_slots_dispatch<8>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
-        else if (jmax <= 12) combine_slots_dispatch<12>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
-        else if (jmax <= 14) combine_slots_dispatch<14>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
-        else combine_slots_dispatch<16>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        if (jmax <= 4) combine_slots_dispatch<4, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 8) combine_slots_dispatch<8, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 12) combine_slots_dispatch<12, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 14) combine_slots_dispatch<14, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else combine_slots_dispatch<16, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
     }
 }
 
@@ -538,7 +542,11 @@ __global__ void __launch_bounds__(64) k_decode_prepare(PrepareArgs a) {
     __syncthreads();
     const uint32_t e = nrep;
     if (status == 0 && accepted < k) status = -3;  // QF_ENOTREADY
-    if (status == 0 && e > emax) status = -1;      // more erasures than capacity
+    // The matrix is built for up to e_lds rows so that duplicated repair rows
+    // (which the reference accepts, decoder.rs:694-697) report a singular
+    // matrix exactly like the reference; only a full-rank system with more
+    // erasures than the output capacity min(k, r) is a shape error.
+    if (status == 0 && e > a.e_lds) status = -1;
     uint32_t W = k + e;
     if (status == 0 && e > 0) {
         // Erased list (ascending source index) and column map.
@@ -623,6 +631,7 @@ __global__ void __launch_bounds__(64) k_decode_prepare(PrepareArgs a) {
             __syncthreads();
         }
     }
+    if (status == 0 && e > emax) status = -1;  // QF_EINVAL: capacity min(k, r)
     // Outputs.  Record layout per (pass, generation): max_rows slot records
     // of 16 coefficient bytes, then one all-zero record (slot max_rows) that
     // the payload pass reads for slots past a lane's bound.
@@ -726,10 +735,10 @@ __global__ void __launch_bounds__(256) k_fill_splitmix(uint8_t* __restrict__ dst
 // ---------------------------------------------------------------------------
 // Launch wrappers (host).
 // ---------------------------------------------------------------------------
-template <int R, int V>
-static hipError_t launch_uniform_rv(const CombineUniformArgs& a, int num_cus, hipStream_t st) {
+template <int R, int V, int PD>
+static hipError_t launch_uniform_rvp(const CombineUniformArgs& a, int num_cus, hipStream_t st) {
     const size_t lds = (size_t)a.k_pad * R * 32;
-    auto kern = k_combine_uniform<R, V>;
+    auto kern = k_combine_uniform<R, V, PD>;
     static bool attr_done = false;
     if (!attr_done) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -750,30 +759,36 @@ static hipError_t launch_uniform_rv(const CombineUniformArgs& a, int num_cus, hi
     return hipGetLastError();
 }
 
-hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int num_cus,
-                                  hipStream_t st) {
-    if (V == 2) {
-        switch (R) {
-            case 1: return launch_uniform_rv<1, 2>(a, num_cus, st);
-            case 2: return launch_uniform_rv<2, 2>(a, num_cus, st);
-            case 4: return launch_uniform_rv<4, 2>(a, num_cus, st);
-            case 8: return launch_uniform_rv<8, 2>(a, num_cus, st);
-            case 16: return launch_uniform_rv<16, 2>(a, num_cus, st);
-        }
-    } else {
-        switch (R) {
-            case 1: return launch_uniform_rv<1, 1>(a, num_cus, st);
-            case 2: return launch_uniform_rv<2, 1>(a, num_cus, st);
-            case 4: return launch_uniform_rv<4, 1>(a, num_cus, st);
-            case 8: return launch_uniform_rv<8, 1>(a, num_cus, st);
-            case 16: return launch_uniform_rv<16, 1>(a, num_cus, st);
-        }
+template <int V, int PD>
+static hipError_t launch_uniform_vp(const CombineUniformArgs& a, int R, int num_cus, hipStream_t st) {
+    switch (R) {
+        case 1: return launch_uniform_rvp<1, V, PD>(a, num_cus, st);
+        case 2: return launch_uniform_rvp<2, V, PD>(a, num_cus, st);
+        case 4: return launch_uniform_rvp<4, V, PD>(a, num_cus, st);
+        case 8: return launch_uniform_rvp<8, V, PD>(a, num_cus, st);
+        // 16 outputs x 2 units do not fit 256 VGPRs without spilling the
+        // in-flight buffers: R = 16 always runs one unit per lane.
+        case 16: return launch_uniform_rvp<16, 1, PD>(a, num_cus, st);
     }
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_combine_slots(const CombineSlotsArgs& a, int num_cus, hipStream_t st) {
-    auto kern = k_combine_slots;
+hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int PD, int num_cus,
+                                  hipStream_t st) {
+    if (V == 2) {
+        if (PD == 1) return launch_uniform_vp<2, 1>(a, R, num_cus, st);
+        if (PD == 2) return launch_uniform_vp<2, 2>(a, R, num_cus, st);
+    } else {
+        if (PD == 1) return launch_uniform_vp<1, 1>(a, R, num_cus, st);
+        if (PD == 2) return launch_uniform_vp<1, 2>(a, R, num_cus, st);
+        if (PD == 3) return launch_uniform_vp<1, 3>(a, R, num_cus, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int PD>
+static hipError_t launch_slots_p(const CombineSlotsArgs& a, int num_cus, hipStream_t st) {
+    auto kern = k_combine_slots<PD>;
     int occ = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, 0);
     if (e != hipSuccess) return e;
@@ -787,13 +802,20 @@ hipError_t launch_combine_slots(const CombineSlotsArgs& a, int num_cus, hipStrea
     return hipGetLastError();
 }
 
+hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st) {
+    if (PD == 1) return launch_slots_p<1>(a, num_cus, st);
+    if (PD == 2) return launch_slots_p<2>(a, num_cus, st);
+    if (PD == 3) return launch_slots_p<3>(a, num_cus, st);
+    return hipErrorInvalidValue;
+}
+
 size_t prepare_lds_bytes(uint32_t k, uint32_t e_max, uint32_t max_rows) {
     const uint32_t max_rows_pad = (max_rows + 7) & ~7u;
     return 768 + 4 * 256 + 2 * 256 * 5 + 2 * (size_t)max_rows_pad + (size_t)e_max * (k + e_max) + 16;
 }
 
 hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st) {
-    const size_t lds = prepare_lds_bytes(a.k, a.e_max, a.max_rows);
+    const size_t lds = prepare_lds_bytes(a.k, a.e_lds, a.max_rows);
     static bool attr_done = false;
     if (!attr_done) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_decode_prepare),

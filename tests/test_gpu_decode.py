@@ -154,7 +154,7 @@ def test_decode_many_erasures_multi_pass(qf, oracle, gpu_ctx):
 def test_decode_no_erasures(qf, oracle, gpu_ctx):
     rng = np.random.default_rng(12)
     k, r, L, G = 16, 4, 32, 5
-    src, gens = make_batch(oracle, rng, k, r, L, G, k + r, erase=0)
+    src, gens = make_batch(oracle, rng, k, r, L, G, k + r, erase=0, shuffle=False)
     out = run_decode(qf, k, r, L, G, k + r, gens, False)
     check(oracle, k, L, src, gens, out, False)
     assert (out[2] == 0).all()
