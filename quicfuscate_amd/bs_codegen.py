@@ -1,0 +1,647 @@
+"""Generator of the bit-sliced Cauchy encode kernel for gfx950 (assembly).
+
+Why: on gfx950 v_perm_b32 / v_bitop3_b32 issue at about half rate while
+2-operand v_xor_b32 / v_and_b32 / shifts are full rate (tools/ubench.hip,
+profiles/r01_ubench_valu_rates.json).  The reference's repair coefficients
+are a fixed Cauchy matrix per (k, r) (decoder.rs:280-298), so multiplication
+by each coefficient can be specialised into straight-line XOR code over
+bit-planes:
+
+  * a lane owns a 32-byte chunk of a row (8 dwords);
+  * a 3-stage delta-swap network transposes the chunk into 8 bit-planes
+    (plane a = bit a of all 32 bytes);
+  * c * x over GF(2^8) is the GF(2)-linear map M_c (column a = c * 2^a), so
+    output plane b = XOR_a M_c[b][a] * plane_a;
+  * the 15 nonzero XOR combinations of planes 0..3 (L[v]) and of planes 4..7
+    (H[v]) are formed once per row, so every output plane of every
+    coefficient is acc ^= L[lo] ^= H[hi]: ~15 full-rate v_xor_b32 per
+    coefficient for 32 bytes x 64 lanes = 2048 byte multiply-adds;
+  * the same delta-swap network (an involution) turns the accumulated
+    planes back into bytes.
+
+The row loop is fully unrolled (coefficients are immediates of the code, ~100
+KB of straight-line code; tools/ubench_icache.hip shows no instruction-cache
+penalty at that size).  Rows stream through a ring of PD+1 register buffers
+with explicit global_load_dwordx4 / s_waitcnt vmcnt(N).
+
+The generator builds a small IR that is (1) emitted as assembly and (2)
+executed by `Emulator` (64 lanes, numpy) in the CPU test-suite, which checks
+results against the oracle, every memory access against the buffer bounds
+and every register read against outstanding loads (a missing vmcnt wait).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import numpy as np
+
+MASK32 = 0xFFFFFFFF
+
+# --------------------------------------------------------------------------
+# GF(2^8) (poly 0x11D, generator 2) -- gf_tables.rs:384-408
+# --------------------------------------------------------------------------
+_EXP = [0] * 512
+_LOG = [0] * 256
+_x = 1
+for _i in range(255):
+    _EXP[_i] = _EXP[_i + 255] = _x
+    _LOG[_x] = _i
+    _x <<= 1
+    if _x >= 256:
+        _x ^= 0x11D
+
+
+def gf_mul(a: int, b: int) -> int:
+    return 0 if a == 0 or b == 0 else _EXP[_LOG[a] + _LOG[b]]
+
+
+def gf_inv(a: int) -> int:
+    if a == 0:
+        raise ZeroDivisionError
+    return _EXP[255 - _LOG[a]]
+
+
+def cauchy(k: int, r: int) -> list[list[int]]:
+    """decoder.rs:280-298: C[j][i] = inv((i as u8) ^ ((k + j) as u8))."""
+    return [[gf_inv((i & 0xFF) ^ ((k + j) & 0xFF)) for i in range(k)] for j in range(r)]
+
+
+def mul_matrix_rows(c: int) -> list[int]:
+    """Row b of M_c as a bitmask over input planes a (bit a set iff
+    bit b of c * 2^a is set)."""
+    cols = [gf_mul(c, 1 << a) for a in range(8)]
+    return [sum(((cols[a] >> b) & 1) << a for a in range(8)) for b in range(8)]
+
+
+# --------------------------------------------------------------------------
+# IR
+# --------------------------------------------------------------------------
+@dataclasses.dataclass
+class Op:
+    name: str
+    args: tuple
+
+    def asm(self) -> str:
+        f = _ASM.get(self.name)
+        return f(*self.args) if f else f"{self.name} " + ", ".join(map(str, self.args))
+
+
+def V(i):
+    return f"v{i}"
+
+
+def VP(i):
+    return f"v[{i}:{i + 1}]"
+
+
+def VQ(i):
+    return f"v[{i}:{i + 3}]"
+
+
+def SP(i):
+    return f"s[{i}:{i + 1}]"
+
+
+_ASM = {
+    "label": lambda n: f"{n}:",
+    "v_xor": lambda d, a, b: f"v_xor_b32_e32 {V(d)}, {V(a)}, {V(b)}",
+    "v_mov": lambda d, a: f"v_mov_b32_e32 {V(d)}, {V(a)}",
+    "v_movk": lambda d, k: f"v_mov_b32_e32 {V(d)}, {k}",
+    "v_andk": lambda d, k, a: f"v_and_b32_e32 {V(d)}, 0x{k:08x}, {V(a)}",
+    "v_lshr": lambda d, s, a: f"v_lshrrev_b32_e32 {V(d)}, {s}, {V(a)}",
+    "v_lshl": lambda d, s, a: f"v_lshlrev_b32_e32 {V(d)}, {s}, {V(a)}",
+    "v_lshr_s": lambda d, s, a: f"v_lshrrev_b32_e64 {V(d)}, s{s}, {V(a)}",
+    "v_addk": lambda d, k, a: f"v_add_u32_e32 {V(d)}, {k}, {V(a)}",
+    "v_sub": lambda d, a, b: f"v_sub_u32_e32 {V(d)}, {V(a)}, {V(b)}",
+    "v_lshl_add_s": lambda d, s, sh, a: f"v_lshl_add_u32 {V(d)}, s{s}, {sh}, {V(a)}",
+    "v_mul_hi_s": lambda d, a, s: f"v_mul_hi_u32 {V(d)}, {V(a)}, s{s}",
+    "v_mul_lo_s": lambda d, a, s: f"v_mul_lo_u32 {V(d)}, {V(a)}, s{s}",
+    "v_movs": lambda d, s: f"v_mov_b32_e32 {V(d)}, s{s}",
+    "v_mad64_s": lambda d, a, s, c: f"v_mad_u64_u32 {VP(d)}, s[36:37], {V(a)}, s{s}, {VP(c)}",
+    "v_mad64_k": lambda d, a, k, c: f"v_mad_u64_u32 {VP(d)}, s[36:37], {V(a)}, {k}, {VP(c)}",
+    "v_add64_s": lambda d, a, s: f"v_lshl_add_u64 {VP(d)}, {VP(a)}, 0, {SP(s)}",
+    "v_cmp_gt_s": lambda sd, s, a: f"v_cmp_gt_u32_e64 {SP(sd)}, s{s}, {V(a)}",
+    "v_cmp_ge_s": lambda sd, s, a: f"v_cmp_ge_u32_e64 {SP(sd)}, s{s}, {V(a)}",
+    "v_readfirstlane": lambda s, a: f"v_readfirstlane_b32 s{s}, {V(a)}",
+    "load16": lambda d, a, off: f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
+    "store16": lambda a, d, off: f"global_store_dwordx4 {VP(a)}, {VQ(d)}, off" + (f" offset:{off}" if off else ""),
+    "s_exec": lambda s: "s_mov_b64 exec, -1" if s is None else f"s_mov_b64 exec, {SP(s)}",
+    "s_and64": lambda d, a, b: f"s_and_b64 {SP(d)}, {SP(a)}, {SP(b)}",
+    "s_mov": lambda d, a: f"s_mov_b32 s{d}, s{a}",
+    "s_movk": lambda d, k: f"s_mov_b32 s{d}, {k}",
+    "s_add": lambda d, a, b: f"s_add_u32 s{d}, s{a}, s{b}",
+    "s_lshl": lambda d, a, k: f"s_lshl_b32 s{d}, s{a}, {k}",
+    "s_cmp_ge_br": lambda a, b, lbl: f"s_cmp_ge_u32 s{a}, s{b}\n\ts_cbranch_scc1 {lbl}",
+    "s_branch": lambda lbl: f"s_branch {lbl}",
+    "s_waitcnt_vm": lambda n: f"s_waitcnt vmcnt({n})",
+    "s_waitcnt_lgkm": lambda: "s_waitcnt lgkmcnt(0)",
+    "s_nop": lambda n: f"s_nop {n}",
+    "s_load_args": lambda: "s_load_dwordx16 s[4:19], s[0:1], 0x0\n\ts_load_dwordx4 s[20:23], s[0:1], 0x40",
+    "s_endpgm": lambda: "s_endpgm",
+}
+
+
+# --------------------------------------------------------------------------
+# Kernel layout
+# --------------------------------------------------------------------------
+# kernarg (80 bytes): s[4:5] src, s[6:7] dst, s8 src_gen_stride (u32), s9 pad,
+# s10 dst_gen_stride (u32), s11 pad, s12 src_row_stride, s13 dst_row_stride,
+# s14 L, s15 U (32-byte chunks per row), s16 total chunks, s17 magic,
+# s18 shift, s19 n_items, s20 total waves, s21..s23 pad.
+# SGPRs: s[24:25] full-chunk mask, s[26:27] valid mask, s28 item,
+# s29 wave, s[32:33] {src_row_stride, 0}, s[34:35] {dst_row_stride, 0},
+# s[36:37] mad carry sink.
+KERNARG_BYTES = 80
+V_LANE, V_F, V_SRC, V_DST, V_G, V_U = 0, 1, 2, 4, 6, 7   # v2:3 src ptr, v4:5 dst ptr
+V_T = 8          # v8..v11 temps
+V_COMBO = 12     # 22 combo registers v12..v33
+V_RING = 40      # ring buffers v40.. (8 per buffer)
+SGPR_NEXT_FREE = 40
+
+
+@dataclasses.dataclass
+class KernelSpec:
+    k: int
+    r: int
+    pd: int = 4
+
+    @property
+    def name(self) -> str:
+        return f"qf_cauchy_bs_k{self.k}_r{self.r}"
+
+    @property
+    def nbuf(self) -> int:
+        return self.pd + 1
+
+    @property
+    def acc0(self) -> int:
+        return V_RING + 8 * self.nbuf
+
+    @property
+    def next_free_vgpr(self) -> int:
+        n = self.acc0 + 8 * self.r
+        return (n + 7) // 8 * 8
+
+
+_TRANSPOSE = [(4, 0x0F0F0F0F, [(0, 4), (1, 5), (2, 6), (3, 7)]),
+              (2, 0x33333333, [(0, 2), (1, 3), (4, 6), (5, 7)]),
+              (1, 0x55555555, [(0, 1), (2, 3), (4, 5), (6, 7)])]
+
+# combo register for nonzero 4-bit masks (low group L, high group H)
+_COMBO_BUILD = {  # mask: (a, b) meaning combo = a ^ b, where a/b are masks
+    3: (1, 2), 5: (1, 4), 6: (2, 4), 7: (3, 4), 9: (1, 8), 10: (2, 8), 11: (3, 8),
+    12: (4, 8), 13: (12, 1), 14: (12, 2), 15: (7, 8),
+}
+
+
+def _transpose_ops(base: int) -> list[Op]:
+    ops = []
+    for sh, mask, pairs in _TRANSPOSE:
+        t = [V_T + q for q in range(4)]
+        ops += [Op("v_lshr", (t[q], sh, base + a)) for q, (a, b) in enumerate(pairs)]
+        ops += [Op("v_xor", (t[q], t[q], base + b)) for q, (a, b) in enumerate(pairs)]
+        ops += [Op("v_andk", (t[q], mask, t[q])) for q, (a, b) in enumerate(pairs)]
+        ops += [Op("v_xor", (base + b, base + b, t[q])) for q, (a, b) in enumerate(pairs)]
+        ops += [Op("v_lshl", (t[q], sh, t[q])) for q, (a, b) in enumerate(pairs)]
+        ops += [Op("v_xor", (base + a, base + a, t[q])) for q, (a, b) in enumerate(pairs)]
+    return ops
+
+
+def _combo_regs(base: int) -> tuple[dict, dict]:
+    """Register of each nonzero 4-bit combination: singles are the planes."""
+    lo = {1: base + 0, 2: base + 1, 4: base + 2, 8: base + 3}
+    hi = {1: base + 4, 2: base + 5, 4: base + 6, 8: base + 7}
+    nxt = V_COMBO
+    for m in sorted(_COMBO_BUILD):
+        lo[m] = nxt
+        nxt += 1
+    for m in sorted(_COMBO_BUILD):
+        hi[m] = nxt
+        nxt += 1
+    return lo, hi
+
+
+def _combo_ops(lo: dict, hi: dict, needed_lo: set, needed_hi: set) -> list[Op]:
+    ops = []
+    for tab, need in ((lo, needed_lo), (hi, needed_hi)):
+        # close the needed set under the build dependencies
+        want = set(need)
+        changed = True
+        while changed:
+            changed = False
+            for m in list(want):
+                if m in _COMBO_BUILD:
+                    for d in _COMBO_BUILD[m]:
+                        if d not in want:
+                            want.add(d)
+                            changed = True
+        for m in sorted(_COMBO_BUILD):
+            if m in want:
+                a, b = _COMBO_BUILD[m]
+                ops.append(Op("v_xor", (tab[m], tab[a], tab[b])))
+    return ops
+
+
+def generate(spec: KernelSpec) -> list[Op]:
+    k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
+    C = cauchy(k, r)
+    acc0 = spec.acc0
+    ops: list[Op] = []
+    E = ops.append
+    E(Op("s_load_args", ()))
+    # wave id = workgroup * 4 + (tid >> 6); lane = tid & 63
+    E(Op("v_lshr", (V_T, 6, V_LANE)))
+    E(Op("v_andk", (V_LANE, 63, V_LANE)))
+    E(Op("v_readfirstlane", (29, V_T)))
+    E(Op("s_nop", (4,)))
+    E(Op("s_lshl", (30, 2, 2)))              # s30 = workgroup_id * 4   (s2 = workgroup id)
+    E(Op("s_add", (28, 29, 30)))             # s28 = item = global wave id
+    E(Op("s_waitcnt_lgkm", ()))
+    E(Op("s_mov", (32, 12)))
+    E(Op("s_movk", (33, 0)))
+    E(Op("s_mov", (34, 13)))
+    E(Op("s_movk", (35, 0)))
+    E(Op("label", (".Litem",)))
+    E(Op("s_cmp_ge_br", (28, 19, ".Lend")))
+    # f = item*64 + lane; valid = f < total
+    E(Op("v_lshl_add_s", (V_F, 28, 6, V_LANE)))
+    E(Op("v_cmp_gt_s", (26, 16, V_F)))
+    # g = mulhi(f, magic) >> shift ; u = f - g*U
+    E(Op("v_mul_hi_s", (V_G, V_F, 17)))
+    E(Op("v_lshr_s", (V_G, 18, V_G)))
+    E(Op("v_mul_lo_s", (V_U, V_G, 15)))
+    E(Op("v_sub", (V_U, V_F, V_U)))
+    # src = src + g*src_gen_stride + 32u ; dst likewise
+    # (VOP3 on gfx9 reads at most one SGPR: bases go through VGPRs)
+    E(Op("v_movs", (V_SRC, 4)))
+    E(Op("v_movs", (V_SRC + 1, 5)))
+    E(Op("v_mad64_s", (V_SRC, V_G, 8, V_SRC)))
+    E(Op("v_mad64_k", (V_SRC, V_U, 32, V_SRC)))
+    E(Op("v_movs", (V_DST, 6)))
+    E(Op("v_movs", (V_DST + 1, 7)))
+    E(Op("v_mad64_s", (V_DST, V_G, 10, V_DST)))
+    E(Op("v_mad64_k", (V_DST, V_U, 32, V_DST)))
+    # full chunk: 32u + 32 <= L
+    E(Op("v_lshl", (V_T, 5, V_U)))
+    E(Op("v_addk", (V_T, 32, V_T)))
+    E(Op("v_cmp_ge_s", (24, 14, V_T)))
+    E(Op("s_nop", (4,)))
+    E(Op("s_and64", (24, 24, 26)))
+    # zero the ring (second halves of half chunks are never loaded)
+    for q in range(8 * nbuf):
+        E(Op("v_movk", (V_RING + q, 0)))
+
+    def load_row(row: int):
+        b = V_RING + 8 * (row % nbuf)
+        E(Op("s_exec", (26,)))
+        E(Op("load16", (b, V_SRC, 0)))
+        E(Op("s_exec", (24,)))
+        E(Op("load16", (b + 4, V_SRC, 16)))
+        E(Op("s_exec", (None,)))
+        E(Op("v_add64_s", (V_SRC, V_SRC, 32)))
+
+    for row in range(min(pd, k)):
+        load_row(row)
+    lo, hi = _combo_regs(0)  # placeholder bases are patched per buffer below
+    for i in range(k):
+        if i + pd < k:
+            load_row(i + pd)
+        after = min(pd, k - 1 - i)
+        E(Op("s_waitcnt_vm", (2 * after,)))
+        base = V_RING + 8 * (i % nbuf)
+        ops.extend(_transpose_ops(base))
+        lo, hi = _combo_regs(base)
+        rows = [mul_matrix_rows(C[j][i]) for j in range(r)]
+        need_lo = {rb & 15 for rr in rows for rb in rr} - {0}
+        need_hi = {rb >> 4 for rr in rows for rb in rr} - {0}
+        ops.extend(_combo_ops(lo, hi, need_lo, need_hi))
+        for j in range(r):
+            first_pass, second = [], []
+            for b in range(8):
+                acc = acc0 + 8 * j + b
+                m_lo, m_hi = rows[j][b] & 15, rows[j][b] >> 4
+                if i == 0:
+                    if m_lo and m_hi:
+                        first_pass.append(Op("v_xor", (acc, lo[m_lo], hi[m_hi])))
+                    elif m_lo:
+                        first_pass.append(Op("v_mov", (acc, lo[m_lo])))
+                    elif m_hi:
+                        first_pass.append(Op("v_mov", (acc, hi[m_hi])))
+                    else:
+                        first_pass.append(Op("v_movk", (acc, 0)))
+                else:
+                    if m_lo:
+                        first_pass.append(Op("v_xor", (acc, acc, lo[m_lo])))
+                    if m_hi:
+                        (second if m_lo else first_pass).append(Op("v_xor", (acc, acc, hi[m_hi])))
+            ops.extend(first_pass + second)
+    # planes -> bytes, store 32 bytes per lane per repair
+    for j in range(r):
+        base = acc0 + 8 * j
+        ops.extend(_transpose_ops(base))
+    E(Op("s_nop", (4,)))
+    for j in range(r):
+        base = acc0 + 8 * j
+        E(Op("s_exec", (26,)))
+        E(Op("store16", (V_DST, base, 0)))
+        E(Op("s_exec", (24,)))
+        E(Op("store16", (V_DST, base + 4, 16)))
+        E(Op("s_exec", (None,)))
+        E(Op("v_add64_s", (V_DST, V_DST, 34)))
+    E(Op("s_nop", (4,)))  # store data/address VGPRs are rewritten by the next item
+    E(Op("s_add", (28, 28, 20)))
+    E(Op("s_branch", (".Litem",)))
+    E(Op("label", (".Lend",)))
+    E(Op("s_endpgm", ()))
+    return ops
+
+
+# --------------------------------------------------------------------------
+# Assembly text
+# --------------------------------------------------------------------------
+def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
+    name = spec.name
+    body = []
+    for op in ops:
+        s = op.asm()
+        if op.name == "label":
+            body.append(s.replace(".L", f".L{name}_"))
+        else:
+            body.append("\t" + s.replace(".Litem", f".L{name}_item").replace(".Lend", f".L{name}_end"))
+    nv = spec.next_free_vgpr
+    meta_args = [
+        ("src", 0, 8, "global_buffer"), ("dst", 8, 8, "global_buffer"),
+    ]
+    args_yaml = []
+    for nm, off, sz, kind in meta_args:
+        args_yaml.append(f"""      - .address_space:  global
+        .name:           {nm}
+        .offset:         {off}
+        .size:           {sz}
+        .value_kind:     {kind}""")
+    args_yaml.append(f"""      - .name:           params
+        .offset:         16
+        .size:           {KERNARG_BYTES - 16}
+        .value_kind:     by_value""")
+    return f"""\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"
+\t.amdhsa_code_object_version 6
+\t.text
+\t.globl\t{name}
+\t.p2align\t8
+\t.type\t{name},@function
+{name}:
+""" + "\n".join(body) + f"""
+\t.section\t.rodata,"a",@progbits
+\t.p2align\t6, 0x0
+\t.amdhsa_kernel {name}
+\t\t.amdhsa_group_segment_fixed_size 0
+\t\t.amdhsa_private_segment_fixed_size 0
+\t\t.amdhsa_kernarg_size {KERNARG_BYTES}
+\t\t.amdhsa_user_sgpr_count 2
+\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1
+\t\t.amdhsa_system_sgpr_workgroup_id_x 1
+\t\t.amdhsa_system_vgpr_workitem_id 0
+\t\t.amdhsa_next_free_vgpr {nv}
+\t\t.amdhsa_next_free_sgpr {SGPR_NEXT_FREE}
+\t\t.amdhsa_accum_offset {nv}
+\t\t.amdhsa_reserve_vcc 0
+\t\t.amdhsa_float_denorm_mode_32 3
+\t\t.amdhsa_float_denorm_mode_16_64 3
+\t.end_amdhsa_kernel
+\t.text
+.Lfunc_end_{name}:
+\t.size\t{name}, .Lfunc_end_{name}-{name}
+
+\t.amdgpu_metadata
+---
+amdhsa.kernels:
+  - .args:
+{chr(10).join(args_yaml)}
+    .group_segment_fixed_size: 0
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: {KERNARG_BYTES}
+    .max_flat_workgroup_size: 256
+    .name:           {name}
+    .private_segment_fixed_size: 0
+    .sgpr_count:     {SGPR_NEXT_FREE + 6}
+    .sgpr_spill_count: 0
+    .symbol:         {name}.kd
+    .vgpr_count:     {nv}
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+    .agpr_count:     0
+amdhsa.target:   amdgcn-amd-amdhsa--gfx950
+amdhsa.version:
+  - 1
+  - 2
+...
+\t.end_amdgpu_metadata
+"""
+
+
+# --------------------------------------------------------------------------
+# Host-side launch parameters
+# --------------------------------------------------------------------------
+def magic_for(U: int) -> tuple[int, int]:
+    """g = mulhi(f, magic) >> shift == f // U for f < 2**31 (U >= 2)."""
+    s = (U - 1).bit_length()  # 2**(s-1) < U <= 2**s
+    magic = -(-(1 << (31 + s)) // U)
+    assert magic < (1 << 32)
+    return magic, s - 1
+
+
+def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
+             total_waves: int) -> bytes:
+    U = (L + 31) // 32
+    total = G * U
+    magic, shift = magic_for(U)
+    n_items = (total + 63) // 64
+    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, 0, dgs, 0, srs, drs, L, U, total,
+             magic, shift, n_items, total_waves, 0, 0, 0]
+    return np.array(words, dtype=np.uint32).tobytes()
+
+
+# --------------------------------------------------------------------------
+# Emulator (64 lanes, one wave at a time) -- test infrastructure
+# --------------------------------------------------------------------------
+class EmuError(RuntimeError):
+    pass
+
+
+class Emulator:
+    """Executes the IR for every wave of a grid against a flat byte memory.
+
+    Loads are asynchronous: their destination registers are marked pending
+    until an s_waitcnt vmcnt(n) retires them in issue order; reading a pending
+    register raises.  Every access is bounds-checked against the registered
+    buffers."""
+
+    def __init__(self, ops: list[Op]):
+        self.ops = ops
+        self.labels = {op.args[0]: n for n, op in enumerate(ops) if op.name == "label"}
+        self.buffers: list[tuple[int, int]] = []
+        self.mem = {}
+
+    def add_buffer(self, base: int, data: np.ndarray):
+        self.buffers.append((base, len(data)))
+        self.mem[base] = data
+
+    def _find(self, addr: int, n: int):
+        for base, size in self.buffers:
+            if base <= addr and addr + n <= base + size:
+                return base
+        raise EmuError(f"out-of-bounds access 0x{addr:x}+{n}")
+
+    def read(self, addr: int, n: int) -> bytes:
+        b = self._find(addr, n)
+        return self.mem[b][addr - b: addr - b + n].tobytes()
+
+    def write(self, addr: int, data: bytes):
+        b = self._find(addr, len(data))
+        self.mem[b][addr - b: addr - b + len(data)] = np.frombuffer(data, np.uint8)
+
+    def run_wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int):
+        v = np.zeros((256, 64), dtype=np.uint64)
+        s = [0] * 64
+        ka = np.frombuffer(kernarg, np.uint32)
+        pending = []  # list of (regs, values, lanes) in issue order
+        busy = set()
+        exec_ = np.ones(64, bool)
+        tid = np.arange(64, dtype=np.uint64) + 64 * wave_in_wg
+        v[0] = tid
+        s[2] = workgroup
+
+        def rv(i):
+            if i in busy:
+                raise EmuError(f"read of v{i} with a load outstanding")
+            return v[i]
+
+        def wv(i, val):
+            if i in busy:
+                raise EmuError(f"write of v{i} with a load outstanding")
+            v[i] = np.where(exec_, np.asarray(val, dtype=np.uint64) & MASK32, v[i])
+
+        def rv64(i):
+            return rv(i) | (rv(i + 1) << np.uint64(32))
+
+        def wv64(i, val):
+            val = np.asarray(val, dtype=np.uint64)
+            wv(i, val & np.uint64(MASK32))
+            wv(i + 1, val >> np.uint64(32))
+
+        def smask(i):
+            m = s[i] | (s[i + 1] << 32)
+            return np.array([(m >> l) & 1 for l in range(64)], bool)
+
+        def set_smask(i, arr):
+            m = 0
+            for l in range(64):
+                if arr[l]:
+                    m |= 1 << l
+            s[i], s[i + 1] = m & MASK32, m >> 32
+
+        pc = 0
+        ops = self.ops
+        scc = 0
+        steps = 0
+        while True:
+            op = ops[pc]
+            pc += 1
+            steps += 1
+            n, a = op.name, op.args
+            if n == "label" or n == "s_nop" or n == "s_waitcnt_lgkm":
+                continue
+            if n == "s_load_args":
+                for q in range(20):
+                    s[4 + q] = int(ka[q])
+            elif n == "v_xor":
+                wv(a[0], rv(a[1]) ^ rv(a[2]))
+            elif n == "v_mov":
+                wv(a[0], rv(a[1]))
+            elif n == "v_movk":
+                wv(a[0], np.full(64, a[1], np.uint64))
+            elif n == "v_andk":
+                wv(a[0], rv(a[2]) & np.uint64(a[1]))
+            elif n == "v_lshr":
+                wv(a[0], rv(a[2]) >> np.uint64(a[1]))
+            elif n == "v_lshl":
+                wv(a[0], (rv(a[2]) << np.uint64(a[1])) & np.uint64(MASK32))
+            elif n == "v_lshr_s":
+                wv(a[0], rv(a[2]) >> np.uint64(s[a[1]] & 31))
+            elif n == "v_addk":
+                wv(a[0], (rv(a[2]) + np.uint64(a[1])) & np.uint64(MASK32))
+            elif n == "v_sub":
+                wv(a[0], (rv(a[1]) - rv(a[2])) & np.uint64(MASK32))
+            elif n == "v_lshl_add_s":
+                wv(a[0], ((np.uint64(s[a[1]]) << np.uint64(a[2])) + rv(a[3])) & np.uint64(MASK32))
+            elif n == "v_mul_hi_s":
+                wv(a[0], (rv(a[1]) * np.uint64(s[a[2]])) >> np.uint64(32))
+            elif n == "v_mul_lo_s":
+                wv(a[0], (rv(a[1]) * np.uint64(s[a[2]])) & np.uint64(MASK32))
+            elif n == "v_movs":
+                wv(a[0], np.full(64, s[a[1]], np.uint64))
+            elif n == "v_mad64_s":
+                wv64(a[0], rv(a[1]) * np.uint64(s[a[2]]) + rv64(a[3]))
+            elif n == "v_mad64_k":
+                wv64(a[0], rv(a[1]) * np.uint64(a[2]) + rv64(a[3]))
+            elif n == "v_add64_s":
+                wv64(a[0], rv64(a[1]) + np.uint64(s[a[2]] | (s[a[2] + 1] << 32)))
+            elif n in ("v_cmp_gt_s", "v_cmp_ge_s"):
+                x = rv(a[2])
+                sv = np.uint64(s[a[1]])
+                res = (sv > x) if n == "v_cmp_gt_s" else (sv >= x)
+                set_smask(a[0], res & exec_)
+            elif n == "v_readfirstlane":
+                lane = int(np.argmax(exec_))
+                s[a[0]] = int(rv(a[1])[lane])
+            elif n == "load16":
+                d, ar, off = a
+                addr = rv64(ar)
+                vals = np.zeros((4, 64), np.uint64)
+                lanes = np.nonzero(exec_)[0]
+                for l in lanes:
+                    raw = self.read(int(addr[l]) + off, 16)
+                    vals[:, l] = np.frombuffer(raw, np.uint32)
+                regs = [d + q for q in range(4)]
+                for rg in regs:
+                    if rg in busy:
+                        raise EmuError(f"load into v{rg} with a load outstanding")
+                    busy.add(rg)
+                pending.append((regs, vals, exec_.copy()))
+            elif n == "store16":
+                ar, d, off = a
+                addr = rv64(ar)
+                vals = np.stack([rv(d + q) for q in range(4)]).astype(np.uint32)
+                for l in np.nonzero(exec_)[0]:
+                    self.write(int(addr[l]) + off, vals[:, l].tobytes())
+            elif n == "s_waitcnt_vm":
+                while len(pending) > a[0]:
+                    regs, vals, lanes = pending.pop(0)
+                    for q, rg in enumerate(regs):
+                        busy.discard(rg)
+                        v[rg] = np.where(lanes, vals[q], v[rg])
+            elif n == "s_exec":
+                exec_ = np.ones(64, bool) if a[0] is None else smask(a[0])
+            elif n == "s_and64":
+                set_smask(a[0], smask(a[1]) & smask(a[2]))
+            elif n == "s_mov":
+                s[a[0]] = s[a[1]]
+            elif n == "s_movk":
+                s[a[0]] = a[1] & MASK32
+            elif n == "s_add":
+                s[a[0]] = (s[a[1]] + s[a[2]]) & MASK32
+            elif n == "s_lshl":
+                s[a[0]] = (s[a[1]] << a[2]) & MASK32
+            elif n == "s_cmp_ge_br":
+                if s[a[0]] >= s[a[1]]:
+                    pc = self.labels[a[2]]
+            elif n == "s_branch":
+                pc = self.labels[a[0]]
+            elif n == "s_endpgm":
+                if pending:
+                    # stores/loads may be outstanding at the end: retire them
+                    pending.clear()
+                return steps
+            else:
+                raise EmuError(f"unknown op {n}")

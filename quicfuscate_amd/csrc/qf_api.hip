@@ -18,6 +18,7 @@
 #include "gf256_tables.h"
 #include "qf_fec.h"
 #include "qf_kernels.h"
+#include "qf_bs.h"
 
 namespace qf {
 const Gf256& gf() {
@@ -65,6 +66,8 @@ struct qf_ctx {
     uint8_t* d_stage_src[kPipe] = {nullptr, nullptr, nullptr};
     uint8_t* d_stage_rep[kPipe] = {nullptr, nullptr, nullptr};
     size_t stage_src_bytes = 0, stage_rep_bytes = 0;
+    // bit-sliced Cauchy kernels (loaded on first use)
+    qf::BsCache bs;
     std::mutex mu;
 };
 
@@ -164,6 +167,17 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     if (!coeff) {
         int s = cauchy_matrix(k, r, cm);
         if (s != QF_OK) return s;
+    }
+    // Fast path: bit-sliced kernel specialised to the reference's Cauchy
+    // matrix of (k, r) (bs_codegen.py), for whole 16-byte rows.
+    const char* nobs = getenv("QF_DISABLE_BS");
+    if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && L % 16 == 0 && L >= 64 &&
+        sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
+        sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
+        (uint64_t)G * ((L + 31) / 32) < (1ull << 31)) {
+        QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
+                                   sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G));
+        return QF_OK;
     }
     for (uint32_t p = 0; p < passes; ++p) {
         const uint32_t j0 = p * 16;
@@ -323,6 +337,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->d_custom) hipFree(c->d_custom);
     if (c->custom_done) hipEventDestroy(c->custom_done);
     if (c->d_work) hipFree(c->d_work);
+    qf::bs_unload(c->bs);
     for (int i = 0; i < qf_ctx::kPipe; ++i) {
         if (c->pstream[i]) {
             hipStreamSynchronize(c->pstream[i]);

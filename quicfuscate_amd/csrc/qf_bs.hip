@@ -1,0 +1,97 @@
+// qf_bs.hip -- loader / launcher of the bit-sliced Cauchy encode kernels.
+//
+// The kernels are generated gfx950 assembly (quicfuscate_amd/bs_codegen.py):
+// multiplication by each coefficient of the reference's fixed Cauchy matrix
+// (decoder.rs:280-298) is specialised into straight-line full-rate v_xor_b32
+// over bit-planes.  build_lib.py assembles them and embeds the code objects
+// (qf_bs_blobs.inc); this file loads them into the context's device with
+// hipModuleLoadData and launches them with a packed kernarg buffer.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "qf_bs.h"
+
+struct QfBsEntry {
+    uint32_t k, r, pd;
+    const char* name;
+    const unsigned char* data;
+    size_t size;
+};
+#include "qf_bs_blobs.inc"
+
+namespace qf {
+
+static const QfBsEntry* bs_find(uint32_t k, uint32_t r) {
+    for (const auto& e : qf_bs_table)
+        if (e.k == k && e.r == r) return &e;
+    return nullptr;
+}
+
+bool bs_available(uint32_t k, uint32_t r) { return bs_find(k, r) != nullptr; }
+
+static void magic_for(uint32_t U, uint32_t* magic, uint32_t* shift) {
+    uint32_t s = 0;
+    while ((1u << s) < U) ++s;  // 2^(s-1) < U <= 2^s
+    const uint64_t num = 1ull << (31 + s);
+    *magic = (uint32_t)((num + U - 1) / U);
+    *shift = s - 1;
+}
+
+hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                     const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
+                     uint64_t drs, uint32_t L, uint32_t G) {
+    const QfBsEntry* e = bs_find(k, r);
+    if (!e) return hipErrorInvalidValue;
+    int idx = (int)(e - qf_bs_table);
+    if (idx >= BsCache::kMax) return hipErrorInvalidValue;
+    if (!cache.fn[idx]) {
+        hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
+        if (err != hipSuccess) return err;
+        err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
+        if (err != hipSuccess) return err;
+    }
+    const uint32_t U = (L + 31) / 32;
+    const uint64_t total = (uint64_t)G * U;
+    if (total >= (1ull << 31) || U < 2) return hipErrorInvalidValue;
+    uint32_t magic, shift;
+    magic_for(U, &magic, &shift);
+    const uint32_t n_items = (uint32_t)((total + 63) / 64);
+    // 208 VGPRs -> 2 waves per SIMD -> two 256-thread blocks per CU
+    uint32_t blocks = (n_items + 3) / 4;
+    const uint32_t cap = (uint32_t)num_cus * 2;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return hipSuccess;
+    uint32_t a[20];
+    memset(a, 0, sizeof(a));
+    a[0] = (uint32_t)(uintptr_t)src;
+    a[1] = (uint32_t)((uintptr_t)src >> 32);
+    a[2] = (uint32_t)(uintptr_t)dst;
+    a[3] = (uint32_t)((uintptr_t)dst >> 32);
+    a[4] = (uint32_t)sgs;
+    a[6] = (uint32_t)dgs;
+    a[8] = (uint32_t)srs;
+    a[9] = (uint32_t)drs;
+    a[10] = L;
+    a[11] = U;
+    a[12] = (uint32_t)total;
+    a[13] = magic;
+    a[14] = shift;
+    a[15] = n_items;
+    a[16] = blocks * 4;
+    size_t sz = sizeof(a);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+}
+
+void bs_unload(BsCache& cache) {
+    for (int i = 0; i < BsCache::kMax; ++i)
+        if (cache.mod[i]) {
+            hipModuleUnload(cache.mod[i]);
+            cache.mod[i] = nullptr;
+            cache.fn[i] = nullptr;
+        }
+}
+
+}  // namespace qf

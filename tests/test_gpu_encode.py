@@ -45,13 +45,24 @@ CASES = [
     (64, 40, 100, 3),      # r > 16 -> passes of 16
     (96, 15, 9000, 2),     # jumbo payload (Normal ratio 1.15: r = 15 at k = 96)
     (63, 16, 1201, 7),     # k % 4 = 3, L % 16 = 1
+    # shapes with a bit-sliced Cauchy kernel (bs_codegen.py): whole and half
+    # 32-byte chunks, several generations per wave
+    (32, 16, 96, 10),
+    (64, 10, 64, 21),
+    (16, 16, 80, 13),
+    (64, 16, 1216, 11),
 ]
 
 
 @pytest.mark.parametrize("k,r,L,G", CASES)
-@pytest.mark.parametrize("V", ["1", "2"])
+@pytest.mark.parametrize("V", ["1", "2", "perm"])
 def test_encode_matches_oracle(qf, oracle, gpu_ctx, k, r, L, G, V, monkeypatch):
-    monkeypatch.setenv("QF_ENCODE_V", V)
+    # V=1/2: default dispatch (bit-sliced kernel where one exists);
+    # "perm": force the general v_perm kernel
+    if V == "perm":
+        monkeypatch.setenv("QF_DISABLE_BS", "1")
+    else:
+        monkeypatch.setenv("QF_ENCODE_V", V)
     rng = np.random.default_rng(k * 1000 + r * 10 + L)
     rs = _r16(L) + (16 if k % 2 else 0)
     gs = k * rs + 32

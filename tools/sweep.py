@@ -52,8 +52,17 @@ def main():
     dst = torch.empty_like(src)
     ms, mn = timeit(lambda: dst.copy_(src))
     res["copy_src_GBps"] = round(2 * src.numel() / (mn / 1e3) / 1e9, 1)
-    for r in (1, 4, 8, 16):
-        for V, PD in ((1, 1), (1, 2), (1, 3), (2, 1), (2, 2)):
+    for r in (10, 16):
+        os.environ.pop("QF_DISABLE_BS", None)
+        f = lambda: fec.encode_batch(src, rep, k, r, Lb, src_row_stride=Lb, src_gen_stride=k * Lb,
+                                     rep_row_stride=Lb, rep_gen_stride=r * Lb, G=G, ctx=ctx)
+        ms, mn = timeit(f)
+        byt = G * (k + r) * Lb
+        res[f"enc_r{r}_bitsliced"] = {"ms": round(mn, 4), "GBps": round(byt / (mn / 1e3) / 1e9, 1)}
+        print(f"enc r={r} bitsliced: {res[f'enc_r{r}_bitsliced']}", flush=True)
+    os.environ["QF_DISABLE_BS"] = "1"
+    for r in (1, 16):
+        for V, PD in ((1, 1), (1, 2)):
             if r >= 9 and V == 2:
                 continue
             os.environ["QF_ENCODE_V"] = str(V)
@@ -67,6 +76,7 @@ def main():
             print(f"enc r={r} V={V} PD={PD}: {res[f'enc_r{r}_V{V}_PD{PD}']}", flush=True)
     os.environ.pop("QF_ENCODE_V", None)
     os.environ.pop("QF_ENCODE_PD", None)
+    os.environ.pop("QF_DISABLE_BS", None)
     fec.encode_batch(src, rep, k, 16, Lb, src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lb,
                      rep_gen_stride=16 * Lb, G=G, ctx=ctx)
     del dst
