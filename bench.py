@@ -65,7 +65,7 @@ def parse(argv=None):
     ap.add_argument("--r", type=int, default=16)
     ap.add_argument("--L", type=int, default=1200)
     ap.add_argument("--erase", type=int, default=13, help="erased sources per generation (20%% of 64)")
-    ap.add_argument("--cpu-sample", type=int, default=2048, help="generations in the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=4096, help="generations in the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-path-G", type=int, default=16384, help="generations for the pinned-host encode rate (0=skip)")
     return ap.parse_args(argv)
@@ -142,6 +142,7 @@ def main(argv=None):
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ctx.profile(True)  # per-kernel HIP events on the launch stream
     t0 = time.perf_counter()
     for s in range(args.steps):
         ev[s][0].record(stream)
@@ -154,6 +155,10 @@ def main(argv=None):
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    ktimes = ctx.kernel_times()
+    ctx.profile(False)
+    kern_ms = {n: ms / max(1, cnt) for n, (cnt, ms) in ktimes.items()}  # per launch
+    kern_step_ms = {n: ms / args.steps for n, (cnt, ms) in ktimes.items()}
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     step_ms = wall * 1e3 / args.steps
@@ -180,15 +185,43 @@ def main(argv=None):
     enc_gibps = src_bytes_total / (enc_ms_max / 1e3) / gib
     dec_gibps = src_bytes_total / (dec_ms_max / 1e3) / gib
 
-    # roofline of the dominant kernel (encode: k_combine_uniform, one launch per call)
-    enc_bytes = G * (k + r) * Lb                       # SURVEY 8(d) B_enc per generation x G
-    dec_bytes = G * (k * Lb + e * k + e * Lb)          # B_dec per generation x G
-    achieved = enc_bytes / (enc_ms / 1e3) / 1e9
+    # Roofline of the dominant kernel (largest time per step), algorithmic
+    # bytes per launch (DESIGN.md "Kernels"):
+    #   encode (bit-sliced or v_perm): read k rows, write r rows / generation
+    #   syndromes (decode stage A): read the k accepted rows + slot map,
+    #     write e syndrome rows
+    #   slots combine: stage B after syndromes (read e syndrome rows + e+1
+    #     records, write e rows) or, on the general path, read k rows +
+    #     records, write e rows
+    #   prepare: row indices in, slot map / records / indices out
+    fast_decode = any(n.startswith("qf_cauchy_syn") for n in ktimes)
+    map_stride = (k + r + 15) // 16 * 16
+    enc_bytes = G * (k + r) * Lb
+    syn_bytes = G * ((k + e) * Lb + map_stride)
+    if fast_decode:
+        slots_bytes = G * (2 * e * Lb + (e + 1) * 16)
+    else:
+        slots_bytes = G * (k * Lb + e * Lb + (n_slots + 1) * 16)
+    prep_bytes = G * (n_slots * 2 + map_stride + (r + 1) * 16 + e * 2 + 12)
+    dec_bytes = G * (k * Lb + e * k + e * Lb)  # decode as a whole (SURVEY B_dec)
+
+    def alg_bytes(name):
+        if name.startswith("qf_cauchy_syn"):
+            return syn_bytes
+        if name.startswith("k_combine_slots"):
+            return slots_bytes
+        if name.startswith("k_decode_prepare"):
+            return prep_bytes
+        return enc_bytes
+
+    dom = max(kern_step_ms, key=kern_step_ms.get)
+    dom_ms = kern_ms[dom]
+    achieved = alg_bytes(dom) / (dom_ms / 1e3) / 1e9
     traffic = None
-    tfile = REPO / "profiles" / "traffic_encode.json"
+    tfile = REPO / "profiles" / "traffic.json"
     if tfile.exists():
         try:
-            tj = json.loads(tfile.read_text())
+            tj = json.loads(tfile.read_text()).get(dom, {})
             if tj.get("k") == k and tj.get("r") == r and tj.get("L") == Lb and tj.get("G") == G:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
@@ -218,15 +251,18 @@ def main(argv=None):
         "encode_ms": round(enc_ms_max, 4),
         "decode_ms": round(dec_ms_max, 4),
         "decode_hbm_gbps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
+        "kernel_ms_per_launch": {n: round(v, 4) for n, v in kern_ms.items()},
+        "kernel_gbps": {n: round(alg_bytes(n) / (v / 1e3) / 1e9, 1) for n, v in kern_ms.items()},
         "roofline": {
-            "kernel": "k_combine_uniform<16,V> (encode)",
+            "kernel": dom,
+            "launch_ms": round(dom_ms, 4),
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": PEAK_HBM_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBPS, 4),
             "traffic": traffic,
-            "algorithmic_bytes_per_launch": enc_bytes,
+            "algorithmic_bytes_per_launch": alg_bytes(dom),
         },
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,

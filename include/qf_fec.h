@@ -72,6 +72,17 @@ int qf_ctx_set_stream(qf_ctx *ctx, void *stream);
 void *qf_ctx_stream(qf_ctx *ctx);
 int qf_sync(qf_ctx *ctx);
 
+/* Kernel timing (no reference counterpart; benches/ replacement).  While on,
+ * every kernel the context launches is bracketed by HIP events recorded on
+ * the stream it runs on; totals accumulate per kernel name.  on != 0 clears
+ * the totals and starts, on == 0 stops.  qf_ctx_profile_read synchronises
+ * the pending events and returns the i-th kernel (first-launch order):
+ * name (owned by ctx), number of launches, summed duration in ms;
+ * QF_EINVAL once i >= number of kernels seen. */
+int qf_ctx_profile(qf_ctx *ctx, int on);
+int qf_ctx_profile_read(qf_ctx *ctx, uint32_t i, const char **name, uint32_t *launches,
+                        double *total_ms);
+
 /* ---------------------------------------------------------------------------
  * Element-wise slice multiply on the device.
  * replaces gf_tables.rs:255-274 gf_mul_slice (benches/gf_mul_slice_bench.rs)

@@ -70,6 +70,9 @@ _SIGS = {
     "qf_ctx_set_stream": (_I, [_P, _P]),
     "qf_ctx_stream": (_P, [_P]),
     "qf_sync": (_I, [_P]),
+    "qf_ctx_profile": (_I, [_P, _I]),
+    "qf_ctx_profile_read": (_I, [_P, _U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U32),
+                                 ctypes.POINTER(ctypes.c_double)]),
     "qf_gf256_mul_slice_dev": (_I, [_P, _P, _P, _P, _SZ]),
     "qf_encode_batch": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
     "qf_encode_batch_host": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),

@@ -124,6 +124,9 @@ _ASM = {
     "v_cmp_gt_s": lambda sd, s, a: f"v_cmp_gt_u32_e64 {SP(sd)}, s{s}, {V(a)}",
     "v_cmp_ge_s": lambda sd, s, a: f"v_cmp_ge_u32_e64 {SP(sd)}, s{s}, {V(a)}",
     "v_readfirstlane": lambda s, a: f"v_readfirstlane_b32 s{s}, {V(a)}",
+    "v_bfe": lambda d, a, off, w: f"v_bfe_u32 {V(d)}, {V(a)}, {off}, {w}",
+    "v_cmp_ne_s": lambda sd, s, a: f"v_cmp_ne_u32_e64 {SP(sd)}, s{s}, {V(a)}",
+    "v_cndmask_0": lambda d, a, sm: f"v_cndmask_b32_e64 {V(d)}, 0, {V(a)}, {SP(sm)}",
     "load16": lambda d, a, off: f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
     "store16": lambda a, d, off: f"global_store_dwordx4 {VP(a)}, {VQ(d)}, off" + (f" offset:{off}" if off else ""),
     "s_exec": lambda s: "s_mov_b64 exec, -1" if s is None else f"s_mov_b64 exec, {SP(s)}",
@@ -152,12 +155,26 @@ _ASM = {
 # SGPRs: s[24:25] full-chunk mask, s[26:27] valid mask, s28 item,
 # s29 wave, s[32:33] {src_row_stride, 0}, s[34:35] {dst_row_stride, 0},
 # s[36:37] mad carry sink.
+#
+# Syndrome mode ("syn", decode stage A) uses the same registers with:
+# s[4:5] received rows, s[6:7] syndrome rows, s8 rows_gen_stride,
+# s10 syn_gen_stride, s12 row_stride, s13 syn_row_stride, s21 slot-map
+# generation stride, s[22:23] slot map; s[38:39] mask temp, s[40+2q] the
+# present-lane mask of ring buffer q; v2:3 = generation base of the lane's
+# chunk, v34:35 per-row address, v36 slot; map registers after the
+# accumulators.
 KERNARG_BYTES = 80
 V_LANE, V_F, V_SRC, V_DST, V_G, V_U = 0, 1, 2, 4, 6, 7   # v2:3 src ptr, v4:5 dst ptr
 V_T = 8          # v8..v11 temps
 V_COMBO = 12     # 22 combo registers v12..v33
+V_ADDR = 34      # v34:35 gathered row address (syn)
+V_SLOT = 36      # slot temp (syn)
 V_RING = 40      # ring buffers v40.. (8 per buffer)
 SGPR_NEXT_FREE = 40
+S_TMP = 38
+S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
+S_MASK0 = 40
+ABSENT = 0xFF    # slot-map value of a row that was not accepted
 
 
 @dataclasses.dataclass
@@ -165,10 +182,12 @@ class KernelSpec:
     k: int
     r: int
     pd: int = 4
+    mode: str = "enc"   # "enc": repairs of the Cauchy code; "syn": decode syndromes
 
     @property
     def name(self) -> str:
-        return f"qf_cauchy_bs_k{self.k}_r{self.r}"
+        tag = "bs" if self.mode == "enc" else "syn"
+        return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
 
     @property
     def nbuf(self) -> int:
@@ -179,9 +198,26 @@ class KernelSpec:
         return V_RING + 8 * self.nbuf
 
     @property
+    def map_quads(self) -> int:
+        return (self.k + self.r + 15) // 16 if self.mode == "syn" else 0
+
+    @property
+    def map0(self) -> int:
+        return self.acc0 + 8 * self.r
+
+    @property
+    def map_stride(self) -> int:
+        """Bytes per generation in the slot map (k source + r repair slots)."""
+        return 16 * self.map_quads
+
+    @property
     def next_free_vgpr(self) -> int:
-        n = self.acc0 + 8 * self.r
+        n = self.map0 + 4 * self.map_quads
         return (n + 7) // 8 * 8
+
+    @property
+    def next_free_sgpr(self) -> int:
+        return SGPR_NEXT_FREE if self.mode == "enc" else S_MASK0 + 2 * self.nbuf
 
 
 _TRANSPOSE = [(4, 0x0F0F0F0F, [(0, 4), (1, 5), (2, 6), (3, 7)]),
@@ -243,12 +279,43 @@ def _combo_ops(lo: dict, hi: dict, needed_lo: set, needed_hi: set) -> list[Op]:
     return ops
 
 
-def generate(spec: KernelSpec) -> list[Op]:
-    k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
-    C = cauchy(k, r)
-    acc0 = spec.acc0
-    ops: list[Op] = []
-    E = ops.append
+def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict, init: bool):
+    """acc[b] (^)= M_c[b] * planes for one coefficient (rows_j = M_c rows)."""
+    first_pass, second = [], []
+    for b in range(8):
+        a = acc + b
+        m_lo, m_hi = rows_j[b] & 15, rows_j[b] >> 4
+        if init:
+            if m_lo and m_hi:
+                first_pass.append(Op("v_xor", (a, lo[m_lo], hi[m_hi])))
+            elif m_lo:
+                first_pass.append(Op("v_mov", (a, lo[m_lo])))
+            elif m_hi:
+                first_pass.append(Op("v_mov", (a, hi[m_hi])))
+            else:
+                first_pass.append(Op("v_movk", (a, 0)))
+        else:
+            if m_lo:
+                first_pass.append(Op("v_xor", (a, a, lo[m_lo])))
+            if m_hi:
+                (second if m_lo else first_pass).append(Op("v_xor", (a, a, hi[m_hi])))
+    ops.extend(first_pass + second)
+
+
+def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool):
+    """Transpose one source row (ring buffer at `base`) and accumulate it into
+    all r repair accumulators with the Cauchy coefficients of column i."""
+    ops.extend(_transpose_ops(base))
+    lo, hi = _combo_regs(base)
+    rows = [mul_matrix_rows(C[j][i]) for j in range(r)]
+    need_lo = {rb & 15 for rr in rows for rb in rr} - {0}
+    need_hi = {rb >> 4 for rr in rows for rb in rr} - {0}
+    ops.extend(_combo_ops(lo, hi, need_lo, need_hi))
+    for j in range(r):
+        _coeff_block(ops, rows[j], acc0 + 8 * j, lo, hi, init)
+
+
+def _prologue(E):
     E(Op("s_load_args", ()))
     # wave id = workgroup * 4 + (tid >> 6); lane = tid & 63
     E(Op("v_lshr", (V_T, 6, V_LANE)))
@@ -288,6 +355,27 @@ def generate(spec: KernelSpec) -> list[Op]:
     E(Op("v_cmp_ge_s", (24, 14, V_T)))
     E(Op("s_nop", (4,)))
     E(Op("s_and64", (24, 24, 26)))
+
+
+def _epilogue_next_item(E):
+    E(Op("s_nop", (4,)))  # store data/address VGPRs are rewritten by the next item
+    E(Op("s_add", (28, 28, 20)))
+    E(Op("s_branch", (".Litem",)))
+    E(Op("label", (".Lend",)))
+    E(Op("s_endpgm", ()))
+
+
+def generate(spec: KernelSpec) -> list[Op]:
+    return _generate_enc(spec) if spec.mode == "enc" else _generate_syn(spec)
+
+
+def _generate_enc(spec: KernelSpec) -> list[Op]:
+    k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
+    C = cauchy(k, r)
+    acc0 = spec.acc0
+    ops: list[Op] = []
+    E = ops.append
+    _prologue(E)
     # zero the ring (second halves of half chunks are never loaded)
     for q in range(8 * nbuf):
         E(Op("v_movk", (V_RING + q, 0)))
@@ -303,43 +391,15 @@ def generate(spec: KernelSpec) -> list[Op]:
 
     for row in range(min(pd, k)):
         load_row(row)
-    lo, hi = _combo_regs(0)  # placeholder bases are patched per buffer below
     for i in range(k):
         if i + pd < k:
             load_row(i + pd)
         after = min(pd, k - 1 - i)
         E(Op("s_waitcnt_vm", (2 * after,)))
-        base = V_RING + 8 * (i % nbuf)
-        ops.extend(_transpose_ops(base))
-        lo, hi = _combo_regs(base)
-        rows = [mul_matrix_rows(C[j][i]) for j in range(r)]
-        need_lo = {rb & 15 for rr in rows for rb in rr} - {0}
-        need_hi = {rb >> 4 for rr in rows for rb in rr} - {0}
-        ops.extend(_combo_ops(lo, hi, need_lo, need_hi))
-        for j in range(r):
-            first_pass, second = [], []
-            for b in range(8):
-                acc = acc0 + 8 * j + b
-                m_lo, m_hi = rows[j][b] & 15, rows[j][b] >> 4
-                if i == 0:
-                    if m_lo and m_hi:
-                        first_pass.append(Op("v_xor", (acc, lo[m_lo], hi[m_hi])))
-                    elif m_lo:
-                        first_pass.append(Op("v_mov", (acc, lo[m_lo])))
-                    elif m_hi:
-                        first_pass.append(Op("v_mov", (acc, hi[m_hi])))
-                    else:
-                        first_pass.append(Op("v_movk", (acc, 0)))
-                else:
-                    if m_lo:
-                        first_pass.append(Op("v_xor", (acc, acc, lo[m_lo])))
-                    if m_hi:
-                        (second if m_lo else first_pass).append(Op("v_xor", (acc, acc, hi[m_hi])))
-            ops.extend(first_pass + second)
+        _source_row(ops, C, i, r, V_RING + 8 * (i % nbuf), acc0, init=(i == 0))
     # planes -> bytes, store 32 bytes per lane per repair
     for j in range(r):
-        base = acc0 + 8 * j
-        ops.extend(_transpose_ops(base))
+        ops.extend(_transpose_ops(acc0 + 8 * j))
     E(Op("s_nop", (4,)))
     for j in range(r):
         base = acc0 + 8 * j
@@ -349,11 +409,95 @@ def generate(spec: KernelSpec) -> list[Op]:
         E(Op("store16", (V_DST, base + 4, 16)))
         E(Op("s_exec", (None,)))
         E(Op("v_add64_s", (V_DST, V_DST, 34)))
-    E(Op("s_nop", (4,)))  # store data/address VGPRs are rewritten by the next item
-    E(Op("s_add", (28, 28, 20)))
-    E(Op("s_branch", (".Litem",)))
-    E(Op("label", (".Lend",)))
-    E(Op("s_endpgm", ()))
+    _epilogue_next_item(E)
+    return ops
+
+
+def _generate_syn(spec: KernelSpec) -> list[Op]:
+    """Decode stage A: syndromes s_j = p_j ^ sum_{i present} C[j][i] x_i of
+    every accepted repair j, for the generation of each lane.
+
+    The slot map (per generation: k source slots then r repair slots, one
+    byte each, ABSENT if the row was not accepted) says where each row sits
+    among the received rows.  Rows stream through the ring in the order
+    repairs 0..r-1, sources 0..k-1; a lane whose generation lacks a row loads
+    slot 0 instead (always readable) and is switched off by EXEC while that
+    row is accumulated.  Syndromes are stored only for accepted repairs."""
+    k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
+    C = cauchy(k, r)
+    acc0, map0 = spec.acc0, spec.map0
+    seq = [("rep", j) for j in range(r)] + [("src", i) for i in range(k)]
+    ops: list[Op] = []
+    E = ops.append
+    _prologue(E)
+    E(Op("s_movk", (S_ABSENT, ABSENT)))
+    # slot map of the lane's generation: v[map0 ...] <- map + g * map_stride
+    E(Op("v_movs", (V_ADDR, 22)))
+    E(Op("v_movs", (V_ADDR + 1, 23)))
+    E(Op("v_mad64_s", (V_ADDR, V_G, 21, V_ADDR)))
+    E(Op("s_exec", (26,)))
+    for q in range(spec.map_quads):
+        E(Op("load16", (map0 + 4 * q, V_ADDR, 16 * q)))
+    E(Op("s_exec", (None,)))
+    for q in range(8 * r):
+        E(Op("v_movk", (acc0 + q, 0)))
+    E(Op("s_waitcnt_vm", (0,)))
+
+    def map_byte(entry) -> int:
+        kind, idx = entry
+        return idx if kind == "src" else k + idx
+
+    def slot_mask(entry, sm: int):
+        """v_slot <- slot (0 when absent), s[sm] <- valid & present."""
+        pos = map_byte(entry)
+        E(Op("s_exec", (26,)))
+        E(Op("v_bfe", (V_SLOT, map0 + pos // 4, 8 * (pos % 4), 8)))
+        E(Op("v_cmp_ne_s", (sm, S_ABSENT, V_SLOT)))
+        E(Op("s_nop", (4,)))
+        E(Op("v_cndmask_0", (V_SLOT, V_SLOT, sm)))
+
+    def load_row(n: int):
+        b = V_RING + 8 * (n % nbuf)
+        sm = S_MASK0 + 2 * (n % nbuf)
+        slot_mask(seq[n], sm)
+        E(Op("v_mad64_s", (V_ADDR, V_SLOT, 12, V_SRC)))
+        E(Op("load16", (b, V_ADDR, 0)))
+        E(Op("s_exec", (24,)))
+        E(Op("load16", (b + 4, V_ADDR, 16)))
+        E(Op("s_exec", (None,)))
+
+    n_seq = len(seq)
+    for n in range(min(pd, n_seq)):
+        load_row(n)
+    for n, (kind, idx) in enumerate(seq):
+        if n + pd < n_seq:
+            load_row(n + pd)
+        after = min(pd, n_seq - 1 - n)
+        E(Op("s_waitcnt_vm", (2 * after,)))
+        base = V_RING + 8 * (n % nbuf)
+        E(Op("s_exec", (S_MASK0 + 2 * (n % nbuf),)))
+        if kind == "rep":
+            ops.extend(_transpose_ops(base))
+            for b in range(8):
+                a = acc0 + 8 * idx + b
+                E(Op("v_xor", (a, a, base + b)))
+        else:
+            _source_row(ops, C, idx, r, base, acc0, init=False)
+        E(Op("s_exec", (None,)))
+    for j in range(r):
+        ops.extend(_transpose_ops(acc0 + 8 * j))
+    E(Op("s_nop", (4,)))
+    for j in range(r):
+        base = acc0 + 8 * j
+        slot_mask(("rep", j), S_TMP)
+        E(Op("s_exec", (S_TMP,)))
+        E(Op("store16", (V_DST, base, 0)))
+        E(Op("s_and64", (S_TMP, S_TMP, 24)))
+        E(Op("s_exec", (S_TMP,)))
+        E(Op("store16", (V_DST, base + 4, 16)))
+        E(Op("s_exec", (None,)))
+        E(Op("v_add64_s", (V_DST, V_DST, 34)))
+    _epilogue_next_item(E)
     return ops
 
 
@@ -403,7 +547,7 @@ def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
 \t\t.amdhsa_system_sgpr_workgroup_id_x 1
 \t\t.amdhsa_system_vgpr_workitem_id 0
 \t\t.amdhsa_next_free_vgpr {nv}
-\t\t.amdhsa_next_free_sgpr {SGPR_NEXT_FREE}
+\t\t.amdhsa_next_free_sgpr {spec.next_free_sgpr}
 \t\t.amdhsa_accum_offset {nv}
 \t\t.amdhsa_reserve_vcc 0
 \t\t.amdhsa_float_denorm_mode_32 3
@@ -424,7 +568,7 @@ amdhsa.kernels:
     .max_flat_workgroup_size: 256
     .name:           {name}
     .private_segment_fixed_size: 0
-    .sgpr_count:     {SGPR_NEXT_FREE + 6}
+    .sgpr_count:     {spec.next_free_sgpr + 6}
     .sgpr_spill_count: 0
     .symbol:         {name}.kd
     .vgpr_count:     {nv}
@@ -460,6 +604,36 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
     words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, 0, dgs, 0, srs, drs, L, U, total,
              magic, shift, n_items, total_waves, 0, 0, 0]
     return np.array(words, dtype=np.uint32).tobytes()
+
+
+def kernargs_syn(rows: int, syn: int, rgs: int, sgs: int, rs: int, srs: int, L: int, G: int,
+                 total_waves: int, smap: int, map_stride: int) -> bytes:
+    """Syndrome kernel: encode layout plus s21 = slot-map generation stride,
+    s[22:23] = slot map."""
+    w = np.frombuffer(kernargs(rows, syn, rgs, sgs, rs, srs, L, G, total_waves), np.uint32).copy()
+    w[17], w[18], w[19] = map_stride, smap & MASK32, smap >> 32
+    return w.tobytes()
+
+
+def cauchy_inverse(k: int, J: list[int], E: list[int]) -> list[list[int]]:
+    """D = C[J, E]^-1 in closed form (rows: erased sources E, columns: the
+    accepted repairs J in the given order).  With X_a = k + J[a] and
+    Y_b = E[b] (all distinct, k + r <= 256):
+      D[b][a] = A_a B_b / ((X_a + Y_b) E_a F_b),  A_a = prod_t (X_a + Y_t),
+      B_b = prod_t (X_t + Y_b), E_a = prod_{t!=a} (X_a + X_t),
+      F_b = prod_{t!=b} (Y_b + Y_t)."""
+    X = [(k + j) & 0xFF for j in J]
+    Y = list(E)
+    e = len(X)
+
+    def lg(v):
+        return _LOG[v]
+    lA = [sum(lg(X[a] ^ Y[t]) for t in range(e)) for a in range(e)]
+    lB = [sum(lg(X[t] ^ Y[b]) for t in range(e)) for b in range(e)]
+    lE = [sum(lg(X[a] ^ X[t]) for t in range(e) if t != a) for a in range(e)]
+    lF = [sum(lg(Y[b] ^ Y[t]) for t in range(e) if t != b) for b in range(e)]
+    return [[_EXP[(lA[a] + lB[b] - lg(X[a] ^ Y[b]) - lE[a] - lF[b]) % 255] for a in range(e)]
+            for b in range(e)]
 
 
 # --------------------------------------------------------------------------
@@ -595,6 +769,12 @@ class Emulator:
             elif n == "v_readfirstlane":
                 lane = int(np.argmax(exec_))
                 s[a[0]] = int(rv(a[1])[lane])
+            elif n == "v_bfe":
+                wv(a[0], (rv(a[1]) >> np.uint64(a[2])) & np.uint64((1 << a[3]) - 1))
+            elif n == "v_cmp_ne_s":
+                set_smask(a[0], (rv(a[2]) != np.uint64(s[a[1]])) & exec_)
+            elif n == "v_cndmask_0":
+                wv(a[0], np.where(smask(a[2]), rv(a[1]), np.uint64(0)))
             elif n == "load16":
                 d, ar, off = a
                 addr = rv64(ar)

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -68,6 +69,20 @@ struct qf_ctx {
     size_t stage_src_bytes = 0, stage_rep_bytes = 0;
     // bit-sliced Cauchy kernels (loaded on first use)
     qf::BsCache bs;
+    // kernel timing (qf_ctx_profile)
+    struct ProfPending {
+        size_t slot;
+        hipEvent_t a, b;
+    };
+    struct ProfTotal {
+        std::string name;
+        uint32_t launches;
+        double ms;
+    };
+    bool prof = false;
+    std::vector<ProfPending> prof_pending;
+    std::vector<ProfTotal> prof_tot;
+    std::vector<hipEvent_t> ev_free;
     std::mutex mu;
 };
 
@@ -145,6 +160,54 @@ int grow_work(qf_ctx* ctx, size_t bytes) {
     return QF_OK;
 }
 
+// --- kernel timing ---------------------------------------------------------
+hipEvent_t prof_begin(qf_ctx* ctx, hipStream_t st) {
+    if (!ctx->prof) return nullptr;
+    hipEvent_t a = nullptr;
+    if (!ctx->ev_free.empty()) {
+        a = ctx->ev_free.back();
+        ctx->ev_free.pop_back();
+    } else if (hipEventCreate(&a) != hipSuccess) {
+        return nullptr;
+    }
+    if (hipEventRecord(a, st) != hipSuccess) {
+        ctx->ev_free.push_back(a);
+        return nullptr;
+    }
+    return a;
+}
+
+void prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t a, const std::string& name) {
+    if (!a) return;
+    hipEvent_t b = nullptr;
+    if (!ctx->ev_free.empty()) {
+        b = ctx->ev_free.back();
+        ctx->ev_free.pop_back();
+    } else if (hipEventCreate(&b) != hipSuccess) {
+        ctx->ev_free.push_back(a);
+        return;
+    }
+    hipEventRecord(b, st);
+    size_t slot = 0;
+    while (slot < ctx->prof_tot.size() && ctx->prof_tot[slot].name != name) ++slot;
+    if (slot == ctx->prof_tot.size()) ctx->prof_tot.push_back({name, 0u, 0.0});
+    ctx->prof_pending.push_back({slot, a, b});
+}
+
+int prof_drain(qf_ctx* ctx) {
+    for (auto& p : ctx->prof_pending) {
+        QF_CHECK_HIP(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        QF_CHECK_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        ctx->prof_tot[p.slot].launches++;
+        ctx->prof_tot[p.slot].ms += ms;
+        ctx->ev_free.push_back(p.a);
+        ctx->ev_free.push_back(p.b);
+    }
+    ctx->prof_pending.clear();
+    return QF_OK;
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
@@ -175,8 +238,10 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
         sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
         (uint64_t)G * ((L + 31) / 32) < (1ull << 31)) {
+        hipEvent_t ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
                                    sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G));
+        prof_end(ctx, st, ev, qf::bs_name(k, r));
         return QF_OK;
     }
     for (uint32_t p = 0; p < passes; ++p) {
@@ -235,13 +300,82 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         a.L = L;
         a.Lu = Lu;
         a.total_units = (uint64_t)G * Lu;
+        hipEvent_t ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::launch_combine_uniform(a, (int)R, V, PD, ctx->num_cus, st));
+        prof_end(ctx, st, ev,
+                 "k_combine_uniform<" + std::to_string(R) + "," + std::to_string(V) + "," + std::to_string(PD) + ">");
         if (coeff) {
             QF_CHECK_HIP(hipEventRecord(ctx->custom_done, st));
             // a second pass rewrites the staging: wait for this pass first
             if (p + 1 < passes) QF_CHECK_HIP(hipEventSynchronize(ctx->custom_done));
         }
     }
+    return QF_OK;
+}
+
+// Decode of the reference's Cauchy code by syndromes (no row_coeffs):
+//   k_decode_prepare_cauchy  acceptance, slot map, D = C[J,E]^-1 (closed form)
+//   qf_cauchy_syn_k*_r*      s_j = p_j ^ sum_{i present} C[j][i] x_i  (bit-sliced)
+//   k_combine_slots          x_E = D s_J
+int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                  const uint16_t* row_index, const uint32_t* n_rows, uint8_t* rec,
+                  uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    const uint32_t ms = qf::syn_map_stride(k, r);
+    const uint64_t coef_gen_stride = (uint64_t)(r + 1) * 16;
+    const size_t off_bound = round_up((size_t)G * coef_gen_stride, 256);
+    const size_t off_map = round_up(off_bound + (size_t)G * 4, 256);
+    const size_t off_syn = round_up(off_map + (size_t)G * ms, 256);
+    const size_t total = off_syn + (size_t)G * r * L;
+    int s = grow_work(ctx, total);
+    if (s) return s;
+    uint8_t* w = ctx->d_work;
+    uint32_t* d_bound = reinterpret_cast<uint32_t*>(w + off_bound);
+    qf::PrepareCauchyArgs pa{};
+    pa.row_index = row_index;
+    pa.n_rows = n_rows;
+    pa.explog = ctx->d_explog;
+    pa.coef_out = w;
+    pa.smap = w + off_map;
+    pa.n_out = n_rec;
+    pa.bound = d_bound;
+    pa.rec_index = rec_index;
+    pa.status = status;
+    pa.k = k;
+    pa.r = r;
+    pa.e_max = std::min(k, r);
+    pa.max_rows = sh->max_rows;
+    pa.map_stride = ms;
+    pa.G = G;
+    hipStream_t st = ctx->stream;
+    hipEvent_t ev = prof_begin(ctx, st);
+    QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
+    prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
+    ev = prof_begin(ctx, st);
+    QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows, w + off_syn, sh->rows_gen_stride,
+                                (uint64_t)r * L, sh->row_stride, L, L, G, w + off_map, ms));
+    prof_end(ctx, st, ev, qf::syn_name(k, r));
+    qf::CombineSlotsArgs a{};
+    a.rows = w + off_syn;
+    a.rows_gen_stride = (uint64_t)r * L;
+    a.row_stride = L;
+    a.dst = rec;
+    a.dst_gen_stride = sh->rec_gen_stride;
+    a.dst_row_stride = sh->rec_row_stride;
+    a.coef = w;
+    a.coef_gen_stride = coef_gen_stride;
+    a.n_out = n_rec;
+    a.bound = d_bound;
+    a.tab256 = ctx->d_tab256;
+    a.pass = 0;
+    a.L = L;
+    a.Lu = (L + 15) / 16;
+    a.zero_slot = r;
+    a.total_units = (uint64_t)G * a.Lu;
+    const int PD = pick_PD("QF_DECODE_PD", 1, 2);
+    ev = prof_begin(ctx, st);
+    QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
+    prof_end(ctx, st, ev, "k_combine_slots<" + std::to_string(PD) + ">");
     return QF_OK;
 }
 
@@ -338,6 +472,11 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->custom_done) hipEventDestroy(c->custom_done);
     if (c->d_work) hipFree(c->d_work);
     qf::bs_unload(c->bs);
+    for (auto& p : c->prof_pending) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    for (auto e : c->ev_free) hipEventDestroy(e);
     for (int i = 0; i < qf_ctx::kPipe; ++i) {
         if (c->pstream[i]) {
             hipStreamSynchronize(c->pstream[i]);
@@ -365,6 +504,28 @@ int qf_ctx_set_stream(qf_ctx* ctx, void* stream) {
         QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
         ctx->own_stream = true;
     }
+    return QF_OK;
+}
+
+int qf_ctx_profile(qf_ctx* ctx, int on) {
+    if (!ctx) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = prof_drain(ctx);
+    if (s) return s;
+    if (on) ctx->prof_tot.clear();
+    ctx->prof = on != 0;
+    return QF_OK;
+}
+
+int qf_ctx_profile_read(qf_ctx* ctx, uint32_t i, const char** name, uint32_t* launches, double* total_ms) {
+    if (!ctx) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = prof_drain(ctx);
+    if (s) return s;
+    if (i >= ctx->prof_tot.size()) return QF_EINVAL;
+    if (name) *name = ctx->prof_tot[i].name.c_str();
+    if (launches) *launches = ctx->prof_tot[i].launches;
+    if (total_ms) *total_ms = ctx->prof_tot[i].ms;
     return QF_OK;
 }
 
@@ -476,6 +637,11 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     std::lock_guard<std::mutex> g(ctx->mu);
     int s = ensure_device(ctx);
     if (s) return s;
+    const char* nobs = getenv("QF_DISABLE_BS");
+    if (!row_coeffs && !(nobs && atoi(nobs)) && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
+        max_rows <= 255 && L % 16 == 0 && L >= 64 && sh->rows_gen_stride < (1ull << 32) &&
+        sh->row_stride < (1ull << 32) && (uint64_t)G * ((L + 31) / 32) < (1ull << 31))
+        return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
     const uint32_t passes = (e_max + 15) / 16;
     const uint64_t coef_gen_stride = ((uint64_t)max_rows + 1) * 16;
     const size_t coef_bytes = (size_t)std::max<uint32_t>(passes, 1) * G * coef_gen_stride;
@@ -498,12 +664,15 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     pa.k = k;
     pa.e_max = e_max;
     pa.e_lds = std::min<uint32_t>(k, 128);
+    pa.rep_limit = row_coeffs ? 256 : r;
     pa.max_rows = max_rows;
     pa.max_rows_pad = (max_rows + 7) & ~7u;
     pa.passes = passes;
     pa.G = G;
     if (qf::prepare_lds_bytes(k, pa.e_lds, max_rows) > 160 * 1024) return QF_EINVAL;
+    hipEvent_t ev = prof_begin(ctx, ctx->stream);
     QF_CHECK_HIP(qf::launch_decode_prepare(pa, ctx->stream));
+    prof_end(ctx, ctx->stream, ev, "k_decode_prepare");
     const uint32_t Lu = (L + 15) / 16;
     for (uint32_t p = 0; p < passes; ++p) {
         qf::CombineSlotsArgs a{};
@@ -523,7 +692,10 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
         a.Lu = Lu;
         a.zero_slot = max_rows;
         a.total_units = (uint64_t)G * Lu;
-        QF_CHECK_HIP(qf::launch_combine_slots(a, pick_PD("QF_DECODE_PD", 1, 2), ctx->num_cus, ctx->stream));
+        const int PD = pick_PD("QF_DECODE_PD", 1, 2);
+        hipEvent_t ev2 = prof_begin(ctx, ctx->stream);
+        QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, ctx->stream));
+        prof_end(ctx, ctx->stream, ev2, "k_combine_slots<" + std::to_string(PD) + ">");
     }
     return QF_OK;
 }

@@ -14,6 +14,8 @@
 
 struct QfBsEntry {
     uint32_t k, r, pd;
+    char mode;  // 'e' encode, 's' decode syndromes
+    uint32_t map_stride;
     const char* name;
     const unsigned char* data;
     size_t size;
@@ -22,13 +24,29 @@ struct QfBsEntry {
 
 namespace qf {
 
-static const QfBsEntry* bs_find(uint32_t k, uint32_t r) {
+static const QfBsEntry* find(char mode, uint32_t k, uint32_t r) {
     for (const auto& e : qf_bs_table)
-        if (e.k == k && e.r == r) return &e;
+        if (e.mode == mode && e.k == k && e.r == r) return &e;
     return nullptr;
 }
 
-bool bs_available(uint32_t k, uint32_t r) { return bs_find(k, r) != nullptr; }
+bool bs_available(uint32_t k, uint32_t r) { return find('e', k, r) != nullptr; }
+bool syn_available(uint32_t k, uint32_t r) { return find('s', k, r) != nullptr; }
+
+const char* bs_name(uint32_t k, uint32_t r) {
+    const QfBsEntry* e = find('e', k, r);
+    return e ? e->name : nullptr;
+}
+
+const char* syn_name(uint32_t k, uint32_t r) {
+    const QfBsEntry* e = find('s', k, r);
+    return e ? e->name : nullptr;
+}
+
+uint32_t syn_map_stride(uint32_t k, uint32_t r) {
+    const QfBsEntry* e = find('s', k, r);
+    return e ? e->map_stride : 0;
+}
 
 static void magic_for(uint32_t U, uint32_t* magic, uint32_t* shift) {
     uint32_t s = 0;
@@ -38,10 +56,10 @@ static void magic_for(uint32_t U, uint32_t* magic, uint32_t* shift) {
     *shift = s - 1;
 }
 
-hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
-                     const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
-                     uint64_t drs, uint32_t L, uint32_t G) {
-    const QfBsEntry* e = bs_find(k, r);
+// Shared launch: kernarg words 0..16 as bs_codegen.kernargs, 17..19 extra.
+static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStream_t st,
+                         const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
+                         uint64_t drs, uint32_t L, uint32_t G, const uint32_t extra[3]) {
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return hipErrorInvalidValue;
@@ -57,7 +75,7 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     uint32_t magic, shift;
     magic_for(U, &magic, &shift);
     const uint32_t n_items = (uint32_t)((total + 63) / 64);
-    // 208 VGPRs -> 2 waves per SIMD -> two 256-thread blocks per CU
+    // > 128 VGPRs -> 2 waves per SIMD -> two 256-thread blocks per CU
     uint32_t blocks = (n_items + 3) / 4;
     const uint32_t cap = (uint32_t)num_cus * 2;
     if (blocks > cap) blocks = cap;
@@ -79,10 +97,30 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     a[14] = shift;
     a[15] = n_items;
     a[16] = blocks * 4;
+    if (extra) {
+        a[17] = extra[0];
+        a[18] = extra[1];
+        a[19] = extra[2];
+    }
     size_t sz = sizeof(a);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
     return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+}
+
+hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                     const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
+                     uint64_t drs, uint32_t L, uint32_t G) {
+    return launch(cache, find('e', k, r), num_cus, st, src, dst, sgs, dgs, srs, drs, L, G, nullptr);
+}
+
+hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                      const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
+                      uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride) {
+    const QfBsEntry* e = find('s', k, r);
+    if (!e || map_stride != e->map_stride) return hipErrorInvalidValue;
+    const uint32_t extra[3] = {map_stride, (uint32_t)(uintptr_t)smap, (uint32_t)((uintptr_t)smap >> 32)};
+    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, extra);
 }
 
 void bs_unload(BsCache& cache) {

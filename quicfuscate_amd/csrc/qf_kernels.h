@@ -62,12 +62,36 @@ struct PrepareArgs {
     int32_t* status;
     uint32_t k;
     uint32_t e_max;   // output capacity min(k, r)
+    uint32_t rep_limit;  // repair index j = row_index - k must be < rep_limit
     uint32_t e_lds;   // matrix rows held in LDS, min(k, 128)
     uint32_t max_rows;
     uint32_t max_rows_pad;
     uint32_t passes;
     uint32_t G;
 };
+
+// Decode control for the reference's Cauchy code (no row_coeffs): row
+// acceptance as k_decode_prepare, then the closed-form inverse of the square
+// Cauchy submatrix C[J, E] (no elimination).  Outputs the slot map of the
+// syndrome kernel and the stage-B coefficient records (slot j = syndrome of
+// repair j, record r all zero).
+struct PrepareCauchyArgs {
+    const uint16_t* row_index;
+    const uint32_t* n_rows;
+    const uint8_t* explog;
+    uint8_t* coef_out;      // [G][(r + 1) * 16]
+    uint8_t* smap;          // [G][map_stride]: k source slots, r repair slots, 0xFF absent
+    uint32_t* n_out;
+    uint32_t* bound;
+    uint16_t* rec_index;    // [G][e_max]
+    int32_t* status;
+    uint32_t k, r;
+    uint32_t e_max;
+    uint32_t max_rows;      // <= 255
+    uint32_t map_stride;
+    uint32_t G;
+};
+hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st);
 
 // PD: prefetch depth in row pairs (V=1: 1..3, V=2: 1..2); k_pad must be a
 // multiple of 2*(PD+1).

@@ -507,7 +507,7 @@ __global__ void __launch_bounds__(64) k_decode_prepare(PrepareArgs a) {
     for (uint32_t s = lane; s < n; s += 64) {
         const uint32_t idx = ridx[s];
         if (idx < k) atomicMin(&L.first[idx], s);
-        else if (idx - k >= 256) bad = true;
+        else if (idx - k >= a.rep_limit) bad = true;
     }
     for (uint32_t s = lane; s < a.max_rows; s += 64) L.slot_col[s] = 0xFFFF;
     __syncthreads();
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(64) k_decode_prepare(PrepareArgs a) {
         bool cand = false;
         if (s < n) {
             idx = ridx[s];
-            cand = idx >= k ? (idx - k < 256) : (L.first[idx] == s);
+            cand = idx >= k ? (idx - k < a.rep_limit) : (L.first[idx] == s);
         }
         const uint64_t bc = __ballot(cand);
         const uint32_t pos = accepted + __popcll(bc & lt_mask);
@@ -661,6 +661,160 @@ __global__ void __launch_bounds__(64) k_decode_prepare(PrepareArgs a) {
         a.status[g] = status;
         a.n_out[g] = status == 0 ? e : 0;
         a.bound[g] = status == 0 ? bound : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decode control, Cauchy code: one wave per generation.
+//
+// Acceptance is k_decode_prepare's (first k candidate rows in arrival order;
+// a source counts once, at its first slot; decoder.rs:678-701).  With the
+// accepted repairs J (arrival order) and the erased sources E (ascending),
+// the syndromes s_J = C[J, E] x_E come from the syndrome kernel and
+// x_E = D s_J with D = C[J, E]^-1 in closed form (Cauchy matrix,
+// X_a = k + J[a], Y_b = E[b]):
+//   D[b][a] = A_a B_b / ((X_a + Y_b) E_a F_b),
+//   A_a = prod_t (X_a + Y_t), B_b = prod_t (X_t + Y_b),
+//   E_a = prod_{t != a} (X_a + X_t), F_b = prod_{t != b} (Y_b + Y_t).
+// A square Cauchy matrix is nonsingular, so the only singular systems are
+// repeated repair indices (identical rows), reported as QF_ERANK exactly as
+// Gauss-Jordan does.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs a) {
+    __shared__ uint8_t sexp[512];
+    __shared__ uint8_t slog[256];
+    __shared__ uint32_t first[256];
+    __shared__ uint8_t sys_slot[256];
+    __shared__ uint8_t rep_slot[256];   // by repair index j
+    __shared__ uint32_t rep_cnt[256];
+    __shared__ uint8_t J[256], Eidx[256];
+    __shared__ uint32_t lA[256], lB[256], lE[256], lF[256];
+    __shared__ __attribute__((aligned(16))) uint8_t rec[17 * 16];
+    const uint32_t g = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k = a.k, r = a.r;
+    for (uint32_t i = lane; i < 768; i += 64) {
+        if (i < 512) sexp[i] = a.explog[i];
+        else slog[i - 512] = a.explog[i];
+    }
+    for (uint32_t i = lane; i < 256; i += 64) {
+        first[i] = 0xFFFFFFFFu;
+        sys_slot[i] = 0xFF;
+        rep_slot[i] = 0xFF;
+        rep_cnt[i] = 0;
+    }
+    for (uint32_t i = lane; i < 17 * 16; i += 64) rec[i] = 0;
+    __syncthreads();
+    const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
+    const uint16_t* ridx = a.row_index + (uint64_t)g * a.max_rows;
+    bool bad = false;
+    for (uint32_t s = lane; s < n; s += 64) {
+        const uint32_t idx = ridx[s];
+        if (idx < k) atomicMin(&first[idx], s);
+        else if (idx - k >= r) bad = true;
+    }
+    __syncthreads();
+    int32_t status = __any(bad) ? -1 : 0;  // QF_EINVAL
+    uint32_t accepted = 0, nrep = 0, bound = 0;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t s0 = 0; s0 < n && accepted < k; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        uint32_t idx = 0;
+        bool cand = false;
+        if (s < n) {
+            idx = ridx[s];
+            cand = idx >= k ? (idx - k < r) : (first[idx] == s);
+        }
+        const uint64_t bc = __ballot(cand);
+        const uint32_t pos = accepted + __popcll(bc & lt_mask);
+        const bool acc = cand && pos < k;
+        const bool isrep = acc && idx >= k;
+        const uint64_t br = __ballot(isrep);
+        const uint32_t rpos = nrep + __popcll(br & lt_mask);
+        if (acc) {
+            if (idx < k) {
+                sys_slot[idx] = (uint8_t)s;
+            } else {
+                const uint32_t j = idx - k;
+                J[rpos] = (uint8_t)j;
+                rep_slot[j] = (uint8_t)s;
+                atomicAdd(&rep_cnt[j], 1u);
+                bound = max(bound, j + 1);
+            }
+        }
+        accepted += __popcll(__ballot(acc));
+        nrep += __popcll(br);
+    }
+    // wave max of the highest accepted repair index
+    for (int off = 32; off >= 1; off >>= 1) bound = max(bound, (uint32_t)__shfl_xor((int)bound, off, 64));
+    __syncthreads();
+    const uint32_t e = nrep;
+    if (status == 0 && accepted < k) status = -3;  // QF_ENOTREADY
+    bool dup = false;
+    for (uint32_t j = lane; j < r; j += 64) dup |= rep_cnt[j] > 1;
+    if (status == 0 && __any(dup)) status = -4;    // QF_ERANK: repeated repair rows
+    if (status == 0 && e > 0) {
+        uint32_t ne = 0;
+        for (uint32_t i0 = 0; i0 < k; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool miss = i < k && sys_slot[i] == 0xFF;
+            const uint64_t bm = __ballot(miss);
+            if (miss) Eidx[ne + __popcll(bm & lt_mask)] = (uint8_t)i;
+            ne += __popcll(bm);
+        }
+        __syncthreads();
+        for (uint32_t q = lane; q < e; q += 64) {
+            const uint32_t X = (k + J[q]) & 0xFF, Y = Eidx[q];
+            uint32_t sa = 0, sb = 0, se = 0, sf = 0;
+            for (uint32_t t = 0; t < e; ++t) {
+                const uint32_t Xt = (k + J[t]) & 0xFF, Yt = Eidx[t];
+                sa += slog[X ^ Yt];
+                sb += slog[Xt ^ Y];
+                if (t != q) {
+                    se += slog[X ^ Xt];
+                    sf += slog[Y ^ Yt];
+                }
+            }
+            lA[q] = sa % 255;
+            lB[q] = sb % 255;
+            lE[q] = se % 255;
+            lF[q] = sf % 255;
+        }
+        __syncthreads();
+        for (uint32_t t = lane; t < e * e; t += 64) {
+            const uint32_t b = t / e, q = t - b * e;
+            const uint32_t X = (k + J[q]) & 0xFF, Y = Eidx[b];
+            const uint32_t num = lA[q] + lB[b];
+            const uint32_t den = slog[X ^ Y] + lE[q] + lF[b];  // < 3 * 255
+            const uint32_t l = (num + 3 * 255 - den) % 255;
+            rec[J[q] * 16 + b] = sexp[l];
+        }
+        __syncthreads();
+    }
+    const bool ok = status == 0;
+    // stage-B records: slot j < r = syndrome of repair j, slot r = zero
+    uint8_t* co = a.coef_out + (uint64_t)g * (r + 1) * 16;
+    for (uint32_t j = lane; j <= r; j += 64) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ok && j < r) v = *reinterpret_cast<const uint4*>(rec + j * 16);
+        *reinterpret_cast<uint4*>(co + j * 16) = v;
+    }
+    // slot map for the syndrome kernel (all absent when the generation fails)
+    uint8_t* sm = a.smap + (uint64_t)g * a.map_stride;
+    for (uint32_t q = lane; q < a.map_stride; q += 64) {
+        uint8_t v = 0xFF;
+        if (ok) {
+            if (q < k) v = sys_slot[q];
+            else if (q < k + r) v = rep_slot[q - k];
+        }
+        sm[q] = v;
+    }
+    if (ok)
+        for (uint32_t b = lane; b < e; b += 64) a.rec_index[(uint64_t)g * a.e_max + b] = Eidx[b];
+    if (lane == 0) {
+        a.status[g] = status;
+        a.n_out[g] = ok ? e : 0;
+        a.bound[g] = ok ? bound : 0;
     }
 }
 
@@ -825,6 +979,13 @@ hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st) {
     }
     if (a.G == 0) return hipSuccess;
     hipLaunchKernelGGL(k_decode_prepare, dim3(a.G), dim3(64), lds, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st) {
+    if (a.G == 0) return hipSuccess;
+    if (a.r > 16 || a.k + a.r > 256 || a.max_rows > 255 || a.map_stride < a.k + a.r) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_decode_prepare_cauchy, dim3(a.G), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

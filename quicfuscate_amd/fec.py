@@ -83,6 +83,24 @@ class Context:
     def sync(self) -> None:
         check(L._lib().qf_sync(self.handle), "sync")
 
+    def profile(self, on: bool) -> None:
+        """Start (clearing totals) or stop per-kernel event timing."""
+        check(L._lib().qf_ctx_profile(self.handle, 1 if on else 0), "profile")
+
+    def kernel_times(self) -> dict:
+        """{kernel name: (launches, total ms)} accumulated while profiling."""
+        out = {}
+        i = 0
+        lib = L._lib()
+        while True:
+            name, n, ms = ctypes.c_char_p(), ctypes.c_uint32(), ctypes.c_double()
+            s = lib.qf_ctx_profile_read(self.handle, i, ctypes.byref(name), ctypes.byref(n), ctypes.byref(ms))
+            if s == L.QF_EINVAL:
+                return out
+            check(s, "profile_read")
+            out[name.value.decode()] = (n.value, ms.value)
+            i += 1
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             L._lib().qf_ctx_destroy(self.handle)

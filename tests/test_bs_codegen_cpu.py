@@ -69,3 +69,118 @@ def test_mul_matrix_rows_reproduce_field():
             for b in range(8):
                 y |= (bin(rows[b] & x).count("1") & 1) << b
             assert y == bs.gf_mul(c, x)
+
+
+def _gf_matvec(D, rows):
+    """sum_a D[b][a] * rows[a] over GF(256) (rows: e x L uint8)."""
+    out = np.zeros((len(D), rows.shape[1]), np.uint8)
+    for b, Db in enumerate(D):
+        for a, c in enumerate(Db):
+            out[b] ^= np.array([bs.gf_mul(c, int(x)) for x in range(256)], np.uint8)[rows[a]]
+    return out
+
+
+@pytest.mark.parametrize("k,r,pd,L,G,waves", [
+    (8, 4, 2, 96, 6, 2),
+    (8, 4, 3, 80, 7, 2),      # half chunks
+    (16, 16, 4, 64, 5, 1),
+    (5, 3, 1, 64, 9, 1),
+])
+def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves):
+    """Decode stage A on the emulator: syndromes of the accepted repairs, and
+    the closed-form Cauchy inverse applied to them gives the erased sources."""
+    spec = bs.KernelSpec(k, r, pd, mode="syn")
+    ops = bs.generate(spec)
+    rng = np.random.default_rng(7 * k + r + L)
+    rs = L + 16
+    n_slots = k + 2
+    rgs = n_slots * rs + 16
+    srs = L + 32
+    sgs = r * srs
+    mstride = spec.map_stride
+    rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
+    smap = np.full(G * mstride, 0xFF, np.uint8)
+    syn = np.full(G * sgs, 0xEE, np.uint8)
+    plans = []
+    for g in range(G):
+        src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        rep = oracle.encode(src, r)
+        e = int(rng.integers(0, min(k, r) + 1))
+        E = sorted(rng.choice(k, e, replace=False).tolist())
+        J = rng.choice(r, e, replace=False).tolist()
+        present = [("s", i) for i in range(k) if i not in E] + [("p", j) for j in J]
+        order = rng.permutation(len(present))
+        slots = rng.choice(n_slots, len(present), replace=False)  # spare slots stay junk
+        for n, pi in enumerate(order):
+            kind, idx = present[pi]
+            sl = int(slots[n])
+            data = src[idx] if kind == "s" else rep[idx]
+            rows[g * rgs + sl * rs: g * rgs + sl * rs + L] = data
+            smap[g * mstride + (idx if kind == "s" else k + idx)] = sl
+        plans.append((src, rep, E, J))
+    emu = bs.Emulator(ops)
+    ROWS, SYN, MAP = 0x10000000, 0x40000000, 0x70000000
+    emu.add_buffer(ROWS, rows)
+    emu.add_buffer(SYN, syn)
+    emu.add_buffer(MAP, smap)
+    ka = bs.kernargs_syn(ROWS, SYN, rgs, sgs, rs, srs, L, G, waves * 4, MAP, mstride)
+    for wg in range(waves):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    C = np.array(bs.cauchy(k, r), np.uint8)
+    for g, (src, rep, E, J) in enumerate(plans):
+        got = {}
+        for j in range(r):
+            blk = syn[g * sgs + j * srs: g * sgs + (j + 1) * srs]
+            if j not in J:
+                assert (blk == 0xEE).all(), (g, j)
+                continue
+            assert (blk[L:] == 0xEE).all()
+            want = rep[j].copy()
+            for i in range(k):
+                if i not in E:
+                    want ^= np.array([bs.gf_mul(int(C[j, i]), x) for x in range(256)], np.uint8)[src[i]]
+            assert (blk[:L] == want).all(), (g, j)
+            got[j] = blk[:L]
+        if E:
+            D = bs.cauchy_inverse(k, J, E)
+            rec = _gf_matvec(D, np.stack([got[j] for j in J]))
+            assert (rec == src[E]).all(), g
+
+
+def test_cauchy_inverse_closed_form():
+    rng = np.random.default_rng(3)
+    for _ in range(60):
+        k = int(rng.integers(1, 200))
+        r = int(rng.integers(1, min(40, 256 - k) + 1))
+        e = int(rng.integers(1, min(k, r) + 1))
+        E = sorted(rng.choice(k, e, replace=False).tolist())
+        J = rng.choice(r, e, replace=False).tolist()
+        C = [[bs.gf_inv(((k + j) & 255) ^ i) for i in E] for j in J]
+        D = bs.cauchy_inverse(k, J, E)
+        for b in range(e):
+            for c in range(e):
+                acc = 0
+                for a in range(e):
+                    acc ^= bs.gf_mul(D[b][a], C[a][c])
+                assert acc == (1 if b == c else 0)
+
+
+@pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "syn"), (16, 1, "syn"), (32, 16, "enc")])
+def test_declared_register_budget_covers_code(k, r, mode):
+    """Every VGPR / SGPR the generated code names lies below the
+    .amdhsa_next_free_* counts of its kernel descriptor."""
+    import re
+
+    spec = bs.KernelSpec(k, r, 4, mode)
+    text = bs.emit_asm(spec, bs.generate(spec))
+    body, desc = text.split(".amdhsa_kernel", 1)
+    nv = int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", desc).group(1))
+    ns = int(re.search(r"\.amdhsa_next_free_sgpr (\d+)", desc).group(1))
+    vmax = smax = 0
+    for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", body):
+        vmax = max(vmax, int(m.group(2) or m.group(3)))
+    for m in re.finditer(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b", body):
+        smax = max(smax, int(m.group(2) or m.group(3)))
+    assert vmax < nv, (vmax, nv)
+    assert smax < ns, (smax, ns)

@@ -13,7 +13,7 @@ def _r16(x):
 
 
 def make_batch(oracle, rng, k, r, L, G, max_rows, *, dup_prob=0.0, shuffle=True, erase=None,
-               coeff_mode="cauchy"):
+               coeff_mode="cauchy", trim_prob=0.0):
     """Per generation: source rows, repairs, an arrival list (row index per slot)."""
     src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
     gens = []
@@ -33,6 +33,8 @@ def make_batch(oracle, rng, k, r, L, G, max_rows, *, dup_prob=0.0, shuffle=True,
             for a in extra:
                 arr.insert(int(rng.integers(0, len(arr) + 1)), a)
         arr = arr[:max_rows]
+        if trim_prob and rng.random() < trim_prob:  # fewer rows than needed -> ENOTREADY
+            arr = arr[: int(rng.integers(0, k))]
         rows = np.stack([src[g, a] if a < k else rep[a - k] for a in arr]) if arr else np.zeros((0, L), np.uint8)
         rc = np.stack([np.zeros(k, np.uint8) if a < k else C[a - k] for a in arr]) if arr else None
         gens.append((arr, rows, rc))
@@ -95,9 +97,25 @@ def check(oracle, k, L, src, gens, out, with_coeffs):
             assert (rec[g * rec_gs + m * rrs + L: g * rec_gs + (m + 1) * rrs] == 0x5A).all()
 
 
+PATHS = ["default", "general"]
+
+
+def _path(monkeypatch, path):
+    # "default": syndrome decode where a bit-sliced kernel exists for (k, r)
+    # (Cauchy code, L % 16 == 0); "general": Gauss-Jordan + slots kernel
+    if path == "general":
+        monkeypatch.setenv("QF_DISABLE_BS", "1")
+    else:
+        monkeypatch.delenv("QF_DISABLE_BS", raising=False)
+
+
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("k,r,L,G", [(64, 16, 1200, 40), (16, 16, 100, 30), (4, 2, 8, 20),
-                                     (10, 2, 8, 20), (33, 7, 37, 25), (1, 3, 16, 10)])
-def test_decode_matches_oracle_random_erasures(qf, oracle, gpu_ctx, k, r, L, G):
+                                     (10, 2, 8, 20), (33, 7, 37, 25), (1, 3, 16, 10),
+                                     (16, 16, 96, 30), (32, 16, 64, 25), (64, 10, 1216, 20),
+                                     (16, 1, 64, 40), (64, 16, 80, 50)])
+def test_decode_matches_oracle_random_erasures(qf, oracle, gpu_ctx, k, r, L, G, path, monkeypatch):
+    _path(monkeypatch, path)
     rng = np.random.default_rng(k + r + L)
     max_rows = k + r
     src, gens = make_batch(oracle, rng, k, r, L, G, max_rows)
@@ -105,7 +123,23 @@ def test_decode_matches_oracle_random_erasures(qf, oracle, gpu_ctx, k, r, L, G):
     check(oracle, k, L, src, gens, out, False)
 
 
-def test_decode_bench_shape_fixed_13_erasures(qf, oracle, gpu_ctx):
+@pytest.mark.parametrize("path", PATHS)
+def test_decode_cauchy_duplicates_and_short_generations(qf, oracle, gpu_ctx, path, monkeypatch):
+    # duplicated sources (counted once) and repairs (singular -> ERANK), and
+    # generations with fewer than k rows (ENOTREADY), mixed in one batch
+    _path(monkeypatch, path)
+    rng = np.random.default_rng(99)
+    k, r, L, G = 16, 16, 64, 120
+    max_rows = 48
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, dup_prob=0.08, trim_prob=0.15)
+    out = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+    assert {0, -3, -4} <= set(out[3].tolist())
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_decode_bench_shape_fixed_13_erasures(qf, oracle, gpu_ctx, path, monkeypatch):
+    _path(monkeypatch, path)
     # k=64, 13 erased sources, arrival = surviving sources then repairs
     rng = np.random.default_rng(2024)
     k, r, L, G = 64, 16, 1200, 24
@@ -123,6 +157,24 @@ def test_decode_explicit_coefficients_and_duplicates(qf, oracle, gpu_ctx):
     out = run_decode(qf, k, r, L, G, max_rows, gens, True)
     check(oracle, k, L, src, gens, out, True)
     assert set(out[3].tolist()) >= {0}
+
+
+def test_decode_repair_index_out_of_range(qf, oracle, gpu_ctx):
+    # without row_coeffs a repair row's index must be < k + r (its Cauchy row)
+    rng = np.random.default_rng(4)
+    k, r, L = 16, 16, 64
+    src = rng.integers(0, 256, (2, k, L), dtype=np.uint8)
+    rep = oracle.encode(src[0], r)
+    gens = [(list(range(1, k)) + [k + r], np.vstack([src[0, 1:], rep[:1]]), None),
+            (list(range(k)), src[1], None)]
+    for path in PATHS:
+        import os
+        os.environ.pop("QF_DISABLE_BS", None)
+        if path == "general":
+            os.environ["QF_DISABLE_BS"] = "1"
+        out = run_decode(qf, k, r, L, 2, k, gens, False)
+        os.environ.pop("QF_DISABLE_BS", None)
+        assert list(out[3]) == [-1, 0], path
 
 
 def test_decode_not_enough_rows_and_singular(qf, oracle, gpu_ctx):
