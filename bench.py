@@ -55,6 +55,21 @@ def arrival_index(erased: np.ndarray, k: int, r: int) -> np.ndarray:
     return np.concatenate([surv, reps], axis=1).astype(np.uint16)
 
 
+def payload_word_offset(rank: int, G: int, k: int, L: int) -> int:
+    """splitmix64 word index of a rank's first source byte: every rank
+    encodes distinct payload (the global generation index picks the words)."""
+    return (rank * G * k * L) // 8
+
+
+def reduce_max(torch, dist, values, world: int, device) -> list:
+    """Max over ranks of [step_ms, enc_ms, dec_ms, failed] (the bench
+    contract: the slowest rank defines the step time; any failure fails)."""
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,7 +114,7 @@ def main(argv=None):
     # --- inputs (resident in HBM before timing) ---------------------------
     src = torch.empty(G * k * Lb, dtype=torch.uint8, device=dev)
     rep = torch.empty(G * r * Lb, dtype=torch.uint8, device=dev)
-    word_off = (rank * G * k * Lb) // 8  # global generation index -> distinct payload
+    word_off = payload_word_offset(rank, G, k, Lb)
     L.check(lib.qf_fill_splitmix_dev(ctx.handle, src.data_ptr(), src.numel(), SEED, word_off), "fill")
     enc_args = dict(src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lb, rep_gen_stride=r * Lb, G=G)
     fec.encode_batch(src, rep, k, r, Lb, ctx=ctx, **enc_args)
@@ -174,10 +189,8 @@ def main(argv=None):
     checksum = int(rep.view(torch.int64).sum().item()) & ((1 << 64) - 1)
     verified = st_ok and n_ok and idx_ok and bytes_ok
 
-    t = torch.tensor([step_ms, enc_ms, dec_ms, 0.0 if verified else 1.0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    step_ms_max, enc_ms_max, dec_ms_max, fails = t.tolist()
+    step_ms_max, enc_ms_max, dec_ms_max, fails = reduce_max(
+        torch, dist, [step_ms, enc_ms, dec_ms, 0.0 if verified else 1.0], world, dev)
 
     src_bytes_total = world * G * k * Lb
     gib = 1 << 30

@@ -1,0 +1,80 @@
+"""Multi-rank bench logic on CPU (gloo, world size 2): generation sharding,
+distinct per-rank payload, and the max-over-ranks reduction bench.py uses
+(independent generations, no data-path collective)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bench
+
+
+def test_shards_partition_generations():
+    for total in (1, 7, 65536, 156250):
+        for world in (1, 2, 4, 8):
+            ranges = [bench.shard_generations(total, r, world) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == total
+            for (a, b), (c, d) in zip(ranges, ranges[1:]):
+                assert b == c and a <= b
+            sizes = [b - a for a, b in ranges]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_payload_offsets_distinct_and_disjoint():
+    G, k, L = 1000, 64, 1200
+    offs = [bench.payload_word_offset(r, G, k, L) for r in range(8)]
+    words = G * k * L // 8
+    assert all(b - a == words for a, b in zip(offs, offs[1:]))
+
+
+def test_erasure_plan_seeded_and_arrival_order():
+    e1 = bench.erasure_plan(50, 64, 13, 7)
+    e2 = bench.erasure_plan(50, 64, 13, 7)
+    assert (e1 == e2).all() and e1.shape == (50, 13)
+    assert all(len(set(row)) == 13 and list(row) == sorted(row) for row in e1)
+    a = bench.arrival_index(e1, 64, 16)
+    assert a.shape == (50, 64 - 13 + 16)
+    for g in range(50):
+        surv = [i for i in range(64) if i not in set(e1[g])]
+        assert list(a[g]) == surv + list(range(64, 80))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = bench.shard_generations(1000, rank, world)
+    # rank-dependent "timings"; rank 1 reports a failed verification
+    vals = [10.0 + rank, 3.0 * (rank + 1), 7.0 - rank, float(rank == 1)]
+    out = bench.reduce_max(torch, dist, vals, world, "cpu")
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, lo, hi, out))
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_max_over_ranks():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert [(r, lo, hi) for r, lo, hi, _ in res] == [(0, 0, 500), (1, 500, 1000)]
+    for _, _, _, out in res:
+        assert np.allclose(out, [11.0, 6.0, 7.0, 1.0])
