@@ -107,6 +107,7 @@ _ASM = {
     "label": lambda n: f"{n}:",
     "v_xor": lambda d, a, b: f"v_xor_b32_e32 {V(d)}, {V(a)}, {V(b)}",
     "v_mov": lambda d, a: f"v_mov_b32_e32 {V(d)}, {V(a)}",
+    "v_xor3": lambda d, a, b, c: f"v_bitop3_b32 {V(d)}, {V(a)}, {V(b)}, {V(c)} bitop3:0x96",
     "v_movk": lambda d, k: f"v_mov_b32_e32 {V(d)}, {k}",
     "v_andk": lambda d, k, a: f"v_and_b32_e32 {V(d)}, 0x{k:08x}, {V(a)}",
     "v_lshr": lambda d, s, a: f"v_lshrrev_b32_e32 {V(d)}, {s}, {V(a)}",
@@ -126,7 +127,7 @@ _ASM = {
     "v_readfirstlane": lambda s, a: f"v_readfirstlane_b32 s{s}, {V(a)}",
     "v_bfe": lambda d, a, off, w: f"v_bfe_u32 {V(d)}, {V(a)}, {off}, {w}",
     "v_cmp_ne_s": lambda sd, s, a: f"v_cmp_ne_u32_e64 {SP(sd)}, s{s}, {V(a)}",
-    "v_cndmask_0": lambda d, a, sm: f"v_cndmask_b32_e64 {V(d)}, 0, {V(a)}, {SP(sm)}",
+    "v_cndmask": lambda d, a, b, sm: f"v_cndmask_b32_e64 {V(d)}, {V(a)}, {V(b)}, {SP(sm)}",
     "load16": lambda d, a, off: f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
     "store16": lambda a, d, off: f"global_store_dwordx4 {VP(a)}, {VQ(d)}, off" + (f" offset:{off}" if off else ""),
     "s_exec": lambda s: "s_mov_b64 exec, -1" if s is None else f"s_mov_b64 exec, {SP(s)}",
@@ -148,32 +149,33 @@ _ASM = {
 # --------------------------------------------------------------------------
 # Kernel layout
 # --------------------------------------------------------------------------
-# kernarg (80 bytes): s[4:5] src, s[6:7] dst, s8 src_gen_stride (u32), s9 pad,
-# s10 dst_gen_stride (u32), s11 pad, s12 src_row_stride, s13 dst_row_stride,
-# s14 L, s15 U (32-byte chunks per row), s16 total chunks, s17 magic,
-# s18 shift, s19 n_items, s20 total waves, s21..s23 pad.
-# SGPRs: s[24:25] full-chunk mask, s[26:27] valid mask, s28 item,
-# s29 wave, s[32:33] {src_row_stride, 0}, s[34:35] {dst_row_stride, 0},
-# s[36:37] mad carry sink.
+# Work unit: a wave handles one "item" of 128 consecutive 16-byte units of
+# the flat (generation, unit) space; lane l owns units A = 128*item + l and
+# B = A + 64, so every global_load_dwordx4 / store covers 1 KiB of
+# consecutive units (two row segments at most).  A lane's two halves may
+# belong to different generations: the encode coefficients are the same for
+# all generations, and in syndrome mode each half gathers its own rows.
 #
-# Syndrome mode ("syn", decode stage A) uses the same registers with:
-# s[4:5] received rows, s[6:7] syndrome rows, s8 rows_gen_stride,
-# s10 syn_gen_stride, s12 row_stride, s13 syn_row_stride, s21 slot-map
-# generation stride, s[22:23] slot map; s[38:39] mask temp, s[40+2q] the
-# present-lane mask of ring buffer q; v2:3 = generation base of the lane's
-# chunk, v34:35 per-row address, v36 slot; map registers after the
-# accumulators.
+# kernarg (80 bytes, s4..s23):
+#   s[4:5] src (syn: received rows)   s[6:7] dst (syn: syndrome rows)
+#   s8  src generation stride (u32)   s9  dst generation stride (u32)
+#   s10 src row stride                s11 dst row stride
+#   s12 L   s13 Lu = L/16   s14 total units G*Lu   s15 magic   s16 shift
+#   s17 n_items   s18 total waves in the grid
+#   s19 slot-map generation stride    s[20:21] slot map   s[22:23] zero row (syn)
+# SGPRs: s[24:25] valid B, s[26:27] valid A, s28 item, s29 wave in group,
+# s30 temp, s31 ABSENT constant, s[32:33] {src row stride, 0},
+# s[34:35] {dst row stride, 0}, s[36:37] mad carry sink, s[38:39] and
+# s[40:41] mask temps.
 KERNARG_BYTES = 80
-V_LANE, V_F, V_SRC, V_DST, V_G, V_U = 0, 1, 2, 4, 6, 7   # v2:3 src ptr, v4:5 dst ptr
-V_T = 8          # v8..v11 temps
-V_COMBO = 12     # 22 combo registers v12..v33
-V_ADDR = 34      # v34:35 gathered row address (syn)
-V_SLOT = 36      # slot temp (syn)
-V_RING = 40      # ring buffers v40.. (8 per buffer)
-SGPR_NEXT_FREE = 40
-S_TMP = 38
+V_LANE, V_F, V_GA, V_UA, V_GB, V_UB = 0, 1, 2, 3, 4, 5
+V_SRCA, V_SRCB, V_DSTA, V_DSTB = 6, 8, 10, 12   # 64-bit pointers (even-aligned)
+V_T = 14         # v14..v17 transpose temps
+V_COMBO = 18     # 22 combo registers v18..v39
+V_ZA, V_ZB, V_ADDR, V_SLOT = 40, 42, 44, 46      # syn only
+SGPR_NEXT_FREE = 42
+S_TMP, S_TMP2 = 38, 40
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
-S_MASK0 = 40
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
 
 
@@ -181,8 +183,9 @@ ABSENT = 0xFF    # slot-map value of a row that was not accepted
 class KernelSpec:
     k: int
     r: int
-    pd: int = 4
+    pd: int = 3
     mode: str = "enc"   # "enc": repairs of the Cauchy code; "syn": decode syndromes
+    xor3: bool = True   # acc ^= L ^ H as one v_bitop3_b32 (3-input XOR, full rate)
 
     @property
     def name(self) -> str:
@@ -194,16 +197,24 @@ class KernelSpec:
         return self.pd + 1
 
     @property
+    def ring0(self) -> int:
+        return 40 if self.mode == "enc" else 48
+
+    @property
     def acc0(self) -> int:
-        return V_RING + 8 * self.nbuf
+        return self.ring0 + 8 * self.nbuf
 
     @property
     def map_quads(self) -> int:
         return (self.k + self.r + 15) // 16 if self.mode == "syn" else 0
 
     @property
-    def map0(self) -> int:
+    def map_a(self) -> int:
         return self.acc0 + 8 * self.r
+
+    @property
+    def map_b(self) -> int:
+        return self.map_a + 4 * self.map_quads
 
     @property
     def map_stride(self) -> int:
@@ -212,12 +223,15 @@ class KernelSpec:
 
     @property
     def next_free_vgpr(self) -> int:
-        n = self.map0 + 4 * self.map_quads
-        return (n + 7) // 8 * 8
+        n = self.map_b + 4 * self.map_quads
+        n = (n + 7) // 8 * 8
+        if n > 256:
+            raise ValueError(f"{self.name}: {n} VGPRs > 256 (lower pd)")
+        return n
 
     @property
     def next_free_sgpr(self) -> int:
-        return SGPR_NEXT_FREE if self.mode == "enc" else S_MASK0 + 2 * self.nbuf
+        return SGPR_NEXT_FREE
 
 
 _TRANSPOSE = [(4, 0x0F0F0F0F, [(0, 4), (1, 5), (2, 6), (3, 7)]),
@@ -232,6 +246,8 @@ _COMBO_BUILD = {  # mask: (a, b) meaning combo = a ^ b, where a/b are masks
 
 
 def _transpose_ops(base: int) -> list[Op]:
+    """32 bytes in 8 dwords <-> 8 bit-planes (3 delta-swap stages; an
+    involution, so the same network maps planes back to bytes)."""
     ops = []
     for sh, mask, pairs in _TRANSPOSE:
         t = [V_T + q for q in range(4)]
@@ -279,7 +295,8 @@ def _combo_ops(lo: dict, hi: dict, needed_lo: set, needed_hi: set) -> list[Op]:
     return ops
 
 
-def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict, init: bool):
+def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict, init: bool,
+                 xor3: bool = False):
     """acc[b] (^)= M_c[b] * planes for one coefficient (rows_j = M_c rows)."""
     first_pass, second = [], []
     for b in range(8):
@@ -294,6 +311,8 @@ def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict,
                 first_pass.append(Op("v_mov", (a, hi[m_hi])))
             else:
                 first_pass.append(Op("v_movk", (a, 0)))
+        elif xor3 and m_lo and m_hi:
+            first_pass.append(Op("v_xor3", (a, a, lo[m_lo], hi[m_hi])))
         else:
             if m_lo:
                 first_pass.append(Op("v_xor", (a, a, lo[m_lo])))
@@ -302,7 +321,7 @@ def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict,
     ops.extend(first_pass + second)
 
 
-def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool):
+def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool, xor3: bool = False):
     """Transpose one source row (ring buffer at `base`) and accumulate it into
     all r repair accumulators with the Cauchy coefficients of column i."""
     ops.extend(_transpose_ops(base))
@@ -312,10 +331,10 @@ def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bo
     need_hi = {rb >> 4 for rr in rows for rb in rr} - {0}
     ops.extend(_combo_ops(lo, hi, need_lo, need_hi))
     for j in range(r):
-        _coeff_block(ops, rows[j], acc0 + 8 * j, lo, hi, init)
+        _coeff_block(ops, rows[j], acc0 + 8 * j, lo, hi, init, xor3)
 
 
-def _prologue(E):
+def _prologue(E, spec: KernelSpec):
     E(Op("s_load_args", ()))
     # wave id = workgroup * 4 + (tid >> 6); lane = tid & 63
     E(Op("v_lshr", (V_T, 6, V_LANE)))
@@ -325,41 +344,44 @@ def _prologue(E):
     E(Op("s_lshl", (30, 2, 2)))              # s30 = workgroup_id * 4   (s2 = workgroup id)
     E(Op("s_add", (28, 29, 30)))             # s28 = item = global wave id
     E(Op("s_waitcnt_lgkm", ()))
-    E(Op("s_mov", (32, 12)))
+    E(Op("s_mov", (32, 10)))
     E(Op("s_movk", (33, 0)))
-    E(Op("s_mov", (34, 13)))
+    E(Op("s_mov", (34, 11)))
     E(Op("s_movk", (35, 0)))
+    E(Op("s_movk", (S_ABSENT, ABSENT)))
     E(Op("label", (".Litem",)))
-    E(Op("s_cmp_ge_br", (28, 19, ".Lend")))
-    # f = item*64 + lane; valid = f < total
-    E(Op("v_lshl_add_s", (V_F, 28, 6, V_LANE)))
-    E(Op("v_cmp_gt_s", (26, 16, V_F)))
-    # g = mulhi(f, magic) >> shift ; u = f - g*U
-    E(Op("v_mul_hi_s", (V_G, V_F, 17)))
-    E(Op("v_lshr_s", (V_G, 18, V_G)))
-    E(Op("v_mul_lo_s", (V_U, V_G, 15)))
-    E(Op("v_sub", (V_U, V_F, V_U)))
-    # src = src + g*src_gen_stride + 32u ; dst likewise
-    # (VOP3 on gfx9 reads at most one SGPR: bases go through VGPRs)
-    E(Op("v_movs", (V_SRC, 4)))
-    E(Op("v_movs", (V_SRC + 1, 5)))
-    E(Op("v_mad64_s", (V_SRC, V_G, 8, V_SRC)))
-    E(Op("v_mad64_k", (V_SRC, V_U, 32, V_SRC)))
-    E(Op("v_movs", (V_DST, 6)))
-    E(Op("v_movs", (V_DST + 1, 7)))
-    E(Op("v_mad64_s", (V_DST, V_G, 10, V_DST)))
-    E(Op("v_mad64_k", (V_DST, V_U, 32, V_DST)))
-    # full chunk: 32u + 32 <= L
-    E(Op("v_lshl", (V_T, 5, V_U)))
-    E(Op("v_addk", (V_T, 32, V_T)))
-    E(Op("v_cmp_ge_s", (24, 14, V_T)))
+    E(Op("s_cmp_ge_br", (28, 17, ".Lend")))
+    # unit A = item*128 + lane, unit B = A + 64; valid = unit < total
+    for h, (gv, uv, sv, dv, vm) in enumerate(((V_GA, V_UA, V_SRCA, V_DSTA, 26),
+                                              (V_GB, V_UB, V_SRCB, V_DSTB, 24))):
+        if h == 0:
+            E(Op("v_lshl_add_s", (V_F, 28, 7, V_LANE)))
+        else:
+            E(Op("v_addk", (V_F, 64, V_F)))
+        E(Op("v_cmp_gt_s", (vm, 14, V_F)))
+        # g = mulhi(f, magic) >> shift ; u = f - g*Lu
+        E(Op("v_mul_hi_s", (gv, V_F, 15)))
+        E(Op("v_lshr_s", (gv, 16, gv)))
+        E(Op("v_mul_lo_s", (uv, gv, 13)))
+        E(Op("v_sub", (uv, V_F, uv)))
+        # src/dst + g * gen_stride + 16 u   (VOP3 reads at most one SGPR)
+        for ptr, base_s, gs_s in ((sv, 4, 8), (dv, 6, 9)):
+            E(Op("v_movs", (ptr, base_s)))
+            E(Op("v_movs", (ptr + 1, base_s + 1)))
+            E(Op("v_mad64_s", (ptr, gv, gs_s, ptr)))
+            E(Op("v_mad64_k", (ptr, uv, 16, ptr)))
+        if spec.mode == "syn":
+            z = V_ZA if h == 0 else V_ZB
+            E(Op("v_movs", (z, 22)))
+            E(Op("v_movs", (z + 1, 23)))
+            E(Op("v_mad64_k", (z, uv, 16, z)))
     E(Op("s_nop", (4,)))
-    E(Op("s_and64", (24, 24, 26)))
+    E(Op("label", (".Lbody",)))  # marks the end of the per-item setup (tools/bs_lab.py)
 
 
 def _epilogue_next_item(E):
     E(Op("s_nop", (4,)))  # store data/address VGPRs are rewritten by the next item
-    E(Op("s_add", (28, 28, 20)))
+    E(Op("s_add", (28, 28, 18)))
     E(Op("s_branch", (".Litem",)))
     E(Op("label", (".Lend",)))
     E(Op("s_endpgm", ()))
@@ -369,25 +391,33 @@ def generate(spec: KernelSpec) -> list[Op]:
     return _generate_enc(spec) if spec.mode == "enc" else _generate_syn(spec)
 
 
+def _store_pair(E, acc: int, ma: int, mb: int):
+    E(Op("s_exec", (ma,)))
+    E(Op("store16", (V_DSTA, acc, 0)))
+    E(Op("s_exec", (mb,)))
+    E(Op("store16", (V_DSTB, acc + 4, 0)))
+    E(Op("s_exec", (None,)))
+    E(Op("v_add64_s", (V_DSTA, V_DSTA, 34)))
+    E(Op("v_add64_s", (V_DSTB, V_DSTB, 34)))
+
+
 def _generate_enc(spec: KernelSpec) -> list[Op]:
     k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
     C = cauchy(k, r)
-    acc0 = spec.acc0
+    acc0, ring0 = spec.acc0, spec.ring0
     ops: list[Op] = []
     E = ops.append
-    _prologue(E)
-    # zero the ring (second halves of half chunks are never loaded)
-    for q in range(8 * nbuf):
-        E(Op("v_movk", (V_RING + q, 0)))
+    _prologue(E, spec)
 
     def load_row(row: int):
-        b = V_RING + 8 * (row % nbuf)
+        b = ring0 + 8 * (row % nbuf)
         E(Op("s_exec", (26,)))
-        E(Op("load16", (b, V_SRC, 0)))
+        E(Op("load16", (b, V_SRCA, 0)))
         E(Op("s_exec", (24,)))
-        E(Op("load16", (b + 4, V_SRC, 16)))
+        E(Op("load16", (b + 4, V_SRCB, 0)))
         E(Op("s_exec", (None,)))
-        E(Op("v_add64_s", (V_SRC, V_SRC, 32)))
+        E(Op("v_add64_s", (V_SRCA, V_SRCA, 32)))
+        E(Op("v_add64_s", (V_SRCB, V_SRCB, 32)))
 
     for row in range(min(pd, k)):
         load_row(row)
@@ -396,75 +426,67 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
             load_row(i + pd)
         after = min(pd, k - 1 - i)
         E(Op("s_waitcnt_vm", (2 * after,)))
-        _source_row(ops, C, i, r, V_RING + 8 * (i % nbuf), acc0, init=(i == 0))
-    # planes -> bytes, store 32 bytes per lane per repair
+        _source_row(ops, C, i, r, ring0 + 8 * (i % nbuf), acc0, init=(i == 0), xor3=spec.xor3)
+    # planes -> bytes, store 2 x 16 bytes per lane per repair
     for j in range(r):
         ops.extend(_transpose_ops(acc0 + 8 * j))
     E(Op("s_nop", (4,)))
     for j in range(r):
-        base = acc0 + 8 * j
-        E(Op("s_exec", (26,)))
-        E(Op("store16", (V_DST, base, 0)))
-        E(Op("s_exec", (24,)))
-        E(Op("store16", (V_DST, base + 4, 16)))
-        E(Op("s_exec", (None,)))
-        E(Op("v_add64_s", (V_DST, V_DST, 34)))
+        _store_pair(E, acc0 + 8 * j, 26, 24)
     _epilogue_next_item(E)
     return ops
 
 
 def _generate_syn(spec: KernelSpec) -> list[Op]:
     """Decode stage A: syndromes s_j = p_j ^ sum_{i present} C[j][i] x_i of
-    every accepted repair j, for the generation of each lane.
+    every accepted repair j, for the generation of each half-lane.
 
     The slot map (per generation: k source slots then r repair slots, one
     byte each, ABSENT if the row was not accepted) says where each row sits
     among the received rows.  Rows stream through the ring in the order
-    repairs 0..r-1, sources 0..k-1; a lane whose generation lacks a row loads
-    slot 0 instead (always readable) and is switched off by EXEC while that
-    row is accumulated.  Syndromes are stored only for accepted repairs."""
+    repairs 0..r-1 (which initialise the accumulators), sources 0..k-1; a
+    half whose generation lacks a row reads the zero row instead.
+    Syndromes are stored only for accepted repairs."""
     k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
     C = cauchy(k, r)
-    acc0, map0 = spec.acc0, spec.map0
+    acc0, ring0 = spec.acc0, spec.ring0
+    maps = (spec.map_a, spec.map_b)
     seq = [("rep", j) for j in range(r)] + [("src", i) for i in range(k)]
     ops: list[Op] = []
     E = ops.append
-    _prologue(E)
-    E(Op("s_movk", (S_ABSENT, ABSENT)))
-    # slot map of the lane's generation: v[map0 ...] <- map + g * map_stride
-    E(Op("v_movs", (V_ADDR, 22)))
-    E(Op("v_movs", (V_ADDR + 1, 23)))
-    E(Op("v_mad64_s", (V_ADDR, V_G, 21, V_ADDR)))
-    E(Op("s_exec", (26,)))
-    for q in range(spec.map_quads):
-        E(Op("load16", (map0 + 4 * q, V_ADDR, 16 * q)))
-    E(Op("s_exec", (None,)))
-    for q in range(8 * r):
-        E(Op("v_movk", (acc0 + q, 0)))
+    _prologue(E, spec)
+    # slot maps of both halves' generations
+    for h, (gv, vm) in enumerate(((V_GA, 26), (V_GB, 24))):
+        E(Op("v_movs", (V_ADDR, 20)))
+        E(Op("v_movs", (V_ADDR + 1, 21)))
+        E(Op("v_mad64_s", (V_ADDR, gv, 19, V_ADDR)))
+        E(Op("s_exec", (vm,)))
+        for q in range(spec.map_quads):
+            E(Op("load16", (maps[h] + 4 * q, V_ADDR, 16 * q)))
+        E(Op("s_exec", (None,)))
     E(Op("s_waitcnt_vm", (0,)))
 
     def map_byte(entry) -> int:
         kind, idx = entry
         return idx if kind == "src" else k + idx
 
-    def slot_mask(entry, sm: int):
-        """v_slot <- slot (0 when absent), s[sm] <- valid & present."""
-        pos = map_byte(entry)
-        E(Op("s_exec", (26,)))
-        E(Op("v_bfe", (V_SLOT, map0 + pos // 4, 8 * (pos % 4), 8)))
+    def present(pos: int, h: int, sm: int):
+        """v_slot <- slot byte of half h, s[sm] <- slot != ABSENT."""
+        E(Op("v_bfe", (V_SLOT, maps[h] + pos // 4, 8 * (pos % 4), 8)))
         E(Op("v_cmp_ne_s", (sm, S_ABSENT, V_SLOT)))
         E(Op("s_nop", (4,)))
-        E(Op("v_cndmask_0", (V_SLOT, V_SLOT, sm)))
 
     def load_row(n: int):
-        b = V_RING + 8 * (n % nbuf)
-        sm = S_MASK0 + 2 * (n % nbuf)
-        slot_mask(seq[n], sm)
-        E(Op("v_mad64_s", (V_ADDR, V_SLOT, 12, V_SRC)))
-        E(Op("load16", (b, V_ADDR, 0)))
-        E(Op("s_exec", (24,)))
-        E(Op("load16", (b + 4, V_ADDR, 16)))
-        E(Op("s_exec", (None,)))
+        b = ring0 + 8 * (n % nbuf)
+        pos = map_byte(seq[n])
+        for h, (base, z, vm) in enumerate(((V_SRCA, V_ZA, 26), (V_SRCB, V_ZB, 24))):
+            present(pos, h, S_TMP)
+            E(Op("v_mad64_s", (V_ADDR, V_SLOT, 10, base)))
+            E(Op("v_cndmask", (V_ADDR, z, V_ADDR, S_TMP)))
+            E(Op("v_cndmask", (V_ADDR + 1, z + 1, V_ADDR + 1, S_TMP)))
+            E(Op("s_exec", (vm,)))
+            E(Op("load16", (b + 4 * h, V_ADDR, 0)))
+            E(Op("s_exec", (None,)))
 
     n_seq = len(seq)
     for n in range(min(pd, n_seq)):
@@ -474,29 +496,22 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
             load_row(n + pd)
         after = min(pd, n_seq - 1 - n)
         E(Op("s_waitcnt_vm", (2 * after,)))
-        base = V_RING + 8 * (n % nbuf)
-        E(Op("s_exec", (S_MASK0 + 2 * (n % nbuf),)))
+        base = ring0 + 8 * (n % nbuf)
         if kind == "rep":
             ops.extend(_transpose_ops(base))
             for b in range(8):
-                a = acc0 + 8 * idx + b
-                E(Op("v_xor", (a, a, base + b)))
+                E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
         else:
-            _source_row(ops, C, idx, r, base, acc0, init=False)
-        E(Op("s_exec", (None,)))
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3)
     for j in range(r):
         ops.extend(_transpose_ops(acc0 + 8 * j))
     E(Op("s_nop", (4,)))
     for j in range(r):
-        base = acc0 + 8 * j
-        slot_mask(("rep", j), S_TMP)
-        E(Op("s_exec", (S_TMP,)))
-        E(Op("store16", (V_DST, base, 0)))
-        E(Op("s_and64", (S_TMP, S_TMP, 24)))
-        E(Op("s_exec", (S_TMP,)))
-        E(Op("store16", (V_DST, base + 4, 16)))
-        E(Op("s_exec", (None,)))
-        E(Op("v_add64_s", (V_DST, V_DST, 34)))
+        present(k + j, 0, S_TMP)
+        E(Op("s_and64", (S_TMP, S_TMP, 26)))
+        present(k + j, 1, S_TMP2)
+        E(Op("s_and64", (S_TMP2, S_TMP2, 24)))
+        _store_pair(E, acc0 + 8 * j, S_TMP, S_TMP2)
     _epilogue_next_item(E)
     return ops
 
@@ -595,24 +610,29 @@ def magic_for(U: int) -> tuple[int, int]:
     return magic, s - 1
 
 
+def launch_geometry(L: int, G: int) -> tuple[int, int, int]:
+    """(Lu, total units, items) of a batch: 16-byte units, 128 per item."""
+    if L % 16 or L < 32:
+        raise ValueError("bit-sliced kernels need L % 16 == 0 and L >= 32")
+    Lu = L // 16
+    total = G * Lu
+    if total >= 1 << 31:
+        raise ValueError("too many units for one launch")
+    return Lu, total, (total + 127) // 128
+
+
 def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
-             total_waves: int) -> bytes:
-    U = (L + 31) // 32
-    total = G * U
-    magic, shift = magic_for(U)
-    n_items = (total + 63) // 64
-    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, 0, dgs, 0, srs, drs, L, U, total,
-             magic, shift, n_items, total_waves, 0, 0, 0]
+             total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0) -> bytes:
+    """80-byte kernarg block (layout above).  Syndrome mode: src = received
+    rows, dst = syndrome rows, plus slot map and zero row."""
+    Lu, total, n_items = launch_geometry(L, G)
+    magic, shift = magic_for(Lu)
+    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, L, Lu, total,
+             magic, shift, n_items, total_waves, map_stride, smap & MASK32, smap >> 32,
+             zero & MASK32, zero >> 32]
+    for w in words:
+        assert 0 <= w < 1 << 32, words
     return np.array(words, dtype=np.uint32).tobytes()
-
-
-def kernargs_syn(rows: int, syn: int, rgs: int, sgs: int, rs: int, srs: int, L: int, G: int,
-                 total_waves: int, smap: int, map_stride: int) -> bytes:
-    """Syndrome kernel: encode layout plus s21 = slot-map generation stride,
-    s[22:23] = slot map."""
-    w = np.frombuffer(kernargs(rows, syn, rgs, sgs, rs, srs, L, G, total_waves), np.uint32).copy()
-    w[17], w[18], w[19] = map_stride, smap & MASK32, smap >> 32
-    return w.tobytes()
 
 
 def cauchy_inverse(k: int, J: list[int], E: list[int]) -> list[list[int]]:
@@ -733,6 +753,8 @@ class Emulator:
                 wv(a[0], rv(a[1]) ^ rv(a[2]))
             elif n == "v_mov":
                 wv(a[0], rv(a[1]))
+            elif n == "v_xor3":
+                wv(a[0], rv(a[1]) ^ rv(a[2]) ^ rv(a[3]))
             elif n == "v_movk":
                 wv(a[0], np.full(64, a[1], np.uint64))
             elif n == "v_andk":
@@ -773,8 +795,8 @@ class Emulator:
                 wv(a[0], (rv(a[1]) >> np.uint64(a[2])) & np.uint64((1 << a[3]) - 1))
             elif n == "v_cmp_ne_s":
                 set_smask(a[0], (rv(a[2]) != np.uint64(s[a[1]])) & exec_)
-            elif n == "v_cndmask_0":
-                wv(a[0], np.where(smask(a[2]), rv(a[1]), np.uint64(0)))
+            elif n == "v_cndmask":
+                wv(a[0], np.where(smask(a[3]), rv(a[2]), rv(a[1])))
             elif n == "load16":
                 d, ar, off = a
                 addr = rv64(ar)

@@ -28,7 +28,7 @@ SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip", "qf_bs.hip"]
 # (k, r) Cauchy configurations that get a bit-sliced assembly kernel
 # (bs_codegen.py); every other shape runs the general v_perm kernel.
 BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1)]
-BS_PD = 4
+BS_PD = 3
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
 
 
@@ -90,28 +90,34 @@ def _check_no_scratch(remarks: str) -> dict[str, dict[str, int]]:
     return usage
 
 
+def assemble(name: str, asm_text: str, out_dir: Path) -> Path:
+    """gfx950 assembly text -> code object (.hsaco) via clang + ld.lld."""
+    clang = _clangxx().replace("clang++", "clang")
+    lld = str(Path(clang).parent / "ld.lld")
+    asm = out_dir / f"{name}.s"
+    asm.write_text(asm_text)
+    obj = asm.with_suffix(".o")
+    hsaco = asm.with_suffix(".hsaco")
+    res = subprocess.run([clang, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", f"-mcpu={ARCH}",
+                          "-c", str(asm), "-o", str(obj)], capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"assembling {asm.name} failed:\n{res.stderr[-3000:]}")
+    res = subprocess.run([lld, "-shared", str(obj), "-o", str(hsaco)], capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"linking {asm.name} failed:\n{res.stderr[-3000:]}")
+    return hsaco
+
+
 def _bs_kernels(build_dir: Path) -> Path:
     """Generate + assemble the bit-sliced kernels; emit a C include that
     embeds the code objects."""
     from . import bs_codegen as bs
 
-    clang = _clangxx().replace("clang++", "clang")
-    lld = str(Path(clang).parent / "ld.lld")
     entries, blobs = [], []
     specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn") for (k, r) in BS_CONFIGS]
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
-        asm = build_dir / f"{spec.name}.s"
-        asm.write_text(bs.emit_asm(spec, bs.generate(spec)))
-        obj = asm.with_suffix(".o")
-        hsaco = asm.with_suffix(".hsaco")
-        res = subprocess.run([clang, "-x", "assembler", "-target", "amdgcn-amd-amdhsa", f"-mcpu={ARCH}",
-                              "-c", str(asm), "-o", str(obj)], capture_output=True, text=True)
-        if res.returncode != 0:
-            raise RuntimeError(f"assembling {asm.name} failed:\n{res.stderr[-3000:]}")
-        res = subprocess.run([lld, "-shared", str(obj), "-o", str(hsaco)], capture_output=True, text=True)
-        if res.returncode != 0:
-            raise RuntimeError(f"linking {asm.name} failed:\n{res.stderr[-3000:]}")
+        hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
         data = hsaco.read_bytes()
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")

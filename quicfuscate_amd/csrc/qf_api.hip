@@ -61,6 +61,9 @@ struct qf_ctx {
     // decode workspace
     uint8_t* d_work = nullptr;
     size_t work_bytes = 0;
+    // zero row read by the syndrome kernel for rows a generation lacks
+    uint8_t* d_zero = nullptr;
+    size_t zero_bytes = 0;
     // host-memory pipeline
     static const int kPipe = 3;
     hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
@@ -234,10 +237,10 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     // Fast path: bit-sliced kernel specialised to the reference's Cauchy
     // matrix of (k, r) (bs_codegen.py), for whole 16-byte rows.
     const char* nobs = getenv("QF_DISABLE_BS");
-    if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && L % 16 == 0 && L >= 64 &&
+    if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && L % 16 == 0 && L >= 32 &&
         sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
         sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
-        (uint64_t)G * ((L + 31) / 32) < (1ull << 31)) {
+        (uint64_t)G * (L / 16) < (1ull << 31)) {
         hipEvent_t ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
                                    sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G));
@@ -331,6 +334,18 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     if (s) return s;
     uint8_t* w = ctx->d_work;
     uint32_t* d_bound = reinterpret_cast<uint32_t*>(w + off_bound);
+    if (ctx->zero_bytes < L) {
+        if (ctx->d_zero) {
+            QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+            hipFree(ctx->d_zero);
+            ctx->d_zero = nullptr;
+            ctx->zero_bytes = 0;
+        }
+        const size_t zb = round_up(L, 4096);
+        if (hipMalloc(&ctx->d_zero, zb) != hipSuccess) return QF_ENOMEM;
+        QF_CHECK_HIP(hipMemset(ctx->d_zero, 0, zb));
+        ctx->zero_bytes = zb;
+    }
     qf::PrepareCauchyArgs pa{};
     pa.row_index = row_index;
     pa.n_rows = n_rows;
@@ -353,7 +368,7 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
     ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows, w + off_syn, sh->rows_gen_stride,
-                                (uint64_t)r * L, sh->row_stride, L, L, G, w + off_map, ms));
+                                (uint64_t)r * L, sh->row_stride, L, L, G, w + off_map, ms, ctx->d_zero));
     prof_end(ctx, st, ev, qf::syn_name(k, r));
     qf::CombineSlotsArgs a{};
     a.rows = w + off_syn;
@@ -471,6 +486,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->d_custom) hipFree(c->d_custom);
     if (c->custom_done) hipEventDestroy(c->custom_done);
     if (c->d_work) hipFree(c->d_work);
+    if (c->d_zero) hipFree(c->d_zero);
     qf::bs_unload(c->bs);
     for (auto& p : c->prof_pending) {
         hipEventDestroy(p.a);
@@ -639,8 +655,9 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     if (s) return s;
     const char* nobs = getenv("QF_DISABLE_BS");
     if (!row_coeffs && !(nobs && atoi(nobs)) && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
-        max_rows <= 255 && L % 16 == 0 && L >= 64 && sh->rows_gen_stride < (1ull << 32) &&
-        sh->row_stride < (1ull << 32) && (uint64_t)G * ((L + 31) / 32) < (1ull << 31))
+        max_rows <= 255 && L % 16 == 0 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
+        sh->row_stride < (1ull << 32) && (uint64_t)G * (L / 16) < (1ull << 31) &&
+        (uint64_t)r * L < (1ull << 32))
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
     const uint32_t passes = (e_max + 15) / 16;
     const uint64_t coef_gen_stride = ((uint64_t)max_rows + 1) * 16;

@@ -15,18 +15,20 @@ struct BsCache {
 bool bs_available(uint32_t k, uint32_t r);
 // Kernel symbol of that configuration (nullptr if none).
 const char* bs_name(uint32_t k, uint32_t r);
-// Encode G generations (rows of L bytes, L % 16 == 0, L >= 64; strides and
-// generation strides < 2^32, 16-byte aligned).
+// Encode G generations (rows of L bytes, L % 16 == 0, L >= 32; strides and
+// generation strides < 2^32, 16-byte aligned; G * L / 16 < 2^31).
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                      uint64_t drs, uint32_t L, uint32_t G);
 // Decode stage A: syndromes of the accepted repairs (bs_codegen.py "syn").
+// zero: >= L zero bytes (read in place of rows a generation does not have).
 bool syn_available(uint32_t k, uint32_t r);
 const char* syn_name(uint32_t k, uint32_t r);
 uint32_t syn_map_stride(uint32_t k, uint32_t r);
 hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
-                      uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride);
+                      uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
+                      const uint8_t* zero);
 void bs_unload(BsCache& cache);
 
 }  // namespace qf

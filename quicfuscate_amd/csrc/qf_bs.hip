@@ -56,52 +56,55 @@ static void magic_for(uint32_t U, uint32_t* magic, uint32_t* shift) {
     *shift = s - 1;
 }
 
-// Shared launch: kernarg words 0..16 as bs_codegen.kernargs, 17..19 extra.
+// Shared launch: kernarg words as bs_codegen.kernargs (80 bytes).  Items of
+// 128 16-byte units, one wave per item (non-persistent grid: staggered wave
+// start-up overlaps one wave's loads with another's XOR work).
 static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStream_t st,
                          const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
-                         uint64_t drs, uint32_t L, uint32_t G, const uint32_t extra[3]) {
+                         uint64_t drs, uint32_t L, uint32_t G, const uint8_t* smap,
+                         uint32_t map_stride, const uint8_t* zero) {
+    (void)num_cus;
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return hipErrorInvalidValue;
+    if (L % 16 || L < 32 || sgs >= (1ull << 32) || dgs >= (1ull << 32) || srs >= (1ull << 32) ||
+        drs >= (1ull << 32))
+        return hipErrorInvalidValue;
     if (!cache.fn[idx]) {
         hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
         if (err != hipSuccess) return err;
         err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
         if (err != hipSuccess) return err;
     }
-    const uint32_t U = (L + 31) / 32;
-    const uint64_t total = (uint64_t)G * U;
-    if (total >= (1ull << 31) || U < 2) return hipErrorInvalidValue;
+    const uint32_t Lu = L / 16;
+    const uint64_t total = (uint64_t)G * Lu;
+    if (total >= (1ull << 31)) return hipErrorInvalidValue;
     uint32_t magic, shift;
-    magic_for(U, &magic, &shift);
-    const uint32_t n_items = (uint32_t)((total + 63) / 64);
-    // > 128 VGPRs -> 2 waves per SIMD -> two 256-thread blocks per CU
-    uint32_t blocks = (n_items + 3) / 4;
-    const uint32_t cap = (uint32_t)num_cus * 2;
-    if (blocks > cap) blocks = cap;
+    magic_for(Lu, &magic, &shift);
+    const uint32_t n_items = (uint32_t)((total + 127) / 128);
+    const uint32_t blocks = (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     uint32_t a[20];
-    memset(a, 0, sizeof(a));
     a[0] = (uint32_t)(uintptr_t)src;
     a[1] = (uint32_t)((uintptr_t)src >> 32);
     a[2] = (uint32_t)(uintptr_t)dst;
     a[3] = (uint32_t)((uintptr_t)dst >> 32);
     a[4] = (uint32_t)sgs;
-    a[6] = (uint32_t)dgs;
-    a[8] = (uint32_t)srs;
-    a[9] = (uint32_t)drs;
-    a[10] = L;
-    a[11] = U;
-    a[12] = (uint32_t)total;
-    a[13] = magic;
-    a[14] = shift;
-    a[15] = n_items;
-    a[16] = blocks * 4;
-    if (extra) {
-        a[17] = extra[0];
-        a[18] = extra[1];
-        a[19] = extra[2];
-    }
+    a[5] = (uint32_t)dgs;
+    a[6] = (uint32_t)srs;
+    a[7] = (uint32_t)drs;
+    a[8] = L;
+    a[9] = Lu;
+    a[10] = (uint32_t)total;
+    a[11] = magic;
+    a[12] = shift;
+    a[13] = n_items;
+    a[14] = blocks * 4;
+    a[15] = map_stride;
+    a[16] = (uint32_t)(uintptr_t)smap;
+    a[17] = (uint32_t)((uintptr_t)smap >> 32);
+    a[18] = (uint32_t)(uintptr_t)zero;
+    a[19] = (uint32_t)((uintptr_t)zero >> 32);
     size_t sz = sizeof(a);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
@@ -111,16 +114,17 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                      uint64_t drs, uint32_t L, uint32_t G) {
-    return launch(cache, find('e', k, r), num_cus, st, src, dst, sgs, dgs, srs, drs, L, G, nullptr);
+    return launch(cache, find('e', k, r), num_cus, st, src, dst, sgs, dgs, srs, drs, L, G, nullptr, 0,
+                  nullptr);
 }
 
 hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
-                      uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride) {
+                      uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
+                      const uint8_t* zero) {
     const QfBsEntry* e = find('s', k, r);
-    if (!e || map_stride != e->map_stride) return hipErrorInvalidValue;
-    const uint32_t extra[3] = {map_stride, (uint32_t)(uintptr_t)smap, (uint32_t)((uintptr_t)smap >> 32)};
-    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, extra);
+    if (!e || map_stride != e->map_stride || !zero) return hipErrorInvalidValue;
+    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, smap, map_stride, zero);
 }
 
 void bs_unload(BsCache& cache) {

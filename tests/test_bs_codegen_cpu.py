@@ -14,6 +14,7 @@ from quicfuscate_amd import bs_codegen as bs
     (5, 3, 3, 64, 4, 1),     # odd k, prefetch deeper than k
     (1, 1, 1, 64, 3, 1),
     (16, 16, 4, 1200, 3, 2), # a full-width accumulator set
+    (64, 16, 3, 1200, 2, 1), # the benchmark kernel (units of two generations per lane)
 ])
 def test_emulated_kernel_matches_oracle(oracle, k, r, pd, L, G, waves):
     spec = bs.KernelSpec(k, r, pd)
@@ -119,11 +120,12 @@ def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves):
             smap[g * mstride + (idx if kind == "s" else k + idx)] = sl
         plans.append((src, rep, E, J))
     emu = bs.Emulator(ops)
-    ROWS, SYN, MAP = 0x10000000, 0x40000000, 0x70000000
+    ROWS, SYN, MAP, ZERO = 0x10000000, 0x40000000, 0x70000000, 0x78000000
     emu.add_buffer(ROWS, rows)
     emu.add_buffer(SYN, syn)
     emu.add_buffer(MAP, smap)
-    ka = bs.kernargs_syn(ROWS, SYN, rgs, sgs, rs, srs, L, G, waves * 4, MAP, mstride)
+    emu.add_buffer(ZERO, np.zeros(L, np.uint8))
+    ka = bs.kernargs(ROWS, SYN, rgs, sgs, rs, srs, L, G, waves * 4, smap=MAP, map_stride=mstride, zero=ZERO)
     for wg in range(waves):
         for w in range(4):
             emu.run_wave(ka, wg, w)
@@ -184,3 +186,36 @@ def test_declared_register_budget_covers_code(k, r, mode):
         smax = max(smax, int(m.group(2) or m.group(3)))
     assert vmax < nv, (vmax, nv)
     assert smax < ns, (smax, ns)
+
+
+@pytest.mark.parametrize("mode", ["enc", "syn"])
+def test_xor3_variant_matches_plain(oracle, mode):
+    """The v_bitop3 accumulate variant computes the same repairs/syndromes."""
+    k, r, L, G = 8, 4, 80, 5
+    rng = np.random.default_rng(17)
+    outs = []
+    for x3 in (False, True):
+        spec = bs.KernelSpec(k, r, 2, mode, xor3=x3)
+        emu = bs.Emulator(bs.generate(spec))
+        src = rng.integers(0, 256, G * k * L, dtype=np.uint8) if not outs else outs[0][0]
+        dst = np.zeros(G * r * L, np.uint8)
+        emu.add_buffer(0x1000000, src)
+        emu.add_buffer(0x9000000, dst)
+        if mode == "enc":
+            ka = bs.kernargs(0x1000000, 0x9000000, k * L, r * L, L, L, L, G, 4)
+        else:
+            smap = np.full(G * spec.map_stride, 0xFF, np.uint8)
+            for g in range(G):
+                smap[g * spec.map_stride: g * spec.map_stride + k] = np.arange(k)
+                smap[g * spec.map_stride + k: g * spec.map_stride + k + 2] = [0, 1]  # repairs 0,1 at slots 0,1
+            emu.add_buffer(0x5000000, smap)
+            emu.add_buffer(0x6000000, np.zeros(L, np.uint8))
+            ka = bs.kernargs(0x1000000, 0x9000000, k * L, r * L, L, L, L, G, 4, smap=0x5000000,
+                             map_stride=spec.map_stride, zero=0x6000000)
+        emu.run_wave(ka, 0, 0)
+        emu.run_wave(ka, 0, 1)
+        emu.run_wave(ka, 0, 2)
+        emu.run_wave(ka, 0, 3)
+        outs.append((src, dst.copy()))
+    assert (outs[0][1] == outs[1][1]).all()
+    assert outs[0][1].any()

@@ -1,0 +1,161 @@
+#!/usr/bin/env python3
+"""Bit-sliced kernel lab: variants of the generated kernels, timed on the GPU.
+
+    python tools/bs_lab.py build            # here: generate + assemble -> tools/lab_build/
+    python tools/bs_lab.py run [--G 65536]  # GPU box: load each code object, time it
+
+Variants strip parts of the body (loads, stores, coefficient XORs, all
+compute) or change prefetch depth / grid size, to separate the memory and
+VALU costs of the real kernel.  Diagnostic only; the library embeds the
+unmodified kernels.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+OUT = REPO / "tools" / "lab_build"
+
+VALU = {"v_xor", "v_andk", "v_lshl", "v_lshr", "v_mov", "v_movk"}
+
+
+def variant_ops(bs, spec, flags):
+    ops = bs.generate(spec)
+    body = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Lbody")
+    acc_lo, acc_hi = spec.acc0, spec.acc0 + 8 * spec.r
+    out = []
+    for n, op in enumerate(ops):
+        if n > body:
+            if "noload" in flags and op.name in ("load16", "s_waitcnt_vm"):
+                continue
+            if "nostore" in flags and op.name == "store16":
+                continue
+            if "nocoeff" in flags and op.name in ("v_xor", "v_mov", "v_movk") and acc_lo <= op.args[0] < acc_hi:
+                continue
+            if "nocompute" in flags and op.name in VALU:
+                continue
+        out.append(op)
+    return out
+
+
+ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
+VARIANTS = [
+    # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3;
+    # "ld:<bits>" / "st:<bits>" append cache-policy bits to loads / stores)
+    ("base", 64, 16, 3, (), ALL),
+    ("ld_nt", 64, 16, 3, ("ld:nt",), ALL),
+    ("st_nt", 64, 16, 3, ("st:nt",), ALL),
+    ("ldst_nt", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("st_sc1", 64, 16, 3, ("st:sc1",), ALL),
+    ("st_sc0sc1", 64, 16, 3, ("st:sc0 sc1",), ALL),
+    ("ldnt_stsc1", 64, 16, 3, ("ld:nt", "st:sc1"), ALL),
+    ("nocompute", 64, 16, 3, ("nocompute",), ALL),
+    ("nocompute_ldst_nt", 64, 16, 3, ("nocompute", "ld:nt", "st:nt"), ALL),
+    ("nocompute_stsc1", 64, 16, 3, ("nocompute", "st:sc1"), ALL),
+    ("readonly", 64, 16, 3, ("nocompute", "nostore"), ALL),
+    ("readonly_nt", 64, 16, 3, ("nocompute", "nostore", "ld:nt"), ALL),
+    ("writeonly", 64, 16, 3, ("nocompute", "noload"), ALL),
+]
+
+
+def policy(text: str, flags) -> str:
+    ld = next((f[3:] for f in flags if f.startswith("ld:")), None)
+    st = next((f[3:] for f in flags if f.startswith("st:")), None)
+    out = []
+    for line in text.split("\n"):
+        t = line.strip()
+        if ld and t.startswith("global_load_dwordx4"):
+            line = line + " " + ld
+        if st and t.startswith("global_store_dwordx4"):
+            line = line + " " + st
+        out.append(line)
+    return "\n".join(out)
+
+
+def build():
+    from quicfuscate_amd import bs_codegen as bs
+    from quicfuscate_amd.build_lib import assemble
+
+    OUT.mkdir(parents=True, exist_ok=True)
+    manifest = []
+    for name, k, r, pd, flags, bpc in VARIANTS:
+        spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags)
+        text = policy(bs.emit_asm(spec, variant_ops(bs, spec, set(flags))), flags)
+        h = assemble(f"lab_{name}", text.replace(spec.name, f"lab_{name}"), OUT)
+        manifest.append({"name": name, "k": k, "r": r, "pd": pd, "flags": list(flags), "blocks_per_cu": bpc,
+                         "hsaco": h.name, "symbol": f"lab_{name}", "vgprs": spec.next_free_vgpr})
+        print(name, h.stat().st_size)
+    (OUT / "manifest.json").write_text(json.dumps(manifest, indent=1))
+
+
+def run(G: int, reps: int):
+    import torch
+
+    from quicfuscate_amd import bs_codegen as bs
+
+    hip = ctypes.CDLL(str(Path(torch.__file__).parent / "lib" / "libamdhip64.so"))
+    dev = torch.device("cuda")
+    manifest = json.loads((OUT / "manifest.json").read_text())
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    L = 1200
+    kmax, rmax = 64, 16
+    src = torch.randint(0, 256, (G * kmax * L,), dtype=torch.uint8, device=dev)
+    dst = torch.empty(G * rmax * L, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    res = {}
+    for m in manifest:
+        k, r = m["k"], m["r"]
+        mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        data = (OUT / m["hsaco"]).read_bytes()
+        buf = ctypes.create_string_buffer(data, len(data))
+        assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
+        _, _, n_items = bs.launch_geometry(L, G)
+        blocks = min((n_items + 3) // 4, ncu * m["blocks_per_cu"])
+        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * L, r * L, L, L, L, G, blocks * 4)
+        kbuf = ctypes.create_string_buffer(ka, len(ka))
+        size = ctypes.c_size_t(len(ka))
+        extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
+                                     ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+
+        def launch():
+            e = hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(stream.cuda_stream),
+                                          None, extra)
+            assert e == 0, e
+
+        launch()
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record(stream)
+        for _ in range(reps):
+            launch()
+        t1.record(stream)
+        torch.cuda.synchronize()
+        ms = t0.elapsed_time(t1) / reps
+        gb = G * (k + r) * L / (ms / 1e3) / 1e9
+        res[m["name"]] = {"ms": round(ms, 4), "GBps_alg": round(gb, 1), "pd": m["pd"], "flags": m["flags"],
+                          "blocks_per_cu": m["blocks_per_cu"], "vgprs": m["vgprs"]}
+        print(m["name"], res[m["name"]], flush=True)
+        hip.hipModuleUnload(mod)
+    return res
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--G", type=int, default=65536)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default="gpurun_out/bs_lab.json")
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build()
+    else:
+        r = run(a.G, a.reps)
+        Path(a.out).parent.mkdir(exist_ok=True)
+        Path(a.out).write_text(json.dumps(r, indent=1))
