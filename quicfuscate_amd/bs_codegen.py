@@ -128,8 +128,10 @@ _ASM = {
     "v_bfe": lambda d, a, off, w: f"v_bfe_u32 {V(d)}, {V(a)}, {off}, {w}",
     "v_cmp_ne_s": lambda sd, s, a: f"v_cmp_ne_u32_e64 {SP(sd)}, s{s}, {V(a)}",
     "v_cndmask": lambda d, a, b, sm: f"v_cndmask_b32_e64 {V(d)}, {V(a)}, {V(b)}, {SP(sm)}",
-    "load16": lambda d, a, off: f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
-    "store16": lambda a, d, off: f"global_store_dwordx4 {VP(a)}, {VQ(d)}, off" + (f" offset:{off}" if off else ""),
+    "load16": lambda d, a, off, pol="": f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off"
+              + (f" offset:{off}" if off else "") + (f" {pol}" if pol else ""),
+    "store16": lambda a, d, off, pol="": f"global_store_dwordx4 {VP(a)}, {VQ(d)}, off"
+               + (f" offset:{off}" if off else "") + (f" {pol}" if pol else ""),
     "s_exec": lambda s: "s_mov_b64 exec, -1" if s is None else f"s_mov_b64 exec, {SP(s)}",
     "s_and64": lambda d, a, b: f"s_and_b64 {SP(d)}, {SP(a)}, {SP(b)}",
     "s_mov": lambda d, a: f"s_mov_b32 s{d}, s{a}",
@@ -186,6 +188,10 @@ class KernelSpec:
     pd: int = 3
     mode: str = "enc"   # "enc": repairs of the Cauchy code; "syn": decode syndromes
     xor3: bool = True   # acc ^= L ^ H as one v_bitop3_b32 (3-input XOR, full rate)
+    # cache policy of the streamed rows: read once / written once, so
+    # non-temporal (tools/bs_lab.py: -9 % at C2 vs the default policy)
+    ld_policy: str = "nt"
+    st_policy: str = "nt"
 
     @property
     def name(self) -> str:
@@ -391,11 +397,11 @@ def generate(spec: KernelSpec) -> list[Op]:
     return _generate_enc(spec) if spec.mode == "enc" else _generate_syn(spec)
 
 
-def _store_pair(E, acc: int, ma: int, mb: int):
+def _store_pair(E, acc: int, ma: int, mb: int, pol: str = ""):
     E(Op("s_exec", (ma,)))
-    E(Op("store16", (V_DSTA, acc, 0)))
+    E(Op("store16", (V_DSTA, acc, 0, pol)))
     E(Op("s_exec", (mb,)))
-    E(Op("store16", (V_DSTB, acc + 4, 0)))
+    E(Op("store16", (V_DSTB, acc + 4, 0, pol)))
     E(Op("s_exec", (None,)))
     E(Op("v_add64_s", (V_DSTA, V_DSTA, 34)))
     E(Op("v_add64_s", (V_DSTB, V_DSTB, 34)))
@@ -412,9 +418,9 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     def load_row(row: int):
         b = ring0 + 8 * (row % nbuf)
         E(Op("s_exec", (26,)))
-        E(Op("load16", (b, V_SRCA, 0)))
+        E(Op("load16", (b, V_SRCA, 0, spec.ld_policy)))
         E(Op("s_exec", (24,)))
-        E(Op("load16", (b + 4, V_SRCB, 0)))
+        E(Op("load16", (b + 4, V_SRCB, 0, spec.ld_policy)))
         E(Op("s_exec", (None,)))
         E(Op("v_add64_s", (V_SRCA, V_SRCA, 32)))
         E(Op("v_add64_s", (V_SRCB, V_SRCB, 32)))
@@ -432,7 +438,7 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         ops.extend(_transpose_ops(acc0 + 8 * j))
     E(Op("s_nop", (4,)))
     for j in range(r):
-        _store_pair(E, acc0 + 8 * j, 26, 24)
+        _store_pair(E, acc0 + 8 * j, 26, 24, spec.st_policy)
     _epilogue_next_item(E)
     return ops
 
@@ -485,7 +491,7 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
             E(Op("v_cndmask", (V_ADDR, z, V_ADDR, S_TMP)))
             E(Op("v_cndmask", (V_ADDR + 1, z + 1, V_ADDR + 1, S_TMP)))
             E(Op("s_exec", (vm,)))
-            E(Op("load16", (b + 4 * h, V_ADDR, 0)))
+            E(Op("load16", (b + 4 * h, V_ADDR, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
     n_seq = len(seq)
@@ -511,7 +517,7 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         E(Op("s_and64", (S_TMP, S_TMP, 26)))
         present(k + j, 1, S_TMP2)
         E(Op("s_and64", (S_TMP2, S_TMP2, 24)))
-        _store_pair(E, acc0 + 8 * j, S_TMP, S_TMP2)
+        _store_pair(E, acc0 + 8 * j, S_TMP, S_TMP2, spec.st_policy)
     _epilogue_next_item(E)
     return ops
 
@@ -798,7 +804,7 @@ class Emulator:
             elif n == "v_cndmask":
                 wv(a[0], np.where(smask(a[3]), rv(a[2]), rv(a[1])))
             elif n == "load16":
-                d, ar, off = a
+                d, ar, off = a[:3]
                 addr = rv64(ar)
                 vals = np.zeros((4, 64), np.uint64)
                 lanes = np.nonzero(exec_)[0]
@@ -812,7 +818,7 @@ class Emulator:
                     busy.add(rg)
                 pending.append((regs, vals, exec_.copy()))
             elif n == "store16":
-                ar, d, off = a
+                ar, d, off = a[:3]
                 addr = rv64(ar)
                 vals = np.stack([rv(d + q) for q in range(4)]).astype(np.uint32)
                 for l in np.nonzero(exec_)[0]:

@@ -47,35 +47,19 @@ def variant_ops(bs, spec, flags):
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
     # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3;
-    # "ld:<bits>" / "st:<bits>" append cache-policy bits to loads / stores)
-    ("base", 64, 16, 3, (), ALL),
-    ("ld_nt", 64, 16, 3, ("ld:nt",), ALL),
-    ("st_nt", 64, 16, 3, ("st:nt",), ALL),
+    # "ld:<bits>" / "st:<bits>" append cache-policy bits to loads / stores;
+    # "L:<n>" payload bytes, default 1200)
     ("ldst_nt", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("st_sc1", 64, 16, 3, ("st:sc1",), ALL),
-    ("st_sc0sc1", 64, 16, 3, ("st:sc0 sc1",), ALL),
-    ("ldnt_stsc1", 64, 16, 3, ("ld:nt", "st:sc1"), ALL),
-    ("nocompute", 64, 16, 3, ("nocompute",), ALL),
-    ("nocompute_ldst_nt", 64, 16, 3, ("nocompute", "ld:nt", "st:nt"), ALL),
-    ("nocompute_stsc1", 64, 16, 3, ("nocompute", "st:sc1"), ALL),
-    ("readonly", 64, 16, 3, ("nocompute", "nostore"), ALL),
-    ("readonly_nt", 64, 16, 3, ("nocompute", "nostore", "ld:nt"), ALL),
+    ("ldst_nt_L1280", 64, 16, 3, ("ld:nt", "st:nt", "L:1280"), ALL),
+    ("ldst_nt_L1024", 64, 16, 3, ("ld:nt", "st:nt", "L:1024"), ALL),
     ("writeonly", 64, 16, 3, ("nocompute", "noload"), ALL),
+    ("writeonly_nt", 64, 16, 3, ("nocompute", "noload", "st:nt"), ALL),
+    ("writeonly_L1280", 64, 16, 3, ("nocompute", "noload", "L:1280"), ALL),
+    ("writeonly_L1024", 64, 16, 3, ("nocompute", "noload", "L:1024"), ALL),
+    ("writeonly_nt_L1024", 64, 16, 3, ("nocompute", "noload", "st:nt", "L:1024"), ALL),
+    ("readonly_nt", 64, 16, 3, ("nocompute", "nostore", "ld:nt"), ALL),
+    ("readonly_nt_L1024", 64, 16, 3, ("nocompute", "nostore", "ld:nt", "L:1024"), ALL),
 ]
-
-
-def policy(text: str, flags) -> str:
-    ld = next((f[3:] for f in flags if f.startswith("ld:")), None)
-    st = next((f[3:] for f in flags if f.startswith("st:")), None)
-    out = []
-    for line in text.split("\n"):
-        t = line.strip()
-        if ld and t.startswith("global_load_dwordx4"):
-            line = line + " " + ld
-        if st and t.startswith("global_store_dwordx4"):
-            line = line + " " + st
-        out.append(line)
-    return "\n".join(out)
 
 
 def build():
@@ -83,12 +67,17 @@ def build():
     from quicfuscate_amd.build_lib import assemble
 
     OUT.mkdir(parents=True, exist_ok=True)
+    for old in OUT.glob("lab_*"):
+        old.unlink()
     manifest = []
     for name, k, r, pd, flags, bpc in VARIANTS:
-        spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags)
-        text = policy(bs.emit_asm(spec, variant_ops(bs, spec, set(flags))), flags)
+        ld = next((f[3:] for f in flags if f.startswith("ld:")), "")
+        st = next((f[3:] for f in flags if f.startswith("st:")), "")
+        spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st)
+        text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"lab_{name}", text.replace(spec.name, f"lab_{name}"), OUT)
-        manifest.append({"name": name, "k": k, "r": r, "pd": pd, "flags": list(flags), "blocks_per_cu": bpc,
+        Lv = next((int(f[2:]) for f in flags if f.startswith("L:")), 1200)
+        manifest.append({"name": name, "k": k, "r": r, "pd": pd, "flags": list(flags), "blocks_per_cu": bpc, "L": Lv,
                          "hsaco": h.name, "symbol": f"lab_{name}", "vgprs": spec.next_free_vgpr})
         print(name, h.stat().st_size)
     (OUT / "manifest.json").write_text(json.dumps(manifest, indent=1))
@@ -103,14 +92,13 @@ def run(G: int, reps: int):
     dev = torch.device("cuda")
     manifest = json.loads((OUT / "manifest.json").read_text())
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    L = 1200
-    kmax, rmax = 64, 16
-    src = torch.randint(0, 256, (G * kmax * L,), dtype=torch.uint8, device=dev)
-    dst = torch.empty(G * rmax * L, dtype=torch.uint8, device=dev)
+    kmax, rmax, Lmax = 64, 16, 1280
+    src = torch.randint(0, 256, (G * kmax * Lmax,), dtype=torch.uint8, device=dev)
+    dst = torch.empty(G * rmax * Lmax, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     res = {}
     for m in manifest:
-        k, r = m["k"], m["r"]
+        k, r, L = m["k"], m["r"], m["L"]
         mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
         data = (OUT / m["hsaco"]).read_bytes()
         buf = ctypes.create_string_buffer(data, len(data))
