@@ -387,7 +387,7 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     a.Lu = (L + 15) / 16;
     a.zero_slot = r;
     a.total_units = (uint64_t)G * a.Lu;
-    const int PD = pick_PD("QF_DECODE_PD", 1, 2);
+    const int PD = pick_PD("QF_DECODE_PD", 1, 1);
     ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
     prof_end(ctx, st, ev, "k_combine_slots<" + std::to_string(PD) + ">");
@@ -709,7 +709,7 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
         a.Lu = Lu;
         a.zero_slot = max_rows;
         a.total_units = (uint64_t)G * Lu;
-        const int PD = pick_PD("QF_DECODE_PD", 1, 2);
+        const int PD = pick_PD("QF_DECODE_PD", 1, 1);
         hipEvent_t ev2 = prof_begin(ctx, ctx->stream);
         QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, ctx->stream));
         prof_end(ctx, ctx->stream, ev2, "k_combine_slots<" + std::to_string(PD) + ">");

@@ -450,6 +450,7 @@ __global__ void __launch_bounds__(256, (PD == 1 ? 3 : 2)) k_combine_slots(Combin
         if (jmax <= 4) combine_slots_dispatch<4, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
         else if (jmax <= 8) combine_slots_dispatch<8, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
         else if (jmax <= 12) combine_slots_dispatch<12, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+        else if (jmax <= 13) combine_slots_dispatch<13, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
         else if (jmax <= 14) combine_slots_dispatch<14, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
         else combine_slots_dispatch<16, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
     }
