@@ -211,6 +211,98 @@ int qf_decoder_get_decoded_packets(qf_decoder *dec, uint8_t *out_data, uint32_t 
                                    uint32_t *out_len, uint64_t *out_ids, uint32_t *count);
 
 /* ---------------------------------------------------------------------------
+ * Adaptive FEC driver (adaptive.rs:44-631, mod.rs:56-79): loss estimator
+ * (EMA + burst window + optional Kalman filter), PID-driven mode manager with
+ * dwell time, hysteresis, emergency override and dynamic window, and the
+ * per-connection sliding-window codec with a 32-packet cross-fade between
+ * configurations.  The arithmetic is f32 exactly as the reference (no FP
+ * contraction).  Time is in seconds on a monotonic clock; the *_at variants
+ * take it explicitly (deterministic tests), the others read CLOCK_MONOTONIC.
+ *
+ * Codec: GF(2^8) encoder/decoder objects above.  A configuration the GF(2^8)
+ * Cauchy code cannot realise (k + r > 256, where the reference panics in
+ * gf_inv(0); or Extreme mode, which the reference runs in GF(2^16)) has no
+ * codec: on_send still emits the systematic packet and returns QF_ERANGE.
+ * ------------------------------------------------------------------------- */
+#define QF_MODE_ZERO 0
+#define QF_MODE_LIGHT 1
+#define QF_MODE_NORMAL 2
+#define QF_MODE_MEDIUM 3
+#define QF_MODE_STRONG 4
+#define QF_MODE_EXTREME 5
+#define QF_CROSS_FADE_LEN 32   /* ModeManager::CROSS_FADE_LEN (adaptive.rs:114) */
+
+typedef struct qf_fec_config {   /* FecConfig (adaptive.rs:338-349) */
+    float lambda;                /* EMA smoothing factor */
+    uint32_t burst_window;       /* burst-detection window (packets) */
+    float hysteresis;
+    float kp, ki, kd;            /* PidConfig */
+    int32_t initial_mode;
+    int32_t kalman_enabled;
+    float kalman_q, kalman_r;
+    uint32_t window_sizes[6];    /* initial window W0 per mode */
+    uint32_t max_len;            /* payload capacity of the codec objects (bytes) */
+} qf_fec_config;
+
+/* FecConfig::default (adaptive.rs:435-452) + default_windows (352-362);
+ * max_len = 1500. */
+void qf_fec_config_default(qf_fec_config *cfg);
+/* FecConfig::validate (adaptive.rs:455-471): QF_EINVAL on a bad field. */
+int qf_fec_config_validate(const qf_fec_config *cfg);
+/* ModeManager::params_for (adaptive.rs:149-153): k = window,
+ * n = ceil(window * overhead_ratio(mode)) in f32. */
+int qf_mode_params_for(int32_t mode, uint32_t window, uint32_t *k, uint32_t *n);
+/* ModeManager::window_range (adaptive.rs:124-133). */
+int qf_mode_window_range(int32_t mode, uint32_t *lo, uint32_t *hi);
+/* ModeManager::overhead_ratio (adaptive.rs:135-147). */
+float qf_mode_overhead_ratio(int32_t mode);
+
+typedef struct qf_packet_desc {
+    uint64_t id;
+    uint32_t len;            /* payload bytes */
+    uint32_t coeff_len;      /* coefficient bytes of a repair packet, else 0 */
+    int32_t is_systematic;
+    uint32_t reserved;
+} qf_packet_desc;
+
+typedef struct qf_adaptive qf_adaptive;
+/* AdaptiveFec::new (adaptive.rs:473-508).  ctx may be NULL: controller only
+ * (no codec objects; on_send emits the systematic packet, on_receive
+ * recovers nothing) -- the mode logic then runs without a GPU. */
+int qf_adaptive_new(qf_ctx *ctx, const qf_fec_config *cfg, qf_adaptive **out);
+int qf_adaptive_new_at(qf_ctx *ctx, const qf_fec_config *cfg, double now_s, qf_adaptive **out);
+int qf_adaptive_free(qf_adaptive *a);
+/* current_mode / is_transitioning (adaptive.rs:510-517) and the rest of the
+ * controller state (any pointer may be NULL). */
+int qf_adaptive_state(const qf_adaptive *a, int32_t *mode, uint32_t *window, uint32_t *k,
+                      uint32_t *n, int32_t *transitioning, uint32_t *transition_left,
+                      float *estimated_loss);
+/* Largest number of packets one on_send can emit (1 + repairs of the
+ * current and the cross-fade configuration). */
+uint32_t qf_adaptive_max_send_packets(const qf_adaptive *a);
+/* AdaptiveFec::on_send (adaptive.rs:519-544) + emit_repairs (546-562): the
+ * systematic packet, then the cross-fade configuration's repairs (while more
+ * than CROSS_FADE_LEN/2 packets of the fade remain), then the current
+ * configuration's repairs.  Packet i goes to out_data + i*out_stride (and
+ * its coefficients to out_coeffs + i*coeff_stride); *n_out packets.
+ * QF_ETOOSMALL if out_cap is too small (nothing is consumed then). */
+int qf_adaptive_on_send(qf_adaptive *a, uint64_t id, const uint8_t *data, uint32_t len,
+                        uint8_t *out_data, uint32_t out_stride, uint8_t *out_coeffs,
+                        uint32_t coeff_stride, qf_packet_desc *out_desc, uint32_t out_cap,
+                        uint32_t *n_out);
+/* AdaptiveFec::on_receive (adaptive.rs:566-599): recovered packets (the
+ * whole generation, ids 0..k-1, when a decoder completes).  QF_EINVAL for
+ * a repair packet without coefficients. */
+int qf_adaptive_on_receive(qf_adaptive *a, uint64_t id, int is_systematic, const uint8_t *data,
+                           uint32_t len, const uint8_t *coeffs, uint32_t coeff_len,
+                           uint8_t *out_data, uint32_t out_stride, qf_packet_desc *out_desc,
+                           uint32_t out_cap, uint32_t *n_out);
+/* AdaptiveFec::report_loss (adaptive.rs:602-630).  QF_EINVAL if lost > total
+ * (the reference underflows). */
+int qf_adaptive_report_loss(qf_adaptive *a, uint32_t lost, uint32_t total);
+int qf_adaptive_report_loss_at(qf_adaptive *a, uint32_t lost, uint32_t total, double now_s);
+
+/* ---------------------------------------------------------------------------
  * Wire framing, byte-compatible with encoder.rs:124-152 (to_raw) and
  * encoder.rs:18-68 (from_raw): [u8 sys(1/0)] [u16 BE coeff_len][coeffs] payload
  * (the coefficient header is present only when coeffs != NULL).

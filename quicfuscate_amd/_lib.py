@@ -57,6 +57,24 @@ class DecodeShape(ctypes.Structure):
     ]
 
 
+class FecConfig(ctypes.Structure):
+    _fields_ = [
+        ("lambda_", ctypes.c_float), ("burst_window", _U32), ("hysteresis", ctypes.c_float),
+        ("kp", ctypes.c_float), ("ki", ctypes.c_float), ("kd", ctypes.c_float),
+        ("initial_mode", ctypes.c_int32), ("kalman_enabled", ctypes.c_int32),
+        ("kalman_q", ctypes.c_float), ("kalman_r", ctypes.c_float),
+        ("window_sizes", _U32 * 6), ("max_len", _U32),
+    ]
+
+
+class PacketDesc(ctypes.Structure):
+    _fields_ = [("id", _U64), ("len", _U32), ("coeff_len", _U32), ("is_systematic", ctypes.c_int32),
+                ("reserved", _U32)]
+
+
+_F = ctypes.c_float
+_D = ctypes.c_double
+
 _SIGS = {
     "qf_abi_version": (_I, []),
     "qf_strerror": (ctypes.c_char_p, [_I]),
@@ -92,6 +110,20 @@ _SIGS = {
     "qf_packet_from_raw": (_I, [_P, _U32, _P, _P, _P, _P, _P]),
     "qf_fill_splitmix_dev": (_I, [_P, _P, _SZ, _U64, _U64]),
     "qf_selftest_split_tables": (_I, []),
+    "qf_fec_config_default": (None, [ctypes.POINTER(FecConfig)]),
+    "qf_fec_config_validate": (_I, [ctypes.POINTER(FecConfig)]),
+    "qf_mode_params_for": (_I, [ctypes.c_int32, _U32, _P, _P]),
+    "qf_mode_window_range": (_I, [ctypes.c_int32, _P, _P]),
+    "qf_mode_overhead_ratio": (_F, [ctypes.c_int32]),
+    "qf_adaptive_new": (_I, [_P, ctypes.POINTER(FecConfig), ctypes.POINTER(_P)]),
+    "qf_adaptive_new_at": (_I, [_P, ctypes.POINTER(FecConfig), _D, ctypes.POINTER(_P)]),
+    "qf_adaptive_free": (_I, [_P]),
+    "qf_adaptive_state": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "qf_adaptive_max_send_packets": (_U32, [_P]),
+    "qf_adaptive_on_send": (_I, [_P, _U64, _P, _U32, _P, _U32, _P, _U32, _P, _U32, _P]),
+    "qf_adaptive_on_receive": (_I, [_P, _U64, _I, _P, _U32, _P, _U32, _P, _U32, _P, _U32, _P]),
+    "qf_adaptive_report_loss": (_I, [_P, _U32, _U32]),
+    "qf_adaptive_report_loss_at": (_I, [_P, _U32, _U32, _D]),
 }
 
 _LIB: ctypes.CDLL | None = None

@@ -365,3 +365,197 @@ class Decoder:
             L._lib().qf_decoder_free(self.handle)
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------------------
+# Adaptive FEC driver (adaptive.rs:11-631) over qf_adaptive_*
+# ---------------------------------------------------------------------------
+import enum
+from collections import deque as _deque
+from dataclasses import dataclass as _dataclass, field as _field
+
+
+class FecMode(enum.IntEnum):
+    """adaptive.rs:13-21 (with FromStr aliases, 23-37)."""
+    Zero = 0
+    Light = 1
+    Normal = 2
+    Medium = 3
+    Strong = 4
+    Extreme = 5
+
+    @classmethod
+    def parse(cls, s: str) -> "FecMode":
+        names = {"0": 0, "zero": 0, "1": 1, "light": 1, "leicht": 1, "2": 2, "normal": 2,
+                 "3": 3, "medium": 3, "mittel": 3, "4": 4, "strong": 4, "stark": 4, "5": 5, "extreme": 5}
+        try:
+            return cls(names[s.lower()])
+        except KeyError:
+            raise ValueError(f"unknown FEC mode {s!r}") from None
+
+
+def default_windows() -> dict:
+    """FecConfig::default_windows (adaptive.rs:352-362)."""
+    return {FecMode.Zero: 0, FecMode.Light: 16, FecMode.Normal: 64, FecMode.Medium: 128,
+            FecMode.Strong: 512, FecMode.Extreme: 1024}
+
+
+@_dataclass
+class PidConfig:
+    kp: float = 1.2
+    ki: float = 0.5
+    kd: float = 0.1
+
+
+@_dataclass
+class FecConfig:
+    """adaptive.rs:338-349, defaults 435-452."""
+    lambda_: float = 0.1
+    burst_window: int = 20
+    hysteresis: float = 0.02
+    pid: PidConfig = _field(default_factory=PidConfig)
+    initial_mode: FecMode = FecMode.Zero
+    kalman_enabled: bool = False
+    kalman_q: float = 0.001
+    kalman_r: float = 0.01
+    window_sizes: dict = _field(default_factory=default_windows)
+    max_len: int = 1500
+
+    def to_c(self) -> "L.FecConfig":
+        c = L.FecConfig()
+        c.lambda_, c.burst_window, c.hysteresis = self.lambda_, self.burst_window, self.hysteresis
+        c.kp, c.ki, c.kd = self.pid.kp, self.pid.ki, self.pid.kd
+        c.initial_mode = int(self.initial_mode)
+        c.kalman_enabled = 1 if self.kalman_enabled else 0
+        c.kalman_q, c.kalman_r = self.kalman_q, self.kalman_r
+        for m in FecMode:
+            c.window_sizes[int(m)] = int(self.window_sizes.get(m, default_windows()[m]))
+        c.max_len = self.max_len
+        return c
+
+    def validate(self) -> None:
+        """FecConfig::validate (adaptive.rs:455-471)."""
+        c = self.to_c()
+        check(L._lib().qf_fec_config_validate(ctypes.byref(c)), "FecConfig.validate")
+
+
+class ModeManager:
+    """The static parts of adaptive.rs:102-153."""
+    CROSS_FADE_LEN = 32
+    ALPHA_K = 0.5
+
+    @staticmethod
+    def params_for(mode: FecMode, window: int) -> tuple[int, int]:
+        k, n = ctypes.c_uint32(), ctypes.c_uint32()
+        check(L._lib().qf_mode_params_for(int(mode), window, ctypes.byref(k), ctypes.byref(n)))
+        return k.value, n.value
+
+    @staticmethod
+    def window_range(mode: FecMode) -> tuple[int, int]:
+        lo, hi = ctypes.c_uint32(), ctypes.c_uint32()
+        check(L._lib().qf_mode_window_range(int(mode), ctypes.byref(lo), ctypes.byref(hi)))
+        return lo.value, hi.value
+
+    @staticmethod
+    def overhead_ratio(mode: FecMode) -> float:
+        return L._lib().qf_mode_overhead_ratio(int(mode))
+
+
+class AdaptiveFec:
+    """adaptive.rs:326-631.  `ctx=None` with `codec=False` runs the controller
+    alone (no GPU); `now` arguments inject the monotonic clock in seconds."""
+
+    def __init__(self, config: FecConfig, pool: Optional[MemoryPool] = None, *, ctx: Optional[Context] = None,
+                 codec: bool = True, now: Optional[float] = None):
+        self._lib = L._lib()
+        self.config = config
+        self.pool = pool
+        self.ctx = (ctx or default_context()) if codec else None
+        h = ctypes.c_void_p()
+        c = config.to_c()
+        cptr = self.ctx.handle if self.ctx is not None else None
+        if now is None:
+            check(self._lib.qf_adaptive_new(cptr, ctypes.byref(c), ctypes.byref(h)), "AdaptiveFec.new")
+        else:
+            check(self._lib.qf_adaptive_new_at(cptr, ctypes.byref(c), float(now), ctypes.byref(h)),
+                  "AdaptiveFec.new")
+        self.handle = h
+
+    def state(self) -> dict:
+        mode, window, k, n = ctypes.c_int32(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        tr, left, est = ctypes.c_int32(), ctypes.c_uint32(), ctypes.c_float()
+        check(self._lib.qf_adaptive_state(self.handle, ctypes.byref(mode), ctypes.byref(window), ctypes.byref(k),
+                                          ctypes.byref(n), ctypes.byref(tr), ctypes.byref(left), ctypes.byref(est)))
+        return {"mode": FecMode(mode.value), "window": window.value, "k": k.value, "n": n.value,
+                "transitioning": bool(tr.value), "transition_left": left.value, "estimated_loss": est.value}
+
+    def current_mode(self) -> FecMode:
+        return self.state()["mode"]
+
+    def is_transitioning(self) -> bool:
+        return self.state()["transitioning"]
+
+    def report_loss(self, lost: int, total: int, now: Optional[float] = None) -> None:
+        if now is None:
+            check(self._lib.qf_adaptive_report_loss(self.handle, lost, total), "report_loss")
+        else:
+            check(self._lib.qf_adaptive_report_loss_at(self.handle, lost, total, float(now)), "report_loss")
+
+    def on_send(self, pkt: Packet, outgoing_queue) -> int:
+        """Pushes the systematic packet and its repairs onto outgoing_queue.
+        Returns the status (QF_ERANGE when the configuration has no GF(2^8)
+        code -- the reference panics or switches to GF(2^16) there)."""
+        cap = self._lib.qf_adaptive_max_send_packets(self.handle)
+        stride = max(self.config.max_len, 1)
+        kmax = 256
+        data = (ctypes.c_uint8 * (cap * stride))()
+        co = (ctypes.c_uint8 * (cap * kmax))()
+        desc = (L.PacketDesc * cap)()
+        n = ctypes.c_uint32()
+        pay = pkt.payload()
+        buf = (ctypes.c_uint8 * max(1, len(pay))).from_buffer_copy(pay.ljust(max(1, len(pay)), b"\0"))
+        s = self._lib.qf_adaptive_on_send(self.handle, pkt.id, buf, len(pay), data, stride, co, kmax, desc, cap,
+                                          ctypes.byref(n))
+        if s not in (L.QF_OK, L.QF_ERANGE):
+            check(s, "on_send")
+        raw, cr = bytes(data), bytes(co)
+        for i in range(n.value):
+            d = desc[i]
+            payload = bytearray(raw[i * stride: i * stride + d.len])
+            coeffs = cr[i * kmax: i * kmax + d.coeff_len] if not d.is_systematic else None
+            outgoing_queue.append(Packet(d.id, payload, d.len, bool(d.is_systematic), coeffs, d.coeff_len))
+        return s
+
+    def on_receive(self, pkt: Packet) -> list:
+        st = self.state()
+        cap = max(1, st["k"] + 1024)
+        stride = max(self.config.max_len, 1)
+        data = (ctypes.c_uint8 * (cap * stride))()
+        desc = (L.PacketDesc * cap)()
+        n = ctypes.c_uint32()
+        pay = pkt.payload()
+        buf = (ctypes.c_uint8 * max(1, len(pay))).from_buffer_copy(pay.ljust(max(1, len(pay)), b"\0"))
+        co = None
+        if pkt.coefficients is not None:
+            co = (ctypes.c_uint8 * max(1, pkt.coeff_len)).from_buffer_copy(
+                bytes(pkt.coefficients[: pkt.coeff_len]).ljust(max(1, pkt.coeff_len), b"\0"))
+        s = self._lib.qf_adaptive_on_receive(self.handle, pkt.id, 1 if pkt.is_systematic else 0, buf, len(pay),
+                                             ctypes.cast(co, ctypes.c_void_p) if co is not None else None,
+                                             pkt.coeff_len, data, stride, desc, cap, ctypes.byref(n))
+        if s == L.QF_EINVAL and not pkt.is_systematic and pkt.coefficients is None:
+            raise QfError(s, "Repair packet missing coefficients.")
+        check(s, "on_receive")
+        raw = bytes(data)
+        return [Packet(desc[i].id, bytearray(raw[i * stride: i * stride + desc[i].len]), desc[i].len, True)
+                for i in range(n.value)]
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.qf_adaptive_free(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
