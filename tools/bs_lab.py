@@ -47,18 +47,18 @@ def variant_ops(bs, spec, flags):
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
     # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3;
-    # "ld:<bits>" / "st:<bits>" append cache-policy bits to loads / stores;
-    # "L:<n>" payload bytes, default 1200)
-    ("ldst_nt", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("ldst_nt_L1280", 64, 16, 3, ("ld:nt", "st:nt", "L:1280"), ALL),
-    ("ldst_nt_L1024", 64, 16, 3, ("ld:nt", "st:nt", "L:1024"), ALL),
-    ("writeonly", 64, 16, 3, ("nocompute", "noload"), ALL),
-    ("writeonly_nt", 64, 16, 3, ("nocompute", "noload", "st:nt"), ALL),
-    ("writeonly_L1280", 64, 16, 3, ("nocompute", "noload", "L:1280"), ALL),
-    ("writeonly_L1024", 64, 16, 3, ("nocompute", "noload", "L:1024"), ALL),
-    ("writeonly_nt_L1024", 64, 16, 3, ("nocompute", "noload", "st:nt", "L:1024"), ALL),
-    ("readonly_nt", 64, 16, 3, ("nocompute", "nostore", "ld:nt"), ALL),
-    ("readonly_nt_L1024", 64, 16, 3, ("nocompute", "nostore", "ld:nt", "L:1024"), ALL),
+    # "ld:<bits>" / "st:<bits>" cache-policy bits; "L:<n>" payload bytes;
+    # "dst:wide" destination rows 2 KiB apart, generations 32 KiB apart, so a
+    # wave's stores cover ~32 KiB contiguously (timing only, not the layout
+    # of the real output))
+    ("base", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("dstwide", 64, 16, 3, ("ld:nt", "st:nt", "dst:wide"), ALL),
+    ("writeonly", 64, 16, 3, ("nocompute", "noload", "st:nt"), ALL),
+    ("writeonly_dstwide", 64, 16, 3, ("nocompute", "noload", "st:nt", "dst:wide"), ALL),
+    ("writeonly_persist2", 64, 16, 3, ("nocompute", "noload", "st:nt"), 2),
+    ("writeonly_persist8", 64, 16, 3, ("nocompute", "noload", "st:nt"), 8),
+    ("nocompute", 64, 16, 3, ("nocompute", "ld:nt", "st:nt"), ALL),
+    ("nocompute_dstwide", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "dst:wide"), ALL),
 ]
 
 
@@ -94,7 +94,7 @@ def run(G: int, reps: int):
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     kmax, rmax, Lmax = 64, 16, 1280
     src = torch.randint(0, 256, (G * kmax * Lmax,), dtype=torch.uint8, device=dev)
-    dst = torch.empty(G * rmax * Lmax, dtype=torch.uint8, device=dev)
+    dst = torch.empty(G * 32768, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     res = {}
     for m in manifest:
@@ -106,7 +106,9 @@ def run(G: int, reps: int):
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
         _, _, n_items = bs.launch_geometry(L, G)
         blocks = min((n_items + 3) // 4, ncu * m["blocks_per_cu"])
-        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * L, r * L, L, L, L, G, blocks * 4)
+        wide = "dst:wide" in m["flags"]
+        drs, dgs = (2048, 32768) if wide else (L, r * L)
+        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * L, dgs, L, drs, L, G, blocks * 4)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
