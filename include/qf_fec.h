@@ -317,6 +317,37 @@ int qf_packet_from_raw(const uint8_t *raw, uint32_t raw_len, int *is_systematic,
                        const uint8_t **payload, uint32_t *len);
 
 /* ---------------------------------------------------------------------------
+ * Wire framing on the device (encoder.rs:18-152): the
+ * step between UDP datagrams and the batch codec.
+ * ------------------------------------------------------------------------- */
+/* Frames of an encode batch, as Packet::to_raw writes them (encoder.rs:124-152):
+ * generation g's k sources then its r repairs, frame f = g*(k+r) + i at
+ * frames_dev + f*frame_stride:
+ *   source i  0x01 | payload (L bytes)                                1 + L bytes
+ *   repair j  0x00 | k as BE u16 | C[j][0..k) | payload (L bytes)     3 + k + L bytes
+ * with C the reference's Cauchy rows (decoder.rs:280-298).  frame_len_dev
+ * (may be NULL) receives each frame's length.  frame_stride % 16 == 0,
+ * >= 3 + k + L; bytes of a frame past its length are not written. */
+int qf_frame_batch_dev(qf_ctx *ctx, const qf_encode_shape *shape, uint32_t G, const uint8_t *src_dev,
+                       const uint8_t *rep_dev, uint8_t *frames_dev, uint64_t frame_stride,
+                       uint32_t *frame_len_dev);
+/* Received frames -> qf_decode_batch input (Packet::from_raw, encoder.rs:18-68,
+ * then Decoder::add_packet's column rule, decoder.rs:684).  Frame s of
+ * generation g: frames_dev + (g*max_rows + s)*frame_stride, frame_len_dev[g*max_rows+s]
+ * bytes, transport id ids_dev[g*max_rows+s]; n_frames_dev[g] frames (NULL: max_rows).
+ * Valid frames are compacted in arrival order into rows_dev (payload zero
+ * padded to L) with row_index_dev = id % k for a systematic frame, k + j for a
+ * repair whose coefficient vector is Cauchy row j < r; n_rows_dev[g] = their
+ * count.  frame_status_dev: QF_OK, QF_EINVAL (empty, payload > L),
+ * QF_ETOOSMALL (coefficient length or coefficients truncated), QF_ERANGE
+ * (coefficients are not a Cauchy row of this (k, r)).  max_rows <= 1024. */
+int qf_parse_frames_dev(qf_ctx *ctx, uint32_t k, uint32_t r, uint32_t L, uint32_t G, uint32_t max_rows,
+                        const uint8_t *frames_dev, uint64_t frame_stride, const uint32_t *frame_len_dev,
+                        const uint64_t *ids_dev, const uint32_t *n_frames_dev, uint8_t *rows_dev,
+                        uint64_t row_stride, uint64_t rows_gen_stride, uint16_t *row_index_dev,
+                        uint32_t *n_rows_dev, int32_t *frame_status_dev);
+
+/* ---------------------------------------------------------------------------
  * Synthetic payload (bench / tests): byte t of the region is byte (t & 7) of
  * splitmix64(seed + word_offset + t/8), little endian.  Device kernel.
  * ------------------------------------------------------------------------- */

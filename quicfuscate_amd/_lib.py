@@ -110,6 +110,9 @@ _SIGS = {
     "qf_packet_from_raw": (_I, [_P, _U32, _P, _P, _P, _P, _P]),
     "qf_fill_splitmix_dev": (_I, [_P, _P, _SZ, _U64, _U64]),
     "qf_selftest_split_tables": (_I, []),
+    "qf_frame_batch_dev": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P, _U64, _P]),
+    "qf_parse_frames_dev": (_I, [_P, _U32, _U32, _U32, _U32, _U32, _P, _U64, _P, _P, _P, _P, _U64, _U64, _P,
+                                 _P, _P]),
     "qf_fec_config_default": (None, [ctypes.POINTER(FecConfig)]),
     "qf_fec_config_validate": (_I, [ctypes.POINTER(FecConfig)]),
     "qf_mode_params_for": (_I, [ctypes.c_int32, _U32, _P, _P]),

@@ -396,6 +396,17 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
 
 }  // namespace
 
+namespace qf {
+hipError_t launch_frame_batch(const uint8_t* src, const uint8_t* rep, const qf_encode_shape& sh, uint32_t G,
+                              uint8_t* frames, uint64_t frame_stride, uint32_t* frame_len,
+                              const uint8_t* explog, int num_cus, hipStream_t st);
+hipError_t launch_parse_frames(const uint8_t* frames, uint64_t frame_stride, const uint32_t* frame_len,
+                               const uint64_t* ids, const uint32_t* n_frames, uint32_t k, uint32_t r, uint32_t L,
+                               uint32_t G, uint32_t max_rows, uint8_t* rows, uint64_t row_stride,
+                               uint64_t rows_gen_stride, uint16_t* row_index, uint32_t* n_rows,
+                               int32_t* frame_status, const uint8_t* explog, hipStream_t st);
+}  // namespace qf
+
 extern "C" {
 
 int qf_abi_version(void) { return QF_ABI_VERSION; }
@@ -714,6 +725,49 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
         QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, ctx->stream));
         prof_end(ctx, ctx->stream, ev2, "k_combine_slots<" + std::to_string(PD) + ">");
     }
+    return QF_OK;
+}
+
+int qf_frame_batch_dev(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
+                       const uint8_t* rep, uint8_t* frames, uint64_t frame_stride, uint32_t* frame_len) {
+    if (!ctx || !sh) return QF_EINVAL;
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    if (k == 0 || k + r > 256) return k == 0 ? QF_EINVAL : QF_ERANGE;
+    if (G == 0 || L == 0) return QF_OK;
+    if (!src || !frames || (r && !rep)) return QF_EINVAL;
+    if (frame_stride < 3ull + k + L || (frame_stride & 15) || !aligned16(frames)) return QF_EINVAL;
+    if (!aligned16(src) || (sh->src_row_stride & 15) || (sh->src_gen_stride & 15)) return QF_EINVAL;
+    if (r && (!aligned16(rep) || (sh->rep_row_stride & 15) || (sh->rep_gen_stride & 15))) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    hipEvent_t ev = prof_begin(ctx, ctx->stream);
+    QF_CHECK_HIP(qf::launch_frame_batch(src, rep, *sh, G, frames, frame_stride, frame_len, ctx->d_explog,
+                                        ctx->num_cus, ctx->stream));
+    prof_end(ctx, ctx->stream, ev, "k_frame_batch");
+    return QF_OK;
+}
+
+int qf_parse_frames_dev(qf_ctx* ctx, uint32_t k, uint32_t r, uint32_t L, uint32_t G, uint32_t max_rows,
+                        const uint8_t* frames, uint64_t frame_stride, const uint32_t* frame_len,
+                        const uint64_t* ids, const uint32_t* n_frames, uint8_t* rows, uint64_t row_stride,
+                        uint64_t rows_gen_stride, uint16_t* row_index, uint32_t* n_rows, int32_t* frame_status) {
+    if (!ctx) return QF_EINVAL;
+    if (k == 0 || k + r > 256) return k == 0 ? QF_EINVAL : QF_ERANGE;
+    if (G == 0) return QF_OK;
+    if (max_rows == 0 || max_rows > 1024 || L == 0) return QF_EINVAL;
+    if (!frames || !frame_len || !ids || !rows || !row_index || !n_rows || !frame_status) return QF_EINVAL;
+    if ((frame_stride & 15) || !aligned16(frames) || !aligned16(rows) || (row_stride & 15) ||
+        (rows_gen_stride & 15) || row_stride < L)
+        return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    hipEvent_t ev = prof_begin(ctx, ctx->stream);
+    QF_CHECK_HIP(qf::launch_parse_frames(frames, frame_stride, frame_len, ids, n_frames, k, r, L, G, max_rows, rows,
+                                         row_stride, rows_gen_stride, row_index, n_rows, frame_status,
+                                         ctx->d_explog, ctx->stream));
+    prof_end(ctx, ctx->stream, ev, "k_parse_frames");
     return QF_OK;
 }
 
