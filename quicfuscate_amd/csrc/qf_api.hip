@@ -326,10 +326,21 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     const uint32_t k = sh->k, r = sh->r, L = sh->L;
     const uint32_t ms = qf::syn_map_stride(k, r);
     const uint64_t coef_gen_stride = (uint64_t)(r + 1) * 16;
+    // QF_DECODE_CHUNK=n runs stages A/B over chunks of n generations (the
+    // syndromes of a chunk can stay in the Infinity Cache).  Measured at C3:
+    // 3-5 % less kernel time per generation but more launch gaps than that
+    // saves (2.46 ms at 10,485 generations per chunk vs 2.25 ms unchunked), so
+    // the default is one chunk.
+    uint64_t chunk = G;
+    {
+        const char* e = getenv("QF_DECODE_CHUNK");
+        const long long c = e ? atoll(e) : 0;
+        if (c > 0 && (uint64_t)c < chunk) chunk = (uint64_t)c;
+    }
     const size_t off_bound = round_up((size_t)G * coef_gen_stride, 256);
     const size_t off_map = round_up(off_bound + (size_t)G * 4, 256);
     const size_t off_syn = round_up(off_map + (size_t)G * ms, 256);
-    const size_t total = off_syn + (size_t)G * r * L;
+    const size_t total = off_syn + (size_t)chunk * r * L;
     int s = grow_work(ctx, total);
     if (s) return s;
     uint8_t* w = ctx->d_work;
@@ -366,31 +377,36 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
-    ev = prof_begin(ctx, st);
-    QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows, w + off_syn, sh->rows_gen_stride,
-                                (uint64_t)r * L, sh->row_stride, L, L, G, w + off_map, ms, ctx->d_zero));
-    prof_end(ctx, st, ev, qf::syn_name(k, r));
-    qf::CombineSlotsArgs a{};
-    a.rows = w + off_syn;
-    a.rows_gen_stride = (uint64_t)r * L;
-    a.row_stride = L;
-    a.dst = rec;
-    a.dst_gen_stride = sh->rec_gen_stride;
-    a.dst_row_stride = sh->rec_row_stride;
-    a.coef = w;
-    a.coef_gen_stride = coef_gen_stride;
-    a.n_out = n_rec;
-    a.bound = d_bound;
-    a.tab256 = ctx->d_tab256;
-    a.pass = 0;
-    a.L = L;
-    a.Lu = (L + 15) / 16;
-    a.zero_slot = r;
-    a.total_units = (uint64_t)G * a.Lu;
     const int PD = pick_PD("QF_DECODE_PD", 1, 1);
-    ev = prof_begin(ctx, st);
-    QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
-    prof_end(ctx, st, ev, "k_combine_slots<" + std::to_string(PD) + ">");
+    const std::string slots_name = "k_combine_slots<" + std::to_string(PD) + ">";
+    for (uint64_t g0 = 0; g0 < G; g0 += chunk) {
+        const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
+        ev = prof_begin(ctx, st);
+        QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows + g0 * sh->rows_gen_stride, w + off_syn,
+                                    sh->rows_gen_stride, (uint64_t)r * L, sh->row_stride, L, L, Gc,
+                                    w + off_map + g0 * ms, ms, ctx->d_zero));
+        prof_end(ctx, st, ev, qf::syn_name(k, r));
+        qf::CombineSlotsArgs a{};
+        a.rows = w + off_syn;
+        a.rows_gen_stride = (uint64_t)r * L;
+        a.row_stride = L;
+        a.dst = rec + g0 * sh->rec_gen_stride;
+        a.dst_gen_stride = sh->rec_gen_stride;
+        a.dst_row_stride = sh->rec_row_stride;
+        a.coef = w + g0 * coef_gen_stride;
+        a.coef_gen_stride = coef_gen_stride;
+        a.n_out = n_rec + g0;
+        a.bound = d_bound + g0;
+        a.tab256 = ctx->d_tab256;
+        a.pass = 0;
+        a.L = L;
+        a.Lu = (L + 15) / 16;
+        a.zero_slot = r;
+        a.total_units = (uint64_t)Gc * a.Lu;
+        ev = prof_begin(ctx, st);
+        QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
+        prof_end(ctx, st, ev, slots_name);
+    }
     return QF_OK;
 }
 

@@ -11,12 +11,18 @@ from quicfuscate_amd import _lib as L
 pytestmark = pytest.mark.gpu
 
 
+def _r16(x):
+    return (x + 15) // 16 * 16
+
+
 def _frame_batch(qf, src, rep, k, r, Lb, G, fs):
+    """src / rep: rows of round16(Lb) bytes."""
     import torch
 
+    rs = _r16(Lb)
     frames = torch.full((G * (k + r) * fs,), 0xCC, dtype=torch.uint8, device="cuda")
     flen = torch.zeros(G * (k + r), dtype=torch.int32, device="cuda")
-    sh = L.EncodeShape(k, r, Lb, 0, Lb, k * Lb, Lb, r * Lb)
+    sh = L.EncodeShape(k, r, Lb, 0, rs, k * rs, rs, r * rs)
     L.check(L._lib().qf_frame_batch_dev(qf.default_context().handle, ctypes.byref(sh), G, src.data_ptr(),
                                         rep.data_ptr(), frames.data_ptr(), fs, flen.data_ptr()), "frame")
     qf.default_context().sync()
@@ -31,9 +37,10 @@ def test_frames_equal_to_raw(qf, oracle, gpu_ctx, k, r, Lb):
     G = 3
     fs = (3 + k + Lb + 15) // 16 * 16
     src_np = rng.integers(0, 256, (G, k, Lb), dtype=np.uint8)
-    src = torch.from_numpy(src_np.reshape(-1)).cuda()
     rep_np = np.stack([oracle.encode(src_np[g], r) for g in range(G)])
-    rep = torch.from_numpy(rep_np.reshape(-1)).cuda()
+    pad = _r16(Lb) - Lb
+    src = torch.from_numpy(np.pad(src_np, ((0, 0), (0, 0), (0, pad))).reshape(-1)).cuda()
+    rep = torch.from_numpy(np.pad(rep_np, ((0, 0), (0, 0), (0, pad))).reshape(-1)).cuda()
     frames, flen = _frame_batch(qf, src, rep, k, r, Lb, G, fs)
     C = oracle.cauchy(k, r)
     for g in range(G):
