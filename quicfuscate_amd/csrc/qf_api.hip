@@ -64,6 +64,9 @@ struct qf_ctx {
     // zero row read by the syndrome kernel for rows a generation lacks
     uint8_t* d_zero = nullptr;
     size_t zero_bytes = 0;
+    // decode pipelining: auxiliary stream + dependency events
+    hipStream_t aux = nullptr;
+    std::vector<hipEvent_t> dep;
     // host-memory pipeline
     static const int kPipe = 3;
     hipStream_t pstream[kPipe] = {nullptr, nullptr, nullptr};
@@ -326,21 +329,27 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     const uint32_t k = sh->k, r = sh->r, L = sh->L;
     const uint32_t ms = qf::syn_map_stride(k, r);
     const uint64_t coef_gen_stride = (uint64_t)(r + 1) * 16;
-    // QF_DECODE_CHUNK=n runs stages A/B over chunks of n generations (the
-    // syndromes of a chunk can stay in the Infinity Cache).  Measured at C3:
-    // 3-5 % less kernel time per generation but more launch gaps than that
-    // saves (2.46 ms at 10,485 generations per chunk vs 2.25 ms unchunked), so
+    // Optional pipelining of stage A (syndromes) and stage B (v_perm combine)
+    // over chunks of QF_DECODE_CHUNK generations: B of chunk c on an
+    // auxiliary stream while A of chunk c + 1 runs on the context's stream
+    // (double-buffered syndromes); QF_DECODE_OVERLAP=0 keeps both on the
+    // context's stream.  Measured at C3 (profiles/r01_decode_pipeline.json):
+    // the two kernels slow each other down when co-resident (A is not idle on
+    // the VALU), so 8 chunks with overlap take 2.49 ms and one chunk 2.25 ms:
     // the default is one chunk.
     uint64_t chunk = G;
     {
         const char* e = getenv("QF_DECODE_CHUNK");
-        const long long c = e ? atoll(e) : 0;
-        if (c > 0 && (uint64_t)c < chunk) chunk = (uint64_t)c;
+        if (e && atoll(e) > 0) chunk = std::min<uint64_t>((uint64_t)atoll(e), G);
     }
+    const char* ov = getenv("QF_DECODE_OVERLAP");
+    const uint64_t n_chunks = (G + chunk - 1) / chunk;
+    const bool overlap = n_chunks > 1 && !(ov && atoi(ov) == 0);
+    const size_t syn_bytes = round_up((size_t)chunk * r * L, 256);
     const size_t off_bound = round_up((size_t)G * coef_gen_stride, 256);
     const size_t off_map = round_up(off_bound + (size_t)G * 4, 256);
     const size_t off_syn = round_up(off_map + (size_t)G * ms, 256);
-    const size_t total = off_syn + (size_t)chunk * r * L;
+    const size_t total = off_syn + syn_bytes * (overlap ? 2 : 1);
     int s = grow_work(ctx, total);
     if (s) return s;
     uint8_t* w = ctx->d_work;
@@ -356,6 +365,16 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         if (hipMalloc(&ctx->d_zero, zb) != hipSuccess) return QF_ENOMEM;
         QF_CHECK_HIP(hipMemset(ctx->d_zero, 0, zb));
         ctx->zero_bytes = zb;
+    }
+    hipStream_t st = ctx->stream, sb = ctx->stream;
+    if (overlap) {
+        if (!ctx->aux) QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+        sb = ctx->aux;
+        while (ctx->dep.size() < 2 * n_chunks + 1) {
+            hipEvent_t e;
+            QF_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ctx->dep.push_back(e);
+        }
     }
     qf::PrepareCauchyArgs pa{};
     pa.row_index = row_index;
@@ -373,21 +392,28 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     pa.max_rows = sh->max_rows;
     pa.map_stride = ms;
     pa.G = G;
-    hipStream_t st = ctx->stream;
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
     const int PD = pick_PD("QF_DECODE_PD", 1, 1);
     const std::string slots_name = "k_combine_slots<" + std::to_string(PD) + ">";
-    for (uint64_t g0 = 0; g0 < G; g0 += chunk) {
+    for (uint64_t c = 0; c < n_chunks; ++c) {
+        const uint64_t g0 = c * chunk;
         const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
+        uint8_t* syn = w + off_syn + (overlap ? (c & 1) * syn_bytes : 0);
+        hipEvent_t evA = overlap ? ctx->dep[2 * c] : nullptr, evB = overlap ? ctx->dep[2 * c + 1] : nullptr;
+        if (overlap && c >= 2) QF_CHECK_HIP(hipStreamWaitEvent(st, ctx->dep[2 * (c - 2) + 1], 0));
         ev = prof_begin(ctx, st);
-        QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows + g0 * sh->rows_gen_stride, w + off_syn,
+        QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows + g0 * sh->rows_gen_stride, syn,
                                     sh->rows_gen_stride, (uint64_t)r * L, sh->row_stride, L, L, Gc,
                                     w + off_map + g0 * ms, ms, ctx->d_zero));
         prof_end(ctx, st, ev, qf::syn_name(k, r));
+        if (overlap) {
+            QF_CHECK_HIP(hipEventRecord(evA, st));
+            QF_CHECK_HIP(hipStreamWaitEvent(sb, evA, 0));
+        }
         qf::CombineSlotsArgs a{};
-        a.rows = w + off_syn;
+        a.rows = syn;
         a.rows_gen_stride = (uint64_t)r * L;
         a.row_stride = L;
         a.dst = rec + g0 * sh->rec_gen_stride;
@@ -403,9 +429,15 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         a.Lu = (L + 15) / 16;
         a.zero_slot = r;
         a.total_units = (uint64_t)Gc * a.Lu;
-        ev = prof_begin(ctx, st);
-        QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
-        prof_end(ctx, st, ev, slots_name);
+        ev = prof_begin(ctx, sb);
+        QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, sb));
+        prof_end(ctx, sb, ev, slots_name);
+        if (overlap) QF_CHECK_HIP(hipEventRecord(evB, sb));
+    }
+    if (overlap) {
+        // the caller's stream sees the whole decode: join the last B launches
+        QF_CHECK_HIP(hipStreamWaitEvent(st, ctx->dep[2 * (n_chunks - 1) + 1], 0));
+        if (n_chunks >= 2) QF_CHECK_HIP(hipStreamWaitEvent(st, ctx->dep[2 * (n_chunks - 2) + 1], 0));
     }
     return QF_OK;
 }
@@ -514,6 +546,11 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->custom_done) hipEventDestroy(c->custom_done);
     if (c->d_work) hipFree(c->d_work);
     if (c->d_zero) hipFree(c->d_zero);
+    if (c->aux) {
+        hipStreamSynchronize(c->aux);
+        hipStreamDestroy(c->aux);
+    }
+    for (auto e : c->dep) hipEventDestroy(e);
     qf::bs_unload(c->bs);
     for (auto& p : c->prof_pending) {
         hipEventDestroy(p.a);

@@ -210,3 +210,18 @@ def test_decode_no_erasures(qf, oracle, gpu_ctx):
     out = run_decode(qf, k, r, L, G, k + r, gens, False)
     check(oracle, k, L, src, gens, out, False)
     assert (out[2] == 0).all()
+
+
+@pytest.mark.parametrize("chunk,overlap", [("7", "1"), ("7", "0"), ("16", "1")])
+def test_decode_chunked_pipeline(qf, oracle, gpu_ctx, chunk, overlap, monkeypatch):
+    # stages A/B over chunks of generations, B on an auxiliary stream
+    # (double-buffered syndromes); twice in a row on the same context
+    monkeypatch.setenv("QF_DECODE_CHUNK", chunk)
+    monkeypatch.setenv("QF_DECODE_OVERLAP", overlap)
+    monkeypatch.delenv("QF_DISABLE_BS", raising=False)
+    for seed in (1, 2):
+        rng = np.random.default_rng(seed)
+        k, r, L, G = 64, 16, 1200, 53
+        src, gens = make_batch(oracle, rng, k, r, L, G, k + r, shuffle=True)
+        out = run_decode(qf, k, r, L, G, k + r, gens, False)
+        check(oracle, k, L, src, gens, out, False)
