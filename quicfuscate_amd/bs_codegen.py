@@ -108,6 +108,8 @@ _ASM = {
     "v_xor": lambda d, a, b: f"v_xor_b32_e32 {V(d)}, {V(a)}, {V(b)}",
     "v_mov": lambda d, a: f"v_mov_b32_e32 {V(d)}, {V(a)}",
     "v_xor3": lambda d, a, b, c: f"v_bitop3_b32 {V(d)}, {V(a)}, {V(b)}, {V(c)} bitop3:0x96",
+    # d = (s[m] & a) | (~s[m] & b): bit select (truth table index s0*4 + s1*2 + s2)
+    "v_bitsel_s": lambda d, m, a, b: f"v_bitop3_b32 {V(d)}, s{m}, {V(a)}, {V(b)} bitop3:0xca",
     "v_movk": lambda d, k: f"v_mov_b32_e32 {V(d)}, {k}",
     "v_andk": lambda d, k, a: f"v_and_b32_e32 {V(d)}, 0x{k:08x}, {V(a)}",
     "v_lshr": lambda d, s, a: f"v_lshrrev_b32_e32 {V(d)}, {s}, {V(a)}",
@@ -175,8 +177,9 @@ V_SRCA, V_SRCB, V_DSTA, V_DSTB = 6, 8, 10, 12   # 64-bit pointers (even-aligned)
 V_T = 14         # v14..v17 transpose temps
 V_COMBO = 18     # 22 combo registers v18..v39
 V_ZA, V_ZB, V_ADDR, V_SLOT = 40, 42, 44, 46      # syn only
-SGPR_NEXT_FREE = 42
+SGPR_NEXT_FREE = 46
 S_TMP, S_TMP2 = 38, 40
+S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
 
@@ -192,6 +195,9 @@ class KernelSpec:
     # non-temporal (tools/bs_lab.py: -9 % at C2 vs the default policy)
     ld_policy: str = "nt"
     st_policy: str = "nt"
+    # transpose swaps as shift + bit-select (4 ops per pair) instead of the
+    # classic xor/and/xor delta swap (6 ops per pair)
+    bfi_transpose: bool = True
 
     @property
     def name(self) -> str:
@@ -251,10 +257,24 @@ _COMBO_BUILD = {  # mask: (a, b) meaning combo = a ^ b, where a/b are masks
 }
 
 
-def _transpose_ops(base: int) -> list[Op]:
+def _transpose_ops(base: int, bfi: bool = False) -> list[Op]:
     """32 bytes in 8 dwords <-> 8 bit-planes (3 delta-swap stages; an
-    involution, so the same network maps planes back to bytes)."""
+    involution, so the same network maps planes back to bytes).
+
+    bfi: each swap of (a, b) with shift s and mask M is
+      a' = (M & a) | (~M & (b << s)),  b' = (M & (a >> s)) | (~M & b)
+    i.e. two shifts and two v_bitop3 bit-selects with M in an SGPR."""
     ops = []
+    if bfi:
+        for stage, (sh, mask, pairs) in enumerate(_TRANSPOSE):
+            sm = S_TMASK + stage
+            for q, (a, b) in enumerate(pairs):
+                t, u = V_T + 2 * (q & 1), V_T + 2 * (q & 1) + 1
+                ops.append(Op("v_lshl", (t, sh, base + b)))
+                ops.append(Op("v_lshr", (u, sh, base + a)))
+                ops.append(Op("v_bitsel_s", (base + a, sm, base + a, t)))
+                ops.append(Op("v_bitsel_s", (base + b, sm, u, base + b)))
+        return ops
     for sh, mask, pairs in _TRANSPOSE:
         t = [V_T + q for q in range(4)]
         ops += [Op("v_lshr", (t[q], sh, base + a)) for q, (a, b) in enumerate(pairs)]
@@ -327,10 +347,11 @@ def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict,
     ops.extend(first_pass + second)
 
 
-def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool, xor3: bool = False):
+def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool, xor3: bool = False,
+                bfi: bool = False):
     """Transpose one source row (ring buffer at `base`) and accumulate it into
     all r repair accumulators with the Cauchy coefficients of column i."""
-    ops.extend(_transpose_ops(base))
+    ops.extend(_transpose_ops(base, bfi))
     lo, hi = _combo_regs(base)
     rows = [mul_matrix_rows(C[j][i]) for j in range(r)]
     need_lo = {rb & 15 for rr in rows for rb in rr} - {0}
@@ -355,6 +376,8 @@ def _prologue(E, spec: KernelSpec):
     E(Op("s_mov", (34, 11)))
     E(Op("s_movk", (35, 0)))
     E(Op("s_movk", (S_ABSENT, ABSENT)))
+    for q, (_, mask, _) in enumerate(_TRANSPOSE):
+        E(Op("s_movk", (S_TMASK + q, mask)))
     E(Op("label", (".Litem",)))
     E(Op("s_cmp_ge_br", (28, 17, ".Lend")))
     # unit A = item*128 + lane, unit B = A + 64; valid = unit < total
@@ -432,10 +455,11 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
             load_row(i + pd)
         after = min(pd, k - 1 - i)
         E(Op("s_waitcnt_vm", (2 * after,)))
-        _source_row(ops, C, i, r, ring0 + 8 * (i % nbuf), acc0, init=(i == 0), xor3=spec.xor3)
+        _source_row(ops, C, i, r, ring0 + 8 * (i % nbuf), acc0, init=(i == 0), xor3=spec.xor3,
+                    bfi=spec.bfi_transpose)
     # planes -> bytes, store 2 x 16 bytes per lane per repair
     for j in range(r):
-        ops.extend(_transpose_ops(acc0 + 8 * j))
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
     E(Op("s_nop", (4,)))
     for j in range(r):
         _store_pair(E, acc0 + 8 * j, 26, 24, spec.st_policy)
@@ -504,13 +528,13 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         E(Op("s_waitcnt_vm", (2 * after,)))
         base = ring0 + 8 * (n % nbuf)
         if kind == "rep":
-            ops.extend(_transpose_ops(base))
+            ops.extend(_transpose_ops(base, spec.bfi_transpose))
             for b in range(8):
                 E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
         else:
-            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3)
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose)
     for j in range(r):
-        ops.extend(_transpose_ops(acc0 + 8 * j))
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
     E(Op("s_nop", (4,)))
     for j in range(r):
         present(k + j, 0, S_TMP)
@@ -761,6 +785,9 @@ class Emulator:
                 wv(a[0], rv(a[1]))
             elif n == "v_xor3":
                 wv(a[0], rv(a[1]) ^ rv(a[2]) ^ rv(a[3]))
+            elif n == "v_bitsel_s":
+                m = np.uint64(s[a[1]])
+                wv(a[0], (m & rv(a[2])) | (~m & np.uint64(MASK32) & rv(a[3])))
             elif n == "v_movk":
                 wv(a[0], np.full(64, a[1], np.uint64))
             elif n == "v_andk":

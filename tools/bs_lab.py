@@ -46,19 +46,15 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
-    # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3;
-    # "ld:<bits>" / "st:<bits>" cache-policy bits; "L:<n>" payload bytes;
-    # "dst:wide" destination rows 2 KiB apart, generations 32 KiB apart, so a
-    # wave's stores cover ~32 KiB contiguously (timing only, not the layout
-    # of the real output))
+    # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3 xor;
+    # "nobfi" = classic 6-op delta swaps; "ld:/st:<bits>" cache policy;
+    # "L:<n>" payload bytes; "dst:wide" synthetic destination layout)
     ("base", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("dstwide", 64, 16, 3, ("ld:nt", "st:nt", "dst:wide"), ALL),
-    ("writeonly", 64, 16, 3, ("nocompute", "noload", "st:nt"), ALL),
-    ("writeonly_dstwide", 64, 16, 3, ("nocompute", "noload", "st:nt", "dst:wide"), ALL),
-    ("writeonly_persist2", 64, 16, 3, ("nocompute", "noload", "st:nt"), 2),
-    ("writeonly_persist8", 64, 16, 3, ("nocompute", "noload", "st:nt"), 8),
-    ("nocompute", 64, 16, 3, ("nocompute", "ld:nt", "st:nt"), ALL),
-    ("nocompute_dstwide", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "dst:wide"), ALL),
+    ("nobfi", 64, 16, 3, ("ld:nt", "st:nt", "nobfi"), ALL),
+    ("compute", 64, 16, 3, ("noload", "nostore"), ALL),
+    ("compute_nobfi", 64, 16, 3, ("noload", "nostore", "nobfi"), ALL),
+    ("pd4", 64, 16, 4, ("ld:nt", "st:nt"), ALL),
+    ("pd2", 64, 16, 2, ("ld:nt", "st:nt"), ALL),
 ]
 
 
@@ -73,7 +69,8 @@ def build():
     for name, k, r, pd, flags, bpc in VARIANTS:
         ld = next((f[3:] for f in flags if f.startswith("ld:")), "")
         st = next((f[3:] for f in flags if f.startswith("st:")), "")
-        spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st)
+        spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st,
+                             bfi_transpose="nobfi" not in flags)
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"lab_{name}", text.replace(spec.name, f"lab_{name}"), OUT)
         Lv = next((int(f[2:]) for f in flags if f.startswith("L:")), 1200)
