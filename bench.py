@@ -94,9 +94,17 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU over RCCL ("nccl"); QF_BENCH_BACKEND=gloo rehearses
+    # the multi-rank path on fewer GPUs (ranks share devices round robin)
+    backend = os.environ.get("QF_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from quicfuscate_amd import _lib as L
     from quicfuscate_amd import fec
@@ -190,7 +198,8 @@ def main(argv=None):
     verified = st_ok and n_ok and idx_ok and bytes_ok
 
     step_ms_max, enc_ms_max, dec_ms_max, fails = reduce_max(
-        torch, dist, [step_ms, enc_ms, dec_ms, 0.0 if verified else 1.0], world, dev)
+        torch, dist, [step_ms, enc_ms, dec_ms, 0.0 if verified else 1.0], world,
+        dev if backend == "nccl" else "cpu")
 
     src_bytes_total = world * G * k * Lb
     gib = 1 << 30

@@ -140,6 +140,10 @@ _ASM = {
     "s_movk": lambda d, k: f"s_mov_b32 s{d}, {k}",
     "s_add": lambda d, a, b: f"s_add_u32 s{d}, s{a}, s{b}",
     "s_lshl": lambda d, a, k: f"s_lshl_b32 s{d}, s{a}, {k}",
+    "s_lshrk": lambda d, a, k: f"s_lshr_b32 s{d}, s{a}, {k}",
+    "s_andk": lambda d, a, k: f"s_and_b32 s{d}, s{a}, {k}",
+    "s_mul": lambda d, a, b: f"s_mul_i32 s{d}, s{a}, s{b}",
+    "s_min": lambda d, a, b: f"s_min_u32 s{d}, s{a}, s{b}",
     "s_cmp_ge_br": lambda a, b, lbl: f"s_cmp_ge_u32 s{a}, s{b}\n\ts_cbranch_scc1 {lbl}",
     "s_branch": lambda lbl: f"s_branch {lbl}",
     "s_waitcnt_vm": lambda n: f"s_waitcnt vmcnt({n})",
@@ -177,7 +181,7 @@ V_SRCA, V_SRCB, V_DSTA, V_DSTB = 6, 8, 10, 12   # 64-bit pointers (even-aligned)
 V_T = 14         # v14..v17 transpose temps
 V_COMBO = 18     # 22 combo registers v18..v39
 V_ZA, V_ZB, V_ADDR, V_SLOT = 40, 42, 44, 46      # syn only
-SGPR_NEXT_FREE = 46
+SGPR_NEXT_FREE = 48
 S_TMP, S_TMP2 = 38, 40
 S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
@@ -198,6 +202,9 @@ class KernelSpec:
     # transpose swaps as shift + bit-select (4 ops per pair) instead of the
     # classic xor/and/xor delta swap (6 ops per pair)
     bfi_transpose: bool = True
+    # workgroup w processes items of a contiguous range per XCD (blocks go to
+    # XCD w % 8), so lines shared by neighbouring items meet in one L2
+    xcd_remap: bool = True
 
     @property
     def name(self) -> str:
@@ -368,9 +375,23 @@ def _prologue(E, spec: KernelSpec):
     E(Op("v_andk", (V_LANE, 63, V_LANE)))
     E(Op("v_readfirstlane", (29, V_T)))
     E(Op("s_nop", (4,)))
-    E(Op("s_lshl", (30, 2, 2)))              # s30 = workgroup_id * 4   (s2 = workgroup id)
-    E(Op("s_add", (28, 29, 30)))             # s28 = item = global wave id
     E(Op("s_waitcnt_lgkm", ()))
+    if spec.xcd_remap:
+        # w' = base(w % 8) + w / 8 with XCD x owning c_x = q + (x < rem)
+        # consecutive workgroups, q = nwg / 8, rem = nwg % 8 (a bijection)
+        E(Op("s_lshrk", (46, 18, 2)))        # nwg = total waves / 4
+        E(Op("s_andk", (47, 2, 7)))          # x
+        E(Op("s_lshrk", (30, 46, 3)))        # q
+        E(Op("s_mul", (30, 47, 30)))         # x * q
+        E(Op("s_andk", (46, 46, 7)))         # rem
+        E(Op("s_min", (46, 47, 46)))         # min(x, rem)
+        E(Op("s_add", (30, 30, 46)))
+        E(Op("s_lshrk", (46, 2, 3)))         # w / 8
+        E(Op("s_add", (30, 30, 46)))
+        E(Op("s_lshl", (30, 30, 2)))         # w' * 4
+    else:
+        E(Op("s_lshl", (30, 2, 2)))          # s30 = workgroup_id * 4   (s2 = workgroup id)
+    E(Op("s_add", (28, 29, 30)))             # s28 = item = global wave id
     E(Op("s_mov", (32, 10)))
     E(Op("s_movk", (33, 0)))
     E(Op("s_mov", (34, 11)))
@@ -868,6 +889,14 @@ class Emulator:
                 s[a[0]] = (s[a[1]] + s[a[2]]) & MASK32
             elif n == "s_lshl":
                 s[a[0]] = (s[a[1]] << a[2]) & MASK32
+            elif n == "s_lshrk":
+                s[a[0]] = s[a[1]] >> a[2]
+            elif n == "s_andk":
+                s[a[0]] = s[a[1]] & a[2]
+            elif n == "s_mul":
+                s[a[0]] = (s[a[1]] * s[a[2]]) & MASK32
+            elif n == "s_min":
+                s[a[0]] = min(s[a[1]], s[a[2]])
             elif n == "s_cmp_ge_br":
                 if s[a[0]] >= s[a[1]]:
                     pc = self.labels[a[2]]

@@ -219,3 +219,10 @@ def test_xor3_variant_matches_plain(oracle, mode):
         outs.append((src, dst.copy()))
     assert (outs[0][1] == outs[1][1]).all()
     assert outs[0][1].any()
+
+
+def test_xcd_remap_is_a_bijection():
+    for nwg in range(1, 400):
+        q, rem = nwg // 8, nwg % 8
+        got = sorted((w % 8) * q + min(w % 8, rem) + w // 8 for w in range(nwg))
+        assert got == list(range(nwg))

@@ -47,14 +47,15 @@ def variant_ops(bs, spec, flags):
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
     # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3 xor;
-    # "nobfi" = classic 6-op delta swaps; "ld:/st:<bits>" cache policy;
-    # "L:<n>" payload bytes; "dst:wide" synthetic destination layout)
-    ("base", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("nobfi", 64, 16, 3, ("ld:nt", "st:nt", "nobfi"), ALL),
-    ("compute", 64, 16, 3, ("noload", "nostore"), ALL),
-    ("compute_nobfi", 64, 16, 3, ("noload", "nostore", "nobfi"), ALL),
-    ("pd4", 64, 16, 4, ("ld:nt", "st:nt"), ALL),
-    ("pd2", 64, 16, 2, ("ld:nt", "st:nt"), ALL),
+    # "nobfi" = classic 6-op delta swaps; "noremap" = no XCD-aware item order;
+    # "ld:/st:<bits>" cache policy; "L:<n>" payload bytes)
+    ("warm", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("remap", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("noremap", 64, 16, 3, ("ld:nt", "st:nt", "noremap"), ALL),
+    ("remap_b", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("noremap_b", 64, 16, 3, ("ld:nt", "st:nt", "noremap"), ALL),
+    ("mem_remap", 64, 16, 3, ("nocompute", "ld:nt", "st:nt"), ALL),
+    ("mem_noremap", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "noremap"), ALL),
 ]
 
 
@@ -70,7 +71,7 @@ def build():
         ld = next((f[3:] for f in flags if f.startswith("ld:")), "")
         st = next((f[3:] for f in flags if f.startswith("st:")), "")
         spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st,
-                             bfi_transpose="nobfi" not in flags)
+                             bfi_transpose="nobfi" not in flags, xcd_remap="noremap" not in flags)
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"lab_{name}", text.replace(spec.name, f"lab_{name}"), OUT)
         Lv = next((int(f[2:]) for f in flags if f.startswith("L:")), 1200)
