@@ -70,6 +70,26 @@ def reduce_max(torch, dist, values, world: int, device) -> list:
     return t.tolist()
 
 
+def xor_fold(torch, buf) -> int:
+    """XOR of all 64-bit words of a device buffer (length % 8 == 0)."""
+    w = buf.view(torch.int64)
+    while w.numel() > 1:
+        if w.numel() % 2:
+            w = torch.cat([w, torch.zeros(1, dtype=torch.int64, device=w.device)])
+        w = torch.bitwise_xor(w[0::2], w[1::2])
+    return int(w.item()) & ((1 << 64) - 1)
+
+
+def gather_folds(torch, dist, fold: int, world: int, device) -> list:
+    """Every rank's repair XOR-fold (RCCL all_gather: XOR is not a reduction op)."""
+    t = torch.tensor([fold - (1 << 64) if fold >= 1 << 63 else fold], dtype=torch.int64, device=device)
+    if world == 1:
+        return [fold]
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [int(x.item()) & ((1 << 64) - 1) for x in out]
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,6 +215,7 @@ def main(argv=None):
     gi = torch.arange(G, device=dev)[:, None].expand(-1, e)
     bytes_ok = bool((recv == srcv[gi, er_t]).all().item())
     checksum = int(rep.view(torch.int64).sum().item()) & ((1 << 64) - 1)
+    folds = gather_folds(torch, dist, xor_fold(torch, rep), world, dev if backend == "nccl" else "cpu")
     verified = st_ok and n_ok and idx_ok and bytes_ok
 
     step_ms_max, enc_ms_max, dec_ms_max, fails = reduce_max(
@@ -288,6 +309,7 @@ def main(argv=None):
         },
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,
+        "repair_xor_fold_by_rank": [f"{f:016x}" for f in folds],
     }
 
     if rank == 0 and world == 1 and args.host_path_G > 0:
@@ -296,6 +318,7 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e,
                                            min(args.cpu_sample, G))
+        out["cpu_variants"] = cpu_variants(src, rep, k, r, Lb, min(args.cpu_sample, G))
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -320,6 +343,34 @@ def host_path_rate(torch, lib, L, ctx, k, r, Lb, G):
     dt = (time.perf_counter() - t0) / reps
     return {"generations": G, "encode_src_gibps_incl_pcie": round(G * k * Lb / dt / (1 << 30), 3),
             "bytes_moved_gb": round(G * (k + r) * Lb / 1e9, 3), "seconds": round(dt, 4)}
+
+
+def cpu_variants(src, rep, k, r, Lb, S):
+    """SURVEY 8(d) CPU comparison encoders (oracle/cpu_variants.c): the
+    reference's table loop and an AVX2 split-nibble encoder, 1 thread and the
+    box's CPU share (16 threads); encode only, outputs checked against the GPU
+    repairs of the same sample.  Reported beside cpu_baseline, not instead."""
+    import sys
+
+    sys.path.insert(0, str(REPO))
+    from tests import oracle_py as oracle  # test infrastructure
+
+    src_h = src[: S * k * Lb].cpu().numpy().reshape(S, k, Lb)
+    rep_h = rep[: S * r * Lb].cpu().numpy().reshape(S, r, Lb)
+    threads = min(16, os.cpu_count() or 1)
+    res = {"threads_available": os.cpu_count(), "unit": "GiB/s (source payload, encode)"}
+    for kind in ("table", "avx2"):
+        if kind == "avx2" and not oracle.has_avx2():
+            res[kind] = "no AVX2 on this host"
+            continue
+        for nt in (1, threads):
+            n = S if (kind == "avx2" or nt > 1) else max(1, S // 4)
+            t0 = time.perf_counter()
+            got = oracle.cpu_encode(kind, src_h[:n], r, nt)
+            dt = time.perf_counter() - t0
+            res[f"{kind}_{nt}t"] = {"gibps": round(n * k * Lb / dt / (1 << 30), 4), "generations": n,
+                                    "seconds": round(dt, 3), "matches_gpu": bool((got == rep_h[:n]).all())}
+    return res
 
 
 def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):

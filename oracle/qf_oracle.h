@@ -102,6 +102,15 @@ int oracle_decode_generation_as_written(uint32_t k, uint32_t L, uint32_t n_rows,
  * byte (t & 7) of splitmix64(seed + (t >> 3)). */
 void oracle_fill_splitmix(uint8_t *buf, size_t n, uint64_t seed, uint64_t word_offset);
 
+
+/* cpu_variants.c: CPU comparison encoders for bench.py; G dense
+ * generations, generations split over `threads` pthreads. */
+int cpu_encode_table(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
+                     uint8_t *rep, uint32_t threads);
+int cpu_encode_avx2(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
+                    uint8_t *rep, uint32_t threads);
+int cpu_has_avx2(void);
+
 #ifdef __cplusplus
 }
 #endif

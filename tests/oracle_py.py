@@ -15,6 +15,9 @@ _lib = ctypes.CDLL(str(_LIB_PATH))
 _P = ctypes.c_void_p
 _U32 = ctypes.c_uint32
 _SZ = ctypes.c_size_t
+_lib.cpu_encode_table.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
+_lib.cpu_encode_avx2.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
+_lib.cpu_has_avx2.argtypes = []
 _lib.oracle_gf_mul.restype = ctypes.c_uint8
 _lib.oracle_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
 _lib.oracle_gf_mul_shift.restype = ctypes.c_uint8
@@ -88,6 +91,23 @@ def encode(src: np.ndarray, r: int, coeff: np.ndarray | None = None, L: int | No
     if s != 0:
         raise ValueError(f"oracle encode status {s}")
     return rep[:, :L]
+
+
+def cpu_encode(kind: str, src: np.ndarray, r: int, threads: int = 1) -> np.ndarray:
+    """Comparison encoders of oracle/cpu_variants.c over dense generations:
+    src (G, k, L) -> (G, r, L).  kind: "table" or "avx2"."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    G, k, L = src.shape
+    rep = np.zeros((G, r, L), np.uint8)
+    fn = _lib.cpu_encode_table if kind == "table" else _lib.cpu_encode_avx2
+    s = fn(k, r, L, G, _p(src), _p(rep), threads)
+    if s != 0:
+        raise ValueError(f"cpu_encode({kind}) status {s}")
+    return rep
+
+
+def has_avx2() -> bool:
+    return bool(_lib.cpu_has_avx2())
 
 
 def encode_clmul_fold(src: np.ndarray, r: int) -> np.ndarray:

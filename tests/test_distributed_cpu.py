@@ -21,6 +21,16 @@ def test_shards_partition_generations():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_xor_fold():
+    import functools
+    import operator
+
+    import torch
+
+    x = torch.arange(1001, dtype=torch.int64) * 0x9E3779B97F4A7C15 % (1 << 62)
+    assert bench.xor_fold(torch, x.view(torch.uint8)) == functools.reduce(operator.xor, x.tolist())
+
+
 def test_payload_offsets_distinct_and_disjoint():
     G, k, L = 1000, 64, 1200
     offs = [bench.payload_word_offset(r, G, k, L) for r in range(8)]
@@ -56,6 +66,8 @@ def _worker(rank, world, port, q):
     # rank-dependent "timings"; rank 1 reports a failed verification
     vals = [10.0 + rank, 3.0 * (rank + 1), 7.0 - rank, float(rank == 1)]
     out = bench.reduce_max(torch, dist, vals, world, "cpu")
+    folds = bench.gather_folds(torch, dist, (0xF000000000000000 | rank), world, "cpu")
+    assert folds == [0xF000000000000000, 0xF000000000000001]
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank, lo, hi, out))

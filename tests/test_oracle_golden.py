@@ -133,3 +133,15 @@ def test_splitmix_golden(oracle):
     a = oracle.fill_splitmix(100, 7)
     b = oracle.fill_splitmix(60, 7, 5)
     assert (a[40:100] == b).all()
+
+
+@pytest.mark.parametrize("kind", ["table", "avx2"])
+@pytest.mark.parametrize("k,r,L,G,threads", [(64, 16, 1200, 5, 3), (7, 5, 33, 4, 2), (16, 1, 31, 3, 1)])
+def test_cpu_comparison_encoders_match_oracle(oracle, kind, k, r, L, G, threads):
+    if kind == "avx2" and not oracle.has_avx2():
+        pytest.skip("no AVX2 on this host")
+    rng = np.random.default_rng(k + L)
+    src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
+    got = oracle.cpu_encode(kind, src, r, threads)
+    for g in range(G):
+        assert (got[g] == oracle.encode(src[g], r)).all()
