@@ -140,18 +140,24 @@ def main(argv=None):
     ctx = fec.Context(local, stream.cuda_stream)
 
     # --- inputs (resident in HBM before timing) ---------------------------
+    # Repair rows are blocks of Lr = round_up(L, 128) bytes that are zero
+    # beyond L, as the reference's pool blocks (decoder.rs:182/264,
+    # optimize.rs:524); QF_ENCODE_ZERO_TAIL lets the kernel write the tail, so
+    # it stores whole 128-B lines.  Algorithmic bytes count L per row.
+    Lr = (Lb + 127) // 128 * 128
     src = torch.empty(G * k * Lb, dtype=torch.uint8, device=dev)
-    rep = torch.empty(G * r * Lb, dtype=torch.uint8, device=dev)
+    rep = torch.zeros(G * r * Lr, dtype=torch.uint8, device=dev)
     word_off = payload_word_offset(rank, G, k, Lb)
     L.check(lib.qf_fill_splitmix_dev(ctx.handle, src.data_ptr(), src.numel(), SEED, word_off), "fill")
-    enc_args = dict(src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lb, rep_gen_stride=r * Lb, G=G)
+    enc_args = dict(src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lr, rep_gen_stride=r * Lr, G=G,
+                    zero_tail=True)
     fec.encode_batch(src, rep, k, r, Lb, ctx=ctx, **enc_args)
 
     erased = erasure_plan(G, k, e, SEED + rank)
     aidx = arrival_index(erased, k, r)
     n_slots = aidx.shape[1]
     rows = torch.empty(G * n_slots * Lb, dtype=torch.uint8, device=dev)
-    srcv, repv, rowsv = src.view(G, k, Lb), rep.view(G, r, Lb), rows.view(G, n_slots, Lb)
+    srcv, repv, rowsv = src.view(G, k, Lb), rep.view(G, r, Lr)[:, :, :Lb], rows.view(G, n_slots, Lb)
     aidx_t = torch.from_numpy(aidx.astype(np.int64)).to(dev)
     CH = 4096
     for g0 in range(0, G, CH):
@@ -214,9 +220,10 @@ def main(argv=None):
     recv = rec.view(G, emax, Lb)[:, :e]
     gi = torch.arange(G, device=dev)[:, None].expand(-1, e)
     bytes_ok = bool((recv == srcv[gi, er_t]).all().item())
+    tails_zero = bool((rep.view(G, r, Lr)[:, :, Lb:] == 0).all().item())
     checksum = int(rep.view(torch.int64).sum().item()) & ((1 << 64) - 1)
     folds = gather_folds(torch, dist, xor_fold(torch, rep), world, dev if backend == "nccl" else "cpu")
-    verified = st_ok and n_ok and idx_ok and bytes_ok
+    verified = st_ok and n_ok and idx_ok and bytes_ok and tails_zero
 
     step_ms_max, enc_ms_max, dec_ms_max, fails = reduce_max(
         torch, dist, [step_ms, enc_ms, dec_ms, 0.0 if verified else 1.0], world,
@@ -316,9 +323,10 @@ def main(argv=None):
         out["host_path"] = host_path_rate(torch, lib, L, ctx, k, r, Lb, min(args.host_path_G, G))
 
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e,
-                                           min(args.cpu_sample, G))
-        out["cpu_variants"] = cpu_variants(src, rep, k, r, Lb, min(args.cpu_sample, G))
+        S = min(args.cpu_sample, G)
+        rep_dense = repv[:S].contiguous().view(-1)
+        out["cpu_baseline"] = cpu_baseline(src, rep_dense, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S)
+        out["cpu_variants"] = cpu_variants(src, rep_dense, k, r, Lb, S)
 
     if rank == 0:
         print(json.dumps(out), flush=True)

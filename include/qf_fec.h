@@ -98,17 +98,24 @@ int qf_gf256_mul_slice_dev(qf_ctx *ctx, const uint8_t *a_dev, const uint8_t *b_d
  *   rep[g][j][t] = XOR_{i<k} C[j][i] * src[g][i][t]      (t < L, j < r)
  * Row i of generation g starts at src_dev + g*src_gen_stride + i*src_row_stride;
  * repair j at rep_dev + g*rep_gen_stride + j*rep_row_stride.  Exactly L bytes
- * per repair row are written.  coeff_rxk (host, r*k bytes, row-major) or NULL
+ * per repair row are written (plus the zero tail with QF_ENCODE_ZERO_TAIL).  coeff_rxk (host, r*k bytes, row-major) or NULL
  * for the reference's Cauchy matrix (decoder.rs:280-298).
  * Sliding windows (adaptive.rs:519-562, one window per source packet) are the
  * special case src_gen_stride == src_row_stride.
  * Fast path: src/rep pointers and strides 16-byte aligned (any L).
  * ------------------------------------------------------------------------- */
+/* qf_encode_shape.flags: the caller lets the library write zeros to bytes
+ * [L, round_up(L, 128)) of every repair row when rep_row_stride covers them
+ * (the reference's repair is a pool block that is zero beyond L,
+ * decoder.rs:182/264 + optimize.rs:524).  With 128-B aligned repair rows this
+ * lets the encode kernel store whole 128-B lines only. */
+#define QF_ENCODE_ZERO_TAIL 1u
+
 typedef struct qf_encode_shape {
     uint32_t k;              /* generation (window) size, 1..255 */
     uint32_t r;              /* repairs per generation, k + r <= 256 for Cauchy */
     uint32_t L;              /* payload bytes per packet */
-    uint32_t reserved;
+    uint32_t flags;          /* QF_ENCODE_* bits; 0: exactly L bytes per repair row */
     uint64_t src_row_stride;
     uint64_t src_gen_stride;
     uint64_t rep_row_stride;

@@ -43,7 +43,7 @@ class QfError(RuntimeError):
 
 class EncodeShape(ctypes.Structure):
     _fields_ = [
-        ("k", _U32), ("r", _U32), ("L", _U32), ("reserved", _U32),
+        ("k", _U32), ("r", _U32), ("L", _U32), ("flags", _U32),
         ("src_row_stride", _U64), ("src_gen_stride", _U64),
         ("rep_row_stride", _U64), ("rep_gen_stride", _U64),
     ]

@@ -136,6 +136,7 @@ _ASM = {
                + (f" offset:{off}" if off else "") + (f" {pol}" if pol else ""),
     "s_exec": lambda s: "s_mov_b64 exec, -1" if s is None else f"s_mov_b64 exec, {SP(s)}",
     "s_and64": lambda d, a, b: f"s_and_b64 {SP(d)}, {SP(a)}, {SP(b)}",
+    "s_andn2_64": lambda d, a, b: f"s_andn2_b64 {SP(d)}, {SP(a)}, {SP(b)}",
     "s_mov": lambda d, a: f"s_mov_b32 s{d}, s{a}",
     "s_movk": lambda d, k: f"s_mov_b32 s{d}, {k}",
     "s_add": lambda d, a, b: f"s_add_u32 s{d}, s{a}, s{b}",
@@ -168,21 +169,31 @@ _ASM = {
 #   s[4:5] src (syn: received rows)   s[6:7] dst (syn: syndrome rows)
 #   s8  src generation stride (u32)   s9  dst generation stride (u32)
 #   s10 src row stride                s11 dst row stride
-#   s12 L   s13 Lu = L/16   s14 total units G*Lu   s15 magic   s16 shift
+#   s12 Lu = L/16 (payload units per row: lanes with u >= Lu load nothing)
+#   s13 Lv >= Lu (lane units per row: the (generation, unit) lane space is
+#       G x Lv; Lv = Lu rounded up to 8 puts every item boundary and row
+#       start of a 128-B aligned layout on a 128-B line boundary)
+#   s14 total units G*Lv   s15 magic (division by Lv)   s16 shift
 #   s17 n_items   s18 total waves in the grid
-#   s19 slot-map generation stride    s[20:21] slot map   s[22:23] zero row (syn)
-# SGPRs: s[24:25] valid B, s[26:27] valid A, s28 item, s29 wave in group,
-# s30 temp, s31 ABSENT constant, s[32:33] {src row stride, 0},
+#   s19 enc: units stored per row (Lu, or Lv: the zero tail [L, 16 Lv) of
+#       each repair row is written too, so every stored line is whole);
+#       syn: slot-map generation stride (syndromes of all Lv units are
+#       stored: the syndrome rows live in the library's workspace)
+#   s[20:21] slot map   s[22:23] zero row (syn)
+# SGPRs: s[24:25] load mask B, s[26:27] load mask A, s28 item, s29 wave in
+# group, s30 temp, s31 ABSENT constant, s[32:33] {src row stride, 0},
 # s[34:35] {dst row stride, 0}, s[36:37] mad carry sink, s[38:39] and
-# s[40:41] mask temps.
+# s[40:41] mask temps, s[48:49] store mask A, s[50:51] store mask B,
+# s[52:53] mask temp.
 KERNARG_BYTES = 80
 V_LANE, V_F, V_GA, V_UA, V_GB, V_UB = 0, 1, 2, 3, 4, 5
 V_SRCA, V_SRCB, V_DSTA, V_DSTB = 6, 8, 10, 12   # 64-bit pointers (even-aligned)
 V_T = 14         # v14..v17 transpose temps
 V_COMBO = 18     # 22 combo registers v18..v39
 V_ZA, V_ZB, V_ADDR, V_SLOT = 40, 42, 44, 46      # syn only
-SGPR_NEXT_FREE = 48
+SGPR_NEXT_FREE = 54
 S_TMP, S_TMP2 = 38, 40
+S_STA, S_STB, S_PAD = 48, 50, 52   # store masks of halves A / B, mask temp
 S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
@@ -402,8 +413,8 @@ def _prologue(E, spec: KernelSpec):
     E(Op("label", (".Litem",)))
     E(Op("s_cmp_ge_br", (28, 17, ".Lend")))
     # unit A = item*128 + lane, unit B = A + 64; valid = unit < total
-    for h, (gv, uv, sv, dv, vm) in enumerate(((V_GA, V_UA, V_SRCA, V_DSTA, 26),
-                                              (V_GB, V_UB, V_SRCB, V_DSTB, 24))):
+    for h, (gv, uv, sv, dv, vm, sm) in enumerate(((V_GA, V_UA, V_SRCA, V_DSTA, 26, S_STA),
+                                                  (V_GB, V_UB, V_SRCB, V_DSTB, 24, S_STB))):
         if h == 0:
             E(Op("v_lshl_add_s", (V_F, 28, 7, V_LANE)))
         else:
@@ -414,6 +425,14 @@ def _prologue(E, spec: KernelSpec):
         E(Op("v_lshr_s", (gv, 16, gv)))
         E(Op("v_mul_lo_s", (uv, gv, 13)))
         E(Op("v_sub", (uv, V_F, uv)))
+        # load mask: unit in range and u < Lu; store mask: unit in range and
+        # (enc) u < s19 / (syn) any u < Lv
+        E(Op("v_cmp_gt_s", (S_PAD, 12, uv)))
+        if spec.mode == "enc":
+            E(Op("v_cmp_gt_s", (S_TMP, 19, uv)))
+        E(Op("s_nop", (4,)))
+        E(Op("s_and64", (sm, vm, S_TMP if spec.mode == "enc" else vm)))
+        E(Op("s_and64", (vm, vm, S_PAD)))
         # src/dst + g * gen_stride + 16 u   (VOP3 reads at most one SGPR)
         for ptr, base_s, gs_s in ((sv, 4, 8), (dv, 6, 9)):
             E(Op("v_movs", (ptr, base_s)))
@@ -481,9 +500,20 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     # planes -> bytes, store 2 x 16 bytes per lane per repair
     for j in range(r):
         ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+    # padding lanes (stored, not loaded: the zero tail) hold garbage, since
+    # masked loads leave stale planes in their half of the ring; byte
+    # positions are independent, so clearing their half of the repairs here
+    # is enough
+    for h, (vm, sm) in enumerate(((26, S_STA), (24, S_STB))):
+        E(Op("s_andn2_64", (S_PAD, sm, vm)))
+        E(Op("s_exec", (S_PAD,)))
+        for j in range(r):
+            for q in range(4):
+                E(Op("v_movk", (acc0 + 8 * j + 4 * h + q, 0)))
+    E(Op("s_exec", (None,)))
     E(Op("s_nop", (4,)))
     for j in range(r):
-        _store_pair(E, acc0 + 8 * j, 26, 24, spec.st_policy)
+        _store_pair(E, acc0 + 8 * j, S_STA, S_STB, spec.st_policy)
     _epilogue_next_item(E)
     return ops
 
@@ -507,7 +537,9 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
     E = ops.append
     _prologue(E, spec)
     # slot maps of both halves' generations
-    for h, (gv, vm) in enumerate(((V_GA, 26), (V_GB, 24))):
+    # (store masks: padding lanes read their generation's map too, so they
+    # store only the accepted repairs' rows, like the payload lanes)
+    for h, (gv, vm) in enumerate(((V_GA, S_STA), (V_GB, S_STB))):
         E(Op("v_movs", (V_ADDR, 20)))
         E(Op("v_movs", (V_ADDR + 1, 21)))
         E(Op("v_mad64_s", (V_ADDR, gv, 19, V_ADDR)))
@@ -559,9 +591,9 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
     E(Op("s_nop", (4,)))
     for j in range(r):
         present(k + j, 0, S_TMP)
-        E(Op("s_and64", (S_TMP, S_TMP, 26)))
+        E(Op("s_and64", (S_TMP, S_TMP, S_STA)))
         present(k + j, 1, S_TMP2)
-        E(Op("s_and64", (S_TMP2, S_TMP2, 24)))
+        E(Op("s_and64", (S_TMP2, S_TMP2, S_STB)))
         _store_pair(E, acc0 + 8 * j, S_TMP, S_TMP2, spec.st_policy)
     _epilogue_next_item(E)
     return ops
@@ -661,25 +693,37 @@ def magic_for(U: int) -> tuple[int, int]:
     return magic, s - 1
 
 
-def launch_geometry(L: int, G: int) -> tuple[int, int, int]:
-    """(Lu, total units, items) of a batch: 16-byte units, 128 per item."""
+def padded_units(L: int) -> int:
+    """Lane units per row that align items to 128-B lines: ceil(L/16) rounded up to 8."""
+    return (L // 16 + 7) // 8 * 8
+
+
+def launch_geometry(L: int, G: int, Lv: Optional[int] = None) -> tuple[int, int, int]:
+    """(Lv, total units, items) of a batch: 16-byte units, 128 per item, Lv
+    lane units per row (default L/16)."""
     if L % 16 or L < 32:
         raise ValueError("bit-sliced kernels need L % 16 == 0 and L >= 32")
     Lu = L // 16
-    total = G * Lu
+    Lv = Lu if Lv is None else Lv
+    if Lv < Lu:
+        raise ValueError("Lv < L/16")
+    total = G * Lv
     if total >= 1 << 31:
         raise ValueError("too many units for one launch")
-    return Lu, total, (total + 127) // 128
+    return Lv, total, (total + 127) // 128
 
 
 def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
-             total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0) -> bytes:
+             total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
+             Lv: Optional[int] = None, zero_tail: bool = False) -> bytes:
     """80-byte kernarg block (layout above).  Syndrome mode: src = received
-    rows, dst = syndrome rows, plus slot map and zero row."""
-    Lu, total, n_items = launch_geometry(L, G)
-    magic, shift = magic_for(Lu)
-    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, L, Lu, total,
-             magic, shift, n_items, total_waves, map_stride, smap & MASK32, smap >> 32,
+    rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
+    also write zeros to bytes [L, 16 Lv) of every repair row."""
+    Lv, total, n_items = launch_geometry(L, G, Lv)
+    magic, shift = magic_for(Lv)
+    s19 = map_stride if smap else (Lv if zero_tail else L // 16)
+    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, L // 16, Lv, total,
+             magic, shift, n_items, total_waves, s19, smap & MASK32, smap >> 32,
              zero & MASK32, zero >> 32]
     for w in words:
         assert 0 <= w < 1 << 32, words
@@ -881,6 +925,8 @@ class Emulator:
                 exec_ = np.ones(64, bool) if a[0] is None else smask(a[0])
             elif n == "s_and64":
                 set_smask(a[0], smask(a[1]) & smask(a[2]))
+            elif n == "s_andn2_64":
+                set_smask(a[0], smask(a[1]) & ~smask(a[2]))
             elif n == "s_mov":
                 s[a[0]] = s[a[1]]
             elif n == "s_movk":

@@ -219,7 +219,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
                 uint8_t* rep, const uint8_t* coeff, hipStream_t st) {
     const uint32_t k = sh->k, r = sh->r, L = sh->L;
-    if (k == 0 || k > 256) return QF_EINVAL;
+    if (k == 0 || k > 256 || (sh->flags & ~QF_ENCODE_ZERO_TAIL)) return QF_EINVAL;
     if (G == 0 || r == 0 || L == 0) return QF_OK;
     if (!src || !rep) return QF_EINVAL;
     if (!aligned16(src) || !aligned16(rep) || (sh->src_row_stride & 15) || (sh->src_gen_stride & 15) ||
@@ -244,9 +244,13 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
         sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
         (uint64_t)G * (L / 16) < (1ull << 31)) {
+        const bool zero_tail = (sh->flags & QF_ENCODE_ZERO_TAIL) &&
+                               qf::bs_zero_tail_fits(r, L, sh->rep_row_stride, sh->rep_gen_stride) &&
+                               (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31);
         hipEvent_t ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
-                                   sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G));
+                                   sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G,
+                                   zero_tail));
         prof_end(ctx, st, ev, qf::bs_name(k, r));
         return QF_OK;
     }
@@ -345,7 +349,10 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     const char* ov = getenv("QF_DECODE_OVERLAP");
     const uint64_t n_chunks = (G + chunk - 1) / chunk;
     const bool overlap = n_chunks > 1 && !(ov && atoi(ov) == 0);
-    const size_t syn_bytes = round_up((size_t)chunk * r * L, 256);
+    // syndrome rows: the padded lane space of the syndrome kernel (whole
+    // 128-B lines per row; qf_bs.h)
+    const uint64_t syn_rs = 16ull * qf::bs_padded_units(L);
+    const size_t syn_bytes = round_up((size_t)chunk * r * syn_rs, 256);
     const size_t off_bound = round_up((size_t)G * coef_gen_stride, 256);
     const size_t off_map = round_up(off_bound + (size_t)G * 4, 256);
     const size_t off_syn = round_up(off_map + (size_t)G * ms, 256);
@@ -405,7 +412,7 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         if (overlap && c >= 2) QF_CHECK_HIP(hipStreamWaitEvent(st, ctx->dep[2 * (c - 2) + 1], 0));
         ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows + g0 * sh->rows_gen_stride, syn,
-                                    sh->rows_gen_stride, (uint64_t)r * L, sh->row_stride, L, L, Gc,
+                                    sh->rows_gen_stride, (uint64_t)r * syn_rs, sh->row_stride, syn_rs, L, Gc,
                                     w + off_map + g0 * ms, ms, ctx->d_zero));
         prof_end(ctx, st, ev, qf::syn_name(k, r));
         if (overlap) {
@@ -414,8 +421,8 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         }
         qf::CombineSlotsArgs a{};
         a.rows = syn;
-        a.rows_gen_stride = (uint64_t)r * L;
-        a.row_stride = L;
+        a.rows_gen_stride = (uint64_t)r * syn_rs;
+        a.row_stride = syn_rs;
         a.dst = rec + g0 * sh->rec_gen_stride;
         a.dst_gen_stride = sh->rec_gen_stride;
         a.dst_row_stride = sh->rec_row_stride;
@@ -720,8 +727,8 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     const char* nobs = getenv("QF_DISABLE_BS");
     if (!row_coeffs && !(nobs && atoi(nobs)) && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
         max_rows <= 255 && L % 16 == 0 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
-        sh->row_stride < (1ull << 32) && (uint64_t)G * (L / 16) < (1ull << 31) &&
-        (uint64_t)r * L < (1ull << 32))
+        sh->row_stride < (1ull << 32) && (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31) &&
+        (uint64_t)r * 16 * qf::bs_padded_units(L) < (1ull << 32))
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
     const uint32_t passes = (e_max + 15) / 16;
     const uint64_t coef_gen_stride = ((uint64_t)max_rows + 1) * 16;

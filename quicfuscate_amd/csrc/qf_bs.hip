@@ -59,10 +59,12 @@ static void magic_for(uint32_t U, uint32_t* magic, uint32_t* shift) {
 // Shared launch: kernarg words as bs_codegen.kernargs (80 bytes).  Items of
 // 128 16-byte units, one wave per item (non-persistent grid: staggered wave
 // start-up overlaps one wave's loads with another's XOR work).
+// Lv: lane units per row (>= L/16); s19: enc = units stored per row, syn =
+// slot-map stride (bs_codegen.py kernarg layout).
 static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStream_t st,
                          const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
-                         uint64_t drs, uint32_t L, uint32_t G, const uint8_t* smap,
-                         uint32_t map_stride, const uint8_t* zero) {
+                         uint64_t drs, uint32_t L, uint32_t G, uint32_t Lv, uint32_t s19,
+                         const uint8_t* smap, const uint8_t* zero) {
     (void)num_cus;
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
@@ -77,10 +79,11 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
         if (err != hipSuccess) return err;
     }
     const uint32_t Lu = L / 16;
-    const uint64_t total = (uint64_t)G * Lu;
+    if (Lv < Lu) return hipErrorInvalidValue;
+    const uint64_t total = (uint64_t)G * Lv;
     if (total >= (1ull << 31)) return hipErrorInvalidValue;
     uint32_t magic, shift;
-    magic_for(Lu, &magic, &shift);
+    magic_for(Lv, &magic, &shift);
     const uint32_t n_items = (uint32_t)((total + 127) / 128);
     const uint32_t blocks = (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
@@ -93,14 +96,14 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[5] = (uint32_t)dgs;
     a[6] = (uint32_t)srs;
     a[7] = (uint32_t)drs;
-    a[8] = L;
-    a[9] = Lu;
+    a[8] = Lu;
+    a[9] = Lv;
     a[10] = (uint32_t)total;
     a[11] = magic;
     a[12] = shift;
     a[13] = n_items;
     a[14] = blocks * 4;
-    a[15] = map_stride;
+    a[15] = s19;
     a[16] = (uint32_t)(uintptr_t)smap;
     a[17] = (uint32_t)((uintptr_t)smap >> 32);
     a[18] = (uint32_t)(uintptr_t)zero;
@@ -111,10 +114,24 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
+uint32_t bs_padded_units(uint32_t L) { return (L / 16 + 7) / 8 * 8; }
+
+bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs) {
+    const uint64_t row = 16ull * bs_padded_units(L);
+    return (r == 1 || drs >= row) && dgs >= (uint64_t)(r - 1) * drs + row;
+}
+
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
-                     uint64_t drs, uint32_t L, uint32_t G) {
-    return launch(cache, find('e', k, r), num_cus, st, src, dst, sgs, dgs, srs, drs, L, G, nullptr, 0,
+                     uint64_t drs, uint32_t L, uint32_t G, bool zero_tail) {
+    // zero tail: lane space padded to whole 128-B lines per row and the tail
+    // [L, 16 Lv) of every repair row written with zeros, so every line the
+    // kernel stores is whole (tools/bs_lab.py: partial lines shared by two
+    // waves cut the write rate from ~5.7 to ~4 TB/s at L = 1200)
+    const uint32_t Lu = L / 16;
+    const uint32_t Lv = zero_tail ? bs_padded_units(L) : Lu;
+    if (zero_tail && !bs_zero_tail_fits(r, L, drs, dgs)) return hipErrorInvalidValue;
+    return launch(cache, find('e', k, r), num_cus, st, src, dst, sgs, dgs, srs, drs, L, G, Lv, Lv, nullptr,
                   nullptr);
 }
 
@@ -124,7 +141,11 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       const uint8_t* zero) {
     const QfBsEntry* e = find('s', k, r);
     if (!e || map_stride != e->map_stride || !zero) return hipErrorInvalidValue;
-    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, smap, map_stride, zero);
+    // syndrome rows live in the library's workspace: always the padded lane
+    // space (srs >= 16 * bs_padded_units(L); the tail holds junk)
+    const uint32_t Lv = bs_padded_units(L);
+    if (srs < 16ull * Lv) return hipErrorInvalidValue;
+    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, Lv, map_stride, smap, zero);
 }
 
 void bs_unload(BsCache& cache) {

@@ -151,10 +151,14 @@ def gf_mul_slice(a: bytes, b: bytes, ctx: Optional[Context] = None) -> bytes:
 # ---------------------------------------------------------------------------
 def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_gen_stride: int,
                  rep_row_stride: int, rep_gen_stride: int, G: int,
-                 coeff: Optional[bytes] = None, ctx: Optional[Context] = None) -> None:
-    """qf_encode_batch: repairs of G generations (decoder.rs:172-275)."""
+                 coeff: Optional[bytes] = None, ctx: Optional[Context] = None,
+                 zero_tail: bool = False) -> None:
+    """qf_encode_batch: repairs of G generations (decoder.rs:172-275).
+    zero_tail: QF_ENCODE_ZERO_TAIL (the library may zero [L, round_up(L, 128))
+    of each repair row)."""
     ctx = ctx or default_context()
-    sh = L.EncodeShape(k, r, Lb, 0, src_row_stride, src_gen_stride, rep_row_stride, rep_gen_stride)
+    sh = L.EncodeShape(k, r, Lb, 1 if zero_tail else 0, src_row_stride, src_gen_stride, rep_row_stride,
+                       rep_gen_stride)
     cbuf = None
     if coeff is not None:
         if len(coeff) != k * r:

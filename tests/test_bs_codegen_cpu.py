@@ -43,6 +43,47 @@ def test_emulated_kernel_matches_oracle(oracle, k, r, pd, L, G, waves):
             assert (dst[off + L: off + drs] == 0xEE).all()
 
 
+@pytest.mark.parametrize("k,r,L,G,zero_tail", [
+    (8, 4, 80, 7, True),      # L = 5 units -> Lv = 8: three padding lanes per row
+    (8, 4, 1200, 3, True),    # the benchmark row length: Lv = 80
+    (5, 3, 96, 9, False),     # padded lane space without tail writes
+    (64, 16, 1200, 2, True),
+])
+def test_emulated_kernel_padded_lanes(oracle, k, r, L, G, zero_tail):
+    """Lane space of Lv = round_up(L/16, 8) units per row: padding lanes load
+    nothing; with zero_tail they write zeros to [L, 16 Lv) of every repair
+    row, and never past it."""
+    spec = bs.KernelSpec(k, r, 3)
+    ops = bs.generate(spec)
+    Lv = bs.padded_units(L)
+    rng = np.random.default_rng(k + 3 * L + G)
+    srs = L + 16 * (k % 2)
+    sgs = k * srs
+    drs = 16 * Lv + 128
+    dgs = r * drs
+    src = rng.integers(0, 256, G * sgs, dtype=np.uint8)
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    emu = bs.Emulator(ops)
+    SRC, DST = 0x10000000, 0x40000000
+    emu.add_buffer(SRC, src)
+    emu.add_buffer(DST, dst)
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    waves = (items + 3) // 4
+    ka = bs.kernargs(SRC, DST, sgs, dgs, srs, drs, L, G, waves * 4, Lv=Lv, zero_tail=zero_tail)
+    for wg in range(waves):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, r)
+        for j in range(r):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            tail = dst[off + L: off + 16 * Lv]
+            assert (tail == (0 if zero_tail else 0xEE)).all(), (g, j)
+            assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
+
+
 def test_emulator_catches_missing_wait():
     spec = bs.KernelSpec(4, 2, 2)
     ops = [op for op in bs.generate(spec) if not (op.name == "s_waitcnt_vm" and op.args[0] == 2)]
@@ -87,7 +128,8 @@ def _gf_matvec(D, rows):
     (16, 16, 4, 64, 5, 1),
     (5, 3, 1, 64, 9, 1),
 ])
-def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves):
+@pytest.mark.parametrize("padded", [False, True])
+def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves, padded):
     """Decode stage A on the emulator: syndromes of the accepted repairs, and
     the closed-form Cauchy inverse applied to them gives the erased sources."""
     spec = bs.KernelSpec(k, r, pd, mode="syn")
@@ -96,7 +138,8 @@ def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves):
     rs = L + 16
     n_slots = k + 2
     rgs = n_slots * rs + 16
-    srs = L + 32
+    Lv = bs.padded_units(L) if padded else None
+    srs = (16 * Lv if padded else L) + 32
     sgs = r * srs
     mstride = spec.map_stride
     rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
@@ -125,7 +168,9 @@ def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves):
     emu.add_buffer(SYN, syn)
     emu.add_buffer(MAP, smap)
     emu.add_buffer(ZERO, np.zeros(L, np.uint8))
-    ka = bs.kernargs(ROWS, SYN, rgs, sgs, rs, srs, L, G, waves * 4, smap=MAP, map_stride=mstride, zero=ZERO)
+    ka = bs.kernargs(ROWS, SYN, rgs, sgs, rs, srs, L, G, waves * 4, smap=MAP, map_stride=mstride, zero=ZERO,
+                     Lv=Lv)
+    waves = max(waves, (bs.launch_geometry(L, G, Lv)[2] + 3) // 4)
     for wg in range(waves):
         for w in range(4):
             emu.run_wave(ka, wg, w)
@@ -137,7 +182,7 @@ def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves):
             if j not in J:
                 assert (blk == 0xEE).all(), (g, j)
                 continue
-            assert (blk[L:] == 0xEE).all()
+            assert (blk[(16 * Lv if padded else L):] == 0xEE).all()
             want = rep[j].copy()
             for i in range(k):
                 if i not in E:

@@ -18,7 +18,7 @@ def _r16(x):
     return (x + 15) // 16 * 16
 
 
-def run_encode(qf, src_np, k, r, L, G, rs, gs, rrs, rgs, coeff=None):
+def run_encode(qf, src_np, k, r, L, G, rs, gs, rrs, rgs, coeff=None, zero_tail=False):
     import torch
 
     dev = torch.device("cuda")
@@ -26,7 +26,7 @@ def run_encode(qf, src_np, k, r, L, G, rs, gs, rrs, rgs, coeff=None):
     rep = torch.full((G * rgs + 64,), 0xA5, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     qf.encode_batch(src, rep, k, r, L, src_row_stride=rs, src_gen_stride=gs, rep_row_stride=rrs,
-                    rep_gen_stride=rgs, G=G, coeff=coeff)
+                    rep_gen_stride=rgs, G=G, coeff=coeff, zero_tail=zero_tail)
     qf.default_context().sync()
     return rep.cpu().numpy()
 
@@ -52,6 +52,46 @@ CASES = [
     (16, 16, 80, 13),
     (64, 16, 1216, 11),
 ]
+
+
+ZERO_TAIL_CASES = [
+    # k, r, L, G, repair row stride, repair generation stride
+    (64, 16, 1200, 41, 1280, 16 * 1280),         # the benchmark layout
+    (64, 16, 1200, 9, 1296, 16 * 1296 + 48),     # room beyond the tail: untouched
+    (16, 1, 1200, 17, 1200, 1280),               # r = 1: the tail fits the generation
+    (32, 16, 96, 23, 128, 16 * 128),             # 6 units -> 8: two padding lanes per row
+    (64, 10, 64, 50, 64, 640),                   # 4 units -> 8, no room for the tail: plain path
+    (64, 16, 1200, 5, 1216, 16 * 1216),          # stride too short for the tail: plain path
+    (7, 5, 33, 11, 48, 5 * 48),                  # no bit-sliced kernel: flag ignored
+]
+
+
+@pytest.mark.parametrize("k,r,L,G,rrs,rgs", ZERO_TAIL_CASES)
+def test_encode_zero_tail(qf, oracle, gpu_ctx, k, r, L, G, rrs, rgs):
+    """QF_ENCODE_ZERO_TAIL: repairs bit-exact; bytes [L, round_up(L, 128)) of
+    a row are zero or untouched (zero exactly when the tail fits the layout
+    and a bit-sliced kernel runs); nothing beyond them is written."""
+    rng = np.random.default_rng(k + r + L + G)
+    rs = _r16(L)
+    gs = k * rs
+    src = rng.integers(0, 256, G * gs, dtype=np.uint8)
+    rep = run_encode(qf, src, k, r, L, G, rs, gs, rrs, rgs, zero_tail=True)
+    tail = (L // 16 + 7) // 8 * 128 if L % 16 == 0 else L
+    fits = (r == 1 or rrs >= tail) and rgs >= (r - 1) * rrs + tail
+    bs_shape = (k, r) in {(64, 16), (64, 10), (32, 16), (16, 16), (16, 1)} and L % 16 == 0 and L >= 32
+    if not fits:
+        tail = L
+    for g in range(G):
+        rows = np.stack([src[g * gs + i * rs: g * gs + i * rs + L] for i in range(k)])
+        want = oracle.encode(rows, r)
+        for j in range(r):
+            off = g * rgs + j * rrs
+            assert (rep[off: off + L] == want[j]).all(), (g, j)
+            t = rep[off + L: off + tail]
+            assert (t == (0 if fits and bs_shape else 0xA5)).all(), (g, j)
+            if j + 1 < r:
+                assert (rep[off + tail: off + rrs] == 0xA5).all()
+        assert (rep[g * rgs + (r - 1) * rrs + tail: (g + 1) * rgs] == 0xA5).all()
 
 
 @pytest.mark.parametrize("k,r,L,G", CASES)

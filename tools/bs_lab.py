@@ -22,7 +22,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 OUT = REPO / "tools" / "lab_build"
 
-VALU = {"v_xor", "v_andk", "v_lshl", "v_lshr", "v_mov", "v_movk"}
+VALU = {"v_xor", "v_andk", "v_lshl", "v_lshr", "v_mov", "v_movk", "v_xor3", "v_bitsel_s"}
 
 
 def variant_ops(bs, spec, flags):
@@ -36,7 +36,7 @@ def variant_ops(bs, spec, flags):
                 continue
             if "nostore" in flags and op.name == "store16":
                 continue
-            if "nocoeff" in flags and op.name in ("v_xor", "v_mov", "v_movk") and acc_lo <= op.args[0] < acc_hi:
+            if "nocoeff" in flags and op.name in ("v_xor", "v_xor3", "v_mov", "v_movk") and acc_lo <= op.args[0] < acc_hi:
                 continue
             if "nocompute" in flags and op.name in VALU:
                 continue
@@ -48,14 +48,20 @@ ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
     # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3 xor;
     # "nobfi" = classic 6-op delta swaps; "noremap" = no XCD-aware item order;
-    # "ld:/st:<bits>" cache policy; "L:<n>" payload bytes)
+    # "ld:/st:<bits>" cache policy; "L:<n>" payload bytes; "dst:wide" 2048-B
+    # repair rows; "ztail" padded lane space + zero tail, 128-B repair rows;
+    # "nocompute" drops every VALU op of the body (incl. v_bitop3))
     ("warm", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("remap", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("noremap", 64, 16, 3, ("ld:nt", "st:nt", "noremap"), ALL),
-    ("remap_b", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
-    ("noremap_b", 64, 16, 3, ("ld:nt", "st:nt", "noremap"), ALL),
-    ("mem_remap", 64, 16, 3, ("nocompute", "ld:nt", "st:nt"), ALL),
-    ("mem_noremap", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "noremap"), ALL),
+    ("full", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("full_ztail", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
+    ("mem_ztail", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "ztail"), ALL),
+    ("writeonly_ztail", 64, 16, 3, ("nocompute", "noload", "ld:nt", "st:nt", "ztail"), ALL),
+    ("full_ztail_pd2", 64, 16, 2, ("ld:nt", "st:nt", "ztail"), ALL),
+    ("full_ztail_pd4", 64, 16, 4, ("ld:nt", "st:nt", "ztail"), ALL),
+    ("full_ztail_stdef", 64, 16, 3, ("ld:nt", "ztail"), ALL),
+    ("full_ztail_noremap", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "noremap"), ALL),
+    ("full_2", 64, 16, 3, ("ld:nt", "st:nt"), ALL),
+    ("full_ztail_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
 ]
 
 
@@ -102,11 +108,13 @@ def run(G: int, reps: int):
         buf = ctypes.create_string_buffer(data, len(data))
         assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
-        _, _, n_items = bs.launch_geometry(L, G)
+        zt = "ztail" in m["flags"]
+        Lv = bs.padded_units(L) if zt else None
+        _, _, n_items = bs.launch_geometry(L, G, Lv)
         blocks = min((n_items + 3) // 4, ncu * m["blocks_per_cu"])
         wide = "dst:wide" in m["flags"]
-        drs, dgs = (2048, 32768) if wide else (L, r * L)
-        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * L, dgs, L, drs, L, G, blocks * 4)
+        drs, dgs = (2048, 32768) if wide else ((16 * Lv, 16 * Lv * r) if zt else (L, r * L))
+        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * L, dgs, L, drs, L, G, blocks * 4, Lv=Lv, zero_tail=zt)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
