@@ -147,10 +147,24 @@ _ASM = {
     "s_min": lambda d, a, b: f"s_min_u32 s{d}, s{a}, s{b}",
     "s_cmp_ge_br": lambda a, b, lbl: f"s_cmp_ge_u32 s{a}, s{b}\n\ts_cbranch_scc1 {lbl}",
     "s_branch": lambda lbl: f"s_branch {lbl}",
+    "s_cmp_lt_br": lambda a, b, lbl: f"s_cmp_lt_u32 s{a}, s{b}\n\ts_cbranch_scc1 {lbl}",
+    # branch beyond the +-128 KiB of s_branch (the dec kernel is ~200 KiB):
+    # pc-relative 64-bit jump through s[66:67]
+    "s_far_jump": lambda lbl, n: (f"s_getpc_b64 s[66:67]\n.Lfar{n}:\n\ts_add_u32 s66, s66, ({lbl}-.Lfar{n})&4294967295"
+                                  f"\n\ts_addc_u32 s67, s67, ({lbl}-.Lfar{n})>>32\n\ts_setpc_b64 s[66:67]"),
     "s_waitcnt_vm": lambda n: f"s_waitcnt vmcnt({n})",
     "s_waitcnt_lgkm": lambda: "s_waitcnt lgkmcnt(0)",
     "s_nop": lambda n: f"s_nop {n}",
     "s_load_args": lambda: "s_load_dwordx16 s[4:19], s[0:1], 0x0\n\ts_load_dwordx4 s[20:23], s[0:1], 0x40",
+    "s_load_args_dec": lambda: "s_load_dwordx8 s[56:63], s[0:1], 0x50",
+    "v_perm": lambda d, hi, lo, sel: f"v_perm_b32 {V(d)}, {V(hi)}, {V(lo)}, {V(sel)}",
+    "ds_read_b128": lambda d, a, off: f"ds_read_b128 {VQ(d)}, {V(a)}" + (f" offset:{off}" if off else ""),
+    "ds_read_b32": lambda d, a, off: f"ds_read_b32 {V(d)}, {V(a)}" + (f" offset:{off}" if off else ""),
+    "ds_write_b128": lambda a, d, off: f"ds_write_b128 {V(a)}, {VQ(d)}" + (f" offset:{off}" if off else ""),
+    "s_waitcnt_lgkm_n": lambda n: f"s_waitcnt lgkmcnt({n})",
+    "s_cmp_le_k_br": lambda s, kk, lbl: f"s_cmp_le_u32 s{s}, {kk}\n\ts_cbranch_scc1 {lbl}",
+    "s_or64": lambda d, a, b: f"s_or_b64 {SP(d)}, {SP(a)}, {SP(b)}",
+    "s_cmp_lg64_br": lambda s, lbl: f"s_cmp_lg_u64 {SP(s)}, 0\n\ts_cbranch_scc1 {lbl}",
     "s_endpgm": lambda: "s_endpgm",
 }
 
@@ -194,6 +208,38 @@ V_ZA, V_ZB, V_ADDR, V_SLOT = 40, 42, 44, 46      # syn only
 SGPR_NEXT_FREE = 54
 S_TMP, S_TMP2 = 38, 40
 S_STA, S_STB, S_PAD = 48, 50, 52   # store masks of halves A / B, mask temp
+
+# dec mode (fused decode: syndromes + in-register LU solve, see _generate_syn):
+# extra kernarg dwords 20..27 at 0x50 -> s[56:63]:
+#   s[56:57] LU records   s58 LU record stride   s59 unused
+#   s[60:61] split tables (256 x 32 B, gf256_tables.h perm_record)
+#   s[62:63] {4096, 0} after the table copy (address constant)
+# s64 jmax: 1 + the largest repair index any lane of the item has accepted.
+KERNARG_BYTES_DEC = 112
+SGPR_NEXT_FREE_DEC = 68      # s[66:67]: far-jump target
+S_JMAX = 64
+LDS_TAB_BYTES = 8192
+LU_REC_BYTES = 272          # 16 columns x 16 B, then 16 rank bytes
+# LU-phase VGPRs (regions free once the row loop is done; dec mode with
+# r = 16: acc blocks v80..v207, slot maps v208..v247 are dead by then)
+R_P = 14                    # 3 product temps (v14..v16)
+R_SEL = 18                  # selectors s0[4], s1[4], s2[4] (v18..v29)
+R_TB = (30, 36)             # table buffers T0lo T0hi T1lo T1hi T2 (v30..34, v36..40)
+R_TA = (41, 42)             # their LDS addresses
+R_FP = 44                   # LU record pointer (2)
+
+
+def lu_layout(spec) -> tuple[list[int], tuple[int, int]]:
+    """4-register slots of the LU phase in the ring and the slot maps (both
+    dead after the row loop): the r columns of one half's record and the two
+    halves' rank records.  Store addresses reuse the column slots."""
+    slots = [spec.ring0 + 4 * q for q in range(2 * spec.nbuf)]
+    slots += [spec.map_a + 4 * q for q in range(2 * spec.map_quads)]
+    end = spec.map_b + 4 * spec.map_quads
+    while len(slots) < spec.r + 2:     # small pd / k: extra registers past the maps
+        slots.append(end)
+        end += 4
+    return slots[2: 2 + spec.r], (slots[0], slots[1])
 S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
@@ -216,10 +262,15 @@ class KernelSpec:
     # workgroup w processes items of a contiguous range per XCD (blocks go to
     # XCD w % 8), so lines shared by neighbouring items meet in one L2
     xcd_remap: bool = True
+    # dec mode: accumulator blocks j >= guard_min are skipped when no lane of
+    # the item has accepted repair j (j >= jmax)
+    guard_min: int = 4
+    # dec mode: solve in registers (False: store the syndromes unsolved; lab only)
+    lu: bool = True
 
     @property
     def name(self) -> str:
-        tag = "bs" if self.mode == "enc" else "syn"
+        tag = {"enc": "bs", "syn": "syn", "dec": "dec"}[self.mode]
         return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
 
     @property
@@ -236,7 +287,7 @@ class KernelSpec:
 
     @property
     def map_quads(self) -> int:
-        return (self.k + self.r + 15) // 16 if self.mode == "syn" else 0
+        return (self.k + self.r + 15) // 16 if self.mode != "enc" else 0
 
     @property
     def map_a(self) -> int:
@@ -254,6 +305,8 @@ class KernelSpec:
     @property
     def next_free_vgpr(self) -> int:
         n = self.map_b + 4 * self.map_quads
+        if self.mode == "dec":
+            n = max(n, max(lu_layout(self)[0]) + 4)
         n = (n + 7) // 8 * 8
         if n > 256:
             raise ValueError(f"{self.name}: {n} VGPRs > 256 (lower pd)")
@@ -261,7 +314,15 @@ class KernelSpec:
 
     @property
     def next_free_sgpr(self) -> int:
-        return SGPR_NEXT_FREE
+        return SGPR_NEXT_FREE_DEC if self.mode == "dec" else SGPR_NEXT_FREE
+
+    @property
+    def kernarg_bytes(self) -> int:
+        return KERNARG_BYTES_DEC if self.mode == "dec" else KERNARG_BYTES
+
+    @property
+    def lds_bytes(self) -> int:
+        return LDS_TAB_BYTES if self.mode == "dec" else 0
 
 
 _TRANSPOSE = [(4, 0x0F0F0F0F, [(0, 4), (1, 5), (2, 6), (3, 7)]),
@@ -366,9 +427,11 @@ def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict,
 
 
 def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool, xor3: bool = False,
-                bfi: bool = False):
+                bfi: bool = False, guard: Optional[tuple[int, str]] = None):
     """Transpose one source row (ring buffer at `base`) and accumulate it into
-    all r repair accumulators with the Cauchy coefficients of column i."""
+    all r repair accumulators with the Cauchy coefficients of column i.
+    guard = (j0, label): blocks j >= j0 are skipped (jump to label) once
+    j >= jmax (dec mode)."""
     ops.extend(_transpose_ops(base, bfi))
     lo, hi = _combo_regs(base)
     rows = [mul_matrix_rows(C[j][i]) for j in range(r)]
@@ -376,7 +439,11 @@ def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bo
     need_hi = {rb >> 4 for rr in rows for rb in rr} - {0}
     ops.extend(_combo_ops(lo, hi, need_lo, need_hi))
     for j in range(r):
+        if guard is not None and j >= guard[0]:
+            ops.append(Op("s_cmp_le_k_br", (S_JMAX, j, guard[1])))
         _coeff_block(ops, rows[j], acc0 + 8 * j, lo, hi, init, xor3)
+    if guard is not None and guard[0] < r:
+        ops.append(Op("label", (guard[1],)))
 
 
 def _prologue(E, spec: KernelSpec):
@@ -385,8 +452,26 @@ def _prologue(E, spec: KernelSpec):
     E(Op("v_lshr", (V_T, 6, V_LANE)))
     E(Op("v_andk", (V_LANE, 63, V_LANE)))
     E(Op("v_readfirstlane", (29, V_T)))
+    if spec.mode == "dec":
+        E(Op("s_load_args_dec", ()))
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
+    if spec.mode == "dec":
+        # every wave copies the whole 8 KB split-table set into LDS (no
+        # barrier: waves of a workgroup write identical bytes)
+        E(Op("s_movk", (62, 4096)))
+        E(Op("s_movk", (63, 0)))
+        E(Op("v_movs", (V_ADDR, 60)))
+        E(Op("v_movs", (V_ADDR + 1, 61)))
+        E(Op("v_mad64_k", (V_ADDR, V_LANE, 16, V_ADDR)))
+        E(Op("v_add64_s", (V_SRCA, V_ADDR, 62)))
+        for q in range(8):
+            E(Op("load16", (48 + 4 * q, V_ADDR if q < 4 else V_SRCA, 1024 * (q % 4))))
+        E(Op("v_lshl", (V_T, 4, V_LANE)))
+        E(Op("s_waitcnt_vm", (0,)))
+        for q in range(8):
+            E(Op("ds_write_b128", (V_T, 48 + 4 * q, 1024 * q)))
+        E(Op("s_waitcnt_lgkm_n", (0,)))
     if spec.xcd_remap:
         # w' = base(w % 8) + w / 8 with XCD x owning c_x = q + (x < rem)
         # consecutive workgroups, q = nwg / 8, rem = nwg % 8 (a bijection)
@@ -411,7 +496,12 @@ def _prologue(E, spec: KernelSpec):
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (S_TMASK + q, mask)))
     E(Op("label", (".Litem",)))
-    E(Op("s_cmp_ge_br", (28, 17, ".Lend")))
+    if spec.mode == "dec":
+        E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
+        E(Op("s_far_jump", (".Lend", 0)))
+        E(Op("label", (".Lgo",)))
+    else:
+        E(Op("s_cmp_ge_br", (28, 17, ".Lend")))
     # unit A = item*128 + lane, unit B = A + 64; valid = unit < total
     for h, (gv, uv, sv, dv, vm, sm) in enumerate(((V_GA, V_UA, V_SRCA, V_DSTA, 26, S_STA),
                                                   (V_GB, V_UB, V_SRCB, V_DSTB, 24, S_STB))):
@@ -431,7 +521,8 @@ def _prologue(E, spec: KernelSpec):
         if spec.mode == "enc":
             E(Op("v_cmp_gt_s", (S_TMP, 19, uv)))
         E(Op("s_nop", (4,)))
-        E(Op("s_and64", (sm, vm, S_TMP if spec.mode == "enc" else vm)))
+        # (dec: the recovered rows are caller memory -> payload lanes only)
+        E(Op("s_and64", (sm, vm, {"enc": S_TMP, "syn": vm, "dec": S_PAD}[spec.mode])))
         E(Op("s_and64", (vm, vm, S_PAD)))
         # src/dst + g * gen_stride + 16 u   (VOP3 reads at most one SGPR)
         for ptr, base_s, gs_s in ((sv, 4, 8), (dv, 6, 9)):
@@ -439,7 +530,7 @@ def _prologue(E, spec: KernelSpec):
             E(Op("v_movs", (ptr + 1, base_s + 1)))
             E(Op("v_mad64_s", (ptr, gv, gs_s, ptr)))
             E(Op("v_mad64_k", (ptr, uv, 16, ptr)))
-        if spec.mode == "syn":
+        if spec.mode != "enc":
             z = V_ZA if h == 0 else V_ZB
             E(Op("v_movs", (z, 22)))
             E(Op("v_movs", (z + 1, 23)))
@@ -448,16 +539,18 @@ def _prologue(E, spec: KernelSpec):
     E(Op("label", (".Lbody",)))  # marks the end of the per-item setup (tools/bs_lab.py)
 
 
-def _epilogue_next_item(E):
+def _epilogue_next_item(E, far: bool = False):
     E(Op("s_nop", (4,)))  # store data/address VGPRs are rewritten by the next item
     E(Op("s_add", (28, 28, 18)))
-    E(Op("s_branch", (".Litem",)))
+    E(Op("s_far_jump", (".Litem", 1)) if far else Op("s_branch", (".Litem",)))
     E(Op("label", (".Lend",)))
     E(Op("s_endpgm", ()))
 
 
 def generate(spec: KernelSpec) -> list[Op]:
-    return _generate_enc(spec) if spec.mode == "enc" else _generate_syn(spec)
+    if spec.mode == "enc":
+        return _generate_enc(spec)
+    return _generate_syn(spec)
 
 
 def _store_pair(E, acc: int, ma: int, mb: int, pol: str = ""):
@@ -518,6 +611,153 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     return ops
 
 
+def _jmax(E, k: int, r: int, present):
+    """s[S_JMAX] <- 1 + the largest repair index accepted by any lane (both
+    halves, payload lanes), 0 if none."""
+    for j in reversed(range(r)):
+        present(k + j, 0, S_TMP)
+        E(Op("s_and64", (S_TMP, S_TMP, S_STA)))
+        present(k + j, 1, S_TMP2)
+        E(Op("s_and64", (S_TMP2, S_TMP2, S_STB)))
+        E(Op("s_or64", (S_TMP, S_TMP, S_TMP2)))
+        E(Op("s_movk", (S_JMAX, j + 1)))
+        E(Op("s_cmp_lg64_br", (S_TMP, ".Ljdone")))
+    E(Op("s_movk", (S_JMAX, 0)))
+    E(Op("label", (".Ljdone",)))
+
+
+def _lu_solve_and_store(E, spec: KernelSpec):
+    """Decode stage B in registers: per half, solve C[J, E] x = s in place on
+    the syndrome blocks by the packed LU record of the half's generation
+    (written by k_decode_prepare_cauchy with lu_out), then store block t to
+    recovered row rank[t] of its generation.
+
+    Blocks are the repair indices t < r; the record embeds the e x e LU of
+    C[J, E] (J accepted repairs ascending, E erased sources ascending) into
+    a 16 x 16 byte matrix, column u at byte 16u: byte t < u = U[t][u],
+    byte u = 1 / U[u][u], byte t > u = L[t][u] (0 where t or u is not
+    accepted), then rank[t] at byte 256 + t (0xFF: not accepted).
+    Multiplication by a per-lane coefficient c uses the split tables of
+    gf256_tables.h from LDS: c * x = T0[x & 7] ^ T1[x >> 3 & 7] ^ T2[x >> 6]
+    with v_perm_b32 (four byte lookups per instruction).  The 17 record
+    loads of a half are issued together; table reads run one coefficient
+    ahead of the v_perm work (two table buffers)."""
+    r, acc0 = spec.r, spec.acc0
+    masks = (S_STA, S_STB)
+    gvs = (V_GA, V_GB)
+    R_COLS, R_RANK = lu_layout(spec)
+    lu = spec.lu
+    # store address pairs in the (then dead) column slots
+    st_addr = [c + 2 * q for c in R_COLS for q in range(2)]
+
+    def blk(t, h, d):
+        return acc0 + 8 * t + 4 * h + d
+
+    def col(u):
+        return R_COLS[u]
+
+    def selectors(u, h):
+        for d in range(4):
+            x = blk(u, h, d)
+            E(Op("v_andk", (R_SEL + d, 0x07070707, x)))
+            E(Op("v_lshr", (R_SEL + 4 + d, 3, x)))
+            E(Op("v_andk", (R_SEL + 4 + d, 0x07070707, R_SEL + 4 + d)))
+            E(Op("v_lshr", (R_SEL + 8 + d, 6, x)))
+            E(Op("v_andk", (R_SEL + 8 + d, 0x03030303, R_SEL + 8 + d)))
+
+    def table_read(u, byte, buf):
+        a, tb = R_TA[buf], R_TB[buf]
+        E(Op("v_bfe", (a, col(u) + byte // 4, 8 * (byte % 4), 8)))
+        E(Op("v_lshl", (a, 5, a)))
+        E(Op("ds_read_b128", (tb, a, 0)))
+        E(Op("ds_read_b32", (tb + 4, a, 16)))
+
+    def products(d, buf):
+        tb = R_TB[buf]
+        E(Op("v_perm", (R_P, tb + 1, tb, R_SEL + d)))
+        E(Op("v_perm", (R_P + 1, tb + 3, tb + 2, R_SEL + 4 + d)))
+        E(Op("v_perm", (R_P + 2, tb + 4, tb + 4, R_SEL + 8 + d)))
+
+    def mul_acc(t, h, buf):
+        for d in range(4):
+            products(d, buf)
+            E(Op("v_xor3", (blk(t, h, d), blk(t, h, d), R_P, R_P + 1)))
+            E(Op("v_xor", (blk(t, h, d), blk(t, h, d), R_P + 2)))
+
+    def scale(u, h, buf):
+        for d in range(4):
+            products(d, buf)
+            E(Op("v_xor3", (blk(u, h, d), R_P, R_P + 1, R_P + 2)))
+
+    def column(u, h, steps, end_label, guard_from):
+        """steps: [(kind, t)] with kind "acc" (block t ^= c_t x_u) or "scale"
+        (block u = c_u y_u, then the selectors of x_u); c_t = byte t of
+        column u.  Steps at index >= guard_from stop the column (jump to
+        end_label) once t >= jmax."""
+        table_read(u, steps[0][1], 0)
+        for n, (kind, t) in enumerate(steps):
+            buf = n % 2
+            if n + 1 < len(steps):
+                table_read(u, steps[n + 1][1], 1 - buf)
+                E(Op("s_waitcnt_lgkm_n", (2,)))
+            else:
+                E(Op("s_waitcnt_lgkm_n", (0,)))
+            if kind == "acc":
+                mul_acc(t, h, buf)
+            else:
+                scale(u, h, buf)
+                selectors(u, h)
+            if n + 1 < len(steps) and n + 1 >= guard_from:
+                E(Op("s_cmp_le_k_br", (S_JMAX, steps[n + 1][1], end_label)))
+        E(Op("label", (end_label,)))
+        E(Op("s_waitcnt_lgkm_n", (0,)))
+
+    for h in range(2):
+        E(Op("v_movs", (R_FP, 56)))
+        E(Op("v_movs", (R_FP + 1, 57)))
+        E(Op("v_mad64_s", (R_FP, gvs[h], 58, R_FP)))
+        E(Op("s_exec", (masks[h],)))
+        for u in range(r if lu else 0):
+            E(Op("load16", (col(u), R_FP, 16 * u)))
+        E(Op("load16", (R_RANK[h], R_FP, 256)))
+        E(Op("s_exec", (None,)))
+        if not lu:
+            E(Op("s_waitcnt_vm", (0,)))
+            continue
+        # forward substitution with unit-lower L, column by column
+        for u in range(r - 1):
+            E(Op("s_cmp_le_k_br", (S_JMAX, u + 1, f".Lfwd_end{h}")))
+            E(Op("s_waitcnt_vm", (r - u,)))      # column u (and the ones before) landed
+            selectors(u, h)
+            column(u, h, [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}_{h}", 1)
+        E(Op("label", (f".Lfwd_end{h}",)))
+        E(Op("s_waitcnt_vm", (0,)))
+        # backward substitution with U: x_u = y_u / U[u][u], then
+        # y_t ^= U[t][u] x_u for t < u
+        for u in reversed(range(r)):
+            E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lbwd{u}_{h}")))
+            selectors(u, h)
+            column(u, h, [("scale", u)] + [("acc", t) for t in range(u)], f".Lbwd{u}_{h}", r + 1)
+    # stores: block t of half h -> recovered row rank[t] of the half's generation
+    E(Op("s_nop", (4,)))
+    na = 0
+    for t in range(r):
+        E(Op("s_cmp_le_k_br", (S_JMAX, t, ".Lst_end")))
+        for h in range(2):
+            rk = R_RANK[h]
+            a = st_addr[na % len(st_addr)]
+            na += 1
+            E(Op("v_bfe", (V_SLOT, rk + t // 4, 8 * (t % 4), 8)))
+            E(Op("v_cmp_ne_s", (S_TMP, S_ABSENT, V_SLOT)))
+            E(Op("s_nop", (4,)))
+            E(Op("s_and64", (S_TMP, S_TMP, masks[h])))
+            E(Op("v_mad64_s", (a, V_SLOT, 11, V_DSTA if h == 0 else V_DSTB)))
+            E(Op("s_exec", (S_TMP,)))
+            E(Op("store16", (a, blk(t, h, 0), 0, spec.st_policy)))
+            E(Op("s_exec", (None,)))
+    E(Op("label", (".Lst_end",)))
+
+
 def _generate_syn(spec: KernelSpec) -> list[Op]:
     """Decode stage A: syndromes s_j = p_j ^ sum_{i present} C[j][i] x_i of
     every accepted repair j, for the generation of each half-lane.
@@ -571,6 +811,10 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
             E(Op("load16", (b + 4 * h, V_ADDR, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
+    dec = spec.mode == "dec"
+    if dec:
+        _jmax(E, k, r, present)
+    g0 = spec.guard_min
     n_seq = len(seq)
     for n in range(min(pd, n_seq)):
         load_row(n)
@@ -581,13 +825,26 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         E(Op("s_waitcnt_vm", (2 * after,)))
         base = ring0 + 8 * (n % nbuf)
         if kind == "rep":
+            if dec and idx >= g0:
+                E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
             ops.extend(_transpose_ops(base, spec.bfi_transpose))
             for b in range(8):
                 E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
+            if dec and idx >= g0:
+                E(Op("label", (f".Lrep{idx}",)))
         else:
-            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose)
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose,
+                        guard=(g0, f".Lrow{n}") if dec else None)
     for j in range(r):
+        if dec and j >= g0:
+            E(Op("s_cmp_le_k_br", (S_JMAX, j, ".Lfin")))
         ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+    if dec:
+        if g0 < r:
+            E(Op("label", (".Lfin",)))
+        _lu_solve_and_store(E, spec)
+        _epilogue_next_item(E, far=True)
+        return ops
     E(Op("s_nop", (4,)))
     for j in range(r):
         present(k + j, 0, S_TMP)
@@ -610,7 +867,7 @@ def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
         if op.name == "label":
             body.append(s.replace(".L", f".L{name}_"))
         else:
-            body.append("\t" + s.replace(".Litem", f".L{name}_item").replace(".Lend", f".L{name}_end"))
+            body.append("\t" + s.replace(".L", f".L{name}_"))
     nv = spec.next_free_vgpr
     meta_args = [
         ("src", 0, 8, "global_buffer"), ("dst", 8, 8, "global_buffer"),
@@ -624,7 +881,7 @@ def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
         .value_kind:     {kind}""")
     args_yaml.append(f"""      - .name:           params
         .offset:         16
-        .size:           {KERNARG_BYTES - 16}
+        .size:           {spec.kernarg_bytes - 16}
         .value_kind:     by_value""")
     return f"""\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"
 \t.amdhsa_code_object_version 6
@@ -637,9 +894,9 @@ def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
 \t.section\t.rodata,"a",@progbits
 \t.p2align\t6, 0x0
 \t.amdhsa_kernel {name}
-\t\t.amdhsa_group_segment_fixed_size 0
+\t\t.amdhsa_group_segment_fixed_size {spec.lds_bytes}
 \t\t.amdhsa_private_segment_fixed_size 0
-\t\t.amdhsa_kernarg_size {KERNARG_BYTES}
+\t\t.amdhsa_kernarg_size {spec.kernarg_bytes}
 \t\t.amdhsa_user_sgpr_count 2
 \t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1
 \t\t.amdhsa_system_sgpr_workgroup_id_x 1
@@ -660,9 +917,9 @@ def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
 amdhsa.kernels:
   - .args:
 {chr(10).join(args_yaml)}
-    .group_segment_fixed_size: 0
+    .group_segment_fixed_size: {spec.lds_bytes}
     .kernarg_segment_align: 8
-    .kernarg_segment_size: {KERNARG_BYTES}
+    .kernarg_segment_size: {spec.kernarg_bytes}
     .max_flat_workgroup_size: 256
     .name:           {name}
     .private_segment_fixed_size: 0
@@ -715,19 +972,73 @@ def launch_geometry(L: int, G: int, Lv: Optional[int] = None) -> tuple[int, int,
 
 def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
              total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
-             Lv: Optional[int] = None, zero_tail: bool = False) -> bytes:
+             Lv: Optional[int] = None, zero_tail: bool = False, lu: Optional[tuple[int, int]] = None,
+             tables: int = 0) -> bytes:
     """80-byte kernarg block (layout above).  Syndrome mode: src = received
     rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
-    also write zeros to bytes [L, 16 Lv) of every repair row."""
+    also write zeros to bytes [L, 16 Lv) of every repair row.  Dec mode
+    (lu = (records, record stride), tables = split-table base): dst, dgs and
+    drs are the recovered rows' base, generation and row strides; 112 bytes."""
     Lv, total, n_items = launch_geometry(L, G, Lv)
     magic, shift = magic_for(Lv)
     s19 = map_stride if smap else (Lv if zero_tail else L // 16)
     words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, L // 16, Lv, total,
              magic, shift, n_items, total_waves, s19, smap & MASK32, smap >> 32,
              zero & MASK32, zero >> 32]
+    if lu is not None:
+        words += [lu[0] & MASK32, lu[0] >> 32, lu[1], 0, tables & MASK32, tables >> 32, 0, 0]
     for w in words:
         assert 0 <= w < 1 << 32, words
     return np.array(words, dtype=np.uint32).tobytes()
+
+
+def perm_record(c: int) -> list[int]:
+    """gf256_tables.h perm_record: {T0lo, T0hi, T1lo, T1hi, T2, 0, 0, 0}."""
+    t0 = [gf_mul(c, v) for v in range(8)]
+    t1 = [gf_mul(c, v << 3) for v in range(8)]
+    t2 = [gf_mul(c, v << 6) for v in range(4)]
+
+    def pk(b):
+        return b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24
+    return [pk(t0[:4]), pk(t0[4:]), pk(t1[:4]), pk(t1[4:]), pk(t2), 0, 0, 0]
+
+
+def split_tables() -> np.ndarray:
+    """The 256 x 32-byte table set the dec kernel copies into LDS."""
+    return np.array([perm_record(c) for c in range(256)], np.uint32).reshape(-1).view(np.uint8)
+
+
+def lu_record(k: int, r: int, accepted: list[int], E: list[int]) -> np.ndarray:
+    """Host restatement of k_decode_prepare_lu's per-generation record: the
+    LU factors (no pivoting) of A = C[J, E] with J = accepted repairs
+    ascending and E = erased sources ascending, embedded by repair index
+    (LU_REC_BYTES bytes; layout in _lu_solve_and_store).  Every leading minor
+    of a Cauchy matrix is non-zero, so the factorisation needs no pivoting."""
+    J = sorted(accepted)
+    e = len(J)
+    assert e == len(E) and e <= 16 and r <= 16
+    A = [[gf_inv(((k + j) & 0xFF) ^ i) for i in E] for j in J]
+    Lm = [[0] * e for _ in range(e)]
+    for p in range(e):
+        inv = gf_inv(A[p][p])
+        for i in range(p + 1, e):
+            f = gf_mul(A[i][p], inv)
+            Lm[i][p] = f
+            for c in range(p, e):
+                A[i][c] ^= gf_mul(f, A[p][c])
+    rec = np.zeros(LU_REC_BYTES, np.uint8)
+    rec[256:272] = 0xFF
+    for b, t in enumerate(J):
+        rec[256 + t] = b
+        for c, u in enumerate(J):
+            if b < c:
+                v = A[b][c]
+            elif b == c:
+                v = gf_inv(A[b][b])
+            else:
+                v = Lm[b][c]
+            rec[16 * u + t] = v
+    return rec
 
 
 def cauchy_inverse(k: int, J: list[int], E: list[int]) -> list[list[int]]:
@@ -792,7 +1103,9 @@ class Emulator:
 
     def run_wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int):
         v = np.zeros((256, 64), dtype=np.uint64)
-        s = [0] * 64
+        s = [0] * 80
+        lds = np.zeros(LDS_TAB_BYTES, np.uint8)
+        pend_lgkm = []
         ka = np.frombuffer(kernarg, np.uint32)
         pending = []  # list of (regs, values, lanes) in issue order
         busy = set()
@@ -844,6 +1157,58 @@ class Emulator:
             if n == "s_load_args":
                 for q in range(20):
                     s[4 + q] = int(ka[q])
+            elif n == "s_load_args_dec":
+                for q in range(8):
+                    s[56 + q] = int(ka[20 + q])
+            elif n == "v_perm":
+                pool = (rv(a[1]) << np.uint64(32)) | rv(a[2])
+                sel = rv(a[3])
+                res = np.zeros(64, np.uint64)
+                for b in range(4):
+                    sb = (sel >> np.uint64(8 * b)) & np.uint64(0xFF)
+                    if (sb >= 8).any():
+                        raise EmuError("v_perm selector outside 0..7")
+                    res |= ((pool >> (sb * np.uint64(8))) & np.uint64(0xFF)) << np.uint64(8 * b)
+                wv(a[0], res)
+            elif n in ("ds_read_b128", "ds_read_b32"):
+                d, ar, off = a
+                nd = 4 if n == "ds_read_b128" else 1
+                addr = rv(ar)
+                vals = np.zeros((nd, 64), np.uint64)
+                for l in np.nonzero(exec_)[0]:
+                    p0 = int(addr[l]) + off
+                    if p0 < 0 or p0 + 4 * nd > len(lds):
+                        raise EmuError(f"LDS access out of range 0x{p0:x}")
+                    vals[:, l] = np.frombuffer(lds[p0: p0 + 4 * nd].tobytes(), np.uint32)
+                regs = [d + q for q in range(nd)]
+                for rg in regs:
+                    if rg in busy:
+                        raise EmuError(f"ds_read into v{rg} with a load outstanding")
+                    busy.add(rg)
+                pend_lgkm.append((regs, vals, exec_.copy()))
+            elif n == "ds_write_b128":
+                ar, d, off = a
+                addr = rv(ar)
+                vals = np.stack([rv(d + q) for q in range(4)]).astype(np.uint32)
+                for l in np.nonzero(exec_)[0]:
+                    p0 = int(addr[l]) + off
+                    if p0 < 0 or p0 + 16 > len(lds):
+                        raise EmuError(f"LDS access out of range 0x{p0:x}")
+                    lds[p0: p0 + 16] = np.frombuffer(vals[:, l].tobytes(), np.uint8)
+            elif n == "s_waitcnt_lgkm_n":
+                while len(pend_lgkm) > a[0]:
+                    regs, vals, lanes = pend_lgkm.pop(0)
+                    for q, rg in enumerate(regs):
+                        busy.discard(rg)
+                        v[rg] = np.where(lanes, vals[q], v[rg])
+            elif n == "s_cmp_le_k_br":
+                if s[a[0]] <= a[1]:
+                    pc = self.labels[a[2]]
+            elif n == "s_or64":
+                set_smask(a[0], smask(a[1]) | smask(a[2]))
+            elif n == "s_cmp_lg64_br":
+                if s[a[0]] or s[a[0] + 1]:
+                    pc = self.labels[a[1]]
             elif n == "v_xor":
                 wv(a[0], rv(a[1]) ^ rv(a[2]))
             elif n == "v_mov":
@@ -946,8 +1311,11 @@ class Emulator:
             elif n == "s_cmp_ge_br":
                 if s[a[0]] >= s[a[1]]:
                     pc = self.labels[a[2]]
-            elif n == "s_branch":
+            elif n == "s_branch" or n == "s_far_jump":
                 pc = self.labels[a[0]]
+            elif n == "s_cmp_lt_br":
+                if s[a[0]] < s[a[1]]:
+                    pc = self.labels[a[2]]
             elif n == "s_endpgm":
                 if pending:
                     # stores/loads may be outstanding at the end: retire them

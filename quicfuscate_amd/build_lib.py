@@ -114,14 +114,14 @@ def _bs_kernels(build_dir: Path) -> Path:
     from . import bs_codegen as bs
 
     entries, blobs = [], []
-    specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn") for (k, r) in BS_CONFIGS]
+    specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn", "dec") for (k, r) in BS_CONFIGS]
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
         data = hsaco.read_bytes()
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
-        mode = "e" if spec.mode == "enc" else "s"
+        mode = {"enc": "e", "syn": "s", "dec": "d"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {BS_PD}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
     inc = build_dir / "qf_bs_blobs.inc"

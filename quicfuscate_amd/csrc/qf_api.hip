@@ -323,6 +323,67 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     return QF_OK;
 }
 
+// Fused decode of the reference's Cauchy code (no row_coeffs), one pass over
+// the received rows:
+//   k_decode_prepare_cauchy (lu_out)  acceptance, slot map, LU of C[J,E]
+//   qf_cauchy_dec_k*_r*               syndromes (bit-sliced), then the LU
+//                                     solve in registers, recovered rows out
+// A device buffer of >= L zero bytes (read in place of absent rows).
+int ensure_zero(qf_ctx* ctx, uint32_t L) {
+    if (ctx->zero_bytes >= L) return QF_OK;
+    if (ctx->d_zero) {
+        QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        hipFree(ctx->d_zero);
+        ctx->d_zero = nullptr;
+        ctx->zero_bytes = 0;
+    }
+    const size_t zb = round_up(L, 4096);
+    if (hipMalloc(&ctx->d_zero, zb) != hipSuccess) return QF_ENOMEM;
+    QF_CHECK_HIP(hipMemset(ctx->d_zero, 0, zb));
+    ctx->zero_bytes = zb;
+    return QF_OK;
+}
+
+int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                 const uint16_t* row_index, const uint32_t* n_rows, uint8_t* rec,
+                 uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    const uint32_t ms = qf::syn_map_stride(k, r);
+    const uint32_t lu_stride = 272;
+    const size_t off_map = round_up((size_t)G * lu_stride, 256);
+    int s = grow_work(ctx, off_map + (size_t)G * ms);
+    if (s) return s;
+    s = ensure_zero(ctx, L);
+    if (s) return s;
+    uint8_t* w = ctx->d_work;
+    hipStream_t st = ctx->stream;
+    qf::PrepareCauchyArgs pa{};
+    pa.row_index = row_index;
+    pa.n_rows = n_rows;
+    pa.explog = ctx->d_explog;
+    pa.smap = w + off_map;
+    pa.n_out = n_rec;
+    pa.rec_index = rec_index;
+    pa.status = status;
+    pa.k = k;
+    pa.r = r;
+    pa.e_max = std::min(k, r);
+    pa.max_rows = sh->max_rows;
+    pa.map_stride = ms;
+    pa.G = G;
+    pa.lu_out = w;
+    pa.lu_stride = lu_stride;
+    hipEvent_t ev = prof_begin(ctx, st);
+    QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
+    prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
+    ev = prof_begin(ctx, st);
+    QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
+                                sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
+                                ctx->d_zero, w, lu_stride, ctx->d_tab256));
+    prof_end(ctx, st, ev, qf::dec_name(k, r));
+    return QF_OK;
+}
+
 // Decode of the reference's Cauchy code by syndromes (no row_coeffs):
 //   k_decode_prepare_cauchy  acceptance, slot map, D = C[J,E]^-1 (closed form)
 //   qf_cauchy_syn_k*_r*      s_j = p_j ^ sum_{i present} C[j][i] x_i  (bit-sliced)
@@ -361,18 +422,8 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     if (s) return s;
     uint8_t* w = ctx->d_work;
     uint32_t* d_bound = reinterpret_cast<uint32_t*>(w + off_bound);
-    if (ctx->zero_bytes < L) {
-        if (ctx->d_zero) {
-            QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-            hipFree(ctx->d_zero);
-            ctx->d_zero = nullptr;
-            ctx->zero_bytes = 0;
-        }
-        const size_t zb = round_up(L, 4096);
-        if (hipMalloc(&ctx->d_zero, zb) != hipSuccess) return QF_ENOMEM;
-        QF_CHECK_HIP(hipMemset(ctx->d_zero, 0, zb));
-        ctx->zero_bytes = zb;
-    }
+    s = ensure_zero(ctx, L);
+    if (s) return s;
     hipStream_t st = ctx->stream, sb = ctx->stream;
     if (overlap) {
         if (!ctx->aux) QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
@@ -728,8 +779,15 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     if (!row_coeffs && !(nobs && atoi(nobs)) && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
         max_rows <= 255 && L % 16 == 0 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
         sh->row_stride < (1ull << 32) && (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31) &&
-        (uint64_t)r * 16 * qf::bs_padded_units(L) < (1ull << 32))
+        (uint64_t)r * 16 * qf::bs_padded_units(L) < (1ull << 32)) {
+        // fused single-pass decode unless QF_DECODE_SYN=1 asks for the
+        // two-kernel syndrome + v_perm combine path
+        const char* two = getenv("QF_DECODE_SYN");
+        if (qf::dec_available(k, r) && !(two && atoi(two)) && sh->rec_gen_stride < (1ull << 32) &&
+            sh->rec_row_stride < (1ull << 32))
+            return decode_fused(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
+    }
     const uint32_t passes = (e_max + 15) / 16;
     const uint64_t coef_gen_stride = ((uint64_t)max_rows + 1) * 16;
     const size_t coef_bytes = (size_t)std::max<uint32_t>(passes, 1) * G * coef_gen_stride;

@@ -37,6 +37,17 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
                       uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero);
+// Fused decode (bs_codegen.py "dec"): syndromes of the accepted repairs,
+// then C[J, E] x = s solved in registers by the per-generation LU records of
+// k_decode_prepare_cauchy (lu_out), recovered rows stored to
+// rec + g * rec_gs + rank * rec_rs.  Only the payload bytes [0, L) of a
+// recovered row are written.
+bool dec_available(uint32_t k, uint32_t r);
+const char* dec_name(uint32_t k, uint32_t r);
+hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                      const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
+                      uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
+                      const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256);
 void bs_unload(BsCache& cache);
 
 }  // namespace qf

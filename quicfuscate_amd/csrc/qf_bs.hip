@@ -64,7 +64,8 @@ static void magic_for(uint32_t U, uint32_t* magic, uint32_t* shift) {
 static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStream_t st,
                          const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                          uint64_t drs, uint32_t L, uint32_t G, uint32_t Lv, uint32_t s19,
-                         const uint8_t* smap, const uint8_t* zero) {
+                         const uint8_t* smap, const uint8_t* zero, const uint8_t* lu = nullptr,
+                         uint32_t lu_stride = 0, const uint32_t* tab256 = nullptr) {
     (void)num_cus;
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
@@ -87,7 +88,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     const uint32_t n_items = (uint32_t)((total + 127) / 128);
     const uint32_t blocks = (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    uint32_t a[20];
+    uint32_t a[28] = {};
     a[0] = (uint32_t)(uintptr_t)src;
     a[1] = (uint32_t)((uintptr_t)src >> 32);
     a[2] = (uint32_t)(uintptr_t)dst;
@@ -108,7 +109,12 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[17] = (uint32_t)((uintptr_t)smap >> 32);
     a[18] = (uint32_t)(uintptr_t)zero;
     a[19] = (uint32_t)((uintptr_t)zero >> 32);
-    size_t sz = sizeof(a);
+    a[20] = (uint32_t)(uintptr_t)lu;
+    a[21] = (uint32_t)((uintptr_t)lu >> 32);
+    a[22] = lu_stride;
+    a[24] = (uint32_t)(uintptr_t)tab256;
+    a[25] = (uint32_t)((uintptr_t)tab256 >> 32);
+    size_t sz = e->mode == 'd' ? 28 * 4 : 20 * 4;
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
     return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
@@ -146,6 +152,26 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
     const uint32_t Lv = bs_padded_units(L);
     if (srs < 16ull * Lv) return hipErrorInvalidValue;
     return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, Lv, map_stride, smap, zero);
+}
+
+bool dec_available(uint32_t k, uint32_t r) { return find('d', k, r) != nullptr; }
+
+const char* dec_name(uint32_t k, uint32_t r) {
+    const QfBsEntry* e = find('d', k, r);
+    return e ? e->name : nullptr;
+}
+
+hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                      const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
+                      uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
+                      const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256) {
+    const QfBsEntry* e = find('d', k, r);
+    if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
+        return hipErrorInvalidValue;
+    // the LU record pointer is computed with a 32-bit stride multiply
+    if ((uint64_t)G * lu_stride >= (1ull << 40)) return hipErrorInvalidValue;
+    return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, bs_padded_units(L), map_stride,
+                  smap, zero, lu, lu_stride, tab256);
 }
 
 void bs_unload(BsCache& cache) {

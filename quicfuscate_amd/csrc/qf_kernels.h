@@ -90,6 +90,11 @@ struct PrepareCauchyArgs {
     uint32_t max_rows;      // <= 255
     uint32_t map_stride;
     uint32_t G;
+    // fused decode (qf_cauchy_dec_*): when lu_out != nullptr the kernel
+    // writes the packed LU record of C[J, E] per generation (lu_stride bytes,
+    // layout bs_codegen._lu_solve_and_store) instead of coef_out / bound
+    uint8_t* lu_out;
+    uint32_t lu_stride;
 };
 hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st);
 

@@ -691,6 +691,7 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
     __shared__ uint8_t J[256], Eidx[256];
     __shared__ uint32_t lA[256], lB[256], lE[256], lF[256];
     __shared__ __attribute__((aligned(16))) uint8_t rec[17 * 16];
+    __shared__ uint8_t Js[16], rank[16], M[16][16], Lf[16][16];
     const uint32_t g = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const uint32_t k = a.k, r = a.r;
@@ -754,6 +755,87 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
     bool dup = false;
     for (uint32_t j = lane; j < r; j += 64) dup |= rep_cnt[j] > 1;
     if (status == 0 && __any(dup)) status = -4;    // QF_ERANK: repeated repair rows
+    if (a.lu_out) {
+        // Fused decode: LU (no pivoting) of A = C[J, E], J = accepted repairs
+        // ascending, E = erased sources ascending.  Every leading minor of a
+        // Cauchy matrix is a Cauchy determinant, non-zero for distinct
+        // points, so Gaussian elimination never meets a zero pivot.
+        if (lane < 16) rank[lane] = 0xFF;
+        __syncthreads();
+        if (status == 0 && e > 0) {
+            uint32_t ne = 0;
+            for (uint32_t i0 = 0; i0 < k; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const bool miss = i < k && sys_slot[i] == 0xFF;
+                const uint64_t bm = __ballot(miss);
+                if (miss) Eidx[ne + __popcll(bm & lt_mask)] = (uint8_t)i;
+                ne += __popcll(bm);
+            }
+            const bool accj = lane < r && rep_slot[lane] != 0xFF;
+            const uint64_t bj = __ballot(accj);
+            if (accj) {
+                const uint32_t p = __popcll(bj & lt_mask);
+                Js[p] = (uint8_t)lane;
+                rank[lane] = (uint8_t)p;
+            }
+            __syncthreads();
+            for (uint32_t t = lane; t < e * e; t += 64) {
+                const uint32_t b = t / e, c = t - b * e;
+                const uint32_t x = ((k + Js[b]) & 0xFF) ^ Eidx[c];  // != 0: k + j >= k > E
+                M[b][c] = sexp[255 - slog[x]];
+            }
+            for (uint32_t p = 0; p < e; ++p) {
+                __syncthreads();
+                const uint32_t lp = 255 - slog[M[p][p]];  // log of the pivot inverse
+                for (uint32_t i = p + 1 + lane; i < e; i += 64) {
+                    const uint32_t v = M[i][p];
+                    Lf[i][p] = v ? sexp[slog[v] + lp] : 0;
+                }
+                __syncthreads();
+                const uint32_t w = e - p - 1;
+                for (uint32_t t = lane; t < w * w; t += 64) {
+                    const uint32_t i = p + 1 + t / w, c = p + 1 + t % w;
+                    const uint32_t f = Lf[i][p], m = M[p][c];
+                    if (f && m) M[i][c] ^= sexp[slog[f] + slog[m]];
+                }
+            }
+            __syncthreads();
+        }
+        const bool ok = status == 0;
+        uint8_t* lo = a.lu_out + (uint64_t)g * a.lu_stride;
+        for (uint32_t q = lane; q < 272; q += 64) {
+            uint8_t v;
+            if (q >= 256) {
+                v = ok ? rank[q - 256] : 0xFF;
+            } else {
+                const uint32_t u = q >> 4, t = q & 15;
+                v = 0;
+                if (ok && rank[t] != 0xFF && rank[u] != 0xFF) {
+                    const uint32_t b = rank[t], c = rank[u];
+                    if (b < c) v = M[b][c];
+                    else if (b == c) v = sexp[255 - slog[M[b][b]]];
+                    else v = Lf[b][c];
+                }
+            }
+            lo[q] = v;
+        }
+        uint8_t* sm = a.smap + (uint64_t)g * a.map_stride;
+        for (uint32_t q = lane; q < a.map_stride; q += 64) {
+            uint8_t v = 0xFF;
+            if (ok) {
+                if (q < k) v = sys_slot[q];
+                else if (q < k + r) v = rep_slot[q - k];
+            }
+            sm[q] = v;
+        }
+        if (ok)
+            for (uint32_t b = lane; b < e; b += 64) a.rec_index[(uint64_t)g * a.e_max + b] = Eidx[b];
+        if (lane == 0) {
+            a.status[g] = status;
+            a.n_out[g] = ok ? e : 0;
+        }
+        return;
+    }
     if (status == 0 && e > 0) {
         uint32_t ne = 0;
         for (uint32_t i0 = 0; i0 < k; i0 += 64) {

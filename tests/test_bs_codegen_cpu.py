@@ -213,7 +213,8 @@ def test_cauchy_inverse_closed_form():
                 assert acc == (1 if b == c else 0)
 
 
-@pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "syn"), (16, 1, "syn"), (32, 16, "enc")])
+@pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "syn"), (16, 1, "syn"), (32, 16, "enc"),
+                                      (64, 16, "dec"), (16, 1, "dec")])
 def test_declared_register_budget_covers_code(k, r, mode):
     """Every VGPR / SGPR the generated code names lies below the
     .amdhsa_next_free_* counts of its kernel descriptor."""
@@ -271,3 +272,95 @@ def test_xcd_remap_is_a_bijection():
         q, rem = nwg // 8, nwg % 8
         got = sorted((w % 8) * q + min(w % 8, rem) + w // 8 for w in range(nwg))
         assert got == list(range(nwg))
+
+
+def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True):
+    """Run the fused decode kernel (mode "dec") on the emulator: random
+    erasures (or `erase` sources), random accepted repairs in random slots,
+    LU records from bs.lu_record; returns the number of wrong rows."""
+    spec = bs.KernelSpec(k, r, pd, mode="dec")
+    rng = np.random.default_rng(seed)
+    rs = L + 16
+    n_slots = k + 2
+    rgs = n_slots * rs + 16
+    Lv = bs.padded_units(L) if padded else None
+    rrs = L + 32
+    emax = min(k, r)
+    ogs = emax * rrs + 16
+    ms = spec.map_stride
+    rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
+    smap = np.full(G * ms, 0xFF, np.uint8)
+    recs = np.zeros(G * bs.LU_REC_BYTES, np.uint8)
+    out = np.full(G * ogs, 0xEE, np.uint8)
+    plans = []
+    for g in range(G):
+        src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        rep = oracle.encode(src, r)
+        e = int(rng.integers(0, emax + 1)) if erase is None else erase
+        E = sorted(rng.choice(k, e, replace=False).tolist())
+        J = rng.choice(r, e, replace=False).tolist()
+        present = [("s", i) for i in range(k) if i not in E] + [("p", j) for j in J]
+        slots = rng.choice(n_slots, len(present), replace=False)
+        for n, pi in enumerate(rng.permutation(len(present))):
+            kind, idx = present[pi]
+            sl = int(slots[n])
+            rows[g * rgs + sl * rs: g * rgs + sl * rs + L] = src[idx] if kind == "s" else rep[idx]
+            smap[g * ms + (idx if kind == "s" else k + idx)] = sl
+        recs[g * bs.LU_REC_BYTES:(g + 1) * bs.LU_REC_BYTES] = bs.lu_record(k, r, J, E)
+        plans.append((src, E))
+    emu = bs.Emulator(bs.generate(spec))
+    ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
+    for base, buf in ((ROWS, rows), (OUT, out), (MAP, smap), (ZERO, np.zeros(L, np.uint8)), (REC, recs),
+                      (TAB, bs.split_tables())):
+        emu.add_buffer(base, buf)
+    waves = (bs.launch_geometry(L, G, Lv)[2] + 3) // 4
+    ka = bs.kernargs(ROWS, OUT, rgs, ogs, rs, rrs, L, G, waves * 4, smap=MAP, map_stride=ms, zero=ZERO,
+                     Lv=Lv, lu=(REC, bs.LU_REC_BYTES), tables=TAB)
+    for wg in range(waves):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    bad = 0
+    for g, (src, E) in enumerate(plans):
+        blk = out[g * ogs: (g + 1) * ogs]
+        for b, i in enumerate(E):
+            bad += int(not (blk[b * rrs: b * rrs + L] == src[i]).all())
+            assert (blk[b * rrs + L: (b + 1) * rrs] == 0xEE).all(), "bytes past L written"
+        assert (blk[len(E) * rrs:] == 0xEE).all(), "rows past e written"
+    return bad
+
+
+@pytest.mark.parametrize("k,r,pd,L,G,seed,erase", [
+    (8, 4, 2, 96, 6, 1, None),
+    (8, 4, 3, 80, 7, 2, None),      # half chunks, padded lane space
+    (16, 16, 4, 64, 5, 3, None),    # every block can be a pivot
+    (16, 16, 2, 96, 4, 4, 16),      # e = r: all 16 blocks, jmax = 16
+    (5, 3, 1, 64, 9, 5, 0),         # nothing erased: no stores at all
+])
+def test_emulated_fused_decode(oracle, k, r, pd, L, G, seed, erase):
+    """Fused decode on the emulator: syndromes, in-register LU solve with the
+    split tables from LDS, recovered rows equal the erased sources."""
+    assert _dec_case(oracle, k, r, pd, L, G, seed, erase) == 0
+
+
+def test_lu_record_reconstructs_cauchy_submatrix():
+    """The packed LU record's factors multiply back to C[J, E] (J ascending)."""
+    rng = np.random.default_rng(11)
+    for _ in range(40):
+        k = int(rng.integers(1, 240))
+        r = int(rng.integers(1, min(16, 256 - k) + 1))
+        e = int(rng.integers(1, min(k, r) + 1))
+        E = sorted(rng.choice(k, e, replace=False).tolist())
+        J = rng.choice(r, e, replace=False).tolist()
+        rec = bs.lu_record(k, r, J, E)
+        Js = sorted(J)
+        for t in range(16):
+            assert rec[256 + t] == (Js.index(t) if t in Js else 0xFF)
+        Lm = [[1 if b == c else (rec[16 * Js[c] + Js[b]] if b > c else 0) for c in range(e)] for b in range(e)]
+        Um = [[(bs.gf_inv(rec[16 * Js[c] + Js[b]]) if b == c else rec[16 * Js[c] + Js[b]]) if b <= c else 0
+               for c in range(e)] for b in range(e)]
+        for b in range(e):
+            for c in range(e):
+                acc = 0
+                for q in range(e):
+                    acc ^= bs.gf_mul(Lm[b][q], Um[q][c])
+                assert acc == bs.gf_inv(((k + Js[b]) & 0xFF) ^ E[c])

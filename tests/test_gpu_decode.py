@@ -97,16 +97,22 @@ def check(oracle, k, L, src, gens, out, with_coeffs):
             assert (rec[g * rec_gs + m * rrs + L: g * rec_gs + (m + 1) * rrs] == 0x5A).all()
 
 
-PATHS = ["default", "general"]
+PATHS = ["default", "syn", "general"]
 
 
 def _path(monkeypatch, path):
-    # "default": syndrome decode where a bit-sliced kernel exists for (k, r)
-    # (Cauchy code, L % 16 == 0); "general": Gauss-Jordan + slots kernel
+    # "default": fused decode (syndromes + LU solve in one kernel) where a
+    # bit-sliced kernel exists for (k, r) (Cauchy code, L % 16 == 0);
+    # "syn": syndrome kernel + v_perm combine (two kernels);
+    # "general": Gauss-Jordan + slots kernel
     if path == "general":
         monkeypatch.setenv("QF_DISABLE_BS", "1")
     else:
         monkeypatch.delenv("QF_DISABLE_BS", raising=False)
+    if path == "syn":
+        monkeypatch.setenv("QF_DECODE_SYN", "1")
+    else:
+        monkeypatch.delenv("QF_DECODE_SYN", raising=False)
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -218,6 +224,7 @@ def test_decode_chunked_pipeline(qf, oracle, gpu_ctx, chunk, overlap, monkeypatc
     # (double-buffered syndromes); twice in a row on the same context
     monkeypatch.setenv("QF_DECODE_CHUNK", chunk)
     monkeypatch.setenv("QF_DECODE_OVERLAP", overlap)
+    monkeypatch.setenv("QF_DECODE_SYN", "1")
     monkeypatch.delenv("QF_DISABLE_BS", raising=False)
     for seed in (1, 2):
         rng = np.random.default_rng(seed)

@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Fused-decode kernel lab: variants of qf_cauchy_dec_k64_r16 timed on the GPU
+on the C3 workload shape (k=64, r=16, L=1200, 13 erased sources, arrival =
+surviving sources then repairs).
+
+    python tools/dec_lab.py build     # here: generate + assemble -> tools/lab_build/dec_*
+    python tools/dec_lab.py run       # GPU box
+
+Slot maps follow the C3 arrival rule exactly; LU records are those of 256
+distinct random erasure patterns, tiled (timing only: the recovered bytes
+are not checked here -- tests/ do that).  Diagnostic only."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "tools"))
+OUT = REPO / "tools" / "lab_build"
+
+VARIANTS = [
+    # name, spec kwargs, body-strip flags (bs_lab.variant_ops)
+    ("warm", {}, ()),
+    ("full", {}, ()),
+    ("nolu", {"lu": False}, ()),
+    ("noguard", {"guard_min": 16}, ()),
+    ("nolu_noguard", {"lu": False, "guard_min": 16}, ()),
+    ("noload", {}, ("noload",)),
+    ("full_2", {}, ()),
+]
+
+
+def build():
+    from bs_lab import variant_ops
+
+    from quicfuscate_amd import bs_codegen as bs
+    from quicfuscate_amd.build_lib import assemble
+
+    OUT.mkdir(parents=True, exist_ok=True)
+    for old in OUT.glob("dec_*"):
+        old.unlink()
+    man = []
+    for name, kw, flags in VARIANTS:
+        spec = bs.KernelSpec(64, 16, 3, "dec", **kw)
+        text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
+        h = assemble(f"dec_{name}", text.replace(spec.name, f"dec_{name}"), OUT)
+        man.append({"name": name, "hsaco": h.name, "symbol": f"dec_{name}", "kw": kw, "flags": list(flags),
+                    "vgprs": spec.next_free_vgpr})
+        print(name, h.stat().st_size)
+    (OUT / "dec_manifest.json").write_text(json.dumps(man, indent=1))
+
+
+def c3_inputs(G, k, r, L, e, seed=0x51464543):
+    rng = np.random.default_rng(seed)
+    keys = rng.random((G, k), dtype=np.float32)
+    erased = np.sort(np.argsort(keys, axis=1)[:, :e], axis=1)
+    keep = np.ones((G, k), bool)
+    np.put_along_axis(keep, erased, False, axis=1)
+    ms = (k + r + 15) // 16 * 16
+    smap = np.full((G, ms), 0xFF, np.uint8)
+    slot_of = np.cumsum(keep, axis=1) - 1
+    smap[:, :k] = np.where(keep, slot_of, 0xFF)
+    smap[:, k:k + e] = (k - e) + np.arange(e)
+    return erased, smap
+
+
+def run(G, reps):
+    import torch
+
+    from quicfuscate_amd import bs_codegen as bs
+
+    hip = ctypes.CDLL(str(Path(torch.__file__).parent / "lib" / "libamdhip64.so"))
+    dev = torch.device("cuda")
+    k, r, L, e = 64, 16, 1200, 13
+    n_slots = k - e + r
+    erased, smap = c3_inputs(G, k, r, L, e)
+    recs = np.zeros((256, bs.LU_REC_BYTES), np.uint8)
+    for q in range(256):
+        recs[q] = bs.lu_record(k, r, list(range(e)), erased[q].tolist())
+    lu = np.tile(recs, (G // 256 + 1, 1))[:G]
+    rows = torch.randint(0, 256, (G * n_slots * L,), dtype=torch.uint8, device=dev)
+    rec = torch.empty(G * e * L, dtype=torch.uint8, device=dev)
+    d_map = torch.from_numpy(smap.reshape(-1)).to(dev)
+    d_lu = torch.from_numpy(lu.reshape(-1)).to(dev)
+    d_tab = torch.from_numpy(bs.split_tables()).to(dev)
+    zero = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    res = {}
+    for m in json.loads((OUT / "dec_manifest.json").read_text()):
+        mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        data = (OUT / m["hsaco"]).read_bytes()
+        buf = ctypes.create_string_buffer(data, len(data))
+        assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
+        Lv = bs.padded_units(L)
+        _, _, n_items = bs.launch_geometry(L, G, Lv)
+        blocks = (n_items + 3) // 4
+        ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * L, e * L, L, L, L, G, blocks * 4,
+                         smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
+                         lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr())
+        kbuf = ctypes.create_string_buffer(ka, len(ka))
+        size = ctypes.c_size_t(len(ka))
+        extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
+                                     ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+
+        def launch():
+            assert hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(stream.cuda_stream),
+                                             None, extra) == 0
+
+        launch()
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record(stream)
+        for _ in range(reps):
+            launch()
+        t1.record(stream)
+        torch.cuda.synchronize()
+        ms = t0.elapsed_time(t1) / reps
+        alg = G * ((k + e) * L)
+        res[m["name"]] = {"ms": round(ms, 4), "GBps_alg": round(alg / (ms / 1e3) / 1e9, 1), "kw": m["kw"],
+                          "flags": m["flags"], "vgprs": m["vgprs"]}
+        print(m["name"], res[m["name"]], flush=True)
+        hip.hipModuleUnload(mod)
+    return res
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--G", type=int, default=65536)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default="gpurun_out/dec_lab.json")
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build()
+    else:
+        r = run(a.G, a.reps)
+        Path(a.out).parent.mkdir(exist_ok=True)
+        Path(a.out).write_text(json.dumps(r, indent=1))

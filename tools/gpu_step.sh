@@ -1,5 +1,10 @@
-cd $GRAFT_REPO_ROOT
+#!/bin/bash
+# Quick GPU iteration: gpu tests (own time limit) then the bench line.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 300 python tools/bs_lab.py run --reps 20 > gpurun_out/lab.log 2>&1 && \
-timeout -k 10 600 python -u -m pytest tests/test_gpu_encode.py tests/test_gpu_decode.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log; cat gpurun_out/lab.log | grep -v amdgpu.ids
-[ $rc -eq 0 ] && timeout -k 10 300 python bench.py --no-cpu --host-path-G 0 > gpurun_out/bench.log 2>&1; tail -2 gpurun_out/bench.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -8 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu --host-path-G 0 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench.log
+exit $rc
