@@ -244,18 +244,26 @@ def main(argv=None):
     #     records, write e rows) or, on the general path, read k rows +
     #     records, write e rows
     #   prepare: row indices in, slot map / records / indices out
+    #   fused decode: read the k accepted rows + slot map + LU record, write
+    #     the e recovered rows
     fast_decode = any(n.startswith("qf_cauchy_syn") for n in ktimes)
     map_stride = (k + r + 15) // 16 * 16
     enc_bytes = G * (k + r) * Lb
     syn_bytes = G * ((k + e) * Lb + map_stride)
+    dec_kernel_bytes = G * ((k + e) * Lb + map_stride + 272)
     if fast_decode:
         slots_bytes = G * (2 * e * Lb + (e + 1) * 16)
     else:
         slots_bytes = G * (k * Lb + e * Lb + (n_slots + 1) * 16)
-    prep_bytes = G * (n_slots * 2 + map_stride + (r + 1) * 16 + e * 2 + 12)
+    if any(n.startswith("qf_cauchy_dec") for n in ktimes):
+        prep_bytes = G * (n_slots * 2 + map_stride + 272 + e * 2 + 8)   # row indices in; map, LU record out
+    else:
+        prep_bytes = G * (n_slots * 2 + map_stride + (r + 1) * 16 + e * 2 + 12)
     dec_bytes = G * (k * Lb + e * k + e * Lb)  # decode as a whole (SURVEY B_dec)
 
     def alg_bytes(name):
+        if name.startswith("qf_cauchy_dec"):
+            return dec_kernel_bytes
         if name.startswith("qf_cauchy_syn"):
             return syn_bytes
         if name.startswith("k_combine_slots"):

@@ -155,9 +155,11 @@ _ASM = {
     "s_waitcnt_vm": lambda n: f"s_waitcnt vmcnt({n})",
     "s_waitcnt_lgkm": lambda: "s_waitcnt lgkmcnt(0)",
     "s_nop": lambda n: f"s_nop {n}",
+    "s_setprio": lambda n: f"s_setprio {n}",
     "s_load_args": lambda: "s_load_dwordx16 s[4:19], s[0:1], 0x0\n\ts_load_dwordx4 s[20:23], s[0:1], 0x40",
     "s_load_args_dec": lambda: "s_load_dwordx8 s[56:63], s[0:1], 0x50",
     "v_perm": lambda d, hi, lo, sel: f"v_perm_b32 {V(d)}, {V(hi)}, {V(lo)}, {V(sel)}",
+    "v_perm_s": lambda d, hi, lo, s: f"v_perm_b32 {V(d)}, {V(hi)}, {V(lo)}, s{s}",
     "ds_read_b128": lambda d, a, off: f"ds_read_b128 {VQ(d)}, {V(a)}" + (f" offset:{off}" if off else ""),
     "ds_read_b32": lambda d, a, off: f"ds_read_b32 {V(d)}, {V(a)}" + (f" offset:{off}" if off else ""),
     "ds_write_b128": lambda a, d, off: f"ds_write_b128 {V(a)}, {VQ(d)}" + (f" offset:{off}" if off else ""),
@@ -216,9 +218,11 @@ S_STA, S_STB, S_PAD = 48, 50, 52   # store masks of halves A / B, mask temp
 #   s[62:63] {4096, 0} after the table copy (address constant)
 # s64 jmax: 1 + the largest repair index any lane of the item has accepted.
 KERNARG_BYTES_DEC = 112
-SGPR_NEXT_FREE_DEC = 68      # s[66:67]: far-jump target
+SGPR_NEXT_FREE_DEC = 72      # s[66:67]: far-jump target, s68..s71: byte-pick selectors
 S_JMAX = 64
-LDS_TAB_BYTES = 8192
+S_PICK = 68                  # v_perm selector placing byte b of a dword at bits 8..15
+LDS_TAB_STRIDE = 256         # split-table record c at LDS byte c * 256 (address = byte << 8)
+LDS_TAB_BYTES = 256 * LDS_TAB_STRIDE
 LU_REC_BYTES = 272          # 16 columns x 16 B, then 16 rank bytes
 # LU-phase VGPRs (regions free once the row loop is done; dec mode with
 # r = 16: acc blocks v80..v207, slot maps v208..v247 are dead by then)
@@ -267,6 +271,8 @@ class KernelSpec:
     guard_min: int = 4
     # dec mode: solve in registers (False: store the syndromes unsolved; lab only)
     lu: bool = True
+    # dec mode: wave priority (s_setprio) of the row loop / the LU phase
+    prio: tuple = (0, 0)
 
     @property
     def name(self) -> str:
@@ -467,10 +473,18 @@ def _prologue(E, spec: KernelSpec):
         E(Op("v_add64_s", (V_SRCA, V_ADDR, 62)))
         for q in range(8):
             E(Op("load16", (48 + 4 * q, V_ADDR if q < 4 else V_SRCA, 1024 * (q % 4))))
-        E(Op("v_lshl", (V_T, 4, V_LANE)))
+        # global bytes q*1024 + 16 l = record 32 q + l/2, half l % 2 -> LDS
+        # (32 q + l/2) * 256 + 16 (l % 2)
+        E(Op("v_lshr", (V_T, 1, V_LANE)))
+        E(Op("v_lshl", (V_T, 8, V_T)))
+        E(Op("v_andk", (V_T + 1, 1, V_LANE)))
+        E(Op("v_lshl", (V_T + 1, 4, V_T + 1)))
+        E(Op("v_xor", (V_T, V_T, V_T + 1)))
+        for b in range(4):
+            E(Op("s_movk", (S_PICK + b, 0x0C0C000C | (b << 8))))
         E(Op("s_waitcnt_vm", (0,)))
         for q in range(8):
-            E(Op("ds_write_b128", (V_T, 48 + 4 * q, 1024 * q)))
+            E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * LDS_TAB_STRIDE * q)))
         E(Op("s_waitcnt_lgkm_n", (0,)))
     if spec.xcd_remap:
         # w' = base(w % 8) + w / 8 with XCD x owning c_x = q + (x < rem)
@@ -634,9 +648,11 @@ def _lu_solve_and_store(E, spec: KernelSpec):
 
     Blocks are the repair indices t < r; the record embeds the e x e LU of
     C[J, E] (J accepted repairs ascending, E erased sources ascending) into
-    a 16 x 16 byte matrix, column u at byte 16u: byte t < u = U[t][u],
-    byte u = 1 / U[u][u], byte t > u = L[t][u] (0 where t or u is not
-    accepted), then rank[t] at byte 256 + t (0xFF: not accepted).
+    a 16 x 16 byte matrix, column u at byte 16u: byte t < u =
+    U'[t][u] = U[t][u] / U[t][t], byte u = 1 / U[u][u], byte t > u = L[t][u]
+    (0 where t or u is not accepted), then rank[t] at byte 256 + t (0xFF:
+    not accepted).  Forward: y_t ^= L[t][u] y_u (t > u) and y_u /= U[u][u]
+    with the same selectors of y_u; backward: x_t ^= U'[t][u] x_u (t < u).
     Multiplication by a per-lane coefficient c uses the split tables of
     gf256_tables.h from LDS: c * x = T0[x & 7] ^ T1[x >> 3 & 7] ^ T2[x >> 6]
     with v_perm_b32 (four byte lookups per instruction).  The 17 record
@@ -667,8 +683,7 @@ def _lu_solve_and_store(E, spec: KernelSpec):
 
     def table_read(u, byte, buf):
         a, tb = R_TA[buf], R_TB[buf]
-        E(Op("v_bfe", (a, col(u) + byte // 4, 8 * (byte % 4), 8)))
-        E(Op("v_lshl", (a, 5, a)))
+        E(Op("v_perm_s", (a, col(u) + byte // 4, col(u) + byte // 4, S_PICK + byte % 4)))
         E(Op("ds_read_b128", (tb, a, 0)))
         E(Op("ds_read_b32", (tb + 4, a, 16)))
 
@@ -705,8 +720,7 @@ def _lu_solve_and_store(E, spec: KernelSpec):
             if kind == "acc":
                 mul_acc(t, h, buf)
             else:
-                scale(u, h, buf)
-                selectors(u, h)
+                scale(u, h, buf)   # y_u /= U[u][u]; the selectors still hold y_u
             if n + 1 < len(steps) and n + 1 >= guard_from:
                 E(Op("s_cmp_le_k_br", (S_JMAX, steps[n + 1][1], end_label)))
         E(Op("label", (end_label,)))
@@ -724,20 +738,20 @@ def _lu_solve_and_store(E, spec: KernelSpec):
         if not lu:
             E(Op("s_waitcnt_vm", (0,)))
             continue
-        # forward substitution with unit-lower L, column by column
-        for u in range(r - 1):
-            E(Op("s_cmp_le_k_br", (S_JMAX, u + 1, f".Lfwd_end{h}")))
+        # forward substitution with unit-lower L, column by column; each
+        # final y_u is divided by its pivot with the same selectors
+        for u in range(r):
+            E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lfwd_end{h}")))
             E(Op("s_waitcnt_vm", (r - u,)))      # column u (and the ones before) landed
             selectors(u, h)
-            column(u, h, [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}_{h}", 1)
+            column(u, h, [("scale", u)] + [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}_{h}", 1)
         E(Op("label", (f".Lfwd_end{h}",)))
         E(Op("s_waitcnt_vm", (0,)))
-        # backward substitution with U: x_u = y_u / U[u][u], then
-        # y_t ^= U[t][u] x_u for t < u
-        for u in reversed(range(r)):
+        # backward substitution with unit-upper U': y_t ^= U'[t][u] x_u, t < u
+        for u in reversed(range(1, r)):
             E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lbwd{u}_{h}")))
             selectors(u, h)
-            column(u, h, [("scale", u)] + [("acc", t) for t in range(u)], f".Lbwd{u}_{h}", r + 1)
+            column(u, h, [("acc", t) for t in range(u)], f".Lbwd{u}_{h}", r + 1)
     # stores: block t of half h -> recovered row rank[t] of the half's generation
     E(Op("s_nop", (4,)))
     na = 0
@@ -772,7 +786,14 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
     C = cauchy(k, r)
     acc0, ring0 = spec.acc0, spec.ring0
     maps = (spec.map_a, spec.map_b)
-    seq = [("rep", j) for j in range(r)] + [("src", i) for i in range(k)]
+    dec = spec.mode == "dec"
+    # dec: sources first (row 0 initialises the accumulators), then the
+    # repairs, each XORed in byte form right after its block is transposed
+    # back (no transpose of the repair rows themselves)
+    if dec:
+        seq = [("src", i) for i in range(k)] + [("rep", j) for j in range(r)]
+    else:
+        seq = [("rep", j) for j in range(r)] + [("src", i) for i in range(k)]
     ops: list[Op] = []
     E = ops.append
     _prologue(E, spec)
@@ -811,9 +832,10 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
             E(Op("load16", (b + 4 * h, V_ADDR, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
-    dec = spec.mode == "dec"
     if dec:
         _jmax(E, k, r, present)
+        if spec.prio != (0, 0):
+            E(Op("s_setprio", (spec.prio[0],)))
     g0 = spec.guard_min
     n_seq = len(seq)
     for n in range(min(pd, n_seq)):
@@ -824,27 +846,27 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         after = min(pd, n_seq - 1 - n)
         E(Op("s_waitcnt_vm", (2 * after,)))
         base = ring0 + 8 * (n % nbuf)
-        if kind == "rep":
-            if dec and idx >= g0:
-                E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
+        if kind == "rep" and dec:
+            E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
+            ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose))
+            for b in range(8):
+                E(Op("v_xor", (acc0 + 8 * idx + b, acc0 + 8 * idx + b, base + b)))
+            E(Op("label", (f".Lrep{idx}",)))
+        elif kind == "rep":
             ops.extend(_transpose_ops(base, spec.bfi_transpose))
             for b in range(8):
                 E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
-            if dec and idx >= g0:
-                E(Op("label", (f".Lrep{idx}",)))
         else:
-            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose,
-                        guard=(g0, f".Lrow{n}") if dec else None)
-    for j in range(r):
-        if dec and j >= g0:
-            E(Op("s_cmp_le_k_br", (S_JMAX, j, ".Lfin")))
-        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+            _source_row(ops, C, idx, r, base, acc0, init=dec and idx == 0, xor3=spec.xor3,
+                        bfi=spec.bfi_transpose, guard=(g0, f".Lrow{n}") if dec else None)
     if dec:
-        if g0 < r:
-            E(Op("label", (".Lfin",)))
+        if spec.prio != (0, 0):
+            E(Op("s_setprio", (spec.prio[1],)))
         _lu_solve_and_store(E, spec)
         _epilogue_next_item(E, far=True)
         return ops
+    for j in range(r):
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
     E(Op("s_nop", (4,)))
     for j in range(r):
         present(k + j, 0, S_TMP)
@@ -1011,7 +1033,9 @@ def split_tables() -> np.ndarray:
 def lu_record(k: int, r: int, accepted: list[int], E: list[int]) -> np.ndarray:
     """Host restatement of k_decode_prepare_lu's per-generation record: the
     LU factors (no pivoting) of A = C[J, E] with J = accepted repairs
-    ascending and E = erased sources ascending, embedded by repair index
+    ascending and E = erased sources ascending (U with unit diagonal after
+    dividing each row by its pivot; the pivots' inverses on the diagonal),
+    embedded by repair index
     (LU_REC_BYTES bytes; layout in _lu_solve_and_store).  Every leading minor
     of a Cauchy matrix is non-zero, so the factorisation needs no pivoting."""
     J = sorted(accepted)
@@ -1032,7 +1056,7 @@ def lu_record(k: int, r: int, accepted: list[int], E: list[int]) -> np.ndarray:
         rec[256 + t] = b
         for c, u in enumerate(J):
             if b < c:
-                v = A[b][c]
+                v = gf_mul(A[b][c], gf_inv(A[b][b]))    # U'[b][c] = U[b][c] / U[b][b]
             elif b == c:
                 v = gf_inv(A[b][b])
             else:
@@ -1152,7 +1176,7 @@ class Emulator:
             pc += 1
             steps += 1
             n, a = op.name, op.args
-            if n == "label" or n == "s_nop" or n == "s_waitcnt_lgkm":
+            if n == "label" or n == "s_nop" or n == "s_waitcnt_lgkm" or n == "s_setprio":
                 continue
             if n == "s_load_args":
                 for q in range(20):
@@ -1160,15 +1184,17 @@ class Emulator:
             elif n == "s_load_args_dec":
                 for q in range(8):
                     s[56 + q] = int(ka[20 + q])
-            elif n == "v_perm":
+            elif n in ("v_perm", "v_perm_s"):
                 pool = (rv(a[1]) << np.uint64(32)) | rv(a[2])
-                sel = rv(a[3])
+                sel = rv(a[3]) if n == "v_perm" else np.full(64, s[a[3]], np.uint64)
                 res = np.zeros(64, np.uint64)
                 for b in range(4):
                     sb = (sel >> np.uint64(8 * b)) & np.uint64(0xFF)
-                    if (sb >= 8).any():
-                        raise EmuError("v_perm selector outside 0..7")
-                    res |= ((pool >> (sb * np.uint64(8))) & np.uint64(0xFF)) << np.uint64(8 * b)
+                    if ((sb >= 8) & (sb != 12)).any():
+                        raise EmuError("v_perm selector outside 0..7, 12")
+                    byte = np.where(sb == 12, np.uint64(0),
+                                    (pool >> (np.minimum(sb, 7) * np.uint64(8))) & np.uint64(0xFF))
+                    res |= byte << np.uint64(8 * b)
                 wv(a[0], res)
             elif n in ("ds_read_b128", "ds_read_b32"):
                 d, ar, off = a

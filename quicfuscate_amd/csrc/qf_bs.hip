@@ -170,8 +170,10 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
         return hipErrorInvalidValue;
     // the LU record pointer is computed with a 32-bit stride multiply
     if ((uint64_t)G * lu_stride >= (1ull << 40)) return hipErrorInvalidValue;
-    return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, bs_padded_units(L), map_stride,
-                  smap, zero, lu, lu_stride, tab256);
+    // unpadded lane space: the kernel is VALU-bound, padding lanes would be
+    // pure extra work (and the recovered rows are caller memory, payload only)
+    return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, L / 16, map_stride, smap, zero,
+                  lu, lu_stride, tab256);
 }
 
 void bs_unload(BsCache& cache) {

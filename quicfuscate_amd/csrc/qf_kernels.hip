@@ -691,7 +691,6 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
     __shared__ uint8_t J[256], Eidx[256];
     __shared__ uint32_t lA[256], lB[256], lE[256], lF[256];
     __shared__ __attribute__((aligned(16))) uint8_t rec[17 * 16];
-    __shared__ uint8_t Js[16], rank[16], M[16][16], Lf[16][16];
     const uint32_t g = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const uint32_t k = a.k, r = a.r;
@@ -755,87 +754,6 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
     bool dup = false;
     for (uint32_t j = lane; j < r; j += 64) dup |= rep_cnt[j] > 1;
     if (status == 0 && __any(dup)) status = -4;    // QF_ERANK: repeated repair rows
-    if (a.lu_out) {
-        // Fused decode: LU (no pivoting) of A = C[J, E], J = accepted repairs
-        // ascending, E = erased sources ascending.  Every leading minor of a
-        // Cauchy matrix is a Cauchy determinant, non-zero for distinct
-        // points, so Gaussian elimination never meets a zero pivot.
-        if (lane < 16) rank[lane] = 0xFF;
-        __syncthreads();
-        if (status == 0 && e > 0) {
-            uint32_t ne = 0;
-            for (uint32_t i0 = 0; i0 < k; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                const bool miss = i < k && sys_slot[i] == 0xFF;
-                const uint64_t bm = __ballot(miss);
-                if (miss) Eidx[ne + __popcll(bm & lt_mask)] = (uint8_t)i;
-                ne += __popcll(bm);
-            }
-            const bool accj = lane < r && rep_slot[lane] != 0xFF;
-            const uint64_t bj = __ballot(accj);
-            if (accj) {
-                const uint32_t p = __popcll(bj & lt_mask);
-                Js[p] = (uint8_t)lane;
-                rank[lane] = (uint8_t)p;
-            }
-            __syncthreads();
-            for (uint32_t t = lane; t < e * e; t += 64) {
-                const uint32_t b = t / e, c = t - b * e;
-                const uint32_t x = ((k + Js[b]) & 0xFF) ^ Eidx[c];  // != 0: k + j >= k > E
-                M[b][c] = sexp[255 - slog[x]];
-            }
-            for (uint32_t p = 0; p < e; ++p) {
-                __syncthreads();
-                const uint32_t lp = 255 - slog[M[p][p]];  // log of the pivot inverse
-                for (uint32_t i = p + 1 + lane; i < e; i += 64) {
-                    const uint32_t v = M[i][p];
-                    Lf[i][p] = v ? sexp[slog[v] + lp] : 0;
-                }
-                __syncthreads();
-                const uint32_t w = e - p - 1;
-                for (uint32_t t = lane; t < w * w; t += 64) {
-                    const uint32_t i = p + 1 + t / w, c = p + 1 + t % w;
-                    const uint32_t f = Lf[i][p], m = M[p][c];
-                    if (f && m) M[i][c] ^= sexp[slog[f] + slog[m]];
-                }
-            }
-            __syncthreads();
-        }
-        const bool ok = status == 0;
-        uint8_t* lo = a.lu_out + (uint64_t)g * a.lu_stride;
-        for (uint32_t q = lane; q < 272; q += 64) {
-            uint8_t v;
-            if (q >= 256) {
-                v = ok ? rank[q - 256] : 0xFF;
-            } else {
-                const uint32_t u = q >> 4, t = q & 15;
-                v = 0;
-                if (ok && rank[t] != 0xFF && rank[u] != 0xFF) {
-                    const uint32_t b = rank[t], c = rank[u];
-                    if (b < c) v = M[b][c];
-                    else if (b == c) v = sexp[255 - slog[M[b][b]]];
-                    else v = Lf[b][c];
-                }
-            }
-            lo[q] = v;
-        }
-        uint8_t* sm = a.smap + (uint64_t)g * a.map_stride;
-        for (uint32_t q = lane; q < a.map_stride; q += 64) {
-            uint8_t v = 0xFF;
-            if (ok) {
-                if (q < k) v = sys_slot[q];
-                else if (q < k + r) v = rep_slot[q - k];
-            }
-            sm[q] = v;
-        }
-        if (ok)
-            for (uint32_t b = lane; b < e; b += 64) a.rec_index[(uint64_t)g * a.e_max + b] = Eidx[b];
-        if (lane == 0) {
-            a.status[g] = status;
-            a.n_out[g] = ok ? e : 0;
-        }
-        return;
-    }
     if (status == 0 && e > 0) {
         uint32_t ne = 0;
         for (uint32_t i0 = 0; i0 < k; i0 += 64) {
@@ -898,6 +816,188 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
         a.status[g] = status;
         a.n_out[g] = ok ? e : 0;
         a.bound[g] = ok ? bound : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decode control of the fused decode: one wave per generation, kPrepWaves
+// generations per workgroup sharing the log/exp tables.  Acceptance exactly
+// as k_decode_prepare_cauchy (decoder.rs:678-701: first k rows win,
+// duplicate systematic rows ignored); then the packed LU record of C[J, E]
+// in closed form (bs_codegen._lu_solve_and_store has the layout), the slot
+// map, rec_index, n_out and status.  Only wave-local synchronisation after
+// the shared tables are loaded.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPrepWaves = 4;
+
+QF_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+struct PrepWave {
+    uint32_t first[256];     // first slot of systematic index i (0xFFFFFFFF none)
+    uint32_t rep_cnt[16];
+    uint8_t sys_slot[256];   // accepted slot of source i (0xFF none)
+    uint8_t rep_slot[16];    // accepted slot of repair j
+    uint8_t Js[16], rank[16], Eidx[16];
+    uint8_t LU[16][16];
+};
+
+__global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCauchyArgs a) {
+    __shared__ uint8_t sexp[512];
+    __shared__ uint8_t slog[256];
+    __shared__ PrepWave pw[kPrepWaves];
+    for (uint32_t i = threadIdx.x; i < 768; i += blockDim.x) {
+        if (i < 512) sexp[i] = a.explog[i];
+        else slog[i - 512] = a.explog[i];
+    }
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t g = blockIdx.x * kPrepWaves + w;
+    if (g >= a.G) return;  // no block-wide barrier below
+    PrepWave& P = pw[w];
+    const uint32_t k = a.k, r = a.r;
+    for (uint32_t i = lane; i < 256; i += 64) {
+        P.first[i] = 0xFFFFFFFFu;
+        P.sys_slot[i] = 0xFF;
+    }
+    if (lane < 16) {
+        P.rep_slot[lane] = 0xFF;
+        P.rep_cnt[lane] = 0;
+        P.rank[lane] = 0xFF;
+    }
+    wave_sync();
+    const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
+    const uint16_t* ridx = a.row_index + (uint64_t)g * a.max_rows;
+    bool bad = false;
+    for (uint32_t s = lane; s < n; s += 64) {
+        const uint32_t idx = ridx[s];
+        if (idx < k) atomicMin(&P.first[idx], s);
+        else if (idx - k >= r) bad = true;
+    }
+    wave_sync();
+    int32_t status = __any(bad) ? -1 : 0;  // QF_EINVAL
+    uint32_t accepted = 0, nrep = 0;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t s0 = 0; s0 < n && accepted < k; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        uint32_t idx = 0;
+        bool cand = false;
+        if (s < n) {
+            idx = ridx[s];
+            cand = idx >= k ? (idx - k < r) : (P.first[idx] == s);
+        }
+        const uint64_t bc = __ballot(cand);
+        const uint32_t pos = accepted + __popcll(bc & lt_mask);
+        const bool acc = cand && pos < k;
+        const bool isrep = acc && idx >= k;
+        if (acc) {
+            if (idx < k) {
+                P.sys_slot[idx] = (uint8_t)s;
+            } else {
+                P.rep_slot[idx - k] = (uint8_t)s;
+                atomicAdd(&P.rep_cnt[idx - k], 1u);
+            }
+        }
+        accepted += __popcll(__ballot(acc));
+        nrep += __popcll(__ballot(isrep));
+    }
+    wave_sync();
+    const uint32_t e = nrep;
+    if (status == 0 && accepted < k) status = -3;  // QF_ENOTREADY
+    const bool dup = lane < r && P.rep_cnt[lane] > 1;
+    if (status == 0 && __any(dup)) status = -4;    // QF_ERANK: repeated repair rows
+    const bool ok = status == 0;
+    if (ok && e > 0) {
+        uint32_t ne = 0;
+        for (uint32_t i0 = 0; i0 < k; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool miss = i < k && P.sys_slot[i] == 0xFF;
+            const uint64_t bm = __ballot(miss);
+            if (miss) P.Eidx[ne + __popcll(bm & lt_mask)] = (uint8_t)i;
+            ne += __popcll(bm);
+        }
+        const bool accj = lane < r && P.rep_slot[lane] != 0xFF;
+        const uint64_t bj = __ballot(accj);
+        if (accj) {
+            const uint32_t p = __popcll(bj & lt_mask);
+            P.Js[p] = (uint8_t)lane;
+            P.rank[lane] = (uint8_t)p;
+        }
+        wave_sync();
+        // closed-form LU of A[b][c] = 1 / (x_b + y_c) (see k_decode_prepare_cauchy)
+        for (uint32_t t = lane; t < e * e; t += 64) {
+            const uint32_t i = t / e, j = t - i * e;
+            const uint32_t xi = (k + P.Js[i]) & 0xFF, xj = (k + P.Js[j]) & 0xFF;
+            const uint32_t yj = P.Eidx[j];
+            int32_t l;
+            if (i > j) {
+                l = (int32_t)slog[xj ^ yj] - (int32_t)slog[xi ^ yj];
+                for (uint32_t q = 0; q < j; ++q) {
+                    const uint32_t xq = (k + P.Js[q]) & 0xFF, yq = P.Eidx[q];
+                    l += (int32_t)slog[xi ^ xq] + (int32_t)slog[xj ^ yq] - (int32_t)slog[xj ^ xq] -
+                         (int32_t)slog[xi ^ yq];
+                }
+            } else if (i == j) {
+                l = (int32_t)slog[xi ^ yj];
+                for (uint32_t q = 0; q < i; ++q) {
+                    const uint32_t xq = (k + P.Js[q]) & 0xFF, yq = P.Eidx[q];
+                    l -= (int32_t)slog[xi ^ xq] + (int32_t)slog[yj ^ yq] - (int32_t)slog[xi ^ yq] -
+                         (int32_t)slog[xq ^ yj];
+                }
+            } else {
+                const uint32_t yi = P.Eidx[i];
+                l = (int32_t)slog[xi ^ yi] - (int32_t)slog[xi ^ yj];
+                for (uint32_t q = 0; q < i; ++q) {
+                    const uint32_t xq = (k + P.Js[q]) & 0xFF, yq = P.Eidx[q];
+                    l += (int32_t)slog[yj ^ yq] + (int32_t)slog[xq ^ yi] - (int32_t)slog[xq ^ yj] -
+                         (int32_t)slog[yi ^ yq];
+                }
+            }
+            l %= 255;
+            if (l < 0) l += 255;
+            P.LU[i][j] = sexp[l];
+        }
+        wave_sync();
+    }
+    // record: 16 columns x 16 bytes, then 16 rank bytes; 17 x 16 bytes, one
+    // 16-byte store per lane
+    uint8_t* lo = a.lu_out + (uint64_t)g * a.lu_stride;
+    if (lane < 17) {
+        uint32_t wd[4];
+        for (uint32_t q = 0; q < 4; ++q) {
+            uint32_t v = 0;
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t t = 4 * q + b;
+                uint32_t x;
+                if (lane == 16) {
+                    x = ok ? P.rank[t] : 0xFF;
+                } else {
+                    const uint32_t u = lane;
+                    x = (ok && P.rank[t] != 0xFF && P.rank[u] != 0xFF) ? P.LU[P.rank[t]][P.rank[u]] : 0;
+                }
+                v |= x << (8 * b);
+            }
+            wd[q] = v;
+        }
+        *reinterpret_cast<uint4*>(lo + 16 * lane) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
+    uint8_t* sm = a.smap + (uint64_t)g * a.map_stride;
+    for (uint32_t q = lane; q < a.map_stride; q += 64) {
+        uint8_t v = 0xFF;
+        if (ok) {
+            if (q < k) v = P.sys_slot[q];
+            else if (q < k + r) v = P.rep_slot[q - k];
+        }
+        sm[q] = v;
+    }
+    if (ok)
+        for (uint32_t b = lane; b < e; b += 64) a.rec_index[(uint64_t)g * a.e_max + b] = P.Eidx[b];
+    if (lane == 0) {
+        a.status[g] = status;
+        a.n_out[g] = ok ? e : 0;
     }
 }
 
@@ -1068,7 +1168,12 @@ hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st) {
 hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st) {
     if (a.G == 0) return hipSuccess;
     if (a.r > 16 || a.k + a.r > 256 || a.max_rows > 255 || a.map_stride < a.k + a.r) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_decode_prepare_cauchy, dim3(a.G), dim3(64), 0, st, a);
+    if (a.lu_out) {
+        const uint32_t blocks = (a.G + kPrepWaves - 1) / kPrepWaves;
+        hipLaunchKernelGGL(k_decode_prepare_lu, dim3(blocks), dim3(64 * kPrepWaves), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(k_decode_prepare_cauchy, dim3(a.G), dim3(64), 0, st, a);
+    }
     return hipGetLastError();
 }
 

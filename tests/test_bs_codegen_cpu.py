@@ -356,7 +356,8 @@ def test_lu_record_reconstructs_cauchy_submatrix():
         for t in range(16):
             assert rec[256 + t] == (Js.index(t) if t in Js else 0xFF)
         Lm = [[1 if b == c else (rec[16 * Js[c] + Js[b]] if b > c else 0) for c in range(e)] for b in range(e)]
-        Um = [[(bs.gf_inv(rec[16 * Js[c] + Js[b]]) if b == c else rec[16 * Js[c] + Js[b]]) if b <= c else 0
+        piv = [bs.gf_inv(rec[16 * Js[b] + Js[b]]) for b in range(e)]    # U[b][b]
+        Um = [[(piv[b] if b == c else bs.gf_mul(rec[16 * Js[c] + Js[b]], piv[b])) if b <= c else 0
                for c in range(e)] for b in range(e)]
         for b in range(e):
             for c in range(e):
@@ -364,3 +365,10 @@ def test_lu_record_reconstructs_cauchy_submatrix():
                 for q in range(e):
                     acc ^= bs.gf_mul(Lm[b][q], Um[q][c])
                 assert acc == bs.gf_inv(((k + Js[b]) & 0xFF) ^ E[c])
+
+
+def test_emulated_fused_decode_unpadded_lanes(oracle):
+    """The library launches the fused decode over the unpadded lane space
+    (L/16 units per row): halves of a lane straddle generations."""
+    assert _dec_case(oracle, 8, 4, 2, 80, 9, 6, None, padded=False) == 0
+    assert _dec_case(oracle, 16, 16, 3, 1200, 2, 7, 13, padded=False) == 0

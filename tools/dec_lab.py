@@ -29,9 +29,8 @@ VARIANTS = [
     ("warm", {}, ()),
     ("full", {}, ()),
     ("nolu", {"lu": False}, ()),
-    ("noguard", {"guard_min": 16}, ()),
-    ("nolu_noguard", {"lu": False, "guard_min": 16}, ()),
-    ("noload", {}, ("noload",)),
+    ("prio_main", {"prio": (2, 0)}, ()),
+    ("prio_lu", {"prio": (0, 2)}, ()),
     ("full_2", {}, ()),
 ]
 
@@ -47,7 +46,9 @@ def build():
         old.unlink()
     man = []
     for name, kw, flags in VARIANTS:
-        spec = bs.KernelSpec(64, 16, 3, "dec", **kw)
+        kw2 = dict(kw)
+        pd = kw2.pop("pd", 3)
+        spec = bs.KernelSpec(64, 16, pd, "dec", **kw2)
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"dec_{name}", text.replace(spec.name, f"dec_{name}"), OUT)
         man.append({"name": name, "hsaco": h.name, "symbol": f"dec_{name}", "kw": kw, "flags": list(flags),
@@ -98,7 +99,7 @@ def run(G, reps):
         buf = ctypes.create_string_buffer(data, len(data))
         assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
-        Lv = bs.padded_units(L)
+        Lv = None
         _, _, n_items = bs.launch_geometry(L, G, Lv)
         blocks = (n_items + 3) // 4
         ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * L, e * L, L, L, L, G, blocks * 4,
