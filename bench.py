@@ -273,17 +273,24 @@ def main(argv=None):
         return enc_bytes
 
     dom = max(kern_step_ms, key=kern_step_ms.get)
-    dom_ms = kern_ms[dom]
-    achieved = alg_bytes(dom) / (dom_ms / 1e3) / 1e9
-    traffic = None
     tfile = REPO / "profiles" / "traffic.json"
-    if tfile.exists():
-        try:
-            tj = json.loads(tfile.read_text()).get(dom, {})
-            if tj.get("k") == k and tj.get("r") == r and tj.get("L") == Lb and tj.get("G") == G:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+
+    def roofline(name):
+        ms = kern_ms[name]
+        achieved = alg_bytes(name) / (ms / 1e3) / 1e9
+        traffic = None
+        if tfile.exists():
+            try:
+                tj = json.loads(tfile.read_text()).get(name, {})
+                if tj.get("k") == k and tj.get("r") == r and tj.get("L") == Lb and tj.get("G") == G:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        return {"kernel": name, "launch_ms": round(ms, 4), "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": PEAK_HBM_GBPS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
+                "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes(name)}
+
+    enc_kernel = next((n for n in kern_ms if n.startswith(("qf_cauchy_bs", "k_combine_uniform"))), None)
 
     out = {
         "metric": "GF(256) RLNC encode+decode GiB/s device-resident, 1200B pkts gen=64, 1/2/4/8 GPU",
@@ -311,17 +318,12 @@ def main(argv=None):
         "decode_hbm_gbps": round(dec_bytes / (dec_ms / 1e3) / 1e9, 1),
         "kernel_ms_per_launch": {n: round(v, 4) for n, v in kern_ms.items()},
         "kernel_gbps": {n: round(alg_bytes(n) / (v / 1e3) / 1e9, 1) for n, v in kern_ms.items()},
-        "roofline": {
-            "kernel": dom,
-            "launch_ms": round(dom_ms, 4),
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": PEAK_HBM_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved / PEAK_HBM_GBPS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": alg_bytes(dom),
-        },
+        # dominant kernel (largest time per step); the fused decode is
+        # VALU-issue-bound, its HBM fraction is reported as measured
+        # (profiles/ SQ counters)
+        "roofline": roofline(dom),
+        # the encode kernel BASELINE.json's north star targets (>= 70 % HBM)
+        "roofline_encode": roofline(enc_kernel) if enc_kernel else None,
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,
         "repair_xor_fold_by_rank": [f"{f:016x}" for f in folds],

@@ -273,6 +273,8 @@ class KernelSpec:
     lu: bool = True
     # dec mode: wave priority (s_setprio) of the row loop / the LU phase
     prio: tuple = (0, 0)
+    # lab only: drop the payload row loads (keeps maps, records, compute)
+    lab_norows: bool = False
 
     @property
     def name(self) -> str:
@@ -829,7 +831,8 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
             E(Op("v_cndmask", (V_ADDR, z, V_ADDR, S_TMP)))
             E(Op("v_cndmask", (V_ADDR + 1, z + 1, V_ADDR + 1, S_TMP)))
             E(Op("s_exec", (vm,)))
-            E(Op("load16", (b + 4 * h, V_ADDR, 0, spec.ld_policy)))
+            if not spec.lab_norows:
+                E(Op("load16", (b + 4 * h, V_ADDR, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
     if dec:
@@ -844,7 +847,7 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         if n + pd < n_seq:
             load_row(n + pd)
         after = min(pd, n_seq - 1 - n)
-        E(Op("s_waitcnt_vm", (2 * after,)))
+        E(Op("s_waitcnt_vm", (0 if spec.lab_norows else 2 * after,)))
         base = ring0 + 8 * (n % nbuf)
         if kind == "rep" and dec:
             E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))

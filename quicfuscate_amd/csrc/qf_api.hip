@@ -375,7 +375,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     pa.lu_stride = lu_stride;
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
-    prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
+    prof_end(ctx, st, ev, "k_decode_prepare_lu");
     ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,

@@ -29,8 +29,8 @@ VARIANTS = [
     ("warm", {}, ()),
     ("full", {}, ()),
     ("nolu", {"lu": False}, ()),
-    ("prio_main", {"prio": (2, 0)}, ()),
-    ("prio_lu", {"prio": (0, 2)}, ()),
+    ("norows", {"lab_norows": True}, ()),
+    ("nolu_norows", {"lu": False, "lab_norows": True}, ()),
     ("full_2", {}, ()),
 ]
 

@@ -19,7 +19,8 @@ import json
 from collections import defaultdict
 from pathlib import Path
 
-OUR_KERNELS = ("qf_cauchy_bs_", "qf_cauchy_syn_", "k_combine_uniform", "k_combine_slots", "k_decode_prepare", "k_mul_slice")
+OUR_KERNELS = ("qf_cauchy_bs_", "qf_cauchy_syn_", "qf_cauchy_dec_", "k_combine_uniform", "k_combine_slots",
+               "k_decode_prepare", "k_mul_slice")
 
 
 def per_dispatch(root: Path, counter: str) -> dict[str, list[float]]:
