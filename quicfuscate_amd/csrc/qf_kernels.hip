@@ -852,13 +852,23 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
         if (i < 512) sexp[i] = a.explog[i];
         else slog[i - 512] = a.explog[i];
     }
-    __syncthreads();
+    __syncthreads();  // the only block-wide barrier
     const uint32_t w = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t g = blockIdx.x * kPrepWaves + w;
-    if (g >= a.G) return;  // no block-wide barrier below
     PrepWave& P = pw[w];
     const uint32_t k = a.k, r = a.r;
+    // persistent: each wave takes generations blockIdx*4 + w, + gridDim*4, ...
+    for (uint32_t g = blockIdx.x * kPrepWaves + w; g < a.G; g += gridDim.x * kPrepWaves) {
+    // the row indices of this generation stay in registers (max_rows <= 255:
+    // four slots per lane)
+    const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
+    uint32_t idxs[4] = {0xFFFF, 0xFFFF, 0xFFFF, 0xFFFF};
+    {
+        const uint16_t* ridx = a.row_index + (uint64_t)g * a.max_rows;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            if (lane + 64 * q < n) idxs[q] = ridx[lane + 64 * q];
+    }
     for (uint32_t i = lane; i < 256; i += 64) {
         P.first[i] = 0xFFFFFFFFu;
         P.sys_slot[i] = 0xFF;
@@ -867,28 +877,27 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
         P.rep_slot[lane] = 0xFF;
         P.rep_cnt[lane] = 0;
         P.rank[lane] = 0xFF;
+        P.Js[lane] = 0;
+        P.Eidx[lane] = 0;
     }
     wave_sync();
-    const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
-    const uint16_t* ridx = a.row_index + (uint64_t)g * a.max_rows;
     bool bad = false;
-    for (uint32_t s = lane; s < n; s += 64) {
-        const uint32_t idx = ridx[s];
-        if (idx < k) atomicMin(&P.first[idx], s);
-        else if (idx - k >= r) bad = true;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t s = lane + 64 * q, idx = idxs[q];
+        if (s < n) {
+            if (idx < k) atomicMin(&P.first[idx], s);
+            else if (idx - k >= r) bad = true;
+        }
     }
     wave_sync();
     int32_t status = __any(bad) ? -1 : 0;  // QF_EINVAL
     uint32_t accepted = 0, nrep = 0;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t s0 = 0; s0 < n && accepted < k; s0 += 64) {
-        const uint32_t s = s0 + lane;
-        uint32_t idx = 0;
-        bool cand = false;
-        if (s < n) {
-            idx = ridx[s];
-            cand = idx >= k ? (idx - k < r) : (P.first[idx] == s);
-        }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t s = lane + 64 * q, idx = idxs[q];
+        const bool cand = s < n && (idx >= k ? (idx - k < r) : (P.first[idx] == s));
         const uint64_t bc = __ballot(cand);
         const uint32_t pos = accepted + __popcll(bc & lt_mask);
         const bool acc = cand && pos < k;
@@ -927,34 +936,47 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
             P.rank[lane] = (uint8_t)p;
         }
         wave_sync();
-        // closed-form LU of A[b][c] = 1 / (x_b + y_c) (see k_decode_prepare_cauchy)
-        for (uint32_t t = lane; t < e * e; t += 64) {
-            const uint32_t i = t / e, j = t - i * e;
-            const uint32_t xi = (k + P.Js[i]) & 0xFF, xj = (k + P.Js[j]) & 0xFF;
-            const uint32_t yj = P.Eidx[j];
+        // closed-form LU of A[b][c] = 1 / (x_b + y_c) (formulas at
+        // k_decode_prepare_cauchy); x, y held in registers, so every log
+        // lookup of an entry is independent of the others
+        uint32_t X[16], Y[16];
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q) {
+            X[q] = (k + P.Js[q]) & 0xFF;
+            Y[q] = P.Eidx[q];
+        }
+#pragma unroll
+        for (uint32_t pass = 0; pass < 4; ++pass) {
+            const uint32_t t = lane + 64 * pass, i = t >> 4, j = t & 15;
+            if (i >= e || j >= e) continue;
+            uint32_t xi = 0, xj = 0, yi = 0, yj = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 16; ++q) {
+                if (q == i) { xi = X[q]; yi = Y[q]; }
+                if (q == j) { xj = X[q]; yj = Y[q]; }
+            }
             int32_t l;
             if (i > j) {
                 l = (int32_t)slog[xj ^ yj] - (int32_t)slog[xi ^ yj];
-                for (uint32_t q = 0; q < j; ++q) {
-                    const uint32_t xq = (k + P.Js[q]) & 0xFF, yq = P.Eidx[q];
-                    l += (int32_t)slog[xi ^ xq] + (int32_t)slog[xj ^ yq] - (int32_t)slog[xj ^ xq] -
-                         (int32_t)slog[xi ^ yq];
-                }
+#pragma unroll
+                for (uint32_t q = 0; q < 15; ++q)
+                    if (q < j)
+                        l += (int32_t)slog[xi ^ X[q]] + (int32_t)slog[xj ^ Y[q]] - (int32_t)slog[xj ^ X[q]] -
+                             (int32_t)slog[xi ^ Y[q]];
             } else if (i == j) {
                 l = (int32_t)slog[xi ^ yj];
-                for (uint32_t q = 0; q < i; ++q) {
-                    const uint32_t xq = (k + P.Js[q]) & 0xFF, yq = P.Eidx[q];
-                    l -= (int32_t)slog[xi ^ xq] + (int32_t)slog[yj ^ yq] - (int32_t)slog[xi ^ yq] -
-                         (int32_t)slog[xq ^ yj];
-                }
+#pragma unroll
+                for (uint32_t q = 0; q < 15; ++q)
+                    if (q < i)
+                        l -= (int32_t)slog[xi ^ X[q]] + (int32_t)slog[yj ^ Y[q]] - (int32_t)slog[xi ^ Y[q]] -
+                             (int32_t)slog[X[q] ^ yj];
             } else {
-                const uint32_t yi = P.Eidx[i];
                 l = (int32_t)slog[xi ^ yi] - (int32_t)slog[xi ^ yj];
-                for (uint32_t q = 0; q < i; ++q) {
-                    const uint32_t xq = (k + P.Js[q]) & 0xFF, yq = P.Eidx[q];
-                    l += (int32_t)slog[yj ^ yq] + (int32_t)slog[xq ^ yi] - (int32_t)slog[xq ^ yj] -
-                         (int32_t)slog[yi ^ yq];
-                }
+#pragma unroll
+                for (uint32_t q = 0; q < 15; ++q)
+                    if (q < i)
+                        l += (int32_t)slog[yj ^ Y[q]] + (int32_t)slog[X[q] ^ yi] - (int32_t)slog[X[q] ^ yj] -
+                             (int32_t)slog[yi ^ Y[q]];
             }
             l %= 255;
             if (l < 0) l += 255;
@@ -998,6 +1020,8 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
     if (lane == 0) {
         a.status[g] = status;
         a.n_out[g] = ok ? e : 0;
+    }
+    wave_sync();  // P is rewritten for the next generation
     }
 }
 
@@ -1169,6 +1193,8 @@ hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t 
     if (a.G == 0) return hipSuccess;
     if (a.r > 16 || a.k + a.r > 256 || a.max_rows > 255 || a.map_stride < a.k + a.r) return hipErrorInvalidValue;
     if (a.lu_out) {
+        // one generation per wave (a persistent grid measured slower: the
+        // kernel is LDS/VALU-issue-bound per CU, not launch-bound)
         const uint32_t blocks = (a.G + kPrepWaves - 1) / kPrepWaves;
         hipLaunchKernelGGL(k_decode_prepare_lu, dim3(blocks), dim3(64 * kPrepWaves), 0, st, a);
     } else {
