@@ -111,6 +111,16 @@ int cpu_encode_avx2(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_
                     uint8_t *rep, uint32_t threads);
 int cpu_has_avx2(void);
 
+/* ---- GF(2^16) Extreme mode (qf_oracle16.c) ----------------------------- */
+uint16_t oracle_gf16_mul(uint16_t a, uint16_t b);
+int oracle_gf16_inv(uint16_t a, uint16_t *out);
+int oracle_cauchy16(uint32_t k, uint32_t r, uint16_t *out_rxk);
+int oracle_encode16(uint32_t k, uint32_t r, uint32_t L, const uint8_t *src, size_t src_stride,
+                    const uint16_t *coeff, uint8_t *rep, size_t rep_stride);
+int oracle_decode16(uint32_t k, uint32_t L, uint32_t n_rows, const uint16_t *row_index,
+                    const uint8_t *rows, size_t row_stride, const uint16_t *row_coeffs,
+                    uint8_t *out, size_t out_stride, uint8_t *received_mask);
+
 #ifdef __cplusplus
 }
 #endif

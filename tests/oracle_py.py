@@ -143,3 +143,49 @@ def fill_splitmix(n: int, seed: int, word_offset: int = 0) -> np.ndarray:
     out = np.zeros(n, np.uint8)
     _lib.oracle_fill_splitmix(_p(out), n, seed, word_offset)
     return out
+
+
+# ---- GF(2^16) Extreme mode (oracle/qf_oracle16.c) ---------------------------
+_lib.oracle_gf16_mul.restype = ctypes.c_uint16
+_lib.oracle_gf16_mul.argtypes = [ctypes.c_uint16, ctypes.c_uint16]
+_lib.oracle_gf16_inv.argtypes = [ctypes.c_uint16, _P]
+_lib.oracle_cauchy16.argtypes = [_U32, _U32, _P]
+_lib.oracle_encode16.argtypes = [_U32, _U32, _U32, _P, _SZ, _P, _P, _SZ]
+_lib.oracle_decode16.argtypes = [_U32, _U32, _U32, _P, _P, _SZ, _P, _P, _SZ, _P]
+
+
+def mul16(a: int, b: int) -> int:
+    return int(_lib.oracle_gf16_mul(a, b))
+
+
+def inv16(a: int) -> int | None:
+    o = ctypes.c_uint16()
+    return None if _lib.oracle_gf16_inv(a, ctypes.byref(o)) else int(o.value)
+
+
+def cauchy16(k: int, r: int) -> np.ndarray | None:
+    out = np.zeros((r, k), np.uint16)
+    return None if _lib.oracle_cauchy16(k, r, _p(out)) else out
+
+
+def encode16(src: np.ndarray, r: int, coeff: np.ndarray | None = None) -> np.ndarray:
+    """src: (k, L) uint8 -> (r, L) repairs (big-endian u16 symbols)."""
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    k, L = src.shape
+    rep = np.zeros((r, L), np.uint8)
+    c = None if coeff is None else np.ascontiguousarray(coeff, dtype=np.uint16)
+    s = _lib.oracle_encode16(k, r, L, _p(src), L, _p(c), _p(rep), L)
+    assert s == 0, s
+    return rep
+
+
+def decode16(k: int, row_index, rows: np.ndarray, row_coeffs: np.ndarray | None = None):
+    """rows: (n, L) in arrival order -> (status, out (k, L), received mask)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    n, L = rows.shape
+    ri = np.ascontiguousarray(row_index, dtype=np.uint16)
+    out = np.zeros((k, max(L, 1)), np.uint8)
+    mask = np.zeros(k, np.uint8)
+    rc = None if row_coeffs is None else np.ascontiguousarray(row_coeffs, dtype=np.uint16)
+    s = _lib.oracle_decode16(k, L, n, _p(ri), _p(rows), L, _p(rc), _p(out), out.shape[1], _p(mask))
+    return s, out[:, :L], mask
