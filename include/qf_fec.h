@@ -355,6 +355,40 @@ int qf_parse_frames_dev(qf_ctx *ctx, uint32_t k, uint32_t r, uint32_t L, uint32_
                         uint32_t *n_rows_dev, int32_t *frame_status_dev);
 
 /* ---------------------------------------------------------------------------
+ * GF(2^16) "Extreme mode" codec.
+ * replaces gf_tables.rs:331-380 (gf16_mul / gf16_pow / gf16_inv / gf16_mul_add)
+ * and decoder.rs:10-88 (Encoder16), 536-656 (Decoder16).  Field mod 0x1100B
+ * with the reduction gf16_mul intends (as written its u16 test of bit 16
+ * never fires).  Payload symbols are big-endian u16 byte pairs
+ * (decoder.rs:42-54); L must be even.
+ * ------------------------------------------------------------------------- */
+/* gf_tables.rs:333 gf16_mul (host helper) */
+uint16_t qf_gf16_mul(uint16_t a, uint16_t b);
+/* gf_tables.rs:370 gf16_inv; QF_ERANGE for 0 (the reference panics) */
+int qf_gf16_inv(uint16_t a, uint16_t *out);
+/* decoder.rs:77-80: out[j*k + i] = gf16_inv((u16)i ^ (u16)(k + j));
+ * QF_ERANGE when k + r > 65536 (gf16_inv(0)). */
+int qf_cauchy16_coeffs(uint32_t k, uint32_t r, uint16_t *out_rxk);
+/* replaces decoder.rs:21-75 Encoder16::generate_repair_packet for r repairs
+ * of G generations (layout as qf_encode_batch, shape->flags must be 0);
+ * coeff_rxk: host u16 r x k matrix or NULL for the Cauchy rows. */
+int qf_encode16_batch(qf_ctx *ctx, const qf_encode_shape *shape, uint32_t G, const uint8_t *src_dev,
+                      uint8_t *rep_dev, const uint16_t *coeff_rxk);
+/* replaces decoder.rs:563-656 Decoder16::{add_packet, try_decode,
+ * get_decoded_packets} for G generations (layout as qf_decode_batch).
+ * Acceptance as Decoder16: the first k rows, row index < k = systematic
+ * column (the reference's id % k), no duplicate filtering (a duplicated
+ * column is singular: QF_ERANK).  row_coeffs_dev: NULL (row index k + j
+ * carries Cauchy row j; r only sizes the output) or k u16 per slot at (g*max_rows + slot)*k (the
+ * packet's big-endian coefficient block, converted).  min(k, r) <= 64,
+ * k <= 4096, max_rows <= 8192 (QF_EINVAL beyond).  Recovered rows: erased
+ * sources ascending, with rec_index / n_rec / status as qf_decode_batch. */
+int qf_decode16_batch(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G, const uint8_t *rows_dev,
+                      const uint16_t *row_index_dev, const uint32_t *n_rows_dev,
+                      const uint16_t *row_coeffs_dev, uint8_t *rec_dev, uint16_t *rec_index_dev,
+                      uint32_t *n_rec_dev, int32_t *status_dev);
+
+/* ---------------------------------------------------------------------------
  * Synthetic payload (bench / tests): byte t of the region is byte (t & 7) of
  * splitmix64(seed + word_offset + t/8), little endian.  Device kernel.
  * ------------------------------------------------------------------------- */

@@ -20,6 +20,7 @@
 #include "qf_fec.h"
 #include "qf_kernels.h"
 #include "qf_bs.h"
+#include "qf_internal.h"
 
 namespace qf {
 const Gf256& gf() {
@@ -75,6 +76,9 @@ struct qf_ctx {
     size_t stage_src_bytes = 0, stage_rep_bytes = 0;
     // bit-sliced Cauchy kernels (loaded on first use)
     qf::BsCache bs;
+    // GF(2^16) log / exp tables (qf_gf16.hip, built on first use)
+    uint16_t* d_gf16_log = nullptr;
+    uint16_t* d_gf16_exp = nullptr;
     // kernel timing (qf_ctx_profile)
     struct ProfPending {
         size_t slot;
@@ -503,6 +507,48 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
 }  // namespace
 
 namespace qf {
+int ctx_lock(qf_ctx* ctx, std::unique_lock<std::mutex>& lk) {
+    lk = std::unique_lock<std::mutex>(ctx->mu);
+    return ensure_device(ctx);
+}
+hipStream_t ctx_stream(qf_ctx* ctx) { return ctx->stream; }
+int ctx_num_cus(qf_ctx* ctx) { return ctx->num_cus; }
+int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
+    int s = grow_work(ctx, bytes);
+    if (s) return s;
+    *out = ctx->d_work;
+    return QF_OK;
+}
+int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp) {
+    if (!ctx->d_gf16_log) {
+        std::vector<uint16_t> lg(65536, 0), ex(2 * 65535);
+        uint32_t x = 1;
+        for (uint32_t i = 0; i < 65535; ++i) {  // generator 2 of GF(2^16) mod 0x1100B
+            ex[i] = ex[i + 65535] = (uint16_t)x;
+            lg[x] = (uint16_t)i;
+            x <<= 1;
+            if (x & 0x10000u) x ^= 0x1100Bu;
+        }
+        uint16_t *dl = nullptr, *de = nullptr;
+        if (hipMalloc(&dl, lg.size() * 2) != hipSuccess) return QF_ENOMEM;
+        if (hipMalloc(&de, ex.size() * 2) != hipSuccess) {
+            hipFree(dl);
+            return QF_ENOMEM;
+        }
+        QF_CHECK_HIP(hipMemcpy(dl, lg.data(), lg.size() * 2, hipMemcpyHostToDevice));
+        QF_CHECK_HIP(hipMemcpy(de, ex.data(), ex.size() * 2, hipMemcpyHostToDevice));
+        ctx->d_gf16_log = dl;
+        ctx->d_gf16_exp = de;
+    }
+    *log = ctx->d_gf16_log;
+    *exp = ctx->d_gf16_exp;
+    return QF_OK;
+}
+hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st) { return prof_begin(ctx, st); }
+void ctx_prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t ev, const std::string& name) {
+    prof_end(ctx, st, ev, name);
+}
+
 hipError_t launch_frame_batch(const uint8_t* src, const uint8_t* rep, const qf_encode_shape& sh, uint32_t G,
                               uint8_t* frames, uint64_t frame_stride, uint32_t* frame_len,
                               const uint8_t* explog, int num_cus, hipStream_t st);
@@ -604,6 +650,8 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->custom_done) hipEventDestroy(c->custom_done);
     if (c->d_work) hipFree(c->d_work);
     if (c->d_zero) hipFree(c->d_zero);
+    if (c->d_gf16_log) hipFree(c->d_gf16_log);
+    if (c->d_gf16_exp) hipFree(c->d_gf16_exp);
     if (c->aux) {
         hipStreamSynchronize(c->aux);
         hipStreamDestroy(c->aux);

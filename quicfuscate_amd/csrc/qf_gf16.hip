@@ -1,0 +1,857 @@
+// qf_gf16.hip -- the GF(2^16) "Extreme mode" codec on the device
+// (SURVEY 8(f) rank 3): Encoder16 / Decoder16 of decoder.rs:10-88 and
+// 536-656 over gf_tables.rs:331-380, batched like the GF(2^8) path.
+//
+// Field: GF(2^16) mod 0x1100B (primitive; generator 2), multiplication as
+// gf16_mul intends it (gf_tables.rs:333-353).  Symbols are
+// big-endian u16 pairs of payload bytes (decoder.rs:42-54); L must be even.
+//
+// Multiplication by a coefficient c is exp[log c + log x] with the exp
+// table in LDS (128 KB, one period) and the log table read from global
+// memory (L2-resident, 128 KB).  log x of a payload symbol is computed once
+// per row and reused for every coefficient applied to it.
+//
+//   k_encode16          repairs of G generations, up to 8 repairs per pass
+//   k_decode16_prepare  acceptance exactly as Decoder16::add_packet
+//                       (decoder.rs:563-592: the first k rows, systematic
+//                       column id % k, no duplicate filtering), Gauss-Jordan
+//                       inverse of the erased-column block (e <= 64) in LDS,
+//                       per-slot recovery coefficients W = C[J,E]^-1 [I | C[J,S]]
+//   k_combine16         recovered rows = W x received rows
+// Deviation from Decoder16 (as for GF(2^8)): systematic rows carry
+// their payloads, so the recovered bytes are the original bytes; decoding
+// happens whenever k rows are present (Decoder16 only tries after a repair
+// row, decoder.rs:592, so a generation whose k-th row is systematic never
+// decodes there).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+#include "qf_fec.h"
+#include "qf_internal.h"
+
+namespace {
+
+#define QF_DEV __device__ __forceinline__
+
+constexpr uint32_t kOrder = 65535;  // multiplicative group order
+constexpr uint32_t kNoLog = 0xFFFF; // log of 0 (no product)
+constexpr uint32_t kEMax = 64;      // erasures per generation the decode handles
+constexpr int kR16 = 8;             // outputs per pass (encode and combine)
+constexpr int kThreads16 = 512;
+
+// ---- host arithmetic ------------------------------------------------------
+uint16_t h_mul(uint16_t a, uint16_t b) {
+    uint32_t aa = a, res = 0;
+    while (b) {
+        if (b & 1) res ^= aa;
+        b >>= 1;
+        aa <<= 1;
+        if (aa & 0x10000u) aa ^= 0x1100Bu;
+    }
+    return (uint16_t)res;
+}
+
+bool h_inv(uint16_t a, uint16_t* out) {
+    if (!a) return false;
+    uint16_t r = 1, x = a;
+    for (uint32_t p = 0x10000u - 2; p; p >>= 1) {
+        if (p & 1) r = h_mul(r, x);
+        x = h_mul(x, x);
+    }
+    *out = r;
+    return true;
+}
+
+// ---- device helpers ---------------------------------------------------------
+// 16 payload bytes -> 8 big-endian symbols, as 4 dwords of two symbols each
+// (bytes b0 b1 b2 b3 -> b1 | b0 << 8 | b3 << 16 | b2 << 24)
+QF_DEV uint32_t bswap16x2(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x02030001u); }
+
+QF_DEV uint4 load16_partial(const uint8_t* p, uint32_t nb) {
+    if (nb >= 16) return *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t b = 0; b < nb; ++b) w[b >> 2] |= (uint32_t)p[b] << (8 * (b & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+QF_DEV void store16_partial(uint8_t* p, const uint32_t (&w)[4], uint32_t nb) {
+    if (nb >= 16) {
+        *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+        return;
+    }
+    for (uint32_t b = 0; b < nb; ++b) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+}
+
+// logs of the 8 symbols of a unit (kNoLog for zero symbols)
+QF_DEV void symbol_logs(const uint4& raw, const uint16_t* __restrict__ glog, uint32_t (&lx)[8]) {
+    const uint32_t w[4] = {bswap16x2(raw.x), bswap16x2(raw.y), bswap16x2(raw.z), bswap16x2(raw.w)};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t s = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFF;
+        lx[q] = s ? (uint32_t)glog[s] : kNoLog;
+    }
+}
+
+// acc[q] ^= exp[lc + lx[q]] (exp one period in LDS)
+QF_DEV void mul_acc(uint32_t (&acc)[8], uint32_t lc, const uint32_t (&lx)[8], const uint16_t* sexp) {
+    if (lc == kNoLog) return;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        if (lx[q] == kNoLog) continue;
+        uint32_t t = lx[q] + lc;
+        t = t >= kOrder ? t - kOrder : t;
+        acc[q] ^= sexp[t];
+    }
+}
+
+QF_DEV void pack_symbols(const uint32_t (&acc)[8], uint32_t (&w)[4]) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) w[d] = bswap16x2(acc[2 * d] | (acc[2 * d + 1] << 16));
+}
+
+QF_DEV void load_exp_lds(uint16_t* sexp, const uint16_t* gexp) {
+    const uint4* g = reinterpret_cast<const uint4*>(gexp);
+    uint4* l = reinterpret_cast<uint4*>(sexp);
+    for (uint32_t w = threadIdx.x; w < (kOrder + 1) / 8; w += blockDim.x) l[w] = g[w];
+    __syncthreads();
+}
+
+// ---- generalized row combination -------------------------------------------
+// out[b] = base[b] ^ sum_c M[b][c] * in[c] for the rows of one or many
+// generations; lanes over (generation, block of 8 outputs, 16-B unit), units
+// fastest so a wave reads consecutive units of one row.  Encode, the
+// syndromes and the final solve are all this kernel.
+struct Mv16Args {
+    const uint8_t* in;
+    uint64_t igs, irs;
+    const uint16_t* isel;   // row slot of input c: isel[g*isel_gs + c] (null: c)
+    uint64_t isel_gs;
+    const uint8_t* base;    // optional XOR base rows
+    uint64_t bgs, brs;
+    const uint16_t* bsel;   // row slot of base b (null: b)
+    uint64_t bsel_gs;
+    uint8_t* out;
+    uint64_t ogs, ors;
+    const uint16_t* m;      // logs, m[g*mgs + b*mrs + c] (kNoLog = 0)
+    uint64_t mgs, mrs;
+    const uint32_t* nout_g; // outputs of generation g (null: nout)
+    const uint32_t* nin_g;  // inputs of generation g (null: nin)
+    const uint16_t* log;
+    const uint16_t* exp;
+    uint32_t nout, nin, L, Lu, nob;
+    uint64_t total_units;
+};
+
+__global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
+    extern __shared__ uint16_t sexp[];
+    load_exp_lds(sexp, a.exp);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.total_units; f += stride) {
+        const uint64_t t = f / a.Lu;
+        const uint32_t u = (uint32_t)(f - t * a.Lu);
+        const uint64_t g = t / a.nob;
+        const uint32_t b0 = (uint32_t)(t - g * a.nob) * kR16;
+        const uint32_t nout = a.nout_g ? min(a.nout_g[g], a.nout) : a.nout;
+        if (b0 >= nout) continue;
+        const uint32_t no = min((uint32_t)kR16, nout - b0);
+        const uint32_t nin = a.nin_g ? min(a.nin_g[g], a.nin) : a.nin;
+        const uint32_t nb = min(16u, a.L - 16 * u);
+        uint32_t acc[kR16][8];
+#pragma unroll
+        for (int bb = 0; bb < kR16; ++bb) {
+            uint32_t w[4] = {0, 0, 0, 0};
+            if (a.base && (uint32_t)bb < no) {
+                const uint32_t slot = a.bsel ? a.bsel[g * a.bsel_gs + b0 + bb] : b0 + bb;
+                const uint4 raw = load16_partial(a.base + g * a.bgs + (uint64_t)slot * a.brs + 16ull * u, nb);
+                w[0] = bswap16x2(raw.x);
+                w[1] = bswap16x2(raw.y);
+                w[2] = bswap16x2(raw.z);
+                w[3] = bswap16x2(raw.w);
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[bb][q] = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFF;
+        }
+        const uint8_t* ip = a.in + g * a.igs + 16ull * u;
+        const uint16_t* isel = a.isel ? a.isel + g * a.isel_gs : nullptr;
+        const uint16_t* m = a.m + g * a.mgs + (uint64_t)b0 * a.mrs;
+        for (uint32_t c = 0; c < nin; ++c) {
+            const uint32_t slot = isel ? isel[c] : c;
+            uint32_t lx[8];
+            symbol_logs(load16_partial(ip + (uint64_t)slot * a.irs, nb), a.log, lx);
+#pragma unroll
+            for (int bb = 0; bb < kR16; ++bb)
+                if ((uint32_t)bb < no) mul_acc(acc[bb], m[(uint64_t)bb * a.mrs + c], lx, sexp);
+        }
+        uint8_t* op = a.out + g * a.ogs + 16ull * u;
+#pragma unroll
+        for (int bb = 0; bb < kR16; ++bb) {
+            if ((uint32_t)bb >= no) break;
+            uint32_t w[4];
+            pack_symbols(acc[bb], w);
+            store16_partial(op + (uint64_t)(b0 + bb) * a.ors, w, nb);
+        }
+    }
+}
+
+// ---- decode -----------------------------------------------------------------
+QF_DEV uint32_t dmul(uint32_t a, uint32_t b, const uint16_t* glog, const uint16_t* gexp) {
+    if (!a || !b) return 0;
+    return gexp[(uint32_t)glog[a] + glog[b]];
+}
+
+QF_DEV uint32_t dinv(uint32_t a, const uint16_t* glog, const uint16_t* gexp) {
+    return gexp[kOrder - glog[a]];  // a != 0
+}
+
+QF_DEV uint32_t lmod(int64_t x) {
+    int64_t m = x % (int64_t)kOrder;
+    return (uint32_t)(m < 0 ? m + kOrder : m);
+}
+
+// Per-generation decode state in the workspace (the large-erasure path).
+struct Dec16State {
+    uint32_t e, nin;                // erasures, systematic rows among the first k
+};
+
+struct Dec16Args {
+    const uint16_t* row_index;
+    const uint32_t* n_rows;
+    const uint16_t* row_coeffs;  // [g][max_rows][k] or null (Cauchy rows)
+    const uint16_t* log;
+    const uint16_t* exp;
+    uint16_t* wl;                // small path: [g][e_max][k] logs of W
+    uint32_t* n_out;
+    uint16_t* rec_index;         // [g][e_max]
+    int32_t* status;
+    uint32_t k, r, e_max, max_rows;
+};
+
+// coefficient of source column i in the repair row at slot s (index idx)
+QF_DEV uint32_t coef(const uint16_t* row_coeffs, uint64_t g, uint32_t max_rows, uint32_t k, uint32_t s,
+                     uint32_t idx, uint32_t i, const uint16_t* glog, const uint16_t* gexp) {
+    if (row_coeffs) return row_coeffs[(g * max_rows + s) * k + i];
+    return dinv(i ^ idx, glog, gexp);  // decoder.rs:77-80: (i as u16) ^ ((k + j) as u16); i < k <= idx
+}
+
+// Small path (e_max <= 64): one block per generation; acceptance, Gauss-
+// Jordan inverse of C[J,E] in LDS, W = C[J,E]^-1 [I | C[J,S]] over the first
+// k slots, so that the recovered rows are one k_matvec16 over the rows.
+__global__ void __launch_bounds__(256) k_decode16_prepare(Dec16Args a) {
+    __shared__ uint16_t aug[kEMax][2 * kEMax];
+    __shared__ __align__(4) uint8_t present[4096];
+    __shared__ uint16_t J[kEMax], Jslot[kEMax], E[kEMax];
+    __shared__ int32_t s_status;
+    __shared__ uint32_t s_e, s_piv;
+    const uint64_t g = blockIdx.x;
+    const uint32_t tid = threadIdx.x, k = a.k;
+    const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
+    const uint16_t* ridx = a.row_index + g * a.max_rows;
+    for (uint32_t i = tid; i < k; i += blockDim.x) present[i] = 0;
+    if (tid == 0) s_status = n < k ? QF_ENOTREADY : QF_OK;
+    __syncthreads();
+    // the first k rows (decoder.rs:563-566); systematic column id % k: the
+    // batch row index < k is that column.  A duplicated column makes the
+    // system singular (Decoder16 does not filter duplicates).
+    if (s_status == QF_OK) {
+        for (uint32_t s = tid; s < k; s += blockDim.x) {
+            const uint32_t idx = ridx[s];
+            if (idx < k &&
+                (atomicAdd(reinterpret_cast<uint32_t*>(&present[idx & ~3u]), 1u << (8 * (idx & 3))) &
+                 (0xFFu << (8 * (idx & 3)))))
+                s_status = QF_ERANK;
+        }
+    }
+    __syncthreads();
+    if (s_status == QF_OK && tid == 0) {
+        uint32_t e = 0, nj = 0;
+        for (uint32_t i = 0; i < k; ++i)
+            if (!present[i]) {
+                if (e < kEMax) E[e] = (uint16_t)i;
+                ++e;
+            }
+        for (uint32_t s = 0; s < k && nj < kEMax; ++s)
+            if (ridx[s] >= k) {
+                J[nj] = ridx[s];
+                Jslot[nj] = (uint16_t)s;
+                ++nj;
+            }
+        if (e > a.e_max) s_status = QF_ERANGE;
+        s_e = e;
+    }
+    __syncthreads();
+    const uint32_t e = s_e;
+    if (s_status == QF_OK) {
+        // [C[J,E] | I] in LDS, Gauss-Jordan with a pivot search (decoder.rs:598-640)
+        for (uint32_t t = tid; t < e * 2 * e; t += blockDim.x) {
+            const uint32_t b = t / (2 * e), c = t % (2 * e);
+            aug[b][c] = c < e ? (uint16_t)coef(a.row_coeffs, g, a.max_rows, k, Jslot[b], J[b], E[c], a.log, a.exp)
+                              : (uint16_t)(c - e == b);
+        }
+        __syncthreads();
+        for (uint32_t c = 0; c < e; ++c) {
+            if (tid == 0) {
+                uint32_t p = c;
+                while (p < e && aug[p][c] == 0) ++p;
+                s_piv = p;
+                if (p == e) s_status = QF_ERANK;
+            }
+            __syncthreads();
+            if (s_status != QF_OK) break;
+            const uint32_t p = s_piv;
+            if (p != c) {
+                for (uint32_t t = tid; t < 2 * e; t += blockDim.x) {
+                    const uint16_t v = aug[c][t];
+                    aug[c][t] = aug[p][t];
+                    aug[p][t] = v;
+                }
+                __syncthreads();
+            }
+            const uint32_t iv = dinv(aug[c][c], a.log, a.exp);
+            __syncthreads();
+            for (uint32_t t = tid; t < 2 * e; t += blockDim.x) aug[c][t] = (uint16_t)dmul(aug[c][t], iv, a.log, a.exp);
+            __syncthreads();
+            for (uint32_t t = tid; t < e * 2 * e; t += blockDim.x) {
+                const uint32_t b = t / (2 * e), cc = t % (2 * e);
+                if (b == c || cc == c) continue;
+                const uint32_t f = aug[b][c];
+                if (f) aug[b][cc] ^= (uint16_t)dmul(f, aug[c][cc], a.log, a.exp);
+            }
+            __syncthreads();
+            for (uint32_t b = tid; b < e; b += blockDim.x)
+                if (b != c) aug[b][c] = 0;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    const bool ok = s_status == QF_OK;
+    // W[b][slot] over the first k slots: repair slot Jslot[a'] -> D[b][a'];
+    // systematic slot of source i -> sum_a' D[b][a'] C[J[a'], i]
+    uint16_t* wl = a.wl + g * a.e_max * k;
+    for (uint32_t t = tid; t < a.e_max * k; t += blockDim.x) {
+        const uint32_t b = t / k, s = t % k;
+        uint32_t w = 0;
+        if (ok && b < e) {
+            const uint32_t idx = ridx[s];
+            if (idx >= k) {
+                uint32_t ap = 0;
+                while (Jslot[ap] != s) ++ap;
+                w = aug[b][e + ap];
+            } else {
+                for (uint32_t ap = 0; ap < e; ++ap)
+                    w ^= dmul(aug[b][e + ap], coef(a.row_coeffs, g, a.max_rows, k, Jslot[ap], J[ap], idx, a.log, a.exp),
+                              a.log, a.exp);
+            }
+        }
+        wl[t] = (uint16_t)(w ? a.log[w] : kNoLog);
+    }
+    for (uint32_t b = tid; b < a.e_max; b += blockDim.x)
+        a.rec_index[g * a.e_max + b] = (ok && b < e) ? E[b] : 0;
+    if (tid == 0) {
+        a.status[g] = s_status;
+        a.n_out[g] = ok ? e : 0;
+    }
+}
+
+// Large path (e_max > 64): one generation at a time, everything in the
+// workspace.  Lists of the accepted rows:
+struct BigWs {
+    Dec16State* st;
+    uint16_t* J;      // repair row index, by repair order a
+    uint16_t* Jslot;  // its slot
+    uint16_t* E;      // erased source columns, ascending
+    uint16_t* Sslot;  // systematic slots (sources present), by slot order
+    uint16_t* Scol;   // their source columns
+    uint16_t* mlog;   // [e_max][k] logs of C[J_a][Scol c]
+    uint16_t* dlog;   // [e_max][e_max] logs of C[J,E]^-1
+    uint16_t* aug;    // [e_max][2 e_max] general Gauss-Jordan
+    uint32_t* mark;   // [e_max] step + 1 at which the row became a pivot
+    uint32_t* pivrow; // [e_max] pivot row of column c
+    uint32_t* lprod;  // [4][e_max] Cauchy log products
+    uint8_t* synd;    // [e_max][Lp] syndrome rows
+};
+
+struct BigArgs {
+    BigWs w;
+    const uint16_t* row_index;   // generation's
+    uint32_t n_rows;
+    const uint32_t* n_rows_dev;  // generation's (or null)
+    const uint16_t* row_coeffs;  // generation's [max_rows][k] or null
+    const uint16_t* log;
+    const uint16_t* exp;
+    uint32_t* n_out;             // generation's
+    uint16_t* rec_index;         // generation's [e_max]
+    int32_t* status;             // generation's
+    uint32_t k, e_max;
+};
+
+QF_DEV void big_fail(const BigArgs& a, int32_t s) {
+    *a.status = s;
+    *a.n_out = 0;
+}
+
+// acceptance (decoder.rs:563-578) and the row lists; one block of 1024
+__global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs a) {
+    __shared__ __align__(4) uint8_t present[4096];
+    __shared__ int32_t s_status;
+    const uint32_t tid = threadIdx.x, k = a.k;
+    const uint32_t n = a.n_rows_dev ? min(*a.n_rows_dev, a.n_rows) : a.n_rows;
+    for (uint32_t i = tid; i < k; i += blockDim.x) present[i] = 0;
+    if (tid == 0) s_status = n < k ? QF_ENOTREADY : QF_OK;
+    __syncthreads();
+    if (s_status == QF_OK)
+        for (uint32_t s = tid; s < k; s += blockDim.x) {
+            const uint32_t idx = a.row_index[s];
+            if (idx < k &&
+                (atomicAdd(reinterpret_cast<uint32_t*>(&present[idx & ~3u]), 1u << (8 * (idx & 3))) &
+                 (0xFFu << (8 * (idx & 3)))))
+                s_status = QF_ERANK;
+        }
+    __syncthreads();
+    for (uint32_t b = tid; b < a.e_max; b += blockDim.x) a.rec_index[b] = 0;
+    if (tid != 0) return;
+    if (s_status != QF_OK) {
+        a.w.st->e = a.w.st->nin = 0;
+        big_fail(a, s_status);
+        return;
+    }
+    uint32_t e = 0, nj = 0, ns = 0;
+    for (uint32_t i = 0; i < k; ++i)
+        if (!present[i]) {
+            if (e < a.e_max) a.w.E[e] = (uint16_t)i;
+            ++e;
+        }
+    for (uint32_t s = 0; s < k; ++s) {
+        const uint32_t idx = a.row_index[s];
+        if (idx >= k) {
+            if (nj < a.e_max) {
+                a.w.J[nj] = (uint16_t)idx;
+                a.w.Jslot[nj] = (uint16_t)s;
+            }
+            ++nj;
+        } else {
+            a.w.Sslot[ns] = (uint16_t)s;
+            a.w.Scol[ns] = (uint16_t)idx;
+            ++ns;
+        }
+    }
+    if (e > a.e_max) {
+        a.w.st->e = a.w.st->nin = 0;
+        big_fail(a, QF_ERANGE);
+        return;
+    }
+    a.w.st->e = e;
+    a.w.st->nin = ns;
+    *a.status = QF_OK;
+    *a.n_out = e;
+    for (uint32_t b = 0; b < e; ++b) a.rec_index[b] = a.w.E[b];
+}
+
+// mlog[a][c] = log C[J_a][Scol c] (syndromes: rows_J ^ C[J,S] x_S)
+__global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs a) {
+    const uint32_t e = a.w.st->e, ns = a.w.st->nin, k = a.k;
+    const uint64_t total = (uint64_t)e * ns;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(t / ns), c = (uint32_t)(t % ns);
+        const uint32_t v = coef(a.row_coeffs, 0, 0, k, a.w.Jslot[r], a.w.J[r], a.w.Scol[c], a.log, a.exp);
+        a.w.mlog[(uint64_t)r * k + c] = (uint16_t)(v ? a.log[v] : kNoLog);
+    }
+}
+
+// Cauchy inverse in closed form: with x_a = J_a, y_b = E_b (C_ab = 1/(x_a ^ y_b)),
+//   (C^-1)_ba = Qx_a Qy_b / ((x_a ^ y_b) Px_a Py_b),
+//   Qx_a = prod_c (x_a ^ y_c), Qy_b = prod_c (x_c ^ y_b),
+//   Px_a = prod_{c != a} (x_a ^ x_c), Py_b = prod_{c != b} (y_b ^ y_c).
+// A repeated repair row (x_a = x_c) is singular: QF_ERANK.
+__global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs a) {
+    const uint32_t e = a.w.st->e;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * e) return;
+    const bool row = t < e;
+    const uint32_t q = row ? t : t - e;
+    const uint32_t v = row ? a.w.J[q] : a.w.E[q];
+    uint64_t lq = 0, lp = 0;
+    for (uint32_t c = 0; c < e; ++c) {
+        lq += a.log[v ^ (row ? a.w.E[c] : a.w.J[c])];
+        if (c != q) {
+            const uint32_t d = v ^ (row ? a.w.J[c] : a.w.E[c]);
+            if (!d) {
+                big_fail(a, QF_ERANK);
+                return;
+            }
+            lp += a.log[d];
+        }
+    }
+    a.w.lprod[(row ? 0 : 2) * a.e_max + q] = (uint32_t)(lq % kOrder);
+    a.w.lprod[(row ? 1 : 3) * a.e_max + q] = (uint32_t)(lp % kOrder);
+}
+
+__global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs a) {
+    const uint32_t e = a.w.st->e;
+    if (*a.status != QF_OK) return;
+    const uint64_t total = (uint64_t)e * e;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t b = (uint32_t)(t / e), r = (uint32_t)(t % e);
+        const int64_t l = (int64_t)a.w.lprod[r] + a.w.lprod[2 * a.e_max + b] - a.log[a.w.J[r] ^ a.w.E[b]] -
+                          a.w.lprod[a.e_max + r] - a.w.lprod[3 * a.e_max + b];
+        a.w.dlog[(uint64_t)b * a.e_max + r] = (uint16_t)lmod(l);
+    }
+}
+
+// General rows: Gauss-Jordan on [C[J,E] | I] in the workspace, one launch per
+// column.  Rows are not swapped: a column's pivot is the first row not yet
+// used as a pivot with a nonzero entry there (the same pivot as the swap-based
+// search of decoder.rs:600-606 up to row order), eliminated from all other rows
+// in the columns to its right only (finished columns are never read again).
+__global__ void __launch_bounds__(256) k_dec16_gj_init(BigArgs a) {
+    const uint32_t e = a.w.st->e;
+    const uint64_t total = (uint64_t)e * 2 * e;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(t / (2 * e)), c = (uint32_t)(t % (2 * e));
+        a.w.aug[(uint64_t)r * 2 * a.e_max + c] =
+            c < e ? (uint16_t)coef(a.row_coeffs, 0, 0, a.k, a.w.Jslot[r], a.w.J[r], a.w.E[c], a.log, a.exp)
+                  : (uint16_t)(c - e == r);
+        if (c == 0) a.w.mark[r] = 0;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_dec16_gj_pivot(BigArgs a, uint32_t c) {
+    const uint32_t e = a.w.st->e;
+    if (c >= e || *a.status != QF_OK) return;
+    __shared__ uint32_t s_p;
+    if (threadIdx.x == 0) s_p = e;
+    __syncthreads();
+    const uint64_t ld = 2 * a.e_max;
+    for (uint32_t p = threadIdx.x; p < e; p += blockDim.x)
+        if (a.w.mark[p] == 0 && a.w.aug[p * ld + c] != 0) atomicMin(&s_p, p);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    if (s_p == e) {
+        big_fail(a, QF_ERANK);
+        return;
+    }
+    a.w.mark[s_p] = c + 1;
+    a.w.pivrow[c] = s_p;
+}
+
+// rows in blockIdx.y, columns (c, 2e) in x
+__global__ void __launch_bounds__(256) k_dec16_gj_step(BigArgs a, uint32_t c) {
+    const uint32_t e = a.w.st->e;
+    const uint32_t r = blockIdx.y;
+    if (c >= e || r >= e || *a.status != QF_OK) return;
+    const uint32_t p = a.w.pivrow[c];
+    const uint64_t ld = 2 * a.e_max;
+    if (r == p) return;
+    const uint32_t f = a.w.aug[r * ld + c];
+    if (!f) return;
+    const uint32_t lf = lmod((int64_t)a.log[f] - a.log[a.w.aug[(uint64_t)p * ld + c]]);
+    for (uint32_t cc = c + 1 + blockIdx.x * blockDim.x + threadIdx.x; cc < 2 * e; cc += gridDim.x * blockDim.x) {
+        const uint32_t v = a.w.aug[(uint64_t)p * ld + cc];
+        if (v) {
+            uint32_t t = a.log[v] + lf;
+            t = t >= kOrder ? t - kOrder : t;
+            a.w.aug[(uint64_t)r * ld + cc] ^= a.exp[t];
+        }
+    }
+}
+
+// dlog[c][a] = log(aug[piv c][e + a] / aug[piv c][c])
+__global__ void __launch_bounds__(256) k_dec16_gj_final(BigArgs a) {
+    const uint32_t e = a.w.st->e;
+    if (*a.status != QF_OK) return;
+    const uint64_t ld = 2 * a.e_max;
+    const uint64_t total = (uint64_t)e * e;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = (uint32_t)(t / e), r = (uint32_t)(t % e);
+        const uint32_t p = a.w.pivrow[c];
+        const uint32_t v = a.w.aug[p * ld + e + r];
+        a.w.dlog[(uint64_t)c * a.e_max + r] =
+            (uint16_t)(v ? lmod((int64_t)a.log[v] - a.log[a.w.aug[p * ld + c]]) : kNoLog);
+    }
+}
+
+size_t exp_lds_bytes() { return (kOrder + 1) * 2; }
+
+int grid16(qf_ctx* ctx, uint64_t units) {
+    const uint64_t want = (units + kThreads16 - 1) / kThreads16;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)qf::ctx_num_cus(ctx) * 2));
+}
+
+#define QF_HIP(x)                                 \
+    do {                                          \
+        if ((x) != hipSuccess) return QF_EDEVICE; \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+uint16_t qf_gf16_mul(uint16_t a, uint16_t b) { return h_mul(a, b); }
+
+int qf_gf16_inv(uint16_t a, uint16_t* out) {
+    if (!out) return QF_EINVAL;
+    return h_inv(a, out) ? QF_OK : QF_ERANGE;
+}
+
+int qf_cauchy16_coeffs(uint32_t k, uint32_t r, uint16_t* out_rxk) {
+    if (!out_rxk || k == 0) return QF_EINVAL;
+    for (uint32_t j = 0; j < r; ++j) {
+        const uint16_t y = (uint16_t)(k + j);
+        for (uint32_t i = 0; i < k; ++i)
+            if (!h_inv((uint16_t)((uint16_t)i ^ y), &out_rxk[(size_t)j * k + i])) return QF_ERANGE;
+    }
+    return QF_OK;
+}
+
+namespace {
+
+std::vector<uint16_t> host_log16() {
+    std::vector<uint16_t> lg(65536, (uint16_t)kNoLog);
+    uint32_t x = 1;
+    for (uint32_t i = 0; i < kOrder; ++i) {
+        lg[x] = (uint16_t)i;
+        x <<= 1;
+        if (x & 0x10000u) x ^= 0x1100Bu;
+    }
+    return lg;
+}
+
+int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name) {
+    a.Lu = (a.L + 15) / 16;
+    a.nob = (a.nout + kR16 - 1) / kR16;
+    a.total_units = G * a.nob * a.Lu;
+    if (!a.total_units) return QF_OK;
+    hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
+    hipLaunchKernelGGL(k_matvec16, dim3(grid16(ctx, a.total_units)), dim3(kThreads16), exp_lds_bytes(), st, a);
+    QF_HIP(hipGetLastError());
+    qf::ctx_prof_end(ctx, st, ev, name);
+    return QF_OK;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src, uint8_t* rep,
+                      const uint16_t* coeff_rxk) {
+    if (!ctx || !sh) return QF_EINVAL;
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    if (k == 0 || k > 65535 || (L & 1) || sh->flags) return QF_EINVAL;
+    if (G == 0 || r == 0 || L == 0) return QF_OK;
+    if (!src || !rep || (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(rep) & 15) ||
+        (sh->src_row_stride & 15) || (sh->src_gen_stride & 15) || (sh->rep_row_stride & 15) ||
+        (sh->rep_gen_stride & 15))
+        return QF_EINVAL;
+    std::vector<uint16_t> c((size_t)r * k);
+    if (coeff_rxk) {
+        memcpy(c.data(), coeff_rxk, c.size() * 2);
+    } else {
+        int s = qf_cauchy16_coeffs(k, r, c.data());
+        if (s) return s;
+    }
+    std::unique_lock<std::mutex> lk;
+    int s = qf::ctx_lock(ctx, lk);
+    if (s) return s;
+    const uint16_t *glog, *gexp;
+    s = qf::ctx_gf16_tables(ctx, &glog, &gexp);
+    if (s) return s;
+    // coefficient logs (host tables: the same field)
+    static const std::vector<uint16_t> lg = host_log16();
+    for (auto& v : c) v = lg[v];
+    uint8_t* w;
+    s = qf::ctx_work(ctx, c.size() * 2, &w);
+    if (s) return s;
+    hipStream_t st = qf::ctx_stream(ctx);
+    QF_HIP(hipMemcpyAsync(w, c.data(), c.size() * 2, hipMemcpyHostToDevice, st));
+    Mv16Args a{};
+    a.in = src;
+    a.igs = sh->src_gen_stride;
+    a.irs = sh->src_row_stride;
+    a.out = rep;
+    a.ogs = sh->rep_gen_stride;
+    a.ors = sh->rep_row_stride;
+    a.m = reinterpret_cast<const uint16_t*>(w);
+    a.mrs = k;
+    a.log = glog;
+    a.exp = gexp;
+    a.nout = r;
+    a.nin = k;
+    a.L = L;
+    s = launch_matvec(ctx, st, a, G, "k_encode16");
+    if (s) return s;
+    // the coefficient upload reads host memory: finish before returning
+    QF_HIP(hipStreamSynchronize(st));
+    return QF_OK;
+}
+
+int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                      const uint16_t* row_index, const uint32_t* n_rows, const uint16_t* row_coeffs, uint8_t* rec,
+                      uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    if (!ctx || !sh) return QF_EINVAL;
+    const uint32_t k = sh->k, r = sh->r, L = sh->L, max_rows = sh->max_rows;
+    const uint32_t e_max = std::min(k, r);
+    if (k == 0 || k > 4096 || (L & 1) || max_rows == 0 || max_rows > 65536) return QF_EINVAL;
+    if (G == 0) return QF_OK;
+    if (!rows || !row_index || !n_rec || !status || (e_max && (!rec || !rec_index))) return QF_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(rows) & 15) || (sh->row_stride & 15) || (sh->rows_gen_stride & 15) ||
+        (e_max && ((reinterpret_cast<uintptr_t>(rec) & 15) || (sh->rec_row_stride & 15) || (sh->rec_gen_stride & 15))))
+        return QF_EINVAL;
+    std::unique_lock<std::mutex> lk;
+    int s = qf::ctx_lock(ctx, lk);
+    if (s) return s;
+    const uint16_t *glog, *gexp;
+    s = qf::ctx_gf16_tables(ctx, &glog, &gexp);
+    if (s) return s;
+    hipStream_t st = qf::ctx_stream(ctx);
+    const uint32_t ew = std::max<uint32_t>(e_max, 1);
+    uint8_t* w;
+    if (e_max <= kEMax) {
+        // small path: every generation at once
+        s = qf::ctx_work(ctx, (size_t)G * ew * k * 2, &w);
+        if (s) return s;
+        Dec16Args d{};
+        d.row_index = row_index;
+        d.n_rows = n_rows;
+        d.row_coeffs = row_coeffs;
+        d.log = glog;
+        d.exp = gexp;
+        d.wl = reinterpret_cast<uint16_t*>(w);
+        d.n_out = n_rec;
+        d.rec_index = rec_index ? rec_index : reinterpret_cast<uint16_t*>(w);  // e_max == 0: nothing recorded
+        d.status = status;
+        d.k = k;
+        d.r = r;
+        d.e_max = ew;
+        d.max_rows = max_rows;
+        if (!e_max) return QF_EINVAL;  // r == 0: nothing to solve with (k > 0)
+        hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
+        hipLaunchKernelGGL(k_decode16_prepare, dim3(G), dim3(256), 0, st, d);
+        QF_HIP(hipGetLastError());
+        qf::ctx_prof_end(ctx, st, ev, "k_decode16_prepare");
+        Mv16Args c{};
+        c.in = rows;
+        c.igs = sh->rows_gen_stride;
+        c.irs = sh->row_stride;
+        c.out = rec;
+        c.ogs = sh->rec_gen_stride;
+        c.ors = sh->rec_row_stride;
+        c.m = d.wl;
+        c.mgs = (uint64_t)ew * k;
+        c.mrs = k;
+        c.nout_g = n_rec;
+        c.log = glog;
+        c.exp = gexp;
+        c.nout = e_max;
+        c.nin = k;
+        c.L = L;
+        return launch_matvec(ctx, st, c, G, "k_combine16");
+    }
+    // large path (e_max > 64, Extreme windows of 1024..4096): one generation
+    // at a time, inverse in closed form (Cauchy rows) or by Gauss-Jordan
+    const size_t Lp = ((size_t)L + 15) / 16 * 16;
+    size_t off[13], tot = 0;
+    const size_t sz[13] = {sizeof(Dec16State), 2ull * e_max, 2ull * e_max, 2ull * e_max, 2ull * k, 2ull * k,
+                           2ull * e_max * k, 2ull * e_max * e_max, row_coeffs ? 4ull * e_max * e_max : 0,
+                           4ull * e_max, 4ull * e_max, 16ull * e_max, Lp * e_max};
+    for (int q = 0; q < 13; ++q) {
+        off[q] = tot;
+        tot += align256(std::max<size_t>(sz[q], 1));
+    }
+    s = qf::ctx_work(ctx, tot, &w);
+    if (s) return s;
+    BigArgs b{};
+    b.w.st = reinterpret_cast<Dec16State*>(w + off[0]);
+    b.w.J = reinterpret_cast<uint16_t*>(w + off[1]);
+    b.w.Jslot = reinterpret_cast<uint16_t*>(w + off[2]);
+    b.w.E = reinterpret_cast<uint16_t*>(w + off[3]);
+    b.w.Sslot = reinterpret_cast<uint16_t*>(w + off[4]);
+    b.w.Scol = reinterpret_cast<uint16_t*>(w + off[5]);
+    b.w.mlog = reinterpret_cast<uint16_t*>(w + off[6]);
+    b.w.dlog = reinterpret_cast<uint16_t*>(w + off[7]);
+    b.w.aug = reinterpret_cast<uint16_t*>(w + off[8]);
+    b.w.mark = reinterpret_cast<uint32_t*>(w + off[9]);
+    b.w.pivrow = reinterpret_cast<uint32_t*>(w + off[10]);
+    b.w.lprod = reinterpret_cast<uint32_t*>(w + off[11]);
+    b.w.synd = w + off[12];
+    b.log = glog;
+    b.exp = gexp;
+    b.k = k;
+    b.e_max = e_max;
+    b.n_rows = max_rows;
+    const int cus = qf::ctx_num_cus(ctx);
+    const uint32_t mgrid = (uint32_t)std::min<uint64_t>(((uint64_t)e_max * k + 255) / 256, 8ull * cus);
+    const uint32_t dgrid = (uint32_t)std::min<uint64_t>(((uint64_t)e_max * e_max + 255) / 256, 8ull * cus);
+    for (uint32_t g = 0; g < G; ++g) {
+        b.row_index = row_index + (size_t)g * max_rows;
+        b.n_rows_dev = n_rows ? n_rows + g : nullptr;
+        b.row_coeffs = row_coeffs ? row_coeffs + (size_t)g * max_rows * k : nullptr;
+        b.n_out = n_rec + g;
+        b.rec_index = rec_index + (size_t)g * e_max;
+        b.status = status + g;
+        hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
+        hipLaunchKernelGGL(k_dec16_accept, dim3(1), dim3(1024), 0, st, b);
+        hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid), dim3(256), 0, st, b);
+        if (!row_coeffs) {
+            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3((2 * e_max + 255) / 256), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid), dim3(256), 0, st, b);
+        } else {
+            hipLaunchKernelGGL(k_dec16_gj_init, dim3((uint32_t)std::min<uint64_t>(((uint64_t)e_max * 2 * e_max + 255) / 256,
+                                                                                  8ull * cus)),
+                               dim3(256), 0, st, b);
+            // the erasure count is on the device: launch for e_max columns,
+            // the steps past e return at once
+            for (uint32_t c = 0; c < e_max; ++c) {
+                hipLaunchKernelGGL(k_dec16_gj_pivot, dim3(1), dim3(1024), 0, st, b, c);
+                hipLaunchKernelGGL(k_dec16_gj_step, dim3((2 * e_max - c + 255) / 256, e_max), dim3(256), 0, st, b, c);
+            }
+            hipLaunchKernelGGL(k_dec16_gj_final, dim3(dgrid), dim3(256), 0, st, b);
+        }
+        QF_HIP(hipGetLastError());
+        qf::ctx_prof_end(ctx, st, ev, "k_dec16_prepare_large");
+        // syndromes s_a = row(J_a) ^ C[J_a, S] x_S
+        Mv16Args sy{};
+        sy.in = rows + (size_t)g * sh->rows_gen_stride;
+        sy.irs = sh->row_stride;
+        sy.isel = b.w.Sslot;
+        sy.base = sy.in;
+        sy.brs = sh->row_stride;
+        sy.bsel = b.w.Jslot;
+        sy.out = b.w.synd;
+        sy.ors = Lp;
+        sy.m = b.w.mlog;
+        sy.mrs = k;
+        sy.nout_g = n_rec + g;
+        sy.nin_g = &b.w.st->nin;
+        sy.log = glog;
+        sy.exp = gexp;
+        sy.nout = e_max;
+        sy.nin = k;
+        sy.L = L;
+        s = launch_matvec(ctx, st, sy, 1, "k_syndromes16");
+        if (s) return s;
+        // x_E = C[J,E]^-1 s
+        Mv16Args so{};
+        so.in = b.w.synd;
+        so.irs = Lp;
+        so.out = rec + (size_t)g * sh->rec_gen_stride;
+        so.ors = sh->rec_row_stride;
+        so.m = b.w.dlog;
+        so.mrs = e_max;
+        so.nout_g = n_rec + g;
+        so.nin_g = n_rec + g;
+        so.log = glog;
+        so.exp = gexp;
+        so.nout = e_max;
+        so.nin = e_max;
+        so.L = L;
+        s = launch_matvec(ctx, st, so, 1, "k_combine16");
+        if (s) return s;
+    }
+    return QF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,28 @@
+// qf_internal.h -- context services for the library's other translation
+// units (defined in qf_api.hip; not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <mutex>
+#include <string>
+
+#include "qf_fec.h"
+
+namespace qf {
+
+// Locks the context and makes its device current.
+int ctx_lock(qf_ctx* ctx, std::unique_lock<std::mutex>& lk);
+hipStream_t ctx_stream(qf_ctx* ctx);
+int ctx_num_cus(qf_ctx* ctx);
+// The context's device workspace, grown to at least `bytes` (shared with the
+// decode paths; valid until the next call on this context).
+int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out);
+// GF(2^16) tables on the device, built on first use: log[65536] (log[0]
+// unused) and exp[2 * 65535] (exp[i + 65535] = exp[i]).
+int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp);
+// qf_ctx_profile bracketing of a launch.
+hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st);
+void ctx_prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t ev, const std::string& name);
+
+}  // namespace qf

@@ -21,6 +21,7 @@ __all__ = [
     "QfError", "Context", "default_context", "init_gf_tables", "gf_mul", "gf_mul_table",
     "gf_mul_add", "gf_inv", "gf_mul_slice", "cauchy_coefficients", "MemoryPool", "Packet",
     "Encoder", "Decoder", "encode_batch", "decode_batch",
+    "gf16_mul", "gf16_inv", "cauchy16_coefficients", "encode16_batch", "decode16_batch", "Encoder16", "Decoder16",
 ]
 
 
@@ -369,6 +370,176 @@ class Decoder:
             L._lib().qf_decoder_free(self.handle)
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------------------
+# GF(2^16) Extreme mode (gf_tables.rs:331-380, decoder.rs:10-88, 536-656)
+# ---------------------------------------------------------------------------
+def gf16_mul(a: int, b: int) -> int:
+    """gf_tables.rs:333 gf16_mul with the reduction it intends."""
+    return int(L._lib().qf_gf16_mul(a & 0xFFFF, b & 0xFFFF))
+
+
+def gf16_inv(a: int) -> int:
+    """gf_tables.rs:370 gf16_inv; raises for 0."""
+    out = ctypes.c_uint16(0)
+    check(L._lib().qf_gf16_inv(a & 0xFFFF, ctypes.byref(out)), "gf16_inv")
+    return int(out.value)
+
+
+def cauchy16_coefficients(k: int, r: int) -> list[list[int]]:
+    """decoder.rs:77-80 for repairs 0..r-1."""
+    buf = (ctypes.c_uint16 * max(1, k * r))()
+    check(L._lib().qf_cauchy16_coeffs(k, r, buf), "cauchy16")
+    return [list(buf[j * k: (j + 1) * k]) for j in range(r)]
+
+
+def encode16_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_gen_stride: int,
+                   rep_row_stride: int, rep_gen_stride: int, G: int, coeff=None,
+                   ctx: Optional[Context] = None) -> None:
+    """qf_encode16_batch: GF(2^16) repairs of G generations (Encoder16,
+    decoder.rs:33-75).  coeff: optional r x k u16 rows (default Cauchy)."""
+    ctx = ctx or default_context()
+    sh = L.EncodeShape(k, r, Lb, 0, src_row_stride, src_gen_stride, rep_row_stride, rep_gen_stride)
+    cbuf = None
+    if coeff is not None:
+        flat = [int(v) for row in coeff for v in row]
+        if len(flat) != k * r:
+            raise ValueError("coeff must be r x k")
+        cbuf = (ctypes.c_uint16 * len(flat))(*flat)
+    check(L._lib().qf_encode16_batch(ctx.handle, ctypes.byref(sh), G, _ptr(src), _ptr(rep),
+                                      ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None),
+          "encode16_batch")
+
+
+def decode16_batch(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int, Lb: int, *,
+                   max_rows: int, row_stride: int, rows_gen_stride: int, rec_row_stride: int,
+                   rec_gen_stride: int, G: int, n_rows=None, row_coeffs=None,
+                   ctx: Optional[Context] = None) -> None:
+    """qf_decode16_batch: Decoder16 (decoder.rs:563-656) over G generations;
+    row_coeffs: optional u16 tensor [G, max_rows, k]."""
+    ctx = ctx or default_context()
+    sh = L.DecodeShape(k, r, Lb, max_rows, row_stride, rows_gen_stride, rec_row_stride, rec_gen_stride)
+    check(L._lib().qf_decode16_batch(
+        ctx.handle, ctypes.byref(sh), G, _ptr(rows), _ptr(row_index),
+        _ptr(n_rows) if n_rows is not None else None,
+        _ptr(row_coeffs) if row_coeffs is not None else None,
+        _ptr(rec) if rec is not None else None, _ptr(rec_index) if rec_index is not None else None,
+        _ptr(n_rec), _ptr(status)), "decode16_batch")
+
+
+def _be16(vals) -> bytes:
+    return b"".join(int(v).to_bytes(2, "big") for v in vals)
+
+
+class Encoder16:
+    """decoder.rs:10-88 Encoder16: sliding window of k packets, repair j carries
+    the Cauchy row y = k + j as a big-endian u16 coefficient block."""
+
+    def __init__(self, k: int, n: int, ctx: Optional[Context] = None):
+        self.k, self.n = k, n
+        self.ctx = ctx or default_context()
+        self.window: _deque = _deque(maxlen=k)
+
+    def add_source_packet(self, packet: Packet) -> None:
+        self.window.append(packet)
+
+    def generate_repair_packet(self, repair_packet_index: int, pool: Optional[MemoryPool] = None) -> Optional[Packet]:
+        if len(self.window) < self.k:
+            return None
+        import torch
+
+        L_ = self.window[0].len
+        if L_ & 1:
+            raise QfError(L.QF_EINVAL, "Encoder16: odd packet length")
+        row = [gf16_inv((i ^ (self.k + repair_packet_index)) & 0xFFFF) for i in range(self.k)]
+        stride = max(16, (L_ + 15) // 16 * 16)
+        host = bytearray(self.k * stride)
+        for i, p in enumerate(self.window):
+            host[i * stride: i * stride + L_] = bytes(p.data[:L_]).ljust(L_, b"\0")
+        dev = f"cuda:{self.ctx.device}"
+        src = torch.frombuffer(host, dtype=torch.uint8).to(dev)
+        rep = torch.zeros(stride, dtype=torch.uint8, device=dev)
+        torch.cuda.current_stream(self.ctx.device).synchronize()
+        encode16_batch(src, rep, self.k, 1, L_, src_row_stride=stride, src_gen_stride=self.k * stride,
+                       rep_row_stride=stride, rep_gen_stride=stride, G=1, coeff=[row], ctx=self.ctx)
+        self.ctx.sync()
+        data = bytes(rep[:L_].cpu().numpy().tobytes())
+        block = pool.alloc() if pool is not None else bytearray(max(L_, 1))
+        block[:L_] = data
+        return Packet(self.window[-1].id + 1 + repair_packet_index, block, L_, False, _be16(row), 2 * self.k)
+
+
+class Decoder16:
+    """decoder.rs:536-656 Decoder16: the first k packets (systematic column
+    id % k, repair rows from their big-endian u16 coefficient blocks), no
+    duplicate filtering.  Systematic payloads are carried (F4-style fix), and
+    decoding runs once k rows are present, whatever the last row's kind."""
+
+    def __init__(self, k: int, ctx: Optional[Context] = None):
+        self.k = k
+        self.ctx = ctx or default_context()
+        self.rows: list[tuple[int, bytes, Optional[list[int]]]] = []
+        self.is_decoded = False
+        self._decoded: list[Packet] = []
+
+    def add_packet(self, packet: Packet) -> bool:
+        if self.is_decoded or len(self.rows) >= self.k:
+            return self.is_decoded
+        if packet.is_systematic:
+            self.rows.append((packet.id % self.k, packet.payload(), None))
+        elif packet.coefficients is not None:
+            c = bytes(packet.coefficients)
+            self.rows.append((self.k, packet.payload(), [int.from_bytes(c[2 * i: 2 * i + 2], "big")
+                                                          for i in range(self.k)]))
+        else:
+            raise QfError(L.QF_EINVAL, "missing coeffs")
+        if len(self.rows) == self.k:
+            self._try_decode()
+        return self.is_decoded
+
+    def _try_decode(self) -> None:
+        import numpy as np
+        import torch
+
+        k = self.k
+        L_ = max(len(p) for _, p, _ in self.rows)
+        if L_ & 1:
+            raise QfError(L.QF_EINVAL, "Decoder16: odd packet length")
+        stride = max(16, (L_ + 15) // 16 * 16)
+        rows = np.zeros((k, stride), np.uint8)
+        coef = np.zeros((k, k), np.uint16)
+        idx = np.zeros(k, np.uint16)
+        for s, (i, p, c) in enumerate(self.rows):
+            rows[s, : len(p)] = np.frombuffer(p, np.uint8)
+            idx[s] = i
+            if c is not None:
+                coef[s] = c
+        e_max = k
+        dev = f"cuda:{self.ctx.device}"
+        t_rows = torch.from_numpy(rows.reshape(-1)).to(dev)
+        t_idx = torch.from_numpy(idx.view(np.int16)).to(dev)
+        t_coef = torch.from_numpy(coef.view(np.int16).reshape(-1)).to(dev)
+        t_rec = torch.zeros(e_max * stride, dtype=torch.uint8, device=dev)
+        t_ri = torch.zeros(e_max, dtype=torch.int16, device=dev)
+        t_n = torch.zeros(1, dtype=torch.int32, device=dev)
+        t_st = torch.zeros(1, dtype=torch.int32, device=dev)
+        torch.cuda.current_stream(self.ctx.device).synchronize()
+        decode16_batch(t_rows, t_idx, t_rec, t_ri, t_n, t_st, k, e_max, L_, max_rows=k, row_stride=stride,
+                       rows_gen_stride=k * stride, rec_row_stride=stride, rec_gen_stride=e_max * stride, G=1,
+                       row_coeffs=t_coef, ctx=self.ctx)
+        self.ctx.sync()
+        if int(t_st[0]) != L.QF_OK:
+            return  # singular: stays undecoded, as try_decode returning false
+        n = int(t_n[0])
+        rec = t_rec.cpu().numpy().reshape(e_max, stride)
+        ri = t_ri.cpu().numpy().view(np.uint16)
+        self._decoded = [Packet(int(ri[b]), bytearray(rec[b, :L_].tobytes()), L_, True) for b in range(n)]
+        self.is_decoded = True
+
+    def get_decoded_packets(self) -> list[Packet]:
+        out, self._decoded = self._decoded, []
+        return out
 
 
 # ---------------------------------------------------------------------------

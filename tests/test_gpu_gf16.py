@@ -1,0 +1,221 @@
+"""GF(2^16) Extreme mode on the MI355X (k_matvec16 / k_decode16_prepare / the
+large-erasure path) against the oracle (oracle/qf_oracle16.c: Encoder16 and
+Decoder16 of decoder.rs:10-88, 536-656 with the intended reduction) and the
+reference's contract tests/fec.rs:52-82.  Bit-exact."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _r16(x):
+    return (x + 15) // 16 * 16
+
+
+def run_encode16(qf, src, r, coeff=None):
+    """src: (G, k, L) -> (G, r, L); padded strides, guard bytes checked."""
+    import torch
+
+    G, k, L = src.shape
+    rs, rrs = _r16(L) + 16, _r16(L) + 32
+    gs, rgs = k * rs + 16, r * rrs + 48
+    host = np.zeros(G * gs, np.uint8)
+    for g in range(G):
+        for i in range(k):
+            host[g * gs + i * rs: g * gs + i * rs + L] = src[g, i]
+    t_src = torch.from_numpy(host).to("cuda")
+    t_rep = torch.full((G * rgs + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    qf.encode16_batch(t_src, t_rep, k, r, L, src_row_stride=rs, src_gen_stride=gs, rep_row_stride=rrs,
+                      rep_gen_stride=rgs, G=G, coeff=coeff)
+    qf.default_context().sync()
+    out = t_rep.cpu().numpy()
+    rep = np.zeros((G, r, L), np.uint8)
+    guard = np.ones(out.shape, bool)
+    for g in range(G):
+        for j in range(r):
+            o = g * rgs + j * rrs
+            rep[g, j] = out[o: o + L]
+            guard[o: o + L] = False
+    assert (out[guard] == 0xA5).all(), "encode16 wrote outside [0, L) of a repair row"
+    return rep
+
+
+@pytest.mark.parametrize("k,r,L,G", [(8, 4, 8, 1), (1, 1, 2, 3), (16, 9, 100, 4), (64, 16, 1200, 6),
+                                     (5, 17, 34, 2), (300, 8, 258, 2)])
+def test_encode16_matches_oracle(qf, oracle, gpu_ctx, k, r, L, G):
+    rng = np.random.default_rng(k * 1000 + r)
+    src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
+    src[0, 0, :4] = 0  # zero symbols (no log)
+    rep = run_encode16(qf, src, r)
+    for g in range(G):
+        assert np.array_equal(rep[g], oracle.encode16(src[g], r)), g
+
+
+def test_encode16_explicit_coefficients(qf, oracle, gpu_ctx):
+    rng = np.random.default_rng(11)
+    k, r, L = 12, 5, 66
+    src = rng.integers(0, 256, (2, k, L), dtype=np.uint8)
+    C = rng.integers(0, 65536, (r, k), dtype=np.uint16)
+    C[0, :3] = 0
+    C[1, 0] = 1
+    rep = run_encode16(qf, src, r, coeff=C.tolist())
+    for g in range(2):
+        assert np.array_equal(rep[g], oracle.encode16(src[g], r, C))
+
+
+def test_encode16_odd_length_rejected(qf, gpu_ctx):
+    import torch
+
+    t = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(qf.QfError):
+        qf.encode16_batch(t, t, 2, 1, 3, src_row_stride=16, src_gen_stride=32, rep_row_stride=16,
+                          rep_gen_stride=16, G=1)
+
+
+def make_gens(oracle, rng, k, r, L, G, *, coeff_mode="cauchy", erase=None, dup=False, short=False):
+    src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
+    gens = []
+    for g in range(G):
+        C = oracle.cauchy16(k, r) if coeff_mode == "cauchy" else rng.integers(1, 65536, (r, k), dtype=np.uint16)
+        rep = oracle.encode16(src[g], r, C)
+        e = int(rng.integers(0, min(k, r) + 1)) if erase is None else erase
+        er = set(rng.choice(k, e, replace=False).tolist())
+        arr = [i for i in range(k) if i not in er]
+        rng.shuffle(arr)
+        reps = [k + j for j in rng.permutation(r)[:e].tolist()]
+        arr = arr + reps + [k + j for j in range(r) if k + j not in reps]
+        first = arr[:k]  # the first k rows are the system, in a random order
+        rng.shuffle(first)
+        arr = first + arr[k:]
+        if dup and k > 1:
+            arr.insert(1, arr[0])
+        if short:
+            arr = arr[: k - 1]
+        rows = np.stack([src[g, a] if a < k else rep[a - k] for a in arr])
+        rc = np.stack([np.zeros(k, np.uint16) if a < k else C[a - k] for a in arr])
+        gens.append((arr, rows, rc))
+    return src, gens
+
+
+def run_decode16(qf, k, r, L, G, gens, with_coeffs):
+    import torch
+
+    max_rows = max(len(a) for a, _, _ in gens)
+    rs = _r16(L) + 16
+    rgs = max_rows * rs
+    emax = min(k, r)
+    rrs = _r16(L) + 16
+    rec_gs = emax * rrs + 32
+    rows = np.zeros(G * rgs, np.uint8)
+    ridx = np.zeros((G, max_rows), np.uint16)
+    nrows = np.zeros(G, np.uint32)
+    rcoef = np.zeros((G, max_rows, k), np.uint16)
+    for g, (arr, rw, rc) in enumerate(gens):
+        nrows[g] = len(arr)
+        ridx[g, : len(arr)] = arr
+        for s in range(len(arr)):
+            rows[g * rgs + s * rs: g * rgs + s * rs + L] = rw[s]
+        rcoef[g, : len(arr)] = rc
+    t_rows = torch.from_numpy(rows).to("cuda")
+    t_idx = torch.from_numpy(ridx.view(np.int16)).to("cuda")
+    t_n = torch.from_numpy(nrows.view(np.int32)).to("cuda")
+    t_coef = torch.from_numpy(rcoef.view(np.int16).reshape(-1)).to("cuda") if with_coeffs else None
+    t_rec = torch.full((G * rec_gs + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+    t_ri = torch.zeros(G * emax, dtype=torch.int16, device="cuda")
+    t_nrec = torch.zeros(G, dtype=torch.int32, device="cuda")
+    t_st = torch.full((G,), 77, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    qf.decode16_batch(t_rows, t_idx, t_rec, t_ri, t_nrec, t_st, k, r, L, max_rows=max_rows, row_stride=rs,
+                      rows_gen_stride=rgs, rec_row_stride=rrs, rec_gen_stride=rec_gs, G=G, n_rows=t_n,
+                      row_coeffs=t_coef)
+    qf.default_context().sync()
+    return (t_rec.cpu().numpy(), t_ri.cpu().numpy().view(np.uint16).reshape(G, emax), t_nrec.cpu().numpy(),
+            t_st.cpu().numpy(), rrs, rec_gs)
+
+
+def check_decode(oracle, src, gens, k, L, res):
+    rec, ri, nrec, st, rrs, rec_gs = res
+    for g, (arr, rows, rc) in enumerate(gens):
+        ost, out, mask = oracle.decode16(k, arr, rows, rc if any(a >= k for a in arr) else None)
+        assert st[g] == ost, (g, st[g], ost)
+        if ost != 0:
+            assert nrec[g] == 0
+            continue
+        erased = [i for i in range(k) if not mask[i]]
+        assert nrec[g] == len(erased)
+        assert ri[g, : len(erased)].tolist() == erased
+        for b, i in enumerate(erased):
+            o = g * rec_gs + b * rrs
+            got = rec[o: o + L]
+            assert np.array_equal(got, out[i]), (g, i)
+            assert np.array_equal(got, src[g, i]), (g, i)
+
+
+@pytest.mark.parametrize("k,r,L,G,with_coeffs", [(8, 4, 8, 5, False), (16, 16, 100, 8, False),
+                                                 (64, 16, 1200, 12, False), (64, 64, 258, 4, False),
+                                                 (10, 6, 34, 6, True), (40, 20, 66, 4, True)])
+def test_decode16_small_path(qf, oracle, gpu_ctx, k, r, L, G, with_coeffs):
+    rng = np.random.default_rng(k * 7 + r)
+    src, gens = make_gens(oracle, rng, k, r, L, G, coeff_mode="cauchy" if not with_coeffs else "random")
+    check_decode(oracle, src, gens, k, L, run_decode16(qf, k, r, L, G, gens, with_coeffs))
+
+
+def test_decode16_statuses(qf, oracle, gpu_ctx):
+    rng = np.random.default_rng(5)
+    k, r, L = 12, 6, 40
+    _, g1 = make_gens(oracle, rng, k, r, L, 1, erase=3, short=True)   # ENOTREADY
+    _, g2 = make_gens(oracle, rng, k, r, L, 1, erase=3, dup=True)     # duplicated row: singular
+    src, g3 = make_gens(oracle, rng, k, r, L, 1, erase=6)
+    gens = g1 + g2 + g3
+    srcs = np.concatenate([np.zeros((2, k, L), np.uint8), src])
+    res = run_decode16(qf, k, r, L, 3, gens, False)
+    assert res[3].tolist()[:2] == [-3, -4]
+    check_decode(oracle, srcs, gens, k, L, res)
+
+
+@pytest.mark.parametrize("k,r,L,erase,with_coeffs", [(128, 96, 200, 80, False), (256, 128, 130, 128, False),
+                                                     (160, 80, 66, 70, True)])
+def test_decode16_large_path(qf, oracle, gpu_ctx, k, r, L, erase, with_coeffs):
+    rng = np.random.default_rng(k + erase)
+    src, gens = make_gens(oracle, rng, k, r, L, 2, coeff_mode="random" if with_coeffs else "cauchy", erase=erase)
+    check_decode(oracle, src, gens, k, L, run_decode16(qf, k, r, L, 2, gens, with_coeffs))
+
+
+def test_decode16_extreme_window_roundtrip(qf, oracle, gpu_ctx):
+    """An Extreme-mode window (adaptive.rs:131: 1024..4096): k = 1024 sources,
+    half erased, recovered from Cauchy repairs; checked against the sources
+    (size-independent property: decode(encode(x)) == x)."""
+    rng = np.random.default_rng(21)
+    k, r, L, e = 1024, 1024, 256, 512
+    src = rng.integers(0, 256, (1, k, L), dtype=np.uint8)
+    rep = run_encode16(qf, src, r)[0]
+    er = sorted(rng.choice(k, e, replace=False).tolist())
+    arr = [i for i in range(k) if i not in set(er)] + [k + j for j in rng.permutation(r)[:e].tolist()]
+    rng.shuffle(arr)
+    rows = np.stack([src[0, a] if a < k else rep[a - k] for a in arr])
+    rc = np.zeros((len(arr), k), np.uint16)
+    rec, ri, nrec, st, rrs, rec_gs = run_decode16(qf, k, r, L, 1, [(arr, rows, rc)], False)
+    assert st[0] == 0 and nrec[0] == e
+    assert ri[0, :e].tolist() == er
+    for b, i in enumerate(er):
+        assert np.array_equal(rec[b * rrs: b * rrs + L], src[0, i])
+
+
+def test_reference_contract_gf16_encode_decode(qf, gpu_ctx):
+    """tests/fec.rs:52-82 through the Encoder16 / Decoder16 mirror: k = 8,
+    n = 12, packet 0 dropped, every source's first byte comes back."""
+    k, n, L = 8, 12, 8
+    enc = qf.Encoder16(k, n)
+    pk = [qf.Packet(i, bytearray([i % 255] * L), L, True) for i in range(k)]
+    for p in pk:
+        enc.add_source_packet(p)
+    repairs = [enc.generate_repair_packet(j) for j in range(n - k)]
+    assert all(p is not None and p.coeff_len == 2 * k for p in repairs)
+    dec = qf.Decoder16(k)
+    done = False
+    for p in pk[1:] + repairs:
+        done = dec.add_packet(p)
+    assert done
+    got = dec.get_decoded_packets()
+    assert [(p.id, bytes(p.data[:L])) for p in got] == [(0, bytes(L))]
