@@ -521,7 +521,7 @@ int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
 }
 int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp) {
     if (!ctx->d_gf16_log) {
-        std::vector<uint16_t> lg(65536, 0), ex(2 * 65535);
+        std::vector<uint16_t> lg(65536, 0xFFFF), ex(2 * 65535);  // log 0: 0xFFFF (no product)
         uint32_t x = 1;
         for (uint32_t i = 0; i < 65535; ++i) {  // generator 2 of GF(2^16) mod 0x1100B
             ex[i] = ex[i + 65535] = (uint16_t)x;

@@ -42,7 +42,7 @@ constexpr uint32_t kOrder = 65535;  // multiplicative group order
 constexpr uint32_t kNoLog = 0xFFFF; // log of 0 (no product)
 constexpr uint32_t kEMax = 64;      // erasures per generation the decode handles
 constexpr int kR16 = 8;             // outputs per pass (encode and combine)
-constexpr int kThreads16 = 512;
+constexpr int kThreads16 = 1024;
 
 // ---- host arithmetic ------------------------------------------------------
 uint16_t h_mul(uint16_t a, uint16_t b) {
@@ -87,31 +87,47 @@ QF_DEV void store16_partial(uint8_t* p, const uint32_t (&w)[4], uint32_t nb) {
     for (uint32_t b = 0; b < nb; ++b) p[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
 }
 
-// logs of the 8 symbols of a unit (kNoLog for zero symbols)
+// Branch-free products: operands are byte offsets 2*log into the LDS exp
+// table, a zero operand is kZeroOff (far beyond any sum of two logs).  The
+// sum of two offsets is reduced mod 2*65535 by min(t, t - 2*65535) (the
+// subtraction wraps for t below the period) and clamped to 2*65535, the
+// offset of the table's extra zero entry: 3 VALU ops and one LDS read.
+constexpr uint32_t kZeroOff = 0x40000000u;
+constexpr uint32_t kPeriodOff = 2 * kOrder;
+
+QF_DEV uint32_t log_off(uint32_t lg) { return lg == kNoLog ? kZeroOff : 2 * lg; }
+
+// log offsets of the 8 symbols of a unit
 QF_DEV void symbol_logs(const uint4& raw, const uint16_t* __restrict__ glog, uint32_t (&lx)[8]) {
     const uint32_t w[4] = {bswap16x2(raw.x), bswap16x2(raw.y), bswap16x2(raw.z), bswap16x2(raw.w)};
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const uint32_t s = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFF;
-        lx[q] = s ? (uint32_t)glog[s] : kNoLog;
+        // glog[0] = kNoLog: gather unconditionally, select (no branch)
+        const uint32_t lg = glog[(w[q >> 1] >> (16 * (q & 1))) & 0xFFFF];
+        lx[q] = lg == kNoLog ? kZeroOff : 2u * lg;
     }
 }
 
-// acc[q] ^= exp[lc + lx[q]] (exp one period in LDS)
-QF_DEV void mul_acc(uint32_t (&acc)[8], uint32_t lc, const uint32_t (&lx)[8], const uint16_t* sexp) {
-    if (lc == kNoLog) return;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        if (lx[q] == kNoLog) continue;
-        uint32_t t = lx[q] + lc;
-        t = t >= kOrder ? t - kOrder : t;
-        acc[q] ^= sexp[t];
-    }
+QF_DEV uint32_t prod_lds(const char* base, uint32_t lx, uint32_t lc) {
+    const uint32_t t = lx + lc;
+    return *reinterpret_cast<const uint16_t*>(base + min(min(t, t - kPeriodOff), kPeriodOff));
 }
 
-QF_DEV void pack_symbols(const uint32_t (&acc)[8], uint32_t (&w)[4]) {
+// acc ^= c * x for 8 symbols held as 4 dwords of (symbol 2d | symbol 2d+1 << 16),
+// lc = log_off(log c)
+QF_DEV void mul_acc(uint32_t (&acc)[4], uint32_t lc, const uint32_t (&lx)[8], const uint16_t* sexp) {
+    const char* base = reinterpret_cast<const char*>(sexp);
+    uint32_t p[8];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) w[d] = bswap16x2(acc[2 * d] | (acc[2 * d + 1] << 16));
+    for (int q = 0; q < 8; ++q) p[q] = prod_lds(base, lx[q], lc);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[d] ^= p[2 * d] | (p[2 * d + 1] << 16);
+}
+
+// packed symbols <-> 16 payload bytes (big-endian symbols)
+QF_DEV void pack_symbols(const uint32_t (&acc)[4], uint32_t (&w)[4]) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) w[d] = bswap16x2(acc[d]);
 }
 
 QF_DEV void load_exp_lds(uint16_t* sexp, const uint16_t* gexp) {
@@ -119,13 +135,18 @@ QF_DEV void load_exp_lds(uint16_t* sexp, const uint16_t* gexp) {
     uint4* l = reinterpret_cast<uint4*>(sexp);
     for (uint32_t w = threadIdx.x; w < (kOrder + 1) / 8; w += blockDim.x) l[w] = g[w];
     __syncthreads();
+    if (threadIdx.x == 0) sexp[kOrder] = 0;  // the zero product (offset kPeriodOff)
+    __syncthreads();
 }
 
 // ---- generalized row combination -------------------------------------------
 // out[b] = base[b] ^ sum_c M[b][c] * in[c] for the rows of one or many
-// generations; lanes over (generation, block of 8 outputs, 16-B unit), units
-// fastest so a wave reads consecutive units of one row.  Encode, the
-// syndromes and the final solve are all this kernel.
+// generations; lanes over (generation, block of 8 outputs, input chunk,
+// 16-B unit), units fastest so a wave reads consecutive units of one row.
+// Encode, the syndromes and the final solve are all this kernel.  With one
+// input chunk the lane stores its rows; with several (few generations, long
+// rows: an Extreme window) every chunk XORs its partial rows into a zeroed
+// padded accumulator with 32-bit atomics and k_finish16 copies them out.
 struct Mv16Args {
     const uint8_t* in;
     uint64_t igs, irs;
@@ -143,58 +164,114 @@ struct Mv16Args {
     const uint32_t* nin_g;  // inputs of generation g (null: nin)
     const uint16_t* log;
     const uint16_t* exp;
-    uint32_t nout, nin, L, Lu, nob;
+    uint32_t* acc_ws;       // split: [g][nout][Lp/4] accumulator (zeroed)
+    uint32_t nout, nin, L, Lu, nob, nsplit, kchunk;
     uint64_t total_units;
 };
 
 __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
-    extern __shared__ uint16_t sexp[];
+    __shared__ uint16_t sexp[kOrder + 1];  // static: LDS offsets fold into the reads
     load_exp_lds(sexp, a.exp);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.total_units; f += stride) {
-        const uint64_t t = f / a.Lu;
+        uint64_t t = f / a.Lu;
         const uint32_t u = (uint32_t)(f - t * a.Lu);
+        const uint32_t ks = (uint32_t)(t % a.nsplit);
+        t /= a.nsplit;
         const uint64_t g = t / a.nob;
         const uint32_t b0 = (uint32_t)(t - g * a.nob) * kR16;
         const uint32_t nout = a.nout_g ? min(a.nout_g[g], a.nout) : a.nout;
         if (b0 >= nout) continue;
         const uint32_t no = min((uint32_t)kR16, nout - b0);
         const uint32_t nin = a.nin_g ? min(a.nin_g[g], a.nin) : a.nin;
+        const uint32_t c0 = ks * a.kchunk, c1 = min(nin, c0 + a.kchunk);
         const uint32_t nb = min(16u, a.L - 16 * u);
-        uint32_t acc[kR16][8];
+        uint32_t acc[kR16][4];
 #pragma unroll
         for (int bb = 0; bb < kR16; ++bb) {
-            uint32_t w[4] = {0, 0, 0, 0};
-            if (a.base && (uint32_t)bb < no) {
+            acc[bb][0] = acc[bb][1] = acc[bb][2] = acc[bb][3] = 0;
+            if (a.base && ks == 0 && (uint32_t)bb < no) {
                 const uint32_t slot = a.bsel ? a.bsel[g * a.bsel_gs + b0 + bb] : b0 + bb;
                 const uint4 raw = load16_partial(a.base + g * a.bgs + (uint64_t)slot * a.brs + 16ull * u, nb);
-                w[0] = bswap16x2(raw.x);
-                w[1] = bswap16x2(raw.y);
-                w[2] = bswap16x2(raw.z);
-                w[3] = bswap16x2(raw.w);
+                acc[bb][0] = bswap16x2(raw.x);
+                acc[bb][1] = bswap16x2(raw.y);
+                acc[bb][2] = bswap16x2(raw.z);
+                acc[bb][3] = bswap16x2(raw.w);
             }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) acc[bb][q] = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFF;
         }
         const uint8_t* ip = a.in + g * a.igs + 16ull * u;
         const uint16_t* isel = a.isel ? a.isel + g * a.isel_gs : nullptr;
         const uint16_t* m = a.m + g * a.mgs + (uint64_t)b0 * a.mrs;
-        for (uint32_t c = 0; c < nin; ++c) {
-            const uint32_t slot = isel ? isel[c] : c;
-            uint32_t lx[8];
-            symbol_logs(load16_partial(ip + (uint64_t)slot * a.irs, nb), a.log, lx);
+        // software pipeline: row c + 2's bytes and row c + 1's log gathers
+        // are in flight while row c's products are formed
+        uint4 nxt = make_uint4(0, 0, 0, 0);
+        uint32_t lxn[8];
+        if (c0 < c1) symbol_logs(load16_partial(ip + (uint64_t)(isel ? isel[c0] : c0) * a.irs, nb), a.log, lxn);
+        if (c0 + 1 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c0 + 1] : c0 + 1) * a.irs, nb);
+        for (uint32_t c = c0; c < c1; ++c) {
+            uint32_t lx[8], lc[kR16];
 #pragma unroll
-            for (int bb = 0; bb < kR16; ++bb)
-                if ((uint32_t)bb < no) mul_acc(acc[bb], m[(uint64_t)bb * a.mrs + c], lx, sexp);
-        }
-        uint8_t* op = a.out + g * a.ogs + 16ull * u;
+            for (int q = 0; q < 8; ++q) lx[q] = lxn[q];
+            if (c + 1 < c1) {
+                symbol_logs(nxt, a.log, lxn);
+                if (c + 2 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c + 2] : c + 2) * a.irs, nb);
+            }
+            // coefficients of the outputs past `no` read a valid row and count as 0
 #pragma unroll
-        for (int bb = 0; bb < kR16; ++bb) {
-            if ((uint32_t)bb >= no) break;
-            uint32_t w[4];
-            pack_symbols(acc[bb], w);
-            store16_partial(op + (uint64_t)(b0 + bb) * a.ors, w, nb);
+            for (int bb = 0; bb < kR16; ++bb) {
+                const uint32_t v = m[(uint64_t)min((uint32_t)bb, no - 1) * a.mrs + c];
+                lc[bb] = (uint32_t)bb < no ? log_off(v) : kZeroOff;
+            }
+#pragma unroll
+            for (int bb = 0; bb < kR16; ++bb) mul_acc(acc[bb], lc[bb], lx, sexp);
         }
+        if (a.nsplit == 1) {
+            uint8_t* op = a.out + g * a.ogs + 16ull * u;
+#pragma unroll
+            for (int bb = 0; bb < kR16; ++bb) {
+                if ((uint32_t)bb >= no) break;
+                uint32_t w[4];
+                pack_symbols(acc[bb], w);
+                store16_partial(op + (uint64_t)(b0 + bb) * a.ors, w, nb);
+            }
+        } else {
+            uint32_t* wp = a.acc_ws + ((g * a.nout + b0) * a.Lu + u) * 4;
+#pragma unroll
+            for (int bb = 0; bb < kR16; ++bb) {
+                if ((uint32_t)bb >= no) break;
+                uint32_t w[4];
+                pack_symbols(acc[bb], w);
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    if (w[d]) atomicXor(wp + (uint64_t)bb * a.Lu * 4 + d, w[d]);
+            }
+        }
+    }
+}
+
+// split accumulator -> output rows (exactly L bytes per row)
+__global__ void __launch_bounds__(256) k_finish16(Mv16Args a) {
+    const uint64_t total = (uint64_t)(a.total_units / ((uint64_t)a.nsplit * a.nob)) * a.nout;  // G * nout * Lu
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total; f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = f / a.Lu;
+        const uint32_t u = (uint32_t)(f - t * a.Lu);
+        const uint64_t g = t / a.nout;
+        const uint32_t b = (uint32_t)(t - g * a.nout);
+        const uint32_t nout = a.nout_g ? min(a.nout_g[g], a.nout) : a.nout;
+        if (b >= nout) continue;
+        const uint4 v = reinterpret_cast<const uint4*>(a.acc_ws)[f];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        store16_partial(a.out + g * a.ogs + (uint64_t)b * a.ors + 16ull * u, w, min(16u, a.L - 16 * u));
+    }
+}
+
+// logs of the Cauchy rows: m[j][i] = log inv(i ^ (k + j)) = -log(i ^ (k + j))
+__global__ void __launch_bounds__(256) k_cauchy16_logs(uint16_t* m, uint32_t k, uint32_t r, const uint16_t* glog) {
+    const uint64_t total = (uint64_t)k * r;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t j = (uint32_t)(t / k), i = (uint32_t)(t % k);
+        const uint32_t l = glog[i ^ ((k + j) & 0xFFFF)];
+        m[t] = (uint16_t)(l ? kOrder - l : 0);
     }
 }
 
@@ -394,61 +471,97 @@ QF_DEV void big_fail(const BigArgs& a, int32_t s) {
     *a.n_out = 0;
 }
 
-// acceptance (decoder.rs:563-578) and the row lists; one block of 1024
+// exclusive prefix sum of one count per thread over a block of 1024
+QF_DEV uint32_t block_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+    const uint32_t tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t x = tid >= d ? sh[tid - d] : 0;
+        __syncthreads();
+        sh[tid] += x;
+        __syncthreads();
+    }
+    const uint32_t incl = sh[tid];
+    *total = sh[1023];
+    __syncthreads();
+    return incl - v;
+}
+
+// acceptance (decoder.rs:563-578) and the row lists; one block of 1024,
+// thread t owns slots / columns [4t, 4t + 4) (k <= 4096), lists compacted in
+// order with block scans
 __global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs a) {
     __shared__ __align__(4) uint8_t present[4096];
+    __shared__ uint32_t scan[1024];
     __shared__ int32_t s_status;
     const uint32_t tid = threadIdx.x, k = a.k;
     const uint32_t n = a.n_rows_dev ? min(*a.n_rows_dev, a.n_rows) : a.n_rows;
     for (uint32_t i = tid; i < k; i += blockDim.x) present[i] = 0;
     if (tid == 0) s_status = n < k ? QF_ENOTREADY : QF_OK;
     __syncthreads();
-    if (s_status == QF_OK)
-        for (uint32_t s = tid; s < k; s += blockDim.x) {
-            const uint32_t idx = a.row_index[s];
-            if (idx < k &&
-                (atomicAdd(reinterpret_cast<uint32_t*>(&present[idx & ~3u]), 1u << (8 * (idx & 3))) &
-                 (0xFFu << (8 * (idx & 3)))))
-                s_status = QF_ERANK;
-        }
+    uint32_t idx[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t sl = 4 * tid + q;
+        idx[q] = (s_status == QF_OK && sl < k) ? a.row_index[sl] : 0xFFFFFFFFu;
+        if (idx[q] < k &&
+            (atomicAdd(reinterpret_cast<uint32_t*>(&present[idx[q] & ~3u]), 1u << (8 * (idx[q] & 3))) &
+             (0xFFu << (8 * (idx[q] & 3)))))
+            s_status = QF_ERANK;
+    }
     __syncthreads();
     for (uint32_t b = tid; b < a.e_max; b += blockDim.x) a.rec_index[b] = 0;
-    if (tid != 0) return;
     if (s_status != QF_OK) {
-        a.w.st->e = a.w.st->nin = 0;
-        big_fail(a, s_status);
+        if (tid == 0) {
+            a.w.st->e = a.w.st->nin = 0;
+            big_fail(a, s_status);
+        }
         return;
     }
-    uint32_t e = 0, nj = 0, ns = 0;
-    for (uint32_t i = 0; i < k; ++i)
-        if (!present[i]) {
-            if (e < a.e_max) a.w.E[e] = (uint16_t)i;
-            ++e;
-        }
-    for (uint32_t s = 0; s < k; ++s) {
-        const uint32_t idx = a.row_index[s];
-        if (idx >= k) {
-            if (nj < a.e_max) {
-                a.w.J[nj] = (uint16_t)idx;
-                a.w.Jslot[nj] = (uint16_t)s;
-            }
-            ++nj;
-        } else {
-            a.w.Sslot[ns] = (uint16_t)s;
-            a.w.Scol[ns] = (uint16_t)idx;
-            ++ns;
-        }
+    // erased columns, ascending
+    uint32_t ce = 0, cj = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        ce += (4 * tid + q < k && !present[4 * tid + q]);
+        cj += (idx[q] != 0xFFFFFFFFu && idx[q] >= k);
     }
+    uint32_t e, nj;
+    uint32_t oe = block_scan(ce, scan, &e);
+    uint32_t oj = block_scan(cj, scan, &nj);
+    uint32_t os = 4 * tid - oj;  // systematic slots before this thread's
     if (e > a.e_max) {
-        a.w.st->e = a.w.st->nin = 0;
-        big_fail(a, QF_ERANGE);
+        if (tid == 0) {
+            a.w.st->e = a.w.st->nin = 0;
+            big_fail(a, QF_ERANGE);
+        }
         return;
     }
-    a.w.st->e = e;
-    a.w.st->nin = ns;
-    *a.status = QF_OK;
-    *a.n_out = e;
-    for (uint32_t b = 0; b < e; ++b) a.rec_index[b] = a.w.E[b];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t i = 4 * tid + q;
+        if (i < k && !present[i]) {
+            a.w.E[oe] = (uint16_t)i;
+            a.rec_index[oe] = (uint16_t)i;
+            ++oe;
+        }
+        if (idx[q] == 0xFFFFFFFFu) continue;
+        if (idx[q] >= k) {
+            a.w.J[oj] = (uint16_t)idx[q];
+            a.w.Jslot[oj] = (uint16_t)i;
+            ++oj;
+        } else {
+            a.w.Sslot[os] = (uint16_t)i;
+            a.w.Scol[os] = (uint16_t)idx[q];
+            ++os;
+        }
+    }
+    if (tid == 0) {
+        a.w.st->e = e;
+        a.w.st->nin = k - nj;
+        *a.status = QF_OK;
+        *a.n_out = e;
+    }
 }
 
 // mlog[a][c] = log C[J_a][Scol c] (syndromes: rows_J ^ C[J,S] x_S)
@@ -466,28 +579,48 @@ __global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs a) {
 //   (C^-1)_ba = Qx_a Qy_b / ((x_a ^ y_b) Px_a Py_b),
 //   Qx_a = prod_c (x_a ^ y_c), Qy_b = prod_c (x_c ^ y_b),
 //   Px_a = prod_{c != a} (x_a ^ x_c), Py_b = prod_{c != b} (y_b ^ y_c).
-// A repeated repair row (x_a = x_c) is singular: QF_ERANK.
+// One block per row / column value, logs summed across the block.  A
+// repeated repair row (x_a = x_c) is singular: QF_ERANK.
 __global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs a) {
+    __shared__ uint64_t sq[256], sp[256];
+    __shared__ uint32_t s_zero;
     const uint32_t e = a.w.st->e;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = blockIdx.x;
     if (t >= 2 * e) return;
     const bool row = t < e;
     const uint32_t q = row ? t : t - e;
     const uint32_t v = row ? a.w.J[q] : a.w.E[q];
+    const uint16_t* other = row ? a.w.E : a.w.J;  // Q partners
+    const uint16_t* same = row ? a.w.J : a.w.E;   // P partners
+    if (threadIdx.x == 0) s_zero = 0;
     uint64_t lq = 0, lp = 0;
-    for (uint32_t c = 0; c < e; ++c) {
-        lq += a.log[v ^ (row ? a.w.E[c] : a.w.J[c])];
+    bool zero = false;
+    for (uint32_t c = threadIdx.x; c < e; c += blockDim.x) {
+        lq += a.log[v ^ other[c]];
         if (c != q) {
-            const uint32_t d = v ^ (row ? a.w.J[c] : a.w.E[c]);
-            if (!d) {
-                big_fail(a, QF_ERANK);
-                return;
-            }
-            lp += a.log[d];
+            const uint32_t d = v ^ same[c];
+            zero |= d == 0;
+            lp += d ? a.log[d] : 0;
         }
     }
-    a.w.lprod[(row ? 0 : 2) * a.e_max + q] = (uint32_t)(lq % kOrder);
-    a.w.lprod[(row ? 1 : 3) * a.e_max + q] = (uint32_t)(lp % kOrder);
+    sq[threadIdx.x] = lq;
+    sp[threadIdx.x] = lp;
+    __syncthreads();
+    if (zero) s_zero = 1;
+    for (uint32_t d = 128; d; d >>= 1) {
+        if (threadIdx.x < d) {
+            sq[threadIdx.x] += sq[threadIdx.x + d];
+            sp[threadIdx.x] += sp[threadIdx.x + d];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    if (s_zero) {
+        big_fail(a, QF_ERANK);
+        return;
+    }
+    a.w.lprod[(row ? 0 : 2) * a.e_max + q] = (uint32_t)(sq[0] % kOrder);
+    a.w.lprod[(row ? 1 : 3) * a.e_max + q] = (uint32_t)(sp[0] % kOrder);
 }
 
 __global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs a) {
@@ -574,11 +707,10 @@ __global__ void __launch_bounds__(256) k_dec16_gj_final(BigArgs a) {
     }
 }
 
-size_t exp_lds_bytes() { return (kOrder + 1) * 2; }
 
 int grid16(qf_ctx* ctx, uint64_t units) {
     const uint64_t want = (units + kThreads16 - 1) / kThreads16;
-    return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)qf::ctx_num_cus(ctx) * 2));
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)qf::ctx_num_cus(ctx)));
 }
 
 #define QF_HIP(x)                                 \
@@ -620,14 +752,39 @@ std::vector<uint16_t> host_log16() {
     return lg;
 }
 
-int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name) {
+// lanes for 4 waves per SIMD: fewer lanes than this split the inputs
+uint64_t matvec_lanes_wanted(qf_ctx* ctx) { return (uint64_t)qf::ctx_num_cus(ctx) * 4 * 4 * 64; }
+
+// bytes of split accumulator launch_matvec needs for G generations (0: no split)
+size_t matvec_acc_bytes(qf_ctx* ctx, uint64_t G, uint32_t nout, uint32_t nin, uint32_t L) {
+    const uint64_t lanes = G * ((nout + kR16 - 1) / kR16) * ((L + 15) / 16);
+    if (lanes >= matvec_lanes_wanted(ctx) || nin < 64) return 0;
+    return G * nout * (((size_t)L + 15) / 16 * 16);
+}
+
+// acc: workspace of matvec_acc_bytes (null: never split)
+int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name, uint8_t* acc = nullptr) {
     a.Lu = (a.L + 15) / 16;
     a.nob = (a.nout + kR16 - 1) / kR16;
-    a.total_units = G * a.nob * a.Lu;
-    if (!a.total_units) return QF_OK;
+    const uint64_t lanes = G * a.nob * a.Lu;
+    if (!lanes || !a.nin) return QF_OK;
+    // enough lanes for 4 waves per SIMD, input chunks of at least 32 rows
+    const uint64_t want = matvec_lanes_wanted(ctx);
+    uint32_t ns = 1;
+    if (acc && lanes < want) ns = (uint32_t)std::min<uint64_t>((want + lanes - 1) / lanes, std::max(1u, a.nin / 32));
+    a.nsplit = ns;
+    a.kchunk = (a.nin + ns - 1) / ns;
+    a.acc_ws = reinterpret_cast<uint32_t*>(acc);
+    a.total_units = lanes * ns;
     hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-    hipLaunchKernelGGL(k_matvec16, dim3(grid16(ctx, a.total_units)), dim3(kThreads16), exp_lds_bytes(), st, a);
+    if (ns > 1) QF_HIP(hipMemsetAsync(acc, 0, G * a.nout * (size_t)a.Lu * 16, st));
+    hipLaunchKernelGGL(k_matvec16, dim3(grid16(ctx, a.total_units)), dim3(kThreads16), 0, st, a);
     QF_HIP(hipGetLastError());
+    if (ns > 1) {
+        const uint64_t n = G * a.nout * a.Lu;
+        hipLaunchKernelGGL(k_finish16, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st, a);
+        QF_HIP(hipGetLastError());
+    }
     qf::ctx_prof_end(ctx, st, ev, name);
     return QF_OK;
 }
@@ -646,27 +803,32 @@ int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const 
         (sh->src_row_stride & 15) || (sh->src_gen_stride & 15) || (sh->rep_row_stride & 15) ||
         (sh->rep_gen_stride & 15))
         return QF_EINVAL;
-    std::vector<uint16_t> c((size_t)r * k);
-    if (coeff_rxk) {
-        memcpy(c.data(), coeff_rxk, c.size() * 2);
-    } else {
-        int s = qf_cauchy16_coeffs(k, r, c.data());
-        if (s) return s;
-    }
+    if (!coeff_rxk && (uint64_t)k + r > 65536) return QF_ERANGE;  // gf16_inv(0) in the Cauchy rows
     std::unique_lock<std::mutex> lk;
     int s = qf::ctx_lock(ctx, lk);
     if (s) return s;
     const uint16_t *glog, *gexp;
     s = qf::ctx_gf16_tables(ctx, &glog, &gexp);
     if (s) return s;
-    // coefficient logs (host tables: the same field)
-    static const std::vector<uint16_t> lg = host_log16();
-    for (auto& v : c) v = lg[v];
+    const size_t cb = align256((size_t)r * k * 2), ab = matvec_acc_bytes(ctx, G, r, k, L);
     uint8_t* w;
-    s = qf::ctx_work(ctx, c.size() * 2, &w);
+    s = qf::ctx_work(ctx, cb + ab, &w);
     if (s) return s;
     hipStream_t st = qf::ctx_stream(ctx);
-    QF_HIP(hipMemcpyAsync(w, c.data(), c.size() * 2, hipMemcpyHostToDevice, st));
+    if (coeff_rxk) {
+        // coefficient logs (host tables: the same field); the upload reads
+        // host memory, so the call finishes before returning
+        static const std::vector<uint16_t> lg = host_log16();
+        std::vector<uint16_t> c((size_t)r * k);
+        for (size_t q = 0; q < c.size(); ++q) c[q] = lg[coeff_rxk[q]];
+        QF_HIP(hipMemcpyAsync(w, c.data(), c.size() * 2, hipMemcpyHostToDevice, st));
+        QF_HIP(hipStreamSynchronize(st));
+    } else {
+        const uint64_t n = (uint64_t)r * k;
+        hipLaunchKernelGGL(k_cauchy16_logs, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                           reinterpret_cast<uint16_t*>(w), k, r, glog);
+        QF_HIP(hipGetLastError());
+    }
     Mv16Args a{};
     a.in = src;
     a.igs = sh->src_gen_stride;
@@ -681,11 +843,7 @@ int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const 
     a.nout = r;
     a.nin = k;
     a.L = L;
-    s = launch_matvec(ctx, st, a, G, "k_encode16");
-    if (s) return s;
-    // the coefficient upload reads host memory: finish before returning
-    QF_HIP(hipStreamSynchronize(st));
-    return QF_OK;
+    return launch_matvec(ctx, st, a, G, "k_encode16", ab ? w + cb : nullptr);
 }
 
 int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
@@ -711,7 +869,8 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     uint8_t* w;
     if (e_max <= kEMax) {
         // small path: every generation at once
-        s = qf::ctx_work(ctx, (size_t)G * ew * k * 2, &w);
+        const size_t wb = align256((size_t)G * ew * k * 2), ab = matvec_acc_bytes(ctx, G, e_max, k, L);
+        s = qf::ctx_work(ctx, wb + ab, &w);
         if (s) return s;
         Dec16Args d{};
         d.row_index = row_index;
@@ -748,16 +907,17 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         c.nout = e_max;
         c.nin = k;
         c.L = L;
-        return launch_matvec(ctx, st, c, G, "k_combine16");
+        return launch_matvec(ctx, st, c, G, "k_combine16", ab ? w + wb : nullptr);
     }
     // large path (e_max > 64, Extreme windows of 1024..4096): one generation
     // at a time, inverse in closed form (Cauchy rows) or by Gauss-Jordan
     const size_t Lp = ((size_t)L + 15) / 16 * 16;
-    size_t off[13], tot = 0;
-    const size_t sz[13] = {sizeof(Dec16State), 2ull * e_max, 2ull * e_max, 2ull * e_max, 2ull * k, 2ull * k,
+    size_t off[14], tot = 0;
+    const size_t sz[14] = {sizeof(Dec16State), 2ull * e_max, 2ull * e_max, 2ull * e_max, 2ull * k, 2ull * k,
                            2ull * e_max * k, 2ull * e_max * e_max, row_coeffs ? 4ull * e_max * e_max : 0,
-                           4ull * e_max, 4ull * e_max, 16ull * e_max, Lp * e_max};
-    for (int q = 0; q < 13; ++q) {
+                           4ull * e_max, 4ull * e_max, 16ull * e_max, Lp * e_max,
+                           matvec_acc_bytes(ctx, 1, e_max, k, L)};
+    for (int q = 0; q < 14; ++q) {
         off[q] = tot;
         tot += align256(std::max<size_t>(sz[q], 1));
     }
@@ -796,7 +956,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         hipLaunchKernelGGL(k_dec16_accept, dim3(1), dim3(1024), 0, st, b);
         hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid), dim3(256), 0, st, b);
         if (!row_coeffs) {
-            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3((2 * e_max + 255) / 256), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max), dim3(256), 0, st, b);
             hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid), dim3(256), 0, st, b);
         } else {
             hipLaunchKernelGGL(k_dec16_gj_init, dim3((uint32_t)std::min<uint64_t>(((uint64_t)e_max * 2 * e_max + 255) / 256,
@@ -831,7 +991,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         sy.nout = e_max;
         sy.nin = k;
         sy.L = L;
-        s = launch_matvec(ctx, st, sy, 1, "k_syndromes16");
+        s = launch_matvec(ctx, st, sy, 1, "k_syndromes16", sz[13] ? w + off[13] : nullptr);
         if (s) return s;
         // x_E = C[J,E]^-1 s
         Mv16Args so{};
@@ -848,7 +1008,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         so.nout = e_max;
         so.nin = e_max;
         so.L = L;
-        s = launch_matvec(ctx, st, so, 1, "k_combine16");
+        s = launch_matvec(ctx, st, so, 1, "k_combine16", sz[13] ? w + off[13] : nullptr);
         if (s) return s;
     }
     return QF_OK;
