@@ -226,10 +226,12 @@ int qf_decoder_get_decoded_packets(qf_decoder *dec, uint8_t *out_data, uint32_t 
  * contraction).  Time is in seconds on a monotonic clock; the *_at variants
  * take it explicitly (deterministic tests), the others read CLOCK_MONOTONIC.
  *
- * Codec: GF(2^8) encoder/decoder objects above.  A configuration the GF(2^8)
- * Cauchy code cannot realise (k + r > 256, where the reference panics in
- * gf_inv(0); or Extreme mode, which the reference runs in GF(2^16)) has no
- * codec: on_send still emits the systematic packet and returns QF_ERANGE.
+ * Codec: the GF(2^8) encoder/decoder objects above, and in Extreme mode the
+ * GF(2^16) ones (decoder.rs:96-102; coefficient blocks of 2k bytes, so
+ * coeff_stride >= 2k there).  A configuration the field cannot realise
+ * (GF(2^8): k + r > 256, where the reference panics in gf_inv(0); GF(2^16):
+ * k > 4096 or n > 65536) has no codec: on_send still emits the systematic
+ * packet and returns QF_ERANGE.
  * ------------------------------------------------------------------------- */
 #define QF_MODE_ZERO 0
 #define QF_MODE_LIGHT 1
@@ -387,6 +389,44 @@ int qf_decode16_batch(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G, con
                       const uint16_t *row_index_dev, const uint32_t *n_rows_dev,
                       const uint16_t *row_coeffs_dev, uint8_t *rec_dev, uint16_t *rec_index_dev,
                       uint32_t *n_rec_dev, int32_t *status_dev);
+
+/* GF(2^16) per-connection objects (the Extreme-mode codec of
+ * EncoderVariant / DecoderVariant, decoder.rs:90-153).  k <= 4096 (Extreme
+ * windows, adaptive.rs:131).  Coefficient blocks are 2k bytes, big-endian u16
+ * (decoder.rs:62-66). */
+typedef struct qf_encoder16 qf_encoder16;
+/* replaces decoder.rs:17 Encoder16::new(k, n) */
+int qf_encoder16_new(qf_ctx *ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_encoder16 **out);
+int qf_encoder16_free(qf_encoder16 *enc);
+/* replaces decoder.rs:25 Encoder16::add_source_packet (slides the window) */
+int qf_encoder16_add_source_packet(qf_encoder16 *enc, uint64_t id, const uint8_t *data, uint32_t len);
+/* replaces decoder.rs:33 Encoder16::generate_repair_packet(j): QF_ENOTREADY
+ * while the window is not full (None); len = window[0].len (an odd last
+ * byte is 0, decoder.rs:44); out_coeffs 2k bytes; id = last.id + 1 + j. */
+int qf_encoder16_generate_repair_packet(qf_encoder16 *enc, uint32_t repair_index, uint8_t *out_data,
+                                        uint32_t out_cap, uint32_t *out_len, uint8_t *out_coeffs,
+                                        uint64_t *out_id);
+/* Repairs first..first+count-1 of the window in one launch; coefficient
+ * blocks packed 2k bytes apart.  QF_ERANGE when k + first + count > 65536. */
+int qf_encoder16_generate_repairs(qf_encoder16 *enc, uint32_t first, uint32_t count, uint8_t *out_data,
+                                  uint32_t out_stride, uint32_t *out_len, uint8_t *out_coeffs,
+                                  uint64_t *out_ids);
+int qf_encoder16_window_len(const qf_encoder16 *enc);
+typedef struct qf_decoder16 qf_decoder16;
+/* replaces decoder.rs:545 Decoder16::new(k, pool) */
+int qf_decoder16_new(qf_ctx *ctx, uint32_t k, uint32_t max_len, qf_decoder16 **out);
+int qf_decoder16_free(qf_decoder16 *dec);
+/* replaces decoder.rs:555 Decoder16::add_packet: the first k packets are the
+ * system (no duplicate filtering); decoding runs when the k-th arrives
+ * (whatever its kind).  1 = decoded, 0 = not (yet, or singular: stays so),
+ * QF_EINVAL for a repair without coefficients ("missing coeffs"). */
+int qf_decoder16_add_packet(qf_decoder16 *dec, uint64_t id, int is_systematic, const uint8_t *data,
+                            uint32_t len, const uint8_t *coeffs, uint32_t coeff_len);
+int qf_decoder16_is_decoded(const qf_decoder16 *dec);
+/* replaces decoder.rs:643 get_decoded_packets: drains the k source packets in
+ * index order (as qf_decoder_get_decoded_packets). */
+int qf_decoder16_get_decoded_packets(qf_decoder16 *dec, uint8_t *out_data, uint32_t out_stride,
+                                     uint32_t *out_len, uint64_t *out_ids, uint32_t *count);
 
 /* ---------------------------------------------------------------------------
  * Synthetic payload (bench / tests): byte t of the region is byte (t & 7) of

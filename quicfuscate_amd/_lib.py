@@ -113,6 +113,17 @@ _SIGS = {
     "qf_cauchy16_coeffs": (_I, [_U32, _U32, _P]),
     "qf_encode16_batch": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
     "qf_decode16_batch": (_I, [_P, ctypes.POINTER(DecodeShape), _U32, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "qf_encoder16_new": (_I, [_P, _U32, _U32, _U32, ctypes.POINTER(_P)]),
+    "qf_encoder16_free": (_I, [_P]),
+    "qf_encoder16_add_source_packet": (_I, [_P, _U64, _P, _U32]),
+    "qf_encoder16_generate_repair_packet": (_I, [_P, _U32, _P, _U32, _P, _P, _P]),
+    "qf_encoder16_generate_repairs": (_I, [_P, _U32, _U32, _P, _U32, _P, _P, _P]),
+    "qf_encoder16_window_len": (_I, [_P]),
+    "qf_decoder16_new": (_I, [_P, _U32, _U32, ctypes.POINTER(_P)]),
+    "qf_decoder16_free": (_I, [_P]),
+    "qf_decoder16_add_packet": (_I, [_P, _U64, _I, _P, _U32, _P, _U32]),
+    "qf_decoder16_is_decoded": (_I, [_P]),
+    "qf_decoder16_get_decoded_packets": (_I, [_P, _P, _U32, _P, _P, _P]),
     "qf_fill_splitmix_dev": (_I, [_P, _P, _SZ, _U64, _U64]),
     "qf_selftest_split_tables": (_I, []),
     "qf_frame_batch_dev": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P, _U64, _P]),

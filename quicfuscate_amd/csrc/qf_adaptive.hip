@@ -3,8 +3,9 @@
 //
 // A restatement of the reference's controller and its per-connection codec
 // plumbing (adaptive.rs:44-631, mod.rs:56-79, decoder.rs:90-153) over the
-// GF(2^8) encoder / decoder objects of qf_objects.hip.  Host logic only: the
-// payload arithmetic runs in the objects' device kernels.
+// GF(2^8) encoder / decoder objects of qf_objects.hip and, in Extreme mode,
+// the GF(2^16) ones of qf_objects16.hip.  Host logic only: the payload
+// arithmetic runs in the objects' device kernels.
 //
 // Arithmetic is f32 and evaluated operation by operation as Rust does (no
 // FMA contraction), so mode and window decisions match the reference for the
@@ -172,20 +173,29 @@ void params_for(int32_t mode, uint32_t window, uint32_t* k, uint32_t* n) {
     *n = sat_u32(ceilf((float)window * kRatio[mode]));
 }
 
-// EncoderVariant / DecoderVariant (decoder.rs:90-153) restricted to GF(2^8)
+// EncoderVariant / DecoderVariant (decoder.rs:90-153): GF(2^16) objects in
+// Extreme mode, GF(2^8) otherwise
 struct Codec {
     int32_t mode = QF_MODE_ZERO;
     uint32_t k = 0, n = 0;
     qf_encoder* enc = nullptr;
     qf_decoder* dec = nullptr;
-    int status = QF_OK;  // QF_ERANGE: no GF(2^8) realisation of (mode, k, n)
+    qf_encoder16* enc16 = nullptr;
+    qf_decoder16* dec16 = nullptr;
+    int status = QF_OK;  // QF_ERANGE: the field cannot realise (mode, k, n)
     bool decoded = false;
 
+    bool has_enc() const { return enc || enc16; }
+    uint32_t coeff_bytes() const { return enc16 ? 2 * k : k; }
     void release() {
         if (enc) qf_encoder_free(enc);
         if (dec) qf_decoder_free(dec);
+        if (enc16) qf_encoder16_free(enc16);
+        if (dec16) qf_decoder16_free(dec16);
         enc = nullptr;
         dec = nullptr;
+        enc16 = nullptr;
+        dec16 = nullptr;
     }
 };
 
@@ -210,10 +220,27 @@ int make_codec(qf_adaptive* a, int32_t mode, uint32_t k, uint32_t n, Codec* c) {
     c->n = n;
     c->enc = nullptr;
     c->dec = nullptr;
+    c->enc16 = nullptr;
+    c->dec16 = nullptr;
     c->decoded = false;
     c->status = QF_OK;
     if (k == 0) return QF_OK;  // Zero mode: nothing to encode or decode
-    if (mode == QF_MODE_EXTREME || k > 255 || n > 256) {
+    if (mode == QF_MODE_EXTREME) {
+        // decoder.rs:96-102: GF(2^16); repairs 0..n-k need k + (n - k) <= 65536
+        if (k > 4096 || n > 65536) {
+            c->status = QF_ERANGE;
+            return QF_OK;
+        }
+        if (!a->ctx) return QF_OK;
+        int s = qf_encoder16_new(a->ctx, k, n, a->cfg.max_len, &c->enc16);
+        if (s == QF_OK) s = qf_decoder16_new(a->ctx, k, a->cfg.max_len, &c->dec16);
+        if (s != QF_OK) {
+            c->release();
+            return s;
+        }
+        return QF_OK;
+    }
+    if (k > 255 || n > 256) {
         c->status = QF_ERANGE;
         return QF_OK;
     }
@@ -227,30 +254,39 @@ int make_codec(qf_adaptive* a, int32_t mode, uint32_t k, uint32_t n, Codec* c) {
     return QF_OK;
 }
 
+int add_source(Codec& c, uint64_t id, const uint8_t* data, uint32_t len) {
+    if (c.enc16) return qf_encoder16_add_source_packet(c.enc16, id, data, len);
+    if (c.enc) return qf_encoder_add_source_packet(c.enc, id, data, len);
+    return QF_OK;
+}
+
 // emit_repairs (adaptive.rs:546-562): repairs 0..n-k of a full window
 int emit_repairs(Codec& c, uint8_t* out_data, uint32_t out_stride, uint8_t* out_coeffs,
                  uint32_t coeff_stride, qf_packet_desc* desc, uint32_t* n) {
-    if (!c.enc) return QF_OK;
+    if (!c.has_enc()) return QF_OK;
     const uint32_t r = c.n - c.k;
     if (r == 0) return QF_OK;
     std::vector<uint32_t> lens(r);
     std::vector<uint64_t> ids(r);
-    int s = qf_encoder_generate_repairs(c.enc, 0, r, out_data + (size_t)*n * out_stride, out_stride,
-                                        lens.data(), out_coeffs ? out_coeffs + (size_t)*n * coeff_stride : nullptr,
-                                        ids.data());
+    uint8_t* co = out_coeffs ? out_coeffs + (size_t)*n * coeff_stride : nullptr;
+    int s = c.enc16 ? qf_encoder16_generate_repairs(c.enc16, 0, r, out_data + (size_t)*n * out_stride, out_stride,
+                                                    lens.data(), co, ids.data())
+                    : qf_encoder_generate_repairs(c.enc, 0, r, out_data + (size_t)*n * out_stride, out_stride,
+                                                  lens.data(), co, ids.data());
     if (s == QF_ENOTREADY) return QF_OK;  // window not full: generate_repair_packet -> None
     if (s != QF_OK) return s;
-    if (out_coeffs && coeff_stride != c.k) {
-        // generate_repairs packs coefficients k bytes apart: spread them
+    const uint32_t cb = c.coeff_bytes();
+    if (out_coeffs && coeff_stride != cb) {
+        // generate_repairs packs the coefficient blocks cb bytes apart: spread them
         for (uint32_t q = r; q-- > 1;)
-            memmove(out_coeffs + (size_t)(*n + q) * coeff_stride, out_coeffs + (size_t)*n * coeff_stride + (size_t)q * c.k,
-                    c.k);
+            memmove(out_coeffs + (size_t)(*n + q) * coeff_stride, out_coeffs + (size_t)*n * coeff_stride + (size_t)q * cb,
+                    cb);
     }
     for (uint32_t q = 0; q < r; ++q) {
         qf_packet_desc& d = desc[*n + q];
         d.id = ids[q];
         d.len = lens[q];
-        d.coeff_len = c.k;
+        d.coeff_len = cb;
         d.is_systematic = 0;
         d.reserved = 0;
     }
@@ -264,8 +300,10 @@ int drain_decoded(Codec& c, uint8_t* out_data, uint32_t out_stride, qf_packet_de
     std::vector<uint32_t> lens(c.k);
     std::vector<uint64_t> ids(c.k);
     uint32_t cnt = 0;
-    int s = qf_decoder_get_decoded_packets(c.dec, out_data + (size_t)*n * out_stride, out_stride, lens.data(),
-                                           ids.data(), &cnt);
+    int s = c.dec16 ? qf_decoder16_get_decoded_packets(c.dec16, out_data + (size_t)*n * out_stride, out_stride,
+                                                       lens.data(), ids.data(), &cnt)
+                    : qf_decoder_get_decoded_packets(c.dec, out_data + (size_t)*n * out_stride, out_stride, lens.data(),
+                                                     ids.data(), &cnt);
     if (s != QF_OK) return s;
     for (uint32_t q = 0; q < cnt; ++q) {
         qf_packet_desc& d = desc[*n + q];
@@ -283,13 +321,14 @@ int drain_decoded(Codec& c, uint8_t* out_data, uint32_t out_stride, qf_packet_de
 int receive_into(Codec& c, uint64_t id, int sys, const uint8_t* data, uint32_t len, const uint8_t* coeffs,
                  uint32_t coeff_len, uint8_t* out_data, uint32_t out_stride, qf_packet_desc* desc,
                  uint32_t out_cap, uint32_t* n) {
-    if (c.k == 0 || !c.dec) {
-        // Zero mode (decoder.rs:679: num_rows >= k) or no GF(2^8) codec
+    if (c.k == 0 || !(c.dec || c.dec16)) {
+        // Zero mode (decoder.rs:679: num_rows >= k) or no codec for the configuration
         if (!sys && !coeffs) return QF_EINVAL;
         return QF_OK;
     }
     const bool was = c.decoded;
-    int s = qf_decoder_add_packet(c.dec, id, sys, data, len, coeffs, coeff_len);
+    int s = c.dec16 ? qf_decoder16_add_packet(c.dec16, id, sys, data, len, coeffs, coeff_len)
+                    : qf_decoder_add_packet(c.dec, id, sys, data, len, coeffs, coeff_len);
     if (s < 0) return s;
     c.decoded = s == 1;
     if (!was && c.decoded) return drain_decoded(c, out_data, out_stride, desc, out_cap, n);
@@ -403,8 +442,8 @@ int qf_adaptive_state(const qf_adaptive* a, int32_t* mode, uint32_t* window, uin
 uint32_t qf_adaptive_max_send_packets(const qf_adaptive* a) {
     if (!a) return 0;
     uint32_t m = 1;
-    if (a->cur.enc) m += a->cur.n - a->cur.k;
-    if (a->has_fade && a->fade.enc) m += a->fade.n - a->fade.k;
+    if (a->cur.has_enc()) m += a->cur.n - a->cur.k;
+    if (a->has_fade && a->fade.has_enc()) m += a->fade.n - a->fade.k;
     return m;
 }
 
@@ -415,19 +454,18 @@ int qf_adaptive_on_send(qf_adaptive* a, uint64_t id, const uint8_t* data, uint32
     *n_out = 0;
     if (len > a->cfg.max_len || out_stride < len) return QF_EINVAL;
     const bool fade_repairs = a->has_fade && a->transition_left > kFade / 2;
-    uint32_t need = 1 + (a->cur.enc ? a->cur.n - a->cur.k : 0) +
-                    (fade_repairs && a->fade.enc ? a->fade.n - a->fade.k : 0);
+    uint32_t need = 1 + (a->cur.has_enc() ? a->cur.n - a->cur.k : 0) +
+                    (fade_repairs && a->fade.has_enc() ? a->fade.n - a->fade.k : 0);
     if (need > out_cap) return QF_ETOOSMALL;
     if (out_coeffs) {
-        uint32_t kmax = a->cur.enc ? a->cur.k : 0;
-        if (fade_repairs && a->fade.enc && a->fade.k > kmax) kmax = a->fade.k;
-        if (coeff_stride < kmax) return QF_ETOOSMALL;
+        uint32_t cmax = a->cur.has_enc() ? a->cur.coeff_bytes() : 0;
+        if (fade_repairs && a->fade.has_enc() && a->fade.coeff_bytes() > cmax) cmax = a->fade.coeff_bytes();
+        if (coeff_stride < cmax) return QF_ETOOSMALL;
     }
     // adaptive.rs:520-526: both encoders take a copy; the systematic packet is sent
     int s;
-    if (a->has_fade && a->fade.enc && (s = qf_encoder_add_source_packet(a->fade.enc, id, data, len)) != QF_OK)
-        return s;
-    if (a->cur.enc && (s = qf_encoder_add_source_packet(a->cur.enc, id, data, len)) != QF_OK) return s;
+    if (a->has_fade && (s = add_source(a->fade, id, data, len)) != QF_OK) return s;
+    if ((s = add_source(a->cur, id, data, len)) != QF_OK) return s;
     uint32_t n = 0;
     if (len) memcpy(out_data, data, len);
     out_desc[0].id = id;
@@ -448,7 +486,7 @@ int qf_adaptive_on_send(qf_adaptive* a, uint64_t id, const uint8_t* data, uint32
         }
     }
     *n_out = n;
-    return a->cur.status;  // QF_ERANGE: this configuration has no GF(2^8) repairs
+    return a->cur.status;  // QF_ERANGE: the field has no code for this configuration
 }
 
 int qf_adaptive_on_receive(qf_adaptive* a, uint64_t id, int is_systematic, const uint8_t* data, uint32_t len,

@@ -265,13 +265,25 @@ __global__ void __launch_bounds__(256) k_finish16(Mv16Args a) {
     }
 }
 
-// logs of the Cauchy rows: m[j][i] = log inv(i ^ (k + j)) = -log(i ^ (k + j))
-__global__ void __launch_bounds__(256) k_cauchy16_logs(uint16_t* m, uint32_t k, uint32_t r, const uint16_t* glog) {
+// Logs of the Cauchy rows first..first+r-1 over a ring of k source slots
+// whose window position i sits in slot (rot + i) % k:
+//   m[q][slot] = log inv(i ^ (k + first + q)) = -log(i ^ y)   (decoder.rs:77-80)
+// be_out (optional): each row's coefficient block in window order, big-endian
+// u16 (decoder.rs:62-66).
+__global__ void __launch_bounds__(256) k_cauchy16_logs(uint16_t* m, uint32_t k, uint32_t r, uint32_t first, uint32_t rot,
+                                                       const uint16_t* glog, const uint16_t* gexp, uint8_t* be_out) {
     const uint64_t total = (uint64_t)k * r;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t j = (uint32_t)(t / k), i = (uint32_t)(t % k);
-        const uint32_t l = glog[i ^ ((k + j) & 0xFFFF)];
-        m[t] = (uint16_t)(l ? kOrder - l : 0);
+        const uint32_t q = (uint32_t)(t / k), slot = (uint32_t)(t % k);
+        const uint32_t i = slot >= rot ? slot - rot : slot + k - rot;
+        const uint32_t l = glog[i ^ ((k + first + q) & 0xFFFF)];  // i ^ y != 0: i < k <= y
+        const uint32_t nl = l ? kOrder - l : 0;
+        m[t] = (uint16_t)nl;
+        if (be_out) {
+            const uint32_t c = gexp[nl];
+            be_out[((uint64_t)q * k + i) * 2] = (uint8_t)(c >> 8);
+            be_out[((uint64_t)q * k + i) * 2 + 1] = (uint8_t)c;
+        }
     }
 }
 
@@ -793,8 +805,12 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
-int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src, uint8_t* rep,
-                      const uint16_t* coeff_rxk) {
+}  // extern "C"
+
+namespace qf {
+
+int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src, uint8_t* rep,
+                    const uint16_t* coeff_rxk, uint32_t first, uint32_t rot, uint8_t* coeff_be_dev) {
     if (!ctx || !sh) return QF_EINVAL;
     const uint32_t k = sh->k, r = sh->r, L = sh->L;
     if (k == 0 || k > 65535 || (L & 1) || sh->flags) return QF_EINVAL;
@@ -803,7 +819,8 @@ int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const 
         (sh->src_row_stride & 15) || (sh->src_gen_stride & 15) || (sh->rep_row_stride & 15) ||
         (sh->rep_gen_stride & 15))
         return QF_EINVAL;
-    if (!coeff_rxk && (uint64_t)k + r > 65536) return QF_ERANGE;  // gf16_inv(0) in the Cauchy rows
+    if (!coeff_rxk && (uint64_t)k + first + r > 65536) return QF_ERANGE;  // gf16_inv(0) in the Cauchy rows
+    if (rot >= k || (coeff_rxk && (first || rot || coeff_be_dev))) return QF_EINVAL;
     std::unique_lock<std::mutex> lk;
     int s = qf::ctx_lock(ctx, lk);
     if (s) return s;
@@ -826,7 +843,7 @@ int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const 
     } else {
         const uint64_t n = (uint64_t)r * k;
         hipLaunchKernelGGL(k_cauchy16_logs, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
-                           reinterpret_cast<uint16_t*>(w), k, r, glog);
+                           reinterpret_cast<uint16_t*>(w), k, r, first, rot, glog, gexp, coeff_be_dev);
         QF_HIP(hipGetLastError());
     }
     Mv16Args a{};
@@ -844,6 +861,15 @@ int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const 
     a.nin = k;
     a.L = L;
     return launch_matvec(ctx, st, a, G, "k_encode16", ab ? w + cb : nullptr);
+}
+
+}  // namespace qf
+
+extern "C" {
+
+int qf_encode16_batch(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src, uint8_t* rep,
+                      const uint16_t* coeff_rxk) {
+    return qf::encode16_window(ctx, sh, G, src, rep, coeff_rxk, 0, 0, nullptr);
 }
 
 int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,

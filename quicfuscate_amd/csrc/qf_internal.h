@@ -18,11 +18,22 @@ int ctx_num_cus(qf_ctx* ctx);
 // The context's device workspace, grown to at least `bytes` (shared with the
 // decode paths; valid until the next call on this context).
 int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out);
-// GF(2^16) tables on the device, built on first use: log[65536] (log[0]
-// unused) and exp[2 * 65535] (exp[i + 65535] = exp[i]).
+// GF(2^16) tables on the device, built on first use: log[65536] (log[0] =
+// 0xFFFF, no product) and exp[2 * 65535] (exp[i + 65535] = exp[i]).
 int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp);
 // qf_ctx_profile bracketing of a launch.
 hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st);
 void ctx_prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t ev, const std::string& name);
+
+}  // namespace qf
+
+namespace qf {
+
+// qf_encode16_batch over a ring of k source slots: window position i in slot
+// (rot + i) % k, repairs = Cauchy rows first..first+r-1 (coeff_rxk must be
+// NULL for first/rot != 0); coeff_be_dev (optional, device) receives each
+// repair's big-endian coefficient block in window order.  (qf_gf16.hip)
+int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src, uint8_t* rep,
+                    const uint16_t* coeff_rxk, uint32_t first, uint32_t rot, uint8_t* coeff_be_dev);
 
 }  // namespace qf

@@ -428,118 +428,109 @@ def decode16_batch(rows, row_index, rec, rec_index, n_rec, status, k: int, r: in
         _ptr(n_rec), _ptr(status)), "decode16_batch")
 
 
-def _be16(vals) -> bytes:
-    return b"".join(int(v).to_bytes(2, "big") for v in vals)
-
-
 class Encoder16:
-    """decoder.rs:10-88 Encoder16: sliding window of k packets, repair j carries
-    the Cauchy row y = k + j as a big-endian u16 coefficient block."""
+    """decoder.rs:10-88 Encoder16 over qf_encoder16_*: sliding window of k
+    packets; repair j carries the Cauchy row y = k + j as a big-endian u16
+    coefficient block of 2k bytes."""
 
-    def __init__(self, k: int, n: int, ctx: Optional[Context] = None):
-        self.k, self.n = k, n
+    def __init__(self, k: int, n: int, max_len: int = 4096, ctx: Optional[Context] = None):
+        self.k, self.n, self.max_len = k, n, max_len
         self.ctx = ctx or default_context()
-        self.window: _deque = _deque(maxlen=k)
+        h = ctypes.c_void_p()
+        check(L._lib().qf_encoder16_new(self.ctx.handle, k, n, max_len, ctypes.byref(h)), "Encoder16::new")
+        self.handle = h
 
     def add_source_packet(self, packet: Packet) -> None:
-        self.window.append(packet)
+        data = packet.payload()
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data.ljust(max(1, len(data)), b"\0"))
+        check(L._lib().qf_encoder16_add_source_packet(self.handle, packet.id, buf, len(data)), "add_source_packet")
 
     def generate_repair_packet(self, repair_packet_index: int, pool: Optional[MemoryPool] = None) -> Optional[Packet]:
-        if len(self.window) < self.k:
+        out = (ctypes.c_uint8 * self.max_len)()
+        coeffs = (ctypes.c_uint8 * (2 * self.k))()
+        n = ctypes.c_uint32(0)
+        pid = ctypes.c_uint64(0)
+        s = L._lib().qf_encoder16_generate_repair_packet(self.handle, repair_packet_index, out, self.max_len,
+                                                         ctypes.byref(n), coeffs, ctypes.byref(pid))
+        if s == L.QF_ENOTREADY:
             return None
-        import torch
+        check(s, "generate_repair_packet")
+        block = pool.alloc() if pool is not None else bytearray(max(n.value, 1))
+        block[: n.value] = bytes(out)[: n.value]
+        return Packet(pid.value, block, n.value, False, bytes(coeffs), 2 * self.k)
 
-        L_ = self.window[0].len
-        if L_ & 1:
-            raise QfError(L.QF_EINVAL, "Encoder16: odd packet length")
-        row = [gf16_inv((i ^ (self.k + repair_packet_index)) & 0xFFFF) for i in range(self.k)]
-        stride = max(16, (L_ + 15) // 16 * 16)
-        host = bytearray(self.k * stride)
-        for i, p in enumerate(self.window):
-            host[i * stride: i * stride + L_] = bytes(p.data[:L_]).ljust(L_, b"\0")
-        dev = f"cuda:{self.ctx.device}"
-        src = torch.frombuffer(host, dtype=torch.uint8).to(dev)
-        rep = torch.zeros(stride, dtype=torch.uint8, device=dev)
-        torch.cuda.current_stream(self.ctx.device).synchronize()
-        encode16_batch(src, rep, self.k, 1, L_, src_row_stride=stride, src_gen_stride=self.k * stride,
-                       rep_row_stride=stride, rep_gen_stride=stride, G=1, coeff=[row], ctx=self.ctx)
-        self.ctx.sync()
-        data = bytes(rep[:L_].cpu().numpy().tobytes())
-        block = pool.alloc() if pool is not None else bytearray(max(L_, 1))
-        block[:L_] = data
-        return Packet(self.window[-1].id + 1 + repair_packet_index, block, L_, False, _be16(row), 2 * self.k)
+    def generate_repairs(self, first: int, count: int) -> list[Packet]:
+        stride = (self.max_len + 15) // 16 * 16
+        out = (ctypes.c_uint8 * (stride * count))()
+        coeffs = (ctypes.c_uint8 * (2 * self.k * count))()
+        lens = (ctypes.c_uint32 * count)()
+        ids = (ctypes.c_uint64 * count)()
+        s = L._lib().qf_encoder16_generate_repairs(self.handle, first, count, out, stride, lens, coeffs, ids)
+        if s == L.QF_ENOTREADY:
+            return []
+        check(s, "generate_repairs")
+        raw, cb, kb = bytes(out), bytes(coeffs), 2 * self.k
+        return [Packet(ids[q], bytearray(raw[q * stride: q * stride + lens[q]]), lens[q], False,
+                       cb[q * kb: (q + 1) * kb], kb) for q in range(count)]
+
+    def __del__(self):  # pragma: no cover
+        try:
+            L._lib().qf_encoder16_free(self.handle)
+        except Exception:
+            pass
 
 
 class Decoder16:
-    """decoder.rs:536-656 Decoder16: the first k packets (systematic column
-    id % k, repair rows from their big-endian u16 coefficient blocks), no
-    duplicate filtering.  Systematic payloads are carried (F4-style fix), and
-    decoding runs once k rows are present, whatever the last row's kind."""
+    """decoder.rs:536-656 Decoder16 over qf_decoder16_*: the first k packets
+    (systematic column id % k, repair rows from their big-endian u16
+    coefficient blocks), no duplicate filtering.  Systematic payloads are
+    carried (F4-style fix) and decoding runs once k rows are present, whatever
+    the last row's kind; get_decoded_packets returns the whole generation."""
 
-    def __init__(self, k: int, ctx: Optional[Context] = None):
+    def __init__(self, k: int, pool: Optional[MemoryPool] = None, max_len: int = 4096,
+                 ctx: Optional[Context] = None):
         self.k = k
         self.ctx = ctx or default_context()
-        self.rows: list[tuple[int, bytes, Optional[list[int]]]] = []
-        self.is_decoded = False
-        self._decoded: list[Packet] = []
+        self.max_len = pool.block_size if pool is not None else max_len
+        h = ctypes.c_void_p()
+        check(L._lib().qf_decoder16_new(self.ctx.handle, k, self.max_len, ctypes.byref(h)), "Decoder16::new")
+        self.handle = h
+
+    @property
+    def is_decoded(self) -> bool:
+        return bool(check(L._lib().qf_decoder16_is_decoded(self.handle)))
 
     def add_packet(self, packet: Packet) -> bool:
-        if self.is_decoded or len(self.rows) >= self.k:
-            return self.is_decoded
-        if packet.is_systematic:
-            self.rows.append((packet.id % self.k, packet.payload(), None))
-        elif packet.coefficients is not None:
-            c = bytes(packet.coefficients)
-            self.rows.append((self.k, packet.payload(), [int.from_bytes(c[2 * i: 2 * i + 2], "big")
-                                                          for i in range(self.k)]))
-        else:
+        data = packet.payload()
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data.ljust(max(1, len(data)), b"\0"))
+        co = None
+        if packet.coefficients is not None:
+            cb = bytes(packet.coefficients[: packet.coeff_len])
+            co = (ctypes.c_uint8 * max(1, len(cb))).from_buffer_copy(cb.ljust(max(1, len(cb)), b"\0"))
+        elif not packet.is_systematic:
             raise QfError(L.QF_EINVAL, "missing coeffs")
-        if len(self.rows) == self.k:
-            self._try_decode()
-        return self.is_decoded
-
-    def _try_decode(self) -> None:
-        import numpy as np
-        import torch
-
-        k = self.k
-        L_ = max(len(p) for _, p, _ in self.rows)
-        if L_ & 1:
-            raise QfError(L.QF_EINVAL, "Decoder16: odd packet length")
-        stride = max(16, (L_ + 15) // 16 * 16)
-        rows = np.zeros((k, stride), np.uint8)
-        coef = np.zeros((k, k), np.uint16)
-        idx = np.zeros(k, np.uint16)
-        for s, (i, p, c) in enumerate(self.rows):
-            rows[s, : len(p)] = np.frombuffer(p, np.uint8)
-            idx[s] = i
-            if c is not None:
-                coef[s] = c
-        e_max = k
-        dev = f"cuda:{self.ctx.device}"
-        t_rows = torch.from_numpy(rows.reshape(-1)).to(dev)
-        t_idx = torch.from_numpy(idx.view(np.int16)).to(dev)
-        t_coef = torch.from_numpy(coef.view(np.int16).reshape(-1)).to(dev)
-        t_rec = torch.zeros(e_max * stride, dtype=torch.uint8, device=dev)
-        t_ri = torch.zeros(e_max, dtype=torch.int16, device=dev)
-        t_n = torch.zeros(1, dtype=torch.int32, device=dev)
-        t_st = torch.zeros(1, dtype=torch.int32, device=dev)
-        torch.cuda.current_stream(self.ctx.device).synchronize()
-        decode16_batch(t_rows, t_idx, t_rec, t_ri, t_n, t_st, k, e_max, L_, max_rows=k, row_stride=stride,
-                       rows_gen_stride=k * stride, rec_row_stride=stride, rec_gen_stride=e_max * stride, G=1,
-                       row_coeffs=t_coef, ctx=self.ctx)
-        self.ctx.sync()
-        if int(t_st[0]) != L.QF_OK:
-            return  # singular: stays undecoded, as try_decode returning false
-        n = int(t_n[0])
-        rec = t_rec.cpu().numpy().reshape(e_max, stride)
-        ri = t_ri.cpu().numpy().view(np.uint16)
-        self._decoded = [Packet(int(ri[b]), bytearray(rec[b, :L_].tobytes()), L_, True) for b in range(n)]
-        self.is_decoded = True
+        s = L._lib().qf_decoder16_add_packet(self.handle, packet.id, 1 if packet.is_systematic else 0, buf,
+                                             len(data), ctypes.cast(co, ctypes.c_void_p) if co is not None else None,
+                                             packet.coeff_len)
+        return bool(check(s, "add_packet"))
 
     def get_decoded_packets(self) -> list[Packet]:
-        out, self._decoded = self._decoded, []
-        return out
+        stride = (self.max_len + 15) // 16 * 16
+        out = (ctypes.c_uint8 * (stride * self.k))()
+        lens = (ctypes.c_uint32 * self.k)()
+        ids = (ctypes.c_uint64 * self.k)()
+        cnt = ctypes.c_uint32(0)
+        check(L._lib().qf_decoder16_get_decoded_packets(self.handle, out, stride, lens, ids, ctypes.byref(cnt)),
+              "get_decoded_packets")
+        raw = bytes(out)
+        return [Packet(ids[i], bytearray(raw[i * stride: i * stride + lens[i]]), lens[i], True)
+                for i in range(cnt.value)]
+
+    def __del__(self):  # pragma: no cover
+        try:
+            L._lib().qf_decoder16_free(self.handle)
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------
@@ -678,11 +669,12 @@ class AdaptiveFec:
 
     def on_send(self, pkt: Packet, outgoing_queue) -> int:
         """Pushes the systematic packet and its repairs onto outgoing_queue.
-        Returns the status (QF_ERANGE when the configuration has no GF(2^8)
-        code -- the reference panics or switches to GF(2^16) there)."""
+        Returns the status (QF_ERANGE when the field has no code for the
+        configuration -- GF(2^8) with k + r > 256, where the reference panics)."""
         cap = self._lib.qf_adaptive_max_send_packets(self.handle)
         stride = max(self.config.max_len, 1)
-        kmax = 256
+        st = self.state()
+        kmax = max(256, 2 * st["k"])  # coefficient bytes: k (GF(2^8)) or 2k (GF(2^16), Extreme)
         data = (ctypes.c_uint8 * (cap * stride))()
         co = (ctypes.c_uint8 * (cap * kmax))()
         desc = (L.PacketDesc * cap)()

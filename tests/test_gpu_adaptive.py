@@ -78,3 +78,46 @@ def test_cross_fade_with_codecs(qf, gpu_ctx):
         assert snd.on_send(qf.Packet(i, bytearray([i % 256] * 16), 16, True), out) == L.QF_OK
         assert len(out) == 1      # neither window (64 / 109 packets) is full yet
     assert not snd.is_transitioning()
+
+
+@pytest.mark.parametrize("window,L_,lost", [(24, 40, (0, 5, 23)), (1024, 64, tuple(range(0, 1024, 9)))])
+def test_extreme_mode_gf16_codec(qf, oracle, gpu_ctx, window, L_, lost):
+    """Extreme mode runs the GF(2^16) codec (decoder.rs:96-102, 125-131):
+    sliding-window repairs equal the GF(2^16) oracle's encode of the window
+    with 2k-byte big-endian coefficient blocks, and a receiver recovers the
+    generation through Decoder16 (closed-form path: aligned-window Cauchy rows)."""
+    M = qf.FecMode
+    wins = qf.default_windows()
+    wins[M.Extreme] = window
+    cfg = qf.FecConfig(initial_mode=M.Extreme, max_len=1500, window_sizes=wins)
+    snd, rcv = qf.AdaptiveFec(cfg, now=0.0), qf.AdaptiveFec(cfg, now=0.0)
+    k, n = snd.state()["k"], snd.state()["n"]
+    assert (k, n) == (window, 2 * window)
+    r = n - k
+    rng = np.random.default_rng(window)
+    src = rng.integers(0, 256, (k, L_), dtype=np.uint8)
+    reps = None
+    for i in range(k):
+        out = []
+        assert snd.on_send(qf.Packet(i, bytearray(src[i].tobytes()), L_, True), out) == L.QF_OK
+        assert out[0].is_systematic and out[0].payload() == src[i].tobytes()
+        if i < k - 1:
+            assert len(out) == 1
+        else:
+            reps = out[1:]
+    assert len(reps) == r
+    C = oracle.cauchy16(k, r)
+    check = sorted(set([0, 1, r - 1] + rng.integers(0, r, 5).tolist()))
+    want = oracle.encode16(src, r, C[check]) if window <= 64 else None
+    for q, j in enumerate(check):
+        p = reps[j]
+        assert not p.is_systematic and p.id == k + j and p.coeff_len == 2 * k
+        assert bytes(p.coefficients) == b"".join(int(c).to_bytes(2, "big") for c in C[j])
+        if want is not None:
+            assert p.payload() == want[q].tobytes(), j
+    got = []
+    for p in [qf.Packet(i, bytearray(src[i].tobytes()), L_, True) for i in range(k) if i not in set(lost)] + reps:
+        got += rcv.on_receive(p)
+    assert [p.id for p in got] == list(range(k))
+    for p in got:
+        assert p.payload() == src[p.id].tobytes(), p.id

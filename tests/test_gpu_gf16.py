@@ -203,8 +203,8 @@ def test_decode16_extreme_window_roundtrip(qf, oracle, gpu_ctx):
 
 
 def test_reference_contract_gf16_encode_decode(qf, gpu_ctx):
-    """tests/fec.rs:52-82 through the Encoder16 / Decoder16 mirror: k = 8,
-    n = 12, packet 0 dropped, every source's first byte comes back."""
+    """tests/fec.rs:52-82 through Encoder16 / Decoder16: k = 8, n = 12, packet
+    0 dropped, every source's first byte comes back (the whole generation)."""
     k, n, L = 8, 12, 8
     enc = qf.Encoder16(k, n)
     pk = [qf.Packet(i, bytearray([i % 255] * L), L, True) for i in range(k)]
@@ -213,9 +213,59 @@ def test_reference_contract_gf16_encode_decode(qf, gpu_ctx):
     repairs = [enc.generate_repair_packet(j) for j in range(n - k)]
     assert all(p is not None and p.coeff_len == 2 * k for p in repairs)
     dec = qf.Decoder16(k)
-    done = False
     for p in pk[1:] + repairs:
-        done = dec.add_packet(p)
-    assert done
-    got = dec.get_decoded_packets()
-    assert [(p.id, bytes(p.data[:L])) for p in got] == [(0, bytes(L))]
+        dec.add_packet(p)
+    assert dec.is_decoded
+    out = dec.get_decoded_packets()
+    assert len(out) == k
+    assert [p.data[0] for p in out] == [i % 255 for i in range(k)]
+    assert dec.get_decoded_packets() == []  # take()n
+
+
+def test_encoder16_window_and_odd_length(qf, oracle, gpu_ctx):
+    """Encoder16 (decoder.rs:25-75): None until the window is full, the window
+    slides, repair j = Cauchy row y = k + j over the window in order, id =
+    last.id + 1 + j, and an odd length leaves the last repair byte 0."""
+    k, L = 6, 11
+    rng = np.random.default_rng(2)
+    src = rng.integers(0, 256, (k + 4, L), dtype=np.uint8)
+    enc = qf.Encoder16(k, k + 3)
+    for i in range(k + 4):
+        if i < k:
+            assert enc.generate_repair_packet(0) is None
+        enc.add_source_packet(qf.Packet(100 + i, bytearray(src[i].tobytes()), L, True))
+    win = src[4:]
+    want = oracle.encode16(np.ascontiguousarray(win[:, : L - 1]), 3)
+    for j in range(3):
+        p = enc.generate_repair_packet(j)
+        assert p.id == 100 + k + 3 + 1 + j and p.len == L
+        assert p.payload()[: L - 1] == want[j].tobytes() and p.payload()[L - 1] == 0
+
+
+def test_decoder16_reference_shapes(qf, gpu_ctx):
+    """tests/fec.rs:128-228 (gf16_large_window / gf16_window_1024) drop a third
+    / half of the sources but send only 8 repairs, so fewer than k rows arrive
+    and the generation cannot decode; those tests' success assertions are
+    unsatisfiable (as tests/high_loss.rs).  The decoder reports not
+    decoded; with enough repairs the same shape decodes."""
+    for k, keep in ((512, lambda i: i % 3 != 0), (1024, lambda i: i % 2 == 0)):
+        L = 16
+        enc = qf.Encoder16(k, k + 8)
+        pk = [qf.Packet(i, bytearray([i % 255] * L), L, True) for i in range(k)]
+        for p in pk:
+            enc.add_source_packet(p)
+        dec = qf.Decoder16(k)
+        for p in [p for i, p in enumerate(pk) if keep(i)] + [enc.generate_repair_packet(j) for j in range(8)]:
+            dec.add_packet(p)
+        assert not dec.is_decoded and dec.get_decoded_packets() == []
+    k = 512
+    enc = qf.Encoder16(k, 2 * k)
+    pk = [qf.Packet(i, bytearray([i % 255] * 16), 16, True) for i in range(k)]
+    for p in pk:
+        enc.add_source_packet(p)
+    dec = qf.Decoder16(k)
+    kept = [p for i, p in enumerate(pk) if i % 3 != 0]
+    for p in kept + enc.generate_repairs(0, k - len(kept)):
+        dec.add_packet(p)
+    assert dec.is_decoded
+    assert [p.data[0] for p in dec.get_decoded_packets()] == [i % 255 for i in range(k)]
