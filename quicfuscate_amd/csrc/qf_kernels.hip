@@ -842,6 +842,7 @@ struct PrepWave {
     uint8_t rep_slot[16];    // accepted slot of repair j
     uint8_t Js[16], rank[16], Eidx[16];
     uint8_t LU[16][16];
+    int16_t PP[2][16][17];   // log prefix sums of the closed-form LU
 };
 
 __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCauchyArgs a) {
@@ -937,49 +938,48 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
         }
         wave_sync();
         // closed-form LU of A[b][c] = 1 / (x_b + y_c) (formulas at
-        // k_decode_prepare_cauchy); x, y held in registers, so every log
-        // lookup of an entry is independent of the others
+        // k_decode_prepare_cauchy) through prefix sums of logs:
+        //   P1[a][m] = sum_{q<m} log(x_a + x_q) - log(x_a + y_q)
+        //   P2[a][m] = sum_{q<m} log(y_a + x_q) - log(y_a + y_q)
+        //   L  (i > j): log(x_j + y_j) - log(x_i + y_j) + P1[i][j] - P1[j][j]
+        //   U  (i = j): log(x_i + y_i) + P2[i][i] - P1[i][i]
+        //   U' (i < j): log(x_i + y_i) - log(x_i + y_j) + P2[i][i] - P2[j][i]
+        // (the q = a term, log 0, only enters prefixes past a, never read)
         uint32_t X[16], Y[16];
 #pragma unroll
         for (uint32_t q = 0; q < 16; ++q) {
             X[q] = (k + P.Js[q]) & 0xFF;
             Y[q] = P.Eidx[q];
         }
+        const uint32_t Xl = (k + P.Js[lane & 15]) & 0xFF, Yl = P.Eidx[lane & 15];
+        {
+            // lanes 0-15: P1 rows, 16-31: P2 rows, one prefix step per q
+            const uint32_t which = (lane >> 4) & 1, ra = lane & 15;
+            const uint32_t v = which ? Yl : Xl;
+            int32_t acc = 0;
+            if (lane < 32) P.PP[which][ra][0] = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 16; ++q) {
+                if (q >= e) break;  // wave-uniform
+                acc += (int32_t)slog[v ^ X[q]] - (int32_t)slog[v ^ Y[q]];
+                if (lane < 32) P.PP[which][ra][q + 1] = (int16_t)acc;
+            }
+        }
+        wave_sync();
 #pragma unroll
         for (uint32_t pass = 0; pass < 4; ++pass) {
             const uint32_t t = lane + 64 * pass, i = t >> 4, j = t & 15;
+            // x_i, y_i, x_j, y_j by lane permutes (lane q & 15 holds X[q], Y[q]);
+            // taken with every lane active
+            const uint32_t xi = __shfl(Xl, (int)i), yi = __shfl(Yl, (int)i);
+            const uint32_t xj = __shfl(Xl, (int)j), yj = __shfl(Yl, (int)j);
             if (i >= e || j >= e) continue;
-            uint32_t xi = 0, xj = 0, yi = 0, yj = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 16; ++q) {
-                if (q == i) { xi = X[q]; yi = Y[q]; }
-                if (q == j) { xj = X[q]; yj = Y[q]; }
-            }
-            int32_t l;
-            if (i > j) {
-                l = (int32_t)slog[xj ^ yj] - (int32_t)slog[xi ^ yj];
-#pragma unroll
-                for (uint32_t q = 0; q < 15; ++q)
-                    if (q < j)
-                        l += (int32_t)slog[xi ^ X[q]] + (int32_t)slog[xj ^ Y[q]] - (int32_t)slog[xj ^ X[q]] -
-                             (int32_t)slog[xi ^ Y[q]];
-            } else if (i == j) {
-                l = (int32_t)slog[xi ^ yj];
-#pragma unroll
-                for (uint32_t q = 0; q < 15; ++q)
-                    if (q < i)
-                        l -= (int32_t)slog[xi ^ X[q]] + (int32_t)slog[yj ^ Y[q]] - (int32_t)slog[xi ^ Y[q]] -
-                             (int32_t)slog[X[q] ^ yj];
-            } else {
-                l = (int32_t)slog[xi ^ yi] - (int32_t)slog[xi ^ yj];
-#pragma unroll
-                for (uint32_t q = 0; q < 15; ++q)
-                    if (q < i)
-                        l += (int32_t)slog[yj ^ Y[q]] + (int32_t)slog[X[q] ^ yi] - (int32_t)slog[X[q] ^ yj] -
-                             (int32_t)slog[yi ^ Y[q]];
-            }
-            l %= 255;
-            if (l < 0) l += 255;
+            const bool lo_ = i > j, di = i == j;
+            const uint32_t u = lo_ ? (xj ^ yj) : (xi ^ yi);
+            const int32_t t1 = lo_ ? P.PP[0][i][j] : P.PP[1][i][i];
+            const int32_t t2 = lo_ ? P.PP[0][j][j] : (di ? P.PP[0][i][i] : P.PP[1][j][i]);
+            const int32_t l0 = (int32_t)slog[u] - (di ? 0 : (int32_t)slog[xi ^ yj]) + t1 - t2;
+            const uint32_t l = (uint32_t)(l0 + 64 * 255) % 255u;  // |t1 - t2| < 32 * 255
             P.LU[i][j] = sexp[l];
         }
         wave_sync();
