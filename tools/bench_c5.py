@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""BASELINE C5 throughput on the MI355X (diagnostic beside bench.py): the
+adaptive sliding-window shapes of SURVEY 8(d) -- k 32..196, r = ceil(k*ratio)-k,
+9000-byte jumbo payloads -- in block mode (independent generations) and
+sliding mode (one window per source packet: generation stride = row stride),
+encode and decode at 20 % source loss, device-resident, HIP-event kernel
+times.  Algorithmic bytes: encode (k + r) L per generation, decode (k + e) L.
+
+    python tools/bench_c5.py [--bytes 2e9] [--out gpurun_out/c5_bench.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+L_JUMBO, RS = 9000, 9008
+SHAPES = [(k, int(np.ceil(np.float32(k) * np.float32(ratio))) - k)
+          for k, ratio in ((32, 1.15), (48, 1.15), (64, 1.15), (96, 1.15), (128, 1.15), (160, 1.30), (196, 1.30))]
+
+
+def timed(ctx, fn, reps):
+    fn()
+    ctx.sync()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    ctx.sync()
+    wall = (time.perf_counter() - t0) / reps * 1e3
+    kt = {n: (c / reps, ms / reps) for n, (c, ms) in ctx.kernel_times().items()}
+    ctx.profile(False)
+    return wall, kt
+
+
+def main():
+    import torch
+
+    from quicfuscate_amd import fec as qf
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bytes", type=float, default=2e9, help="source bytes per shape and mode")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default="gpurun_out/c5_bench.json")
+    a = ap.parse_args()
+    ctx = qf.default_context()
+    res = {}
+    for k, r in SHAPES:
+        G = max(1, int(a.bytes // (k * L_JUMBO)))
+        for mode in ("block", "sliding"):
+            if mode == "block":
+                src = torch.randint(0, 256, (G * k * RS,), dtype=torch.uint8, device="cuda")
+                gs = k * RS
+            else:
+                src = torch.randint(0, 256, ((G + k - 1) * RS,), dtype=torch.uint8, device="cuda")
+                gs = RS
+            rep = torch.empty(G * r * RS, dtype=torch.uint8, device="cuda")
+
+            def enc():
+                qf.encode_batch(src, rep, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=RS,
+                                rep_gen_stride=r * RS, G=G)
+
+            wall, kt = timed(ctx, enc, a.reps)
+            kms = sum(ms for _, ms in kt.values())
+            res[f"k{k}_r{r}/{mode}/encode"] = {"G": G, "wall_ms": round(wall, 3), "kernels": kt,
+                                               "GiBps_alg": round(G * (k + r) * L_JUMBO / (kms / 1e3) / 2**30, 1),
+                                               "frac_of_8TBps": round(G * (k + r) * L_JUMBO / (kms / 1e3) / 8e12, 3)}
+            if mode == "block":
+                # decode at 20 % source loss (first k rows: survivors then repairs)
+                e = min(r, max(1, round(0.2 * k)))
+                max_rows = k - e + r
+                rng = np.random.default_rng(k)
+                ridx = np.zeros((G, max_rows), np.uint16)
+                for g in range(G):
+                    E = set(rng.choice(k, e, replace=False).tolist())
+                    ridx[g] = [i for i in range(k) if i not in E] + [k + j for j in range(r)]
+                ai = torch.from_numpy(ridx.astype(np.int64)).cuda()
+                src3 = src.view(G, k, RS)
+                rep3 = rep.view(G, r, RS)
+                rows = torch.empty((G, max_rows, RS), dtype=torch.uint8, device="cuda")
+                for g0 in range(0, G, 256):
+                    g1 = min(G, g0 + 256)
+                    sel = ai[g0:g1]
+                    gi = torch.arange(g0, g1, device="cuda")[:, None]
+                    rows[g0:g1] = torch.where((sel < k)[..., None], src3[gi, sel.clamp(max=k - 1)],
+                                              rep3[gi, (sel - k).clamp(min=0)])
+                t_idx = torch.from_numpy(ridx.view(np.int16).reshape(-1)).cuda()
+                rec = torch.empty(G * e * RS, dtype=torch.uint8, device="cuda")
+                rec_index = torch.empty(G * e, dtype=torch.int16, device="cuda")
+                n_rec = torch.empty(G, dtype=torch.int32, device="cuda")
+                status = torch.empty(G, dtype=torch.int32, device="cuda")
+
+                def dec():
+                    qf.decode_batch(rows.view(-1), t_idx, rec, rec_index, n_rec, status, k, r, L_JUMBO,
+                                    max_rows=max_rows, row_stride=RS, rows_gen_stride=max_rows * RS,
+                                    rec_row_stride=RS, rec_gen_stride=e * RS, G=G)
+
+                wall, kt = timed(ctx, dec, a.reps)
+                assert (status == 0).all().item() and (n_rec == e).all().item()
+                g = G - 1
+                E = sorted(set(range(k)) - set(int(x) for x in ridx[g] if x < k))
+                assert torch.equal(rec.view(G, e, RS)[g, :, :L_JUMBO], src3[g, E, :L_JUMBO])
+                kms = sum(ms for _, ms in kt.values())
+                res[f"k{k}_r{r}/block/decode"] = {"G": G, "erased": e, "wall_ms": round(wall, 3), "kernels": kt,
+                                                   "GiBps_alg": round(G * (k + e) * L_JUMBO / (kms / 1e3) / 2**30, 1)}
+                del rows, rec
+            del src, rep
+            torch.cuda.empty_cache()
+        print(k, r, {kk: v["GiBps_alg"] for kk, v in res.items() if kk.startswith(f"k{k}_")}, flush=True)
+    Path(a.out).parent.mkdir(exist_ok=True)
+    Path(a.out).write_text(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
