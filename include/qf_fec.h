@@ -108,7 +108,11 @@ int qf_gf256_mul_slice_dev(qf_ctx *ctx, const uint8_t *a_dev, const uint8_t *b_d
  * [L, round_up(L, 128)) of every repair row when rep_row_stride covers them
  * (the reference's repair is a pool block that is zero beyond L,
  * decoder.rs:182/264 + optimize.rs:524).  With 128-B aligned repair rows this
- * lets the encode kernel store whole 128-B lines only. */
+ * lets the encode kernel store whole 128-B lines only.  When
+ * L % 16 != 0 the kernel then also reads each source row's last 16-byte unit
+ * whole (up to round_up(L, 16): inside the 16-byte row stride, and for the
+ * buffer's last row within the same page); those extra bytes never reach the
+ * output. */
 #define QF_ENCODE_ZERO_TAIL 1u
 
 typedef struct qf_encode_shape {

@@ -129,6 +129,9 @@ _ASM = {
     "v_readfirstlane": lambda s, a: f"v_readfirstlane_b32 s{s}, {V(a)}",
     "v_bfe": lambda d, a, off, w: f"v_bfe_u32 {V(d)}, {V(a)}, {off}, {w}",
     "v_cmp_ne_s": lambda sd, s, a: f"v_cmp_ne_u32_e64 {SP(sd)}, s{s}, {V(a)}",
+    "v_cmp_eq_s": lambda sd, s, a: f"v_cmp_eq_u32_e64 {SP(sd)}, s{s}, {V(a)}",
+    "v_and_s": lambda d, s, a: f"v_and_b32_e32 {V(d)}, s{s}, {V(a)}",
+    "s_cbranch_execz": lambda lbl: f"s_cbranch_execz {lbl}",
     "v_cndmask": lambda d, a, b, sm: f"v_cndmask_b32_e64 {V(d)}, {V(a)}, {V(b)}, {SP(sm)}",
     "load16": lambda d, a, off, pol="": f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off"
               + (f" offset:{off}" if off else "") + (f" {pol}" if pol else ""),
@@ -185,7 +188,9 @@ _ASM = {
 #   s[4:5] src (syn: received rows)   s[6:7] dst (syn: syndrome rows)
 #   s8  src generation stride (u32)   s9  dst generation stride (u32)
 #   s10 src row stride                s11 dst row stride
-#   s12 Lu = L/16 (payload units per row: lanes with u >= Lu load nothing)
+#   s12 Lu = ceil(L/16) (payload units per row: lanes with u >= Lu load
+#       nothing; a partial last unit is loaded whole -- the 16-B unit holding
+#       byte L-1 never crosses a page -- and masked before the store)
 #   s13 Lv >= Lu (lane units per row: the (generation, unit) lane space is
 #       G x Lv; Lv = Lu rounded up to 8 puts every item boundary and row
 #       start of a 128-B aligned layout on a 128-B line boundary)
@@ -196,6 +201,7 @@ _ASM = {
 #       syn: slot-map generation stride (syndromes of all Lv units are
 #       stored: the syndrome rows live in the library's workspace)
 #   s[20:21] slot map   s[22:23] zero row (syn)
+#   s20..s23 enc: byte masks of the last unit's dwords (tail_masks(L))
 # SGPRs: s[24:25] load mask B, s[26:27] load mask A, s28 item, s29 wave in
 # group, s30 temp, s31 ABSENT constant, s[32:33] {src row stride, 0},
 # s[34:35] {dst row stride, 0}, s[36:37] mad carry sink, s[38:39] and
@@ -275,10 +281,20 @@ class KernelSpec:
     prio: tuple = (0, 0)
     # lab only: drop the payload row loads (keeps maps, records, compute)
     lab_norows: bool = False
+    # enc mode, one pass of a code with more repairs than a kernel holds:
+    # repairs j0 .. j0 + r - 1 of the Cauchy matrix of (k, r_total)
+    r_total: int = 0
+    j0: int = 0
+
+    @property
+    def rt(self) -> int:
+        return self.r_total or self.r
 
     @property
     def name(self) -> str:
         tag = {"enc": "bs", "syn": "syn", "dec": "dec"}[self.mode]
+        if self.rt != self.r or self.j0:
+            return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}"
         return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
 
     @property
@@ -322,7 +338,15 @@ class KernelSpec:
 
     @property
     def next_free_sgpr(self) -> int:
-        return SGPR_NEXT_FREE_DEC if self.mode == "dec" else SGPR_NEXT_FREE
+        if self.mode == "dec":
+            return SGPR_NEXT_FREE_DEC
+        return 68 if self.far else SGPR_NEXT_FREE   # s[66:67]: far-jump target
+
+    @property
+    def far(self) -> bool:
+        """Item loop branches as 64-bit pc-relative jumps: the straight-line
+        body exceeds the +-128 KiB of s_branch (dec always; enc for large k*r)."""
+        return self.mode == "dec" or (self.mode == "enc" and self.k * (70 + 8 * self.r) > 14000)
 
     @property
     def kernarg_bytes(self) -> int:
@@ -512,7 +536,7 @@ def _prologue(E, spec: KernelSpec):
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (S_TMASK + q, mask)))
     E(Op("label", (".Litem",)))
-    if spec.mode == "dec":
+    if spec.far:
         E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
         E(Op("s_far_jump", (".Lend", 0)))
         E(Op("label", (".Lgo",)))
@@ -581,7 +605,8 @@ def _store_pair(E, acc: int, ma: int, mb: int, pol: str = ""):
 
 def _generate_enc(spec: KernelSpec) -> list[Op]:
     k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
-    C = cauchy(k, r)
+    assert spec.j0 + r <= spec.rt
+    C = cauchy(k, spec.rt)[spec.j0: spec.j0 + r]
     acc0, ring0 = spec.acc0, spec.ring0
     ops: list[Op] = []
     E = ops.append
@@ -619,11 +644,27 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         for j in range(r):
             for q in range(4):
                 E(Op("v_movk", (acc0 + 8 * j + 4 * h + q, 0)))
+    # the row's last unit when L % 16 != 0 (zero tail only): its bytes >= L
+    # come from the source rows' padding; AND them away with the per-dword
+    # byte masks s20..s23 (all ones when L % 16 == 0)
+    for h, (uv, sm) in enumerate(((V_UA, S_STA), (V_UB, S_STB))):
+        E(Op("s_exec", (None,)))
+        E(Op("v_addk", (V_T, 1, uv)))
+        E(Op("v_cmp_eq_s", (S_PAD, 12, V_T)))     # u + 1 == Lu
+        E(Op("s_nop", (4,)))
+        E(Op("s_and64", (S_PAD, S_PAD, sm)))
+        E(Op("s_exec", (S_PAD,)))
+        E(Op("s_cbranch_execz", (f".Ltail{h}",)))
+        for j in range(r):
+            for q in range(4):
+                x = acc0 + 8 * j + 4 * h + q
+                E(Op("v_and_s", (x, 20 + q, x)))
+        E(Op("label", (f".Ltail{h}",)))
     E(Op("s_exec", (None,)))
     E(Op("s_nop", (4,)))
     for j in range(r):
         _store_pair(E, acc0 + 8 * j, S_STA, S_STB, spec.st_policy)
-    _epilogue_next_item(E)
+    _epilogue_next_item(E, far=spec.far)
     return ops
 
 
@@ -977,15 +1018,23 @@ def magic_for(U: int) -> tuple[int, int]:
 
 def padded_units(L: int) -> int:
     """Lane units per row that align items to 128-B lines: ceil(L/16) rounded up to 8."""
-    return (L // 16 + 7) // 8 * 8
+    return ((L + 15) // 16 + 7) // 8 * 8
+
+
+def tail_masks(L: int) -> list[int]:
+    """Per-dword byte masks of a row's last 16-B unit (enc kernarg words 16..19):
+    bytes < L % 16 kept, all ones when L % 16 == 0."""
+    tb = L % 16 or 16
+    return [MASK32 if tb - 4 * d >= 4 else (1 << (8 * max(0, tb - 4 * d))) - 1 for d in range(4)]
 
 
 def launch_geometry(L: int, G: int, Lv: Optional[int] = None) -> tuple[int, int, int]:
     """(Lv, total units, items) of a batch: 16-byte units, 128 per item, Lv
-    lane units per row (default L/16)."""
-    if L % 16 or L < 32:
-        raise ValueError("bit-sliced kernels need L % 16 == 0 and L >= 32")
-    Lu = L // 16
+    lane units per row (default ceil(L/16); L % 16 != 0 needs the zero-tail
+    lane space)."""
+    if L < 32 or (L % 16 and Lv is None):
+        raise ValueError("bit-sliced kernels need L >= 32, and the zero tail when L % 16 != 0")
+    Lu = (L + 15) // 16
     Lv = Lu if Lv is None else Lv
     if Lv < Lu:
         raise ValueError("Lv < L/16")
@@ -1007,9 +1056,11 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
     Lv, total, n_items = launch_geometry(L, G, Lv)
     magic, shift = magic_for(Lv)
     s19 = map_stride if smap else (Lv if zero_tail else L // 16)
-    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, L // 16, Lv, total,
-             magic, shift, n_items, total_waves, s19, smap & MASK32, smap >> 32,
-             zero & MASK32, zero >> 32]
+    if L % 16 and not (zero_tail or smap):
+        raise ValueError("enc with L % 16 != 0 needs the zero tail")
+    tail = [smap & MASK32, smap >> 32, zero & MASK32, zero >> 32] if smap else tail_masks(L)
+    words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, (L + 15) // 16, Lv, total,
+             magic, shift, n_items, total_waves, s19] + tail
     if lu is not None:
         words += [lu[0] & MASK32, lu[0] >> 32, lu[1], 0, tables & MASK32, tables >> 32, 0, 0]
     for w in words:
@@ -1287,6 +1338,13 @@ class Emulator:
                 wv(a[0], (rv(a[1]) >> np.uint64(a[2])) & np.uint64((1 << a[3]) - 1))
             elif n == "v_cmp_ne_s":
                 set_smask(a[0], (rv(a[2]) != np.uint64(s[a[1]])) & exec_)
+            elif n == "v_cmp_eq_s":
+                set_smask(a[0], (rv(a[2]) == np.uint64(s[a[1]])) & exec_)
+            elif n == "v_and_s":
+                wv(a[0], rv(a[2]) & np.uint64(s[a[1]]))
+            elif n == "s_cbranch_execz":
+                if not exec_.any():
+                    pc = self.labels[a[0]]
             elif n == "v_cndmask":
                 wv(a[0], np.where(smask(a[3]), rv(a[2]), rv(a[1])))
             elif n == "load16":

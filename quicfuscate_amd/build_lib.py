@@ -29,6 +29,10 @@ SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip", "qf_bs.hip", "qf_ad
 # (k, r) Cauchy configurations that get a bit-sliced assembly kernel
 # (bs_codegen.py); every other shape runs the general v_perm kernel.
 BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1)]
+# encode-only kernels for the C5 adaptive shapes (Normal/Medium
+# windows, r = ceil(k * ratio) - k); codes with r > 16 in passes of <= 16 repairs
+BS_ENC_ONLY = [(32, 5), (48, 8), (96, 15), (128, 20), (160, 48), (196, 59)]
+BS_PASS = 16
 BS_PD = 3
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
 
@@ -116,6 +120,9 @@ def _bs_kernels(build_dir: Path) -> Path:
 
     entries, blobs = [], []
     specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn", "dec") for (k, r) in BS_CONFIGS]
+    for k, rt in BS_ENC_ONLY:
+        for j0 in range(0, rt, BS_PASS):
+            specs.append(bs.KernelSpec(k, min(BS_PASS, rt - j0), BS_PD, "enc", r_total=rt, j0=j0))
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
@@ -123,7 +130,7 @@ def _bs_kernels(build_dir: Path) -> Path:
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         mode = {"enc": "e", "syn": "s", "dec": "d"}[spec.mode]
-        entries.append(f"    {{{k}u, {r}u, {BS_PD}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
+        entries.append(f"    {{{k}u, {r}u, {BS_PD}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
     inc = build_dir / "qf_bs_blobs.inc"
     inc.write_text("// generated by quicfuscate_amd/build_lib.py from bs_codegen.py -- do not edit\n"

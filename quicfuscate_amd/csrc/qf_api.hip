@@ -244,13 +244,14 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     // Fast path: bit-sliced kernel specialised to the reference's Cauchy
     // matrix of (k, r) (bs_codegen.py), for whole 16-byte rows.
     const char* nobs = getenv("QF_DISABLE_BS");
-    if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && L % 16 == 0 && L >= 32 &&
+    // (L % 16 != 0: only with the zero tail, whose lane space masks the last unit)
+    const bool zero_tail = (sh->flags & QF_ENCODE_ZERO_TAIL) &&
+                           qf::bs_zero_tail_fits(r, L, sh->rep_row_stride, sh->rep_gen_stride) &&
+                           (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31);
+    if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && (L % 16 == 0 || zero_tail) && L >= 32 &&
         sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
         sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
-        (uint64_t)G * (L / 16) < (1ull << 31)) {
-        const bool zero_tail = (sh->flags & QF_ENCODE_ZERO_TAIL) &&
-                               qf::bs_zero_tail_fits(r, L, sh->rep_row_stride, sh->rep_gen_stride) &&
-                               (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31);
+        (uint64_t)G * ((L + 15) / 16) < (1ull << 31)) {
         hipEvent_t ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
                                    sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G,

@@ -6,7 +6,7 @@
 namespace qf {
 
 struct BsCache {
-    static const int kMax = 32;
+    static const int kMax = 64;
     hipModule_t mod[kMax] = {};
     hipFunction_t fn[kMax] = {};
 };
@@ -15,14 +15,15 @@ struct BsCache {
 bool bs_available(uint32_t k, uint32_t r);
 // Kernel symbol of that configuration (nullptr if none).
 const char* bs_name(uint32_t k, uint32_t r);
-// Lane units per row of the padded lane space: L/16 rounded up to 8 (128 B).
+// Lane units per row of the padded lane space: ceil(L/16) rounded up to 8 (128 B).
 uint32_t bs_padded_units(uint32_t L);
 // Does every repair row's zero tail stay inside its own row / generation?
 bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs);
-// Encode G generations (rows of L bytes, L % 16 == 0, L >= 32; strides and
-// generation strides < 2^32, 16-byte aligned; G * L / 16 < 2^31).  zero_tail:
-// also write zeros to bytes [L, 16 * bs_padded_units(L)) of every repair row
-// (needs drs >= that).
+// Encode G generations (rows of L >= 32 bytes; strides and generation strides
+// < 2^32, 16-byte aligned; G * L / 16 < 2^31), one launch per pass of at most
+// 16 repairs.  zero_tail: also write zeros to bytes [L, 16 * bs_padded_units(L))
+// of every repair row (needs drs >= that); required when L % 16 != 0 (the
+// last unit of each source row is then read whole, up to round_up(L, 16)).
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                      uint64_t drs, uint32_t L, uint32_t G, bool zero_tail);

@@ -14,7 +14,8 @@
 
 struct QfBsEntry {
     uint32_t k, r, pd;
-    char mode;  // 'e' encode, 's' decode syndromes
+    uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
+    char mode;  // 'e' encode, 's' decode syndromes, 'd' fused decode
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -24,9 +25,10 @@ struct QfBsEntry {
 
 namespace qf {
 
+// the kernel (first pass, j0 = 0) of the (k, r) code
 static const QfBsEntry* find(char mode, uint32_t k, uint32_t r) {
     for (const auto& e : qf_bs_table)
-        if (e.mode == mode && e.k == k && e.r == r) return &e;
+        if (e.mode == mode && e.k == k && e.rt == r && e.j0 == 0) return &e;
     return nullptr;
 }
 
@@ -70,8 +72,10 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return hipErrorInvalidValue;
-    if (L % 16 || L < 32 || sgs >= (1ull << 32) || dgs >= (1ull << 32) || srs >= (1ull << 32) ||
-        drs >= (1ull << 32))
+    // a partial last unit only in the enc zero-tail lane space (its bytes >= L
+    // are masked to zero before the store)
+    if ((L % 16 && (e->mode != 'e' || Lv != s19)) || L < 32 || sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
+        srs >= (1ull << 32) || drs >= (1ull << 32))
         return hipErrorInvalidValue;
     if (!cache.fn[idx]) {
         hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
@@ -79,7 +83,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
         err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
         if (err != hipSuccess) return err;
     }
-    const uint32_t Lu = L / 16;
+    const uint32_t Lu = (L + 15) / 16;
     if (Lv < Lu) return hipErrorInvalidValue;
     const uint64_t total = (uint64_t)G * Lv;
     if (total >= (1ull << 31)) return hipErrorInvalidValue;
@@ -105,10 +109,19 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[13] = n_items;
     a[14] = blocks * 4;
     a[15] = s19;
-    a[16] = (uint32_t)(uintptr_t)smap;
-    a[17] = (uint32_t)((uintptr_t)smap >> 32);
-    a[18] = (uint32_t)(uintptr_t)zero;
-    a[19] = (uint32_t)((uintptr_t)zero >> 32);
+    if (e->mode == 'e') {
+        // byte masks of the last unit's dwords (bs_codegen.tail_masks)
+        const uint32_t tb = L % 16 ? L % 16 : 16;
+        for (uint32_t d = 0; d < 4; ++d) {
+            const int32_t valid = (int32_t)tb - 4 * (int32_t)d;
+            a[16 + d] = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1);
+        }
+    } else {
+        a[16] = (uint32_t)(uintptr_t)smap;
+        a[17] = (uint32_t)((uintptr_t)smap >> 32);
+        a[18] = (uint32_t)(uintptr_t)zero;
+        a[19] = (uint32_t)((uintptr_t)zero >> 32);
+    }
     a[20] = (uint32_t)(uintptr_t)lu;
     a[21] = (uint32_t)((uintptr_t)lu >> 32);
     a[22] = lu_stride;
@@ -120,7 +133,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
-uint32_t bs_padded_units(uint32_t L) { return (L / 16 + 7) / 8 * 8; }
+uint32_t bs_padded_units(uint32_t L) { return ((L + 15) / 16 + 7) / 8 * 8; }
 
 bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs) {
     const uint64_t row = 16ull * bs_padded_units(L);
@@ -137,8 +150,17 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     const uint32_t Lu = L / 16;
     const uint32_t Lv = zero_tail ? bs_padded_units(L) : Lu;
     if (zero_tail && !bs_zero_tail_fits(r, L, drs, dgs)) return hipErrorInvalidValue;
-    return launch(cache, find('e', k, r), num_cus, st, src, dst, sgs, dgs, srs, drs, L, G, Lv, Lv, nullptr,
-                  nullptr);
+    if (!zero_tail && L % 16) return hipErrorInvalidValue;
+    if (!find('e', k, r)) return hipErrorInvalidValue;
+    // one launch per pass of repairs (codes with more repairs than a kernel
+    // holds): pass j0 writes repair rows j0 .. j0 + r_pass - 1
+    for (const auto& e : qf_bs_table) {
+        if (e.mode != 'e' || e.k != k || e.rt != r) continue;
+        hipError_t err = launch(cache, &e, num_cus, st, src, dst + (uint64_t)e.j0 * drs, sgs, dgs, srs, drs, L, G,
+                                Lv, Lv, nullptr, nullptr);
+        if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
 }
 
 hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,

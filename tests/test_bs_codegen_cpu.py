@@ -372,3 +372,68 @@ def test_emulated_fused_decode_unpadded_lanes(oracle):
     (L/16 units per row): halves of a lane straddle generations."""
     assert _dec_case(oracle, 8, 4, 2, 80, 9, 6, None, padded=False) == 0
     assert _dec_case(oracle, 16, 16, 3, 1200, 2, 7, 13, padded=False) == 0
+
+
+@pytest.mark.parametrize("k,rt,L,G,split", [
+    (8, 4, 72, 5, 4),      # L % 16 = 8: partial last unit, one pass
+    (6, 5, 100, 4, 3),     # L % 16 = 4, passes of 3 + 2 repairs
+    (5, 7, 33, 6, 4),      # one byte in the last unit, passes of 4 + 3
+    (4, 20, 64, 3, 16),    # whole units, passes of 16 + 4
+])
+def test_emulated_kernel_tail_and_passes(oracle, k, rt, L, G, split):
+    """Zero-tail lane space with a partial last unit (its bytes >= L, read from
+    the source rows' padding, are masked to zero) and codes split into
+    passes of repairs j0.. (each pass writes its own repair rows)."""
+    Lv = bs.padded_units(L)
+    rng = np.random.default_rng(k * 31 + L + rt)
+    srs = (L + 15) // 16 * 16 + 16 * (k % 2)
+    sgs = k * srs
+    drs = 16 * Lv + 64
+    dgs = rt * drs
+    src = rng.integers(0, 256, G * sgs, dtype=np.uint8)   # padding bytes are garbage too
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    SRC, DST = 0x10000000, 0x40000000
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    waves = (items + 3) // 4
+    for j0 in range(0, rt, split):
+        spec = bs.KernelSpec(k, min(split, rt - j0), 3, r_total=rt, j0=j0)
+        emu = bs.Emulator(bs.generate(spec))
+        emu.add_buffer(SRC, src)
+        emu.add_buffer(DST, dst)
+        ka = bs.kernargs(SRC, DST + j0 * drs, sgs, dgs, srs, drs, L, G, waves * 4, Lv=Lv, zero_tail=True)
+        for wg in range(waves):
+            for w in range(4):
+                emu.run_wave(ka, wg, w)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, rt)
+        for j in range(rt):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            assert (dst[off + L: off + 16 * Lv] == 0).all(), (g, j)
+            assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
+
+
+def test_tail_masks():
+    assert bs.tail_masks(64) == [0xFFFFFFFF] * 4
+    assert bs.tail_masks(72) == [0xFFFFFFFF, 0xFFFFFFFF, 0, 0]
+    assert bs.tail_masks(33) == [0xFF, 0, 0, 0]
+    assert bs.tail_masks(9000) == [0xFFFFFFFF, 0xFFFFFFFF, 0, 0]
+    assert bs.tail_masks(46) == [0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFF]
+
+
+def test_register_budget_large_pass_kernel():
+    """A C5 pass kernel (k = 196, repairs 16..31 of r = 59) is past the
+    s_branch range: far jumps through s[66:67], within its declared SGPRs."""
+    import re
+
+    spec = bs.KernelSpec(196, 16, 3, "enc", r_total=59, j0=16)
+    assert spec.far and spec.name == "qf_cauchy_bs_k196_r59_j16"
+    text = bs.emit_asm(spec, bs.generate(spec))
+    body, desc = text.split(".amdhsa_kernel", 1)
+    ns = int(re.search(r"\.amdhsa_next_free_sgpr (\d+)", desc).group(1))
+    nv = int(re.search(r"\.amdhsa_next_free_vgpr (\d+)", desc).group(1))
+    smax = max(int(m.group(2) or m.group(3)) for m in re.finditer(r"\bs\[(\d+):(\d+)\]|\bs(\d+)\b", body))
+    vmax = max(int(m.group(2) or m.group(3)) for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", body))
+    assert smax < ns and vmax < nv, (smax, ns, vmax, nv)
+    assert "s_setpc_b64 s[66:67]" in body

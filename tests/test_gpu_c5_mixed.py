@@ -11,6 +11,7 @@ from quicfuscate_amd import _lib as L
 pytestmark = pytest.mark.gpu
 L_JUMBO = 9000
 RS = 9008          # row stride: 16-byte multiple (C ABI), rows zero padded
+REP_RS = 9088      # pool-block repair rows: round_up(9000, 128), the zero tail fits
 SHAPES = [(k, int(np.ceil(np.float32(k) * np.float32(ratio))) - k)
           for k, ratio in ((32, 1.15), (48, 1.15), (64, 1.15), (96, 1.15), (128, 1.15), (160, 1.30), (196, 1.30))]
 
@@ -22,12 +23,17 @@ def test_c5_shapes():
 
 @pytest.mark.parametrize("k,r", SHAPES)
 @pytest.mark.parametrize("sliding", [False, True])
-def test_c5_encode_matches_oracle(qf, oracle, gpu_ctx, k, r, sliding):
+@pytest.mark.parametrize("zero_tail", [False, True])
+def test_c5_encode_matches_oracle(qf, oracle, gpu_ctx, k, r, sliding, zero_tail):
+    """zero_tail: pool-block repair rows (QF_ENCODE_ZERO_TAIL) run the
+    bit-sliced pass kernels with the masked partial last unit; without it,
+    the general kernel writes exactly L bytes."""
     import torch
 
     rng = np.random.default_rng(k * 7 + sliding)
     G = 3
     rs = RS
+    drs = REP_RS if zero_tail else RS
     if sliding:   # one window per source packet: generation stride = row stride
         P = k + G - 1
         src = rng.integers(0, 256, P * rs, dtype=np.uint8)
@@ -36,14 +42,16 @@ def test_c5_encode_matches_oracle(qf, oracle, gpu_ctx, k, r, sliding):
         src = rng.integers(0, 256, G * k * rs, dtype=np.uint8)
         gs = k * rs
     t_src = torch.from_numpy(src).cuda()
-    rep = torch.empty(G * r * rs, dtype=torch.uint8, device="cuda")
-    qf.encode_batch(t_src, rep, k, r, L_JUMBO, src_row_stride=rs, src_gen_stride=gs, rep_row_stride=rs,
-                    rep_gen_stride=r * rs, G=G)
+    rep = torch.full((G * r * drs,), 0xEE, dtype=torch.uint8, device="cuda")
+    qf.encode_batch(t_src, rep, k, r, L_JUMBO, src_row_stride=rs, src_gen_stride=gs, rep_row_stride=drs,
+                    rep_gen_stride=r * drs, G=G, zero_tail=zero_tail)
     qf.default_context().sync()
-    got = rep.cpu().numpy().reshape(G, r, rs)
+    got = rep.cpu().numpy().reshape(G, r, drs)
     for g in range(G):
         rows = src[g * gs: g * gs + k * rs].reshape(k, rs)[:, :L_JUMBO]
         assert (got[g][:, :L_JUMBO] == oracle.encode(rows, r)).all(), g
+        # the library writes [L, 16 * padded units) as zeros with the flag, else nothing past L
+        assert (got[g][:, L_JUMBO:] == (0 if zero_tail else 0xEE)).all(), g
 
 
 @pytest.mark.parametrize("k,r", SHAPES)

@@ -23,6 +23,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 L_JUMBO, RS = 9000, 9008
+REP_RS = 9088   # pool-block repair rows (QF_ENCODE_ZERO_TAIL): bit-sliced pass kernels
 SHAPES = [(k, int(np.ceil(np.float32(k) * np.float32(ratio))) - k)
           for k, ratio in ((32, 1.15), (48, 1.15), (64, 1.15), (96, 1.15), (128, 1.15), (160, 1.30), (196, 1.30))]
 
@@ -50,6 +51,8 @@ def main():
     ap.add_argument("--bytes", type=float, default=2e9, help="source bytes per shape and mode")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="gpurun_out/c5_bench.json")
+    ap.add_argument("--exact-rows", action="store_true",
+                    help="dense repair rows without the zero tail (general v_perm encode kernel)")
     a = ap.parse_args()
     ctx = qf.default_context()
     res = {}
@@ -62,11 +65,12 @@ def main():
             else:
                 src = torch.randint(0, 256, ((G + k - 1) * RS,), dtype=torch.uint8, device="cuda")
                 gs = RS
-            rep = torch.empty(G * r * RS, dtype=torch.uint8, device="cuda")
+            drs = RS if a.exact_rows else REP_RS
+            rep = torch.empty(G * r * drs, dtype=torch.uint8, device="cuda")
 
             def enc():
-                qf.encode_batch(src, rep, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=RS,
-                                rep_gen_stride=r * RS, G=G)
+                qf.encode_batch(src, rep, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=drs,
+                                rep_gen_stride=r * drs, G=G, zero_tail=not a.exact_rows)
 
             wall, kt = timed(ctx, enc, a.reps)
             kms = sum(ms for _, ms in kt.values())
@@ -84,7 +88,7 @@ def main():
                     ridx[g] = [i for i in range(k) if i not in E] + [k + j for j in range(r)]
                 ai = torch.from_numpy(ridx.astype(np.int64)).cuda()
                 src3 = src.view(G, k, RS)
-                rep3 = rep.view(G, r, RS)
+                rep3 = rep.view(G, r, drs)[:, :, :RS]
                 rows = torch.empty((G, max_rows, RS), dtype=torch.uint8, device="cuda")
                 for g0 in range(0, G, 256):
                     g1 = min(G, g0 + 256)
