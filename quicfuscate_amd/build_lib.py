@@ -32,7 +32,7 @@ BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1)]
 # encode-only kernels for the C5 adaptive shapes (Normal/Medium
 # windows, r = ceil(k * ratio) - k); codes with r > 16 in passes of <= 16 repairs
 BS_ENC_ONLY = [(32, 5), (48, 8), (96, 15), (128, 20), (160, 48), (196, 59)]
-BS_PASS = 16
+BS_PASS = 22   # repairs per pass: 8 r accumulator VGPRs, r <= 22 fits 256 at pd 3
 BS_PD = 3
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
 
@@ -121,8 +121,12 @@ def _bs_kernels(build_dir: Path) -> Path:
     entries, blobs = [], []
     specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn", "dec") for (k, r) in BS_CONFIGS]
     for k, rt in BS_ENC_ONLY:
-        for j0 in range(0, rt, BS_PASS):
-            specs.append(bs.KernelSpec(k, min(BS_PASS, rt - j0), BS_PD, "enc", r_total=rt, j0=j0))
+        npass = -(-rt // BS_PASS)   # balanced passes (each pass re-reads the sources)
+        j0 = 0
+        for p in range(npass):
+            rp = (rt - j0) // (npass - p)
+            specs.append(bs.KernelSpec(k, rp, BS_PD, "enc", r_total=rt, j0=j0))
+            j0 += rp
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
