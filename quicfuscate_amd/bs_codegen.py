@@ -132,6 +132,7 @@ _ASM = {
     "v_cmp_eq_s": lambda sd, s, a: f"v_cmp_eq_u32_e64 {SP(sd)}, s{s}, {V(a)}",
     "v_and_s": lambda d, s, a: f"v_and_b32_e32 {V(d)}, s{s}, {V(a)}",
     "s_cbranch_execz": lambda lbl: f"s_cbranch_execz {lbl}",
+    "s_cmp_eq_k_br": lambda s, kk, lbl: f"s_cmp_eq_u32 s{s}, 0x{kk:x}\n\ts_cbranch_scc1 {lbl}",
     "v_cndmask": lambda d, a, b, sm: f"v_cndmask_b32_e64 {V(d)}, {V(a)}, {V(b)}, {SP(sm)}",
     "load16": lambda d, a, off, pol="": f"global_load_dwordx4 {VQ(d)}, {VP(a)}, off"
               + (f" offset:{off}" if off else "") + (f" {pol}" if pol else ""),
@@ -647,6 +648,8 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     # the row's last unit when L % 16 != 0 (zero tail only): its bytes >= L
     # come from the source rows' padding; AND them away with the per-dword
     # byte masks s20..s23 (all ones when L % 16 == 0)
+    E(Op("s_exec", (None,)))
+    E(Op("s_cmp_eq_k_br", (23, MASK32, ".Ltail1")))   # L % 16 == 0: no partial unit
     for h, (uv, sm) in enumerate(((V_UA, S_STA), (V_UB, S_STB))):
         E(Op("s_exec", (None,)))
         E(Op("v_addk", (V_T, 1, uv)))
@@ -1342,6 +1345,9 @@ class Emulator:
                 set_smask(a[0], (rv(a[2]) == np.uint64(s[a[1]])) & exec_)
             elif n == "v_and_s":
                 wv(a[0], rv(a[2]) & np.uint64(s[a[1]]))
+            elif n == "s_cmp_eq_k_br":
+                if s[a[0]] == a[1]:
+                    pc = self.labels[a[2]]
             elif n == "s_cbranch_execz":
                 if not exec_.any():
                     pc = self.labels[a[0]]
