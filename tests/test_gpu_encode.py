@@ -188,3 +188,35 @@ def test_gf_mul_slice_exhaustive_matches_table(qf, oracle, gpu_ctx):
     b = (255 - np.arange(1029)).astype(np.uint8)
     got = np.frombuffer(qf.gf_mul_slice(a.tobytes(), b.tobytes()), np.uint8)
     assert all(int(got[i]) == oracle.mul(int(a[i]), int(b[i])) for i in range(1029))
+
+
+BS_SHAPES = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1), (32, 5), (48, 8), (96, 15), (128, 20), (160, 48),
+             (196, 59)]
+
+
+@pytest.mark.parametrize("k,r", BS_SHAPES)
+def test_bit_sliced_partial_last_unit_random_lengths(qf, oracle, gpu_ctx, k, r):
+    """Every generated encode kernel with the zero tail at random L (mostly
+    L % 16 != 0): bytes < L bit-exact, [L, round_up(L, 128)) zero, nothing
+    beyond; the source rows' padding is random and must not leak."""
+    rng = np.random.default_rng(1000 * k + r)
+    for trial in range(3):
+        L = int(rng.integers(32, 1500))
+        if trial == 0:
+            L |= 1                               # odd length
+        G = int(rng.integers(1, 6))
+        rs = _r16(L) + 16 * int(rng.integers(0, 2))
+        gs = k * rs
+        tail = (L + 127) // 128 * 128
+        rrs = tail + 16 * int(rng.integers(0, 3))
+        rgs = r * rrs
+        src = rng.integers(0, 256, G * gs, dtype=np.uint8)
+        rep = run_encode(qf, src, k, r, L, G, rs, gs, rrs, rgs, zero_tail=True)
+        for g in range(G):
+            rows = np.stack([src[g * gs + i * rs: g * gs + i * rs + L] for i in range(k)])
+            want = oracle.encode(rows, r)
+            for j in range(r):
+                off = g * rgs + j * rrs
+                assert (rep[off: off + L] == want[j]).all(), (L, g, j)
+                assert (rep[off + L: off + tail] == 0).all(), (L, g, j)
+                assert (rep[off + tail: off + rrs] == 0xA5).all(), (L, g, j)
