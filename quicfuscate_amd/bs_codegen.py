@@ -346,8 +346,8 @@ class KernelSpec:
     @property
     def far(self) -> bool:
         """Item loop branches as 64-bit pc-relative jumps: the straight-line
-        body exceeds the +-128 KiB of s_branch (dec always; enc for large k*r)."""
-        return self.mode == "dec" or (self.mode == "enc" and self.k * (70 + 8 * self.r) > 14000)
+        body exceeds the +-128 KiB of s_branch (dec always; enc / syn for large k*r)."""
+        return self.mode == "dec" or self.k * (70 + 8 * self.r) > 14000
 
     @property
     def kernarg_bytes(self) -> int:
@@ -921,7 +921,7 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         present(k + j, 1, S_TMP2)
         E(Op("s_and64", (S_TMP2, S_TMP2, S_STB)))
         _store_pair(E, acc0 + 8 * j, S_TMP, S_TMP2, spec.st_policy)
-    _epilogue_next_item(E)
+    _epilogue_next_item(E, far=spec.far)
     return ops
 
 

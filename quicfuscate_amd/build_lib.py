@@ -28,10 +28,11 @@ SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip", "qf_bs.hip", "qf_ad
            "qf_gf16.hip", "qf_objects16.hip"]
 # (k, r) Cauchy configurations that get a bit-sliced assembly kernel
 # (bs_codegen.py); every other shape runs the general v_perm kernel.
-BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1)]
-# encode-only kernels for the C5 adaptive shapes (Normal/Medium
-# windows, r = ceil(k * ratio) - k); codes with r > 16 in passes of <= 16 repairs
-BS_ENC_ONLY = [(32, 5), (48, 8), (96, 15), (128, 20), (160, 48), (196, 59)]
+BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1), (32, 5), (48, 8), (96, 15)]
+# C5 adaptive shapes (Normal/Medium windows, r = ceil(k * ratio) - k):
+# r <= 16 above (encode, syndrome and fused decode kernels); larger r encode
+# only, in passes
+BS_ENC_ONLY = [(128, 20), (160, 48), (196, 59)]
 BS_PASS = 22   # repairs per pass: 8 r accumulator VGPRs, r <= 22 fits 256 at pd 3
 BS_PD = 3
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")

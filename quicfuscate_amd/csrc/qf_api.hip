@@ -826,13 +826,15 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     if (s) return s;
     const char* nobs = getenv("QF_DISABLE_BS");
     if (!row_coeffs && !(nobs && atoi(nobs)) && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
-        max_rows <= 255 && L % 16 == 0 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
+        max_rows <= 255 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
         sh->row_stride < (1ull << 32) && (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31) &&
         (uint64_t)r * 16 * qf::bs_padded_units(L) < (1ull << 32)) {
         // fused single-pass decode unless QF_DECODE_SYN=1 asks for the
         // two-kernel syndrome + v_perm combine path
         const char* two = getenv("QF_DECODE_SYN");
-        if (qf::dec_available(k, r) && !(two && atoi(two)) && sh->rec_gen_stride < (1ull << 32) &&
+        // (L % 16 != 0: the fused kernel's 16-B stores would pass L; the
+        // syndrome path reads the last unit whole and stores exactly L bytes)
+        if (qf::dec_available(k, r) && !(two && atoi(two)) && L % 16 == 0 && sh->rec_gen_stride < (1ull << 32) &&
             sh->rec_row_stride < (1ull << 32))
             return decode_fused(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);

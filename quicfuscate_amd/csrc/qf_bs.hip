@@ -72,9 +72,10 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return hipErrorInvalidValue;
-    // a partial last unit only in the enc zero-tail lane space (its bytes >= L
-    // are masked to zero before the store)
-    if ((L % 16 && (e->mode != 'e' || Lv != s19)) || L < 32 || sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
+    // a partial last unit: enc in the zero-tail lane space (its bytes >= L are
+    // masked to zero before the store); syn (the syndrome rows' tail is junk
+    // the combine never stores); never the fused decode (caller rows)
+    if ((L % 16 && (e->mode == 'd' || (e->mode == 'e' && Lv != s19))) || L < 32 || sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
         return hipErrorInvalidValue;
     if (!cache.fn[idx]) {

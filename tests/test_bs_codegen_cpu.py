@@ -127,11 +127,17 @@ def _gf_matvec(D, rows):
     (8, 4, 3, 80, 7, 2),      # half chunks
     (16, 16, 4, 64, 5, 1),
     (5, 3, 1, 64, 9, 1),
+    (8, 4, 3, 72, 5, 2),      # partial last unit (padded lane space only)
+    (6, 5, 3, 41, 7, 1),
 ])
 @pytest.mark.parametrize("padded", [False, True])
 def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves, padded):
     """Decode stage A on the emulator: syndromes of the accepted repairs, and
-    the closed-form Cauchy inverse applied to them gives the erased sources."""
+    the closed-form Cauchy inverse applied to them gives the erased sources.
+    With L % 16 != 0 the last unit is read whole (bytes past L are junk in
+    the syndrome rows; the combine stores only L bytes)."""
+    if L % 16 and not padded:
+        pytest.skip("a partial last unit needs the padded lane space")
     spec = bs.KernelSpec(k, r, pd, mode="syn")
     ops = bs.generate(spec)
     rng = np.random.default_rng(7 * k + r + L)
@@ -167,7 +173,7 @@ def test_emulated_syndrome_kernel(oracle, k, r, pd, L, G, waves, padded):
     emu.add_buffer(ROWS, rows)
     emu.add_buffer(SYN, syn)
     emu.add_buffer(MAP, smap)
-    emu.add_buffer(ZERO, np.zeros(L, np.uint8))
+    emu.add_buffer(ZERO, np.zeros((L + 15) // 16 * 16, np.uint8))
     ka = bs.kernargs(ROWS, SYN, rgs, sgs, rs, srs, L, G, waves * 4, smap=MAP, map_stride=mstride, zero=ZERO,
                      Lv=Lv)
     waves = max(waves, (bs.launch_geometry(L, G, Lv)[2] + 3) // 4)
