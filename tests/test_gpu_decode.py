@@ -119,7 +119,10 @@ def _path(monkeypatch, path):
 @pytest.mark.parametrize("k,r,L,G", [(64, 16, 1200, 40), (16, 16, 100, 30), (4, 2, 8, 20),
                                      (10, 2, 8, 20), (33, 7, 37, 25), (1, 3, 16, 10),
                                      (16, 16, 96, 30), (32, 16, 64, 25), (64, 10, 1216, 20),
-                                     (16, 1, 64, 40), (64, 16, 80, 50)])
+                                     (16, 1, 64, 40), (64, 16, 80, 50),
+                                     # C5 shapes with generated kernels; 9000: partial last unit
+                                     (32, 5, 1200, 30), (48, 8, 1200, 30), (96, 15, 1200, 20),
+                                     (96, 15, 9000, 4), (48, 8, 1000, 12)])
 def test_decode_matches_oracle_random_erasures(qf, oracle, gpu_ctx, k, r, L, G, path, monkeypatch):
     _path(monkeypatch, path)
     rng = np.random.default_rng(k + r + L)
