@@ -32,7 +32,7 @@ BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1), (32, 5), (48, 8),
 # C5 adaptive shapes (Normal/Medium windows, r = ceil(k * ratio) - k):
 # r <= 16 above (encode, syndrome and fused decode kernels); larger r encode
 # only, in passes
-BS_ENC_ONLY = [(128, 20), (160, 48), (196, 59)]
+BS_ENC_ONLY = [(128, 20), (128, 39), (160, 48), (196, 59)]   # (128, 39): Medium default window
 BS_PASS = 22   # repairs per pass: 8 r accumulator VGPRs, r <= 22 fits 256 at pd 3
 BS_PD = 3
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")

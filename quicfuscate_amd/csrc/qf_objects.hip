@@ -22,13 +22,18 @@ static inline uint32_t round16(uint32_t x) { return (x + 15) & ~15u; }
 struct qf_encoder {
     qf_ctx* ctx = nullptr;
     uint32_t k = 0, n = 0, max_len = 0, stride = 0;
-    uint8_t* d_ring = nullptr;  // k slots of `stride` bytes (zero padded)
+    // 2k slots of `stride` bytes (zero padded): packet c sits in slots c % k
+    // and c % k + k, so the window (oldest first) is always the k contiguous
+    // slots from `head` -- a plain batch encode with the cached Cauchy matrix
+    uint8_t* d_ring = nullptr;
     uint8_t* d_out = nullptr;   // up to 256 repair rows
     std::vector<uint32_t> lens;
     std::vector<uint64_t> ids;
     uint32_t count = 0;  // packets in the window (<= k)
     uint32_t head = 0;   // next slot to write (== oldest slot once full)
-    std::vector<uint8_t> stage;
+    uint8_t* h_stage = nullptr;      // pinned staging of one packet
+    hipEvent_t stage_done = nullptr; // its copies have landed
+    std::vector<uint8_t> win;        // Cauchy rows 0..r-1 in window order (cached)
 };
 
 struct qf_decoder {
@@ -67,10 +72,11 @@ int qf_encoder_new(qf_ctx* ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_enc
     e->stride = round16(max_len);
     e->lens.assign(k, 0);
     e->ids.assign(k, 0);
-    e->stage.assign(e->stride, 0);
-    if (hipMalloc(&e->d_ring, (size_t)k * e->stride) != hipSuccess ||
+    if (hipMalloc(&e->d_ring, (size_t)2 * k * e->stride) != hipSuccess ||
         hipMalloc(&e->d_out, (size_t)256 * e->stride) != hipSuccess ||
-        hipMemset(e->d_ring, 0, (size_t)k * e->stride) != hipSuccess) {
+        hipMemset(e->d_ring, 0, (size_t)2 * k * e->stride) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&e->h_stage), e->stride) != hipSuccess ||
+        hipEventCreateWithFlags(&e->stage_done, hipEventDisableTiming) != hipSuccess) {
         qf_encoder_free(e);
         return QF_ENOMEM;
     }
@@ -80,6 +86,11 @@ int qf_encoder_new(qf_ctx* ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_enc
 
 int qf_encoder_free(qf_encoder* e) {
     if (!e) return QF_OK;
+    if (e->stage_done) {
+        hipEventSynchronize(e->stage_done);
+        hipEventDestroy(e->stage_done);
+    }
+    if (e->h_stage) hipHostFree(e->h_stage);
     if (e->d_ring) hipFree(e->d_ring);
     if (e->d_out) hipFree(e->d_out);
     delete e;
@@ -91,12 +102,17 @@ int qf_encoder_window_len(const qf_encoder* e) { return e ? (int)e->count : QF_E
 // decoder.rs:164-169: when the window holds k packets the oldest is dropped.
 int qf_encoder_add_source_packet(qf_encoder* e, uint64_t id, const uint8_t* data, uint32_t len) {
     if (!e || (len && !data) || len > e->max_len) return QF_EINVAL;
-    memset(e->stage.data(), 0, e->stride);
-    if (len) memcpy(e->stage.data(), data, len);
+    // the staging buffer is reused: the previous packet's copies must have landed
+    QF_CHECK_HIP(hipEventSynchronize(e->stage_done));
+    memset(e->h_stage, 0, e->stride);
+    if (len) memcpy(e->h_stage, data, len);
     const uint32_t slot = e->head;
-    QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)slot * e->stride, e->stage.data(), e->stride,
-                                hipMemcpyHostToDevice, (hipStream_t)qf_ctx_stream(e->ctx)));
-    QF_CHECK_HIP(hipStreamSynchronize((hipStream_t)qf_ctx_stream(e->ctx)));
+    hipStream_t st = (hipStream_t)qf_ctx_stream(e->ctx);
+    QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)slot * e->stride, e->h_stage, e->stride,
+                                hipMemcpyHostToDevice, st));
+    QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)(slot + e->k) * e->stride, e->h_stage, e->stride,
+                                hipMemcpyHostToDevice, st));
+    QF_CHECK_HIP(hipEventRecord(e->stage_done, st));
     e->lens[slot] = len;
     e->ids[slot] = id;
     e->head = (e->head + 1) % e->k;
@@ -114,19 +130,22 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
     const uint32_t L = e->lens[oldest];  // packet_len = window[0].len
     const uint32_t newest = (e->head + k - 1) % k;
     if (out_data && out_stride < L) return QF_ETOOSMALL;
-    // Cauchy rows first..first+count-1 in window order (decoder.rs:280-298)
-    std::vector<uint8_t> win((size_t)count * k), slotc((size_t)count * k);
-    const auto& f = qf::gf();
-    for (uint32_t q = 0; q < count; ++q) {
-        const uint8_t y = (uint8_t)(k + first + q);
-        for (uint32_t i = 0; i < k; ++i) {
-            uint8_t c;
-            if (!f.inv((uint8_t)((uint8_t)i ^ y), &c)) return QF_ERANGE;
-            win[(size_t)q * k + i] = c;
-            slotc[(size_t)q * k + (oldest + i) % k] = c;  // ring slot of window position i
-        }
+    // Cauchy rows first..first+count-1 in window order (decoder.rs:280-298),
+    // computed once per encoder
+    if ((uint64_t)k + first + count > 256) return QF_ERANGE;  // gf_inv(0)
+    const uint32_t rows = first + count;
+    if (e->win.size() < (size_t)rows * k) {
+        const auto& f = qf::gf();
+        e->win.resize((size_t)rows * k);
+        for (uint32_t q = 0; q < rows; ++q)
+            for (uint32_t i = 0; i < k; ++i)
+                if (!f.inv((uint8_t)((uint8_t)i ^ (uint8_t)(k + q)), &e->win[(size_t)q * k + i])) return QF_ERANGE;
     }
+    const uint8_t* win = e->win.data() + (size_t)first * k;
     if (L > 0) {
+        // the window is contiguous in the double ring: repairs 0..count-1 are
+        // the cached Cauchy code (k, count) (generated kernel or cached
+        // tables); a later first row goes through explicit coefficients
         qf_encode_shape sh{};
         sh.k = k;
         sh.r = count;
@@ -135,7 +154,8 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
         sh.src_gen_stride = (uint64_t)k * e->stride;
         sh.rep_row_stride = e->stride;
         sh.rep_gen_stride = (uint64_t)count * e->stride;
-        int s = qf_encode_batch(e->ctx, &sh, 1, e->d_ring, e->d_out, slotc.data());
+        int s = qf_encode_batch(e->ctx, &sh, 1, e->d_ring + (size_t)oldest * e->stride, e->d_out,
+                                first == 0 ? nullptr : win);
         if (s != QF_OK) return s;
         if (out_data) {
             QF_CHECK_HIP(hipMemcpy2DAsync(out_data, out_stride, e->d_out, e->stride, L, count,
@@ -146,7 +166,7 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
     for (uint32_t q = 0; q < count; ++q) {
         if (out_len) out_len[q] = L;
         if (out_ids) out_ids[q] = e->ids[newest] + 1 + first + q;  // decoder.rs:267
-        if (out_coeffs) memcpy(out_coeffs + (size_t)q * k, win.data() + (size_t)q * k, k);
+        if (out_coeffs) memcpy(out_coeffs + (size_t)q * k, win + (size_t)q * k, k);
     }
     return QF_OK;
 }

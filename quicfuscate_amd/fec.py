@@ -675,9 +675,11 @@ class AdaptiveFec:
         stride = max(self.config.max_len, 1)
         st = self.state()
         kmax = max(256, 2 * st["k"])  # coefficient bytes: k (GF(2^8)) or 2k (GF(2^16), Extreme)
-        data = (ctypes.c_uint8 * (cap * stride))()
-        co = (ctypes.c_uint8 * (cap * kmax))()
-        desc = (L.PacketDesc * cap)()
+        key = (cap, stride, kmax)
+        if getattr(self, "_send_bufs", (None,))[0] != key:   # reused across calls
+            self._send_bufs = (key, (ctypes.c_uint8 * (cap * stride))(), (ctypes.c_uint8 * (cap * kmax))(),
+                               (L.PacketDesc * cap)())
+        _, data, co, desc = self._send_bufs
         n = ctypes.c_uint32()
         pay = pkt.payload()
         buf = (ctypes.c_uint8 * max(1, len(pay))).from_buffer_copy(pay.ljust(max(1, len(pay)), b"\0"))
@@ -685,11 +687,11 @@ class AdaptiveFec:
                                           ctypes.byref(n))
         if s not in (L.QF_OK, L.QF_ERANGE):
             check(s, "on_send")
-        raw, cr = bytes(data), bytes(co)
+        mv_d, mv_c = memoryview(data), memoryview(co)
         for i in range(n.value):
             d = desc[i]
-            payload = bytearray(raw[i * stride: i * stride + d.len])
-            coeffs = cr[i * kmax: i * kmax + d.coeff_len] if not d.is_systematic else None
+            payload = bytearray(mv_d[i * stride: i * stride + d.len])
+            coeffs = bytes(mv_c[i * kmax: i * kmax + d.coeff_len]) if not d.is_systematic else None
             outgoing_queue.append(Packet(d.id, payload, d.len, bool(d.is_systematic), coeffs, d.coeff_len))
         return s
 
