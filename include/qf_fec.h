@@ -385,10 +385,14 @@ int qf_encode16_batch(qf_ctx *ctx, const qf_encode_shape *shape, uint32_t G, con
  * Acceptance as Decoder16: the first k rows, row index < k = systematic
  * column (the reference's id % k), no duplicate filtering (a duplicated
  * column is singular: QF_ERANK).  row_coeffs_dev: NULL (row index k + j
- * carries Cauchy row j; r only sizes the output) or k u16 per slot at (g*max_rows + slot)*k (the
- * packet's big-endian coefficient block, converted).  min(k, r) <= 64,
- * k <= 4096, max_rows <= 8192 (QF_EINVAL beyond).  Recovered rows: erased
- * sources ascending, with rec_index / n_rec / status as qf_decode_batch. */
+ * carries Cauchy row j) or k u16 per slot at (g*max_rows + slot)*k (the
+ * packet's big-endian coefficient block, converted).  r sizes the output:
+ * up to min(k, r) erasures per generation (QF_ERANGE status beyond).
+ * min(k, r) <= 64: all generations at once (Gauss-Jordan in LDS); larger:
+ * one generation at a time (closed-form Cauchy inverse, or Gauss-Jordan in
+ * the workspace for explicit coefficients).  k <= 4096, r >= 1,
+ * max_rows <= 65536 (QF_EINVAL beyond).  Recovered rows: erased sources
+ * ascending, with rec_index / n_rec / status as qf_decode_batch. */
 int qf_decode16_batch(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G, const uint8_t *rows_dev,
                       const uint16_t *row_index_dev, const uint32_t *n_rows_dev,
                       const uint16_t *row_coeffs_dev, uint8_t *rec_dev, uint16_t *rec_index_dev,

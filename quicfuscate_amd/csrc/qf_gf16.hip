@@ -878,11 +878,12 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     if (!ctx || !sh) return QF_EINVAL;
     const uint32_t k = sh->k, r = sh->r, L = sh->L, max_rows = sh->max_rows;
     const uint32_t e_max = std::min(k, r);
-    if (k == 0 || k > 4096 || (L & 1) || max_rows == 0 || max_rows > 65536) return QF_EINVAL;
+    // r sizes the recovered rows (e <= min(k, r)); r = 0 leaves nothing to solve with
+    if (k == 0 || r == 0 || k > 4096 || (L & 1) || max_rows == 0 || max_rows > 65536) return QF_EINVAL;
     if (G == 0) return QF_OK;
-    if (!rows || !row_index || !n_rec || !status || (e_max && (!rec || !rec_index))) return QF_EINVAL;
+    if (!rows || !row_index || !n_rec || !status || !rec || !rec_index) return QF_EINVAL;
     if ((reinterpret_cast<uintptr_t>(rows) & 15) || (sh->row_stride & 15) || (sh->rows_gen_stride & 15) ||
-        (e_max && ((reinterpret_cast<uintptr_t>(rec) & 15) || (sh->rec_row_stride & 15) || (sh->rec_gen_stride & 15))))
+        (reinterpret_cast<uintptr_t>(rec) & 15) || (sh->rec_row_stride & 15) || (sh->rec_gen_stride & 15))
         return QF_EINVAL;
     std::unique_lock<std::mutex> lk;
     int s = qf::ctx_lock(ctx, lk);
@@ -906,13 +907,12 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         d.exp = gexp;
         d.wl = reinterpret_cast<uint16_t*>(w);
         d.n_out = n_rec;
-        d.rec_index = rec_index ? rec_index : reinterpret_cast<uint16_t*>(w);  // e_max == 0: nothing recorded
+        d.rec_index = rec_index;
         d.status = status;
         d.k = k;
         d.r = r;
         d.e_max = ew;
         d.max_rows = max_rows;
-        if (!e_max) return QF_EINVAL;  // r == 0: nothing to solve with (k > 0)
         hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
         hipLaunchKernelGGL(k_decode16_prepare, dim3(G), dim3(256), 0, st, d);
         QF_HIP(hipGetLastError());
