@@ -161,7 +161,8 @@ struct Mv16Args {
     const uint16_t* m;      // logs, m[g*mgs + b*mrs + c] (kNoLog = 0)
     uint64_t mgs, mrs;
     const uint32_t* nout_g; // outputs of generation g (null: nout)
-    const uint32_t* nin_g;  // inputs of generation g (null: nin)
+    const uint32_t* nin_g;  // inputs of generation g at nin_g[g * nin_gs] (null: nin)
+    uint32_t nin_gs;
     const uint16_t* log;
     const uint16_t* exp;
     uint32_t* acc_ws;       // split: [g][nout][Lp/4] accumulator (zeroed)
@@ -183,7 +184,7 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
         const uint32_t nout = a.nout_g ? min(a.nout_g[g], a.nout) : a.nout;
         if (b0 >= nout) continue;
         const uint32_t no = min((uint32_t)kR16, nout - b0);
-        const uint32_t nin = a.nin_g ? min(a.nin_g[g], a.nin) : a.nin;
+        const uint32_t nin = a.nin_g ? min(a.nin_g[g * a.nin_gs], a.nin) : a.nin;
         const uint32_t c0 = ks * a.kchunk, c1 = min(nin, c0 + a.kchunk);
         const uint32_t nb = min(16u, a.L - 16 * u);
         uint32_t acc[kR16][4];
@@ -205,22 +206,28 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
         // software pipeline: row c + 2's bytes and row c + 1's log gathers
         // are in flight while row c's products are formed
         uint4 nxt = make_uint4(0, 0, 0, 0);
-        uint32_t lxn[8];
-        if (c0 < c1) symbol_logs(load16_partial(ip + (uint64_t)(isel ? isel[c0] : c0) * a.irs, nb), a.log, lxn);
+        uint32_t lxn[8], lcr[kR16];
+        // coefficient logs of row c (outputs past `no` read a valid row and count as 0)
+        auto coef_row = [&](uint32_t c, uint32_t (&out)[kR16]) {
+#pragma unroll
+            for (int bb = 0; bb < kR16; ++bb) out[bb] = m[(uint64_t)min((uint32_t)bb, no - 1) * a.mrs + c];
+        };
+        if (c0 < c1) {
+            symbol_logs(load16_partial(ip + (uint64_t)(isel ? isel[c0] : c0) * a.irs, nb), a.log, lxn);
+            coef_row(c0, lcr);
+        }
         if (c0 + 1 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c0 + 1] : c0 + 1) * a.irs, nb);
         for (uint32_t c = c0; c < c1; ++c) {
             uint32_t lx[8], lc[kR16];
 #pragma unroll
             for (int q = 0; q < 8; ++q) lx[q] = lxn[q];
-            if (c + 1 < c1) {
-                symbol_logs(nxt, a.log, lxn);
-                if (c + 2 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c + 2] : c + 2) * a.irs, nb);
-            }
-            // coefficients of the outputs past `no` read a valid row and count as 0
 #pragma unroll
-            for (int bb = 0; bb < kR16; ++bb) {
-                const uint32_t v = m[(uint64_t)min((uint32_t)bb, no - 1) * a.mrs + c];
-                lc[bb] = (uint32_t)bb < no ? log_off(v) : kZeroOff;
+            for (int bb = 0; bb < kR16; ++bb) lc[bb] = (uint32_t)bb < no ? log_off(lcr[bb]) : kZeroOff;
+            if (c + 1 < c1) {
+                // next row's log gathers and coefficients in flight during this row
+                symbol_logs(nxt, a.log, lxn);
+                coef_row(c + 1, lcr);
+                if (c + 2 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c + 2] : c + 2) * a.irs, nb);
             }
 #pragma unroll
             for (int bb = 0; bb < kR16; ++bb) mul_acc(acc[bb], lc[bb], lx, sexp);
@@ -446,8 +453,9 @@ __global__ void __launch_bounds__(256) k_decode16_prepare(Dec16Args a) {
     }
 }
 
-// Large path (e_max > 64): one generation at a time, everything in the
-// workspace.  Lists of the accepted rows:
+// Large path (e_max > 64, Extreme windows): chunks of generations, one grid
+// z-slice per generation, everything in the workspace (per-generation
+// strides below).  Lists of the accepted rows:
 struct BigWs {
     Dec16State* st;
     uint16_t* J;      // repair row index, by repair order a
@@ -466,17 +474,44 @@ struct BigWs {
 
 struct BigArgs {
     BigWs w;
-    const uint16_t* row_index;   // generation's
-    uint32_t n_rows;
-    const uint32_t* n_rows_dev;  // generation's (or null)
-    const uint16_t* row_coeffs;  // generation's [max_rows][k] or null
+    const uint16_t* row_index;   // [g][max_rows]
+    uint32_t n_rows;             // max_rows
+    const uint32_t* n_rows_dev;  // [g] (or null)
+    const uint16_t* row_coeffs;  // [g][max_rows][k] or null
     const uint16_t* log;
     const uint16_t* exp;
-    uint32_t* n_out;             // generation's
-    uint16_t* rec_index;         // generation's [e_max]
-    int32_t* status;             // generation's
+    uint32_t* n_out;             // [g]
+    uint16_t* rec_index;         // [g][e_max]
+    int32_t* status;             // [g]
     uint32_t k, e_max;
+    uint64_t Lp;                 // syndrome row bytes
 };
+
+// the arguments of generation g of the chunk (pointers offset by its strides)
+QF_DEV BigArgs view(const BigArgs& A, uint32_t g) {
+    BigArgs a = A;
+    const uint64_t em = A.e_max, k = A.k;
+    a.w.st = A.w.st + g;
+    a.w.J = A.w.J + g * em;
+    a.w.Jslot = A.w.Jslot + g * em;
+    a.w.E = A.w.E + g * em;
+    a.w.Sslot = A.w.Sslot + g * k;
+    a.w.Scol = A.w.Scol + g * k;
+    a.w.mlog = A.w.mlog + g * em * k;
+    a.w.dlog = A.w.dlog + g * em * em;
+    a.w.aug = A.w.aug ? A.w.aug + g * em * 2 * em : nullptr;
+    a.w.mark = A.w.mark + g * em;
+    a.w.pivrow = A.w.pivrow + g * em;
+    a.w.lprod = A.w.lprod + g * 4 * em;
+    a.w.synd = A.w.synd + g * em * A.Lp;
+    a.row_index = A.row_index + (uint64_t)g * A.n_rows;
+    a.n_rows_dev = A.n_rows_dev ? A.n_rows_dev + g : nullptr;
+    a.row_coeffs = A.row_coeffs ? A.row_coeffs + (uint64_t)g * A.n_rows * k : nullptr;
+    a.n_out = A.n_out + g;
+    a.rec_index = A.rec_index + g * em;
+    a.status = A.status + g;
+    return a;
+}
 
 QF_DEV void big_fail(const BigArgs& a, int32_t s) {
     *a.status = s;
@@ -503,7 +538,8 @@ QF_DEV uint32_t block_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
 // acceptance (decoder.rs:563-578) and the row lists; one block of 1024,
 // thread t owns slots / columns [4t, 4t + 4) (k <= 4096), lists compacted in
 // order with block scans
-__global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs a) {
+__global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs A) {
+    const BigArgs a = view(A, blockIdx.z);
     __shared__ __align__(4) uint8_t present[4096];
     __shared__ uint32_t scan[1024];
     __shared__ int32_t s_status;
@@ -577,7 +613,8 @@ __global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs a) {
 }
 
 // mlog[a][c] = log C[J_a][Scol c] (syndromes: rows_J ^ C[J,S] x_S)
-__global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs a) {
+__global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs A) {
+    const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e, ns = a.w.st->nin, k = a.k;
     const uint64_t total = (uint64_t)e * ns;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -593,7 +630,8 @@ __global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs a) {
 //   Px_a = prod_{c != a} (x_a ^ x_c), Py_b = prod_{c != b} (y_b ^ y_c).
 // One block per row / column value, logs summed across the block.  A
 // repeated repair row (x_a = x_c) is singular: QF_ERANK.
-__global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs a) {
+__global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs A) {
+    const BigArgs a = view(A, blockIdx.z);
     __shared__ uint64_t sq[256], sp[256];
     __shared__ uint32_t s_zero;
     const uint32_t e = a.w.st->e;
@@ -635,7 +673,8 @@ __global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs a) {
     a.w.lprod[(row ? 1 : 3) * a.e_max + q] = (uint32_t)(sp[0] % kOrder);
 }
 
-__global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs a) {
+__global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs A) {
+    const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e;
     if (*a.status != QF_OK) return;
     const uint64_t total = (uint64_t)e * e;
@@ -652,7 +691,8 @@ __global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs a) {
 // used as a pivot with a nonzero entry there (the same pivot as the swap-based
 // search of decoder.rs:600-606 up to row order), eliminated from all other rows
 // in the columns to its right only (finished columns are never read again).
-__global__ void __launch_bounds__(256) k_dec16_gj_init(BigArgs a) {
+__global__ void __launch_bounds__(256) k_dec16_gj_init(BigArgs A) {
+    const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e;
     const uint64_t total = (uint64_t)e * 2 * e;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
@@ -664,7 +704,8 @@ __global__ void __launch_bounds__(256) k_dec16_gj_init(BigArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(1024) k_dec16_gj_pivot(BigArgs a, uint32_t c) {
+__global__ void __launch_bounds__(1024) k_dec16_gj_pivot(BigArgs A, uint32_t c) {
+    const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e;
     if (c >= e || *a.status != QF_OK) return;
     __shared__ uint32_t s_p;
@@ -684,7 +725,8 @@ __global__ void __launch_bounds__(1024) k_dec16_gj_pivot(BigArgs a, uint32_t c) 
 }
 
 // rows in blockIdx.y, columns (c, 2e) in x
-__global__ void __launch_bounds__(256) k_dec16_gj_step(BigArgs a, uint32_t c) {
+__global__ void __launch_bounds__(256) k_dec16_gj_step(BigArgs A, uint32_t c) {
+    const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e;
     const uint32_t r = blockIdx.y;
     if (c >= e || r >= e || *a.status != QF_OK) return;
@@ -705,7 +747,8 @@ __global__ void __launch_bounds__(256) k_dec16_gj_step(BigArgs a, uint32_t c) {
 }
 
 // dlog[c][a] = log(aug[piv c][e + a] / aug[piv c][c])
-__global__ void __launch_bounds__(256) k_dec16_gj_final(BigArgs a) {
+__global__ void __launch_bounds__(256) k_dec16_gj_final(BigArgs A) {
+    const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e;
     if (*a.status != QF_OK) return;
     const uint64_t ld = 2 * a.e_max;
@@ -776,6 +819,7 @@ size_t matvec_acc_bytes(qf_ctx* ctx, uint64_t G, uint32_t nout, uint32_t nin, ui
 
 // acc: workspace of matvec_acc_bytes (null: never split)
 int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name, uint8_t* acc = nullptr) {
+    if (!a.nin_gs) a.nin_gs = 1;
     a.Lu = (a.L + 15) / 16;
     a.nob = (a.nout + kR16 - 1) / kR16;
     const uint64_t lanes = G * a.nob * a.Lu;
@@ -935,18 +979,26 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         c.L = L;
         return launch_matvec(ctx, st, c, G, "k_combine16", ab ? w + wb : nullptr);
     }
-    // large path (e_max > 64, Extreme windows of 1024..4096): one generation
-    // at a time, inverse in closed form (Cauchy rows) or by Gauss-Jordan
+    // large path (e_max > 64, Extreme windows of 1024..4096): chunks of
+    // generations (grid z = generation), inverse in closed form (Cauchy rows)
+    // or by Gauss-Jordan in the workspace
     const size_t Lp = ((size_t)L + 15) / 16 * 16;
+    const uint64_t em = e_max;
+    const size_t per_gen[13] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
+                                row_coeffs ? 4 * em * em : 0, 4 * em, 4 * em, 16 * em, Lp * em};
+    size_t gen_bytes = 0;
+    for (int q = 0; q < 13; ++q) gen_bytes += per_gen[q];
+    // chunk: <= 65535 generations (grid z) and about 1 GiB of workspace
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)G, 65535ull,
+                                                                             (1ull << 30) / gen_bytes}));
     size_t off[14], tot = 0;
-    const size_t sz[14] = {sizeof(Dec16State), 2ull * e_max, 2ull * e_max, 2ull * e_max, 2ull * k, 2ull * k,
-                           2ull * e_max * k, 2ull * e_max * e_max, row_coeffs ? 4ull * e_max * e_max : 0,
-                           4ull * e_max, 4ull * e_max, 16ull * e_max, Lp * e_max,
-                           matvec_acc_bytes(ctx, 1, e_max, k, L)};
-    for (int q = 0; q < 14; ++q) {
+    for (int q = 0; q < 13; ++q) {
         off[q] = tot;
-        tot += align256(std::max<size_t>(sz[q], 1));
+        tot += align256(std::max<size_t>(per_gen[q] * chunk, 1));
     }
+    const size_t acc_bytes = matvec_acc_bytes(ctx, chunk, e_max, k, L);
+    off[13] = tot;
+    tot += align256(std::max<size_t>(acc_bytes, 1));
     s = qf::ctx_work(ctx, tot, &w);
     if (s) return s;
     BigArgs b{};
@@ -958,7 +1010,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     b.w.Scol = reinterpret_cast<uint16_t*>(w + off[5]);
     b.w.mlog = reinterpret_cast<uint16_t*>(w + off[6]);
     b.w.dlog = reinterpret_cast<uint16_t*>(w + off[7]);
-    b.w.aug = reinterpret_cast<uint16_t*>(w + off[8]);
+    b.w.aug = row_coeffs ? reinterpret_cast<uint16_t*>(w + off[8]) : nullptr;
     b.w.mark = reinterpret_cast<uint32_t*>(w + off[9]);
     b.w.pivrow = reinterpret_cast<uint32_t*>(w + off[10]);
     b.w.lprod = reinterpret_cast<uint32_t*>(w + off[11]);
@@ -968,73 +1020,87 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     b.k = k;
     b.e_max = e_max;
     b.n_rows = max_rows;
+    b.Lp = Lp;
+    uint8_t* acc = acc_bytes ? w + off[13] : nullptr;
     const int cus = qf::ctx_num_cus(ctx);
-    const uint32_t mgrid = (uint32_t)std::min<uint64_t>(((uint64_t)e_max * k + 255) / 256, 8ull * cus);
-    const uint32_t dgrid = (uint32_t)std::min<uint64_t>(((uint64_t)e_max * e_max + 255) / 256, 8ull * cus);
-    for (uint32_t g = 0; g < G; ++g) {
-        b.row_index = row_index + (size_t)g * max_rows;
-        b.n_rows_dev = n_rows ? n_rows + g : nullptr;
-        b.row_coeffs = row_coeffs ? row_coeffs + (size_t)g * max_rows * k : nullptr;
-        b.n_out = n_rec + g;
-        b.rec_index = rec_index + (size_t)g * e_max;
-        b.status = status + g;
+    const uint32_t mgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((em * k + 255) / 256, 8ull * cus / 1));
+    const uint32_t dgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((em * em + 255) / 256, 8ull * cus));
+    for (uint32_t g0 = 0; g0 < G; g0 += chunk) {
+        const uint32_t gc = std::min(chunk, G - g0);
+        b.row_index = row_index + (size_t)g0 * max_rows;
+        b.n_rows_dev = n_rows ? n_rows + g0 : nullptr;
+        b.row_coeffs = row_coeffs ? row_coeffs + (size_t)g0 * max_rows * k : nullptr;
+        b.n_out = n_rec + g0;
+        b.rec_index = rec_index + (size_t)g0 * e_max;
+        b.status = status + g0;
         hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-        hipLaunchKernelGGL(k_dec16_accept, dim3(1), dim3(1024), 0, st, b);
-        hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid), dim3(256), 0, st, b);
+        hipLaunchKernelGGL(k_dec16_accept, dim3(1, 1, gc), dim3(1024), 0, st, b);
+        hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid, 1, gc), dim3(256), 0, st, b);
         if (!row_coeffs) {
-            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max), dim3(256), 0, st, b);
-            hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max, 1, gc), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid, 1, gc), dim3(256), 0, st, b);
         } else {
-            hipLaunchKernelGGL(k_dec16_gj_init, dim3((uint32_t)std::min<uint64_t>(((uint64_t)e_max * 2 * e_max + 255) / 256,
-                                                                                  8ull * cus)),
+            hipLaunchKernelGGL(k_dec16_gj_init,
+                               dim3((uint32_t)std::min<uint64_t>((em * 2 * em + 255) / 256, 8ull * cus), 1, gc),
                                dim3(256), 0, st, b);
-            // the erasure count is on the device: launch for e_max columns,
-            // the steps past e return at once
+            // the erasure counts are on the device: launch for e_max columns,
+            // the steps past a generation's e return at once
             for (uint32_t c = 0; c < e_max; ++c) {
-                hipLaunchKernelGGL(k_dec16_gj_pivot, dim3(1), dim3(1024), 0, st, b, c);
-                hipLaunchKernelGGL(k_dec16_gj_step, dim3((2 * e_max - c + 255) / 256, e_max), dim3(256), 0, st, b, c);
+                hipLaunchKernelGGL(k_dec16_gj_pivot, dim3(1, 1, gc), dim3(1024), 0, st, b, c);
+                hipLaunchKernelGGL(k_dec16_gj_step, dim3((2 * e_max - c + 255) / 256, e_max, gc), dim3(256), 0, st,
+                                   b, c);
             }
-            hipLaunchKernelGGL(k_dec16_gj_final, dim3(dgrid), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(k_dec16_gj_final, dim3(dgrid, 1, gc), dim3(256), 0, st, b);
         }
         QF_HIP(hipGetLastError());
         qf::ctx_prof_end(ctx, st, ev, "k_dec16_prepare_large");
         // syndromes s_a = row(J_a) ^ C[J_a, S] x_S
         Mv16Args sy{};
-        sy.in = rows + (size_t)g * sh->rows_gen_stride;
+        sy.in = rows + (size_t)g0 * sh->rows_gen_stride;
+        sy.igs = sh->rows_gen_stride;
         sy.irs = sh->row_stride;
         sy.isel = b.w.Sslot;
+        sy.isel_gs = k;
         sy.base = sy.in;
+        sy.bgs = sh->rows_gen_stride;
         sy.brs = sh->row_stride;
         sy.bsel = b.w.Jslot;
+        sy.bsel_gs = e_max;
         sy.out = b.w.synd;
+        sy.ogs = em * Lp;
         sy.ors = Lp;
         sy.m = b.w.mlog;
+        sy.mgs = em * k;
         sy.mrs = k;
-        sy.nout_g = n_rec + g;
+        sy.nout_g = n_rec + g0;
         sy.nin_g = &b.w.st->nin;
+        sy.nin_gs = sizeof(Dec16State) / 4;
         sy.log = glog;
         sy.exp = gexp;
         sy.nout = e_max;
         sy.nin = k;
         sy.L = L;
-        s = launch_matvec(ctx, st, sy, 1, "k_syndromes16", sz[13] ? w + off[13] : nullptr);
+        s = launch_matvec(ctx, st, sy, gc, "k_syndromes16", acc);
         if (s) return s;
         // x_E = C[J,E]^-1 s
         Mv16Args so{};
         so.in = b.w.synd;
+        so.igs = em * Lp;
         so.irs = Lp;
-        so.out = rec + (size_t)g * sh->rec_gen_stride;
+        so.out = rec + (size_t)g0 * sh->rec_gen_stride;
+        so.ogs = sh->rec_gen_stride;
         so.ors = sh->rec_row_stride;
         so.m = b.w.dlog;
+        so.mgs = em * em;
         so.mrs = e_max;
-        so.nout_g = n_rec + g;
-        so.nin_g = n_rec + g;
+        so.nout_g = n_rec + g0;
+        so.nin_g = n_rec + g0;
         so.log = glog;
         so.exp = gexp;
         so.nout = e_max;
         so.nin = e_max;
         so.L = L;
-        s = launch_matvec(ctx, st, so, 1, "k_combine16", sz[13] ? w + off[13] : nullptr);
+        s = launch_matvec(ctx, st, so, gc, "k_combine16", acc);
         if (s) return s;
     }
     return QF_OK;
