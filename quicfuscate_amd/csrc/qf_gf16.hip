@@ -25,6 +25,7 @@
 // decodes there).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -938,7 +939,11 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     hipStream_t st = qf::ctx_stream(ctx);
     const uint32_t ew = std::max<uint32_t>(e_max, 1);
     uint8_t* w;
-    if (e_max <= kEMax) {
+    // QF_GF16_LDS_GJ=1: the all-generations-at-once Gauss-Jordan in LDS
+    // (W = C[J,E]^-1 [I | C[J,S]] over every slot) for e_max <= 64; default:
+    // the syndrome path below for every shape
+    const char* lds_gj = getenv("QF_GF16_LDS_GJ");
+    if (e_max <= kEMax && lds_gj && atoi(lds_gj)) {
         // small path: every generation at once
         const size_t wb = align256((size_t)G * ew * k * 2), ab = matvec_acc_bytes(ctx, G, e_max, k, L);
         s = qf::ctx_work(ctx, wb + ab, &w);
@@ -979,9 +984,9 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         c.L = L;
         return launch_matvec(ctx, st, c, G, "k_combine16", ab ? w + wb : nullptr);
     }
-    // large path (e_max > 64, Extreme windows of 1024..4096): chunks of
-    // generations (grid z = generation), inverse in closed form (Cauchy rows)
-    // or by Gauss-Jordan in the workspace
+    // syndrome path: chunks of generations (grid z = generation), syndromes
+    // s = p_J ^ C[J,S] x_S, then x_E = C[J,E]^-1 s with the inverse in closed
+    // form (Cauchy rows) or by Gauss-Jordan in the workspace
     const size_t Lp = ((size_t)L + 15) / 16 * 16;
     const uint64_t em = e_max;
     const size_t per_gen[13] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,

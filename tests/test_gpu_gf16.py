@@ -152,16 +152,22 @@ def check_decode(oracle, src, gens, k, L, res):
             assert np.array_equal(got, src[g, i]), (g, i)
 
 
+@pytest.mark.parametrize("lds_gj", ["0", "1"])
 @pytest.mark.parametrize("k,r,L,G,with_coeffs", [(8, 4, 8, 5, False), (16, 16, 100, 8, False),
                                                  (64, 16, 1200, 12, False), (64, 64, 258, 4, False),
                                                  (10, 6, 34, 6, True), (40, 20, 66, 4, True)])
-def test_decode16_small_path(qf, oracle, gpu_ctx, k, r, L, G, with_coeffs):
+def test_decode16_small_path(qf, oracle, gpu_ctx, k, r, L, G, with_coeffs, lds_gj, monkeypatch):
+    """Both decode paths for e <= 64: syndromes + closed-form / workspace
+    inverse (default) and the all-generations Gauss-Jordan in LDS."""
+    monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
     rng = np.random.default_rng(k * 7 + r)
     src, gens = make_gens(oracle, rng, k, r, L, G, coeff_mode="cauchy" if not with_coeffs else "random")
     check_decode(oracle, src, gens, k, L, run_decode16(qf, k, r, L, G, gens, with_coeffs))
 
 
-def test_decode16_statuses(qf, oracle, gpu_ctx):
+@pytest.mark.parametrize("lds_gj", ["0", "1"])
+def test_decode16_statuses(qf, oracle, gpu_ctx, lds_gj, monkeypatch):
+    monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
     rng = np.random.default_rng(5)
     k, r, L = 12, 6, 40
     _, g1 = make_gens(oracle, rng, k, r, L, 1, erase=3, short=True)   # ENOTREADY
