@@ -41,7 +41,7 @@ struct qf_decoder {
     uint32_t k = 0, max_len = 0, stride = 0;
     bool decoded = false, drained = false;
     // accepted rows, in arrival order (the first k win)
-    std::vector<uint8_t> rows;     // k * stride
+    uint8_t* rows = nullptr;     // k * stride, pinned: each row is uploaded as it arrives
     std::vector<uint32_t> lens;    // k
     std::vector<uint16_t> index;   // k: source index (< k) or k (repair)
     std::vector<uint8_t> coeffs;   // k * k (repair rows)
@@ -58,6 +58,7 @@ struct qf_decoder {
     uint16_t* d_rec_index = nullptr;
     uint32_t* d_nrec = nullptr;
     int32_t* d_status = nullptr;
+    uint8_t* h_rec = nullptr;       // pinned download of the recovered rows
 };
 
 extern "C" {
@@ -187,7 +188,6 @@ int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) 
     d->k = k;
     d->max_len = max_len;
     d->stride = round16(max_len);
-    d->rows.assign((size_t)k * d->stride, 0);
     d->lens.assign(k, 0);
     d->index.assign(k, 0);
     d->coeffs.assign((size_t)k * k, 0);
@@ -198,7 +198,9 @@ int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) 
               hipMalloc(&d->d_index, (size_t)k * 2) == hipSuccess &&
               hipMalloc(&d->d_rec, (size_t)emax * d->stride) == hipSuccess &&
               hipMalloc(&d->d_rec_index, (size_t)emax * 2) == hipSuccess &&
-              hipMalloc(&d->d_nrec, 4) == hipSuccess && hipMalloc(&d->d_status, 4) == hipSuccess;
+              hipMalloc(&d->d_nrec, 4) == hipSuccess && hipMalloc(&d->d_status, 4) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&d->rows), (size_t)k * d->stride) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&d->h_rec), (size_t)emax * d->stride) == hipSuccess;
     if (!ok) {
         qf_decoder_free(d);
         return QF_ENOMEM;
@@ -216,6 +218,11 @@ int qf_decoder_free(qf_decoder* d) {
     hipFree(d->d_rec_index);
     hipFree(d->d_nrec);
     hipFree(d->d_status);
+    if (d->rows) {
+        hipStreamSynchronize((hipStream_t)qf_ctx_stream(d->ctx));  // row uploads in flight
+        hipHostFree(d->rows);
+    }
+    if (d->h_rec) hipHostFree(d->h_rec);
     delete d;
     return QF_OK;
 }
@@ -229,7 +236,7 @@ static int decoder_try_decode(qf_decoder* d) {
     for (uint32_t q = 0; q < k; ++q) L = d->lens[q] > L ? d->lens[q] : L;
     if (L == 0) L = 1;
     hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows, d->rows.data(), (size_t)k * d->stride, hipMemcpyHostToDevice, st));
+    // the rows are on the device already (uploaded as they arrived)
     QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
     QF_CHECK_HIP(hipMemcpyAsync(d->d_index, d->index.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
     const uint32_t emax = k < 128 ? k : 128;
@@ -252,10 +259,10 @@ static int decoder_try_decode(qf_decoder* d) {
     QF_CHECK_HIP(hipStreamSynchronize(st));
     if (status != QF_OK) return status;  // singular: stays undecoded (decoder.rs:756-758)
     std::vector<uint16_t> ridx(nrec);
-    std::vector<uint8_t> rec((size_t)nrec * d->stride);
+    const uint8_t* rec = d->h_rec;
     if (nrec) {
         QF_CHECK_HIP(hipMemcpyAsync(ridx.data(), d->d_rec_index, (size_t)nrec * 2, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipMemcpyAsync(rec.data(), d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipMemcpyAsync(d->h_rec, d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
         QF_CHECK_HIP(hipStreamSynchronize(st));
     }
     d->out.assign((size_t)k * d->stride, 0);
@@ -269,7 +276,7 @@ static int decoder_try_decode(qf_decoder* d) {
     }
     for (uint32_t m = 0; m < nrec; ++m) {
         const uint32_t i = ridx[m];
-        memcpy(&d->out[(size_t)i * d->stride], &rec[(size_t)m * d->stride], L);
+        memcpy(&d->out[(size_t)i * d->stride], rec + (size_t)m * d->stride, L);
         d->out_len[i] = L;
     }
     d->decoded = true;
@@ -298,6 +305,10 @@ int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const u
     }
     memset(&d->rows[(size_t)q * d->stride], 0, d->stride);
     if (len) memcpy(&d->rows[(size_t)q * d->stride], data, len);
+    // to the device now; rows is pinned and slot q is not rewritten while
+    // this decoder lives, so the copy needs no wait
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows + (size_t)q * d->stride, &d->rows[(size_t)q * d->stride], d->stride,
+                                hipMemcpyHostToDevice, (hipStream_t)qf_ctx_stream(d->ctx)));
     d->lens[q] = len;
     d->accepted++;
     if (d->accepted == k) {

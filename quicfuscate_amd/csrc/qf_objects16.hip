@@ -73,7 +73,7 @@ struct qf_decoder16 {
     uint32_t k = 0, max_len = 0, stride = 0;
     bool decoded = false, drained = false;
     // the first k rows, arrival order (decoder.rs:563-566)
-    std::vector<uint8_t> rows;      // k * stride
+    uint8_t* rows = nullptr;      // k * stride, pinned: each row is uploaded as it arrives
     std::vector<uint32_t> lens;
     std::vector<uint16_t> index;    // source column (systematic) or k (repair)
     std::vector<uint16_t> coeffs;   // k * k, repair rows (from the big-endian block)
@@ -85,6 +85,8 @@ struct qf_decoder16 {
     uint16_t *d_index = nullptr, *d_coeffs = nullptr, *d_rec_index = nullptr;
     uint32_t* d_nrec = nullptr;
     int32_t* d_status = nullptr;
+    uint8_t* h_rec = nullptr;       // pinned download of the recovered rows (grown)
+    size_t h_rec_bytes = 0;
 };
 
 extern "C" {
@@ -196,7 +198,6 @@ int qf_decoder16_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder16** o
     d->k = k;
     d->max_len = max_len;
     d->stride = round16(max_len);
-    d->rows.assign((size_t)k * d->stride, 0);
     d->lens.assign(k, 0);
     d->index.assign(k, 0);
     d->coeffs.assign((size_t)k * k, 0);
@@ -206,7 +207,8 @@ int qf_decoder16_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder16** o
                     hipMalloc(&d->d_index, (size_t)k * 2) == hipSuccess &&
                     hipMalloc(&d->d_coeffs, (size_t)k * k * 2) == hipSuccess &&
                     hipMalloc(&d->d_rec_index, (size_t)k * 2) == hipSuccess &&
-                    hipMalloc(&d->d_nrec, 4) == hipSuccess && hipMalloc(&d->d_status, 4) == hipSuccess;
+                    hipMalloc(&d->d_nrec, 4) == hipSuccess && hipMalloc(&d->d_status, 4) == hipSuccess &&
+                    hipHostMalloc(reinterpret_cast<void**>(&d->rows), (size_t)k * d->stride) == hipSuccess;
     if (!ok) {
         qf_decoder16_free(d);
         return QF_ENOMEM;
@@ -224,6 +226,11 @@ int qf_decoder16_free(qf_decoder16* d) {
     hipFree(d->d_rec_index);
     hipFree(d->d_nrec);
     hipFree(d->d_status);
+    if (d->rows) {
+        hipStreamSynchronize((hipStream_t)qf_ctx_stream(d->ctx));  // row uploads in flight
+        hipHostFree(d->rows);
+    }
+    if (d->h_rec) hipHostFree(d->h_rec);
     delete d;
     return QF_OK;
 }
@@ -261,7 +268,7 @@ static int decoder16_try_decode(qf_decoder16* d) {
         for (uint32_t q = 0; q < k; ++q)
             if (d->repair[q]) idx[q] = (uint16_t)k;
     hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows, d->rows.data(), (size_t)k * d->stride, hipMemcpyHostToDevice, st));
+    // the rows are on the device already (uploaded as they arrived)
     QF_CHECK_HIP(hipMemcpyAsync(d->d_index, idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
     if (!cauchy)
         QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k * 2, hipMemcpyHostToDevice, st));
@@ -284,12 +291,20 @@ static int decoder16_try_decode(qf_decoder16* d) {
     QF_CHECK_HIP(hipStreamSynchronize(st));
     if (status != QF_OK) return status;  // singular: try_decode -> false (decoder.rs:604-606)
     std::vector<uint16_t> ridx(nrec);
-    std::vector<uint8_t> rec((size_t)nrec * d->stride);
     if (nrec) {
+        const size_t need = (size_t)nrec * d->stride;
+        if (need > d->h_rec_bytes) {
+            if (d->h_rec) hipHostFree(d->h_rec);
+            d->h_rec = nullptr;
+            d->h_rec_bytes = 0;
+            if (hipHostMalloc(reinterpret_cast<void**>(&d->h_rec), need) != hipSuccess) return QF_ENOMEM;
+            d->h_rec_bytes = need;
+        }
         QF_CHECK_HIP(hipMemcpyAsync(ridx.data(), d->d_rec_index, (size_t)nrec * 2, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipMemcpyAsync(rec.data(), d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipMemcpyAsync(d->h_rec, d->d_rec, need, hipMemcpyDeviceToHost, st));
         QF_CHECK_HIP(hipStreamSynchronize(st));
     }
+    const uint8_t* rec = d->h_rec;
     d->out.assign((size_t)k * d->stride, 0);
     d->out_len.assign(k, 0);
     for (uint32_t q = 0; q < k; ++q)
@@ -300,7 +315,7 @@ static int decoder16_try_decode(qf_decoder16* d) {
         }
     for (uint32_t m = 0; m < nrec; ++m) {
         const uint32_t i = ridx[m];
-        memcpy(&d->out[(size_t)i * d->stride], &rec[(size_t)m * d->stride], Le);
+        memcpy(&d->out[(size_t)i * d->stride], rec + (size_t)m * d->stride, Le);
         d->out_len[i] = L;  // an odd length's last byte carries no symbol: 0
     }
     d->decoded = true;
@@ -327,6 +342,10 @@ int qf_decoder16_add_packet(qf_decoder16* d, uint64_t id, int is_systematic, con
     }
     memset(&d->rows[(size_t)q * d->stride], 0, d->stride);
     if (len) memcpy(&d->rows[(size_t)q * d->stride], data, len);
+    // to the device now; rows is pinned and slot q is not rewritten while
+    // this decoder lives, so the copy needs no wait
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows + (size_t)q * d->stride, &d->rows[(size_t)q * d->stride], d->stride,
+                                hipMemcpyHostToDevice, (hipStream_t)qf_ctx_stream(d->ctx)));
     d->lens[q] = len;
     d->accepted++;
     if (d->accepted == k) {

@@ -699,8 +699,10 @@ class AdaptiveFec:
         st = self.state()
         cap = max(1, st["k"] + 1024)
         stride = max(self.config.max_len, 1)
-        data = (ctypes.c_uint8 * (cap * stride))()
-        desc = (L.PacketDesc * cap)()
+        key = (cap, stride)
+        if getattr(self, "_recv_bufs", (None,))[0] != key:   # reused across calls
+            self._recv_bufs = (key, (ctypes.c_uint8 * (cap * stride))(), (L.PacketDesc * cap)())
+        _, data, desc = self._recv_bufs
         n = ctypes.c_uint32()
         pay = pkt.payload()
         buf = (ctypes.c_uint8 * max(1, len(pay))).from_buffer_copy(pay.ljust(max(1, len(pay)), b"\0"))
@@ -714,8 +716,8 @@ class AdaptiveFec:
         if s == L.QF_EINVAL and not pkt.is_systematic and pkt.coefficients is None:
             raise QfError(s, "Repair packet missing coefficients.")
         check(s, "on_receive")
-        raw = bytes(data)
-        return [Packet(desc[i].id, bytearray(raw[i * stride: i * stride + desc[i].len]), desc[i].len, True)
+        mv = memoryview(data)
+        return [Packet(desc[i].id, bytearray(mv[i * stride: i * stride + desc[i].len]), desc[i].len, True)
                 for i in range(n.value)]
 
     def close(self) -> None:

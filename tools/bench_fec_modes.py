@@ -69,6 +69,52 @@ def main():
                 oracle.encode(src, r)
                 cpu = time.perf_counter() - t0
             entry["oracle_us_per_call"] = round(cpu * 1e6, 1)
+        # receive side: a fresh generation of packets 0..k-1 with 20 % of the
+        # sources lost, completed by the window's repairs (adaptive.rs:566-599)
+        if s == L.QF_OK and r:
+            snd = qf.AdaptiveFec(qf.FecConfig(initial_mode=mode, max_len=2048), now=0.0)
+            rcv = qf.AdaptiveFec(qf.FecConfig(initial_mode=mode, max_len=2048), now=0.0)
+            pk = [qf.Packet(i, bytearray(np.random.default_rng(i).integers(0, 256, a.len, dtype=np.uint8).tobytes()),
+                            a.len, True) for i in range(k)]
+            reps = []
+            for p in pk:
+                q = []
+                snd.on_send(p, q)
+                reps = q[1:]
+            lost = set(range(0, k, 5)) if r >= len(range(0, k, 5)) else set(range(r))
+            # warm-up generation on a separate receiver (first-use allocations)
+            warm = qf.AdaptiveFec(qf.FecConfig(initial_mode=mode, max_len=2048), now=0.0)
+            for p in [p for p in pk if p.id not in lost] + reps[: len(lost)]:
+                warm.on_receive(p)
+            warm.close()
+            arrivals = [p for p in pk if p.id not in lost] + reps[: len(lost)]
+            t0 = time.perf_counter()
+            for p in arrivals[:-1]:
+                rcv.on_receive(p)
+            t1 = time.perf_counter()
+            # the k-th row decodes: time the library call itself (the mirror's
+            # Python packet objects for k recovered packets are not the product)
+            import ctypes
+            p = arrivals[-1]
+            cap, stride = k + 1024, 2048
+            data = (ctypes.c_uint8 * (cap * stride))()
+            desc = (L.PacketDesc * cap)()
+            nn = ctypes.c_uint32()
+            pay = p.payload()
+            buf = (ctypes.c_uint8 * len(pay)).from_buffer_copy(pay)
+            co = (ctypes.c_uint8 * p.coeff_len).from_buffer_copy(bytes(p.coefficients[: p.coeff_len]))
+            t1 = time.perf_counter()
+            st_ = rcv._lib.qf_adaptive_on_receive(rcv.handle, p.id, 0, buf, len(pay), co, p.coeff_len, data, stride,
+                                                  desc, cap, ctypes.byref(nn))
+            t2 = time.perf_counter()
+            assert st_ == 0 and nn.value == k
+            mv = memoryview(data)
+            assert all(bytes(mv[i * stride: i * stride + desc[i].len]) == pk[desc[i].id].payload() for i in range(k))
+            entry["receive_us_per_packet"] = round((t1 - t0) / max(1, len(arrivals) - 1) * 1e6, 1)  # (incl. buffers)
+            entry["decode_us_kth_packet"] = round((t2 - t1) * 1e6, 1)
+            entry["erased"] = len(lost)
+            snd.close()
+            rcv.close()
         res[mode.name] = entry
         print(mode.name, entry, flush=True)
         fec.close()
