@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "gf256_tables.h"
@@ -236,21 +237,48 @@ static int decoder_try_decode(qf_decoder* d) {
     for (uint32_t q = 0; q < k; ++q) L = d->lens[q] > L ? d->lens[q] : L;
     if (L == 0) L = 1;
     hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
-    // the rows are on the device already (uploaded as they arrived)
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_index, d->index.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
     const uint32_t emax = k < 128 ? k : 128;
+    // Repair rows that are Cauchy rows of this k (c_i = gf_inv(i ^ y), y =
+    // k + j: what Encoder emits for a window aligned with the generation)
+    // decode by their repair index on the Cauchy paths (generated kernels);
+    // any other row keeps the whole system explicit.
+    const auto& f = qf::gf();
+    std::vector<uint16_t> idx(d->index);
+    uint32_t rmax = 0;
+    bool cauchy = true;
+    for (uint32_t q = 0; q < k && cauchy; ++q) {
+        if (d->index[q] != k) continue;  // systematic
+        const uint8_t* c = &d->coeffs[(size_t)q * k];
+        uint8_t y = 0;
+        if (!f.inv(c[0], &y) || y < k) {   // c_0 = gf_inv(y)
+            cauchy = false;
+            break;
+        }
+        for (uint32_t i = 0; i < k && cauchy; ++i) {
+            uint8_t v = 0;
+            cauchy = f.inv((uint8_t)(i ^ y), &v) && v == c[i];
+        }
+        idx[q] = y;
+        rmax = std::max<uint32_t>(rmax, (uint32_t)y - k + 1);
+    }
+    cauchy = cauchy && rmax <= emax;
+    if (!cauchy) {
+        idx = d->index;
+        QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
+    }
+    // the rows are on the device already (uploaded as they arrived)
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_index, idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
     qf_decode_shape sh{};
     sh.k = k;
-    sh.r = emax;
+    sh.r = cauchy ? std::max<uint32_t>(rmax, 1) : emax;
     sh.L = L;
     sh.max_rows = k;
     sh.row_stride = d->stride;
     sh.rows_gen_stride = (uint64_t)k * d->stride;
     sh.rec_row_stride = d->stride;
     sh.rec_gen_stride = (uint64_t)emax * d->stride;
-    int s = qf_decode_batch(d->ctx, &sh, 1, d->d_rows, d->d_index, nullptr, d->d_coeffs, d->d_rec,
-                            d->d_rec_index, d->d_nrec, d->d_status);
+    int s = qf_decode_batch(d->ctx, &sh, 1, d->d_rows, d->d_index, nullptr, cauchy ? nullptr : d->d_coeffs,
+                            d->d_rec, d->d_rec_index, d->d_nrec, d->d_status);
     if (s != QF_OK) return s;
     int32_t status = 0;
     uint32_t nrec = 0;
