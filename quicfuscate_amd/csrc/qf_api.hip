@@ -389,6 +389,106 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     return QF_OK;
 }
 
+// Decode of Cauchy codes with more repairs than a syndrome kernel holds
+// (r <= 64, e <= 64) when the encode kernels of (k, r) exist:
+//   k_decode_prepare_cauchy  acceptance, slot map, D = C[J,E]^-1 (closed form)
+//   k_gather_sources         x' = accepted sources in order, erased ones zero
+//   qf_cauchy_bs_k*_r*       C x' = C[., S] x_S                (bit-sliced)
+//   k_xor_repairs            s_J = p_J ^ C[J, S] x_S
+//   k_combine_slots          x_E = D s_J, passes of 16 outputs
+int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                      const uint16_t* row_index, const uint32_t* n_rows, uint8_t* rec,
+                      uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    const uint32_t k = sh->k, r = sh->r, L = sh->L;
+    const uint32_t e_max = std::min(k, r), passes = (e_max + 15) / 16;
+    const uint32_t ms = (uint32_t)round_up(k + r, 16);
+    const uint64_t cgs = (uint64_t)(r + 1) * 16;
+    const uint64_t Lp = 16ull * qf::bs_padded_units(L);  // zero-tail encode rows
+    const uint32_t Lu = (L + 15) / 16;
+    // generations per chunk: gathered sources + syndromes of about 1 GiB
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(G, (1ull << 30) / ((uint64_t)(k + r) * Lp)));
+    const size_t off_bound = round_up((size_t)passes * G * cgs, 256);
+    const size_t off_map = round_up(off_bound + (size_t)G * 4, 256);
+    const size_t off_x = round_up(off_map + (size_t)G * ms, 256);
+    const size_t off_syn = round_up(off_x + (size_t)chunk * k * Lp, 256);
+    int s = grow_work(ctx, off_syn + (size_t)chunk * r * Lp);
+    if (s) return s;
+    uint8_t* w = ctx->d_work;
+    uint32_t* d_bound = reinterpret_cast<uint32_t*>(w + off_bound);
+    hipStream_t st = ctx->stream;
+    qf::PrepareCauchyArgs pa{};
+    pa.row_index = row_index;
+    pa.n_rows = n_rows;
+    pa.explog = ctx->d_explog;
+    pa.coef_out = w;
+    pa.smap = w + off_map;
+    pa.n_out = n_rec;
+    pa.bound = d_bound;
+    pa.rec_index = rec_index;
+    pa.status = status;
+    pa.k = k;
+    pa.r = r;
+    pa.e_max = e_max;
+    pa.max_rows = sh->max_rows;
+    pa.map_stride = ms;
+    pa.G = G;
+    hipEvent_t ev = prof_begin(ctx, st);
+    QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
+    prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
+    const int PD = pick_PD("QF_DECODE_PD", 1, 1);
+    for (uint64_t g0 = 0; g0 < G; g0 += chunk) {
+        const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
+        qf::GatherArgs ga{};
+        ga.rows = rows + g0 * sh->rows_gen_stride;
+        ga.rows_gen_stride = sh->rows_gen_stride;
+        ga.row_stride = sh->row_stride;
+        ga.smap = w + off_map + g0 * ms;
+        ga.map_stride = ms;
+        ga.out = w + off_x;
+        ga.out_gen_stride = (uint64_t)k * Lp;
+        ga.out_row_stride = Lp;
+        ga.k = k;
+        ga.r = r;
+        ga.Lu = Lu;
+        ga.G = Gc;
+        ev = prof_begin(ctx, st);
+        QF_CHECK_HIP(qf::launch_gather_sources(ga, ctx->num_cus, st));
+        prof_end(ctx, st, ev, "k_gather_sources");
+        ev = prof_begin(ctx, st);
+        QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, w + off_x, w + off_syn, (uint64_t)k * Lp,
+                                   (uint64_t)r * Lp, Lp, Lp, L, Gc, true));
+        prof_end(ctx, st, ev, qf::bs_name(k, r));
+        ga.out = w + off_syn;
+        ga.out_gen_stride = (uint64_t)r * Lp;
+        ev = prof_begin(ctx, st);
+        QF_CHECK_HIP(qf::launch_xor_repairs(ga, ctx->num_cus, st));
+        prof_end(ctx, st, ev, "k_xor_repairs");
+        for (uint32_t p = 0; p < passes; ++p) {
+            qf::CombineSlotsArgs a{};
+            a.rows = w + off_syn;
+            a.rows_gen_stride = (uint64_t)r * Lp;
+            a.row_stride = Lp;
+            a.dst = rec + g0 * sh->rec_gen_stride + (uint64_t)p * 16 * sh->rec_row_stride;
+            a.dst_gen_stride = sh->rec_gen_stride;
+            a.dst_row_stride = sh->rec_row_stride;
+            a.coef = w + ((uint64_t)p * G + g0) * cgs;
+            a.coef_gen_stride = cgs;
+            a.n_out = n_rec + g0;
+            a.bound = d_bound + g0;
+            a.tab256 = ctx->d_tab256;
+            a.pass = p;
+            a.L = L;
+            a.Lu = Lu;
+            a.zero_slot = r;
+            a.total_units = (uint64_t)Gc * Lu;
+            ev = prof_begin(ctx, st);
+            QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
+            prof_end(ctx, st, ev, "k_combine_slots<" + std::to_string(PD) + ">");
+        }
+    }
+    return QF_OK;
+}
+
 // Decode of the reference's Cauchy code by syndromes (no row_coeffs):
 //   k_decode_prepare_cauchy  acceptance, slot map, D = C[J,E]^-1 (closed form)
 //   qf_cauchy_syn_k*_r*      s_j = p_j ^ sum_{i present} C[j][i] x_i  (bit-sliced)
@@ -839,6 +939,12 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
             return decode_fused(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
     }
+    // codes without a syndrome kernel but with encode kernels (C5 Medium
+    // windows: r up to 64): syndromes through the encode kernels
+    if (!row_coeffs && !(nobs && atoi(nobs)) && !qf::syn_available(k, r) && qf::bs_available(k, r) && r <= 64 &&
+        e_max <= 64 && k + r <= 256 && max_rows <= 255 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
+        sh->row_stride < (1ull << 32) && (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31))
+        return decode_cauchy_enc(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
     const uint32_t passes = (e_max + 15) / 16;
     const uint64_t coef_gen_stride = ((uint64_t)max_rows + 1) * 16;
     const size_t coef_bytes = (size_t)std::max<uint32_t>(passes, 1) * G * coef_gen_stride;

@@ -79,7 +79,7 @@ struct PrepareCauchyArgs {
     const uint16_t* row_index;
     const uint32_t* n_rows;
     const uint8_t* explog;
-    uint8_t* coef_out;      // [G][(r + 1) * 16]
+    uint8_t* coef_out;      // [pass][G][(r + 1) * 16], passes of 16 outputs (e_max <= 64)
     uint8_t* smap;          // [G][map_stride]: k source slots, r repair slots, 0xFF absent
     uint32_t* n_out;
     uint32_t* bound;
@@ -97,6 +97,22 @@ struct PrepareCauchyArgs {
     uint32_t lu_stride;
 };
 hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st);
+
+// Syndromes of codes without a syndrome kernel: gather the accepted sources
+// (zero rows for erased ones) in source order, encode them with the
+// bit-sliced encode kernels, XOR the accepted repair rows in.  Rows are read
+// in whole 16-B units (Lu = ceil(L / 16)).
+struct GatherArgs {
+    const uint8_t* rows;   // received rows
+    uint64_t rows_gen_stride, row_stride;
+    const uint8_t* smap;   // [G][map_stride]: k source slots, r repair slots
+    uint32_t map_stride;
+    uint8_t* out;          // gather: sources [G][k]; xor: syndromes [G][r]
+    uint64_t out_gen_stride, out_row_stride;
+    uint32_t k, r, Lu, G;
+};
+hipError_t launch_gather_sources(const GatherArgs& a, int num_cus, hipStream_t st);
+hipError_t launch_xor_repairs(const GatherArgs& a, int num_cus, hipStream_t st);
 
 // PD: prefetch depth in row pairs (V=1: 1..3, V=2: 1..2); k_pad must be a
 // multiple of 2*(PD+1).

@@ -690,7 +690,9 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
     __shared__ uint32_t rep_cnt[256];
     __shared__ uint8_t J[256], Eidx[256];
     __shared__ uint32_t lA[256], lB[256], lE[256], lF[256];
-    __shared__ __attribute__((aligned(16))) uint8_t rec[17 * 16];
+    // D = C[J,E]^-1 by repair index: row j holds D[b][.] for outputs b < 64
+    // (r <= 64, e <= 64), written out as 16-output pass records
+    __shared__ __attribute__((aligned(16))) uint8_t rec[65 * 64];
     const uint32_t g = blockIdx.x;
     const uint32_t lane = threadIdx.x;
     const uint32_t k = a.k, r = a.r;
@@ -704,7 +706,7 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
         rep_slot[i] = 0xFF;
         rep_cnt[i] = 0;
     }
-    for (uint32_t i = lane; i < 17 * 16; i += 64) rec[i] = 0;
+    for (uint32_t i = lane; i < 65 * 64; i += 64) rec[i] = 0;
     __syncthreads();
     const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
     const uint16_t* ridx = a.row_index + (uint64_t)g * a.max_rows;
@@ -788,17 +790,21 @@ __global__ void __launch_bounds__(64) k_decode_prepare_cauchy(PrepareCauchyArgs 
             const uint32_t num = lA[q] + lB[b];
             const uint32_t den = slog[X ^ Y] + lE[q] + lF[b];  // < 3 * 255
             const uint32_t l = (num + 3 * 255 - den) % 255;
-            rec[J[q] * 16 + b] = sexp[l];
+            rec[J[q] * 64 + b] = sexp[l];
         }
         __syncthreads();
     }
     const bool ok = status == 0;
-    // stage-B records: slot j < r = syndrome of repair j, slot r = zero
-    uint8_t* co = a.coef_out + (uint64_t)g * (r + 1) * 16;
-    for (uint32_t j = lane; j <= r; j += 64) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (ok && j < r) v = *reinterpret_cast<const uint4*>(rec + j * 16);
-        *reinterpret_cast<uint4*>(co + j * 16) = v;
+    // stage-B records, one set per pass of 16 outputs (pass-major over the
+    // batch): slot j < r = syndrome of repair j, slot r = zero
+    const uint32_t passes = (a.e_max + 15) / 16;
+    for (uint32_t p = 0; p < passes; ++p) {
+        uint8_t* co = a.coef_out + ((uint64_t)p * a.G + g) * (r + 1) * 16;
+        for (uint32_t j = lane; j <= r; j += 64) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (ok && j < r) v = *reinterpret_cast<const uint4*>(rec + j * 64 + 16 * p);
+            *reinterpret_cast<uint4*>(co + j * 16) = v;
+        }
     }
     // slot map for the syndrome kernel (all absent when the generation fails)
     uint8_t* sm = a.smap + (uint64_t)g * a.map_stride;
@@ -1189,9 +1195,69 @@ hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Syndromes through the encode kernels (codes with more repairs than a
+// syndrome kernel holds): the accepted systematic rows of each generation in
+// source order, erased sources zero (k_gather_sources); the bit-sliced encode
+// of that gives C x' = C[., S] x_S; XOR the accepted repair rows in
+// (k_xor_repairs): s_J = p_J ^ C[J, S] x_S.
+__global__ void __launch_bounds__(256) k_gather_sources(GatherArgs a) {
+    const uint64_t total = (uint64_t)a.G * a.k * a.Lu;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = f / a.Lu;
+        const uint32_t u = (uint32_t)(f - t * a.Lu);
+        const uint64_t g = t / a.k;
+        const uint32_t i = (uint32_t)(t - g * a.k);
+        const uint32_t slot = a.smap[g * a.map_stride + i];
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (slot != 0xFF) v = *reinterpret_cast<const uint4*>(a.rows + g * a.rows_gen_stride + slot * a.row_stride + 16ull * u);
+        *reinterpret_cast<uint4*>(a.out + g * a.out_gen_stride + i * a.out_row_stride + 16ull * u) = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_xor_repairs(GatherArgs a) {
+    const uint64_t total = (uint64_t)a.G * a.r * a.Lu;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = f / a.Lu;
+        const uint32_t u = (uint32_t)(f - t * a.Lu);
+        const uint64_t g = t / a.r;
+        const uint32_t j = (uint32_t)(t - g * a.r);
+        const uint32_t slot = a.smap[g * a.map_stride + a.k + j];
+        if (slot == 0xFF) continue;
+        const uint4 p = *reinterpret_cast<const uint4*>(a.rows + g * a.rows_gen_stride + slot * a.row_stride + 16ull * u);
+        uint4* s = reinterpret_cast<uint4*>(a.out + g * a.out_gen_stride + j * a.out_row_stride + 16ull * u);
+        uint4 v = *s;
+        v.x ^= p.x;
+        v.y ^= p.y;
+        v.z ^= p.z;
+        v.w ^= p.w;
+        *s = v;
+    }
+}
+
+hipError_t launch_gather_sources(const GatherArgs& a, int num_cus, hipStream_t st) {
+    const uint64_t total = (uint64_t)a.G * a.k * a.Lu;
+    if (!total) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, (uint64_t)num_cus * 16);
+    hipLaunchKernelGGL(k_gather_sources, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_xor_repairs(const GatherArgs& a, int num_cus, hipStream_t st) {
+    const uint64_t total = (uint64_t)a.G * a.r * a.Lu;
+    if (!total) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, (uint64_t)num_cus * 16);
+    hipLaunchKernelGGL(k_xor_repairs, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st) {
     if (a.G == 0) return hipSuccess;
-    if (a.r > 16 || a.k + a.r > 256 || a.max_rows > 255 || a.map_stride < a.k + a.r) return hipErrorInvalidValue;
+    // fused decode records: r <= 16; stage-B records: r <= 64 (e <= 64)
+    if (a.r > (a.lu_out ? 16u : 64u) || a.e_max > 64 || a.k + a.r > 256 || a.max_rows > 255 ||
+        a.map_stride < a.k + a.r)
+        return hipErrorInvalidValue;
     if (a.lu_out) {
         // one generation per wave (a persistent grid measured slower: the
         // kernel is LDS/VALU-issue-bound per CU, not launch-bound)

@@ -122,7 +122,10 @@ def _path(monkeypatch, path):
                                      (16, 1, 64, 40), (64, 16, 80, 50),
                                      # C5 shapes with generated kernels; 9000: partial last unit
                                      (32, 5, 1200, 30), (48, 8, 1200, 30), (96, 15, 1200, 20),
-                                     (96, 15, 9000, 4), (48, 8, 1000, 12)])
+                                     (96, 15, 9000, 4), (48, 8, 1000, 12),
+                                     # r > 16: syndromes through the encode kernels, passes of 16 outputs
+                                     (128, 20, 1200, 8), (128, 39, 1000, 6), (160, 48, 700, 4),
+                                     (196, 59, 9000, 2)])
 def test_decode_matches_oracle_random_erasures(qf, oracle, gpu_ctx, k, r, L, G, path, monkeypatch):
     _path(monkeypatch, path)
     rng = np.random.default_rng(k + r + L)
