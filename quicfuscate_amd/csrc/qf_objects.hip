@@ -11,6 +11,7 @@
 
 #include "gf256_tables.h"
 #include "qf_fec.h"
+#include "qf_bs.h"
 
 #define QF_CHECK_HIP(expr)                         \
     do {                                           \
@@ -270,7 +271,17 @@ static int decoder_try_decode(qf_decoder* d) {
     QF_CHECK_HIP(hipMemcpyAsync(d->d_index, idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
     qf_decode_shape sh{};
     sh.k = k;
-    sh.r = cauchy ? std::max<uint32_t>(rmax, 1) : emax;
+    uint32_t rc = std::max<uint32_t>(rmax, 1);
+    if (cauchy) {
+        // the Cauchy code of (k, r') holds rows 0..r'-1: take the smallest r'
+        // >= rmax with generated kernels, so the decode runs on them
+        for (uint32_t r2 = rc; r2 <= emax && k + r2 <= 256; ++r2)
+            if (qf::syn_available(k, r2) || qf::bs_available(k, r2)) {
+                rc = r2;
+                break;
+            }
+    }
+    sh.r = cauchy ? rc : emax;
     sh.L = L;
     sh.max_rows = k;
     sh.row_stride = d->stride;
