@@ -90,3 +90,46 @@ def test_gloo_world2_max_over_ranks():
     assert [(r, lo, hi) for r, lo, hi, _ in res] == [(0, 0, 500), (1, 500, 1000)]
     for _, _, _, out in res:
         assert np.allclose(out, [11.0, 6.0, 7.0, 1.0])
+
+
+def _halo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from quicfuscate_amd import stream_shard as ss
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        P, k, stride = 37, 8, 16
+        g = torch.arange(P * stride, dtype=torch.int64).view(P, stride).remainder(251).to(torch.uint8)
+        lo, hi = ss.packet_range(P, rank, world)
+        ext = ss.halo_exchange(torch, dist, g[lo:hi].clone(), k, rank, world)
+        first, nwin = ss.local_windows(lo, hi, k)
+        wins = [ext[t - lo: t - lo + k].clone() for t in range(first, first + nwin)]
+        ok = all(torch.equal(w, g[t - k + 1: t + 1]) for w, t in zip(wins, range(first, first + nwin)))
+        q.put((rank, lo, hi, first, nwin, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sliding_halo_exchange_gloo():
+    """Sliding-window sharding: after the k - 1 packet halo
+    from the previous rank, every rank's windows equal the global stream's,
+    and the ranks' windows together cover every window exactly once."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_halo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for *_, ok in res)
+    ends = [t for _, lo, hi, first, nwin, _ in res for t in range(first, first + nwin)]
+    assert ends == list(range(8 - 1, 37))
