@@ -519,26 +519,27 @@ QF_DEV void big_fail(const BigArgs& a, int32_t s) {
     *a.n_out = 0;
 }
 
-// exclusive prefix sum of one count per thread over a block of 1024
+// exclusive prefix sum of one count per thread over the block (power of two)
 QF_DEV uint32_t block_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, n = blockDim.x;
     sh[tid] = v;
     __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
+    for (uint32_t d = 1; d < n; d <<= 1) {
         const uint32_t x = tid >= d ? sh[tid - d] : 0;
         __syncthreads();
         sh[tid] += x;
         __syncthreads();
     }
     const uint32_t incl = sh[tid];
-    *total = sh[1023];
+    *total = sh[n - 1];
     __syncthreads();
     return incl - v;
 }
 
-// acceptance (decoder.rs:563-578) and the row lists; one block of 1024,
-// thread t owns slots / columns [4t, 4t + 4) (k <= 4096), lists compacted in
-// order with block scans
+// acceptance (decoder.rs:563-578) and the row lists; one block per
+// generation of a power of two >= k / 4 threads (64..1024), thread t owns
+// slots / columns [4t, 4t + 4) (k <= 4096), lists compacted in order with
+// block scans
 __global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs A) {
     const BigArgs a = view(A, blockIdx.z);
     __shared__ __align__(4) uint8_t present[4096];
@@ -658,7 +659,7 @@ __global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs A) {
     sp[threadIdx.x] = lp;
     __syncthreads();
     if (zero) s_zero = 1;
-    for (uint32_t d = 128; d; d >>= 1) {
+    for (uint32_t d = blockDim.x / 2; d; d >>= 1) {   // blockDim: power of two, 64..256
         if (threadIdx.x < d) {
             sq[threadIdx.x] += sq[threadIdx.x + d];
             sp[threadIdx.x] += sp[threadIdx.x + d];
@@ -1039,10 +1040,14 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         b.rec_index = rec_index + (size_t)g0 * e_max;
         b.status = status + g0;
         hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-        hipLaunchKernelGGL(k_dec16_accept, dim3(1, 1, gc), dim3(1024), 0, st, b);
+        uint32_t acc_threads = 64;
+        while (acc_threads * 4 < k) acc_threads <<= 1;
+        hipLaunchKernelGGL(k_dec16_accept, dim3(1, 1, gc), dim3(acc_threads), 0, st, b);
         hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid, 1, gc), dim3(256), 0, st, b);
         if (!row_coeffs) {
-            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max, 1, gc), dim3(256), 0, st, b);
+            uint32_t prod_threads = 64;
+            while (prod_threads < e_max && prod_threads < 256) prod_threads <<= 1;
+            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max, 1, gc), dim3(prod_threads), 0, st, b);
             hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid, 1, gc), dim3(256), 0, st, b);
         } else {
             hipLaunchKernelGGL(k_dec16_gj_init,
