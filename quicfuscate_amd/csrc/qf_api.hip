@@ -831,7 +831,9 @@ int qf_gf256_mul_slice_dev(qf_ctx* ctx, const uint8_t* a, const uint8_t* b, uint
     int s = ensure_device(ctx);
     if (s) return s;
     if (!aligned16(a) || !aligned16(b) || !aligned16(out)) return QF_EINVAL;
+    hipEvent_t ev = prof_begin(ctx, ctx->stream);
     QF_CHECK_HIP(qf::launch_mul_slice(a, b, out, n, ctx->d_explog, ctx->num_cus, ctx->stream));
+    prof_end(ctx, ctx->stream, ev, "k_mul_slice");
     return QF_OK;
 }
 

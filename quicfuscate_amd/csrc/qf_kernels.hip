@@ -1073,6 +1073,55 @@ __global__ void __launch_bounds__(256) k_mul_slice(const uint8_t* __restrict__ a
     }
 }
 
+// Large slices: the whole 64 KiB product table T[a * 256 + b] in LDS (built
+// per block from exp/log), one LDS byte read per product and no branches;
+// index pairs are formed two at a time with v_perm.  Persistent grid.
+__global__ void __launch_bounds__(1024) k_mul_slice_tab(const uint8_t* __restrict__ a,
+                                                        const uint8_t* __restrict__ b,
+                                                        uint8_t* __restrict__ out, uint64_t n,
+                                                        const uint8_t* __restrict__ explog) {
+    __shared__ uint8_t sexp[512];
+    __shared__ uint8_t slog[256];
+    __shared__ __attribute__((aligned(16))) uint8_t tab[65536];
+    for (uint32_t i = threadIdx.x; i < 768; i += blockDim.x) {
+        if (i < 512) sexp[i] = explog[i];
+        else slog[i - 512] = explog[i];
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < 65536 / 4; w += blockDim.x) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t t = 4 * w + q, xa = t >> 8, yb = t & 0xFF;
+            const uint32_t p = (xa && yb) ? sexp[(uint32_t)slog[xa] + slog[yb]] : 0u;
+            v |= p << (8 * q);
+        }
+        reinterpret_cast<uint32_t*>(tab)[w] = v;
+    }
+    __syncthreads();
+    const uint64_t nvec = n / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nvec; w += stride) {
+        const uint4 va = reinterpret_cast<const uint4*>(a)[w];
+        const uint4 vb = reinterpret_cast<const uint4*>(b)[w];
+        uint4 r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t x = comp(va, c), y = comp(vb, c);
+            // indices (a_q << 8 | b_q) for bytes 0,1 and 2,3 of the dword
+            const uint32_t i01 = vperm(x, y, 0x05010400u);  // bytes: b0 a0 b1 a1
+            const uint32_t i23 = vperm(x, y, 0x07030602u);  // bytes: b2 a2 b3 a3
+            const uint32_t p0 = tab[i01 & 0xFFFF], p1 = tab[i01 >> 16];
+            const uint32_t p2 = tab[i23 & 0xFFFF], p3 = tab[i23 >> 16];
+            set_comp(r, c, p0 | (p1 << 8) | (p2 << 16) | (p3 << 24));
+        }
+        reinterpret_cast<uint4*>(out)[w] = r;
+    }
+    const uint64_t t0 = nvec * 16;
+    for (uint64_t t = t0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride)
+        out[t] = tab[(uint32_t)a[t] << 8 | b[t]];
+}
+
 QF_DEV uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1275,6 +1324,12 @@ hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, ui
     if (blocks < 1) blocks = 1;
     const uint64_t cap = (uint64_t)num_cus * 8;
     if (blocks > cap) blocks = cap;
+    // from 16 MiB the table kernel (one LDS read per product) wins; below, the
+    // 64 KiB per-block table build is not amortised
+    if (n >= (16u << 20)) {
+        hipLaunchKernelGGL(k_mul_slice_tab, dim3((uint32_t)num_cus), dim3(1024), 0, st, a, b, out, n, explog);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_mul_slice, dim3((uint32_t)blocks), dim3(256), 0, st, a, b, out, n, explog);
     return hipGetLastError();
 }

@@ -220,3 +220,24 @@ def test_bit_sliced_partial_last_unit_random_lengths(qf, oracle, gpu_ctx, k, r):
                 assert (rep[off: off + L] == want[j]).all(), (L, g, j)
                 assert (rep[off + L: off + tail] == 0).all(), (L, g, j)
                 assert (rep[off + tail: off + rrs] == 0xA5).all(), (L, g, j)
+
+
+def test_gf_mul_slice_large_table_kernel(qf, oracle, gpu_ctx):
+    """Slices from 16 MiB use the 64 KiB product-table kernel: every byte
+    (and the n % 16 tail) equals gf_mul_table (gf_tables.rs:47-57)."""
+    import torch
+
+    from quicfuscate_amd import _lib as L
+
+    n = (16 << 20) + 7
+    a = torch.randint(0, 256, (n + 9,), dtype=torch.uint8, device="cuda")[:n]
+    b = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    out = torch.empty(n + 16, dtype=torch.uint8, device="cuda").fill_(0xA5)
+    torch.cuda.synchronize()
+    ctx = qf.default_context()
+    L.check(L._lib().qf_gf256_mul_slice_dev(ctx.handle, a.data_ptr(), b.data_ptr(), out.data_ptr(), n), "slice")
+    ctx.sync()
+    tab = torch.from_numpy(oracle.mul_table_full().reshape(-1)).cuda()
+    want = tab[a.long() * 256 + b.long()]
+    assert torch.equal(out[:n], want)
+    assert (out[n:] == 0xA5).all()
