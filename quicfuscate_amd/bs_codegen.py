@@ -160,6 +160,11 @@ _ASM = {
     "s_waitcnt_lgkm": lambda: "s_waitcnt lgkmcnt(0)",
     "s_nop": lambda n: f"s_nop {n}",
     "s_setprio": lambda n: f"s_setprio {n}",
+    # workgroups lo <= s2 < lo + width sleep iters x 127 x 64 cycles (s46/s47 scratch)
+    "s_stagger": lambda lo, width, iters: (f"s_sub_u32 s46, s2, {lo}\n\ts_cmp_lt_u32 s46, {width}\n"
+                                           f"\ts_cbranch_scc0 .Lstag_end\n\ts_mov_b32 s47, {iters}\n.Lstag:\n"
+                                           f"\ts_sleep 127\n\ts_sub_u32 s47, s47, 1\n\ts_cmp_lg_u32 s47, 0\n"
+                                           f"\ts_cbranch_scc1 .Lstag\n.Lstag_end:"),
     "s_load_args": lambda: "s_load_dwordx16 s[4:19], s[0:1], 0x0\n\ts_load_dwordx4 s[20:23], s[0:1], 0x40",
     "s_load_args_dec": lambda: "s_load_dwordx8 s[56:63], s[0:1], 0x50",
     "v_perm": lambda d, hi, lo, sel: f"v_perm_b32 {V(d)}, {V(hi)}, {V(lo)}, {V(sel)}",
@@ -280,6 +285,10 @@ class KernelSpec:
     lu: bool = True
     # dec mode: wave priority (s_setprio) of the row loop / the LU phase
     prio: tuple = (0, 0)
+    # (lo, width, iters): workgroups lo..lo+width-1 sleep about iters x 8 k cycles
+    # before their first item, so co-resident waves run their memory (row loop) and
+    # compute (LU) phases out of step instead of in lock-step
+    stagger: tuple = ()
     # lab only: drop the payload row loads (keeps maps, records, compute)
     lab_norows: bool = False
     # enc mode, one pass of a code with more repairs than a kernel holds:
@@ -513,6 +522,8 @@ def _prologue(E, spec: KernelSpec):
         for q in range(8):
             E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * LDS_TAB_STRIDE * q)))
         E(Op("s_waitcnt_lgkm_n", (0,)))
+    if spec.stagger:
+        E(Op("s_stagger", tuple(spec.stagger)))
     if spec.xcd_remap:
         # w' = base(w % 8) + w / 8 with XCD x owning c_x = q + (x < rem)
         # consecutive workgroups, q = nwg / 8, rem = nwg % 8 (a bijection)
@@ -1233,7 +1244,7 @@ class Emulator:
             pc += 1
             steps += 1
             n, a = op.name, op.args
-            if n == "label" or n == "s_nop" or n == "s_waitcnt_lgkm" or n == "s_setprio":
+            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger"):
                 continue
             if n == "s_load_args":
                 for q in range(20):

@@ -32,6 +32,18 @@ VARIANTS = [
     ("norows", {"lab_norows": True}, ()),
     ("nolu_norows", {"lu": False, "lab_norows": True}, ()),
     ("full_2", {}, ()),
+    # deeper row ring (pd 4 = 256 VGPRs, still 2 waves per SIMD) and wave priorities
+    ("pd4", {"pd": 4}, ()),
+    ("pd4_nolu", {"pd": 4, "lu": False}, ()),
+    ("prio_rows", {"prio": (1, 0)}, ()),
+    ("prio_lu", {"prio": (0, 1)}, ()),
+    ("pd4_prio_rows", {"pd": 4, "prio": (1, 0)}, ()),
+    ("pd2", {"pd": 2}, ()),
+    # second residency round (workgroups 256..511) starts ~iters x 3.4 us late
+    ("stag6", {"stagger": (256, 256, 6)}, ()),
+    ("stag12", {"stagger": (256, 256, 12)}, ()),
+    ("stag18", {"stagger": (256, 256, 18)}, ()),
+    ("stag12_all", {"stagger": (256, 1 << 30, 12)}, ()),
 ]
 
 
