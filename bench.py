@@ -103,6 +103,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-sample", type=int, default=4096, help="generations in the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-path-G", type=int, default=16384, help="generations for the pinned-host encode rate (0=skip)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the step's encode and decode (independent batches) on two HIP streams")
     return ap.parse_args(argv)
 
 
@@ -175,41 +177,69 @@ def main(argv=None):
     dec_args = dict(max_rows=n_slots, row_stride=Lb, rows_gen_stride=n_slots * Lb, rec_row_stride=Lb,
                     rec_gen_stride=emax * Lb, G=G)
 
+    # --overlap: the step's encode and decode work on different buffers (the
+    # decode reads `rows`, built before timing; the encode writes `rep`), so
+    # they can run on two streams forked from and joined back into `stream`:
+    # the HBM-bound encode and the VALU-bound decode then share the CUs.
+    if args.overlap:
+        s_enc, s_dec = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        ctx_enc, ctx_dec = fec.Context(local, s_enc.cuda_stream), fec.Context(local, s_dec.cuda_stream)
+    else:
+        s_enc = s_dec = stream
+        ctx_enc = ctx_dec = ctx
+    ctxs = [ctx_enc] if ctx_enc is ctx_dec else [ctx_enc, ctx_dec]
+
     def encode():
-        fec.encode_batch(src, rep, k, r, Lb, ctx=ctx, **enc_args)
+        fec.encode_batch(src, rep, k, r, Lb, ctx=ctx_enc, **enc_args)
 
     def decode():
-        fec.decode_batch(rows, row_index, rec, rec_index, n_rec, status, k, r, Lb, ctx=ctx, **dec_args)
+        fec.decode_batch(rows, row_index, rec, rec_index, n_rec, status, k, r, Lb, ctx=ctx_dec, **dec_args)
+
+    def step(e0, e_enc, e_dec, e1):
+        e0.record(stream)
+        if args.overlap:
+            s_enc.wait_event(e0)
+            s_dec.wait_event(e0)
+        encode()
+        e_enc.record(s_enc)
+        decode()
+        e_dec.record(s_dec)
+        if args.overlap:
+            stream.wait_event(e_enc)
+            stream.wait_event(e_dec)
+        e1.record(stream)
+
+    def events():
+        return tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
 
     for _ in range(args.warmup):
-        encode()
-        decode()
+        step(*events())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    ctx.profile(True)  # per-kernel HIP events on the launch stream
+    ev = [events() for _ in range(args.steps)]
+    for c in ctxs:
+        c.profile(True)  # per-kernel HIP events on each launch stream
     t0 = time.perf_counter()
     for s in range(args.steps):
-        ev[s][0].record(stream)
-        encode()
-        ev[s][1].record(stream)
-        decode()
-        ev[s][2].record(stream)
+        step(*ev[s])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ktimes = ctx.kernel_times()
-    ctx.profile(False)
+    ktimes = {}
+    for c in ctxs:
+        ktimes.update(c.kernel_times())
+        c.profile(False)
     kern_ms = {n: ms / max(1, cnt) for n, (cnt, ms) in ktimes.items()}  # per launch
     kern_step_ms = {n: ms / args.steps for n, (cnt, ms) in ktimes.items()}
-    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    # encode: step start -> encode done; decode: encode done (serial) or step
+    # start (overlap) -> decode done
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
+    dec_ms = float(np.mean([(a if args.overlap else b).elapsed_time(c) for a, b, c, _ in ev]))
     step_ms = wall * 1e3 / args.steps
 
     # --- verification (size-independent round trip on the device) ---------
@@ -324,6 +354,7 @@ def main(argv=None):
         "roofline": roofline(dom),
         # the encode kernel BASELINE.json's north star targets (>= 70 % HBM)
         "roofline_encode": roofline(enc_kernel) if enc_kernel else None,
+        "streams": "encode || decode (2 HIP streams)" if args.overlap else "encode then decode (1 stream)",
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,
         "repair_xor_fold_by_rank": [f"{f:016x}" for f in folds],
@@ -342,6 +373,9 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if args.overlap:
+        ctx_enc.close()
+        ctx_dec.close()
     ctx.close()
 
 
