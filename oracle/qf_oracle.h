@@ -110,6 +110,12 @@ int cpu_encode_table(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8
 int cpu_encode_avx2(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
                     uint8_t *rep, uint32_t threads);
 int cpu_has_avx2(void);
+int cpu_encode_gfni(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
+                    uint8_t *rep, uint32_t threads);
+int cpu_encode_clmul(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
+                     uint8_t *rep, uint32_t threads);
+int cpu_has_gfni(void);
+int cpu_has_pclmul(void);
 
 /* ---- GF(2^16) Extreme mode (qf_oracle16.c) ----------------------------- */
 uint16_t oracle_gf16_mul(uint16_t a, uint16_t b);

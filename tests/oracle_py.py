@@ -18,6 +18,10 @@ _SZ = ctypes.c_size_t
 _lib.cpu_encode_table.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
 _lib.cpu_encode_avx2.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
 _lib.cpu_has_avx2.argtypes = []
+_lib.cpu_encode_gfni.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
+_lib.cpu_encode_clmul.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
+_lib.cpu_has_gfni.argtypes = []
+_lib.cpu_has_pclmul.argtypes = []
 _lib.oracle_gf_mul.restype = ctypes.c_uint8
 _lib.oracle_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
 _lib.oracle_gf_mul_shift.restype = ctypes.c_uint8
@@ -95,11 +99,14 @@ def encode(src: np.ndarray, r: int, coeff: np.ndarray | None = None, L: int | No
 
 def cpu_encode(kind: str, src: np.ndarray, r: int, threads: int = 1) -> np.ndarray:
     """Comparison encoders of oracle/cpu_variants.c over dense generations:
-    src (G, k, L) -> (G, r, L).  kind: "table" or "avx2"."""
+    src (G, k, L) -> (G, r, L).  kind: "table", "avx2", "gfni" or "clmul"
+    (the reference's as-written per-byte PCLMULQDQ fold: timing only, its
+    output is the defective fold product)."""
     src = np.ascontiguousarray(src, dtype=np.uint8)
     G, k, L = src.shape
     rep = np.zeros((G, r, L), np.uint8)
-    fn = _lib.cpu_encode_table if kind == "table" else _lib.cpu_encode_avx2
+    fn = {"table": _lib.cpu_encode_table, "avx2": _lib.cpu_encode_avx2, "gfni": _lib.cpu_encode_gfni,
+          "clmul": _lib.cpu_encode_clmul}[kind]
     s = fn(k, r, L, G, _p(src), _p(rep), threads)
     if s != 0:
         raise ValueError(f"cpu_encode({kind}) status {s}")
@@ -108,6 +115,12 @@ def cpu_encode(kind: str, src: np.ndarray, r: int, threads: int = 1) -> np.ndarr
 
 def has_avx2() -> bool:
     return bool(_lib.cpu_has_avx2())
+
+
+def has_cpu_kind(kind: str) -> bool:
+    """Whether this host can run cpu_encode(kind)."""
+    return {"table": lambda: True, "avx2": _lib.cpu_has_avx2, "gfni": _lib.cpu_has_gfni,
+            "clmul": _lib.cpu_has_pclmul}[kind]() != 0
 
 
 def encode_clmul_fold(src: np.ndarray, r: int) -> np.ndarray:

@@ -135,13 +135,30 @@ def test_splitmix_golden(oracle):
     assert (a[40:100] == b).all()
 
 
-@pytest.mark.parametrize("kind", ["table", "avx2"])
-@pytest.mark.parametrize("k,r,L,G,threads", [(64, 16, 1200, 5, 3), (7, 5, 33, 4, 2), (16, 1, 31, 3, 1)])
+@pytest.mark.parametrize("kind", ["table", "avx2", "gfni"])
+@pytest.mark.parametrize("k,r,L,G,threads", [(64, 16, 1200, 5, 3), (7, 5, 33, 4, 2), (16, 1, 31, 3, 1),
+                                             (5, 3, 64, 2, 1), (9, 4, 129, 2, 2)])
 def test_cpu_comparison_encoders_match_oracle(oracle, kind, k, r, L, G, threads):
-    if kind == "avx2" and not oracle.has_avx2():
-        pytest.skip("no AVX2 on this host")
+    if not oracle.has_cpu_kind(kind):
+        pytest.skip(f"no {kind} on this host")
     rng = np.random.default_rng(k + L)
     src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
     got = oracle.cpu_encode(kind, src, r, threads)
     for g in range(G):
         assert (got[g] == oracle.encode(src[g], r)).all()
+
+
+def test_cpu_clmul_as_written_is_the_defective_fold(oracle):
+    """cpu_encode("clmul") restates the reference's per-byte PCLMULQDQ path
+    (gf_tables.rs:129-141 inside decoder.rs:228-259) for timing; its output
+    must equal the same loop over the restated fold (oracle_gf_mul_clmul_fold),
+    and differ from the correct table encode."""
+    if not oracle.has_cpu_kind("clmul"):
+        pytest.skip("no PCLMULQDQ on this host")
+    k, r, L = 16, 4, 37
+    rng = np.random.default_rng(3)
+    src = rng.integers(0, 256, (2, k, L), dtype=np.uint8)
+    got = oracle.cpu_encode("clmul", src, r, 2)
+    for g in range(2):
+        assert (got[g] == oracle.encode_clmul_fold(src[g], r)).all()
+    assert not (got[0] == oracle.encode(src[0], r)).all()
