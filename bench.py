@@ -105,6 +105,8 @@ def parse(argv=None):
     ap.add_argument("--host-path-G", type=int, default=16384, help="generations for the pinned-host encode rate (0=skip)")
     ap.add_argument("--overlap", action="store_true",
                     help="run the step's encode and decode (independent batches) on two HIP streams")
+    ap.add_argument("--split", action="store_true",
+                    help="decode acceptance pass on a 2nd stream beside the encode, payload pass after it")
     return ap.parse_args(argv)
 
 
@@ -181,9 +183,17 @@ def main(argv=None):
     # decode reads `rows`, built before timing; the encode writes `rep`), so
     # they can run on two streams forked from and joined back into `stream`:
     # the HBM-bound encode and the VALU-bound decode then share the CUs.
+    #
+    # --split: the encode stays on `stream`; the decode's acceptance pass
+    # (row indices only) runs on a second stream beside the encode, and its
+    # payload pass waits for the encode (qf_ctx_set_payload_wait), so the two
+    # heavy kernels still run one after the other.
     if args.overlap:
         s_enc, s_dec = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
         ctx_enc, ctx_dec = fec.Context(local, s_enc.cuda_stream), fec.Context(local, s_dec.cuda_stream)
+    elif args.split:
+        s_enc, s_dec = stream, torch.cuda.Stream(dev)
+        ctx_enc, ctx_dec = ctx, fec.Context(local, s_dec.cuda_stream)
     else:
         s_enc = s_dec = stream
         ctx_enc = ctx_dec = ctx
@@ -200,12 +210,18 @@ def main(argv=None):
         if args.overlap:
             s_enc.wait_event(e0)
             s_dec.wait_event(e0)
+        if args.split:
+            s_dec.wait_event(e0)
         encode()
         e_enc.record(s_enc)
+        if args.split:
+            ctx_dec.set_payload_wait(e_enc)
         decode()
         e_dec.record(s_dec)
         if args.overlap:
             stream.wait_event(e_enc)
+            stream.wait_event(e_dec)
+        if args.split:
             stream.wait_event(e_dec)
         e1.record(stream)
 
@@ -354,7 +370,9 @@ def main(argv=None):
         "roofline": roofline(dom),
         # the encode kernel BASELINE.json's north star targets (>= 70 % HBM)
         "roofline_encode": roofline(enc_kernel) if enc_kernel else None,
-        "streams": "encode || decode (2 HIP streams)" if args.overlap else "encode then decode (1 stream)",
+        "streams": ("encode || decode (2 HIP streams)" if args.overlap else
+                    "encode, then decode payload pass; decode acceptance pass on a 2nd stream beside the encode"
+                    if args.split else "encode then decode (1 stream)"),
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,
         "repair_xor_fold_by_rank": [f"{f:016x}" for f in folds],
@@ -376,6 +394,8 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if args.split:
+        ctx_dec.close()
     if args.overlap:
         ctx_enc.close()
         ctx_dec.close()

@@ -70,6 +70,16 @@ int qf_ctx_create(int device, void *stream, qf_ctx **out);
 int qf_ctx_destroy(qf_ctx *ctx);
 int qf_ctx_set_stream(qf_ctx *ctx, void *stream);
 void *qf_ctx_stream(qf_ctx *ctx);
+/* Split-phase decode.  The next qf_decode_batch on ctx enqueues its
+ * acceptance pass (row indices only: first k rows win, slot map, LU/inverse
+ * records -- the bookkeeping the reference's Decoder::add_packet does on
+ * arrival, decoder.rs:678-701) at once, and makes its payload pass
+ * (Decoder::try_decode / gaussian_elimination, decoder.rs:720-783) wait for
+ * `event` (a hipEvent_t recorded on any stream, e.g. after the H2D copy of
+ * the rows).  The setting is cleared when that qf_decode_batch returns;
+ * NULL clears it.  No reference counterpart beyond the add_packet /
+ * try_decode split. */
+int qf_ctx_set_payload_wait(qf_ctx *ctx, void *event);
 int qf_sync(qf_ctx *ctx);
 
 /* Kernel timing (no reference counterpart; benches/ replacement).  While on,

@@ -87,6 +87,7 @@ _SIGS = {
     "qf_ctx_destroy": (_I, [_P]),
     "qf_ctx_set_stream": (_I, [_P, _P]),
     "qf_ctx_stream": (_P, [_P]),
+    "qf_ctx_set_payload_wait": (_I, [_P, _P]),
     "qf_sync": (_I, [_P]),
     "qf_ctx_profile": (_I, [_P, _I]),
     "qf_ctx_profile_read": (_I, [_P, _U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U32),

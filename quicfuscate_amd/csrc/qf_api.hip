@@ -59,6 +59,8 @@ struct qf_ctx {
     uint32_t* d_custom = nullptr;
     size_t custom_words = 0;
     hipEvent_t custom_done = nullptr;
+    // qf_ctx_set_payload_wait: event the next decode's payload pass waits for
+    hipEvent_t payload_wait = nullptr;
     // decode workspace
     uint8_t* d_work = nullptr;
     size_t work_bytes = 0;
@@ -333,6 +335,15 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
 //   k_decode_prepare_cauchy (lu_out)  acceptance, slot map, LU of C[J,E]
 //   qf_cauchy_dec_k*_r*               syndromes (bit-sliced), then the LU
 //                                     solve in registers, recovered rows out
+// Split-phase decode (qf_ctx_set_payload_wait): the acceptance pass needs the
+// row indices only, as the reference's add_packet bookkeeping runs at arrival
+// (decoder.rs:678-701); the payload pass (try_decode, decoder.rs:720-783)
+// waits for the caller's event, e.g. the H2D copy of the rows.
+int payload_gate(qf_ctx* ctx, hipStream_t st) {
+    if (ctx->payload_wait) QF_CHECK_HIP(hipStreamWaitEvent(st, ctx->payload_wait, 0));
+    return QF_OK;
+}
+
 // A device buffer of >= L zero bytes (read in place of absent rows).
 int ensure_zero(qf_ctx* ctx, uint32_t L) {
     if (ctx->zero_bytes >= L) return QF_OK;
@@ -378,9 +389,18 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     pa.G = G;
     pa.lu_out = w;
     pa.lu_stride = lu_stride;
+    if (ctx->payload_wait) {
+        // split phase: the acceptance pass runs beside the caller's other
+        // work, on a capped persistent grid (QF_PREPARE_GRID blocks, default
+        // one per two CUs: beside the C2 encode it then takes ~1 ms, under
+        // the encode, and slows it by ~2 %; 4 blocks per CU slowed it 10 %)
+        const char* pg = getenv("QF_PREPARE_GRID");
+        pa.grid_cap = pg ? (uint32_t)atoi(pg) : std::max<uint32_t>(1, (uint32_t)ctx->num_cus / 2);
+    }
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_lu");
+    if (int gs = payload_gate(ctx, st)) return gs;
     ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
@@ -435,6 +455,7 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
+    if (int gs = payload_gate(ctx, st)) return gs;
     const int PD = pick_PD("QF_DECODE_PD", 1, 1);
     for (uint64_t g0 = 0; g0 < G; g0 += chunk) {
         const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
@@ -558,6 +579,7 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
+    if (int gs = payload_gate(ctx, st)) return gs;
     const int PD = pick_PD("QF_DECODE_PD", 1, 1);
     const std::string slots_name = "k_combine_slots<" + std::to_string(PD) + ">";
     for (uint64_t c = 0; c < n_chunks; ++c) {
@@ -909,9 +931,30 @@ int qf_encode_batch_host(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, con
     return QF_OK;
 }
 
+static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                             const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
+                             uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status);
+
 int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
                     const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
                     uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    if (!ctx) return QF_EINVAL;
+    const int s = decode_batch_impl(ctx, sh, G, rows, row_index, n_rows, row_coeffs, rec, rec_index, n_rec, status);
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->payload_wait = nullptr;  // one decode call only, whatever its outcome
+    return s;
+}
+
+int qf_ctx_set_payload_wait(qf_ctx* ctx, void* event) {
+    if (!ctx) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->payload_wait = reinterpret_cast<hipEvent_t>(event);
+    return QF_OK;
+}
+
+static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                             const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
+                             uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
     if (!ctx || !sh) return QF_EINVAL;
     const uint32_t k = sh->k, r = sh->r, L = sh->L, max_rows = sh->max_rows;
     if (k == 0 || k > 256 || max_rows == 0 || max_rows > 4096 || L == 0) return QF_EINVAL;
@@ -978,6 +1021,7 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
     hipEvent_t ev = prof_begin(ctx, ctx->stream);
     QF_CHECK_HIP(qf::launch_decode_prepare(pa, ctx->stream));
     prof_end(ctx, ctx->stream, ev, "k_decode_prepare");
+    if (int gs = payload_gate(ctx, ctx->stream)) return gs;
     const uint32_t Lu = (L + 15) / 16;
     for (uint32_t p = 0; p < passes; ++p) {
         qf::CombineSlotsArgs a{};

@@ -95,6 +95,7 @@ struct PrepareCauchyArgs {
     // layout bs_codegen._lu_solve_and_store) instead of coef_out / bound
     uint8_t* lu_out;
     uint32_t lu_stride;
+    uint32_t grid_cap;   // k_decode_prepare_lu: max blocks (0 = one generation per wave)
 };
 hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st);
 

@@ -1310,7 +1310,10 @@ hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t 
     if (a.lu_out) {
         // one generation per wave (a persistent grid measured slower: the
         // kernel is LDS/VALU-issue-bound per CU, not launch-bound)
-        const uint32_t blocks = (a.G + kPrepWaves - 1) / kPrepWaves;
+        uint32_t blocks = (a.G + kPrepWaves - 1) / kPrepWaves;
+        // a capped persistent grid when the pass runs beside other work
+        // (split-phase decode): fewer CUs taken from the concurrent kernel
+        if (a.grid_cap && blocks > a.grid_cap) blocks = a.grid_cap;
         hipLaunchKernelGGL(k_decode_prepare_lu, dim3(blocks), dim3(64 * kPrepWaves), 0, st, a);
     } else {
         hipLaunchKernelGGL(k_decode_prepare_cauchy, dim3(a.G), dim3(64), 0, st, a);

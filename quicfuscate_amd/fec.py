@@ -81,6 +81,13 @@ class Context:
     def set_stream(self, stream: int) -> None:
         check(L._lib().qf_ctx_set_stream(self.handle, ctypes.c_void_p(stream)))
 
+    def set_payload_wait(self, event) -> None:
+        """qf_ctx_set_payload_wait: the next decode_batch runs its acceptance
+        pass at once and its payload pass after `event` (a torch.cuda.Event
+        that has been recorded, or a raw hipEvent_t handle; None clears)."""
+        h = event if (event is None or isinstance(event, int)) else event.cuda_event
+        check(L._lib().qf_ctx_set_payload_wait(self.handle, ctypes.c_void_p(h)), "payload_wait")
+
     def sync(self) -> None:
         check(L._lib().qf_sync(self.handle), "sync")
 

@@ -238,3 +238,60 @@ def test_decode_chunked_pipeline(qf, oracle, gpu_ctx, chunk, overlap, monkeypatc
         src, gens = make_batch(oracle, rng, k, r, L, G, k + r, shuffle=True)
         out = run_decode(qf, k, r, L, G, k + r, gens, False)
         check(oracle, k, L, src, gens, out, False)
+
+
+@pytest.mark.parametrize("path", PATHS)
+def test_decode_payload_wait_orders_the_rows_copy(qf, oracle, gpu_ctx, path, monkeypatch):
+    """qf_ctx_set_payload_wait: the rows land on another stream after a
+    delay; the decode's payload pass must wait for that stream's event (the
+    acceptance pass needs only the indices).  Without the gate it would read
+    the 0xEE placeholder rows."""
+    import torch
+
+    _path(monkeypatch, path)
+    k, r, L, G = 64, 16, 1200, 300
+    max_rows = k + r
+    rng = np.random.default_rng(11)
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, erase=13)
+    rs, emax = _r16(L), min(k, r)
+    rgs, rec_gs = max_rows * rs, emax * rs
+    rows = np.zeros(G * rgs, np.uint8)
+    ridx = np.zeros((G, max_rows), np.uint16)
+    nrows = np.zeros(G, np.uint32)
+    for g, (arr, rw, _) in enumerate(gens):
+        nrows[g] = len(arr)
+        ridx[g, : len(arr)] = arr
+        for s in range(len(arr)):
+            rows[g * rgs + s * rs: g * rgs + s * rs + L] = rw[s]
+    staged = torch.from_numpy(rows).cuda()
+    t_rows = torch.full_like(staged, 0xEE)
+    t_idx = torch.from_numpy(ridx.view(np.int16)).cuda()
+    t_n = torch.from_numpy(nrows.view(np.int32)).cuda()
+    t_rec = torch.zeros(G * rec_gs, dtype=torch.uint8, device="cuda")
+    t_recidx = torch.zeros(G * emax, dtype=torch.int16, device="cuda")
+    t_nrec = torch.zeros(G, dtype=torch.int32, device="cuda")
+    t_status = torch.full((G,), 77, dtype=torch.int32, device="cuda")
+    big_a = torch.ones(1 << 30, dtype=torch.uint8, device="cuda")
+    big_b = torch.empty_like(big_a)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    landed = torch.cuda.Event()
+    with torch.cuda.stream(side):
+        for _ in range(4):          # ~2 ms of HBM traffic ahead of the rows
+            big_b.copy_(big_a)
+        t_rows.copy_(staged)
+        landed.record(side)
+    ctx = qf.default_context()
+    ctx.set_payload_wait(landed)
+    qf.decode_batch(t_rows, t_idx, t_rec, t_recidx, t_nrec, t_status, k, r, L, max_rows=max_rows,
+                    row_stride=rs, rows_gen_stride=rgs, rec_row_stride=rs, rec_gen_stride=rec_gs,
+                    G=G, n_rows=t_n, ctx=ctx)
+    ctx.sync()
+    torch.cuda.synchronize()
+    out = (t_rec.cpu().numpy(), t_recidx.cpu().numpy().view(np.uint16).reshape(G, -1),
+           t_nrec.cpu().numpy(), t_status.cpu().numpy(), rs, rec_gs)
+    assert (out[3] == 0).all()
+    check(oracle, k, L, src, gens, out, False)
+    # the gate is one call only: a plain decode afterwards runs unchanged
+    ctx.set_payload_wait(None)
+    del big_a, big_b

@@ -130,3 +130,29 @@ def test_large_windows_error_where_reference_panics(qf, gpu_ctx, k, n):
         for i in range(k):
             enc.add_source_packet(qf.Packet(i, bytearray(8), 8, True))
         enc.generate_repair_packet(0, pool)
+
+
+def test_empty_and_degenerate_batches(qf, gpu_ctx):
+    """Empty inputs are no-ops that touch no memory (null buffers allowed);
+    malformed shapes are QF_EINVAL, never a fault (SURVEY 8(b) errors)."""
+    from quicfuscate_amd import _lib as L
+
+    lib, h = L._lib(), gpu_ctx.handle
+    enc = lambda k, r, Lb, G, flags=0: lib.qf_encode_batch(  # noqa: E731
+        h, L.EncodeShape(k, r, Lb, flags, Lb, k * Lb, Lb, r * Lb), G, None, None, None)
+    assert enc(64, 16, 1200, 0) == 0          # G = 0
+    assert enc(64, 0, 1200, 4) == 0           # r = 0: nothing to emit
+    assert enc(64, 16, 0, 4) == 0             # L = 0: empty payloads
+    assert enc(0, 16, 1200, 4) == L.QF_EINVAL
+    assert enc(257, 1, 1200, 4) == L.QF_EINVAL
+    assert enc(64, 16, 1200, 4, flags=0x80) == L.QF_EINVAL
+    assert enc(64, 16, 1200, 4) == L.QF_EINVAL  # G > 0 with null buffers
+    dec = lambda k, r, Lb, mr, G: lib.qf_decode_batch(  # noqa: E731
+        h, L.DecodeShape(k, r, Lb, mr, Lb, mr * Lb, Lb, r * Lb), G, None, None, None, None, None, None,
+        None, None)
+    assert dec(64, 16, 1200, 80, 0) == 0      # G = 0
+    assert dec(64, 16, 0, 80, 1) == L.QF_EINVAL
+    assert dec(64, 16, 1200, 0, 1) == L.QF_EINVAL
+    assert dec(0, 16, 1200, 80, 1) == L.QF_EINVAL
+    assert dec(64, 16, 1200, 80, 1) == L.QF_EINVAL  # G > 0 with null buffers
+    gpu_ctx.sync()
