@@ -383,6 +383,8 @@ def main(argv=None):
 
     if rank == 0 and world == 1 and args.host_path_G > 0:
         out["host_path"] = host_path_rate(torch, lib, L, ctx, k, r, Lb, min(args.host_path_G, G))
+        out["host_path"]["decode"] = host_decode_rate(torch, lib, L, ctx, rows, row_index, rec, e, n_slots, k, r,
+                                                      Lb, min(args.host_path_G, G))
 
     if rank == 0 and world == 1 and not args.no_cpu:
         S = min(args.cpu_sample, G)
@@ -418,6 +420,42 @@ def host_path_rate(torch, lib, L, ctx, k, r, Lb, G):
     dt = (time.perf_counter() - t0) / reps
     return {"generations": G, "encode_src_gibps_incl_pcie": round(G * k * Lb / dt / (1 << 30), 3),
             "bytes_moved_gb": round(G * (k + r) * Lb / 1e9, 3), "seconds": round(dt, 4)}
+
+
+def host_decode_rate(torch, lib, L, ctx, rows, row_index, rec, e, n_slots, k, r, Lb, G):
+    """Pinned host rows -> H2D -> decode -> D2H recovered rows
+    (qf_decode_batch_host); results compared with the device decode of the
+    same generations.  Reported in DESIGN.md; never `value`."""
+    import ctypes
+
+    emax = min(k, r)
+    rows_h = torch.empty(G * n_slots * Lb, dtype=torch.uint8, pin_memory=True)
+    rows_h.copy_(rows[: G * n_slots * Lb])
+    idx_h = torch.empty(G * n_slots, dtype=torch.int16, pin_memory=True)
+    idx_h.copy_(row_index[:G].reshape(-1))
+    rec_h = torch.empty(G * emax * Lb, dtype=torch.uint8, pin_memory=True)
+    ridx_h = torch.empty(G * emax, dtype=torch.int16, pin_memory=True)
+    nrec_h = torch.empty(G, dtype=torch.int32, pin_memory=True)
+    st_h = torch.empty(G, dtype=torch.int32, pin_memory=True)
+    sh = L.DecodeShape(k, r, Lb, n_slots, Lb, n_slots * Lb, Lb, emax * Lb)
+
+    def run():
+        L.check(lib.qf_decode_batch_host(ctx.handle, ctypes.byref(sh), G, rows_h.data_ptr(), idx_h.data_ptr(), None,
+                                         None, rec_h.data_ptr(), ridx_h.data_ptr(), nrec_h.data_ptr(),
+                                         st_h.data_ptr()), "decode_batch_host")
+
+    run()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        run()
+    dt = (time.perf_counter() - t0) / reps
+    got = rec_h.view(G, emax, Lb)[:, :e]
+    want = rec[: G * emax * Lb].view(G, emax, Lb)[:, :e].cpu()
+    ok = bool((st_h == 0).all()) and bool((got == want).all())
+    return {"generations": G, "decode_src_gibps_incl_pcie": round(G * k * Lb / dt / (1 << 30), 3),
+            "bytes_moved_gb": round(G * (n_slots + e) * Lb / 1e9, 3), "seconds": round(dt, 4),
+            "matches_device_decode": ok}
 
 
 def cpu_variants(src, rep, k, r, Lb, S):

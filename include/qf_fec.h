@@ -185,6 +185,22 @@ int qf_decode_batch(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G,
                     uint8_t *rec_dev, uint16_t *rec_index_dev, uint32_t *n_rec_dev,
                     int32_t *status_dev);
 
+/* Same, every buffer host-resident (pinned memory recommended): the receive
+ * side starting from datagrams in host memory (core.rs:203-232).  Chunks of
+ * about 64 MiB of rows are streamed H2D -> decode -> D2H on several HIP
+ * streams; each chunk's acceptance pass starts once its indices have landed
+ * and its payload pass once its rows have (qf_ctx_set_payload_wait).
+ * Generation g's rows must lie in [g*rows_gen_stride, (g+1)*rows_gen_stride);
+ * recovered rows must be dense per generation (rec_gen_stride ==
+ * min(k, r) * rec_row_stride).  Bytes [0, L) of recovered rows
+ * n_rec[g] .. min(k, r) - 1 of a generation are unspecified on return (the
+ * device path leaves them untouched).  Synchronous on return. */
+int qf_decode_batch_host(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G,
+                         const uint8_t *rows_host, const uint16_t *row_index_host,
+                         const uint32_t *n_rows_host, const uint8_t *row_coeffs_host,
+                         uint8_t *rec_host, uint16_t *rec_index_host, uint32_t *n_rec_host,
+                         int32_t *status_host);
+
 /* ---------------------------------------------------------------------------
  * Per-connection objects mirroring the reference's Rust API one call at a
  * time (what core.rs drives).  Payload state lives in HBM.

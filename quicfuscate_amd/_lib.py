@@ -96,6 +96,7 @@ _SIGS = {
     "qf_encode_batch": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
     "qf_encode_batch_host": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
     "qf_decode_batch": (_I, [_P, ctypes.POINTER(DecodeShape), _U32, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "qf_decode_batch_host": (_I, [_P, ctypes.POINTER(DecodeShape), _U32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "qf_encoder_new": (_I, [_P, _U32, _U32, _U32, ctypes.POINTER(_P)]),
     "qf_encoder_free": (_I, [_P]),
     "qf_encoder_add_source_packet": (_I, [_P, _U64, _P, _U32]),

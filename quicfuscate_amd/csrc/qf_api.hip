@@ -76,6 +76,13 @@ struct qf_ctx {
     uint8_t* d_stage_src[kPipe] = {nullptr, nullptr, nullptr};
     uint8_t* d_stage_rep[kPipe] = {nullptr, nullptr, nullptr};
     size_t stage_src_bytes = 0, stage_rep_bytes = 0;
+    // host-memory decode pipeline: one staging block per pipe slot and the
+    // slot's events (indices landed, rows landed, decode done)
+    uint8_t* d_dstage[kPipe] = {nullptr, nullptr, nullptr};
+    size_t dstage_bytes = 0;
+    hipEvent_t ev_idx[kPipe] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_rows[kPipe] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_done[kPipe] = {nullptr, nullptr, nullptr};
     // bit-sliced Cauchy kernels (loaded on first use)
     qf::BsCache bs;
     // GF(2^16) log / exp tables (qf_gf16.hip, built on first use)
@@ -793,6 +800,9 @@ int qf_ctx_destroy(qf_ctx* c) {
         }
         if (c->d_stage_src[i]) hipFree(c->d_stage_src[i]);
         if (c->d_stage_rep[i]) hipFree(c->d_stage_rep[i]);
+        if (c->d_dstage[i]) hipFree(c->d_dstage[i]);
+        for (hipEvent_t e : {c->ev_idx[i], c->ev_rows[i], c->ev_done[i]})
+            if (e) hipEventDestroy(e);
     }
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -950,6 +960,108 @@ int qf_ctx_set_payload_wait(qf_ctx* ctx, void* event) {
     std::lock_guard<std::mutex> g(ctx->mu);
     ctx->payload_wait = reinterpret_cast<hipEvent_t>(event);
     return QF_OK;
+}
+
+// Host-memory decode: the receive side of the reference starts from UDP
+// datagrams in host memory (core.rs:203-232).  Chunks of ~64 MiB of rows go
+// through pipe slot c % kPipe:
+//   pstream[slot]: H2D indices (+ n_rows, coefficients) -> ev_idx,
+//                  H2D rows -> ev_rows
+//   ctx->stream:   wait ev_idx; decode (acceptance pass at once, payload pass
+//                  after ev_rows: qf_ctx_set_payload_wait) -> ev_done
+//   pstream[slot]: wait ev_done; D2H recovered rows, indices, counts, status
+// Every kernel runs on ctx->stream, so the decode workspace is reused in
+// stream order; a slot's next H2D follows its previous D2H on the same
+// stream, so the staging is never overwritten early.
+static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+int qf_decode_batch_host(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
+                         const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
+                         uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+    if (!ctx || !sh) return QF_EINVAL;
+    const uint32_t k = sh->k, r = sh->r, L = sh->L, mr = sh->max_rows;
+    if (k == 0 || k > 256 || mr == 0 || mr > 4096 || L == 0) return QF_EINVAL;
+    if (G == 0) return QF_OK;
+    const uint32_t e_max = std::min(k, r);
+    if (!rows || !row_index || !n_rec || !status || (e_max && (!rec || !rec_index))) return QF_EINVAL;
+    // generation g's rows lie in [g * rows_gen_stride, +rows_gen_stride);
+    // recovered rows are dense per generation (copied back row by row)
+    if (sh->rows_gen_stride < (uint64_t)(mr - 1) * sh->row_stride + L ||
+        (e_max && sh->rec_gen_stride != (uint64_t)e_max * sh->rec_row_stride) || sh->rec_row_stride < L)
+        return QF_EINVAL;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        int s = ensure_device(ctx);
+        if (s) return s;
+    }
+    const uint64_t per_gen_in = sh->rows_gen_stride + 2ull * mr + 4 + (row_coeffs ? (uint64_t)mr * k : 0);
+    uint64_t per = std::max<uint64_t>(1, (64ull << 20) / per_gen_in);
+    per = std::min<uint64_t>(per, G);
+    // staging layout of one slot (256-B aligned parts)
+    const size_t o_rows = 0, o_idx = al256(per * sh->rows_gen_stride), o_n = o_idx + al256(per * mr * 2),
+                 o_coef = o_n + al256(per * 4), o_rec = o_coef + (row_coeffs ? al256(per * mr * k) : 0),
+                 o_ridx = o_rec + al256(per * sh->rec_gen_stride), o_nrec = o_ridx + al256(per * e_max * 2 + 2),
+                 o_st = o_nrec + al256(per * 4), total = o_st + al256(per * 4);
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        if (total > ctx->dstage_bytes) {
+            for (int i = 0; i < qf_ctx::kPipe; ++i) {
+                if (ctx->pstream[i]) QF_CHECK_HIP(hipStreamSynchronize(ctx->pstream[i]));
+                if (ctx->d_dstage[i]) hipFree(ctx->d_dstage[i]);
+                ctx->d_dstage[i] = nullptr;
+            }
+            QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+            ctx->dstage_bytes = 0;
+            for (int i = 0; i < qf_ctx::kPipe; ++i)
+                if (hipMalloc(&ctx->d_dstage[i], total) != hipSuccess) return QF_ENOMEM;
+            ctx->dstage_bytes = total;
+        }
+        for (int i = 0; i < qf_ctx::kPipe; ++i) {
+            if (!ctx->pstream[i]) QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->pstream[i], hipStreamNonBlocking));
+            for (hipEvent_t* e : {&ctx->ev_idx[i], &ctx->ev_rows[i], &ctx->ev_done[i]})
+                if (!*e) QF_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        }
+    }
+    int first_err = QF_OK;
+    uint32_t c = 0;
+    for (uint64_t g0 = 0; g0 < G; g0 += per, ++c) {
+        const uint64_t n = std::min<uint64_t>(per, G - g0);
+        const int slot = c % qf_ctx::kPipe;
+        hipStream_t ps = ctx->pstream[slot];
+        uint8_t* d = ctx->d_dstage[slot];
+        QF_CHECK_HIP(hipMemcpyAsync(d + o_idx, row_index + g0 * mr, n * mr * 2, hipMemcpyHostToDevice, ps));
+        if (n_rows) QF_CHECK_HIP(hipMemcpyAsync(d + o_n, n_rows + g0, n * 4, hipMemcpyHostToDevice, ps));
+        if (row_coeffs)
+            QF_CHECK_HIP(hipMemcpyAsync(d + o_coef, row_coeffs + g0 * mr * k, n * mr * k, hipMemcpyHostToDevice, ps));
+        QF_CHECK_HIP(hipEventRecord(ctx->ev_idx[slot], ps));
+        QF_CHECK_HIP(hipMemcpyAsync(d + o_rows, rows + g0 * sh->rows_gen_stride, n * sh->rows_gen_stride,
+                                    hipMemcpyHostToDevice, ps));
+        QF_CHECK_HIP(hipEventRecord(ctx->ev_rows[slot], ps));
+        QF_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_idx[slot], 0));
+        // (row coefficients, read by the acceptance pass, landed before ev_idx)
+        qf_ctx_set_payload_wait(ctx, ctx->ev_rows[slot]);
+        int e = qf_decode_batch(ctx, sh, (uint32_t)n, d + o_rows, reinterpret_cast<const uint16_t*>(d + o_idx),
+                                n_rows ? reinterpret_cast<const uint32_t*>(d + o_n) : nullptr,
+                                row_coeffs ? d + o_coef : nullptr, e_max ? d + o_rec : nullptr,
+                                e_max ? reinterpret_cast<uint16_t*>(d + o_ridx) : nullptr,
+                                reinterpret_cast<uint32_t*>(d + o_nrec), reinterpret_cast<int32_t*>(d + o_st));
+        if (e != QF_OK) {
+            first_err = e;
+            break;
+        }
+        QF_CHECK_HIP(hipEventRecord(ctx->ev_done[slot], ctx->stream));
+        QF_CHECK_HIP(hipStreamWaitEvent(ps, ctx->ev_done[slot], 0));
+        if (e_max) {
+            QF_CHECK_HIP(hipMemcpy2DAsync(rec + g0 * sh->rec_gen_stride, sh->rec_row_stride, d + o_rec,
+                                          sh->rec_row_stride, L, n * e_max, hipMemcpyDeviceToHost, ps));
+            QF_CHECK_HIP(hipMemcpyAsync(rec_index + g0 * e_max, d + o_ridx, n * e_max * 2, hipMemcpyDeviceToHost, ps));
+        }
+        QF_CHECK_HIP(hipMemcpyAsync(n_rec + g0, d + o_nrec, n * 4, hipMemcpyDeviceToHost, ps));
+        QF_CHECK_HIP(hipMemcpyAsync(status + g0, d + o_st, n * 4, hipMemcpyDeviceToHost, ps));
+    }
+    for (int i = 0; i < qf_ctx::kPipe; ++i) QF_CHECK_HIP(hipStreamSynchronize(ctx->pstream[i]));
+    QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return first_err;
 }
 
 static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,

@@ -177,6 +177,22 @@ def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_
           "encode_batch")
 
 
+def decode_batch_host(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int, Lb: int, *,
+                      max_rows: int, row_stride: int, rows_gen_stride: int, rec_row_stride: int,
+                      rec_gen_stride: int, G: int, n_rows=None, row_coeffs=None,
+                      ctx: Optional[Context] = None) -> None:
+    """qf_decode_batch_host: decode_batch with every buffer in host memory
+    (torch CPU tensors, pinned recommended); synchronous."""
+    ctx = ctx or default_context()
+    sh = L.DecodeShape(k, r, Lb, max_rows, row_stride, rows_gen_stride, rec_row_stride, rec_gen_stride)
+    check(L._lib().qf_decode_batch_host(
+        ctx.handle, ctypes.byref(sh), G, _ptr(rows), _ptr(row_index),
+        _ptr(n_rows) if n_rows is not None else None,
+        _ptr(row_coeffs) if row_coeffs is not None else None,
+        _ptr(rec) if rec is not None else None, _ptr(rec_index) if rec_index is not None else None,
+        _ptr(n_rec), _ptr(status)), "decode_batch_host")
+
+
 def decode_batch(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int, Lb: int, *,
                  max_rows: int, row_stride: int, rows_gen_stride: int, rec_row_stride: int,
                  rec_gen_stride: int, G: int, n_rows=None, row_coeffs=None,

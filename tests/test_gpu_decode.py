@@ -295,3 +295,41 @@ def test_decode_payload_wait_orders_the_rows_copy(qf, oracle, gpu_ctx, path, mon
     # the gate is one call only: a plain decode afterwards runs unchanged
     ctx.set_payload_wait(None)
     del big_a, big_b
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("k,r,L,G,pin", [(64, 16, 1200, 2000, True), (16, 16, 100, 37, False),
+                                         (96, 15, 9000, 120, True)])
+def test_decode_batch_host_matches_oracle(qf, oracle, gpu_ctx, path, k, r, L, G, pin, monkeypatch):
+    """qf_decode_batch_host: rows, indices and outputs in host memory,
+    several pipelined chunks (k=64: ~96 KB per generation -> G=2000 spans 3
+    chunks of 64 MiB); same results as the oracle."""
+    import torch
+
+    _path(monkeypatch, path)
+    rng = np.random.default_rng(k * 7 + L)
+    max_rows = k + r
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, trim_prob=0.02)
+    rs, emax = _r16(L), min(k, r)
+    rgs, rec_gs = max_rows * rs, emax * rs
+    rows = torch.zeros(G * rgs, dtype=torch.uint8, pin_memory=pin)
+    rows_np = rows.numpy()
+    ridx = np.zeros((G, max_rows), np.uint16)
+    nrows = np.zeros(G, np.uint32)
+    for g, (arr, rw, _) in enumerate(gens):
+        nrows[g] = len(arr)
+        ridx[g, : len(arr)] = arr
+        for s in range(len(arr)):
+            rows_np[g * rgs + s * rs: g * rgs + s * rs + L] = rw[s]
+    t_idx = torch.from_numpy(ridx.view(np.int16).reshape(-1).copy())
+    t_n = torch.from_numpy(nrows.view(np.int32).copy())
+    t_rec = torch.full((G * rec_gs,), 0x5A, dtype=torch.uint8, pin_memory=pin)
+    t_recidx = torch.zeros(G * emax, dtype=torch.int16, pin_memory=pin)
+    t_nrec = torch.zeros(G, dtype=torch.int32, pin_memory=pin)
+    t_status = torch.full((G,), 77, dtype=torch.int32, pin_memory=pin)
+    qf.decode_batch_host(rows, t_idx, t_rec, t_recidx, t_nrec, t_status, k, r, L, max_rows=max_rows,
+                         row_stride=rs, rows_gen_stride=rgs, rec_row_stride=rs, rec_gen_stride=rec_gs,
+                         G=G, n_rows=t_n)
+    out = (t_rec.numpy(), t_recidx.numpy().view(np.uint16).reshape(G, -1), t_nrec.numpy(), t_status.numpy(),
+           rs, rec_gs)
+    check(oracle, k, L, src, gens, out, False)
