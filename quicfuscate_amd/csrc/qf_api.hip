@@ -59,6 +59,8 @@ struct qf_ctx {
     uint32_t* d_custom = nullptr;
     size_t custom_words = 0;
     hipEvent_t custom_done = nullptr;
+    // device copies of Cauchy matrices (r x k) for the small-batch encode
+    std::map<std::pair<uint32_t, uint32_t>, uint8_t*> small_coef;
     // qf_ctx_set_payload_wait: event the next decode's payload pass waits for
     hipEvent_t payload_wait = nullptr;
     // decode workspace
@@ -249,6 +251,43 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     if (!coeff) {
         int s = cauchy_matrix(k, r, cm);
         if (s != QF_OK) return s;
+    }
+    // Few windows (the per-packet send path): the bit-sliced kernels would
+    // run fewer than 64 waves, each doing all k rows x r repairs; the
+    // small-batch kernel spreads (generation, repair, unit) over lanes.
+    // QF_ENCODE_SMALL=0/1 forces it off/on (tests run both).
+    {
+        const char* sm = getenv("QF_ENCODE_SMALL");
+        const int force = sm ? atoi(sm) : -1;
+        const bool few = (uint64_t)G * qf::bs_padded_units(L) < 64ull * 128;
+        if (!coeff && force != 0 && (force == 1 || few)) {
+            const auto key = std::make_pair(k, r);
+            auto it = ctx->small_coef.find(key);
+            if (it == ctx->small_coef.end()) {
+                uint8_t* d = nullptr;
+                if (hipMalloc(&d, cm.size()) != hipSuccess) return QF_ENOMEM;
+                QF_CHECK_HIP(hipMemcpy(d, cm.data(), cm.size(), hipMemcpyHostToDevice));
+                it = ctx->small_coef.emplace(key, d).first;
+            }
+            qf::EncodeSmallArgs a{};
+            a.src = src;
+            a.src_gen_stride = sh->src_gen_stride;
+            a.src_row_stride = sh->src_row_stride;
+            a.rep = rep;
+            a.rep_gen_stride = sh->rep_gen_stride;
+            a.rep_row_stride = sh->rep_row_stride;
+            a.coef = it->second;
+            a.tab256 = ctx->d_tab256;
+            a.k = k;
+            a.r = r;
+            a.L = L;
+            a.Lu = Lu;
+            a.G = G;
+            hipEvent_t ev = prof_begin(ctx, st);
+            QF_CHECK_HIP(qf::launch_encode_small(a, ctx->num_cus, st));
+            prof_end(ctx, st, ev, "k_encode_small");
+            return QF_OK;
+        }
     }
     // Fast path: bit-sliced kernel specialised to the reference's Cauchy
     // matrix of (k, r) (bs_codegen.py), for whole 16-byte rows.
@@ -773,6 +812,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto& kv : c->cauchy) hipFree(kv.second.dev);
+    for (auto& kv : c->small_coef) hipFree(kv.second);
     if (c->d_tab256) hipFree(c->d_tab256);
     if (c->d_explog) hipFree(c->d_explog);
     if (c->h_custom) hipHostFree(c->h_custom);

@@ -127,4 +127,18 @@ hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, ui
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t word_offset,
                                 int num_cus, hipStream_t st);
 
+// Small-batch encode (the per-packet send path: one or a few windows).
+// repair[g][j] = sum_i coef[j*k + i] * src[g][i] over L bytes; lanes over
+// (generation, repair, 16-B unit), units fastest.
+struct EncodeSmallArgs {
+    const uint8_t* src;
+    uint64_t src_gen_stride, src_row_stride;
+    uint8_t* rep;
+    uint64_t rep_gen_stride, rep_row_stride;
+    const uint8_t* coef;     // r x k device bytes
+    const uint32_t* tab256;  // split-table records (8 dwords) of every coefficient
+    uint32_t k, r, L, Lu, G;
+};
+hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st);
+
 }  // namespace qf

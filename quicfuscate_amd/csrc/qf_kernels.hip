@@ -1348,4 +1348,86 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n, uint64_t seed, uint64_
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Small-batch encode: the bit-sliced kernels run one wave per 128 units, so a
+// single 1 KiB window (AdaptiveFec::on_send -> generate_repair_packet,
+// adaptive.rs:546-562, decoder.rs:172-275) was one wave doing all k rows x r
+// repairs (60 us per pass at k = 128).  Here a block takes one (generation,
+// repair, 64 units) tile, its four waves split the k rows, and a lane sums
+// its quarter with split-table products (v_perm, records of gf256_tables.h in
+// LDS); the loop is memory-latency-bound at this size, so each batch of 8
+// rows has all its loads in flight before its products.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
+    // tile = (generation g, repair j, 64 consecutive units); the block's four
+    // waves take a quarter of the k rows each (batches of 8 rows whose loads
+    // are all in flight before the products), then reduce through LDS
+    __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 8];
+    __shared__ uint4 part[3][64];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.tab256);
+        uint4* l = reinterpret_cast<uint4*>(tab);
+        for (uint32_t w = threadIdx.x; w < 256 * 2; w += blockDim.x) l[w] = g[w];
+    }
+    __syncthreads();
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(tab);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t ut = (a.Lu + 63) / 64;                     // unit tiles per row
+    const uint64_t tiles = (uint64_t)a.G * a.r * ut;
+    const uint32_t kc = ((a.k + 3) / 4 + 7) & ~7u;            // rows per wave (multiple of 8)
+    const uint32_t i0 = wv * kc, i1 = min(a.k, i0 + kc);
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const uint64_t gj = t / ut;
+        const uint32_t u = (uint32_t)(t - gj * ut) * 64 + lane;
+        const uint64_t g = gj / a.r;
+        const uint32_t j = (uint32_t)(gj - g * a.r);
+        const bool act = u < a.Lu;
+        const uint32_t nb = act ? min(16u, a.L - 16 * u) : 0u;
+        const uint8_t* sp = a.src + g * a.src_gen_stride + 16ull * (act ? u : 0);
+        const uint8_t* cp = a.coef + (uint64_t)j * a.k;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        for (uint32_t ib = i0; ib < i1; ib += 8) {
+            uint4 x[8];
+            uint32_t c[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t i = ib + q;
+                const bool ok = act && i < i1;
+                x[q] = ok ? load_unit(sp + (uint64_t)i * a.src_row_stride, nb) : make_uint4(0, 0, 0, 0);
+                c[q] = (i < i1) ? ((uint32_t)cp[i] << 5) : 0u;    // record 0: zero products
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+                const uint4 A = *reinterpret_cast<const uint4*>(tb + c[q]);
+                const uint32_t a2 = *reinterpret_cast<const uint32_t*>(tb + c[q] + 16);
+                const uint4 B = *reinterpret_cast<const uint4*>(tb + c[q + 1]);
+                const uint32_t b2 = *reinterpret_cast<const uint32_t*>(tb + c[q + 1] + 16);
+                fma_pair(acc, A, a2, selectors(x[q]), B, b2, selectors(x[q + 1]));
+            }
+        }
+        if (wv > 0) part[wv - 1][lane] = acc;
+        __syncthreads();
+        if (wv == 0 && act) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const uint4 p = part[q][lane];
+                acc.x ^= p.x;
+                acc.y ^= p.y;
+                acc.z ^= p.z;
+                acc.w ^= p.w;
+            }
+            store_unit(a.rep + g * a.rep_gen_stride + (uint64_t)j * a.rep_row_stride + 16ull * u, acc, nb);
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st) {
+    const uint64_t tiles = (uint64_t)a.G * a.r * ((a.Lu + 63) / 64);
+    if (!tiles || a.k == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>(tiles, (uint64_t)num_cus * 8);
+    hipLaunchKernelGGL(k_encode_small, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 }  // namespace qf

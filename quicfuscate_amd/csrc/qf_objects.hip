@@ -36,6 +36,8 @@ struct qf_encoder {
     uint8_t* h_stage = nullptr;      // pinned staging of one packet
     hipEvent_t stage_done = nullptr; // its copies have landed
     std::vector<uint8_t> win;        // Cauchy rows 0..r-1 in window order (cached)
+    uint8_t* h_out = nullptr;        // pinned download of the repair rows
+    size_t h_out_bytes = 0;
 };
 
 struct qf_decoder {
@@ -94,6 +96,7 @@ int qf_encoder_free(qf_encoder* e) {
         hipEventDestroy(e->stage_done);
     }
     if (e->h_stage) hipHostFree(e->h_stage);
+    if (e->h_out) hipHostFree(e->h_out);
     if (e->d_ring) hipFree(e->d_ring);
     if (e->d_out) hipFree(e->d_out);
     delete e;
@@ -160,11 +163,28 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
         int s = qf_encode_batch(e->ctx, &sh, 1, e->d_ring + (size_t)oldest * e->stride, e->d_out,
                                 first == 0 ? nullptr : win);
         if (s != QF_OK) return s;
+        hipStream_t st = (hipStream_t)qf_ctx_stream(e->ctx);
         if (out_data) {
-            QF_CHECK_HIP(hipMemcpy2DAsync(out_data, out_stride, e->d_out, e->stride, L, count,
-                                          hipMemcpyDeviceToHost, (hipStream_t)qf_ctx_stream(e->ctx)));
+            // one contiguous D2H into pinned memory (a copy into the caller's
+            // pageable rows would go through the runtime's staging), then
+            // the rows out on the host
+            const size_t bytes = (size_t)count * e->stride;
+            if (e->h_out_bytes < bytes) {
+                QF_CHECK_HIP(hipStreamSynchronize(st));
+                if (e->h_out) hipHostFree(e->h_out);
+                e->h_out = nullptr;
+                e->h_out_bytes = 0;
+                if (hipHostMalloc(reinterpret_cast<void**>(&e->h_out), (size_t)256 * e->stride) != hipSuccess)
+                    return QF_ENOMEM;
+                e->h_out_bytes = (size_t)256 * e->stride;
+            }
+            QF_CHECK_HIP(hipMemcpyAsync(e->h_out, e->d_out, bytes, hipMemcpyDeviceToHost, st));
+            QF_CHECK_HIP(hipStreamSynchronize(st));
+            for (uint32_t q = 0; q < count; ++q)
+                memcpy(out_data + (size_t)q * out_stride, e->h_out + (size_t)q * e->stride, L);
+        } else {
+            QF_CHECK_HIP(hipStreamSynchronize(st));
         }
-        QF_CHECK_HIP(hipStreamSynchronize((hipStream_t)qf_ctx_stream(e->ctx)));
     }
     for (uint32_t q = 0; q < count; ++q) {
         if (out_len) out_len[q] = L;

@@ -11,6 +11,15 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _bit_sliced_encode(monkeypatch):
+    # these tests pin the bit-sliced kernels (and their zero tails) at small
+    # G; the small-batch kernel has its own cases (test_gpu_encode.py)
+    monkeypatch.setenv("QF_ENCODE_SMALL", "0")
+
+
 GOLDEN = json.loads((Path(__file__).parent / "golden" / "golden.json").read_text())
 
 
@@ -241,3 +250,25 @@ def test_gf_mul_slice_large_table_kernel(qf, oracle, gpu_ctx):
     want = tab[a.long() * 256 + b.long()]
     assert torch.equal(out[:n], want)
     assert (out[n:] == 0xA5).all()
+
+
+@pytest.mark.parametrize("k,r,L,G", CASES + [(128, 39, 1024, 1), (64, 10, 1024, 1), (16, 1, 1024, 1),
+                                             (196, 59, 9000, 1), (64, 16, 1200, 700)])
+def test_encode_small_batch_kernel(qf, oracle, gpu_ctx, k, r, L, G, monkeypatch):
+    """k_encode_small (lanes over generation x repair x unit; the per-packet
+    send path's kernel) is bit-exact against the oracle on every case,
+    including odd k (zero second coefficient), partial last units and
+    k + r = 256."""
+    monkeypatch.setenv("QF_ENCODE_SMALL", "1")
+    rng = np.random.default_rng(k * 3 + r + L + G)
+    rs = _r16(L) + 16
+    gs = k * rs + 32
+    src = rng.integers(0, 256, G * gs, dtype=np.uint8)
+    rrs = _r16(L) + 32
+    rgs = r * rrs + 16
+    rep = run_encode(qf, src, k, r, L, G, rs, gs, rrs, rgs)
+    for g in range(G):
+        want = oracle.encode(np.stack([src[g * gs + i * rs: g * gs + i * rs + L] for i in range(k)]), r)
+        for j in range(r):
+            assert (rep[g * rgs + j * rrs: g * rgs + j * rrs + L] == want[j]).all(), (g, j)
+            assert (rep[g * rgs + j * rrs + L: g * rgs + (j + 1) * rrs] == 0xA5).all(), (g, j)  # nothing past L

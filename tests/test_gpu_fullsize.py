@@ -23,6 +23,13 @@ import bench
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _bit_sliced_encode(monkeypatch):
+    # these tests pin the bit-sliced kernels (and their zero tails) at small
+    # G; the small-batch kernel has its own cases (test_gpu_encode.py)
+    monkeypatch.setenv("QF_ENCODE_SMALL", "0")
+
 K, R, L = 64, 16, 1200
 SEED = 0x51464543
 
