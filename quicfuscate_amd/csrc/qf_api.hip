@@ -231,6 +231,23 @@ int prof_drain(qf_ctx* ctx) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// device copy of the Cauchy matrix (r x k), cached per (k, r)
+int small_coef_matrix(qf_ctx* ctx, uint32_t k, uint32_t r, const uint8_t** out) {
+    const auto key = std::make_pair(k, r);
+    auto it = ctx->small_coef.find(key);
+    if (it == ctx->small_coef.end()) {
+        std::vector<uint8_t> cm;
+        int s = cauchy_matrix(k, r, cm);
+        if (s != QF_OK) return s;
+        uint8_t* d = nullptr;
+        if (hipMalloc(&d, cm.size()) != hipSuccess) return QF_ENOMEM;
+        QF_CHECK_HIP(hipMemcpy(d, cm.data(), cm.size(), hipMemcpyHostToDevice));
+        it = ctx->small_coef.emplace(key, d).first;
+    }
+    *out = it->second;
+    return QF_OK;
+}
+
 int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src,
                 uint8_t* rep, const uint8_t* coeff, hipStream_t st) {
     const uint32_t k = sh->k, r = sh->r, L = sh->L;
@@ -261,22 +278,18 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         const int force = sm ? atoi(sm) : -1;
         const bool few = (uint64_t)G * qf::bs_padded_units(L) < 64ull * 128;
         if (!coeff && force != 0 && (force == 1 || few)) {
-            const auto key = std::make_pair(k, r);
-            auto it = ctx->small_coef.find(key);
-            if (it == ctx->small_coef.end()) {
-                uint8_t* d = nullptr;
-                if (hipMalloc(&d, cm.size()) != hipSuccess) return QF_ENOMEM;
-                QF_CHECK_HIP(hipMemcpy(d, cm.data(), cm.size(), hipMemcpyHostToDevice));
-                it = ctx->small_coef.emplace(key, d).first;
-            }
+            const uint8_t* dcoef = nullptr;
+            int s = small_coef_matrix(ctx, k, r, &dcoef);
+            if (s != QF_OK) return s;
             qf::EncodeSmallArgs a{};
+            a.rot = 0;
             a.src = src;
             a.src_gen_stride = sh->src_gen_stride;
             a.src_row_stride = sh->src_row_stride;
             a.rep = rep;
             a.rep_gen_stride = sh->rep_gen_stride;
             a.rep_row_stride = sh->rep_row_stride;
-            a.coef = it->second;
+            a.coef = dcoef;
             a.tab256 = ctx->d_tab256;
             a.k = k;
             a.r = r;
@@ -682,6 +695,41 @@ int ctx_lock(qf_ctx* ctx, std::unique_lock<std::mutex>& lk) {
 }
 hipStream_t ctx_stream(qf_ctx* ctx) { return ctx->stream; }
 int ctx_num_cus(qf_ctx* ctx) { return ctx->num_cus; }
+bool small_encode_enabled() {
+    const char* sm = getenv("QF_ENCODE_SMALL");
+    return !(sm && atoi(sm) == 0);
+}
+int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, uint32_t L, const uint8_t* ring,
+                       uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride) {
+    if (!ctx || !ring || !rep || k == 0 || count == 0 || rot >= k) return QF_EINVAL;
+    if ((uint64_t)k + first + count > 256) return QF_ERANGE;  // gf_inv(0)
+    if (L == 0) return QF_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    const uint8_t* dcoef = nullptr;
+    s = small_coef_matrix(ctx, k, first + count, &dcoef);  // Cauchy row j depends on (k, j) only
+    if (s != QF_OK) return s;
+    qf::EncodeSmallArgs a{};
+    a.src = ring;
+    a.src_gen_stride = (uint64_t)k * stride;
+    a.src_row_stride = stride;
+    a.rep = rep;
+    a.rep_gen_stride = (uint64_t)count * rep_stride;
+    a.rep_row_stride = rep_stride;
+    a.coef = dcoef + (size_t)first * k;
+    a.tab256 = ctx->d_tab256;
+    a.k = k;
+    a.r = count;
+    a.L = L;
+    a.Lu = (L + 15) / 16;
+    a.G = 1;
+    a.rot = rot;
+    hipEvent_t ev = prof_begin(ctx, ctx->stream);
+    QF_CHECK_HIP(qf::launch_encode_small(a, ctx->num_cus, ctx->stream));
+    prof_end(ctx, ctx->stream, ev, "k_encode_small");
+    return QF_OK;
+}
 int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
     int s = grow_work(ctx, bytes);
     if (s) return s;

@@ -36,4 +36,13 @@ namespace qf {
 int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_t* src, uint8_t* rep,
                     const uint16_t* coeff_rxk, uint32_t first, uint32_t rot, uint8_t* coeff_be_dev);
 
+// One GF(2^8) window over a ring of k source slots (slot stride `stride`):
+// window position i in slot (rot + i) % k; repairs = Cauchy rows
+// first..first+count-1 into rep (row stride rep_stride), on the small-batch
+// kernel.  QF_ERANGE when k + first + count > 256.  (qf_api.hip)
+int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, uint32_t L,
+                       const uint8_t* ring, uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride);
+// Whether the small-batch encode is enabled (QF_ENCODE_SMALL != 0).
+bool small_encode_enabled();
+
 }  // namespace qf

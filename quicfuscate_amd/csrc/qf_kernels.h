@@ -138,6 +138,7 @@ struct EncodeSmallArgs {
     const uint8_t* coef;     // r x k device bytes
     const uint32_t* tab256;  // split-table records (8 dwords) of every coefficient
     uint32_t k, r, L, Lu, G;
+    uint32_t rot;            // window row i is source row (i + rot) % k (a ring; 0: plain)
 };
 hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st);
 

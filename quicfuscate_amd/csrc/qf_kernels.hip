@@ -1393,7 +1393,8 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
             for (int q = 0; q < 8; ++q) {
                 const uint32_t i = ib + q;
                 const bool ok = act && i < i1;
-                x[q] = ok ? load_unit(sp + (uint64_t)i * a.src_row_stride, nb) : make_uint4(0, 0, 0, 0);
+                const uint32_t row = i + a.rot >= a.k ? i + a.rot - a.k : i + a.rot;
+                x[q] = ok ? load_unit(sp + (uint64_t)row * a.src_row_stride, nb) : make_uint4(0, 0, 0, 0);
                 c[q] = (i < i1) ? ((uint32_t)cp[i] << 5) : 0u;    // record 0: zero products
             }
 #pragma unroll

@@ -12,6 +12,7 @@
 #include "gf256_tables.h"
 #include "qf_fec.h"
 #include "qf_bs.h"
+#include "qf_internal.h"
 
 #define QF_CHECK_HIP(expr)                         \
     do {                                           \
@@ -36,6 +37,10 @@ struct qf_encoder {
     uint8_t* h_stage = nullptr;      // pinned staging of one packet
     hipEvent_t stage_done = nullptr; // its copies have landed
     std::vector<uint8_t> win;        // Cauchy rows 0..r-1 in window order (cached)
+    // small-batch kernel (QF_ENCODE_SMALL != 0): it reads the ring rotated,
+    // so each packet is uploaded once; otherwise the double ring keeps the
+    // window contiguous for the bit-sliced kernels
+    bool ring_rot = true;
     uint8_t* h_out = nullptr;        // pinned download of the repair rows
     size_t h_out_bytes = 0;
 };
@@ -77,6 +82,7 @@ int qf_encoder_new(qf_ctx* ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_enc
     e->stride = round16(max_len);
     e->lens.assign(k, 0);
     e->ids.assign(k, 0);
+    e->ring_rot = qf::small_encode_enabled();
     if (hipMalloc(&e->d_ring, (size_t)2 * k * e->stride) != hipSuccess ||
         hipMalloc(&e->d_out, (size_t)256 * e->stride) != hipSuccess ||
         hipMemset(e->d_ring, 0, (size_t)2 * k * e->stride) != hipSuccess ||
@@ -116,8 +122,9 @@ int qf_encoder_add_source_packet(qf_encoder* e, uint64_t id, const uint8_t* data
     hipStream_t st = (hipStream_t)qf_ctx_stream(e->ctx);
     QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)slot * e->stride, e->h_stage, e->stride,
                                 hipMemcpyHostToDevice, st));
-    QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)(slot + e->k) * e->stride, e->h_stage, e->stride,
-                                hipMemcpyHostToDevice, st));
+    if (!e->ring_rot)
+        QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)(slot + e->k) * e->stride, e->h_stage, e->stride,
+                                    hipMemcpyHostToDevice, st));
     QF_CHECK_HIP(hipEventRecord(e->stage_done, st));
     e->lens[slot] = len;
     e->ids[slot] = id;
@@ -152,16 +159,22 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
         // the window is contiguous in the double ring: repairs 0..count-1 are
         // the cached Cauchy code (k, count) (generated kernel or cached
         // tables); a later first row goes through explicit coefficients
-        qf_encode_shape sh{};
-        sh.k = k;
-        sh.r = count;
-        sh.L = L;
-        sh.src_row_stride = e->stride;
-        sh.src_gen_stride = (uint64_t)k * e->stride;
-        sh.rep_row_stride = e->stride;
-        sh.rep_gen_stride = (uint64_t)count * e->stride;
-        int s = qf_encode_batch(e->ctx, &sh, 1, e->d_ring + (size_t)oldest * e->stride, e->d_out,
+        int s;
+        if (e->ring_rot) {
+            s = qf::encode_ring_window(e->ctx, k, first, count, L, e->d_ring, e->stride, oldest, e->d_out,
+                                       e->stride);
+        } else {
+            qf_encode_shape sh{};
+            sh.k = k;
+            sh.r = count;
+            sh.L = L;
+            sh.src_row_stride = e->stride;
+            sh.src_gen_stride = (uint64_t)k * e->stride;
+            sh.rep_row_stride = e->stride;
+            sh.rep_gen_stride = (uint64_t)count * e->stride;
+            s = qf_encode_batch(e->ctx, &sh, 1, e->d_ring + (size_t)oldest * e->stride, e->d_out,
                                 first == 0 ? nullptr : win);
+        }
         if (s != QF_OK) return s;
         hipStream_t st = (hipStream_t)qf_ctx_stream(e->ctx);
         if (out_data) {
