@@ -354,6 +354,16 @@ int qf_packet_to_raw(int is_systematic, const uint8_t *coeffs, uint32_t coeff_le
 int qf_packet_from_raw(const uint8_t *raw, uint32_t raw_len, int *is_systematic,
                        const uint8_t **coeffs, uint32_t *coeff_len,
                        const uint8_t **payload, uint32_t *len);
+/* replaces Packet::from_block (encoder.rs:72-121), the receive path of
+ * core.rs:219-224: a frame of `len` valid bytes in a block of block_len bytes
+ * is parsed in place; the coefficients are copied to coeffs_out (coeffs_cap
+ * bytes) and the payload is moved to the front of the block (copy_within).
+ * QF_EINVAL: len == 0 or len > block_len ("Invalid raw packet length");
+ * QF_ETOOSMALL: coefficient length or coefficients truncated, or longer than
+ * coeffs_cap / the block (where the reference would panic). */
+int qf_packet_from_block(uint8_t *block, uint32_t block_len, uint32_t len, int *is_systematic,
+                         uint8_t *coeffs_out, uint32_t coeffs_cap, uint32_t *coeff_len,
+                         uint32_t *payload_len);
 
 /* ---------------------------------------------------------------------------
  * Wire framing on the device (encoder.rs:18-152): the

@@ -18,6 +18,19 @@
  *                     reduction mod 0x11D); the per-byte FeatureDetector/HashMap
  *                     dispatch of optimize.rs:385-408 is not modelled, so this
  *                     is a lower bound on the reference's cost.
+ *   cpu_encode_clmul_dispatch  the reference as written INCLUDING its per-byte
+ *                     dispatch (timing only, same defective output): every
+ *                     gf_mul (gf_tables.rs:283-300) calls
+ *                     optimize::dispatch_bitslice (optimize.rs:385-408):
+ *                     FeatureDetector::instance() (a Once, i.e. an acquire load,
+ *                     optimize.rs:216-285), then has_feature lookups in a
+ *                     HashMap<CpuFeature, bool> (std RandomState = SipHash-1-3
+ *                     with random keys over the enum discriminant written as
+ *                     isize; a SwissTable probe) -- AVX512F, AVX512VBMI and
+ *                     PCLMULQDQ on an AVX-512 host, AVX2 + PCLMULQDQ or SSE2 +
+ *                     PCLMULQDQ after a miss -- then the chosen member
+ *                     (gf_mul_bitsliced_avx512: 512-bit broadcast + VPCLMULQDQ
+ *                     + fold, gf_tables.rs:76-94; else the SSE2 member).
  * Both take G dense generations (src[g][i][t], rep[g][j][t], row stride L) and
  * split the generations over `threads` pthreads.  Results equal
  * oracle_encode_window (checked by tests/test_oracle_golden.py).
@@ -38,7 +51,7 @@ typedef struct {
     const uint8_t *src;
     uint8_t *rep;
     const uint8_t *coeff; /* r x k */
-    int simd;             /* 0 table, 1 avx2, 2 gfni, 3 clmul (as written) */
+    int simd;             /* 0 table, 1 avx2, 2 gfni, 3 clmul (as written), 4 clmul + dispatch */
 } job_t;
 
 static void encode_table_gen(const job_t *j, uint32_t g) {
@@ -162,6 +175,132 @@ __attribute__((target("sse2,pclmul"))) static void encode_clmul_gen(const job_t 
         }
     }
 }
+
+/* ---- optimize.rs FeatureDetector + HashMap<CpuFeature, bool> model -------- */
+/* CpuFeature discriminants (optimize.rs:186-202 declaration order) */
+enum { F_AVX = 0, F_AVX2, F_SSE2, F_AVX512F, F_AVX512BW, F_AVX512VBMI, F_VAES, F_AESNI, F_PCLMULQDQ, F_NEON };
+
+#define ROTL(x, b) (uint64_t)(((x) << (b)) | ((x) >> (64 - (b))))
+#define SIPROUND                                                           \
+    do {                                                                   \
+        v0 += v1; v1 = ROTL(v1, 13); v1 ^= v0; v0 = ROTL(v0, 32);          \
+        v2 += v3; v3 = ROTL(v3, 16); v3 ^= v2;                             \
+        v0 += v3; v3 = ROTL(v3, 21); v3 ^= v0;                             \
+        v2 += v1; v1 = ROTL(v1, 17); v1 ^= v2; v2 = ROTL(v2, 32);          \
+    } while (0)
+
+/* SipHash-1-3 of one 8-byte message (Hash::hash of a fieldless enum writes
+ * its discriminant as isize) */
+static inline uint64_t siphash13_u64(uint64_t k0, uint64_t k1, uint64_t m) {
+    uint64_t v0 = k0 ^ 0x736f6d6570736575ULL, v1 = k1 ^ 0x646f72616e646f6dULL;
+    uint64_t v2 = k0 ^ 0x6c7967656e657261ULL, v3 = k1 ^ 0x7465646279746573ULL;
+    v3 ^= m;
+    SIPROUND;
+    v0 ^= m;
+    const uint64_t b = (uint64_t)8 << 56; /* length byte, no tail */
+    v3 ^= b;
+    SIPROUND;
+    v0 ^= b;
+    v2 ^= 0xff;
+    SIPROUND;
+    SIPROUND;
+    SIPROUND;
+    return v0 ^ v1 ^ v2 ^ v3;
+}
+
+typedef struct {
+    uint64_t k0, k1;          /* RandomState keys */
+    uint8_t ctrl[16];         /* SwissTable control bytes (h2 tag or 0xFF empty) */
+    uint8_t key[16];
+    uint8_t val[16];
+} feature_map;
+
+static feature_map g_features;
+static int g_detector_state; /* Once: 0 new, 2 complete */
+static int g_have_vpclmul;   /* this host can run the 512-bit member (avx512dq + vpclmulqdq) */
+
+static void map_insert(feature_map *m, uint8_t f, uint8_t v) {
+    const uint64_t h = siphash13_u64(m->k0, m->k1, f);
+    uint32_t pos = (uint32_t)h & 15;
+    while (m->ctrl[pos] != 0xFF) pos = (pos + 1) & 15;
+    m->ctrl[pos] = (uint8_t)(h >> 57);
+    m->key[pos] = f;
+    m->val[pos] = v;
+}
+
+/* FeatureDetector::instance (optimize.rs:216-285): Once + detection */
+static const feature_map *detector_instance(void) {
+    if (__atomic_load_n(&g_detector_state, __ATOMIC_ACQUIRE) != 2) {
+        feature_map *m = &g_features;
+        m->k0 = 0x0706050403020100ULL ^ (uint64_t)(uintptr_t)&g_features;
+        m->k1 = 0x0f0e0d0c0b0a0908ULL ^ (uint64_t)(uintptr_t)&g_detector_state;
+        memset(m->ctrl, 0xFF, sizeof m->ctrl);
+        map_insert(m, F_AVX, (uint8_t)!!__builtin_cpu_supports("avx"));
+        map_insert(m, F_AVX2, (uint8_t)!!__builtin_cpu_supports("avx2"));
+        map_insert(m, F_SSE2, (uint8_t)!!__builtin_cpu_supports("sse2"));
+        map_insert(m, F_AVX512F,
+                   (uint8_t)(__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw")));
+        map_insert(m, F_AVX512BW, (uint8_t)!!__builtin_cpu_supports("avx512bw"));
+        map_insert(m, F_AVX512VBMI, (uint8_t)!!__builtin_cpu_supports("avx512vbmi"));
+        map_insert(m, F_VAES, (uint8_t)!!__builtin_cpu_supports("vaes"));
+        map_insert(m, F_AESNI, (uint8_t)!!__builtin_cpu_supports("aes"));
+        map_insert(m, F_PCLMULQDQ, (uint8_t)!!__builtin_cpu_supports("pclmul"));
+        g_have_vpclmul = __builtin_cpu_supports("avx512dq") && __builtin_cpu_supports("vpclmulqdq");
+        __atomic_store_n(&g_detector_state, 2, __ATOMIC_RELEASE);
+    }
+    return &g_features;
+}
+
+/* FeatureDetector::has_feature (optimize.rs:288-290): hash, probe, compare */
+static inline int has_feature(const feature_map *m, uint8_t f) {
+    const uint64_t h = siphash13_u64(m->k0, m->k1, f);
+    const uint8_t tag = (uint8_t)(h >> 57);
+    uint32_t pos = (uint32_t)h & 15;
+    for (int n = 0; n < 16; ++n, pos = (pos + 1) & 15) {
+        if (m->ctrl[pos] == 0xFF) return 0;
+        if (m->ctrl[pos] == tag && m->key[pos] == f) return m->val[pos];
+    }
+    return 0;
+}
+
+/* gf_tables.rs:76-94 gf_mul_bitsliced_avx512 as written */
+__attribute__((target("avx512f,avx512dq,avx512vbmi,vpclmulqdq,pclmul"))) static uint8_t clmul_fold_avx512(uint8_t a,
+                                                                                             uint8_t b) {
+    const __m512i va = _mm512_broadcast_i64x2(_mm_set_epi64x(0, a));
+    const __m512i vb = _mm512_broadcast_i64x2(_mm_set_epi64x(0, b));
+    const __m512i prod = _mm512_clmulepi64_epi128(va, vb, 0x00);
+    uint16_t t = (uint16_t)_mm_extract_epi16(_mm512_castsi512_si128(prod), 0);
+    t ^= t >> 8;
+    t ^= t >> 4;
+    t ^= t >> 2;
+    t ^= t >> 1;
+    return (uint8_t)(t & 0xFF);
+}
+
+/* gf_tables.rs:283-300 gf_mul through optimize.rs:385-408 dispatch_bitslice */
+__attribute__((noinline)) static uint8_t gf_mul_dispatched(uint8_t a, uint8_t b) {
+    const feature_map *d = detector_instance();
+    if (has_feature(d, F_AVX512F) && has_feature(d, F_AVX512VBMI) && has_feature(d, F_PCLMULQDQ))
+        return g_have_vpclmul ? clmul_fold_avx512(a, b) : clmul_fold(a, b);
+    if (has_feature(d, F_AVX2) && has_feature(d, F_PCLMULQDQ)) return clmul_fold(a, b);
+    if (has_feature(d, F_SSE2) && has_feature(d, F_PCLMULQDQ)) return clmul_fold(a, b);
+    return oracle_gf_mul(a, b);
+}
+
+static void encode_clmul_dispatch_gen(const job_t *j, uint32_t g) {
+    const uint8_t *s = j->src + (size_t)g * j->k * j->L;
+    uint8_t *o = j->rep + (size_t)g * j->r * j->L;
+    for (uint32_t q = 0; q < j->r; ++q) {
+        uint8_t *acc = o + (size_t)q * j->L;
+        memset(acc, 0, j->L);
+        for (uint32_t i = 0; i < j->k; ++i) {
+            const uint8_t c = j->coeff[(size_t)q * j->k + i];
+            if (c == 0) continue;
+            const uint8_t *x = s + (size_t)i * j->L;
+            for (uint32_t t = 0; t < j->L; ++t) acc[t] ^= gf_mul_dispatched(c, x[t]); /* gf_mul_add */
+        }
+    }
+}
 #endif
 
 static void *worker(void *arg) {
@@ -178,6 +317,10 @@ static void *worker(void *arg) {
         }
         if (j->simd == 3) {
             encode_clmul_gen(j, g);
+            continue;
+        }
+        if (j->simd == 4) {
+            encode_clmul_dispatch_gen(j, g);
             continue;
         }
 #endif
@@ -257,4 +400,14 @@ int cpu_encode_clmul(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8
                      uint32_t threads) {
     if (!cpu_has_pclmul()) return -3;
     return run(k, r, L, G, src, rep, threads, 3);
+}
+
+/* timing only: the as-written path with its per-byte dispatch (optimize.rs:385-408) */
+int cpu_encode_clmul_dispatch(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src, uint8_t *rep,
+                              uint32_t threads) {
+    if (!cpu_has_pclmul()) return -3;
+#if defined(__x86_64__)
+    (void)detector_instance();
+#endif
+    return run(k, r, L, G, src, rep, threads, 4);
 }

@@ -98,6 +98,24 @@ int oracle_decode_generation_as_written(uint32_t k, uint32_t L, uint32_t n_rows,
                                         const uint8_t *row_coeffs,
                                         uint8_t *out, size_t out_stride);
 
+/* ---- Packet framing (qf_oracle_wire.c, encoder.rs:18-152) --------------
+ * One code per reference error string: */
+#define ORACLE_FR_EMPTY (-10)             /* "Raw data is empty" (encoder.rs:25) */
+#define ORACLE_FR_NO_COEFF_LEN (-11)      /* "Buffer too short for coefficient length" */
+#define ORACLE_FR_COEFF_TRUNCATED (-12)   /* "Buffer too short for coefficients" */
+#define ORACLE_FR_POOL_TOO_SMALL (-13)    /* "Buffer from pool is too small" (encoder.rs:55) */
+#define ORACLE_FR_INVALID_LEN (-14)       /* "Invalid raw packet length" (encoder.rs:81) */
+#define ORACLE_FR_BUFFER_TOO_SHORT (-15)  /* quiche::Error::BufferTooShort (encoder.rs:130) */
+#define ORACLE_FR_PANIC (-16)             /* coefficient vector longer than a pool block */
+int oracle_packet_to_raw(int is_systematic, int has_coeffs, const uint8_t *coeffs,
+                         uint32_t coeff_len, int has_data, const uint8_t *data, uint32_t len,
+                         uint8_t *buffer, size_t buffer_len, size_t *written);
+int oracle_packet_from_raw(const uint8_t *raw, size_t raw_len, size_t block_size,
+                           int *is_systematic, uint32_t *coeff_len, size_t *coeff_off,
+                           size_t *payload_off, size_t *len);
+int oracle_packet_from_block(uint8_t *block, size_t block_len, size_t len, int *is_systematic,
+                             uint8_t *coeffs_out, uint32_t *coeff_len, size_t *payload_len);
+
 /* Deterministic synthetic payload: byte t of the flat buffer is
  * byte (t & 7) of splitmix64(seed + (t >> 3)). */
 void oracle_fill_splitmix(uint8_t *buf, size_t n, uint64_t seed, uint64_t word_offset);
@@ -114,6 +132,8 @@ int cpu_encode_gfni(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_
                     uint8_t *rep, uint32_t threads);
 int cpu_encode_clmul(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
                      uint8_t *rep, uint32_t threads);
+int cpu_encode_clmul_dispatch(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *src,
+                              uint8_t *rep, uint32_t threads);
 int cpu_has_gfni(void);
 int cpu_has_pclmul(void);
 

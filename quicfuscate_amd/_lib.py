@@ -110,6 +110,7 @@ _SIGS = {
     "qf_decoder_get_decoded_packets": (_I, [_P, _P, _U32, _P, _P, _P]),
     "qf_packet_to_raw": (_I, [_I, _P, _U32, _P, _U32, _P, _U32, _P]),
     "qf_packet_from_raw": (_I, [_P, _U32, _P, _P, _P, _P, _P]),
+    "qf_packet_from_block": (_I, [_P, _U32, _U32, _P, _P, _U32, _P, _P]),
     "qf_gf16_mul": (ctypes.c_uint16, [ctypes.c_uint16, ctypes.c_uint16]),
     "qf_gf16_inv": (_I, [ctypes.c_uint16, _P]),
     "qf_cauchy16_coeffs": (_I, [_U32, _U32, _P]),

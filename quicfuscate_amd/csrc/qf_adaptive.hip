@@ -457,6 +457,9 @@ int qf_adaptive_on_send(qf_adaptive* a, uint64_t id, const uint8_t* data, uint32
     uint32_t need = 1 + (a->cur.has_enc() ? a->cur.n - a->cur.k : 0) +
                     (fade_repairs && a->fade.has_enc() ? a->fade.n - a->fade.k : 0);
     if (need > out_cap) return QF_ETOOSMALL;
+    // repairs are window[0].len <= max_len bytes long: check the stride before
+    // the windows advance, so a failing call leaves no state behind
+    if (need > 1 && out_stride < a->cfg.max_len) return QF_ETOOSMALL;
     if (out_coeffs) {
         uint32_t cmax = a->cur.has_enc() ? a->cur.coeff_bytes() : 0;
         if (fade_repairs && a->fade.has_enc() && a->fade.coeff_bytes() > cmax) cmax = a->fade.coeff_bytes();

@@ -1354,4 +1354,26 @@ int qf_packet_from_raw(const uint8_t* raw, uint32_t raw_len, int* is_systematic,
     return QF_OK;
 }
 
+int qf_packet_from_block(uint8_t* block, uint32_t block_len, uint32_t len, int* is_systematic,
+                         uint8_t* coeffs_out, uint32_t coeffs_cap, uint32_t* coeff_len, uint32_t* payload_len) {
+    if (!block || !is_systematic || !coeff_len || !payload_len) return QF_EINVAL;
+    if (len == 0 || len > block_len) return QF_EINVAL;  // "Invalid raw packet length" (encoder.rs:78-82)
+    const int sys = block[0] == 1;
+    uint32_t off = 1, cl = 0;
+    if (!sys) {
+        if (len < 3) return QF_ETOOSMALL;  // coefficient length missing (encoder.rs:88-92)
+        cl = ((uint32_t)block[1] << 8) | block[2];
+        off = 3;
+        if (len < off + cl) return QF_ETOOSMALL;  // coefficients truncated (encoder.rs:95-99)
+        if (cl > block_len || cl > coeffs_cap || (cl && !coeffs_out)) return QF_ETOOSMALL;
+        if (cl) memcpy(coeffs_out, block + off, cl);
+        off += cl;
+    }
+    memmove(block, block + off, len - off);  // copy_within(payload_offset..len, 0) (encoder.rs:108-110)
+    *is_systematic = sys;
+    *coeff_len = cl;
+    *payload_len = len - off;
+    return QF_OK;
+}
+
 }  // extern "C"

@@ -55,6 +55,7 @@ struct qf_decoder {
     std::vector<uint16_t> index;   // k: source index (< k) or k (repair)
     std::vector<uint8_t> coeffs;   // k * k (repair rows)
     std::vector<int32_t> sys_slot; // per source index: accepted slot or -1
+    std::vector<uint64_t> sys_id;  // per source index: the received packet's own id
     uint32_t accepted = 0;
     // decoded output, source index order
     std::vector<uint8_t> out;      // k * stride
@@ -227,6 +228,7 @@ int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) 
     d->index.assign(k, 0);
     d->coeffs.assign((size_t)k * k, 0);
     d->sys_slot.assign(k, -1);
+    d->sys_id.assign(k, 0);
     const uint32_t emax = k < 128 ? k : 128;
     bool ok = hipMalloc(&d->d_rows, (size_t)k * d->stride) == hipSuccess &&
               hipMalloc(&d->d_coeffs, (size_t)k * k) == hipSuccess &&
@@ -367,6 +369,7 @@ int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const u
         const uint32_t idx = (uint32_t)(id % k);  // decoder.rs:684
         if (d->sys_slot[idx] >= 0) return d->decoded ? 1 : 0;  // duplicate (687-691)
         d->sys_slot[idx] = (int32_t)q;
+        d->sys_id[idx] = id;  // systematic_packets[index] = Some(packet) keeps packet.id (decoder.rs:688)
         d->index[q] = (uint16_t)idx;
         memset(&d->coeffs[(size_t)q * k], 0, k);
     } else {
@@ -402,7 +405,9 @@ int qf_decoder_get_decoded_packets(qf_decoder* d, uint8_t* out_data, uint32_t ou
     for (uint32_t i = 0; i < d->k; ++i) {
         if (out_data) memcpy(out_data + (size_t)i * out_stride, &d->out[(size_t)i * d->stride], d->out_len[i]);
         if (out_len) out_len[i] = d->out_len[i];
-        if (out_ids) out_ids[i] = i;  // decoder.rs:771
+        // a received systematic packet keeps its own id (decoder.rs:688); a
+        // reconstructed one gets id = i (decoder.rs:771)
+        if (out_ids) out_ids[i] = d->sys_slot[i] >= 0 ? d->sys_id[i] : i;
     }
     *count = d->k;
     d->drained = true;  // get_decoded_packets take()s the packets

@@ -177,6 +177,23 @@ def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_
           "encode_batch")
 
 
+def encode_batch_host(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, rep_row_stride: int, G: int,
+                      coeff: Optional[bytes] = None, ctx: Optional[Context] = None) -> None:
+    """qf_encode_batch_host: encode_batch with src / rep in host memory (torch
+    CPU tensors, pinned recommended; dense generations); synchronous.  The
+    send side of core.rs:252-317, starting from UDP datagrams in host memory."""
+    ctx = ctx or default_context()
+    sh = L.EncodeShape(k, r, Lb, 0, src_row_stride, k * src_row_stride, rep_row_stride, r * rep_row_stride)
+    cbuf = None
+    if coeff is not None:
+        if len(coeff) != k * r:
+            raise ValueError("coeff must be r*k bytes")
+        cbuf = (ctypes.c_uint8 * len(coeff)).from_buffer_copy(coeff)
+    check(L._lib().qf_encode_batch_host(ctx.handle, ctypes.byref(sh), G, _ptr(src), _ptr(rep),
+                                         ctypes.cast(cbuf, ctypes.c_void_p) if cbuf is not None else None),
+          "encode_batch_host")
+
+
 def decode_batch_host(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int, Lb: int, *,
                       max_rows: int, row_stride: int, rows_gen_stride: int, rec_row_stride: int,
                       rec_gen_stride: int, G: int, n_rows=None, row_coeffs=None,
@@ -280,10 +297,27 @@ class Packet:
         off = pptr.value - base
         payload = bytearray(raw[off: off + plen.value])
         if pool is not None:
+            if len(payload) > pool.block_size:   # "Buffer from pool is too small" (encoder.rs:52-56)
+                raise QfError(L.QF_ETOOSMALL, "from_raw: pool buffer too small")
             block = pool.alloc()
             block[: len(payload)] = payload
             payload = block
         return Packet(pid, payload, plen.value, bool(sys_.value), coeffs, clen.value)
+
+    @staticmethod
+    def from_block(pid: int, block: bytearray, length: int) -> "Packet":
+        """encoder.rs:72-121: parse a received frame held in a pool block of
+        `length` valid bytes; the payload is moved to the front of the same
+        block (qf_packet_from_block)."""
+        lib = L._lib()
+        buf = (ctypes.c_uint8 * max(1, len(block))).from_buffer(block) if len(block) else (ctypes.c_uint8 * 1)()
+        sys_ = ctypes.c_int(0)
+        coeffs = (ctypes.c_uint8 * max(1, len(block)))()
+        clen, plen = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        check(lib.qf_packet_from_block(buf, len(block), length, ctypes.byref(sys_), coeffs, len(block),
+                                       ctypes.byref(clen), ctypes.byref(plen)), "from_block")
+        co = bytes(coeffs)[: clen.value] if not sys_.value else None
+        return Packet(pid, block, plen.value, bool(sys_.value), co, clen.value)
 
 
 class Encoder:

@@ -31,9 +31,14 @@ def halo_exchange(torch, dist, rows, k: int, rank: int, world: int):
         return ext
     # gloo moves host tensors only: stage device rows through the host there
     host = dist.get_backend() == "gloo" and rows.device.type != "cpu"
+    # every rank learns whether any sender is short BEFORE the first send /
+    # recv: a rank raising alone would leave its successor blocked in recv
+    ok = torch.tensor([1 if (rank + 1 == world or n >= h) else 0], dtype=torch.int32,
+                      device="cpu" if (host or rows.device.type == "cpu") else rows.device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        raise ValueError("sliding shard smaller than the window halo on some rank")
     if rank + 1 < world:
-        if n < h:
-            raise ValueError("sliding shard smaller than the window halo")
         out = rows[n - h:].contiguous()
         dist.send(out.cpu() if host else out, dst=rank + 1)
     if rank > 0:

@@ -20,6 +20,7 @@ _lib.cpu_encode_avx2.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32
 _lib.cpu_has_avx2.argtypes = []
 _lib.cpu_encode_gfni.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
 _lib.cpu_encode_clmul.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
+_lib.cpu_encode_clmul_dispatch.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
 _lib.cpu_has_gfni.argtypes = []
 _lib.cpu_has_pclmul.argtypes = []
 _lib.oracle_gf_mul.restype = ctypes.c_uint8
@@ -99,14 +100,16 @@ def encode(src: np.ndarray, r: int, coeff: np.ndarray | None = None, L: int | No
 
 def cpu_encode(kind: str, src: np.ndarray, r: int, threads: int = 1) -> np.ndarray:
     """Comparison encoders of oracle/cpu_variants.c over dense generations:
-    src (G, k, L) -> (G, r, L).  kind: "table", "avx2", "gfni" or "clmul"
-    (the reference's as-written per-byte PCLMULQDQ fold: timing only, its
-    output is the defective fold product)."""
+    src (G, k, L) -> (G, r, L).  kind: "table", "avx2", "gfni", "clmul" (the
+    reference's as-written per-byte PCLMULQDQ fold without its dispatch: a
+    lower bound) or "clmul_dispatch" (the same, paying optimize.rs:385-408's
+    per-byte FeatureDetector + HashMap dispatch).  Both clmul kinds are timing
+    only: their output is the defective fold product, SURVEY F3."""
     src = np.ascontiguousarray(src, dtype=np.uint8)
     G, k, L = src.shape
     rep = np.zeros((G, r, L), np.uint8)
     fn = {"table": _lib.cpu_encode_table, "avx2": _lib.cpu_encode_avx2, "gfni": _lib.cpu_encode_gfni,
-          "clmul": _lib.cpu_encode_clmul}[kind]
+          "clmul": _lib.cpu_encode_clmul, "clmul_dispatch": _lib.cpu_encode_clmul_dispatch}[kind]
     s = fn(k, r, L, G, _p(src), _p(rep), threads)
     if s != 0:
         raise ValueError(f"cpu_encode({kind}) status {s}")
@@ -120,7 +123,7 @@ def has_avx2() -> bool:
 def has_cpu_kind(kind: str) -> bool:
     """Whether this host can run cpu_encode(kind)."""
     return {"table": lambda: True, "avx2": _lib.cpu_has_avx2, "gfni": _lib.cpu_has_gfni,
-            "clmul": _lib.cpu_has_pclmul}[kind]() != 0
+            "clmul": _lib.cpu_has_pclmul, "clmul_dispatch": _lib.cpu_has_pclmul}[kind]() != 0
 
 
 def encode_clmul_fold(src: np.ndarray, r: int) -> np.ndarray:
@@ -156,6 +159,58 @@ def fill_splitmix(n: int, seed: int, word_offset: int = 0) -> np.ndarray:
     out = np.zeros(n, np.uint8)
     _lib.oracle_fill_splitmix(_p(out), n, seed, word_offset)
     return out
+
+
+# ---- packet framing (oracle/qf_oracle_wire.c, encoder.rs:18-152) -------------
+FR_EMPTY, FR_NO_COEFF_LEN, FR_COEFF_TRUNCATED, FR_POOL_TOO_SMALL = -10, -11, -12, -13
+FR_INVALID_LEN, FR_BUFFER_TOO_SHORT, FR_PANIC = -14, -15, -16
+_SZP = ctypes.POINTER(ctypes.c_size_t)
+_lib.oracle_packet_to_raw.argtypes = [ctypes.c_int, ctypes.c_int, _P, _U32, ctypes.c_int, _P, _U32, _P, _SZ, _P]
+_lib.oracle_packet_from_raw.argtypes = [_P, _SZ, _SZ, _P, _P, _P, _P, _P]
+_lib.oracle_packet_from_block.argtypes = [_P, _SZ, _SZ, _P, _P, _P, _P]
+
+
+def packet_to_raw(is_systematic: bool, payload: bytes, coeffs: bytes | None = None, buffer_len: int | None = None,
+                  has_data: bool = True, fill: int = 0):
+    """encoder.rs:124-152 -> (status, frame bytes).  coeffs None = no
+    coefficient block (the Option is None)."""
+    payload = bytes(payload)
+    cb = np.frombuffer(coeffs, np.uint8).copy() if coeffs else np.zeros(1, np.uint8)
+    pb = np.frombuffer(payload, np.uint8).copy() if payload else np.zeros(1, np.uint8)
+    need = len(payload) + 1 + (2 + len(coeffs) if coeffs is not None else 0)
+    n = need if buffer_len is None else buffer_len
+    buf = np.full(max(n, 1), fill, np.uint8)
+    w = ctypes.c_size_t(0)
+    s = _lib.oracle_packet_to_raw(1 if is_systematic else 0, 0 if coeffs is None else 1, _p(cb),
+                                  0 if coeffs is None else len(coeffs), 1 if has_data else 0, _p(pb), len(payload),
+                                  _p(buf), n, ctypes.byref(w))
+    return s, (buf[: w.value].tobytes() if s == 0 else b"")
+
+
+def packet_from_raw(raw: bytes, block_size: int = 4096):
+    """encoder.rs:18-68 -> (status, is_systematic, coeffs, payload)."""
+    raw = bytes(raw)
+    rb = np.frombuffer(raw, np.uint8).copy() if raw else np.zeros(1, np.uint8)
+    sy, cl = ctypes.c_int(0), ctypes.c_uint32(0)
+    co, po, ln = ctypes.c_size_t(0), ctypes.c_size_t(0), ctypes.c_size_t(0)
+    s = _lib.oracle_packet_from_raw(_p(rb), len(raw), block_size, ctypes.byref(sy), ctypes.byref(cl),
+                                    ctypes.byref(co), ctypes.byref(po), ctypes.byref(ln))
+    if s:
+        return s, None, None, None
+    coeffs = raw[co.value: co.value + cl.value] if not sy.value else None
+    return s, bool(sy.value), coeffs, raw[po.value: po.value + ln.value]
+
+
+def packet_from_block(block: bytes, length: int):
+    """encoder.rs:72-121 -> (status, is_systematic, coeffs, payload_len, block after the move)."""
+    b = np.frombuffer(bytes(block), np.uint8).copy()
+    co = np.zeros(len(block) + 1, np.uint8)
+    sy, cl, pl = ctypes.c_int(0), ctypes.c_uint32(0), ctypes.c_size_t(0)
+    s = _lib.oracle_packet_from_block(_p(b), len(block), length, ctypes.byref(sy), _p(co), ctypes.byref(cl),
+                                      ctypes.byref(pl))
+    if s:
+        return s, None, None, None, None
+    return s, bool(sy.value), (co[: cl.value].tobytes() if not sy.value else None), pl.value, b.tobytes()
 
 
 # ---- GF(2^16) Extreme mode (oracle/qf_oracle16.c) ---------------------------

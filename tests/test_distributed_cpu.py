@@ -133,3 +133,42 @@ def test_sliding_halo_exchange_gloo():
     assert all(ok for *_, ok in res)
     ends = [t for _, lo, hi, first, nwin, _ in res for t in range(first, first + nwin)]
     assert ends == list(range(8 - 1, 37))
+
+
+def _short_halo_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from quicfuscate_amd import stream_shard as ss
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        k = 8
+        n = 3 if rank == 0 else 10          # rank 0 cannot send a k - 1 = 7 packet halo
+        try:
+            ss.halo_exchange(torch, dist, torch.zeros((n, 16), dtype=torch.uint8), k, rank, world)
+            q.put((rank, "no error"))
+        except ValueError:
+            q.put((rank, "raised"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_halo_short_shard_raises_on_every_rank():
+    """A shard smaller than the halo is an error on ALL ranks before any
+    send / recv (a lone raise would leave the successor blocked in recv)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_short_halo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res == [(0, "raised"), (1, "raised")]

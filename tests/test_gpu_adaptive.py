@@ -108,13 +108,12 @@ def test_extreme_mode_gf16_codec(qf, oracle, gpu_ctx, window, L_, lost):
     assert len(reps) == r
     C = oracle.cauchy16(k, r)
     check = sorted(set([0, 1, r - 1] + rng.integers(0, r, 5).tolist()))
-    want = oracle.encode16(src, r, C[check]) if window <= 64 else None
+    want = oracle.encode16(src, r, C[check])   # every window size, k = 1,024 included
     for q, j in enumerate(check):
         p = reps[j]
         assert not p.is_systematic and p.id == k + j and p.coeff_len == 2 * k
         assert bytes(p.coefficients) == b"".join(int(c).to_bytes(2, "big") for c in C[j])
-        if want is not None:
-            assert p.payload() == want[q].tobytes(), j
+        assert p.payload() == want[q].tobytes(), j
     got = []
     for p in [qf.Packet(i, bytearray(src[i].tobytes()), L_, True) for i in range(k) if i not in set(lost)] + reps:
         got += rcv.on_receive(p)

@@ -156,3 +156,59 @@ def test_empty_and_degenerate_batches(qf, gpu_ctx):
     assert dec(0, 16, 1200, 80, 1) == L.QF_EINVAL
     assert dec(64, 16, 1200, 80, 1) == L.QF_EINVAL  # G > 0 with null buffers
     gpu_ctx.sync()
+
+
+def test_decoded_packet_ids_follow_reference_rule(qf, gpu_ctx):
+    """decoder.rs:688 / 771: a received systematic packet keeps its own id; a
+    reconstructed one gets id = i.  Stream ids that are not 0..k-1 (here
+    1000..) must survive the decode unchanged."""
+    k, n = 8, 12
+    pool = qf.MemoryPool(32, 64)
+    enc = qf.Encoder(k, n, max_len=64)
+    pk = []
+    for i in range(k):
+        p = make_packet(qf, 1000 + i, 40 + i, pool)   # 1000 % 8 == 0: column i
+        enc.add_source_packet(p.clone())
+        pk.append(p)
+    reps = [enc.generate_repair_packet(j, pool) for j in range(n - k)]
+    lost = {2, 5}
+    dec = qf.Decoder(k, pool)
+    for i, p in enumerate(pk):
+        if i not in lost:
+            dec.add_packet(p.clone())
+    for rp in reps[: len(lost)]:
+        dec.add_packet(rp)
+    assert dec.is_decoded
+    out = dec.get_decoded_packets()
+    assert [p.id for p in out] == [i if i in lost else 1000 + i for i in range(k)]
+    assert [p.data[0] for p in out] == [40 + i for i in range(k)]
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+@pytest.mark.parametrize("k", [16, 64, 128])
+def test_ring_encoder_every_rotation(qf, oracle, gpu_ctx, monkeypatch, small, k):
+    """The encoder object's window lives in a ring read rotated by the
+    small-batch kernel (QF_ENCODE_SMALL=1) or doubled for the bit-sliced
+    kernels (=0).  After 3k packets every rotation has been passed; the
+    repairs of each window must equal the oracle's encode of the last k
+    packets (decoder.rs:164-275)."""
+    import numpy as np
+
+    monkeypatch.setenv("QF_ENCODE_SMALL", small)
+    Lb, r = 1200, 4
+    enc = qf.Encoder(k, k + r, max_len=Lb)
+    rng = np.random.default_rng(k)
+    data = rng.integers(0, 256, (3 * k, Lb), dtype=np.uint8)
+    pool = qf.MemoryPool(4, Lb)
+    checked = 0
+    for t in range(3 * k):
+        enc.add_source_packet(qf.Packet(t, bytearray(data[t].tobytes()), Lb, True))
+        if t + 1 < k or (t % 7 != 3 and t != 3 * k - 1):
+            continue
+        want = oracle.encode(data[t + 1 - k: t + 1], r)
+        for j in range(r):
+            rp = enc.generate_repair_packet(j, pool)
+            assert bytes(rp.data[:Lb]) == want[j].tobytes(), (t, j)
+            assert rp.id == t + 1 + j
+        checked += 1
+    assert checked >= 6

@@ -1,6 +1,8 @@
-"""Wire framing on the device (encoder.rs:18-152): frames byte-equal to
-Packet::to_raw, and frames -> parse -> decode recovers the sources, with
-lost, reordered and malformed frames."""
+"""Wire framing on the device (encoder.rs:18-152): frames byte-equal to the
+oracle's restatement of Packet::to_raw (oracle/qf_oracle_wire.c), parse
+statuses and payloads equal to the oracle's Packet::from_raw, and frames ->
+parse -> decode recovers the sources, with lost, reordered and malformed
+frames."""
 import ctypes
 
 import numpy as np
@@ -46,9 +48,10 @@ def test_frames_equal_to_raw(qf, oracle, gpu_ctx, k, r, Lb):
     for g in range(G):
         for i in range(k + r):
             if i < k:
-                want = qf.Packet(i, bytearray(src_np[g, i].tobytes()), Lb, True).to_raw()
+                st, want = oracle.packet_to_raw(True, src_np[g, i].tobytes())
             else:
-                want = qf.Packet(i, bytearray(rep_np[g, i - k].tobytes()), Lb, False, bytes(C[i - k]), k).to_raw()
+                st, want = oracle.packet_to_raw(False, rep_np[g, i - k].tobytes(), bytes(C[i - k]))
+            assert st == 0
             assert flen[g, i] == len(want)
             assert frames[g, i, : len(want)].tobytes() == want, (g, i)
             assert (frames[g, i, len(want):] == 0xCC).all()
@@ -112,14 +115,29 @@ def test_frames_parse_decode_round_trip(qf, oracle, gpu_ctx):
     ri = ridx.cpu().numpy().view(np.uint16).reshape(G, max_rows)
     nr = nrows.cpu().numpy()
     rw = rows.cpu().numpy().reshape(G, max_rows, Lb)
+    C = oracle.cauchy(k, r)
     for g in range(G):
         valid = [e for e in expect[g] if e[3] == 0]
         assert list(st[g, : n_fr[g]]) == [e[3] for e in expect[g]]
+        # every status and payload follows the oracle's Packet::from_raw, plus the
+        # batch rules (Cauchy row of this (k, r); payload <= L)
+        for s_, (fb, ln, pid, want_st, _) in enumerate(expect[g]):
+            os_, osys, oco, opay = oracle.packet_from_raw(fb[:ln].tobytes())
+            if os_:
+                exp = {oracle.FR_EMPTY: L.QF_EINVAL}.get(os_, L.QF_ETOOSMALL)
+            elif not osys and (len(oco) != k or not any(bytes(C[j]) == oco for j in range(r))):
+                exp = L.QF_ERANGE
+            elif len(opay) > Lb:
+                exp = L.QF_EINVAL
+            else:
+                exp = 0
+            assert st[g, s_] == exp == want_st, (g, s_)
         assert nr[g] == len(valid)
         for s, (fb, ln, pid, _, i) in enumerate(valid):
             assert ri[g, s] == (pid % k if i < k else i)
             payload = src_np[g, i] if i < k else rep_np[g, i - k]
             assert (rw[g, s] == payload).all()
+            assert rw[g, s].tobytes() == oracle.packet_from_raw(fb[:ln].tobytes())[3].ljust(Lb, b"\0")
     # decode straight from the parsed rows
     emax = min(k, r)
     rec = torch.empty(G * emax * Lb, dtype=torch.uint8, device=dev)

@@ -162,3 +162,5 @@ def test_cpu_clmul_as_written_is_the_defective_fold(oracle):
     for g in range(2):
         assert (got[g] == oracle.encode_clmul_fold(src[g], r)).all()
     assert not (got[0] == oracle.encode(src[0], r)).all()
+    # the same product through the per-byte dispatch model (optimize.rs:385-408)
+    assert (oracle.cpu_encode("clmul_dispatch", src, r, 2) == got).all()
