@@ -68,6 +68,7 @@ def _worker(rank, world, port, q):
     out = bench.reduce_max(torch, dist, vals, world, "cpu")
     folds = bench.gather_folds(torch, dist, (0xF000000000000000 | rank), world, "cpu")
     assert folds == [0xF000000000000000, 0xF000000000000001]
+    assert bench.gather_flags(torch, dist, rank == 0, world, "cpu") == [1, 0]
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank, lo, hi, out))

@@ -28,3 +28,11 @@ def test_bench_two_ranks_gloo_rehearsal():
     folds = d["repair_xor_fold_by_rank"]
     assert len(folds) == 2 and folds[0] != folds[1]
     assert d["value"] > 0 and d["ms_per_step"] > 0
+    # C4 shape at N > 1 (reduced G here): per-rank oracle samples, the process
+    # group's own world size, and the sliding-window halo leg over it
+    assert d["config"]["workload"].startswith("C4") and d["config"]["generations_per_gpu"] == 2048
+    assert d["rank_oracle_sample"]["pass_by_rank"] == [True, True]
+    assert d["rank_oracle_sample"]["generations_per_rank"] >= 64
+    assert d["process_group"]["world_size"] == 2 and d["process_group"]["backend"] == "gloo"
+    sh = d["sliding_halo"]
+    assert sh["first_window_matches"] and sh["halo_packets"] == 63 and sh["ms_per_step_max"] > 0
