@@ -202,6 +202,44 @@ int qf_decode_batch_host(qf_ctx *ctx, const qf_decode_shape *shape, uint32_t G,
                          int32_t *status_host);
 
 /* ---------------------------------------------------------------------------
+ * Heterogeneous batches (SURVEY 8(b) qf_gen_desc): one call over generations
+ * whose (k, r, L) and placement differ per generation -- the ASW-RLNC-X mix
+ * of window sizes (adaptive.rs:124-153, BASELINE config C5).  Generations
+ * are grouped by shape inside the call; each group runs the batch kernels
+ * above with per-generation offset tables (no payload is copied).
+ * replaces per-generation Encoder::generate_repair_packet (decoder.rs:171-275)
+ * / Decoder::add_packet + try_decode (decoder.rs:678-791) calls.
+ * ------------------------------------------------------------------------- */
+typedef struct qf_gen_desc {
+    uint32_t k, r, L;        /* generation size, repairs (k + r <= 256), payload bytes */
+    uint32_t flags;          /* QF_ENCODE_ZERO_TAIL: bytes [L, 16*ceil8(L/16)) of each repair row may be zeroed */
+    uint64_t src_offset;     /* source row i at src_dev + src_offset + i * src_row_stride */
+    uint64_t src_row_stride;
+    uint64_t rep_offset;     /* repair row j at rep_dev + rep_offset + j * rep_row_stride */
+    uint64_t rep_row_stride;
+} qf_gen_desc;
+/* Offsets and strides are multiples of 16; QF_ERANGE if any k + r > 256. */
+int qf_encode_batch_desc(qf_ctx *ctx, const qf_gen_desc *gens_host, uint32_t G, const uint8_t *src_dev,
+                         uint8_t *rep_dev);
+
+typedef struct qf_dec_desc {
+    uint32_t k, r, L;
+    uint32_t n_rows;            /* received rows of this generation (<= 255), arrival order */
+    uint64_t rows_offset;       /* received row s at rows_dev + rows_offset + s * row_stride */
+    uint64_t row_stride;
+    uint64_t row_index_offset;  /* its n_rows indices (< k source, k + j repair j) at row_index_dev + this (elements) */
+    uint64_t rec_offset;        /* recovered row m at rec_dev + rec_offset + m * rec_row_stride */
+    uint64_t rec_row_stride;
+    uint64_t rec_index_offset;  /* min(k, r) u16 entries at rec_index_dev + this (elements) */
+} qf_dec_desc;
+/* Cauchy-coded generations (repair coefficients = the Cauchy row of the
+ * repair index, decoder.rs:280-298).  n_rec_dev / status_dev: one entry per
+ * descriptor, in descriptor order (status as qf_decode_batch). */
+int qf_decode_batch_desc(qf_ctx *ctx, const qf_dec_desc *gens_host, uint32_t G, const uint8_t *rows_dev,
+                         const uint16_t *row_index_dev, uint8_t *rec_dev, uint16_t *rec_index_dev,
+                         uint32_t *n_rec_dev, int32_t *status_dev);
+
+/* ---------------------------------------------------------------------------
  * Per-connection objects mirroring the reference's Rust API one call at a
  * time (what core.rs drives).  Payload state lives in HBM.
  * ------------------------------------------------------------------------- */

@@ -57,6 +57,24 @@ class DecodeShape(ctypes.Structure):
     ]
 
 
+class GenDesc(ctypes.Structure):
+    """qf_gen_desc (heterogeneous encode batch)."""
+    _fields_ = [
+        ("k", _U32), ("r", _U32), ("L", _U32), ("flags", _U32),
+        ("src_offset", _U64), ("src_row_stride", _U64),
+        ("rep_offset", _U64), ("rep_row_stride", _U64),
+    ]
+
+
+class DecDesc(ctypes.Structure):
+    """qf_dec_desc (heterogeneous decode batch)."""
+    _fields_ = [
+        ("k", _U32), ("r", _U32), ("L", _U32), ("n_rows", _U32),
+        ("rows_offset", _U64), ("row_stride", _U64), ("row_index_offset", _U64),
+        ("rec_offset", _U64), ("rec_row_stride", _U64), ("rec_index_offset", _U64),
+    ]
+
+
 class FecConfig(ctypes.Structure):
     _fields_ = [
         ("lambda_", ctypes.c_float), ("burst_window", _U32), ("hysteresis", ctypes.c_float),
@@ -95,6 +113,8 @@ _SIGS = {
     "qf_gf256_mul_slice_dev": (_I, [_P, _P, _P, _P, _SZ]),
     "qf_encode_batch": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
     "qf_encode_batch_host": (_I, [_P, ctypes.POINTER(EncodeShape), _U32, _P, _P, _P]),
+    "qf_encode_batch_desc": (_I, [_P, ctypes.POINTER(GenDesc), _U32, _P, _P]),
+    "qf_decode_batch_desc": (_I, [_P, ctypes.POINTER(DecDesc), _U32, _P, _P, _P, _P, _P, _P]),
     "qf_decode_batch": (_I, [_P, ctypes.POINTER(DecodeShape), _U32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "qf_decode_batch_host": (_I, [_P, ctypes.POINTER(DecodeShape), _U32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "qf_encoder_new": (_I, [_P, _U32, _U32, _U32, ctypes.POINTER(_P)]),

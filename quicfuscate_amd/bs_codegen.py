@@ -167,6 +167,10 @@ _ASM = {
                                            f"\ts_cbranch_scc1 .Lstag\n.Lstag_end:"),
     "s_load_args": lambda: "s_load_dwordx16 s[4:19], s[0:1], 0x0\n\ts_load_dwordx4 s[20:23], s[0:1], 0x40",
     "s_load_args_dec": lambda: "s_load_dwordx8 s[56:63], s[0:1], 0x50",
+    "s_load_args_offs": lambda off: f"s_load_dwordx4 s[72:75], s[0:1], 0x{off:x}",
+    "s_cmp_eq64_0_br": lambda s_, lbl: f"s_cmp_eq_u64 {SP(s_)}, 0\n\ts_cbranch_scc1 {lbl}",
+    "load8": lambda d, a, off: f"global_load_dwordx2 {VP(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
+    "v_add64_v": lambda d, a, b: f"v_lshl_add_u64 {VP(d)}, {VP(a)}, 0, {VP(b)}",
     "v_perm": lambda d, hi, lo, sel: f"v_perm_b32 {V(d)}, {V(hi)}, {V(lo)}, {V(sel)}",
     "v_perm_s": lambda d, hi, lo, s: f"v_perm_b32 {V(d)}, {V(hi)}, {V(lo)}, s{s}",
     "ds_read_b128": lambda d, a, off: f"ds_read_b128 {VQ(d)}, {V(a)}" + (f" offset:{off}" if off else ""),
@@ -213,7 +217,7 @@ _ASM = {
 # s[34:35] {dst row stride, 0}, s[36:37] mad carry sink, s[38:39] and
 # s[40:41] mask temps, s[48:49] store mask A, s[50:51] store mask B,
 # s[52:53] mask temp.
-KERNARG_BYTES = 80
+KERNARG_BYTES = 96          # + s[72:75]: per-generation offset tables (see _gen_base)
 V_LANE, V_F, V_GA, V_UA, V_GB, V_UB = 0, 1, 2, 3, 4, 5
 V_SRCA, V_SRCB, V_DSTA, V_DSTB = 6, 8, 10, 12   # 64-bit pointers (even-aligned)
 V_T = 14         # v14..v17 transpose temps
@@ -229,8 +233,14 @@ S_STA, S_STB, S_PAD = 48, 50, 52   # store masks of halves A / B, mask temp
 #   s[60:61] split tables (256 x 32 B, gf256_tables.h perm_record)
 #   s[62:63] {4096, 0} after the table copy (address constant)
 # s64 jmax: 1 + the largest repair index any lane of the item has accepted.
-KERNARG_BYTES_DEC = 112
-SGPR_NEXT_FREE_DEC = 72      # s[66:67]: far-jump target, s68..s71: byte-pick selectors
+KERNARG_BYTES_DEC = 128
+SGPR_NEXT_FREE_DEC = 76      # s[66:67]: far-jump target, s68..s71: byte-pick selectors
+# s[72:73] / s[74:75]: the source (syn / dec: received rows) and destination
+# (dec: recovered rows) generation offset tables, or 0 (kernarg words at
+# KERNARG_BYTES - 16 / KERNARG_BYTES_DEC - 16): generation g's base is then
+# base + table[g] (64-bit byte offsets) instead of base + g * gen_stride --
+# the heterogeneous batch API (qf_encode_batch_desc / qf_decode_batch_desc)
+S_OFFS = 72
 S_JMAX = 64
 S_PICK = 68                  # v_perm selector placing byte b of a dword at bits 8..15
 LDS_TAB_STRIDE = 256         # split-table record c at LDS byte c * 256 (address = byte << 8)
@@ -350,7 +360,7 @@ class KernelSpec:
     def next_free_sgpr(self) -> int:
         if self.mode == "dec":
             return SGPR_NEXT_FREE_DEC
-        return 68 if self.far else SGPR_NEXT_FREE   # s[66:67]: far-jump target
+        return S_OFFS + 4   # s[66:67]: far-jump target, s[72:75]: offset tables
 
     @property
     def far(self) -> bool:
@@ -496,6 +506,7 @@ def _prologue(E, spec: KernelSpec):
     E(Op("v_readfirstlane", (29, V_T)))
     if spec.mode == "dec":
         E(Op("s_load_args_dec", ()))
+    E(Op("s_load_args_offs", (spec.kernarg_bytes - 16,)))
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
     if spec.mode == "dec":
@@ -574,13 +585,13 @@ def _prologue(E, spec: KernelSpec):
             E(Op("v_cmp_gt_s", (S_TMP, 19, uv)))
         E(Op("s_nop", (4,)))
         # (dec: the recovered rows are caller memory -> payload lanes only)
+        E(Op("s_and64", (S_TMP2, vm, vm)))   # lanes with a unit (offset-table loads)
         E(Op("s_and64", (sm, vm, {"enc": S_TMP, "syn": vm, "dec": S_PAD}[spec.mode])))
         E(Op("s_and64", (vm, vm, S_PAD)))
-        # src/dst + g * gen_stride + 16 u   (VOP3 reads at most one SGPR)
-        for ptr, base_s, gs_s in ((sv, 4, 8), (dv, 6, 9)):
-            E(Op("v_movs", (ptr, base_s)))
-            E(Op("v_movs", (ptr + 1, base_s + 1)))
-            E(Op("v_mad64_s", (ptr, gv, gs_s, ptr)))
+        # src/dst + g * gen_stride + 16 u   (VOP3 reads at most one SGPR), or
+        # src/dst + table[g] + 16 u with a generation offset table
+        for x, (ptr, base_s, gs_s) in enumerate(((sv, 4, 8), (dv, 6, 9))):
+            _gen_base(E, ptr, base_s, gs_s, S_OFFS + 2 * x, gv, S_TMP2, f"{h}{x}")
             E(Op("v_mad64_k", (ptr, uv, 16, ptr)))
         if spec.mode != "enc":
             z = V_ZA if h == 0 else V_ZB
@@ -589,6 +600,27 @@ def _prologue(E, spec: KernelSpec):
             E(Op("v_mad64_k", (z, uv, 16, z)))
     E(Op("s_nop", (4,)))
     E(Op("label", (".Lbody",)))  # marks the end of the per-item setup (tools/bs_lab.py)
+
+
+def _gen_base(E, ptr: int, base_s: int, gs_s: int, tab_s: int, gv: int, lanes: int, tag: str):
+    """ptr <- base + g * gen_stride, or base + table[g] when the table
+    pointer s[tab_s:tab_s+1] is non-zero (wave-uniform branch; the table load
+    runs on the lanes of `lanes` only, other lanes keep base)."""
+    E(Op("v_movs", (ptr, base_s)))
+    E(Op("v_movs", (ptr + 1, base_s + 1)))
+    E(Op("s_cmp_eq64_0_br", (tab_s, f".Lstrided{tag}")))
+    E(Op("v_movs", (V_T, tab_s)))
+    E(Op("v_movs", (V_T + 1, tab_s + 1)))
+    E(Op("v_mad64_k", (V_T, gv, 8, V_T)))
+    E(Op("s_exec", (lanes,)))
+    E(Op("load8", (V_T + 2, V_T, 0)))
+    E(Op("s_waitcnt_vm", (0,)))
+    E(Op("v_add64_v", (ptr, ptr, V_T + 2)))
+    E(Op("s_exec", (None,)))
+    E(Op("s_branch", (f".Lbased{tag}",)))
+    E(Op("label", (f".Lstrided{tag}",)))
+    E(Op("v_mad64_s", (ptr, gv, gs_s, ptr)))
+    E(Op("label", (f".Lbased{tag}",)))
 
 
 def _epilogue_next_item(E, far: bool = False):
@@ -1061,8 +1093,8 @@ def launch_geometry(L: int, G: int, Lv: Optional[int] = None) -> tuple[int, int,
 def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
              total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
              Lv: Optional[int] = None, zero_tail: bool = False, lu: Optional[tuple[int, int]] = None,
-             tables: int = 0) -> bytes:
-    """80-byte kernarg block (layout above).  Syndrome mode: src = received
+             tables: int = 0, src_offs: int = 0, dst_offs: int = 0) -> bytes:
+    """96-byte kernarg block (layout above; 128 bytes in dec mode).  Syndrome mode: src = received
     rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
     also write zeros to bytes [L, 16 Lv) of every repair row.  Dec mode
     (lu = (records, record stride), tables = split-table base): dst, dgs and
@@ -1077,6 +1109,8 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
              magic, shift, n_items, total_waves, s19] + tail
     if lu is not None:
         words += [lu[0] & MASK32, lu[0] >> 32, lu[1], 0, tables & MASK32, tables >> 32, 0, 0]
+    # generation offset tables (0: strided generations)
+    words += [src_offs & MASK32, src_offs >> 32, dst_offs & MASK32, dst_offs >> 32]
     for w in words:
         assert 0 <= w < 1 << 32, words
     return np.array(words, dtype=np.uint32).tobytes()
@@ -1195,7 +1229,7 @@ class Emulator:
 
     def run_wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int):
         v = np.zeros((256, 64), dtype=np.uint64)
-        s = [0] * 80
+        s = [0] * 96
         lds = np.zeros(LDS_TAB_BYTES, np.uint8)
         pend_lgkm = []
         ka = np.frombuffer(kernarg, np.uint32)
@@ -1252,6 +1286,26 @@ class Emulator:
             elif n == "s_load_args_dec":
                 for q in range(8):
                     s[56 + q] = int(ka[20 + q])
+            elif n == "s_load_args_offs":
+                for q in range(4):
+                    s[72 + q] = int(ka[a[0] // 4 + q])
+            elif n == "s_cmp_eq64_0_br":
+                if s[a[0]] == 0 and s[a[0] + 1] == 0:
+                    pc = self.labels[a[1]]
+            elif n == "load8":
+                d, ar, off = a
+                addr = rv64(ar)
+                vals = np.zeros((2, 64), np.uint64)
+                for l in np.nonzero(exec_)[0]:
+                    vals[:, l] = np.frombuffer(self.read(int(addr[l]) + off, 8), np.uint32)
+                regs = [d, d + 1]
+                for rg in regs:
+                    if rg in busy:
+                        raise EmuError(f"load into v{rg} with a load outstanding")
+                    busy.add(rg)
+                pending.append((regs, vals, exec_.copy()))
+            elif n == "v_add64_v":
+                wv64(a[0], rv64(a[1]) + rv64(a[2]))
             elif n in ("v_perm", "v_perm_s"):
                 pool = (rv(a[1]) << np.uint64(32)) | rv(a[2])
                 sel = rv(a[3]) if n == "v_perm" else np.full(64, s[a[3]], np.uint64)

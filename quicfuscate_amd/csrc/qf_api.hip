@@ -63,6 +63,16 @@ struct qf_ctx {
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> small_coef;
     // qf_ctx_set_payload_wait: event the next decode's payload pass waits for
     hipEvent_t payload_wait = nullptr;
+    // heterogeneous batch API (qf_*_batch_desc): the generation offset tables
+    // of the class being launched (nullptr: strided generations) and the
+    // device / pinned buffers holding a call's per-generation metadata
+    const uint64_t* offs_in = nullptr;
+    const uint64_t* offs_out = nullptr;
+    uint8_t* d_desc = nullptr;
+    size_t desc_bytes = 0;
+    uint8_t* h_desc = nullptr;
+    size_t h_desc_bytes = 0;
+    hipEvent_t desc_done = nullptr;
     // decode workspace
     uint8_t* d_work = nullptr;
     size_t work_bytes = 0;
@@ -283,6 +293,8 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
             if (s != QF_OK) return s;
             qf::EncodeSmallArgs a{};
             a.rot = 0;
+            a.src_offs = ctx->offs_in;
+            a.rep_offs = ctx->offs_out;
             a.src = src;
             a.src_gen_stride = sh->src_gen_stride;
             a.src_row_stride = sh->src_row_stride;
@@ -307,7 +319,8 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     const char* nobs = getenv("QF_DISABLE_BS");
     // (L % 16 != 0: only with the zero tail, whose lane space masks the last unit)
     const bool zero_tail = (sh->flags & QF_ENCODE_ZERO_TAIL) &&
-                           qf::bs_zero_tail_fits(r, L, sh->rep_row_stride, sh->rep_gen_stride) &&
+                           (ctx->offs_out ? (r == 1 || sh->rep_row_stride >= 16ull * qf::bs_padded_units(L))
+                                          : qf::bs_zero_tail_fits(r, L, sh->rep_row_stride, sh->rep_gen_stride)) &&
                            (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31);
     if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && (L % 16 == 0 || zero_tail) && L >= 32 &&
         sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
@@ -316,7 +329,7 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         hipEvent_t ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
                                    sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G,
-                                   zero_tail));
+                                   zero_tail, ctx->offs_in, ctx->offs_out));
         prof_end(ctx, st, ev, qf::bs_name(k, r));
         return QF_OK;
     }
@@ -363,6 +376,8 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
             d_tabs = ctx->d_custom;
         }
         qf::CombineUniformArgs a{};
+        a.src_offs = ctx->offs_in;
+        a.dst_offs = ctx->offs_out;
         a.src = src;
         a.src_gen_stride = sh->src_gen_stride;
         a.src_row_stride = sh->src_row_stride;
@@ -463,7 +478,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
-                                ctx->d_zero, w, lu_stride, ctx->d_tab256));
+                                ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
     prof_end(ctx, st, ev, qf::dec_name(k, r));
     return QF_OK;
 }
@@ -521,6 +536,7 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         qf::GatherArgs ga{};
         ga.rows = rows + g0 * sh->rows_gen_stride;
         ga.rows_gen_stride = sh->rows_gen_stride;
+        ga.rows_offs = ctx->offs_in ? ctx->offs_in + g0 : nullptr;
         ga.row_stride = sh->row_stride;
         ga.smap = w + off_map + g0 * ms;
         ga.map_stride = ms;
@@ -550,6 +566,7 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
             a.row_stride = Lp;
             a.dst = rec + g0 * sh->rec_gen_stride + (uint64_t)p * 16 * sh->rec_row_stride;
             a.dst_gen_stride = sh->rec_gen_stride;
+            a.dst_offs = ctx->offs_out ? ctx->offs_out + g0 : nullptr;
             a.dst_row_stride = sh->rec_row_stride;
             a.coef = w + ((uint64_t)p * G + g0) * cgs;
             a.coef_gen_stride = cgs;
@@ -650,7 +667,8 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         ev = prof_begin(ctx, st);
         QF_CHECK_HIP(qf::syn_launch(ctx->bs, ctx->num_cus, st, k, r, rows + g0 * sh->rows_gen_stride, syn,
                                     sh->rows_gen_stride, (uint64_t)r * syn_rs, sh->row_stride, syn_rs, L, Gc,
-                                    w + off_map + g0 * ms, ms, ctx->d_zero));
+                                    w + off_map + g0 * ms, ms, ctx->d_zero,
+                                    ctx->offs_in ? ctx->offs_in + g0 : nullptr));
         prof_end(ctx, st, ev, qf::syn_name(k, r));
         if (overlap) {
             QF_CHECK_HIP(hipEventRecord(evA, st));
@@ -662,6 +680,7 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         a.row_stride = syn_rs;
         a.dst = rec + g0 * sh->rec_gen_stride;
         a.dst_gen_stride = sh->rec_gen_stride;
+        a.dst_offs = ctx->offs_out ? ctx->offs_out + g0 : nullptr;
         a.dst_row_stride = sh->rec_row_stride;
         a.coef = w + g0 * coef_gen_stride;
         a.coef_gen_stride = coef_gen_stride;
@@ -867,6 +886,9 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->d_custom) hipFree(c->d_custom);
     if (c->custom_done) hipEventDestroy(c->custom_done);
     if (c->d_work) hipFree(c->d_work);
+    if (c->d_desc) hipFree(c->d_desc);
+    if (c->h_desc) hipHostFree(c->h_desc);
+    if (c->desc_done) hipEventDestroy(c->desc_done);
     if (c->d_zero) hipFree(c->d_zero);
     if (c->d_gf16_log) hipFree(c->d_gf16_log);
     if (c->d_gf16_exp) hipFree(c->d_gf16_exp);
@@ -1227,6 +1249,8 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         qf::CombineSlotsArgs a{};
         a.rows = rows;
         a.rows_gen_stride = sh->rows_gen_stride;
+        a.rows_offs = ctx->offs_in;
+        a.dst_offs = ctx->offs_out;
         a.row_stride = sh->row_stride;
         a.dst = rec + (uint64_t)p * 16 * sh->rec_row_stride;
         a.dst_gen_stride = sh->rec_gen_stride;
@@ -1289,6 +1313,212 @@ int qf_parse_frames_dev(qf_ctx* ctx, uint32_t k, uint32_t r, uint32_t L, uint32_
                                          row_stride, rows_gen_stride, row_index, n_rows, frame_status,
                                          ctx->d_explog, ctx->stream));
     prof_end(ctx, ctx->stream, ev, "k_parse_frames");
+    return QF_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Heterogeneous batches (SURVEY 8(b) qf_gen_desc): one call over generations
+// of different (k, r, L) at arbitrary offsets.  Generations are grouped by
+// shape; each class runs the batch implementation above with per-generation
+// offset tables (every kernel addresses generation g at base + table[g]).
+// ---------------------------------------------------------------------------
+namespace {
+
+// pinned staging (reused per call: the previous upload must have landed)
+int desc_stage(qf_ctx* ctx, size_t bytes) {
+    if (!ctx->desc_done) QF_CHECK_HIP(hipEventCreateWithFlags(&ctx->desc_done, hipEventDisableTiming));
+    else QF_CHECK_HIP(hipEventSynchronize(ctx->desc_done));
+    if (bytes > ctx->h_desc_bytes) {
+        if (ctx->h_desc) hipHostFree(ctx->h_desc);
+        ctx->h_desc = nullptr;
+        ctx->h_desc_bytes = 0;
+        const size_t b = round_up(bytes, 1 << 16);
+        if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_desc), b) != hipSuccess) return QF_ENOMEM;
+        ctx->h_desc_bytes = b;
+    }
+    if (bytes > ctx->desc_bytes) {
+        if (ctx->d_desc) {
+            QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+            hipFree(ctx->d_desc);
+        }
+        ctx->d_desc = nullptr;
+        ctx->desc_bytes = 0;
+        const size_t b = round_up(bytes, 1 << 16);
+        if (hipMalloc(&ctx->d_desc, b) != hipSuccess) return QF_ENOMEM;
+        ctx->desc_bytes = b;
+    }
+    return QF_OK;
+}
+
+int desc_upload(qf_ctx* ctx, size_t bytes) {
+    QF_CHECK_HIP(hipMemcpyAsync(ctx->d_desc, ctx->h_desc, bytes, hipMemcpyHostToDevice, ctx->stream));
+    QF_CHECK_HIP(hipEventRecord(ctx->desc_done, ctx->stream));
+    return QF_OK;
+}
+
+struct OffsScope {  // the class's offset tables for the launches inside the batch implementation
+    qf_ctx* ctx;
+    OffsScope(qf_ctx* c, const uint64_t* in, const uint64_t* out) : ctx(c) {
+        ctx->offs_in = in;
+        ctx->offs_out = out;
+    }
+    ~OffsScope() {
+        ctx->offs_in = nullptr;
+        ctx->offs_out = nullptr;
+    }
+};
+
+}  // namespace
+
+int qf_encode_batch_desc(qf_ctx* ctx, const qf_gen_desc* gens, uint32_t G, const uint8_t* src, uint8_t* rep) {
+    if (!ctx) return QF_EINVAL;
+    if (G == 0) return QF_OK;
+    if (!gens || !src || !rep || !aligned16(src) || !aligned16(rep)) return QF_EINVAL;
+    typedef std::tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint64_t, uint64_t> Key;
+    std::map<Key, std::vector<uint32_t>> cls;
+    for (uint32_t i = 0; i < G; ++i) {
+        const qf_gen_desc& d = gens[i];
+        if (d.k == 0 || d.k > 256 || (d.flags & ~QF_ENCODE_ZERO_TAIL)) return QF_EINVAL;
+        if (d.k + d.r > 256) return QF_ERANGE;  // gf_inv(0) in the Cauchy rows (decoder.rs:290-296)
+        if (d.r == 0 || d.L == 0) continue;      // nothing to emit
+        if ((d.src_offset | d.src_row_stride | d.rep_offset | d.rep_row_stride) & 15) return QF_EINVAL;
+        if ((d.src_row_stride < d.L && d.k > 1) || (d.rep_row_stride < d.L && d.r > 1)) return QF_EINVAL;
+        cls[Key(d.k, d.r, d.L, d.flags, d.src_row_stride, d.rep_row_stride)].push_back(i);
+    }
+    std::lock_guard<std::mutex> g(ctx->mu);
+    int s = ensure_device(ctx);
+    if (s) return s;
+    size_t n = 0;
+    for (auto& kv : cls) n += kv.second.size();
+    if (n == 0) return QF_OK;
+    if ((s = desc_stage(ctx, 16 * n)) != QF_OK) return s;
+    uint64_t* h = reinterpret_cast<uint64_t*>(ctx->h_desc);
+    size_t o = 0;
+    for (auto& kv : cls) {   // per class: source offsets, then repair offsets
+        for (uint32_t i : kv.second) h[o++] = gens[i].src_offset;
+        for (uint32_t i : kv.second) h[o++] = gens[i].rep_offset;
+    }
+    if ((s = desc_upload(ctx, 16 * n)) != QF_OK) return s;
+    const uint64_t* dt = reinterpret_cast<const uint64_t*>(ctx->d_desc);
+    o = 0;
+    for (auto& kv : cls) {
+        const uint32_t Gc = (uint32_t)kv.second.size();
+        qf_encode_shape sh{};
+        std::tie(sh.k, sh.r, sh.L, sh.flags, sh.src_row_stride, sh.rep_row_stride) = kv.first;
+        OffsScope scope(ctx, dt + o, dt + o + Gc);
+        s = encode_impl(ctx, &sh, Gc, src, rep, nullptr, ctx->stream);
+        if (s != QF_OK) return s;
+        o += 2 * (size_t)Gc;
+    }
+    return QF_OK;
+}
+
+int qf_decode_batch_desc(qf_ctx* ctx, const qf_dec_desc* gens, uint32_t G, const uint8_t* rows,
+                         const uint16_t* row_index, uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec,
+                         int32_t* status) {
+    if (!ctx) return QF_EINVAL;
+    if (G == 0) return QF_OK;
+    if (!gens || !rows || !row_index || !n_rec || !status || !aligned16(rows)) return QF_EINVAL;
+    typedef std::tuple<uint32_t, uint32_t, uint32_t, uint64_t, uint64_t> Key;
+    std::map<Key, std::vector<uint32_t>> cls;
+    bool any_rec = false;
+    for (uint32_t i = 0; i < G; ++i) {
+        const qf_dec_desc& d = gens[i];
+        if (d.k == 0 || d.k > 256 || d.L == 0 || d.n_rows > 255) return QF_EINVAL;
+        if (std::min(d.k, d.r) > 128) return QF_EINVAL;
+        if ((d.rows_offset | d.row_stride | d.rec_offset | d.rec_row_stride) & 15) return QF_EINVAL;
+        if (d.row_stride < d.L && d.n_rows > 1) return QF_EINVAL;
+        any_rec = any_rec || std::min(d.k, d.r) > 0;
+        cls[Key(d.k, d.r, d.L, d.row_stride, d.rec_row_stride)].push_back(i);
+    }
+    if (any_rec && (!rec || !rec_index || !aligned16(rec))) return QF_EINVAL;
+    int s;
+    // metadata per generation (class order): rows / rec offset tables (8 + 8),
+    // row-index / rec-index element offsets (8 + 8), n_rows and descriptor id
+    // (4 + 4); per class also the gathered row indices, n_rows, and the
+    // class's recovered indices, counts and statuses before the scatter
+    size_t meta = 0, scratch = 0;
+    std::vector<size_t> cls_scratch;
+    for (auto& kv : cls) {
+        const uint32_t Gc = (uint32_t)kv.second.size(), k = std::get<0>(kv.first), r = std::get<1>(kv.first);
+        uint32_t mr = 1;
+        for (uint32_t i : kv.second) mr = std::max(mr, gens[i].n_rows);
+        const size_t emax = std::min(k, r);
+        meta += 40 * (size_t)Gc;
+        cls_scratch.push_back(scratch);
+        scratch += round_up((size_t)Gc * mr * 2, 256) + round_up((size_t)Gc * emax * 2, 256) + round_up((size_t)Gc * 12, 256);
+    }
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        if ((s = ensure_device(ctx)) != QF_OK) return s;
+        if ((s = desc_stage(ctx, round_up(meta, 256) + scratch)) != QF_OK) return s;
+        uint8_t* h = ctx->h_desc;
+        size_t o = 0;
+        for (auto& kv : cls) {
+            const size_t Gc = kv.second.size();
+            uint64_t* ro = reinterpret_cast<uint64_t*>(h + o);
+            uint64_t* co = ro + Gc;
+            uint64_t* rio = co + Gc;
+            uint64_t* cio = rio + Gc;
+            uint32_t* nr = reinterpret_cast<uint32_t*>(cio + Gc);
+            uint32_t* id = nr + Gc;
+            for (size_t q = 0; q < Gc; ++q) {
+                const qf_dec_desc& d = gens[kv.second[q]];
+                ro[q] = d.rows_offset;
+                co[q] = d.rec_offset;
+                rio[q] = d.row_index_offset;
+                cio[q] = d.rec_index_offset;
+                nr[q] = d.n_rows;
+                id[q] = kv.second[q];
+            }
+            o += 40 * Gc;
+        }
+        if ((s = desc_upload(ctx, meta)) != QF_OK) return s;
+    }
+    uint8_t* dm = ctx->d_desc;
+    uint8_t* dsc = ctx->d_desc + round_up(meta, 256);
+    size_t o = 0, c = 0;
+    for (auto& kv : cls) {
+        const uint32_t Gc = (uint32_t)kv.second.size();
+        qf_decode_shape sh{};
+        std::tie(sh.k, sh.r, sh.L, sh.row_stride, sh.rec_row_stride) = kv.first;
+        uint32_t mr = 1;
+        for (uint32_t i : kv.second) mr = std::max(mr, gens[i].n_rows);
+        const uint32_t emax = std::min(sh.k, sh.r);
+        sh.max_rows = mr;
+        const uint64_t* ro = reinterpret_cast<const uint64_t*>(dm + o);
+        const uint64_t* co = ro + Gc;
+        const uint64_t* rio = co + Gc;
+        const uint64_t* cio = rio + Gc;
+        const uint32_t* nr = reinterpret_cast<const uint32_t*>(cio + Gc);
+        const uint32_t* id = nr + Gc;
+        uint8_t* sc = dsc + cls_scratch[c];
+        uint16_t* ri_ws = reinterpret_cast<uint16_t*>(sc);
+        uint16_t* rec_ws = reinterpret_cast<uint16_t*>(sc + round_up((size_t)Gc * mr * 2, 256));
+        uint32_t* nrec_ws = reinterpret_cast<uint32_t*>(sc + round_up((size_t)Gc * mr * 2, 256) +
+                                                        round_up((size_t)Gc * emax * 2, 256));
+        int32_t* st_ws = reinterpret_cast<int32_t*>(nrec_ws + Gc);
+        {
+            std::lock_guard<std::mutex> g(ctx->mu);
+            qf::DescIndexArgs ia{row_index, rio, nr, ri_ws, mr, Gc};
+            QF_CHECK_HIP(qf::launch_desc_gather_index(ia, ctx->stream));
+            ctx->offs_in = ro;
+            ctx->offs_out = co;
+        }
+        s = decode_batch_impl(ctx, &sh, Gc, rows, ri_ws, nr, nullptr, rec, rec_ws, nrec_ws, st_ws);
+        {
+            std::lock_guard<std::mutex> g(ctx->mu);
+            ctx->offs_in = ctx->offs_out = nullptr;
+            if (s != QF_OK) return s;
+            qf::DescOutArgs oa{rec_ws, nrec_ws, st_ws, cio, id, rec_index, n_rec, status, emax, Gc};
+            QF_CHECK_HIP(qf::launch_desc_scatter_out(oa, ctx->stream));
+        }
+        o += 40 * (size_t)Gc;
+        ++c;
+    }
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->payload_wait = nullptr;  // as qf_decode_batch: one decode call only
     return QF_OK;
 }
 

@@ -26,7 +26,10 @@ bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs);
 // last unit of each source row is then read whole, up to round_up(L, 16)).
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
-                     uint64_t drs, uint32_t L, uint32_t G, bool zero_tail);
+                     uint64_t drs, uint32_t L, uint32_t G, bool zero_tail, const uint64_t* src_offs = nullptr,
+                     const uint64_t* dst_offs = nullptr);
+// (src_offs / dst_offs: generation offset tables -- generation g at src +
+// src_offs[g] / dst + dst_offs[g] instead of g * gen_stride -- or nullptr)
 // Decode stage A: syndromes of the accepted repairs (bs_codegen.py "syn").
 // zero: >= L zero bytes (read in place of rows a generation does not have).
 // srs >= 16 * bs_padded_units(L): syndromes are computed over the padded lane
@@ -37,7 +40,7 @@ uint32_t syn_map_stride(uint32_t k, uint32_t r);
 hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
                       uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
-                      const uint8_t* zero);
+                      const uint8_t* zero, const uint64_t* rows_offs = nullptr);
 // Fused decode (bs_codegen.py "dec"): syndromes of the accepted repairs,
 // then C[J, E] x = s solved in registers by the per-generation LU records of
 // k_decode_prepare_cauchy (lu_out), recovered rows stored to
@@ -48,7 +51,8 @@ const char* dec_name(uint32_t k, uint32_t r);
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
-                      const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256);
+                      const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
+                      const uint64_t* rows_offs = nullptr, const uint64_t* rec_offs = nullptr);
 void bs_unload(BsCache& cache);
 
 }  // namespace qf

@@ -67,7 +67,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
                          const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                          uint64_t drs, uint32_t L, uint32_t G, uint32_t Lv, uint32_t s19,
                          const uint8_t* smap, const uint8_t* zero, const uint8_t* lu = nullptr,
-                         uint32_t lu_stride = 0, const uint32_t* tab256 = nullptr) {
+                         uint32_t lu_stride = 0, const uint32_t* tab256 = nullptr,
+                         const uint64_t* src_offs = nullptr, const uint64_t* dst_offs = nullptr) {
     (void)num_cus;
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
@@ -93,7 +94,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     const uint32_t n_items = (uint32_t)((total + 127) / 128);
     const uint32_t blocks = (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
-    uint32_t a[28] = {};
+    uint32_t a[32] = {};
     a[0] = (uint32_t)(uintptr_t)src;
     a[1] = (uint32_t)((uintptr_t)src >> 32);
     a[2] = (uint32_t)(uintptr_t)dst;
@@ -128,7 +129,13 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[22] = lu_stride;
     a[24] = (uint32_t)(uintptr_t)tab256;
     a[25] = (uint32_t)((uintptr_t)tab256 >> 32);
-    size_t sz = e->mode == 'd' ? 28 * 4 : 20 * 4;
+    // generation offset tables, the last 16 kernarg bytes (bs_codegen S_OFFS)
+    const int ot = e->mode == 'd' ? 28 : 20;
+    a[ot] = (uint32_t)(uintptr_t)src_offs;
+    a[ot + 1] = (uint32_t)((uintptr_t)src_offs >> 32);
+    a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
+    a[ot + 3] = (uint32_t)((uintptr_t)dst_offs >> 32);
+    size_t sz = (size_t)(ot + 4) * 4;
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
     return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
@@ -143,14 +150,18 @@ bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs) {
 
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
-                     uint64_t drs, uint32_t L, uint32_t G, bool zero_tail) {
+                     uint64_t drs, uint32_t L, uint32_t G, bool zero_tail, const uint64_t* src_offs,
+                     const uint64_t* dst_offs) {
     // zero tail: lane space padded to whole 128-B lines per row and the tail
     // [L, 16 Lv) of every repair row written with zeros, so every line the
     // kernel stores is whole (tools/bs_lab.py: partial lines shared by two
     // waves cut the write rate from ~5.7 to ~4 TB/s at L = 1200)
     const uint32_t Lu = L / 16;
     const uint32_t Lv = zero_tail ? bs_padded_units(L) : Lu;
-    if (zero_tail && !bs_zero_tail_fits(r, L, drs, dgs)) return hipErrorInvalidValue;
+    // (with a destination offset table each generation's repair block is the
+    // caller's: only the row stride is checked here)
+    if (zero_tail && !(dst_offs ? (r == 1 || drs >= 16ull * bs_padded_units(L)) : bs_zero_tail_fits(r, L, drs, dgs)))
+        return hipErrorInvalidValue;
     if (!zero_tail && L % 16) return hipErrorInvalidValue;
     if (!find('e', k, r)) return hipErrorInvalidValue;
     // one launch per pass of repairs (codes with more repairs than a kernel
@@ -158,7 +169,7 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     for (const auto& e : qf_bs_table) {
         if (e.mode != 'e' || e.k != k || e.rt != r) continue;
         hipError_t err = launch(cache, &e, num_cus, st, src, dst + (uint64_t)e.j0 * drs, sgs, dgs, srs, drs, L, G,
-                                Lv, Lv, nullptr, nullptr);
+                                Lv, Lv, nullptr, nullptr, nullptr, 0, nullptr, src_offs, dst_offs);
         if (err != hipSuccess) return err;
     }
     return hipSuccess;
@@ -167,14 +178,15 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
 hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
                       uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
-                      const uint8_t* zero) {
+                      const uint8_t* zero, const uint64_t* rows_offs) {
     const QfBsEntry* e = find('s', k, r);
     if (!e || map_stride != e->map_stride || !zero) return hipErrorInvalidValue;
     // syndrome rows live in the library's workspace: always the padded lane
     // space (srs >= 16 * bs_padded_units(L); the tail holds junk)
     const uint32_t Lv = bs_padded_units(L);
     if (srs < 16ull * Lv) return hipErrorInvalidValue;
-    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, Lv, map_stride, smap, zero);
+    return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, Lv, map_stride, smap, zero, nullptr, 0,
+                  nullptr, rows_offs, nullptr);
 }
 
 bool dec_available(uint32_t k, uint32_t r) { return find('d', k, r) != nullptr; }
@@ -187,7 +199,8 @@ const char* dec_name(uint32_t k, uint32_t r) {
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
-                      const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256) {
+                      const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
+                      const uint64_t* rows_offs, const uint64_t* rec_offs) {
     const QfBsEntry* e = find('d', k, r);
     if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
         return hipErrorInvalidValue;
@@ -196,7 +209,7 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
     // unpadded lane space: the kernel is VALU-bound, padding lanes would be
     // pure extra work (and the recovered rows are caller memory, payload only)
     return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, L / 16, map_stride, smap, zero,
-                  lu, lu_stride, tab256);
+                  lu, lu_stride, tab256, rows_offs, rec_offs);
 }
 
 void bs_unload(BsCache& cache) {

@@ -24,6 +24,10 @@ struct CombineUniformArgs {
     uint32_t Lu;
     uint32_t pad0;
     uint64_t total_units;
+    // generation offset tables (nullptr: g * gen_stride), the heterogeneous
+    // batch API: generation g starts at src + src_offs[g] / dst + dst_offs[g]
+    const uint64_t* src_offs = nullptr;
+    const uint64_t* dst_offs = nullptr;
 };
 
 // Decode payload pass (one 16-output pass):
@@ -47,6 +51,8 @@ struct CombineSlotsArgs {
     uint32_t Lu;
     uint32_t zero_slot;  // index of an all-zero coefficient record
     uint64_t total_units;
+    const uint64_t* rows_offs = nullptr;  // generation offset tables (nullptr: strided)
+    const uint64_t* dst_offs = nullptr;
 };
 
 struct PrepareArgs {
@@ -111,6 +117,7 @@ struct GatherArgs {
     uint8_t* out;          // gather: sources [G][k]; xor: syndromes [G][r]
     uint64_t out_gen_stride, out_row_stride;
     uint32_t k, r, Lu, G;
+    const uint64_t* rows_offs = nullptr;  // generation offset table of the received rows (nullptr: strided)
 };
 hipError_t launch_gather_sources(const GatherArgs& a, int num_cus, hipStream_t st);
 hipError_t launch_xor_repairs(const GatherArgs& a, int num_cus, hipStream_t st);
@@ -139,7 +146,40 @@ struct EncodeSmallArgs {
     const uint32_t* tab256;  // split-table records (8 dwords) of every coefficient
     uint32_t k, r, L, Lu, G;
     uint32_t rot;            // window row i is source row (i + rot) % k (a ring; 0: plain)
+    const uint64_t* src_offs = nullptr;  // generation offset tables (nullptr: strided)
+    const uint64_t* rep_offs = nullptr;
 };
+
+// Heterogeneous decode batches (qf_decode_batch_desc): a class's row indices
+// gathered from the caller's arrays into [G][max_rows] (zero past n_rows)...
+struct DescIndexArgs {
+    const uint16_t* row_index;  // caller's row-index array
+    const uint64_t* ri_off;     // [G] element offset of each generation's indices
+    const uint32_t* n_rows;     // [G]
+    uint16_t* out;              // [G][max_rows]
+    uint32_t max_rows, G;
+};
+hipError_t launch_desc_gather_index(const DescIndexArgs& a, hipStream_t st);
+// ... and its outputs scattered back: recovered indices to the caller's
+// offsets, counts and statuses to the descriptors' positions
+struct DescOutArgs {
+    const uint16_t* rec_index_ws;  // [G][emax]
+    const uint32_t* n_rec_ws;
+    const int32_t* status_ws;
+    const uint64_t* rec_index_off;  // [G]
+    const uint32_t* desc_id;        // [G]
+    uint16_t* rec_index;
+    uint32_t* n_rec;
+    int32_t* status;
+    uint32_t emax, G;
+};
+hipError_t launch_desc_scatter_out(const DescOutArgs& a, hipStream_t st);
+
+// base of generation g: base + offs[g] with an offset table, else base + g * stride
+template <typename T>
+__host__ __device__ inline T* gen_base(T* base, uint64_t g, uint64_t stride, const uint64_t* offs) {
+    return base + (offs ? offs[g] : g * stride);
+}
 hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st);
 
 }  // namespace qf

@@ -298,8 +298,8 @@ __global__ void __launch_bounds__(256, (V == 1 && PD == 1 ? 3 : 2)) k_combine_un
             if (f < a.total_units) {
                 const uint64_t g = f / a.Lu;
                 const uint32_t u = (uint32_t)(f - g * a.Lu);
-                sp[v] = a.src + g * a.src_gen_stride + (uint64_t)u * 16;
-                dp[v] = a.dst + g * a.dst_gen_stride + (uint64_t)u * 16;
+                sp[v] = gen_base(a.src, g, a.src_gen_stride, a.src_offs) + (uint64_t)u * 16;
+                dp[v] = gen_base(a.dst, g, a.dst_gen_stride, a.dst_offs) + (uint64_t)u * 16;
                 const uint32_t rem = a.L - u * 16;
                 nbytes[v] = rem < 16 ? rem : 16;
             }
@@ -431,8 +431,8 @@ __global__ void __launch_bounds__(256, (PD == 1 ? 3 : 2)) k_combine_slots(Combin
         if (f < a.total_units) {
             const uint64_t g = f / a.Lu;
             const uint32_t u = (uint32_t)(f - g * a.Lu);
-            rowp = a.rows + g * a.rows_gen_stride + (uint64_t)u * 16;
-            outp = a.dst + g * a.dst_gen_stride + (uint64_t)u * 16;
+            rowp = gen_base(a.rows, g, a.rows_gen_stride, a.rows_offs) + (uint64_t)u * 16;
+            outp = gen_base(a.dst, g, a.dst_gen_stride, a.dst_offs) + (uint64_t)u * 16;
             coefp = a.coef + g * a.coef_gen_stride;
             const uint32_t rem = a.L - u * 16;
             nbytes = rem < 16 ? rem : 16;
@@ -1259,7 +1259,9 @@ __global__ void __launch_bounds__(256) k_gather_sources(GatherArgs a) {
         const uint32_t i = (uint32_t)(t - g * a.k);
         const uint32_t slot = a.smap[g * a.map_stride + i];
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (slot != 0xFF) v = *reinterpret_cast<const uint4*>(a.rows + g * a.rows_gen_stride + slot * a.row_stride + 16ull * u);
+        if (slot != 0xFF)
+            v = *reinterpret_cast<const uint4*>(gen_base(a.rows, g, a.rows_gen_stride, a.rows_offs) +
+                                                slot * a.row_stride + 16ull * u);
         *reinterpret_cast<uint4*>(a.out + g * a.out_gen_stride + i * a.out_row_stride + 16ull * u) = v;
     }
 }
@@ -1274,7 +1276,8 @@ __global__ void __launch_bounds__(256) k_xor_repairs(GatherArgs a) {
         const uint32_t j = (uint32_t)(t - g * a.r);
         const uint32_t slot = a.smap[g * a.map_stride + a.k + j];
         if (slot == 0xFF) continue;
-        const uint4 p = *reinterpret_cast<const uint4*>(a.rows + g * a.rows_gen_stride + slot * a.row_stride + 16ull * u);
+        const uint4 p = *reinterpret_cast<const uint4*>(gen_base(a.rows, g, a.rows_gen_stride, a.rows_offs) +
+                                                        slot * a.row_stride + 16ull * u);
         uint4* s = reinterpret_cast<uint4*>(a.out + g * a.out_gen_stride + j * a.out_row_stride + 16ull * u);
         uint4 v = *s;
         v.x ^= p.x;
@@ -1383,7 +1386,7 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
         const uint32_t j = (uint32_t)(gj - g * a.r);
         const bool act = u < a.Lu;
         const uint32_t nb = act ? min(16u, a.L - 16 * u) : 0u;
-        const uint8_t* sp = a.src + g * a.src_gen_stride + 16ull * (act ? u : 0);
+        const uint8_t* sp = gen_base(a.src, g, a.src_gen_stride, a.src_offs) + 16ull * (act ? u : 0);
         const uint8_t* cp = a.coef + (uint64_t)j * a.k;
         uint4 acc = make_uint4(0, 0, 0, 0);
         for (uint32_t ib = i0; ib < i1; ib += 8) {
@@ -1417,7 +1420,8 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
                 acc.z ^= p.z;
                 acc.w ^= p.w;
             }
-            store_unit(a.rep + g * a.rep_gen_stride + (uint64_t)j * a.rep_row_stride + 16ull * u, acc, nb);
+            store_unit(gen_base(a.rep, g, a.rep_gen_stride, a.rep_offs) + (uint64_t)j * a.rep_row_stride + 16ull * u,
+                       acc, nb);
         }
         __syncthreads();
     }
@@ -1428,6 +1432,49 @@ hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_
     if (!tiles || a.k == 0) return hipSuccess;
     const uint64_t blocks = std::min<uint64_t>(tiles, (uint64_t)num_cus * 8);
     hipLaunchKernelGGL(k_encode_small, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// --- heterogeneous decode batches: metadata gather / scatter -----------------
+__global__ void __launch_bounds__(256) k_desc_gather_index(DescIndexArgs a) {
+    const uint64_t total = (uint64_t)a.G * a.max_rows;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = f / a.max_rows;
+        const uint32_t s = (uint32_t)(f - g * a.max_rows);
+        a.out[f] = s < a.n_rows[g] ? a.row_index[a.ri_off[g] + s] : (uint16_t)0;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_desc_scatter_out(DescOutArgs a) {
+    const uint32_t w = a.emax + 1;
+    const uint64_t total = (uint64_t)a.G * w;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = f / w;
+        const uint32_t m = (uint32_t)(f - g * w);
+        if (m < a.emax) {
+            a.rec_index[a.rec_index_off[g] + m] = a.rec_index_ws[g * a.emax + m];
+        } else {
+            a.n_rec[a.desc_id[g]] = a.n_rec_ws[g];
+            a.status[a.desc_id[g]] = a.status_ws[g];
+        }
+    }
+}
+
+hipError_t launch_desc_gather_index(const DescIndexArgs& a, hipStream_t st) {
+    const uint64_t total = (uint64_t)a.G * a.max_rows;
+    if (!total) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_desc_gather_index, dim3((uint32_t)blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_desc_scatter_out(const DescOutArgs& a, hipStream_t st) {
+    const uint64_t total = (uint64_t)a.G * (a.emax + 1);
+    if (!total) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_desc_scatter_out, dim3((uint32_t)blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

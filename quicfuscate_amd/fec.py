@@ -177,6 +177,31 @@ def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_
           "encode_batch")
 
 
+def encode_batch_desc(src, rep, descs, ctx: Optional[Context] = None) -> None:
+    """qf_encode_batch_desc: one call over generations of different (k, r, L)
+    at arbitrary offsets.  descs: sequence of dicts or tuples
+    (k, r, L, flags, src_offset, src_row_stride, rep_offset, rep_row_stride)."""
+    ctx = ctx or default_context()
+    arr = (L.GenDesc * max(1, len(descs)))()
+    for i, d in enumerate(descs):
+        arr[i] = L.GenDesc(**d) if isinstance(d, dict) else L.GenDesc(*d)
+    check(L._lib().qf_encode_batch_desc(ctx.handle, arr, len(descs), _ptr(src), _ptr(rep)), "encode_batch_desc")
+
+
+def decode_batch_desc(rows, row_index, rec, rec_index, n_rec, status, descs, ctx: Optional[Context] = None) -> None:
+    """qf_decode_batch_desc: descs are dicts / tuples of qf_dec_desc (k, r, L,
+    n_rows, rows_offset, row_stride, row_index_offset, rec_offset,
+    rec_row_stride, rec_index_offset); n_rec / status: one entry per descriptor."""
+    ctx = ctx or default_context()
+    arr = (L.DecDesc * max(1, len(descs)))()
+    for i, d in enumerate(descs):
+        arr[i] = L.DecDesc(**d) if isinstance(d, dict) else L.DecDesc(*d)
+    check(L._lib().qf_decode_batch_desc(ctx.handle, arr, len(descs), _ptr(rows), _ptr(row_index),
+                                         _ptr(rec) if rec is not None else None,
+                                         _ptr(rec_index) if rec_index is not None else None, _ptr(n_rec),
+                                         _ptr(status)), "decode_batch_desc")
+
+
 def encode_batch_host(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, rep_row_stride: int, G: int,
                       coeff: Optional[bytes] = None, ctx: Optional[Context] = None) -> None:
     """qf_encode_batch_host: encode_batch with src / rep in host memory (torch

@@ -443,3 +443,35 @@ def test_register_budget_large_pass_kernel():
     vmax = max(int(m.group(2) or m.group(3)) for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", body))
     assert smax < ns and vmax < nv, (smax, ns, vmax, nv)
     assert "s_setpc_b64 s[66:67]" in body
+
+
+def test_emulated_offset_tables_encode(oracle):
+    """Generation offset tables (the heterogeneous batch API): generation g's
+    rows start at base + table[g] (any order, any gaps) instead of
+    base + g * gen_stride; encode and fused decode both honour them."""
+    k, r, L, G = 8, 4, 96, 5
+    rng = np.random.default_rng(44)
+    srs = L
+    blk = k * srs
+    perm = rng.permutation(G)
+    src_off = np.array([int(p) * (blk + 48) + 16 for p in perm], np.uint64)       # shuffled, gapped
+    rep_off = np.array([int(p) * (r * L + 32) for p in rng.permutation(G)], np.uint64)
+    src = rng.integers(0, 256, G * (blk + 48) + 64, dtype=np.uint8)
+    dst = np.full(G * (r * L + 32) + 64, 0xEE, np.uint8)
+    spec = bs.KernelSpec(k, r, 2)
+    emu = bs.Emulator(bs.generate(spec))
+    SRC, DST, T1, T2 = 0x10000000, 0x40000000, 0x60000000, 0x61000000
+    emu.add_buffer(SRC, src)
+    emu.add_buffer(DST, dst)
+    emu.add_buffer(T1, src_off.view(np.uint8))
+    emu.add_buffer(T2, rep_off.view(np.uint8))
+    ka = bs.kernargs(SRC, DST, 0, 0, srs, L, L, G, 8, src_offs=T1, dst_offs=T2)
+    for wg in range(2):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        so, ro = int(src_off[g]), int(rep_off[g])
+        rows = np.stack([src[so + i * srs: so + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, r)
+        for j in range(r):
+            assert (dst[ro + j * L: ro + (j + 1) * L] == want[j]).all(), (g, j)
