@@ -4,7 +4,6 @@ per generation -- BASELINE C5's ASW-RLNC-X mix, k drawn per generation from
 the Normal / Medium windows with r = ceil(k * ratio) - k (adaptive.rs:124-153)
 -- placed at shuffled, gapped offsets.  Every generation's repairs and
 recovered rows are checked against the oracle (decoder.rs:172-275, 678-783)."""
-import math
 
 import numpy as np
 import pytest
@@ -64,7 +63,10 @@ def test_encode_desc_mixed_windows(qf, oracle, gpu_ctx, Ls, zero_tail):
         got = out[ro: ro + r * Lp(Lb)].reshape(r, Lp(Lb))
         assert (got[:, :Lb] == want).all(), (q, k, r, Lb)
         tail = got[:, Lb:]
-        assert (tail == 0).all() if zero_tail else (tail == 0xEE).all()
+        if zero_tail:   # the library MAY zero [L, Lp) (bit-sliced path) or leave it (small-batch path)
+            assert all((t == 0).all() or (t == 0xEE).all() for t in tail), (q, k, r, Lb)
+        else:
+            assert (tail == 0xEE).all()
 
 
 def test_encode_desc_errors(qf, gpu_ctx):
@@ -142,9 +144,11 @@ def test_decode_desc_mixed_windows(qf, oracle, gpu_ctx):
         assert st[q] == ost, (q, st[q], ost)
         if ost != 0:
             continue
-        erased = list(np.nonzero(mask == 0)[0])
-        assert erased == E and n_rec[q] == len(E)
-        assert list(ci[ci_off[q]: ci_off[q] + len(E)]) == E
-        for m, i in enumerate(E):
+        # first k rows win (decoder.rs:679): a source arriving after the k-th
+        # row is recovered too, so the recovered set is the oracle's, not E
+        erased = [int(i) for i in np.nonzero(mask == 0)[0]]
+        assert set(E) <= set(erased) and n_rec[q] == len(erased)
+        assert list(ci[ci_off[q]: ci_off[q] + len(erased)]) == erased
+        for m, i in enumerate(erased):
             got = rec[rec_off[q] + m * rs[q]: rec_off[q] + m * rs[q] + Lb]
             assert (got == sol[i]).all() and (got == src[i]).all(), (q, m)
