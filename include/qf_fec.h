@@ -368,8 +368,9 @@ int qf_adaptive_on_send(qf_adaptive *a, uint64_t id, const uint8_t *data, uint32
                         uint32_t coeff_stride, qf_packet_desc *out_desc, uint32_t out_cap,
                         uint32_t *n_out);
 /* AdaptiveFec::on_receive (adaptive.rs:566-599): recovered packets (the
- * whole generation, ids 0..k-1, when a decoder completes).  QF_EINVAL for
- * a repair packet without coefficients. */
+ * whole generation when a decoder completes, in source order: a received
+ * systematic packet keeps its id, a reconstructed one gets id = i,
+ * decoder.rs:688/771).  QF_EINVAL for a repair packet without coefficients. */
 int qf_adaptive_on_receive(qf_adaptive *a, uint64_t id, int is_systematic, const uint8_t *data,
                            uint32_t len, const uint8_t *coeffs, uint32_t coeff_len,
                            uint8_t *out_data, uint32_t out_stride, qf_packet_desc *out_desc,

@@ -1,0 +1,321 @@
+/*
+ * qf_abi_test.c -- drives libqf_fec.so through include/qf_fec.h from plain C
+ * (TEST INFRASTRUCTURE: the caller a Rust / C integration would be), and
+ * checks every result against the CPU oracle (oracle/liboracle.so).
+ *
+ *   batch     qf_encode_batch / qf_decode_batch       decoder.rs:172-275, 678-791
+ *   desc      qf_encode_batch_desc / qf_decode_batch_desc (mixed windows)
+ *   objects   qf_encoder_* / qf_decoder_*             decoder.rs:155-299, 658-791
+ *   adaptive  qf_adaptive_on_send / on_receive / state adaptive.rs:508-599
+ *   framing   qf_packet_to_raw / from_raw / from_block encoder.rs:18-152
+ *
+ * Exit status 0 and "ALL OK" on success; the first mismatch is printed.
+ */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/qf_fec.h"
+#include "../../oracle/qf_oracle.h"
+
+#define CHECK(cond, ...)                                            \
+    do {                                                            \
+        if (!(cond)) {                                              \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);    \
+            fprintf(stderr, __VA_ARGS__);                           \
+            fprintf(stderr, "\n");                                  \
+            exit(1);                                                \
+        }                                                           \
+    } while (0)
+#define QF(call) CHECK((call) == QF_OK, "%s -> %s", #call, qf_strerror(call))
+#define HIP(call) CHECK((call) == hipSuccess, "%s", #call)
+
+static uint64_t rng_state = 0x51464543u;
+static uint8_t rnd8(void) {
+    rng_state = rng_state * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint8_t)(rng_state >> 56);
+}
+static uint32_t rnd(uint32_t n) {
+    rng_state = rng_state * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint32_t)((rng_state >> 33) % n);
+}
+
+static void *dev_alloc(size_t n) {
+    void *p = NULL;
+    HIP(hipMalloc(&p, n ? n : 16));
+    return p;
+}
+
+/* e distinct sorted source indices < k */
+static void erasures(uint32_t k, uint32_t e, uint32_t *E) {
+    uint8_t taken[256] = {0};
+    for (uint32_t q = 0; q < e;) {
+        uint32_t i = rnd(k);
+        if (!taken[i]) taken[i] = 1, ++q;
+    }
+    for (uint32_t i = 0, q = 0; i < k; ++i)
+        if (taken[i]) E[q++] = i;
+}
+
+static void test_gf(void) {
+    oracle_gf_init();
+    QF(qf_gf256_init());
+    for (int a = 0; a < 256; ++a)
+        for (int b = 0; b < 256; ++b)
+            CHECK(qf_gf256_mul((uint8_t)a, (uint8_t)b) == oracle_gf_mul((uint8_t)a, (uint8_t)b), "mul %d %d", a, b);
+    uint8_t c[64 * 16], o[64 * 16];
+    QF(qf_cauchy_coeffs(64, 16, c));
+    CHECK(oracle_cauchy_coeffs(64, 16, o) == 0 && memcmp(c, o, sizeof c) == 0, "cauchy 64/16");
+    uint8_t x;
+    CHECK(qf_gf256_inv(0, &x) == QF_ERANGE, "inv(0) must be ERANGE (reference panics)");
+}
+
+static void test_batch(qf_ctx *ctx) {
+    const uint32_t k = 64, r = 16, L = 1200, G = 48, e = 13, n = k - e + r, emax = 16;
+    const size_t sb = (size_t)G * k * L, rb = (size_t)G * r * L;
+    uint8_t *src = malloc(sb), *rep = malloc(rb), *want = malloc((size_t)r * L);
+    for (size_t t = 0; t < sb; ++t) src[t] = rnd8();
+    uint8_t *d_src = dev_alloc(sb), *d_rep = dev_alloc(rb);
+    HIP(hipMemcpy(d_src, src, sb, hipMemcpyHostToDevice));
+    qf_encode_shape sh = {k, r, L, 0, L, (uint64_t)k * L, L, (uint64_t)r * L};
+    QF(qf_encode_batch(ctx, &sh, G, d_src, d_rep, NULL));
+    QF(qf_sync(ctx));
+    HIP(hipMemcpy(rep, d_rep, rb, hipMemcpyDeviceToHost));
+    for (uint32_t g = 0; g < G; ++g) {
+        CHECK(oracle_encode_window(k, r, L, src + (size_t)g * k * L, L, NULL, want, L) == 0, "oracle encode");
+        CHECK(memcmp(want, rep + (size_t)g * r * L, (size_t)r * L) == 0, "encode generation %u", g);
+    }
+    /* decode: surviving sources then repairs, first k rows win */
+    uint8_t *rows = malloc((size_t)G * n * L), *rec = malloc((size_t)G * emax * L), *sol = malloc((size_t)k * L);
+    uint16_t *idx = malloc((size_t)G * n * 2), *ridx = malloc((size_t)G * emax * 2);
+    uint32_t E[64], *nrec = malloc(G * 4);
+    int32_t *st = malloc(G * 4);
+    uint32_t *Es = malloc((size_t)G * e * 4);
+    for (uint32_t g = 0; g < G; ++g) {
+        erasures(k, e, E);
+        memcpy(Es + g * e, E, e * 4);
+        uint32_t s = 0;
+        for (uint32_t i = 0, q = 0; i < k; ++i) {
+            if (q < e && E[q] == i) { ++q; continue; }
+            idx[g * n + s] = (uint16_t)i;
+            memcpy(rows + ((size_t)g * n + s++) * L, src + ((size_t)g * k + i) * L, L);
+        }
+        for (uint32_t j = 0; j < r; ++j) {
+            idx[g * n + s] = (uint16_t)(k + j);
+            memcpy(rows + ((size_t)g * n + s++) * L, rep + ((size_t)g * r + j) * L, L);
+        }
+    }
+    uint8_t *d_rows = dev_alloc((size_t)G * n * L), *d_rec = dev_alloc((size_t)G * emax * L);
+    uint16_t *d_idx = dev_alloc((size_t)G * n * 2), *d_ridx = dev_alloc((size_t)G * emax * 2);
+    uint32_t *d_nrec = dev_alloc(G * 4);
+    int32_t *d_st = dev_alloc(G * 4);
+    HIP(hipMemcpy(d_rows, rows, (size_t)G * n * L, hipMemcpyHostToDevice));
+    HIP(hipMemcpy(d_idx, idx, (size_t)G * n * 2, hipMemcpyHostToDevice));
+    qf_decode_shape dsh = {k, r, L, n, L, (uint64_t)n * L, L, (uint64_t)emax * L};
+    QF(qf_decode_batch(ctx, &dsh, G, d_rows, d_idx, NULL, NULL, d_rec, d_ridx, d_nrec, d_st));
+    QF(qf_sync(ctx));
+    HIP(hipMemcpy(rec, d_rec, (size_t)G * emax * L, hipMemcpyDeviceToHost));
+    HIP(hipMemcpy(ridx, d_ridx, (size_t)G * emax * 2, hipMemcpyDeviceToHost));
+    HIP(hipMemcpy(nrec, d_nrec, G * 4, hipMemcpyDeviceToHost));
+    HIP(hipMemcpy(st, d_st, G * 4, hipMemcpyDeviceToHost));
+    uint8_t mask[64];
+    for (uint32_t g = 0; g < G; ++g) {
+        CHECK(st[g] == QF_OK && nrec[g] == e, "decode status %d / n_rec %u of generation %u", st[g], nrec[g], g);
+        CHECK(oracle_decode_generation(k, L, n, idx + g * n, rows + (size_t)g * n * L, L, NULL, sol, L, mask) == 0,
+              "oracle decode");
+        for (uint32_t m = 0; m < e; ++m) {
+            const uint32_t i = Es[g * e + m];
+            CHECK(ridx[g * emax + m] == i && !mask[i], "rec index g %u m %u", g, m);
+            CHECK(memcmp(rec + ((size_t)g * emax + m) * L, sol + (size_t)i * L, L) == 0, "recovered g %u row %u", g, i);
+            CHECK(memcmp(sol + (size_t)i * L, src + ((size_t)g * k + i) * L, L) == 0, "oracle != source");
+        }
+    }
+    hipFree(d_src); hipFree(d_rep); hipFree(d_rows); hipFree(d_rec); hipFree(d_idx); hipFree(d_ridx);
+    hipFree(d_nrec); hipFree(d_st);
+    free(src); free(rep); free(want); free(rows); free(rec); free(sol); free(idx); free(ridx); free(nrec);
+    free(st); free(Es);
+    printf("batch ok\n");
+}
+
+static void test_desc(qf_ctx *ctx) {
+    /* two window shapes interleaved at reversed offsets (C5: Normal 64/10, Medium 160/48) */
+    const uint32_t G = 6, L = 1200;
+    const uint32_t ks[6] = {64, 160, 64, 160, 64, 160}, rs[6] = {10, 48, 10, 48, 10, 48};
+    qf_gen_desc d[6];
+    size_t so = 0, ro = 0;
+    for (int q = 5; q >= 0; --q) {
+        d[q].k = ks[q]; d[q].r = rs[q]; d[q].L = L; d[q].flags = 0;
+        d[q].src_offset = so; d[q].src_row_stride = L;
+        d[q].rep_offset = ro; d[q].rep_row_stride = L;
+        so += (size_t)ks[q] * L + 64;
+        ro += (size_t)rs[q] * L + 32;
+    }
+    uint8_t *src = malloc(so), *rep = malloc(ro), *want = malloc((size_t)48 * L);
+    for (size_t t = 0; t < so; ++t) src[t] = rnd8();
+    uint8_t *d_src = dev_alloc(so), *d_rep = dev_alloc(ro);
+    HIP(hipMemcpy(d_src, src, so, hipMemcpyHostToDevice));
+    QF(qf_encode_batch_desc(ctx, d, G, d_src, d_rep));
+    QF(qf_sync(ctx));
+    HIP(hipMemcpy(rep, d_rep, ro, hipMemcpyDeviceToHost));
+    for (uint32_t q = 0; q < G; ++q) {
+        CHECK(oracle_encode_window(ks[q], rs[q], L, src + d[q].src_offset, L, NULL, want, L) == 0, "oracle");
+        CHECK(memcmp(want, rep + d[q].rep_offset, (size_t)rs[q] * L) == 0, "desc encode generation %u", q);
+    }
+    hipFree(d_src); hipFree(d_rep);
+    free(src); free(rep); free(want);
+    printf("desc ok\n");
+}
+
+static void test_objects(qf_ctx *ctx) {
+    const uint32_t k = 16, n = 20, r = 4, L = 1200, T = 40;
+    qf_encoder *enc;
+    QF(qf_encoder_new(ctx, k, n, L, &enc));
+    uint8_t *pk = malloc((size_t)T * L), out[4 * 1200], coeffs[4 * 16], want[4 * 1200];
+    uint32_t lens[4];
+    uint64_t ids[4];
+    for (size_t t = 0; t < (size_t)T * L; ++t) pk[t] = rnd8();
+    for (uint32_t t = 0; t < T; ++t) {
+        QF(qf_encoder_add_source_packet(enc, 1000 + t, pk + (size_t)t * L, L));
+        const int s = qf_encoder_generate_repairs(enc, 0, r, out, L, lens, coeffs, ids);
+        if (t + 1 < k) {
+            CHECK(s == QF_ENOTREADY, "window not full must be ENOTREADY (reference: None)");
+            continue;
+        }
+        CHECK(s == QF_OK, "generate_repairs %d", s);
+        CHECK(oracle_encode_window(k, r, L, pk + (size_t)(t + 1 - k) * L, L, NULL, want, L) == 0, "oracle");
+        CHECK(memcmp(out, want, sizeof want) == 0, "object repairs after packet %u", t);
+        for (uint32_t j = 0; j < r; ++j) CHECK(ids[j] == 1000 + t + 1 + j && lens[j] == L, "repair id / len");
+    }
+    /* decoder: generation = the last window (ids 1024..1039), 3 sources lost */
+    qf_decoder *dec;
+    QF(qf_decoder_new(ctx, k, L, &dec));
+    const uint32_t lost[3] = {1, 7, 12};
+    int decoded = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        if (i == lost[0] || i == lost[1] || i == lost[2]) continue;
+        decoded = qf_decoder_add_packet(dec, 1024 + i, 1, pk + (size_t)(24 + i) * L, L, NULL, 0);
+        CHECK(decoded == 0, "decoded too early");
+    }
+    CHECK(qf_decoder_add_packet(dec, 99, 0, out, L, NULL, 0) == QF_EINVAL,
+          "repair without coefficients (decoder.rs:699)");
+    for (uint32_t j = 0; j < 3; ++j) decoded = qf_decoder_add_packet(dec, 1040 + j, 0, out + j * L, L, coeffs + j * k, k);
+    CHECK(decoded == 1 && qf_decoder_is_decoded(dec) == 1, "generation not decoded");
+    uint8_t *got = malloc((size_t)k * L);
+    uint32_t glen[16], cnt;
+    uint64_t gid[16];
+    QF(qf_decoder_get_decoded_packets(dec, got, L, glen, gid, &cnt));
+    CHECK(cnt == k, "count %u", cnt);
+    for (uint32_t i = 0; i < k; ++i) {
+        const int was_lost = i == lost[0] || i == lost[1] || i == lost[2];
+        CHECK(gid[i] == (was_lost ? i : 1024 + i), "id rule (decoder.rs:688/771) for packet %u: %llu", i,
+              (unsigned long long)gid[i]);
+        CHECK(glen[i] == L && memcmp(got + (size_t)i * L, pk + (size_t)(24 + i) * L, L) == 0, "packet %u", i);
+    }
+    QF(qf_decoder_get_decoded_packets(dec, got, L, glen, gid, &cnt));
+    CHECK(cnt == 0, "get_decoded_packets drains (take())");
+    QF(qf_decoder_free(dec));
+    QF(qf_encoder_free(enc));
+    free(pk); free(got);
+    printf("objects ok\n");
+}
+
+static void test_adaptive(qf_ctx *ctx) {
+    qf_fec_config cfg;
+    qf_fec_config_default(&cfg);
+    cfg.initial_mode = QF_MODE_NORMAL;
+    cfg.max_len = 1200;
+    QF(qf_fec_config_validate(&cfg));
+    qf_adaptive *snd, *rcv;
+    QF(qf_adaptive_new_at(ctx, &cfg, 0.0, &snd));
+    QF(qf_adaptive_new_at(ctx, &cfg, 0.0, &rcv));
+    int32_t mode, trans;
+    uint32_t k, n;
+    QF(qf_adaptive_state(snd, &mode, NULL, &k, &n, &trans, NULL, NULL));
+    CHECK(mode == QF_MODE_NORMAL && k == 64 && n == 74 && !trans, "Normal mode params_for(64) = (64, 74)");
+    const uint32_t L = 1000, cap = qf_adaptive_max_send_packets(snd);
+    uint8_t *pk = malloc((size_t)k * L), *out = malloc((size_t)cap * 1200), *co = malloc((size_t)cap * 256);
+    qf_packet_desc *desc = malloc(cap * sizeof(qf_packet_desc));
+    uint8_t *want = malloc((size_t)10 * L);
+    for (size_t t = 0; t < (size_t)k * L; ++t) pk[t] = rnd8();
+    uint32_t nout = 0;
+    CHECK(qf_adaptive_on_send(snd, 0, pk, L, out, 100, co, 256, desc, cap, &nout) == QF_ETOOSMALL,
+          "out_stride below max_len must fail before any state change");
+    for (uint32_t i = 0; i < k; ++i) {
+        QF(qf_adaptive_on_send(snd, i, pk + (size_t)i * L, L, out, 1200, co, 256, desc, cap, &nout));
+        CHECK(desc[0].is_systematic && desc[0].id == i && memcmp(out, pk + (size_t)i * L, L) == 0, "systematic out");
+        CHECK(nout == (i + 1 < k ? 1 : 1 + n - k), "packets out after %u: %u", i, nout);
+    }
+    CHECK(oracle_encode_window(k, n - k, L, pk, L, NULL, want, L) == 0, "oracle");
+    for (uint32_t j = 0; j < n - k; ++j)
+        CHECK(memcmp(out + (size_t)(1 + j) * 1200, want + (size_t)j * L, L) == 0 && desc[1 + j].coeff_len == k,
+              "adaptive repair %u", j);
+    /* receiver: 5 sources lost, then the repairs; recovery completes the generation */
+    uint8_t *rout = malloc((size_t)k * 1200);
+    qf_packet_desc *rdesc = malloc(k * sizeof(qf_packet_desc));
+    uint32_t got = 0, m = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        if (i % 13 == 5) continue;
+        QF(qf_adaptive_on_receive(rcv, i, 1, pk + (size_t)i * L, L, NULL, 0, rout, 1200, rdesc, k, &m));
+        got += m;
+    }
+    for (uint32_t j = 0; j < n - k && !got; ++j) {
+        QF(qf_adaptive_on_receive(rcv, k + j, 0, out + (size_t)(1 + j) * 1200, L, co + (size_t)(1 + j) * 256, k,
+                                  rout, 1200, rdesc, k, &m));
+        got += m;
+    }
+    CHECK(got == k, "recovered %u of %u", got, k);
+    for (uint32_t i = 0; i < k; ++i)
+        CHECK(rdesc[i].id == i && memcmp(rout + (size_t)i * 1200, pk + (size_t)i * L, L) == 0, "received %u", i);
+    QF(qf_adaptive_free(snd));
+    QF(qf_adaptive_free(rcv));
+    free(pk); free(out); free(co); free(desc); free(want); free(rout); free(rdesc);
+    printf("adaptive ok\n");
+}
+
+static void test_framing(void) {
+    uint8_t payload[1200], coeffs[64], frame[1300], oframe[1300];
+    for (int t = 0; t < 1200; ++t) payload[t] = rnd8();
+    for (int t = 0; t < 64; ++t) coeffs[t] = rnd8();
+    uint32_t len;
+    size_t olen;
+    QF(qf_packet_to_raw(0, coeffs, 64, payload, 1200, frame, sizeof frame, &len));
+    CHECK(oracle_packet_to_raw(0, 1, coeffs, 64, 1, payload, 1200, oframe, sizeof oframe, &olen) == 0, "oracle");
+    CHECK(len == 1267 && olen == len && memcmp(frame, oframe, len) == 0, "repair frame (1 + 2 + 64 + 1200 B)");
+    CHECK(qf_packet_to_raw(0, coeffs, 64, payload, 1200, frame, 1266, &len) == QF_ETOOSMALL, "BufferTooShort");
+    int sys;
+    const uint8_t *c, *p;
+    uint32_t cl, pl;
+    QF(qf_packet_from_raw(oframe, (uint32_t)olen, &sys, &c, &cl, &p, &pl));
+    CHECK(!sys && cl == 64 && pl == 1200 && memcmp(p, payload, 1200) == 0, "from_raw");
+    uint8_t block[1300] = {0}, blk2[1300] = {0}, cout[64];
+    memcpy(block, oframe, olen);
+    memcpy(blk2, oframe, olen);
+    uint32_t bcl, bpl;
+    QF(qf_packet_from_block(block, sizeof block, (uint32_t)olen, &sys, cout, sizeof cout, &bcl, &bpl));
+    int osys;
+    uint32_t ocl;
+    size_t opl;
+    uint8_t ocout[64];
+    CHECK(oracle_packet_from_block(blk2, sizeof blk2, olen, &osys, ocout, &ocl, &opl) == 0, "oracle from_block");
+    CHECK(sys == osys && bcl == ocl && bpl == opl && memcmp(block, blk2, sizeof block) == 0 &&
+          memcmp(cout, ocout, 64) == 0, "from_block == oracle");
+    printf("framing ok\n");
+}
+
+int main(void) {
+    CHECK(qf_abi_version() == QF_ABI_VERSION, "ABI version");
+    test_gf();
+    test_framing();
+    qf_ctx *ctx;
+    QF(qf_ctx_create(0, NULL, &ctx));
+    test_batch(ctx);
+    test_desc(ctx);
+    test_objects(ctx);
+    test_adaptive(ctx);
+    QF(qf_ctx_destroy(ctx));
+    printf("ALL OK\n");
+    return 0;
+}
