@@ -116,6 +116,7 @@ _ASM = {
     "v_lshl": lambda d, s, a: f"v_lshlrev_b32_e32 {V(d)}, {s}, {V(a)}",
     "v_lshr_s": lambda d, s, a: f"v_lshrrev_b32_e64 {V(d)}, s{s}, {V(a)}",
     "v_addk": lambda d, k, a: f"v_add_u32_e32 {V(d)}, {k}, {V(a)}",
+    "v_add_s": lambda d, s_, a: f"v_add_u32_e32 {V(d)}, s{s_}, {V(a)}",
     "v_sub": lambda d, a, b: f"v_sub_u32_e32 {V(d)}, {V(a)}, {V(b)}",
     "v_lshl_add_s": lambda d, s, sh, a: f"v_lshl_add_u32 {V(d)}, s{s}, {sh}, {V(a)}",
     "v_mul_hi_s": lambda d, a, s: f"v_mul_hi_u32 {V(d)}, {V(a)}, s{s}",
@@ -305,6 +306,11 @@ class KernelSpec:
     # repairs j0 .. j0 + r - 1 of the Cauchy matrix of (k, r_total)
     r_total: int = 0
     j0: int = 0
+    # dec mode, lane-chunk layout: lane l of item w owns units q and q + Q of
+    # ONE generation (f = 64 w + l, g = f / Q, q = f % Q, Q = ceil(Lu / 2)),
+    # so each lane has one slot map, one LU record and one table read per
+    # coefficient for both 16-byte halves (_generate_dec_chunked)
+    chunked: bool = False
 
     @property
     def rt(self) -> int:
@@ -313,6 +319,8 @@ class KernelSpec:
     @property
     def name(self) -> str:
         tag = {"enc": "bs", "syn": "syn", "dec": "dec"}[self.mode]
+        if self.chunked:
+            tag = "decc"
         if self.rt != self.r or self.j0:
             return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}"
         return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
@@ -334,12 +342,16 @@ class KernelSpec:
         return (self.k + self.r + 15) // 16 if self.mode != "enc" else 0
 
     @property
+    def n_maps(self) -> int:
+        return 1 if self.chunked else 2
+
+    @property
     def map_a(self) -> int:
         return self.acc0 + 8 * self.r
 
     @property
     def map_b(self) -> int:
-        return self.map_a + 4 * self.map_quads
+        return self.map_a + (0 if self.chunked else 4 * self.map_quads)
 
     @property
     def map_stride(self) -> int:
@@ -349,7 +361,9 @@ class KernelSpec:
     @property
     def next_free_vgpr(self) -> int:
         n = self.map_b + 4 * self.map_quads
-        if self.mode == "dec":
+        if self.mode == "dec" and self.chunked:
+            n = max(n, lu_layout_chunked(self)["end"])
+        elif self.mode == "dec":
             n = max(n, max(lu_layout(self)[0]) + 4)
         n = (n + 7) // 8 * 8
         if n > 256:
@@ -359,7 +373,7 @@ class KernelSpec:
     @property
     def next_free_sgpr(self) -> int:
         if self.mode == "dec":
-            return SGPR_NEXT_FREE_DEC
+            return SGPR_NEXT_FREE_DEC + (2 if self.chunked else 0)   # chunked: s[76:77] = {16 Q, 0}
         return S_OFFS + 4   # s[66:67]: far-jump target, s[72:75]: offset tables
 
     @property
@@ -634,6 +648,8 @@ def _epilogue_next_item(E, far: bool = False):
 def generate(spec: KernelSpec) -> list[Op]:
     if spec.mode == "enc":
         return _generate_enc(spec)
+    if spec.mode == "dec" and spec.chunked:
+        return _generate_dec_chunked(spec)
     return _generate_syn(spec)
 
 
@@ -969,6 +985,298 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
 
 
 # --------------------------------------------------------------------------
+# Fused decode, lane-chunk layout (spec.chunked)
+# --------------------------------------------------------------------------
+S_QB = 76   # s[76:77] = {16 Q, 0}: byte offset of a lane's B unit from its A unit
+
+
+def lu_layout_chunked(spec) -> dict:
+    """LU-phase registers of the chunked dec kernel (all dead in the row loop
+    unless noted): 16 column quads over the ring, the slot map and the top of
+    the file; the rank quad in the B-pointer / spare pointer registers."""
+    cols = [spec.ring0 + 4 * q for q in range(2 * spec.nbuf)]
+    cols += [spec.map_a + 4 * q for q in range(spec.map_quads)]
+    top = spec.map_a + 4 * spec.map_quads
+    top = (top + 3) // 4 * 4
+    sel = 18                                 # 24 selectors: v18..v41 (combos, zero pointers)
+    tb = (top, top + 6)                      # two table buffers of 5 dwords (b128 at even registers)
+    ta = (top + 5, top + 11)
+    fp = top + 12                            # LU record pointer (2)
+    nxt = top + 14
+    nxt = (nxt + 3) // 4 * 4
+    while len(cols) < spec.r:
+        cols.append(nxt)
+        nxt += 4
+    return {"cols": cols[: spec.r], "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": fp,
+            "end": max(nxt, fp + 2)}
+
+
+def _prologue_chunked(E, spec: KernelSpec):
+    """Prologue of the chunked dec kernel: lane-chunk f = 64 item + lane,
+    g = f / Q, q = f % Q; A unit q, B unit q + Q (loaded iff q + Q < Lu).
+    kernarg s12 = Lu, s13 = Q, s14 = G * Q, s15 / s16 = magic / shift of Q."""
+    E(Op("s_load_args", ()))
+    E(Op("v_lshr", (V_T, 6, V_LANE)))
+    E(Op("v_andk", (V_LANE, 63, V_LANE)))
+    E(Op("v_readfirstlane", (29, V_T)))
+    E(Op("s_load_args_dec", ()))
+    E(Op("s_load_args_offs", (spec.kernarg_bytes - 16,)))
+    E(Op("s_nop", (4,)))
+    E(Op("s_waitcnt_lgkm", ()))
+    # split tables -> LDS (as _prologue)
+    E(Op("s_movk", (62, 4096)))
+    E(Op("s_movk", (63, 0)))
+    E(Op("v_movs", (V_ADDR, 60)))
+    E(Op("v_movs", (V_ADDR + 1, 61)))
+    E(Op("v_mad64_k", (V_ADDR, V_LANE, 16, V_ADDR)))
+    E(Op("v_add64_s", (V_SRCA, V_ADDR, 62)))
+    for q in range(8):
+        E(Op("load16", (48 + 4 * q, V_ADDR if q < 4 else V_SRCA, 1024 * (q % 4))))
+    E(Op("v_lshr", (V_T, 1, V_LANE)))
+    E(Op("v_lshl", (V_T, 8, V_T)))
+    E(Op("v_andk", (V_T + 1, 1, V_LANE)))
+    E(Op("v_lshl", (V_T + 1, 4, V_T + 1)))
+    E(Op("v_xor", (V_T, V_T, V_T + 1)))
+    for b in range(4):
+        E(Op("s_movk", (S_PICK + b, 0x0C0C000C | (b << 8))))
+    E(Op("s_waitcnt_vm", (0,)))
+    for q in range(8):
+        E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * LDS_TAB_STRIDE * q)))
+    E(Op("s_waitcnt_lgkm_n", (0,)))
+    if spec.xcd_remap:
+        E(Op("s_lshrk", (46, 18, 2)))
+        E(Op("s_andk", (47, 2, 7)))
+        E(Op("s_lshrk", (30, 46, 3)))
+        E(Op("s_mul", (30, 47, 30)))
+        E(Op("s_andk", (46, 46, 7)))
+        E(Op("s_min", (46, 47, 46)))
+        E(Op("s_add", (30, 30, 46)))
+        E(Op("s_lshrk", (46, 2, 3)))
+        E(Op("s_add", (30, 30, 46)))
+        E(Op("s_lshl", (30, 30, 2)))
+    else:
+        E(Op("s_lshl", (30, 2, 2)))
+    E(Op("s_add", (28, 29, 30)))
+    E(Op("s_mov", (32, 10)))
+    E(Op("s_movk", (33, 0)))
+    E(Op("s_mov", (34, 11)))
+    E(Op("s_movk", (35, 0)))
+    E(Op("s_lshl", (S_QB, 13, 4)))           # 16 Q
+    E(Op("s_movk", (S_QB + 1, 0)))
+    E(Op("s_movk", (S_ABSENT, ABSENT)))
+    for q, (_, mask, _) in enumerate(_TRANSPOSE):
+        E(Op("s_movk", (S_TMASK + q, mask)))
+    E(Op("label", (".Litem",)))
+    E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
+    E(Op("s_far_jump", (".Lend", 0)))
+    E(Op("label", (".Lgo",)))
+    E(Op("v_lshl_add_s", (V_F, 28, 6, V_LANE)))   # f = 64 item + lane
+    E(Op("v_cmp_gt_s", (26, 14, V_F)))             # f < G * Q
+    E(Op("v_mul_hi_s", (V_GA, V_F, 15)))
+    E(Op("v_lshr_s", (V_GA, 16, V_GA)))            # g
+    E(Op("v_mul_lo_s", (V_UA, V_GA, 13)))
+    E(Op("v_sub", (V_UA, V_F, V_UA)))              # q
+    E(Op("v_add_s", (V_UB, 13, V_UA)))             # q + Q
+    E(Op("v_cmp_gt_s", (S_PAD, 12, V_UB)))         # q + Q < Lu
+    E(Op("s_nop", (4,)))
+    E(Op("s_and64", (S_TMP2, 26, 26)))
+    E(Op("s_and64", (24, 26, S_PAD)))
+    E(Op("s_and64", (S_STA, 26, 26)))
+    E(Op("s_and64", (S_STB, 24, 24)))
+    _gen_base(E, V_SRCA, 4, 8, S_OFFS, V_GA, S_TMP2, "r")
+    E(Op("v_mad64_k", (V_SRCA, V_UA, 16, V_SRCA)))
+    _gen_base(E, V_DSTA, 6, 9, S_OFFS + 2, V_GA, S_TMP2, "d")
+    E(Op("v_mad64_k", (V_DSTA, V_UA, 16, V_DSTA)))
+    E(Op("v_movs", (V_ZA, 22)))
+    E(Op("v_movs", (V_ZA + 1, 23)))
+    E(Op("v_mad64_k", (V_ZA, V_UA, 16, V_ZA)))
+    E(Op("s_nop", (4,)))
+    E(Op("label", (".Lbody",)))
+
+
+def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
+    """Fused decode (syndromes + in-register LU solve, as _generate_syn's dec
+    mode) over the lane-chunk layout: each lane's 32 bytes belong to one
+    generation, so the slot-map gather runs once per row (B address = A +
+    16 Q), and the LU reads each coefficient's split tables once for all 8
+    dwords of a block."""
+    k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
+    C = cauchy(k, r)
+    acc0, ring0, mp = spec.acc0, spec.ring0, spec.map_a
+    ops: list[Op] = []
+    E = ops.append
+    _prologue_chunked(E, spec)
+    # the generation's slot map (payload lanes; padding-free: every lane with a chunk)
+    E(Op("v_movs", (V_ADDR, 20)))
+    E(Op("v_movs", (V_ADDR + 1, 21)))
+    E(Op("v_mad64_s", (V_ADDR, V_GA, 19, V_ADDR)))
+    E(Op("s_exec", (S_STA,)))
+    for q in range(spec.map_quads):
+        E(Op("load16", (mp + 4 * q, V_ADDR, 16 * q)))
+    E(Op("s_exec", (None,)))
+    E(Op("s_waitcnt_vm", (0,)))
+    seq = [("src", i) for i in range(k)] + [("rep", j) for j in range(r)]
+
+    def present(pos: int, sm: int):
+        E(Op("v_bfe", (V_SLOT, mp + pos // 4, 8 * (pos % 4), 8)))
+        E(Op("v_cmp_ne_s", (sm, S_ABSENT, V_SLOT)))
+        E(Op("s_nop", (4,)))
+
+    # jmax over the item's payload lanes
+    for j in reversed(range(r)):
+        present(k + j, S_TMP)
+        E(Op("s_and64", (S_TMP, S_TMP, S_STA)))
+        E(Op("s_movk", (S_JMAX, j + 1)))
+        E(Op("s_cmp_lg64_br", (S_TMP, ".Ljdone")))
+    E(Op("s_movk", (S_JMAX, 0)))
+    E(Op("label", (".Ljdone",)))
+
+    def load_row(n: int):
+        b = ring0 + 8 * (n % nbuf)
+        kind, idx = seq[n]
+        present(idx if kind == "src" else k + idx, S_TMP)
+        E(Op("v_mad64_s", (V_ADDR, V_SLOT, 10, V_SRCA)))
+        E(Op("v_cndmask", (V_ADDR, V_ZA, V_ADDR, S_TMP)))
+        E(Op("v_cndmask", (V_ADDR + 1, V_ZA + 1, V_ADDR + 1, S_TMP)))
+        E(Op("v_add64_s", (V_SRCB, V_ADDR, S_QB)))
+        E(Op("s_exec", (26,)))
+        if not spec.lab_norows:
+            E(Op("load16", (b, V_ADDR, 0, spec.ld_policy)))
+        E(Op("s_exec", (24,)))
+        if not spec.lab_norows:
+            E(Op("load16", (b + 4, V_SRCB, 0, spec.ld_policy)))
+        E(Op("s_exec", (None,)))
+
+    n_seq = len(seq)
+    for n in range(min(pd, n_seq)):
+        load_row(n)
+    for n, (kind, idx) in enumerate(seq):
+        if n + pd < n_seq:
+            load_row(n + pd)
+        after = min(pd, n_seq - 1 - n)
+        E(Op("s_waitcnt_vm", (0 if spec.lab_norows else 2 * after,)))
+        base = ring0 + 8 * (n % nbuf)
+        if kind == "rep":
+            E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
+            ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose))
+            for b in range(8):
+                E(Op("v_xor", (acc0 + 8 * idx + b, acc0 + 8 * idx + b, base + b)))
+            E(Op("label", (f".Lrep{idx}",)))
+        else:
+            _source_row(ops, C, idx, r, base, acc0, init=idx == 0, xor3=spec.xor3, bfi=spec.bfi_transpose,
+                        guard=(spec.guard_min, f".Lrow{n}"))
+    _lu_solve_and_store_chunked(E, spec)
+    _epilogue_next_item(E, far=True)
+    return ops
+
+
+def _lu_solve_and_store_chunked(E, spec: KernelSpec):
+    """_lu_solve_and_store for one generation per lane: one record, 8 dwords
+    per block, one split-table read per coefficient."""
+    r, acc0 = spec.r, spec.acc0
+    lay = lu_layout_chunked(spec)
+    cols, rank, sel, tbs, tas, fp = lay["cols"], lay["rank"], lay["sel"], lay["tb"], lay["ta"], lay["fp"]
+    lu = spec.lu
+
+    def blk(t, d):
+        return acc0 + 8 * t + d
+
+    def selectors(u):
+        for d in range(8):
+            x = blk(u, d)
+            E(Op("v_andk", (sel + d, 0x07070707, x)))
+            E(Op("v_lshr", (sel + 8 + d, 3, x)))
+            E(Op("v_andk", (sel + 8 + d, 0x07070707, sel + 8 + d)))
+            E(Op("v_lshr", (sel + 16 + d, 6, x)))
+            E(Op("v_andk", (sel + 16 + d, 0x03030303, sel + 16 + d)))
+
+    def table_read(u, byte, buf):
+        a, tb = tas[buf], tbs[buf]
+        E(Op("v_perm_s", (a, cols[u] + byte // 4, cols[u] + byte // 4, S_PICK + byte % 4)))
+        E(Op("ds_read_b128", (tb, a, 0)))
+        E(Op("ds_read_b32", (tb + 4, a, 16)))
+
+    def products(d, buf):
+        tb = tbs[buf]
+        E(Op("v_perm", (R_P, tb + 1, tb, sel + d)))
+        E(Op("v_perm", (R_P + 1, tb + 3, tb + 2, sel + 8 + d)))
+        E(Op("v_perm", (R_P + 2, tb + 4, tb + 4, sel + 16 + d)))
+
+    def mul_acc(t, buf):
+        for d in range(8):
+            products(d, buf)
+            E(Op("v_xor3", (blk(t, d), blk(t, d), R_P, R_P + 1)))
+            E(Op("v_xor", (blk(t, d), blk(t, d), R_P + 2)))
+
+    def scale(u, buf):
+        for d in range(8):
+            products(d, buf)
+            E(Op("v_xor3", (blk(u, d), R_P, R_P + 1, R_P + 2)))
+
+    def column(u, steps, end_label, guard_from):
+        table_read(u, steps[0][1], 0)
+        for n, (kind, t) in enumerate(steps):
+            buf = n % 2
+            if n + 1 < len(steps):
+                table_read(u, steps[n + 1][1], 1 - buf)
+                E(Op("s_waitcnt_lgkm_n", (2,)))
+            else:
+                E(Op("s_waitcnt_lgkm_n", (0,)))
+            if kind == "acc":
+                mul_acc(t, buf)
+            else:
+                scale(u, buf)
+            if n + 1 < len(steps) and n + 1 >= guard_from:
+                E(Op("s_cmp_le_k_br", (S_JMAX, steps[n + 1][1], end_label)))
+        E(Op("label", (end_label,)))
+        E(Op("s_waitcnt_lgkm_n", (0,)))
+
+    E(Op("v_movs", (fp, 56)))
+    E(Op("v_movs", (fp + 1, 57)))
+    E(Op("v_mad64_s", (fp, V_GA, 58, fp)))
+    E(Op("s_exec", (S_STA,)))
+    for u in range(r if lu else 0):
+        E(Op("load16", (cols[u], fp, 16 * u)))
+    E(Op("load16", (rank, fp, 256)))
+    E(Op("s_exec", (None,)))
+    if lu:
+        for u in range(r):
+            E(Op("s_cmp_le_k_br", (S_JMAX, u, ".Lfwd_end")))
+            E(Op("s_waitcnt_vm", (r - u,)))
+            selectors(u)
+            column(u, [("scale", u)] + [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}", 1)
+        E(Op("label", (".Lfwd_end",)))
+        E(Op("s_waitcnt_vm", (0,)))
+        for u in reversed(range(1, r)):
+            E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lbwd{u}")))
+            selectors(u)
+            column(u, [("acc", t) for t in range(u)], f".Lbwd{u}", r + 1)
+    else:
+        E(Op("s_waitcnt_vm", (0,)))
+    # stores: block t -> recovered row rank[t]; A half, then B half at + 16 Q
+    E(Op("s_nop", (4,)))
+    st = [c for c in cols]     # column quads are dead now: store address pairs
+    na = 0
+    for t in range(r):
+        E(Op("s_cmp_le_k_br", (S_JMAX, t, ".Lst_end")))
+        a = st[na % len(st)]
+        na += 1
+        E(Op("v_bfe", (V_SLOT, rank + t // 4, 8 * (t % 4), 8)))
+        E(Op("v_cmp_ne_s", (S_TMP, S_ABSENT, V_SLOT)))
+        E(Op("s_nop", (4,)))
+        E(Op("v_mad64_s", (a, V_SLOT, 11, V_DSTA)))
+        E(Op("v_add64_s", (a + 2, a, S_QB)))
+        E(Op("s_and64", (S_TMP2, S_TMP, S_STA)))
+        E(Op("s_exec", (S_TMP2,)))
+        E(Op("store16", (a, blk(t, 0), 0, spec.st_policy)))
+        E(Op("s_and64", (S_TMP2, S_TMP, S_STB)))
+        E(Op("s_exec", (S_TMP2,)))
+        E(Op("store16", (a + 2, blk(t, 4), 0, spec.st_policy)))
+        E(Op("s_exec", (None,)))
+    E(Op("label", (".Lst_end",)))
+
+
+# --------------------------------------------------------------------------
 # Assembly text
 # --------------------------------------------------------------------------
 def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
@@ -1093,7 +1401,7 @@ def launch_geometry(L: int, G: int, Lv: Optional[int] = None) -> tuple[int, int,
 def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
              total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
              Lv: Optional[int] = None, zero_tail: bool = False, lu: Optional[tuple[int, int]] = None,
-             tables: int = 0, src_offs: int = 0, dst_offs: int = 0) -> bytes:
+             tables: int = 0, src_offs: int = 0, dst_offs: int = 0, chunked: bool = False) -> bytes:
     """96-byte kernarg block (layout above; 128 bytes in dec mode).  Syndrome mode: src = received
     rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
     also write zeros to bytes [L, 16 Lv) of every repair row.  Dec mode
@@ -1101,6 +1409,11 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
     drs are the recovered rows' base, generation and row strides; 112 bytes."""
     Lv, total, n_items = launch_geometry(L, G, Lv)
     magic, shift = magic_for(Lv)
+    if chunked:   # lane-chunk layout (_prologue_chunked): Lv <- Q = ceil(Lu / 2)
+        Lv = ((L + 15) // 16 + 1) // 2
+        total = G * Lv
+        n_items = (total + 63) // 64
+        magic, shift = magic_for(Lv)
     s19 = map_stride if smap else (Lv if zero_tail else L // 16)
     if L % 16 and not (zero_tail or smap):
         raise ValueError("enc with L % 16 != 0 needs the zero tail")
@@ -1378,6 +1691,8 @@ class Emulator:
                 wv(a[0], rv(a[2]) >> np.uint64(s[a[1]] & 31))
             elif n == "v_addk":
                 wv(a[0], (rv(a[2]) + np.uint64(a[1])) & np.uint64(MASK32))
+            elif n == "v_add_s":
+                wv(a[0], (rv(a[2]) + np.uint64(s[a[1]])) & np.uint64(MASK32))
             elif n == "v_sub":
                 wv(a[0], (rv(a[1]) - rv(a[2])) & np.uint64(MASK32))
             elif n == "v_lshl_add_s":

@@ -479,7 +479,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
                                 ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
-    prof_end(ctx, st, ev, qf::dec_name(k, r));
+    prof_end(ctx, st, ev, qf::dec_name(k, r, L));
     return QF_OK;
 }
 

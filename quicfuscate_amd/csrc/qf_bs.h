@@ -47,7 +47,7 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // rec + g * rec_gs + rank * rec_rs.  Only the payload bytes [0, L) of a
 // recovered row are written.
 bool dec_available(uint32_t k, uint32_t r);
-const char* dec_name(uint32_t k, uint32_t r);
+const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0);
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,

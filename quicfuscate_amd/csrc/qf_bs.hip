@@ -8,6 +8,7 @@
 // hipModuleLoadData and launches them with a packed kernarg buffer.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "qf_bs.h"
@@ -76,7 +77,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // a partial last unit: enc in the zero-tail lane space (its bytes >= L are
     // masked to zero before the store); syn (the syndrome rows' tail is junk
     // the combine never stores); never the fused decode (caller rows)
-    if ((L % 16 && (e->mode == 'd' || (e->mode == 'e' && Lv != s19))) || L < 32 || sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
+    if ((L % 16 && (e->mode == 'd' || e->mode == 'c' || (e->mode == 'e' && Lv != s19))) || L < 32 ||
+        sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
         return hipErrorInvalidValue;
     if (!cache.fn[idx]) {
@@ -86,12 +88,16 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
         if (err != hipSuccess) return err;
     }
     const uint32_t Lu = (L + 15) / 16;
-    if (Lv < Lu) return hipErrorInvalidValue;
+    // lane-chunk layout of the chunked fused decode ('c'): lane-chunk = units
+    // q and q + Q of one generation, Q = ceil(Lu / 2), 64 lane-chunks per item
+    if (e->mode == 'c') Lv = (Lu + 1) / 2;
+    else if (Lv < Lu) return hipErrorInvalidValue;
+    if (Lv < 2) return hipErrorInvalidValue;
     const uint64_t total = (uint64_t)G * Lv;
     if (total >= (1ull << 31)) return hipErrorInvalidValue;
     uint32_t magic, shift;
     magic_for(Lv, &magic, &shift);
-    const uint32_t n_items = (uint32_t)((total + 127) / 128);
+    const uint32_t n_items = (uint32_t)(e->mode == 'c' ? (total + 63) / 64 : (total + 127) / 128);
     const uint32_t blocks = (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     uint32_t a[32] = {};
@@ -130,7 +136,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[24] = (uint32_t)(uintptr_t)tab256;
     a[25] = (uint32_t)((uintptr_t)tab256 >> 32);
     // generation offset tables, the last 16 kernarg bytes (bs_codegen S_OFFS)
-    const int ot = e->mode == 'd' ? 28 : 20;
+    const int ot = (e->mode == 'd' || e->mode == 'c') ? 28 : 20;
     a[ot] = (uint32_t)(uintptr_t)src_offs;
     a[ot + 1] = (uint32_t)((uintptr_t)src_offs >> 32);
     a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
@@ -189,10 +195,19 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                   nullptr, rows_offs, nullptr);
 }
 
-bool dec_available(uint32_t k, uint32_t r) { return find('d', k, r) != nullptr; }
+// the chunked fused decode unless QF_DECODE_LEGACY=1 (or the row is too short
+// for two units per lane-chunk pair)
+static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L) {
+    const char* leg = getenv("QF_DECODE_LEGACY");
+    const QfBsEntry* c = find('c', k, r);
+    if (c && !(leg && atoi(leg)) && (L == 0 || (L + 15) / 16 >= 3)) return c;
+    return find('d', k, r);
+}
 
-const char* dec_name(uint32_t k, uint32_t r) {
-    const QfBsEntry* e = find('d', k, r);
+bool dec_available(uint32_t k, uint32_t r) { return find_dec(k, r, 0) != nullptr; }
+
+const char* dec_name(uint32_t k, uint32_t r, uint32_t L) {
+    const QfBsEntry* e = find_dec(k, r, L);
     return e ? e->name : nullptr;
 }
 
@@ -201,7 +216,7 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
                       const uint64_t* rows_offs, const uint64_t* rec_offs) {
-    const QfBsEntry* e = find('d', k, r);
+    const QfBsEntry* e = find_dec(k, r, L);
     if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
         return hipErrorInvalidValue;
     // the LU record pointer is computed with a 32-bit stride multiply
