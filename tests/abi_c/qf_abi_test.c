@@ -241,7 +241,7 @@ static void test_adaptive(qf_ctx *ctx) {
     uint8_t *want = malloc((size_t)10 * L);
     for (size_t t = 0; t < (size_t)k * L; ++t) pk[t] = rnd8();
     uint32_t nout = 0;
-    CHECK(qf_adaptive_on_send(snd, 0, pk, L, out, 100, co, 256, desc, cap, &nout) == QF_ETOOSMALL,
+    CHECK(qf_adaptive_on_send(snd, 0, pk, L, out, L, co, 256, desc, cap, &nout) == QF_ETOOSMALL,
           "out_stride below max_len must fail before any state change");
     for (uint32_t i = 0; i < k; ++i) {
         QF(qf_adaptive_on_send(snd, i, pk + (size_t)i * L, L, out, 1200, co, 256, desc, cap, &nout));
