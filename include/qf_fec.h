@@ -367,6 +367,23 @@ int qf_adaptive_on_send(qf_adaptive *a, uint64_t id, const uint8_t *data, uint32
                         uint8_t *out_data, uint32_t out_stride, uint8_t *out_coeffs,
                         uint32_t coeff_stride, qf_packet_desc *out_desc, uint32_t out_cap,
                         uint32_t *n_out);
+/* on_send for M connections at once (the server side of many QUIC
+ * connections, core.rs:170-188 per packet): conns[m] sends packet (ids[m],
+ * data[m], lens[m]).  The result is that of calling qf_adaptive_on_send for
+ * m = 0..M-1 in order -- connection m's packets occupy out_data rows
+ * [first_m, first_m + n_out[m]) with first_m = n_out[0] + ... + n_out[m-1],
+ * and statuses[m] (nullable) gets that call's status -- but the steady-state
+ * GF(2^8) connections of one context share one upload, one small-batch
+ * encode launch per (k, n) class and one download.  A connection may appear
+ * more than once (its packets are taken in order).  out_cap must cover the
+ * sum of qf_adaptive_max_send_packets; out_stride / coeff_stride follow
+ * qf_adaptive_on_send.  An argument error fails the whole call before any
+ * state changes (QF_EINVAL / QF_ETOOSMALL); otherwise QF_OK. */
+int qf_adaptive_on_send_batch(qf_adaptive *const *conns, uint32_t M, const uint64_t *ids,
+                              const uint8_t *const *data, const uint32_t *lens, uint8_t *out_data,
+                              uint32_t out_stride, uint8_t *out_coeffs, uint32_t coeff_stride,
+                              qf_packet_desc *out_desc, uint32_t out_cap, uint32_t *n_out,
+                              int32_t *statuses);
 /* AdaptiveFec::on_receive (adaptive.rs:566-599): recovered packets (the
  * whole generation when a decoder completes, in source order: a received
  * systematic packet keeps its id, a reconstructed one gets id = i,

@@ -23,10 +23,13 @@
 #include <string.h>
 #include <time.h>
 
+#include <algorithm>
 #include <deque>
+#include <unordered_set>
 #include <vector>
 
 #include "qf_fec.h"
+#include "qf_internal.h"
 
 #pragma clang fp contract(off)
 
@@ -335,6 +338,45 @@ int receive_into(Codec& c, uint64_t id, int sys, const uint8_t* data, uint32_t l
     return QF_OK;
 }
 
+// qf_adaptive_on_send's argument checks (no state changes): *need = the
+// packets the call may emit
+int send_check(const qf_adaptive* a, uint32_t len, uint32_t out_stride, const uint8_t* out_coeffs,
+               uint32_t coeff_stride, uint32_t* need) {
+    if (len > a->cfg.max_len || out_stride < len) return QF_EINVAL;
+    const bool fade_repairs = a->has_fade && a->transition_left > kFade / 2;
+    *need = 1 + (a->cur.has_enc() ? a->cur.n - a->cur.k : 0) +
+            (fade_repairs && a->fade.has_enc() ? a->fade.n - a->fade.k : 0);
+    // repairs are window[0].len <= max_len bytes long: check the stride before
+    // the windows advance, so a failing call leaves no state behind
+    if (*need > 1 && out_stride < a->cfg.max_len) return QF_ETOOSMALL;
+    if (out_coeffs) {
+        uint32_t cmax = a->cur.has_enc() ? a->cur.coeff_bytes() : 0;
+        if (fade_repairs && a->fade.has_enc() && a->fade.coeff_bytes() > cmax) cmax = a->fade.coeff_bytes();
+        if (coeff_stride < cmax) return QF_ETOOSMALL;
+    }
+    return QF_OK;
+}
+
+void put_systematic(uint64_t id, const uint8_t* data, uint32_t len, uint8_t* out, qf_packet_desc* d) {
+    if (len) memcpy(out, data, len);
+    d->id = id;
+    d->len = len;
+    d->coeff_len = 0;
+    d->is_systematic = 1;
+    d->reserved = 0;
+}
+
+// adaptive.rs:537-543
+void finish_send(qf_adaptive* a) {
+    if (a->transition_left > 0) {
+        a->transition_left--;
+        if (a->transition_left == kFade / 2) {
+            a->fade.release();
+            a->has_fade = false;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -452,44 +494,117 @@ int qf_adaptive_on_send(qf_adaptive* a, uint64_t id, const uint8_t* data, uint32
                         uint32_t out_cap, uint32_t* n_out) {
     if (!a || !n_out || !out_data || !out_desc || (len && !data)) return QF_EINVAL;
     *n_out = 0;
-    if (len > a->cfg.max_len || out_stride < len) return QF_EINVAL;
-    const bool fade_repairs = a->has_fade && a->transition_left > kFade / 2;
-    uint32_t need = 1 + (a->cur.has_enc() ? a->cur.n - a->cur.k : 0) +
-                    (fade_repairs && a->fade.has_enc() ? a->fade.n - a->fade.k : 0);
+    uint32_t need = 0;
+    int s = send_check(a, len, out_stride, out_coeffs, coeff_stride, &need);
+    if (s != QF_OK) return s;
     if (need > out_cap) return QF_ETOOSMALL;
-    // repairs are window[0].len <= max_len bytes long: check the stride before
-    // the windows advance, so a failing call leaves no state behind
-    if (need > 1 && out_stride < a->cfg.max_len) return QF_ETOOSMALL;
-    if (out_coeffs) {
-        uint32_t cmax = a->cur.has_enc() ? a->cur.coeff_bytes() : 0;
-        if (fade_repairs && a->fade.has_enc() && a->fade.coeff_bytes() > cmax) cmax = a->fade.coeff_bytes();
-        if (coeff_stride < cmax) return QF_ETOOSMALL;
-    }
+    const bool fade_repairs = a->has_fade && a->transition_left > kFade / 2;
     // adaptive.rs:520-526: both encoders take a copy; the systematic packet is sent
-    int s;
     if (a->has_fade && (s = add_source(a->fade, id, data, len)) != QF_OK) return s;
     if ((s = add_source(a->cur, id, data, len)) != QF_OK) return s;
     uint32_t n = 0;
-    if (len) memcpy(out_data, data, len);
-    out_desc[0].id = id;
-    out_desc[0].len = len;
-    out_desc[0].coeff_len = 0;
-    out_desc[0].is_systematic = 1;
-    out_desc[0].reserved = 0;
+    put_systematic(id, data, len, out_data, out_desc);
     n = 1;
     if (fade_repairs && (s = emit_repairs(a->fade, out_data, out_stride, out_coeffs, coeff_stride, out_desc, &n)) != QF_OK)
         return s;
     if ((s = emit_repairs(a->cur, out_data, out_stride, out_coeffs, coeff_stride, out_desc, &n)) != QF_OK) return s;
-    // adaptive.rs:537-543
-    if (a->transition_left > 0) {
-        a->transition_left--;
-        if (a->transition_left == kFade / 2) {
-            a->fade.release();
-            a->has_fade = false;
-        }
-    }
+    finish_send(a);
     *n_out = n;
     return a->cur.status;  // QF_ERANGE: the field has no code for this configuration
+}
+
+int qf_adaptive_on_send_batch(qf_adaptive* const* conns, uint32_t M, const uint64_t* ids, const uint8_t* const* data,
+                              const uint32_t* lens, uint8_t* out_data, uint32_t out_stride, uint8_t* out_coeffs,
+                              uint32_t coeff_stride, qf_packet_desc* out_desc, uint32_t out_cap, uint32_t* n_out,
+                              int32_t* statuses) {
+    if (M == 0) return QF_OK;
+    if (!conns || !ids || !data || !lens || !out_data || !out_desc || !n_out) return QF_EINVAL;
+    // every argument check before any state changes: a connection's need
+    // does not grow from one on_send to the next (only report_loss starts a
+    // cross-fade), so the current state bounds repeated connections too
+    uint64_t total = 0;
+    for (uint32_t m = 0; m < M; ++m) {
+        if (!conns[m] || (lens[m] && !data[m])) return QF_EINVAL;
+        uint32_t need = 0;
+        int s = send_check(conns[m], lens[m], out_stride, out_coeffs, coeff_stride, &need);
+        if (s != QF_OK) return s;
+        total += need;
+        n_out[m] = 0;
+        if (statuses) statuses[m] = QF_OK;
+    }
+    if (total > out_cap) return QF_ETOOSMALL;
+    uint32_t pos = 0;
+    std::vector<qf::EncSend> batch;
+    std::vector<uint32_t> batch_m, predicted;
+    std::unordered_set<const qf_adaptive*> seen;
+    seen.reserve(M);
+    for (uint32_t m0 = 0; m0 < M;) {
+        // a segment: each connection at most once (a repeat starts the next)
+        batch.clear();
+        batch_m.clear();
+        predicted.clear();
+        seen.clear();
+        qf_ctx* ctx = nullptr;
+        uint32_t m = m0;
+        for (; m < M; ++m) {
+            qf_adaptive* a = conns[m];
+            if (!seen.insert(a).second) break;
+            const bool steady = a->ctx && !a->has_fade && a->cur.enc && (!ctx || a->ctx == ctx);
+            if (!steady) {  // cross-fade, GF(2^16), Zero mode, controller only: one on_send
+                uint32_t n = 0;
+                int s = qf_adaptive_on_send(a, ids[m], data[m], lens[m], out_data + (size_t)pos * out_stride,
+                                            out_stride, out_coeffs ? out_coeffs + (size_t)pos * coeff_stride : nullptr,
+                                            coeff_stride, out_desc + pos, out_cap - pos, &n);
+                if (s < 0 && s != QF_ERANGE) return s;
+                if (statuses) statuses[m] = s;
+                n_out[m] = n;
+                pos += n;
+                continue;
+            }
+            ctx = a->ctx;
+            const Codec& c = a->cur;
+            const uint32_t cnt = (uint32_t)qf_encoder_window_len(c.enc);
+            const uint32_t n_rep = (cnt + 1 >= c.k && c.n > c.k) ? c.n - c.k : 0;
+            put_systematic(ids[m], data[m], lens[m], out_data + (size_t)pos * out_stride, out_desc + pos);
+            qf::EncSend x{};
+            x.e = c.enc;
+            x.id = ids[m];
+            x.data = data[m];
+            x.len = lens[m];
+            x.rep_data = out_data + (size_t)(pos + 1) * out_stride;
+            x.rep_stride = out_stride;
+            x.rep_coeffs = out_coeffs ? out_coeffs + (size_t)(pos + 1) * coeff_stride : nullptr;
+            x.coeff_stride = coeff_stride;
+            x.rep_desc = out_desc + pos + 1;
+            batch.push_back(x);
+            batch_m.push_back(m);
+            predicted.push_back(n_rep);
+            n_out[m] = 1 + n_rep;
+            pos += 1 + n_rep;
+        }
+        if (batch.size() == 1) {
+            // one steady connection: the per-packet path (no staging table,
+            // no scatter launch); its rows were placed above, rerun in place
+            const uint32_t mm = batch_m[0];
+            const uint32_t p0 = (uint32_t)(batch[0].rep_desc - out_desc) - 1;
+            uint32_t n = 0;
+            int s = qf_adaptive_on_send(conns[mm], ids[mm], data[mm], lens[mm], out_data + (size_t)p0 * out_stride,
+                                        out_stride, out_coeffs ? out_coeffs + (size_t)p0 * coeff_stride : nullptr,
+                                        coeff_stride, out_desc + p0, out_cap - p0, &n);
+            if (s < 0 && s != QF_ERANGE) return s;
+            if (n != predicted[0] + 1) return QF_EDEVICE;  // internal inconsistency
+            if (statuses) statuses[mm] = s;
+        } else if (!batch.empty()) {
+            int s = qf::encoders_send_batch(ctx, batch.data(), (uint32_t)batch.size());
+            if (s != QF_OK) return s;
+            for (size_t b = 0; b < batch.size(); ++b) {
+                if (batch[b].n_rep != predicted[b]) return QF_EDEVICE;  // internal inconsistency
+                finish_send(conns[batch_m[b]]);
+            }
+        }
+        m0 = m;
+    }
+    return QF_OK;
 }
 
 int qf_adaptive_on_receive(qf_adaptive* a, uint64_t id, int is_systematic, const uint8_t* data, uint32_t len,

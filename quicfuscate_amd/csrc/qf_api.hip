@@ -73,6 +73,8 @@ struct qf_ctx {
     uint8_t* h_desc = nullptr;
     size_t h_desc_bytes = 0;
     hipEvent_t desc_done = nullptr;
+    // send batches: one event per download chunk
+    std::vector<hipEvent_t> send_ev;
     // decode workspace
     uint8_t* d_work = nullptr;
     size_t work_bytes = 0;
@@ -705,6 +707,9 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     return QF_OK;
 }
 
+int desc_stage(qf_ctx* ctx, size_t bytes);
+int desc_upload(qf_ctx* ctx, size_t bytes);
+
 }  // namespace
 
 namespace qf {
@@ -747,6 +752,56 @@ int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, 
     hipEvent_t ev = prof_begin(ctx, ctx->stream);
     QF_CHECK_HIP(qf::launch_encode_small(a, ctx->num_cus, ctx->stream));
     prof_end(ctx, ctx->stream, ev, "k_encode_small");
+    return QF_OK;
+}
+int encode_ring_windows(qf_ctx* ctx, uint32_t k, uint32_t r, uint32_t G, uint32_t max_L, const uint8_t* src,
+                        uint8_t* rep, const RingWin* wins) {
+    if (!ctx || !src || !rep || !wins || k == 0 || r == 0) return QF_EINVAL;
+    if ((uint64_t)k + r > 256) return QF_ERANGE;  // gf_inv(0)
+    if (G == 0 || max_L == 0) return QF_OK;
+    const uint8_t* dcoef = nullptr;
+    int s = small_coef_matrix(ctx, k, r, &dcoef);
+    if (s != QF_OK) return s;
+    qf::EncodeSmallArgs a{};
+    a.src = src;
+    a.rep = rep;
+    a.coef = dcoef;
+    a.tab256 = ctx->d_tab256;
+    a.k = k;
+    a.r = r;
+    a.L = max_L;
+    a.Lu = (max_L + 15) / 16;
+    a.G = G;
+    a.wins = wins;
+    // all repairs of a tile per block once there are enough tiles to fill
+    // the chip; below that the one-repair tiles spread a few windows wider
+    static const uint64_t min_tiles = [] {
+        const char* e = getenv("QF_SEND_WINDOWS_MIN_TILES");
+        return e ? strtoull(e, nullptr, 10) : 256ull;
+    }();
+    const uint64_t tiles = (uint64_t)G * ((a.Lu + 63) / 64);
+    const bool wide = tiles >= min_tiles;
+    hipEvent_t ev = prof_begin(ctx, ctx->stream);
+    QF_CHECK_HIP(wide ? qf::launch_encode_windows(a, ctx->num_cus, ctx->stream)
+                      : qf::launch_encode_small(a, ctx->num_cus, ctx->stream));
+    prof_end(ctx, ctx->stream, ev, wide ? "k_encode_windows" : "k_encode_small");
+    return QF_OK;
+}
+int ctx_desc_buffers(qf_ctx* ctx, size_t bytes, uint8_t** h, uint8_t** d) {
+    int s = desc_stage(ctx, bytes);
+    if (s != QF_OK) return s;
+    *h = ctx->h_desc;
+    *d = ctx->d_desc;
+    return QF_OK;
+}
+int ctx_desc_upload(qf_ctx* ctx, size_t bytes) { return desc_upload(ctx, bytes); }
+int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out) {
+    while (ctx->send_ev.size() < n) {
+        hipEvent_t e = nullptr;
+        QF_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->send_ev.push_back(e);
+    }
+    *out = ctx->send_ev.data();
     return QF_OK;
 }
 int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
@@ -889,6 +944,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->d_desc) hipFree(c->d_desc);
     if (c->h_desc) hipHostFree(c->h_desc);
     if (c->desc_done) hipEventDestroy(c->desc_done);
+    for (hipEvent_t e : c->send_ev) hipEventDestroy(e);
     if (c->d_zero) hipFree(c->d_zero);
     if (c->d_gf16_log) hipFree(c->d_gf16_log);
     if (c->d_gf16_exp) hipFree(c->d_gf16_exp);

@@ -45,4 +45,39 @@ int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, 
 // Whether the small-batch encode is enabled (QF_ENCODE_SMALL != 0).
 bool small_encode_enabled();
 
+// Multi-connection send batches (qf_objects.hip).  The caller holds the
+// context lock (ctx_lock) across these.
+// The context's per-call metadata buffers, pinned host and device, `bytes`
+// each, once the previous call's upload has landed.
+int ctx_desc_buffers(qf_ctx* ctx, size_t bytes, uint8_t** h, uint8_t** d);
+// The first `bytes` of the host buffer to the device buffer, on the context stream.
+int ctx_desc_upload(qf_ctx* ctx, size_t bytes);
+// At least n events of the context (download chunks of a send batch).
+int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out);
+// Small-batch encode of G ring windows of one (k, r) class, repairs = Cauchy
+// rows 0..r-1: window g per wins[g] (device records), rings addressed from
+// src, repairs from rep; max_L (>= every window's L) sizes the grid.
+int encode_ring_windows(qf_ctx* ctx, uint32_t k, uint32_t r, uint32_t G, uint32_t max_L, const uint8_t* src,
+                        uint8_t* rep, const struct RingWin* wins);
+
+// One connection's share of a send batch: a source packet for encoder e, and
+// where repairs 0..n-k-1 of its window go when the add fills it.
+struct EncSend {
+    qf_encoder* e;
+    uint64_t id;
+    const uint8_t* data;
+    uint32_t len;
+    uint8_t* rep_data;            // rows rep_stride apart, >= window[0].len bytes each
+    uint32_t rep_stride;
+    uint8_t* rep_coeffs;          // nullable: k coefficient bytes per repair, coeff_stride apart
+    uint32_t coeff_stride;
+    qf_packet_desc* rep_desc;
+    uint32_t n_rep;               // out: repairs emitted (0, or n - k)
+};
+// qf_encoder_add_source_packet + qf_encoder_generate_repairs(0, n - k) for M
+// distinct encoders of ctx (lengths already checked): one upload, one ring
+// scatter, one small-batch encode per (k, r) class, one download.  The
+// caller does not hold the context lock.
+int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M);
+
 }  // namespace qf

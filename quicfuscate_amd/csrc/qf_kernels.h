@@ -134,6 +134,14 @@ hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, ui
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n, uint64_t seed, uint64_t word_offset,
                                 int num_cus, hipStream_t st);
 
+// One encoder window of a multi-connection send batch: the window's ring at
+// src + src_off (position i in slot (rot + i) % k), its repairs at
+// rep + rep_off, rows rep_row_stride apart.
+struct RingWin {
+    uint64_t src_off, rep_off;
+    uint32_t rot, L, src_row_stride, rep_row_stride;
+};
+
 // Small-batch encode (the per-packet send path: one or a few windows).
 // repair[g][j] = sum_i coef[j*k + i] * src[g][i] over L bytes; lanes over
 // (generation, repair, 16-B unit), units fastest.
@@ -148,7 +156,22 @@ struct EncodeSmallArgs {
     uint32_t rot;            // window row i is source row (i + rot) % k (a ring; 0: plain)
     const uint64_t* src_offs = nullptr;  // generation offset tables (nullptr: strided)
     const uint64_t* rep_offs = nullptr;
+    // per-window records (nullptr: the scalar fields above); L / Lu above are
+    // then the class maxima that size the tile grid
+    const RingWin* wins = nullptr;
 };
+
+// Source packets of a send batch into their encoders' ring slots: bytes
+// [0, len) from the staged copy at stage + src_off (zero padded to 16 bytes
+// by the host), zeros to the slot's stride; dst2 (nullable) is the slot's
+// twin in a double ring.
+struct RingSlot {
+    uint64_t src_off;
+    uint8_t* dst;
+    uint8_t* dst2;
+    uint32_t len, stride;
+};
+hipError_t launch_ring_scatter(const uint8_t* stage, const RingSlot* slots, uint32_t M, hipStream_t st);
 
 // Heterogeneous decode batches (qf_decode_batch_desc): a class's row indices
 // gathered from the caller's arrays into [G][max_rows] (zero past n_rows)...
@@ -181,5 +204,8 @@ __host__ __device__ inline T* gen_base(T* base, uint64_t g, uint64_t stride, con
     return base + (offs ? offs[g] : g * stride);
 }
 hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st);
+// The same over per-window records (a.wins != nullptr), all repairs of a
+// 64-unit tile per block (send batches of many windows).
+hipError_t launch_encode_windows(const EncodeSmallArgs& a, int num_cus, hipStream_t st);
 
 }  // namespace qf

@@ -1384,9 +1384,25 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
         const uint32_t u = (uint32_t)(t - gj * ut) * 64 + lane;
         const uint64_t g = gj / a.r;
         const uint32_t j = (uint32_t)(gj - g * a.r);
-        const bool act = u < a.Lu;
-        const uint32_t nb = act ? min(16u, a.L - 16 * u) : 0u;
-        const uint8_t* sp = gen_base(a.src, g, a.src_gen_stride, a.src_offs) + 16ull * (act ? u : 0);
+        uint32_t L = a.L, rot = a.rot;
+        uint64_t srs = a.src_row_stride, rrs = a.rep_row_stride;
+        const uint8_t* sbase;
+        uint8_t* rbase;
+        if (a.wins) {   // one ring window per generation (send batches)
+            const RingWin w = a.wins[g];
+            L = w.L;
+            rot = w.rot;
+            srs = w.src_row_stride;
+            rrs = w.rep_row_stride;
+            sbase = a.src + w.src_off;
+            rbase = a.rep + w.rep_off;
+        } else {
+            sbase = gen_base(a.src, g, a.src_gen_stride, a.src_offs);
+            rbase = gen_base(a.rep, g, a.rep_gen_stride, a.rep_offs);
+        }
+        const bool act = 16 * u < L;
+        const uint32_t nb = act ? min(16u, L - 16 * u) : 0u;
+        const uint8_t* sp = sbase + 16ull * (act ? u : 0);
         const uint8_t* cp = a.coef + (uint64_t)j * a.k;
         uint4 acc = make_uint4(0, 0, 0, 0);
         for (uint32_t ib = i0; ib < i1; ib += 8) {
@@ -1396,8 +1412,8 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
             for (int q = 0; q < 8; ++q) {
                 const uint32_t i = ib + q;
                 const bool ok = act && i < i1;
-                const uint32_t row = i + a.rot >= a.k ? i + a.rot - a.k : i + a.rot;
-                x[q] = ok ? load_unit(sp + (uint64_t)row * a.src_row_stride, nb) : make_uint4(0, 0, 0, 0);
+                const uint32_t row = i + rot >= a.k ? i + rot - a.k : i + rot;
+                x[q] = ok ? load_unit(sp + (uint64_t)row * srs, nb) : make_uint4(0, 0, 0, 0);
                 c[q] = (i < i1) ? ((uint32_t)cp[i] << 5) : 0u;    // record 0: zero products
             }
 #pragma unroll
@@ -1420,11 +1436,136 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
                 acc.z ^= p.z;
                 acc.w ^= p.w;
             }
-            store_unit(gen_base(a.rep, g, a.rep_gen_stride, a.rep_offs) + (uint64_t)j * a.rep_row_stride + 16ull * u,
-                       acc, nb);
+            store_unit(rbase + (uint64_t)j * rrs + 16ull * u, acc, nb);
         }
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// Send batches (qf_adaptive_on_send_batch): many windows, each with its own
+// ring rotation and length.  k_encode_small gives a tile one repair, so a
+// window's ring is read r times; here a tile = (window, 64 units, RC
+// repairs): each source unit is loaded once per tile and feeds RC
+// accumulators.  The block's four waves split the k rows, the coefficient
+// bytes are wave-uniform (scalar loads), their split-table records LDS
+// broadcasts.  Ring rows are zero padded to their 16-byte stride, so every
+// active lane loads whole units; only the store is cut at L.
+// ---------------------------------------------------------------------------
+template <int RC>
+__global__ void __launch_bounds__(256) k_encode_windows(EncodeSmallArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 8];
+    __shared__ uint4 part[3][RC][64];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.tab256);
+        uint4* l = reinterpret_cast<uint4*>(tab);
+        for (uint32_t w = threadIdx.x; w < 256 * 2; w += blockDim.x) l[w] = g[w];
+    }
+    __syncthreads();
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(tab);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ut = (a.Lu + 63) / 64, nj = (a.r + RC - 1) / RC;
+    const uint64_t tiles = (uint64_t)a.G * ut * nj;
+    const uint32_t kc = ((a.k + 3) / 4 + 1) & ~1u;   // rows per wave (even)
+    const uint32_t i0 = min(a.k, wv * kc), i1 = min(a.k, i0 + kc);
+    for (uint64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
+        const uint64_t g = t / ((uint64_t)ut * nj);
+        const uint32_t rem = (uint32_t)(t - g * ut * nj);
+        const uint32_t jc = rem / ut, u = (rem - jc * ut) * 64 + lane;
+        const RingWin w = a.wins[g];
+        const bool act = 16 * u < w.L;
+        const uint8_t* sp = a.src + w.src_off + 16ull * u;
+        const uint8_t* cp = a.coef + (uint64_t)jc * RC * a.k;
+        const uint32_t jn = min((uint32_t)RC, a.r - jc * RC);
+        uint4 acc[RC];
+#pragma unroll
+        for (int j = 0; j < RC; ++j) acc[j] = make_uint4(0, 0, 0, 0);
+        for (uint32_t i = i0; i < i1; i += 2) {
+            const bool two = i + 1 < i1;
+            const uint32_t ra = i + w.rot >= a.k ? i + w.rot - a.k : i + w.rot;
+            const uint32_t rb = ra + 1 == a.k ? 0 : ra + 1;
+            uint4 xa = make_uint4(0, 0, 0, 0), xb = make_uint4(0, 0, 0, 0);
+            if (act) {
+                xa = *reinterpret_cast<const uint4*>(sp + (uint64_t)ra * w.src_row_stride);
+                if (two) xb = *reinterpret_cast<const uint4*>(sp + (uint64_t)rb * w.src_row_stride);
+            }
+            const Sel sa = selectors(xa), sb = selectors(xb);
+#pragma unroll
+            for (int j = 0; j < RC; ++j) {
+                // rows past the chunk's repairs / the wave's rows: record 0 (zero products)
+                const uint32_t ca = (uint32_t)j < jn ? (uint32_t)cp[(uint64_t)j * a.k + i] << 5 : 0u;
+                const uint32_t cb = ((uint32_t)j < jn && two) ? (uint32_t)cp[(uint64_t)j * a.k + i + 1] << 5 : 0u;
+                const uint4 A = *reinterpret_cast<const uint4*>(tb + ca);
+                const uint32_t a2 = *reinterpret_cast<const uint32_t*>(tb + ca + 16);
+                const uint4 B = *reinterpret_cast<const uint4*>(tb + cb);
+                const uint32_t b2 = *reinterpret_cast<const uint32_t*>(tb + cb + 16);
+                fma_pair(acc[j], A, a2, sa, B, b2, sb);
+            }
+        }
+        if (wv > 0) {
+#pragma unroll
+            for (int j = 0; j < RC; ++j) part[wv - 1][j][lane] = acc[j];
+        }
+        __syncthreads();
+        if (wv == 0 && act) {
+            const uint32_t nb = min(16u, w.L - 16 * u);
+            uint8_t* dp = a.rep + w.rep_off + 16ull * u;
+#pragma unroll
+            for (int j = 0; j < RC; ++j) {
+                if ((uint32_t)j >= jn) continue;
+                uint4 v = acc[j];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const uint4 p = part[q][j][lane];
+                    v.x ^= p.x;
+                    v.y ^= p.y;
+                    v.z ^= p.z;
+                    v.w ^= p.w;
+                }
+                store_unit(dp + (uint64_t)(jc * RC + j) * w.rep_row_stride, v, nb);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_encode_windows(const EncodeSmallArgs& a, int num_cus, hipStream_t st) {
+    if (!a.wins || a.k == 0 || a.r == 0 || a.G == 0 || a.Lu == 0) return hipSuccess;
+    // at most 8 accumulators per lane (more spill); r split into equal chunks
+    const uint32_t ut = (a.Lu + 63) / 64, chunks = (a.r + 7) / 8, per = (a.r + chunks - 1) / chunks;
+    const int RC = per <= 2 ? 2 : per <= 3 ? 3 : per <= 4 ? 4 : per <= 5 ? 5 : per <= 6 ? 6 : 8;
+    const uint64_t tiles = (uint64_t)a.G * ut * ((a.r + RC - 1) / RC);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)num_cus * 8);
+    switch (RC) {
+        case 2: hipLaunchKernelGGL(k_encode_windows<2>, dim3(blocks), dim3(256), 0, st, a); break;
+        case 3: hipLaunchKernelGGL(k_encode_windows<3>, dim3(blocks), dim3(256), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_encode_windows<4>, dim3(blocks), dim3(256), 0, st, a); break;
+        case 5: hipLaunchKernelGGL(k_encode_windows<5>, dim3(blocks), dim3(256), 0, st, a); break;
+        case 6: hipLaunchKernelGGL(k_encode_windows<6>, dim3(blocks), dim3(256), 0, st, a); break;
+        default: hipLaunchKernelGGL(k_encode_windows<8>, dim3(blocks), dim3(256), 0, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+// send batches: block m copies packet m into its ring slot(s), zero padded
+__global__ void __launch_bounds__(128) k_ring_scatter(const uint8_t* stage, const RingSlot* slots, uint32_t M) {
+    for (uint32_t m = blockIdx.x; m < M; m += gridDim.x) {
+        const RingSlot s = slots[m];
+        const uint32_t have = (s.len + 15) / 16, units = s.stride / 16;
+        for (uint32_t v = threadIdx.x; v < units; v += blockDim.x) {
+            const uint4 x = v < have ? *reinterpret_cast<const uint4*>(stage + s.src_off + 16ull * v)
+                                     : make_uint4(0, 0, 0, 0);
+            *reinterpret_cast<uint4*>(s.dst + 16ull * v) = x;
+            if (s.dst2) *reinterpret_cast<uint4*>(s.dst2 + 16ull * v) = x;
+        }
+    }
+}
+
+hipError_t launch_ring_scatter(const uint8_t* stage, const RingSlot* slots, uint32_t M, hipStream_t st) {
+    if (!M) return hipSuccess;
+    hipLaunchKernelGGL(k_ring_scatter, dim3(std::min<uint32_t>(M, 4096)), dim3(128), 0, st, stage, slots, M);
+    return hipGetLastError();
 }
 
 hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st) {

@@ -7,12 +7,20 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <thread>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "gf256_tables.h"
 #include "qf_fec.h"
 #include "qf_bs.h"
 #include "qf_internal.h"
+#include "qf_kernels.h"
 
 #define QF_CHECK_HIP(expr)                         \
     do {                                           \
@@ -70,6 +78,23 @@ struct qf_decoder {
     int32_t* d_status = nullptr;
     uint8_t* h_rec = nullptr;       // pinned download of the recovered rows
 };
+
+namespace {
+
+// Cauchy rows 0..rows-1 in window order (decoder.rs:280-298), cached per encoder
+bool window_rows(qf_encoder* e, uint32_t rows) {
+    const uint32_t k = e->k;
+    if (e->win.size() >= (size_t)rows * k) return true;
+    const auto& f = qf::gf();
+    std::vector<uint8_t> w((size_t)rows * k);
+    for (uint32_t q = 0; q < rows; ++q)
+        for (uint32_t i = 0; i < k; ++i)
+            if (!f.inv((uint8_t)((uint8_t)i ^ (uint8_t)(k + q)), &w[(size_t)q * k + i])) return false;
+    e->win.swap(w);
+    return true;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -147,14 +172,7 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
     // Cauchy rows first..first+count-1 in window order (decoder.rs:280-298),
     // computed once per encoder
     if ((uint64_t)k + first + count > 256) return QF_ERANGE;  // gf_inv(0)
-    const uint32_t rows = first + count;
-    if (e->win.size() < (size_t)rows * k) {
-        const auto& f = qf::gf();
-        e->win.resize((size_t)rows * k);
-        for (uint32_t q = 0; q < rows; ++q)
-            for (uint32_t i = 0; i < k; ++i)
-                if (!f.inv((uint8_t)((uint8_t)i ^ (uint8_t)(k + q)), &e->win[(size_t)q * k + i])) return QF_ERANGE;
-    }
+    if (!window_rows(e, first + count)) return QF_ERANGE;
     const uint8_t* win = e->win.data() + (size_t)first * k;
     if (L > 0) {
         // the window is contiguous in the double ring: repairs 0..count-1 are
@@ -415,3 +433,264 @@ int qf_decoder_get_decoded_packets(qf_decoder* d, uint8_t* out_data, uint32_t ou
 }
 
 }  // extern "C"
+
+namespace qf {
+
+namespace {
+// QF_SEND_PROFILE=1: per-phase host wall time of send batches, printed at exit
+struct SendProfile {
+    bool on = false;
+    uint64_t calls = 0, seen = 0;
+    double t[4] = {0, 0, 0, 0};
+    double u[4] = {0, 0, 0, 0};
+    SendProfile() {
+        const char* e = getenv("QF_SEND_PROFILE");
+        on = e && atoi(e) != 0;
+    }
+    ~SendProfile() {
+        if (on && calls)
+            fprintf(stderr, "[qf send batch] %llu calls, us/call: stage %.1f  launch %.1f  wait %.1f  copy-out %.1f\n",
+                    (unsigned long long)calls, 1e6 * t[0] / calls, 1e6 * t[1] / calls, 1e6 * t[2] / calls,
+                    1e6 * t[3] / calls);
+        if (on && calls)
+            fprintf(stderr, "[qf send batch] stage = host %.1f + buffers %.1f + packets %.1f + upload %.1f\n",
+                    1e6 * u[0] / calls, 1e6 * u[1] / calls, 1e6 * u[2] / calls, 1e6 * u[3] / calls);
+    }
+} g_send_prof;
+double wall() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Host copy-out of large send batches: a few persistent workers plus the
+// calling thread take items off a shared counter (a single-thread memcpy of
+// the ~12 MB of repairs of 1024 windows runs at ~12 GB/s).  QF_COPY_THREADS
+// sets the worker count (0: the calling thread alone).
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static CopyPool p;
+        return p;
+    }
+    // fn(i) for every i < n, across the workers and the calling thread
+    void run(uint32_t n, const std::function<void(uint32_t)>& fn) {
+        if (th_.empty() || n < 2) {
+            for (uint32_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (contexts may send concurrently)
+        std::unique_lock<std::mutex> lk(mu_);
+        job_ = &fn;
+        n_ = n;
+        next_.store(0);
+        busy_ = (uint32_t)th_.size();
+        ++gen_;
+        lk.unlock();
+        cv_.notify_all();
+        drain(fn, n);
+        lk.lock();
+        done_.wait(lk, [&] { return busy_ == 0; });
+        job_ = nullptr;
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+
+  private:
+    CopyPool() {
+        const char* e = getenv("QF_COPY_THREADS");
+        unsigned hw = std::thread::hardware_concurrency();
+        unsigned n = e ? (unsigned)atoi(e) : std::min(7u, hw > 2 ? hw / 2 - 1 : 0u);
+        for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    void drain(const std::function<void(uint32_t)>& fn, uint32_t n) {
+        for (uint32_t i; (i = next_.fetch_add(1)) < n;) fn(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            const std::function<void(uint32_t)>* fn = job_;
+            const uint32_t n = n_;
+            lk.unlock();
+            drain(*fn, n);
+            lk.lock();
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t)>* job_ = nullptr;
+    std::atomic<uint32_t> next_{0};
+    uint32_t n_ = 0, busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+}  // namespace
+
+int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
+    if (!ctx || (M && !v)) return QF_EINVAL;
+    if (M == 0) return QF_OK;
+    const double tp0 = g_send_prof.on ? wall() : 0.0;
+    for (uint32_t m = 0; m < M; ++m) {
+        qf_encoder* e = v[m].e;
+        if (!e || e->ctx != ctx || (v[m].len && !v[m].data) || v[m].len > e->max_len) return QF_EINVAL;
+        if (e->n > e->k && !window_rows(e, e->n - e->k)) return QF_ERANGE;
+    }
+    std::unique_lock<std::mutex> lk;
+    int s = ctx_lock(ctx, lk);
+    if (s) return s;
+    hipStream_t st = ctx_stream(ctx);
+    // the adds (decoder.rs:164-169) on the host side, and the windows they fill
+    struct Win {
+        uint32_t m, rot, L;
+    };
+    std::vector<RingSlot> slots(M);
+    std::vector<Win> wins;
+    size_t pk = 0;
+    for (uint32_t m = 0; m < M; ++m) {
+        qf_encoder* e = v[m].e;
+        const uint32_t slot = e->head;
+        slots[m].src_off = pk;  // relative to the packet area for now
+        slots[m].dst = e->d_ring + (size_t)slot * e->stride;
+        slots[m].dst2 = e->ring_rot ? nullptr : e->d_ring + (size_t)(slot + e->k) * e->stride;
+        slots[m].len = v[m].len;
+        slots[m].stride = e->stride;
+        pk += round16(v[m].len);
+        e->lens[slot] = v[m].len;
+        e->ids[slot] = v[m].id;
+        e->head = (e->head + 1) % e->k;
+        if (e->count < e->k) e->count++;
+        v[m].n_rep = 0;
+        if (e->count == e->k && e->n > e->k) wins.push_back({m, e->head, e->lens[e->head]});
+    }
+    // windows grouped by (k, r) class, repairs packed L-rounded per window
+    std::sort(wins.begin(), wins.end(), [&](const Win& a, const Win& b) {
+        const qf_encoder *x = v[a.m].e, *y = v[b.m].e;
+        return x->k != y->k ? x->k < y->k : x->n != y->n ? x->n < y->n : a.m < b.m;
+    });
+    const size_t slots_off = 0, wins_off = round16((uint32_t)(sizeof(RingSlot) * M));
+    const size_t pk_off = wins_off + round16((uint32_t)(sizeof(RingWin) * wins.size()));
+    const size_t rep_off0 = (pk_off + pk + 255) & ~(size_t)255;
+    std::vector<size_t> rep_off(wins.size());
+    size_t rep_bytes = 0;
+    for (size_t w = 0; w < wins.size(); ++w) {
+        rep_off[w] = rep_off0 + rep_bytes;
+        rep_bytes += (size_t)(v[wins[w].m].e->n - v[wins[w].m].e->k) * round16(wins[w].L);
+    }
+    uint8_t *h = nullptr, *d = nullptr;
+    const double tpa = g_send_prof.on ? wall() : 0.0;
+    if ((s = ctx_desc_buffers(ctx, rep_off0 + rep_bytes, &h, &d)) != QF_OK) return s;
+    const double tpb = g_send_prof.on ? wall() : 0.0;
+    for (uint32_t m = 0; m < M; ++m) {
+        uint8_t* dst = h + pk_off + slots[m].src_off;
+        const uint32_t n = v[m].len, n16 = round16(n);
+        if (n) memcpy(dst, v[m].data, n);
+        if (n16 > n) memset(dst + n, 0, n16 - n);
+        slots[m].src_off += pk_off;
+    }
+    memcpy(h + slots_off, slots.data(), sizeof(RingSlot) * M);
+    const double tpc = g_send_prof.on ? wall() : 0.0;
+    RingWin* hw = reinterpret_cast<RingWin*>(h + wins_off);
+    for (size_t w = 0; w < wins.size(); ++w) {
+        const qf_encoder* e = v[wins[w].m].e;
+        hw[w].src_off = (uint64_t)(uintptr_t)e->d_ring - (uint64_t)(uintptr_t)d;  // wraps when the ring is below d
+        hw[w].rep_off = rep_off[w];
+        hw[w].rot = wins[w].rot;
+        hw[w].L = wins[w].L;
+        hw[w].src_row_stride = e->stride;
+        hw[w].rep_row_stride = round16(wins[w].L);
+    }
+    if ((s = ctx_desc_upload(ctx, pk_off + pk)) != QF_OK) return s;
+    const double tp1 = g_send_prof.on ? wall() : 0.0;
+    QF_CHECK_HIP(launch_ring_scatter(d, reinterpret_cast<const RingSlot*>(d + slots_off), M, st));
+    for (size_t w0 = 0; w0 < wins.size();) {
+        const qf_encoder* e = v[wins[w0].m].e;
+        size_t w1 = w0;
+        uint32_t max_L = 0;
+        while (w1 < wins.size() && v[wins[w1].m].e->k == e->k && v[wins[w1].m].e->n == e->n)
+            max_L = std::max(max_L, wins[w1++].L);
+        s = encode_ring_windows(ctx, e->k, e->n - e->k, (uint32_t)(w1 - w0), max_L, d, d,
+                                reinterpret_cast<const RingWin*>(d + wins_off) + w0);
+        if (s != QF_OK) return s;
+        w0 = w1;
+    }
+    const double tp2 = g_send_prof.on ? wall() : 0.0;
+    // the repairs out (decoder.rs:172-275): window[0].len bytes, ids after the newest
+    auto copy_out = [&](uint32_t w) {
+        EncSend& x = v[wins[w].m];
+        const qf_encoder* e = x.e;
+        const uint32_t r = e->n - e->k, L = wins[w].L, Lr = round16(L);
+        const uint64_t newest = e->ids[(e->head + e->k - 1) % e->k];
+        for (uint32_t q = 0; q < r; ++q) {
+            if (L) memcpy(x.rep_data + (size_t)q * x.rep_stride, h + rep_off[w] + (size_t)q * Lr, L);
+            if (x.rep_coeffs) memcpy(x.rep_coeffs + (size_t)q * x.coeff_stride, e->win.data() + (size_t)q * e->k, e->k);
+            qf_packet_desc& dd = x.rep_desc[q];
+            dd.id = newest + 1 + q;
+            dd.len = L;
+            dd.coeff_len = e->k;
+            dd.is_systematic = 0;
+            dd.reserved = 0;
+        }
+        x.n_rep = r;
+    };
+    // download in chunks of windows, each copied out on the host while the
+    // next one is in flight; large chunks go through the copy workers
+    const uint32_t nw = (uint32_t)wins.size();
+    static const uint32_t max_chunks = [] {
+        const char* e = getenv("QF_SEND_CHUNKS");
+        return e ? std::max(1u, std::min(8u, (uint32_t)atoi(e))) : 1u;
+    }();
+    const uint32_t chunks = nw == 0 ? 0 : std::max(1u, std::min<uint32_t>(max_chunks, (uint32_t)(rep_bytes >> 20)));
+    hipEvent_t* ev = nullptr;
+    if (chunks && (s = ctx_send_events(ctx, chunks, &ev)) != QF_OK) return s;
+    std::vector<uint32_t> cw(chunks + 1, nw);  // first window of each chunk
+    cw[0] = 0;
+    for (uint32_t c = 1, w = 0; c < chunks; ++c) {
+        const size_t target = rep_bytes * c / chunks;
+        while (w < nw && rep_off[w] - rep_off0 < target) ++w;
+        cw[c] = w;
+    }
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const size_t b0 = cw[c] < nw ? rep_off[cw[c]] : rep_off0 + rep_bytes;
+        const size_t b1 = cw[c + 1] < nw ? rep_off[cw[c + 1]] : rep_off0 + rep_bytes;
+        if (b1 > b0) QF_CHECK_HIP(hipMemcpyAsync(h + b0, d + b0, b1 - b0, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipEventRecord(ev[c], st));
+    }
+    double t_wait = 0.0;
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const double tw = g_send_prof.on ? wall() : 0.0;
+        QF_CHECK_HIP(hipEventSynchronize(ev[c]));
+        if (g_send_prof.on) t_wait += wall() - tw;
+        const uint32_t w0 = cw[c], n = cw[c + 1] - cw[c];
+        if ((size_t)(chunks > 1 ? rep_bytes / chunks : rep_bytes) >= ((size_t)1 << 20)) {
+            CopyPool::get().run(n, [&](uint32_t i) { copy_out(w0 + i); });
+        } else {
+            for (uint32_t i = 0; i < n; ++i) copy_out(w0 + i);
+        }
+    }
+    const double tp3 = tp2 + t_wait;
+    if (g_send_prof.on && rep_bytes && ++g_send_prof.seen > 4) {   // steady state: windows full, buffers grown
+        const double tp4 = wall();
+        g_send_prof.calls++;
+        g_send_prof.t[0] += tp1 - tp0;
+        g_send_prof.u[0] += tpa - tp0;
+        g_send_prof.u[1] += tpb - tpa;
+        g_send_prof.u[2] += tpc - tpb;
+        g_send_prof.u[3] += tp1 - tpc;
+        g_send_prof.t[1] += tp2 - tp1;
+        g_send_prof.t[2] += tp3 - tp2;
+        g_send_prof.t[3] += tp4 - tp3;
+    }
+    return QF_OK;
+}
+
+}  // namespace qf

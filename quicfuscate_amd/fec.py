@@ -812,3 +812,45 @@ class AdaptiveFec:
             self.close()
         except Exception:
             pass
+
+
+def on_send_batch(fecs, packets, queues=None):
+    """AdaptiveFec.on_send for many connections in one call
+    (qf_adaptive_on_send_batch): fecs[m] sends packets[m] (a connection may
+    appear more than once; its packets are taken in order).  Appends each
+    connection's outgoing packets to queues[m] (new lists when None) and
+    returns (queues, statuses) -- the same packets and statuses as calling
+    fecs[m].on_send(packets[m], queues[m]) for m in order."""
+    M = len(fecs)
+    if len(packets) != M:
+        raise ValueError("one packet per connection")
+    queues = [[] for _ in range(M)] if queues is None else queues
+    if M == 0:
+        return queues, []
+    lib = L._lib()
+    cap = sum(lib.qf_adaptive_max_send_packets(f.handle) for f in fecs)
+    stride = max(max(f.config.max_len for f in fecs), 1)
+    kmax = max(256, max(2 * f.state()["k"] for f in fecs))
+    conns = (ctypes.c_void_p * M)(*[f.handle for f in fecs])
+    ids = (ctypes.c_uint64 * M)(*[p.id for p in packets])
+    pays = [p.payload() for p in packets]
+    bufs = [(ctypes.c_uint8 * max(1, len(b))).from_buffer_copy(b.ljust(max(1, len(b)), b"\0")) for b in pays]
+    data = (ctypes.c_void_p * M)(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint32 * M)(*[len(b) for b in pays])
+    out = (ctypes.c_uint8 * (cap * stride))()
+    co = (ctypes.c_uint8 * (cap * kmax))()
+    desc = (L.PacketDesc * cap)()
+    n_out = (ctypes.c_uint32 * M)()
+    st = (ctypes.c_int32 * M)()
+    check(lib.qf_adaptive_on_send_batch(conns, M, ids, data, lens, out, stride, co, kmax, desc, cap, n_out, st),
+          "on_send_batch")
+    mv_d, mv_c = memoryview(out), memoryview(co)
+    pos = 0
+    for m in range(M):
+        for i in range(pos, pos + n_out[m]):
+            d = desc[i]
+            payload = bytearray(mv_d[i * stride: i * stride + d.len])
+            coeffs = bytes(mv_c[i * kmax: i * kmax + d.coeff_len]) if not d.is_systematic else None
+            queues[m].append(Packet(d.id, payload, d.len, bool(d.is_systematic), coeffs, d.coeff_len))
+        pos += n_out[m]
+    return queues, list(st)

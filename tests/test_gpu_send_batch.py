@@ -1,0 +1,160 @@
+"""Multi-connection send batches (qf_adaptive_on_send_batch): M connection
+states each send one packet per call, the steady GF(2^8) ones through one
+upload, one small-batch encode launch per (k, n) class and one download.
+Every connection's output equals its twin driven by per-packet on_send
+(adaptive.rs:519-562), and every GF(2^8) repair equals the oracle's encode
+of that connection's window (decoder.rs:172-275)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from quicfuscate_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(qf, mode, max_len=1500, **kw):
+    w = qf.default_windows()
+    w[qf.FecMode.Normal] = kw.pop("normal_window", 64)
+    return qf.FecConfig(initial_mode=mode, max_len=max_len, window_sizes=w, **kw)
+
+
+def _pair(qf, cfg, codec=True):
+    return qf.AdaptiveFec(cfg, now=0.0, codec=codec), qf.AdaptiveFec(cfg, now=0.0, codec=codec)
+
+
+def _same(p, q):
+    return (p.id, p.len, p.is_systematic, p.payload(), p.coeff_len,
+            None if p.coefficients is None else bytes(p.coefficients[: p.coeff_len])) == \
+           (q.id, q.len, q.is_systematic, q.payload(), q.coeff_len,
+            None if q.coefficients is None else bytes(q.coefficients[: q.coeff_len]))
+
+
+def _check_oracle(oracle, k, r, hist, reps):
+    """reps: repairs emitted right after hist[-1] was sent (window = hist[-k:])."""
+    win = hist[-k:]
+    Lw = len(win[0])
+    stride = max([Lw] + [len(b) for b in win])
+    src = np.zeros((k, max(stride, 1)), np.uint8)
+    for i, b in enumerate(win):
+        src[i, : len(b)] = np.frombuffer(b, np.uint8)
+    want = oracle.encode(src, r, L=Lw)
+    C = oracle.cauchy(k, r)
+    assert len(reps) == r
+    for j, p in enumerate(reps):
+        assert p.len == Lw and p.payload() == want[j, :Lw].tobytes()
+        assert p.coeff_len == k and bytes(p.coefficients) == bytes(C[j])
+
+
+def test_send_batch_mixed_connections(qf, oracle, gpu_ctx):
+    M = qf.FecMode
+    specs = [
+        ("normal64", _cfg(qf, M.Normal), True, 1200),
+        ("normal24", _cfg(qf, M.Normal, normal_window=24), True, 1200),
+        ("light_short_stride", _cfg(qf, M.Light, max_len=300), True, 300),
+        ("light_dup", _cfg(qf, M.Light), True, 64),          # appears twice per call
+        ("extreme", None, True, 40),                         # GF(2^16): per-connection path
+        ("zero", _cfg(qf, M.Zero), True, 100),
+        ("controller", _cfg(qf, M.Normal), False, 100),
+        ("fade", _cfg(qf, M.Normal, pid=qf.PidConfig(1.0, 0.0, 0.0), lambda_=0.01, burst_window=50), True, 16),
+        ("strong", _cfg(qf, M.Strong), True, 32),            # QF_ERANGE: no GF(2^8) code
+    ]
+    w = qf.default_windows()
+    w[qf.FecMode.Extreme] = 24
+    specs[4] = ("extreme", qf.FecConfig(initial_mode=M.Extreme, window_sizes=w), True, 40)
+    names = [s[0] for s in specs]
+    pairs = {name: _pair(qf, cfg, codec) for name, cfg, codec, _ in specs}
+    maxlen = {name: ml for name, _, _, ml in specs}
+    pairs["fade"][0].report_loss(0, 20, now=1.0)
+    pairs["fade"][1].report_loss(0, 20, now=1.0)
+    assert pairs["fade"][0].is_transitioning()
+    rng = np.random.default_rng(7)
+    hist = {n: [] for n in names}
+    next_id = {n: 1000 * i for i, n in enumerate(names)}
+    n_checked = 0
+    for rnd in range(72):
+        order = names + ["light_dup"]
+        order = [order[i] for i in rng.permutation(len(order))]
+        fecs, pkts = [], []
+        for n in order:
+            ln = int(rng.integers(0, maxlen[n] + 1)) if rnd % 5 else maxlen[n]
+            b = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            fecs.append(pairs[n][0])
+            pkts.append((n, qf.Packet(next_id[n], bytearray(b), ln, True)))
+            next_id[n] += 1
+        queues, st = qf.on_send_batch(fecs, [p for _, p in pkts])
+        for m, (n, p) in enumerate(pkts):
+            twin_out = []
+            s = pairs[n][1].on_send(qf.Packet(p.id, bytearray(p.payload()), p.len, True), twin_out)
+            assert st[m] == s, (rnd, n)
+            assert len(queues[m]) == len(twin_out), (rnd, n)
+            assert all(_same(a, b) for a, b in zip(queues[m], twin_out)), (rnd, n)
+            hist[n].append(p.payload())
+            sd = pairs[n][0].state()
+            if n in ("normal64", "normal24", "light_short_stride", "light_dup") and len(queues[m]) > 1:
+                _check_oracle(oracle, sd["k"], sd["n"] - sd["k"], hist[n], queues[m][1:])
+                n_checked += 1
+        assert pairs["fade"][0].state() == pairs["fade"][1].state()
+    assert n_checked > 100
+    assert not pairs["fade"][0].is_transitioning()
+
+
+def test_send_batch_many_connections(qf, oracle, gpu_ctx):
+    """384 connections in three (k, n) classes (r = 3, 1, 12: the all-repairs
+    tile kernel with one and two repair chunks), full windows from the k-th call."""
+    M = qf.FecMode
+    w = qf.default_windows()
+    w[M.Medium] = 40
+    cfgs = [_cfg(qf, M.Normal, normal_window=20, max_len=1200), _cfg(qf, M.Light, max_len=1200),
+            qf.FecConfig(initial_mode=M.Medium, max_len=1200, window_sizes=w)]
+    fecs = [qf.AdaptiveFec(cfgs[i % 3], now=0.0) for i in range(384)]
+    ks = [f.state()["k"] for f in fecs]
+    rng = np.random.default_rng(11)
+    hist = [[] for _ in fecs]
+    for rnd in range(max(ks) + 2):
+        pays = [rng.integers(0, 256, 1200 if (rnd + m) % 3 else int(rng.integers(1, 1200)), dtype=np.uint8).tobytes()
+                for m in range(len(fecs))]
+        queues, st = qf.on_send_batch(fecs, [qf.Packet(rnd, bytearray(b), len(b), True) for b in pays])
+        assert st == [L.QF_OK] * len(fecs)
+        for m, f in enumerate(fecs):
+            hist[m].append(pays[m])
+            k, n = f.state()["k"], f.state()["n"]
+            assert queues[m][0].payload() == pays[m]
+            if rnd + 1 < k:
+                assert len(queues[m]) == 1
+            elif m % 7 == 0 or rnd == max(ks) + 1:
+                _check_oracle(oracle, k, n - k, hist[m], queues[m][1:])
+
+
+def test_send_batch_argument_errors(qf, gpu_ctx):
+    lib = L._lib()
+    f = qf.AdaptiveFec(_cfg(qf, qf.FecMode.Light, max_len=100), now=0.0)
+    conns = (ctypes.c_void_p * 2)(f.handle, f.handle)
+    ids = (ctypes.c_uint64 * 2)(1, 2)
+    b = (ctypes.c_uint8 * 100)()
+    data = (ctypes.c_void_p * 2)(ctypes.addressof(b), ctypes.addressof(b))
+    lens = (ctypes.c_uint32 * 2)(100, 100)
+    out = (ctypes.c_uint8 * (100 * 64))()
+    desc = (L.PacketDesc * 64)()
+    n_out = (ctypes.c_uint32 * 2)()
+    cap = lib.qf_adaptive_max_send_packets(f.handle)
+    # out_cap below the sum of max_send_packets: nothing consumed
+    s = lib.qf_adaptive_on_send_batch(conns, 2, ids, data, lens, out, 100, None, 0, desc, 2 * cap - 1, n_out, None)
+    assert s == L.QF_ETOOSMALL
+    lens[1] = 101   # longer than max_len
+    assert lib.qf_adaptive_on_send_batch(conns, 2, ids, data, lens, out, 100, None, 0, desc, 64, n_out,
+                                         None) == L.QF_EINVAL
+    lens[1] = 100   # repairs need out_stride >= max_len
+    assert lib.qf_adaptive_on_send_batch(conns, 2, ids, data, lens, out, 99, None, 0, desc, 64, n_out,
+                                         None) == L.QF_EINVAL
+    assert lib.qf_adaptive_on_send_batch(conns, 0, None, None, None, None, 0, None, 0, None, 0, None, None) == 0
+    # the failed calls left the window empty: a twin that saw nothing agrees
+    twin = qf.AdaptiveFec(_cfg(qf, qf.FecMode.Light, max_len=100), now=0.0)
+    k = f.state()["k"]
+    for i in range(k):
+        q1, _ = qf.on_send_batch([f], [qf.Packet(i, bytearray([i] * 10), 10, True)])
+        q2 = []
+        twin.on_send(qf.Packet(i, bytearray([i] * 10), 10, True), q2)
+        assert len(q1[0]) == len(q2) and all(_same(a, b) for a, b in zip(q1[0], q2))
+    assert len(q1[0]) > 1
