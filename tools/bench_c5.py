@@ -6,7 +6,10 @@ sliding mode (one window per source packet: generation stride = row stride),
 encode and decode at 20 % source loss, device-resident, HIP-event kernel
 times.  Algorithmic bytes: encode (k + r) L per generation, decode (k + e) L.
 
-    python tools/bench_c5.py [--bytes 2e9] [--out gpurun_out/c5_bench.json]
+    python tools/bench_c5.py [--bytes 2e9] [--out gpurun_out/c5_bench.json] [--mixed-only]
+
+The first leg is one heterogeneous batch of all shapes (qf_encode_batch_desc /
+qf_decode_batch_desc, k drawn per generation).
 """
 from __future__ import annotations
 
@@ -42,6 +45,84 @@ def timed(ctx, fn, reps):
     return wall, kt
 
 
+def mixed_leg(qf, ctx, nbytes: float, reps: int, seed: int = 5) -> dict:
+    """One heterogeneous batch (qf_encode_batch_desc / qf_decode_batch_desc):
+    k drawn per generation from the C5 shapes, jumbo rows, 20 % source loss,
+    encoded in one call and decoded in one call.  Every generation's
+    recovered rows are compared with its erased sources (round trip; the
+    oracle comparison is tests/test_gpu_desc.py)."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    mean_k = float(np.mean([k for k, _ in SHAPES]))
+    G = max(len(SHAPES), int(nbytes // (mean_k * L_JUMBO)))
+    kind = rng.integers(0, len(SHAPES), G)
+    ks = np.array([SHAPES[i][0] for i in kind])
+    rs = np.array([SHAPES[i][1] for i in kind])
+    es = np.minimum(rs, np.maximum(1, np.round(0.2 * ks))).astype(np.int64)
+    src_row0 = np.concatenate([[0], np.cumsum(ks)[:-1]])          # first source row of each generation
+    rep_row0 = np.concatenate([[0], np.cumsum(rs)[:-1]])
+    nrows = ks - es + rs
+    row0 = np.concatenate([[0], np.cumsum(nrows)[:-1]])
+    rec_row0 = np.concatenate([[0], np.cumsum(es)[:-1]])
+    src = torch.randint(0, 256, (int(ks.sum()) * RS,), dtype=torch.uint8, device="cuda")
+    rep = torch.empty(int(rs.sum()) * REP_RS, dtype=torch.uint8, device="cuda")
+    gdesc = [dict(k=int(ks[g]), r=int(rs[g]), L=L_JUMBO, flags=1, src_offset=int(src_row0[g]) * RS, src_row_stride=RS,
+                  rep_offset=int(rep_row0[g]) * REP_RS, rep_row_stride=REP_RS) for g in range(G)]
+
+    def enc():
+        qf.encode_batch_desc(src, rep, gdesc)
+
+    wall_e, kt_e = timed(ctx, enc, reps)
+    # received rows: survivors in source order, then every repair; the first
+    # k rows are accepted (decoder.rs:679), so the first e repairs decode
+    ridx, s_from, s_to, r_from, r_to, lost_src, lost_rec = [], [], [], [], [], [], []
+    for g in range(G):
+        k, r, e = int(ks[g]), int(rs[g]), int(es[g])
+        E = np.sort(rng.choice(k, e, replace=False))
+        keep = np.setdiff1d(np.arange(k), E)
+        ridx.append(np.concatenate([keep, k + np.arange(r)]).astype(np.uint16))
+        s_from.append(src_row0[g] + keep)
+        s_to.append(row0[g] + np.arange(k - e))
+        r_from.append(rep_row0[g] + np.arange(r))
+        r_to.append(row0[g] + k - e + np.arange(r))
+        lost_src.append(src_row0[g] + E)
+        lost_rec.append(rec_row0[g] + np.arange(e))
+    cat = lambda xs: torch.from_numpy(np.concatenate(xs).astype(np.int64)).cuda()  # noqa: E731
+    src2 = src.view(-1, RS)
+    rep2 = rep.view(-1, REP_RS)[:, :RS]
+    rows = torch.empty((int(nrows.sum()), RS), dtype=torch.uint8, device="cuda")
+    rows[cat(s_to)] = src2[cat(s_from)]
+    rows[cat(r_to)] = rep2[cat(r_from)]
+    t_idx = torch.from_numpy(np.concatenate(ridx).view(np.int16)).cuda()
+    rec = torch.empty((int(es.sum()), RS), dtype=torch.uint8, device="cuda")
+    rec_index = torch.empty(int(rs.sum()), dtype=torch.int16, device="cuda")   # min(k, r) = r entries each
+    n_rec = torch.empty(G, dtype=torch.int32, device="cuda")
+    status = torch.empty(G, dtype=torch.int32, device="cuda")
+    ddesc = [dict(k=int(ks[g]), r=int(rs[g]), L=L_JUMBO, n_rows=int(nrows[g]), rows_offset=int(row0[g]) * RS,
+                  row_stride=RS, row_index_offset=int(row0[g]), rec_offset=int(rec_row0[g]) * RS, rec_row_stride=RS,
+                  rec_index_offset=int(rep_row0[g])) for g in range(G)]
+
+    def dec():
+        qf.decode_batch_desc(rows.view(-1), t_idx, rec.view(-1), rec_index, n_rec, status, ddesc)
+
+    wall_d, kt_d = timed(ctx, dec, reps)
+    ok = bool((status == 0).all().item() and torch.equal(n_rec.cpu(), torch.from_numpy(es.astype(np.int32))))
+    ok = ok and torch.equal(rec[:, :L_JUMBO], src2[cat(lost_src)][:, :L_JUMBO])
+    kms_e = sum(ms for _, ms in kt_e.values())
+    kms_d = sum(ms for _, ms in kt_d.values())
+    enc_b = float(((ks + rs) * L_JUMBO).sum())
+    dec_b = float(((ks + es) * L_JUMBO).sum())
+    return {"G": G, "shapes": {f"k{k}_r{r}": int((kind == i).sum()) for i, (k, r) in enumerate(SHAPES)},
+            "round_trip_ok": ok,
+            "encode": {"wall_ms": round(wall_e, 3), "kernels": kt_e,
+                       "GiBps_alg": round(enc_b / (kms_e / 1e3) / 2**30, 1),
+                       "GiBps_wall": round(enc_b / (wall_e / 1e3) / 2**30, 1)},
+            "decode": {"wall_ms": round(wall_d, 3), "kernels": kt_d,
+                       "GiBps_alg": round(dec_b / (kms_d / 1e3) / 2**30, 1),
+                       "GiBps_wall": round(dec_b / (wall_d / 1e3) / 2**30, 1)}}
+
+
 def main():
     import torch
 
@@ -53,10 +134,13 @@ def main():
     ap.add_argument("--out", default="gpurun_out/c5_bench.json")
     ap.add_argument("--exact-rows", action="store_true",
                     help="dense repair rows without the zero tail (general v_perm encode kernel)")
+    ap.add_argument("--mixed-only", action="store_true", help="only the heterogeneous (desc API) batch")
     a = ap.parse_args()
     ctx = qf.default_context()
-    res = {}
-    for k, r in SHAPES:
+    res = {"mixed_desc_batch": mixed_leg(qf, ctx, a.bytes, a.reps)}
+    print("mixed", {k: v for k, v in res["mixed_desc_batch"].items() if k in ("G", "round_trip_ok")},
+          res["mixed_desc_batch"]["encode"]["GiBps_alg"], res["mixed_desc_batch"]["decode"]["GiBps_alg"], flush=True)
+    for k, r in ([] if a.mixed_only else SHAPES):
         G = max(1, int(a.bytes // (k * L_JUMBO)))
         for mode in ("block", "sliding"):
             if mode == "block":
