@@ -182,6 +182,23 @@ _ASM = {
     "s_or64": lambda d, a, b: f"s_or_b64 {SP(d)}, {SP(a)}, {SP(b)}",
     "s_cmp_lg64_br": lambda s, lbl: f"s_cmp_lg_u64 {SP(s)}, 0\n\ts_cbranch_scc1 {lbl}",
     "s_endpgm": lambda: "s_endpgm",
+    # synw (wave-uniform slot lookup): scalar map / base arithmetic, saddr loads
+    "s_load_karg_x2": lambda d, off: f"s_load_dwordx2 {SP(d)}, s[0:1], 0x{off:x}",
+    "s_load_x1": lambda d, a, off: f"s_load_dword s{d}, {SP(a)}, 0x{off:x}",
+    "s_load_x2": lambda d, a, off: f"s_load_dwordx2 {SP(d)}, {SP(a)}, 0x{off:x}",
+    "s_load_x4": lambda d, a, off: f"s_load_dwordx4 s[{d}:{d + 3}], {SP(a)}, 0x{off:x}",
+    "s_addk": lambda d, a, k: f"s_add_u32 s{d}, s{a}, {k}",
+    "s_add_cc": lambda d, a, b: f"s_add_u32 s{d}, s{a}, s{b}",
+    "s_addc": lambda d, a, b: f"s_addc_u32 s{d}, s{a}, s{b}",
+    "s_addck": lambda d, a, k: f"s_addc_u32 s{d}, s{a}, {k}",
+    "s_mul_hi": lambda d, a, b: f"s_mul_hi_u32 s{d}, s{a}, s{b}",
+    "s_max": lambda d, a, b: f"s_max_u32 s{d}, s{a}, s{b}",
+    "s_lshr_s": lambda d, a, b: f"s_lshr_b32 s{d}, s{a}, s{b}",
+    "s_bfe_k": lambda d, a, off, w: f"s_bfe_u32 s{d}, s{a}, 0x{off | (w << 16):x}",
+    "s_cmp_eq_k": lambda a, k: f"s_cmp_eq_u32 s{a}, 0x{k:x}",
+    "s_cselect64": lambda d, a, b: f"s_cselect_b64 {SP(d)}, {SP(a)}, {SP(b)}",
+    "load16_saddr": lambda d, voff, sb, pol="": f"global_load_dwordx4 {VQ(d)}, {V(voff)}, {SP(sb)}"
+                    + (f" {pol}" if pol else ""),
 }
 
 
@@ -267,6 +284,22 @@ def lu_layout(spec) -> tuple[list[int], tuple[int, int]]:
         slots.append(end)
         end += 4
     return slots[2: 2 + spec.r], (slots[0], slots[1])
+# synw mode (wave-uniform slot lookup, _generate_synw): kernarg words 24..25
+# (byte 0x60) = per-generation bound (1 + the largest accepted repair index,
+# k_decode_prepare_cauchy) or 0.  An item's units lie in generations g0 and
+# g1 = min(g0 + 1, G - 1); per row, the scalar unit reads both generations'
+# slot bytes and forms each one's row address (zero row if absent), and the
+# halves load with that address as saddr under the lanes of each generation.
+KERNARG_BYTES_SYNW = 104
+SW_A0, SW_A1, SW_B0, SW_B1 = 54, 56, 58, 60   # load lanes: half A / B x generation g0 / g1
+SW_R0, SW_R1 = 62, 64                         # received-row bases of g0 / g1
+SW_M0, SW_M1 = 68, 70                         # slot-map pointers of g0 / g1
+SW_BOUND = 76                                 # s[76:77] bound table (kernarg)
+SW_G0, SW_G1, SW_GLAST = 78, 79, 80           # g0, g1, G - 1
+SW_Q0, SW_Q1 = 84, 88                         # the current map quad of g0 / g1 (4 SGPRs each)
+SW_BASE0, SW_BASE1 = 92, 94                   # this row's address in g0 / g1
+SW_T0, SW_T1 = 96, 97                         # slot bytes / temps
+SW_NEXT_FREE = 98
 S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
@@ -277,7 +310,9 @@ class KernelSpec:
     k: int
     r: int
     pd: int = 3
-    mode: str = "enc"   # "enc": repairs of the Cauchy code; "syn": decode syndromes
+    mode: str = "enc"   # "enc": repairs of the Cauchy code; "syn": decode syndromes;
+    # "synw": decode syndromes with the slot map read per row by the scalar unit
+    # (an item spans at most two generations: padded row units >= 128)
     xor3: bool = True   # acc ^= L ^ H as one v_bitop3_b32 (3-input XOR, full rate)
     # cache policy of the streamed rows: read once / written once, so
     # non-temporal (tools/bs_lab.py: -9 % at C2 vs the default policy)
@@ -318,7 +353,7 @@ class KernelSpec:
 
     @property
     def name(self) -> str:
-        tag = {"enc": "bs", "syn": "syn", "dec": "dec"}[self.mode]
+        tag = {"enc": "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
             tag = "decc"
         if self.rt != self.r or self.j0:
@@ -339,7 +374,8 @@ class KernelSpec:
 
     @property
     def map_quads(self) -> int:
-        return (self.k + self.r + 15) // 16 if self.mode != "enc" else 0
+        """Slot-map quads held in VGPRs per half (synw reads the map with scalar loads)."""
+        return (self.k + self.r + 15) // 16 if self.mode in ("syn", "dec") else 0
 
     @property
     def n_maps(self) -> int:
@@ -356,6 +392,8 @@ class KernelSpec:
     @property
     def map_stride(self) -> int:
         """Bytes per generation in the slot map (k source + r repair slots)."""
+        if self.mode == "synw":
+            return 16 * ((self.k + self.rt + 15) // 16)
         return 16 * self.map_quads
 
     @property
@@ -372,6 +410,8 @@ class KernelSpec:
 
     @property
     def next_free_sgpr(self) -> int:
+        if self.mode == "synw":
+            return SW_NEXT_FREE
         if self.mode == "dec":
             return SGPR_NEXT_FREE_DEC + (2 if self.chunked else 0)   # chunked: s[76:77] = {16 Q, 0}
         return S_OFFS + 4   # s[66:67]: far-jump target, s[72:75]: offset tables
@@ -384,7 +424,14 @@ class KernelSpec:
 
     @property
     def kernarg_bytes(self) -> int:
+        if self.mode == "synw":
+            return KERNARG_BYTES_SYNW
         return KERNARG_BYTES_DEC if self.mode == "dec" else KERNARG_BYTES
+
+    @property
+    def offs_kernarg(self) -> int:
+        """Byte offset of the generation offset tables in the kernarg block."""
+        return KERNARG_BYTES - 16 if self.mode == "synw" else self.kernarg_bytes - 16
 
     @property
     def lds_bytes(self) -> int:
@@ -520,7 +567,9 @@ def _prologue(E, spec: KernelSpec):
     E(Op("v_readfirstlane", (29, V_T)))
     if spec.mode == "dec":
         E(Op("s_load_args_dec", ()))
-    E(Op("s_load_args_offs", (spec.kernarg_bytes - 16,)))
+    E(Op("s_load_args_offs", (spec.offs_kernarg,)))
+    if spec.mode == "synw":
+        E(Op("s_load_karg_x2", (SW_BOUND, KERNARG_BYTES)))   # kernarg words 24..25
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
     if spec.mode == "dec":
@@ -570,6 +619,10 @@ def _prologue(E, spec: KernelSpec):
     E(Op("s_mov", (34, 11)))
     E(Op("s_movk", (35, 0)))
     E(Op("s_movk", (S_ABSENT, ABSENT)))
+    if spec.mode == "synw":   # G - 1 = (total - 1) / Lv
+        E(Op("s_addk", (SW_GLAST, 14, -1)))
+        E(Op("s_mul_hi", (SW_GLAST, SW_GLAST, 15)))
+        E(Op("s_lshr_s", (SW_GLAST, SW_GLAST, 16)))
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (S_TMASK + q, mask)))
     E(Op("label", (".Litem",)))
@@ -600,14 +653,17 @@ def _prologue(E, spec: KernelSpec):
         E(Op("s_nop", (4,)))
         # (dec: the recovered rows are caller memory -> payload lanes only)
         E(Op("s_and64", (S_TMP2, vm, vm)))   # lanes with a unit (offset-table loads)
-        E(Op("s_and64", (sm, vm, {"enc": S_TMP, "syn": vm, "dec": S_PAD}[spec.mode])))
+        E(Op("s_and64", (sm, vm, {"enc": S_TMP, "syn": vm, "synw": vm, "dec": S_PAD}[spec.mode])))
         E(Op("s_and64", (vm, vm, S_PAD)))
         # src/dst + g * gen_stride + 16 u   (VOP3 reads at most one SGPR), or
         # src/dst + table[g] + 16 u with a generation offset table
         for x, (ptr, base_s, gs_s) in enumerate(((sv, 4, 8), (dv, 6, 9))):
+            if spec.mode == "synw" and x == 0:
+                E(Op("v_lshl", (sv, 4, uv)))     # synw: the row address is scalar, the lane adds 16 u
+                continue
             _gen_base(E, ptr, base_s, gs_s, S_OFFS + 2 * x, gv, S_TMP2, f"{h}{x}")
             E(Op("v_mad64_k", (ptr, uv, 16, ptr)))
-        if spec.mode != "enc":
+        if spec.mode in ("syn", "dec"):
             z = V_ZA if h == 0 else V_ZB
             E(Op("v_movs", (z, 22)))
             E(Op("v_movs", (z + 1, 23)))
@@ -648,6 +704,8 @@ def _epilogue_next_item(E, far: bool = False):
 def generate(spec: KernelSpec) -> list[Op]:
     if spec.mode == "enc":
         return _generate_enc(spec)
+    if spec.mode == "synw":
+        return _generate_synw(spec)
     if spec.mode == "dec" and spec.chunked:
         return _generate_dec_chunked(spec)
     return _generate_syn(spec)
@@ -984,6 +1042,138 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
     return ops
 
 
+def _scalar_gen_base(E, dst: int, base_s: int, gs_s: int, tab_s: int, g: int, tag: str):
+    """s[dst:dst+1] <- s[base_s:+1] + g * s[gs_s], or + table[g] when the
+    64-bit table pointer s[tab_s:tab_s+1] is non-zero (scalar unit)."""
+    E(Op("s_cmp_eq64_0_br", (tab_s, f".Lsgs{tag}")))
+    E(Op("s_lshl", (SW_T0, g, 3)))
+    E(Op("s_lshrk", (SW_T1, g, 29)))
+    E(Op("s_add_cc", (SW_T0, SW_T0, tab_s)))
+    E(Op("s_addc", (SW_T1, SW_T1, tab_s + 1)))
+    E(Op("s_load_x2", (dst, SW_T0, 0)))
+    E(Op("s_waitcnt_lgkm", ()))
+    E(Op("s_add_cc", (dst, dst, base_s)))
+    E(Op("s_addc", (dst + 1, dst + 1, base_s + 1)))
+    E(Op("s_branch", (f".Lsgd{tag}",)))
+    E(Op("label", (f".Lsgs{tag}",)))
+    E(Op("s_mul", (dst, g, gs_s)))
+    E(Op("s_mul_hi", (dst + 1, g, gs_s)))
+    E(Op("s_add_cc", (dst, dst, base_s)))
+    E(Op("s_addc", (dst + 1, dst + 1, base_s + 1)))
+    E(Op("label", (f".Lsgd{tag}",)))
+
+
+def _synw_item_setup(E, spec: KernelSpec):
+    """Per item: g0 / g1, the four load-lane masks, both generations' row
+    bases and slot-map pointers; items whose generations accepted no repair
+    of this pass (bound <= j0 for both) skip to the next item."""
+    E(Op("s_exec", (None,)))
+    E(Op("v_readfirstlane", (SW_G0, V_GA)))          # lane 0, unit A: the item's first unit
+    E(Op("s_addk", (SW_G1, SW_G0, 1)))
+    E(Op("s_min", (SW_G1, SW_G1, SW_GLAST)))
+    for gv, vm, m0, m1 in ((V_GA, 26, SW_A0, SW_A1), (V_GB, 24, SW_B0, SW_B1)):
+        E(Op("v_cmp_eq_s", (S_TMP, SW_G0, gv)))
+        E(Op("s_nop", (4,)))
+        E(Op("s_and64", (m0, vm, S_TMP)))
+        E(Op("s_andn2_64", (m1, vm, S_TMP)))
+    for t, (g, R, Mp) in enumerate(((SW_G0, SW_R0, SW_M0), (SW_G1, SW_R1, SW_M1))):
+        _scalar_gen_base(E, R, 4, 8, S_OFFS, g, f"r{t}")
+        E(Op("s_mul", (Mp, g, 19)))
+        E(Op("s_mul_hi", (Mp + 1, g, 19)))
+        E(Op("s_add_cc", (Mp, Mp, 20)))
+        E(Op("s_addc", (Mp + 1, Mp + 1, 21)))
+    # pass skip: no lane's generation accepted a repair >= j0
+    E(Op("s_cmp_eq64_0_br", (SW_BOUND, ".Lnobound")))
+    for t, g in enumerate((SW_G0, SW_G1)):
+        E(Op("s_lshl", (SW_BASE0, g, 2)))
+        E(Op("s_add_cc", (SW_BASE0, SW_BASE0, SW_BOUND)))
+        E(Op("s_addck", (SW_BASE0 + 1, SW_BOUND + 1, 0)))
+        E(Op("s_load_x1", (SW_T0 + t, SW_BASE0, 0)))
+        E(Op("s_waitcnt_lgkm", ()))
+    E(Op("s_max", (SW_T0, SW_T0, SW_T1)))
+    E(Op("s_cmp_le_k_br", (SW_T0, spec.j0, ".Lskipnear")))
+    E(Op("s_branch", (".Lnobound",)))
+    E(Op("label", (".Lskipnear",)))
+    E(Op("s_far_jump", (".Lskip", 2)) if spec.far else Op("s_branch", (".Lskip",)))
+    E(Op("label", (".Lnobound",)))
+
+
+def _generate_synw(spec: KernelSpec) -> list[Op]:
+    """Decode stage A for long rows (padded units per row >= 128): syndromes
+    s_j = p_j ^ sum_{i present} C[j][i] x_i of repairs j0 .. j0 + r - 1 of the
+    (k, r_total) code, for every unit of every generation, without the slot
+    map in VGPRs -- so it takes r up to 22 per pass at any k.
+
+    An item (128 consecutive units) lies in at most two generations.  For
+    each row the scalar unit loads the slot bytes of both (one 16-byte map
+    quad per 16 rows and generation), forms the row address of each (the
+    zero row when absent) and the halves load with it as saddr plus 16 u,
+    under the lanes of the respective generation (four loads per row).
+    Rows stream as in _generate_syn (repairs initialise the accumulators);
+    syndromes of all r repairs are stored, the unaccepted ones are junk the
+    combine never reads."""
+    k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
+    C = cauchy(k, spec.rt)[spec.j0: spec.j0 + r]
+    acc0, ring0 = spec.acc0, spec.ring0
+    seq = [("rep", j) for j in range(r)] + [("src", i) for i in range(k)]
+    ops: list[Op] = []
+    E = ops.append
+    _prologue(E, spec)
+    _synw_item_setup(E, spec)
+    quad = [None]
+
+    def load_row(n: int):
+        kind, idx = seq[n]
+        pos = k + spec.j0 + idx if kind == "rep" else idx
+        q = pos // 16
+        if quad[0] != q:
+            E(Op("s_load_x4", (SW_Q0, SW_M0, 16 * q)))
+            E(Op("s_load_x4", (SW_Q1, SW_M1, 16 * q)))
+            E(Op("s_waitcnt_lgkm", ()))
+            quad[0] = q
+        w, sh = (pos % 16) // 4, 8 * (pos % 4)
+        for qb, base, R, t in ((SW_Q0, SW_BASE0, SW_R0, SW_T0), (SW_Q1, SW_BASE1, SW_R1, SW_T1)):
+            E(Op("s_bfe_k", (t, qb + w, sh, 8)))
+            E(Op("s_mul", (base, t, 10)))
+            E(Op("s_mul_hi", (base + 1, t, 10)))
+            E(Op("s_add_cc", (base, base, R)))
+            E(Op("s_addc", (base + 1, base + 1, R + 1)))
+            E(Op("s_cmp_eq_k", (t, ABSENT)))
+            E(Op("s_cselect64", (base, 22, base)))
+        b = ring0 + 8 * (n % nbuf)
+        for mask, voff, d, sb in ((SW_A0, V_SRCA, b, SW_BASE0), (SW_A1, V_SRCA, b, SW_BASE1),
+                                  (SW_B0, V_SRCB, b + 4, SW_BASE0), (SW_B1, V_SRCB, b + 4, SW_BASE1)):
+            E(Op("s_exec", (mask,)))
+            if not spec.lab_norows:
+                E(Op("load16_saddr", (d, voff, sb, spec.ld_policy)))
+        E(Op("s_exec", (None,)))
+
+    n_seq = len(seq)
+    per_row = 0 if spec.lab_norows else 4
+    for n in range(min(pd, n_seq)):
+        load_row(n)
+    for n, (kind, idx) in enumerate(seq):
+        if n + pd < n_seq:
+            load_row(n + pd)
+        after = min(pd, n_seq - 1 - n)
+        E(Op("s_waitcnt_vm", (per_row * after,)))
+        base = ring0 + 8 * (n % nbuf)
+        if kind == "rep":
+            ops.extend(_transpose_ops(base, spec.bfi_transpose))
+            for b in range(8):
+                E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
+        else:
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose)
+    for j in range(r):
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+    E(Op("s_nop", (4,)))
+    for j in range(r):
+        _store_pair(E, acc0 + 8 * j, S_STA, S_STB, spec.st_policy)
+    E(Op("label", (".Lskip",)))
+    _epilogue_next_item(E, far=spec.far)
+    return ops
+
+
 # --------------------------------------------------------------------------
 # Fused decode, lane-chunk layout (spec.chunked)
 # --------------------------------------------------------------------------
@@ -1020,7 +1210,9 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("v_andk", (V_LANE, 63, V_LANE)))
     E(Op("v_readfirstlane", (29, V_T)))
     E(Op("s_load_args_dec", ()))
-    E(Op("s_load_args_offs", (spec.kernarg_bytes - 16,)))
+    E(Op("s_load_args_offs", (spec.offs_kernarg,)))
+    if spec.mode == "synw":
+        E(Op("s_load_karg_x2", (SW_BOUND, KERNARG_BYTES)))   # kernarg words 24..25
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
     # split tables -> LDS (as _prologue)
@@ -1064,6 +1256,10 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("s_lshl", (S_QB, 13, 4)))           # 16 Q
     E(Op("s_movk", (S_QB + 1, 0)))
     E(Op("s_movk", (S_ABSENT, ABSENT)))
+    if spec.mode == "synw":   # G - 1 = (total - 1) / Lv
+        E(Op("s_addk", (SW_GLAST, 14, -1)))
+        E(Op("s_mul_hi", (SW_GLAST, SW_GLAST, 15)))
+        E(Op("s_lshr_s", (SW_GLAST, SW_GLAST, 16)))
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (S_TMASK + q, mask)))
     E(Op("label", (".Litem",)))
@@ -1401,7 +1597,8 @@ def launch_geometry(L: int, G: int, Lv: Optional[int] = None) -> tuple[int, int,
 def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int, G: int,
              total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
              Lv: Optional[int] = None, zero_tail: bool = False, lu: Optional[tuple[int, int]] = None,
-             tables: int = 0, src_offs: int = 0, dst_offs: int = 0, chunked: bool = False) -> bytes:
+             tables: int = 0, src_offs: int = 0, dst_offs: int = 0, chunked: bool = False,
+             bound: Optional[int] = None) -> bytes:
     """96-byte kernarg block (layout above; 128 bytes in dec mode).  Syndrome mode: src = received
     rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
     also write zeros to bytes [L, 16 Lv) of every repair row.  Dec mode
@@ -1424,6 +1621,8 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
         words += [lu[0] & MASK32, lu[0] >> 32, lu[1], 0, tables & MASK32, tables >> 32, 0, 0]
     # generation offset tables (0: strided generations)
     words += [src_offs & MASK32, src_offs >> 32, dst_offs & MASK32, dst_offs >> 32]
+    if bound is not None:   # synw: per-generation pass bound table (0: none)
+        words += [bound & MASK32, bound >> 32]
     for w in words:
         assert 0 <= w < 1 << 32, words
     return np.array(words, dtype=np.uint32).tobytes()
@@ -1542,19 +1741,20 @@ class Emulator:
 
     def run_wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int):
         v = np.zeros((256, 64), dtype=np.uint64)
-        s = [0] * 96
+        s = [0] * 104
         lds = np.zeros(LDS_TAB_BYTES, np.uint8)
         pend_lgkm = []
         ka = np.frombuffer(kernarg, np.uint32)
         pending = []  # list of (regs, values, lanes) in issue order
         busy = set()
+        busy_lanes = {}   # load16_saddr: register -> lanes with a load outstanding
         exec_ = np.ones(64, bool)
         tid = np.arange(64, dtype=np.uint64) + 64 * wave_in_wg
         v[0] = tid
         s[2] = workgroup
 
         def rv(i):
-            if i in busy:
+            if i in busy or (i in busy_lanes and busy_lanes[i].any()):
                 raise EmuError(f"read of v{i} with a load outstanding")
             return v[i]
 
@@ -1758,7 +1958,59 @@ class Emulator:
                     regs, vals, lanes = pending.pop(0)
                     for q, rg in enumerate(regs):
                         busy.discard(rg)
+                        if rg in busy_lanes:
+                            busy_lanes[rg] &= ~lanes
                         v[rg] = np.where(lanes, vals[q], v[rg])
+            elif n == "load16_saddr":
+                d, voff, sb = a[:3]
+                base = s[sb] | (s[sb + 1] << 32)
+                off = rv(voff)
+                vals = np.zeros((4, 64), np.uint64)
+                for l in np.nonzero(exec_)[0]:
+                    vals[:, l] = np.frombuffer(self.read(base + int(off[l]), 16), np.uint32)
+                regs = [d + q for q in range(4)]
+                for rg in regs:
+                    bl = busy_lanes.setdefault(rg, np.zeros(64, bool))
+                    if rg in busy or (bl & exec_).any():
+                        raise EmuError(f"load into v{rg} lanes with a load outstanding")
+                    bl |= exec_
+                pending.append((regs, vals, exec_.copy()))
+            elif n == "s_load_karg_x2":
+                s[a[0]], s[a[0] + 1] = int(ka[a[1] // 4]), int(ka[a[1] // 4 + 1])
+            elif n in ("s_load_x1", "s_load_x2", "s_load_x4"):
+                d, ar, off = a
+                nd = {"s_load_x1": 1, "s_load_x2": 2, "s_load_x4": 4}[n]
+                addr = (s[ar] | (s[ar + 1] << 32)) + off
+                if addr % 4:
+                    raise EmuError("unaligned scalar load")
+                w = np.frombuffer(self.read(addr, 4 * nd), np.uint32)
+                for q in range(nd):
+                    s[d + q] = int(w[q])
+            elif n == "s_addk":
+                t = s[a[1]] + (a[2] & MASK32)
+                s[a[0]], scc = t & MASK32, int(t > MASK32)
+            elif n == "s_add_cc":
+                t = s[a[1]] + s[a[2]]
+                s[a[0]], scc = t & MASK32, int(t > MASK32)
+            elif n == "s_addc":
+                t = s[a[1]] + s[a[2]] + scc
+                s[a[0]], scc = t & MASK32, int(t > MASK32)
+            elif n == "s_addck":
+                t = s[a[1]] + (a[2] & MASK32) + scc
+                s[a[0]], scc = t & MASK32, int(t > MASK32)
+            elif n == "s_mul_hi":
+                s[a[0]] = (s[a[1]] * s[a[2]]) >> 32
+            elif n == "s_max":
+                s[a[0]] = max(s[a[1]], s[a[2]])
+            elif n == "s_lshr_s":
+                s[a[0]] = s[a[1]] >> (s[a[2]] & 31)
+            elif n == "s_bfe_k":
+                s[a[0]] = (s[a[1]] >> a[2]) & ((1 << a[3]) - 1)
+            elif n == "s_cmp_eq_k":
+                scc = int(s[a[0]] == a[1])
+            elif n == "s_cselect64":
+                src = a[1] if scc else a[2]
+                s[a[0]], s[a[0] + 1] = s[src], s[src + 1]
             elif n == "s_exec":
                 exec_ = np.ones(64, bool) if a[0] is None else smask(a[0])
             elif n == "s_and64":

@@ -131,13 +131,23 @@ def _bs_kernels(build_dir: Path) -> Path:
             rp = (rt - j0) // (npass - p)
             specs.append(bs.KernelSpec(k, rp, BS_PD, "enc", r_total=rt, j0=j0))
             j0 += rp
+    # decode syndromes of the same codes for long rows (slot map read by the
+    # scalar unit, _generate_synw): same balanced passes, items whose
+    # generations accepted no repair of a pass skip it
+    for k, rt in BS_ENC_ONLY:
+        npass = -(-rt // BS_PASS)
+        j0 = 0
+        for p in range(npass):
+            rp = (rt - j0) // (npass - p)
+            specs.append(bs.KernelSpec(k, rp, BS_PD, "synw", r_total=rt, j0=j0))
+            j0 += rp
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
         data = hsaco.read_bytes()
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
-        mode = "c" if spec.chunked else {"enc": "e", "syn": "s", "dec": "d"}[spec.mode]
+        mode = "c" if spec.chunked else {"enc": "e", "syn": "s", "dec": "d", "synw": "w"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {BS_PD}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
     inc = build_dir / "qf_bs_blobs.inc"

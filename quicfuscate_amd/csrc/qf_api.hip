@@ -501,14 +501,20 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     const uint64_t cgs = (uint64_t)(r + 1) * 16;
     const uint64_t Lp = 16ull * qf::bs_padded_units(L);  // zero-tail encode rows
     const uint32_t Lu = (L + 15) / 16;
+    // long rows (padded units >= 128): the syndrome passes read the received
+    // rows through the slot map themselves (qf_cauchy_synw_*), no gather
+    const char* nosw = getenv("QF_DECODE_NO_SYNW");
+    const bool synw = qf::synw_available(k, r) && Lp >= 16 * 128 && !(nosw && atoi(nosw));
     // generations per chunk: gathered sources + syndromes of about 1 GiB
-    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(G, (1ull << 30) / ((uint64_t)(k + r) * Lp)));
+    const uint64_t chunk = std::max<uint64_t>(
+        1, std::min<uint64_t>(G, (1ull << 30) / ((uint64_t)((synw ? 0 : k) + r) * Lp)));
     const size_t off_bound = round_up((size_t)passes * G * cgs, 256);
     const size_t off_map = round_up(off_bound + (size_t)G * 4, 256);
     const size_t off_x = round_up(off_map + (size_t)G * ms, 256);
-    const size_t off_syn = round_up(off_x + (size_t)chunk * k * Lp, 256);
+    const size_t off_syn = round_up(off_x + (synw ? 0 : (size_t)chunk * k * Lp), 256);
     int s = grow_work(ctx, off_syn + (size_t)chunk * r * Lp);
     if (s) return s;
+    if (synw && (s = ensure_zero(ctx, (uint32_t)Lp)) != QF_OK) return s;
     uint8_t* w = ctx->d_work;
     uint32_t* d_bound = reinterpret_cast<uint32_t*>(w + off_bound);
     hipStream_t st = ctx->stream;
@@ -535,6 +541,15 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     const int PD = pick_PD("QF_DECODE_PD", 1, 1);
     for (uint64_t g0 = 0; g0 < G; g0 += chunk) {
         const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
+        if (synw) {
+            ev = prof_begin(ctx, st);
+            QF_CHECK_HIP(qf::synw_launch(ctx->bs, ctx->num_cus, st, k, r,
+                                         ctx->offs_in ? rows : rows + g0 * sh->rows_gen_stride, w + off_syn,
+                                         ctx->offs_in ? 0 : sh->rows_gen_stride, (uint64_t)r * Lp, sh->row_stride, Lp, L,
+                                         Gc, w + off_map + g0 * ms, ms, ctx->d_zero, d_bound + g0,
+                                         ctx->offs_in ? ctx->offs_in + g0 : nullptr));
+            prof_end(ctx, st, ev, std::string("qf_cauchy_synw_k") + std::to_string(k) + "_r" + std::to_string(r));
+        }
         qf::GatherArgs ga{};
         ga.rows = rows + g0 * sh->rows_gen_stride;
         ga.rows_gen_stride = sh->rows_gen_stride;
@@ -549,18 +564,20 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         ga.r = r;
         ga.Lu = Lu;
         ga.G = Gc;
-        ev = prof_begin(ctx, st);
-        QF_CHECK_HIP(qf::launch_gather_sources(ga, ctx->num_cus, st));
-        prof_end(ctx, st, ev, "k_gather_sources");
-        ev = prof_begin(ctx, st);
-        QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, w + off_x, w + off_syn, (uint64_t)k * Lp,
-                                   (uint64_t)r * Lp, Lp, Lp, L, Gc, true));
-        prof_end(ctx, st, ev, qf::bs_name(k, r));
-        ga.out = w + off_syn;
-        ga.out_gen_stride = (uint64_t)r * Lp;
-        ev = prof_begin(ctx, st);
-        QF_CHECK_HIP(qf::launch_xor_repairs(ga, ctx->num_cus, st));
-        prof_end(ctx, st, ev, "k_xor_repairs");
+        if (!synw) {
+            ev = prof_begin(ctx, st);
+            QF_CHECK_HIP(qf::launch_gather_sources(ga, ctx->num_cus, st));
+            prof_end(ctx, st, ev, "k_gather_sources");
+            ev = prof_begin(ctx, st);
+            QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, w + off_x, w + off_syn, (uint64_t)k * Lp,
+                                       (uint64_t)r * Lp, Lp, Lp, L, Gc, true));
+            prof_end(ctx, st, ev, qf::bs_name(k, r));
+            ga.out = w + off_syn;
+            ga.out_gen_stride = (uint64_t)r * Lp;
+            ev = prof_begin(ctx, st);
+            QF_CHECK_HIP(qf::launch_xor_repairs(ga, ctx->num_cus, st));
+            prof_end(ctx, st, ev, "k_xor_repairs");
+        }
         for (uint32_t p = 0; p < passes; ++p) {
             qf::CombineSlotsArgs a{};
             a.rows = w + off_syn;

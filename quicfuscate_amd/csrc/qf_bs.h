@@ -35,6 +35,14 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
 // srs >= 16 * bs_padded_units(L): syndromes are computed over the padded lane
 // space (the tail bytes are junk).
 bool syn_available(uint32_t k, uint32_t r);
+// Syndromes for long rows (padded units >= 128) with the slot map read by
+// the scalar unit, every repair pass of (k, r); items whose generations'
+// bound (1 + largest accepted repair) <= a pass's first repair skip it.
+bool synw_available(uint32_t k, uint32_t r);
+hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
+                       uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
+                       const uint8_t* zero, const uint32_t* bound, const uint64_t* rows_offs);
 const char* syn_name(uint32_t k, uint32_t r);
 uint32_t syn_map_stride(uint32_t k, uint32_t r);
 hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,

@@ -16,7 +16,7 @@
 struct QfBsEntry {
     uint32_t k, r, pd;
     uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
-    char mode;  // 'e' encode, 's' decode syndromes, 'd' fused decode
+    char mode;  // 'e' encode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -34,6 +34,7 @@ static const QfBsEntry* find(char mode, uint32_t k, uint32_t r) {
 }
 
 bool bs_available(uint32_t k, uint32_t r) { return find('e', k, r) != nullptr; }
+bool synw_available(uint32_t k, uint32_t r) { return find('w', k, r) != nullptr; }
 bool syn_available(uint32_t k, uint32_t r) { return find('s', k, r) != nullptr; }
 
 const char* bs_name(uint32_t k, uint32_t r) {
@@ -69,7 +70,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
                          uint64_t drs, uint32_t L, uint32_t G, uint32_t Lv, uint32_t s19,
                          const uint8_t* smap, const uint8_t* zero, const uint8_t* lu = nullptr,
                          uint32_t lu_stride = 0, const uint32_t* tab256 = nullptr,
-                         const uint64_t* src_offs = nullptr, const uint64_t* dst_offs = nullptr) {
+                         const uint64_t* src_offs = nullptr, const uint64_t* dst_offs = nullptr,
+                         const uint32_t* bound = nullptr) {
     (void)num_cus;
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
@@ -142,6 +144,11 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
     a[ot + 3] = (uint32_t)((uintptr_t)dst_offs >> 32);
     size_t sz = (size_t)(ot + 4) * 4;
+    if (e->mode == 'w') {   // per-generation pass bound (bs_codegen KERNARG_BYTES_SYNW)
+        a[24] = (uint32_t)(uintptr_t)bound;
+        a[25] = (uint32_t)((uintptr_t)bound >> 32);
+        sz = 26 * 4;
+    }
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
     return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
@@ -193,6 +200,24 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
     if (srs < 16ull * Lv) return hipErrorInvalidValue;
     return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, Lv, map_stride, smap, zero, nullptr, 0,
                   nullptr, rows_offs, nullptr);
+}
+
+hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
+                       const uint8_t* rows, uint8_t* syn, uint64_t rgs, uint64_t sgs, uint64_t rs,
+                       uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
+                       const uint8_t* zero, const uint32_t* bound, const uint64_t* rows_offs) {
+    const QfBsEntry* first = find('w', k, r);
+    if (!first || map_stride != first->map_stride || !zero) return hipErrorInvalidValue;
+    // an item (128 units) must lie in at most two generations
+    const uint32_t Lv = bs_padded_units(L);
+    if (Lv < 128 || srs < 16ull * Lv) return hipErrorInvalidValue;
+    for (const auto& e : qf_bs_table) {
+        if (e.mode != 'w' || e.k != k || e.rt != r) continue;
+        hipError_t err = launch(cache, &e, num_cus, st, rows, syn + (uint64_t)e.j0 * srs, rgs, sgs, rs, srs, L, G, Lv,
+                                map_stride, smap, zero, nullptr, 0, nullptr, rows_offs, nullptr, bound);
+        if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
 }
 
 // the chunked fused decode unless QF_DECODE_LEGACY=1 (or the row is too short

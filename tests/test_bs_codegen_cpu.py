@@ -220,7 +220,7 @@ def test_cauchy_inverse_closed_form():
 
 
 @pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "syn"), (16, 1, "syn"), (32, 16, "enc"),
-                                      (64, 16, "dec"), (16, 1, "dec")])
+                                      (64, 16, "dec"), (16, 1, "dec"), (128, 20, "synw")])
 def test_declared_register_budget_covers_code(k, r, mode):
     """Every VGPR / SGPR the generated code names lies below the
     .amdhsa_next_free_* counts of its kernel descriptor."""
@@ -510,7 +510,8 @@ def test_emulated_fused_decode_chunked(oracle, k, r, pd, L, G, seed, erase, offs
 
 @pytest.mark.parametrize("k,r,mode,chunked", [(64, 16, "enc", False), (64, 16, "syn", False),
                                                (64, 16, "dec", False), (64, 16, "dec", True),
-                                               (16, 1, "dec", True), (96, 15, "dec", True)])
+                                               (16, 1, "dec", True), (96, 15, "dec", True),
+                                               (128, 20, "synw", False)])
 def test_register_tuples_even_aligned(k, r, mode, chunked):
     """gfx950 requires every multi-register VGPR operand (v[a:b]) to start at
     an even register; the assembler rejects odd tuples.  Checked on the IR's
@@ -524,3 +525,102 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
     if chunked:
         nv = spec.next_free_vgpr
         assert nv <= 256
+
+
+def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True):
+    """The wave-uniform syndrome kernel (mode "synw") on the emulator for
+    every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
+    generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
+    generations' bound <= j0 are skipped."""
+    rng = np.random.default_rng(seed)
+    rs = L + 48
+    n_slots = k + rt
+    rgs = n_slots * rs + 32
+    Lv = bs.padded_units(L)
+    srs = 16 * Lv + 16
+    sgs = rt * srs
+    specs = [bs.KernelSpec(k, min(rp, rt - j0), 2, mode="synw", r_total=rt, j0=j0) for j0 in range(0, rt, rp)]
+    ms = specs[0].map_stride
+    rows = rng.integers(0, 256, G * rgs + 4096, dtype=np.uint8)
+    smap = np.full(G * ms, 0xFF, np.uint8)
+    syn = np.full(G * sgs, 0xEE, np.uint8)
+    bound = np.zeros(G, np.uint32)
+    gen_off = rng.permutation(G) * rgs if offs else np.arange(G) * rgs   # rows of g at gen_off[g]
+    plans = []
+    for g in range(G):
+        src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        rep = oracle.encode(src, rt)
+        e = int(rng.integers(0, min(k, rt) + 1)) if g % 3 else 0      # every third: nothing lost
+        E = sorted(rng.choice(k, e, replace=False).tolist())
+        J = sorted(rng.choice(rt, e, replace=False).tolist())
+        present = [("s", i) for i in range(k) if i not in E] + [("p", j) for j in J]
+        slots = rng.choice(n_slots, len(present), replace=False)
+        for n, (kind, idx) in enumerate(present):
+            sl = int(slots[n])
+            data = src[idx] if kind == "s" else rep[idx]
+            o = int(gen_off[g]) + sl * rs
+            rows[o: o + L] = data
+            smap[g * ms + (idx if kind == "s" else k + idx)] = sl
+        bound[g] = (max(J) + 1) if J else 0
+        plans.append((src, rep, E, J))
+    emu_bufs = {}
+    ROWS, SYN, MAP, ZERO, OFFS, BOUND = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
+    for spec in specs:
+        emu = bs.Emulator(bs.generate(spec))
+        emu.add_buffer(ROWS, rows)
+        emu.add_buffer(SYN, syn)
+        emu.add_buffer(MAP, smap)
+        emu.add_buffer(ZERO, np.zeros(16 * Lv, np.uint8))
+        emu.add_buffer(OFFS, np.asarray(gen_off, np.uint64).view(np.uint8).copy())
+        emu.add_buffer(BOUND, bound.view(np.uint8).copy())
+        ka = bs.kernargs(ROWS, SYN + spec.j0 * srs, 0 if offs else rgs, sgs, rs, srs, L, G, 8, smap=MAP,
+                         map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
+                         bound=BOUND if use_bound else 0)
+        n_items = bs.launch_geometry(L, G, Lv)[2]
+        for wv in range(n_items):
+            emu.run_wave(ka, wv // 4, wv % 4)
+        emu_bufs[spec.j0] = emu
+    C = np.array(bs.cauchy(k, rt), np.uint8)
+    mul = np.array([[bs.gf_mul(c, x) for x in range(256)] for c in range(256)], np.uint8)
+    checked = 0
+    for g, (src, rep, E, J) in enumerate(plans):
+        for j in J:
+            want = rep[j].copy()
+            for i in range(k):
+                if i not in E:
+                    want ^= mul[C[j, i]][src[i]]
+            blk = syn[g * sgs + j * srs: g * sgs + j * srs + L]
+            assert (blk == want).all(), (g, j)
+            checked += 1
+    # skipped items: a generation (and its item neighbours) with bound <= j0 of
+    # every pass it could have been processed in left its rows untouched
+    if use_bound:
+        for g in range(G):
+            nb = [bound[x] for x in (g - 1, g, g + 1) if 0 <= x < G]
+            for spec in specs:
+                if max(nb) <= spec.j0:
+                    blk = syn[g * sgs + spec.j0 * srs: g * sgs + (spec.j0 + spec.r) * srs]
+                    assert (blk == 0xEE).all(), (g, spec.j0)
+    return checked
+
+
+@pytest.mark.parametrize("k,rt,rp,L,G,offs", [
+    (8, 6, 3, 2048, 5, False),     # two passes, exact units
+    (8, 6, 6, 2100, 4, False),     # one pass, partial last unit, padded lanes (Lv = 136: items straddle)
+    (12, 7, 4, 2064, 4, True),     # generation offset table, uneven passes
+    (5, 3, 2, 2200, 3, False),
+])
+def test_emulated_synw_kernel(oracle, k, rt, rp, L, G, offs):
+    assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L, offs=offs) > 0
+
+
+def test_emulated_synw_without_bound(oracle):
+    assert _synw_case(oracle, 8, 5, 5, 2048, 3, seed=3, use_bound=False) > 0
+
+
+def test_synw_register_budget():
+    """The C5 shapes' synw passes fit 256 VGPRs (pd 3) and the SGPR budget."""
+    for k, rt, rp in ((128, 20, 20), (160, 48, 16), (196, 59, 20), (128, 39, 20)):
+        for j0 in range(0, rt, rp):
+            spec = bs.KernelSpec(k, min(rp, rt - j0), 3, mode="synw", r_total=rt, j0=j0)
+            assert spec.next_free_vgpr <= 256 and spec.next_free_sgpr <= 102
