@@ -392,6 +392,25 @@ int qf_adaptive_on_receive(qf_adaptive *a, uint64_t id, int is_systematic, const
                            uint32_t len, const uint8_t *coeffs, uint32_t coeff_len,
                            uint8_t *out_data, uint32_t out_stride, qf_packet_desc *out_desc,
                            uint32_t out_cap, uint32_t *n_out);
+/* on_receive for M connections at once: conns[m] receives packet m (ids,
+ * is_systematic, data/lens, coeffs/coeff_lens: coeffs and coeff_lens may be
+ * NULL when no packet carries coefficients).  The result is that of calling
+ * qf_adaptive_on_receive for m = 0..M-1 in order -- connection m's recovered
+ * packets occupy out_data rows [first_m, first_m + n_out[m]), first_m =
+ * n_out[0] + ... + n_out[m-1], statuses[m] (nullable) gets that call's status
+ * (e.g. QF_EINVAL for a repair without coefficients; such a packet is
+ * dropped and the batch goes on) -- but the GF(2^8) decoders of one context
+ * take their rows in one upload, and the generations that complete in the
+ * call decode in one heterogeneous decode with one download.  out_cap must
+ * cover the sum over connections of their decoders' k (the most one
+ * on_receive can recover).  An argument error fails the whole call before any
+ * state changes. */
+int qf_adaptive_on_receive_batch(qf_adaptive *const *conns, uint32_t M, const uint64_t *ids,
+                                 const int32_t *is_systematic, const uint8_t *const *data,
+                                 const uint32_t *lens, const uint8_t *const *coeffs,
+                                 const uint32_t *coeff_lens, uint8_t *out_data, uint32_t out_stride,
+                                 qf_packet_desc *out_desc, uint32_t out_cap, uint32_t *n_out,
+                                 int32_t *statuses);
 /* AdaptiveFec::report_loss (adaptive.rs:602-630).  QF_EINVAL if lost > total
  * (the reference underflows). */
 int qf_adaptive_report_loss(qf_adaptive *a, uint32_t lost, uint32_t total);

@@ -164,6 +164,7 @@ _SIGS = {
     "qf_adaptive_max_send_packets": (_U32, [_P]),
     "qf_adaptive_on_send": (_I, [_P, _U64, _P, _U32, _P, _U32, _P, _U32, _P, _U32, _P]),
     "qf_adaptive_on_send_batch": (_I, [_P, _U32, _P, _P, _P, _P, _U32, _P, _U32, _P, _U32, _P, _P]),
+    "qf_adaptive_on_receive_batch": (_I, [_P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32, _P, _P]),
     "qf_adaptive_on_receive": (_I, [_P, _U64, _I, _P, _U32, _P, _U32, _P, _U32, _P, _U32, _P]),
     "qf_adaptive_report_loss": (_I, [_P, _U32, _U32]),
     "qf_adaptive_report_loss_at": (_I, [_P, _U32, _U32, _D]),

@@ -628,6 +628,104 @@ int qf_adaptive_on_receive(qf_adaptive* a, uint64_t id, int is_systematic, const
     return QF_OK;
 }
 
+int qf_adaptive_on_receive_batch(qf_adaptive* const* conns, uint32_t M, const uint64_t* ids,
+                                 const int32_t* is_systematic, const uint8_t* const* data, const uint32_t* lens,
+                                 const uint8_t* const* coeffs, const uint32_t* coeff_lens, uint8_t* out_data,
+                                 uint32_t out_stride, qf_packet_desc* out_desc, uint32_t out_cap, uint32_t* n_out,
+                                 int32_t* statuses) {
+    if (M == 0) return QF_OK;
+    if (!conns || !ids || !is_systematic || !data || !lens || !n_out) return QF_EINVAL;
+    // every argument check before any state changes (as the send batch): a
+    // connection's need (the k of its decoders) does not change on receive
+    uint64_t total = 0;
+    for (uint32_t m = 0; m < M; ++m) {
+        const qf_adaptive* a = conns[m];
+        if (!a || (lens[m] && !data[m])) return QF_EINVAL;
+        const uint32_t need = a->cur.k + (a->has_fade ? a->fade.k : 0);
+        if (need && (!out_data || !out_desc || out_stride < a->cfg.max_len)) return QF_ETOOSMALL;
+        total += need;
+        n_out[m] = 0;
+        if (statuses) statuses[m] = QF_OK;
+    }
+    if (total > out_cap) return QF_ETOOSMALL;
+    uint32_t pos = 0;
+    std::vector<qf::DecAdd> batch;
+    std::vector<uint32_t> batch_m;
+    std::vector<uint8_t> was;
+    std::unordered_set<const qf_adaptive*> seen;
+    seen.reserve(M);
+    for (uint32_t m0 = 0; m0 < M;) {
+        // a segment: each connection at most once (a repeat starts the next)
+        batch.clear();
+        batch_m.clear();
+        was.clear();
+        seen.clear();
+        qf_ctx* ctx = nullptr;
+        uint32_t m = m0;
+        for (; m < M; ++m) {
+            qf_adaptive* a = conns[m];
+            if (!seen.insert(a).second) break;
+            const bool to_fade = a->has_fade && a->transition_left > kFade / 2;
+            if (a->ctx && a->cur.dec && !to_fade && a->cur.k > 0 && (!ctx || a->ctx == ctx)) {
+                ctx = a->ctx;
+                qf::DecAdd x{};
+                x.d = a->cur.dec;
+                x.id = ids[m];
+                x.is_systematic = is_systematic[m];
+                x.data = data[m];
+                x.len = lens[m];
+                x.coeffs = coeffs ? coeffs[m] : nullptr;
+                x.coeff_len = coeff_lens ? coeff_lens[m] : 0;
+                batch.push_back(x);
+                batch_m.push_back(m);
+                was.push_back(a->cur.decoded ? 1 : 0);
+            }
+        }
+        if (batch.size() == 1) {   // one connection: the per-packet path (no staging, no scatter launch)
+            batch.clear();
+            batch_m.clear();
+            was.clear();
+        }
+        if (!batch.empty()) {
+            int s = qf::decoders_add_batch(ctx, batch.data(), (uint32_t)batch.size());
+            if (s != QF_OK) return s;
+        }
+        // outputs in connection order: batched connections drain their decoders,
+        // the others run the per-packet on_receive here
+        for (uint32_t i = m0, b = 0; i < m; ++i) {
+            qf_adaptive* a = conns[i];
+            uint32_t n = 0;
+            int s;
+            if (b < batch_m.size() && batch_m[b] == i) {
+                const qf::DecAdd& x = batch[b];
+                Codec& c = a->cur;
+                s = x.result < 0 ? x.result : QF_OK;
+                if (s == QF_OK) {
+                    c.decoded = x.result == 1;
+                    if (!was[b] && c.decoded)
+                        s = drain_decoded(c, out_data + (size_t)pos * out_stride, out_stride, out_desc + pos,
+                                          out_cap - pos, &n);
+                    // drain_decoded writes from row 0 of the slice it is given
+                    // (its *n starts at 0)
+                }
+                ++b;
+            } else {
+                s = qf_adaptive_on_receive(a, ids[i], is_systematic[i], data[i], lens[i], coeffs ? coeffs[i] : nullptr,
+                                           coeff_lens ? coeff_lens[i] : 0, out_data ? out_data + (size_t)pos * out_stride : nullptr,
+                                           out_stride, out_desc ? out_desc + pos : nullptr, out_cap - pos, &n);
+            }
+            if (s < 0) {
+                if (statuses) statuses[i] = s;
+                n = 0;
+            }
+            n_out[i] = n;
+            pos += n;
+        }
+        m0 = m;
+    }
+    return QF_OK;
+}
+
 int qf_adaptive_report_loss_at(qf_adaptive* a, uint32_t lost, uint32_t total, double now_s) {
     if (!a || lost > total) return QF_EINVAL;
     a->est.report(lost, total);

@@ -75,6 +75,11 @@ struct qf_ctx {
     hipEvent_t desc_done = nullptr;
     // send batches: one event per download chunk
     std::vector<hipEvent_t> send_ev;
+    // receive batches: pinned / device staging (rows, row indices, decode outputs)
+    uint8_t* h_recv = nullptr;
+    uint8_t* d_recv = nullptr;
+    size_t recv_bytes = 0;
+    hipEvent_t recv_done = nullptr;
     // decode workspace
     uint8_t* d_work = nullptr;
     size_t work_bytes = 0;
@@ -812,6 +817,29 @@ int ctx_desc_buffers(qf_ctx* ctx, size_t bytes, uint8_t** h, uint8_t** d) {
     return QF_OK;
 }
 int ctx_desc_upload(qf_ctx* ctx, size_t bytes) { return desc_upload(ctx, bytes); }
+int ctx_recv_buffers(qf_ctx* ctx, size_t bytes, uint8_t** h, uint8_t** d) {
+    if (!ctx->recv_done) QF_CHECK_HIP(hipEventCreateWithFlags(&ctx->recv_done, hipEventDisableTiming));
+    else QF_CHECK_HIP(hipEventSynchronize(ctx->recv_done));
+    if (bytes > ctx->recv_bytes) {
+        QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        if (ctx->h_recv) hipHostFree(ctx->h_recv);
+        if (ctx->d_recv) hipFree(ctx->d_recv);
+        ctx->h_recv = nullptr;
+        ctx->d_recv = nullptr;
+        ctx->recv_bytes = 0;
+        const size_t b = round_up(bytes, 1 << 20);
+        if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_recv), b) != hipSuccess) return QF_ENOMEM;
+        if (hipMalloc(&ctx->d_recv, b) != hipSuccess) return QF_ENOMEM;
+        ctx->recv_bytes = b;
+    }
+    *h = ctx->h_recv;
+    *d = ctx->d_recv;
+    return QF_OK;
+}
+int ctx_recv_release(qf_ctx* ctx) {
+    QF_CHECK_HIP(hipEventRecord(ctx->recv_done, ctx->stream));
+    return QF_OK;
+}
 int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out) {
     while (ctx->send_ev.size() < n) {
         hipEvent_t e = nullptr;
@@ -962,6 +990,12 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->h_desc) hipHostFree(c->h_desc);
     if (c->desc_done) hipEventDestroy(c->desc_done);
     for (hipEvent_t e : c->send_ev) hipEventDestroy(e);
+    if (c->recv_done) {
+        hipEventSynchronize(c->recv_done);
+        hipEventDestroy(c->recv_done);
+    }
+    if (c->h_recv) hipHostFree(c->h_recv);
+    if (c->d_recv) hipFree(c->d_recv);
     if (c->d_zero) hipFree(c->d_zero);
     if (c->d_gf16_log) hipFree(c->d_gf16_log);
     if (c->d_gf16_exp) hipFree(c->d_gf16_exp);

@@ -52,6 +52,11 @@ bool small_encode_enabled();
 int ctx_desc_buffers(qf_ctx* ctx, size_t bytes, uint8_t** h, uint8_t** d);
 // The first `bytes` of the host buffer to the device buffer, on the context stream.
 int ctx_desc_upload(qf_ctx* ctx, size_t bytes);
+// Receive batches: pinned + device buffers of >= bytes each, once the
+// previous user's host reads/writes are done (ctx_recv_release records that
+// point on the context stream).  The caller does not hold the context lock.
+int ctx_recv_buffers(qf_ctx* ctx, size_t bytes, uint8_t** h, uint8_t** d);
+int ctx_recv_release(qf_ctx* ctx);
 // At least n events of the context (download chunks of a send batch).
 int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out);
 // Small-batch encode of G ring windows of one (k, r) class, repairs = Cauchy
@@ -79,5 +84,22 @@ struct EncSend {
 // scatter, one small-batch encode per (k, r) class, one download.  The
 // caller does not hold the context lock.
 int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M);
+
+// One packet for each of M distinct GF(2^8) decoders of ctx
+// (qf_decoder_add_packet semantics, result per packet: 1 decoded, 0 not, < 0
+// error): the accepted rows go up in one copy and one scatter; decoders that
+// reach k rows decode together (one qf_decode_batch_desc over the Cauchy
+// ones), with one download of all their outputs.
+struct DecAdd {
+    qf_decoder* d;
+    uint64_t id;
+    int is_systematic;
+    const uint8_t* data;
+    uint32_t len;
+    const uint8_t* coeffs;
+    uint32_t coeff_len;
+    int result;
+};
+int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M);
 
 }  // namespace qf

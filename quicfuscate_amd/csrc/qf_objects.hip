@@ -284,20 +284,25 @@ int qf_decoder_free(qf_decoder* d) {
 
 int qf_decoder_is_decoded(const qf_decoder* d) { return d ? (d->decoded ? 1 : 0) : QF_EINVAL; }
 
-// decoder.rs:704-783 for the k accepted rows, on the device.
-static int decoder_try_decode(qf_decoder* d) {
+// How the k accepted rows decode (decoder.rs:704-783): repair rows that are
+// Cauchy rows of this k (c_i = gf_inv(i ^ y), y = k + j: what Encoder emits
+// for a window aligned with the generation) decode by their repair index on
+// the Cauchy paths (generated kernels); any other row keeps the whole system
+// explicit.
+struct DecPlan {
+    uint32_t L = 1, rc = 1;
+    bool cauchy = true;
+    std::vector<uint16_t> idx;
+};
+
+static void decoder_plan(const qf_decoder* d, DecPlan* p) {
     const uint32_t k = d->k;
     uint32_t L = 0;
     for (uint32_t q = 0; q < k; ++q) L = d->lens[q] > L ? d->lens[q] : L;
-    if (L == 0) L = 1;
-    hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
+    p->L = L == 0 ? 1 : L;
     const uint32_t emax = k < 128 ? k : 128;
-    // Repair rows that are Cauchy rows of this k (c_i = gf_inv(i ^ y), y =
-    // k + j: what Encoder emits for a window aligned with the generation)
-    // decode by their repair index on the Cauchy paths (generated kernels);
-    // any other row keeps the whole system explicit.
     const auto& f = qf::gf();
-    std::vector<uint16_t> idx(d->index);
+    p->idx = d->index;
     uint32_t rmax = 0;
     bool cauchy = true;
     for (uint32_t q = 0; q < k && cauchy; ++q) {
@@ -312,20 +317,13 @@ static int decoder_try_decode(qf_decoder* d) {
             uint8_t v = 0;
             cauchy = f.inv((uint8_t)(i ^ y), &v) && v == c[i];
         }
-        idx[q] = y;
+        p->idx[q] = y;
         rmax = std::max<uint32_t>(rmax, (uint32_t)y - k + 1);
     }
-    cauchy = cauchy && rmax <= emax;
-    if (!cauchy) {
-        idx = d->index;
-        QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
-    }
-    // the rows are on the device already (uploaded as they arrived)
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_index, idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
-    qf_decode_shape sh{};
-    sh.k = k;
+    p->cauchy = cauchy && rmax <= emax;
+    if (!p->cauchy) p->idx = d->index;
     uint32_t rc = std::max<uint32_t>(rmax, 1);
-    if (cauchy) {
+    if (p->cauchy) {
         // the Cauchy code of (k, r') holds rows 0..r'-1: take the smallest r'
         // >= rmax with generated kernels, so the decode runs on them
         for (uint32_t r2 = rc; r2 <= emax && k + r2 <= 256; ++r2)
@@ -334,29 +332,14 @@ static int decoder_try_decode(qf_decoder* d) {
                 break;
             }
     }
-    sh.r = cauchy ? rc : emax;
-    sh.L = L;
-    sh.max_rows = k;
-    sh.row_stride = d->stride;
-    sh.rows_gen_stride = (uint64_t)k * d->stride;
-    sh.rec_row_stride = d->stride;
-    sh.rec_gen_stride = (uint64_t)emax * d->stride;
-    int s = qf_decode_batch(d->ctx, &sh, 1, d->d_rows, d->d_index, nullptr, cauchy ? nullptr : d->d_coeffs,
-                            d->d_rec, d->d_rec_index, d->d_nrec, d->d_status);
-    if (s != QF_OK) return s;
-    int32_t status = 0;
-    uint32_t nrec = 0;
-    QF_CHECK_HIP(hipMemcpyAsync(&status, d->d_status, 4, hipMemcpyDeviceToHost, st));
-    QF_CHECK_HIP(hipMemcpyAsync(&nrec, d->d_nrec, 4, hipMemcpyDeviceToHost, st));
-    QF_CHECK_HIP(hipStreamSynchronize(st));
-    if (status != QF_OK) return status;  // singular: stays undecoded (decoder.rs:756-758)
-    std::vector<uint16_t> ridx(nrec);
-    const uint8_t* rec = d->h_rec;
-    if (nrec) {
-        QF_CHECK_HIP(hipMemcpyAsync(ridx.data(), d->d_rec_index, (size_t)nrec * 2, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipMemcpyAsync(d->h_rec, d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipStreamSynchronize(st));
-    }
+    p->rc = p->cauchy ? rc : emax;
+}
+
+// decoder.rs:763-780: the generation in source order -- received systematic
+// rows as they came, recovered rows (ridx[m] <- rec row m) at L bytes.
+static void decoder_assemble(qf_decoder* d, uint32_t L, uint32_t nrec, const uint16_t* ridx, const uint8_t* rec,
+                             uint64_t rec_stride) {
+    const uint32_t k = d->k;
     d->out.assign((size_t)k * d->stride, 0);
     d->out_len.assign(k, 0);
     for (uint32_t i = 0; i < k; ++i) {
@@ -368,15 +351,58 @@ static int decoder_try_decode(qf_decoder* d) {
     }
     for (uint32_t m = 0; m < nrec; ++m) {
         const uint32_t i = ridx[m];
-        memcpy(&d->out[(size_t)i * d->stride], rec + (size_t)m * d->stride, L);
+        memcpy(&d->out[(size_t)i * d->stride], rec + (size_t)m * rec_stride, L);
         d->out_len[i] = L;
     }
     d->decoded = true;
+}
+
+// decoder.rs:704-783 for the k accepted rows, on the device.
+static int decoder_try_decode(qf_decoder* d) {
+    const uint32_t k = d->k;
+    hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
+    const uint32_t emax = k < 128 ? k : 128;
+    DecPlan plan;
+    decoder_plan(d, &plan);
+    const uint32_t L = plan.L;
+    if (!plan.cauchy)
+        QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
+    // the rows are on the device already (uploaded as they arrived)
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_index, plan.idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
+    qf_decode_shape sh{};
+    sh.k = k;
+    sh.r = plan.rc;
+    sh.L = L;
+    sh.max_rows = k;
+    sh.row_stride = d->stride;
+    sh.rows_gen_stride = (uint64_t)k * d->stride;
+    sh.rec_row_stride = d->stride;
+    sh.rec_gen_stride = (uint64_t)emax * d->stride;
+    int s = qf_decode_batch(d->ctx, &sh, 1, d->d_rows, d->d_index, nullptr, plan.cauchy ? nullptr : d->d_coeffs,
+                            d->d_rec, d->d_rec_index, d->d_nrec, d->d_status);
+    if (s != QF_OK) return s;
+    int32_t status = 0;
+    uint32_t nrec = 0;
+    QF_CHECK_HIP(hipMemcpyAsync(&status, d->d_status, 4, hipMemcpyDeviceToHost, st));
+    QF_CHECK_HIP(hipMemcpyAsync(&nrec, d->d_nrec, 4, hipMemcpyDeviceToHost, st));
+    QF_CHECK_HIP(hipStreamSynchronize(st));
+    if (status != QF_OK) return status;  // singular: stays undecoded (decoder.rs:756-758)
+    std::vector<uint16_t> ridx(nrec);
+    if (nrec) {
+        QF_CHECK_HIP(hipMemcpyAsync(ridx.data(), d->d_rec_index, (size_t)nrec * 2, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipMemcpyAsync(d->h_rec, d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipStreamSynchronize(st));
+    }
+    decoder_assemble(d, L, nrec, ridx.data(), d->h_rec, d->stride);
     return QF_OK;
 }
 
-int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const uint8_t* data,
-                          uint32_t len, const uint8_t* coeffs, uint32_t coeff_len) {
+// decoder.rs:679-699 on the host: *slot = the accepted row's slot (its bytes
+// are in d->rows), or -1 when the packet is not taken.  Returns what
+// add_packet returns when nothing more happens (1 decoded / 0), or an error.
+static int decoder_accept(qf_decoder* d, uint64_t id, int is_systematic, const uint8_t* data, uint32_t len,
+                          const uint8_t* coeffs, uint32_t coeff_len, int32_t* slot) {
+    *slot = -1;
     if (!d || (len && !data)) return QF_EINVAL;
     if (len > d->max_len) return QF_EINVAL;
     // decoder.rs:679-681
@@ -398,16 +424,25 @@ int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const u
     }
     memset(&d->rows[(size_t)q * d->stride], 0, d->stride);
     if (len) memcpy(&d->rows[(size_t)q * d->stride], data, len);
+    d->lens[q] = len;
+    d->accepted++;
+    *slot = (int32_t)q;
+    return 0;
+}
+
+int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const uint8_t* data,
+                          uint32_t len, const uint8_t* coeffs, uint32_t coeff_len) {
+    int32_t q = -1;
+    const int s = decoder_accept(d, id, is_systematic, data, len, coeffs, coeff_len, &q);
+    if (s != 0 || q < 0) return s;
     // to the device now; rows is pinned and slot q is not rewritten while
     // this decoder lives, so the copy needs no wait
     QF_CHECK_HIP(hipMemcpyAsync(d->d_rows + (size_t)q * d->stride, &d->rows[(size_t)q * d->stride], d->stride,
                                 hipMemcpyHostToDevice, (hipStream_t)qf_ctx_stream(d->ctx)));
-    d->lens[q] = len;
-    d->accepted++;
-    if (d->accepted == k) {
-        int s = decoder_try_decode(d);
-        if (s == QF_ERANK) return 0;
-        if (s != QF_OK) return s;
+    if (d->accepted == d->k) {
+        int e = decoder_try_decode(d);
+        if (e == QF_ERANK) return 0;
+        if (e != QF_OK) return e;
     }
     return d->decoded ? 1 : 0;
 }
@@ -689,6 +724,146 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         g_send_prof.t[1] += tp2 - tp1;
         g_send_prof.t[2] += tp3 - tp2;
         g_send_prof.t[3] += tp4 - tp3;
+    }
+    return QF_OK;
+}
+
+int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
+    if (!ctx || (M && !v)) return QF_EINVAL;
+    if (M == 0) return QF_OK;
+    {
+        std::vector<const qf_decoder*> ds(M);
+        for (uint32_t m = 0; m < M; ++m) {
+            if (!v[m].d || v[m].d->ctx != ctx) return QF_EINVAL;
+            ds[m] = v[m].d;
+        }
+        std::sort(ds.begin(), ds.end());
+        if (std::adjacent_find(ds.begin(), ds.end()) != ds.end()) return QF_EINVAL;   // one packet per decoder
+    }
+    {
+        std::unique_lock<std::mutex> lk;
+        int s = ctx_lock(ctx, lk);   // device current
+        if (s) return s;
+    }
+    // decoder.rs:679-699 on the host, in order
+    struct Up {
+        uint32_t m, slot;
+    };
+    std::vector<Up> up;
+    std::vector<uint32_t> done;          // packets whose decoder now holds k rows
+    size_t pk = 0;
+    for (uint32_t m = 0; m < M; ++m) {
+        DecAdd& x = v[m];
+        int32_t q = -1;
+        x.result = decoder_accept(x.d, x.id, x.is_systematic, x.data, x.len, x.coeffs, x.coeff_len, &q);
+        if (q < 0) continue;
+        up.push_back({m, (uint32_t)q});
+        pk += round16(x.len);
+        if (x.d->accepted == x.d->k) done.push_back(m);
+    }
+    // decode plans: Cauchy generations go into one heterogeneous decode
+    std::vector<DecPlan> plans(done.size());
+    std::vector<uint32_t> cau, expl;
+    size_t ri_n = 0, ri_pad = 0, rec_rows = 0, rec_idx = 0;
+    for (size_t t = 0; t < done.size(); ++t) {
+        decoder_plan(v[done[t]].d, &plans[t]);
+        if (plans[t].cauchy) {
+            cau.push_back((uint32_t)t);
+            const qf_decoder* d = v[done[t]].d;
+            ri_n += d->k;
+            rec_idx += std::min(d->k, plans[t].rc);
+            rec_rows += (size_t)std::min(d->k, plans[t].rc) * d->stride;
+        } else {
+            expl.push_back((uint32_t)t);
+        }
+    }
+    (void)ri_pad;
+    const size_t n_up = up.size(), G = cau.size();
+    const size_t o_slots = 0, o_ri = round16((uint32_t)(sizeof(RingSlot) * n_up));
+    const size_t o_pk = o_ri + ((ri_n * 2 + 255) & ~(size_t)255);
+    const size_t o_out = (o_pk + pk + 255) & ~(size_t)255;            // downloads from here
+    const size_t o_nrec = o_out, o_st = o_nrec + 4 * G, o_ci = (o_st + 4 * G + 255) & ~(size_t)255;
+    const size_t o_rec = (o_ci + 2 * rec_idx + 255) & ~(size_t)255;
+    const size_t total = o_rec + rec_rows;
+    uint8_t *h = nullptr, *dv = nullptr;
+    int s = ctx_recv_buffers(ctx, total, &h, &dv);
+    if (s != QF_OK) return s;
+    hipStream_t st = ctx_stream(ctx);
+    RingSlot* hs = reinterpret_cast<RingSlot*>(h + o_slots);
+    size_t off = 0;
+    for (size_t u = 0; u < n_up; ++u) {
+        const DecAdd& x = v[up[u].m];
+        qf_decoder* d = x.d;
+        const uint32_t n16 = round16(x.len);
+        if (x.len) memcpy(h + o_pk + off, x.data, x.len);
+        if (n16 > x.len) memset(h + o_pk + off + x.len, 0, n16 - x.len);
+        hs[u].src_off = o_pk + off;
+        hs[u].dst = d->d_rows + (size_t)up[u].slot * d->stride;
+        hs[u].dst2 = nullptr;
+        hs[u].len = x.len;
+        hs[u].stride = d->stride;
+        off += n16;
+    }
+    // row indices of the Cauchy decodes, and their descriptors
+    std::vector<qf_dec_desc> descs(G);
+    const uint8_t* rows_base = nullptr;
+    for (size_t c = 0; c < G; ++c) {
+        const qf_decoder* d = v[done[cau[c]]].d;
+        if (!rows_base || d->d_rows < rows_base) rows_base = d->d_rows;
+    }
+    uint16_t* hri = reinterpret_cast<uint16_t*>(h + o_ri);
+    size_t ri_o = 0, ci_o = 0, rr_o = 0;
+    for (size_t c = 0; c < G; ++c) {
+        const DecPlan& pl = plans[cau[c]];
+        const qf_decoder* d = v[done[cau[c]]].d;
+        memcpy(hri + ri_o, pl.idx.data(), (size_t)d->k * 2);
+        qf_dec_desc& q = descs[c];
+        q.k = d->k;
+        q.r = pl.rc;
+        q.L = pl.L;
+        q.n_rows = d->k;
+        q.rows_offset = (uint64_t)(d->d_rows - rows_base);
+        q.row_stride = d->stride;
+        q.row_index_offset = ri_o;
+        q.rec_offset = rr_o;
+        q.rec_row_stride = d->stride;
+        q.rec_index_offset = ci_o;
+        ri_o += d->k;
+        ci_o += std::min(d->k, pl.rc);
+        rr_o += (size_t)std::min(d->k, pl.rc) * d->stride;
+    }
+    if (o_pk + pk) QF_CHECK_HIP(hipMemcpyAsync(dv, h, o_pk + pk, hipMemcpyHostToDevice, st));
+    QF_CHECK_HIP(launch_ring_scatter(dv, reinterpret_cast<const RingSlot*>(dv + o_slots), (uint32_t)n_up, st));
+    if (G) {
+        s = qf_decode_batch_desc(ctx, descs.data(), (uint32_t)G, rows_base, reinterpret_cast<const uint16_t*>(dv + o_ri),
+                                 dv + o_rec, reinterpret_cast<uint16_t*>(dv + o_ci),
+                                 reinterpret_cast<uint32_t*>(dv + o_nrec), reinterpret_cast<int32_t*>(dv + o_st));
+        if (s != QF_OK) {
+            ctx_recv_release(ctx);
+            return s;
+        }
+        QF_CHECK_HIP(hipMemcpyAsync(h + o_out, dv + o_out, total - o_out, hipMemcpyDeviceToHost, st));
+        QF_CHECK_HIP(hipStreamSynchronize(st));
+        const uint32_t* nrec = reinterpret_cast<const uint32_t*>(h + o_nrec);
+        const int32_t* stt = reinterpret_cast<const int32_t*>(h + o_st);
+        for (size_t c = 0; c < G; ++c) {
+            DecAdd& x = v[done[cau[c]]];
+            const qf_dec_desc& q = descs[c];
+            if (stt[c] == QF_OK) {
+                decoder_assemble(x.d, q.L, nrec[c], reinterpret_cast<const uint16_t*>(h + o_ci) + q.rec_index_offset,
+                                 h + o_rec + q.rec_offset, q.rec_row_stride);
+                x.result = 1;
+            } else {
+                x.result = stt[c] == QF_ERANK ? 0 : stt[c];   // singular: stays undecoded (decoder.rs:756-758)
+            }
+        }
+    }
+    if ((s = ctx_recv_release(ctx)) != QF_OK) return s;
+    // explicit coefficient rows: the per-generation path (rows are on the device, stream order)
+    for (uint32_t t : expl) {
+        DecAdd& x = v[done[t]];
+        const int e = decoder_try_decode(x.d);
+        x.result = e == QF_ERANK ? 0 : (e != QF_OK ? e : (x.d->decoded ? 1 : 0));
     }
     return QF_OK;
 }

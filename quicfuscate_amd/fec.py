@@ -17,6 +17,21 @@ from typing import Optional
 from . import _lib as L
 from ._lib import QfError, check
 
+# Objects still alive when the interpreter exits are not freed through the
+# library: the process is ending, and the HIP runtime may already be torn
+# down by then (a late hipFree / hipEventSynchronize can crash the exit).
+_SHUTDOWN = False
+
+
+def _mark_shutdown() -> None:
+    global _SHUTDOWN
+    _SHUTDOWN = True
+
+
+import atexit as _atexit  # noqa: E402
+
+_atexit.register(_mark_shutdown)
+
 __all__ = [
     "QfError", "Context", "default_context", "init_gf_tables", "gf_mul", "gf_mul_table",
     "gf_mul_add", "gf_inv", "gf_mul_slice", "cauchy_coefficients", "MemoryPool", "Packet",
@@ -115,6 +130,8 @@ class Context:
             self.handle = None
 
     def __del__(self):  # pragma: no cover - best effort
+        if _SHUTDOWN:
+            return
         try:
             self.close()
         except Exception:
@@ -394,6 +411,8 @@ class Encoder:
                        cb[q * self.k: (q + 1) * self.k], self.k) for q in range(count)]
 
     def __del__(self):  # pragma: no cover
+        if _SHUTDOWN:
+            return
         try:
             L._lib().qf_encoder_free(self.handle)
         except Exception:
@@ -448,6 +467,8 @@ class Decoder:
         return res
 
     def __del__(self):  # pragma: no cover
+        if _SHUTDOWN:
+            return
         try:
             L._lib().qf_decoder_free(self.handle)
         except Exception:
@@ -556,6 +577,8 @@ class Encoder16:
                        cb[q * kb: (q + 1) * kb], kb) for q in range(count)]
 
     def __del__(self):  # pragma: no cover
+        if _SHUTDOWN:
+            return
         try:
             L._lib().qf_encoder16_free(self.handle)
         except Exception:
@@ -609,6 +632,8 @@ class Decoder16:
                 for i in range(cnt.value)]
 
     def __del__(self):  # pragma: no cover
+        if _SHUTDOWN:
+            return
         try:
             L._lib().qf_decoder16_free(self.handle)
         except Exception:
@@ -808,6 +833,8 @@ class AdaptiveFec:
             self.handle = None
 
     def __del__(self):  # pragma: no cover
+        if _SHUTDOWN:
+            return
         try:
             self.close()
         except Exception:
@@ -854,3 +881,42 @@ def on_send_batch(fecs, packets, queues=None):
             queues[m].append(Packet(d.id, payload, d.len, bool(d.is_systematic), coeffs, d.coeff_len))
         pos += n_out[m]
     return queues, list(st)
+
+
+def on_receive_batch(fecs, packets):
+    """AdaptiveFec.on_receive for many connections in one call
+    (qf_adaptive_on_receive_batch): fecs[m] receives packets[m].  Returns
+    (recovered, statuses): recovered[m] is the list on_receive would return
+    (empty on a per-packet error, whose status is in statuses[m])."""
+    M = len(fecs)
+    if len(packets) != M:
+        raise ValueError("one packet per connection")
+    if M == 0:
+        return [], []
+    lib = L._lib()
+    cap = max(1, sum(f.state()["k"] + 1024 for f in fecs))
+    stride = max(max(f.config.max_len for f in fecs), 1)
+    conns = (ctypes.c_void_p * M)(*[f.handle for f in fecs])
+    ids = (ctypes.c_uint64 * M)(*[p.id for p in packets])
+    sysf = (ctypes.c_int32 * M)(*[1 if p.is_systematic else 0 for p in packets])
+    pays = [p.payload() for p in packets]
+    bufs = [(ctypes.c_uint8 * max(1, len(b))).from_buffer_copy(b.ljust(max(1, len(b)), b"\0")) for b in pays]
+    data = (ctypes.c_void_p * M)(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint32 * M)(*[len(b) for b in pays])
+    cbufs = [None if p.coefficients is None else (ctypes.c_uint8 * max(1, p.coeff_len)).from_buffer_copy(
+        bytes(p.coefficients[: p.coeff_len]).ljust(max(1, p.coeff_len), b"\0")) for p in packets]
+    co = (ctypes.c_void_p * M)(*[None if c is None else ctypes.addressof(c) for c in cbufs])
+    cl = (ctypes.c_uint32 * M)(*[p.coeff_len if p.coefficients is not None else 0 for p in packets])
+    out = (ctypes.c_uint8 * (cap * stride))()
+    desc = (L.PacketDesc * cap)()
+    n_out = (ctypes.c_uint32 * M)()
+    st = (ctypes.c_int32 * M)()
+    check(lib.qf_adaptive_on_receive_batch(conns, M, ids, sysf, data, lens, co, cl, out, stride, desc, cap, n_out,
+                                           st), "on_receive_batch")
+    mv = memoryview(out)
+    res, pos = [], 0
+    for m in range(M):
+        res.append([Packet(desc[i].id, bytearray(mv[i * stride: i * stride + desc[i].len]), desc[i].len, True)
+                    for i in range(pos, pos + n_out[m])])
+        pos += n_out[m]
+    return res, list(st)

@@ -21,9 +21,10 @@ def main(tag: str) -> None:
         stats[name] = [{k: r[k] for k in ("Name", "Calls", "AverageNs")} for r in csv.DictReader(open(src))]
     doc = {
         "what": "AdaptiveFec.on_send over M connections (Normal mode, k=64, n=74, 1200-byte packets, full "
-                "windows: 10 repairs per packet); host wall clock per source packet",
+                "windows: 10 repairs per packet); host wall clock per source packet.  Rows with leg=receive: "
+                "on_receive of one generation per connection (58 of 64 sources + 10 repairs), per packet",
         "tool": "tools/send_batch/qf_send_bench.c (run_on_gpu.sh)",
-        "batch": "qf_adaptive_on_send_batch: one call per round of M packets",
+        "batch": "qf_adaptive_on_send_batch / qf_adaptive_on_receive_batch: one call per round of M packets",
         "sequential": "qf_adaptive_on_send per packet (the per-connection path)",
         "results": rows,
         "phase_profile_us_per_call": phases,

@@ -7,9 +7,12 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 rm -f gpurun_out/send_bench.jsonl gpurun_out/send_bench.err
 timeout -k 10 400 python -u -m pytest -x -v --timeout 150 --timeout-method thread \
-    tests/test_gpu_send_batch.py > gpurun_out/send_tests.log 2>&1
+    tests/test_gpu_send_batch.py tests/test_gpu_recv_batch.py > gpurun_out/send_tests.log 2>&1
 for M in 1 64 1024; do
   QF_SEND_PROFILE=1 timeout -k 10 200 tools/send_batch/build/qf_send_bench $M >> gpurun_out/send_bench.jsonl 2>> gpurun_out/send_bench.err
+done
+for M in 1 64 1024; do
+  timeout -k 10 200 tools/send_batch/build/qf_send_bench --recv $M >> gpurun_out/send_bench.jsonl 2>> gpurun_out/send_bench.err
 done
 R=$PWD
 cd /tmp && export TMPDIR=/tmp
