@@ -114,6 +114,8 @@ _ASM = {
     "v_andk": lambda d, k, a: f"v_and_b32_e32 {V(d)}, 0x{k:08x}, {V(a)}",
     "v_lshr": lambda d, s, a: f"v_lshrrev_b32_e32 {V(d)}, {s}, {V(a)}",
     "v_lshl": lambda d, s, a: f"v_lshlrev_b32_e32 {V(d)}, {s}, {V(a)}",
+    "v_lshl64": lambda d, s, a: f"v_lshlrev_b64 {VP(d)}, {s}, {VP(a)}",
+    "v_lshr64": lambda d, s, a: f"v_lshrrev_b64 {VP(d)}, {s}, {VP(a)}",
     "v_lshr_s": lambda d, s, a: f"v_lshrrev_b32_e64 {V(d)}, s{s}, {V(a)}",
     "v_addk": lambda d, k, a: f"v_add_u32_e32 {V(d)}, {k}, {V(a)}",
     "v_add_s": lambda d, s_, a: f"v_add_u32_e32 {V(d)}, s{s_}, {V(a)}",
@@ -457,6 +459,30 @@ def _transpose_ops(base: int, bfi: bool = False) -> list[Op]:
       a' = (M & a) | (~M & (b << s)),  b' = (M & (a >> s)) | (~M & b)
     i.e. two shifts and two v_bitop3 bit-selects with M in an SGPR."""
     ops = []
+    if bfi == "s64":
+        # stages 1 and 2 shift register pairs with one 64-bit shift: the bits a
+        # v_lshlrev_b64 carries into the high dword land where the bit-select
+        # takes the other operand (and likewise for the right shift into the
+        # low dword), so they never reach the result
+        for stage, (sh, mask, pairs) in enumerate(_TRANSPOSE):
+            sm = S_TMASK + stage
+            if stage == 2:
+                for q, (a, b) in enumerate(pairs):
+                    t, u = V_T + 2 * (q & 1), V_T + 2 * (q & 1) + 1
+                    ops.append(Op("v_lshl", (t, sh, base + b)))
+                    ops.append(Op("v_lshr", (u, sh, base + a)))
+                    ops.append(Op("v_bitsel_s", (base + a, sm, base + a, t)))
+                    ops.append(Op("v_bitsel_s", (base + b, sm, u, base + b)))
+                continue
+            for q in range(0, 4, 2):
+                (a0, b0), (a1, b1) = pairs[q], pairs[q + 1]
+                assert a1 == a0 + 1 and b1 == b0 + 1 and (base + a0) % 2 == 0 and (base + b0) % 2 == 0
+                ops.append(Op("v_lshl64", (V_T, sh, base + b0)))        # t pair = (b0, b1) << sh
+                ops.append(Op("v_lshr64", (V_T + 2, sh, base + a0)))    # u pair = (a0, a1) >> sh
+                for x, (a, b) in enumerate(((a0, b0), (a1, b1))):
+                    ops.append(Op("v_bitsel_s", (base + a, sm, base + a, V_T + x)))
+                    ops.append(Op("v_bitsel_s", (base + b, sm, V_T + 2 + x, base + b)))
+        return ops
     if bfi:
         for stage, (sh, mask, pairs) in enumerate(_TRANSPOSE):
             sm = S_TMASK + stage
@@ -1887,6 +1913,10 @@ class Emulator:
                 wv(a[0], rv(a[2]) >> np.uint64(a[1]))
             elif n == "v_lshl":
                 wv(a[0], (rv(a[2]) << np.uint64(a[1])) & np.uint64(MASK32))
+            elif n == "v_lshl64":
+                wv64(a[0], rv64(a[2]) << np.uint64(a[1]))
+            elif n == "v_lshr64":
+                wv64(a[0], rv64(a[2]) >> np.uint64(a[1]))
             elif n == "v_lshr_s":
                 wv(a[0], rv(a[2]) >> np.uint64(s[a[1]] & 31))
             elif n == "v_addk":

@@ -624,3 +624,73 @@ def test_synw_register_budget():
         for j0 in range(0, rt, rp):
             spec = bs.KernelSpec(k, min(rp, rt - j0), 3, mode="synw", r_total=rt, j0=j0)
             assert spec.next_free_vgpr <= 256 and spec.next_free_sgpr <= 102
+
+
+def test_transpose_shift64_equals_bfi():
+    """The 64-bit-shift transpose network (stages 1-2 on register pairs) maps
+    every 32-byte chunk to the same planes as the 32-bit one (and back)."""
+    rng = np.random.default_rng(8)
+    data = rng.integers(0, 1 << 32, (16, 64), dtype=np.uint64)
+    end = [bs.Op("s_endpgm", ())]
+    a = _run_regs(bs._transpose_ops(48, True) + bs._transpose_ops(56, True) + end, data)
+    b = _run_regs(bs._transpose_ops(48, "s64") + bs._transpose_ops(56, "s64") + end, data)
+    assert (a == b).all()
+    twice = _run_regs(bs._transpose_ops(48, "s64") + bs._transpose_ops(48, "s64") + end, data)
+    assert (twice[:8] == data[:8]).all()   # an involution
+
+
+def _run_regs(ops, regs):
+    """Execute straight-line transpose ops with v48..v63 preloaded; returns v48..v63."""
+    v = np.zeros((256, 64), np.uint64)
+    v[48:64] = regs
+    s = [0] * 104
+    s[bs.S_TMASK], s[bs.S_TMASK + 1], s[bs.S_TMASK + 2] = 0x0F0F0F0F, 0x33333333, 0x55555555
+    M = np.uint64(0xFFFFFFFF)
+    for op in ops:
+        n, a = op.name, op.args
+        if n == "v_lshl":
+            v[a[0]] = (v[a[2]] << np.uint64(a[1])) & M
+        elif n == "v_lshr":
+            v[a[0]] = v[a[2]] >> np.uint64(a[1])
+        elif n in ("v_lshl64", "v_lshr64"):
+            x = v[a[2]] | (v[a[2] + 1] << np.uint64(32))
+            x = (x << np.uint64(a[1])) if n == "v_lshl64" else (x >> np.uint64(a[1]))
+            v[a[0]], v[a[0] + 1] = x & M, x >> np.uint64(32)
+        elif n == "v_bitsel_s":
+            m = np.uint64(s[a[1]])
+            v[a[0]] = (m & v[a[2]]) | (~m & M & v[a[3]])
+        elif n == "s_endpgm":
+            break
+        else:
+            raise AssertionError(n)
+    return v[48:64]
+
+
+@pytest.mark.parametrize("mode", ["enc", "syn"])
+def test_shift64_kernels_match_default(oracle, mode):
+    """Whole kernels with the 64-bit-shift transposes compute the same bytes."""
+    k, r, L, G = 8, 4, 96, 5
+    rng = np.random.default_rng(23)
+    outs = []
+    for bfi in (True, "s64"):
+        spec = bs.KernelSpec(k, r, 2, mode, bfi_transpose=bfi)
+        emu = bs.Emulator(bs.generate(spec))
+        src = rng.integers(0, 256, G * k * L, dtype=np.uint8) if not outs else outs[0][0]
+        dst = np.zeros(G * r * L, np.uint8)
+        emu.add_buffer(0x1000000, src)
+        emu.add_buffer(0x9000000, dst)
+        if mode == "enc":
+            ka = bs.kernargs(0x1000000, 0x9000000, k * L, r * L, L, L, L, G, 4)
+        else:
+            smap = np.full(G * spec.map_stride, 0xFF, np.uint8)
+            for g in range(G):
+                smap[g * spec.map_stride: g * spec.map_stride + k] = np.arange(k)
+                smap[g * spec.map_stride + k: g * spec.map_stride + k + 2] = [0, 1]
+            emu.add_buffer(0x5000000, smap)
+            emu.add_buffer(0x6000000, np.zeros(L, np.uint8))
+            ka = bs.kernargs(0x1000000, 0x9000000, k * L, r * L, L, L, L, G, 4, smap=0x5000000,
+                             map_stride=spec.map_stride, zero=0x6000000)
+        for w in range(8):
+            emu.run_wave(ka, w // 4, w % 4)
+        outs.append((src, dst.copy()))
+    assert (outs[0][1] == outs[1][1]).all() and outs[0][1].any()

@@ -41,6 +41,22 @@ KERNEL(k_bfi, BFI)
 KERNEL(k_perms, PERMS)
 KERNEL(k_pkadd, PKADD)
 
+// 64-bit shifts (register pairs): would let the transpose network shift two
+// dwords per instruction
+#define LSHL64(x) asm volatile("v_lshlrev_b64 %0, 4, %0" : "+v"(x));
+#define LSHR64(x) asm volatile("v_lshrrev_b64 %0, 2, %0" : "+v"(x));
+#define KERNEL64(NAME, OP)                                                               \
+    __global__ void __launch_bounds__(256) NAME(uint32_t* out, uint32_t seed, uint32_t u1) { \
+        uint64_t a0 = threadIdx.x * 0x100000001ull + seed, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3,  \
+                 a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                       \
+        for (int i = 0; i < N_ITER; ++i) {                                               \
+            BODY8(OP) BODY8(OP) BODY8(OP) BODY8(OP) BODY8(OP) BODY8(OP) BODY8(OP) BODY8(OP) \
+        }                                                                                \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
+    }
+KERNEL64(k_lshl64, LSHL64)
+KERNEL64(k_lshr64, LSHR64)
+
 // mixed: the encode inner-loop ratio, 2 perm : 1 bitop3
 #define MIX(x) PERM(x) PERM(x) BITOP3(x)
 __global__ void __launch_bounds__(256) k_mix(uint32_t* out, uint32_t seed, uint32_t u1) {
@@ -90,7 +106,7 @@ int main() {
         {"v_perm_b32", k_perm, 64}, {"v_bitop3_b32", k_bitop3, 64}, {"v_xor_b32", k_xor, 64},
         {"v_and_b32", k_and, 64}, {"v_lshrrev_b32", k_lshr, 64}, {"v_and_or_b32", k_andor, 64},
         {"v_bfi_b32", k_bfi, 64}, {"v_perm_b32(sgpr)", k_perms, 64}, {"v_pk_add_u16", k_pkadd, 64},
-        {"mix 2perm:1bitop3", k_mix, 192},
+        {"mix 2perm:1bitop3", k_mix, 192}, {"v_lshlrev_b64", k_lshl64, 64}, {"v_lshrrev_b64", k_lshr64, 64},
     };
     hipEvent_t a, b;
     hipEventCreate(&a);
