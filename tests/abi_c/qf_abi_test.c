@@ -7,6 +7,7 @@
  *   desc      qf_encode_batch_desc / qf_decode_batch_desc (mixed windows)
  *   objects   qf_encoder_* / qf_decoder_*             decoder.rs:155-299, 658-791
  *   adaptive  qf_adaptive_on_send / on_receive / state adaptive.rs:508-599
+ *             and their multi-connection batches (_on_send_batch / _on_receive_batch)
  *   framing   qf_packet_to_raw / from_raw / from_block encoder.rs:18-152
  *
  * Exit status 0 and "ALL OK" on success; the first mismatch is printed.
@@ -275,6 +276,104 @@ static void test_adaptive(qf_ctx *ctx) {
     printf("adaptive ok\n");
 }
 
+/* qf_adaptive_on_send_batch / on_receive_batch over C connections: every
+ * connection's repairs equal the oracle's encode of its window, and every
+ * receiver recovers its generation. */
+static void test_adaptive_batch(qf_ctx *ctx) {
+    enum { C = 8 };
+    qf_fec_config cfg;
+    qf_fec_config_default(&cfg);
+    cfg.initial_mode = QF_MODE_NORMAL;
+    cfg.max_len = 1200;
+    qf_adaptive *snd[C], *rcv[C];
+    for (int c = 0; c < C; ++c) {
+        QF(qf_adaptive_new_at(ctx, &cfg, 0.0, &snd[c]));
+        QF(qf_adaptive_new_at(ctx, &cfg, 0.0, &rcv[c]));
+    }
+    uint32_t k, n;
+    QF(qf_adaptive_state(snd[0], NULL, NULL, &k, &n, NULL, NULL, NULL));
+    const uint32_t r = n - k, per = qf_adaptive_max_send_packets(snd[0]), cap = per * C;
+    const uint32_t L = 1100;
+    uint8_t *pk = malloc((size_t)C * k * L), *out = malloc((size_t)cap * 1200), *co = malloc((size_t)cap * 256);
+    uint8_t *rep = malloc((size_t)C * r * 1200), *rco = malloc((size_t)C * r * 256), *want = malloc((size_t)r * L);
+    qf_packet_desc *desc = malloc(cap * sizeof(qf_packet_desc));
+    uint32_t n_out[C];
+    int32_t st[C];
+    for (size_t t = 0; t < (size_t)C * k * L; ++t) pk[t] = rnd8();
+    for (uint32_t i = 0; i < k; ++i) {
+        uint64_t ids[C];
+        const uint8_t *data[C];
+        uint32_t lens[C];
+        for (int c = 0; c < C; ++c) ids[c] = i, data[c] = pk + ((size_t)c * k + i) * L, lens[c] = L;
+        QF(qf_adaptive_on_send_batch(snd, C, ids, data, lens, out, 1200, co, 256, desc, cap, n_out, st));
+        uint32_t pos = 0;
+        for (int c = 0; c < C; ++c) {
+            CHECK(st[c] == QF_OK && n_out[c] == (i + 1 < k ? 1 : 1 + r), "send batch count %u/%d: %u", i, c, n_out[c]);
+            CHECK(desc[pos].is_systematic && desc[pos].id == i && memcmp(out + (size_t)pos * 1200, data[c], L) == 0,
+                  "send batch systematic %u/%d", i, c);
+            for (uint32_t j = 0; j + 1 < n_out[c]; ++j) {
+                memcpy(rep + ((size_t)c * r + j) * 1200, out + (size_t)(pos + 1 + j) * 1200, 1200);
+                memcpy(rco + ((size_t)c * r + j) * 256, co + (size_t)(pos + 1 + j) * 256, 256);
+                CHECK(desc[pos + 1 + j].id == k + j && desc[pos + 1 + j].coeff_len == k, "repair desc");
+            }
+            pos += n_out[c];
+        }
+    }
+    for (int c = 0; c < C; ++c) {
+        CHECK(oracle_encode_window(k, r, L, pk + (size_t)c * k * L, L, NULL, want, L) == 0, "oracle");
+        for (uint32_t j = 0; j < r; ++j)
+            CHECK(memcmp(rep + ((size_t)c * r + j) * 1200, want + (size_t)j * L, L) == 0, "batch repair %d/%u", c, j);
+    }
+    /* receivers: connection c loses sources c + 7 q (q < 3), then gets the repairs */
+    uint8_t *rout = malloc((size_t)C * k * 1200);
+    qf_packet_desc *rdesc = malloc((size_t)C * k * sizeof(qf_packet_desc));
+    uint32_t got[C] = {0};
+    uint8_t *recv = calloc((size_t)C * k, 1200);
+    for (uint32_t t = 0; t < k + r; ++t) {
+        uint64_t ids[C];
+        int32_t sys[C];
+        const uint8_t *data[C], *cf[C];
+        uint32_t lens[C], cl[C];
+        uint32_t M = 0;
+        qf_adaptive *conns[C];
+        int which[C];
+        for (int c = 0; c < C; ++c) {
+            if (t < k && (t == (uint32_t)c || t == (uint32_t)c + 7 || t == (uint32_t)c + 14)) continue;  /* lost */
+            conns[M] = rcv[c];
+            which[M] = c;
+            if (t < k) {
+                ids[M] = t, sys[M] = 1, data[M] = pk + ((size_t)c * k + t) * L, lens[M] = L, cf[M] = NULL, cl[M] = 0;
+            } else {
+                const uint32_t j = t - k;
+                ids[M] = k + j, sys[M] = 0, data[M] = rep + ((size_t)c * r + j) * 1200, lens[M] = L;
+                cf[M] = rco + ((size_t)c * r + j) * 256, cl[M] = k;
+            }
+            ++M;
+        }
+        QF(qf_adaptive_on_receive_batch(conns, M, ids, sys, data, lens, cf, cl, rout, 1200, rdesc, C * k, n_out, st));
+        uint32_t pos = 0;
+        for (uint32_t q = 0; q < M; ++q) {
+            CHECK(st[q] == QF_OK, "receive batch status %d", st[q]);
+            for (uint32_t i = 0; i < n_out[q]; ++i) {
+                const qf_packet_desc *d = &rdesc[pos + i];
+                CHECK(d->id < k && d->len == L, "recovered id/len");
+                memcpy(recv + ((size_t)which[q] * k + d->id) * 1200, rout + (size_t)(pos + i) * 1200, L);
+            }
+            got[which[q]] += n_out[q];
+            pos += n_out[q];
+        }
+    }
+    for (int c = 0; c < C; ++c) {
+        CHECK(got[c] == k, "connection %d recovered %u of %u", c, got[c], k);
+        for (uint32_t i = 0; i < k; ++i)
+            CHECK(memcmp(recv + ((size_t)c * k + i) * 1200, pk + ((size_t)c * k + i) * L, L) == 0, "payload %d/%u", c, i);
+        QF(qf_adaptive_free(snd[c]));
+        QF(qf_adaptive_free(rcv[c]));
+    }
+    free(pk); free(out); free(co); free(rep); free(rco); free(want); free(desc); free(rout); free(rdesc); free(recv);
+    printf("adaptive batch ok\n");
+}
+
 static void test_framing(void) {
     uint8_t payload[1200], coeffs[64], frame[1300], oframe[1300];
     for (int t = 0; t < 1200; ++t) payload[t] = rnd8();
@@ -315,6 +414,7 @@ int main(void) {
     test_desc(ctx);
     test_objects(ctx);
     test_adaptive(ctx);
+    test_adaptive_batch(ctx);
     QF(qf_ctx_destroy(ctx));
     printf("ALL OK\n");
     return 0;
