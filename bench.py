@@ -80,6 +80,23 @@ def xor_fold(torch, buf) -> int:
     return int(w.item()) & ((1 << 64) - 1)
 
 
+def broadcast_descriptor(torch, dist, lib, k: int, r: int, Lb: int, G: int, e: int, world: int, device) -> bool:
+    """rank 0 broadcasts the run descriptor and the r x k Cauchy
+    coefficient matrix; every rank checks them against its own (the shards
+    must encode the same code).  Returns this rank's match flag."""
+    import ctypes
+
+    mine = np.zeros(r * k, np.uint8)
+    if lib.qf_cauchy_coeffs(k, r, mine.ctypes.data_as(ctypes.c_void_p)) != 0:
+        return False
+    d = torch.tensor([k, r, Lb, G, e, SEED], dtype=torch.int64, device=device)
+    c = torch.from_numpy(mine.copy()).to(device)
+    if world > 1:
+        dist.broadcast(d, src=0)
+        dist.broadcast(c, src=0)
+    return d.tolist() == [k, r, Lb, G, e, SEED] and bool((c.cpu().numpy() == mine).all())
+
+
 def gather_folds(torch, dist, fold: int, world: int, device) -> list:
     """Every rank's repair XOR-fold (RCCL all_gather: XOR is not a reduction op)."""
     t = torch.tensor([fold - (1 << 64) if fold >= 1 << 63 else fold], dtype=torch.int64, device=device)
@@ -145,6 +162,7 @@ def main(argv=None):
         args.G = 156250 if c4 else 65536   # C4: 10,000,000 packets / 64 per generation
     k, r, Lb, G, e = args.k, args.r, args.L, args.G, args.erase
     dev = torch.device("cuda", local)
+    desc_ok = broadcast_descriptor(torch, dist, lib, k, r, Lb, G, e, world, dev if backend == "nccl" else "cpu")
     # A dedicated stream for the library AND torch: torch's default stream is
     # handle 0, which the C ABI would replace by a private stream, and the
     # timing events must be recorded on the stream the kernels run on.
@@ -287,8 +305,9 @@ def main(argv=None):
         sample_ok = rank_oracle_sample(torch, src, rep, rows, aidx, rec, k, r, Lb, Lr, e, G, args.rank_sample,
                                        SEED + rank)
     sample_flags = gather_flags(torch, dist, -1 if sample_ok is None else int(sample_ok), world, coll_dev)
+    desc_flags = gather_flags(torch, dist, int(desc_ok), world, coll_dev)
     step_ms_max, enc_ms_max, dec_ms_max, fails = reduce_max(
-        torch, dist, [step_ms, enc_ms, dec_ms, 0.0 if (verified and sample_ok is not False) else 1.0], world,
+        torch, dist, [step_ms, enc_ms, dec_ms, 0.0 if (verified and sample_ok is not False and desc_ok) else 1.0], world,
         coll_dev)
 
     src_bytes_total = world * G * k * Lb
@@ -402,6 +421,8 @@ def main(argv=None):
         "process_group": {"backend": dist.get_backend() if world > 1 else None,
                           "world_size": dist.get_world_size() if world > 1 else 1,
                           "env_world_size": world},
+        "run_descriptor": {"broadcast_from_rank0": world > 1, "fields": ["k", "r", "L", "G", "erased", "seed"],
+                           "cauchy_matrix_bytes": r * k, "matches_by_rank": [bool(f == 1) for f in desc_flags]},
     }
     if c4:
         out["config"]["workload"] = (f"C4 independent-generation encode + C3-shape decode sharded over {world} rank(s): "

@@ -69,6 +69,10 @@ def _worker(rank, world, port, q):
     folds = bench.gather_folds(torch, dist, (0xF000000000000000 | rank), world, "cpu")
     assert folds == [0xF000000000000000, 0xF000000000000001]
     assert bench.gather_flags(torch, dist, rank == 0, world, "cpu") == [1, 0]
+    # rank 0's run descriptor + Cauchy matrix reach every rank (host-only ABI call)
+    from quicfuscate_amd import _lib as L
+
+    assert bench.broadcast_descriptor(torch, dist, L._lib(), 64, 16, 1200, 1000, 13, world, "cpu")
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank, lo, hi, out))

@@ -34,5 +34,6 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert d["rank_oracle_sample"]["pass_by_rank"] == [True, True]
     assert d["rank_oracle_sample"]["generations_per_rank"] >= 64
     assert d["process_group"]["world_size"] == 2 and d["process_group"]["backend"] == "gloo"
+    assert d["run_descriptor"]["broadcast_from_rank0"] and d["run_descriptor"]["matches_by_rank"] == [True, True]
     sh = d["sliding_halo"]
     assert sh["first_window_matches"] and sh["halo_packets"] == 63 and sh["ms_per_step_max"] > 0
