@@ -130,3 +130,31 @@ def test_recv_batch_many_generations_decode_together(qf, gpu_ctx):
         for p in got[c]:
             o = origs[c][p.id]
             assert p.payload()[: len(o)] == o and not any(p.payload()[len(o):]), (c, p.id)
+
+
+def test_recv_batch_explicit_coefficients_and_second_context(qf, gpu_ctx):
+    """Repairs whose coefficient vectors are not Cauchy rows of the
+    generation take the per-decoder Gauss-Jordan path inside the batch, and
+    a connection on another context takes the per-connection path; both equal
+    their per-packet twins."""
+    M = qf.FecMode
+    rng = np.random.default_rng(77)
+    cfg = _cfg(qf, M.Normal, normal=20, max_len=512)
+    ctx2 = qf.Context(0)
+    recv = [qf.AdaptiveFec(cfg, now=0.0) for _ in range(3)] + [qf.AdaptiveFec(cfg, now=0.0, ctx=ctx2)]
+    twin = [qf.AdaptiveFec(cfg, now=0.0) for _ in range(4)]
+    k = recv[0].state()["k"]
+    streams = []
+    for c in range(4):
+        src = [rng.integers(0, 256, 512, dtype=np.uint8).tobytes() for _ in range(k)]
+        pk = [qf.Packet(i, bytearray(src[i]), 512, True) for i in range(k) if i not in (2, 11)]
+        for j in range(3):   # random (invertible with high probability) coefficient vectors
+            co = rng.integers(1, 256, k, dtype=np.uint8)
+            pay = rng.integers(0, 256, 512, dtype=np.uint8).tobytes()
+            pk.append(qf.Packet(k + j, bytearray(pay), 512, False, bytes(co), k))
+        streams.append(pk)
+    for t in range(len(streams[0])):
+        res, st = qf.on_receive_batch(recv, [s[t] for s in streams])
+        for c in range(4):
+            want = twin[c].on_receive(streams[c][t])
+            assert st[c] == L.QF_OK and _same(res[c], want), (t, c)

@@ -158,3 +158,20 @@ def test_send_batch_argument_errors(qf, gpu_ctx):
         twin.on_send(qf.Packet(i, bytearray([i] * 10), 10, True), q2)
         assert len(q1[0]) == len(q2) and all(_same(a, b) for a, b in zip(q1[0], q2))
     assert len(q1[0]) > 1
+
+
+def test_send_batch_second_context(qf, oracle, gpu_ctx):
+    """A connection on another context takes the per-connection path inside
+    the batch; every connection equals its twin."""
+    ctx2 = qf.Context(0)
+    cfg = _cfg(qf, qf.FecMode.Normal, normal_window=20, max_len=600)
+    conns = [qf.AdaptiveFec(cfg, now=0.0), qf.AdaptiveFec(cfg, now=0.0, ctx=ctx2), qf.AdaptiveFec(cfg, now=0.0)]
+    twins = [qf.AdaptiveFec(cfg, now=0.0) for _ in conns]
+    rng = np.random.default_rng(3)
+    for i in range(25):
+        pays = [rng.integers(0, 256, 600, dtype=np.uint8).tobytes() for _ in conns]
+        q, st = qf.on_send_batch(conns, [qf.Packet(i, bytearray(b), 600, True) for b in pays])
+        for c in range(3):
+            want = []
+            twins[c].on_send(qf.Packet(i, bytearray(pays[c]), 600, True), want)
+            assert st[c] == L.QF_OK and len(q[c]) == len(want) and all(_same(a, b) for a, b in zip(q[c], want))
