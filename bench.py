@@ -125,6 +125,8 @@ def parse(argv=None):
     ap.add_argument("--erase", type=int, default=13, help="erased sources per generation (20%% of 64)")
     ap.add_argument("--cpu-sample", type=int, default=4096, help="generations in the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c3b-G", type=int, default=65536,
+                    help="generations of the C3 secondary variant (i.i.d. 20 %% loss over all k + r rows; 0 = skip)")
     ap.add_argument("--host-path-G", type=int, default=16384, help="generations for the pinned-host encode rate (0=skip)")
     ap.add_argument("--overlap", action="store_true",
                     help="run the step's encode and decode (independent batches) on two HIP streams")
@@ -436,6 +438,9 @@ def main(argv=None):
     if rank == 0 and world == 1:
         out["hbm_copy_context"] = copy_bandwidth(torch)
 
+    if rank == 0 and world == 1 and args.c3b_G > 0:
+        out["c3_bernoulli"] = c3_bernoulli_leg(torch, fec, ctx, srcv, repv, k, r, Lb, min(args.c3b_G, G), dev)
+
     if rank == 0 and world == 1 and args.host_path_G > 0:
         out["host_path"] = host_path_rate(torch, lib, L, ctx, k, r, Lb, min(args.host_path_G, G))
         out["host_path"]["decode"] = host_decode_rate(torch, lib, L, ctx, rows, row_index, rec, e, n_slots, k, r,
@@ -541,6 +546,77 @@ def sliding_halo_leg(torch, dist, ctx, lib, L, rank, world, dev, backend, packet
     return {"packets_per_rank": packets, "k": k, "r": r, "L": Lb, "halo_packets": k - 1,
             "backend": dist.get_backend(), "ms_per_step_max": round(ms_max, 4),
             "windows_per_s": round(P / (ms_max / 1e3), 1), "first_window_matches": bad == 0}
+
+
+def c3_bernoulli_leg(torch, fec, ctx, srcv, repv, k, r, Lb, G, dev, p_loss=0.2, reps=3) -> dict:
+    """SURVEY 8(d) C3 secondary variant: every one of the k + r rows of a
+    generation is lost i.i.d. with p = 0.2; arrivals are the surviving sources
+    in index order, then the surviving repairs.  A generation decodes iff at
+    least k rows arrive (decoder.rs:679); the success rate is compared with
+    the row counts and with P(Binom(k + r, p) <= r), and every recovered byte
+    with the source it replaces."""
+    import math
+
+    n = k + r
+    rng = np.random.default_rng(SEED ^ 0xB3)
+    keep = rng.random((G, n)) >= p_loss
+    n_rows = keep.sum(axis=1).astype(np.int32)
+    order = np.argsort(~keep, axis=1, kind="stable")          # kept rows first, in index order
+    aidx = np.where(np.arange(n)[None, :] < n_rows[:, None], order, 0).astype(np.uint16)
+    rows = torch.empty(G * n * Lb, dtype=torch.uint8, device=dev)
+    rowsv = rows.view(G, n, Lb)
+    aidx_t = torch.from_numpy(aidx.astype(np.int64)).to(dev)
+    CH = 4096
+    for g0 in range(0, G, CH):
+        g1 = min(G, g0 + CH)
+        both = torch.cat([srcv[g0:g1], repv[g0:g1]], dim=1)
+        gi = torch.arange(g1 - g0, device=dev)[:, None].expand(-1, n)
+        rowsv[g0:g1] = both[gi, aidx_t[g0:g1]]
+        del both
+    row_index = torch.from_numpy(aidx.view(np.int16)).to(dev)
+    n_rows_t = torch.from_numpy(n_rows).to(dev)
+    emax = min(k, r)
+    rec = torch.empty(G * emax * Lb, dtype=torch.uint8, device=dev)
+    rec_index = torch.empty(G * emax, dtype=torch.int16, device=dev)
+    n_rec = torch.empty(G, dtype=torch.int32, device=dev)
+    status = torch.empty(G, dtype=torch.int32, device=dev)
+    args = dict(max_rows=n, row_stride=Lb, rows_gen_stride=n * Lb, rec_row_stride=Lb, rec_gen_stride=emax * Lb, G=G,
+                n_rows=n_rows_t, ctx=ctx)
+
+    def dec():
+        fec.decode_batch(rows, row_index, rec, rec_index, n_rec, status, k, r, Lb, **args)
+
+    dec()
+    torch.cuda.synchronize()
+    ctx.profile(True)
+    for _ in range(reps):
+        dec()
+    torch.cuda.synchronize()
+    kt = ctx.kernel_times()
+    ctx.profile(False)
+    dec_ms = sum(ms for _, ms in kt.values()) / reps
+    st = status.cpu().numpy()
+    ok = st == 0
+    expect = n_rows >= k
+    # recovered rows: the sources that did not arrive (all arrivals that are
+    # sources come first, so every received source is accepted)
+    nr = n_rec.cpu().numpy()
+    verified = bool((ok == expect).all() and (nr[ok] == (k - keep[ok, :k].sum(axis=1))).all()
+                    and ((st[~ok] == -3).all()))
+    if verified and ok.any():
+        ri = rec_index.view(G, emax).long()
+        gsel = torch.from_numpy(np.nonzero(ok)[0]).to(dev)
+        m = torch.from_numpy(np.arange(emax)[None, :] < nr[ok][:, None]).to(dev)
+        got = rec.view(G, emax, Lb)[gsel]
+        want = srcv[gsel[:, None].expand(-1, emax), ri[gsel].clamp(0, k - 1)]
+        verified = bool(((got == want) | ~m[..., None]).all().item())
+    p_ok = sum(math.comb(n, j) * p_loss ** j * (1 - p_loss) ** (n - j) for j in range(0, r + 1))
+    src_bytes = float(ok.sum()) * k * Lb
+    return {"generations": G, "loss": p_loss, "rows_per_generation": n,
+            "success_rate": round(float(ok.mean()), 4), "expected_success_rate": round(p_ok, 4),
+            "success_iff_k_rows_arrived": bool((ok == expect).all()), "verified": verified,
+            "decode_ms": round(dec_ms, 4), "kernels": {n_: round(ms / reps, 4) for n_, (c, ms) in kt.items()},
+            "decode_gibps_source_of_decoded_generations": round(src_bytes / (dec_ms / 1e3) / 2**30, 1)}
 
 
 def host_path_rate(torch, lib, L, ctx, k, r, Lb, G):
