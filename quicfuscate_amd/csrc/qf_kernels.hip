@@ -990,27 +990,24 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
         }
         wave_sync();
     }
-    // record: 16 columns x 16 bytes, then 16 rank bytes; 17 x 16 bytes, one
-    // 16-byte store per lane
+    // record: 16 columns x 16 bytes, then 16 rank bytes = 68 dwords, one
+    // dword per lane (column u = d / 4, bytes t = 4 (d % 4) .. + 3): the
+    // lookups of a lane are independent, so they overlap
     uint8_t* lo = a.lu_out + (uint64_t)g * a.lu_stride;
-    if (lane < 17) {
-        uint32_t wd[4];
-        for (uint32_t q = 0; q < 4; ++q) {
-            uint32_t v = 0;
-            for (uint32_t b = 0; b < 4; ++b) {
-                const uint32_t t = 4 * q + b;
-                uint32_t x;
-                if (lane == 16) {
-                    x = ok ? P.rank[t] : 0xFF;
-                } else {
-                    const uint32_t u = lane;
-                    x = (ok && P.rank[t] != 0xFF && P.rank[u] != 0xFF) ? P.LU[P.rank[t]][P.rank[u]] : 0;
-                }
-                v |= x << (8 * b);
-            }
-            wd[q] = v;
+    for (uint32_t d = lane; d < 68; d += 64) {
+        const uint32_t u = d >> 2, q = d & 3;
+        const uint32_t ru = u < 16 ? P.rank[u] : 0xFF;
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t t = 4 * q + b;
+            const uint32_t rt = P.rank[t];
+            uint32_t x;
+            if (u == 16) x = ok ? rt : 0xFF;
+            else x = (ok && rt != 0xFF && ru != 0xFF) ? P.LU[rt][ru] : 0;
+            v |= x << (8 * b);
         }
-        *reinterpret_cast<uint4*>(lo + 16 * lane) = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        *reinterpret_cast<uint32_t*>(lo + 4 * d) = v;
     }
     uint8_t* sm = a.smap + (uint64_t)g * a.map_stride;
     for (uint32_t q = lane; q < a.map_stride; q += 64) {
