@@ -72,7 +72,6 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
                          uint32_t lu_stride = 0, const uint32_t* tab256 = nullptr,
                          const uint64_t* src_offs = nullptr, const uint64_t* dst_offs = nullptr,
                          const uint32_t* bound = nullptr) {
-    (void)num_cus;
     if (!e) return hipErrorInvalidValue;
     int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return hipErrorInvalidValue;
@@ -100,8 +99,17 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     uint32_t magic, shift;
     magic_for(Lv, &magic, &shift);
     const uint32_t n_items = (uint32_t)(e->mode == 'c' ? (total + 63) / 64 : (total + 127) / 128);
-    const uint32_t blocks = (n_items + 3) / 4;
+    uint32_t blocks = (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
+    // persistent grids (the item loop strides by the grid's wave count):
+    // QF_ENC_BLOCKS_PER_CU / QF_DEC_BLOCKS_PER_CU cap the grid at that many
+    // 4-wave blocks per CU, so an encode and a decode launched on two streams
+    // can be resident on every SIMD at once
+    {
+        const char* cap = getenv(e->mode == 'e' ? "QF_ENC_BLOCKS_PER_CU" : "QF_DEC_BLOCKS_PER_CU");
+        const int c = cap ? atoi(cap) : 0;
+        if (c > 0 && num_cus > 0 && blocks > (uint32_t)(c * num_cus)) blocks = (uint32_t)(c * num_cus);
+    }
     uint32_t a[32] = {};
     a[0] = (uint32_t)(uintptr_t)src;
     a[1] = (uint32_t)((uintptr_t)src >> 32);
