@@ -348,6 +348,10 @@ class KernelSpec:
     # so each lane has one slot map, one LU record and one table read per
     # coefficient for both 16-byte halves (_generate_dec_chunked)
     chunked: bool = False
+    # lab only (chunked): one generation per wave (item = generation, lanes
+    # q < Q active), so row presence is wave-uniform and the row loop skips
+    # the erased sources (tools/dec_lab.py)
+    wave_gen: bool = False
 
     @property
     def rt(self) -> int:
@@ -1292,8 +1296,17 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
     E(Op("s_far_jump", (".Lend", 0)))
     E(Op("label", (".Lgo",)))
-    E(Op("v_lshl_add_s", (V_F, 28, 6, V_LANE)))   # f = 64 item + lane
-    E(Op("v_cmp_gt_s", (26, 14, V_F)))             # f < G * Q
+    if spec.wave_gen:
+        # f = Q item + (lane < Q ? lane : 0): lanes past Q alias lane 0 and store nothing
+        E(Op("v_cmp_gt_s", (26, 13, V_LANE)))
+        E(Op("v_movk", (V_T, 0)))
+        E(Op("s_nop", (4,)))
+        E(Op("v_cndmask", (V_T, V_T, V_LANE, 26)))
+        E(Op("s_mul", (S_TMP, 28, 13)))
+        E(Op("v_add_s", (V_F, S_TMP, V_T)))
+    else:
+        E(Op("v_lshl_add_s", (V_F, 28, 6, V_LANE)))   # f = 64 item + lane
+        E(Op("v_cmp_gt_s", (26, 14, V_F)))             # f < G * Q
     E(Op("v_mul_hi_s", (V_GA, V_F, 15)))
     E(Op("v_lshr_s", (V_GA, 16, V_GA)))            # g
     E(Op("v_mul_lo_s", (V_UA, V_GA, 13)))
@@ -1352,6 +1365,9 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         E(Op("s_cmp_lg64_br", (S_TMP, ".Ljdone")))
     E(Op("s_movk", (S_JMAX, 0)))
     E(Op("label", (".Ljdone",)))
+    if spec.wave_gen:   # any source row may be skipped, so no row initialises
+        for a in range(acc0, acc0 + 8 * r):
+            E(Op("v_movk", (a, 0)))
 
     def load_row(n: int):
         b = ring0 + 8 * (n % nbuf)
@@ -1384,6 +1400,13 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
             for b in range(8):
                 E(Op("v_xor", (acc0 + 8 * idx + b, acc0 + 8 * idx + b, base + b)))
             E(Op("label", (f".Lrep{idx}",)))
+        elif spec.wave_gen:
+            present(idx, S_TMP)
+            E(Op("s_and64", (S_TMP, S_TMP, S_STA)))
+            E(Op("s_cmp_eq64_0_br", (S_TMP, f".Lskip{n}")))
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose,
+                        guard=(spec.guard_min, f".Lrow{n}"))
+            E(Op("label", (f".Lskip{n}",)))
         else:
             _source_row(ops, C, idx, r, base, acc0, init=idx == 0, xor3=spec.xor3, bfi=spec.bfi_transpose,
                         guard=(spec.guard_min, f".Lrow{n}"))
@@ -1624,7 +1647,7 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
              total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
              Lv: Optional[int] = None, zero_tail: bool = False, lu: Optional[tuple[int, int]] = None,
              tables: int = 0, src_offs: int = 0, dst_offs: int = 0, chunked: bool = False,
-             bound: Optional[int] = None) -> bytes:
+             bound: Optional[int] = None, wave_gen: bool = False) -> bytes:
     """96-byte kernarg block (layout above; 128 bytes in dec mode).  Syndrome mode: src = received
     rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
     also write zeros to bytes [L, 16 Lv) of every repair row.  Dec mode
@@ -1635,7 +1658,7 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
     if chunked:   # lane-chunk layout (_prologue_chunked): Lv <- Q = ceil(Lu / 2)
         Lv = ((L + 15) // 16 + 1) // 2
         total = G * Lv
-        n_items = (total + 63) // 64
+        n_items = G if wave_gen else (total + 63) // 64
         magic, shift = magic_for(Lv)
     s19 = map_stride if smap else (Lv if zero_tail else L // 16)
     if L % 16 and not (zero_tail or smap):

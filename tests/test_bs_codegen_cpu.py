@@ -280,11 +280,12 @@ def test_xcd_remap_is_a_bijection():
         assert got == list(range(nwg))
 
 
-def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=False, offs=False):
+def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=False, offs=False,
+              wave_gen=False):
     """Run the fused decode kernel (mode "dec") on the emulator: random
     erasures (or `erase` sources), random accepted repairs in random slots,
     LU records from bs.lu_record; returns the number of wrong rows."""
-    spec = bs.KernelSpec(k, r, pd, mode="dec", chunked=chunked)
+    spec = bs.KernelSpec(k, r, pd, mode="dec", chunked=chunked, wave_gen=wave_gen)
     rng = np.random.default_rng(seed)
     rs = L + 16
     n_slots = k + 2
@@ -321,7 +322,7 @@ def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=Fal
         emu.add_buffer(base, buf)
     if chunked:
         Lv = None
-        items = (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
+        items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
         waves = (items + 3) // 4
     else:
         waves = (bs.launch_geometry(L, G, Lv)[2] + 3) // 4
@@ -335,7 +336,8 @@ def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=Fal
         rows_l = rows.reshape(G, rgs)[::-1].copy().reshape(-1)
         emu.mem[ROWS][:] = rows_l
     ka = bs.kernargs(ROWS, OUT, gs_r, gs_o, rs, rrs, L, G, waves * 4, smap=MAP, map_stride=ms, zero=ZERO,
-                     Lv=Lv, lu=(REC, bs.LU_REC_BYTES), tables=TAB, src_offs=so, dst_offs=do, chunked=chunked)
+                     Lv=Lv, lu=(REC, bs.LU_REC_BYTES), tables=TAB, src_offs=so, dst_offs=do, chunked=chunked,
+                     wave_gen=wave_gen)
     for wg in range(waves):
         for w in range(4):
             emu.run_wave(ka, wg, w)
@@ -506,6 +508,16 @@ def test_emulated_fused_decode_chunked(oracle, k, r, pd, L, G, seed, erase, offs
     q + Q) recovers the erased sources, with strided generations or offset
     tables, and writes nothing else."""
     assert _dec_case(oracle, k, r, pd, L, G, seed, erase, padded=False, chunked=True, offs=offs) == 0
+
+
+@pytest.mark.parametrize("k,r,pd,L,G,seed,erase", [
+    (8, 4, 2, 96, 6, 1, None),
+    (16, 16, 3, 1200, 2, 7, 13),
+])
+def test_emulated_fused_decode_wave_gen(oracle, k, r, pd, L, G, seed, erase):
+    """Lab variant (tools/dec_lab.py): one generation per wave, erased source
+    rows skipped by a wave-uniform branch; same recovered rows."""
+    assert _dec_case(oracle, k, r, pd, L, G, seed, erase, padded=False, chunked=True, wave_gen=True) == 0
 
 
 @pytest.mark.parametrize("k,r,mode,chunked", [(64, 16, "enc", False), (64, 16, "syn", False),

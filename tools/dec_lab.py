@@ -44,6 +44,13 @@ VARIANTS = [
     ("stag12", {"stagger": (256, 256, 12)}, ()),
     ("stag18", {"stagger": (256, 256, 18)}, ()),
     ("stag12_all", {"stagger": (256, 1 << 30, 12)}, ()),
+    # round 2: the lane-chunk layout (the library default) against one
+    # generation per wave (Q = 38 of 64 lanes active, erased source rows skipped)
+    ("decc", {"chunked": True}, ()),
+    ("decc_nolu", {"chunked": True, "lu": False}, ()),
+    ("wavegen", {"chunked": True, "wave_gen": True}, ()),
+    ("wavegen_nolu", {"chunked": True, "wave_gen": True, "lu": False}, ()),
+    ("decc_2", {"chunked": True}, ()),
 ]
 
 
@@ -112,11 +119,15 @@ def run(G, reps):
         assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
         Lv = None
+        chunked, wave_gen = m["kw"].get("chunked", False), m["kw"].get("wave_gen", False)
         _, _, n_items = bs.launch_geometry(L, G, Lv)
+        if chunked:
+            n_items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
         blocks = (n_items + 3) // 4
         ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * L, e * L, L, L, L, G, blocks * 4,
                          smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
-                         lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr())
+                         lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr(), chunked=chunked,
+                         wave_gen=wave_gen)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
@@ -136,7 +147,8 @@ def run(G, reps):
         torch.cuda.synchronize()
         ms = t0.elapsed_time(t1) / reps
         alg = G * ((k + e) * L)
-        res[m["name"]] = {"ms": round(ms, 4), "GBps_alg": round(alg / (ms / 1e3) / 1e9, 1), "kw": m["kw"],
+        res[m["name"]] = {"ms": round(ms, 4), "GBps_alg": round(alg / (ms / 1e3) / 1e9, 1), "items": n_items,
+                          "kw": m["kw"],
                           "flags": m["flags"], "vgprs": m["vgprs"]}
         print(m["name"], res[m["name"]], flush=True)
         hip.hipModuleUnload(mod)
