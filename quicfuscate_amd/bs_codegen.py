@@ -201,6 +201,23 @@ _ASM = {
     "s_cselect64": lambda d, a, b: f"s_cselect_b64 {SP(d)}, {SP(a)}, {SP(b)}",
     "load16_saddr": lambda d, voff, sb, pol="": f"global_load_dwordx4 {VQ(d)}, {V(voff)}, {SP(sb)}"
                     + (f" {pol}" if pol else ""),
+    # cmb (bit-sliced payload pass with wave-uniform runtime coefficients)
+    "s_load_n": lambda d, base, n, soff, imm: (f"s_load_dword{'' if n == 1 else f'x{n}'} "
+                                              + (f"s{d}" if n == 1 else f"s[{d}:{d + n - 1}]")
+                                              + f", {SP(base)}, " + (f"s{soff}" if soff is not None else f"0x{imm:x}")
+                                              + (f" offset:0x{imm:x}" if soff is not None and imm else "")),
+    "s_sub": lambda d, a, b: f"s_sub_u32 s{d}, s{a}, s{b}",
+    "s_cselect32": lambda d, a, b: f"s_cselect_b32 s{d}, s{a}, s{b}",
+    "v_min_s": lambda d, s_, a: f"v_min_u32_e32 {V(d)}, s{s_}, {V(a)}",
+    "s_idx_on": lambda s_: f"s_set_gpr_idx_on s{s_}, gpr_idx(SRC0)",
+    "s_idx": lambda s_: f"s_set_gpr_idx_idx s{s_}",
+    "s_idx_off": lambda: "s_set_gpr_idx_off",
+    # d = v[base + M0] ^ b: src0 indexed while the gpr_idx mode is on
+    "v_xor_rel": lambda d, base, b: f"v_xor_b32_e32 {V(d)}, {V(base)}, {V(b)}",
+    "store16_saddr": lambda voff, d, sb, pol="": f"global_store_dwordx4 {V(voff)}, {VQ(d)}, {SP(sb)}"
+                     + (f" {pol}" if pol else ""),
+    "store_byte_saddr": lambda voff, d, sb, off: f"global_store_byte {V(voff)}, {V(d)}, {SP(sb)}"
+                        + (f" offset:{off}" if off else ""),
 }
 
 
@@ -359,6 +376,8 @@ class KernelSpec:
 
     @property
     def name(self) -> str:
+        if self.mode == "cmb":
+            return f"qf_combine_bs_r{self.r}"
         tag = {"enc": "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
             tag = "decc"
@@ -404,6 +423,8 @@ class KernelSpec:
 
     @property
     def next_free_vgpr(self) -> int:
+        if self.mode == "cmb":
+            return CMB_NEXT_FREE_VGPR
         n = self.map_b + 4 * self.map_quads
         if self.mode == "dec" and self.chunked:
             n = max(n, lu_layout_chunked(self)["end"])
@@ -416,6 +437,8 @@ class KernelSpec:
 
     @property
     def next_free_sgpr(self) -> int:
+        if self.mode == "cmb":
+            return CMB_NEXT_FREE_SGPR
         if self.mode == "synw":
             return SW_NEXT_FREE
         if self.mode == "dec":
@@ -430,6 +453,8 @@ class KernelSpec:
 
     @property
     def kernarg_bytes(self) -> int:
+        if self.mode == "cmb":
+            return KERNARG_BYTES_CMB
         if self.mode == "synw":
             return KERNARG_BYTES_SYNW
         return KERNARG_BYTES_DEC if self.mode == "dec" else KERNARG_BYTES
@@ -732,6 +757,8 @@ def _epilogue_next_item(E, far: bool = False):
 
 
 def generate(spec: KernelSpec) -> list[Op]:
+    if spec.mode == "cmb":
+        return _generate_cmb(spec)
     if spec.mode == "enc":
         return _generate_enc(spec)
     if spec.mode == "synw":
@@ -1522,6 +1549,276 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
 
 
 # --------------------------------------------------------------------------
+# Bit-sliced payload pass with wave-uniform runtime coefficients ("cmb")
+# --------------------------------------------------------------------------
+# x_E = D s for the decode paths' k_combine_slots records (one 16-byte record
+# of 16 output coefficients per input row and pass), one generation per item:
+# item = (g, t), lanes q = 64 t + l < Q own units q and q + Q of each row
+# (Q = ceil(Lu / 2)), so every coefficient is wave-uniform.  Per input row:
+# 8 bit planes (transpose), their 4-bit combinations LO[0..15] / HI[0..15]
+# (LO[0] = HI[0] = 0), then per output j
+#     acc_j[p] ^= LO[M_c row p & 15];  acc_j[p] ^= HI[M_c row p >> 4]
+# with the register chosen by the scalar unit: s_set_gpr_idx_{on,idx} and a
+# v_xor_b32 whose src0 is M0-indexed, the 16 indices of c read as one
+# s_load_dwordx16 from a 256 x 64-byte table (cmb_index_table).
+# tools/ubench_idx.py: 16 indexed XORs + 17 index writes issue at about half
+# the plain XOR rate, against 24 v_perm + 8 v_bitop3 per product in
+# k_combine_slots.
+#
+# kernarg (128 bytes, s4..s35):
+#   s[4:5] rows  s[6:7] dst  s[8:9] rows gen stride  s[10:11] dst gen stride
+#   s12 row stride  s13 dst row stride  s[14:15] coefficient records
+#   s16 record gen stride  s17 pass  s[18:19] n_out  s[20:21] bound
+#   s[22:23] index table  s[24:25] rows offset table  s[26:27] dst offset table
+#   s28 L  s29 Lu  s30 Q  s31 items per generation  s32 items  s33 grid waves
+#   s34 / s35 magic / shift of the division by s31
+KERNARG_BYTES_CMB = 128
+CMB_NEXT_FREE_VGPR = 192
+CMB_NEXT_FREE_SGPR = 102
+C_OA, C_OB = 2, 3                 # lane byte offsets of units A / B in a row
+C_BUF = (4, 12)                   # two 8-dword row buffers (A: +0..3, B: +4..7)
+C_T = 20                          # v20..v23 transpose temps
+C_LO, C_HI = 24, 40               # LO[0..15], HI[0..15]
+C_ACC = 56                        # 16 x 8 accumulators v56..v183
+C_QV, C_QC, C_UB, C_UBC, C_TB = 184, 185, 186, 187, 188
+# SGPRs
+CS_ITEM, CS_G, CS_T, CS_EW, CS_BOUND, CS_SLOT = 36, 37, 38, 39, 40, 41
+CS_ROWG, CS_CUR, CS_NEXT, CS_COEFG, CS_DSTG = 42, 44, 46, 48, 50
+CS_REC = 52                       # s52..s55 (4-aligned for s_load_dwordx4)
+CS_IDX = (56, 72)                 # two 16-SGPR index buffers (4-aligned)
+CS_VALID, CS_FULLB, CS_TAIL, CS_TMP64 = 88, 90, 92, 94
+CS_MASKS = 96                     # s96..s98 transpose masks
+CS_T0, CS_T1, CS_TBYTES = 99, 100, 3
+
+
+def cmb_index_table() -> np.ndarray:
+    """256 x 16 dwords: for coefficient c and output plane p, dword 2p = the
+    LO index (row p of M_c, input planes 0-3) and 2p + 1 = the HI index."""
+    t = np.zeros((256, 16), np.uint32)
+    for c in range(256):
+        rows = mul_matrix_rows(c)
+        for p in range(8):
+            t[c, 2 * p], t[c, 2 * p + 1] = rows[p] & 15, rows[p] >> 4
+    return t
+
+
+def _cmb_transpose(E, base: int, last_dst: Optional[list] = None):
+    """bfi delta-swap network on 8 registers (plane p <- bit p of every byte);
+    the last stage writes plane p to last_dst[p] (default: in place)."""
+    for stage, (sh, _mask, pairs) in enumerate(_TRANSPOSE):
+        sm = CS_MASKS + stage
+        for q, (a, b) in enumerate(pairs):
+            t, u = C_T + 2 * (q & 1), C_T + 2 * (q & 1) + 1
+            da, db = base + a, base + b
+            if stage == 2 and last_dst is not None:
+                da, db = last_dst[a], last_dst[b]
+            E(Op("v_lshl", (t, sh, base + b)))
+            E(Op("v_lshr", (u, sh, base + a)))
+            E(Op("v_bitsel_s", (da, sm, base + a, t)))
+            E(Op("v_bitsel_s", (db, sm, u, base + b)))
+
+
+def _cmb_gen_addr(E, dst: int, base: int, gs: int, offs: int, tag: str):
+    """s[dst:dst+1] <- base + g * gen_stride (64-bit stride s[gs:gs+1]), or
+    base + offs[g] when the offset table pointer is non-zero."""
+    E(Op("s_cmp_eq64_0_br", (offs, f".Lcs{tag}")))
+    E(Op("s_lshl", (CS_T0, CS_G, 3)))
+    E(Op("s_load_n", (CS_TMP64, offs, 2, CS_T0, 0)))
+    E(Op("s_waitcnt_lgkm", ()))
+    E(Op("s_branch", (f".Lca{tag}",)))
+    E(Op("label", (f".Lcs{tag}",)))
+    E(Op("s_mul", (CS_TMP64, CS_G, gs)))            # lo(g * gs_lo)
+    E(Op("s_mul_hi", (CS_TMP64 + 1, CS_G, gs)))     # hi(g * gs_lo)
+    E(Op("s_mul", (CS_T0, CS_G, gs + 1)))
+    E(Op("s_add", (CS_TMP64 + 1, CS_TMP64 + 1, CS_T0)))
+    E(Op("label", (f".Lca{tag}",)))
+    E(Op("s_add_cc", (dst, base, CS_TMP64)))
+    E(Op("s_addc", (dst + 1, base + 1, CS_TMP64 + 1)))
+
+
+def _cmb_row(E, spec, buf: int, other: int, tag: str):
+    """One input row (slot CS_SLOT, data in `buf`): prefetch the next row into
+    `other`, bit-slice, combinations, then the ew products."""
+    E(Op("s_lshl", (CS_T0, CS_SLOT, 4)))
+    E(Op("s_load_n", (CS_REC, CS_COEFG, 4, CS_T0, 0)))
+    E(Op("s_addk", (CS_T0, CS_SLOT, 1)))
+    E(Op("s_cmp_ge_br", (CS_T0, CS_BOUND, f".Lnopf{tag}")))
+    E(Op("s_add_cc", (CS_NEXT, CS_CUR, 12)))
+    E(Op("s_addck", (CS_NEXT + 1, CS_CUR + 1, 0)))
+    E(Op("load16_saddr", (other, C_OA, CS_NEXT, spec.ld_policy)))
+    E(Op("load16_saddr", (other + 4, C_OB, CS_NEXT, spec.ld_policy)))
+    E(Op("s_waitcnt_vm", (2,)))
+    E(Op("s_branch", (f".Lrow{tag}",)))
+    E(Op("label", (f".Lnopf{tag}",)))
+    E(Op("s_waitcnt_vm", (0,)))
+    E(Op("label", (f".Lrow{tag}",)))
+    singles = [C_LO + 1, C_LO + 2, C_LO + 4, C_LO + 8, C_HI + 1, C_HI + 2, C_HI + 4, C_HI + 8]
+    _cmb_transpose(E, buf, singles)
+    for tab in (C_LO, C_HI):
+        for m in sorted(_COMBO_BUILD):
+            a, b = _COMBO_BUILD[m]
+            E(Op("v_xor", (tab + m, tab + a, tab + b)))
+    E(Op("s_waitcnt_lgkm", ()))
+    # index rows of output 0's coefficient
+    E(Op("s_bfe_k", (CS_T0, CS_REC, 0, 8)))
+    E(Op("s_lshl", (CS_T0, CS_T0, 6)))
+    E(Op("s_load_n", (CS_IDX[0], 22, 16, CS_T0, 0)))
+    for j in range(spec.r):
+        if j:
+            E(Op("s_cmp_le_k_br", (CS_EW, j, f".Lpe{tag}")))
+        E(Op("s_waitcnt_lgkm", ()))
+        if j + 1 < spec.r:   # the next output's indices load during this product
+            E(Op("s_bfe_k", (CS_T0, CS_REC + (j + 1) // 4, 8 * ((j + 1) % 4), 8)))
+            E(Op("s_lshl", (CS_T0, CS_T0, 6)))
+            E(Op("s_load_n", (CS_IDX[(j + 1) % 2], 22, 16, CS_T0, 0)))
+        ix = CS_IDX[j % 2]
+        for p in range(8):
+            acc = C_ACC + 8 * j + p
+            E(Op("s_idx_on" if p == 0 else "s_idx", (ix + 2 * p,)))
+            E(Op("v_xor_rel", (acc, C_LO, acc)))
+            E(Op("s_idx", (ix + 2 * p + 1,)))
+            E(Op("v_xor_rel", (acc, C_HI, acc)))
+        E(Op("s_idx_off", ()))
+    E(Op("label", (f".Lpe{tag}",)))
+    E(Op("s_waitcnt_lgkm", ()))
+
+
+def _generate_cmb(spec: KernelSpec) -> list[Op]:
+    ops: list[Op] = []
+    E = ops.append
+    R = spec.r
+    assert R <= 16 and C_ACC + 8 * R <= C_QV
+    E(Op("s_load_n", (4, 0, 16, None, 0)))
+    E(Op("s_load_n", (20, 0, 16, None, 64)))
+    E(Op("v_lshr", (1, 6, 0)))
+    E(Op("v_andk", (0, 63, 0)))
+    E(Op("v_readfirstlane", (CS_T0, 1)))
+    for q, (_, mask, _) in enumerate(_TRANSPOSE):
+        E(Op("s_movk", (CS_MASKS + q, mask)))
+    E(Op("v_movk", (C_LO, 0)))
+    E(Op("v_movk", (C_HI, 0)))
+    E(Op("s_waitcnt_lgkm", ()))
+    E(Op("s_lshl", (CS_ITEM, 2, 2)))
+    E(Op("s_add", (CS_ITEM, CS_ITEM, CS_T0)))
+    E(Op("s_andk", (CS_TBYTES, 28, 15)))            # L % 16: bytes of a partial last unit
+    E(Op("label", (".Litem",)))
+    E(Op("s_cmp_lt_br", (CS_ITEM, 32, ".Lgo")))
+    E(Op("s_branch", (".Lend",)))
+    E(Op("label", (".Lgo",)))
+    # g = item / ipg (ipg == 1: g = item), t = item - g ipg
+    E(Op("s_mul_hi", (CS_G, CS_ITEM, 34)))
+    E(Op("s_lshr_s", (CS_G, CS_G, 35)))
+    E(Op("s_cmp_eq_k", (31, 1)))
+    E(Op("s_cselect32", (CS_G, CS_ITEM, CS_G)))
+    E(Op("s_mul", (CS_T0, CS_G, 31)))
+    E(Op("s_sub", (CS_T, CS_ITEM, CS_T0)))
+    E(Op("s_lshl", (CS_T0, CS_G, 2)))
+    E(Op("s_load_n", (CS_T1, 18, 1, CS_T0, 0)))      # e = n_out[g]
+    E(Op("s_load_n", (CS_BOUND, 20, 1, CS_T0, 0)))   # bound[g]
+    E(Op("s_waitcnt_lgkm", ()))
+    # outputs of this pass: ew = min(e - 16 pass, R); none -> next item
+    E(Op("s_lshl", (CS_T0, 17, 4)))
+    E(Op("s_cmp_ge_br", (CS_T0, CS_T1, ".Lnext")))
+    E(Op("s_sub", (CS_EW, CS_T1, CS_T0)))
+    E(Op("s_movk", (CS_T0, R)))
+    E(Op("s_min", (CS_EW, CS_EW, CS_T0)))
+    _cmb_gen_addr(E, CS_ROWG, 4, 8, 24, "r")
+    _cmb_gen_addr(E, CS_DSTG, 6, 10, 26, "d")
+    E(Op("s_mul", (CS_TMP64, CS_G, 16)))
+    E(Op("s_mul_hi", (CS_TMP64 + 1, CS_G, 16)))
+    E(Op("s_add_cc", (CS_COEFG, 14, CS_TMP64)))
+    E(Op("s_addc", (CS_COEFG + 1, 15, CS_TMP64 + 1)))
+    # lanes: qv = 64 t + l; valid = qv < Q; qc = min(qv, Q - 1); ub = qc + Q
+    E(Op("v_lshl_add_s", (C_QV, CS_T, 6, 0)))
+    E(Op("v_cmp_gt_s", (CS_VALID, 30, C_QV)))
+    E(Op("s_addk", (CS_T0, 30, -1)))
+    E(Op("v_min_s", (C_QC, CS_T0, C_QV)))
+    E(Op("v_add_s", (C_UB, 30, C_QC)))
+    E(Op("v_cmp_gt_s", (CS_FULLB, 29, C_UB)))        # ub < Lu
+    E(Op("s_addk", (CS_T0, 29, -1)))
+    E(Op("v_min_s", (C_UBC, CS_T0, C_UB)))
+    E(Op("v_cmp_eq_s", (CS_TAIL, CS_T0, C_UB)))      # ub == Lu - 1
+    E(Op("s_nop", (4,)))
+    E(Op("s_and64", (CS_FULLB, CS_FULLB, CS_VALID)))
+    E(Op("s_and64", (CS_TAIL, CS_TAIL, CS_FULLB)))
+    E(Op("s_movk", (CS_TMP64, 0)))
+    E(Op("s_movk", (CS_TMP64 + 1, 0)))
+    E(Op("s_cmp_eq_k", (CS_TBYTES, 0)))
+    E(Op("s_cselect64", (CS_TAIL, CS_TMP64, CS_TAIL)))   # whole last unit: no tail lane
+    E(Op("s_andn2_64", (CS_FULLB, CS_FULLB, CS_TAIL)))
+    E(Op("v_lshl", (C_OA, 4, C_QC)))
+    E(Op("v_lshl", (C_OB, 4, C_UBC)))
+    for a in range(C_ACC, C_ACC + 8 * R):
+        E(Op("v_movk", (a, 0)))
+    # input rows, two per loop trip (ring of two row buffers)
+    E(Op("s_movk", (CS_SLOT, 0)))
+    E(Op("s_mov", (CS_CUR, CS_ROWG)))
+    E(Op("s_mov", (CS_CUR + 1, CS_ROWG + 1)))
+    E(Op("s_cmp_le_k_br", (CS_BOUND, 0, ".Lstores")))
+    E(Op("load16_saddr", (C_BUF[0], C_OA, CS_CUR, spec.ld_policy)))
+    E(Op("load16_saddr", (C_BUF[0] + 4, C_OB, CS_CUR, spec.ld_policy)))
+    E(Op("label", (".Lslot",)))
+    for h in range(2):
+        _cmb_row(E, spec, C_BUF[h], C_BUF[1 - h], f"{h}")
+        E(Op("s_addk", (CS_SLOT, CS_SLOT, 1)))
+        E(Op("s_cmp_ge_br", (CS_SLOT, CS_BOUND, ".Lstores")))
+        E(Op("s_mov", (CS_CUR, CS_NEXT)))
+        E(Op("s_mov", (CS_CUR + 1, CS_NEXT + 1)))
+    E(Op("s_branch", (".Lslot",)))
+    # recovered rows: bytes back (inverse transpose), unit A on valid lanes,
+    # unit B where it is a whole unit, and the partial last unit bytewise
+    E(Op("label", (".Lstores",)))
+    for j in range(R):
+        acc = C_ACC + 8 * j
+        E(Op("s_cmp_le_k_br", (CS_EW, j, ".Lst_end")))
+        _cmb_transpose(E, acc)
+        E(Op("s_movk", (CS_T0, j)))
+        E(Op("s_mul", (CS_T0, CS_T0, 13)))
+        E(Op("s_add_cc", (CS_TMP64, CS_DSTG, CS_T0)))
+        E(Op("s_addck", (CS_TMP64 + 1, CS_DSTG + 1, 0)))
+        E(Op("s_exec", (CS_VALID,)))
+        E(Op("store16_saddr", (C_OA, acc, CS_TMP64, spec.st_policy)))
+        E(Op("s_exec", (CS_FULLB,)))
+        E(Op("store16_saddr", (C_OB, acc + 4, CS_TMP64, spec.st_policy)))
+        E(Op("s_exec", (CS_TAIL,)))
+        E(Op("s_cbranch_execz", (f".Ltl{j}",)))
+        for b in range(15):
+            E(Op("s_cmp_le_k_br", (CS_TBYTES, b, f".Ltl{j}")))
+            E(Op("v_lshr", (C_TB, 8 * (b % 4), acc + 4 + b // 4)))
+            E(Op("store_byte_saddr", (C_OB, C_TB, CS_TMP64, b)))
+            E(Op("s_nop", (0,)))
+        E(Op("label", (f".Ltl{j}",)))
+        E(Op("s_exec", (None,)))
+        E(Op("s_nop", (1,)))   # store data registers are not rewritten right after the store
+    E(Op("label", (".Lst_end",)))
+    E(Op("label", (".Lnext",)))
+    E(Op("s_nop", (4,)))
+    E(Op("s_add", (CS_ITEM, CS_ITEM, 33)))
+    E(Op("s_branch", (".Litem",)))
+    E(Op("label", (".Lend",)))
+    E(Op("s_endpgm", ()))
+    return ops
+
+
+def cmb_kernargs(rows: int, dst: int, rgs: int, dgs: int, rs: int, drs: int, coef: int, cgs: int, pas: int,
+                 n_out: int, bound: int, idxtab: int, L: int, G: int, total_waves: int,
+                 rows_offs: int = 0, dst_offs: int = 0) -> tuple[bytes, int]:
+    """Kernarg block of qf_combine_bs (layout above) and the item count."""
+    Lu = (L + 15) // 16
+    Q = (Lu + 1) // 2
+    ipg = (Q + 63) // 64
+    magic, shift = magic_for(ipg) if ipg >= 2 else (0, 0)
+    n_items = G * ipg
+    words = [rows & MASK32, rows >> 32, dst & MASK32, dst >> 32, rgs & MASK32, rgs >> 32, dgs & MASK32, dgs >> 32,
+             rs, drs, coef & MASK32, coef >> 32, cgs, pas, n_out & MASK32, n_out >> 32, bound & MASK32,
+             bound >> 32, idxtab & MASK32, idxtab >> 32, rows_offs & MASK32, rows_offs >> 32,
+             dst_offs & MASK32, dst_offs >> 32, L, Lu, Q, ipg, n_items, total_waves, magic, shift]
+    for w in words:
+        assert 0 <= w < 1 << 32, words
+    return np.array(words, np.uint32).tobytes(), n_items
+
+
+# --------------------------------------------------------------------------
 # Assembly text
 # --------------------------------------------------------------------------
 def emit_asm(spec: KernelSpec, ops: list[Op]) -> str:
@@ -1835,11 +2132,24 @@ class Emulator:
         ops = self.ops
         scc = 0
         steps = 0
+        pend_s = []        # s_load_n: (first SGPR, values) written at the next lgkmcnt(0)
+        idx_mode, m0 = False, 0
+
+        def retire_s():
+            for d0, w in pend_s:
+                for q, x in enumerate(w):
+                    s[d0 + q] = int(x)
+            pend_s.clear()
+
         while True:
             op = ops[pc]
             pc += 1
             steps += 1
             n, a = op.name, op.args
+            if idx_mode and n.startswith("v_") and n != "v_xor_rel":
+                raise EmuError(f"{n} while the gpr_idx mode is on")
+            if n == "s_waitcnt_lgkm" or (n == "s_waitcnt_lgkm_n" and a[0] == 0):
+                retire_s()
             if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger"):
                 continue
             if n == "s_load_args":
@@ -2094,6 +2404,42 @@ class Emulator:
             elif n == "s_cmp_lt_br":
                 if s[a[0]] < s[a[1]]:
                     pc = self.labels[a[2]]
+            elif n == "s_load_n":
+                d, base, nd, soff, imm = a
+                if base == 0:   # s[0:1]: the kernarg segment
+                    pend_s.append((d, ka[imm // 4: imm // 4 + nd].copy()))
+                    continue
+                addr = (s[base] | (s[base + 1] << 32)) + (s[soff] if soff is not None else 0) + imm
+                if addr % 4:
+                    raise EmuError("unaligned scalar load")
+                pend_s.append((d, np.frombuffer(self.read(addr, 4 * nd), np.uint32).copy()))
+            elif n == "s_sub":
+                t = s[a[1]] - s[a[2]]
+                s[a[0]], scc = t & MASK32, int(t < 0)
+            elif n == "s_cselect32":
+                s[a[0]] = s[a[1]] if scc else s[a[2]]
+            elif n == "v_min_s":
+                wv(a[0], np.minimum(rv(a[2]), np.uint64(s[a[1]])))
+            elif n in ("s_idx_on", "s_idx"):
+                if n == "s_idx" and not idx_mode:
+                    raise EmuError("s_set_gpr_idx_idx outside the gpr_idx mode")
+                idx_mode, m0 = True, s[a[0]] & 0xFF
+            elif n == "s_idx_off":
+                idx_mode = False
+            elif n == "v_xor_rel":
+                if not idx_mode:
+                    raise EmuError("v_xor_rel outside the gpr_idx mode")
+                wv(a[0], rv(a[1] + m0) ^ rv(a[2]))
+            elif n in ("store16_saddr", "store_byte_saddr"):
+                voff, d, sb = a[:3]
+                base = s[sb] | (s[sb + 1] << 32)
+                off = rv(voff)
+                for l in np.nonzero(exec_)[0]:
+                    if n == "store16_saddr":
+                        self.write(base + int(off[l]),
+                                   np.array([rv(d + q)[l] for q in range(4)], np.uint32).tobytes())
+                    else:
+                        self.write(base + int(off[l]) + a[3], bytes([int(rv(d)[l]) & 0xFF]))
             elif n == "s_endpgm":
                 if pending:
                     # stores/loads may be outstanding at the end: retire them

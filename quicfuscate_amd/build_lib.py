@@ -141,13 +141,15 @@ def _bs_kernels(build_dir: Path) -> Path:
             rp = (rt - j0) // (npass - p)
             specs.append(bs.KernelSpec(k, rp, BS_PD, "synw", r_total=rt, j0=j0))
             j0 += rp
+    # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
         data = hsaco.read_bytes()
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
-        mode = "c" if spec.chunked else {"enc": "e", "syn": "s", "dec": "d", "synw": "w"}[spec.mode]
+        mode = "c" if spec.chunked else {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {BS_PD}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
     inc = build_dir / "qf_bs_blobs.inc"

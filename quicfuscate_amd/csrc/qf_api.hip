@@ -52,6 +52,7 @@ struct qf_ctx {
     int num_cus = 256;
     uint32_t* d_tab256 = nullptr;  // 256 split-table records (8 dwords each)
     uint8_t* d_explog = nullptr;   // exp[512] | log[256]
+    uint32_t* d_cmbidx = nullptr;  // qf_combine_bs plane-index table (256 x 16 dwords)
     // Cauchy split tables, keyed by (k, r, pass, k_pad)
     std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, EncTab> cauchy;
     // custom coefficient tables: pinned host staging + device buffer
@@ -490,6 +491,34 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     return QF_OK;
 }
 
+// Decode payload pass x_E = D s over one pass's coefficient records: the
+// bit-sliced qf_combine_bs (wave-uniform coefficients, one generation per
+// item) for rows of at least QF_COMBINE_BS_MIN_Q (default 64) lane-chunks of
+// 32 bytes, else k_combine_slots; QF_COMBINE_BS=0 keeps k_combine_slots.  The
+// bit-sliced kernel reads whole 16-byte units, so with L % 16 != 0 its rows
+// must start 16-byte aligned (strided, aligned base and strides).
+static bool combine_bs_ok(const qf::CombineSlotsArgs& a) {
+    const char* on = getenv("QF_COMBINE_BS");
+    if ((on && !atoi(on)) || !qf::cmb_available()) return false;
+    const char* mq = getenv("QF_COMBINE_BS_MIN_Q");
+    const uint32_t min_q = mq ? (uint32_t)atoi(mq) : 64u;
+    // (Lu >= 2: the partial last unit is then always some lane's unit B)
+    if (a.Lu < 2 || (a.Lu + 1) / 2 < min_q) return false;
+    if (a.L % 16 && (a.rows_offs || ((uintptr_t)a.rows | a.row_stride | a.rows_gen_stride) % 16)) return false;
+    return true;
+}
+
+static hipError_t combine_payload(qf_ctx* ctx, const qf::CombineSlotsArgs& a, int PD, hipStream_t st,
+                                  std::string* name) {
+    if (combine_bs_ok(a)) {
+        if (name) *name = "qf_combine_bs_r16";
+        return qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx);
+    }
+    if (name) *name = "k_combine_slots<" + std::to_string(PD) + ">";
+    return qf::launch_combine_slots(a, PD, ctx->num_cus, st);
+}
+
+
 // Decode of Cauchy codes with more repairs than a syndrome kernel holds
 // (r <= 64, e <= 64) when the encode kernels of (k, r) exist:
 //   k_decode_prepare_cauchy  acceptance, slot map, D = C[J,E]^-1 (closed form)
@@ -603,8 +632,9 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
             a.zero_slot = r;
             a.total_units = (uint64_t)Gc * Lu;
             ev = prof_begin(ctx, st);
-            QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, st));
-            prof_end(ctx, st, ev, "k_combine_slots<" + std::to_string(PD) + ">");
+            std::string cname;
+            QF_CHECK_HIP(combine_payload(ctx, a, PD, st, &cname));
+            prof_end(ctx, st, ev, cname);
         }
     }
     return QF_OK;
@@ -681,7 +711,6 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
     if (int gs = payload_gate(ctx, st)) return gs;
     const int PD = pick_PD("QF_DECODE_PD", 1, 1);
-    const std::string slots_name = "k_combine_slots<" + std::to_string(PD) + ">";
     for (uint64_t c = 0; c < n_chunks; ++c) {
         const uint64_t g0 = c * chunk;
         const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
@@ -717,8 +746,9 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
         a.zero_slot = r;
         a.total_units = (uint64_t)Gc * a.Lu;
         ev = prof_begin(ctx, sb);
-        QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, sb));
-        prof_end(ctx, sb, ev, slots_name);
+        std::string cname;
+        QF_CHECK_HIP(combine_payload(ctx, a, PD, sb, &cname));
+        prof_end(ctx, sb, ev, cname);
         if (overlap) QF_CHECK_HIP(hipEventRecord(evB, sb));
     }
     if (overlap) {
@@ -961,8 +991,24 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
     std::vector<uint8_t> el(768);
     memcpy(el.data(), gf().exp, 512);
     memcpy(el.data() + 512, gf().log, 256);
+    // plane indices of the bit-sliced payload pass (bs_codegen.cmb_index_table):
+    // dword 2p / 2p + 1 of record c = low / high nibble of row p of M_c
+    std::vector<uint32_t> cidx(256 * 16);
+    for (int v = 0; v < 256; ++v) {
+        uint8_t rows[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int a = 0; a < 8; ++a) {
+            const uint8_t col = gf().mul((uint8_t)v, (uint8_t)(1u << a));
+            for (int b = 0; b < 8; ++b) rows[b] |= (uint8_t)(((col >> b) & 1u) << a);
+        }
+        for (int p = 0; p < 8; ++p) {
+            cidx[v * 16 + 2 * p] = rows[p] & 15u;
+            cidx[v * 16 + 2 * p + 1] = rows[p] >> 4;
+        }
+    }
     bool ok = hipMalloc(&c->d_tab256, tab.size() * 4) == hipSuccess &&
               hipMalloc(&c->d_explog, 768) == hipSuccess &&
+              hipMalloc(&c->d_cmbidx, cidx.size() * 4) == hipSuccess &&
+              hipMemcpy(c->d_cmbidx, cidx.data(), cidx.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(c->d_tab256, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(c->d_explog, el.data(), 768, hipMemcpyHostToDevice) == hipSuccess &&
               hipEventCreateWithFlags(&c->custom_done, hipEventDisableTiming) == hipSuccess;
@@ -982,6 +1028,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     for (auto& kv : c->small_coef) hipFree(kv.second);
     if (c->d_tab256) hipFree(c->d_tab256);
     if (c->d_explog) hipFree(c->d_explog);
+    if (c->d_cmbidx) hipFree(c->d_cmbidx);
     if (c->h_custom) hipHostFree(c->h_custom);
     if (c->d_custom) hipFree(c->d_custom);
     if (c->custom_done) hipEventDestroy(c->custom_done);
@@ -1374,8 +1421,9 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         a.total_units = (uint64_t)G * Lu;
         const int PD = pick_PD("QF_DECODE_PD", 1, 1);
         hipEvent_t ev2 = prof_begin(ctx, ctx->stream);
-        QF_CHECK_HIP(qf::launch_combine_slots(a, PD, ctx->num_cus, ctx->stream));
-        prof_end(ctx, ctx->stream, ev2, "k_combine_slots<" + std::to_string(PD) + ">");
+        std::string cname;
+        QF_CHECK_HIP(combine_payload(ctx, a, PD, ctx->stream, &cname));
+        prof_end(ctx, ctx->stream, ev2, cname);
     }
     return QF_OK;
 }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "qf_kernels.h"
+
 namespace qf {
 
 struct BsCache {
@@ -61,6 +63,15 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
                       const uint64_t* rows_offs = nullptr, const uint64_t* rec_offs = nullptr);
+// Decode payload pass x_E = D s (the k_combine_slots records of one pass)
+// bit-sliced with wave-uniform coefficients (bs_codegen.py "cmb"): one
+// generation per item, units q and q + Q of a row per lane.  idxtab: the
+// 256 x 64-byte plane-index table (bs_codegen.cmb_index_table).  Rows are
+// read in whole 16-byte units (the unit holding byte L - 1 too); only bytes
+// [0, L) of the output rows are written.
+bool cmb_available();
+hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
+                      const uint32_t* idxtab);
 void bs_unload(BsCache& cache);
 
 }  // namespace qf

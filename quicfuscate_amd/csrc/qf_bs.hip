@@ -260,6 +260,49 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                   lu, lu_stride, tab256, rows_offs, rec_offs);
 }
 
+// Bit-sliced payload pass (bs_codegen.py "cmb", mode 'm'): one generation
+// per item, wave-uniform coefficients (kernarg layout: bs_codegen.cmb_kernargs)
+bool cmb_available() { return find('m', 0, 16) != nullptr; }
+
+hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
+                      const uint32_t* idxtab) {
+    const QfBsEntry* e = find('m', 0, 16);
+    if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || a.dst_row_stride >= (1ull << 32) ||
+        a.coef_gen_stride >= (1ull << 32))
+        return hipErrorInvalidValue;
+    const int idx = (int)(e - qf_bs_table);
+    if (idx >= BsCache::kMax) return hipErrorInvalidValue;
+    if (!cache.fn[idx]) {
+        hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
+        if (err != hipSuccess) return err;
+        err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
+        if (err != hipSuccess) return err;
+    }
+    const uint32_t Lu = (a.L + 15) / 16, Q = (Lu + 1) / 2, ipg = (Q + 63) / 64;
+    const uint64_t G = a.total_units / Lu;
+    const uint64_t n_items = G * ipg;
+    if (n_items == 0) return hipSuccess;
+    if (n_items >= (1ull << 31)) return hipErrorInvalidValue;
+    uint32_t magic = 0, shift = 0;
+    if (ipg >= 2) magic_for(ipg, &magic, &shift);
+    // persistent grid: two 4-wave blocks per CU (192 VGPRs: two waves per SIMD)
+    uint64_t blocks = (n_items + 3) / 4;
+    const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * 2;
+    if (blocks > cap) blocks = cap;
+    auto lo = [](const void* p) { return (uint32_t)(uintptr_t)p; };
+    auto hi = [](const void* p) { return (uint32_t)((uintptr_t)p >> 32); };
+    uint32_t w[32] = {lo(a.rows), hi(a.rows), lo(a.dst), hi(a.dst),
+                      (uint32_t)a.rows_gen_stride, (uint32_t)(a.rows_gen_stride >> 32),
+                      (uint32_t)a.dst_gen_stride, (uint32_t)(a.dst_gen_stride >> 32),
+                      (uint32_t)a.row_stride, (uint32_t)a.dst_row_stride, lo(a.coef), hi(a.coef),
+                      (uint32_t)a.coef_gen_stride, a.pass, lo(a.n_out), hi(a.n_out), lo(a.bound), hi(a.bound),
+                      lo(idxtab), hi(idxtab), lo(a.rows_offs), hi(a.rows_offs), lo(a.dst_offs), hi(a.dst_offs),
+                      a.L, Lu, Q, ipg, (uint32_t)n_items, (uint32_t)blocks * 4, magic, shift};
+    size_t sz = sizeof(w);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, w, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+}
+
 void bs_unload(BsCache& cache) {
     for (int i = 0; i < BsCache::kMax; ++i)
         if (cache.mod[i]) {

@@ -706,3 +706,82 @@ def test_shift64_kernels_match_default(oracle, mode):
             emu.run_wave(ka, w // 4, w % 4)
         outs.append((src, dst.copy()))
     assert (outs[0][1] == outs[1][1]).all() and outs[0][1].any()
+
+
+def _gf_table():
+    t = np.zeros((256, 256), np.uint8)
+    for a in range(256):
+        for b in range(256):
+            t[a, b] = bs.gf_mul(a, b)
+    return t
+
+
+_GFT = None
+
+
+def _cmb_case(L, G, seed, pas=0, offs=False, R=16):
+    """qf_combine_bs on the emulator: out[j] = sum_{s < bound[g]} rec[g][s][j] *
+    rows[g][s] for j < min(e[g] - 16 pass, R), bytes [0, L) only."""
+    global _GFT
+    if _GFT is None:
+        _GFT = _gf_table()
+    rng = np.random.default_rng(seed)
+    spec = bs.KernelSpec(0, R, mode="cmb")
+    Lp = (L + 15) // 16 * 16
+    rs, drs = Lp + 32, Lp + 48
+    nslot = 24
+    rgs, dgs = nslot * rs + 16, 16 * drs + 32
+    cgs = (nslot + 1) * 16
+    rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
+    rec = rng.integers(0, 256, G * cgs, dtype=np.uint8)
+    e = rng.integers(16 * pas + 1, 16 * pas + R + 4, G).astype(np.uint32)
+    bound = rng.integers(1, nslot + 1, G).astype(np.uint32)
+    if G > 3:   # a generation without outputs in this pass, one without input rows
+        e[1], bound[2] = 16 * pas, 0
+    out = np.full(G * dgs, 0xEE, np.uint8)
+    ROWS, OUT, REC, NO, BD, TAB, T1, T2 = (0x10000000, 0x40000000, 0x50000000, 0x60000000, 0x61000000,
+                                           0x62000000, 0x63000000, 0x64000000)
+    emu = bs.Emulator(bs.generate(spec))
+    so = do = 0
+    rgs_k, dgs_k = rgs, dgs
+    if offs:   # generations at reversed block positions through offset tables
+        emu.add_buffer(T1, np.array([(G - 1 - g) * rgs for g in range(G)], np.uint64).view(np.uint8))
+        emu.add_buffer(T2, np.array([(G - 1 - g) * dgs for g in range(G)], np.uint64).view(np.uint8))
+        so, do, rgs_k, dgs_k = T1, T2, 0, 0
+    for base, buf in ((ROWS, rows), (OUT, out), (REC, rec), (NO, e), (BD, bound),
+                      (TAB, bs.cmb_index_table().reshape(-1).view(np.uint8))):
+        emu.add_buffer(base, buf.view(np.uint8))
+    waves = 8
+    ka, n_items = bs.cmb_kernargs(ROWS, OUT, rgs_k, dgs_k, rs, drs, REC, cgs, pas, NO, BD, TAB, L, G, waves,
+                                  rows_offs=so, dst_offs=do)
+    for w in range(waves):
+        emu.run_wave(ka, w // 4, w % 4)
+    bad = 0
+    for g in range(G):
+        gr = (G - 1 - g) if offs else g
+        ew = int(min(max(int(e[g]) - 16 * pas, 0), R))
+        blk = out[gr * dgs:(gr + 1) * dgs]
+        for j in range(16):
+            row = blk[j * drs:(j + 1) * drs]
+            if j < ew:
+                want = np.zeros(L, np.uint8)
+                for sl in range(int(bound[g])):
+                    c = rec[g * cgs + 16 * sl + j]
+                    x = rows[gr * rgs + sl * rs: gr * rgs + sl * rs + L]
+                    want ^= _GFT[c][x]
+                bad += int(not (row[:L] == want).all())
+                assert (row[L:] == 0xEE).all(), (g, j, "bytes past L written")
+            else:
+                assert (row == 0xEE).all(), (g, j, "row past ew written")
+    return bad
+
+
+@pytest.mark.parametrize("L,G,seed,pas,offs", [
+    (64, 5, 1, 0, False),       # Lu = 4, Q = 2: one item per generation
+    (100, 4, 2, 0, False),      # partial last unit (4 bytes)
+    (1200, 2, 3, 1, True),      # second pass (outputs 16..), offset tables
+    (4100, 2, 4, 0, False),     # Q = 129: three items per generation, tail of 4 bytes
+    (33, 3, 5, 0, True),        # Lu = 3: unit B of lane 0 is the partial last unit
+])
+def test_emulated_combine_bs(L, G, seed, pas, offs):
+    assert _cmb_case(L, G, seed, pas, offs) == 0

@@ -97,10 +97,17 @@ def check(oracle, k, L, src, gens, out, with_coeffs):
             assert (rec[g * rec_gs + m * rrs + L: g * rec_gs + (m + 1) * rrs] == 0x5A).all()
 
 
-PATHS = ["default", "syn", "general"]
+PATHS = ["default", "syn", "general", "syn_bs", "general_bs"]
 
 
 def _path(monkeypatch, path):
+    # "*_bs": the payload pass takes the bit-sliced k_combine_bs at every row
+    # length (by default only rows of >= 128 lane-chunks of 32 B do)
+    if path.endswith("_bs"):
+        monkeypatch.setenv("QF_COMBINE_BS_MIN_Q", "1")
+        path = path[:-3]
+    else:
+        monkeypatch.delenv("QF_COMBINE_BS_MIN_Q", raising=False)
     # "default": fused decode (syndromes + LU solve in one kernel) where a
     # bit-sliced kernel exists for (k, r) (Cauchy code, L % 16 == 0);
     # "syn": syndrome kernel + v_perm combine (two kernels);

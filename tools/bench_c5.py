@@ -135,14 +135,22 @@ def main():
     ap.add_argument("--exact-rows", action="store_true",
                     help="dense repair rows without the zero tail (general v_perm encode kernel)")
     ap.add_argument("--mixed-only", action="store_true", help="only the heterogeneous (desc API) batch")
+    ap.add_argument("--shapes", default="", help="k,r[;k,r...]: only these block/sliding shapes, no mixed batch")
+    ap.add_argument("--modes", default="block,sliding")
     a = ap.parse_args()
     ctx = qf.default_context()
-    res = {"mixed_desc_batch": mixed_leg(qf, ctx, a.bytes, a.reps)}
-    print("mixed", {k: v for k, v in res["mixed_desc_batch"].items() if k in ("G", "round_trip_ok")},
-          res["mixed_desc_batch"]["encode"]["GiBps_alg"], res["mixed_desc_batch"]["decode"]["GiBps_alg"], flush=True)
-    for k, r in ([] if a.mixed_only else SHAPES):
+    res = {}
+    shapes = SHAPES
+    if a.shapes:
+        shapes = [tuple(int(x) for x in s.split(",")) for s in a.shapes.split(";")]
+    else:
+        res["mixed_desc_batch"] = mixed_leg(qf, ctx, a.bytes, a.reps)
+        print("mixed", {k: v for k, v in res["mixed_desc_batch"].items() if k in ("G", "round_trip_ok")},
+              res["mixed_desc_batch"]["encode"]["GiBps_alg"], res["mixed_desc_batch"]["decode"]["GiBps_alg"],
+              flush=True)
+    for k, r in ([] if a.mixed_only else shapes):
         G = max(1, int(a.bytes // (k * L_JUMBO)))
-        for mode in ("block", "sliding"):
+        for mode in a.modes.split(","):
             if mode == "block":
                 src = torch.randint(0, 256, (G * k * RS,), dtype=torch.uint8, device="cuda")
                 gs = k * RS

@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""VGPR-indexed XOR micro-benchmark (gfx950): the product step a bit-sliced
+combine with wave-uniform runtime coefficients needs,
+
+    acc_p ^= lo[i_p];  acc_p ^= hi[j_p]      (i_p, j_p in SGPRs)
+
+as s_set_gpr_idx_on / s_set_gpr_idx_idx + v_xor_b32 with an M0-indexed src0,
+against the same 16 XORs with fixed registers.  Checks the indexed results.
+
+    python tools/ubench_idx.py build     # here: tools/lab_build/idx_*.hsaco
+    python tools/ubench_idx.py run       # GPU box"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+OUT = REPO / "tools" / "lab_build"
+LO, HI, ACC = 40, 56, 20
+
+
+def body(kind: str) -> list[str]:
+    ops = []
+    if kind == "idx":
+        for p in range(8):
+            ops.append(f"s_set_gpr_idx_on s{8 + 2 * p}, gpr_idx(SRC0)" if p == 0 else f"s_set_gpr_idx_idx s{8 + 2 * p}")
+            ops.append(f"v_xor_b32_e32 v{ACC + p}, v{LO}, v{ACC + p}")
+            ops.append(f"s_set_gpr_idx_idx s{9 + 2 * p}")
+            ops.append(f"v_xor_b32_e32 v{ACC + p}, v{HI}, v{ACC + p}")
+        ops.append("s_set_gpr_idx_off")
+    elif kind == "plain":
+        for p in range(8):
+            ops.append(f"v_xor_b32_e32 v{ACC + p}, v{LO + p}, v{ACC + p}")
+            ops.append(f"v_xor_b32_e32 v{ACC + p}, v{HI + 15 - p}, v{ACC + p}")
+    elif kind == "plain_salu":   # same SALU count as idx, no indexing
+        for p in range(8):
+            ops.append(f"s_mov_b32 s{40 + 2 * p}, s{8 + 2 * p}")
+            ops.append(f"v_xor_b32_e32 v{ACC + p}, v{LO + p}, v{ACC + p}")
+            ops.append(f"s_mov_b32 s{41 + 2 * p}, s{9 + 2 * p}")
+            ops.append(f"v_xor_b32_e32 v{ACC + p}, v{HI + 15 - p}, v{ACC + p}")
+    return ops
+
+
+def kernel(name: str, kind: str, unroll: int = 4) -> str:
+    lines = [
+        "s_load_dwordx2 s[4:5], s[0:1], 0x0",
+        "s_load_dword s6, s[0:1], 0x8",
+        "v_and_b32_e32 v1, 63, v0",
+        "v_lshlrev_b32_e32 v2, 4, v1",          # 16 lane
+    ]
+    for i in range(16):
+        lines.append(f"v_add_u32_e32 v{LO + i}, {i}, v2")
+        lines.append(f"v_lshlrev_b32_e32 v{HI + i}, 16, v{LO + i}")
+    for p in range(8):
+        lines.append(f"v_mov_b32_e32 v{ACC + p}, 0")
+        lines.append(f"s_mov_b32 s{8 + 2 * p}, {p}")
+        lines.append(f"s_mov_b32 s{9 + 2 * p}, {15 - p}")
+    lines.append("s_waitcnt lgkmcnt(0)")
+    lines.append(".Lloop:")
+    for _ in range(unroll):
+        lines += body(kind)
+    lines += ["s_sub_u32 s6, s6, 1", "s_cmp_lg_u32 s6, 0", "s_cbranch_scc1 .Lloop"]
+    # out + (workgroup * 256 + tid) * 32
+    lines += ["s_lshl_b32 s7, s2, 13", "v_lshlrev_b32_e32 v4, 5, v0", "v_add_u32_e32 v4, s7, v4",
+              "v_mov_b32_e32 v5, 0",
+              "v_lshl_add_u64 v[10:11], v[4:5], 0, s[4:5]",
+              f"global_store_dwordx4 v[10:11], v[{ACC}:{ACC + 3}], off",
+              f"global_store_dwordx4 v[10:11], v[{ACC + 4}:{ACC + 7}], off offset:16",
+              "s_endpgm"]
+    body_s = "\n".join("\t" + x if not x.endswith(":") else x for x in lines).replace(".Lloop", f".L{name}_loop")
+    return f"""\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"
+\t.amdhsa_code_object_version 6
+\t.text
+\t.globl\t{name}
+\t.p2align\t8
+\t.type\t{name},@function
+{name}:
+{body_s}
+\t.section\t.rodata,"a",@progbits
+\t.p2align\t6, 0x0
+\t.amdhsa_kernel {name}
+\t\t.amdhsa_kernarg_size 16
+\t\t.amdhsa_user_sgpr_count 2
+\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1
+\t\t.amdhsa_system_sgpr_workgroup_id_x 1
+\t\t.amdhsa_system_vgpr_workitem_id 0
+\t\t.amdhsa_next_free_vgpr 128
+\t\t.amdhsa_next_free_sgpr 64
+\t\t.amdhsa_accum_offset 128
+\t\t.amdhsa_reserve_vcc 0
+\t.end_amdhsa_kernel
+\t.text
+.Lfunc_end_{name}:
+\t.size\t{name}, .Lfunc_end_{name}-{name}
+\t.amdgpu_metadata
+---
+amdhsa.kernels:
+  - .args:
+      - .address_space:  global
+        .name:           out
+        .offset:         0
+        .size:           8
+        .value_kind:     global_buffer
+      - .name:           iters
+        .offset:         8
+        .size:           4
+        .value_kind:     by_value
+    .group_segment_fixed_size: 0
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: 16
+    .max_flat_workgroup_size: 256
+    .name:           {name}
+    .private_segment_fixed_size: 0
+    .sgpr_count:     70
+    .sgpr_spill_count: 0
+    .symbol:         {name}.kd
+    .vgpr_count:     128
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+    .agpr_count:     0
+amdhsa.target:   amdgcn-amd-amdhsa--gfx950
+amdhsa.version:
+  - 1
+  - 2
+...
+\t.end_amdgpu_metadata
+"""
+
+
+KINDS = ["idx", "plain", "plain_salu"]
+
+
+def build():
+    from quicfuscate_amd.build_lib import assemble
+    OUT.mkdir(parents=True, exist_ok=True)
+    for k in KINDS:
+        print(k, assemble(f"idx_{k}", kernel(f"idx_{k}", k), OUT))
+
+
+def run(out):
+    import torch
+    hip = ctypes.CDLL(str(Path(torch.__file__).parent / "lib" / "libamdhip64.so"))
+    stream = torch.cuda.current_stream()
+    res = {}
+    for k in KINDS:
+        mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        data = (OUT / f"idx_{k}.hsaco").read_bytes()
+        buf = ctypes.create_string_buffer(data, len(data))
+        assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, f"idx_{k}".encode()) == 0
+        for waves_per_simd in (1, 2, 4):
+            blocks = 256 * waves_per_simd
+            o = torch.zeros(blocks * 256 * 8, dtype=torch.int32, device="cuda")
+
+            def launch(iters):
+                ka = np.zeros(4, np.uint32)
+                ka[0], ka[1], ka[2] = o.data_ptr() & 0xFFFFFFFF, o.data_ptr() >> 32, iters
+                kb = ctypes.create_string_buffer(ka.tobytes(), 16)
+                size = ctypes.c_size_t(16)
+                extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kb, ctypes.c_void_p), 2,
+                                             ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+                assert hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0,
+                                                 ctypes.c_void_p(stream.cuda_stream), None, extra) == 0
+            launch(1)   # unroll 4: acc = 4 x the body = 0 -> use 1 iteration with odd unroll check below
+            torch.cuda.synchronize()
+            iters = 20000
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record(stream)
+            launch(iters)
+            t1.record(stream)
+            torch.cuda.synchronize()
+            ms = t0.elapsed_time(t1)
+            waves = blocks * 4
+            xors = waves * iters * 4 * 16
+            res[f"{k}@{waves_per_simd}w"] = {"ms": round(ms, 3),
+                                             "xor_per_simd_per_ns": round(xors / 1024 / (ms * 1e6), 3)}
+            print(k, waves_per_simd, res[f"{k}@{waves_per_simd}w"], flush=True)
+        hip.hipModuleUnload(mod)
+    # correctness of the indexed reads: a build with unroll 1, one iteration
+    from quicfuscate_amd.build_lib import assemble
+    h = (OUT / "idx_check.hsaco")
+    mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+    data = h.read_bytes()
+    buf = ctypes.create_string_buffer(data, len(data))
+    assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+    assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"idx_check") == 0
+    o = torch.zeros(256 * 8, dtype=torch.int32, device="cuda")
+    ka = np.zeros(4, np.uint32)
+    ka[0], ka[1], ka[2] = o.data_ptr() & 0xFFFFFFFF, o.data_ptr() >> 32, 1
+    kb = ctypes.create_string_buffer(ka.tobytes(), 16)
+    size = ctypes.c_size_t(16)
+    extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kb, ctypes.c_void_p), 2,
+                                 ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+    assert hip.hipModuleLaunchKernel(fn, 1, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(stream.cuda_stream), None, extra) == 0
+    torch.cuda.synchronize()
+    got = o.cpu().numpy().view(np.uint32).reshape(256, 8)
+    lane = np.arange(256) % 64
+    want = np.stack([(lane * 16 + p) ^ ((lane * 16 + 15 - p) << 16) for p in range(8)], axis=1).astype(np.uint32)
+    res["idx_correct"] = bool((got == want).all())
+    print("idx correct:", res["idx_correct"], flush=True)
+    Path(out).parent.mkdir(exist_ok=True)
+    Path(out).write_text(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--out", default="gpurun_out/ubench_idx.json")
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build()
+        from quicfuscate_amd.build_lib import assemble
+        print(assemble("idx_check", kernel("idx_check", "idx", unroll=1), OUT))
+    else:
+        run(a.out)
