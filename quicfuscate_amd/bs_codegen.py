@@ -110,6 +110,9 @@ _ASM = {
     "v_xor3": lambda d, a, b, c: f"v_bitop3_b32 {V(d)}, {V(a)}, {V(b)}, {V(c)} bitop3:0x96",
     # d = (s[m] & a) | (~s[m] & b): bit select (truth table index s0*4 + s1*2 + s2)
     "v_bitsel_s": lambda d, m, a, b: f"v_bitop3_b32 {V(d)}, s{m}, {V(a)}, {V(b)} bitop3:0xca",
+    # the same bit-select with the mask in a VGPR: v_bitop3 with an SGPR operand
+    # issues at half the rate of an all-VGPR one (tools/ubench_idx.py)
+    "v_bitsel_v": lambda d, m, a, b: f"v_bitop3_b32 {V(d)}, {V(m)}, {V(a)}, {V(b)} bitop3:0xca",
     "v_movk": lambda d, k: f"v_mov_b32_e32 {V(d)}, {k}",
     "v_andk": lambda d, k, a: f"v_and_b32_e32 {V(d)}, 0x{k:08x}, {V(a)}",
     "v_lshr": lambda d, s, a: f"v_lshrrev_b32_e32 {V(d)}, {s}, {V(a)}",
@@ -369,6 +372,23 @@ class KernelSpec:
     # q < Q active), so row presence is wave-uniform and the row loop skips
     # the erased sources (tools/dec_lab.py)
     wave_gen: bool = False
+    # transpose masks in VGPRs (all-VGPR v_bitop3 issues at full rate, with an
+    # SGPR operand at half: tools/ubench_idx.py, profiles/r02_ubench_idx.json)
+    vgpr_masks: bool = True
+
+    @property
+    def vmask(self) -> Optional[tuple]:
+        """VGPRs holding the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
+        (None: SGPRs s42..s44).  The lane-chunk decode uses registers its
+        layout leaves free (V_DSTB pair, V_ZB); the others append three."""
+        if not self.vgpr_masks or self.mode == "cmb":
+            return None
+        if self.mode == "dec" and self.chunked:
+            return (V_DSTB, V_DSTB + 1, V_ZB)
+        n = self._base_free_vgpr()
+        if n + 3 > 256:   # no room: the masks stay in SGPRs
+            return None
+        return (n, n + 1, n + 2)
 
     @property
     def rt(self) -> int:
@@ -421,15 +441,21 @@ class KernelSpec:
             return 16 * ((self.k + self.rt + 15) // 16)
         return 16 * self.map_quads
 
-    @property
-    def next_free_vgpr(self) -> int:
-        if self.mode == "cmb":
-            return CMB_NEXT_FREE_VGPR
+    def _base_free_vgpr(self) -> int:
         n = self.map_b + 4 * self.map_quads
         if self.mode == "dec" and self.chunked:
             n = max(n, lu_layout_chunked(self)["end"])
         elif self.mode == "dec":
             n = max(n, max(lu_layout(self)[0]) + 4)
+        return n
+
+    @property
+    def next_free_vgpr(self) -> int:
+        if self.mode == "cmb":
+            return CMB_NEXT_FREE_VGPR
+        n = self._base_free_vgpr()
+        if self.vmask is not None and not (self.mode == "dec" and self.chunked):
+            n += 3
         n = (n + 7) // 8 * 8
         if n > 256:
             raise ValueError(f"{self.name}: {n} VGPRs > 256 (lower pd)")
@@ -480,13 +506,19 @@ _COMBO_BUILD = {  # mask: (a, b) meaning combo = a ^ b, where a/b are masks
 }
 
 
-def _transpose_ops(base: int, bfi: bool = False) -> list[Op]:
+def _transpose_ops(base: int, bfi: bool = False, vmask: Optional[tuple] = None) -> list[Op]:
     """32 bytes in 8 dwords <-> 8 bit-planes (3 delta-swap stages; an
     involution, so the same network maps planes back to bytes).
 
     bfi: each swap of (a, b) with shift s and mask M is
       a' = (M & a) | (~M & (b << s)),  b' = (M & (a >> s)) | (~M & b)
-    i.e. two shifts and two v_bitop3 bit-selects with M in an SGPR."""
+    i.e. two shifts and two v_bitop3 bit-selects with M in an SGPR, or in
+    the VGPR vmask[stage] when the kernel keeps the masks in VGPRs."""
+
+    def sel(d, stage, a, b):
+        if vmask is not None:
+            return Op("v_bitsel_v", (d, vmask[stage], a, b))
+        return Op("v_bitsel_s", (d, S_TMASK + stage, a, b))
     ops = []
     if bfi == "s64":
         # stages 1 and 2 shift register pairs with one 64-bit shift: the bits a
@@ -500,8 +532,8 @@ def _transpose_ops(base: int, bfi: bool = False) -> list[Op]:
                     t, u = V_T + 2 * (q & 1), V_T + 2 * (q & 1) + 1
                     ops.append(Op("v_lshl", (t, sh, base + b)))
                     ops.append(Op("v_lshr", (u, sh, base + a)))
-                    ops.append(Op("v_bitsel_s", (base + a, sm, base + a, t)))
-                    ops.append(Op("v_bitsel_s", (base + b, sm, u, base + b)))
+                    ops.append(sel(base + a, stage, base + a, t))
+                    ops.append(sel(base + b, stage, u, base + b))
                 continue
             for q in range(0, 4, 2):
                 (a0, b0), (a1, b1) = pairs[q], pairs[q + 1]
@@ -509,8 +541,8 @@ def _transpose_ops(base: int, bfi: bool = False) -> list[Op]:
                 ops.append(Op("v_lshl64", (V_T, sh, base + b0)))        # t pair = (b0, b1) << sh
                 ops.append(Op("v_lshr64", (V_T + 2, sh, base + a0)))    # u pair = (a0, a1) >> sh
                 for x, (a, b) in enumerate(((a0, b0), (a1, b1))):
-                    ops.append(Op("v_bitsel_s", (base + a, sm, base + a, V_T + x)))
-                    ops.append(Op("v_bitsel_s", (base + b, sm, V_T + 2 + x, base + b)))
+                    ops.append(sel(base + a, stage, base + a, V_T + x))
+                    ops.append(sel(base + b, stage, V_T + 2 + x, base + b))
         return ops
     if bfi:
         for stage, (sh, mask, pairs) in enumerate(_TRANSPOSE):
@@ -519,8 +551,8 @@ def _transpose_ops(base: int, bfi: bool = False) -> list[Op]:
                 t, u = V_T + 2 * (q & 1), V_T + 2 * (q & 1) + 1
                 ops.append(Op("v_lshl", (t, sh, base + b)))
                 ops.append(Op("v_lshr", (u, sh, base + a)))
-                ops.append(Op("v_bitsel_s", (base + a, sm, base + a, t)))
-                ops.append(Op("v_bitsel_s", (base + b, sm, u, base + b)))
+                ops.append(sel(base + a, stage, base + a, t))
+                ops.append(sel(base + b, stage, u, base + b))
         return ops
     for sh, mask, pairs in _TRANSPOSE:
         t = [V_T + q for q in range(4)]
@@ -595,12 +627,12 @@ def _coeff_block(ops: list[Op], rows_j: list[int], acc: int, lo: dict, hi: dict,
 
 
 def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bool, xor3: bool = False,
-                bfi: bool = False, guard: Optional[tuple[int, str]] = None):
+                bfi: bool = False, guard: Optional[tuple[int, str]] = None, vmask: Optional[tuple] = None):
     """Transpose one source row (ring buffer at `base`) and accumulate it into
     all r repair accumulators with the Cauchy coefficients of column i.
     guard = (j0, label): blocks j >= j0 are skipped (jump to label) once
     j >= jmax (dec mode)."""
-    ops.extend(_transpose_ops(base, bfi))
+    ops.extend(_transpose_ops(base, bfi, vmask))
     lo, hi = _combo_regs(base)
     rows = [mul_matrix_rows(C[j][i]) for j in range(r)]
     need_lo = {rb & 15 for rr in rows for rb in rr} - {0}
@@ -680,6 +712,9 @@ def _prologue(E, spec: KernelSpec):
         E(Op("s_lshr_s", (SW_GLAST, SW_GLAST, 16)))
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (S_TMASK + q, mask)))
+    if spec.vmask is not None:
+        for q in range(3):
+            E(Op("v_movs", (spec.vmask[q], S_TMASK + q)))
     E(Op("label", (".Litem",)))
     if spec.far:
         E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
@@ -805,10 +840,10 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         after = min(pd, k - 1 - i)
         E(Op("s_waitcnt_vm", (2 * after,)))
         _source_row(ops, C, i, r, ring0 + 8 * (i % nbuf), acc0, init=(i == 0), xor3=spec.xor3,
-                    bfi=spec.bfi_transpose)
+                    bfi=spec.bfi_transpose, vmask=spec.vmask)
     # planes -> bytes, store 2 x 16 bytes per lane per repair
     for j in range(r):
-        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose, spec.vmask))
     # padding lanes (stored, not loaded: the zero tail) hold garbage, since
     # masked loads leave stale planes in their half of the ring; byte
     # positions are independent, so clearing their half of the repairs here
@@ -1069,17 +1104,17 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         base = ring0 + 8 * (n % nbuf)
         if kind == "rep" and dec:
             E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
-            ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose))
+            ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose, spec.vmask))
             for b in range(8):
                 E(Op("v_xor", (acc0 + 8 * idx + b, acc0 + 8 * idx + b, base + b)))
             E(Op("label", (f".Lrep{idx}",)))
         elif kind == "rep":
-            ops.extend(_transpose_ops(base, spec.bfi_transpose))
+            ops.extend(_transpose_ops(base, spec.bfi_transpose, spec.vmask))
             for b in range(8):
                 E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
         else:
             _source_row(ops, C, idx, r, base, acc0, init=dec and idx == 0, xor3=spec.xor3,
-                        bfi=spec.bfi_transpose, guard=(g0, f".Lrow{n}") if dec else None)
+                        bfi=spec.bfi_transpose, vmask=spec.vmask, guard=(g0, f".Lrow{n}") if dec else None)
     if dec:
         if spec.prio != (0, 0):
             E(Op("s_setprio", (spec.prio[1],)))
@@ -1087,7 +1122,7 @@ def _generate_syn(spec: KernelSpec) -> list[Op]:
         _epilogue_next_item(E, far=True)
         return ops
     for j in range(r):
-        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose, spec.vmask))
     E(Op("s_nop", (4,)))
     for j in range(r):
         present(k + j, 0, S_TMP)
@@ -1216,13 +1251,13 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
         E(Op("s_waitcnt_vm", (per_row * after,)))
         base = ring0 + 8 * (n % nbuf)
         if kind == "rep":
-            ops.extend(_transpose_ops(base, spec.bfi_transpose))
+            ops.extend(_transpose_ops(base, spec.bfi_transpose, spec.vmask))
             for b in range(8):
                 E(Op("v_mov", (acc0 + 8 * idx + b, base + b)))
         else:
-            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose)
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose, vmask=spec.vmask)
     for j in range(r):
-        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose))
+        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose, spec.vmask))
     E(Op("s_nop", (4,)))
     for j in range(r):
         _store_pair(E, acc0 + 8 * j, S_STA, S_STB, spec.st_policy)
@@ -1319,6 +1354,9 @@ def _prologue_chunked(E, spec: KernelSpec):
         E(Op("s_lshr_s", (SW_GLAST, SW_GLAST, 16)))
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (S_TMASK + q, mask)))
+    if spec.vmask is not None:
+        for q in range(3):
+            E(Op("v_movs", (spec.vmask[q], S_TMASK + q)))
     E(Op("label", (".Litem",)))
     E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
     E(Op("s_far_jump", (".Lend", 0)))
@@ -1423,7 +1461,7 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         base = ring0 + 8 * (n % nbuf)
         if kind == "rep":
             E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
-            ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose))
+            ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose, spec.vmask))
             for b in range(8):
                 E(Op("v_xor", (acc0 + 8 * idx + b, acc0 + 8 * idx + b, base + b)))
             E(Op("label", (f".Lrep{idx}",)))
@@ -1431,11 +1469,11 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
             present(idx, S_TMP)
             E(Op("s_and64", (S_TMP, S_TMP, S_STA)))
             E(Op("s_cmp_eq64_0_br", (S_TMP, f".Lskip{n}")))
-            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose,
+            _source_row(ops, C, idx, r, base, acc0, init=False, xor3=spec.xor3, bfi=spec.bfi_transpose, vmask=spec.vmask,
                         guard=(spec.guard_min, f".Lrow{n}"))
             E(Op("label", (f".Lskip{n}",)))
         else:
-            _source_row(ops, C, idx, r, base, acc0, init=idx == 0, xor3=spec.xor3, bfi=spec.bfi_transpose,
+            _source_row(ops, C, idx, r, base, acc0, init=idx == 0, xor3=spec.xor3, bfi=spec.bfi_transpose, vmask=spec.vmask,
                         guard=(spec.guard_min, f".Lrow{n}"))
     _lu_solve_and_store_chunked(E, spec)
     _epilogue_next_item(E, far=True)
@@ -1581,6 +1619,7 @@ C_T = 20                          # v20..v23 transpose temps
 C_LO, C_HI = 24, 40               # LO[0..15], HI[0..15]
 C_ACC = 56                        # 16 x 8 accumulators v56..v183
 C_QV, C_QC, C_UB, C_UBC, C_TB = 184, 185, 186, 187, 188
+C_VM = 189                        # v189..v191 transpose masks (full-rate all-VGPR v_bitop3)
 # SGPRs
 CS_ITEM, CS_G, CS_T, CS_EW, CS_BOUND, CS_SLOT = 36, 37, 38, 39, 40, 41
 CS_ROWG, CS_CUR, CS_NEXT, CS_COEFG, CS_DSTG = 42, 44, 46, 48, 50
@@ -1606,7 +1645,7 @@ def _cmb_transpose(E, base: int, last_dst: Optional[list] = None):
     """bfi delta-swap network on 8 registers (plane p <- bit p of every byte);
     the last stage writes plane p to last_dst[p] (default: in place)."""
     for stage, (sh, _mask, pairs) in enumerate(_TRANSPOSE):
-        sm = CS_MASKS + stage
+        vm = C_VM + stage
         for q, (a, b) in enumerate(pairs):
             t, u = C_T + 2 * (q & 1), C_T + 2 * (q & 1) + 1
             da, db = base + a, base + b
@@ -1614,8 +1653,8 @@ def _cmb_transpose(E, base: int, last_dst: Optional[list] = None):
                 da, db = last_dst[a], last_dst[b]
             E(Op("v_lshl", (t, sh, base + b)))
             E(Op("v_lshr", (u, sh, base + a)))
-            E(Op("v_bitsel_s", (da, sm, base + a, t)))
-            E(Op("v_bitsel_s", (db, sm, u, base + b)))
+            E(Op("v_bitsel_v", (da, vm, base + a, t)))
+            E(Op("v_bitsel_v", (db, vm, u, base + b)))
 
 
 def _cmb_gen_addr(E, dst: int, base: int, gs: int, offs: int, tag: str):
@@ -1695,6 +1734,7 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     E(Op("v_readfirstlane", (CS_T0, 1)))
     for q, (_, mask, _) in enumerate(_TRANSPOSE):
         E(Op("s_movk", (CS_MASKS + q, mask)))
+        E(Op("v_movs", (C_VM + q, CS_MASKS + q)))
     E(Op("v_movk", (C_LO, 0)))
     E(Op("v_movk", (C_HI, 0)))
     E(Op("s_waitcnt_lgkm", ()))
@@ -2237,6 +2277,9 @@ class Emulator:
                 wv(a[0], rv(a[1]) ^ rv(a[2]) ^ rv(a[3]))
             elif n == "v_bitsel_s":
                 m = np.uint64(s[a[1]])
+                wv(a[0], (m & rv(a[2])) | (~m & np.uint64(MASK32) & rv(a[3])))
+            elif n == "v_bitsel_v":
+                m = rv(a[1])
                 wv(a[0], (m & rv(a[2])) | (~m & np.uint64(MASK32) & rv(a[3])))
             elif n == "v_movk":
                 wv(a[0], np.full(64, a[1], np.uint64))

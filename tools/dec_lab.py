@@ -24,6 +24,8 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tools"))
 OUT = REPO / "tools" / "lab_build"
 
+ONLY = None   # --only name,name: build a subset
+
 VARIANTS = [
     # name, spec kwargs, body-strip flags (bs_lab.variant_ops)
     ("warm", {}, ()),
@@ -51,6 +53,11 @@ VARIANTS = [
     ("wavegen", {"chunked": True, "wave_gen": True}, ()),
     ("wavegen_nolu", {"chunked": True, "wave_gen": True, "lu": False}, ()),
     ("decc_2", {"chunked": True}, ()),
+    # transpose masks in SGPRs (half-rate v_bitop3) instead of VGPRs
+    ("decc_smask", {"chunked": True, "vgpr_masks": False}, ()),
+    ("decc_smask_nolu", {"chunked": True, "vgpr_masks": False, "lu": False}, ()),
+    ("decc_3", {"chunked": True}, ()),
+    ("decc_smask_2", {"chunked": True, "vgpr_masks": False}, ()),
 ]
 
 
@@ -65,6 +72,8 @@ def build():
         old.unlink()
     man = []
     for name, kw, flags in VARIANTS:
+        if ONLY and name not in ONLY:
+            continue
         kw2 = dict(kw)
         pd = kw2.pop("pd", 3)
         spec = bs.KernelSpec(64, 16, pd, "dec", **kw2)
@@ -161,7 +170,10 @@ if __name__ == "__main__":
     ap.add_argument("--G", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/dec_lab.json")
+    ap.add_argument("--only", default="", help="comma-separated variant names (build)")
     a = ap.parse_args()
+    if a.only:
+        ONLY = set(a.only.split(","))
     if a.cmd == "build":
         build()
     else:

@@ -1,9 +1,10 @@
 #!/bin/bash
-# Quick GPU iteration: selected GPU tests (TESTS), then one bench run (BENCH_ARGS).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest ${TESTS:-tests} -m gpu -q -x --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_quick.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_quick.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_quick.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench_quick.log; exit $rc
+# GPU box: codec parity (encode, decode, C5, desc, full size) then one bench line.
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/quick
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    tests/test_gpu_encode.py tests/test_gpu_decode.py tests/test_gpu_c5_mixed.py tests/test_gpu_desc.py \
+    tests/test_gpu_fullsize.py > gpurun_out/quick/tests.log 2>&1
+timeout -k 10 300 python bench.py --no-cpu --host-path-G 0 > gpurun_out/quick/bench.log 2>&1
+echo QUICK_OK

@@ -38,6 +38,39 @@ def body(kind: str) -> list[str]:
         for p in range(8):
             ops.append(f"v_xor_b32_e32 v{ACC + p}, v{LO + p}, v{ACC + p}")
             ops.append(f"v_xor_b32_e32 v{ACC + p}, v{HI + 15 - p}, v{ACC + p}")
+    elif kind == "bitop3_banks":   # acc, LO, HI operands in three different VGPR banks
+        for p in range(8):
+            lo = LO + ((1 - (ACC + p)) % 4)          # bank (acc + 1) mod 4 ... chosen below
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, v{ACC + 4 * p}, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)} bitop3:0x96")
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, v{ACC + 4 * p + 1}, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)} bitop3:0x96")
+    elif kind == "bitop3_same":   # LO and HI operands in the accumulator's bank
+        for p in range(8):
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, v{ACC + 4 * p}, v{LO + 4 * (p % 4)}, v{HI + 4 * (p % 3)} bitop3:0x96")
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, v{ACC + 4 * p + 1}, v{LO + 1 + 4 * (p % 3)}, v{HI + 1 + 4 * (p % 3)} bitop3:0x96")
+    elif kind == "xor_banks":
+        for p in range(8):
+            ops.append(f"v_xor_b32_e32 v{ACC + 4 * p}, v{LO + 1 + 4 * (p % 4)}, v{ACC + 4 * p}")
+            ops.append(f"v_xor_b32_e32 v{ACC + 4 * p + 1}, v{LO + 2 + 4 * (p % 3)}, v{ACC + 4 * p + 1}")
+    elif kind == "perm_banks":
+        for p in range(8):
+            ops.append(f"v_perm_b32 v{ACC + 4 * p}, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)}, v{ACC + 4 * p + 3}")
+            ops.append(f"v_perm_b32 v{ACC + 4 * p + 1}, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)}, v{ACC + 4 * p + 3}")
+    elif kind == "bitsel_sgpr":   # the transpose's bit-select: mask in an SGPR
+        for p in range(8):
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, s30, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)} bitop3:0xca")
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, s30, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)} bitop3:0xca")
+    elif kind == "bitsel_vgpr":   # the same bit-select with the mask in a VGPR (v31)
+        for p in range(8):
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, v63, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)} bitop3:0xca")
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, v63, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)} bitop3:0xca")
+    elif kind == "xor3_sgpr":   # 3-input XOR with one SGPR operand
+        for p in range(8):
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, s30, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)} bitop3:0x96")
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, s30, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)} bitop3:0x96")
+    elif kind == "bitsel_vgpr_last":   # mask VGPR as the last operand (truth table 0xd8)
+        for p in range(8):
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)}, v63 bitop3:0xd8")
+            ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)}, v63 bitop3:0xd8")
     elif kind == "plain_salu":   # same SALU count as idx, no indexing
         for p in range(8):
             ops.append(f"s_mov_b32 s{40 + 2 * p}, s{8 + 2 * p}")
@@ -54,11 +87,14 @@ def kernel(name: str, kind: str, unroll: int = 4) -> str:
         "v_and_b32_e32 v1, 63, v0",
         "v_lshlrev_b32_e32 v2, 4, v1",          # 16 lane
     ]
+    for p in range(32):
+        lines.append(f"v_mov_b32_e32 v{ACC + p}, 0")
     for i in range(16):
         lines.append(f"v_add_u32_e32 v{LO + i}, {i}, v2")
         lines.append(f"v_lshlrev_b32_e32 v{HI + i}, 16, v{LO + i}")
+    lines.append("s_mov_b32 s30, 0x0f0f0f0f")
+    lines.append("v_mov_b32_e32 v63, s30")
     for p in range(8):
-        lines.append(f"v_mov_b32_e32 v{ACC + p}, 0")
         lines.append(f"s_mov_b32 s{8 + 2 * p}, {p}")
         lines.append(f"s_mov_b32 s{9 + 2 * p}, {15 - p}")
     lines.append("s_waitcnt lgkmcnt(0)")
@@ -133,7 +169,8 @@ amdhsa.version:
 """
 
 
-KINDS = ["idx", "plain", "plain_salu"]
+KINDS = ["idx", "plain", "plain_salu", "bitop3_banks", "bitop3_same", "xor_banks", "perm_banks", "bitsel_sgpr",
+         "bitsel_vgpr", "xor3_sgpr", "bitsel_vgpr_last"]
 
 
 def build():
@@ -177,7 +214,7 @@ def run(out):
             torch.cuda.synchronize()
             ms = t0.elapsed_time(t1)
             waves = blocks * 4
-            xors = waves * iters * 4 * 16
+            xors = waves * iters * 4 * len([o for o in body(k) if o.startswith("v_")])
             res[f"{k}@{waves_per_simd}w"] = {"ms": round(ms, 3),
                                              "xor_per_simd_per_ns": round(xors / 1024 / (ms * 1e6), 3)}
             print(k, waves_per_simd, res[f"{k}@{waves_per_simd}w"], flush=True)
