@@ -101,17 +101,21 @@ PATHS = ["default", "syn", "general", "syn_bs", "general_bs"]
 
 
 def _path(monkeypatch, path):
-    # "*_bs": the payload pass takes the bit-sliced k_combine_bs at every row
-    # length (by default only rows of >= 128 lane-chunks of 32 B do)
+    # "*_bs": the payload pass takes the bit-sliced qf_combine_bs at every row
+    # length (by default only rows of >= 64 lane-chunks of 32 B do); "general"
+    # keeps k_combine_slots at every length (QF_COMBINE_BS=0)
+    monkeypatch.delenv("QF_COMBINE_BS", raising=False)
     if path.endswith("_bs"):
         monkeypatch.setenv("QF_COMBINE_BS_MIN_Q", "1")
         path = path[:-3]
     else:
         monkeypatch.delenv("QF_COMBINE_BS_MIN_Q", raising=False)
+        if path == "general":
+            monkeypatch.setenv("QF_COMBINE_BS", "0")
     # "default": fused decode (syndromes + LU solve in one kernel) where a
     # bit-sliced kernel exists for (k, r) (Cauchy code, L % 16 == 0);
-    # "syn": syndrome kernel + v_perm combine (two kernels);
-    # "general": Gauss-Jordan + slots kernel
+    # "syn": syndrome kernel + payload pass (two kernels);
+    # "general": Gauss-Jordan + payload pass
     if path == "general":
         monkeypatch.setenv("QF_DISABLE_BS", "1")
     else:
