@@ -776,7 +776,8 @@ bool small_encode_enabled() {
     return !(sm && atoi(sm) == 0);
 }
 int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, uint32_t L, const uint8_t* ring,
-                       uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride) {
+                       uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride, const uint8_t* fresh,
+                       uint8_t* fresh_dst, uint32_t fresh_units) {
     if (!ctx || !ring || !rep || k == 0 || count == 0 || rot >= k) return QF_EINVAL;
     if ((uint64_t)k + first + count > 256) return QF_ERANGE;  // gf_inv(0)
     if (L == 0) return QF_OK;
@@ -802,6 +803,16 @@ int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, 
     a.G = 1;
     a.rot = rot;
     hipEvent_t ev = prof_begin(ctx, ctx->stream);
+    if (fresh) {
+        if (!fresh_dst || rep_stride < 16ull * a.Lu || stride < 16ull * fresh_units ||
+            fresh_units > qf::SEND_PKT_UNITS)
+            return QF_EINVAL;
+        a.fresh_dst = fresh_dst;
+        a.fresh_units = fresh_units;
+        QF_CHECK_HIP(qf::launch_send_window(a, fresh, 16u * fresh_units, ctx->stream));
+        prof_end(ctx, ctx->stream, ev, "k_send_window");
+        return QF_OK;
+    }
     QF_CHECK_HIP(qf::launch_encode_small(a, ctx->num_cus, ctx->stream));
     prof_end(ctx, ctx->stream, ev, "k_encode_small");
     return QF_OK;

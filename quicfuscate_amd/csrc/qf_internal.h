@@ -40,8 +40,13 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
 // window position i in slot (rot + i) % k; repairs = Cauchy rows
 // first..first+count-1 into rep (row stride rep_stride), on the small-batch
 // kernel.  QF_ERANGE when k + first + count > 256.  (qf_api.hip)
+// fresh (fused per-packet send): window position k - 1 is the host packet
+// fresh (fresh_units zero-padded 16-byte units, <= SEND_PKT_UNITS), passed in
+// the kernel arguments and written into the ring slot fresh_dst; rep is then
+// a host-coherent buffer of whole 16-byte units per row.
 int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, uint32_t L,
-                       const uint8_t* ring, uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride);
+                       const uint8_t* ring, uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride,
+                       const uint8_t* fresh = nullptr, uint8_t* fresh_dst = nullptr, uint32_t fresh_units = 0);
 // Whether the small-batch encode is enabled (QF_ENCODE_SMALL != 0).
 bool small_encode_enabled();
 

@@ -159,6 +159,10 @@ struct EncodeSmallArgs {
     // per-window records (nullptr: the scalar fields above); L / Lu above are
     // then the class maxima that size the tile grid
     const RingWin* wins = nullptr;
+    // fused per-packet send (k_send_window): the ring slot of the new packet
+    // and its 16-byte units (the packet itself travels in the arguments)
+    uint8_t* fresh_dst = nullptr;
+    uint32_t fresh_units = 0;
 };
 
 // Source packets of a send batch into their encoders' ring slots: bytes
@@ -203,6 +207,11 @@ template <typename T>
 __host__ __device__ inline T* gen_base(T* base, uint64_t g, uint64_t stride, const uint64_t* offs) {
     return base + (offs ? offs[g] : g * stride);
 }
+// Fused per-packet send: the new packet (pkt_bytes <= 16 fresh_units, in the
+// kernel arguments) is window position k - 1 and goes into the ring slot
+// a.fresh_dst; repairs to a.rep (host-coherent, whole 16-byte units).
+constexpr uint32_t SEND_PKT_UNITS = 224;   // 3,584 bytes: with the arguments under 4 KiB
+hipError_t launch_send_window(const EncodeSmallArgs& a, const uint8_t* pkt, uint32_t pkt_bytes, hipStream_t st);
 hipError_t launch_encode_small(const EncodeSmallArgs& a, int num_cus, hipStream_t st);
 // The same over per-window records (a.wins != nullptr), all repairs of a
 // 64-unit tile per block (send batches of many windows).

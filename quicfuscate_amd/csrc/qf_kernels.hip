@@ -31,6 +31,7 @@
 //  k_fill_splitmix              synthetic payload generator.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "qf_kernels.h"
 
@@ -1358,6 +1359,13 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t n, uint64_t seed, uint64_
 // LDS); the loop is memory-latency-bound at this size, so each batch of 8
 // rows has all its loads in flight before its products.
 // ---------------------------------------------------------------------------
+// system-scope 16-byte store into host-coherent memory (fused send)
+QF_DEV void store_sys16(uint8_t* p, const uint4& v) {
+    v4u x = {v.x, v.y, v.z, v.w};
+    // (s_nop: the store's data VGPRs are not rewritten in the next cycle)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" : : "v"(p), "v"(x) : "memory");
+}
+
 __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
     // tile = (generation g, repair j, 64 consecutive units); the block's four
     // waves take a quarter of the k rows each (batches of 8 rows whose loads
@@ -1437,6 +1445,107 @@ __global__ void __launch_bounds__(256) k_encode_small(EncodeSmallArgs a) {
         }
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// Fused per-packet send (AdaptiveFec::on_send -> emit_repairs for one
+// connection, adaptive.rs:519-562): the packet that completes the window
+// travels in the kernel arguments (SEND_PKT_UNITS 16-byte units), block 0 puts
+// it into its ring slot, and the repairs go straight to a host-coherent
+// buffer -- one launch instead of copy + encode + copy.  A block = (repair j,
+// 64 units); its four waves split the rows and issue all their loads (up to
+// 16 at a time) together with the split-table copy, then sum, reduce through
+// LDS and store with system-scope stores.
+// ---------------------------------------------------------------------------
+struct SendWinArgs {
+    EncodeSmallArgs a;
+    uint4 pkt[SEND_PKT_UNITS];
+};
+
+__global__ void __launch_bounds__(256) k_send_window(SendWinArgs p) {
+    const EncodeSmallArgs& a = p.a;
+    __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 8];
+    __shared__ uint4 part[3][64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t ut = (a.Lu + 63) / 64;
+    const uint32_t t = blockIdx.x;   // one tile per block
+    const uint32_t j = t / ut, u = (t - j * ut) * 64 + lane;
+    const bool act = 16 * u < a.L;
+    const uint32_t kc = (a.k + 3) / 4, i0 = min(a.k, wv * kc), i1 = min(a.k, i0 + kc);
+    const uint8_t* sp = a.src + 16ull * (act ? u : 0);
+    const uint8_t* cp = a.coef + (uint64_t)j * a.k;
+    // split tables: global loads now, into LDS after the row loads are issued
+    const uint4* gt = reinterpret_cast<const uint4*>(a.tab256);
+    const uint4 t0 = gt[threadIdx.x], t1 = gt[threadIdx.x + 256];
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    bool tab_ready = false;
+    for (uint32_t ib = i0; ib < i1; ib += 16) {
+        uint4 x[16];
+        uint32_t c[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t i = ib + q;
+            const bool ok = act && i < i1;
+            const uint32_t row = i + a.rot >= a.k ? i + a.rot - a.k : i + a.rot;
+            if (i == a.k - 1)   // the new packet (window position k - 1)
+                x[q] = ok ? p.pkt[u] : make_uint4(0, 0, 0, 0);
+            else
+                x[q] = ok ? *reinterpret_cast<const uint4*>(sp + (uint64_t)row * a.src_row_stride)
+                          : make_uint4(0, 0, 0, 0);
+            c[q] = (i < i1) ? ((uint32_t)cp[i] << 5) : 0u;   // record 0: zero products
+        }
+        if (!tab_ready) {
+            reinterpret_cast<uint4*>(tab)[threadIdx.x] = t0;
+            reinterpret_cast<uint4*>(tab)[threadIdx.x + 256] = t1;
+            __syncthreads();
+            tab_ready = true;
+        }
+        const uint8_t* tb = reinterpret_cast<const uint8_t*>(tab);
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+            const uint4 A = *reinterpret_cast<const uint4*>(tb + c[q]);
+            const uint32_t a2 = *reinterpret_cast<const uint32_t*>(tb + c[q] + 16);
+            const uint4 B = *reinterpret_cast<const uint4*>(tb + c[q + 1]);
+            const uint32_t b2 = *reinterpret_cast<const uint32_t*>(tb + c[q + 1] + 16);
+            fma_pair(acc, A, a2, selectors(x[q]), B, b2, selectors(x[q + 1]));
+        }
+    }
+    // every wave passes one table barrier (waves without rows too; the
+    // condition is wave-uniform)
+    if (!tab_ready) {
+        reinterpret_cast<uint4*>(tab)[threadIdx.x] = t0;
+        reinterpret_cast<uint4*>(tab)[threadIdx.x + 256] = t1;
+        __syncthreads();
+    }
+    if (wv > 0) part[wv - 1][lane] = acc;
+    __syncthreads();
+    if (wv == 0 && act) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const uint4 pp = part[q][lane];
+            acc.x ^= pp.x;
+            acc.y ^= pp.y;
+            acc.z ^= pp.z;
+            acc.w ^= pp.w;
+        }
+        store_sys16(a.rep + (uint64_t)j * a.rep_row_stride + 16ull * u, acc);   // rows >= 16 Lu bytes
+    }
+    if (blockIdx.x == 0)   // the new packet into its ring slot
+        for (uint32_t v = threadIdx.x; v < a.fresh_units; v += blockDim.x)
+            *reinterpret_cast<uint4*>(a.fresh_dst + 16ull * v) = p.pkt[v];
+}
+
+hipError_t launch_send_window(const EncodeSmallArgs& a, const uint8_t* pkt, uint32_t pkt_bytes, hipStream_t st) {
+    if (!a.fresh_dst || a.G != 1 || a.k == 0 || a.r == 0 || a.Lu == 0 || a.fresh_units > SEND_PKT_UNITS ||
+        a.Lu > a.fresh_units || pkt_bytes > 16u * a.fresh_units)
+        return hipErrorInvalidValue;
+    SendWinArgs p;
+    p.a = a;
+    memset(p.pkt, 0, 16u * a.fresh_units);
+    if (pkt_bytes) memcpy(p.pkt, pkt, pkt_bytes);
+    const uint32_t blocks = a.r * ((a.Lu + 63) / 64);
+    hipLaunchKernelGGL(k_send_window, dim3(blocks), dim3(256), 0, st, p);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -51,6 +51,14 @@ struct qf_encoder {
     bool ring_rot = true;
     uint8_t* h_out = nullptr;        // pinned download of the repair rows
     size_t h_out_bytes = 0;
+    // fused per-packet send (QF_SEND_FUSED != 0, rotated ring): the packet that
+    // fills the window waits in h_fresh until generate_repairs, whose one
+    // kernel gets it in its arguments, writes it into its ring slot and stores
+    // the repairs straight into host-coherent h_rep (no copy kernels)
+    uint8_t* h_fresh = nullptr;
+    uint8_t* h_rep = nullptr;        // 256 rows of `stride` bytes
+    bool pending = false;
+    uint32_t pend_slot = 0;
 };
 
 struct qf_decoder {
@@ -80,6 +88,28 @@ struct qf_decoder {
 };
 
 namespace {
+
+bool send_fused_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("QF_SEND_FUSED");
+        return !(v && !atoi(v));
+    }();
+    return on;
+}
+
+// Upload a packet still waiting for the fused send into its ring slot
+// (through the staging buffer, as add_source_packet does).
+int encoder_flush(qf_encoder* e) {
+    if (!e->pending) return QF_OK;
+    QF_CHECK_HIP(hipEventSynchronize(e->stage_done));
+    memcpy(e->h_stage, e->h_fresh, e->stride);
+    hipStream_t st = (hipStream_t)qf_ctx_stream(e->ctx);
+    QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)e->pend_slot * e->stride, e->h_stage, e->stride,
+                                hipMemcpyHostToDevice, st));
+    QF_CHECK_HIP(hipEventRecord(e->stage_done, st));
+    e->pending = false;
+    return QF_OK;
+}
 
 // Cauchy rows 0..rows-1 in window order (decoder.rs:280-298), cached per encoder
 bool window_rows(qf_encoder* e, uint32_t rows) {
@@ -129,6 +159,9 @@ int qf_encoder_free(qf_encoder* e) {
     }
     if (e->h_stage) hipHostFree(e->h_stage);
     if (e->h_out) hipHostFree(e->h_out);
+    if (e->h_fresh || e->h_rep) hipStreamSynchronize((hipStream_t)qf_ctx_stream(e->ctx));
+    if (e->h_fresh) hipHostFree(e->h_fresh);
+    if (e->h_rep) hipHostFree(e->h_rep);
     if (e->d_ring) hipFree(e->d_ring);
     if (e->d_out) hipFree(e->d_out);
     delete e;
@@ -140,11 +173,31 @@ int qf_encoder_window_len(const qf_encoder* e) { return e ? (int)e->count : QF_E
 // decoder.rs:164-169: when the window holds k packets the oldest is dropped.
 int qf_encoder_add_source_packet(qf_encoder* e, uint64_t id, const uint8_t* data, uint32_t len) {
     if (!e || (len && !data) || len > e->max_len) return QF_EINVAL;
+    // a packet that filled the window but was not encoded goes up first
+    if (int s = encoder_flush(e)) return s;
+    const uint32_t slot = e->head;
+    // (the packet travels in the kernel arguments: stride <= 16 SEND_PKT_UNITS)
+    if (e->ring_rot && e->count + 1 >= e->k && e->stride <= 16 * qf::SEND_PKT_UNITS && send_fused_enabled()) {
+        // the window will be full: keep the packet for the fused send
+        if (!e->h_fresh) {
+            if (hipHostMalloc(reinterpret_cast<void**>(&e->h_fresh), e->stride) != hipSuccess) return QF_ENOMEM;
+        }
+        // (h_fresh is free: the last fused send synchronised its stream, the
+        // last flush copied it out on the host)
+        memset(e->h_fresh, 0, e->stride);
+        if (len) memcpy(e->h_fresh, data, len);
+        e->pending = true;
+        e->pend_slot = slot;
+        e->lens[slot] = len;
+        e->ids[slot] = id;
+        e->head = (e->head + 1) % e->k;
+        if (e->count < e->k) e->count++;
+        return QF_OK;
+    }
     // the staging buffer is reused: the previous packet's copies must have landed
     QF_CHECK_HIP(hipEventSynchronize(e->stage_done));
     memset(e->h_stage, 0, e->stride);
     if (len) memcpy(e->h_stage, data, len);
-    const uint32_t slot = e->head;
     hipStream_t st = (hipStream_t)qf_ctx_stream(e->ctx);
     QF_CHECK_HIP(hipMemcpyAsync(e->d_ring + (size_t)slot * e->stride, e->h_stage, e->stride,
                                 hipMemcpyHostToDevice, st));
@@ -174,6 +227,29 @@ int qf_encoder_generate_repairs(qf_encoder* e, uint32_t first, uint32_t count, u
     if ((uint64_t)k + first + count > 256) return QF_ERANGE;  // gf_inv(0)
     if (!window_rows(e, first + count)) return QF_ERANGE;
     const uint8_t* win = e->win.data() + (size_t)first * k;
+    if (e->pending && L > 0 && out_data) {
+        // fused send: one kernel reads the new packet from h_fresh, puts it in
+        // its ring slot and writes the repairs into h_rep
+        if (!e->h_rep) {
+            if (hipHostMalloc(reinterpret_cast<void**>(&e->h_rep), (size_t)256 * e->stride, hipHostMallocCoherent) !=
+                hipSuccess)
+                return QF_ENOMEM;
+        }
+        int s = qf::encode_ring_window(e->ctx, k, first, count, L, e->d_ring, e->stride, oldest, e->h_rep, e->stride,
+                                       e->h_fresh, e->d_ring + (size_t)e->pend_slot * e->stride, e->stride / 16);
+        if (s != QF_OK) return s;
+        e->pending = false;
+        QF_CHECK_HIP(hipStreamSynchronize((hipStream_t)qf_ctx_stream(e->ctx)));
+        for (uint32_t q = 0; q < count; ++q)
+            memcpy(out_data + (size_t)q * out_stride, e->h_rep + (size_t)q * e->stride, L);
+        for (uint32_t q = 0; q < count; ++q) {
+            if (out_len) out_len[q] = L;
+            if (out_ids) out_ids[q] = e->ids[newest] + 1 + first + q;  // decoder.rs:267
+            if (out_coeffs) memcpy(out_coeffs + (size_t)q * k, win + (size_t)q * k, k);
+        }
+        return QF_OK;
+    }
+    if (int s = encoder_flush(e)) return s;
     if (L > 0) {
         // the window is contiguous in the double ring: repairs 0..count-1 are
         // the cached Cauchy code (k, count) (generated kernel or cached
@@ -580,6 +656,9 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         if (!e || e->ctx != ctx || (v[m].len && !v[m].data) || v[m].len > e->max_len) return QF_EINVAL;
         if (e->n > e->k && !window_rows(e, e->n - e->k)) return QF_ERANGE;
     }
+    // packets a per-packet add left for the fused send go up before the scatter
+    for (uint32_t m = 0; m < M; ++m)
+        if (int fs = encoder_flush(v[m].e)) return fs;
     std::unique_lock<std::mutex> lk;
     int s = ctx_lock(ctx, lk);
     if (s) return s;
