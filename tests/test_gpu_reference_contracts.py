@@ -212,3 +212,42 @@ def test_ring_encoder_every_rotation(qf, oracle, gpu_ctx, monkeypatch, small, k)
             assert rp.id == t + 1 + j
         checked += 1
     assert checked >= 6
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("k,max_len", [(16, 1500), (64, 1200), (5, 9000)])
+def test_fused_send_window(qf, oracle, gpu_ctx, monkeypatch, fused, k, max_len):
+    """The packet that completes a window waits on the host and travels in
+    the arguments of the one fused send kernel (QF_SEND_FUSED, default on;
+    not above 3,584-byte slots).  Repairs of every window equal the oracle's
+    encode of the last k packets, with window[0].len != the new packet's len
+    (decoder.rs:172-275), a first repair other than 0, a generate without
+    output bytes (the packet is uploaded instead), and adds that skip the
+    generate entirely."""
+    import numpy as np
+
+    monkeypatch.setenv("QF_SEND_FUSED", fused)
+    r = 3
+    enc = qf.Encoder(k, k + r, max_len=max_len)
+    rng = np.random.default_rng(k + max_len)
+    pool = qf.MemoryPool(4, max_len)
+    lens = [int(x) for x in rng.integers(1, max_len + 1, 3 * k)]
+    data = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    for t in range(3 * k):
+        enc.add_source_packet(qf.Packet(t, bytearray(data[t]), lens[t], True))
+        if t + 1 < k or t % 3 == 1:
+            continue                    # the next add uploads the waiting packet
+        L = lens[t + 1 - k]
+        window = np.zeros((k, L), np.uint8)
+        for i in range(k):
+            b = np.frombuffer(data[t + 1 - k + i], np.uint8)[:L]
+            window[i, : len(b)] = b
+        want = oracle.encode(window, r)
+        if t % 6 == 5:   # no output bytes: the waiting packet is uploaded instead
+            from quicfuscate_amd import _lib as LL
+            assert LL._lib().qf_encoder_generate_repairs(enc.handle, 0, 1, None, 0, None, None, None) == 0
+        j0 = 2 if t % 3 == 2 else 0     # a first repair other than 0 may consume the packet
+        for j in list(range(j0, r)) + list(range(0, j0)):
+            rp = enc.generate_repair_packet(j, pool)
+            assert rp.len == L and bytes(rp.data[:L]) == want[j].tobytes(), (t, j)
+            assert rp.id == t + 1 + j

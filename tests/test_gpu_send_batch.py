@@ -175,3 +175,39 @@ def test_send_batch_second_context(qf, oracle, gpu_ctx):
             want = []
             twins[c].on_send(qf.Packet(i, bytearray(pays[c]), 600, True), want)
             assert st[c] == L.QF_OK and len(q[c]) == len(want) and all(_same(a, b) for a, b in zip(q[c], want))
+
+
+def test_send_batch_after_per_packet_sends(qf, oracle, gpu_ctx):
+    """A connection driven alternately by per-packet on_send (whose window-
+    completing packet waits for the fused send kernel) and by send batches
+    (which upload any waiting packet before their ring scatter) emits exactly
+    what its per-packet twin emits, and every repair matches the oracle."""
+    cfg = _cfg(qf, qf.FecMode.Normal, normal_window=16, max_len=600)
+    a, twin = _pair(qf, cfg)
+    other, other_twin = _pair(qf, cfg)
+    rng = np.random.default_rng(3)
+    hist = []
+    k = a.state()["k"]
+    r = a.state()["n"] - k
+    for t in range(60):
+        ln = int(rng.integers(1, 600))
+        b = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        b2 = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        hist.append(b)
+        want, want2 = [], []
+        twin.on_send(qf.Packet(t, bytearray(b), ln, True), want)
+        other_twin.on_send(qf.Packet(t, bytearray(b2), ln, True), want2)
+        if t % 4 in (1, 2):     # per-packet
+            got, got2 = [], []
+            a.on_send(qf.Packet(t, bytearray(b), ln, True), got)
+            other.on_send(qf.Packet(t, bytearray(b2), ln, True), got2)
+        else:                   # one batch of both connections
+            outs, st = qf.on_send_batch([a, other], [qf.Packet(t, bytearray(b), ln, True),
+                                                     qf.Packet(t, bytearray(b2), ln, True)])
+            assert st == [L.QF_OK, L.QF_OK]
+            got, got2 = outs[0], outs[1]
+        assert len(got) == len(want) and all(_same(p, q) for p, q in zip(got, want)), t
+        assert len(got2) == len(want2) and all(_same(p, q) for p, q in zip(got2, want2)), t
+        reps = [p for p in got if not p.is_systematic]
+        if reps:
+            _check_oracle(oracle, k, r, hist, reps)
