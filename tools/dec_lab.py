@@ -58,6 +58,11 @@ VARIANTS = [
     ("decc_smask_nolu", {"chunked": True, "vgpr_masks": False, "lu": False}, ()),
     ("decc_3", {"chunked": True}, ()),
     ("decc_smask_2", {"chunked": True, "vgpr_masks": False}, ()),
+    # row prefetch depth of the lane-chunk decode (pd 4: 5 ring buffers, still 256 VGPRs)
+    ("decc_pd4", {"chunked": True, "pd": 4}, ()),
+    ("decc_pd2", {"chunked": True, "pd": 2}, ()),
+    ("decc_pd4_nolu", {"chunked": True, "pd": 4, "lu": False}, ()),
+    ("decc_pd4_2", {"chunked": True, "pd": 4}, ()),
 ]
 
 
