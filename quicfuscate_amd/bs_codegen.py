@@ -221,6 +221,7 @@ _ASM = {
                      + (f" {pol}" if pol else ""),
     "store_byte_saddr": lambda voff, d, sb, off: f"global_store_byte {V(voff)}, {V(d)}, {SP(sb)}"
                         + (f" offset:{off}" if off else ""),
+    "store_byte": lambda a, d, off: f"global_store_byte {VP(a)}, {V(d)}, off" + (f" offset:{off}" if off else ""),
 }
 
 
@@ -269,7 +270,7 @@ S_STA, S_STB, S_PAD = 48, 50, 52   # store masks of halves A / B, mask temp
 
 # dec mode (fused decode: syndromes + in-register LU solve, see _generate_syn):
 # extra kernarg dwords 20..27 at 0x50 -> s[56:63]:
-#   s[56:57] LU records   s58 LU record stride   s59 unused
+#   s[56:57] LU records   s58 LU record stride   s59 L % 16 (lane-chunk decode; 0 otherwise)
 #   s[60:61] split tables (256 x 32 B, gf256_tables.h perm_record)
 #   s[62:63] {4096, 0} after the table copy (address constant)
 # s64 jmax: 1 + the largest repair index any lane of the item has accepted.
@@ -468,7 +469,8 @@ class KernelSpec:
         if self.mode == "synw":
             return SW_NEXT_FREE
         if self.mode == "dec":
-            return SGPR_NEXT_FREE_DEC + (2 if self.chunked else 0)   # chunked: s[76:77] = {16 Q, 0}
+            # chunked: s[76:77] = {16 Q, 0}, s[78:79] the partial-last-unit lane
+            return SGPR_NEXT_FREE_DEC + (4 if self.chunked else 0)
         return S_OFFS + 4   # s[66:67]: far-jump target, s[72:75]: offset tables
 
     @property
@@ -1270,6 +1272,7 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
 # Fused decode, lane-chunk layout (spec.chunked)
 # --------------------------------------------------------------------------
 S_QB = 76   # s[76:77] = {16 Q, 0}: byte offset of a lane's B unit from its A unit
+S_TAIL = 78  # s[78:79]: the lane whose B unit is the partial last unit (L % 16 = s59 != 0)
 
 
 def lu_layout_chunked(spec) -> dict:
@@ -1383,6 +1386,18 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("s_and64", (24, 26, S_PAD)))
     E(Op("s_and64", (S_STA, 26, 26)))
     E(Op("s_and64", (S_STB, 24, 24)))
+    if spec.mode == "dec" and spec.chunked:
+        # L % 16 != 0 (s59 = kernarg word 23): the last unit Lu - 1 is some
+        # lane's unit B; that lane stores it bytewise, the others whole
+        E(Op("s_movk", (S_TAIL, 0)))
+        E(Op("s_movk", (S_TAIL + 1, 0)))
+        E(Op("s_cmp_eq_k_br", (59, 0, ".Lnotail")))
+        E(Op("s_addk", (S_TMP, 12, -1)))
+        E(Op("v_cmp_eq_s", (S_TAIL, S_TMP, V_UB)))
+        E(Op("s_nop", (4,)))
+        E(Op("s_and64", (S_TAIL, S_TAIL, S_STB)))
+        E(Op("s_andn2_64", (S_STB, S_STB, S_TAIL)))
+        E(Op("label", (".Lnotail",)))
     _gen_base(E, V_SRCA, 4, 8, S_OFFS, V_GA, S_TMP2, "r")
     E(Op("v_mad64_k", (V_SRCA, V_UA, 16, V_SRCA)))
     _gen_base(E, V_DSTA, 6, 9, S_OFFS + 2, V_GA, S_TMP2, "d")
@@ -1582,6 +1597,16 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
         E(Op("s_and64", (S_TMP2, S_TMP, S_STB)))
         E(Op("s_exec", (S_TMP2,)))
         E(Op("store16", (a + 2, blk(t, 4), 0, spec.st_policy)))
+        # the partial last unit: bytes [0, L % 16) of the tail lane's unit B
+        E(Op("s_and64", (S_TMP2, S_TMP, S_TAIL)))
+        E(Op("s_exec", (S_TMP2,)))
+        E(Op("s_cbranch_execz", (f".Ltl{t}",)))
+        for b in range(15):
+            E(Op("s_cmp_le_k_br", (59, b, f".Ltl{t}")))
+            E(Op("v_lshr", (V_T, 8 * (b % 4), blk(t, 4 + b // 4))))
+            E(Op("store_byte", (a + 2, V_T, b)))
+            E(Op("s_nop", (0,)))
+        E(Op("label", (f".Ltl{t}",)))
         E(Op("s_exec", (None,)))
     E(Op("label", (".Lst_end",)))
 
@@ -2003,8 +2028,8 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
     tail = [smap & MASK32, smap >> 32, zero & MASK32, zero >> 32] if smap else tail_masks(L)
     words = [src & MASK32, src >> 32, dst & MASK32, dst >> 32, sgs, dgs, srs, drs, (L + 15) // 16, Lv, total,
              magic, shift, n_items, total_waves, s19] + tail
-    if lu is not None:
-        words += [lu[0] & MASK32, lu[0] >> 32, lu[1], 0, tables & MASK32, tables >> 32, 0, 0]
+    if lu is not None:   # word 23: L % 16 (the lane-chunk decode's partial last unit)
+        words += [lu[0] & MASK32, lu[0] >> 32, lu[1], (L % 16) if chunked else 0, tables & MASK32, tables >> 32, 0, 0]
     # generation offset tables (0: strided generations)
     words += [src_offs & MASK32, src_offs >> 32, dst_offs & MASK32, dst_offs >> 32]
     if bound is not None:   # synw: per-generation pass bound table (0: none)
@@ -2473,6 +2498,11 @@ class Emulator:
                 if not idx_mode:
                     raise EmuError("v_xor_rel outside the gpr_idx mode")
                 wv(a[0], rv(a[1] + m0) ^ rv(a[2]))
+            elif n == "store_byte":
+                addr = rv64(a[0])
+                val = rv(a[1])
+                for l in np.nonzero(exec_)[0]:
+                    self.write(int(addr[l]) + a[2], bytes([int(val[l]) & 0xFF]))
             elif n in ("store16_saddr", "store_byte_saddr"):
                 voff, d, sb = a[:3]
                 base = s[sb] | (s[sb + 1] << 32)

@@ -1364,9 +1364,13 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         // fused single-pass decode unless QF_DECODE_SYN=1 asks for the
         // two-kernel syndrome + v_perm combine path
         const char* two = getenv("QF_DECODE_SYN");
-        // (L % 16 != 0: the fused kernel's 16-B stores would pass L; the
-        // syndrome path reads the last unit whole and stores exactly L bytes)
-        if (qf::dec_available(k, r) && !(two && atoi(two)) && L % 16 == 0 && sh->rec_gen_stride < (1ull << 32) &&
+        // (L % 16 != 0: the lane-chunk kernel stores the partial last unit
+        // bytewise but reads it whole, so the rows must start 16-byte aligned;
+        // with generation offset tables that is unknown here)
+        const bool tail_ok = L % 16 == 0 || (qf::dec_name(k, r, L) && !ctx->offs_in &&
+                                             ((uintptr_t)rows | sh->row_stride | sh->rows_gen_stride) % 16 == 0 &&
+                                             std::string(qf::dec_name(k, r, L)).find("decc") != std::string::npos);
+        if (qf::dec_available(k, r) && !(two && atoi(two)) && tail_ok && sh->rec_gen_stride < (1ull << 32) &&
             sh->rec_row_stride < (1ull << 32))
             return decode_fused(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);

@@ -55,7 +55,8 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // then C[J, E] x = s solved in registers by the per-generation LU records of
 // k_decode_prepare_cauchy (lu_out), recovered rows stored to
 // rec + g * rec_gs + rank * rec_rs.  Only the payload bytes [0, L) of a
-// recovered row are written.
+// recovered row are written.  L % 16 != 0 (lane-chunk kernels only): rows are
+// read in whole 16-byte units, so they must start 16-byte aligned.
 bool dec_available(uint32_t k, uint32_t r);
 const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0);
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,

@@ -77,8 +77,9 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     if (idx >= BsCache::kMax) return hipErrorInvalidValue;
     // a partial last unit: enc in the zero-tail lane space (its bytes >= L are
     // masked to zero before the store); syn (the syndrome rows' tail is junk
-    // the combine never stores); never the fused decode (caller rows)
-    if ((L % 16 && (e->mode == 'd' || e->mode == 'c' || (e->mode == 'e' && Lv != s19))) || L < 32 ||
+    // the combine never stores); the lane-chunk decode ('c': the lane holding
+    // the last unit stores it bytewise); never the item-layout decode ('d')
+    if ((L % 16 && (e->mode == 'd' || (e->mode == 'e' && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
         return hipErrorInvalidValue;
@@ -143,6 +144,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[20] = (uint32_t)(uintptr_t)lu;
     a[21] = (uint32_t)((uintptr_t)lu >> 32);
     a[22] = lu_stride;
+    if (e->mode == 'c') a[23] = L % 16;   // bytes of the partial last unit (0: whole)
     a[24] = (uint32_t)(uintptr_t)tab256;
     a[25] = (uint32_t)((uintptr_t)tab256 >> 32);
     // generation offset tables, the last 16 kernarg bytes (bs_codegen S_OFFS)
@@ -256,7 +258,8 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
     if ((uint64_t)G * lu_stride >= (1ull << 40)) return hipErrorInvalidValue;
     // unpadded lane space: the kernel is VALU-bound, padding lanes would be
     // pure extra work (and the recovered rows are caller memory, payload only)
-    return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, L / 16, map_stride, smap, zero,
+    if (L % 16 && e->mode != 'c') return hipErrorInvalidValue;
+    return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, (L + 15) / 16, map_stride, smap, zero,
                   lu, lu_stride, tab256, rows_offs, rec_offs);
 }
 

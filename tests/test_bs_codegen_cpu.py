@@ -317,11 +317,11 @@ def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=Fal
         plans.append((src, E))
     emu = bs.Emulator(bs.generate(spec))
     ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
-    for base, buf in ((ROWS, rows), (OUT, out), (MAP, smap), (ZERO, np.zeros(L, np.uint8)), (REC, recs),
+    for base, buf in ((ROWS, rows), (OUT, out), (MAP, smap), (ZERO, np.zeros((L + 15) // 16 * 16, np.uint8)), (REC, recs),
                       (TAB, bs.split_tables())):
         emu.add_buffer(base, buf)
-    if chunked:
-        Lv = None
+    if chunked:   # (L % 16 != 0: any Lv >= Lu gets past launch_geometry; chunked sets its own)
+        Lv = (L + 15) // 16 if L % 16 else None
         items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
         waves = (items + 3) // 4
     else:
@@ -502,6 +502,9 @@ def test_emulated_offset_tables_encode(oracle):
     (16, 16, 2, 96, 4, 4, 16, False),     # e = r: all 16 blocks
     (5, 3, 1, 64, 9, 5, 0, False),        # nothing erased
     (16, 16, 3, 1200, 2, 7, 13, True),    # the C3 row length (Q = 38: lane-chunks straddle items)
+    (8, 5, 2, 100, 5, 8, None, False),    # L % 16 = 4: the tail lane stores its unit B bytewise
+    (16, 10, 3, 9000, 1, 9, 6, False),    # the C5 jumbo length (Lu = 563, L % 16 = 8)
+    (8, 4, 2, 47, 6, 10, None, True),     # Lu = 3, L % 16 = 15, offset tables
 ])
 def test_emulated_fused_decode_chunked(oracle, k, r, pd, L, G, seed, erase, offs):
     """The lane-chunk fused decode (one generation per lane: units q and
