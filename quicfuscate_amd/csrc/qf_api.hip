@@ -68,6 +68,7 @@ struct qf_ctx {
     // of the class being launched (nullptr: strided generations) and the
     // device / pinned buffers holding a call's per-generation metadata
     const uint64_t* offs_in = nullptr;
+    bool offs_in_al16 = false;  // every generation's input rows (base + offset) start 16-byte aligned
     const uint64_t* offs_out = nullptr;
     uint8_t* d_desc = nullptr;
     size_t desc_bytes = 0;
@@ -497,20 +498,23 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
 // 32 bytes, else k_combine_slots; QF_COMBINE_BS=0 keeps k_combine_slots.  The
 // bit-sliced kernel reads whole 16-byte units, so with L % 16 != 0 its rows
 // must start 16-byte aligned (strided, aligned base and strides).
-static bool combine_bs_ok(const qf::CombineSlotsArgs& a) {
+static bool combine_bs_ok(const qf::CombineSlotsArgs& a, bool offs_al16) {
     const char* on = getenv("QF_COMBINE_BS");
     if ((on && !atoi(on)) || !qf::cmb_available()) return false;
     const char* mq = getenv("QF_COMBINE_BS_MIN_Q");
     const uint32_t min_q = mq ? (uint32_t)atoi(mq) : 64u;
     // (Lu >= 2: the partial last unit is then always some lane's unit B)
     if (a.Lu < 2 || (a.Lu + 1) / 2 < min_q) return false;
-    if (a.L % 16 && (a.rows_offs || ((uintptr_t)a.rows | a.row_stride | a.rows_gen_stride) % 16)) return false;
+    if (a.L % 16 && ((a.rows_offs && !offs_al16) ||
+                     ((uintptr_t)a.rows | a.row_stride | (a.rows_offs ? 0 : a.rows_gen_stride)) % 16))
+        return false;
     return true;
 }
 
 static hipError_t combine_payload(qf_ctx* ctx, const qf::CombineSlotsArgs& a, int PD, hipStream_t st,
                                   std::string* name) {
-    if (combine_bs_ok(a)) {
+    // (rows_offs is the context's input table on the general path only)
+    if (combine_bs_ok(a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16)) {
         if (name) *name = "qf_combine_bs_r16";
         return qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx);
     }
@@ -1366,9 +1370,10 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         const char* two = getenv("QF_DECODE_SYN");
         // (L % 16 != 0: the lane-chunk kernel stores the partial last unit
         // bytewise but reads it whole, so the rows must start 16-byte aligned;
-        // with generation offset tables that is unknown here)
-        const bool tail_ok = L % 16 == 0 || (qf::dec_name(k, r, L) && !ctx->offs_in &&
-                                             ((uintptr_t)rows | sh->row_stride | sh->rows_gen_stride) % 16 == 0 &&
+        // a desc batch's offset tables say so through offs_in_al16)
+        const bool tail_ok = L % 16 == 0 || (qf::dec_name(k, r, L) && (!ctx->offs_in || ctx->offs_in_al16) &&
+                                             ((uintptr_t)rows | sh->row_stride |
+                                              (ctx->offs_in ? 0 : sh->rows_gen_stride)) % 16 == 0 &&
                                              std::string(qf::dec_name(k, r, L)).find("decc") != std::string::npos);
         if (qf::dec_available(k, r) && !(two && atoi(two)) && tail_ok && sh->rec_gen_stride < (1ull << 32) &&
             sh->rec_row_stride < (1ull << 32))
@@ -1675,11 +1680,15 @@ int qf_decode_batch_desc(qf_ctx* ctx, const qf_dec_desc* gens, uint32_t G, const
             QF_CHECK_HIP(qf::launch_desc_gather_index(ia, ctx->stream));
             ctx->offs_in = ro;
             ctx->offs_out = co;
+            bool al = ((uintptr_t)rows % 16) == 0;
+            for (uint32_t i : kv.second) al = al && gens[i].rows_offset % 16 == 0;
+            ctx->offs_in_al16 = al;
         }
         s = decode_batch_impl(ctx, &sh, Gc, rows, ri_ws, nr, nullptr, rec, rec_ws, nrec_ws, st_ws);
         {
             std::lock_guard<std::mutex> g(ctx->mu);
             ctx->offs_in = ctx->offs_out = nullptr;
+            ctx->offs_in_al16 = false;
             if (s != QF_OK) return s;
             qf::DescOutArgs oa{rec_ws, nrec_ws, st_ws, cio, id, rec_index, n_rec, status, emax, Gc};
             QF_CHECK_HIP(qf::launch_desc_scatter_out(oa, ctx->stream));
