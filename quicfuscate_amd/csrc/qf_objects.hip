@@ -73,6 +73,7 @@ struct qf_decoder {
     std::vector<int32_t> sys_slot; // per source index: accepted slot or -1
     std::vector<uint64_t> sys_id;  // per source index: the received packet's own id
     uint32_t accepted = 0;
+    uint32_t uploaded = 0;         // rows [0, uploaded) are on the device
     // decoded output, source index order
     std::vector<uint8_t> out;      // k * stride
     std::vector<uint32_t> out_len;
@@ -434,6 +435,17 @@ static void decoder_assemble(qf_decoder* d, uint32_t L, uint32_t nrec, const uin
 }
 
 // decoder.rs:704-783 for the k accepted rows, on the device.
+// Rows [uploaded, accepted) of the pinned host rows to the device, one copy
+// (rows is pinned and a slot is not rewritten while its decoder lives).
+static int decoder_upload(qf_decoder* d) {
+    if (d->uploaded >= d->accepted) return QF_OK;
+    const size_t o = (size_t)d->uploaded * d->stride, n = (size_t)(d->accepted - d->uploaded) * d->stride;
+    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows + o, d->rows + o, n, hipMemcpyHostToDevice,
+                                (hipStream_t)qf_ctx_stream(d->ctx)));
+    d->uploaded = d->accepted;
+    return QF_OK;
+}
+
 static int decoder_try_decode(qf_decoder* d) {
     const uint32_t k = d->k;
     hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
@@ -443,7 +455,8 @@ static int decoder_try_decode(qf_decoder* d) {
     const uint32_t L = plan.L;
     if (!plan.cauchy)
         QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
-    // the rows are on the device already (uploaded as they arrived)
+    // the rows not on the device yet, in one copy (slots are contiguous)
+    if (int u = decoder_upload(d)) return u;
     QF_CHECK_HIP(hipMemcpyAsync(d->d_index, plan.idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
     qf_decode_shape sh{};
     sh.k = k;
@@ -511,10 +524,8 @@ int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const u
     int32_t q = -1;
     const int s = decoder_accept(d, id, is_systematic, data, len, coeffs, coeff_len, &q);
     if (s != 0 || q < 0) return s;
-    // to the device now; rows is pinned and slot q is not rewritten while
-    // this decoder lives, so the copy needs no wait
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_rows + (size_t)q * d->stride, &d->rows[(size_t)q * d->stride], d->stride,
-                                hipMemcpyHostToDevice, (hipStream_t)qf_ctx_stream(d->ctx)));
+    // the row stays in the pinned host rows until the generation decodes:
+    // one upload of all k rows then, instead of a copy per packet
     if (d->accepted == d->k) {
         int e = decoder_try_decode(d);
         if (e == QF_ERANK) return 0;
@@ -834,8 +845,18 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
     for (uint32_t m = 0; m < M; ++m) {
         DecAdd& x = v[m];
         int32_t q = -1;
+        const uint32_t before = x.d->uploaded;
         x.result = decoder_accept(x.d, x.id, x.is_systematic, x.data, x.len, x.coeffs, x.coeff_len, &q);
         if (q < 0) continue;
+        // rows a per-packet add left on the host go up first (stream order)
+        if (before < (uint32_t)q) {
+            const uint32_t acc = x.d->accepted;
+            x.d->accepted = (uint32_t)q;
+            const int us = decoder_upload(x.d);
+            x.d->accepted = acc;
+            if (us) return us;
+        }
+        x.d->uploaded = (uint32_t)q + 1;   // the scatter below writes slot q
         up.push_back({m, (uint32_t)q});
         pk += round16(x.len);
         if (x.d->accepted == x.d->k) done.push_back(m);
