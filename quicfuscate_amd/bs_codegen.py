@@ -360,6 +360,9 @@ class KernelSpec:
     stagger: tuple = ()
     # lab only: drop the payload row loads (keeps maps, records, compute)
     lab_norows: bool = False
+    # lab only (chunked dec): skip the row loop (the LU phase alone, on whatever
+    # the accumulator registers hold) -- timing of the LU in isolation
+    lab_lu_only: bool = False
     # enc mode, one pass of a code with more repairs than a kernel holds:
     # repairs j0 .. j0 + r - 1 of the Cauchy matrix of (k, r_total)
     r_total: int = 0
@@ -1292,6 +1295,9 @@ def lu_layout_chunked(spec) -> dict:
     while len(cols) < spec.r:
         cols.append(nxt)
         nxt += 4
+    if not spec.lu and not spec.lab_lu_only:   # lab: stores only (record pointer in the dead ring)
+        return {"cols": cols[: spec.r], "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": spec.ring0,
+                "end": top}
     return {"cols": cols[: spec.r], "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": fp,
             "end": max(nxt, fp + 2)}
 
@@ -1465,10 +1471,10 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
             E(Op("load16", (b + 4, V_SRCB, 0, spec.ld_policy)))
         E(Op("s_exec", (None,)))
 
-    n_seq = len(seq)
+    n_seq = 0 if spec.lab_lu_only else len(seq)
     for n in range(min(pd, n_seq)):
         load_row(n)
-    for n, (kind, idx) in enumerate(seq):
+    for n, (kind, idx) in enumerate(seq[:n_seq]):
         if n + pd < n_seq:
             load_row(n + pd)
         after = min(pd, n_seq - 1 - n)

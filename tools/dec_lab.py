@@ -63,7 +63,18 @@ VARIANTS = [
     ("decc_pd2", {"chunked": True, "pd": 2}, ()),
     ("decc_pd4_nolu", {"chunked": True, "pd": 4, "lu": False}, ()),
     ("decc_pd4_2", {"chunked": True, "pd": 4}, ()),
+    # round 2c: warp specialisation test -- the row loop alone with ONE wave per
+    # SIMD (cap = 256 blocks of 4 waves, one per CU) at deeper prefetch, the LU
+    # alone, and both concurrently on two streams (PAIRS): one row-loop wave and
+    # one LU wave per SIMD, the layout a producer/consumer decode would have
+    ("rl_pd3_c1", {"chunked": True, "lu": False, "cap": 256}, ()),
+    ("rl_pd5_c1", {"chunked": True, "lu": False, "pd": 5, "cap": 256}, ()),
+    ("rl_pd6_c1", {"chunked": True, "lu": False, "pd": 6, "cap": 256}, ()),
+    ("rl_pd6", {"chunked": True, "lu": False, "pd": 6}, ()),
+    ("lu_c1", {"chunked": True, "lab_lu_only": True, "cap": 256}, ()),
+    ("lu_full", {"chunked": True, "lab_lu_only": True}, ()),
 ]
+PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]
 
 
 def build():
@@ -81,6 +92,7 @@ def build():
             continue
         kw2 = dict(kw)
         pd = kw2.pop("pd", 3)
+        kw2.pop("cap", None)
         spec = bs.KernelSpec(64, 16, pd, "dec", **kw2)
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"dec_{name}", text.replace(spec.name, f"dec_{name}"), OUT)
@@ -126,7 +138,10 @@ def run(G, reps):
     zero = torch.zeros(4096, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     res = {}
-    for m in json.loads((OUT / "dec_manifest.json").read_text()):
+    prepared = {}
+    s2 = torch.cuda.Stream()
+
+    def prepare(m):
         mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
         data = (OUT / m["hsaco"]).read_bytes()
         buf = ctypes.create_string_buffer(data, len(data))
@@ -138,6 +153,8 @@ def run(G, reps):
         if chunked:
             n_items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
         blocks = (n_items + 3) // 4
+        if m["kw"].get("cap"):
+            blocks = min(blocks, m["kw"]["cap"])
         ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * L, e * L, L, L, L, G, blocks * 4,
                          smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
                          lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr(), chunked=chunked,
@@ -147,10 +164,15 @@ def run(G, reps):
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
                                      ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
 
-        def launch():
-            assert hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(stream.cuda_stream),
+        def launch(st=stream):
+            assert hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(st.cuda_stream),
                                              None, extra) == 0
 
+        prepared[m["name"]] = (launch, mod, (kbuf, size, extra, buf))
+        return launch, n_items
+
+    for m in json.loads((OUT / "dec_manifest.json").read_text()):
+        launch, n_items = prepare(m)
         launch()
         torch.cuda.synchronize()
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -165,6 +187,25 @@ def run(G, reps):
                           "kw": m["kw"],
                           "flags": m["flags"], "vgprs": m["vgprs"]}
         print(m["name"], res[m["name"]], flush=True)
+    for a, b in PAIRS:
+        if a not in prepared or b not in prepared:
+            continue
+        la, lb = prepared[a][0], prepared[b][0]
+        torch.cuda.synchronize()
+        t0, t1, tb = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        t0.record(stream)
+        s2.wait_event(t0)
+        for _ in range(reps):
+            la(stream)
+            lb(s2)
+        tb.record(s2)
+        stream.wait_event(tb)
+        t1.record(stream)
+        torch.cuda.synchronize()
+        ms = t0.elapsed_time(t1) / reps
+        res[f"{a}||{b}"] = {"ms": round(ms, 4)}
+        print(f"{a}||{b}", res[f"{a}||{b}"], flush=True)
+    for launch, mod, _ in prepared.values():
         hip.hipModuleUnload(mod)
     return res
 
