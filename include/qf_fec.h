@@ -266,8 +266,19 @@ int qf_encoder_generate_repairs(qf_encoder *enc, uint32_t first, uint32_t count,
 int qf_encoder_window_len(const qf_encoder *enc);
 
 typedef struct qf_decoder qf_decoder;
-/* replaces decoder.rs:659 Decoder::new(k, pool) */
+/* Largest k of a GF(2^8) decoder: the largest window any mode uses
+ * (Extreme, adaptive.rs:131-133).  k > 256 needs explicit coefficients on
+ * every repair row (the reference's u8 Cauchy rows wrap there). */
+#define QF_DECODER_MAX_K 4096
+/* replaces decoder.rs:659 Decoder::new(k, pool): k <= 256 decodes by
+ * Gauss-Jordan (or the Cauchy kernels), 256 < k <= QF_DECODER_MAX_K by the
+ * Wiedemann strategy (decoder.rs:660-664, 794-975; qf_wiedemann.hip). */
 int qf_decoder_new(qf_ctx *ctx, uint32_t k, uint32_t max_len, qf_decoder **out);
+/* replaces decoder.rs:520-524 DecodingStrategy: 0 GaussianElimination,
+ * 1 Wiedemann, as Decoder::new chose it; QF_EINVAL for NULL. */
+#define QF_STRATEGY_GAUSSIAN 0
+#define QF_STRATEGY_WIEDEMANN 1
+int qf_decoder_strategy(const qf_decoder *dec);
 int qf_decoder_free(qf_decoder *dec);
 /* replaces decoder.rs:678 Decoder::add_packet.  Returns 1 when the generation
  * is decoded, 0 when more packets are needed, QF_EINVAL for a repair packet

@@ -98,6 +98,20 @@ int oracle_decode_generation_as_written(uint32_t k, uint32_t L, uint32_t n_rows,
                                         const uint8_t *row_coeffs,
                                         uint8_t *out, size_t out_stride);
 
+/* decoder.rs:794-975 Decoder::wiedemann_algorithm, the strategy
+ * Decoder::new selects for k > 256 (decoder.rs:659-665), with the two fixes
+ * qf_oracle_wiedemann.c lists (minimal polynomial = reversed connection
+ * polynomial; systematic payloads in B) and a checked solution: init vector
+ * b = 0, 1, ... (decoder.rs:805-807) until A X == B, at most 8 tries.
+ * Same arguments and statuses as oracle_decode_generation, any k <= 65535;
+ * repair rows need row_coeffs unless the reference's u8 Cauchy rows are
+ * defined (otherwise ORACLE_ERANGE, where the reference panics).  *tries
+ * (nullable) = init vectors used. */
+int oracle_wiedemann_decode(uint32_t k, uint32_t L, uint32_t n_rows, const uint16_t *row_index,
+                            const uint8_t *rows, size_t row_stride, const uint8_t *row_coeffs,
+                            uint8_t *out, size_t out_stride, uint8_t *received_mask,
+                            uint32_t *tries);
+
 /* ---- Packet framing (qf_oracle_wire.c, encoder.rs:18-152) --------------
  * One code per reference error string: */
 #define ORACLE_FR_EMPTY (-10)             /* "Raw data is empty" (encoder.rs:25) */

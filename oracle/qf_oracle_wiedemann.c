@@ -1,0 +1,194 @@
+/*
+ * qf_oracle_wiedemann.c -- CPU restatement of the reference's Wiedemann
+ * decoding strategy (decoder.rs:794-975), selected by Decoder::new for
+ * k > 256 (decoder.rs:659-665).
+ *
+ * TEST INFRASTRUCTURE ONLY (see qf_oracle.h): the parity checker for the
+ * library's k > 256 decoder; the product never links or calls it.
+ *
+ * What the reference does (decoder.rs:794-897):
+ *   1. init vectors v_b[i] = (i + b + 1) % 255, b < block = clamp(k/256, 1, 32)
+ *      (decoder.rs:800-809);
+ *   2. block_lanczos_iteration: seq_b[t] = v_b . A^t v_b for t < 2k, A the
+ *      dense k x k coefficient matrix in arrival order (decoder.rs:899-944);
+ *   3. berlekamp_massey(seq_0) (decoder.rs:946-975);
+ *   4. A^-1 = sum_{i>=1} poly[i] / poly[0] * A^(i-1) from explicit powers
+ *      (decoder.rs:856-884), result = A^-1 * B with B the payload matrix
+ *      (decoder.rs:886-887); missing systematic i <- result row i, id i,
+ *      len = the longest payload (decoder.rs:823-830, 889-905).
+ *
+ * Two defects of the as-written code are fixed here, as in the library:
+ *   (a) berlekamp_massey returns the connection polynomial C(x) = 1 + c_1 x +
+ *       ... + c_L x^L, but step 4 needs the minimal polynomial with its
+ *       constant term first, f(x) = x^L C(1/x) (f_i = c_{L-i}).  Its check
+ *       `poly[0] == 0` (decoder.rs:852) can then never fire, because C(0) = 1;
+ *       with f, f_0 = c_L = 0 means x | f, so A is singular.
+ *   (b) systematic rows carry their payloads into B (the F4 fix of the
+ *       Gauss-Jordan path; decoder.rs:692 appends them with None).
+ * A scalar projection can yield a proper divisor of A's minimal polynomial,
+ * which gives a wrong "inverse"; the reference does not check.  Here the
+ * solution is checked (A X == B) and the next init vector b tried, up to
+ * ORACLE_W_TRIES; every try failing reports ERANK.
+ *
+ * Efficiency choices (same results): A v uses the identity rows sparsely,
+ * and sum_i f_i A^(i-1) B runs by Horner on B instead of forming powers.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "qf_oracle.h"
+
+#define ORACLE_W_TRIES 8
+
+/* A v for the accepted rows: identity rows read one entry, repair rows are dense. */
+static void matvec(uint32_t k, const int32_t *sys, const uint8_t *coef, const uint8_t *v, uint8_t *out) {
+    for (uint32_t q = 0; q < k; ++q) {
+        if (sys[q] >= 0) {
+            out[q] = v[sys[q]];
+            continue;
+        }
+        const uint8_t *a = coef + (size_t)q * k;
+        uint8_t acc = 0;
+        for (uint32_t c = 0; c < k; ++c)
+            if (a[c]) acc ^= oracle_gf_mul(a[c], v[c]);
+        out[q] = acc;
+    }
+}
+
+/* decoder.rs:946-975, standard form: returns L and the connection polynomial
+ * c[0..L] (c[0] = 1) with s[i] = sum_{j=1..L} c[j] s[i-j]. */
+static uint32_t berlekamp_massey(const uint8_t *s, uint32_t n, uint8_t *c) {
+    uint8_t *b = (uint8_t *)calloc(n + 1, 1), *t = (uint8_t *)malloc(n + 1);
+    memset(c, 0, n + 1);
+    c[0] = 1;
+    b[0] = 1;
+    uint32_t L = 0, m = 1;
+    uint8_t bd = 1;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint8_t d = s[i];
+        for (uint32_t j = 1; j <= L; ++j) d ^= oracle_gf_mul(c[j], s[i - j]);
+        if (d == 0) {
+            ++m;
+            continue;
+        }
+        uint8_t binv;
+        oracle_gf_inv(bd, &binv);
+        const uint8_t coef = oracle_gf_mul(d, binv);
+        memcpy(t, c, n + 1);
+        for (uint32_t j = 0; j + m <= n; ++j) c[j + m] ^= oracle_gf_mul(coef, b[j]);
+        if (2 * L <= i) {
+            L = i + 1 - L;
+            memcpy(b, t, n + 1);
+            bd = d;
+            m = 1;
+        } else {
+            ++m;
+        }
+    }
+    free(b);
+    free(t);
+    return L;
+}
+
+int oracle_wiedemann_decode(uint32_t k, uint32_t L, uint32_t n_rows, const uint16_t *row_index,
+                            const uint8_t *rows, size_t row_stride, const uint8_t *row_coeffs,
+                            uint8_t *out, size_t out_stride, uint8_t *received_mask,
+                            uint32_t *tries) {
+    oracle_gf_init();
+    if (k == 0 || k > 65535) return ORACLE_EINVAL;
+    int32_t *sys = (int32_t *)malloc(sizeof(int32_t) * k);
+    uint32_t *slot = (uint32_t *)malloc(sizeof(uint32_t) * k);
+    uint8_t *present = (uint8_t *)calloc(k, 1);
+    uint8_t *coef = (uint8_t *)calloc((size_t)k, k);
+    uint8_t *B = (uint8_t *)calloc((size_t)k, L ? L : 1);
+    uint8_t *X = (uint8_t *)calloc((size_t)k, L ? L : 1);
+    uint8_t *T = (uint8_t *)calloc((size_t)k, L ? L : 1);
+    uint8_t *col = (uint8_t *)malloc(k), *col2 = (uint8_t *)malloc(k);
+    uint8_t *v = (uint8_t *)malloc(k), *w = (uint8_t *)malloc(k), *u = (uint8_t *)malloc(k);
+    uint8_t *seq = (uint8_t *)malloc(2 * (size_t)k), *cp = (uint8_t *)malloc(2 * (size_t)k + 1);
+    int status = ORACLE_OK;
+    uint32_t n = 0;
+    if (tries) *tries = 0;
+    /* Decoder::add_packet (decoder.rs:678-701): first k rows, duplicates dropped */
+    for (uint32_t s = 0; s < n_rows && n < k; ++s) {
+        const uint32_t idx = row_index[s];
+        if (idx < k) {
+            if (present[idx]) continue;
+            present[idx] = 1;
+            sys[n] = (int32_t)idx;
+        } else {
+            sys[n] = -1;
+            uint8_t *a = coef + (size_t)n * k;
+            if (row_coeffs) {
+                memcpy(a, row_coeffs + (size_t)s * k, k);
+            } else {   /* decoder.rs:283-296 as written: u8 arithmetic, gf_inv(0) panics */
+                const uint8_t y = (uint8_t)(k + (idx - k));
+                for (uint32_t i = 0; i < k; ++i)
+                    if (oracle_gf_inv((uint8_t)((uint8_t)i ^ y), &a[i]) != 0) { status = ORACLE_ERANGE; goto done; }
+            }
+        }
+        memcpy(B + (size_t)n * L, rows + (size_t)s * row_stride, L);   /* fix (b) */
+        slot[n++] = s;
+    }
+    if (n < k) { status = ORACLE_ENOTREADY; goto done; }
+    status = ORACLE_ERANK;
+    for (uint32_t b = 0; b < ORACLE_W_TRIES; ++b) {
+        if (tries) *tries = b + 1;
+        for (uint32_t i = 0; i < k; ++i) u[i] = (uint8_t)((i + b + 1) % 255);   /* decoder.rs:805-807 */
+        memcpy(v, u, k);
+        for (uint32_t t = 0; t < 2 * k; ++t) {   /* decoder.rs:934-941 */
+            uint8_t dot = 0;
+            for (uint32_t i = 0; i < k; ++i) dot ^= oracle_gf_mul(u[i], v[i]);
+            seq[t] = dot;
+            matvec(k, sys, coef, v, w);
+            memcpy(v, w, k);
+        }
+        const uint32_t Ld = berlekamp_massey(seq, 2 * k, cp);
+        if (Ld == 0) continue;            /* zero sequence: this projection says nothing */
+        /* fix (a): f_i = c_{L-i}; f_0 = c_L */
+        const uint8_t f0 = cp[Ld];
+        if (f0 == 0) break;               /* x | minimal polynomial: A singular */
+        uint8_t f0inv;
+        oracle_gf_inv(f0, &f0inv);
+        /* X = f0^-1 sum_{i=1..L} f_i A^(i-1) B, Horner: Y = f_L B; Y = A Y + f_i B */
+        for (size_t q = 0; q < (size_t)k * L; ++q) X[q] = oracle_gf_mul(cp[0], B[q]);
+        for (uint32_t i = Ld - 1; i >= 1; --i) {
+            const uint8_t fi = cp[Ld - i];
+            for (uint32_t t = 0; t < L; ++t) {
+                for (uint32_t q = 0; q < k; ++q) col[q] = X[(size_t)q * L + t];
+                matvec(k, sys, coef, col, col2);
+                for (uint32_t q = 0; q < k; ++q)
+                    T[(size_t)q * L + t] = col2[q] ^ oracle_gf_mul(fi, B[(size_t)q * L + t]);
+            }
+            memcpy(X, T, (size_t)k * L);
+        }
+        for (size_t q = 0; q < (size_t)k * L; ++q) X[q] = oracle_gf_mul(f0inv, X[q]);
+        /* the check the reference omits: A X == B */
+        int ok = 1;
+        for (uint32_t t = 0; t < L && ok; ++t) {
+            for (uint32_t q = 0; q < k; ++q) col[q] = X[(size_t)q * L + t];
+            matvec(k, sys, coef, col, col2);
+            for (uint32_t q = 0; q < k; ++q)
+                if (col2[q] != B[(size_t)q * L + t]) { ok = 0; break; }
+        }
+        /* and the inverse polynomial on u itself (the whole check when L == 0) */
+        for (uint32_t q = 0; q < k; ++q) v[q] = oracle_gf_mul(cp[0], u[q]);
+        for (uint32_t i = Ld - 1; i >= 1; --i) {
+            matvec(k, sys, coef, v, w);
+            for (uint32_t q = 0; q < k; ++q) v[q] = w[q] ^ oracle_gf_mul(cp[Ld - i], u[q]);
+        }
+        for (uint32_t q = 0; q < k; ++q) v[q] = oracle_gf_mul(f0inv, v[q]);
+        matvec(k, sys, coef, v, w);
+        if (memcmp(w, u, k) != 0) ok = 0;
+        if (ok) { status = ORACLE_OK; break; }
+    }
+    if (status == ORACLE_OK)
+        for (uint32_t i = 0; i < k; ++i) {
+            memcpy(out + (size_t)i * out_stride, X + (size_t)i * L, L);
+            if (received_mask) received_mask[i] = present[i];
+        }
+done:
+    free(sys); free(slot); free(present); free(coef); free(B); free(X); free(T);
+    free(col); free(col2); free(v); free(w); free(u); free(seq); free(cp);
+    return status;
+}

@@ -127,6 +127,7 @@ _SIGS = {
     "qf_decoder_free": (_I, [_P]),
     "qf_decoder_add_packet": (_I, [_P, _U64, _I, _P, _U32, _P, _U32]),
     "qf_decoder_is_decoded": (_I, [_P]),
+    "qf_decoder_strategy": (_I, [_P]),
     "qf_decoder_get_decoded_packets": (_I, [_P, _P, _U32, _P, _P, _P]),
     "qf_packet_to_raw": (_I, [_I, _P, _U32, _P, _U32, _P, _U32, _P]),
     "qf_packet_from_raw": (_I, [_P, _U32, _P, _P, _P, _P, _P]),

@@ -894,6 +894,7 @@ int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out) {
     *out = ctx->send_ev.data();
     return QF_OK;
 }
+const uint32_t* ctx_tab256(qf_ctx* ctx) { return ctx->d_tab256; }
 int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
     int s = grow_work(ctx, bytes);
     if (s) return s;

@@ -21,6 +21,8 @@ int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out);
 // GF(2^16) tables on the device, built on first use: log[65536] (log[0] =
 // 0xFFFF, no product) and exp[2 * 65535] (exp[i + 65535] = exp[i]).
 int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp);
+// The context's 256 split-table records (8 dwords each, gf256_tables.h).
+const uint32_t* ctx_tab256(qf_ctx* ctx);
 // qf_ctx_profile bracketing of a launch.
 hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st);
 void ctx_prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t ev, const std::string& name);
@@ -106,5 +108,17 @@ struct DecAdd {
     int result;
 };
 int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M);
+
+// The k > 256 strategy of the GF(2^8) decoder (qf_wiedemann.hip,
+// decoder.rs:794-975): k accepted rows on the device (slot q at q * stride,
+// zero padded), e of them repairs with coefficient rows A_ek (e x k, host, in
+// repair order), E the e erased sources ascending (host), slot[q] = source
+// index of a systematic slot or 0x80000000 | repair ordinal (host).  Writes
+// recovered row t (source E[t]) to d_rec + t * stride (L bytes, zero padded
+// to 16).  QF_ERANK when the system is singular.  Takes the context lock;
+// asynchronous on the context stream once it returns QF_OK.
+int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, const uint16_t* E,
+                     const uint32_t* slot, const uint8_t* d_rows, uint64_t stride, uint32_t L, uint8_t* d_rec,
+                     uint32_t* tries_out);
 
 }  // namespace qf

@@ -86,6 +86,10 @@ struct qf_decoder {
     uint32_t* d_nrec = nullptr;
     int32_t* d_status = nullptr;
     uint8_t* h_rec = nullptr;       // pinned download of the recovered rows
+    // k > 256 (Wiedemann strategy): recovered rows, grown to e rows on demand
+    uint8_t* d_wrec = nullptr;
+    uint32_t wrec_rows = 0;
+    uint32_t w_tries = 0;           // init vectors the last Wiedemann solve used
 };
 
 namespace {
@@ -313,7 +317,8 @@ int qf_encoder_generate_repair_packet(qf_encoder* e, uint32_t j, uint8_t* out_da
 }
 
 int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) {
-    if (!ctx || !out || k == 0 || k > 256 || max_len == 0) return QF_EINVAL;
+    if (!ctx || !out || k == 0 || k > QF_DECODER_MAX_K || max_len == 0) return QF_EINVAL;
+    const bool wied = k > 256;   // decoder.rs:660-664
     qf_decoder* d = new qf_decoder();
     d->ctx = ctx;
     d->k = k;
@@ -326,7 +331,7 @@ int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) 
     d->sys_id.assign(k, 0);
     const uint32_t emax = k < 128 ? k : 128;
     bool ok = hipMalloc(&d->d_rows, (size_t)k * d->stride) == hipSuccess &&
-              hipMalloc(&d->d_coeffs, (size_t)k * k) == hipSuccess &&
+              (wied || hipMalloc(&d->d_coeffs, (size_t)k * k) == hipSuccess) &&
               hipMalloc(&d->d_index, (size_t)k * 2) == hipSuccess &&
               hipMalloc(&d->d_rec, (size_t)emax * d->stride) == hipSuccess &&
               hipMalloc(&d->d_rec_index, (size_t)emax * 2) == hipSuccess &&
@@ -350,6 +355,7 @@ int qf_decoder_free(qf_decoder* d) {
     hipFree(d->d_rec_index);
     hipFree(d->d_nrec);
     hipFree(d->d_status);
+    hipFree(d->d_wrec);
     if (d->rows) {
         hipStreamSynchronize((hipStream_t)qf_ctx_stream(d->ctx));  // row uploads in flight
         hipHostFree(d->rows);
@@ -360,6 +366,11 @@ int qf_decoder_free(qf_decoder* d) {
 }
 
 int qf_decoder_is_decoded(const qf_decoder* d) { return d ? (d->decoded ? 1 : 0) : QF_EINVAL; }
+
+int qf_decoder_strategy(const qf_decoder* d) {
+    if (!d) return QF_EINVAL;
+    return d->k > 256 ? QF_STRATEGY_WIEDEMANN : QF_STRATEGY_GAUSSIAN;
+}
 
 // How the k accepted rows decode (decoder.rs:704-783): repair rows that are
 // Cauchy rows of this k (c_i = gf_inv(i ^ y), y = k + j: what Encoder emits
@@ -446,8 +457,55 @@ static int decoder_upload(qf_decoder* d) {
     return QF_OK;
 }
 
+// decoder.rs:794-975 for k > 256: the k accepted rows are k - e systematic
+// rows and e repair rows; Wiedemann on the e x e block of the erased sources
+// (qf_wiedemann.hip), then the recovered rows down.
+static int decoder_try_decode_wiedemann(qf_decoder* d) {
+    const uint32_t k = d->k;
+    hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
+    uint32_t L = 0;
+    for (uint32_t q = 0; q < k; ++q) L = d->lens[q] > L ? d->lens[q] : L;
+    std::vector<uint16_t> E;
+    for (uint32_t i = 0; i < k; ++i)
+        if (d->sys_slot[i] < 0) E.push_back((uint16_t)i);
+    const uint32_t e = (uint32_t)E.size();
+    if (e == 0) {   // every source arrived
+        decoder_assemble(d, L == 0 ? 1 : L, 0, nullptr, nullptr, 0);
+        return QF_OK;
+    }
+    std::vector<uint32_t> slot(k);
+    std::vector<uint8_t> A((size_t)e * k);
+    uint32_t p = 0;
+    for (uint32_t q = 0; q < k; ++q) {
+        if (d->index[q] == k) {
+            memcpy(&A[(size_t)p * k], &d->coeffs[(size_t)q * k], k);
+            slot[q] = 0x80000000u | p++;
+        } else {
+            slot[q] = d->index[q];
+        }
+    }
+    if (p != e) return QF_EINVAL;   // k accepted rows: #repairs == #erased
+    if (int u = decoder_upload(d)) return u;
+    if (d->wrec_rows < e) {
+        hipFree(d->d_wrec);
+        d->d_wrec = nullptr;
+        d->wrec_rows = 0;
+        QF_CHECK_HIP(hipMalloc(&d->d_wrec, (size_t)e * d->stride));
+        d->wrec_rows = e;
+    }
+    const int s = qf::wiedemann_decode(d->ctx, k, e, A.data(), E.data(), slot.data(), d->d_rows, d->stride, L,
+                                   d->d_wrec, &d->w_tries);
+    if (s != QF_OK) return s;   // QF_ERANK: singular, stays undecoded (decoder.rs:852-854)
+    std::vector<uint8_t> rec((size_t)e * d->stride);
+    QF_CHECK_HIP(hipMemcpyAsync(rec.data(), d->d_wrec, rec.size(), hipMemcpyDeviceToHost, st));
+    QF_CHECK_HIP(hipStreamSynchronize(st));
+    decoder_assemble(d, L == 0 ? 1 : L, e, E.data(), rec.data(), d->stride);
+    return QF_OK;
+}
+
 static int decoder_try_decode(qf_decoder* d) {
     const uint32_t k = d->k;
+    if (k > 256) return decoder_try_decode_wiedemann(d);
     hipStream_t st = (hipStream_t)qf_ctx_stream(d->ctx);
     const uint32_t emax = k < 128 ? k : 128;
     DecPlan plan;

@@ -420,7 +420,9 @@ class Encoder:
 
 
 class Decoder:
-    """decoder.rs:658-791 Decoder (first k rows win, systematic id % k)."""
+    """decoder.rs:658-791 Decoder (first k rows win, systematic id % k).
+    k <= 256 decodes by Gauss-Jordan / the Cauchy kernels, k > 256 by the
+    Wiedemann strategy (decoder.rs:660-664, 794-975), as Decoder::new picks."""
 
     def __init__(self, k: int, pool: Optional[MemoryPool] = None, max_len: int = 4096,
                  ctx: Optional[Context] = None):
@@ -434,6 +436,12 @@ class Decoder:
     @property
     def is_decoded(self) -> bool:
         return bool(check(L._lib().qf_decoder_is_decoded(self.handle)))
+
+    @property
+    def strategy(self) -> str:
+        """decoder.rs:520-524 DecodingStrategy chosen by Decoder::new."""
+        s = check(L._lib().qf_decoder_strategy(self.handle))
+        return "Wiedemann" if s == 1 else "GaussianElimination"
 
     def add_packet(self, packet: Packet) -> bool:
         """Returns is_decoded; raises for a repair packet without coefficients."""

@@ -37,6 +37,7 @@ _lib.oracle_encode_window.argtypes = [_U32, _U32, _U32, _P, _SZ, _P, _P, _SZ]
 _lib.oracle_encode_window_clmul_fold.argtypes = [_U32, _U32, _U32, _P, _SZ, _P, _P, _SZ]
 _lib.oracle_decode_generation.argtypes = [_U32, _U32, _U32, _P, _P, _SZ, _P, _P, _SZ, _P]
 _lib.oracle_decode_generation_as_written.argtypes = [_U32, _U32, _U32, _P, _P, _SZ, _P, _P, _SZ]
+_lib.oracle_wiedemann_decode.argtypes = [_U32, _U32, _U32, _P, _P, _SZ, _P, _P, _SZ, _P, _P]
 _lib.oracle_fill_splitmix.argtypes = [_P, _SZ, ctypes.c_uint64, ctypes.c_uint64]
 _lib.oracle_gf_init()
 
@@ -144,6 +145,22 @@ def decode(k: int, row_index, rows: np.ndarray, row_coeffs: np.ndarray | None = 
     rc = None if row_coeffs is None else np.ascontiguousarray(row_coeffs, dtype=np.uint8)
     s = _lib.oracle_decode_generation(k, L, n, _p(ri), _p(rows), L, _p(rc), _p(out), out.shape[1], _p(mask))
     return s, out[:, :L], mask
+
+
+def wiedemann(k: int, row_index, rows: np.ndarray, row_coeffs: np.ndarray | None = None):
+    """decoder.rs:794-975 (fixed, checked; oracle/qf_oracle_wiedemann.c): rows
+    (n, L) in arrival order, row_coeffs (n, k) for repair rows -> (status, out
+    (k, L), received mask, init vectors tried)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    n, L = rows.shape
+    ri = np.ascontiguousarray(row_index, dtype=np.uint16)
+    out = np.zeros((k, max(L, 1)), np.uint8)
+    mask = np.zeros(k, np.uint8)
+    tries = ctypes.c_uint32(0)
+    rc = None if row_coeffs is None else np.ascontiguousarray(row_coeffs, dtype=np.uint8)
+    s = _lib.oracle_wiedemann_decode(k, L, n, _p(ri), _p(rows), L, _p(rc), _p(out), out.shape[1], _p(mask),
+                                     ctypes.byref(tries))
+    return s, out[:, :L], mask, int(tries.value)
 
 
 def decode_as_written(k: int, row_index, rows: np.ndarray):
