@@ -168,7 +168,7 @@ def test_received_ids_kept(qf, gpu_ctx):
     k, L = 270, 16
     rng = np.random.default_rng(3)
     src = rng.integers(0, 256, (k, L), dtype=np.uint8)
-    ids = [5000 + 270 * 2 + i for i in range(k)]   # id % k == i
+    ids = [k * 20 + i for i in range(k)]   # id % k == i, id != i
     assert all(x % k == i for i, x in enumerate(ids))
     lost = {0, 269}
     coef = rng.integers(1, 256, (2, k), dtype=np.uint8)
