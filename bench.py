@@ -370,9 +370,16 @@ def main(argv=None):
             except Exception:
                 traffic = None
         # the roof priced is HBM (byte work, no MFMA); what actually limits the
-        # kernel comes from its SQ counters (profiles/*_sq_counters.json): the
-        # fused decode and the multi-pass shapes are VALU-issue-bound
-        limiter = "valu_issue" if name.startswith(("qf_cauchy_dec", "k_combine", "k_decode_prepare")) else "hbm"
+        # kernel comes from its SQ counters and the decode lab (DESIGN 3.2,
+        # profiles/r02d_lab_dec_ws.json): the fused decode's row loop alone is
+        # HBM-bound (1.19 ms), its per-lane LU phase (0.58 ms alone, v_perm
+        # products) is not hidden behind the row loads at two waves per SIMD
+        if name.startswith("qf_cauchy_dec"):
+            limiter = "lu_phase_not_hidden"
+        elif name.startswith(("k_combine", "k_decode_prepare")):
+            limiter = "valu_issue"
+        else:
+            limiter = "hbm"
         return {"kernel": name, "launch_ms": round(ms, 4), "bound": "hbm", "limiter": limiter,
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
