@@ -14,22 +14,27 @@
 //                  (the reference uses the connection polynomial itself, so
 //                  its singularity test poly[0] == 0 never fires: fix (a) in
 //                  oracle/qf_oracle_wiedemann.c);
-//   k_w8_horner    W = f_0^-1 sum_{i>=1} f_i M^(i-1), Horner, one launch per
+//   k_w8_rows      row combinations with wave-uniform coefficients (split-table
+//                  v_perm products), three uses:
+//                  W = f_0^-1 sum_{i>=1} f_i M^(i-1) by Horner, one launch per
 //                  degree (decoder.rs:856-884 sums explicit powers instead);
-//   k_w8_verify    M W == I.  The reference does not check; a projection whose
-//                  sequence misses a factor of M's minimal polynomial gives a
-//                  wrong W, so the host tries the next init vector b;
-//   k_w8_dmat      D = W [A_J on the received sources | I on the repair slots]:
-//                  the e x k recovery matrix over the accepted slots;
-//   k_w8_apply     recovered rows = D . rows (decoder.rs:886-887), split over
-//                  slot chunks and combined with 32-bit atomic XOR.
+//                  the check M W == I (the reference does not check: a
+//                  projection whose sequence misses a factor of M's minimal
+//                  polynomial gives a wrong W, so the host tries the next init
+//                  vector b); and G = W A_J;
+//   k_w8_apply     recovered rows = D . rows (decoder.rs:886-887) with
+//                  D[t][q] = W[t][p] on repair slot q (ordinal p) and G[t][s]
+//                  on the systematic slot of source s, split over slot chunks
+//                  and combined with 32-bit atomic XOR.
 // Systematic rows take part with their payloads (the F4 fix, as on the
-// Gauss-Jordan path).  Products in the small kernels use log/exp tables
-// built in LDS; the payload pass uses the context's split tables (v_perm).
+// Gauss-Jordan path).  The sequence kernel multiplies in the log domain
+// (tables built in LDS, M kept as logs); the others use the context's split
+// tables (v_perm).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -61,31 +66,6 @@ __device__ __forceinline__ uint32_t gf_mul_slow(uint32_t a, uint32_t b) {
     return r;
 }
 
-// exp[0..509] (exp[i + 255] = exp[i]), log[1..255]; threads < 255 each build one entry.
-__device__ void build_tables(uint8_t* ex, uint8_t* lg) {
-    const uint32_t i = threadIdx.x;
-    if (i < 255) {
-        uint32_t x = 1, base = 2, n = i;
-        while (n) {
-            if (n & 1) x = gf_mul_slow(x, base);
-            base = gf_mul_slow(base, base);
-            n >>= 1;
-        }
-        ex[i] = (uint8_t)x;
-        ex[i + 255] = (uint8_t)x;
-        lg[x] = (uint8_t)i;
-    }
-    if (i == 0) {
-        lg[0] = 0;
-        ex[510] = ex[511] = 0;
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ uint32_t gmul(const uint8_t* ex, const uint8_t* lg, uint32_t a, uint32_t b) {
-    return (a && b) ? ex[(uint32_t)lg[a] + lg[b]] : 0u;
-}
-
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
@@ -109,38 +89,66 @@ struct SeqArgs {
     const uint16_t* E;    // e erased sources, ascending
     uint8_t* M;           // e x ep (out)
     uint8_t* P;           // e x ep (out): identity, the Horner start (f_L = 1)
+    uint16_t* LMg;        // e x ep logs of M (global, when they do not fit LDS)
     uint8_t* poly;        // f_0..f_L (out)
     int32_t* info;        // [0] L, [1] 0 ok / 1 zero sequence / 2 singular
     uint32_t e, ep, kp, b;
-    uint32_t m_lds;       // M also staged in LDS (e * e bytes after the vectors)
+    uint32_t lm_lds;      // logs of M in LDS (2 e^2 bytes after the vectors)
 };
+
+constexpr uint32_t kLogZero = 0x200;     // log of 0: every sum with it indexes a zero
+constexpr uint32_t kEx2 = 1040;          // exp over [0, 510), zero above
+
+// Log-domain tables: ex2[lg[a] + lg[b]] = a * b for all a, b (lg[0] = kLogZero).
+__device__ void build_log_tables(uint8_t* ex2, uint16_t* lg) {
+    for (uint32_t i = threadIdx.x; i < kEx2; i += blockDim.x) {
+        uint32_t x = 0;
+        if (i < 510) {
+            uint32_t base = 2, n = i % 255;
+            x = 1;
+            while (n) {
+                if (n & 1) x = gf_mul_slow(x, base);
+                base = gf_mul_slow(base, base);
+                n >>= 1;
+            }
+            if (i < 255) lg[x] = (uint16_t)i;
+        }
+        ex2[i] = (uint8_t)x;
+    }
+    if (threadIdx.x == 0) lg[0] = kLogZero;
+    __syncthreads();
+}
 
 __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t e = a.e, n = 2 * e, tid = threadIdx.x, nt = blockDim.x;
-    uint8_t* ex = lds;
-    uint8_t* lg = ex + 512;
-    uint32_t* red = reinterpret_cast<uint32_t*>(lg + 256);   // 16 words
-    uint8_t* u = lg + 256 + 64;
-    uint8_t* v = u + e;
+    uint8_t* ex2 = lds;
+    uint16_t* lg = reinterpret_cast<uint16_t*>(lds + kEx2);            // 256
+    uint32_t* red = reinterpret_cast<uint32_t*>(lds + kEx2 + 512);     // 16 words
+    uint16_t* lu = reinterpret_cast<uint16_t*>(lds + kEx2 + 512 + 64);
+    uint16_t* lv = lu + e;
+    uint16_t* LMl = lv + e;                                            // e * e when lm_lds
+    uint8_t* v = reinterpret_cast<uint8_t*>(a.lm_lds ? LMl + (size_t)e * e : LMl);
     uint8_t* w = v + e;
     uint8_t* seq = w + e;
     uint8_t* C = seq + n;
     uint8_t* B = C + n + 1;
     uint8_t* T = B + n + 1;
-    uint8_t* Ml = T + n + 1;
-    build_tables(ex, lg);
-    // M[i][j] = A[i][E[j]]; P = I
+    build_log_tables(ex2, lg);
+    uint16_t* LM = a.lm_lds ? LMl : a.LMg;
+    const uint32_t lmp = a.lm_lds ? e : a.ep;
+    // M[i][j] = A[i][E[j]], its logs; P = I
     for (uint32_t q = tid; q < e * e; q += nt) {
         const uint32_t i = q / e, j = q - i * e;
         const uint8_t mij = a.A[(size_t)i * a.kp + a.E[j]];
         a.M[(size_t)i * a.ep + j] = mij;
         a.P[(size_t)i * a.ep + j] = i == j ? 1 : 0;
-        if (a.m_lds) Ml[q] = mij;
+        LM[(size_t)i * lmp + j] = lg[mij];
     }
     for (uint32_t i = tid; i < e; i += nt) {
-        u[i] = (uint8_t)((i + a.b + 1) % 255);
-        v[i] = u[i];
+        const uint8_t ui = (uint8_t)((i + a.b + 1) % 255);
+        lu[i] = lg[ui];
+        v[i] = ui;
     }
     for (uint32_t i = tid; i <= n; i += nt) {
         C[i] = i == 0;
@@ -148,41 +156,59 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
     }
     __threadfence_block();
     __syncthreads();
-    // a_t = u . M^t u
+    // a_t = u . M^t u.  Row i of M v takes S threads (a power of two <= 64,
+    // S = nt / e rounded down), combined by shuffles inside the wave.
+    uint32_t S = 1;
+    while (S * 2 <= 64 && S * 2 * e <= nt) S *= 2;
+    const uint32_t rows_per_pass = nt / S;
     for (uint32_t t = 0; t < n; ++t) {
+        for (uint32_t i = tid; i < e; i += nt) lv[i] = lg[v[i]];
+        __syncthreads();
         uint32_t d = 0;
-        for (uint32_t i = tid; i < e; i += nt) d ^= gmul(ex, lg, u[i], v[i]);
+        for (uint32_t i = tid; i < e; i += nt) d ^= ex2[lu[i] + lv[i]];
         d = block_xor(d, red);
         if (tid == 0) seq[t] = (uint8_t)d;
-        for (uint32_t i = tid; i < e; i += nt) {
-            const uint8_t* m = a.m_lds ? Ml + (size_t)i * e : a.M + (size_t)i * a.ep;
+        for (uint32_t i0 = 0; i0 < e; i0 += rows_per_pass) {
+            const uint32_t i = i0 + tid / S, s0 = tid % S;
             uint32_t acc = 0;
-            for (uint32_t j = 0; j < e; ++j) acc ^= gmul(ex, lg, m[j], v[j]);
-            w[i] = (uint8_t)acc;
+            if (i < e) {
+                const uint16_t* m = LM + (size_t)i * lmp;
+                uint32_t j = s0;
+                for (; j + 3 * S < e; j += 4 * S)
+                    acc ^= ex2[m[j] + lv[j]] ^ ex2[m[j + S] + lv[j + S]] ^ ex2[m[j + 2 * S] + lv[j + 2 * S]] ^
+                           ex2[m[j + 3 * S] + lv[j + 3 * S]];
+                for (; j < e; j += S) acc ^= ex2[m[j] + lv[j]];
+            }
+            for (uint32_t o = 1; o < S; o <<= 1) acc ^= __shfl_xor(acc, o, 64);
+            if (i < e && s0 == 0) w[i] = (uint8_t)acc;
         }
         __syncthreads();
         for (uint32_t i = tid; i < e; i += nt) v[i] = w[i];
         __syncthreads();
     }
-    // Berlekamp-Massey: s[i] = sum_{j=1..L} C[j] s[i-j]
+    // Berlekamp-Massey on wave 0 alone (the other waves end here, so its
+    // barriers wait for nobody): s[i] = sum_{j=1..L} C[j] s[i-j]
+    if (tid >= 64) return;
+    const uint32_t nw = 64;
     uint32_t L = 0, m = 1, bd = 1;
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t d = 0;
-        for (uint32_t j = 1 + tid; j <= L; j += nt) d ^= gmul(ex, lg, C[j], seq[i - j]);
-        d = block_xor(d, red) ^ seq[i];
+        for (uint32_t j = 1 + tid; j <= L; j += nw) d ^= ex2[lg[C[j]] + lg[seq[i - j]]];
+        d = wave_xor(d) ^ seq[i];
         if (d == 0) {
             ++m;
             continue;
         }
-        const uint32_t coef = ex[(uint32_t)lg[d] + 255u - lg[bd]];   // d / bd
+        const uint32_t coef = ex2[(uint32_t)lg[d] + 255u - lg[bd]];   // d / bd
+        const uint32_t lc = lg[coef];
         const bool grow = 2 * L <= i;
         if (grow)
-            for (uint32_t j = tid; j <= n; j += nt) T[j] = C[j];
+            for (uint32_t j = tid; j <= n; j += nw) T[j] = C[j];
         __syncthreads();
-        for (uint32_t j = tid; j + m <= n; j += nt) C[j + m] ^= (uint8_t)gmul(ex, lg, coef, B[j]);
+        for (uint32_t j = tid; j + m <= n; j += nw) C[j + m] ^= ex2[lc + lg[B[j]]];
         __syncthreads();
         if (grow) {
-            for (uint32_t j = tid; j <= n; j += nt) B[j] = T[j];
+            for (uint32_t j = tid; j <= n; j += nw) B[j] = T[j];
             __syncthreads();
             L = i + 1 - L;
             bd = d;
@@ -192,82 +218,10 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
         }
     }
     // f_i = C[L - i]
-    for (uint32_t i = tid; i <= L; i += nt) a.poly[i] = C[L - i];
+    for (uint32_t i = tid; i <= L; i += nw) a.poly[i] = C[L - i];
     if (tid == 0) {
         a.info[0] = (int32_t)L;
         a.info[1] = L == 0 ? 1 : (C[L] == 0 ? 2 : 0);
-    }
-}
-
-// mode 0: Pout = Pin M ^ fi I;  mode 1: Pout = scale Pin.  Block = row i.
-struct HornerArgs {
-    const uint8_t* Pin;
-    uint8_t* Pout;
-    const uint8_t* M;
-    uint32_t e, ep, fi, scale, mode;
-};
-
-__global__ void __launch_bounds__(256) k_w8_horner(HornerArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t* ex = lds;
-    uint8_t* lg = ex + 512;
-    uint8_t* row = lg + 256;
-    build_tables(ex, lg);
-    const uint32_t i = blockIdx.x, e = a.e;
-    for (uint32_t l = threadIdx.x; l < e; l += blockDim.x) row[l] = a.Pin[(size_t)i * a.ep + l];
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < e; j += blockDim.x) {
-        uint32_t acc;
-        if (a.mode == 0) {
-            acc = i == j ? a.fi : 0u;
-            for (uint32_t l = 0; l < e; ++l) acc ^= gmul(ex, lg, row[l], a.M[(size_t)l * a.ep + j]);
-        } else {
-            acc = gmul(ex, lg, a.scale, row[j]);
-        }
-        a.Pout[(size_t)i * a.ep + j] = (uint8_t)acc;
-    }
-}
-
-// info[2] |= 1 where (M W)[i][j] != [i == j].  Block = row i.
-__global__ void __launch_bounds__(256) k_w8_verify(const uint8_t* M, const uint8_t* W, uint32_t e, uint32_t ep,
-                                                   int32_t* info) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t* ex = lds;
-    uint8_t* lg = ex + 512;
-    uint8_t* row = lg + 256;
-    build_tables(ex, lg);
-    const uint32_t i = blockIdx.x;
-    for (uint32_t l = threadIdx.x; l < e; l += blockDim.x) row[l] = M[(size_t)i * ep + l];
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < e; j += blockDim.x) {
-        uint32_t acc = 0;
-        for (uint32_t l = 0; l < e; ++l) acc ^= gmul(ex, lg, row[l], W[(size_t)l * ep + j]);
-        if (acc != (i == j ? 1u : 0u)) atomicOr(&info[2], 1);
-    }
-}
-
-// D[t][q] over the k accepted slots: slot q is repair ordinal p (slot[q] =
-// kRepairBit | p) -> W[t][p]; systematic source s -> sum_p W[t][p] A[p][s].
-__global__ void __launch_bounds__(256) k_w8_dmat(const uint8_t* W, const uint8_t* A, const uint32_t* slot,
-                                                 uint8_t* D, uint32_t e, uint32_t ep, uint32_t k, uint32_t kp) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint8_t* ex = lds;
-    uint8_t* lg = ex + 512;
-    uint8_t* row = lg + 256;
-    build_tables(ex, lg);
-    const uint32_t t = blockIdx.x;
-    for (uint32_t p = threadIdx.x; p < e; p += blockDim.x) row[p] = W[(size_t)t * ep + p];
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < k; q += blockDim.x) {
-        const uint32_t s = slot[q];
-        uint32_t acc;
-        if (s & kRepairBit) {
-            acc = row[s & 0xFFFFu];
-        } else {
-            acc = 0;
-            for (uint32_t p = 0; p < e; ++p) acc ^= gmul(ex, lg, row[p], A[(size_t)p * kp + s]);
-        }
-        D[(size_t)t * kp + q] = (uint8_t)acc;
     }
 }
 
@@ -275,18 +229,90 @@ __device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// c * x for the four bytes of x, c's split-table record r (gf256_tables.h).
+__device__ __forceinline__ uint32_t mul4(const uint32_t* r, uint32_t x) {
+    return vperm(r[1], r[0], x & 0x07070707u) ^ vperm(r[3], r[2], (x >> 3) & 0x07070707u) ^
+           vperm(r[4], r[4], (x >> 6) & 0x03030303u);
+}
+
+// Row combinations out[i][:] = sum_l coef[i][l] * in[l][:] over n input rows
+// of `words` dwords: the Horner step (P M, plus diag on the diagonal), the
+// check (M W == I) and G = W A_J.  Block (i, word chunk of 64); lane = dword,
+// wave q takes l = q, q + 4, ...; the coefficient is wave-uniform (row i of
+// coef staged in LDS), the product the split-table v_perm.
+struct RowsArgs {
+    const uint8_t* coef;
+    const uint8_t* in;
+    uint8_t* out;
+    const uint32_t* tab;
+    uint64_t coef_pitch, in_pitch, out_pitch;
+    uint32_t n, words;
+    uint32_t diag;     // out[i][i] ^= diag
+    uint32_t scale;    // != 0: out = scale * in[i] (no combination)
+    int32_t* check;    // != null: compare with the identity instead of storing
+};
+
+__global__ void __launch_bounds__(256) k_w8_rows(RowsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 8];
+    __shared__ uint32_t part[4][64];
+    extern __shared__ __attribute__((aligned(16))) uint8_t crow[];
+    const uint32_t i = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wd = blockIdx.y * 64 + lane;
+    for (uint32_t q = threadIdx.x; q < 256 * 8; q += blockDim.x) tab[q] = a.tab[q];
+    if (!a.scale)
+        for (uint32_t l = threadIdx.x; l < a.n; l += blockDim.x) crow[l] = a.coef[(uint64_t)i * a.coef_pitch + l];
+    __syncthreads();
+    uint32_t acc = 0;
+    if (wd < a.words) {
+        if (a.scale) {
+            if (wave == 0) acc = mul4(tab + 8 * a.scale, *reinterpret_cast<const uint32_t*>(a.in + (uint64_t)i * a.in_pitch + 4 * wd));
+        } else {
+            const uint8_t* col = a.in + 4 * (uint64_t)wd;
+            uint32_t l = wave;
+            for (; l + 12 < a.n; l += 16) {   // four rows in flight per wave
+                const uint32_t x0 = *reinterpret_cast<const uint32_t*>(col + (uint64_t)l * a.in_pitch);
+                const uint32_t x1 = *reinterpret_cast<const uint32_t*>(col + (uint64_t)(l + 4) * a.in_pitch);
+                const uint32_t x2 = *reinterpret_cast<const uint32_t*>(col + (uint64_t)(l + 8) * a.in_pitch);
+                const uint32_t x3 = *reinterpret_cast<const uint32_t*>(col + (uint64_t)(l + 12) * a.in_pitch);
+                acc ^= mul4(tab + 8 * crow[l], x0) ^ mul4(tab + 8 * crow[l + 4], x1) ^
+                       mul4(tab + 8 * crow[l + 8], x2) ^ mul4(tab + 8 * crow[l + 12], x3);
+            }
+            for (; l < a.n; l += 4)
+                acc ^= mul4(tab + 8 * crow[l], *reinterpret_cast<const uint32_t*>(col + (uint64_t)l * a.in_pitch));
+        }
+    }
+    part[wave][lane] = acc;
+    __syncthreads();
+    if (wave != 0 || wd >= a.words) return;
+    uint32_t v = part[0][lane] ^ part[1][lane] ^ part[2][lane] ^ part[3][lane];
+    if (wd == (i >> 2)) v ^= a.diag << (8 * (i & 3));
+    if (a.check) {
+        const uint32_t want = wd == (i >> 2) ? 1u << (8 * (i & 3)) : 0u;
+        // bytes past n in the last word are padding: compare the real ones
+        const uint32_t nb = a.n - 4 * wd < 4 ? a.n - 4 * wd : 4;
+        const uint32_t mask = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1);
+        if ((v ^ want) & mask) atomicOr(a.check, 1);
+        return;
+    }
+    *reinterpret_cast<uint32_t*>(a.out + (uint64_t)i * a.out_pitch + 4 * wd) = v;
+}
+
 struct ApplyArgs {
     const uint8_t* rows;   // k slots, stride apart (16-B aligned, zero padded)
-    const uint8_t* D;      // e x kp
+    const uint8_t* G;      // e x kp: G[t][s] = sum_p W[t][p] A_J[p][s]
+    const uint8_t* W;      // e x ep
+    const uint32_t* slot;  // k: source index, or kRepairBit | repair ordinal
     const uint32_t* tab;   // 256 split-table records of 8 dwords
     uint8_t* out;          // e rows, stride apart (zeroed)
     uint64_t stride;
-    uint32_t e, k, kp, Lu;
+    uint32_t e, k, kp, ep, Lu;
 };
 
 constexpr uint32_t kApplyOut = 4;      // outputs per block
 constexpr uint32_t kApplySlots = 64;   // slots per block (16 per wave)
 
+// recovered[t] = sum over slots q of D[t][q] rows[q], D[t][q] = W[t][p] for
+// repair slot q (ordinal p), G[t][s] for systematic slot q (source s).
 // grid (ceil(Lu / 64), ceil(e / 4), ceil(k / 64)); lane = 16-byte unit,
 // wave w takes slots z*64 + w + 4m.  Wave partials meet in LDS, then one
 // atomic XOR per dword per output.
@@ -304,26 +330,20 @@ __global__ void __launch_bounds__(256) k_w8_apply(ApplyArgs a) {
         for (uint32_t mm = 0; mm < kApplySlots / 4; ++mm) {
             const uint32_t q = blockIdx.z * kApplySlots + wave + 4 * mm;
             if (q >= a.k) break;
+            const uint32_t sq = a.slot[q];
             const uint4 x = *reinterpret_cast<const uint4*>(a.rows + (uint64_t)q * a.stride + (uint64_t)u * 16);
-            const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (uint32_t o = 0; o < kApplyOut; ++o) {
                 const uint32_t t = t0 + o;
                 if (t >= a.e) break;
-                const uint32_t c = a.D[(size_t)t * a.kp + q];
+                const uint32_t c = (sq & kRepairBit) ? a.W[(size_t)t * a.ep + (sq & 0xFFFFu)]
+                                                     : a.G[(size_t)t * a.kp + sq];
                 if (c == 0) continue;
                 const uint32_t* r = tab + 8 * c;
-                uint32_t y[4];
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const uint32_t s0 = xs[d] & 0x07070707u, s1 = (xs[d] >> 3) & 0x07070707u,
-                                   s2 = (xs[d] >> 6) & 0x03030303u;
-                    y[d] = vperm(r[1], r[0], s0) ^ vperm(r[3], r[2], s1) ^ vperm(r[4], r[4], s2);
-                }
-                acc[o].x ^= y[0];
-                acc[o].y ^= y[1];
-                acc[o].z ^= y[2];
-                acc[o].w ^= y[3];
+                acc[o].x ^= mul4(r, x.x);
+                acc[o].y ^= mul4(r, x.y);
+                acc[o].z ^= mul4(r, x.z);
+                acc[o].w ^= mul4(r, x.w);
             }
         }
     }
@@ -351,6 +371,12 @@ __global__ void __launch_bounds__(256) k_w8_apply(ApplyArgs a) {
 
 static inline uint32_t r16(uint32_t x) { return (x + 15) & ~15u; }
 
+hipError_t launch_rows(const RowsArgs& a, uint32_t rows, hipStream_t st) {
+    const size_t lds = a.scale ? 0 : (size_t)a.n;
+    hipLaunchKernelGGL(k_w8_rows, dim3(rows, (a.words + 63) / 64), dim3(256), lds, st, a);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, const uint16_t* E,
@@ -362,10 +388,12 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     if (int s = ctx_lock(ctx, lk)) return s;
     hipStream_t st = ctx_stream(ctx);
     const uint32_t ep = r16(e), kp = r16(k);
-    // workspace: A, E, slot, M, P0, P1, D, poly, info
+    const uint32_t* tab = ctx_tab256(ctx);
+    // workspace: A, E, slot, M, P0, P1, G, poly, info
     const size_t oA = 0, oE = oA + (size_t)e * kp, oS = oE + r16(2 * e), oM = oS + r16(4 * k);
-    const size_t oP0 = oM + (size_t)e * ep, oP1 = oP0 + (size_t)e * ep, oD = oP1 + (size_t)e * ep;
-    const size_t oPoly = oD + (size_t)e * kp, oInfo = oPoly + r16(2 * e + 2), total = oInfo + 16;
+    const size_t oP0 = oM + (size_t)e * ep, oP1 = oP0 + (size_t)e * ep, oG = oP1 + (size_t)e * ep;
+    const size_t oPoly = oG + (size_t)e * kp, oInfo = oPoly + r16(2 * e + 2), oLM = oInfo + 16;
+    const size_t total = oLM + 2 * (size_t)e * ep;
     uint8_t* w = nullptr;
     if (int s = ctx_work(ctx, total, &w)) return s;
     std::vector<uint8_t> hA((size_t)e * kp, 0);
@@ -374,10 +402,9 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     QF_CHECK_HIP(hipMemcpyAsync(w + oE, E, (size_t)e * 2, hipMemcpyHostToDevice, st));
     QF_CHECK_HIP(hipMemcpyAsync(w + oS, slot, (size_t)k * 4, hipMemcpyHostToDevice, st));
     int32_t* info = reinterpret_cast<int32_t*>(w + oInfo);
-    size_t seq_lds = 512 + 256 + 64 + 3 * (size_t)e + 2 * (size_t)e + 3 * (2 * (size_t)e + 1);
-    const uint32_t m_lds = seq_lds + (size_t)e * e <= 128 * 1024;   // M in LDS up to e = 330
-    if (m_lds) seq_lds += (size_t)e * e;
-    const size_t row_lds = 512 + 256 + ep;
+    size_t seq_lds = kEx2 + 512 + 64 + 4 * (size_t)e + 2 * (size_t)e + 2 * (size_t)e + 3 * (2 * (size_t)e + 1);
+    const uint32_t lm_lds = seq_lds + 2 * (size_t)e * e <= 144 * 1024;   // logs of M in LDS up to e = 262
+    if (lm_lds) seq_lds += 2 * (size_t)e * e;
     if (seq_lds > 64 * 1024) {
         static std::once_flag once;
         hipError_t err = hipSuccess;
@@ -387,13 +414,16 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
         });
         QF_CHECK_HIP(err);
     }
+    // about 8 threads per row of M for the Krylov products (1 wave at e <= 8)
+    const uint32_t seq_threads = std::min<uint32_t>(kSeqThreads, (8 * e + 63) / 64 * 64);
     const auto& f = gf();
     uint8_t* W = nullptr;
+    const uint32_t ew = (e + 3) / 4;
     for (uint32_t b = 0; b < kTries; ++b) {
         if (tries_out) *tries_out = b + 1;
-        SeqArgs sa{w + oA, reinterpret_cast<const uint16_t*>(w + oE), w + oM, w + oP0, w + oPoly, info, e, ep, kp, b,
-                   m_lds};
-        hipLaunchKernelGGL(k_w8_sequence, dim3(1), dim3(kSeqThreads), seq_lds, st, sa);
+        SeqArgs sa{w + oA, reinterpret_cast<const uint16_t*>(w + oE), w + oM, w + oP0,
+                   reinterpret_cast<uint16_t*>(w + oLM), w + oPoly, info, e, ep, kp, b, lm_lds};
+        hipLaunchKernelGGL(k_w8_sequence, dim3(1), dim3(seq_threads), seq_lds, st, sa);
         QF_CHECK_HIP(hipGetLastError());
         int32_t hinfo[2] = {0, 0};
         QF_CHECK_HIP(hipMemcpyAsync(hinfo, info, 8, hipMemcpyDeviceToHost, st));
@@ -410,18 +440,16 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
         uint8_t* Pin = w + oP0;
         uint8_t* Pout = w + oP1;
         for (uint32_t i = Ld - 1; i >= 1; --i) {
-            HornerArgs h{Pin, Pout, w + oM, e, ep, poly[i], 0, 0};
-            hipLaunchKernelGGL(k_w8_horner, dim3(e), dim3(256), row_lds, st, h);
-            QF_CHECK_HIP(hipGetLastError());
+            RowsArgs h{Pin, w + oM, Pout, tab, ep, ep, ep, e, ew, poly[i], 0, nullptr};
+            QF_CHECK_HIP(launch_rows(h, e, st));
             std::swap(Pin, Pout);
         }
-        HornerArgs h{Pin, Pout, w + oM, e, ep, 0, f0inv, 1};
-        hipLaunchKernelGGL(k_w8_horner, dim3(e), dim3(256), row_lds, st, h);
-        QF_CHECK_HIP(hipGetLastError());
+        RowsArgs sc{nullptr, Pin, Pout, tab, 0, ep, ep, e, ew, 0, f0inv, nullptr};
+        QF_CHECK_HIP(launch_rows(sc, e, st));
         W = Pout;
         QF_CHECK_HIP(hipMemsetAsync(info + 2, 0, 4, st));
-        hipLaunchKernelGGL(k_w8_verify, dim3(e), dim3(256), row_lds, st, w + oM, W, e, ep, info);
-        QF_CHECK_HIP(hipGetLastError());
+        RowsArgs vf{w + oM, W, nullptr, tab, ep, ep, 0, e, ew, 0, 0, info + 2};
+        QF_CHECK_HIP(launch_rows(vf, e, st));
         int32_t bad = 0;
         QF_CHECK_HIP(hipMemcpyAsync(&bad, info + 2, 4, hipMemcpyDeviceToHost, st));
         QF_CHECK_HIP(hipStreamSynchronize(st));
@@ -429,13 +457,13 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
         W = nullptr;
     }
     if (!W) return QF_ERANK;
-    hipLaunchKernelGGL(k_w8_dmat, dim3(e), dim3(256), row_lds, st, W, w + oA, reinterpret_cast<const uint32_t*>(w + oS),
-                       w + oD, e, ep, k, kp);
-    QF_CHECK_HIP(hipGetLastError());
+    // G = W A_J (e x k), then the payload pass
+    RowsArgs g{W, w + oA, w + oG, tab, ep, kp, kp, e, (k + 3) / 4, 0, 0, nullptr};
+    QF_CHECK_HIP(launch_rows(g, e, st));
     QF_CHECK_HIP(hipMemsetAsync(d_rec, 0, (size_t)e * stride, st));
     const uint32_t Lu = (L + 15) / 16;
     if (Lu) {
-        ApplyArgs ap{d_rows, w + oD, ctx_tab256(ctx), d_rec, stride, e, k, kp, Lu};
+        ApplyArgs ap{d_rows, w + oG, W, reinterpret_cast<const uint32_t*>(w + oS), tab, d_rec, stride, e, k, kp, ep, Lu};
         dim3 grid((Lu + 63) / 64, (e + kApplyOut - 1) / kApplyOut, (k + kApplySlots - 1) / kApplySlots);
         hipLaunchKernelGGL(k_w8_apply, grid, dim3(256), 0, st, ap);
         QF_CHECK_HIP(hipGetLastError());
