@@ -6,6 +6,7 @@
  *   batch     qf_encode_batch / qf_decode_batch       decoder.rs:172-275, 678-791
  *   desc      qf_encode_batch_desc / qf_decode_batch_desc (mixed windows)
  *   objects   qf_encoder_* / qf_decoder_*             decoder.rs:155-299, 658-791
+ *   wiedemann qf_decoder_* with k > 256                decoder.rs:659-665, 794-975
  *   adaptive  qf_adaptive_on_send / on_receive / state adaptive.rs:508-599
  *             and their multi-connection batches (_on_send_batch / _on_receive_batch)
  *   framing   qf_packet_to_raw / from_raw / from_block encoder.rs:18-152
@@ -223,6 +224,53 @@ static void test_objects(qf_ctx *ctx) {
     printf("objects ok\n");
 }
 
+/* decoder.rs:659-665 / 794-975: a k > 256 decoder takes the Wiedemann strategy;
+ * repairs with explicit coefficients, checked against oracle_wiedemann_decode */
+static void test_wiedemann(qf_ctx *ctx) {
+    const uint32_t k = 300, e = 5, L = 200;
+    qf_decoder *dec;
+    QF(qf_decoder_new(ctx, k, L, &dec));
+    CHECK(qf_decoder_strategy(dec) == QF_STRATEGY_WIEDEMANN, "strategy for k = %u", k);
+    uint8_t *src = malloc((size_t)k * L), *coef = malloc((size_t)e * k), *rep = malloc((size_t)e * L);
+    for (size_t t = 0; t < (size_t)k * L; ++t) src[t] = rnd8();
+    for (size_t t = 0; t < (size_t)e * k; ++t) coef[t] = rnd8();
+    CHECK(oracle_encode_window(k, e, L, src, L, coef, rep, L) == 0, "oracle encode");
+    uint8_t lost[300] = {0};
+    for (uint32_t q = 0; q < e;) {
+        const uint32_t i = rnd(k);
+        if (!lost[i]) lost[i] = 1, ++q;
+    }
+    /* arrival: surviving sources, then the repairs */
+    uint16_t *idx = malloc(sizeof(uint16_t) * k);
+    uint8_t *rows = malloc((size_t)k * L), *rc = calloc((size_t)k, k);
+    uint32_t n = 0;
+    int decoded = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        if (lost[i]) continue;
+        idx[n] = (uint16_t)i;
+        memcpy(rows + (size_t)n++ * L, src + (size_t)i * L, L);
+        decoded = qf_decoder_add_packet(dec, i, 1, src + (size_t)i * L, L, NULL, 0);
+        CHECK(decoded == 0, "decoded too early");
+    }
+    for (uint32_t j = 0; j < e; ++j) {
+        idx[n] = (uint16_t)(k + j);
+        memcpy(rows + (size_t)n * L, rep + (size_t)j * L, L);
+        memcpy(rc + (size_t)n++ * k, coef + (size_t)j * k, k);
+        decoded = qf_decoder_add_packet(dec, 5000 + j, 0, rep + (size_t)j * L, L, coef + (size_t)j * k, k);
+    }
+    CHECK(decoded == 1, "k = %u generation not decoded", k);
+    uint8_t *want = malloc((size_t)k * L), *got = malloc((size_t)k * L);
+    CHECK(oracle_wiedemann_decode(k, L, n, idx, rows, L, rc, want, L, NULL, NULL) == 0, "oracle wiedemann");
+    uint32_t *glen = malloc(4 * k), cnt;
+    uint64_t *gid = malloc(8 * k);
+    QF(qf_decoder_get_decoded_packets(dec, got, L, glen, gid, &cnt));
+    CHECK(cnt == k && memcmp(got, want, (size_t)k * L) == 0 && memcmp(got, src, (size_t)k * L) == 0,
+          "k > 256 decode == oracle");
+    QF(qf_decoder_free(dec));
+    free(src); free(coef); free(rep); free(idx); free(rows); free(rc); free(want); free(got); free(glen); free(gid);
+    printf("wiedemann ok\n");
+}
+
 static void test_adaptive(qf_ctx *ctx) {
     qf_fec_config cfg;
     qf_fec_config_default(&cfg);
@@ -413,6 +461,7 @@ int main(void) {
     test_batch(ctx);
     test_desc(ctx);
     test_objects(ctx);
+    test_wiedemann(ctx);
     test_adaptive(ctx);
     test_adaptive_batch(ctx);
     QF(qf_ctx_destroy(ctx));
