@@ -222,6 +222,8 @@ _ASM = {
     "store_byte_saddr": lambda voff, d, sb, off: f"global_store_byte {V(voff)}, {V(d)}, {SP(sb)}"
                         + (f" offset:{off}" if off else ""),
     "store_byte": lambda a, d, off: f"global_store_byte {VP(a)}, {V(d)}, off" + (f" offset:{off}" if off else ""),
+    # lab: a cache-warming load (the destination is a dummy register)
+    "load4": lambda d, a, off: f"global_load_dword {V(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
 }
 
 
@@ -363,6 +365,15 @@ class KernelSpec:
     # lab only (chunked dec): skip the row loop (the LU phase alone, on whatever
     # the accumulator registers hold) -- timing of the LU in isolation
     lab_lu_only: bool = False
+    # chunked dec: LU products of 2-3 dwords interleaved (their v_perm results in
+    # separate temps) and selectors issued stage by stage, so that dependent
+    # VALU ops sit several instructions apart
+    lu_ilp: bool = False
+    # lab only (chunked dec, strided rows): (n_slots, 16 Q) -- during the
+    # backward LU phase, touch every row the NEXT item will read (one dword
+    # load per half and row into a dummy register), so that its row loop finds
+    # them in L2 / the Infinity Cache while HBM would otherwise idle
+    lab_prefetch: tuple = ()
     # enc mode, one pass of a code with more repairs than a kernel holds:
     # repairs j0 .. j0 + r - 1 of the Cauchy matrix of (k, r_total)
     r_total: int = 0
@@ -1501,6 +1512,54 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
     return ops
 
 
+# lu_ilp: product temps of up to three interleaved dwords -- R_P and low VGPRs
+# the chunked kernel uses only in its row loop or stores (v17, v43, V_ADDR,
+# V_SLOT, v47), free during the LU whatever the (k, r) layout above v48
+LU_ILP_TEMPS = (R_P, R_P + 1, R_P + 2, 17, 43, V_ADDR, V_ADDR + 1, V_SLOT, 47)
+LU_ILP_GROUPS = ((0, 1, 2), (3, 4, 5), (6, 7))
+
+
+def _prefetch_setup(E, spec: KernelSpec):
+    """lab_prefetch: v[44:45] <- the next item's row-0 address of each lane
+    (strided generations), s[38:39] / s[40:41] the lanes whose A / B unit
+    exists; no next item -> skip to .Lnopf."""
+    E(Op("s_add", (46, 28, 18)))
+    E(Op("s_cmp_ge_br", (46, 17, ".Lnopf_far")))
+    E(Op("v_lshl_add_s", (14, 46, 6, V_LANE)))
+    E(Op("v_cmp_gt_s", (S_TMP, 14, 14)))              # f' < G Q
+    E(Op("v_mul_hi_s", (15, 14, 15)))
+    E(Op("v_lshr_s", (15, 16, 15)))                   # g'
+    E(Op("v_mul_lo_s", (16, 15, 13)))
+    E(Op("v_sub", (16, 14, 16)))                      # q'
+    E(Op("v_add_s", (17, 13, 16)))
+    E(Op("v_cmp_gt_s", (S_TMP2, 12, 17)))             # q' + Q < Lu
+    E(Op("s_nop", (4,)))
+    E(Op("s_and64", (S_TMP2, S_TMP2, S_TMP)))
+    E(Op("v_movs", (V_ADDR, 4)))
+    E(Op("v_movs", (V_ADDR + 1, 5)))
+    E(Op("v_mad64_s", (V_ADDR, 15, 8, V_ADDR)))
+    E(Op("v_mad64_k", (V_ADDR, 16, 16, V_ADDR)))
+    E(Op("s_branch", (".Lpf_go",)))
+    E(Op("label", (".Lnopf_far",)))
+    E(Op("s_exec", (None,)))
+    E(Op("s_movk", (S_TMP, 0)))                       # no next item: empty load masks
+    E(Op("s_movk", (S_TMP + 1, 0)))
+    E(Op("s_movk", (S_TMP2, 0)))
+    E(Op("s_movk", (S_TMP2 + 1, 0)))
+    E(Op("label", (".Lpf_go",)))
+
+
+def _prefetch_rows(E, spec: KernelSpec, n: int):
+    _, boff = spec.lab_prefetch
+    for _ in range(n):
+        E(Op("s_exec", (S_TMP,)))
+        E(Op("load4", (47, V_ADDR, 0)))
+        E(Op("s_exec", (S_TMP2,)))
+        E(Op("load4", (47, V_ADDR, boff)))
+        E(Op("s_exec", (None,)))
+        E(Op("v_add64_s", (V_ADDR, V_ADDR, 32)))      # + row stride
+
+
 def _lu_solve_and_store_chunked(E, spec: KernelSpec):
     """_lu_solve_and_store for one generation per lane: one record, 8 dwords
     per block, one split-table read per coefficient."""
@@ -1513,6 +1572,18 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
         return acc0 + 8 * t + d
 
     def selectors(u):
+        if spec.lu_ilp:   # stage by stage: no op depends on the one before it
+            for d in range(8):
+                E(Op("v_andk", (sel + d, 0x07070707, blk(u, d))))
+            for d in range(8):
+                E(Op("v_lshr", (sel + 8 + d, 3, blk(u, d))))
+            for d in range(8):
+                E(Op("v_lshr", (sel + 16 + d, 6, blk(u, d))))
+            for d in range(8):
+                E(Op("v_andk", (sel + 8 + d, 0x07070707, sel + 8 + d)))
+            for d in range(8):
+                E(Op("v_andk", (sel + 16 + d, 0x03030303, sel + 16 + d)))
+            return
         for d in range(8):
             x = blk(u, d)
             E(Op("v_andk", (sel + d, 0x07070707, x)))
@@ -1527,19 +1598,35 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
         E(Op("ds_read_b128", (tb, a, 0)))
         E(Op("ds_read_b32", (tb + 4, a, 16)))
 
-    def products(d, buf):
+    def products(d, buf, p=(R_P, R_P + 1, R_P + 2)):
         tb = tbs[buf]
-        E(Op("v_perm", (R_P, tb + 1, tb, sel + d)))
-        E(Op("v_perm", (R_P + 1, tb + 3, tb + 2, sel + 8 + d)))
-        E(Op("v_perm", (R_P + 2, tb + 4, tb + 4, sel + 16 + d)))
+        E(Op("v_perm", (p[0], tb + 1, tb, sel + d)))
+        E(Op("v_perm", (p[1], tb + 3, tb + 2, sel + 8 + d)))
+        E(Op("v_perm", (p[2], tb + 4, tb + 4, sel + 16 + d)))
 
     def mul_acc(t, buf):
+        if spec.lu_ilp:
+            for grp in LU_ILP_GROUPS:
+                for m, d in enumerate(grp):
+                    products(d, buf, LU_ILP_TEMPS[3 * m: 3 * m + 3])
+                for m, d in enumerate(grp):
+                    E(Op("v_xor3", (blk(t, d), blk(t, d), LU_ILP_TEMPS[3 * m], LU_ILP_TEMPS[3 * m + 1])))
+                for m, d in enumerate(grp):
+                    E(Op("v_xor", (blk(t, d), blk(t, d), LU_ILP_TEMPS[3 * m + 2])))
+            return
         for d in range(8):
             products(d, buf)
             E(Op("v_xor3", (blk(t, d), blk(t, d), R_P, R_P + 1)))
             E(Op("v_xor", (blk(t, d), blk(t, d), R_P + 2)))
 
     def scale(u, buf):
+        if spec.lu_ilp:
+            for grp in LU_ILP_GROUPS:
+                for m, d in enumerate(grp):
+                    products(d, buf, LU_ILP_TEMPS[3 * m: 3 * m + 3])
+                for m, d in enumerate(grp):
+                    E(Op("v_xor3", (blk(u, d),) + tuple(LU_ILP_TEMPS[3 * m: 3 * m + 3])))
+            return
         for d in range(8):
             products(d, buf)
             E(Op("v_xor3", (blk(u, d), R_P, R_P + 1, R_P + 2)))
@@ -1578,10 +1665,20 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
             column(u, [("scale", u)] + [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}", 1)
         E(Op("label", (".Lfwd_end",)))
         E(Op("s_waitcnt_vm", (0,)))
-        for u in reversed(range(1, r)):
+        pf_rows = []
+        if spec.lab_prefetch:
+            n_slots, _ = spec.lab_prefetch
+            _prefetch_setup(E, spec)
+            chunks = r - 1
+            pf_rows = [list(range(n_slots))[c::chunks] for c in range(chunks)]
+        for n_u, u in enumerate(reversed(range(1, r))):
             E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lbwd{u}")))
             selectors(u)
             column(u, [("acc", t) for t in range(u)], f".Lbwd{u}", r + 1)
+            if pf_rows:
+                _prefetch_rows(E, spec, len(pf_rows[n_u]))
+        if spec.lab_prefetch:
+            E(Op("label", (".Lnopf",)))
     else:
         E(Op("s_waitcnt_vm", (0,)))
     # stores: block t -> recovered row rank[t]; A half, then B half at + 16 Q

@@ -281,11 +281,11 @@ def test_xcd_remap_is_a_bijection():
 
 
 def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=False, offs=False,
-              wave_gen=False):
+              wave_gen=False, **spec_kw):
     """Run the fused decode kernel (mode "dec") on the emulator: random
     erasures (or `erase` sources), random accepted repairs in random slots,
     LU records from bs.lu_record; returns the number of wrong rows."""
-    spec = bs.KernelSpec(k, r, pd, mode="dec", chunked=chunked, wave_gen=wave_gen)
+    spec = bs.KernelSpec(k, r, pd, mode="dec", chunked=chunked, wave_gen=wave_gen, **spec_kw)
     rng = np.random.default_rng(seed)
     rs = L + 16
     n_slots = k + 2
@@ -511,6 +511,18 @@ def test_emulated_fused_decode_chunked(oracle, k, r, pd, L, G, seed, erase, offs
     q + Q) recovers the erased sources, with strided generations or offset
     tables, and writes nothing else."""
     assert _dec_case(oracle, k, r, pd, L, G, seed, erase, padded=False, chunked=True, offs=offs) == 0
+
+
+@pytest.mark.parametrize("lu_ilp", [False, True])
+@pytest.mark.parametrize("k,r,pd,L,G,seed,erase", [
+    (16, 16, 2, 96, 4, 4, 16),            # all 16 blocks
+    (16, 16, 3, 1200, 2, 7, 13),
+    (8, 5, 2, 100, 5, 8, None),
+])
+def test_emulated_fused_decode_lu_schedule(oracle, k, r, pd, L, G, seed, erase, lu_ilp):
+    """The interleaved LU schedule (lu_ilp: 2-3 dwords' products in separate
+    temps, selectors stage by stage) recovers the same rows."""
+    assert _dec_case(oracle, k, r, pd, L, G, seed, erase, padded=False, chunked=True, lu_ilp=lu_ilp) == 0
 
 
 @pytest.mark.parametrize("k,r,pd,L,G,seed,erase", [

@@ -73,8 +73,17 @@ VARIANTS = [
     ("rl_pd6", {"chunked": True, "lu": False, "pd": 6}, ()),
     ("lu_c1", {"chunked": True, "lab_lu_only": True, "cap": 256}, ()),
     ("lu_full", {"chunked": True, "lab_lu_only": True}, ()),
+    # round 2d: the LU phase touches the next item's rows (cache warming)
+    ("decc_pf", {"chunked": True, "lab_prefetch": (67, 16 * 38)}, ()),
+    ("decc_4", {"chunked": True}, ()),
+    ("decc_pf_2", {"chunked": True, "lab_prefetch": (67, 16 * 38)}, ()),
+    # interleaved LU schedule (2-3 dwords' products in separate temps)
+    ("decc_ilp", {"chunked": True, "lu_ilp": True}, ()),
+    ("decc_5", {"chunked": True}, ()),
+    ("decc_ilp_2", {"chunked": True, "lu_ilp": True}, ()),
+    ("lu_ilp_full", {"chunked": True, "lab_lu_only": True, "lu_ilp": True}, ()),
 ]
-PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]
+PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]   # need all three built
 
 
 def build():
