@@ -61,6 +61,10 @@ struct qf_encoder {
     uint32_t pend_slot = 0;
 };
 
+// decoder output block: status (4 B), count (4 B), pad, recovered indices
+// (<= 128 x 2 B), then the recovered rows
+constexpr size_t kOutMeta = 512;
+
 struct qf_decoder {
     qf_ctx* ctx = nullptr;
     uint32_t k = 0, max_len = 0, stride = 0;
@@ -77,15 +81,22 @@ struct qf_decoder {
     // decoded output, source index order
     std::vector<uint8_t> out;      // k * stride
     std::vector<uint32_t> out_len;
-    // device buffers for one generation
+    // device buffers for one generation.  d_rows holds the k row slots and,
+    // right after them, the row-index array (d_index), so that the rows still
+    // on the host and the indices go up in one copy; d_out holds status,
+    // count and recovered indices (first 512 bytes) and then the recovered
+    // rows, so that one copy brings all of them down (h_out mirrors it).
     uint8_t* d_rows = nullptr;
     uint8_t* d_coeffs = nullptr;
     uint16_t* d_index = nullptr;
+    uint8_t* d_out = nullptr;
     uint8_t* d_rec = nullptr;
     uint16_t* d_rec_index = nullptr;
     uint32_t* d_nrec = nullptr;
     int32_t* d_status = nullptr;
-    uint8_t* h_rec = nullptr;       // pinned download of the recovered rows
+    uint8_t* h_out = nullptr;       // pinned mirror of d_out
+    uint8_t* h_rec = nullptr;       // h_out + kOutMeta
+    uint16_t* h_index = nullptr;    // pinned, right after the host rows
     // k > 256 (Wiedemann strategy): recovered rows, grown to e rows on demand
     uint8_t* d_wrec = nullptr;
     uint32_t wrec_rows = 0;
@@ -330,18 +341,24 @@ int qf_decoder_new(qf_ctx* ctx, uint32_t k, uint32_t max_len, qf_decoder** out) 
     d->sys_slot.assign(k, -1);
     d->sys_id.assign(k, 0);
     const uint32_t emax = k < 128 ? k : 128;
-    bool ok = hipMalloc(&d->d_rows, (size_t)k * d->stride) == hipSuccess &&
+    const size_t rows_bytes = (size_t)k * d->stride + round16(2 * k);
+    const size_t out_bytes = kOutMeta + (size_t)emax * d->stride;
+    bool ok = hipMalloc(&d->d_rows, rows_bytes) == hipSuccess &&
               (wied || hipMalloc(&d->d_coeffs, (size_t)k * k) == hipSuccess) &&
-              hipMalloc(&d->d_index, (size_t)k * 2) == hipSuccess &&
-              hipMalloc(&d->d_rec, (size_t)emax * d->stride) == hipSuccess &&
-              hipMalloc(&d->d_rec_index, (size_t)emax * 2) == hipSuccess &&
-              hipMalloc(&d->d_nrec, 4) == hipSuccess && hipMalloc(&d->d_status, 4) == hipSuccess &&
-              hipHostMalloc(reinterpret_cast<void**>(&d->rows), (size_t)k * d->stride) == hipSuccess &&
-              hipHostMalloc(reinterpret_cast<void**>(&d->h_rec), (size_t)emax * d->stride) == hipSuccess;
+              hipMalloc(&d->d_out, out_bytes) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&d->rows), rows_bytes) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&d->h_out), out_bytes) == hipSuccess;
     if (!ok) {
         qf_decoder_free(d);
         return QF_ENOMEM;
     }
+    d->d_index = reinterpret_cast<uint16_t*>(d->d_rows + (size_t)k * d->stride);
+    d->h_index = reinterpret_cast<uint16_t*>(d->rows + (size_t)k * d->stride);
+    d->d_status = reinterpret_cast<int32_t*>(d->d_out);
+    d->d_nrec = reinterpret_cast<uint32_t*>(d->d_out + 4);
+    d->d_rec_index = reinterpret_cast<uint16_t*>(d->d_out + 16);
+    d->d_rec = d->d_out + kOutMeta;
+    d->h_rec = d->h_out + kOutMeta;
     *out = d;
     return QF_OK;
 }
@@ -350,17 +367,13 @@ int qf_decoder_free(qf_decoder* d) {
     if (!d) return QF_OK;
     hipFree(d->d_rows);
     hipFree(d->d_coeffs);
-    hipFree(d->d_index);
-    hipFree(d->d_rec);
-    hipFree(d->d_rec_index);
-    hipFree(d->d_nrec);
-    hipFree(d->d_status);
+    hipFree(d->d_out);
     hipFree(d->d_wrec);
     if (d->rows) {
         hipStreamSynchronize((hipStream_t)qf_ctx_stream(d->ctx));  // row uploads in flight
         hipHostFree(d->rows);
     }
-    if (d->h_rec) hipHostFree(d->h_rec);
+    if (d->h_out) hipHostFree(d->h_out);
     delete d;
     return QF_OK;
 }
@@ -513,9 +526,14 @@ static int decoder_try_decode(qf_decoder* d) {
     const uint32_t L = plan.L;
     if (!plan.cauchy)
         QF_CHECK_HIP(hipMemcpyAsync(d->d_coeffs, d->coeffs.data(), (size_t)k * k, hipMemcpyHostToDevice, st));
-    // the rows not on the device yet, in one copy (slots are contiguous)
-    if (int u = decoder_upload(d)) return u;
-    QF_CHECK_HIP(hipMemcpyAsync(d->d_index, plan.idx.data(), (size_t)k * 2, hipMemcpyHostToDevice, st));
+    // the rows not on the device yet and the row indices after them, in one
+    // copy from pinned memory (slots are contiguous, the indices follow them)
+    memcpy(d->h_index, plan.idx.data(), (size_t)k * 2);
+    {
+        const size_t o = (size_t)d->uploaded * d->stride, end = (size_t)k * d->stride + (size_t)k * 2;
+        QF_CHECK_HIP(hipMemcpyAsync(d->d_rows + o, d->rows + o, end - o, hipMemcpyHostToDevice, st));
+        d->uploaded = d->accepted;
+    }
     qf_decode_shape sh{};
     sh.k = k;
     sh.r = plan.rc;
@@ -528,19 +546,16 @@ static int decoder_try_decode(qf_decoder* d) {
     int s = qf_decode_batch(d->ctx, &sh, 1, d->d_rows, d->d_index, nullptr, plan.cauchy ? nullptr : d->d_coeffs,
                             d->d_rec, d->d_rec_index, d->d_nrec, d->d_status);
     if (s != QF_OK) return s;
-    int32_t status = 0;
-    uint32_t nrec = 0;
-    QF_CHECK_HIP(hipMemcpyAsync(&status, d->d_status, 4, hipMemcpyDeviceToHost, st));
-    QF_CHECK_HIP(hipMemcpyAsync(&nrec, d->d_nrec, 4, hipMemcpyDeviceToHost, st));
+    // status, count, indices and up to rc recovered rows (nrec <= rc): one
+    // download into pinned memory, one wait
+    const uint32_t nmax = std::min(plan.rc, emax);
+    QF_CHECK_HIP(hipMemcpyAsync(d->h_out, d->d_out, kOutMeta + (size_t)nmax * d->stride, hipMemcpyDeviceToHost, st));
     QF_CHECK_HIP(hipStreamSynchronize(st));
+    const int32_t status = *reinterpret_cast<const int32_t*>(d->h_out);
+    const uint32_t nrec = *reinterpret_cast<const uint32_t*>(d->h_out + 4);
     if (status != QF_OK) return status;  // singular: stays undecoded (decoder.rs:756-758)
-    std::vector<uint16_t> ridx(nrec);
-    if (nrec) {
-        QF_CHECK_HIP(hipMemcpyAsync(ridx.data(), d->d_rec_index, (size_t)nrec * 2, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipMemcpyAsync(d->h_rec, d->d_rec, (size_t)nrec * d->stride, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipStreamSynchronize(st));
-    }
-    decoder_assemble(d, L, nrec, ridx.data(), d->h_rec, d->stride);
+    if (nrec > nmax) return QF_EDEVICE;
+    decoder_assemble(d, L, nrec, reinterpret_cast<const uint16_t*>(d->h_out + 16), d->h_rec, d->stride);
     return QF_OK;
 }
 
