@@ -184,9 +184,11 @@ _ASM = {
     "ds_write_b128": lambda a, d, off: f"ds_write_b128 {V(a)}, {VQ(d)}" + (f" offset:{off}" if off else ""),
     "s_waitcnt_lgkm_n": lambda n: f"s_waitcnt lgkmcnt({n})",
     "s_cmp_le_k_br": lambda s, kk, lbl: f"s_cmp_le_u32 s{s}, {kk}\n\ts_cbranch_scc1 {lbl}",
+    "s_cmp_lg_k_br": lambda s, kk, lbl: f"s_cmp_lg_u32 s{s}, {kk}\n\ts_cbranch_scc1 {lbl}",
     "s_or64": lambda d, a, b: f"s_or_b64 {SP(d)}, {SP(a)}, {SP(b)}",
     "s_cmp_lg64_br": lambda s, lbl: f"s_cmp_lg_u64 {SP(s)}, 0\n\ts_cbranch_scc1 {lbl}",
     "s_endpgm": lambda: "s_endpgm",
+    "s_barrier": lambda: "s_barrier",
     # synw (wave-uniform slot lookup): scalar map / base arithmetic, saddr loads
     "s_load_karg_x2": lambda d, off: f"s_load_dwordx2 {SP(d)}, s[0:1], 0x{off:x}",
     "s_load_x1": lambda d, a, off: f"s_load_dword s{d}, {SP(a)}, 0x{off:x}",
@@ -289,6 +291,7 @@ S_PICK = 68                  # v_perm selector placing byte b of a dword at bits
 LDS_TAB_STRIDE = 256         # split-table record c at LDS byte c * 256 (address = byte << 8)
 LDS_TAB_BYTES = 256 * LDS_TAB_STRIDE
 LU_REC_BYTES = 272          # 16 columns x 16 B, then 16 rank bytes
+KSPLIT_BLOCK_BYTES = 2048   # one accumulator block of a wave (8 dwords x 64 lanes) in LDS
 # LU-phase VGPRs (regions free once the row loop is done; dec mode with
 # r = 16: acc blocks v80..v207, slot maps v208..v247 are dead by then)
 R_P = 14                    # 3 product temps (v14..v16)
@@ -365,6 +368,11 @@ class KernelSpec:
     # lab only (chunked dec): skip the row loop (the LU phase alone, on whatever
     # the accumulator registers hold) -- timing of the LU in isolation
     lab_lu_only: bool = False
+    # chunked dec, small batches: the four waves of a workgroup share ONE item,
+    # each running every ksplit-th row of it; waves 1..3 hand their partial
+    # syndromes to wave 0 through LDS, which solves and stores (kernel
+    # qf_cauchy_decs_*: a generation's rows no longer run through one wave)
+    ksplit: int = 1
     # chunked dec: LU products of 2-3 dwords interleaved (their v_perm results in
     # separate temps) and selectors issued stage by stage, so that dependent
     # VALU ops sit several instructions apart
@@ -415,7 +423,7 @@ class KernelSpec:
             return f"qf_combine_bs_r{self.r}"
         tag = {"enc": "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
-            tag = "decc"
+            tag = "decs" if self.ksplit > 1 else "decc"
         if self.rt != self.r or self.j0:
             return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}"
         return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
@@ -508,6 +516,8 @@ class KernelSpec:
 
     @property
     def lds_bytes(self) -> int:
+        if self.mode == "dec" and self.ksplit > 1:
+            return LDS_TAB_BYTES + (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
         return LDS_TAB_BYTES if self.mode == "dec" else 0
 
 
@@ -1360,7 +1370,10 @@ def _prologue_chunked(E, spec: KernelSpec):
         E(Op("s_lshl", (30, 30, 2)))
     else:
         E(Op("s_lshl", (30, 2, 2)))
-    E(Op("s_add", (28, 29, 30)))
+    if spec.ksplit > 1:
+        E(Op("s_lshrk", (28, 30, 2)))          # the workgroup's item (all its waves)
+    else:
+        E(Op("s_add", (28, 29, 30)))
     E(Op("s_mov", (32, 10)))
     E(Op("s_movk", (33, 0)))
     E(Op("s_mov", (34, 11)))
@@ -1466,8 +1479,8 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         for a in range(acc0, acc0 + 8 * r):
             E(Op("v_movk", (a, 0)))
 
-    def load_row(n: int):
-        b = ring0 + 8 * (n % nbuf)
+    def load_row(n: int, slot: Optional[int] = None):
+        b = ring0 + 8 * ((n if slot is None else slot) % nbuf)
         kind, idx = seq[n]
         present(idx if kind == "src" else k + idx, S_TMP)
         E(Op("v_mad64_s", (V_ADDR, V_SLOT, 10, V_SRCA)))
@@ -1483,6 +1496,9 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         E(Op("s_exec", (None,)))
 
     n_seq = 0 if spec.lab_lu_only else len(seq)
+    if spec.ksplit > 1:
+        _dec_ksplit(E, ops, spec, seq, load_row, present)
+        return ops
     for n in range(min(pd, n_seq)):
         load_row(n)
     for n, (kind, idx) in enumerate(seq[:n_seq]):
@@ -1558,6 +1574,99 @@ def _prefetch_rows(E, spec: KernelSpec, n: int):
         E(Op("load4", (47, V_ADDR, boff)))
         E(Op("s_exec", (None,)))
         E(Op("v_add64_s", (V_ADDR, V_ADDR, 32)))      # + row stride
+
+
+def _dec_ksplit(E, ops: list, spec: KernelSpec, seq, load_row, present):
+    """ksplit body of the chunked fused decode: wave w of the workgroup runs
+    rows w, w + ks, w + 2 ks, ... of the item (same slot map, same lanes),
+    leaves every block < jmax in byte form (a block's transpose is linear, so
+    partial sums transpose like the whole), waves 1.. write their blocks to
+    LDS, wave 0 adds them in, solves and stores while the others start the
+    next item.  Two barriers per item: partials written / partials read."""
+    k, r, pd, nbuf, ks = spec.k, spec.r, spec.pd, spec.nbuf, spec.ksplit
+    C = cauchy(k, r)
+    acc0, ring0 = spec.acc0, spec.ring0
+    for w in range(1, ks):
+        E(Op("s_cmp_lg_k_br", (29, w, f".Lnsec{w}")))
+        E(Op("s_far_jump", (f".Lsec{w}", 40 + w)))
+        E(Op("label", (f".Lnsec{w}",)))
+    for w in range(ks):
+        E(Op("label", (f".Lsec{w}",)))
+        rows = [n for n in range(len(seq)) if n % ks == w]
+        srcs = [seq[n][1] for n in rows if seq[n][0] == "src"]
+        owned = {seq[n][1] for n in rows if seq[n][0] == "rep"}
+        if not srcs:   # no source row initialises the accumulators
+            for a in range(acc0, acc0 + 8 * r):
+                E(Op("v_movk", (a, 0)))
+        for m in range(min(pd, len(rows))):
+            load_row(rows[m], m)
+        for m, n in enumerate(rows):
+            if m + pd < len(rows):
+                load_row(rows[m + pd], m + pd)
+            after = min(pd, len(rows) - 1 - m)
+            E(Op("s_waitcnt_vm", (2 * after,)))
+            base = ring0 + 8 * (m % nbuf)
+            kind, idx = seq[n]
+            if kind == "rep":
+                E(Op("s_cmp_le_k_br", (S_JMAX, idx, f".Lrep{idx}")))
+                ops.extend(_transpose_ops(acc0 + 8 * idx, spec.bfi_transpose, spec.vmask))
+                for b in range(8):
+                    E(Op("v_xor", (acc0 + 8 * idx + b, acc0 + 8 * idx + b, base + b)))
+                E(Op("label", (f".Lrep{idx}",)))
+            else:
+                _source_row(ops, C, idx, r, base, acc0, init=idx == srcs[0], xor3=spec.xor3,
+                            bfi=spec.bfi_transpose, vmask=spec.vmask, guard=(spec.guard_min, f".Lrow{n}"))
+        # blocks whose repair row another wave holds: back to byte form here
+        for j in range(r):
+            if j in owned:
+                continue
+            E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lbt{w}_{j}")))
+            ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose, spec.vmask))
+            E(Op("label", (f".Lbt{w}_{j}",)))
+        if w + 1 < ks:
+            E(Op("s_far_jump", (".Lsec_end", 50 + w)))
+    E(Op("label", (".Lsec_end",)))
+    E(Op("v_lshl", (V_ADDR, 4, V_LANE)))             # LDS lane offset 16 l
+    E(Op("s_cmp_eq_k_br", (29, 0, ".Lred0")))
+    # waves 1..: partial blocks -> LDS [LDS_TAB_BYTES + (w - 1) r 2 KiB]
+    E(Op("s_addk", (46, 29, -1)))
+    E(Op("s_movk", (47, r * KSPLIT_BLOCK_BYTES)))
+    E(Op("s_mul", (46, 46, 47)))
+    E(Op("s_addk", (46, 46, LDS_TAB_BYTES)))
+    E(Op("v_add_s", (V_ADDR, 46, V_ADDR)))
+    for j in range(r):
+        E(Op("s_cmp_le_k_br", (S_JMAX, j, ".Lwr_end")))
+        E(Op("ds_write_b128", (V_ADDR, acc0 + 8 * j, KSPLIT_BLOCK_BYTES * j)))
+        E(Op("ds_write_b128", (V_ADDR, acc0 + 8 * j + 4, KSPLIT_BLOCK_BYTES * j + 1024)))
+    E(Op("label", (".Lwr_end",)))
+    E(Op("s_waitcnt_lgkm_n", (0,)))
+    E(Op("s_barrier", ()))
+    E(Op("s_barrier", ()))
+    E(Op("s_far_jump", (".Lnext", 60)))
+    # wave 0: add the partials in (temps: the ring, dead now), solve, store
+    E(Op("label", (".Lred0",)))
+    E(Op("s_barrier", ()))
+    for w in range(1, ks):
+        E(Op("v_addk", (V_ADDR + 1, LDS_TAB_BYTES + (w - 1) * r * KSPLIT_BLOCK_BYTES, V_ADDR)))
+        for j in range(r):
+            E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lrd_end{w}")))
+            t = ring0 + 8 * (j % nbuf)
+            E(Op("ds_read_b128", (t, V_ADDR + 1, KSPLIT_BLOCK_BYTES * j)))
+            E(Op("ds_read_b128", (t + 4, V_ADDR + 1, KSPLIT_BLOCK_BYTES * j + 1024)))
+            E(Op("s_waitcnt_lgkm_n", (0,)))
+            for b in range(8):
+                E(Op("v_xor", (acc0 + 8 * j + b, acc0 + 8 * j + b, t + b)))
+        E(Op("label", (f".Lrd_end{w}",)))
+    E(Op("s_waitcnt_lgkm_n", (0,)))
+    E(Op("s_barrier", ()))
+    _lu_solve_and_store_chunked(E, spec)
+    E(Op("label", (".Lnext",)))
+    E(Op("s_nop", (4,)))
+    E(Op("s_lshrk", (46, 18, 2)))                     # item stride: the workgroups
+    E(Op("s_add", (28, 28, 46)))
+    E(Op("s_far_jump", (".Litem", 1)))
+    E(Op("label", (".Lend",)))
+    E(Op("s_endpgm", ()))
 
 
 def _lu_solve_and_store_chunked(E, spec: KernelSpec):
@@ -2254,9 +2363,35 @@ class Emulator:
         self.mem[b][addr - b: addr - b + len(data)] = np.frombuffer(data, np.uint8)
 
     def run_wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int):
+        """One wave alone (an s_barrier lets it through at once)."""
+        gen = self._wave(kernarg, workgroup, wave_in_wg, None)
+        while True:
+            try:
+                next(gen)
+            except StopIteration as e:
+                return e.value
+
+    def run_workgroup(self, kernarg: bytes, workgroup: int, n_waves: int, lds_bytes: int):
+        """The waves of one workgroup over one shared LDS: each runs to its
+        next s_barrier (or its end) in turn, and a barrier releases once every
+        wave still running has reached it (waves that ended do not count, as
+        on the hardware)."""
+        lds = np.zeros(lds_bytes, np.uint8)
+        gens = {w: self._wave(kernarg, workgroup, w, lds) for w in range(n_waves)}
+        steps = 0
+        while gens:
+            for w in list(gens):
+                try:
+                    next(gens[w])
+                except StopIteration as e:
+                    steps += e.value
+                    del gens[w]
+        return steps
+
+    def _wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int, shared_lds):
         v = np.zeros((256, 64), dtype=np.uint64)
         s = [0] * 104
-        lds = np.zeros(LDS_TAB_BYTES, np.uint8)
+        lds = np.zeros(LDS_TAB_BYTES, np.uint8) if shared_lds is None else shared_lds
         pend_lgkm = []
         ka = np.frombuffer(kernarg, np.uint32)
         pending = []  # list of (regs, values, lanes) in issue order
@@ -2462,6 +2597,9 @@ class Emulator:
             elif n == "s_cmp_eq_k_br":
                 if s[a[0]] == a[1]:
                     pc = self.labels[a[2]]
+            elif n == "s_cmp_lg_k_br":
+                if s[a[0]] != a[1]:
+                    pc = self.labels[a[2]]
             elif n == "s_cbranch_execz":
                 if not exec_.any():
                     pc = self.labels[a[0]]
@@ -2616,6 +2754,10 @@ class Emulator:
                                    np.array([rv(d + q)[l] for q in range(4)], np.uint32).tobytes())
                     else:
                         self.write(base + int(off[l]) + a[3], bytes([int(rv(d)[l]) & 0xFF]))
+            elif n == "s_barrier":
+                if pend_lgkm:
+                    raise EmuError("s_barrier with LDS operations outstanding")
+                yield steps
             elif n == "s_endpgm":
                 if pending:
                     # stores/loads may be outstanding at the end: retire them

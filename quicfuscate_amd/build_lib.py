@@ -124,6 +124,8 @@ def _bs_kernels(build_dir: Path) -> Path:
     # fused decode over the lane-chunk layout (one generation per lane; the
     # default decode, 'c'); the 'd' kernels above stay for QF_DECODE_LEGACY=1
     specs += [bs.KernelSpec(k, r, BS_PD, "dec", chunked=True) for (k, r) in BS_CONFIGS]
+    # small batches ('k'): the four waves of a workgroup split one item's rows
+    specs += [bs.KernelSpec(k, r, BS_PD, "dec", chunked=True, ksplit=4) for (k, r) in BS_CONFIGS]
     for k, rt in BS_ENC_ONLY:
         npass = -(-rt // BS_PASS)   # balanced passes (each pass re-reads the sources)
         j0 = 0
@@ -149,7 +151,8 @@ def _bs_kernels(build_dir: Path) -> Path:
         data = hsaco.read_bytes()
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
-        mode = "c" if spec.chunked else {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode]
+        mode = ("k" if spec.ksplit > 1 else "c") if spec.chunked else \
+            {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {BS_PD}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
     inc = build_dir / "qf_bs_blobs.inc"

@@ -488,7 +488,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
                                 ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
-    prof_end(ctx, st, ev, qf::dec_name(k, r, L));
+    prof_end(ctx, st, ev, qf::dec_name(k, r, L, G, ctx->num_cus));
     return QF_OK;
 }
 
@@ -1376,6 +1376,7 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
                                              ((uintptr_t)rows | sh->row_stride |
                                               (ctx->offs_in ? 0 : sh->rows_gen_stride)) % 16 == 0 &&
                                              std::string(qf::dec_name(k, r, L)).find("decc") != std::string::npos);
+        // (the row-split 'decs' kernels of small batches share the decc layout)
         if (qf::dec_available(k, r) && !(two && atoi(two)) && tail_ok && sh->rec_gen_stride < (1ull << 32) &&
             sh->rec_row_stride < (1ull << 32))
             return decode_fused(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);

@@ -58,7 +58,8 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // recovered row are written.  L % 16 != 0 (lane-chunk kernels only): rows are
 // read in whole 16-byte units, so they must start 16-byte aligned.
 bool dec_available(uint32_t k, uint32_t r);
-const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0);
+// the kernel dec_launch runs for (k, r, L) and, given G and num_cus, that batch size
+const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0, uint32_t G = 0, int num_cus = 0);
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,

@@ -16,7 +16,8 @@
 struct QfBsEntry {
     uint32_t k, r, pd;
     uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
-    char mode;  // 'e' encode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode
+    char mode;  // 'e' encode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
+                // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -79,6 +80,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // masked to zero before the store); syn (the syndrome rows' tail is junk
     // the combine never stores); the lane-chunk decode ('c': the lane holding
     // the last unit stores it bytewise); never the item-layout decode ('d')
+    const bool chunked = e->mode == 'c' || e->mode == 'k';
     if ((L % 16 && (e->mode == 'd' || (e->mode == 'e' && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
@@ -92,15 +94,16 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     const uint32_t Lu = (L + 15) / 16;
     // lane-chunk layout of the chunked fused decode ('c'): lane-chunk = units
     // q and q + Q of one generation, Q = ceil(Lu / 2), 64 lane-chunks per item
-    if (e->mode == 'c') Lv = (Lu + 1) / 2;
+    if (chunked) Lv = (Lu + 1) / 2;
     else if (Lv < Lu) return hipErrorInvalidValue;
     if (Lv < 2) return hipErrorInvalidValue;
     const uint64_t total = (uint64_t)G * Lv;
     if (total >= (1ull << 31)) return hipErrorInvalidValue;
     uint32_t magic, shift;
     magic_for(Lv, &magic, &shift);
-    const uint32_t n_items = (uint32_t)(e->mode == 'c' ? (total + 63) / 64 : (total + 127) / 128);
-    uint32_t blocks = (n_items + 3) / 4;
+    const uint32_t n_items = (uint32_t)(chunked ? (total + 63) / 64 : (total + 127) / 128);
+    // 'k': one workgroup per item (160 KB of LDS: one workgroup per CU)
+    uint32_t blocks = e->mode == 'k' ? n_items : (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     // persistent grids (the item loop strides by the grid's wave count):
     // QF_ENC_BLOCKS_PER_CU / QF_DEC_BLOCKS_PER_CU cap the grid at that many
@@ -144,11 +147,11 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[20] = (uint32_t)(uintptr_t)lu;
     a[21] = (uint32_t)((uintptr_t)lu >> 32);
     a[22] = lu_stride;
-    if (e->mode == 'c') a[23] = L % 16;   // bytes of the partial last unit (0: whole)
+    if (chunked) a[23] = L % 16;   // bytes of the partial last unit (0: whole)
     a[24] = (uint32_t)(uintptr_t)tab256;
     a[25] = (uint32_t)((uintptr_t)tab256 >> 32);
     // generation offset tables, the last 16 kernarg bytes (bs_codegen S_OFFS)
-    const int ot = (e->mode == 'd' || e->mode == 'c') ? 28 : 20;
+    const int ot = (e->mode == 'd' || chunked) ? 28 : 20;
     a[ot] = (uint32_t)(uintptr_t)src_offs;
     a[ot + 1] = (uint32_t)((uintptr_t)src_offs >> 32);
     a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
@@ -231,18 +234,30 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
 }
 
 // the chunked fused decode unless QF_DECODE_LEGACY=1 (or the row is too short
-// for two units per lane-chunk pair)
-static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L) {
+// for two units per lane-chunk pair); for a batch of at most one item per CU
+// (G > 0 and num_cus given) its row-split form 'k', unless QF_DECODE_KSPLIT=0
+// (tools/dec_lab.py --small: 32 against 51-56 us from G = 1 to 256 at the C3
+// shape; past one item per CU the one-wave-per-item kernel wins)
+static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G = 0, int num_cus = 0) {
     const char* leg = getenv("QF_DECODE_LEGACY");
     const QfBsEntry* c = find('c', k, r);
-    if (c && !(leg && atoi(leg)) && (L == 0 || (L + 15) / 16 >= 3)) return c;
+    if (c && !(leg && atoi(leg)) && (L == 0 || (L + 15) / 16 >= 3)) {
+        if (G && num_cus > 0 && L) {
+            const char* v = getenv("QF_DECODE_KSPLIT");
+            const bool ks = !(v && !atoi(v));
+            const uint64_t Q = ((L + 15) / 16 + 1) / 2, items = ((uint64_t)G * Q + 63) / 64;
+            const QfBsEntry* kk = find('k', k, r);
+            if (ks && kk && items <= (uint64_t)num_cus) return kk;
+        }
+        return c;
+    }
     return find('d', k, r);
 }
 
 bool dec_available(uint32_t k, uint32_t r) { return find_dec(k, r, 0) != nullptr; }
 
-const char* dec_name(uint32_t k, uint32_t r, uint32_t L) {
-    const QfBsEntry* e = find_dec(k, r, L);
+const char* dec_name(uint32_t k, uint32_t r, uint32_t L, uint32_t G, int num_cus) {
+    const QfBsEntry* e = find_dec(k, r, L, G, num_cus);
     return e ? e->name : nullptr;
 }
 
@@ -251,14 +266,14 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
                       const uint64_t* rows_offs, const uint64_t* rec_offs) {
-    const QfBsEntry* e = find_dec(k, r, L);
+    const QfBsEntry* e = find_dec(k, r, L, G, num_cus);
     if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
         return hipErrorInvalidValue;
     // the LU record pointer is computed with a 32-bit stride multiply
     if ((uint64_t)G * lu_stride >= (1ull << 40)) return hipErrorInvalidValue;
     // unpadded lane space: the kernel is VALU-bound, padding lanes would be
     // pure extra work (and the recovered rows are caller memory, payload only)
-    if (L % 16 && e->mode != 'c') return hipErrorInvalidValue;
+    if (L % 16 && e->mode != 'c' && e->mode != 'k') return hipErrorInvalidValue;
     return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, (L + 15) / 16, map_stride, smap, zero,
                   lu, lu_stride, tab256, rows_offs, rec_offs);
 }

@@ -285,7 +285,8 @@ def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=Fal
     """Run the fused decode kernel (mode "dec") on the emulator: random
     erasures (or `erase` sources), random accepted repairs in random slots,
     LU records from bs.lu_record; returns the number of wrong rows."""
-    spec = bs.KernelSpec(k, r, pd, mode="dec", chunked=chunked, wave_gen=wave_gen, **spec_kw)
+    spec = bs.KernelSpec(k, r, pd, mode="dec", chunked=chunked, wave_gen=wave_gen,
+                         **{a: b for a, b in spec_kw.items() if not a.startswith("_")})
     rng = np.random.default_rng(seed)
     rs = L + 16
     n_slots = k + 2
@@ -324,6 +325,8 @@ def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=Fal
         Lv = (L + 15) // 16 if L % 16 else None
         items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
         waves = (items + 3) // 4
+        if spec.ksplit > 1:   # one workgroup per item (fewer: persistent)
+            waves = max(1, items - spec_kw.get("_fewer_wgs", 0))
     else:
         waves = (bs.launch_geometry(L, G, Lv)[2] + 3) // 4
     so = do = 0
@@ -339,6 +342,9 @@ def _dec_case(oracle, k, r, pd, L, G, seed, erase=None, padded=True, chunked=Fal
                      Lv=Lv, lu=(REC, bs.LU_REC_BYTES), tables=TAB, src_offs=so, dst_offs=do, chunked=chunked,
                      wave_gen=wave_gen)
     for wg in range(waves):
+        if spec.ksplit > 1:
+            emu.run_workgroup(ka, wg, 4, spec.lds_bytes)
+            continue
         for w in range(4):
             emu.run_wave(ka, wg, w)
     if offs:
@@ -523,6 +529,23 @@ def test_emulated_fused_decode_lu_schedule(oracle, k, r, pd, L, G, seed, erase, 
     """The interleaved LU schedule (lu_ilp: 2-3 dwords' products in separate
     temps, selectors stage by stage) recovers the same rows."""
     assert _dec_case(oracle, k, r, pd, L, G, seed, erase, padded=False, chunked=True, lu_ilp=lu_ilp) == 0
+
+
+@pytest.mark.parametrize("k,r,pd,L,G,seed,erase,offs,fewer", [
+    (8, 4, 2, 96, 6, 1, None, False, 0),
+    (16, 16, 3, 1200, 2, 7, 13, False, 0),   # lane-chunks straddle items; jmax up to 16
+    (16, 16, 2, 96, 4, 4, 16, True, 0),      # all 16 blocks, offset tables
+    (5, 3, 1, 64, 9, 5, 0, False, 0),        # nothing erased
+    (8, 5, 2, 100, 5, 8, None, False, 0),    # L % 16 = 4: bytewise tail
+    (3, 4, 2, 64, 5, 11, None, False, 0),    # k < 4: a wave with no source row
+    (16, 10, 3, 1200, 6, 12, 6, False, 2),   # fewer workgroups than items: persistent loop
+])
+def test_emulated_fused_decode_ksplit(oracle, k, r, pd, L, G, seed, erase, offs, fewer):
+    """ksplit = 4 (qf_cauchy_decs_*): the four waves of a workgroup split an
+    item's rows, waves 1..3 hand partial syndromes to wave 0 through LDS
+    (barriers emulated), and the recovered rows equal the sources."""
+    assert _dec_case(oracle, k, r, pd, L, G, seed, erase, padded=False, chunked=True, offs=offs, ksplit=4,
+                     _fewer_wgs=fewer) == 0
 
 
 @pytest.mark.parametrize("k,r,pd,L,G,seed,erase", [

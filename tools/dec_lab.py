@@ -82,6 +82,8 @@ VARIANTS = [
     ("decc_5", {"chunked": True}, ()),
     ("decc_ilp_2", {"chunked": True, "lu_ilp": True}, ()),
     ("lu_ilp_full", {"chunked": True, "lab_lu_only": True, "lu_ilp": True}, ()),
+    # small batches: one wave per item (decc) against four waves per item (decs)
+    ("decs", {"chunked": True, "ksplit": 4}, ()),
 ]
 PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]   # need all three built
 
@@ -135,10 +137,11 @@ def run(G, reps):
     k, r, L, e = 64, 16, 1200, 13
     n_slots = k - e + r
     erased, smap = c3_inputs(G, k, r, L, e)
-    recs = np.zeros((256, bs.LU_REC_BYTES), np.uint8)
-    for q in range(256):
+    nr = min(256, G)
+    recs = np.zeros((nr, bs.LU_REC_BYTES), np.uint8)
+    for q in range(nr):
         recs[q] = bs.lu_record(k, r, list(range(e)), erased[q].tolist())
-    lu = np.tile(recs, (G // 256 + 1, 1))[:G]
+    lu = np.tile(recs, (G // nr + 1, 1))[:G]
     rows = torch.randint(0, 256, (G * n_slots * L,), dtype=torch.uint8, device=dev)
     rec = torch.empty(G * e * L, dtype=torch.uint8, device=dev)
     d_map = torch.from_numpy(smap.reshape(-1)).to(dev)
@@ -162,6 +165,8 @@ def run(G, reps):
         if chunked:
             n_items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
         blocks = (n_items + 3) // 4
+        if m["kw"].get("ksplit", 1) > 1:
+            blocks = n_items
         if m["kw"].get("cap"):
             blocks = min(blocks, m["kw"]["cap"])
         ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * L, e * L, L, L, L, G, blocks * 4,
@@ -176,6 +181,7 @@ def run(G, reps):
         def launch(st=stream):
             assert hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(st.cuda_stream),
                                              None, extra) == 0
+        # (LDS: the code object's own group segment size)
 
         prepared[m["name"]] = (launch, mod, (kbuf, size, extra, buf))
         return launch, n_items
@@ -226,12 +232,16 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/dec_lab.json")
     ap.add_argument("--only", default="", help="comma-separated variant names (build)")
+    ap.add_argument("--small", default="", help="comma-separated G values: run every variant at each")
     a = ap.parse_args()
     if a.only:
         ONLY = set(a.only.split(","))
     if a.cmd == "build":
         build()
     else:
-        r = run(a.G, a.reps)
+        if a.small:
+            r = {f"G{g}": run(int(g), a.reps) for g in a.small.split(",")}
+        else:
+            r = run(a.G, a.reps)
         Path(a.out).parent.mkdir(exist_ok=True)
         Path(a.out).write_text(json.dumps(r, indent=1))
