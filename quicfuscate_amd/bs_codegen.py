@@ -421,7 +421,7 @@ class KernelSpec:
     def name(self) -> str:
         if self.mode == "cmb":
             return f"qf_combine_bs_r{self.r}"
-        tag = {"enc": "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
+        tag = {"enc": "bss" if self.ksplit > 1 else "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
             tag = "decs" if self.ksplit > 1 else "decc"
         if self.rt != self.r or self.j0:
@@ -518,6 +518,8 @@ class KernelSpec:
     def lds_bytes(self) -> int:
         if self.mode == "dec" and self.ksplit > 1:
             return LDS_TAB_BYTES + (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
+        if self.mode == "enc" and self.ksplit > 1:
+            return (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
         return LDS_TAB_BYTES if self.mode == "dec" else 0
 
 
@@ -726,7 +728,10 @@ def _prologue(E, spec: KernelSpec):
         E(Op("s_lshl", (30, 30, 2)))         # w' * 4
     else:
         E(Op("s_lshl", (30, 2, 2)))          # s30 = workgroup_id * 4   (s2 = workgroup id)
-    E(Op("s_add", (28, 29, 30)))             # s28 = item = global wave id
+    if spec.ksplit > 1:
+        E(Op("s_lshrk", (28, 30, 2)))        # s28 = the workgroup's item (all its waves)
+    else:
+        E(Op("s_add", (28, 29, 30)))         # s28 = item = global wave id
     E(Op("s_mov", (32, 10)))
     E(Op("s_movk", (33, 0)))
     E(Op("s_mov", (34, 11)))
@@ -848,6 +853,9 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     E = ops.append
     _prologue(E, spec)
 
+    ks = spec.ksplit
+    step = 46 if ks > 1 else 32       # row pointer step: s[46:47] = {ks * row stride, 0}
+
     def load_row(row: int):
         b = ring0 + 8 * (row % nbuf)
         E(Op("s_exec", (26,)))
@@ -855,21 +863,46 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         E(Op("s_exec", (24,)))
         E(Op("load16", (b + 4, V_SRCB, 0, spec.ld_policy)))
         E(Op("s_exec", (None,)))
-        E(Op("v_add64_s", (V_SRCA, V_SRCA, 32)))
-        E(Op("v_add64_s", (V_SRCB, V_SRCB, 32)))
+        E(Op("v_add64_s", (V_SRCA, V_SRCA, step)))
+        E(Op("v_add64_s", (V_SRCB, V_SRCB, step)))
 
-    for row in range(min(pd, k)):
-        load_row(row)
-    for i in range(k):
-        if i + pd < k:
-            load_row(i + pd)
-        after = min(pd, k - 1 - i)
-        E(Op("s_waitcnt_vm", (2 * after,)))
-        _source_row(ops, C, i, r, ring0 + 8 * (i % nbuf), acc0, init=(i == 0), xor3=spec.xor3,
-                    bfi=spec.bfi_transpose, vmask=spec.vmask)
+    def rows_of(srcs: list[int]):
+        for m in range(min(pd, len(srcs))):
+            load_row(m)
+        for m, i in enumerate(srcs):
+            if m + pd < len(srcs):
+                load_row(m + pd)
+            after = min(pd, len(srcs) - 1 - m)
+            E(Op("s_waitcnt_vm", (2 * after,)))
+            _source_row(ops, C, i, r, ring0 + 8 * (m % nbuf), acc0, init=(m == 0), xor3=spec.xor3,
+                        bfi=spec.bfi_transpose, vmask=spec.vmask)
+
+    if ks > 1:
+        # wave w: sources w, w + ks, ... (k >= ks): start at row w, step ks rows
+        assert k >= ks
+        E(Op("s_mul", (46, 29, 10)))
+        E(Op("s_movk", (47, 0)))
+        E(Op("v_add64_s", (V_SRCA, V_SRCA, 46)))
+        E(Op("v_add64_s", (V_SRCB, V_SRCB, 46)))
+        E(Op("s_movk", (46, ks)))
+        E(Op("s_mul", (46, 46, 10)))
+        for w in range(1, ks):
+            E(Op("s_cmp_lg_k_br", (29, w, f".Lnsec{w}")))
+            E(Op("s_far_jump", (f".Lsec{w}", 40 + w)))
+            E(Op("label", (f".Lnsec{w}",)))
+        for w in range(ks):
+            E(Op("label", (f".Lsec{w}",)))
+            rows_of([i for i in range(k) if i % ks == w])
+            if w + 1 < ks:
+                E(Op("s_far_jump", (".Lsec_end", 50 + w)))
+        E(Op("label", (".Lsec_end",)))
+    else:
+        rows_of(list(range(k)))
     # planes -> bytes, store 2 x 16 bytes per lane per repair
     for j in range(r):
         ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose, spec.vmask))
+    if ks > 1:   # partial repairs of waves 1.. into wave 0 (temps: the ring, dead now)
+        _ksplit_reduce(E, ks, r, acc0, ring0, ring0 + 8, 0, jmax_guard=False)
     # padding lanes (stored, not loaded: the zero tail) hold garbage, since
     # masked loads leave stale planes in their half of the ring; byte
     # positions are independent, so clearing their half of the repairs here
@@ -902,7 +935,10 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     E(Op("s_nop", (4,)))
     for j in range(r):
         _store_pair(E, acc0 + 8 * j, S_STA, S_STB, spec.st_policy)
-    _epilogue_next_item(E, far=spec.far)
+    if ks > 1:
+        _ksplit_epilogue(E)
+    else:
+        _epilogue_next_item(E, far=spec.far)
     return ops
 
 
@@ -1626,40 +1662,51 @@ def _dec_ksplit(E, ops: list, spec: KernelSpec, seq, load_row, present):
         if w + 1 < ks:
             E(Op("s_far_jump", (".Lsec_end", 50 + w)))
     E(Op("label", (".Lsec_end",)))
-    E(Op("v_lshl", (V_ADDR, 4, V_LANE)))             # LDS lane offset 16 l
+    _ksplit_reduce(E, ks, r, acc0, V_ADDR, ring0, LDS_TAB_BYTES, jmax_guard=True)
+    _lu_solve_and_store_chunked(E, spec)
+    _ksplit_epilogue(E)
+
+
+def _ksplit_reduce(E, ks: int, nblk: int, acc0: int, areg: int, tmp: int, lds0: int, jmax_guard: bool):
+    """Partial accumulator blocks (byte form) of waves 1..ks-1 -> LDS at
+    lds0 + (w - 1) nblk 2 KiB, barrier, wave 0 XORs them into its own,
+    barrier; waves 1.. then jump to .Lnext, wave 0 falls through.  areg and
+    areg + 1: LDS address VGPRs, tmp..tmp+7: temps (dead registers)."""
+    E(Op("v_lshl", (areg, 4, V_LANE)))              # LDS lane offset 16 l
     E(Op("s_cmp_eq_k_br", (29, 0, ".Lred0")))
-    # waves 1..: partial blocks -> LDS [LDS_TAB_BYTES + (w - 1) r 2 KiB]
     E(Op("s_addk", (46, 29, -1)))
-    E(Op("s_movk", (47, r * KSPLIT_BLOCK_BYTES)))
+    E(Op("s_movk", (47, nblk * KSPLIT_BLOCK_BYTES)))
     E(Op("s_mul", (46, 46, 47)))
-    E(Op("s_addk", (46, 46, LDS_TAB_BYTES)))
-    E(Op("v_add_s", (V_ADDR, 46, V_ADDR)))
-    for j in range(r):
-        E(Op("s_cmp_le_k_br", (S_JMAX, j, ".Lwr_end")))
-        E(Op("ds_write_b128", (V_ADDR, acc0 + 8 * j, KSPLIT_BLOCK_BYTES * j)))
-        E(Op("ds_write_b128", (V_ADDR, acc0 + 8 * j + 4, KSPLIT_BLOCK_BYTES * j + 1024)))
+    E(Op("s_addk", (46, 46, lds0)))
+    E(Op("v_add_s", (areg, 46, areg)))
+    for j in range(nblk):
+        if jmax_guard:
+            E(Op("s_cmp_le_k_br", (S_JMAX, j, ".Lwr_end")))
+        E(Op("ds_write_b128", (areg, acc0 + 8 * j, KSPLIT_BLOCK_BYTES * j)))
+        E(Op("ds_write_b128", (areg, acc0 + 8 * j + 4, KSPLIT_BLOCK_BYTES * j + 1024)))
     E(Op("label", (".Lwr_end",)))
     E(Op("s_waitcnt_lgkm_n", (0,)))
     E(Op("s_barrier", ()))
     E(Op("s_barrier", ()))
     E(Op("s_far_jump", (".Lnext", 60)))
-    # wave 0: add the partials in (temps: the ring, dead now), solve, store
     E(Op("label", (".Lred0",)))
     E(Op("s_barrier", ()))
     for w in range(1, ks):
-        E(Op("v_addk", (V_ADDR + 1, LDS_TAB_BYTES + (w - 1) * r * KSPLIT_BLOCK_BYTES, V_ADDR)))
-        for j in range(r):
-            E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lrd_end{w}")))
-            t = ring0 + 8 * (j % nbuf)
-            E(Op("ds_read_b128", (t, V_ADDR + 1, KSPLIT_BLOCK_BYTES * j)))
-            E(Op("ds_read_b128", (t + 4, V_ADDR + 1, KSPLIT_BLOCK_BYTES * j + 1024)))
+        E(Op("v_addk", (areg + 1, lds0 + (w - 1) * nblk * KSPLIT_BLOCK_BYTES, areg)))
+        for j in range(nblk):
+            if jmax_guard:
+                E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lrd_end{w}")))
+            E(Op("ds_read_b128", (tmp, areg + 1, KSPLIT_BLOCK_BYTES * j)))
+            E(Op("ds_read_b128", (tmp + 4, areg + 1, KSPLIT_BLOCK_BYTES * j + 1024)))
             E(Op("s_waitcnt_lgkm_n", (0,)))
             for b in range(8):
-                E(Op("v_xor", (acc0 + 8 * j + b, acc0 + 8 * j + b, t + b)))
+                E(Op("v_xor", (acc0 + 8 * j + b, acc0 + 8 * j + b, tmp + b)))
         E(Op("label", (f".Lrd_end{w}",)))
     E(Op("s_waitcnt_lgkm_n", (0,)))
     E(Op("s_barrier", ()))
-    _lu_solve_and_store_chunked(E, spec)
+
+
+def _ksplit_epilogue(E):
     E(Op("label", (".Lnext",)))
     E(Op("s_nop", (4,)))
     E(Op("s_lshrk", (46, 18, 2)))                     # item stride: the workgroups

@@ -132,6 +132,8 @@ def _bs_kernels(build_dir: Path) -> Path:
         for p in range(npass):
             rp = (rt - j0) // (npass - p)
             specs.append(bs.KernelSpec(k, rp, BS_PD, "enc", r_total=rt, j0=j0))
+            # small batches ('f'): the four waves of a workgroup split one item's sources
+            specs.append(bs.KernelSpec(k, rp, BS_PD, "enc", r_total=rt, j0=j0, ksplit=4))
             j0 += rp
     # decode syndromes of the same codes for long rows (slot map read by the
     # scalar unit, _generate_synw): same balanced passes, items whose
@@ -152,9 +154,14 @@ def _bs_kernels(build_dir: Path) -> Path:
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         mode = ("k" if spec.ksplit > 1 else "c") if spec.chunked else \
-            {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode]
+            ("f" if spec.mode == "enc" and spec.ksplit > 1 else
+             {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode])
         entries.append(f"    {{{k}u, {r}u, {BS_PD}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
+    # the loader caches one module per table entry (qf_bs.h BsCache::kMax)
+    kmax = int(re.search(r"kMax = (\d+)", (CSRC / "qf_bs.h").read_text()).group(1))
+    if len(specs) > kmax:
+        raise RuntimeError(f"{len(specs)} generated kernels > BsCache::kMax = {kmax} (qf_bs.h)")
     inc = build_dir / "qf_bs_blobs.inc"
     inc.write_text("// generated by quicfuscate_amd/build_lib.py from bs_codegen.py -- do not edit\n"
                    + "\n".join(blobs) + "\nstatic const QfBsEntry qf_bs_table[] = {\n"

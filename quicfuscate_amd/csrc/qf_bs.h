@@ -8,7 +8,7 @@
 namespace qf {
 
 struct BsCache {
-    static const int kMax = 64;
+    static const int kMax = 128;   // >= the entries of qf_bs_table (build_lib.py checks)
     hipModule_t mod[kMax] = {};
     hipFunction_t fn[kMax] = {};
 };

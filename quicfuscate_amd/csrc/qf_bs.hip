@@ -17,7 +17,8 @@ struct QfBsEntry {
     uint32_t k, r, pd;
     uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
     char mode;  // 'e' encode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
-                // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves
+                // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves,
+                // 'f' the encode (passes of C5 codes) with an item's sources split the same way
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -81,7 +82,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // the combine never stores); the lane-chunk decode ('c': the lane holding
     // the last unit stores it bytewise); never the item-layout decode ('d')
     const bool chunked = e->mode == 'c' || e->mode == 'k';
-    if ((L % 16 && (e->mode == 'd' || (e->mode == 'e' && Lv != s19))) || L < 32 ||
+    const bool enc = e->mode == 'e' || e->mode == 'f';
+    if ((L % 16 && (e->mode == 'd' || (enc && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
         return hipErrorInvalidValue;
@@ -102,15 +104,15 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     uint32_t magic, shift;
     magic_for(Lv, &magic, &shift);
     const uint32_t n_items = (uint32_t)(chunked ? (total + 63) / 64 : (total + 127) / 128);
-    // 'k': one workgroup per item (160 KB of LDS: one workgroup per CU)
-    uint32_t blocks = e->mode == 'k' ? n_items : (n_items + 3) / 4;
+    // 'k' / 'f': one workgroup per item
+    uint32_t blocks = (e->mode == 'k' || e->mode == 'f') ? n_items : (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     // persistent grids (the item loop strides by the grid's wave count):
     // QF_ENC_BLOCKS_PER_CU / QF_DEC_BLOCKS_PER_CU cap the grid at that many
     // 4-wave blocks per CU, so an encode and a decode launched on two streams
     // can be resident on every SIMD at once
     {
-        const char* cap = getenv(e->mode == 'e' ? "QF_ENC_BLOCKS_PER_CU" : "QF_DEC_BLOCKS_PER_CU");
+        const char* cap = getenv(enc ? "QF_ENC_BLOCKS_PER_CU" : "QF_DEC_BLOCKS_PER_CU");
         const int c = cap ? atoi(cap) : 0;
         if (c > 0 && num_cus > 0 && blocks > (uint32_t)(c * num_cus)) blocks = (uint32_t)(c * num_cus);
     }
@@ -131,7 +133,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[13] = n_items;
     a[14] = blocks * 4;
     a[15] = s19;
-    if (e->mode == 'e') {
+    if (enc) {
         // byte masks of the last unit's dwords (bs_codegen.tail_masks)
         const uint32_t tb = L % 16 ? L % 16 : 16;
         for (uint32_t d = 0; d < 4; ++d) {
@@ -190,10 +192,19 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
         return hipErrorInvalidValue;
     if (!zero_tail && L % 16) return hipErrorInvalidValue;
     if (!find('e', k, r)) return hipErrorInvalidValue;
+    // batches of at most one item (128 units) per CU take the 'f' kernels
+    // (the sources of an item split over its workgroup's four waves) where
+    // they exist, unless QF_ENCODE_KSPLIT=0
+    char mode = 'e';
+    {
+        const char* v = getenv("QF_ENCODE_KSPLIT");
+        const uint64_t items = ((uint64_t)G * Lv + 127) / 128;
+        if (!(v && !atoi(v)) && find('f', k, r) && num_cus > 0 && items <= (uint64_t)num_cus) mode = 'f';
+    }
     // one launch per pass of repairs (codes with more repairs than a kernel
     // holds): pass j0 writes repair rows j0 .. j0 + r_pass - 1
     for (const auto& e : qf_bs_table) {
-        if (e.mode != 'e' || e.k != k || e.rt != r) continue;
+        if (e.mode != mode || e.k != k || e.rt != r) continue;
         hipError_t err = launch(cache, &e, num_cus, st, src, dst + (uint64_t)e.j0 * drs, sgs, dgs, srs, drs, L, G,
                                 Lv, Lv, nullptr, nullptr, nullptr, 0, nullptr, src_offs, dst_offs);
         if (err != hipSuccess) return err;

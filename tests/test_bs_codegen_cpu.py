@@ -404,6 +404,45 @@ def test_emulated_fused_decode_unpadded_lanes(oracle):
     assert _dec_case(oracle, 16, 16, 3, 1200, 2, 7, 13, padded=False) == 0
 
 
+@pytest.mark.parametrize("k,rt,L,G,split,fewer", [
+    (8, 4, 72, 5, 4, 0),       # L % 16 = 8: partial last unit, one pass
+    (6, 5, 100, 4, 3, 0),      # passes of 3 + 2 repairs
+    (9, 20, 1200, 3, 16, 0),   # passes of 16 + 4, the C2 row length
+    (4, 3, 64, 40, 3, 2),      # k = ks, 3 items on one workgroup (persistent loop)
+])
+def test_emulated_encode_ksplit(oracle, k, rt, L, G, split, fewer):
+    """ksplit = 4 encode (qf_cauchy_bss_*): the four waves of a workgroup take
+    sources w, w + 4, ... of one item and wave 0 sums the partial repairs
+    through LDS (barriers emulated) before the zero-tail stores."""
+    Lv = bs.padded_units(L)
+    rng = np.random.default_rng(k * 37 + L + rt)
+    srs = (L + 15) // 16 * 16 + 16 * (k % 2)
+    sgs = k * srs
+    drs = 16 * Lv + 64
+    dgs = rt * drs
+    src = rng.integers(0, 256, G * sgs, dtype=np.uint8)
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    SRC, DST = 0x10000000, 0x40000000
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    wgs = max(1, items - fewer)
+    for j0 in range(0, rt, split):
+        spec = bs.KernelSpec(k, min(split, rt - j0), 3, r_total=rt, j0=j0, ksplit=4)
+        emu = bs.Emulator(bs.generate(spec))
+        emu.add_buffer(SRC, src)
+        emu.add_buffer(DST, dst)
+        ka = bs.kernargs(SRC, DST + j0 * drs, sgs, dgs, srs, drs, L, G, wgs * 4, Lv=Lv, zero_tail=True)
+        for wg in range(wgs):
+            emu.run_workgroup(ka, wg, 4, spec.lds_bytes)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, rt)
+        for j in range(rt):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            assert (dst[off + L: off + 16 * Lv] == 0).all(), (g, j)
+            assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
+
+
 @pytest.mark.parametrize("k,rt,L,G,split", [
     (8, 4, 72, 5, 4),      # L % 16 = 8: partial last unit, one pass
     (6, 5, 100, 4, 3),     # L % 16 = 4, passes of 3 + 2 repairs

@@ -102,13 +102,16 @@ PATHS = ["default", "default_1wave", "syn", "general", "syn_bs", "general_bs"]
 
 def _path(monkeypatch, path):
     # "default" at these batch sizes (at most one item per CU) runs the
-    # row-split fused decode (qf_cauchy_decs_*: four waves per item);
-    # "default_1wave" pins the one-wave-per-item kernel (qf_cauchy_decc_*)
+    # row-split kernels (qf_cauchy_decs_*, and qf_cauchy_bss_* for the r > 16
+    # syndrome passes: four waves per item); "default_1wave" pins the
+    # one-wave-per-item kernels (qf_cauchy_decc_*, qf_cauchy_bs_*)
     if path == "default_1wave":
         monkeypatch.setenv("QF_DECODE_KSPLIT", "0")
+        monkeypatch.setenv("QF_ENCODE_KSPLIT", "0")
         path = "default"
     else:
         monkeypatch.delenv("QF_DECODE_KSPLIT", raising=False)
+        monkeypatch.delenv("QF_ENCODE_KSPLIT", raising=False)
     # "*_bs": the payload pass takes the bit-sliced qf_combine_bs at every row
     # length (by default only rows of >= 64 lane-chunks of 32 B do); "general"
     # keeps k_combine_slots at every length (QF_COMBINE_BS=0)
