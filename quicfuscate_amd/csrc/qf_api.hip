@@ -518,7 +518,11 @@ static hipError_t combine_payload(qf_ctx* ctx, const qf::CombineSlotsArgs& a, in
         if (name) *name = "qf_combine_bs_r16";
         return qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx);
     }
-    if (name) *name = "k_combine_slots<" + std::to_string(PD) + ">";
+    if (name) {
+        const char* sp = getenv("QF_COMBINE_SPLIT");
+        const bool split = !(sp && !atoi(sp)) && (a.total_units + 63) / 64 <= (uint64_t)ctx->num_cus;
+        *name = split ? std::string("k_combine_slots_split") : "k_combine_slots<" + std::to_string(PD) + ">";
+    }
     return qf::launch_combine_slots(a, PD, ctx->num_cus, st);
 }
 

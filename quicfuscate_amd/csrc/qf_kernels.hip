@@ -31,6 +31,7 @@
 //  k_fill_splitmix              synthetic payload generator.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "qf_kernels.h"
@@ -454,6 +455,112 @@ __global__ void __launch_bounds__(256, (PD == 1 ? 3 : 2)) k_combine_slots(Combin
         else if (jmax <= 13) combine_slots_dispatch<13, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
         else if (jmax <= 14) combine_slots_dispatch<14, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
         else combine_slots_dispatch<16, PD>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, full);
+    }
+}
+
+// Small batches (at most one 64-unit wave-item per CU): the four waves of a
+// block share one wave-item and split its slot pairs (wave w takes pairs w,
+// w + 4, ...; the next pair's rows and records load while the current one
+// multiplies), the partial outputs of waves 1..3 meet wave 0's in LDS, and
+// wave 0 stores.  Same arithmetic as combine_slots_item, so the same bytes.
+template <int R>
+QF_DEV void combine_slots_split_item(const CombineSlotsArgs& a, const uint32_t* __restrict__ tab256,
+                                     const uint8_t* rowp, uint8_t* outp, const uint8_t* coefp, uint32_t nbytes,
+                                     uint32_t e_lane, uint32_t bound_lane, uint32_t smax, uint32_t wave,
+                                     uint4 (*part)[16][64]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t rs = a.row_stride;
+    const uint32_t zs = a.zero_slot;
+    const uint32_t blast = bound_lane ? bound_lane - 1 : 0;
+    uint4 acc[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) acc[j] = make_uint4(0, 0, 0, 0);
+#define QF_ROW(s) (rowp + (uint64_t)((s) < blast ? (s) : blast) * rs)
+#define QF_COEF(s) (coefp + (uint64_t)((s) < bound_lane ? (s) : zs) * 16)
+    uint32_t s = 2 * wave;
+    if (s < smax) {
+        uint4 xa = load_unit(QF_ROW(s), nbytes), xb = load_unit(QF_ROW(s + 1), nbytes);
+        uint4 ca = *reinterpret_cast<const uint4*>(QF_COEF(s)), cb = *reinterpret_cast<const uint4*>(QF_COEF(s + 1));
+        for (; s < smax; s += 8) {
+            uint4 nxa = xa, nxb = xb, nca = ca, ncb = cb;
+            if (s + 8 < smax) {
+                nxa = load_unit(QF_ROW(s + 8), nbytes);
+                nxb = load_unit(QF_ROW(s + 9), nbytes);
+                nca = *reinterpret_cast<const uint4*>(QF_COEF(s + 8));
+                ncb = *reinterpret_cast<const uint4*>(QF_COEF(s + 9));
+            }
+            fma_rows_slots<R>(acc, tab256, xa, xb, ca, cb);
+            xa = nxa;
+            xb = nxb;
+            ca = nca;
+            cb = ncb;
+        }
+    }
+#undef QF_ROW
+#undef QF_COEF
+    if (wave != 0) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) part[wave - 1][j][lane] = acc[j];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        for (int w = 0; w < 3; ++w) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const uint4 p = part[w][j][lane];
+                acc[j].x ^= p.x;
+                acc[j].y ^= p.y;
+                acc[j].z ^= p.z;
+                acc[j].w ^= p.w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            if ((uint32_t)j < e_lane) store_unit(outp + (uint64_t)j * a.dst_row_stride, acc[j], nbytes);
+    }
+    __syncthreads();   // part[] is rewritten by the next wave-item
+}
+
+__global__ void __launch_bounds__(256) k_combine_slots_split(CombineSlotsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab256[256 * 8];
+    __shared__ uint4 part[3][16][64];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.tab256);
+        uint4* l = reinterpret_cast<uint4*>(tab256);
+        for (uint32_t w = threadIdx.x; w < 512; w += blockDim.x) l[w] = g[w];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // every wave of the block walks the same wave-items: the barriers match
+    for (uint64_t base = (uint64_t)blockIdx.x * 64; base < a.total_units; base += (uint64_t)gridDim.x * 64) {
+        const uint64_t f = base + lane;
+        const uint8_t* rowp = a.rows;
+        uint8_t* outp = a.dst;
+        const uint8_t* coefp = a.coef;
+        uint32_t nbytes = 0, e_lane = 0, bound_lane = 0;
+        if (f < a.total_units) {
+            const uint64_t g = f / a.Lu;
+            const uint32_t u = (uint32_t)(f - g * a.Lu);
+            rowp = gen_base(a.rows, g, a.rows_gen_stride, a.rows_offs) + (uint64_t)u * 16;
+            outp = gen_base(a.dst, g, a.dst_gen_stride, a.dst_offs) + (uint64_t)u * 16;
+            coefp = a.coef + g * a.coef_gen_stride;
+            const uint32_t rem = a.L - u * 16;
+            nbytes = rem < 16 ? rem : 16;
+            const uint32_t e = a.n_out[g];
+            const uint32_t lo = a.pass * 16;
+            e_lane = e > lo ? (e - lo < 16 ? e - lo : 16) : 0;
+            bound_lane = e_lane ? a.bound[g] : 0;
+        }
+        // the same lanes in every wave: jmax and smax are block-uniform
+        const uint32_t jmax = wave_max_u32(e_lane);
+        if (jmax == 0) continue;
+        const uint32_t smax = wave_max_u32(bound_lane);
+        if (jmax <= 4)
+            combine_slots_split_item<4>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, wave, part);
+        else if (jmax <= 8)
+            combine_slots_split_item<8>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, wave, part);
+        else
+            combine_slots_split_item<16>(a, tab256, rowp, outp, coefp, nbytes, e_lane, bound_lane, smax, wave, part);
     }
 }
 
@@ -1217,6 +1324,15 @@ static hipError_t launch_slots_p(const CombineSlotsArgs& a, int num_cus, hipStre
 }
 
 hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st) {
+    // at most one 64-unit wave-item per CU: the slot-split kernel, unless
+    // QF_COMBINE_SPLIT=0
+    const uint64_t items = (a.total_units + 63) / 64;
+    const char* sp = getenv("QF_COMBINE_SPLIT");
+    if (!(sp && !atoi(sp)) && num_cus > 0 && items <= (uint64_t)num_cus) {
+        if (items == 0) return hipSuccess;
+        hipLaunchKernelGGL(k_combine_slots_split, dim3((uint32_t)items), dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (PD == 1) return launch_slots_p<1>(a, num_cus, st);
     if (PD == 2) return launch_slots_p<2>(a, num_cus, st);
     if (PD == 3) return launch_slots_p<3>(a, num_cus, st);

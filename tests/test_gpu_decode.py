@@ -105,13 +105,16 @@ def _path(monkeypatch, path):
     # row-split kernels (qf_cauchy_decs_*, and qf_cauchy_bss_* for the r > 16
     # syndrome passes: four waves per item); "default_1wave" pins the
     # one-wave-per-item kernels (qf_cauchy_decc_*, qf_cauchy_bs_*)
+    # (and the payload pass k_combine_slots_split against k_combine_slots)
     if path == "default_1wave":
         monkeypatch.setenv("QF_DECODE_KSPLIT", "0")
         monkeypatch.setenv("QF_ENCODE_KSPLIT", "0")
+        monkeypatch.setenv("QF_COMBINE_SPLIT", "0")
         path = "default"
     else:
         monkeypatch.delenv("QF_DECODE_KSPLIT", raising=False)
         monkeypatch.delenv("QF_ENCODE_KSPLIT", raising=False)
+        monkeypatch.delenv("QF_COMBINE_SPLIT", raising=False)
     # "*_bs": the payload pass takes the bit-sliced qf_combine_bs at every row
     # length (by default only rows of >= 64 lane-chunks of 32 B do); "general"
     # keeps k_combine_slots at every length (QF_COMBINE_BS=0)
