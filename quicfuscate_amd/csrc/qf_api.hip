@@ -85,6 +85,8 @@ struct qf_ctx {
     // decode workspace
     uint8_t* d_work = nullptr;
     size_t work_bytes = 0;
+    uint8_t* d_logrows = nullptr;   // GF(2^16) inputs in log form (ctx_gf16_logrows)
+    size_t logrows_bytes = 0;
     // zero row read by the syndrome kernel for rows a generation lacks
     uint8_t* d_zero = nullptr;
     size_t zero_bytes = 0;
@@ -899,6 +901,21 @@ int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out) {
     return QF_OK;
 }
 const uint32_t* ctx_tab256(qf_ctx* ctx) { return ctx->d_tab256; }
+int ctx_gf16_logrows(qf_ctx* ctx, size_t bytes, uint8_t** out) {
+    if (bytes > ctx->logrows_bytes) {
+        if (ctx->d_logrows) {
+            QF_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+            QF_CHECK_HIP(hipFree(ctx->d_logrows));
+            ctx->d_logrows = nullptr;
+            ctx->logrows_bytes = 0;
+        }
+        const size_t b = round_up(bytes, 1 << 20);
+        if (hipMalloc(&ctx->d_logrows, b) != hipSuccess) return QF_ENOMEM;
+        ctx->logrows_bytes = b;
+    }
+    *out = ctx->d_logrows;
+    return QF_OK;
+}
 int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
     int s = grow_work(ctx, bytes);
     if (s) return s;
@@ -1047,6 +1064,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     for (auto& kv : c->cauchy) hipFree(kv.second.dev);
     for (auto& kv : c->small_coef) hipFree(kv.second);
     if (c->d_tab256) hipFree(c->d_tab256);
+    if (c->d_logrows) hipFree(c->d_logrows);
     if (c->d_explog) hipFree(c->d_explog);
     if (c->d_cmbidx) hipFree(c->d_cmbidx);
     if (c->h_custom) hipHostFree(c->h_custom);

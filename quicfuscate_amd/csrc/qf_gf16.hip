@@ -44,6 +44,7 @@ constexpr uint32_t kNoLog = 0xFFFF; // log of 0 (no product)
 constexpr uint32_t kEMax = 64;      // erasures per generation the decode handles
 constexpr int kR16 = 8;             // outputs per pass (encode and combine)
 constexpr int kThreads16 = 1024;
+constexpr uint32_t kLogifyBlocks = 4;  // output blocks of 8 from which inputs go to log form first
 
 // ---- host arithmetic ------------------------------------------------------
 uint16_t h_mul(uint16_t a, uint16_t b) {
@@ -169,7 +170,44 @@ struct Mv16Args {
     uint32_t* acc_ws;       // split: [g][nout][Lp/4] accumulator (zeroed)
     uint32_t nout, nin, L, Lu, nob, nsplit, kchunk;
     uint64_t total_units;
+    uint32_t in_log;        // in holds the symbols' logs (k_logify16), not the symbols
 };
+
+// the 8 logs of a unit of a log row (k_logify16): kNoLog -> the zero offset
+QF_DEV void unpack_logs(const uint4& raw, uint32_t (&lx)[8]) {
+    const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t lg = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        lx[q] = lg == kNoLog ? kZeroOff : 2u * lg;
+    }
+}
+
+// Input rows -> log rows, once per matvec: symbol q of unit u of input c of
+// generation g -> its log (kNoLog for 0) at out + ((g nin + c) Lu + u) 16 + 2q.
+// An input feeds every block of 8 outputs, so k_matvec16 would otherwise
+// gather the same logs once per block (128 times for an Extreme window).
+__global__ void __launch_bounds__(256) k_logify16(Mv16Args a, uint64_t G, uint16_t* out) {
+    const uint64_t total = G * a.nin * a.Lu;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = f / a.Lu;
+        const uint32_t u = (uint32_t)(f - t * a.Lu);
+        const uint64_t g = t / a.nin;
+        const uint32_t c = (uint32_t)(t - g * a.nin);
+        const uint32_t nin = a.nin_g ? min(a.nin_g[g * a.nin_gs], a.nin) : a.nin;
+        if (c >= nin) continue;   // never read
+        const uint32_t nb = min(16u, a.L - 16 * u);
+        const uint32_t slot = a.isel ? a.isel[g * a.isel_gs + c] : c;
+        const uint4 raw = load16_partial(a.in + g * a.igs + (uint64_t)slot * a.irs + 16ull * u, nb);
+        const uint32_t w[4] = {bswap16x2(raw.x), bswap16x2(raw.y), bswap16x2(raw.z), bswap16x2(raw.w)};
+        uint32_t o[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            o[d] = (uint32_t)a.log[w[d] & 0xFFFF] | ((uint32_t)a.log[w[d] >> 16] << 16);
+        *reinterpret_cast<uint4*>(out + (f * 8)) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
 
 __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
     __shared__ uint16_t sexp[kOrder + 1];  // static: LDS offsets fold into the reads
@@ -214,7 +252,9 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
             for (int bb = 0; bb < kR16; ++bb) out[bb] = m[(uint64_t)min((uint32_t)bb, no - 1) * a.mrs + c];
         };
         if (c0 < c1) {
-            symbol_logs(load16_partial(ip + (uint64_t)(isel ? isel[c0] : c0) * a.irs, nb), a.log, lxn);
+            const uint4 raw0 = load16_partial(ip + (uint64_t)(isel ? isel[c0] : c0) * a.irs, nb);
+            if (a.in_log) unpack_logs(raw0, lxn);
+            else symbol_logs(raw0, a.log, lxn);
             coef_row(c0, lcr);
         }
         if (c0 + 1 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c0 + 1] : c0 + 1) * a.irs, nb);
@@ -226,7 +266,8 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
             for (int bb = 0; bb < kR16; ++bb) lc[bb] = (uint32_t)bb < no ? log_off(lcr[bb]) : kZeroOff;
             if (c + 1 < c1) {
                 // next row's log gathers and coefficients in flight during this row
-                symbol_logs(nxt, a.log, lxn);
+                if (a.in_log) unpack_logs(nxt, lxn);
+                else symbol_logs(nxt, a.log, lxn);
                 coef_row(c + 1, lcr);
                 if (c + 2 < c1) nxt = load16_partial(ip + (uint64_t)(isel ? isel[c + 2] : c + 2) * a.irs, nb);
             }
@@ -834,6 +875,29 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
     a.kchunk = (a.nin + ns - 1) / ns;
     a.acc_ws = reinterpret_cast<uint32_t*>(acc);
     a.total_units = lanes * ns;
+    // inputs feeding >= kLogifyBlocks blocks of outputs go to log form once
+    // (QF_GF16_LOGIFY=0: gather the logs in the matvec, per block)
+    a.in_log = 0;
+    {
+        const char* v = getenv("QF_GF16_LOGIFY");
+        if (!(v && !atoi(v)) && a.nob >= kLogifyBlocks) {
+            uint8_t* lr = nullptr;
+            const uint64_t n = G * a.nin * a.Lu;
+            int s = qf::ctx_gf16_logrows(ctx, n * 16, &lr);
+            if (s) return s;
+            hipEvent_t ev0 = qf::ctx_prof_begin(ctx, st);
+            hipLaunchKernelGGL(k_logify16, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, st,
+                               a, G, reinterpret_cast<uint16_t*>(lr));
+            QF_HIP(hipGetLastError());
+            qf::ctx_prof_end(ctx, st, ev0, "k_logify16");
+            a.in = lr;
+            a.igs = (uint64_t)a.nin * a.Lu * 16;
+            a.irs = (uint64_t)a.Lu * 16;
+            a.isel = nullptr;
+            a.isel_gs = 0;
+            a.in_log = 1;
+        }
+    }
     hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
     if (ns > 1) QF_HIP(hipMemsetAsync(acc, 0, G * a.nout * (size_t)a.Lu * 16, st));
     hipLaunchKernelGGL(k_matvec16, dim3(grid16(ctx, a.total_units)), dim3(kThreads16), 0, st, a);

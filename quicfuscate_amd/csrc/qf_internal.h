@@ -23,6 +23,9 @@ int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out);
 int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp);
 // The context's 256 split-table records (8 dwords each, gf256_tables.h).
 const uint32_t* ctx_tab256(qf_ctx* ctx);
+// A device buffer of >= bytes for GF(2^16) input rows in log form (its own
+// allocation, so it can sit beside the workspace; valid until the next call).
+int ctx_gf16_logrows(qf_ctx* ctx, size_t bytes, uint8_t** out);
 // qf_ctx_profile bracketing of a launch.
 hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st);
 void ctx_prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t ev, const std::string& name);
