@@ -185,6 +185,30 @@ def test_decode_bench_shape_fixed_13_erasures(qf, oracle, gpu_ctx, path, monkeyp
     check(oracle, k, L, src, gens, out, False)
 
 
+def test_decode_row_split_threshold(qf, oracle, gpu_ctx, monkeypatch):
+    """The fused decode takes the row-split kernel (qf_cauchy_decs_*, four
+    waves per item) up to one item per CU and the one-wave kernel
+    (qf_cauchy_decc_*) beyond: both sides of the switch, bit-exact."""
+    import torch
+
+    _path(monkeypatch, "default")
+    k, r, L = 64, 16, 1200
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    Q = ((L + 15) // 16 + 1) // 2          # lane-chunks per generation
+    g_max = 64 * ncu // Q                  # largest G with ceil(G*Q/64) <= ncu
+    ctx = qf.default_context()
+    for G, want in ((g_max, "decs"), (g_max + 1, "decc")):
+        rng = np.random.default_rng(G)
+        src, gens = make_batch(oracle, rng, k, r, L, G, k - 13 + r, shuffle=False, erase=13)
+        ctx.sync()
+        ctx.profile(True)
+        out = run_decode(qf, k, r, L, G, k - 13 + r, gens, False)
+        names = set(ctx.kernel_times())
+        ctx.profile(False)
+        assert f"qf_cauchy_{want}_k64_r16" in names, (G, names)
+        check(oracle, k, L, src, gens, out, False)
+
+
 def test_decode_explicit_coefficients_and_duplicates(qf, oracle, gpu_ctx):
     # random coefficient matrices (some singular) + duplicate arrivals
     rng = np.random.default_rng(7)
