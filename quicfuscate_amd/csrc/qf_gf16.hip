@@ -167,11 +167,81 @@ struct Mv16Args {
     uint32_t nin_gs;
     const uint16_t* log;
     const uint16_t* exp;
-    uint32_t* acc_ws;       // split: [g][nout][Lp/4] accumulator (zeroed)
+    uint32_t* acc_ws;       // split: nsplit slabs [g][nout][Lu][4 dwords] of partial rows
+    uint64_t slab;          // dwords per slab
     uint32_t nout, nin, L, Lu, nob, nsplit, kchunk;
     uint64_t total_units;
     uint32_t in_log;        // in holds the symbols' logs (k_logify16), not the symbols
+    // device-shaped launch (decode: e_g is known only after acceptance):
+    // k_shape16 sizes nob / nsplit / kchunk / total_units from the largest
+    // nout_g and nin_g instead of nout and nin; null: the fields above
+    struct Mv16Shape* shape;
+    uint64_t G, want;
+    uint32_t ns_cap;        // slabs acc_ws holds
 };
+
+struct Mv16Shape {
+    uint32_t nob, nsplit, kchunk, pad;
+    uint64_t total;
+};
+
+// Input chunks per lane-unit.  The grid holds `want` lanes at once (one
+// 1,024-thread block per CU: the exp table fills the LDS), and every unit
+// costs its chunk's rows, so a launch takes ceil(lanes * ns / want) rounds of
+// ceil(nin / ns) rows.  The old rule (the smallest ns with lanes * ns >=
+// want) could leave a second round a few % full: an Extreme window (9,600
+// lanes, ns 28) ran two rounds of 37 rows where ns 27 runs one of 38.  A
+// split launch adds k_finish16 (priced at 4 rows) and one slab of partial
+// rows per chunk (1/8 row each).
+__host__ __device__ uint32_t matvec_split(uint64_t lanes, uint32_t nin, uint64_t want) {
+    const uint32_t max_ns = nin / 16 > 1 ? nin / 16 : 1;   // chunks of at least 16 rows
+    uint32_t best = 1;
+    uint64_t best_cost = ((lanes + want - 1) / want) * nin;
+    for (uint32_t ns = 2; ns <= max_ns; ++ns) {
+        const uint64_t cost = ((lanes * ns + want - 1) / want) * ((nin + ns - 1) / ns) + 4 + ns / 8;
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = ns;
+        }
+    }
+    return best;
+}
+
+// one block: the launch shape from the largest nout_g / nin_g of the batch
+__global__ void __launch_bounds__(1024) k_shape16(Mv16Args a) {
+    __shared__ uint32_t red[2][16];
+    uint32_t mo = 0, mi = 0;
+    for (uint64_t g = threadIdx.x; g < a.G; g += blockDim.x) {
+        mo = max(mo, a.nout_g ? min(a.nout_g[g], a.nout) : a.nout);
+        mi = max(mi, a.nin_g ? min(a.nin_g[g * a.nin_gs], a.nin) : a.nin);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mo = max(mo, (uint32_t)__shfl_xor((int)mo, o, 64));
+        mi = max(mi, (uint32_t)__shfl_xor((int)mi, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = mo;
+        red[1][threadIdx.x >> 6] = mi;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (uint32_t w = 1; w < blockDim.x / 64; ++w) {
+        mo = max(mo, red[0][w]);
+        mi = max(mi, red[1][w]);
+    }
+    mo = max(mo, red[0][0]);
+    mi = max(mi, red[1][0]);
+    Mv16Shape sh{};
+    sh.nob = (mo + kR16 - 1) / kR16;
+    const uint64_t lanes = a.G * sh.nob * a.Lu;
+    uint32_t ns = lanes && mi && lanes < a.want ? matvec_split(lanes, mi, a.want) : 1;
+    ns = min(ns, max(a.ns_cap, 1u));
+    sh.nsplit = ns;
+    sh.kchunk = mi ? (mi + ns - 1) / ns : 1;
+    sh.total = mi ? lanes * ns : 0;
+    *a.shape = sh;
+}
 
 // the 8 logs of a unit of a log row (k_logify16): kNoLog -> the zero offset
 QF_DEV void unpack_logs(const uint4& raw, uint32_t (&lx)[8]) {
@@ -212,19 +282,28 @@ __global__ void __launch_bounds__(256) k_logify16(Mv16Args a, uint64_t G, uint16
 __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
     __shared__ uint16_t sexp[kOrder + 1];  // static: LDS offsets fold into the reads
     load_exp_lds(sexp, a.exp);
+    uint32_t nob = a.nob, nsplit = a.nsplit, kchunk = a.kchunk;
+    uint64_t total = a.total_units;
+    if (a.shape) {
+        const Mv16Shape sh = *a.shape;
+        nob = sh.nob;
+        nsplit = sh.nsplit;
+        kchunk = sh.kchunk;
+        total = sh.total;
+    }
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.total_units; f += stride) {
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total; f += stride) {
         uint64_t t = f / a.Lu;
         const uint32_t u = (uint32_t)(f - t * a.Lu);
-        const uint32_t ks = (uint32_t)(t % a.nsplit);
-        t /= a.nsplit;
-        const uint64_t g = t / a.nob;
-        const uint32_t b0 = (uint32_t)(t - g * a.nob) * kR16;
+        const uint32_t ks = (uint32_t)(t % nsplit);
+        t /= nsplit;
+        const uint64_t g = t / nob;
+        const uint32_t b0 = (uint32_t)(t - g * nob) * kR16;
         const uint32_t nout = a.nout_g ? min(a.nout_g[g], a.nout) : a.nout;
         if (b0 >= nout) continue;
         const uint32_t no = min((uint32_t)kR16, nout - b0);
         const uint32_t nin = a.nin_g ? min(a.nin_g[g * a.nin_gs], a.nin) : a.nin;
-        const uint32_t c0 = ks * a.kchunk, c1 = min(nin, c0 + a.kchunk);
+        const uint32_t c0 = ks * kchunk, c1 = min(nin, c0 + kchunk);
         const uint32_t nb = min(16u, a.L - 16 * u);
         uint32_t acc[kR16][4];
 #pragma unroll
@@ -274,7 +353,7 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
 #pragma unroll
             for (int bb = 0; bb < kR16; ++bb) mul_acc(acc[bb], lc[bb], lx, sexp);
         }
-        if (a.nsplit == 1) {
+        if (nsplit == 1) {
             uint8_t* op = a.out + g * a.ogs + 16ull * u;
 #pragma unroll
             for (int bb = 0; bb < kR16; ++bb) {
@@ -284,23 +363,24 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
                 store16_partial(op + (uint64_t)(b0 + bb) * a.ors, w, nb);
             }
         } else {
-            uint32_t* wp = a.acc_ws + ((g * a.nout + b0) * a.Lu + u) * 4;
+            // chunk ks's partial rows go to slab ks (plain stores; k_finish16 XORs the slabs)
+            uint32_t* wp = a.acc_ws + ks * a.slab + ((g * a.nout + b0) * a.Lu + u) * 4;
 #pragma unroll
             for (int bb = 0; bb < kR16; ++bb) {
                 if ((uint32_t)bb >= no) break;
                 uint32_t w[4];
                 pack_symbols(acc[bb], w);
-#pragma unroll
-                for (int d = 0; d < 4; ++d)
-                    if (w[d]) atomicXor(wp + (uint64_t)bb * a.Lu * 4 + d, w[d]);
+                *reinterpret_cast<uint4*>(wp + (uint64_t)bb * a.Lu * 4) = make_uint4(w[0], w[1], w[2], w[3]);
             }
         }
     }
 }
 
-// split accumulator -> output rows (exactly L bytes per row)
+// XOR of the split slabs -> output rows (exactly L bytes per row)
 __global__ void __launch_bounds__(256) k_finish16(Mv16Args a) {
-    const uint64_t total = (uint64_t)(a.total_units / ((uint64_t)a.nsplit * a.nob)) * a.nout;  // G * nout * Lu
+    const uint32_t nsplit = a.shape ? a.shape->nsplit : a.nsplit;
+    if (nsplit <= 1) return;   // a device-shaped launch that did not split wrote the rows itself
+    const uint64_t total = a.G * a.nout * a.Lu;
     for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total; f += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = f / a.Lu;
         const uint32_t u = (uint32_t)(f - t * a.Lu);
@@ -308,8 +388,14 @@ __global__ void __launch_bounds__(256) k_finish16(Mv16Args a) {
         const uint32_t b = (uint32_t)(t - g * a.nout);
         const uint32_t nout = a.nout_g ? min(a.nout_g[g], a.nout) : a.nout;
         if (b >= nout) continue;
-        const uint4 v = reinterpret_cast<const uint4*>(a.acc_ws)[f];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t ks = 0; ks < nsplit; ++ks) {
+            const uint4 v = reinterpret_cast<const uint4*>(a.acc_ws + ks * a.slab)[f];
+            w[0] ^= v.x;
+            w[1] ^= v.y;
+            w[2] ^= v.z;
+            w[3] ^= v.w;
+        }
         store16_partial(a.out + g * a.ogs + (uint64_t)b * a.ors + 16ull * u, w, min(16u, a.L - 16 * u));
     }
 }
@@ -853,27 +939,44 @@ std::vector<uint16_t> host_log16() {
 // lanes for 4 waves per SIMD: fewer lanes than this split the inputs
 uint64_t matvec_lanes_wanted(qf_ctx* ctx) { return (uint64_t)qf::ctx_num_cus(ctx) * 4 * 4 * 64; }
 
-// bytes of split accumulator launch_matvec needs for G generations (0: no split)
+constexpr size_t kShapeBytes = 256;   // Mv16Shape at the end of the split workspace
+
+// bytes of split slabs (+ the shape record) launch_matvec wants for G
+// generations (0: no split)
 size_t matvec_acc_bytes(qf_ctx* ctx, uint64_t G, uint32_t nout, uint32_t nin, uint32_t L) {
     const uint64_t lanes = G * ((nout + kR16 - 1) / kR16) * ((L + 15) / 16);
     if (lanes >= matvec_lanes_wanted(ctx) || nin < 64) return 0;
-    return G * nout * (((size_t)L + 15) / 16 * 16);
+    const uint32_t ns = matvec_split(lanes, nin, matvec_lanes_wanted(ctx));
+    return ns > 1 ? (size_t)ns * G * nout * (((size_t)L + 15) / 16 * 16) + kShapeBytes : 0;
 }
 
-// acc: workspace of matvec_acc_bytes (null: never split)
-int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name, uint8_t* acc = nullptr) {
+// acc: acc_bytes of workspace for split slabs (matvec_acc_bytes; null: never
+// split).  With per-generation sizes on the device (nout_g / nin_g, the
+// decode) and a split workspace, k_shape16 sizes the launch from the largest
+// e_g instead of e_max: a window decode with e = 512 of e_max = 1,024 ran
+// three quarters of its lanes idle at the e_max shape.
+int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name, uint8_t* acc = nullptr,
+                  size_t acc_bytes = 0) {
     if (!a.nin_gs) a.nin_gs = 1;
     a.Lu = (a.L + 15) / 16;
     a.nob = (a.nout + kR16 - 1) / kR16;
     const uint64_t lanes = G * a.nob * a.Lu;
     if (!lanes || !a.nin) return QF_OK;
-    // enough lanes for 4 waves per SIMD, input chunks of at least 32 rows
+    // enough lanes for 4 waves per SIMD, input chunks of at least 16 rows
     const uint64_t want = matvec_lanes_wanted(ctx);
-    uint32_t ns = 1;
-    if (acc && lanes < want) ns = (uint32_t)std::min<uint64_t>((want + lanes - 1) / lanes, std::max(1u, a.nin / 32));
+    const uint64_t slab = G * a.nout * a.Lu * 4;   // dwords
+    const uint64_t ns_cap = acc && acc_bytes > kShapeBytes ? (acc_bytes - kShapeBytes) / (4 * slab) : 0;
+    uint32_t ns = acc && lanes < want ? matvec_split(lanes, a.nin, want) : 1;
+    ns = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ns, ns_cap));
+    const bool dyn = acc && ns_cap >= 1 && (a.nout_g || a.nin_g);
+    a.shape = dyn ? reinterpret_cast<Mv16Shape*>(acc + acc_bytes - kShapeBytes) : nullptr;
+    a.G = G;
+    a.want = want;
+    a.ns_cap = (uint32_t)std::min<uint64_t>(ns_cap, 1024);
     a.nsplit = ns;
     a.kchunk = (a.nin + ns - 1) / ns;
     a.acc_ws = reinterpret_cast<uint32_t*>(acc);
+    a.slab = slab;
     a.total_units = lanes * ns;
     // inputs feeding >= kLogifyBlocks blocks of outputs go to log form once
     // (QF_GF16_LOGIFY=0: gather the logs in the matvec, per block)
@@ -899,10 +1002,11 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
         }
     }
     hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-    if (ns > 1) QF_HIP(hipMemsetAsync(acc, 0, G * a.nout * (size_t)a.Lu * 16, st));
-    hipLaunchKernelGGL(k_matvec16, dim3(grid16(ctx, a.total_units)), dim3(kThreads16), 0, st, a);
+    if (dyn) hipLaunchKernelGGL(k_shape16, dim3(1), dim3(1024), 0, st, a);
+    const int grid = dyn ? qf::ctx_num_cus(ctx) : grid16(ctx, a.total_units);
+    hipLaunchKernelGGL(k_matvec16, dim3(grid), dim3(kThreads16), 0, st, a);
     QF_HIP(hipGetLastError());
-    if (ns > 1) {
+    if (ns > 1 || dyn) {
         const uint64_t n = G * a.nout * a.Lu;
         hipLaunchKernelGGL(k_finish16, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st, a);
         QF_HIP(hipGetLastError());
@@ -970,7 +1074,7 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
     a.nout = r;
     a.nin = k;
     a.L = L;
-    return launch_matvec(ctx, st, a, G, "k_encode16", ab ? w + cb : nullptr);
+    return launch_matvec(ctx, st, a, G, "k_encode16", ab ? w + cb : nullptr, ab);
 }
 
 }  // namespace qf
@@ -1047,7 +1151,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         c.nout = e_max;
         c.nin = k;
         c.L = L;
-        return launch_matvec(ctx, st, c, G, "k_combine16", ab ? w + wb : nullptr);
+        return launch_matvec(ctx, st, c, G, "k_combine16", ab ? w + wb : nullptr, ab);
     }
     // syndrome path: chunks of generations (grid z = generation), syndromes
     // s = p_J ^ C[J,S] x_S, then x_E = C[J,E]^-1 s with the inverse in closed
@@ -1066,7 +1170,8 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         off[q] = tot;
         tot += align256(std::max<size_t>(per_gen[q] * chunk, 1));
     }
-    const size_t acc_bytes = matvec_acc_bytes(ctx, chunk, e_max, k, L);
+    const size_t acc_bytes = std::max(matvec_acc_bytes(ctx, chunk, e_max, k, L),
+                                      matvec_acc_bytes(ctx, chunk, e_max, e_max, L));
     off[13] = tot;
     tot += align256(std::max<size_t>(acc_bytes, 1));
     s = qf::ctx_work(ctx, tot, &w);
@@ -1154,7 +1259,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         sy.nout = e_max;
         sy.nin = k;
         sy.L = L;
-        s = launch_matvec(ctx, st, sy, gc, "k_syndromes16", acc);
+        s = launch_matvec(ctx, st, sy, gc, "k_syndromes16", acc, acc_bytes);
         if (s) return s;
         // x_E = C[J,E]^-1 s
         Mv16Args so{};
@@ -1174,7 +1279,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         so.nout = e_max;
         so.nin = e_max;
         so.L = L;
-        s = launch_matvec(ctx, st, so, gc, "k_combine16", acc);
+        s = launch_matvec(ctx, st, so, gc, "k_combine16", acc, acc_bytes);
         if (s) return s;
     }
     return QF_OK;

@@ -180,6 +180,24 @@ def test_decode16_statuses(qf, oracle, gpu_ctx, lds_gj, monkeypatch):
     check_decode(oracle, srcs, gens, k, L, res)
 
 
+@pytest.mark.parametrize("lds_gj", ["0", "1"])
+def test_decode16_mixed_erasures_device_shape(qf, oracle, gpu_ctx, lds_gj, monkeypatch):
+    """Generations with very different e in one batch (0, a few, e_max, a
+    short and a singular one): the split matvecs are shaped on the device from
+    the largest e_g (k_shape16), the rows of every generation still match."""
+    monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
+    rng = np.random.default_rng(17)
+    k, r, L = 128, 64, 200
+    parts = [make_gens(oracle, rng, k, r, L, 1, erase=e) for e in (0, 3, 64, 17)]
+    parts.append(make_gens(oracle, rng, k, r, L, 1, erase=5, short=True))
+    parts.append(make_gens(oracle, rng, k, r, L, 1, erase=9, dup=True))
+    src = np.concatenate([p[0] for p in parts])
+    gens = [p[1][0] for p in parts]
+    res = run_decode16(qf, k, r, L, len(gens), gens, False)
+    assert res[3][4] == -3 and (res[3][:4] == 0).all()   # short: ENOTREADY; the dup one per the oracle
+    check_decode(oracle, src, gens, k, L, res)
+
+
 @pytest.mark.parametrize("k,r,L,erase,with_coeffs", [(128, 96, 200, 80, False), (256, 128, 130, 128, False),
                                                      (160, 80, 66, 70, True)])
 def test_decode16_large_path(qf, oracle, gpu_ctx, k, r, L, erase, with_coeffs):
