@@ -45,6 +45,7 @@ constexpr uint32_t kEMax = 64;      // erasures per generation the decode handle
 constexpr int kR16 = 8;             // outputs per pass (encode and combine)
 constexpr int kThreads16 = 1024;
 constexpr uint32_t kLogifyBlocks = 4;  // output blocks of 8 from which inputs go to log form first
+constexpr uint64_t kLogifyUnits = 1u << 18;  // or input units (16 B) from which they do (large batches)
 
 // ---- host arithmetic ------------------------------------------------------
 uint16_t h_mul(uint16_t a, uint16_t b) {
@@ -257,7 +258,17 @@ QF_DEV void unpack_logs(const uint4& raw, uint32_t (&lx)[8]) {
 // generation g -> its log (kNoLog for 0) at out + ((g nin + c) Lu + u) 16 + 2q.
 // An input feeds every block of 8 outputs, so k_matvec16 would otherwise
 // gather the same logs once per block (128 times for an Extreme window).
-__global__ void __launch_bounds__(256) k_logify16(Mv16Args a, uint64_t G, uint16_t* out) {
+// The log table sits in LDS (65,536 x 2 B = 128 KiB): the 8 random lookups
+// per unit were global gathers (0.57 TB/s of rows for the k = 64 batch),
+// from LDS they cost about what the row traffic does.
+__global__ void __launch_bounds__(kThreads16) k_logify16(Mv16Args a, uint64_t G, uint16_t* out) {
+    __shared__ __attribute__((aligned(16))) uint16_t slog[kOrder + 1];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.log);
+        uint4* l = reinterpret_cast<uint4*>(slog);
+        for (uint32_t w = threadIdx.x; w < (kOrder + 1) / 8; w += blockDim.x) l[w] = g[w];
+        __syncthreads();
+    }
     const uint64_t total = G * a.nin * a.Lu;
     for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total;
          f += (uint64_t)gridDim.x * blockDim.x) {
@@ -273,8 +284,7 @@ __global__ void __launch_bounds__(256) k_logify16(Mv16Args a, uint64_t G, uint16
         const uint32_t w[4] = {bswap16x2(raw.x), bswap16x2(raw.y), bswap16x2(raw.z), bswap16x2(raw.w)};
         uint32_t o[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d)
-            o[d] = (uint32_t)a.log[w[d] & 0xFFFF] | ((uint32_t)a.log[w[d] >> 16] << 16);
+        for (int d = 0; d < 4; ++d) o[d] = (uint32_t)slog[w[d] & 0xFFFF] | ((uint32_t)slog[w[d] >> 16] << 16);
         *reinterpret_cast<uint4*>(out + (f * 8)) = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
@@ -978,19 +988,24 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
     a.acc_ws = reinterpret_cast<uint32_t*>(acc);
     a.slab = slab;
     a.total_units = lanes * ns;
-    // inputs feeding >= kLogifyBlocks blocks of outputs go to log form once
-    // (QF_GF16_LOGIFY=0: gather the logs in the matvec, per block)
+    // inputs feeding >= kLogifyBlocks blocks of outputs, or a batch of at
+    // least kLogifyUnits input units, go to log form once: k_logify16 looks
+    // the logs up in LDS, the matvec would gather them from global memory
+    // (QF_GF16_LOGIFY=0: gather in the matvec; QF_GF16_LOGIFY_MIN_BLOCKS
+    // overrides kLogifyBlocks)
     a.in_log = 0;
     {
         const char* v = getenv("QF_GF16_LOGIFY");
-        if (!(v && !atoi(v)) && a.nob >= kLogifyBlocks) {
+        const char* mb = getenv("QF_GF16_LOGIFY_MIN_BLOCKS");
+        const uint32_t min_blocks = mb ? (uint32_t)atoi(mb) : kLogifyBlocks;
+        const uint64_t n = G * a.nin * a.Lu;
+        if (!(v && !atoi(v)) && (a.nob >= min_blocks || n >= kLogifyUnits)) {
             uint8_t* lr = nullptr;
-            const uint64_t n = G * a.nin * a.Lu;
             int s = qf::ctx_gf16_logrows(ctx, n * 16, &lr);
             if (s) return s;
             hipEvent_t ev0 = qf::ctx_prof_begin(ctx, st);
-            hipLaunchKernelGGL(k_logify16, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 8192)), dim3(256), 0, st,
-                               a, G, reinterpret_cast<uint16_t*>(lr));
+            hipLaunchKernelGGL(k_logify16, dim3(grid16(ctx, n)), dim3(kThreads16), 0, st, a, G,
+                               reinterpret_cast<uint16_t*>(lr));
             QF_HIP(hipGetLastError());
             qf::ctx_prof_end(ctx, st, ev0, "k_logify16");
             a.in = lr;
