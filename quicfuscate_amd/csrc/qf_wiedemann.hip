@@ -94,10 +94,22 @@ struct SeqArgs {
     int32_t* info;        // [0] L, [1] 0 ok / 1 zero sequence / 2 singular
     uint32_t e, ep, kp, b;
     uint32_t lm_lds;      // logs of M in LDS (2 e^2 bytes after the vectors)
+    // baby-step / giant-step Krylov (s > 1): a_{i s + j} = w_i . v_j with
+    // v_j = M^j u (j < s) and w_i = (M^T)^(s i) u, so 2e / s + s dependent
+    // matrix-vector steps instead of 2e
+    uint32_t s;           // 1: plain
+    uint8_t* MT;          // e x ep (out, phase 0): M^T, squared by the host into MsT
+    const uint8_t* MsT;   // e x ep: (M^T)^s
+    uint16_t* LMs;        // e x ep logs of MsT (global)
+    uint8_t* V;           // s x ep: the baby-step vectors (global)
+    uint32_t gather_only; // phase 0: write M, P and MT, then stop
 };
 
 constexpr uint32_t kLogZero = 0x200;     // log of 0: every sum with it indexes a zero
 constexpr uint32_t kEx2 = 1040;          // exp over [0, 510), zero above
+constexpr uint32_t kRed2Bytes = 4096;
+constexpr uint32_t kBsgsMinE = 64;
+constexpr uint32_t kPsMinE = 16, kPsMaxE = 1024;
 
 // Log-domain tables: ex2[lg[a] + lg[b]] = a * b for all a, b (lg[0] = kLogZero).
 __device__ void build_log_tables(uint8_t* ex2, uint16_t* lg) {
@@ -125,7 +137,8 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
     uint8_t* ex2 = lds;
     uint16_t* lg = reinterpret_cast<uint16_t*>(lds + kEx2);            // 256
     uint32_t* red = reinterpret_cast<uint32_t*>(lds + kEx2 + 512);     // 16 words
-    uint16_t* lu = reinterpret_cast<uint16_t*>(lds + kEx2 + 512 + 64);
+    uint32_t* red2 = red + 16;                                         // 1,024 words: giant-step partials
+    uint16_t* lu = reinterpret_cast<uint16_t*>(lds + kEx2 + 512 + 64 + kRed2Bytes);
     uint16_t* lv = lu + e;
     uint16_t* LMl = lv + e;                                            // e * e when lm_lds
     uint8_t* v = reinterpret_cast<uint8_t*>(a.lm_lds ? LMl + (size_t)e * e : LMl);
@@ -144,7 +157,10 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
         a.M[(size_t)i * a.ep + j] = mij;
         a.P[(size_t)i * a.ep + j] = i == j ? 1 : 0;
         LM[(size_t)i * lmp + j] = lg[mij];
+        if (a.gather_only) a.MT[(size_t)j * a.ep + i] = mij;
+        else if (a.s > 1) a.LMs[(size_t)i * a.ep + j] = lg[a.MsT[(size_t)i * a.ep + j]];
     }
+    if (a.gather_only) return;
     for (uint32_t i = tid; i < e; i += nt) {
         const uint8_t ui = (uint8_t)((i + a.b + 1) % 255);
         lu[i] = lg[ui];
@@ -156,23 +172,20 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
     }
     __threadfence_block();
     __syncthreads();
-    // a_t = u . M^t u.  Row i of M v takes S threads (a power of two <= 64,
-    // S = nt / e rounded down), combined by shuffles inside the wave.
+    // y = X x for an e x e matrix X given as logs (pitch xp), x in LDS as
+    // bytes.  Row i takes S threads (a power of two <= 64, S = nt / e rounded
+    // down), combined by shuffles inside the wave.
     uint32_t S = 1;
     while (S * 2 <= 64 && S * 2 * e <= nt) S *= 2;
     const uint32_t rows_per_pass = nt / S;
-    for (uint32_t t = 0; t < n; ++t) {
-        for (uint32_t i = tid; i < e; i += nt) lv[i] = lg[v[i]];
+    auto matvec = [&](const uint16_t* X, uint32_t xp, uint8_t* x) {
+        for (uint32_t i = tid; i < e; i += nt) lv[i] = lg[x[i]];
         __syncthreads();
-        uint32_t d = 0;
-        for (uint32_t i = tid; i < e; i += nt) d ^= ex2[lu[i] + lv[i]];
-        d = block_xor(d, red);
-        if (tid == 0) seq[t] = (uint8_t)d;
         for (uint32_t i0 = 0; i0 < e; i0 += rows_per_pass) {
             const uint32_t i = i0 + tid / S, s0 = tid % S;
             uint32_t acc = 0;
             if (i < e) {
-                const uint16_t* m = LM + (size_t)i * lmp;
+                const uint16_t* m = X + (size_t)i * xp;
                 uint32_t j = s0;
                 for (; j + 3 * S < e; j += 4 * S)
                     acc ^= ex2[m[j] + lv[j]] ^ ex2[m[j + S] + lv[j + S]] ^ ex2[m[j + 2 * S] + lv[j + 2 * S]] ^
@@ -183,8 +196,49 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
             if (i < e && s0 == 0) w[i] = (uint8_t)acc;
         }
         __syncthreads();
-        for (uint32_t i = tid; i < e; i += nt) v[i] = w[i];
+        for (uint32_t i = tid; i < e; i += nt) x[i] = w[i];
         __syncthreads();
+    };
+    if (a.s <= 1) {
+        // a_t = u . M^t u, one step per t
+        for (uint32_t t = 0; t < n; ++t) {
+            uint32_t d = 0;
+            for (uint32_t i = tid; i < e; i += nt) d ^= ex2[lu[i] + lg[v[i]]];
+            d = block_xor(d, red);
+            if (tid == 0) seq[t] = (uint8_t)d;
+            matvec(LM, lmp, v);
+        }
+    } else {
+        // baby steps: V[j] = M^j u (v starts as u)
+        for (uint32_t j = 0; j < a.s; ++j) {
+            for (uint32_t i = tid; i < e; i += nt) a.V[(size_t)j * a.ep + i] = v[i];
+            if (j + 1 < a.s) matvec(LM, lmp, v);
+        }
+        // giant steps: x = (M^T)^(s i) u; a_{i s + j} = x . V[j]; thread
+        // (j = tid % s, stripe tid / s) sums a stripe, threads j < s fold
+        for (uint32_t i = tid; i < e; i += nt) v[i] = (uint8_t)((i + a.b + 1) % 255);
+        __threadfence_block();
+        __syncthreads();
+        const uint32_t sp = a.s, nst = nt / sp;
+        for (uint32_t gi = 0; gi * sp < n; ++gi) {
+            for (uint32_t i = tid; i < e; i += nt) lv[i] = lg[v[i]];
+            __syncthreads();
+            const uint32_t j = tid % sp, st = tid / sp;
+            uint32_t d = 0;
+            if (st < nst)
+                for (uint32_t q = st; q < e; q += nst) d ^= ex2[lv[q] + lg[a.V[(size_t)j * a.ep + q]]];
+            // fold the stripes of each j: lanes tid, tid + sp, ... of a wave by shuffles, waves in LDS
+            for (uint32_t o = sp; o < 64; o <<= 1) d ^= __shfl_xor(d, o, 64);
+            __syncthreads();
+            if ((tid & 63) < sp) red2[(tid >> 6) * sp + (tid & 63)] = d;
+            __syncthreads();
+            if (tid < sp && gi * sp + tid < n) {
+                uint32_t sum = 0;
+                for (uint32_t wv = 0; wv < nt / 64; ++wv) sum ^= red2[wv * sp + tid];
+                seq[gi * sp + tid] = (uint8_t)sum;
+            }
+            if ((gi + 1) * sp < n) matvec(a.LMs, a.ep, v);
+        }
     }
     // Berlekamp-Massey on wave 0 alone (the other waves end here, so its
     // barriers wait for nobody): s[i] = sum_{j=1..L} C[j] s[i-j]
@@ -393,7 +447,22 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     const size_t oA = 0, oE = oA + (size_t)e * kp, oS = oE + r16(2 * e), oM = oS + r16(4 * k);
     const size_t oP0 = oM + (size_t)e * ep, oP1 = oP0 + (size_t)e * ep, oG = oP1 + (size_t)e * ep;
     const size_t oPoly = oG + (size_t)e * kp, oInfo = oPoly + r16(2 * e + 2), oLM = oInfo + 16;
-    const size_t total = oLM + 2 * (size_t)e * ep;
+    // baby-step / giant-step Krylov from e = 64 (below, the squarings cost
+    // more than the steps they save): s = 2^ceil(log2 sqrt(2e)) <= 64
+    uint32_t sb = 1;
+    if (e >= kBsgsMinE)
+        while (sb < 64 && (uint64_t)sb * sb < 2ull * e) sb *= 2;
+    const size_t oMT = oLM + 2 * (size_t)e * ep, oX0 = oMT + (size_t)e * ep, oX1 = oX0 + (size_t)e * ep;
+    const size_t oLMs = oX1 + (size_t)e * ep, oV = oLMs + 2 * (size_t)e * ep;
+    const size_t bsgs_end = sb > 1 ? oV + r16(sb * ep) : oMT;
+    // Paterson-Stockmeyer for W (degree L <= e): powers M^0..M^(s-1) plus a
+    // product slot, M^s, and the block coefficients
+    uint32_t ps_max = 0;
+    if (e >= kPsMinE && e <= kPsMaxE)
+        while ((uint64_t)ps_max * ps_max < e) ++ps_max;
+    const size_t mat = (size_t)e * ep;
+    const size_t oPw = bsgs_end, oMs = oPw + (ps_max + 1) * mat, oPc = oMs + mat;
+    const size_t total = ps_max ? oPc + r16(e * (ps_max + 1)) : bsgs_end;
     uint8_t* w = nullptr;
     if (int s = ctx_work(ctx, total, &w)) return s;
     std::vector<uint8_t> hA((size_t)e * kp, 0);
@@ -402,7 +471,7 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     QF_CHECK_HIP(hipMemcpyAsync(w + oE, E, (size_t)e * 2, hipMemcpyHostToDevice, st));
     QF_CHECK_HIP(hipMemcpyAsync(w + oS, slot, (size_t)k * 4, hipMemcpyHostToDevice, st));
     int32_t* info = reinterpret_cast<int32_t*>(w + oInfo);
-    size_t seq_lds = kEx2 + 512 + 64 + 4 * (size_t)e + 2 * (size_t)e + 2 * (size_t)e + 3 * (2 * (size_t)e + 1);
+    size_t seq_lds = kEx2 + 512 + 64 + kRed2Bytes + 4 * (size_t)e + 2 * (size_t)e + 2 * (size_t)e + 3 * (2 * (size_t)e + 1);
     const uint32_t lm_lds = seq_lds + 2 * (size_t)e * e <= 144 * 1024;   // logs of M in LDS up to e = 262
     if (lm_lds) seq_lds += 2 * (size_t)e * e;
     if (seq_lds > 64 * 1024) {
@@ -419,10 +488,30 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     const auto& f = gf();
     uint8_t* W = nullptr;
     const uint32_t ew = (e + 3) / 4;
+    SeqArgs sa{w + oA, reinterpret_cast<const uint16_t*>(w + oE), w + oM, w + oP0,
+               reinterpret_cast<uint16_t*>(w + oLM), w + oPoly, info, e, ep, kp, 0, lm_lds};
+    sa.s = sb;
+    if (sb > 1) {
+        // M^T (gather pass), then (M^T)^s by squaring: out[i] = sum_l X[i][l] X[l]
+        sa.MT = w + oMT;
+        sa.gather_only = 1;
+        hipLaunchKernelGGL(k_w8_sequence, dim3(1), dim3(seq_threads), seq_lds, st, sa);
+        QF_CHECK_HIP(hipGetLastError());
+        uint8_t* X = w + oMT;
+        uint8_t* bufs[2] = {w + oX0, w + oX1};
+        for (uint32_t p = 1, q = 0; p < sb; p *= 2, q ^= 1) {
+            RowsArgs sq{X, X, bufs[q], tab, ep, ep, ep, e, ew, 0, 0, nullptr};
+            QF_CHECK_HIP(launch_rows(sq, e, st));
+            X = bufs[q];
+        }
+        sa.gather_only = 0;
+        sa.MsT = X;
+        sa.LMs = reinterpret_cast<uint16_t*>(w + oLMs);
+        sa.V = w + oV;
+    }
     for (uint32_t b = 0; b < kTries; ++b) {
         if (tries_out) *tries_out = b + 1;
-        SeqArgs sa{w + oA, reinterpret_cast<const uint16_t*>(w + oE), w + oM, w + oP0,
-                   reinterpret_cast<uint16_t*>(w + oLM), w + oPoly, info, e, ep, kp, b, lm_lds};
+        sa.b = b;
         hipLaunchKernelGGL(k_w8_sequence, dim3(1), dim3(seq_threads), seq_lds, st, sa);
         QF_CHECK_HIP(hipGetLastError());
         int32_t hinfo[2] = {0, 0};
@@ -436,14 +525,51 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
         QF_CHECK_HIP(hipStreamSynchronize(st));
         uint8_t f0inv = 0;
         if (!f.inv(poly[0], &f0inv)) return QF_ERANK;
-        // Horner from P = I (f_L = 1): P <- P M ^ f_i I for i = L-1..1, then W = f_0^-1 P
         uint8_t* Pin = w + oP0;
         uint8_t* Pout = w + oP1;
-        for (uint32_t i = Ld - 1; i >= 1; --i) {
-            RowsArgs h{Pin, w + oM, Pout, tab, ep, ep, ep, e, ew, poly[i], 0, nullptr};
-            QF_CHECK_HIP(launch_rows(h, e, st));
-            std::swap(Pin, Pout);
+        std::vector<uint8_t> pc;
+        if (ps_max && Ld >= kPsMinE) {
+            // P = sum_{m < L} f_(m+1) M^m = sum_q (M^s)^q B_q, B_q = sum_{j < s} f_(qs+j+1) M^j, by
+            // Horner in M^s: s + 2 L / s matrix launches instead of L
+            uint32_t sp = 1;
+            while (sp * sp < Ld) ++sp;
+            const uint32_t Q = (Ld + sp - 1) / sp;
+            uint8_t* Pw = w + oPw;
+            QF_CHECK_HIP(hipMemcpyAsync(Pw, w + oP0, mat, hipMemcpyDeviceToDevice, st));   // M^0 = I
+            QF_CHECK_HIP(hipMemcpyAsync(Pw + mat, w + oM, mat, hipMemcpyDeviceToDevice, st));
+            for (uint32_t j = 2; j <= sp; ++j) {   // M^j = M^(j-1) M; j = sp lands in Ms
+                RowsArgs pw{Pw + (j - 1) * mat, w + oM, j < sp ? Pw + j * mat : w + oMs, tab, ep, ep, ep, e, ew, 0, 0,
+                            nullptr};
+                QF_CHECK_HIP(launch_rows(pw, e, st));
+            }
+            if (sp == 1) QF_CHECK_HIP(hipMemcpyAsync(w + oMs, w + oM, mat, hipMemcpyDeviceToDevice, st));
+            // coefficient rows: q -> f_(qs+j+1) for j < s, then 1 for the product slot
+            pc.assign((size_t)Q * (sp + 1), 0);
+            for (uint32_t q = 0; q < Q; ++q) {
+                for (uint32_t j = 0; j < sp && q * sp + j < Ld; ++j) pc[(size_t)q * (sp + 1) + j] = poly[q * sp + j + 1];
+                pc[(size_t)q * (sp + 1) + sp] = q + 1 < Q ? 1 : 0;
+            }
+            QF_CHECK_HIP(hipMemcpyAsync(w + oPc, pc.data(), pc.size(), hipMemcpyHostToDevice, st));
+            // flattened matrices: one output row of e*ep bytes = sum of the s + 1 slots
+            const uint32_t mw = (uint32_t)(mat / 4);
+            for (uint32_t q = Q; q-- > 0;) {
+                if (q + 1 < Q) {   // product slot = P M^s
+                    RowsArgs pr{Pin, w + oMs, Pw + (size_t)sp * mat, tab, ep, ep, ep, e, ew, 0, 0, nullptr};
+                    QF_CHECK_HIP(launch_rows(pr, e, st));
+                }
+                RowsArgs bq{w + oPc + (size_t)q * (sp + 1), Pw, Pout, tab, 0, mat, 0, sp + 1, mw, 0, 0, nullptr};
+                QF_CHECK_HIP(launch_rows(bq, 1, st));
+                std::swap(Pin, Pout);
+            }
+        } else {
+            // Horner from P = I (f_L = 1): P <- P M ^ f_i I for i = L-1..1
+            for (uint32_t i = Ld - 1; i >= 1; --i) {
+                RowsArgs h{Pin, w + oM, Pout, tab, ep, ep, ep, e, ew, poly[i], 0, nullptr};
+                QF_CHECK_HIP(launch_rows(h, e, st));
+                std::swap(Pin, Pout);
+            }
         }
+        // W = f_0^-1 P
         RowsArgs sc{nullptr, Pin, Pout, tab, 0, ep, ep, e, ew, 0, f0inv, nullptr};
         QF_CHECK_HIP(launch_rows(sc, e, st));
         W = Pout;

@@ -80,6 +80,8 @@ def test_reference_wiedemann_path_decodes(qf, oracle, gpu_ctx):
 @pytest.mark.parametrize("k,e,L,extra", [
     (257, 1, 1200, 0), (300, 7, 1200, 2), (512, 13, 1200, 3), (700, 32, 100, 0), (4096, 3, 64, 1),
     (333, 5, 1, 0), (400, 9, 47, 1), (1000, 2, 9000, 0),
+    # e >= 64: baby-step / giant-step Krylov sequence
+    (300, 64, 40, 1), (320, 97, 33, 0),
 ])
 def test_wiedemann_vs_oracle(qf, oracle, gpu_ctx, k, e, L, extra):
     rng = np.random.default_rng(k * 31 + e)
