@@ -978,7 +978,8 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
     const uint64_t ns_cap = acc && acc_bytes > kShapeBytes ? (acc_bytes - kShapeBytes) / (4 * slab) : 0;
     uint32_t ns = acc && lanes < want ? matvec_split(lanes, a.nin, want) : 1;
     ns = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ns, ns_cap));
-    const bool dyn = acc && ns_cap >= 1 && (a.nout_g || a.nin_g);
+    const char* dv = getenv("QF_GF16_DYN");   // 0: size split launches from e_max on the host
+    const bool dyn = acc && ns_cap >= 1 && (a.nout_g || a.nin_g) && !(dv && !atoi(dv));
     a.shape = dyn ? reinterpret_cast<Mv16Shape*>(acc + acc_bytes - kShapeBytes) : nullptr;
     a.G = G;
     a.want = want;
