@@ -180,12 +180,14 @@ def test_decode16_statuses(qf, oracle, gpu_ctx, lds_gj, monkeypatch):
     check_decode(oracle, srcs, gens, k, L, res)
 
 
+@pytest.mark.parametrize("dyn", ["1", "0"])
 @pytest.mark.parametrize("lds_gj", ["0", "1"])
-def test_decode16_mixed_erasures_device_shape(qf, oracle, gpu_ctx, lds_gj, monkeypatch):
+def test_decode16_mixed_erasures_device_shape(qf, oracle, gpu_ctx, lds_gj, dyn, monkeypatch):
     """Generations with very different e in one batch (0, a few, e_max, a
     short and a singular one): the split matvecs are shaped on the device from
     the largest e_g (k_shape16), the rows of every generation still match."""
     monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
+    monkeypatch.setenv("QF_GF16_DYN", dyn)   # 0: the host's e_max shape
     rng = np.random.default_rng(17)
     k, r, L = 128, 64, 200
     parts = [make_gens(oracle, rng, k, r, L, 1, erase=e) for e in (0, 3, 64, 17)]
