@@ -154,6 +154,8 @@ _ASM = {
     "s_lshrk": lambda d, a, k: f"s_lshr_b32 s{d}, s{a}, {k}",
     "s_andk": lambda d, a, k: f"s_and_b32 s{d}, s{a}, {k}",
     "s_mul": lambda d, a, b: f"s_mul_i32 s{d}, s{a}, s{b}",
+    "s_mul_k": lambda d, a, kk: f"s_mul_i32 s{d}, s{a}, {kk}",
+    "s_ashr31": lambda d, a: f"s_ashr_i32 s{d}, s{a}, 31",
     "s_min": lambda d, a, b: f"s_min_u32 s{d}, s{a}, s{b}",
     "s_cmp_ge_br": lambda a, b, lbl: f"s_cmp_ge_u32 s{a}, s{b}\n\ts_cbranch_scc1 {lbl}",
     "s_branch": lambda lbl: f"s_branch {lbl}",
@@ -398,6 +400,26 @@ class KernelSpec:
     # transpose masks in VGPRs (all-VGPR v_bitop3 issues at full rate, with an
     # SGPR operand at half: tools/ubench_idx.py, profiles/r02_ubench_idx.json)
     vgpr_masks: bool = True
+    # additive-FFT row loop (k a power of two, lch_fft.py): sources stream in
+    # chunks of `fft` rows, each chunk is inverse-transformed in registers and
+    # folded into R coset accumulators, a final transform gives the repairs
+    # (enc) / syndromes (chunked dec).  0: one coefficient block per repair
+    fft: int = 0
+    # fft: the end-of-chunk work (last butterflies + folds into the
+    # accumulators) is spread over the next fft_defer rows, so loads keep
+    # being issued through it (needs fft_defer more ring slots)
+    fft_defer: int = 0
+
+    @property
+    def fplan(self):
+        if not self.fft:
+            return None
+        return _fft_plan(self.k, self.r, self.fft)
+
+    @property
+    def nacc(self) -> int:
+        """Accumulator blocks of 8 planes: the r repairs, or the plan's R."""
+        return self.fplan.R if self.fft else self.r
 
     @property
     def vmask(self) -> Optional[tuple]:
@@ -424,16 +446,22 @@ class KernelSpec:
         tag = {"enc": "bss" if self.ksplit > 1 else "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
             tag = "decs" if self.ksplit > 1 else "decc"
+        if self.fft:
+            tag += f"f{self.fft}"
         if self.rt != self.r or self.j0:
             return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}"
         return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
 
     @property
     def nbuf(self) -> int:
-        return self.pd + 1
+        # fft: a chunk's rows stay in the ring until it is folded in, while the
+        # next chunk's first pd rows land
+        return self.pd + (self.fft + self.fft_defer if self.fft else 1)
 
     @property
     def ring0(self) -> int:
+        if self.fft:     # no plane-combination registers (v18..v39)
+            return FFT_RING0_DEC if self.mode == "dec" else FFT_RING0_ENC
         return 40 if self.mode == "enc" else 48
 
     @property
@@ -451,7 +479,9 @@ class KernelSpec:
 
     @property
     def map_a(self) -> int:
-        return self.acc0 + 8 * self.r
+        if self.fft and self.mode == "dec":
+            return FFT_MAP_DEC      # the plane-combination registers are free
+        return self.acc0 + 8 * self.nacc
 
     @property
     def map_b(self) -> int:
@@ -466,6 +496,8 @@ class KernelSpec:
 
     def _base_free_vgpr(self) -> int:
         n = self.map_b + 4 * self.map_quads
+        if self.fft:
+            n = max(n, self.acc0 + 8 * self.nacc)
         if self.mode == "dec" and self.chunked:
             n = max(n, lu_layout_chunked(self)["end"])
         elif self.mode == "dec":
@@ -499,7 +531,7 @@ class KernelSpec:
     def far(self) -> bool:
         """Item loop branches as 64-bit pc-relative jumps: the straight-line
         body exceeds the +-128 KiB of s_branch (dec always; enc / syn for large k*r)."""
-        return self.mode == "dec" or self.k * (70 + 8 * self.r) > 14000
+        return self.mode == "dec" or bool(self.fft) or self.k * (70 + 8 * self.r) > 14000
 
     @property
     def kernarg_bytes(self) -> int:
@@ -672,6 +704,142 @@ def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bo
         _coeff_block(ops, rows[j], acc0 + 8 * j, lo, hi, init, xor3)
     if guard is not None and guard[0] < r:
         ops.append(Op("label", (guard[1],)))
+
+
+# --------------------------------------------------------------------------
+# Additive-FFT row loop (spec.fft, lch_fft.py)
+# --------------------------------------------------------------------------
+FFT_RING0_ENC = 18     # the ring starts where the plane combinations lived
+FFT_RING0_DEC = 48     # chunked dec keeps its low registers (V_ZA .. v47)
+FFT_MAP_DEC = 18       # chunked dec: slot map quads v18..v37 (dead in the LU phase)
+
+
+def _fft_plan(k: int, r: int, ch: int):
+    from . import lch_fft
+    return lch_fft.best_plan(k, r, ch)
+
+
+def _macc_cost(c: int) -> int:
+    rows = mul_matrix_rows(c)
+    return 0 if c == 0 else sum((bin(w).count("1") + 1) // 2 for w in rows)
+
+
+def _macc(E, dst: int, src: int, c: int, init: bool):
+    """dst (8 planes) ^= c * src, or dst = c * src when init (c a compile-time
+    GF(256) constant: output plane b is the XOR of the input planes of row b
+    of M_c, two per v_bitop3)."""
+    rows = mul_matrix_rows(c)
+    for b in range(8):
+        d = dst + b
+        terms = [src + a for a in range(8) if rows[b] >> a & 1]
+        if init:
+            if not terms:
+                E(Op("v_movk", (d, 0)))
+                continue
+            if len(terms) == 1:
+                E(Op("v_mov", (d, terms[0])))
+                continue
+            if len(terms) == 2:
+                E(Op("v_xor", (d, terms[0], terms[1])))
+                terms = []
+            else:
+                E(Op("v_xor3", (d, terms[0], terms[1], terms[2])))
+                terms = terms[3:]
+        while len(terms) >= 2:
+            E(Op("v_xor3", (d, d, terms[0], terms[1])))
+            terms = terms[2:]
+        if terms:
+            E(Op("v_xor", (d, d, terms[0])))
+
+
+def _fft_stream(E, ops: list, spec: KernelSpec, load_row, wait_row, acc_block, n_rows: int = 0):
+    """The additive-FFT row loop: plan row n (source plan.order[n]) lands in
+    ring slot n % nbuf, is transposed to planes, the chunk's inverse
+    butterflies run as soon as both operands are complete, the chunk is folded
+    into the accumulators after its last row, and the final forward
+    butterflies run after the last chunk.  load_row(n, base) issues the loads
+    of plan row n into the ring slot at `base`; wait_row(n) waits for them;
+    acc_block(t) is the first register of accumulator t.  n_rows > k: rows
+    k .. n_rows - 1 (processed by the caller) are prefetched as well."""
+    P = spec.fplan
+    k, ch, pd, nbuf = spec.k, P.ch, spec.pd, spec.nbuf
+    n_rows = max(n_rows, k)
+    ring0 = spec.ring0
+
+    def slot(n):
+        return ring0 + 8 * (n % nbuf)
+
+    # butterflies of each chunk by the chunk row after which they are ready
+    ready = []
+    for bf in P.chunk_bfly:
+        by_m = {}
+        for i, j, s in bf:
+            q = (j - i).bit_length() - 1
+            m = (i - i % (2 << q)) + (2 << q) - 1
+            by_m.setdefault(m, []).append((i, j, s))
+        ready.append(by_m)
+    inited = set()
+    defer = spec.fft_defer
+    assert defer < ch
+    last_q = ch.bit_length() - 2          # the chunk's last (top) inverse layer
+
+    def butterfly(base, i, j, s):
+        yi, yj = slot(base + i), slot(base + j)
+        for b in range(8):
+            E(Op("v_xor", (yj + b, yj + b, yi + b)))
+        if s:
+            _macc(E, yi, yj, s, init=False)
+
+    def fold(hc, mm):
+        for t, c in P.acc[(hc, mm)]:
+            _macc(E, acc_block(t), slot(hc * ch + mm), c, init=t not in inited)
+            inited.add(t)
+
+    groups = []      # deferred end-of-chunk work, one group per following row
+    for n in range(min(pd, n_rows)):
+        load_row(n, slot(n))
+    for n in range(k):
+        if n + pd < n_rows:
+            load_row(n + pd, slot(n + pd))
+        wait_row(n)
+        ops.extend(_transpose_ops(slot(n), spec.bfi_transpose, spec.vmask))
+        hc, m = divmod(n, ch)
+        base = hc * ch
+        work = []
+        for i, j, s in ready[hc].get(m, ()):
+            work.append((8 + _macc_cost(s), lambda b=base, i=i, j=j, s=s: butterfly(b, i, j, s)))
+            if m == ch - 1 and (j - i).bit_length() - 1 == last_q:
+                for mm in (i, j):
+                    work.append((sum(_macc_cost(c) for _, c in P.acc[(hc, mm)]),
+                                 lambda hc=hc, mm=mm: fold(hc, mm)))
+        if m == ch - 1 and last_q < 0:        # ch == 1: no butterflies
+            work.append((0, lambda hc=hc: fold(hc, 0)))
+        if m == ch - 1 and defer and n < k - 1:
+            # split by cost into defer + 1 consecutive groups (dependency order kept)
+            total = sum(c for c, _ in work)
+            groups = [[] for _ in range(defer + 1)]
+            acc_c = 0
+            for c, emit in work:
+                groups[min(defer, int(acc_c * (defer + 1) / max(1, total)))].append(emit)
+                acc_c += c
+            work = [(0, e) for e in groups.pop(0)]
+        elif groups:
+            work = [(0, e) for e in groups.pop(0)] + work
+        for _, emit in work:
+            emit()
+    for g in groups:
+        for emit in g:
+            emit()
+    for t in range(P.R):
+        if t not in inited:
+            for b in range(8):
+                E(Op("v_movk", (acc_block(t) + b, 0)))
+    for i, j, s in P.final_bfly:
+        ei, ej = acc_block(i), acc_block(j)
+        if s:
+            _macc(E, ei, ej, s, init=False)
+        for b in range(8):
+            E(Op("v_xor", (ej + b, ej + b, ei + b)))
 
 
 def _prologue(E, spec: KernelSpec):
@@ -866,6 +1034,29 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         E(Op("v_add64_s", (V_SRCA, V_SRCA, step)))
         E(Op("v_add64_s", (V_SRCB, V_SRCB, step)))
 
+    if spec.fft:
+        assert ks == 1 and spec.rt == r and spec.j0 == 0
+        cur = [0]      # source row the row pointers address
+
+        def load_fft(n: int, base: int):
+            i = spec.fplan.order[n]
+            if i != cur[0]:
+                E(Op("s_mul_k", (46, 10, i - cur[0])))     # (i - cur) * row stride, signed
+                E(Op("s_ashr31", (47, 46)))
+                E(Op("v_add64_s", (V_SRCA, V_SRCA, 46)))
+                E(Op("v_add64_s", (V_SRCB, V_SRCB, 46)))
+                cur[0] = i
+            E(Op("s_exec", (26,)))
+            E(Op("load16", (base, V_SRCA, 0, spec.ld_policy)))
+            E(Op("s_exec", (24,)))
+            E(Op("load16", (base + 4, V_SRCB, 0, spec.ld_policy)))
+            E(Op("s_exec", (None,)))
+
+        def wait_fft(n: int):
+            E(Op("s_waitcnt_vm", (2 * min(pd, k - 1 - n),)))
+
+        _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t)
+
     def rows_of(srcs: list[int]):
         for m in range(min(pd, len(srcs))):
             load_row(m)
@@ -896,11 +1087,13 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
             if w + 1 < ks:
                 E(Op("s_far_jump", (".Lsec_end", 50 + w)))
         E(Op("label", (".Lsec_end",)))
-    else:
+    elif not spec.fft:
         rows_of(list(range(k)))
+    # accumulator block of repair j
+    blk = (lambda j: acc0 + 8 * spec.fplan.out_block[j]) if spec.fft else (lambda j: acc0 + 8 * j)
     # planes -> bytes, store 2 x 16 bytes per lane per repair
     for j in range(r):
-        ops.extend(_transpose_ops(acc0 + 8 * j, spec.bfi_transpose, spec.vmask))
+        ops.extend(_transpose_ops(blk(j), spec.bfi_transpose, spec.vmask))
     if ks > 1:   # partial repairs of waves 1.. into wave 0 (temps: the ring, dead now)
         _ksplit_reduce(E, ks, r, acc0, ring0, ring0 + 8, 0, jmax_guard=False)
     # padding lanes (stored, not loaded: the zero tail) hold garbage, since
@@ -912,7 +1105,7 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         E(Op("s_exec", (S_PAD,)))
         for j in range(r):
             for q in range(4):
-                E(Op("v_movk", (acc0 + 8 * j + 4 * h + q, 0)))
+                E(Op("v_movk", (blk(j) + 4 * h + q, 0)))
     # the row's last unit when L % 16 != 0 (zero tail only): its bytes >= L
     # come from the source rows' padding; AND them away with the per-dword
     # byte masks s20..s23 (all ones when L % 16 == 0)
@@ -928,13 +1121,13 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         E(Op("s_cbranch_execz", (f".Ltail{h}",)))
         for j in range(r):
             for q in range(4):
-                x = acc0 + 8 * j + 4 * h + q
+                x = blk(j) + 4 * h + q
                 E(Op("v_and_s", (x, 20 + q, x)))
         E(Op("label", (f".Ltail{h}",)))
     E(Op("s_exec", (None,)))
     E(Op("s_nop", (4,)))
     for j in range(r):
-        _store_pair(E, acc0 + 8 * j, S_STA, S_STB, spec.st_policy)
+        _store_pair(E, blk(j), S_STA, S_STB, spec.st_policy)
     if ks > 1:
         _ksplit_epilogue(E)
     else:
@@ -1339,11 +1532,22 @@ def lu_layout_chunked(spec) -> dict:
     """LU-phase registers of the chunked dec kernel (all dead in the row loop
     unless noted): 16 column quads over the ring, the slot map and the top of
     the file; the rank quad in the B-pointer / spare pointer registers."""
+    sel = 18                                 # 24 selectors: v18..v41 (combos, zero pointers)
+    if spec.fft:
+        # additive-FFT layout: the ring (pd + ch slots, dead in the LU phase)
+        # holds the r column quads, then the table buffers and record pointer
+        cols = [spec.ring0 + 4 * q for q in range(spec.r)]
+        top = spec.ring0 + 4 * spec.r
+        tb = (top, top + 6)
+        ta = (top + 5, top + 11)
+        fp = top + 12
+        end = fp + 2
+        assert end <= spec.ring0 + 8 * spec.nbuf, "LU registers exceed the ring"
+        return {"cols": cols, "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": fp, "end": end}
     cols = [spec.ring0 + 4 * q for q in range(2 * spec.nbuf)]
     cols += [spec.map_a + 4 * q for q in range(spec.map_quads)]
     top = spec.map_a + 4 * spec.map_quads
     top = (top + 3) // 4 * 4
-    sel = 18                                 # 24 selectors: v18..v41 (combos, zero pointers)
     tb = (top, top + 6)                      # two table buffers of 5 dwords (b128 at even registers)
     ta = (top + 5, top + 11)
     fp = top + 12                            # LU record pointer (2)
@@ -1535,6 +1739,47 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
     if spec.ksplit > 1:
         _dec_ksplit(E, ops, spec, seq, load_row, present)
         return ops
+    if spec.fft:
+        assert not (spec.wave_gen or spec.lab_lu_only)
+        P = spec.fplan
+        fseq = [("src", i) for i in P.order] + [("rep", j) for j in range(r)]
+        n_all = len(fseq)
+
+        def load_fft(n: int, base: int):
+            kind, idx = fseq[n]
+            present(idx if kind == "src" else k + idx, S_TMP)
+            E(Op("v_mad64_s", (V_ADDR, V_SLOT, 10, V_SRCA)))
+            E(Op("v_cndmask", (V_ADDR, V_ZA, V_ADDR, S_TMP)))
+            E(Op("v_cndmask", (V_ADDR + 1, V_ZA + 1, V_ADDR + 1, S_TMP)))
+            E(Op("v_add64_s", (V_SRCB, V_ADDR, S_QB)))
+            E(Op("s_exec", (26,)))
+            if not spec.lab_norows:
+                E(Op("load16", (base, V_ADDR, 0, spec.ld_policy)))
+            E(Op("s_exec", (24,)))
+            if not spec.lab_norows:
+                E(Op("load16", (base + 4, V_SRCB, 0, spec.ld_policy)))
+            E(Op("s_exec", (None,)))
+
+        def wait_fft(n: int):
+            E(Op("s_waitcnt_vm", (0 if spec.lab_norows else 2 * min(pd, n_all - 1 - n),)))
+
+        _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
+        # the accepted repairs, in byte form, onto their syndrome blocks
+        for n in range(k, n_all):
+            if n + pd < n_all:
+                load_fft(n + pd, ring0 + 8 * ((n + pd) % nbuf))
+            wait_fft(n)
+            j = fseq[n][1]
+            blk0 = acc0 + 8 * P.out_block[j]
+            E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lrep{j}")))
+            ops.extend(_transpose_ops(blk0, spec.bfi_transpose, spec.vmask))
+            base = ring0 + 8 * (n % nbuf)
+            for b in range(8):
+                E(Op("v_xor", (blk0 + b, blk0 + b, base + b)))
+            E(Op("label", (f".Lrep{j}",)))
+        _lu_solve_and_store_chunked(E, spec)
+        _epilogue_next_item(E, far=True)
+        return ops
     for n in range(min(pd, n_seq)):
         load_row(n)
     for n, (kind, idx) in enumerate(seq[:n_seq]):
@@ -1723,9 +1968,10 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
     lay = lu_layout_chunked(spec)
     cols, rank, sel, tbs, tas, fp = lay["cols"], lay["rank"], lay["sel"], lay["tb"], lay["ta"], lay["fp"]
     lu = spec.lu
+    bmap = spec.fplan.out_block if spec.fft else list(range(r))
 
     def blk(t, d):
-        return acc0 + 8 * t + d
+        return acc0 + 8 * bmap[t] + d
 
     def selectors(u):
         if spec.lu_ilp:   # stage by stage: no op depends on the one before it
@@ -2750,6 +2996,10 @@ class Emulator:
                 s[a[0]] = s[a[1]] & a[2]
             elif n == "s_mul":
                 s[a[0]] = (s[a[1]] * s[a[2]]) & MASK32
+            elif n == "s_mul_k":
+                s[a[0]] = (s[a[1]] * a[2]) & MASK32
+            elif n == "s_ashr31":
+                s[a[0]] = MASK32 if s[a[1]] >> 31 else 0
             elif n == "s_min":
                 s[a[0]] = min(s[a[1]], s[a[2]])
             elif n == "s_cmp_ge_br":

@@ -34,6 +34,11 @@ BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1), (32, 5), (48, 8),
 # only, in passes
 BS_ENC_ONLY = [(128, 20), (128, 39), (160, 48), (196, 59)]   # (128, 39): Medium default window
 BS_PASS = 22   # repairs per pass: 8 r accumulator VGPRs, r <= 22 fits 256 at pd 3
+# additive-FFT encode ('E', lch_fft.py): power-of-two k where the plan costs
+# fewer plane ops than one coefficient block per repair
+BS_FFT = [(64, 16), (64, 10), (32, 16), (16, 16)]
+BS_FFT_CH = 8
+BS_FFT_DEC_PD = 2
 BS_PD = 3
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
 
@@ -145,6 +150,9 @@ def _bs_kernels(build_dir: Path) -> Path:
             rp = (rt - j0) // (npass - p)
             specs.append(bs.KernelSpec(k, rp, BS_PD, "synw", r_total=rt, j0=j0))
             j0 += rp
+    specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH) for (k, r) in BS_FFT]
+    # additive-FFT fused decode ('C'): pd 2 (the ring holds a chunk + pd rows)
+    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH) for (k, r) in BS_FFT]
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
     for n, spec in enumerate(specs):
@@ -153,10 +161,11 @@ def _bs_kernels(build_dir: Path) -> Path:
         data = hsaco.read_bytes()
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
-        mode = ("k" if spec.ksplit > 1 else "c") if spec.chunked else \
+        mode = ("C" if spec.fft else "k" if spec.ksplit > 1 else "c") if spec.chunked else \
+            "E" if spec.fft else \
             ("f" if spec.mode == "enc" and spec.ksplit > 1 else
              {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode])
-        entries.append(f"    {{{k}u, {r}u, {BS_PD}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
+        entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
     # the loader caches one module per table entry (qf_bs.h BsCache::kMax)
     kmax = int(re.search(r"kMax = (\d+)", (CSRC / "qf_bs.h").read_text()).group(1))

@@ -338,10 +338,11 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
         sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
         (uint64_t)G * ((L + 15) / 16) < (1ull << 31)) {
         hipEvent_t ev = prof_begin(ctx, st);
+        const char* kname = nullptr;
         QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, src, rep, sh->src_gen_stride,
                                    sh->rep_gen_stride, sh->src_row_stride, sh->rep_row_stride, L, G,
-                                   zero_tail, ctx->offs_in, ctx->offs_out));
-        prof_end(ctx, st, ev, qf::bs_name(k, r));
+                                   zero_tail, ctx->offs_in, ctx->offs_out, &kname));
+        prof_end(ctx, st, ev, kname ? kname : qf::bs_name(k, r));
         return QF_OK;
     }
     for (uint32_t p = 0; p < passes; ++p) {
@@ -490,7 +491,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
                                 ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
-    prof_end(ctx, st, ev, qf::dec_name(k, r, L, G, ctx->num_cus));
+    prof_end(ctx, st, ev, qf::dec_name(k, r, L, G, ctx->num_cus, ctx->bs.fft));
     return QF_OK;
 }
 
@@ -613,9 +614,10 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
             QF_CHECK_HIP(qf::launch_gather_sources(ga, ctx->num_cus, st));
             prof_end(ctx, st, ev, "k_gather_sources");
             ev = prof_begin(ctx, st);
+            const char* kname = nullptr;
             QF_CHECK_HIP(qf::bs_launch(ctx->bs, ctx->num_cus, st, k, r, w + off_x, w + off_syn, (uint64_t)k * Lp,
-                                       (uint64_t)r * Lp, Lp, Lp, L, Gc, true));
-            prof_end(ctx, st, ev, qf::bs_name(k, r));
+                                       (uint64_t)r * Lp, Lp, Lp, L, Gc, true, nullptr, nullptr, &kname));
+            prof_end(ctx, st, ev, kname ? kname : qf::bs_name(k, r));
             ga.out = w + off_syn;
             ga.out_gen_stride = (uint64_t)r * Lp;
             ev = prof_begin(ctx, st);

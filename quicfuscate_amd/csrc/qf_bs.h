@@ -11,12 +11,15 @@ struct BsCache {
     static const int kMax = 128;   // >= the entries of qf_bs_table (build_lib.py checks)
     hipModule_t mod[kMax] = {};
     hipFunction_t fn[kMax] = {};
+    // additive-FFT kernels ('E' encode, 'C' fused decode) where generated;
+    // set from the context options (QF_OPT_FFT_KERNELS)
+    bool fft = true;
 };
 
 // Is there a specialised kernel for the Cauchy matrix of (k, r)?
 bool bs_available(uint32_t k, uint32_t r);
 // Kernel symbol of that configuration (nullptr if none).
-const char* bs_name(uint32_t k, uint32_t r);
+const char* bs_name(uint32_t k, uint32_t r, bool fft = false);
 // Lane units per row of the padded lane space: ceil(L/16) rounded up to 8 (128 B).
 uint32_t bs_padded_units(uint32_t L);
 // Does every repair row's zero tail stay inside its own row / generation?
@@ -29,7 +32,7 @@ bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs);
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                      uint64_t drs, uint32_t L, uint32_t G, bool zero_tail, const uint64_t* src_offs = nullptr,
-                     const uint64_t* dst_offs = nullptr);
+                     const uint64_t* dst_offs = nullptr, const char** name_out = nullptr);
 // (src_offs / dst_offs: generation offset tables -- generation g at src +
 // src_offs[g] / dst + dst_offs[g] instead of g * gen_stride -- or nullptr)
 // Decode stage A: syndromes of the accepted repairs (bs_codegen.py "syn").
@@ -59,7 +62,7 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // read in whole 16-byte units, so they must start 16-byte aligned.
 bool dec_available(uint32_t k, uint32_t r);
 // the kernel dec_launch runs for (k, r, L) and, given G and num_cus, that batch size
-const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0, uint32_t G = 0, int num_cus = 0);
+const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0, uint32_t G = 0, int num_cus = 0, bool fft = false);
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,

@@ -16,7 +16,7 @@
 struct QfBsEntry {
     uint32_t k, r, pd;
     uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
-    char mode;  // 'e' encode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
+    char mode;  // 'e' encode, 'E' additive-FFT encode, 'C' additive-FFT chunked decode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
                 // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves,
                 // 'f' the encode (passes of C5 codes) with an item's sources split the same way
     uint32_t map_stride;
@@ -39,8 +39,9 @@ bool bs_available(uint32_t k, uint32_t r) { return find('e', k, r) != nullptr; }
 bool synw_available(uint32_t k, uint32_t r) { return find('w', k, r) != nullptr; }
 bool syn_available(uint32_t k, uint32_t r) { return find('s', k, r) != nullptr; }
 
-const char* bs_name(uint32_t k, uint32_t r) {
-    const QfBsEntry* e = find('e', k, r);
+const char* bs_name(uint32_t k, uint32_t r, bool fft) {
+    const QfBsEntry* e = fft ? find('E', k, r) : nullptr;
+    if (!e) e = find('e', k, r);
     return e ? e->name : nullptr;
 }
 
@@ -81,8 +82,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // masked to zero before the store); syn (the syndrome rows' tail is junk
     // the combine never stores); the lane-chunk decode ('c': the lane holding
     // the last unit stores it bytewise); never the item-layout decode ('d')
-    const bool chunked = e->mode == 'c' || e->mode == 'k';
-    const bool enc = e->mode == 'e' || e->mode == 'f';
+    const bool chunked = e->mode == 'c' || e->mode == 'k' || e->mode == 'C';
+    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E';
     if ((L % 16 && (e->mode == 'd' || (enc && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
@@ -179,7 +180,7 @@ bool bs_zero_tail_fits(uint32_t r, uint32_t L, uint64_t drs, uint64_t dgs) {
 hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                      const uint8_t* src, uint8_t* dst, uint64_t sgs, uint64_t dgs, uint64_t srs,
                      uint64_t drs, uint32_t L, uint32_t G, bool zero_tail, const uint64_t* src_offs,
-                     const uint64_t* dst_offs) {
+                     const uint64_t* dst_offs, const char** name_out) {
     // zero tail: lane space padded to whole 128-B lines per row and the tail
     // [L, 16 Lv) of every repair row written with zeros, so every line the
     // kernel stores is whole (tools/bs_lab.py: partial lines shared by two
@@ -200,11 +201,13 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
         const char* v = getenv("QF_ENCODE_KSPLIT");
         const uint64_t items = ((uint64_t)G * Lv + 127) / 128;
         if (!(v && !atoi(v)) && find('f', k, r) && num_cus > 0 && items <= (uint64_t)num_cus) mode = 'f';
+        else if (cache.fft && find('E', k, r)) mode = 'E';
     }
     // one launch per pass of repairs (codes with more repairs than a kernel
     // holds): pass j0 writes repair rows j0 .. j0 + r_pass - 1
     for (const auto& e : qf_bs_table) {
         if (e.mode != mode || e.k != k || e.rt != r) continue;
+        if (name_out && e.j0 == 0) *name_out = e.name;
         hipError_t err = launch(cache, &e, num_cus, st, src, dst + (uint64_t)e.j0 * drs, sgs, dgs, srs, drs, L, G,
                                 Lv, Lv, nullptr, nullptr, nullptr, 0, nullptr, src_offs, dst_offs);
         if (err != hipSuccess) return err;
@@ -249,7 +252,8 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
 // (G > 0 and num_cus given) its row-split form 'k', unless QF_DECODE_KSPLIT=0
 // (tools/dec_lab.py --small: 32 against 51-56 us from G = 1 to 256 at the C3
 // shape; past one item per CU the one-wave-per-item kernel wins)
-static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G = 0, int num_cus = 0) {
+static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G = 0, int num_cus = 0,
+                                 bool fft = false) {
     const char* leg = getenv("QF_DECODE_LEGACY");
     const QfBsEntry* c = find('c', k, r);
     if (c && !(leg && atoi(leg)) && (L == 0 || (L + 15) / 16 >= 3)) {
@@ -260,6 +264,10 @@ static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G 
             const QfBsEntry* kk = find('k', k, r);
             if (ks && kk && items <= (uint64_t)num_cus) return kk;
         }
+        if (fft) {
+            const QfBsEntry* cf = find('C', k, r);
+            if (cf) return cf;
+        }
         return c;
     }
     return find('d', k, r);
@@ -267,8 +275,8 @@ static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G 
 
 bool dec_available(uint32_t k, uint32_t r) { return find_dec(k, r, 0) != nullptr; }
 
-const char* dec_name(uint32_t k, uint32_t r, uint32_t L, uint32_t G, int num_cus) {
-    const QfBsEntry* e = find_dec(k, r, L, G, num_cus);
+const char* dec_name(uint32_t k, uint32_t r, uint32_t L, uint32_t G, int num_cus, bool fft) {
+    const QfBsEntry* e = find_dec(k, r, L, G, num_cus, fft);
     return e ? e->name : nullptr;
 }
 
@@ -277,14 +285,14 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
                       const uint64_t* rows_offs, const uint64_t* rec_offs) {
-    const QfBsEntry* e = find_dec(k, r, L, G, num_cus);
+    const QfBsEntry* e = find_dec(k, r, L, G, num_cus, cache.fft);
     if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
         return hipErrorInvalidValue;
     // the LU record pointer is computed with a 32-bit stride multiply
     if ((uint64_t)G * lu_stride >= (1ull << 40)) return hipErrorInvalidValue;
     // unpadded lane space: the kernel is VALU-bound, padding lanes would be
     // pure extra work (and the recovered rows are caller memory, payload only)
-    if (L % 16 && e->mode != 'c' && e->mode != 'k') return hipErrorInvalidValue;
+    if (L % 16 && e->mode != 'c' && e->mode != 'k' && e->mode != 'C') return hipErrorInvalidValue;
     return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, (L + 15) / 16, map_stride, smap, zero,
                   lu, lu_stride, tab256, rows_offs, rec_offs);
 }

@@ -1,0 +1,254 @@
+"""Additive-FFT factorisation of the reference's Cauchy encode for k = 2^a.
+
+The reference's repair coefficients are C[j][i] = inv(i ^ (k + j))
+(decoder.rs:280-298).  When k is a power of two, the source points
+V = {0 .. k-1} form a GF(2)-subspace of GF(2^8) and the repair points k + j
+(j < r <= k) lie in its coset k + V, so
+
+    p_j = sum_i x_i / ((k + j) + i) = R(k + j),  R(t) = N(t) / P_V(t),
+
+with P_V(t) = prod_{v in V} (t + v) the subspace polynomial (GF(2)-linear,
+P_V'(t) = Delta constant) and N = Delta * f, f the degree < k polynomial that
+interpolates x over V.  P_V(k + j) = P_V(k) + P_V(j) = P_V(k), hence
+
+    p_j = kappa * f(k + j),   kappa = Delta / P_V(k).
+
+f is interpolated and evaluated with the Lin-Chung-Han additive FFT in the
+novel polynomial basis X_i = prod_{bit q of i} W_q(t) / W_q(v_q) (W_q the
+subspace polynomial of span(v_0 .. v_{q-1})): an inverse transform over V,
+a fold onto the coset k + V_b (V_b = {0 .. 2^b - 1} >= the r repair points),
+and a forward transform over that coset.  The GPU kernels stream the
+sources in chunks of 2^c rows: each chunk is inverse-transformed in
+registers, every chunk output y_m is added into two of the 2^b coset
+accumulators with compile-time constants (the cross-chunk layers, the fold,
+kappa and the top 2^b / 2^c forward layers, all GF(256)-linear, probed here),
+and a final 2^c-point forward transform per accumulator block gives the
+repairs.  Every constant is a compile-time GF(256) value, so each product is
+a fixed GF(2)-linear map on bit-planes (bs_codegen).
+
+`plan()` builds the schedule and checks it against the Cauchy matrix on
+random vectors before any code is generated.
+"""
+from __future__ import annotations
+
+import dataclasses
+import functools
+import random
+
+# GF(2^8), poly 0x11D, generator 2 (gf_tables.rs:384-408)
+_EXP = [0] * 512
+_LOG = [0] * 256
+_x = 1
+for _i in range(255):
+    _EXP[_i] = _EXP[_i + 255] = _x
+    _LOG[_x] = _i
+    _x <<= 1
+    if _x >= 256:
+        _x ^= 0x11D
+
+
+def mul(a: int, b: int) -> int:
+    return 0 if a == 0 or b == 0 else _EXP[_LOG[a] + _LOG[b]]
+
+
+def inv(a: int) -> int:
+    if a == 0:
+        raise ZeroDivisionError
+    return _EXP[255 - _LOG[a]]
+
+
+def span_point(idx: int, basis: tuple) -> int:
+    p = 0
+    q = 0
+    while idx:
+        if idx & 1:
+            p ^= basis[q]
+        idx >>= 1
+        q += 1
+    return p
+
+
+@functools.lru_cache(maxsize=None)
+def _subspace_poly(b: int, t: int, basis: tuple) -> int:
+    """W_b(t) = prod over span(basis[:b]) of (t + u)."""
+    r = 1
+    for bits in range(1 << b):
+        r = mul(r, t ^ span_point(bits, basis[:b]))
+    return r
+
+
+def xhat(q: int, t: int, basis: tuple) -> int:
+    """Normalised subspace polynomial W_q(t) / W_q(v_q) (GF(2)-linear in t)."""
+    return mul(_subspace_poly(q, t, basis), inv(_subspace_poly(q, basis[q], basis)))
+
+
+def mat_rows(c: int) -> list[int]:
+    """Row b of the GF(2) matrix of x -> c x (bit a set iff bit b of c 2^a)."""
+    cols = [mul(c, 1 << a) for a in range(8)]
+    return [sum(((cols[a] >> b) & 1) << a for a in range(8)) for b in range(8)]
+
+
+def macc_cost(c: int) -> int:
+    """VALU ops of acc ^= c * x on 8 bit-planes with 3-input XORs."""
+    if c == 0:
+        return 0
+    if c == 1:
+        return 8
+    return sum((bin(w).count("1") + 1) // 2 for w in mat_rows(c))
+
+
+@dataclasses.dataclass
+class Plan:
+    k: int
+    r: int
+    ch: int                       # rows per chunk (2^c)
+    R: int                        # coset accumulators (2^b >= r)
+    basis: tuple
+    beta_out: int
+    order: list                   # load order: source index of chunk row n = hc * ch + m
+    chunk_bfly: list              # per chunk: [(i, j, s)] inverse butterflies y_j ^= y_i; y_i ^= s y_j
+    acc: dict                     # (hc, m) -> [(t, c)]: e_t ^= c * y_m
+    final_bfly: list              # [(i, j, s)]: e_i ^= s e_j; e_j ^= e_i
+    out_block: list               # repair j -> accumulator index t
+
+    def cost(self) -> int:
+        n = 0
+        for bf in self.chunk_bfly:
+            n += sum(8 + macc_cost(s) for _, _, s in bf)
+        for hc in range(self.k // self.ch):
+            for m in range(self.ch):
+                for t, c in self.acc[(hc, m)]:
+                    n += macc_cost(c)
+        n += sum(8 + macc_cost(s) for _, _, s in self.final_bfly)
+        return n
+
+    def evaluate(self, xs: list[int]) -> list[int]:
+        """The schedule on scalars (one byte per row): the r repairs."""
+        e = [0] * self.R
+        for hc in range(self.k // self.ch):
+            y = [xs[self.order[hc * self.ch + m]] for m in range(self.ch)]
+            for i, j, s in self.chunk_bfly[hc]:
+                y[j] ^= y[i]
+                y[i] ^= mul(s, y[j])
+            for m in range(self.ch):
+                for t, c in self.acc[(hc, m)]:
+                    e[t] ^= mul(c, y[m])
+        for i, j, s in self.final_bfly:
+            e[i] ^= mul(s, e[j])
+            e[j] ^= e[i]
+        return [e[self.out_block[j]] for j in range(self.r)]
+
+
+def _log2(n: int) -> int:
+    assert n > 0 and n & (n - 1) == 0, n
+    return n.bit_length() - 1
+
+
+def plan(k: int, r: int, ch: int = 8, basis: tuple | None = None, beta_out: int | None = None,
+         check: int = 8) -> Plan:
+    a = _log2(k)
+    R = max(ch, 1 << max(0, (r - 1).bit_length()))
+    b, c = _log2(R), _log2(ch)
+    if not (1 <= r <= k and R <= k and c <= b and k + R <= 256):
+        raise ValueError(f"no additive-FFT plan for k={k}, r={r}, ch={ch}")
+    if basis is None:
+        basis = tuple(1 << q for q in range(8))
+    basis = tuple(basis)
+    if sorted(span_point(i, basis) for i in range(R)) != list(range(R)) or \
+            sorted(span_point(i, basis) for i in range(k)) != list(range(k)):
+        raise ValueError("basis[:b] must span {0..2^b-1} and basis[:a] {0..k-1}")
+    if beta_out is None:
+        beta_out = k
+    assert beta_out ^ k < R
+    order = [span_point(n, basis) for n in range(k)]
+
+    # chunk inverse transforms: layers q = 0 .. c-1 (smallest blocks first)
+    chunk_bfly = []
+    for hc in range(k // ch):
+        bf = []
+        for q in range(c):
+            h = 1 << q
+            for o in range(0, ch, 2 * h):
+                s = xhat(q, span_point(hc * ch + o, basis), basis)
+                bf += [(o + i, o + i + h, s) for i in range(h)]
+        chunk_bfly.append(bf)
+
+    delta = 1
+    for u in range(1, k):
+        delta = mul(delta, u)
+    kappa = mul(delta, inv(_subspace_poly(a, k, basis)))
+    fold = [1] * k
+    for i in range(k):
+        for q in range(b, a):
+            if i >> q & 1:
+                fold[i] = mul(fold[i], xhat(q, beta_out, basis))
+
+    def rest(y: list[int]) -> list[int]:
+        y = list(y)
+        for q in range(c, a):                      # remaining inverse layers
+            h = 1 << q
+            for o in range(0, k, 2 * h):
+                s = xhat(q, span_point(o, basis), basis)
+                for i in range(o, o + h):
+                    y[i + h] ^= y[i]
+                    y[i] ^= mul(s, y[i + h])
+        d = [0] * R
+        for i in range(k):
+            d[i % R] ^= mul(mul(y[i], fold[i]), kappa)
+        for q in reversed(range(c, b)):            # forward layers that mix residues mod ch
+            h = 1 << q
+            for o in range(0, R, 2 * h):
+                s = xhat(q, beta_out ^ span_point(o, basis), basis)
+                for i in range(o, o + h):
+                    d[i] ^= mul(s, d[i + h])
+                    d[i + h] ^= d[i]
+        return d
+
+    acc = {}
+    for hc in range(k // ch):
+        for m in range(ch):
+            y = [0] * k
+            y[hc * ch + m] = 1
+            d = rest(y)
+            acc[(hc, m)] = [(t, d[t]) for t in range(R) if d[t]]
+            assert all(t % ch == m for t, _ in acc[(hc, m)])
+
+    final_bfly = []
+    for blk in range(0, R, ch):
+        for q in reversed(range(c)):
+            h = 1 << q
+            for o in range(blk, blk + ch, 2 * h):
+                s = xhat(q, beta_out ^ span_point(o, basis), basis)
+                final_bfly += [(o + i, o + i + h, s) for i in range(h)]
+    out_block = [0] * r
+    for t in range(R):
+        j = (beta_out ^ span_point(t, basis)) ^ k
+        if j < r:
+            out_block[j] = t
+
+    p = Plan(k, r, ch, R, basis, beta_out, order, chunk_bfly, acc, final_bfly, out_block)
+    rng = random.Random(0x51464543)
+    C = [[inv(i ^ (k + j)) for i in range(k)] for j in range(r)]
+    for _ in range(check):
+        xs = [rng.randrange(256) for _ in range(k)]
+        ref = [0] * r
+        for j in range(r):
+            for i in range(k):
+                ref[j] ^= mul(C[j][i], xs[i])
+        if p.evaluate(xs) != ref:
+            raise AssertionError("additive-FFT plan disagrees with the Cauchy matrix")
+    return p
+
+
+# Bases found by tools/lch_basis_search.py (lowest plane-op count of the
+# schedule; any basis gives the same repairs).  Key: (k, r, ch).
+BEST = {
+    (64, 16, 8): ((4, 1, 11, 9, 19, 57, 64, 128), 76),     # 4,488 plane ops (canonical 5,072)
+}
+
+
+def best_plan(k: int, r: int, ch: int = 8) -> Plan:
+    b = BEST.get((k, r, ch))
+    if b is None:
+        return plan(k, r, ch)
+    return plan(k, r, ch, basis=b[0], beta_out=b[1])

@@ -862,3 +862,108 @@ def _cmb_case(L, G, seed, pas=0, offs=False, R=16):
 ])
 def test_emulated_combine_bs(L, G, seed, pas, offs):
     assert _cmb_case(L, G, seed, pas, offs) == 0
+
+
+# --------------------------------------------------------------------------
+# Additive-FFT row loop (lch_fft.py, KernelSpec.fft)
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("k,r,ch", [(64, 16, 8), (64, 10, 8), (32, 16, 8), (16, 16, 8), (64, 16, 4),
+                                    (64, 16, 16), (32, 5, 8), (128, 16, 8), (16, 1, 8)])
+def test_lch_plan_equals_cauchy(k, r, ch):
+    """The chunked additive-FFT schedule gives the reference's repairs
+    p_j = sum_i inv(i ^ (k + j)) x_i (decoder.rs:280-298) on random bytes,
+    for the canonical basis and the searched ones."""
+    from quicfuscate_amd import lch_fft
+
+    rng = np.random.default_rng(k * r + ch)
+    plans = [lch_fft.plan(k, r, ch, check=0)]
+    if (k, r, ch) in lch_fft.BEST:
+        plans.append(lch_fft.best_plan(k, r, ch))
+    C = bs.cauchy(k, r)
+    for p in plans:
+        for _ in range(6):
+            x = rng.integers(0, 256, k).tolist()
+            want = [0] * r
+            for j in range(r):
+                for i in range(k):
+                    want[j] ^= bs.gf_mul(C[j][i], x[i])
+            assert p.evaluate(x) == want
+
+
+def test_lch_plan_is_cheaper_than_blocks():
+    """The bench shape's plan costs fewer plane ops than one coefficient
+    block per repair (8 r v_bitop3 + 22 combinations per row)."""
+    from quicfuscate_amd import lch_fft
+
+    p = lch_fft.best_plan(64, 16, 8)
+    assert p.cost() + 64 * 48 < 64 * (48 + 22 + 8 * 16) * 0.7
+
+
+@pytest.mark.parametrize("k,r,pd,L,G,zero_tail,defer", [
+    (64, 16, 3, 1200, 2, True, 0),     # the benchmark kernel (zero tail, units of two generations)
+    (64, 16, 3, 96, 5, False, 0),      # several generations per wave
+    (64, 10, 3, 80, 3, True, 2),       # half chunks, r < R, deferred chunk folds
+    (32, 16, 2, 1201, 2, True, 3),     # partial last unit
+    (16, 16, 4, 64, 6, False, 1),
+])
+def test_emulated_fft_encode(oracle, k, r, pd, L, G, zero_tail, defer):
+    spec = bs.KernelSpec(k, r, pd, fft=8, fft_defer=defer)
+    ops = bs.generate(spec)
+    Lv = bs.padded_units(L) if zero_tail else None
+    rng = np.random.default_rng(k + 7 * L + G)
+    srs = L + 16 * (k % 2)
+    sgs = k * srs + 16
+    drs = 16 * (Lv or L // 16) + 128
+    dgs = r * drs
+    src = rng.integers(0, 256, G * sgs, dtype=np.uint8)
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    emu = bs.Emulator(ops)
+    emu.add_buffer(0x10000000, src)
+    emu.add_buffer(0x40000000, dst)
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    waves = (items + 3) // 4
+    ka = bs.kernargs(0x10000000, 0x40000000, sgs, dgs, srs, drs, L, G, waves * 4, Lv=Lv, zero_tail=zero_tail)
+    for wg in range(waves):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, r)
+        for j in range(r):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            tail = 16 * Lv if zero_tail else L
+            assert (dst[off + L: off + tail] == 0).all()
+            assert (dst[off + tail: off + drs] == 0xEE).all()
+
+
+@pytest.mark.parametrize("k,r,L,G,seed,erase,offs", [
+    (64, 16, 1200, 3, 1, 13, False),   # the C3 shape
+    (64, 16, 96, 6, 2, None, True),    # random e, offset tables
+    (64, 16, 80, 5, 3, 16, False),     # e = r: every block a pivot
+    (64, 16, 1201, 2, 4, 5, False),    # partial last unit
+    (64, 10, 320, 4, 5, None, False),  # r < R
+    (16, 16, 96, 4, 6, 16, False),
+    (32, 16, 64, 5, 7, 0, False),      # nothing erased
+])
+def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs):
+    assert _dec_case(oracle, k, r, 2, L, G, seed, erase, chunked=True, offs=offs, fft=8) == 0
+
+
+@pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "dec"), (32, 16, "dec"), (16, 16, "enc")])
+def test_fft_register_budget_covers_code(k, r, mode):
+    """Every VGPR the FFT kernels name lies below the descriptor's
+    next_free_vgpr (<= 256: two waves per SIMD), and register tuples are even."""
+    import re
+
+    spec = bs.KernelSpec(k, r, 2 if mode == "dec" else 3, mode, chunked=mode == "dec", fft=8)
+    text = bs.emit_asm(spec, bs.generate(spec))
+    hi = 0
+    for m in re.finditer(r"\bv(\d+)\b|v\[(\d+):(\d+)\]", text):
+        if m.group(1):
+            hi = max(hi, int(m.group(1)))
+        else:
+            lo, top = int(m.group(2)), int(m.group(3))
+            assert lo % 2 == 0, m.group(0)
+            hi = max(hi, top)
+    assert hi < spec.next_free_vgpr <= 256

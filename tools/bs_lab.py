@@ -28,7 +28,7 @@ VALU = {"v_xor", "v_andk", "v_lshl", "v_lshr", "v_mov", "v_movk", "v_xor3", "v_b
 def variant_ops(bs, spec, flags):
     ops = bs.generate(spec)
     body = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Lbody")
-    acc_lo, acc_hi = spec.acc0, spec.acc0 + 8 * spec.r
+    acc_lo, acc_hi = spec.acc0, spec.acc0 + 8 * spec.nacc
     out = []
     for n, op in enumerate(ops):
         if n > body:
@@ -46,6 +46,22 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 3: the additive-FFT encode ("fft:<ch>", "defer:<rows>")
+    ("warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
+    ("classic", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
+    ("fft_pd3", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_pd4", 64, 16, 4, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_pd5", 64, 16, 5, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_pd3_d2", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8", "defer:2"), ALL),
+    ("fft_pd4_d1", 64, 16, 4, ("ld:nt", "st:nt", "ztail", "fft:8", "defer:1"), ALL),
+    ("fft_pd2_d3", 64, 16, 2, ("ld:nt", "st:nt", "ztail", "fft:8", "defer:3"), ALL),
+    ("fft_nocompute", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_noload", 64, 16, 3, ("noload", "ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_nostore", 64, 16, 3, ("nostore", "ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("classic_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
+    ("fft_pd3_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+]
+VARIANTS_R02 = [
     # name, k, r, pd, flags, blocks_per_cu  (flags: "plain" = no v_bitop3 xor;
     # "nobfi" = classic 6-op delta swaps; "noremap" = no XCD-aware item order;
     # "ld:/st:<bits>" cache policy; "L:<n>" payload bytes; "dst:wide" 2048-B
@@ -77,7 +93,9 @@ def build():
         ld = next((f[3:] for f in flags if f.startswith("ld:")), "")
         st = next((f[3:] for f in flags if f.startswith("st:")), "")
         spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st,
-                             bfi_transpose="nobfi" not in flags, xcd_remap="noremap" not in flags)
+                             bfi_transpose="nobfi" not in flags, xcd_remap="noremap" not in flags,
+                             fft=next((int(f[4:]) for f in flags if f.startswith("fft:")), 0),
+                             fft_defer=next((int(f[6:]) for f in flags if f.startswith("defer:")), 0))
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"lab_{name}", text.replace(spec.name, f"lab_{name}"), OUT)
         Lv = next((int(f[2:]) for f in flags if f.startswith("L:")), 1200)

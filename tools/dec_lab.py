@@ -84,6 +84,16 @@ VARIANTS = [
     ("lu_ilp_full", {"chunked": True, "lab_lu_only": True, "lu_ilp": True}, ()),
     # small batches: one wave per item (decc) against four waves per item (decs)
     ("decs", {"chunked": True, "ksplit": 4}, ()),
+    # round 3: the additive-FFT row loop (lch_fft.py; pd 2 = 10 ring slots, 256 VGPRs)
+    ("f_warm", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    ("f_decc", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    ("f_nolu", {"chunked": True, "fft": 8, "pd": 2, "lu": False}, ()),
+    ("f_norows", {"chunked": True, "fft": 8, "pd": 2, "lab_norows": True}, ()),
+    ("f_nolu_norows", {"chunked": True, "fft": 8, "pd": 2, "lu": False, "lab_norows": True}, ()),
+    ("c_decc", {"chunked": True}, ()),
+    ("c_nolu", {"chunked": True, "lu": False}, ()),
+    ("c_lu_only", {"chunked": True, "lab_lu_only": True}, ()),
+    ("f_decc_2", {"chunked": True, "fft": 8, "pd": 2}, ()),
 ]
 PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]   # need all three built
 
