@@ -113,10 +113,14 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--G", type=int, default=None,
-                    help="generations per GPU (default: 65,536 = C2/C3 at N=1; 156,250 = C4's 10 M packets/GPU "
-                         "with --gpus > 1 or --config c4)")
+                    help="generations per GPU of the headline workload (default 65,536 = C2/C3 at every N; "
+                         "156,250 = C4's 10 M packets/GPU with --config c4)")
     ap.add_argument("--config", choices=("auto", "c2c3", "c4"), default="auto",
-                    help="auto: C2+C3 at N=1, C4 generation count at N>1")
+                    help="auto / c2c3: C2+C3 per GPU at every N (weak scaling, identical per-GPU work); "
+                         "c4: the headline runs C4's 156,250 generations per GPU")
+    ap.add_argument("--c4-G", type=int, default=156250,
+                    help="generations per rank of the separately timed C4 leg (10 M packets/GPU; 0 = skip)")
+    ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--rank-sample", type=int, default=64,
                     help="seeded generations per rank checked against the CPU oracle (N>1 and --config c4)")
     ap.add_argument("--k", type=int, default=64)
@@ -135,8 +139,40 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def launch_plan(args, env, argv=None):
+    """--gpus N > 1 with no launcher in the environment (WORLD_SIZE unset): the
+    command that starts N rank processes (torch.distributed.run on 127.0.0.1,
+    one process per GPU), run as a child before this process touches the GPU.
+    None when this process is a rank (or N == 1); an error string when the
+    launcher's world size disagrees with --gpus."""
+    import sys
+
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus <= 1:
+            return None
+        port = env.get("MASTER_PORT") or str(29500 + (os.getpid() % 2000))
+        return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+                "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + \
+            list(sys.argv[1:] if argv is None else argv)
+    if int(ws) != args.gpus:
+        return f"WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to report a line for the wrong GPU count"
+    return None
+
+
 def main(argv=None):
     args = parse(argv)
+    plan = launch_plan(args, os.environ, argv)
+    if isinstance(plan, str):
+        import sys
+
+        print(f"bench.py: {plan}", file=sys.stderr, flush=True)
+        return 2
+    if plan:
+        import subprocess
+
+        # the ranks run as children; this process never initialises the GPU
+        return subprocess.call(plan)
     import torch
     import torch.distributed as dist
 
@@ -159,7 +195,10 @@ def main(argv=None):
     from quicfuscate_amd import fec
 
     lib = L._lib()
-    c4 = args.config == "c4" or (args.config == "auto" and world > 1)
+    # the headline runs the same per-GPU work at every N (weak scaling); C4's
+    # 10 M packets per GPU run as their own timed leg (c4_leg) unless the
+    # headline itself is C4 (--config c4)
+    c4 = args.config == "c4"
     if args.G is None:
         args.G = 156250 if c4 else 65536   # C4: 10,000,000 packets / 64 per generation
     k, r, Lb, G, e = args.k, args.r, args.L, args.G, args.erase
@@ -459,6 +498,13 @@ def main(argv=None):
         out["cpu_baseline"] = cpu_baseline(src, rep_dense, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S)
         out["cpu_variants"] = cpu_variants(src, rep_dense, k, r, Lb, S)
 
+    if args.c4_G > 0 and not c4:
+        # free the headline's buffers (about 13 GB) before C4's (about 31 GB per rank)
+        del src, rep, rows, rowsv, srcv, repv, rec, rec_index, n_rec, status, aidx_t, row_index, er_t, recv, gi
+        torch.cuda.empty_cache()
+        out["c4"] = c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, r, Lb, e, args.c4_G,
+                           args.c4_steps, args.warmup, args.rank_sample)
+
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -469,6 +515,101 @@ def main(argv=None):
         ctx_enc.close()
         ctx_dec.close()
     ctx.close()
+
+
+def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, r, Lb, e, G, steps, warmup,
+           rank_sample) -> dict:
+    """BASELINE C4: 10 M packets = 156,250 generations per rank,
+    encoded and then decoded at the C3 loss shape (13 erased sources per
+    generation), each rank on its own contiguous generations with distinct
+    payload; timed like the headline (barrier + synchronize around the steps,
+    max over ranks); every recovered byte and zero tail checked on the device,
+    plus seeded generations per rank against the CPU oracle."""
+    Lr = (Lb + 127) // 128 * 128
+    src = torch.empty(G * k * Lb, dtype=torch.uint8, device=dev)
+    rep = torch.zeros(G * r * Lr, dtype=torch.uint8, device=dev)
+    L.check(lib.qf_fill_splitmix_dev(ctx.handle, src.data_ptr(), src.numel(), SEED,
+                                     payload_word_offset(rank, G, k, Lb)), "fill")
+    enc_args = dict(src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lr, rep_gen_stride=r * Lr, G=G,
+                    zero_tail=True, ctx=ctx)
+    fec.encode_batch(src, rep, k, r, Lb, **enc_args)
+    erased = erasure_plan(G, k, e, SEED + 0xC4 + rank)
+    aidx = arrival_index(erased, k, r)
+    n_slots = aidx.shape[1]
+    rows = torch.empty(G * n_slots * Lb, dtype=torch.uint8, device=dev)
+    srcv, repv, rowsv = src.view(G, k, Lb), rep.view(G, r, Lr)[:, :, :Lb], rows.view(G, n_slots, Lb)
+    aidx_t = torch.from_numpy(aidx.astype(np.int64)).to(dev)
+    CH = 4096
+    for g0 in range(0, G, CH):
+        g1 = min(G, g0 + CH)
+        both = torch.cat([srcv[g0:g1], repv[g0:g1]], dim=1)
+        gi = torch.arange(g1 - g0, device=dev)[:, None].expand(-1, n_slots)
+        rowsv[g0:g1] = both[gi, aidx_t[g0:g1]]
+        del both
+    row_index = torch.from_numpy(aidx.view(np.int16)).to(dev)
+    emax = min(k, r)
+    rec = torch.empty(G * emax * Lb, dtype=torch.uint8, device=dev)
+    rec_index = torch.empty(G * emax, dtype=torch.int16, device=dev)
+    n_rec = torch.empty(G, dtype=torch.int32, device=dev)
+    status = torch.empty(G, dtype=torch.int32, device=dev)
+    dec_args = dict(max_rows=n_slots, row_stride=Lb, rows_gen_stride=n_slots * Lb, rec_row_stride=Lb,
+                    rec_gen_stride=emax * Lb, G=G, ctx=ctx)
+
+    def step(ev):
+        ev[0].record(stream)
+        fec.encode_batch(src, rep, k, r, Lb, **enc_args)
+        ev[1].record(stream)
+        fec.decode_batch(rows, row_index, rec, rec_index, n_rec, status, k, r, Lb, **dec_args)
+        ev[2].record(stream)
+
+    for _ in range(max(1, warmup)):
+        step([torch.cuda.Event(enable_timing=True) for _ in range(3)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for s_ in range(steps):
+        step(evs[s_])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) * 1e3 / steps
+    kt = ctx.kernel_times()
+    ctx.profile(False)
+    enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    er_t = torch.from_numpy(erased).to(dev)
+    ok = bool((status == 0).all().item()) and bool((n_rec == e).all().item())
+    ok &= bool((rec_index.view(G, emax)[:, :e].long() == er_t).all().item())
+    for g0 in range(0, G, 16384):     # recovered bytes, in slices (no G x e x L temporary)
+        g1 = min(G, g0 + 16384)
+        gi = torch.arange(g0, g1, device=dev)[:, None].expand(-1, e)
+        ok &= bool((rec.view(G, emax, Lb)[g0:g1, :e] == srcv[gi, er_t[g0:g1]]).all().item())
+    ok &= bool((rep.view(G, r, Lr)[:, :, Lb:] == 0).all().item())
+    sample_ok = True
+    if rank_sample > 0:
+        sample_ok = rank_oracle_sample(torch, src, rep, rows, aidx, rec, k, r, Lb, Lr, e, G, rank_sample,
+                                       SEED + 0xC4 + rank)
+    cdev = dev if backend == "nccl" else "cpu"
+    step_max, enc_max, dec_max, bad = reduce_max(torch, dist, [step_ms, enc_ms, dec_ms,
+                                                               0.0 if ok and sample_ok else 1.0], world, cdev)
+    src_total = world * G * k * Lb
+    del src, rep, rows, rec, rec_index, n_rec, status, row_index, aidx_t
+    torch.cuda.empty_cache()
+    return {"workload": f"C4: {G:,} generations = {G * k:,} packets of {Lb} B per rank, encode (r={r}, zero-tail "
+                        f"repair rows) then decode with {e} erased sources per generation; independent generations "
+                        f"sharded over {world} rank(s), no data-path collective",
+            "generations_per_rank": G, "packets_per_rank": G * k, "ranks": world, "steps": steps,
+            "value": round(src_total / (step_max / 1e3) / 2**30, 3), "unit": "GiB/s",
+            "ms_per_step": round(step_max, 4), "encode_ms": round(enc_max, 4), "decode_ms": round(dec_max, 4),
+            "encode_gibps": round(src_total / (enc_max / 1e3) / 2**30, 3),
+            "decode_gibps": round(src_total / (dec_max / 1e3) / 2**30, 3),
+            "kernel_ms_per_launch": {n: round(ms / max(1, c), 4) for n, (c, ms) in kt.items()},
+            "oracle_sample_generations_per_rank": rank_sample, "verified": bad == 0}
 
 
 def gather_flags(torch, dist, flag: int, world: int, device) -> list:
@@ -820,4 +961,4 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main() or 0)

@@ -155,6 +155,8 @@ _ASM = {
     "s_andk": lambda d, a, k: f"s_and_b32 s{d}, s{a}, {k}",
     "s_mul": lambda d, a, b: f"s_mul_i32 s{d}, s{a}, s{b}",
     "s_mul_k": lambda d, a, kk: f"s_mul_i32 s{d}, s{a}, {kk}",
+    "s_m0": lambda a, kk: f"s_add_u32 m0, s{a}, {kk}",
+    "load16_lds": lambda a, pol="": f"global_load_lds_dwordx4 {VP(a)}, off" + (f" {pol}" if pol else ""),
     "s_ashr31": lambda d, a: f"s_ashr_i32 s{d}, s{a}, 31",
     "s_min": lambda d, a, b: f"s_min_u32 s{d}, s{a}, s{b}",
     "s_cmp_ge_br": lambda a, b, lbl: f"s_cmp_ge_u32 s{a}, s{b}\n\ts_cbranch_scc1 {lbl}",
@@ -409,11 +411,30 @@ class KernelSpec:
     # accumulators) is spread over the next fft_defer rows, so loads keep
     # being issued through it (needs fft_defer more ring slots)
     fft_defer: int = 0
+    # chunked dec with fft: rows land in LDS (global_load_lds_dwordx4, no VGPR
+    # destination) in lds_rows slots per wave, so lds_rows - 1 rows are in
+    # flight whatever the register budget; the split tables then sit at a
+    # 32-B stride (8 KB per workgroup instead of 64 KB)
+    lds_rows: int = 0
+    # fft: (basis, beta_out) of the plan; () = lch_fft.BEST (or canonical)
+    fft_basis: tuple = ()
+
+    @property
+    def ahead(self) -> int:
+        """Rows loaded ahead of the one being processed."""
+        return self.lds_rows - 1 if self.lds_rows else self.pd
+
+    @property
+    def tab_stride(self) -> int:
+        return 32 if self.lds_rows else LDS_TAB_STRIDE
 
     @property
     def fplan(self):
         if not self.fft:
             return None
+        if self.fft_basis:
+            from . import lch_fft
+            return lch_fft.plan(self.k, self.r, self.fft, basis=self.fft_basis[0], beta_out=self.fft_basis[1])
         return _fft_plan(self.k, self.r, self.fft)
 
     @property
@@ -447,7 +468,7 @@ class KernelSpec:
         if self.chunked:
             tag = "decs" if self.ksplit > 1 else "decc"
         if self.fft:
-            tag += f"f{self.fft}"
+            tag += f"f{self.fft}" + (f"l{self.lds_rows}" if self.lds_rows else "")
         if self.rt != self.r or self.j0:
             return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}"
         return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
@@ -456,6 +477,8 @@ class KernelSpec:
     def nbuf(self) -> int:
         # fft: a chunk's rows stay in the ring until it is folded in, while the
         # next chunk's first pd rows land
+        if self.fft and self.lds_rows:
+            return self.fft          # only the chunk itself lives in registers
         return self.pd + (self.fft + self.fft_defer if self.fft else 1)
 
     @property
@@ -511,6 +534,8 @@ class KernelSpec:
         n = self._base_free_vgpr()
         if self.vmask is not None and not (self.mode == "dec" and self.chunked):
             n += 3
+        if self.lds_rows and self.mode == "enc":
+            n += 1          # the ds_read address of the row slots
         n = (n + 7) // 8 * 8
         if n > 256:
             raise ValueError(f"{self.name}: {n} VGPRs > 256 (lower pd)")
@@ -524,8 +549,9 @@ class KernelSpec:
             return SW_NEXT_FREE
         if self.mode == "dec":
             # chunked: s[76:77] = {16 Q, 0}, s[78:79] the partial-last-unit lane
-            return SGPR_NEXT_FREE_DEC + (4 if self.chunked else 0)
-        return S_OFFS + 4   # s[66:67]: far-jump target, s[72:75]: offset tables
+            return SGPR_NEXT_FREE_DEC + (4 if self.chunked else 0) + (2 if self.lds_rows else 0)
+        # s[66:67]: far-jump target, s[72:75]: offset tables (+ s76: LDS row base)
+        return S_OFFS + 4 + (2 if self.lds_rows else 0)
 
     @property
     def far(self) -> bool:
@@ -552,6 +578,10 @@ class KernelSpec:
             return LDS_TAB_BYTES + (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
         if self.mode == "enc" and self.ksplit > 1:
             return (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
+        if self.mode == "dec" and self.lds_rows:
+            return 256 * self.tab_stride + 4 * self.lds_rows * LDS_ROW_BYTES
+        if self.mode == "enc" and self.lds_rows:
+            return 4 * self.lds_rows * LDS_ROW_BYTES
         return LDS_TAB_BYTES if self.mode == "dec" else 0
 
 
@@ -712,6 +742,10 @@ def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bo
 FFT_RING0_ENC = 18     # the ring starts where the plane combinations lived
 FFT_RING0_DEC = 48     # chunked dec keeps its low registers (V_ZA .. v47)
 FFT_MAP_DEC = 18       # chunked dec: slot map quads v18..v37 (dead in the LU phase)
+LDS_ROW_BYTES = 2048   # lds_rows: one row of a wave (64 lanes x 2 units x 16 B) per LDS slot
+S_ROWLDS = 80          # lds_rows: the wave's first LDS row slot (byte address)
+S_ROWLDS_ENC = 76      # the same in the encode kernels
+V_LDSA = 47            # lds_rows: S_ROWLDS + 16 lane (ds_read address of the A half)
 
 
 def _fft_plan(k: int, r: int, ch: int):
@@ -762,7 +796,7 @@ def _fft_stream(E, ops: list, spec: KernelSpec, load_row, wait_row, acc_block, n
     acc_block(t) is the first register of accumulator t.  n_rows > k: rows
     k .. n_rows - 1 (processed by the caller) are prefetched as well."""
     P = spec.fplan
-    k, ch, pd, nbuf = spec.k, P.ch, spec.pd, spec.nbuf
+    k, ch, pd, nbuf = spec.k, P.ch, spec.ahead, spec.nbuf
     n_rows = max(n_rows, k)
     ring0 = spec.ring0
 
@@ -1037,6 +1071,8 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     if spec.fft:
         assert ks == 1 and spec.rt == r and spec.j0 == 0
         cur = [0]      # source row the row pointers address
+        S = spec.lds_rows
+        v_ldsa = spec.next_free_vgpr - 1 if S else None
 
         def load_fft(n: int, base: int):
             i = spec.fplan.order[n]
@@ -1046,15 +1082,28 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
                 E(Op("v_add64_s", (V_SRCA, V_SRCA, 46)))
                 E(Op("v_add64_s", (V_SRCB, V_SRCB, 46)))
                 cur[0] = i
-            E(Op("s_exec", (26,)))
-            E(Op("load16", (base, V_SRCA, 0, spec.ld_policy)))
-            E(Op("s_exec", (24,)))
-            E(Op("load16", (base + 4, V_SRCB, 0, spec.ld_policy)))
+            for h, (vm, va) in enumerate(((26, V_SRCA), (24, V_SRCB))):
+                E(Op("s_exec", (vm,)))
+                if S:
+                    E(Op("s_m0", (S_ROWLDS_ENC, (n % S) * LDS_ROW_BYTES + 1024 * h)))
+                    E(Op("load16_lds", (va, spec.ld_policy)))
+                else:
+                    E(Op("load16", (base + 4 * h, va, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
         def wait_fft(n: int):
-            E(Op("s_waitcnt_vm", (2 * min(pd, k - 1 - n),)))
+            E(Op("s_waitcnt_vm", (2 * min(spec.ahead, k - 1 - n),)))
+            if S:
+                base = ring0 + 8 * (n % spec.nbuf)
+                E(Op("ds_read_b128", (base, v_ldsa, (n % S) * LDS_ROW_BYTES)))
+                E(Op("ds_read_b128", (base + 4, v_ldsa, (n % S) * LDS_ROW_BYTES + 1024)))
+                E(Op("s_waitcnt_lgkm_n", (0,)))
 
+        if S:   # this wave's LDS row slots (lds_rows x 2 KiB per wave) and its ds_read address
+            E(Op("s_movk", (S_ROWLDS_ENC, S * LDS_ROW_BYTES)))
+            E(Op("s_mul", (S_ROWLDS_ENC, S_ROWLDS_ENC, 29)))
+            E(Op("v_lshl", (v_ldsa, 4, V_LANE)))
+            E(Op("v_add_s", (v_ldsa, S_ROWLDS_ENC, v_ldsa)))
         _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t)
 
     def rows_of(srcs: list[int]):
@@ -1536,13 +1585,17 @@ def lu_layout_chunked(spec) -> dict:
     if spec.fft:
         # additive-FFT layout: the ring (pd + ch slots, dead in the LU phase)
         # holds the r column quads, then the table buffers and record pointer
+        # (lds_rows: the ring is only the chunk; those go above the accumulators)
         cols = [spec.ring0 + 4 * q for q in range(spec.r)]
         top = spec.ring0 + 4 * spec.r
+        if spec.lds_rows:
+            top = spec.acc0 + 8 * spec.nacc
+            assert 4 * spec.r <= 8 * spec.nbuf
         tb = (top, top + 6)
         ta = (top + 5, top + 11)
         fp = top + 12
         end = fp + 2
-        assert end <= spec.ring0 + 8 * spec.nbuf, "LU registers exceed the ring"
+        assert spec.lds_rows or end <= spec.ring0 + 8 * spec.nbuf, "LU registers exceed the ring"
         return {"cols": cols, "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": fp, "end": end}
     cols = [spec.ring0 + 4 * q for q in range(2 * spec.nbuf)]
     cols += [spec.map_a + 4 * q for q in range(spec.map_quads)]
@@ -1586,8 +1639,11 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("v_add64_s", (V_SRCA, V_ADDR, 62)))
     for q in range(8):
         E(Op("load16", (48 + 4 * q, V_ADDR if q < 4 else V_SRCA, 1024 * (q % 4))))
+    ts = spec.tab_stride
+    # global bytes q*1024 + 16 l = record 32 q + l/2, half l % 2 -> LDS
+    # (32 q + l/2) * stride + 16 (l % 2)
     E(Op("v_lshr", (V_T, 1, V_LANE)))
-    E(Op("v_lshl", (V_T, 8, V_T)))
+    E(Op("v_lshl", (V_T, ts.bit_length() - 1, V_T)))
     E(Op("v_andk", (V_T + 1, 1, V_LANE)))
     E(Op("v_lshl", (V_T + 1, 4, V_T + 1)))
     E(Op("v_xor", (V_T, V_T, V_T + 1)))
@@ -1595,8 +1651,14 @@ def _prologue_chunked(E, spec: KernelSpec):
         E(Op("s_movk", (S_PICK + b, 0x0C0C000C | (b << 8))))
     E(Op("s_waitcnt_vm", (0,)))
     for q in range(8):
-        E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * LDS_TAB_STRIDE * q)))
+        E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * ts * q)))
     E(Op("s_waitcnt_lgkm_n", (0,)))
+    if spec.lds_rows:   # this wave's row slots: after the tables, lds_rows x 2 KiB per wave
+        E(Op("s_movk", (S_ROWLDS, spec.lds_rows * LDS_ROW_BYTES)))
+        E(Op("s_mul", (S_ROWLDS, S_ROWLDS, 29)))
+        E(Op("s_addk", (S_ROWLDS, S_ROWLDS, 256 * ts)))
+        E(Op("v_lshl", (V_LDSA, 4, V_LANE)))
+        E(Op("v_add_s", (V_LDSA, S_ROWLDS, V_LDSA)))
     if spec.xcd_remap:
         E(Op("s_lshrk", (46, 18, 2)))
         E(Op("s_andk", (47, 2, 7)))
@@ -1745,6 +1807,9 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         fseq = [("src", i) for i in P.order] + [("rep", j) for j in range(r)]
         n_all = len(fseq)
 
+        S = spec.lds_rows
+        ahead = spec.ahead
+
         def load_fft(n: int, base: int):
             kind, idx = fseq[n]
             present(idx if kind == "src" else k + idx, S_TMP)
@@ -1752,22 +1817,30 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
             E(Op("v_cndmask", (V_ADDR, V_ZA, V_ADDR, S_TMP)))
             E(Op("v_cndmask", (V_ADDR + 1, V_ZA + 1, V_ADDR + 1, S_TMP)))
             E(Op("v_add64_s", (V_SRCB, V_ADDR, S_QB)))
-            E(Op("s_exec", (26,)))
-            if not spec.lab_norows:
-                E(Op("load16", (base, V_ADDR, 0, spec.ld_policy)))
-            E(Op("s_exec", (24,)))
-            if not spec.lab_norows:
-                E(Op("load16", (base + 4, V_SRCB, 0, spec.ld_policy)))
+            for h, (vm, va) in enumerate(((26, V_ADDR), (24, V_SRCB))):
+                E(Op("s_exec", (vm,)))
+                if spec.lab_norows:
+                    continue
+                if S:   # -> LDS slot n % S of this wave (no VGPR destination)
+                    E(Op("s_m0", (S_ROWLDS, (n % S) * LDS_ROW_BYTES + 1024 * h)))
+                    E(Op("load16_lds", (va, spec.ld_policy)))
+                else:
+                    E(Op("load16", (base + 4 * h, va, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
         def wait_fft(n: int):
-            E(Op("s_waitcnt_vm", (0 if spec.lab_norows else 2 * min(pd, n_all - 1 - n),)))
+            E(Op("s_waitcnt_vm", (0 if spec.lab_norows else 2 * min(ahead, n_all - 1 - n),)))
+            if S:   # the row from its LDS slot into the chunk registers
+                base = ring0 + 8 * (n % nbuf)
+                E(Op("ds_read_b128", (base, V_LDSA, (n % S) * LDS_ROW_BYTES)))
+                E(Op("ds_read_b128", (base + 4, V_LDSA, (n % S) * LDS_ROW_BYTES + 1024)))
+                E(Op("s_waitcnt_lgkm_n", (0,)))
 
         _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
         # the accepted repairs, in byte form, onto their syndrome blocks
         for n in range(k, n_all):
-            if n + pd < n_all:
-                load_fft(n + pd, ring0 + 8 * ((n + pd) % nbuf))
+            if n + ahead < n_all:
+                load_fft(n + ahead, ring0 + 8 * ((n + ahead) % nbuf))
             wait_fft(n)
             j = fseq[n][1]
             blk0 = acc0 + 8 * P.out_block[j]
@@ -1997,6 +2070,8 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
     def table_read(u, byte, buf):
         a, tb = tas[buf], tbs[buf]
         E(Op("v_perm_s", (a, cols[u] + byte // 4, cols[u] + byte // 4, S_PICK + byte % 4)))
+        if spec.tab_stride != 256:   # c << 8 -> c * stride
+            E(Op("v_lshr", (a, 8 - (spec.tab_stride.bit_length() - 1), a)))
         E(Op("ds_read_b128", (tb, a, 0)))
         E(Op("ds_read_b32", (tb + 4, a, 16)))
 
@@ -2684,7 +2759,9 @@ class Emulator:
     def _wave(self, kernarg: bytes, workgroup: int, wave_in_wg: int, shared_lds):
         v = np.zeros((256, 64), dtype=np.uint64)
         s = [0] * 104
-        lds = np.zeros(LDS_TAB_BYTES, np.uint8) if shared_lds is None else shared_lds
+        lds = np.zeros(160 * 1024, np.uint8) if shared_lds is None else shared_lds
+        m0_lds = 0
+        lds_busy = {}     # LDS byte ranges with an LDS-DMA outstanding: id -> (lo, hi)
         pend_lgkm = []
         ka = np.frombuffer(kernarg, np.uint32)
         pending = []  # list of (regs, values, lanes) in issue order
@@ -2786,6 +2863,21 @@ class Emulator:
                                     (pool >> (np.minimum(sb, 7) * np.uint64(8))) & np.uint64(0xFF))
                     res |= byte << np.uint64(8 * b)
                 wv(a[0], res)
+            elif n == "s_m0":
+                m0_lds = (s[a[0]] + a[1]) & MASK32
+            elif n == "load16_lds":
+                addr = rv64(a[0])
+                base = m0_lds
+                if base < 0 or base + 1024 > len(lds):
+                    raise EmuError(f"LDS-DMA out of range 0x{base:x}")
+                buf = np.zeros(1024, np.uint8)
+                wmask = np.zeros(1024, bool)
+                for l in np.nonzero(exec_)[0]:
+                    buf[16 * l: 16 * l + 16] = np.frombuffer(self.read(int(addr[l]), 16), np.uint8)
+                    wmask[16 * l: 16 * l + 16] = True
+                key = object()
+                lds_busy[key] = (base, base + 1024)
+                pending.append((("lds", key, base, buf, wmask), None, None))
             elif n in ("ds_read_b128", "ds_read_b32"):
                 d, ar, off = a
                 nd = 4 if n == "ds_read_b128" else 1
@@ -2795,6 +2887,9 @@ class Emulator:
                     p0 = int(addr[l]) + off
                     if p0 < 0 or p0 + 4 * nd > len(lds):
                         raise EmuError(f"LDS access out of range 0x{p0:x}")
+                    for lo_, hi_ in lds_busy.values():
+                        if p0 < hi_ and p0 + 4 * nd > lo_:
+                            raise EmuError(f"ds_read of LDS 0x{p0:x} with an LDS-DMA outstanding")
                     vals[:, l] = np.frombuffer(lds[p0: p0 + 4 * nd].tobytes(), np.uint32)
                 regs = [d + q for q in range(nd)]
                 for rg in regs:
@@ -2921,6 +3016,12 @@ class Emulator:
             elif n == "s_waitcnt_vm":
                 while len(pending) > a[0]:
                     regs, vals, lanes = pending.pop(0)
+                    if regs[0] == "lds":      # an LDS-DMA lands
+                        _, key, base, buf, wmask = regs
+                        seg = lds[base: base + 1024]
+                        seg[wmask] = buf[wmask]
+                        del lds_busy[key]
+                        continue
                     for q, rg in enumerate(regs):
                         busy.discard(rg)
                         if rg in busy_lanes:

@@ -152,7 +152,11 @@ def _bs_kernels(build_dir: Path) -> Path:
             j0 += rp
     specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH) for (k, r) in BS_FFT]
     # additive-FFT fused decode ('C'): pd 2 (the ring holds a chunk + pd rows)
-    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH) for (k, r) in BS_FFT]
+    # (default cache policy: neighbouring 1,200-B rows share their boundary
+    # lines, and non-temporal loads / stores drop them before the reuse;
+    # tools/dec_lab.py, profiles/r03_lab_dec_policy.json: 1.485 -> 1.39 ms)
+    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="")
+              for (k, r) in BS_FFT]
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
     for n, spec in enumerate(specs):

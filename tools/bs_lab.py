@@ -32,9 +32,9 @@ def variant_ops(bs, spec, flags):
     out = []
     for n, op in enumerate(ops):
         if n > body:
-            if "noload" in flags and op.name in ("load16", "s_waitcnt_vm"):
+            if "noload" in flags and op.name in ("load16", "load16_lds", "s_waitcnt_vm"):
                 continue
-            if "nostore" in flags and op.name == "store16":
+            if "nostore" in flags and op.name in ("store16", "store_byte"):
                 continue
             if "nocoeff" in flags and op.name in ("v_xor", "v_xor3", "v_mov", "v_movk") and acc_lo <= op.args[0] < acc_hi:
                 continue
@@ -46,6 +46,20 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 3b: rows staged in LDS ("lds:<slots per wave>", global_load_lds_dwordx4)
+    ("warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_pd3", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_l6", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8", "lds:6"), ALL),
+    ("fft_l8", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8", "lds:8"), ALL),
+    ("fft_l9", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8", "lds:9"), ALL),
+    ("fft_l9_nocompute", 64, 16, 3, ("nocompute", "ld:nt", "st:nt", "ztail", "fft:8", "lds:9"), ALL),
+    ("fft_l9_nostore", 64, 16, 3, ("nostore", "ld:nt", "st:nt", "ztail", "fft:8", "lds:9"), ALL),
+    ("fft_l9_stdef", 64, 16, 3, ("ld:nt", "ztail", "fft:8", "lds:9"), ALL),
+    ("fft_l9_lddef", 64, 16, 3, ("st:nt", "ztail", "fft:8", "lds:9"), ALL),
+    ("fft_pd3_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("fft_l9_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8", "lds:9"), ALL),
+]
+VARIANTS_R03A = [
     # round 3: the additive-FFT encode ("fft:<ch>", "defer:<rows>")
     ("warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
     ("classic", 64, 16, 3, ("ld:nt", "st:nt", "ztail"), ALL),
@@ -95,7 +109,8 @@ def build():
         spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st,
                              bfi_transpose="nobfi" not in flags, xcd_remap="noremap" not in flags,
                              fft=next((int(f[4:]) for f in flags if f.startswith("fft:")), 0),
-                             fft_defer=next((int(f[6:]) for f in flags if f.startswith("defer:")), 0))
+                             fft_defer=next((int(f[6:]) for f in flags if f.startswith("defer:")), 0),
+                             lds_rows=next((int(f[4:]) for f in flags if f.startswith("lds:")), 0))
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"lab_{name}", text.replace(spec.name, f"lab_{name}"), OUT)
         Lv = next((int(f[2:]) for f in flags if f.startswith("L:")), 1200)

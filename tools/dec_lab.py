@@ -26,7 +26,59 @@ OUT = REPO / "tools" / "lab_build"
 
 ONLY = None   # --only name,name: build a subset
 
+CANON = ((1, 2, 4, 8, 16, 32, 64, 128), 64)
+D = {"ld_policy": "", "st_policy": ""}
 VARIANTS = [
+    # round 3e: default cache policies combined with the other levers
+    ("f_warm", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
+    ("f_def", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
+    ("f_l9_def", {"chunked": True, "fft": 8, "lds_rows": 9, **D}, ()),
+    ("f_l6_def", {"chunked": True, "fft": 8, "lds_rows": 6, **D}, ()),
+    ("f_def_1280", {"chunked": True, "fft": 8, "pd": 2, "rs": 1280, "rrs": 1280, **D}, ()),
+    ("f_canon_def", {"chunked": True, "fft": 8, "pd": 2, "fft_basis": CANON, **D}, ()),
+    ("f_def_nolu", {"chunked": True, "fft": 8, "pd": 2, "lu": False, **D}, ()),
+    ("f_def_nostore", {"chunked": True, "fft": 8, "pd": 2, **D}, ("nostore",)),
+    ("f_def_norows", {"chunked": True, "fft": 8, "pd": 2, "lab_norows": True, **D}, ()),
+    ("c_def", {"chunked": True, **D}, ()),
+    ("f_ld_sc1", {"chunked": True, "fft": 8, "pd": 2, "ld_policy": "sc1", "st_policy": ""}, ()),
+    ("f_def_2", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
+    ("f_l9_def_2", {"chunked": True, "fft": 8, "lds_rows": 9, **D}, ()),
+]
+VARIANTS_R03D = [
+    # round 3d: cache policy of the recovered-row stores
+    ("f_warm", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    ("f_decc", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    ("f_st_def", {"chunked": True, "fft": 8, "pd": 2, "st_policy": ""}, ()),
+    ("f_st_sc1", {"chunked": True, "fft": 8, "pd": 2, "st_policy": "sc1"}, ()),
+    ("f_st_sc0sc1", {"chunked": True, "fft": 8, "pd": 2, "st_policy": "sc0 sc1"}, ()),
+    ("f_st_ntsc1", {"chunked": True, "fft": 8, "pd": 2, "st_policy": "nt sc1"}, ()),
+    ("f_st_def_1280", {"chunked": True, "fft": 8, "pd": 2, "st_policy": "", "rrs": 1280}, ()),
+    ("f_nolu_st_def", {"chunked": True, "fft": 8, "pd": 2, "st_policy": "", "lu": False}, ()),
+    ("f_nolu", {"chunked": True, "fft": 8, "pd": 2, "lu": False}, ()),
+    ("f_ld_def", {"chunked": True, "fft": 8, "pd": 2, "ld_policy": ""}, ()),
+    ("f_ld_def_st_def", {"chunked": True, "fft": 8, "pd": 2, "ld_policy": "", "st_policy": ""}, ()),
+    ("f_l9_st_def", {"chunked": True, "fft": 8, "lds_rows": 9, "st_policy": ""}, ()),
+    ("f_decc_2", {"chunked": True, "fft": 8, "pd": 2}, ()),
+]
+VARIANTS_R03C = [
+    # round 3c: layouts of the received / recovered rows ("rs" / "rrs": row
+    # strides, 1280 = whole 128-B lines per row), no stores, sequential rows
+    ("f_warm", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    ("f_decc", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    ("f_rrs1280", {"chunked": True, "fft": 8, "pd": 2, "rrs": 1280}, ()),
+    ("f_rs1280", {"chunked": True, "fft": 8, "pd": 2, "rs": 1280}, ()),
+    ("f_both1280", {"chunked": True, "fft": 8, "pd": 2, "rs": 1280, "rrs": 1280}, ()),
+    ("f_nostore", {"chunked": True, "fft": 8, "pd": 2}, ("nostore",)),
+    ("f_nolu_nostore", {"chunked": True, "fft": 8, "pd": 2, "lu": False}, ("nostore",)),
+    ("f_canon", {"chunked": True, "fft": 8, "pd": 2, "fft_basis": CANON}, ()),
+    ("f_canon_nolu", {"chunked": True, "fft": 8, "pd": 2, "fft_basis": CANON, "lu": False}, ()),
+    ("f_nolu", {"chunked": True, "fft": 8, "pd": 2, "lu": False}, ()),
+    ("f_l9_both1280", {"chunked": True, "fft": 8, "lds_rows": 9, "rs": 1280, "rrs": 1280}, ()),
+    ("c_decc", {"chunked": True}, ()),
+    ("c_both1280", {"chunked": True, "rs": 1280, "rrs": 1280}, ()),
+    ("f_decc_2", {"chunked": True, "fft": 8, "pd": 2}, ()),
+]
+VARIANTS_R03 = [
     # name, spec kwargs, body-strip flags (bs_lab.variant_ops)
     ("warm", {}, ()),
     ("full", {}, ()),
@@ -94,6 +146,13 @@ VARIANTS = [
     ("c_nolu", {"chunked": True, "lu": False}, ()),
     ("c_lu_only", {"chunked": True, "lab_lu_only": True}, ()),
     ("f_decc_2", {"chunked": True, "fft": 8, "pd": 2}, ()),
+    # round 3b: rows staged in LDS (lds_rows slots per wave, compact split tables)
+    ("f_l6", {"chunked": True, "fft": 8, "lds_rows": 6}, ()),
+    ("f_l8", {"chunked": True, "fft": 8, "lds_rows": 8}, ()),
+    ("f_l9", {"chunked": True, "fft": 8, "lds_rows": 9}, ()),
+    ("f_l9_nolu", {"chunked": True, "fft": 8, "lds_rows": 9, "lu": False}, ()),
+    ("f_l9_norows", {"chunked": True, "fft": 8, "lds_rows": 9, "lab_norows": True}, ()),
+    ("f_l8_2", {"chunked": True, "fft": 8, "lds_rows": 8}, ()),
 ]
 PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]   # need all three built
 
@@ -113,7 +172,8 @@ def build():
             continue
         kw2 = dict(kw)
         pd = kw2.pop("pd", 3)
-        kw2.pop("cap", None)
+        for key in ("cap", "rs", "rrs"):
+            kw2.pop(key, None)
         spec = bs.KernelSpec(64, 16, pd, "dec", **kw2)
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
         h = assemble(f"dec_{name}", text.replace(spec.name, f"dec_{name}"), OUT)
@@ -152,8 +212,9 @@ def run(G, reps):
     for q in range(nr):
         recs[q] = bs.lu_record(k, r, list(range(e)), erased[q].tolist())
     lu = np.tile(recs, (G // nr + 1, 1))[:G]
-    rows = torch.randint(0, 256, (G * n_slots * L,), dtype=torch.uint8, device=dev)
-    rec = torch.empty(G * e * L, dtype=torch.uint8, device=dev)
+    RS = 1280
+    rows = torch.randint(0, 256, (G * n_slots * RS,), dtype=torch.uint8, device=dev)
+    rec = torch.empty(G * e * RS, dtype=torch.uint8, device=dev)
     d_map = torch.from_numpy(smap.reshape(-1)).to(dev)
     d_lu = torch.from_numpy(lu.reshape(-1)).to(dev)
     d_tab = torch.from_numpy(bs.split_tables()).to(dev)
@@ -179,7 +240,8 @@ def run(G, reps):
             blocks = n_items
         if m["kw"].get("cap"):
             blocks = min(blocks, m["kw"]["cap"])
-        ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * L, e * L, L, L, L, G, blocks * 4,
+        rs, rrs = m["kw"].get("rs", L), m["kw"].get("rrs", L)
+        ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * rs, e * rrs, rs, rrs, L, G, blocks * 4,
                          smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
                          lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr(), chunked=chunked,
                          wave_gen=wave_gen)

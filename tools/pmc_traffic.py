@@ -19,7 +19,7 @@ import json
 from collections import defaultdict
 from pathlib import Path
 
-OUR_KERNELS = ("qf_cauchy_bs_", "qf_cauchy_syn_", "qf_cauchy_decc_", "qf_cauchy_dec_", "k_encode_windows", "k_encode_small", "k_combine_uniform", "k_combine_slots",
+OUR_KERNELS = ("qf_cauchy_", "qf_combine_bs", "k_encode_windows", "k_encode_small", "k_combine_uniform", "k_combine_slots",
                "k_decode_prepare", "k_mul_slice")
 
 
