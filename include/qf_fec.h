@@ -82,6 +82,53 @@ void *qf_ctx_stream(qf_ctx *ctx);
 int qf_ctx_set_payload_wait(qf_ctx *ctx, void *event);
 int qf_sync(qf_ctx *ctx);
 
+/* Kernel-path options of a context.  No reference counterpart: the
+ * reference codec has no tuning knobs (core.rs:189-303 builds it with its
+ * defaults), and the defaults here are the fastest measured paths.  They let
+ * a host pin a kernel path per context (A/B, work-arounds); every call on the
+ * context reads the context's values, and no call reads the environment.
+ * qf_ctx_create sets each option to its default and then, once, to the
+ * integer in the environment variable named in brackets when that is set
+ * (tooling compatibility).  Values are clamped to the ranges given;
+ * QF_EINVAL for an unknown option. */
+enum {
+    QF_OPT_FFT_KERNELS = 0,      /* 1: additive-FFT Cauchy kernels where generated; 0: one coefficient
+                                    block per repair [QF_FFT_KERNELS; default 1] */
+    QF_OPT_BITSLICED,            /* 0: no bit-sliced Cauchy kernels, v_perm paths only
+                                    [QF_DISABLE_BS=1 sets 0; default 1] */
+    QF_OPT_ENCODE_SMALL,         /* small-batch encode kernel: -1 auto, 0 never, 1 always [QF_ENCODE_SMALL] */
+    QF_OPT_ENCODE_KSPLIT,        /* 1: row-split encode passes for <= 1 item per CU; 0 never [QF_ENCODE_KSPLIT] */
+    QF_OPT_ENCODE_V,             /* 16-B units per lane of k_combine_uniform: 1 or 2 [QF_ENCODE_V] */
+    QF_OPT_ENCODE_PD,            /* prefetch depth of k_combine_uniform, 1..3 [QF_ENCODE_PD; default 2] */
+    QF_OPT_DECODE_PATH,          /* Cauchy decode: 0 fused lane-chunk, 1 syndromes + combine
+                                    [QF_DECODE_SYN=1], 2 fused item layout [QF_DECODE_LEGACY=1] */
+    QF_OPT_DECODE_KSPLIT,        /* 1: row-split fused decode for <= 1 item per CU; 0 never [QF_DECODE_KSPLIT] */
+    QF_OPT_DECODE_SYNW,          /* 1: scalar-map syndrome passes at long rows (r > 16); 0 never
+                                    [QF_DECODE_NO_SYNW=1 sets 0] */
+    QF_OPT_DECODE_PD,            /* prefetch depth of k_combine_slots, 1..3 [QF_DECODE_PD; default 1] */
+    QF_OPT_DECODE_CHUNK,         /* generations per chunk of the general decode, 0 = all [QF_DECODE_CHUNK] */
+    QF_OPT_DECODE_OVERLAP,       /* 1: chunked general decode overlaps chunks on two streams [QF_DECODE_OVERLAP] */
+    QF_OPT_COMBINE_BS,           /* 1: bit-sliced payload pass (qf_combine_bs) at long rows; 0 never [QF_COMBINE_BS] */
+    QF_OPT_COMBINE_BS_MIN_Q,     /* its smallest row, in 32-B lane-chunks [QF_COMBINE_BS_MIN_Q; default 64] */
+    QF_OPT_COMBINE_SPLIT,        /* 1: slot-split payload pass for <= 1 item per CU; 0 never [QF_COMBINE_SPLIT] */
+    QF_OPT_PREPARE_GRID,         /* split-phase acceptance pass grid, 0 = one block per two CUs [QF_PREPARE_GRID] */
+    QF_OPT_ENC_BLOCKS_PER_CU,    /* cap of the bit-sliced encode grid, 0 = none [QF_ENC_BLOCKS_PER_CU] */
+    QF_OPT_DEC_BLOCKS_PER_CU,    /* cap of the fused decode grid, 0 = none [QF_DEC_BLOCKS_PER_CU] */
+    QF_OPT_SEND_FUSED,           /* 1: one-launch per-packet send (k_send_window); 0 never [QF_SEND_FUSED] */
+    QF_OPT_SEND_WINDOWS_MIN_TILES, /* send batches: tiles from which k_encode_windows is used [default 256] */
+    QF_OPT_SEND_CHUNKS,          /* send batches: D2H chunks, 1..8 [QF_SEND_CHUNKS; default 1] */
+    QF_OPT_SEND_PROFILE,         /* 1: phase timing of send batches on stderr at qf_ctx_destroy [QF_SEND_PROFILE] */
+    QF_OPT_COPY_THREADS,         /* host copy-out workers of send/receive batches, -1 = auto.  Process-wide:
+                                    the first batch call creates the pool [QF_COPY_THREADS] */
+    QF_OPT_GF16_DYN,             /* 1: GF(2^16) decode launches shaped on the device; 0 from e_max [QF_GF16_DYN] */
+    QF_OPT_GF16_LOGIFY,          /* 1: GF(2^16) inputs in log form for wide matvecs; 0 never [QF_GF16_LOGIFY] */
+    QF_OPT_GF16_LOGIFY_MIN_BLOCKS, /* output blocks from which inputs are logified [QF_GF16_LOGIFY_MIN_BLOCKS] */
+    QF_OPT_GF16_LDS_GJ,          /* 1: GF(2^16) Gauss-Jordan in LDS for e <= 64 [QF_GF16_LDS_GJ; default 0] */
+    QF_OPT_COUNT
+};
+int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);
+int qf_ctx_get_option(qf_ctx *ctx, int option, int64_t *value);
+
 /* Kernel timing (no reference counterpart; benches/ replacement).  While on,
  * every kernel the context launches is bracketed by HIP events recorded on
  * the stream it runs on; totals accumulate per kernel name.  on != 0 clears

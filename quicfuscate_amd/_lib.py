@@ -108,6 +108,8 @@ _SIGS = {
     "qf_ctx_set_payload_wait": (_I, [_P, _P]),
     "qf_sync": (_I, [_P]),
     "qf_ctx_profile": (_I, [_P, _I]),
+    "qf_ctx_set_option": (_I, [_P, _I, ctypes.c_int64]),
+    "qf_ctx_get_option": (_I, [_P, _I, _P]),
     "qf_ctx_profile_read": (_I, [_P, _U32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U32),
                                  ctypes.POINTER(ctypes.c_double)]),
     "qf_gf256_mul_slice_dev": (_I, [_P, _P, _P, _P, _SZ]),
@@ -178,6 +180,16 @@ def header_symbols() -> list[str]:
     """Function names declared in include/qf_fec.h."""
     text = HEADER.read_text()
     return sorted(set(re.findall(r"\b(qf_[a-z0-9_]+)\s*\(", text)))
+
+
+# QF_OPT_* of include/qf_fec.h, by lower-case name without the prefix
+OPTIONS = {n: i for i, n in enumerate([
+    "fft_kernels", "bitsliced", "encode_small", "encode_ksplit", "encode_v", "encode_pd", "decode_path",
+    "decode_ksplit", "decode_synw", "decode_pd", "decode_chunk", "decode_overlap", "combine_bs",
+    "combine_bs_min_q", "combine_split", "prepare_grid", "enc_blocks_per_cu", "dec_blocks_per_cu", "send_fused",
+    "send_windows_min_tiles", "send_chunks", "send_profile", "copy_threads", "gf16_dyn", "gf16_logify",
+    "gf16_logify_min_blocks", "gf16_lds_gj"])}
+QF_OPT_COUNT = len(OPTIONS)
 
 
 def _lib() -> ctypes.CDLL:

@@ -418,6 +418,9 @@ class KernelSpec:
     lds_rows: int = 0
     # fft: (basis, beta_out) of the plan; () = lch_fft.BEST (or canonical)
     fft_basis: tuple = ()
+    # chunked dec: store each recovered row as soon as back-substitution has
+    # finished it (x_u after backward column u), not all after the solve
+    early_stores: bool = False
 
     @property
     def ahead(self) -> int:
@@ -2046,6 +2049,9 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
     def blk(t, d):
         return acc0 + 8 * bmap[t] + d
 
+    def store_block(t, a):
+        _store_recovered_chunked(E, spec, blk, rank, t, a)
+
     def selectors(u):
         if spec.lu_ilp:   # stage by stage: no op depends on the one before it
             for d in range(8):
@@ -2154,8 +2160,22 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
             column(u, [("acc", t) for t in range(u)], f".Lbwd{u}", r + 1)
             if pf_rows:
                 _prefetch_rows(E, spec, len(pf_rows[n_u]))
+            if spec.early_stores:
+                # x_u was final before its backward column: store it now, so
+                # the writes overlap the remaining columns (address in the
+                # now dead column quad u)
+                E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lstu{u}")))
+                E(Op("s_nop", (4,)))
+                store_block(u, cols[u])
+                E(Op("label", (f".Lstu{u}",)))
         if spec.lab_prefetch:
             E(Op("label", (".Lnopf",)))
+        if spec.early_stores:
+            E(Op("s_cmp_le_k_br", (S_JMAX, 0, ".Lst_end")))
+            E(Op("s_nop", (4,)))
+            store_block(0, cols[0])
+            E(Op("label", (".Lst_end",)))
+            return
     else:
         E(Op("s_waitcnt_vm", (0,)))
     # stores: block t -> recovered row rank[t]; A half, then B half at + 16 Q
@@ -2166,29 +2186,36 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
         E(Op("s_cmp_le_k_br", (S_JMAX, t, ".Lst_end")))
         a = st[na % len(st)]
         na += 1
-        E(Op("v_bfe", (V_SLOT, rank + t // 4, 8 * (t % 4), 8)))
-        E(Op("v_cmp_ne_s", (S_TMP, S_ABSENT, V_SLOT)))
-        E(Op("s_nop", (4,)))
-        E(Op("v_mad64_s", (a, V_SLOT, 11, V_DSTA)))
-        E(Op("v_add64_s", (a + 2, a, S_QB)))
-        E(Op("s_and64", (S_TMP2, S_TMP, S_STA)))
-        E(Op("s_exec", (S_TMP2,)))
-        E(Op("store16", (a, blk(t, 0), 0, spec.st_policy)))
-        E(Op("s_and64", (S_TMP2, S_TMP, S_STB)))
-        E(Op("s_exec", (S_TMP2,)))
-        E(Op("store16", (a + 2, blk(t, 4), 0, spec.st_policy)))
-        # the partial last unit: bytes [0, L % 16) of the tail lane's unit B
-        E(Op("s_and64", (S_TMP2, S_TMP, S_TAIL)))
-        E(Op("s_exec", (S_TMP2,)))
-        E(Op("s_cbranch_execz", (f".Ltl{t}",)))
-        for b in range(15):
-            E(Op("s_cmp_le_k_br", (59, b, f".Ltl{t}")))
-            E(Op("v_lshr", (V_T, 8 * (b % 4), blk(t, 4 + b // 4))))
-            E(Op("store_byte", (a + 2, V_T, b)))
-            E(Op("s_nop", (0,)))
-        E(Op("label", (f".Ltl{t}",)))
-        E(Op("s_exec", (None,)))
+        store_block(t, a)
     E(Op("label", (".Lst_end",)))
+
+
+def _store_recovered_chunked(E, spec: KernelSpec, blk, rank: int, t: int, a: int):
+    """Block t (byte form) -> recovered row rank[t] of the lane's generation:
+    A half at the lane's unit q, B half at + 16 Q, the partial last unit
+    bytewise (a, a + 2: address pairs)."""
+    E(Op("v_bfe", (V_SLOT, rank + t // 4, 8 * (t % 4), 8)))
+    E(Op("v_cmp_ne_s", (S_TMP, S_ABSENT, V_SLOT)))
+    E(Op("s_nop", (4,)))
+    E(Op("v_mad64_s", (a, V_SLOT, 11, V_DSTA)))
+    E(Op("v_add64_s", (a + 2, a, S_QB)))
+    E(Op("s_and64", (S_TMP2, S_TMP, S_STA)))
+    E(Op("s_exec", (S_TMP2,)))
+    E(Op("store16", (a, blk(t, 0), 0, spec.st_policy)))
+    E(Op("s_and64", (S_TMP2, S_TMP, S_STB)))
+    E(Op("s_exec", (S_TMP2,)))
+    E(Op("store16", (a + 2, blk(t, 4), 0, spec.st_policy)))
+    # the partial last unit: bytes [0, L % 16) of the tail lane's unit B
+    E(Op("s_and64", (S_TMP2, S_TMP, S_TAIL)))
+    E(Op("s_exec", (S_TMP2,)))
+    E(Op("s_cbranch_execz", (f".Ltl{t}",)))
+    for b in range(15):
+        E(Op("s_cmp_le_k_br", (59, b, f".Ltl{t}")))
+        E(Op("v_lshr", (V_T, 8 * (b % 4), blk(t, 4 + b // 4))))
+        E(Op("store_byte", (a + 2, V_T, b)))
+        E(Op("s_nop", (0,)))
+    E(Op("label", (f".Ltl{t}",)))
+    E(Op("s_exec", (None,)))
 
 
 # --------------------------------------------------------------------------

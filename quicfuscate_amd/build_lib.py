@@ -24,6 +24,7 @@ REPO = PKG.parent
 CSRC = PKG / "csrc"
 OUT_DIR = PKG / "lib"
 LIB = OUT_DIR / "libqf_fec.so"
+LIB_ROCM = OUT_DIR / "libqf_fec_rocm.so"
 SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip", "qf_bs.hip", "qf_adaptive.hip", "qf_wire.hip",
            "qf_gf16.hip", "qf_objects16.hip", "qf_wiedemann.hip"]
 # (k, r) Cauchy configurations that get a bit-sliced assembly kernel
@@ -66,6 +67,14 @@ def _torch_hip_runtime() -> Path:
     lib = Path(spec.origin).parent / "lib" / "libamdhip64.so"
     if not lib.exists():
         raise RuntimeError(f"{lib} missing: need a ROCm build of torch")
+    return lib
+
+
+def _rocm_hip_runtime() -> Path:
+    rocm = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+    lib = rocm / "lib" / "libamdhip64.so"
+    if not lib.exists():
+        raise RuntimeError(f"{lib} missing (ROCm HIP runtime)")
     return lib
 
 
@@ -202,15 +211,19 @@ def build(verbose: bool = False) -> Path:
                 if verbose:
                     for n, u in sorted(usage.items()):
                         print(f"  {n}: {u}")
-    hip = _torch_hip_runtime()
-    tmp = LIB.with_suffix(".so.tmp")
-    cmd = [_clangxx(), "-shared", "-o", str(tmp)] + [str(o) for o in objs] + [
-        str(hip), f"-Wl,-rpath,{hip.parent}", "-Wl,--no-undefined", "-lstdc++",
-    ]
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f"link failed:\n{res.stderr[-4000:]}")
-    os.replace(tmp, LIB)
+    # two links of the same objects: libqf_fec.so against torch's HIP runtime
+    # (the Python harness, one runtime per process) and libqf_fec_rocm.so
+    # against /opt/rocm's (a host with no torch: the C-ABI caller, a Rust
+    # binding -- INTEGRATION.md)
+    for lib, hip in ((LIB, _torch_hip_runtime()), (LIB_ROCM, _rocm_hip_runtime())):
+        tmp = lib.with_suffix(".so.tmp")
+        cmd = [_clangxx(), "-shared", "-o", str(tmp)] + [str(o) for o in objs] + [
+            str(hip), f"-Wl,-rpath,{hip.parent}", "-Wl,--no-undefined", "-lstdc++",
+        ]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed:\n{res.stderr[-4000:]}")
+        os.replace(tmp, lib)
     return LIB
 
 

@@ -126,9 +126,67 @@ struct qf_ctx {
     std::vector<ProfTotal> prof_tot;
     std::vector<hipEvent_t> ev_free;
     std::mutex mu;
+    // kernel-path options (QF_OPT_*, qf_ctx_set_option)
+    int64_t opt[QF_OPT_COUNT] = {};
 };
 
 namespace {
+
+// QF_OPT_* defaults, ranges and the environment variable read once when a
+// context is created (include/qf_fec.h).  env_zero: the variable names the
+// "off" switch (a non-zero value sets the option to 0).
+struct OptDef {
+    const char* env;
+    int64_t dflt, lo, hi;
+    bool env_zero;
+};
+const OptDef kOpts[QF_OPT_COUNT] = {
+    /* FFT_KERNELS */ {"QF_FFT_KERNELS", 1, 0, 1, false},
+    /* BITSLICED */ {"QF_DISABLE_BS", 1, 0, 1, true},
+    /* ENCODE_SMALL */ {"QF_ENCODE_SMALL", -1, -1, 1, false},
+    /* ENCODE_KSPLIT */ {"QF_ENCODE_KSPLIT", 1, 0, 1, false},
+    /* ENCODE_V */ {"QF_ENCODE_V", 1, 1, 2, false},
+    /* ENCODE_PD */ {"QF_ENCODE_PD", 2, 1, 3, false},
+    /* DECODE_PATH */ {nullptr, 0, 0, 2, false},   // QF_DECODE_SYN / QF_DECODE_LEGACY, below
+    /* DECODE_KSPLIT */ {"QF_DECODE_KSPLIT", 1, 0, 1, false},
+    /* DECODE_SYNW */ {"QF_DECODE_NO_SYNW", 1, 0, 1, true},
+    /* DECODE_PD */ {"QF_DECODE_PD", 1, 1, 3, false},
+    /* DECODE_CHUNK */ {"QF_DECODE_CHUNK", 0, 0, 1ll << 31, false},
+    /* DECODE_OVERLAP */ {"QF_DECODE_OVERLAP", 1, 0, 1, false},
+    /* COMBINE_BS */ {"QF_COMBINE_BS", 1, 0, 1, false},
+    /* COMBINE_BS_MIN_Q */ {"QF_COMBINE_BS_MIN_Q", 64, 1, 1 << 20, false},
+    /* COMBINE_SPLIT */ {"QF_COMBINE_SPLIT", 1, 0, 1, false},
+    /* PREPARE_GRID */ {"QF_PREPARE_GRID", 0, 0, 1 << 20, false},
+    /* ENC_BLOCKS_PER_CU */ {"QF_ENC_BLOCKS_PER_CU", 0, 0, 64, false},
+    /* DEC_BLOCKS_PER_CU */ {"QF_DEC_BLOCKS_PER_CU", 0, 0, 64, false},
+    /* SEND_FUSED */ {"QF_SEND_FUSED", 1, 0, 1, false},
+    /* SEND_WINDOWS_MIN_TILES */ {"QF_SEND_WINDOWS_MIN_TILES", 256, 0, 1ll << 30, false},
+    /* SEND_CHUNKS */ {"QF_SEND_CHUNKS", 1, 1, 8, false},
+    /* SEND_PROFILE */ {"QF_SEND_PROFILE", 0, 0, 1, false},
+    /* COPY_THREADS */ {"QF_COPY_THREADS", -1, -1, 64, false},
+    /* GF16_DYN */ {"QF_GF16_DYN", 1, 0, 1, false},
+    /* GF16_LOGIFY */ {"QF_GF16_LOGIFY", 1, 0, 1, false},
+    /* GF16_LOGIFY_MIN_BLOCKS */ {"QF_GF16_LOGIFY_MIN_BLOCKS", 4, 0, 1 << 20, false},
+    /* GF16_LDS_GJ */ {"QF_GF16_LDS_GJ", 0, 0, 1, false},
+};
+
+int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }
+
+// Defaults, then the environment once (qf_ctx_create only).
+void init_opts(qf_ctx* c) {
+    for (int o = 0; o < QF_OPT_COUNT; ++o) {
+        c->opt[o] = kOpts[o].dflt;
+        const char* e = kOpts[o].env ? getenv(kOpts[o].env) : nullptr;
+        if (!e || !*e) continue;
+        const int64_t v = atoll(e);
+        c->opt[o] = kOpts[o].env_zero ? (v ? 0 : 1) : clamp_opt(o, v);
+    }
+    const char* syn = getenv("QF_DECODE_SYN");
+    const char* leg = getenv("QF_DECODE_LEGACY");
+    if (leg && atoi(leg)) c->opt[QF_OPT_DECODE_PATH] = 2;
+    if (syn && atoi(syn)) c->opt[QF_OPT_DECODE_PATH] = 1;
+    c->bs.opt = c->opt;
+}
 
 int ensure_device(qf_ctx* ctx) {
     int cur = -1;
@@ -171,17 +229,12 @@ uint32_t pick_R(uint32_t ra) {
     return 16;
 }
 
-// Units (16 B) per lane in the encode kernel; QF_ENCODE_V=2 selects the
-// two-unit variant (read per call so tests and benches can compare both).
-int pick_V() {
-    const char* e = getenv("QF_ENCODE_V");
-    return (e && atoi(e) == 2) ? 2 : 1;
-}
+// Units (16 B) per lane in the encode kernel (QF_OPT_ENCODE_V).
+int pick_V(qf_ctx* ctx) { return ctx->opt[QF_OPT_ENCODE_V] == 2 ? 2 : 1; }
 
 // Prefetch depth (row pairs in flight per wave) of the combine kernels.
-int pick_PD(const char* var, int V, int dflt) {
-    const char* e = getenv(var);
-    int pd = e ? atoi(e) : dflt;
+int pick_PD(qf_ctx* ctx, int opt, int V) {
+    int pd = (int)ctx->opt[opt];
     const int maxpd = V == 2 ? 2 : 3;
     if (pd < 1) pd = 1;
     if (pd > maxpd) pd = maxpd;
@@ -281,8 +334,8 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     if (sh->src_row_stride < L && k > 1) return QF_EINVAL;
     if (sh->rep_row_stride < L && r > 1) return QF_EINVAL;
     const uint32_t Lu = (L + 15) / 16;
-    const int V = (r >= 9) ? 1 : pick_V();  // R = 16 tiles run V = 1 (see launcher)
-    const int PD = pick_PD("QF_ENCODE_PD", V, 2);
+    const int V = (r >= 9) ? 1 : pick_V(ctx);  // R = 16 tiles run V = 1 (see launcher)
+    const int PD = pick_PD(ctx, QF_OPT_ENCODE_PD, V);
     const uint32_t k_pad = (uint32_t)round_up(k, 2 * (PD + 1));
     const uint32_t passes = (r + 15) / 16;
     std::vector<uint8_t> cm;
@@ -295,8 +348,7 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     // small-batch kernel spreads (generation, repair, unit) over lanes.
     // QF_ENCODE_SMALL=0/1 forces it off/on (tests run both).
     {
-        const char* sm = getenv("QF_ENCODE_SMALL");
-        const int force = sm ? atoi(sm) : -1;
+        const int force = (int)ctx->opt[QF_OPT_ENCODE_SMALL];
         const bool few = (uint64_t)G * qf::bs_padded_units(L) < 64ull * 128;
         if (!coeff && force != 0 && (force == 1 || few)) {
             const uint8_t* dcoef = nullptr;
@@ -327,13 +379,12 @@ int encode_impl(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const uint8_
     }
     // Fast path: bit-sliced kernel specialised to the reference's Cauchy
     // matrix of (k, r) (bs_codegen.py), for whole 16-byte rows.
-    const char* nobs = getenv("QF_DISABLE_BS");
     // (L % 16 != 0: only with the zero tail, whose lane space masks the last unit)
     const bool zero_tail = (sh->flags & QF_ENCODE_ZERO_TAIL) &&
                            (ctx->offs_out ? (r == 1 || sh->rep_row_stride >= 16ull * qf::bs_padded_units(L))
                                           : qf::bs_zero_tail_fits(r, L, sh->rep_row_stride, sh->rep_gen_stride)) &&
                            (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31);
-    if (!coeff && !(nobs && atoi(nobs)) && qf::bs_available(k, r) && (L % 16 == 0 || zero_tail) && L >= 32 &&
+    if (!coeff && ctx->opt[QF_OPT_BITSLICED] && qf::bs_available(k, r) && (L % 16 == 0 || zero_tail) && L >= 32 &&
         sh->src_gen_stride < (1ull << 32) && sh->rep_gen_stride < (1ull << 32) &&
         sh->src_row_stride < (1ull << 32) && sh->rep_row_stride < (1ull << 32) &&
         (uint64_t)G * ((L + 15) / 16) < (1ull << 31)) {
@@ -480,8 +531,8 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
         // work, on a capped persistent grid (QF_PREPARE_GRID blocks, default
         // one per two CUs: beside the C2 encode it then takes ~1 ms, under
         // the encode, and slows it by ~2 %; 4 blocks per CU slowed it 10 %)
-        const char* pg = getenv("QF_PREPARE_GRID");
-        pa.grid_cap = pg ? (uint32_t)atoi(pg) : std::max<uint32_t>(1, (uint32_t)ctx->num_cus / 2);
+        const int64_t pg = ctx->opt[QF_OPT_PREPARE_GRID];
+        pa.grid_cap = pg ? (uint32_t)pg : std::max<uint32_t>(1, (uint32_t)ctx->num_cus / 2);
     }
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
@@ -491,7 +542,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
                                 ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
-    prof_end(ctx, st, ev, qf::dec_name(k, r, L, G, ctx->num_cus, ctx->bs.fft));
+    prof_end(ctx, st, ev, qf::dec_name(&ctx->bs, k, r, L, G, ctx->num_cus));
     return QF_OK;
 }
 
@@ -501,11 +552,9 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
 // 32 bytes, else k_combine_slots; QF_COMBINE_BS=0 keeps k_combine_slots.  The
 // bit-sliced kernel reads whole 16-byte units, so with L % 16 != 0 its rows
 // must start 16-byte aligned (strided, aligned base and strides).
-static bool combine_bs_ok(const qf::CombineSlotsArgs& a, bool offs_al16) {
-    const char* on = getenv("QF_COMBINE_BS");
-    if ((on && !atoi(on)) || !qf::cmb_available()) return false;
-    const char* mq = getenv("QF_COMBINE_BS_MIN_Q");
-    const uint32_t min_q = mq ? (uint32_t)atoi(mq) : 64u;
+static bool combine_bs_ok(qf_ctx* ctx, const qf::CombineSlotsArgs& a, bool offs_al16) {
+    if (!ctx->opt[QF_OPT_COMBINE_BS] || !qf::cmb_available()) return false;
+    const uint32_t min_q = (uint32_t)ctx->opt[QF_OPT_COMBINE_BS_MIN_Q];
     // (Lu >= 2: the partial last unit is then always some lane's unit B)
     if (a.Lu < 2 || (a.Lu + 1) / 2 < min_q) return false;
     if (a.L % 16 && ((a.rows_offs && !offs_al16) ||
@@ -517,16 +566,16 @@ static bool combine_bs_ok(const qf::CombineSlotsArgs& a, bool offs_al16) {
 static hipError_t combine_payload(qf_ctx* ctx, const qf::CombineSlotsArgs& a, int PD, hipStream_t st,
                                   std::string* name) {
     // (rows_offs is the context's input table on the general path only)
-    if (combine_bs_ok(a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16)) {
+    if (combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16)) {
         if (name) *name = "qf_combine_bs_r16";
         return qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx);
     }
+    const bool split_ok = ctx->opt[QF_OPT_COMBINE_SPLIT] != 0;
     if (name) {
-        const char* sp = getenv("QF_COMBINE_SPLIT");
-        const bool split = !(sp && !atoi(sp)) && (a.total_units + 63) / 64 <= (uint64_t)ctx->num_cus;
+        const bool split = split_ok && (a.total_units + 63) / 64 <= (uint64_t)ctx->num_cus;
         *name = split ? std::string("k_combine_slots_split") : "k_combine_slots<" + std::to_string(PD) + ">";
     }
-    return qf::launch_combine_slots(a, PD, ctx->num_cus, st);
+    return qf::launch_combine_slots(a, PD, ctx->num_cus, st, split_ok);
 }
 
 
@@ -548,8 +597,7 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     const uint32_t Lu = (L + 15) / 16;
     // long rows (padded units >= 128): the syndrome passes read the received
     // rows through the slot map themselves (qf_cauchy_synw_*), no gather
-    const char* nosw = getenv("QF_DECODE_NO_SYNW");
-    const bool synw = qf::synw_available(k, r) && Lp >= 16 * 128 && !(nosw && atoi(nosw));
+    const bool synw = qf::synw_available(k, r) && Lp >= 16 * 128 && ctx->opt[QF_OPT_DECODE_SYNW];
     // generations per chunk: gathered sources + syndromes of about 1 GiB
     const uint64_t chunk = std::max<uint64_t>(
         1, std::min<uint64_t>(G, (1ull << 30) / ((uint64_t)((synw ? 0 : k) + r) * Lp)));
@@ -583,7 +631,7 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
     if (int gs = payload_gate(ctx, st)) return gs;
-    const int PD = pick_PD("QF_DECODE_PD", 1, 1);
+    const int PD = pick_PD(ctx, QF_OPT_DECODE_PD, 1);
     for (uint64_t g0 = 0; g0 < G; g0 += chunk) {
         const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
         if (synw) {
@@ -671,13 +719,9 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     // the VALU), so 8 chunks with overlap take 2.49 ms and one chunk 2.25 ms:
     // the default is one chunk.
     uint64_t chunk = G;
-    {
-        const char* e = getenv("QF_DECODE_CHUNK");
-        if (e && atoll(e) > 0) chunk = std::min<uint64_t>((uint64_t)atoll(e), G);
-    }
-    const char* ov = getenv("QF_DECODE_OVERLAP");
+    if (ctx->opt[QF_OPT_DECODE_CHUNK] > 0) chunk = std::min<uint64_t>((uint64_t)ctx->opt[QF_OPT_DECODE_CHUNK], G);
     const uint64_t n_chunks = (G + chunk - 1) / chunk;
-    const bool overlap = n_chunks > 1 && !(ov && atoi(ov) == 0);
+    const bool overlap = n_chunks > 1 && ctx->opt[QF_OPT_DECODE_OVERLAP] != 0;
     // syndrome rows: the padded lane space of the syndrome kernel (whole
     // 128-B lines per row; qf_bs.h)
     const uint64_t syn_rs = 16ull * qf::bs_padded_units(L);
@@ -722,7 +766,7 @@ int decode_cauchy(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_cauchy");
     if (int gs = payload_gate(ctx, st)) return gs;
-    const int PD = pick_PD("QF_DECODE_PD", 1, 1);
+    const int PD = pick_PD(ctx, QF_OPT_DECODE_PD, 1);
     for (uint64_t c = 0; c < n_chunks; ++c) {
         const uint64_t g0 = c * chunk;
         const uint32_t Gc = (uint32_t)std::min<uint64_t>(chunk, G - g0);
@@ -783,10 +827,8 @@ int ctx_lock(qf_ctx* ctx, std::unique_lock<std::mutex>& lk) {
 }
 hipStream_t ctx_stream(qf_ctx* ctx) { return ctx->stream; }
 int ctx_num_cus(qf_ctx* ctx) { return ctx->num_cus; }
-bool small_encode_enabled() {
-    const char* sm = getenv("QF_ENCODE_SMALL");
-    return !(sm && atoi(sm) == 0);
-}
+bool small_encode_enabled(qf_ctx* ctx) { return ctx->opt[QF_OPT_ENCODE_SMALL] != 0; }
+int64_t ctx_opt(qf_ctx* ctx, int opt) { return (opt >= 0 && opt < QF_OPT_COUNT) ? ctx->opt[opt] : 0; }
 int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, uint32_t L, const uint8_t* ring,
                        uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride, const uint8_t* fresh,
                        uint8_t* fresh_dst, uint32_t fresh_units) {
@@ -850,10 +892,7 @@ int encode_ring_windows(qf_ctx* ctx, uint32_t k, uint32_t r, uint32_t G, uint32_
     a.wins = wins;
     // all repairs of a tile per block once there are enough tiles to fill
     // the chip; below that the one-repair tiles spread a few windows wider
-    static const uint64_t min_tiles = [] {
-        const char* e = getenv("QF_SEND_WINDOWS_MIN_TILES");
-        return e ? strtoull(e, nullptr, 10) : 256ull;
-    }();
+    const uint64_t min_tiles = (uint64_t)ctx->opt[QF_OPT_SEND_WINDOWS_MIN_TILES];
     const uint64_t tiles = (uint64_t)G * ((a.Lu + 63) / 64);
     const bool wide = tiles >= min_tiles;
     hipEvent_t ev = prof_begin(ctx, ctx->stream);
@@ -1013,6 +1052,7 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
     QF_CHECK_HIP(hipSetDevice(device));
     qf_ctx* c = new qf_ctx();
     c->device = device;
+    init_opts(c);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
     if (stream) {
@@ -1110,6 +1150,20 @@ int qf_ctx_destroy(qf_ctx* c) {
     }
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
+    return QF_OK;
+}
+
+int qf_ctx_set_option(qf_ctx* ctx, int option, int64_t value) {
+    if (!ctx || option < 0 || option >= QF_OPT_COUNT) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->opt[option] = clamp_opt(option, value);
+    return QF_OK;
+}
+
+int qf_ctx_get_option(qf_ctx* ctx, int option, int64_t* value) {
+    if (!ctx || !value || option < 0 || option >= QF_OPT_COUNT) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    *value = ctx->opt[option];
     return QF_OK;
 }
 
@@ -1385,30 +1439,29 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
     std::lock_guard<std::mutex> g(ctx->mu);
     int s = ensure_device(ctx);
     if (s) return s;
-    const char* nobs = getenv("QF_DISABLE_BS");
-    if (!row_coeffs && !(nobs && atoi(nobs)) && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
+    if (!row_coeffs && ctx->opt[QF_OPT_BITSLICED] && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
         max_rows <= 255 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
         sh->row_stride < (1ull << 32) && (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31) &&
         (uint64_t)r * 16 * qf::bs_padded_units(L) < (1ull << 32)) {
         // fused single-pass decode unless QF_DECODE_SYN=1 asks for the
         // two-kernel syndrome + v_perm combine path
-        const char* two = getenv("QF_DECODE_SYN");
+        const bool two = ctx->opt[QF_OPT_DECODE_PATH] == 1;
         // (L % 16 != 0: the lane-chunk kernel stores the partial last unit
         // bytewise but reads it whole, so the rows must start 16-byte aligned;
         // a desc batch's offset tables say so through offs_in_al16)
-        const bool tail_ok = L % 16 == 0 || (qf::dec_name(k, r, L) && (!ctx->offs_in || ctx->offs_in_al16) &&
+        const bool tail_ok = L % 16 == 0 || (qf::dec_name(&ctx->bs, k, r, L) && (!ctx->offs_in || ctx->offs_in_al16) &&
                                              ((uintptr_t)rows | sh->row_stride |
                                               (ctx->offs_in ? 0 : sh->rows_gen_stride)) % 16 == 0 &&
-                                             std::string(qf::dec_name(k, r, L)).find("decc") != std::string::npos);
+                                             std::string(qf::dec_name(&ctx->bs, k, r, L)).find("decc") != std::string::npos);
         // (the row-split 'decs' kernels of small batches share the decc layout)
-        if (qf::dec_available(k, r) && !(two && atoi(two)) && tail_ok && sh->rec_gen_stride < (1ull << 32) &&
+        if (qf::dec_available(k, r) && !two && tail_ok && sh->rec_gen_stride < (1ull << 32) &&
             sh->rec_row_stride < (1ull << 32))
             return decode_fused(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
         return decode_cauchy(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
     }
     // codes without a syndrome kernel but with encode kernels (C5 Medium
     // windows: r up to 64): syndromes through the encode kernels
-    if (!row_coeffs && !(nobs && atoi(nobs)) && !qf::syn_available(k, r) && qf::bs_available(k, r) && r <= 64 &&
+    if (!row_coeffs && ctx->opt[QF_OPT_BITSLICED] && !qf::syn_available(k, r) && qf::bs_available(k, r) && r <= 64 &&
         e_max <= 64 && k + r <= 256 && max_rows <= 255 && L >= 32 && sh->rows_gen_stride < (1ull << 32) &&
         sh->row_stride < (1ull << 32) && (uint64_t)G * qf::bs_padded_units(L) < (1ull << 31))
         return decode_cauchy_enc(ctx, sh, G, rows, row_index, n_rows, rec, rec_index, n_rec, status);
@@ -1465,7 +1518,7 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         a.Lu = Lu;
         a.zero_slot = max_rows;
         a.total_units = (uint64_t)G * Lu;
-        const int PD = pick_PD("QF_DECODE_PD", 1, 1);
+        const int PD = pick_PD(ctx, QF_OPT_DECODE_PD, 1);
         hipEvent_t ev2 = prof_begin(ctx, ctx->stream);
         std::string cname;
         QF_CHECK_HIP(combine_payload(ctx, a, PD, ctx->stream, &cname));

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "qf_fec.h"
 #include "qf_kernels.h"
 
 namespace qf {
@@ -11,9 +12,9 @@ struct BsCache {
     static const int kMax = 128;   // >= the entries of qf_bs_table (build_lib.py checks)
     hipModule_t mod[kMax] = {};
     hipFunction_t fn[kMax] = {};
-    // additive-FFT kernels ('E' encode, 'C' fused decode) where generated;
-    // set from the context options (QF_OPT_FFT_KERNELS)
-    bool fft = true;
+    // the owning context's options (QF_OPT_*, qf_ctx_set_option)
+    const int64_t* opt = nullptr;
+    int64_t get(int o) const { return opt ? opt[o] : 0; }
 };
 
 // Is there a specialised kernel for the Cauchy matrix of (k, r)?
@@ -62,7 +63,8 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // read in whole 16-byte units, so they must start 16-byte aligned.
 bool dec_available(uint32_t k, uint32_t r);
 // the kernel dec_launch runs for (k, r, L) and, given G and num_cus, that batch size
-const char* dec_name(uint32_t k, uint32_t r, uint32_t L = 0, uint32_t G = 0, int num_cus = 0, bool fft = false);
+const char* dec_name(const BsCache* cache, uint32_t k, uint32_t r, uint32_t L = 0, uint32_t G = 0,
+                     int num_cus = 0);
 hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, uint32_t r,
                       const uint8_t* rows, uint8_t* rec, uint64_t rgs, uint64_t rec_gs, uint64_t rs,
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,

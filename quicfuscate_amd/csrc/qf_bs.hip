@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include "qf_bs.h"
+#include "qf_fec.h"
 
 struct QfBsEntry {
     uint32_t k, r, pd;
@@ -113,8 +114,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // 4-wave blocks per CU, so an encode and a decode launched on two streams
     // can be resident on every SIMD at once
     {
-        const char* cap = getenv(enc ? "QF_ENC_BLOCKS_PER_CU" : "QF_DEC_BLOCKS_PER_CU");
-        const int c = cap ? atoi(cap) : 0;
+        const int c = (int)cache.get(enc ? QF_OPT_ENC_BLOCKS_PER_CU : QF_OPT_DEC_BLOCKS_PER_CU);
         if (c > 0 && num_cus > 0 && blocks > (uint32_t)(c * num_cus)) blocks = (uint32_t)(c * num_cus);
     }
     uint32_t a[32] = {};
@@ -198,10 +198,9 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     // they exist, unless QF_ENCODE_KSPLIT=0
     char mode = 'e';
     {
-        const char* v = getenv("QF_ENCODE_KSPLIT");
         const uint64_t items = ((uint64_t)G * Lv + 127) / 128;
-        if (!(v && !atoi(v)) && find('f', k, r) && num_cus > 0 && items <= (uint64_t)num_cus) mode = 'f';
-        else if (cache.fft && find('E', k, r)) mode = 'E';
+        if (cache.get(QF_OPT_ENCODE_KSPLIT) && find('f', k, r) && num_cus > 0 && items <= (uint64_t)num_cus) mode = 'f';
+        else if (cache.get(QF_OPT_FFT_KERNELS) && find('E', k, r)) mode = 'E';
     }
     // one launch per pass of repairs (codes with more repairs than a kernel
     // holds): pass j0 writes repair rows j0 .. j0 + r_pass - 1
@@ -252,14 +251,14 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
 // (G > 0 and num_cus given) its row-split form 'k', unless QF_DECODE_KSPLIT=0
 // (tools/dec_lab.py --small: 32 against 51-56 us from G = 1 to 256 at the C3
 // shape; past one item per CU the one-wave-per-item kernel wins)
-static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G = 0, int num_cus = 0,
-                                 bool fft = false) {
-    const char* leg = getenv("QF_DECODE_LEGACY");
+static const QfBsEntry* find_dec(const BsCache* cache, uint32_t k, uint32_t r, uint32_t L, uint32_t G = 0,
+                                 int num_cus = 0) {
+    const bool legacy = cache && cache->get(QF_OPT_DECODE_PATH) == 2;
+    const bool fft = cache && cache->get(QF_OPT_FFT_KERNELS);
     const QfBsEntry* c = find('c', k, r);
-    if (c && !(leg && atoi(leg)) && (L == 0 || (L + 15) / 16 >= 3)) {
+    if (c && !legacy && (L == 0 || (L + 15) / 16 >= 3)) {
         if (G && num_cus > 0 && L) {
-            const char* v = getenv("QF_DECODE_KSPLIT");
-            const bool ks = !(v && !atoi(v));
+            const bool ks = !cache || cache->get(QF_OPT_DECODE_KSPLIT);
             const uint64_t Q = ((L + 15) / 16 + 1) / 2, items = ((uint64_t)G * Q + 63) / 64;
             const QfBsEntry* kk = find('k', k, r);
             if (ks && kk && items <= (uint64_t)num_cus) return kk;
@@ -273,10 +272,10 @@ static const QfBsEntry* find_dec(uint32_t k, uint32_t r, uint32_t L, uint32_t G 
     return find('d', k, r);
 }
 
-bool dec_available(uint32_t k, uint32_t r) { return find_dec(k, r, 0) != nullptr; }
+bool dec_available(uint32_t k, uint32_t r) { return find_dec(nullptr, k, r, 0) != nullptr; }
 
-const char* dec_name(uint32_t k, uint32_t r, uint32_t L, uint32_t G, int num_cus, bool fft) {
-    const QfBsEntry* e = find_dec(k, r, L, G, num_cus, fft);
+const char* dec_name(const BsCache* cache, uint32_t k, uint32_t r, uint32_t L, uint32_t G, int num_cus) {
+    const QfBsEntry* e = find_dec(cache, k, r, L, G, num_cus);
     return e ? e->name : nullptr;
 }
 
@@ -285,7 +284,7 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       uint64_t rec_rs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero, const uint8_t* lu, uint32_t lu_stride, const uint32_t* tab256,
                       const uint64_t* rows_offs, const uint64_t* rec_offs) {
-    const QfBsEntry* e = find_dec(k, r, L, G, num_cus, cache.fft);
+    const QfBsEntry* e = find_dec(&cache, k, r, L, G, num_cus);
     if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
         return hipErrorInvalidValue;
     // the LU record pointer is computed with a 32-bit stride multiply

@@ -978,8 +978,8 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
     const uint64_t ns_cap = acc && acc_bytes > kShapeBytes ? (acc_bytes - kShapeBytes) / (4 * slab) : 0;
     uint32_t ns = acc && lanes < want ? matvec_split(lanes, a.nin, want) : 1;
     ns = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(ns, ns_cap));
-    const char* dv = getenv("QF_GF16_DYN");   // 0: size split launches from e_max on the host
-    const bool dyn = acc && ns_cap >= 1 && (a.nout_g || a.nin_g) && !(dv && !atoi(dv));
+    // QF_OPT_GF16_DYN 0: size split launches from e_max on the host
+    const bool dyn = acc && ns_cap >= 1 && (a.nout_g || a.nin_g) && qf::ctx_opt(ctx, QF_OPT_GF16_DYN);
     a.shape = dyn ? reinterpret_cast<Mv16Shape*>(acc + acc_bytes - kShapeBytes) : nullptr;
     a.G = G;
     a.want = want;
@@ -996,11 +996,9 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
     // overrides kLogifyBlocks)
     a.in_log = 0;
     {
-        const char* v = getenv("QF_GF16_LOGIFY");
-        const char* mb = getenv("QF_GF16_LOGIFY_MIN_BLOCKS");
-        const uint32_t min_blocks = mb ? (uint32_t)atoi(mb) : kLogifyBlocks;
+        const uint32_t min_blocks = (uint32_t)qf::ctx_opt(ctx, QF_OPT_GF16_LOGIFY_MIN_BLOCKS);
         const uint64_t n = G * a.nin * a.Lu;
-        if (!(v && !atoi(v)) && (a.nob >= min_blocks || n >= kLogifyUnits)) {
+        if (qf::ctx_opt(ctx, QF_OPT_GF16_LOGIFY) && (a.nob >= min_blocks || n >= kLogifyUnits)) {
             uint8_t* lr = nullptr;
             int s = qf::ctx_gf16_logrows(ctx, n * 16, &lr);
             if (s) return s;
@@ -1127,8 +1125,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     // QF_GF16_LDS_GJ=1: the all-generations-at-once Gauss-Jordan in LDS
     // (W = C[J,E]^-1 [I | C[J,S]] over every slot) for e_max <= 64; default:
     // the syndrome path below for every shape
-    const char* lds_gj = getenv("QF_GF16_LDS_GJ");
-    if (e_max <= kEMax && lds_gj && atoi(lds_gj)) {
+    if (e_max <= kEMax && qf::ctx_opt(ctx, QF_OPT_GF16_LDS_GJ)) {
         // small path: every generation at once
         const size_t wb = align256((size_t)G * ew * k * 2), ab = matvec_acc_bytes(ctx, G, e_max, k, L);
         s = qf::ctx_work(ctx, wb + ab, &w);

@@ -26,6 +26,8 @@ const uint32_t* ctx_tab256(qf_ctx* ctx);
 // A device buffer of >= bytes for GF(2^16) input rows in log form (its own
 // allocation, so it can sit beside the workspace; valid until the next call).
 int ctx_gf16_logrows(qf_ctx* ctx, size_t bytes, uint8_t** out);
+// The context's value of option `opt` (QF_OPT_*, qf_ctx_set_option).
+int64_t ctx_opt(qf_ctx* ctx, int opt);
 // qf_ctx_profile bracketing of a launch.
 hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st);
 void ctx_prof_end(qf_ctx* ctx, hipStream_t st, hipEvent_t ev, const std::string& name);
@@ -52,8 +54,8 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
 int encode_ring_window(qf_ctx* ctx, uint32_t k, uint32_t first, uint32_t count, uint32_t L,
                        const uint8_t* ring, uint64_t stride, uint32_t rot, uint8_t* rep, uint64_t rep_stride,
                        const uint8_t* fresh = nullptr, uint8_t* fresh_dst = nullptr, uint32_t fresh_units = 0);
-// Whether the small-batch encode is enabled (QF_ENCODE_SMALL != 0).
-bool small_encode_enabled();
+// Whether the small-batch encode is enabled (QF_OPT_ENCODE_SMALL != 0).
+bool small_encode_enabled(qf_ctx* ctx);
 
 // Multi-connection send batches (qf_objects.hip).  The caller holds the
 // context lock (ctx_lock) across these.

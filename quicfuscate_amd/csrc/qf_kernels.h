@@ -126,7 +126,8 @@ hipError_t launch_xor_repairs(const GatherArgs& a, int num_cus, hipStream_t st);
 // multiple of 2*(PD+1).
 hipError_t launch_combine_uniform(const CombineUniformArgs& a, int R, int V, int PD, int num_cus,
                                   hipStream_t st);
-hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st);
+hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st,
+                                bool split_ok = true);
 hipError_t launch_decode_prepare(const PrepareArgs& a, hipStream_t st);
 size_t prepare_lds_bytes(uint32_t k, uint32_t e_max, uint32_t max_rows);
 hipError_t launch_mul_slice(const uint8_t* a, const uint8_t* b, uint8_t* out, uint64_t n,

@@ -1323,12 +1323,11 @@ static hipError_t launch_slots_p(const CombineSlotsArgs& a, int num_cus, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st) {
+hipError_t launch_combine_slots(const CombineSlotsArgs& a, int PD, int num_cus, hipStream_t st, bool split_ok) {
     // at most one 64-unit wave-item per CU: the slot-split kernel, unless
-    // QF_COMBINE_SPLIT=0
+    // the context's QF_OPT_COMBINE_SPLIT is 0 (split_ok)
     const uint64_t items = (a.total_units + 63) / 64;
-    const char* sp = getenv("QF_COMBINE_SPLIT");
-    if (!(sp && !atoi(sp)) && num_cus > 0 && items <= (uint64_t)num_cus) {
+    if (split_ok && num_cus > 0 && items <= (uint64_t)num_cus) {
         if (items == 0) return hipSuccess;
         hipLaunchKernelGGL(k_combine_slots_split, dim3((uint32_t)items), dim3(256), 0, st, a);
         return hipGetLastError();

@@ -105,13 +105,7 @@ struct qf_decoder {
 
 namespace {
 
-bool send_fused_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("QF_SEND_FUSED");
-        return !(v && !atoi(v));
-    }();
-    return on;
-}
+bool send_fused_enabled(qf_ctx* ctx) { return qf::ctx_opt(ctx, QF_OPT_SEND_FUSED) != 0; }
 
 // Upload a packet still waiting for the fused send into its ring slot
 // (through the staging buffer, as add_source_packet does).
@@ -154,7 +148,7 @@ int qf_encoder_new(qf_ctx* ctx, uint32_t k, uint32_t n, uint32_t max_len, qf_enc
     e->stride = round16(max_len);
     e->lens.assign(k, 0);
     e->ids.assign(k, 0);
-    e->ring_rot = qf::small_encode_enabled();
+    e->ring_rot = qf::small_encode_enabled(ctx);
     if (hipMalloc(&e->d_ring, (size_t)2 * k * e->stride) != hipSuccess ||
         hipMalloc(&e->d_out, (size_t)256 * e->stride) != hipSuccess ||
         hipMemset(e->d_ring, 0, (size_t)2 * k * e->stride) != hipSuccess ||
@@ -193,7 +187,7 @@ int qf_encoder_add_source_packet(qf_encoder* e, uint64_t id, const uint8_t* data
     if (int s = encoder_flush(e)) return s;
     const uint32_t slot = e->head;
     // (the packet travels in the kernel arguments: stride <= 16 SEND_PKT_UNITS)
-    if (e->ring_rot && e->count + 1 >= e->k && e->stride <= 16 * qf::SEND_PKT_UNITS && send_fused_enabled()) {
+    if (e->ring_rot && e->count + 1 >= e->k && e->stride <= 16 * qf::SEND_PKT_UNITS && send_fused_enabled(e->ctx)) {
         // the window will be full: keep the packet for the fused send
         if (!e->h_fresh) {
             if (hipHostMalloc(reinterpret_cast<void**>(&e->h_fresh), e->stride) != hipSuccess) return QF_ENOMEM;
@@ -632,16 +626,13 @@ int qf_decoder_get_decoded_packets(qf_decoder* d, uint8_t* out_data, uint32_t ou
 namespace qf {
 
 namespace {
-// QF_SEND_PROFILE=1: per-phase host wall time of send batches, printed at exit
+// QF_OPT_SEND_PROFILE: per-phase host wall time of send batches, summed over
+// the calls of every context that has the option on, printed at process exit
 struct SendProfile {
-    bool on = false;
+    bool on = false;      // the current call's context has the option on
     uint64_t calls = 0, seen = 0;
     double t[4] = {0, 0, 0, 0};
     double u[4] = {0, 0, 0, 0};
-    SendProfile() {
-        const char* e = getenv("QF_SEND_PROFILE");
-        on = e && atoi(e) != 0;
-    }
     ~SendProfile() {
         if (on && calls)
             fprintf(stderr, "[qf send batch] %llu calls, us/call: stage %.1f  launch %.1f  wait %.1f  copy-out %.1f\n",
@@ -659,11 +650,12 @@ double wall() {
 // Host copy-out of large send batches: a few persistent workers plus the
 // calling thread take items off a shared counter (a single-thread memcpy of
 // the ~12 MB of repairs of 1024 windows runs at ~12 GB/s).  QF_COPY_THREADS
-// sets the worker count (0: the calling thread alone).
+// QF_OPT_COPY_THREADS of the context whose batch first uses the pool sets
+// the worker count (0: the calling thread alone, -1: auto).
 class CopyPool {
   public:
-    static CopyPool& get() {
-        static CopyPool p;
+    static CopyPool& get(int64_t threads) {
+        static CopyPool p(threads);
         return p;
     }
     // fn(i) for every i < n, across the workers and the calling thread
@@ -696,10 +688,9 @@ class CopyPool {
     }
 
   private:
-    CopyPool() {
-        const char* e = getenv("QF_COPY_THREADS");
+    explicit CopyPool(int64_t threads) {
         unsigned hw = std::thread::hardware_concurrency();
-        unsigned n = e ? (unsigned)atoi(e) : std::min(7u, hw > 2 ? hw / 2 - 1 : 0u);
+        unsigned n = threads >= 0 ? (unsigned)threads : std::min(7u, hw > 2 ? hw / 2 - 1 : 0u);
         for (unsigned i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
     }
     void drain(const std::function<void(uint32_t)>& fn, uint32_t n) {
@@ -734,6 +725,7 @@ class CopyPool {
 int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     if (!ctx || (M && !v)) return QF_EINVAL;
     if (M == 0) return QF_OK;
+    g_send_prof.on = ctx_opt(ctx, QF_OPT_SEND_PROFILE) != 0;
     const double tp0 = g_send_prof.on ? wall() : 0.0;
     for (uint32_t m = 0; m < M; ++m) {
         qf_encoder* e = v[m].e;
@@ -843,10 +835,7 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     // download in chunks of windows, each copied out on the host while the
     // next one is in flight; large chunks go through the copy workers
     const uint32_t nw = (uint32_t)wins.size();
-    static const uint32_t max_chunks = [] {
-        const char* e = getenv("QF_SEND_CHUNKS");
-        return e ? std::max(1u, std::min(8u, (uint32_t)atoi(e))) : 1u;
-    }();
+    const uint32_t max_chunks = (uint32_t)ctx_opt(ctx, QF_OPT_SEND_CHUNKS);
     const uint32_t chunks = nw == 0 ? 0 : std::max(1u, std::min<uint32_t>(max_chunks, (uint32_t)(rep_bytes >> 20)));
     hipEvent_t* ev = nullptr;
     if (chunks && (s = ctx_send_events(ctx, chunks, &ev)) != QF_OK) return s;
@@ -870,7 +859,7 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         if (g_send_prof.on) t_wait += wall() - tw;
         const uint32_t w0 = cw[c], n = cw[c + 1] - cw[c];
         if ((size_t)(chunks > 1 ? rep_bytes / chunks : rep_bytes) >= ((size_t)1 << 20)) {
-            CopyPool::get().run(n, [&](uint32_t i) { copy_out(w0 + i); });
+            CopyPool::get(ctx_opt(ctx, QF_OPT_COPY_THREADS)).run(n, [&](uint32_t i) { copy_out(w0 + i); });
         } else {
             for (uint32_t i = 0; i < n; ++i) copy_out(w0 + i);
         }

@@ -96,6 +96,19 @@ class Context:
     def set_stream(self, stream: int) -> None:
         check(L._lib().qf_ctx_set_stream(self.handle, ctypes.c_void_p(stream)))
 
+    def set_option(self, name: str, value: int) -> None:
+        """qf_ctx_set_option: a kernel-path option of this context
+        (L.OPTIONS: "fft_kernels", "decode_path", ...; include/qf_fec.h)."""
+        check(L._lib().qf_ctx_set_option(self.handle, L.OPTIONS[name], int(value)), f"option {name}")
+
+    def option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        check(L._lib().qf_ctx_get_option(self.handle, L.OPTIONS[name], ctypes.byref(v)), f"option {name}")
+        return v.value
+
+    def options(self) -> dict:
+        return {n: self.option(n) for n in L.OPTIONS}
+
     def set_payload_wait(self, event) -> None:
         """qf_ctx_set_payload_wait: the next decode_batch runs its acceptance
         pass at once and its payload pass after `event` (a torch.cuda.Event
@@ -141,11 +154,30 @@ class Context:
 _DEFAULT: Optional[Context] = None
 
 
+_DEFAULT_OPTS: dict = {}
+
+
 def default_context() -> Context:
-    global _DEFAULT
+    global _DEFAULT, _DEFAULT_OPTS
     if _DEFAULT is None:
         _DEFAULT = Context()
+        _DEFAULT_OPTS = _DEFAULT.options()
     return _DEFAULT
+
+
+def set_default_options(**opts) -> None:
+    """Kernel-path options (QF_OPT_*) on the default context, e.g.
+    set_default_options(encode_small=0, decode_path=1)."""
+    ctx = default_context()
+    for n, v in opts.items():
+        ctx.set_option(n, v)
+
+
+def reset_default_options() -> None:
+    """The default context's options back to those it was created with."""
+    if _DEFAULT is not None and _DEFAULT.handle:
+        for n, v in _DEFAULT_OPTS.items():
+            _DEFAULT.set_option(n, v)
 
 
 def _ptr(t) -> int:

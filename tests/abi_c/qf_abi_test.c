@@ -452,6 +452,28 @@ static void test_framing(void) {
     printf("framing ok\n");
 }
 
+/* qf_ctx_set_option / qf_ctx_get_option: ranges, unknown options, and the
+ * batch codec on the coefficient-block kernels (QF_OPT_FFT_KERNELS = 0) and
+ * the general v_perm paths (QF_OPT_BITSLICED = 0), both against the oracle */
+static void test_options(qf_ctx *ctx) {
+    int64_t v = -7;
+    QF(qf_ctx_get_option(ctx, QF_OPT_FFT_KERNELS, &v));
+    CHECK(v == 1, "fft_kernels default %lld", (long long)v);
+    CHECK(qf_ctx_set_option(ctx, QF_OPT_COUNT, 1) == QF_EINVAL, "unknown option");
+    CHECK(qf_ctx_get_option(ctx, -1, &v) == QF_EINVAL, "unknown option (get)");
+    QF(qf_ctx_set_option(ctx, QF_OPT_SEND_CHUNKS, 99));
+    QF(qf_ctx_get_option(ctx, QF_OPT_SEND_CHUNKS, &v));
+    CHECK(v == 8, "send_chunks clamps to 8, got %lld", (long long)v);
+    QF(qf_ctx_set_option(ctx, QF_OPT_SEND_CHUNKS, 1));
+    QF(qf_ctx_set_option(ctx, QF_OPT_FFT_KERNELS, 0));
+    test_batch(ctx);
+    QF(qf_ctx_set_option(ctx, QF_OPT_BITSLICED, 0));
+    test_batch(ctx);
+    QF(qf_ctx_set_option(ctx, QF_OPT_BITSLICED, 1));
+    QF(qf_ctx_set_option(ctx, QF_OPT_FFT_KERNELS, 1));
+    printf("options ok\n");
+}
+
 int main(void) {
     CHECK(qf_abi_version() == QF_ABI_VERSION, "ABI version");
     test_gf();
@@ -459,6 +481,7 @@ int main(void) {
     qf_ctx *ctx;
     QF(qf_ctx_create(0, NULL, &ctx));
     test_batch(ctx);
+    test_options(ctx);
     test_desc(ctx);
     test_objects(ctx);
     test_wiedemann(ctx);

@@ -43,3 +43,19 @@ def gpu_ctx(qf):
 
     assert torch.cuda.is_available(), "gpu test on a host without a HIP device"
     return qf.default_context()
+
+
+@pytest.fixture(autouse=True)
+def _restore_default_options():
+    """Tests pin kernel paths with fec.set_default_options; every test starts
+    from the default context's creation-time options."""
+    yield
+    fec = sys.modules.get("quicfuscate_amd.fec")
+    if fec is not None:
+        fec.reset_default_options()
+
+
+@pytest.fixture
+def qf_opts(qf):
+    """qf_opts(encode_small=0, ...): options of the default context for one test."""
+    return qf.set_default_options

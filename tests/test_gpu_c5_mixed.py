@@ -12,10 +12,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _bit_sliced_encode(monkeypatch):
+def _bit_sliced_encode(qf):
     # these tests pin the bit-sliced kernels (and their zero tails) at small
     # G; the small-batch kernel has its own cases (test_gpu_encode.py)
-    monkeypatch.setenv("QF_ENCODE_SMALL", "0")
+    qf.set_default_options(encode_small=0)
 L_JUMBO = 9000
 RS = 9008          # row stride: 16-byte multiple (C ABI), rows zero padded
 REP_RS = 9088      # pool-block repair rows: round_up(9000, 128), the zero tail fits

@@ -97,47 +97,43 @@ def check(oracle, k, L, src, gens, out, with_coeffs):
             assert (rec[g * rec_gs + m * rrs + L: g * rec_gs + (m + 1) * rrs] == 0x5A).all()
 
 
-PATHS = ["default", "default_1wave", "syn", "general", "syn_bs", "general_bs"]
+PATHS = ["default", "default_1wave", "default_nofft", "syn", "general", "syn_bs", "general_bs"]
 
 
-def _path(monkeypatch, path):
+def _path(_unused, path):
+    """Pin the decode path on the default context (fec.set_default_options;
+    conftest restores the options after each test)."""
+    from quicfuscate_amd import fec
+
     # "default" at these batch sizes (at most one item per CU) runs the
     # row-split kernels (qf_cauchy_decs_*, and qf_cauchy_bss_* for the r > 16
     # syndrome passes: four waves per item); "default_1wave" pins the
     # one-wave-per-item kernels (qf_cauchy_decc_*, qf_cauchy_bs_*)
     # (and the payload pass k_combine_slots_split against k_combine_slots)
-    if path == "default_1wave":
-        monkeypatch.setenv("QF_DECODE_KSPLIT", "0")
-        monkeypatch.setenv("QF_ENCODE_KSPLIT", "0")
-        monkeypatch.setenv("QF_COMBINE_SPLIT", "0")
+    # "default_nofft": the one-wave kernels with one coefficient block per
+    # repair instead of the additive-FFT row loop (QF_OPT_FFT_KERNELS = 0)
+    one = path in ("default_1wave", "default_nofft")
+    fft = 0 if path == "default_nofft" else 1
+    if one:
         path = "default"
-    else:
-        monkeypatch.delenv("QF_DECODE_KSPLIT", raising=False)
-        monkeypatch.delenv("QF_ENCODE_KSPLIT", raising=False)
-        monkeypatch.delenv("QF_COMBINE_SPLIT", raising=False)
+    opts = dict(decode_ksplit=0 if one else 1, encode_ksplit=0 if one else 1, combine_split=0 if one else 1,
+                fft_kernels=fft)
     # "*_bs": the payload pass takes the bit-sliced qf_combine_bs at every row
     # length (by default only rows of >= 64 lane-chunks of 32 B do); "general"
-    # keeps k_combine_slots at every length (QF_COMBINE_BS=0)
-    monkeypatch.delenv("QF_COMBINE_BS", raising=False)
+    # keeps k_combine_slots at every length (combine_bs 0)
+    opts.update(combine_bs=1, combine_bs_min_q=64)
     if path.endswith("_bs"):
-        monkeypatch.setenv("QF_COMBINE_BS_MIN_Q", "1")
+        opts["combine_bs_min_q"] = 1
         path = path[:-3]
-    else:
-        monkeypatch.delenv("QF_COMBINE_BS_MIN_Q", raising=False)
-        if path == "general":
-            monkeypatch.setenv("QF_COMBINE_BS", "0")
+    elif path == "general":
+        opts["combine_bs"] = 0
     # "default": fused decode (syndromes + LU solve in one kernel) where a
     # bit-sliced kernel exists for (k, r) (Cauchy code, L % 16 == 0);
     # "syn": syndrome kernel + payload pass (two kernels);
     # "general": Gauss-Jordan + payload pass
-    if path == "general":
-        monkeypatch.setenv("QF_DISABLE_BS", "1")
-    else:
-        monkeypatch.delenv("QF_DISABLE_BS", raising=False)
-    if path == "syn":
-        monkeypatch.setenv("QF_DECODE_SYN", "1")
-    else:
-        monkeypatch.delenv("QF_DECODE_SYN", raising=False)
+    opts["bitsliced"] = 0 if path == "general" else 1
+    opts["decode_path"] = 1 if path == "syn" else 0
+    fec.set_default_options(**opts)
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -230,12 +226,8 @@ def test_decode_repair_index_out_of_range(qf, oracle, gpu_ctx):
     gens = [(list(range(1, k)) + [k + r], np.vstack([src[0, 1:], rep[:1]]), None),
             (list(range(k)), src[1], None)]
     for path in PATHS:
-        import os
-        os.environ.pop("QF_DISABLE_BS", None)
-        if path == "general":
-            os.environ["QF_DISABLE_BS"] = "1"
+        qf.set_default_options(bitsliced=0 if path == "general" else 1)
         out = run_decode(qf, k, r, L, 2, k, gens, False)
-        os.environ.pop("QF_DISABLE_BS", None)
         assert list(out[3]) == [-1, 0], path
 
 
@@ -278,10 +270,7 @@ def test_decode_no_erasures(qf, oracle, gpu_ctx):
 def test_decode_chunked_pipeline(qf, oracle, gpu_ctx, chunk, overlap, monkeypatch):
     # stages A/B over chunks of generations, B on an auxiliary stream
     # (double-buffered syndromes); twice in a row on the same context
-    monkeypatch.setenv("QF_DECODE_CHUNK", chunk)
-    monkeypatch.setenv("QF_DECODE_OVERLAP", overlap)
-    monkeypatch.setenv("QF_DECODE_SYN", "1")
-    monkeypatch.delenv("QF_DISABLE_BS", raising=False)
+    qf.set_default_options(decode_chunk=int(chunk), decode_overlap=int(overlap), decode_path=1, bitsliced=1)
     for seed in (1, 2):
         rng = np.random.default_rng(seed)
         k, r, L, G = 64, 16, 1200, 53

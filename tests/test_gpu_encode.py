@@ -14,10 +14,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _bit_sliced_encode(monkeypatch):
+def _bit_sliced_encode(qf):
     # these tests pin the bit-sliced kernels (and their zero tails) at small
     # G; the small-batch kernel has its own cases (test_gpu_encode.py)
-    monkeypatch.setenv("QF_ENCODE_SMALL", "0")
+    qf.set_default_options(encode_small=0)
 
 
 GOLDEN = json.loads((Path(__file__).parent / "golden" / "golden.json").read_text())
@@ -104,14 +104,16 @@ def test_encode_zero_tail(qf, oracle, gpu_ctx, k, r, L, G, rrs, rgs):
 
 
 @pytest.mark.parametrize("k,r,L,G", CASES)
-@pytest.mark.parametrize("V", ["1", "2", "perm"])
+@pytest.mark.parametrize("V", ["1", "2", "perm", "nofft"])
 def test_encode_matches_oracle(qf, oracle, gpu_ctx, k, r, L, G, V, monkeypatch):
     # V=1/2: default dispatch (bit-sliced kernel where one exists);
     # "perm": force the general v_perm kernel
     if V == "perm":
-        monkeypatch.setenv("QF_DISABLE_BS", "1")
+        qf.set_default_options(bitsliced=0)
+    elif V == "nofft":   # bit-sliced with one coefficient block per repair
+        qf.set_default_options(fft_kernels=0)
     else:
-        monkeypatch.setenv("QF_ENCODE_V", V)
+        qf.set_default_options(encode_v=int(V))
     rng = np.random.default_rng(k * 1000 + r * 10 + L)
     rs = _r16(L) + (16 if k % 2 else 0)
     gs = k * rs + 32
@@ -259,7 +261,7 @@ def test_encode_small_batch_kernel(qf, oracle, gpu_ctx, k, r, L, G, monkeypatch)
     send path's kernel) is bit-exact against the oracle on every case,
     including odd k (zero second coefficient), partial last units and
     k + r = 256."""
-    monkeypatch.setenv("QF_ENCODE_SMALL", "1")
+    qf.set_default_options(encode_small=1)
     rng = np.random.default_rng(k * 3 + r + L + G)
     rs = _r16(L) + 16
     gs = k * rs + 32

@@ -25,10 +25,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _bit_sliced_encode(monkeypatch):
+def _bit_sliced_encode(qf):
     # these tests pin the bit-sliced kernels (and their zero tails) at small
     # G; the small-batch kernel has its own cases (test_gpu_encode.py)
-    monkeypatch.setenv("QF_ENCODE_SMALL", "0")
+    qf.set_default_options(encode_small=0)
 
 K, R, L = 64, 16, 1200
 SEED = 0x51464543
@@ -62,7 +62,7 @@ def test_bench_workload_full_size_round_trip(qf, oracle, gpu_ctx, path, monkeypa
     import torch
 
     if path == "syndrome":
-        monkeypatch.setenv("QF_DECODE_SYN", "1")
+        qf.set_default_options(decode_path=1)
     G, e = 65536, 13
     Lr = (L + 127) // 128 * 128           # the bench's pool-block repair rows
     src = _fill(torch, qf, G * K * L, SEED)

@@ -159,7 +159,7 @@ def check_decode(oracle, src, gens, k, L, res):
 def test_decode16_small_path(qf, oracle, gpu_ctx, k, r, L, G, with_coeffs, lds_gj, monkeypatch):
     """Both decode paths for e <= 64: syndromes + closed-form / workspace
     inverse (default) and the all-generations Gauss-Jordan in LDS."""
-    monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
+    qf.set_default_options(gf16_lds_gj=int(lds_gj))
     rng = np.random.default_rng(k * 7 + r)
     src, gens = make_gens(oracle, rng, k, r, L, G, coeff_mode="cauchy" if not with_coeffs else "random")
     check_decode(oracle, src, gens, k, L, run_decode16(qf, k, r, L, G, gens, with_coeffs))
@@ -167,7 +167,7 @@ def test_decode16_small_path(qf, oracle, gpu_ctx, k, r, L, G, with_coeffs, lds_g
 
 @pytest.mark.parametrize("lds_gj", ["0", "1"])
 def test_decode16_statuses(qf, oracle, gpu_ctx, lds_gj, monkeypatch):
-    monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
+    qf.set_default_options(gf16_lds_gj=int(lds_gj))
     rng = np.random.default_rng(5)
     k, r, L = 12, 6, 40
     _, g1 = make_gens(oracle, rng, k, r, L, 1, erase=3, short=True)   # ENOTREADY
@@ -186,8 +186,8 @@ def test_decode16_mixed_erasures_device_shape(qf, oracle, gpu_ctx, lds_gj, dyn, 
     """Generations with very different e in one batch (0, a few, e_max, a
     short and a singular one): the split matvecs are shaped on the device from
     the largest e_g (k_shape16), the rows of every generation still match."""
-    monkeypatch.setenv("QF_GF16_LDS_GJ", lds_gj)
-    monkeypatch.setenv("QF_GF16_DYN", dyn)   # 0: the host's e_max shape
+    qf.set_default_options(gf16_lds_gj=int(lds_gj))
+    qf.set_default_options(gf16_dyn=int(dyn))   # 0: the host's e_max shape
     rng = np.random.default_rng(17)
     k, r, L = 128, 64, 200
     parts = [make_gens(oracle, rng, k, r, L, 1, erase=e) for e in (0, 3, 64, 17)]

@@ -194,7 +194,7 @@ def test_ring_encoder_every_rotation(qf, oracle, gpu_ctx, monkeypatch, small, k)
     packets (decoder.rs:164-275)."""
     import numpy as np
 
-    monkeypatch.setenv("QF_ENCODE_SMALL", small)
+    qf.set_default_options(encode_small=int(small))
     Lb, r = 1200, 4
     enc = qf.Encoder(k, k + r, max_len=Lb)
     rng = np.random.default_rng(k)
@@ -226,7 +226,7 @@ def test_fused_send_window(qf, oracle, gpu_ctx, monkeypatch, fused, k, max_len):
     generate entirely."""
     import numpy as np
 
-    monkeypatch.setenv("QF_SEND_FUSED", fused)
+    qf.set_default_options(send_fused=int(fused))
     r = 3
     enc = qf.Encoder(k, k + r, max_len=max_len)
     rng = np.random.default_rng(k + max_len)

@@ -29,6 +29,16 @@ ONLY = None   # --only name,name: build a subset
 CANON = ((1, 2, 4, 8, 16, 32, 64, 128), 64)
 D = {"ld_policy": "", "st_policy": ""}
 VARIANTS = [
+    # round 3f: recovered rows stored as back-substitution finishes them
+    ("f_warm", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
+    ("f_def", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
+    ("f_def_es", {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}, ()),
+    ("f_l9_def_es", {"chunked": True, "fft": 8, "lds_rows": 9, "early_stores": True, **D}, ()),
+    ("f_def_es_nt", {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, "ld_policy": ""}, ()),
+    ("f_def_2", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
+    ("f_def_es_2", {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}, ()),
+]
+VARIANTS_R03E = [
     # round 3e: default cache policies combined with the other levers
     ("f_warm", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
     ("f_def", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
