@@ -396,6 +396,32 @@ def main(argv=None):
 
     dom = max(kern_step_ms, key=kern_step_ms.get)
     tfile = REPO / "profiles" / "traffic.json"
+    sqfile = REPO / "profiles" / "sq_counters.json"
+    props = torch.cuda.get_device_properties(dev)
+    n_simd = 4 * props.multi_processor_count
+    clk_ghz = (getattr(props, "clock_rate", 0) or 2_400_000) / 1e6   # kHz -> GHz (MI355X engine clock 2.4)
+
+    def valu_roof(name, ms):
+        """VALU issue of the kernel's launch: SQ_INSTS_VALU per wave x waves
+        (rocprofv3 --pmc pass of this workload, profiles/sq_counters.json) at
+        4 cycles per wave64 instruction on n_simd SIMDs, against the launch
+        time measured here.  A lower bound on issue time (half-rate v_perm
+        counts one instruction)."""
+        try:
+            sq = json.loads(sqfile.read_text())
+        except Exception:
+            return None
+        ent = next((v for n_, v in sq.items() if n_ == name or n_.startswith(name)), None)
+        if not ent or not ent.get("SQ_WAVES"):
+            return None
+        per_wave = ent["SQ_INSTS_VALU"] / ent["SQ_WAVES"]
+        waves = ent["SQ_WAVES"]
+        issue_ms = per_wave * waves * 4 / (n_simd * clk_ghz * 1e9) * 1e3
+        peak = n_simd * clk_ghz * 1e9 / 4 / 1e9          # wave-instructions per ns -> G/s
+        return {"bound": "valu", "achieved": round(per_wave * waves / (ms / 1e3) / 1e9, 2), "peak": round(peak, 2),
+                "unit": "G wave64 VALU instr/s", "frac": round(issue_ms / ms, 4),
+                "valu_per_wave": round(per_wave, 1), "waves": int(waves), "issue_ms": round(issue_ms, 4),
+                "source": "profiles/sq_counters.json (SQ_INSTS_VALU / SQ_WAVES, separate --pmc pass of this workload)"}
 
     def roofline(name):
         ms = kern_ms[name]
@@ -419,9 +445,12 @@ def main(argv=None):
             limiter = "valu_issue"
         else:
             limiter = "hbm"
+        vr = valu_roof(name, ms)
+        if vr is not None and vr["frac"] > achieved / PEAK_HBM_GBPS:
+            limiter = "valu_issue"
         return {"kernel": name, "launch_ms": round(ms, 4), "bound": "hbm", "limiter": limiter,
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                "frac": round(achieved / PEAK_HBM_GBPS, 4), "valu": vr, "traffic": traffic,
                 "traffic_source": ("profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE from separate rocprofv3 --pmc "
                                    "runs of this workload, not this run" if traffic is not None else None),
                 "algorithmic_bytes_per_launch": alg_bytes(name)}

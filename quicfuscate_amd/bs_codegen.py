@@ -421,6 +421,9 @@ class KernelSpec:
     # chunked dec: store each recovered row as soon as back-substitution has
     # finished it (x_u after backward column u), not all after the solve
     early_stores: bool = False
+    # fft: plane pairs shared by >= 3 output rows of a constant multiply are
+    # XORed once into the transpose scratch registers
+    fft_cse: bool = True
 
     @property
     def ahead(self) -> int:
@@ -756,19 +759,58 @@ def _fft_plan(k: int, r: int, ch: int):
     return lch_fft.best_plan(k, r, ch)
 
 
-def _macc_cost(c: int) -> int:
-    rows = mul_matrix_rows(c)
-    return 0 if c == 0 else sum((bin(w).count("1") + 1) // 2 for w in rows)
+def _macc_cost(c: int, n_tmp: int = 0) -> int:
+    if c == 0:
+        return 0
+    if c == 1:
+        return 8
+    temps, terms = _cse_pairs(mul_matrix_rows(c), n_tmp)
+    return len(temps) + sum((len(t) + 1) // 2 for t in terms)
 
 
-def _macc(E, dst: int, src: int, c: int, init: bool):
+def _cse_pairs(rows: list[int], n_tmp: int) -> tuple[list, list]:
+    """Greedy common-subexpression pass over the rows of M_c: a pair of input
+    planes shared by >= 3 output rows becomes one temp (1 XOR, and one term
+    less in each of those rows: ~n/2 ops saved).  Returns the temps [(a, b)]
+    (operands: plane index 0..7 or 8 + temp) and each row's term list."""
+    terms = [[a for a in range(8) if w >> a & 1] for w in rows]
+    temps = []
+    while len(temps) < n_tmp:
+        cnt = {}
+        for t in terms:
+            for i in range(len(t)):
+                for j in range(i + 1, len(t)):
+                    cnt[(t[i], t[j])] = cnt.get((t[i], t[j]), 0) + 1
+        if not cnt:
+            break
+        (a, b), n = max(sorted(cnt.items()), key=lambda kv: kv[1])
+        if n < 3:
+            break
+        x = 8 + len(temps)
+        temps.append((a, b))
+        for t in terms:
+            if a in t and b in t:
+                t.remove(a)
+                t.remove(b)
+                t.append(x)
+    return temps, terms
+
+
+def _macc(E, dst: int, src: int, c: int, init: bool, tmp: tuple = ()):
     """dst (8 planes) ^= c * src, or dst = c * src when init (c a compile-time
     GF(256) constant: output plane b is the XOR of the input planes of row b
-    of M_c, two per v_bitop3)."""
+    of M_c, two per v_bitop3).  tmp: scratch VGPRs for shared plane pairs."""
     rows = mul_matrix_rows(c)
+    temps, rterms = _cse_pairs(rows, len(tmp)) if tmp and c not in (0, 1) else ([], None)
+
+    def reg(a):
+        return src + a if a < 8 else tmp[a - 8]
+    for q, (a, b) in enumerate(temps):
+        E(Op("v_xor", (tmp[q], reg(a), reg(b))))
     for b in range(8):
         d = dst + b
-        terms = [src + a for a in range(8) if rows[b] >> a & 1]
+        terms = [reg(a) for a in rterms[b]] if rterms is not None else \
+            [src + a for a in range(8) if rows[b] >> a & 1]
         if init:
             if not terms:
                 E(Op("v_movk", (d, 0)))
@@ -820,16 +862,18 @@ def _fft_stream(E, ops: list, spec: KernelSpec, load_row, wait_row, acc_block, n
     assert defer < ch
     last_q = ch.bit_length() - 2          # the chunk's last (top) inverse layer
 
+    tmp = tuple(range(V_T, V_T + 4)) if spec.fft_cse else ()
+
     def butterfly(base, i, j, s):
         yi, yj = slot(base + i), slot(base + j)
         for b in range(8):
             E(Op("v_xor", (yj + b, yj + b, yi + b)))
         if s:
-            _macc(E, yi, yj, s, init=False)
+            _macc(E, yi, yj, s, init=False, tmp=tmp)
 
     def fold(hc, mm):
         for t, c in P.acc[(hc, mm)]:
-            _macc(E, acc_block(t), slot(hc * ch + mm), c, init=t not in inited)
+            _macc(E, acc_block(t), slot(hc * ch + mm), c, init=t not in inited, tmp=tmp)
             inited.add(t)
 
     groups = []      # deferred end-of-chunk work, one group per following row
@@ -874,7 +918,7 @@ def _fft_stream(E, ops: list, spec: KernelSpec, load_row, wait_row, acc_block, n
     for i, j, s in P.final_bfly:
         ei, ej = acc_block(i), acc_block(j)
         if s:
-            _macc(E, ei, ej, s, init=False)
+            _macc(E, ei, ej, s, init=False, tmp=tmp)
         for b in range(8):
             E(Op("v_xor", (ej + b, ej + b, ei + b)))
 

@@ -164,7 +164,8 @@ def _bs_kernels(build_dir: Path) -> Path:
     # (default cache policy: neighbouring 1,200-B rows share their boundary
     # lines, and non-temporal loads / stores drop them before the reuse;
     # tools/dec_lab.py, profiles/r03_lab_dec_policy.json: 1.485 -> 1.39 ms)
-    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="")
+    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="",
+                            early_stores=True)
               for (k, r) in BS_FFT]
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))

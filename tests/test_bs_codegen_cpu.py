@@ -937,17 +937,22 @@ def test_emulated_fft_encode(oracle, k, r, pd, L, G, zero_tail, defer):
             assert (dst[off + tail: off + drs] == 0xEE).all()
 
 
-@pytest.mark.parametrize("k,r,L,G,seed,erase,offs", [
-    (64, 16, 1200, 3, 1, 13, False),   # the C3 shape
-    (64, 16, 96, 6, 2, None, True),    # random e, offset tables
-    (64, 16, 80, 5, 3, 16, False),     # e = r: every block a pivot
-    (64, 16, 1201, 2, 4, 5, False),    # partial last unit
-    (64, 10, 320, 4, 5, None, False),  # r < R
-    (16, 16, 96, 4, 6, 16, False),
-    (32, 16, 64, 5, 7, 0, False),      # nothing erased
+@pytest.mark.parametrize("k,r,L,G,seed,erase,offs,es,lds", [
+    (64, 16, 1200, 3, 1, 13, False, True, 0),   # the C3 shape, library options
+    (64, 16, 1200, 2, 8, 13, False, False, 9),  # rows staged in LDS (global_load_lds), compact tables
+    (64, 16, 96, 6, 2, None, True, True, 0),    # random e, offset tables
+    (64, 16, 80, 5, 3, 16, False, True, 6),     # e = r: every block a pivot
+    (64, 16, 1201, 2, 4, 5, False, True, 0),    # partial last unit
+    (64, 10, 320, 4, 5, None, False, False, 0),  # r < R
+    (16, 16, 96, 4, 6, 16, False, True, 0),
+    (32, 16, 64, 5, 7, 0, False, True, 0),      # nothing erased
 ])
-def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs):
-    assert _dec_case(oracle, k, r, 2, L, G, seed, erase, chunked=True, offs=offs, fft=8) == 0
+def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs, es, lds):
+    """The additive-FFT fused decode (syndromes through the chunked
+    transform, LU in registers): early stores (each recovered row as soon as
+    back-substitution finishes it) and LDS-staged rows included."""
+    assert _dec_case(oracle, k, r, 2, L, G, seed, erase, chunked=True, offs=offs, fft=8, early_stores=es,
+                     lds_rows=lds) == 0
 
 
 @pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "dec"), (32, 16, "dec"), (16, 16, "enc")])

@@ -28,6 +28,13 @@ ONLY = None   # --only name,name: build a subset
 
 CANON = ((1, 2, 4, 8, 16, 32, 64, 128), 64)
 D = {"ld_policy": "", "st_policy": ""}
+LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # the library's 'C' kernel
+# FETCH_SIZE calibration (tools/traffic_calib.py): the library kernel, and the
+# same kernel with the LU and the stores stripped, which reads a known byte
+# count through the same lane-chunk gather (64 rows + slot map + rank quad
+# per generation from HBM; the 13 zero-row reads hit L2)
+CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
+         ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
     # round 3f: recovered rows stored as back-substitution finishes them
     ("f_warm", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
@@ -314,10 +321,13 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/dec_lab.json")
     ap.add_argument("--only", default="", help="comma-separated variant names (build)")
+    ap.add_argument("--calib", action="store_true", help="build only the FETCH_SIZE calibration pair")
     ap.add_argument("--small", default="", help="comma-separated G values: run every variant at each")
     a = ap.parse_args()
     if a.only:
         ONLY = set(a.only.split(","))
+    if a.calib:
+        VARIANTS = CALIB
     if a.cmd == "build":
         build()
     else:
