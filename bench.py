@@ -524,8 +524,11 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu:
         S = min(args.cpu_sample, G)
         rep_dense = repv[:S].contiguous().view(-1)
+        out["cpu_host"] = cpu_host()
         out["cpu_baseline"] = cpu_baseline(src, rep_dense, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S)
         out["cpu_variants"] = cpu_variants(src, rep_dense, k, r, Lb, S)
+        out["cpu_c1"] = cpu_c1(torch, fec, ctx, Lb)
+        out["cpu_gf_mul_loop"] = cpu_gf_mul_loop()
 
     if args.c4_G > 0 and not c4:
         # free the headline's buffers (about 13 GB) before C4's (about 31 GB per rank)
@@ -912,6 +915,118 @@ def cpu_variants(src, rep, k, r, Lb, S):
             if kind == "clmul_dispatch":
                 ent["note"] = "reference as written incl. per-byte FeatureDetector/HashMap dispatch, timing only (F3)"
             res[f"{kind}_{nt}t"] = ent
+    return res
+
+
+ISA_FLAGS = ("sse2", "ssse3", "avx", "avx2", "avx512f", "avx512bw", "avx512vbmi", "avx512vl", "gfni", "pclmulqdq",
+             "vpclmulqdq", "vaes")
+
+
+def cpu_host() -> dict:
+    """the host the CPU rows ran on -- model, the
+    ISA flags the variants use, CPUs visible / usable, thread pinning."""
+    flags = set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    flags = set(line.split(":", 1)[1].split())
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "usable_cpus": usable,
+            "isa_flags": [f for f in ISA_FLAGS if f in flags],
+            "pinning": "worker w pinned to the w-th CPU of this process's affinity mask (pthread_attr_setaffinity_np) "
+                       "for the cpu_c1 rows; cpu_variants unpinned; cpu_baseline single-threaded"}
+
+
+def cpu_c1(torch, fec, ctx, Lb, seconds=1.5):
+    """BASELINE C1: the reference's CPU encode at its own shape,
+    k = 16 sources of L bytes, r in {16, 1} (adaptive.rs:139 Light = (16, 17);
+    tests/fec.rs:20-50), 0 % loss (the decoder passes the systematic rows
+    through), on 1 thread and on the 16 CPUs the box grants per GPU, threads
+    pinned.  Kinds: "table" = the reference's loop (decoder.rs:228-259) with
+    gf_mul_table semantics (the port); "clmul_dispatch" = the reference as
+    written (per-byte dispatch + CLMUL fold, timing only); "gfni" =
+    an optimized host encoder.  Every output that should equal the GPU's is
+    compared with the GPU encode of the same generations."""
+    import sys
+
+    sys.path.insert(0, str(REPO))
+    from tests import oracle_py as oracle  # test infrastructure: CPU baseline only
+
+    k = 16
+    rng = np.random.default_rng(SEED ^ 0xC1)
+    try:
+        n_all = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n_all = os.cpu_count() or 1
+    threads = sorted({1, min(16, n_all)})
+    res = {"shape": f"k={k}, L={Lb}, r in (16, 1), 0 % loss (encode; decode passes systematic rows through)",
+           "unit": "GiB/s (source payload, encode)", "pinned": True, "thread_counts": threads}
+    oracle.set_pinning(True)
+    per_gen_s = {"table": 1.2e-3, "clmul_dispatch": 20e-3, "gfni": 1e-5}
+    for r in (16, 1):
+        Gs = 4096
+        src = rng.integers(0, 256, (Gs, k, Lb), dtype=np.uint8)
+        # the same generations on the GPU (checker for the CPU outputs)
+        d_src = torch.from_numpy(src.reshape(-1)).cuda()
+        d_rep = torch.empty(Gs * r * Lb, dtype=torch.uint8, device="cuda")
+        fec.encode_batch(d_src, d_rep, k, r, Lb, src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lb,
+                         rep_gen_stride=r * Lb, G=Gs, ctx=ctx)
+        ctx.sync()
+        gpu = d_rep.cpu().numpy().reshape(Gs, r, Lb)
+        del d_src, d_rep
+        for kind in ("table", "clmul_dispatch", "gfni"):
+            if not oracle.has_cpu_kind(kind):
+                res[f"{kind}_r{r}"] = f"no {kind} on this host"
+                continue
+            for nt in threads:
+                # about `seconds` of work per row, at least one generation per thread
+                n = int(max(nt, min(Gs, seconds * nt / (per_gen_s[kind] * r / 16))))
+                t0 = time.perf_counter()
+                got = oracle.cpu_encode(kind, src[:n], r, nt)
+                dt = time.perf_counter() - t0
+                ent = {"gibps": round(n * k * Lb / dt / (1 << 30), 5), "generations": n, "seconds": round(dt, 3)}
+                if kind == "clmul_dispatch":
+                    ent["note"] = "reference as written (defective fold, SURVEY F3): timing only"
+                else:
+                    ent["matches_gpu"] = bool((got == gpu[:n]).all())
+                res[f"{kind}_r{r}_{nt}t"] = ent
+    oracle.set_pinning(False)
+    return res
+
+
+def cpu_gf_mul_loop(target_s=0.3):
+    """The reference's only published numbers (BASELINE.md section 1:
+    docs/gf_bitslice_bench.md 850-4,800 MB/s) come from this 1,024-pair
+    gf_mul micro-loop (benches/gf_bitslice_bench.rs:17-102); restated in
+    oracle/cpu_variants.c cpu_gf_mul_loop and timed here, one thread, so they
+    have a same-host counterpart.  MB/s = 1,024 products (bytes) per pass."""
+    import sys
+
+    sys.path.insert(0, str(REPO))
+    from tests import oracle_py as oracle
+
+    res = {"unit": "MB/s (10^6 products/s, one thread)", "published_mb_s": {
+        "SSE2 table": 850, "AVX2 bit-sliced": 3000, "AVX-512 bit-sliced": 4800, "scalar fallback": 750}}
+    for kind in ("table", "dispatch", "sse2", "avx512"):
+        iters, dt = 64, 0.0
+        while True:
+            t0 = time.perf_counter()
+            acc = oracle.gf_mul_loop(kind, iters)
+            dt = time.perf_counter() - t0
+            if acc < 0 or dt >= target_s or iters >= 1 << 26:
+                break
+            iters *= 4
+        res[kind] = "not available on this host" if acc < 0 else {
+            "mb_s": round(1024 * iters / dt / 1e6, 1), "passes": iters, "seconds": round(dt, 3), "acc": acc}
+    res["note"] = ("table = gf_mul_table; dispatch = gf_mul through dispatch_bitslice (the reference's gf_mul); "
+                   "sse2 / avx512 = the CLMUL-fold members called directly (defective fold, SURVEY F3)")
     return res
 
 

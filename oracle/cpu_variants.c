@@ -35,7 +35,9 @@
  * split the generations over `threads` pthreads.  Results equal
  * oracle_encode_window (checked by tests/test_oracle_golden.py).
  */
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -303,6 +305,11 @@ static void encode_clmul_dispatch_gen(const job_t *j, uint32_t g) {
 }
 #endif
 
+static int g_pin = 0;   /* cpu_set_pinning */
+
+void cpu_set_pinning(int on) { g_pin = on != 0; }
+int cpu_pinning(void) { return g_pin; }
+
 static void *worker(void *arg) {
     const job_t *j = (const job_t *)arg;
     for (uint32_t g = j->g0; g < j->g1; ++g) {
@@ -341,10 +348,26 @@ static int run(uint32_t k, uint32_t r, uint32_t L, uint32_t G, const uint8_t *sr
     if (threads > G) threads = G ? G : 1;
     pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
     job_t *jobs = (job_t *)calloc(threads, sizeof(job_t));
+    /* threads pinned, worker w to the w-th CPU this
+     * process may run on (cpu_set_pinning) */
+    cpu_set_t allowed;
+    int ncpu = 0, cpus[1024];
+    if (g_pin && sched_getaffinity(0, sizeof allowed, &allowed) == 0)
+        for (int c = 0; c < CPU_SETSIZE && ncpu < 1024; ++c)
+            if (CPU_ISSET(c, &allowed)) cpus[ncpu++] = c;
     for (uint32_t w = 0; w < threads; ++w) {
         jobs[w] = (job_t){k, r, L, (uint32_t)((uint64_t)G * w / threads),
                           (uint32_t)((uint64_t)G * (w + 1) / threads), src, rep, coeff, simd};
-        pthread_create(&th[w], NULL, worker, &jobs[w]);
+        pthread_attr_t at;
+        pthread_attr_init(&at);
+        if (ncpu) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus[w % (uint32_t)ncpu], &one);
+            pthread_attr_setaffinity_np(&at, sizeof one, &one);
+        }
+        pthread_create(&th[w], &at, worker, &jobs[w]);
+        pthread_attr_destroy(&at);
     }
     for (uint32_t w = 0; w < threads; ++w) pthread_join(th[w], NULL);
     free(th);
@@ -410,4 +433,81 @@ int cpu_encode_clmul_dispatch(uint32_t k, uint32_t r, uint32_t L, uint32_t G, co
     (void)detector_instance();
 #endif
     return run(k, r, L, G, src, rep, threads, 4);
+}
+
+/* benches/gf_bitslice_bench.rs:17-102 restated (the
+ * only published numbers of the path): a[i] = i, b[i] = 255 - i for i < 1024
+ * (as u8), acc ^= mul(a[i], b[i]), `iters` passes; every operand goes
+ * through a compiler barrier (criterion::black_box).
+ *   kind 0 "table"    gf_mul_table (gf_tables.rs:47-57)
+ *   kind 1 "dispatch" gf_mul -> dispatch_bitslice per byte (gf_tables.rs:283-300,
+ *                     optimize.rs:385-408: FeatureDetector + HashMap lookups,
+ *                     then the CLMUL member) -- the reference's own gf_mul
+ *   kind 2 "sse2"     gf_mul_bitsliced_sse2 (gf_tables.rs:129-141, one PCLMULQDQ + fold)
+ *   kind 3 "avx512"   gf_mul_bitsliced_avx512 (gf_tables.rs:76-94, VPCLMULQDQ)
+ * Kinds 1-3 compute the reference's defective fold: timing only.
+ * Returns the final acc (>= 0), or -3 when this host lacks the instructions. */
+#define BB(x) __asm__ volatile("" : "+r"(x))
+int cpu_gf_mul_loop(int kind, uint64_t iters) {
+    uint8_t a[1024], b[1024];
+    for (int i = 0; i < 1024; ++i) {
+        a[i] = (uint8_t)i;
+        b[i] = (uint8_t)(255 - i);
+    }
+    uint8_t acc = 0;
+    if (kind == 0) {
+        for (uint64_t it = 0; it < iters; ++it) {
+            for (int i = 0; i < 1024; ++i) {
+                uint8_t x = a[i], y = b[i];
+                BB(x);
+                BB(y);
+                acc ^= oracle_gf_mul(x, y);
+            }
+            BB(acc);
+        }
+        return acc;
+    }
+#if defined(__x86_64__)
+    if (!cpu_has_pclmul()) return -3;
+    if (kind == 1) {
+        (void)detector_instance();
+        for (uint64_t it = 0; it < iters; ++it) {
+            for (int i = 0; i < 1024; ++i) {
+                uint8_t x = a[i], y = b[i];
+                BB(x);
+                BB(y);
+                acc ^= gf_mul_dispatched(x, y);
+            }
+            BB(acc);
+        }
+        return acc;
+    }
+    if (kind == 2) {
+        for (uint64_t it = 0; it < iters; ++it) {
+            for (int i = 0; i < 1024; ++i) {
+                uint8_t x = a[i], y = b[i];
+                BB(x);
+                BB(y);
+                acc ^= clmul_fold(x, y);
+            }
+            BB(acc);
+        }
+        return acc;
+    }
+    if (kind == 3) {
+        (void)detector_instance();
+        if (!g_have_vpclmul) return -3;
+        for (uint64_t it = 0; it < iters; ++it) {
+            for (int i = 0; i < 1024; ++i) {
+                uint8_t x = a[i], y = b[i];
+                BB(x);
+                BB(y);
+                acc ^= clmul_fold_avx512(x, y);
+            }
+            BB(acc);
+        }
+        return acc;
+    }
+#endif
+    return -3;
 }

@@ -23,6 +23,9 @@ _lib.cpu_encode_clmul.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint3
 _lib.cpu_encode_clmul_dispatch.argtypes = [ctypes.c_uint32] * 4 + [_P, _P, ctypes.c_uint32]
 _lib.cpu_has_gfni.argtypes = []
 _lib.cpu_has_pclmul.argtypes = []
+_lib.cpu_set_pinning.argtypes = [ctypes.c_int]
+_lib.cpu_pinning.argtypes = []
+_lib.cpu_gf_mul_loop.argtypes = [ctypes.c_int, ctypes.c_uint64]
 _lib.oracle_gf_mul.restype = ctypes.c_uint8
 _lib.oracle_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
 _lib.oracle_gf_mul_shift.restype = ctypes.c_uint8
@@ -274,3 +277,18 @@ def decode16(k: int, row_index, rows: np.ndarray, row_coeffs: np.ndarray | None 
     rc = None if row_coeffs is None else np.ascontiguousarray(row_coeffs, dtype=np.uint16)
     s = _lib.oracle_decode16(k, L, n, _p(ri), _p(rows), L, _p(rc), _p(out), out.shape[1], _p(mask))
     return s, out[:, :L], mask
+
+
+GF_MUL_LOOP_KINDS = {"table": 0, "dispatch": 1, "sse2": 2, "avx512": 3}
+
+
+def gf_mul_loop(kind: str, iters: int) -> int:
+    """oracle/cpu_variants.c cpu_gf_mul_loop: the reference's 1,024-pair
+    gf_mul micro-benchmark (benches/gf_bitslice_bench.rs:17-102); returns acc
+    or -3 when the host lacks the instructions."""
+    return _lib.cpu_gf_mul_loop(GF_MUL_LOOP_KINDS[kind], iters)
+
+
+def set_pinning(on: bool) -> None:
+    """Pin cpu_encode's worker w to the w-th allowed CPU."""
+    _lib.cpu_set_pinning(1 if on else 0)
