@@ -28,7 +28,12 @@
  * A scalar projection can yield a proper divisor of A's minimal polynomial,
  * which gives a wrong "inverse"; the reference does not check.  Here the
  * solution is checked (A X == B) and the next init vector b tried, up to
- * ORACLE_W_TRIES; every try failing reports ERANK.
+ * ORACLE_W_TRIES.  A projection that misses a factor is no rank verdict (a
+ * nonsingular A can defeat every init vector), so when every try fails the
+ * system is solved by exact Gauss-Jordan elimination (*tries = TRIES + 1),
+ * and ERANK means A is singular -- as the library does (qf_wiedemann.hip).
+ * Only the x | f test (f_0 == 0) reports ERANK straight from a projection:
+ * it proves A singular.
  *
  * Efficiency choices (same results): A v uses the identity rows sparsely,
  * and sum_i f_i A^(i-1) B runs by Horner on B instead of forming powers.
@@ -90,6 +95,45 @@ static uint32_t berlekamp_massey(const uint8_t *s, uint32_t n, uint8_t *c) {
     return L;
 }
 
+/* A X = B (A: identity rows sys[q] >= 0, dense rows coef) by Gauss-Jordan on
+ * [A | B]; returns 0 iff A is singular. */
+static int exact_solve(uint32_t k, const int32_t *sys, const uint8_t *coef, const uint8_t *B, uint32_t L,
+                       uint8_t *X) {
+    const size_t w = (size_t)k + L;
+    uint8_t *T = (uint8_t *)calloc((size_t)k * w, 1), *tmp = (uint8_t *)malloc(w);
+    int ok = 1;
+    for (uint32_t q = 0; q < k; ++q) {
+        uint8_t *t = T + (size_t)q * w;
+        if (sys[q] >= 0) t[sys[q]] = 1;
+        else memcpy(t, coef + (size_t)q * k, k);
+        memcpy(t + k, B + (size_t)q * L, L);
+    }
+    for (uint32_t c = 0; c < k && ok; ++c) {
+        uint32_t p = c;
+        while (p < k && T[(size_t)p * w + c] == 0) ++p;
+        if (p == k) { ok = 0; break; }
+        if (p != c) {
+            memcpy(tmp, T + (size_t)p * w, w);
+            memcpy(T + (size_t)p * w, T + (size_t)c * w, w);
+            memcpy(T + (size_t)c * w, tmp, w);
+        }
+        uint8_t *rc = T + (size_t)c * w, iv;
+        oracle_gf_inv(rc[c], &iv);
+        for (size_t j = 0; j < w; ++j) rc[j] = oracle_gf_mul(iv, rc[j]);
+        for (uint32_t i = 0; i < k; ++i) {
+            uint8_t *ri = T + (size_t)i * w;
+            const uint8_t a = ri[c];
+            if (i == c || !a) continue;
+            for (size_t j = 0; j < w; ++j) ri[j] ^= oracle_gf_mul(a, rc[j]);
+        }
+    }
+    if (ok)
+        for (uint32_t q = 0; q < k; ++q) memcpy(X + (size_t)q * L, T + (size_t)q * w + k, L);
+    free(T);
+    free(tmp);
+    return ok;
+}
+
 int oracle_wiedemann_decode(uint32_t k, uint32_t L, uint32_t n_rows, const uint16_t *row_index,
                             const uint8_t *rows, size_t row_stride, const uint8_t *row_coeffs,
                             uint8_t *out, size_t out_stride, uint8_t *received_mask,
@@ -106,7 +150,7 @@ int oracle_wiedemann_decode(uint32_t k, uint32_t L, uint32_t n_rows, const uint1
     uint8_t *col = (uint8_t *)malloc(k), *col2 = (uint8_t *)malloc(k);
     uint8_t *v = (uint8_t *)malloc(k), *w = (uint8_t *)malloc(k), *u = (uint8_t *)malloc(k);
     uint8_t *seq = (uint8_t *)malloc(2 * (size_t)k), *cp = (uint8_t *)malloc(2 * (size_t)k + 1);
-    int status = ORACLE_OK;
+    int status = ORACLE_OK, singular = 0;
     uint32_t n = 0;
     if (tries) *tries = 0;
     /* Decoder::add_packet (decoder.rs:678-701): first k rows, duplicates dropped */
@@ -147,7 +191,7 @@ int oracle_wiedemann_decode(uint32_t k, uint32_t L, uint32_t n_rows, const uint1
         if (Ld == 0) continue;            /* zero sequence: this projection says nothing */
         /* fix (a): f_i = c_{L-i}; f_0 = c_L */
         const uint8_t f0 = cp[Ld];
-        if (f0 == 0) break;               /* x | minimal polynomial: A singular */
+        if (f0 == 0) { singular = 1; break; }   /* x | minimal polynomial: A singular */
         uint8_t f0inv;
         oracle_gf_inv(f0, &f0inv);
         /* X = f0^-1 sum_{i=1..L} f_i A^(i-1) B, Horner: Y = f_L B; Y = A Y + f_i B */
@@ -181,6 +225,10 @@ int oracle_wiedemann_decode(uint32_t k, uint32_t L, uint32_t n_rows, const uint1
         matvec(k, sys, coef, v, w);
         if (memcmp(w, u, k) != 0) ok = 0;
         if (ok) { status = ORACLE_OK; break; }
+    }
+    if (status == ORACLE_ERANK && !singular) {
+        if (tries) *tries = ORACLE_W_TRIES + 1;
+        status = exact_solve(k, sys, coef, B, L, X) ? ORACLE_OK : ORACLE_ERANK;
     }
     if (status == ORACLE_OK)
         for (uint32_t i = 0; i < k; ++i) {

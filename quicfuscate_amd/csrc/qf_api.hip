@@ -1301,7 +1301,8 @@ int qf_encode_batch_host(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, con
 
 static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
                              const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
-                             uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status);
+                             uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status,
+                             bool locked = false);
 
 int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
                     const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
@@ -1422,9 +1423,13 @@ int qf_decode_batch_host(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, con
     return first_err;
 }
 
+// locked: the caller holds ctx->mu (qf_decode_batch_desc keeps it across its
+// classes, so the offset tables it sets on the context and its metadata
+// buffers cannot change under this call)
 static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8_t* rows,
                              const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
-                             uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
+                             uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status,
+                             bool locked) {
     if (!ctx || !sh) return QF_EINVAL;
     const uint32_t k = sh->k, r = sh->r, L = sh->L, max_rows = sh->max_rows;
     if (k == 0 || k > 256 || max_rows == 0 || max_rows > 4096 || L == 0) return QF_EINVAL;
@@ -1436,7 +1441,8 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
     if (!aligned16(rows) || (sh->row_stride & 15) || (sh->rows_gen_stride & 15)) return QF_EINVAL;
     if (e_max && (!aligned16(rec) || (sh->rec_row_stride & 15) || (sh->rec_gen_stride & 15)))
         return QF_EINVAL;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    std::unique_lock<std::mutex> g(ctx->mu, std::defer_lock);
+    if (!locked) g.lock();
     int s = ensure_device(ctx);
     if (s) return s;
     if (!row_coeffs && ctx->opt[QF_OPT_BITSLICED] && r <= 16 && k + r <= 256 && qf::syn_available(k, r) &&
@@ -1703,8 +1709,10 @@ int qf_decode_batch_desc(qf_ctx* ctx, const qf_dec_desc* gens, uint32_t G, const
         cls_scratch.push_back(scratch);
         scratch += round_up((size_t)Gc * mr * 2, 256) + round_up((size_t)Gc * emax * 2, 256) + round_up((size_t)Gc * 12, 256);
     }
+    // one lock for the staging and every class: the offset tables set on the
+    // context and the metadata buffers stay this call's until it returns
+    std::lock_guard<std::mutex> lk(ctx->mu);
     {
-        std::lock_guard<std::mutex> g(ctx->mu);
         if ((s = ensure_device(ctx)) != QF_OK) return s;
         if ((s = desc_stage(ctx, round_up(meta, 256) + scratch)) != QF_OK) return s;
         uint8_t* h = ctx->h_desc;
@@ -1754,7 +1762,6 @@ int qf_decode_batch_desc(qf_ctx* ctx, const qf_dec_desc* gens, uint32_t G, const
                                                         round_up((size_t)Gc * emax * 2, 256));
         int32_t* st_ws = reinterpret_cast<int32_t*>(nrec_ws + Gc);
         {
-            std::lock_guard<std::mutex> g(ctx->mu);
             qf::DescIndexArgs ia{row_index, rio, nr, ri_ws, mr, Gc};
             QF_CHECK_HIP(qf::launch_desc_gather_index(ia, ctx->stream));
             ctx->offs_in = ro;
@@ -1763,19 +1770,18 @@ int qf_decode_batch_desc(qf_ctx* ctx, const qf_dec_desc* gens, uint32_t G, const
             for (uint32_t i : kv.second) al = al && gens[i].rows_offset % 16 == 0;
             ctx->offs_in_al16 = al;
         }
-        s = decode_batch_impl(ctx, &sh, Gc, rows, ri_ws, nr, nullptr, rec, rec_ws, nrec_ws, st_ws);
-        {
-            std::lock_guard<std::mutex> g(ctx->mu);
-            ctx->offs_in = ctx->offs_out = nullptr;
-            ctx->offs_in_al16 = false;
-            if (s != QF_OK) return s;
-            qf::DescOutArgs oa{rec_ws, nrec_ws, st_ws, cio, id, rec_index, n_rec, status, emax, Gc};
-            QF_CHECK_HIP(qf::launch_desc_scatter_out(oa, ctx->stream));
+        s = decode_batch_impl(ctx, &sh, Gc, rows, ri_ws, nr, nullptr, rec, rec_ws, nrec_ws, st_ws, true);
+        ctx->offs_in = ctx->offs_out = nullptr;
+        ctx->offs_in_al16 = false;
+        if (s != QF_OK) {
+            ctx->payload_wait = nullptr;
+            return s;
         }
+        qf::DescOutArgs oa{rec_ws, nrec_ws, st_ws, cio, id, rec_index, n_rec, status, emax, Gc};
+        QF_CHECK_HIP(qf::launch_desc_scatter_out(oa, ctx->stream));
         o += 40 * (size_t)Gc;
         ++c;
     }
-    std::lock_guard<std::mutex> g(ctx->mu);
     ctx->payload_wait = nullptr;  // as qf_decode_batch: one decode call only
     return QF_OK;
 }

@@ -69,6 +69,10 @@ struct qf_decoder {
     qf_ctx* ctx = nullptr;
     uint32_t k = 0, max_len = 0, stride = 0;
     bool decoded = false, drained = false;
+    // a decode attempt failed on the device (not a singular system): the
+    // next add on this decoder re-uploads the k rows from the pinned host
+    // copy and tries again, instead of the generation staying undecodable
+    bool retry = false;
     // accepted rows, in arrival order (the first k win)
     uint8_t* rows = nullptr;     // k * stride, pinned: each row is uploaded as it arrives
     std::vector<uint32_t> lens;    // k
@@ -590,13 +594,19 @@ int qf_decoder_add_packet(qf_decoder* d, uint64_t id, int is_systematic, const u
                           uint32_t len, const uint8_t* coeffs, uint32_t coeff_len) {
     int32_t q = -1;
     const int s = decoder_accept(d, id, is_systematic, data, len, coeffs, coeff_len, &q);
-    if (s != 0 || q < 0) return s;
+    const bool again = s == 0 && q < 0 && d->retry && !d->decoded && d->accepted == d->k;
+    if ((s != 0 || q < 0) && !again) return s;
     // the row stays in the pinned host rows until the generation decodes:
     // one upload of all k rows then, instead of a copy per packet
     if (d->accepted == d->k) {
+        d->retry = false;
         int e = decoder_try_decode(d);
         if (e == QF_ERANK) return 0;
-        if (e != QF_OK) return e;
+        if (e != QF_OK) {
+            d->retry = true;
+            d->uploaded = 0;
+            return e;
+        }
     }
     return d->decoded ? 1 : 0;
 }
@@ -903,20 +913,54 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
     };
     std::vector<Up> up;
     std::vector<uint32_t> done;          // packets whose decoder now holds k rows
+    // a failure before the decodes: the rows of this call's packets are on
+    // the host only, so every decoder touched re-uploads all its rows on its
+    // next add, and one that holds k rows decodes then
+    auto abandon = [&](int err) {
+        for (const Up& u : up) {
+            qf_decoder* d = v[u.m].d;
+            d->uploaded = 0;
+            if (d->accepted == d->k && !d->decoded) d->retry = true;
+        }
+        for (uint32_t m : done) {
+            v[m].d->uploaded = 0;
+            v[m].d->retry = true;
+            v[m].result = err;
+        }
+    };
     size_t pk = 0;
     for (uint32_t m = 0; m < M; ++m) {
         DecAdd& x = v[m];
         int32_t q = -1;
         const uint32_t before = x.d->uploaded;
         x.result = decoder_accept(x.d, x.id, x.is_systematic, x.data, x.len, x.coeffs, x.coeff_len, &q);
-        if (q < 0) continue;
+        if (q < 0) {
+            // a decoder whose last decode failed on the device: its rows go up
+            // again (pinned host copy) and it decodes with this batch
+            qf_decoder* d = x.d;
+            if (x.result == 0 && d->retry && !d->decoded && d->accepted == d->k) {
+                d->retry = false;
+                if (int us = decoder_upload(d)) {
+                    d->retry = true;
+                    x.result = us;
+                    continue;
+                }
+                done.push_back(m);
+            }
+            continue;
+        }
         // rows a per-packet add left on the host go up first (stream order)
         if (before < (uint32_t)q) {
             const uint32_t acc = x.d->accepted;
             x.d->accepted = (uint32_t)q;
             const int us = decoder_upload(x.d);
             x.d->accepted = acc;
-            if (us) return us;
+            if (us) {
+                x.d->uploaded = 0;
+                if (x.d->accepted == x.d->k) x.d->retry = true;
+                abandon(us);
+                return us;
+            }
         }
         x.d->uploaded = (uint32_t)q + 1;   // the scatter below writes slot q
         up.push_back({m, (uint32_t)q});
@@ -929,7 +973,8 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
     size_t ri_n = 0, ri_pad = 0, rec_rows = 0, rec_idx = 0;
     for (size_t t = 0; t < done.size(); ++t) {
         decoder_plan(v[done[t]].d, &plans[t]);
-        if (plans[t].cauchy) {
+        // (k > 256: the Wiedemann strategy, per generation, whatever the rows)
+        if (plans[t].cauchy && v[done[t]].d->k <= 256) {
             cau.push_back((uint32_t)t);
             const qf_decoder* d = v[done[t]].d;
             ri_n += d->k;
@@ -949,7 +994,10 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
     const size_t total = o_rec + rec_rows;
     uint8_t *h = nullptr, *dv = nullptr;
     int s = ctx_recv_buffers(ctx, total, &h, &dv);
-    if (s != QF_OK) return s;
+    if (s != QF_OK) {
+        abandon(s);
+        return s;
+    }
     hipStream_t st = ctx_stream(ctx);
     RingSlot* hs = reinterpret_cast<RingSlot*>(h + o_slots);
     size_t off = 0;
@@ -994,18 +1042,38 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
         ci_o += std::min(d->k, pl.rc);
         rr_o += (size_t)std::min(d->k, pl.rc) * d->stride;
     }
-    if (o_pk + pk) QF_CHECK_HIP(hipMemcpyAsync(dv, h, o_pk + pk, hipMemcpyHostToDevice, st));
-    QF_CHECK_HIP(launch_ring_scatter(dv, reinterpret_cast<const RingSlot*>(dv + o_slots), (uint32_t)n_up, st));
+    if ((o_pk + pk && hipMemcpyAsync(dv, h, o_pk + pk, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        launch_ring_scatter(dv, reinterpret_cast<const RingSlot*>(dv + o_slots), (uint32_t)n_up, st) != hipSuccess) {
+        abandon(QF_EDEVICE);
+        ctx_recv_release(ctx);
+        return QF_EDEVICE;
+    }
+    // a failed batch decode: every connection whose generation was in it gets
+    // the error as its status, and its decoder retries on its next packet
+    // (rows re-uploaded from the pinned host copy); the call goes on with
+    // the explicit-coefficient generations
+    auto fail_cauchy = [&](int err) {
+        for (size_t c = 0; c < G; ++c) {
+            DecAdd& x = v[done[cau[c]]];
+            x.result = err;
+            x.d->retry = true;
+            x.d->uploaded = 0;
+        }
+    };
+    bool failed = false;
     if (G) {
         s = qf_decode_batch_desc(ctx, descs.data(), (uint32_t)G, rows_base, reinterpret_cast<const uint16_t*>(dv + o_ri),
                                  dv + o_rec, reinterpret_cast<uint16_t*>(dv + o_ci),
                                  reinterpret_cast<uint32_t*>(dv + o_nrec), reinterpret_cast<int32_t*>(dv + o_st));
+        if (s == QF_OK && (hipMemcpyAsync(h + o_out, dv + o_out, total - o_out, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                           hipStreamSynchronize(st) != hipSuccess))
+            s = QF_EDEVICE;
         if (s != QF_OK) {
-            ctx_recv_release(ctx);
-            return s;
+            fail_cauchy(s);
+            failed = true;
         }
-        QF_CHECK_HIP(hipMemcpyAsync(h + o_out, dv + o_out, total - o_out, hipMemcpyDeviceToHost, st));
-        QF_CHECK_HIP(hipStreamSynchronize(st));
+    }
+    if (G && !failed) {
         const uint32_t* nrec = reinterpret_cast<const uint32_t*>(h + o_nrec);
         const int32_t* stt = reinterpret_cast<const int32_t*>(h + o_st);
         for (size_t c = 0; c < G; ++c) {
@@ -1025,6 +1093,10 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
     for (uint32_t t : expl) {
         DecAdd& x = v[done[t]];
         const int e = decoder_try_decode(x.d);
+        if (e != QF_OK && e != QF_ERANK) {
+            x.d->retry = true;
+            x.d->uploaded = 0;
+        }
         x.result = e == QF_ERANK ? 0 : (e != QF_OK ? e : (x.d->decoded ? 1 : 0));
     }
     return QF_OK;

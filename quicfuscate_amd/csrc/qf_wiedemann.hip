@@ -21,7 +21,9 @@
 //                  the check M W == I (the reference does not check: a
 //                  projection whose sequence misses a factor of M's minimal
 //                  polynomial gives a wrong W, so the host tries the next init
-//                  vector b); and G = W A_J;
+//                  vector b, and after kTries of them inverts M exactly on the
+//                  host -- a failed projection is not a rank verdict); and
+//                  G = W A_J;
 //   k_w8_apply     recovered rows = D . rows (decoder.rs:886-887) with
 //                  D[t][q] = W[t][p] on repair slot q (ordinal p) and G[t][s]
 //                  on the systematic slot of source s, split over slot chunks
@@ -31,6 +33,7 @@
 // (tables built in LDS, M kept as logs); the others use the context's split
 // tables (v_perm).
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -425,6 +428,78 @@ __global__ void __launch_bounds__(256) k_w8_apply(ApplyArgs a) {
 
 static inline uint32_t r16(uint32_t x) { return (x + 15) & ~15u; }
 
+// dst ^= c * src over n bytes (n % 16 == 0): nibble tables, 16 lookups per pshufb
+__attribute__((target("ssse3"))) static void row_axpy(uint8_t* dst, const uint8_t* src, uint8_t c, size_t n) {
+    const Gf256& f = gf();
+    alignas(16) uint8_t lo[16], hi[16];
+    for (int v = 0; v < 16; ++v) {
+        lo[v] = f.mul(c, (uint8_t)v);
+        hi[v] = f.mul(c, (uint8_t)(v << 4));
+    }
+    const __m128i tl = _mm_load_si128(reinterpret_cast<const __m128i*>(lo));
+    const __m128i th = _mm_load_si128(reinterpret_cast<const __m128i*>(hi));
+    const __m128i m = _mm_set1_epi8(0x0f);
+    for (size_t i = 0; i < n; i += 16) {
+        const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i p = _mm_xor_si128(_mm_shuffle_epi8(tl, _mm_and_si128(x, m)),
+                                        _mm_shuffle_epi8(th, _mm_and_si128(_mm_srli_epi16(x, 4), m)));
+        __m128i* d = reinterpret_cast<__m128i*>(dst + i);
+        _mm_storeu_si128(d, _mm_xor_si128(_mm_loadu_si128(d), p));
+    }
+}
+
+// The exact fallback when no init vector verifies (every projection missed a
+// factor of M's minimal polynomial -- possible for a nonsingular M, so it is
+// not a rank verdict): Gauss-Jordan on [M | I] on the host, W = M^-1 with row
+// stride ep.  Returns false iff M is singular.  O(e^3 / 16) pshufb steps.
+static bool exact_inverse(const uint8_t* A_ek, uint32_t k, const uint16_t* E, uint32_t e, uint32_t ep,
+                          std::vector<uint8_t>& W) {
+    const Gf256& f = gf();
+    const size_t w2 = 2 * (size_t)ep;
+    std::vector<uint8_t> T((size_t)e * w2, 0);
+    for (uint32_t i = 0; i < e; ++i) {
+        for (uint32_t j = 0; j < e; ++j) T[(size_t)i * w2 + j] = A_ek[(size_t)i * k + E[j]];
+        T[(size_t)i * w2 + ep + i] = 1;
+    }
+    for (uint32_t c = 0; c < e; ++c) {
+        uint32_t p = c;
+        while (p < e && T[(size_t)p * w2 + c] == 0) ++p;
+        if (p == e) return false;
+        if (p != c) std::swap_ranges(&T[(size_t)p * w2], &T[(size_t)p * w2] + w2, &T[(size_t)c * w2]);
+        uint8_t* rc = &T[(size_t)c * w2];
+        uint8_t iv = 0;
+        f.inv(rc[c], &iv);
+        if (iv != 1) {
+            for (size_t j = 0; j < w2; ++j) rc[j] = f.mul(iv, rc[j]);
+        }
+        for (uint32_t i = 0; i < e; ++i) {
+            const uint8_t a = T[(size_t)i * w2 + c];
+            if (i != c && a) row_axpy(&T[(size_t)i * w2], rc, a, w2);
+        }
+    }
+    W.assign((size_t)e * ep, 0);
+    for (uint32_t i = 0; i < e; ++i) memcpy(&W[(size_t)i * ep], &T[(size_t)i * w2 + ep], e);
+    return true;
+}
+
+// hipFuncSetAttribute for the sequence kernel's 160 KB of LDS, once per
+// device (the attribute is per device; a failure is remembered and returned)
+static hipError_t seq_lds_attribute() {
+    static std::mutex mu;
+    static hipError_t state[64];
+    static bool set[64] = {};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(mu);
+    if (!set[dev]) {
+        state[dev] = hipFuncSetAttribute(reinterpret_cast<const void*>(k_w8_sequence),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        set[dev] = true;
+    }
+    return state[dev];
+}
+
 hipError_t launch_rows(const RowsArgs& a, uint32_t rows, hipStream_t st) {
     const size_t lds = a.scale ? 0 : (size_t)a.n;
     hipLaunchKernelGGL(k_w8_rows, dim3(rows, (a.words + 63) / 64), dim3(256), lds, st, a);
@@ -474,15 +549,7 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     size_t seq_lds = kEx2 + 512 + 64 + kRed2Bytes + 4 * (size_t)e + 2 * (size_t)e + 2 * (size_t)e + 3 * (2 * (size_t)e + 1);
     const uint32_t lm_lds = seq_lds + 2 * (size_t)e * e <= 144 * 1024;   // logs of M in LDS up to e = 262
     if (lm_lds) seq_lds += 2 * (size_t)e * e;
-    if (seq_lds > 64 * 1024) {
-        static std::once_flag once;
-        hipError_t err = hipSuccess;
-        std::call_once(once, [&] {
-            err = hipFuncSetAttribute(reinterpret_cast<const void*>(k_w8_sequence),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        });
-        QF_CHECK_HIP(err);
-    }
+    if (seq_lds > 64 * 1024) QF_CHECK_HIP(seq_lds_attribute());
     // about 8 threads per row of M for the Krylov products (1 wave at e <= 8)
     const uint32_t seq_threads = std::min<uint32_t>(kSeqThreads, (8 * e + 63) / 64 * 64);
     const auto& f = gf();
@@ -582,7 +649,15 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
         if (!bad) break;
         W = nullptr;
     }
-    if (!W) return QF_ERANK;
+    std::vector<uint8_t> hW;
+    if (!W) {
+        // no projection verified: exact elimination decides (tries = kTries + 1)
+        if (tries_out) *tries_out = kTries + 1;
+        if (!exact_inverse(A_ek, k, E, e, ep, hW)) return QF_ERANK;
+        W = w + oP1;
+        QF_CHECK_HIP(hipMemcpyAsync(W, hW.data(), hW.size(), hipMemcpyHostToDevice, st));
+        QF_CHECK_HIP(hipStreamSynchronize(st));   // (hW is pageable and local)
+    }
     // G = W A_J (e x k), then the payload pass
     RowsArgs g{W, w + oA, w + oG, tab, ep, kp, kp, e, (k + 3) / 4, 0, 0, nullptr};
     QF_CHECK_HIP(launch_rows(g, e, st));

@@ -179,3 +179,37 @@ def test_received_ids_kept(qf, gpu_ctx):
     assert dec.is_decoded
     out = dec.get_decoded_packets()
     assert [p.id for p in out] == [i if i in lost else ids[i] for i in range(k)]
+
+
+@pytest.mark.parametrize("k,lost_n", [(300, 300), (400, 40)])
+def test_wiedemann_exact_fallback(qf, oracle, gpu_ctx, k, lost_n):
+    """No init vector verifies (qf_wiedemann.hip's exact fallback): M on the
+    erased block is diag(c), c = 7 on positions {0, 1, 16, 17} of E and 11
+    elsewhere -- the init vectors XOR to zero over those positions for every
+    b < 8, so no projection sees the eigenvalue 7.  M is nonsingular, so the
+    generation decodes (exact elimination on the host), as in the oracle; the
+    received columns carry random coefficients."""
+    rng = np.random.default_rng(k)
+    L = 40
+    src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    E = sorted(rng.choice(k, lost_n, replace=False).tolist()) if lost_n < k else list(range(k))
+    lost = set(E)
+    coef = np.zeros((lost_n, k), np.uint8)
+    recv = [i for i in range(k) if i not in lost]
+    if recv:
+        coef[:, recv] = rng.integers(0, 256, (lost_n, len(recv)), dtype=np.uint8)
+    for p, col in enumerate(E):
+        coef[p, col] = 7 if p in (0, 1, 16, 17) else 11
+    dec = qf.Decoder(k, max_len=L)
+    res, rep = _feed(qf, dec, k, src, lost, coef)
+    assert dec.is_decoded and res[-1]
+    got = np.stack([np.frombuffer(p.payload(), np.uint8) for p in dec.get_decoded_packets()])
+    assert (got == src).all()
+    idx, rows, rc = _oracle_rows(k, src, lost, coef, rep)
+    s, want, _, _ = oracle.wiedemann(k, idx, rows, rc)
+    assert s == oracle.OK and (want == got).all()
+    # a zero on M's diagonal: singular, stays undecoded
+    coef[3, E[3]] = 0
+    dec = qf.Decoder(k, max_len=L)
+    _feed(qf, dec, k, src, lost, coef)
+    assert not dec.is_decoded

@@ -102,3 +102,36 @@ def test_wiedemann_duplicates_and_no_loss():
     src, lost, idx, rows, rc = _case(rng, k, 0, L)
     s, out, mask, _ = oracle.wiedemann(k, idx, rows, rc)
     assert s == oracle.OK and (out == src).all() and mask.all()
+
+
+def _diag_case(k, L, seed, zero_at=None):
+    """Every source lost, repair p = c_p * source p: A = diag(c).  c_p = 7 on
+    rows {0, 1, 16, 17} and 11 elsewhere: the init vectors u_i = (i + b + 1)
+    % 255 XOR to zero over {0, 1, 16, 17} for every b < 8, so no projection
+    sees the eigenvalue 7 and every try fails verification (or is a zero
+    sequence) although A is nonsingular."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    c = np.full(k, 11, np.uint8)
+    c[[0, 1, 16, 17]] = 7
+    if zero_at is not None:
+        c[zero_at] = 0
+    rc = np.zeros((k, k), np.uint8)
+    rc[np.arange(k), np.arange(k)] = c
+    rows = oracle.encode(src, k, rc)
+    return src, [k + p for p in range(k)], rows, rc
+
+
+def test_wiedemann_exact_fallback():
+    """qf_oracle_wiedemann.c: when no init vector verifies, exact elimination
+    decides -- a nonsingular system decodes (tries = 9), a singular one is
+    ERANK.  (The reference returns its unchecked W here; parity with it is
+    the decoded sources, which are unique.)"""
+    for k in (20, 64):
+        src, idx, rows, rc = _diag_case(k, 24, k)
+        s, out, mask, tries = oracle.wiedemann(k, idx, rows, rc)
+        assert s == oracle.OK and tries == 9
+        assert (out == src).all() and not mask.any()
+    src, idx, rows, rc = _diag_case(20, 24, 3, zero_at=5)
+    s, _, _, _ = oracle.wiedemann(20, idx, rows, rc)
+    assert s == oracle.ERANK
