@@ -26,7 +26,7 @@ OUT_DIR = PKG / "lib"
 LIB = OUT_DIR / "libqf_fec.so"
 LIB_ROCM = OUT_DIR / "libqf_fec_rocm.so"
 SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip", "qf_bs.hip", "qf_adaptive.hip", "qf_wire.hip",
-           "qf_gf16.hip", "qf_objects16.hip", "qf_wiedemann.hip"]
+           "qf_gf16.hip", "qf_objects16.hip", "qf_wiedemann.hip", "qf_gf16_bs.hip"]
 # (k, r) Cauchy configurations that get a bit-sliced assembly kernel
 # (bs_codegen.py); every other shape runs the general v_perm kernel.
 BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1), (32, 5), (48, 8), (96, 15)]
@@ -108,6 +108,19 @@ def _check_no_scratch(remarks: str) -> dict[str, dict[str, int]]:
     if bad:
         raise RuntimeError(f"register spill in asm-pipelined kernels (unsafe): {bad}")
     return usage
+
+
+def _check_gf16_bs(remarks: str) -> None:
+    """The generated GF(2^16) kernels must keep their accumulators in
+    registers: spilling them in the row loop would cost more than the kernel
+    saves (gf16_codegen.py).  A few spilled VGPRs (k = 64: 8, the output
+    pointers, stored once before the rows and reloaded for the stores) are
+    allowed."""
+    usage = _check_no_scratch(remarks)
+    bad = {n: u for n, u in usage.items() if "gf16bs" in n and u.get("VGPRs", 0) > 256}
+    spills = re.findall(r"VGPRs Spill: (\d+)", remarks)
+    if bad or any(int(x) > 16 for x in spills):
+        raise RuntimeError(f"gf16 bit-sliced kernels spill VGPRs: {bad or spills}")
 
 
 def assemble(name: str, asm_text: str, out_dir: Path) -> Path:
@@ -197,16 +210,25 @@ def build(verbose: bool = False) -> Path:
     build_dir.mkdir(exist_ok=True)
     OUT_DIR.mkdir(exist_ok=True)
     _bs_kernels(build_dir)
+    # bit-sliced GF(2^16) Cauchy encode kernels (HIP C++, gf16_codegen.py)
+    from . import gf16_codegen
+    inc16 = build_dir / "qf_gf16_bs.inc"
+    text16 = gf16_codegen.generate_all()
+    if not inc16.exists() or inc16.read_text() != text16:
+        inc16.write_text(text16)
     with cf.ThreadPoolExecutor(max_workers=4) as ex:
         futs = {
             s: ex.submit(_compile, s, build_dir,
-                         ["-Rpass-analysis=kernel-resource-usage"] if s == "qf_kernels.hip" else [])
+                         ["-Rpass-analysis=kernel-resource-usage"] if s in ("qf_kernels.hip", "qf_gf16_bs.hip")
+                         else [])
             for s in SOURCES
         }
         objs = []
         for s in SOURCES:
             obj, err = futs[s].result()
             objs.append(obj)
+            if s == "qf_gf16_bs.hip":
+                _check_gf16_bs(err)
             if s == "qf_kernels.hip":
                 usage = _check_no_scratch(err)
                 if verbose:

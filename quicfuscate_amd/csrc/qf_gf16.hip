@@ -1052,6 +1052,14 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
     std::unique_lock<std::mutex> lk;
     int s = qf::ctx_lock(ctx, lk);
     if (s) return s;
+    hipStream_t st = qf::ctx_stream(ctx);
+    // the reference's fixed Cauchy rows over an unrotated window: the
+    // bit-sliced kernel of (k, r) if one is generated (qf_gf16_bs.hip)
+    if (!coeff_rxk && !first && !rot && !coeff_be_dev && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED)) {
+        s = qf::gf16_bs_encode(ctx, st, k, r, L, G, src, sh->src_gen_stride, sh->src_row_stride, rep,
+                               sh->rep_gen_stride, sh->rep_row_stride);
+        if (s != qf::kGf16BsNone) return s;
+    }
     const uint16_t *glog, *gexp;
     s = qf::ctx_gf16_tables(ctx, &glog, &gexp);
     if (s) return s;
@@ -1059,7 +1067,6 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
     uint8_t* w;
     s = qf::ctx_work(ctx, cb + ab, &w);
     if (s) return s;
-    hipStream_t st = qf::ctx_stream(ctx);
     if (coeff_rxk) {
         // coefficient logs (host tables: the same field); the upload reads
         // host memory, so the call finishes before returning
