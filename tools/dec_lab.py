@@ -36,6 +36,21 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 3k: persistent grids (cap = 2 blocks of 4 waves per CU, every wave
+    # loops over items) with the second residency half started late (stagger:
+    # workgroups 256..511 sleep iters x 3.4 us), to separate phase alignment
+    # from the persistent loop itself
+    ("p_warm", dict(LIB_DEC), ()),
+    ("p_lib", dict(LIB_DEC), ()),
+    ("p_cap2", {**LIB_DEC, "cap": 512}, ()),
+    ("p_cap2_st5", {**LIB_DEC, "cap": 512, "stagger": (256, 256, 5)}, ()),
+    ("p_cap2_st9", {**LIB_DEC, "cap": 512, "stagger": (256, 256, 9)}, ()),
+    ("p_cap2_st14", {**LIB_DEC, "cap": 512, "stagger": (256, 256, 14)}, ()),
+    ("p_nolu_cap2", {**LIB_DEC, "cap": 512, "lu": False}, ()),
+    ("p_nolu", {**LIB_DEC, "lu": False}, ()),
+    ("p_lib_2", dict(LIB_DEC), ()),
+]
+VARIANTS_R03F = [
     # round 3f: recovered rows stored as back-substitution finishes them
     ("f_warm", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
     ("f_def", {"chunked": True, "fft": 8, "pd": 2, **D}, ()),
