@@ -75,19 +75,51 @@ __device__ __forceinline__ void gf16bs_masks(uint32_t (&tm)[4]) {
     asm volatile("v_mov_b32 %0, %1" : "=v"(tm[3]) : "s"(0x00FF00FFu));
 }
 
-// stage i of the involution swaps row bit i with column bit i (gf16_codegen.transpose16)
-__device__ __forceinline__ void gf16bs_transpose(uint32_t (&x)[16], const uint32_t (&tm)[4]) {
+// The bit-plane operations as v_bitop3 intrinsics: the compiler allocates
+// registers, schedules and checks hazards, but does not split, merge or
+// reassociate them (from plain C expressions it produced 40 % more
+// instructions, and opaque inline asm made it pad them with s_nop).
+__device__ __forceinline__ uint32_t bs_bfi(uint32_t m, uint32_t x, uint32_t y) {   // (x & m) | (y & ~m)
+    return __builtin_amdgcn_bitop3_b32(m, x, y, 0xca);
+}
+
+// a ^ b ^ c (gfx950 has no v_xor3_b32: v_bitop3 0x96)
+__device__ __forceinline__ uint32_t bs_xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t bs_xor(uint32_t a, uint32_t b) { return a ^ b; }
+
+template <int S>
+__device__ __forceinline__ uint32_t bs_shl(uint32_t a) {
+    return a << S;
+}
+
+template <int S>
+__device__ __forceinline__ uint32_t bs_shr(uint32_t a) {
+    return a >> S;
+}
+
+// stage i of the involution swaps row bit i with column bit i
+// (gf16_codegen.transpose16): per pair 2 shifts + 2 bit-selects (v_bitop3
+// 0xca with the mask in a VGPR: full rate)
+template <int I>
+__device__ __forceinline__ void gf16bs_stage(uint32_t (&x)[16], uint32_t m) {
+    constexpr int s = 1 << I;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int s = 1 << i;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (r & s) continue;
-            const uint32_t a = x[r], b = x[r + s];
-            x[r] = (a & tm[i]) | ((b << s) & ~tm[i]);
-            x[r + s] = (b & ~tm[i]) | ((a >> s) & tm[i]);
-        }
+    for (int r = 0; r < 16; ++r) {
+        if (r & s) continue;
+        const uint32_t a = x[r], b = x[r + s];
+        x[r] = bs_bfi(m, a, bs_shl<s>(b));
+        x[r + s] = bs_bfi(m, bs_shr<s>(a), b);
     }
+}
+
+__device__ __forceinline__ void gf16bs_transpose(uint32_t (&x)[16], const uint32_t (&tm)[4]) {
+    gf16bs_stage<0>(x, tm[0]);
+    gf16bs_stage<1>(x, tm[1]);
+    gf16bs_stage<2>(x, tm[2]);
+    gf16bs_stage<3>(x, tm[3]);
 }
 
 __device__ __forceinline__ void gf16bs_load_row(const Gf16BsArgs& a, const Gf16BsLane& ln, uint32_t i,

@@ -180,13 +180,32 @@ def _combo_stmts(needed: set[tuple[int, int]]) -> list[str]:
         a = get(g, idx ^ hi)
         b = get(g, hi)
         name = f"c{g}_{idx}"
-        stmts.append(f"const uint32_t {name} = {a} ^ {b};")
+        stmts.append(f"const uint32_t {name} = bs_xor({a}, {b});")
         have[(g, idx)] = name
         return name
 
     for g, idx in sorted(needed):
         get(g, idx)
     return stmts, have
+
+
+def _acc_stmt(acc: str, ops: list[str], init: bool) -> str:
+    """acc (^)= XOR of ops with explicit v_xor3 / v_xor (opaque to the
+    compiler: no reassociation, no re-splitting)."""
+    if init:
+        if not ops:
+            return f"{acc} = 0u;"
+        if len(ops) == 1:
+            return f"{acc} = {ops[0]};"
+        if len(ops) == 2:
+            return f"{acc} = bs_xor({ops[0]}, {ops[1]});"
+        return f"{acc} = bs_xor3({ops[0]}, {ops[1]}, {ops[2]});" + (
+            f" {acc} = bs_xor({acc}, {ops[3]});" if len(ops) == 4 else "")
+    if not ops:
+        return ""
+    if len(ops) == 1:
+        return f"{acc} = bs_xor({acc}, {ops[0]});"
+    return f"{acc} = bs_xor3({acc}, {ops[0]}, {ops[1]});"
 
 
 def kernel_name(k: int, r: int) -> str:
@@ -232,11 +251,7 @@ def generate(k: int, r: int) -> str:
                 for jj in range(nj):
                     for b in range(16):
                         ops = [have[t] for t in T[i][jj][b] if t[0] in gs]
-                        if i == 0 and half == 0:
-                            rhs = " ^ ".join(ops) if ops else "0u"
-                            lines.append(f"                a{jj}_{b} = {rhs};")
-                        elif ops:
-                            lines.append(f"                a{jj}_{b} ^= {' ^ '.join(ops)};")
+                        lines.append("                " + _acc_stmt(f"a{jj}_{b}", ops, i == 0 and half == 0))
                 lines.append("            }")
             # the accumulators through an empty asm: XOR chains are not
             # reassociated across rows (that would keep many rows' combinations
