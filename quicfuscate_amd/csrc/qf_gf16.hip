@@ -751,6 +751,53 @@ __global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs A) {
     }
 }
 
+// Maps of the bit-sliced syndrome kernel (qf_gf16_bs.hip), one block per
+// generation of the chunk: smap[i] = slot of received source i (0xFFFF: not
+// received), rpos[j] / rslot[j] = position in J and slot of the accepted
+// repair k + j.  skip = the kernel leaves the generation alone: failed,
+// nothing erased, or a repair it has no Cauchy row for (index >= k + r, or
+// the same repair twice); nout_fb = e for the last kind, which the general
+// syndrome matvec then computes.
+__global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint16_t* smap, uint16_t* rpos,
+                                                     uint16_t* rslot, uint32_t* skip, uint32_t* nout_fb) {
+    const uint32_t g = blockIdx.z, tid = threadIdx.x;
+    const BigArgs a = view(A, g);
+    const uint32_t k = a.k;
+    __shared__ uint32_t cnt[64];
+    __shared__ uint32_t s_bad;
+    uint16_t* sm = smap + (uint64_t)g * k;
+    uint16_t* rp = rpos + (uint64_t)g * r;
+    uint16_t* rsl = rslot + (uint64_t)g * r;
+    const bool ok = *a.status == QF_OK;
+    const uint32_t e = ok ? a.w.st->e : 0, nin = ok ? a.w.st->nin : 0;
+    for (uint32_t i = tid; i < k; i += 64) sm[i] = 0xFFFF;
+    for (uint32_t j = tid; j < r; j += 64) {
+        rp[j] = 0xFFFF;
+        rsl[j] = 0;
+    }
+    cnt[tid] = 0;
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    for (uint32_t c = tid; c < nin; c += 64) sm[a.w.Scol[c]] = a.w.Sslot[c];   // columns distinct (else ERANK)
+    for (uint32_t q = tid; q < e; q += 64) {
+        const uint32_t j = (uint32_t)a.w.J[q] - k;
+        if (j < r) {
+            atomicAdd(&cnt[j], 1u);
+            rp[j] = (uint16_t)q;
+            rsl[j] = a.w.Jslot[q];
+        } else {
+            s_bad = 1;
+        }
+    }
+    __syncthreads();
+    if (tid < r && cnt[tid] > 1) s_bad = 1;
+    __syncthreads();
+    if (tid == 0) {
+        skip[g] = (!ok || e == 0 || s_bad) ? 1u : 0u;
+        nout_fb[g] = (ok && s_bad) ? e : 0u;
+    }
+}
+
 // mlog[a][c] = log C[J_a][Scol c] (syndromes: rows_J ^ C[J,S] x_S)
 __global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs A) {
     const BigArgs a = view(A, blockIdx.z);
@@ -966,7 +1013,7 @@ size_t matvec_acc_bytes(qf_ctx* ctx, uint64_t G, uint32_t nout, uint32_t nin, ui
 // e_g instead of e_max: a window decode with e = 512 of e_max = 1,024 ran
 // three quarters of its lanes idle at the e_max shape.
 int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const char* name, uint8_t* acc = nullptr,
-                  size_t acc_bytes = 0) {
+                  size_t acc_bytes = 0, bool logify_ok = true) {
     if (!a.nin_gs) a.nin_gs = 1;
     a.Lu = (a.L + 15) / 16;
     a.nob = (a.nout + kR16 - 1) / kR16;
@@ -998,7 +1045,7 @@ int launch_matvec(qf_ctx* ctx, hipStream_t st, Mv16Args& a, uint64_t G, const ch
     {
         const uint32_t min_blocks = (uint32_t)qf::ctx_opt(ctx, QF_OPT_GF16_LOGIFY_MIN_BLOCKS);
         const uint64_t n = G * a.nin * a.Lu;
-        if (qf::ctx_opt(ctx, QF_OPT_GF16_LOGIFY) && (a.nob >= min_blocks || n >= kLogifyUnits)) {
+        if (logify_ok && qf::ctx_opt(ctx, QF_OPT_GF16_LOGIFY) && (a.nob >= min_blocks || n >= kLogifyUnits)) {
             uint8_t* lr = nullptr;
             int s = qf::ctx_gf16_logrows(ctx, n * 16, &lr);
             if (s) return s;
@@ -1178,24 +1225,33 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     // form (Cauchy rows) or by Gauss-Jordan in the workspace
     const size_t Lp = ((size_t)L + 15) / 16 * 16;
     const uint64_t em = e_max;
-    const size_t per_gen[13] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
-                                row_coeffs ? 4 * em * em : 0, 4 * em, 4 * em, 16 * em, Lp * em};
+    // Cauchy rows of a (k, r) with a generated bit-sliced kernel: syndromes
+    // from qf_gf16bs_syn_* (maps 13..17, zero row), the general matvec only
+    // for the generations it skips
+    const bool bs = !row_coeffs && r <= 64 && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED) && qf::gf16_bs_has(k, r);
+    const size_t per_gen[18] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
+                                row_coeffs ? 4 * em * em : 0, 4 * em, 4 * em, 16 * em, Lp * em,
+                                bs ? 2ull * k : 0, bs ? 2ull * r : 0, bs ? 2ull * r : 0, bs ? 4u : 0u, bs ? 4u : 0u};
     size_t gen_bytes = 0;
-    for (int q = 0; q < 13; ++q) gen_bytes += per_gen[q];
+    for (int q = 0; q < 18; ++q) gen_bytes += per_gen[q];
     // chunk: <= 65535 generations (grid z) and about 1 GiB of workspace
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)G, 65535ull,
                                                                              (1ull << 30) / gen_bytes}));
-    size_t off[14], tot = 0;
-    for (int q = 0; q < 13; ++q) {
+    size_t off[20], tot = 0;
+    for (int q = 0; q < 18; ++q) {
         off[q] = tot;
         tot += align256(std::max<size_t>(per_gen[q] * chunk, 1));
     }
     const size_t acc_bytes = std::max(matvec_acc_bytes(ctx, chunk, e_max, k, L),
                                       matvec_acc_bytes(ctx, chunk, e_max, e_max, L));
-    off[13] = tot;
+    off[18] = tot;
     tot += align256(std::max<size_t>(acc_bytes, 1));
+    const size_t zero_bytes = bs ? align256(64 * ((((size_t)L + 15) / 16 + 3) / 4) + 64) : 0;
+    off[19] = tot;
+    tot += zero_bytes;
     s = qf::ctx_work(ctx, tot, &w);
     if (s) return s;
+    if (bs) QF_HIP(hipMemsetAsync(w + off[19], 0, zero_bytes, st));
     BigArgs b{};
     b.w.st = reinterpret_cast<Dec16State*>(w + off[0]);
     b.w.J = reinterpret_cast<uint16_t*>(w + off[1]);
@@ -1216,7 +1272,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     b.e_max = e_max;
     b.n_rows = max_rows;
     b.Lp = Lp;
-    uint8_t* acc = acc_bytes ? w + off[13] : nullptr;
+    uint8_t* acc = acc_bytes ? w + off[18] : nullptr;
     const int cus = qf::ctx_num_cus(ctx);
     const uint32_t mgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((em * k + 255) / 256, 8ull * cus / 1));
     const uint32_t dgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((em * em + 255) / 256, 8ull * cus));
@@ -1254,6 +1310,20 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         QF_HIP(hipGetLastError());
         qf::ctx_prof_end(ctx, st, ev, "k_dec16_prepare_large");
         // syndromes s_a = row(J_a) ^ C[J_a, S] x_S
+        uint32_t* nout_fb = nullptr;
+        if (bs) {
+            uint16_t* smap = reinterpret_cast<uint16_t*>(w + off[13]);
+            uint16_t* rpos = reinterpret_cast<uint16_t*>(w + off[14]);
+            uint16_t* rslot = reinterpret_cast<uint16_t*>(w + off[15]);
+            uint32_t* skip = reinterpret_cast<uint32_t*>(w + off[16]);
+            nout_fb = reinterpret_cast<uint32_t*>(w + off[17]);
+            hipLaunchKernelGGL(k_dec16_bsmaps, dim3(1, 1, gc), dim3(64), 0, st, b, r, smap, rpos, rslot, skip, nout_fb);
+            QF_HIP(hipGetLastError());
+            s = qf::gf16_bs_syndromes(ctx, st, k, r, L, gc, rows + (size_t)g0 * sh->rows_gen_stride,
+                                      sh->rows_gen_stride, sh->row_stride, smap, k, rpos, rslot, skip, w + off[19],
+                                      b.w.synd, em * Lp, Lp);
+            if (s) return s;
+        }
         Mv16Args sy{};
         sy.in = rows + (size_t)g0 * sh->rows_gen_stride;
         sy.igs = sh->rows_gen_stride;
@@ -1271,7 +1341,9 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         sy.m = b.w.mlog;
         sy.mgs = em * k;
         sy.mrs = k;
-        sy.nout_g = n_rec + g0;
+        // (bs: only the generations the bit-sliced kernel skipped, rows gathered
+        // as symbols: no logify pass over the whole batch)
+        sy.nout_g = bs ? nout_fb : n_rec + g0;
         sy.nin_g = &b.w.st->nin;
         sy.nin_gs = sizeof(Dec16State) / 4;
         sy.log = glog;
@@ -1279,7 +1351,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         sy.nout = e_max;
         sy.nin = k;
         sy.L = L;
-        s = launch_matvec(ctx, st, sy, gc, "k_syndromes16", acc, acc_bytes);
+        s = launch_matvec(ctx, st, sy, gc, bs ? "k_syndromes16_fallback" : "k_syndromes16", acc, acc_bytes, !bs);
         if (s) return s;
         // x_E = C[J,E]^-1 s
         Mv16Args so{};

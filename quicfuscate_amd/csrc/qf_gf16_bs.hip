@@ -31,16 +31,26 @@ namespace {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct Gf16BsArgs {
-    const uint8_t* src;
-    uint8_t* rep;
+    const uint8_t* src;        // encode: sources; syn: the received rows (arrival order)
+    uint8_t* rep;              // encode: repairs; syn: the syndrome rows (in accepted-repair order)
     uint64_t sgs, srs, rgs, rrs;
     uint64_t total;   // lane-chunks: G * Q
     uint32_t L, Lu, Q, tail;   // tail: L % 16 (bytes of the last unit; 0 = whole)
+    // syn only (per generation g, built by k_dec16_bsmaps in qf_gf16.hip)
+    const uint16_t* smap;      // [g][smap_gs]: slot of source i (0xFFFF: not received)
+    const uint16_t* rpos;      // [g][r]: position a of accepted repair k + j (0xFFFF: none)
+    const uint16_t* rslot;     // [g][r]: its slot
+    const uint32_t* skip;      // [g]: nonzero = not this kernel's generation
+    const uint8_t* zero;       // >= 64 Q zero bytes (the row of a source not received)
+    uint64_t smap_gs;
+    uint32_t r;
 };
 
 struct Gf16BsLane {
+    uint64_t g;
     const uint8_t* s;   // unit q of row 0 of the lane's generation
     uint8_t* d;
+    const uint8_t* z;   // unit q of the zero row
     uint64_t hq;        // 16 Q: byte distance between the lane's units
     uint32_t off[4];    // load offset of unit h (h 16 Q, or 0 past the row)
     uint32_t valid;     // bit h: unit q + h Q < Lu
@@ -51,8 +61,10 @@ __device__ __forceinline__ Gf16BsLane gf16bs_lane(const Gf16BsArgs& a, uint64_t 
     Gf16BsLane ln;
     const uint64_t g = f / a.Q;
     const uint32_t q = (uint32_t)(f - g * a.Q);
+    ln.g = g;
     ln.s = a.src + g * a.sgs + 16ull * q;
     ln.d = a.rep + g * a.rgs + 16ull * q;
+    ln.z = a.zero + 16ull * q;
     ln.hq = 16ull * a.Q;
     ln.valid = 0;
     ln.tailh = 0;
@@ -156,12 +168,45 @@ __device__ __forceinline__ void gf16bs_store_row(const Gf16BsArgs& a, const Gf16
     }
 }
 
+// syn: source row at slot `slot` of the lane's generation, or the zero row
+__device__ __forceinline__ void gf16bs_load_row_sel(const Gf16BsArgs& a, const Gf16BsLane& ln, uint32_t slot,
+                                                    uint32_t (&x)[16]) {
+    const uint8_t* p = slot == 0xFFFFu ? ln.z : ln.s + (uint64_t)slot * a.srs;
+#pragma unroll
+    for (uint32_t h = 0; h < 4; ++h) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + ln.off[h]));
+        x[4 * h] = v.x;
+        x[4 * h + 1] = v.y;
+        x[4 * h + 2] = v.z;
+        x[4 * h + 3] = v.w;
+    }
+}
+
+// syn: C[j, S] x_S of repair j -> syndrome a = that ^ the accepted row of
+// repair k + j (whole units: the syndrome rows are padded to 16 B)
+__device__ __forceinline__ void gf16bs_store_syn(const Gf16BsArgs& a, const Gf16BsLane& ln, uint32_t j,
+                                                 const uint32_t (&x)[16]) {
+    const uint32_t pos = a.rpos[ln.g * a.r + j];
+    if (pos == 0xFFFFu) return;
+    const uint8_t* p = ln.s + (uint64_t)a.rslot[ln.g * a.r + j] * a.srs;
+    uint8_t* o = ln.d + (uint64_t)pos * a.rrs;
+#pragma unroll
+    for (uint32_t h = 0; h < 4; ++h) {
+        if (!(ln.valid >> h & 1)) continue;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(p + ln.off[h]);
+        const u32x4 w = {x[4 * h] ^ v.x, x[4 * h + 1] ^ v.y, x[4 * h + 2] ^ v.z, x[4 * h + 3] ^ v.w};
+        *reinterpret_cast<u32x4*>(o + ln.off[h]) = w;
+    }
+}
+
 typedef void (*Gf16BsKernel)(Gf16BsArgs);
 
 struct Gf16BsEntry {
     uint32_t k, r, passes;
     Gf16BsKernel fn;
     const char* name;
+    Gf16BsKernel syn;
+    const char* syn_name;
 };
 
 #include "qf_gf16_bs.inc"
@@ -197,6 +242,49 @@ int gf16_bs_encode(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint32_t
     hipLaunchKernelGGL(e->fn, dim3((uint32_t)grid), dim3(256), 0, st, a);
     if (hipGetLastError() != hipSuccess) return QF_EDEVICE;
     ctx_prof_end(ctx, st, ev, e->name);
+    return QF_OK;
+}
+
+bool gf16_bs_has(uint32_t k, uint32_t r) {
+    for (const auto& t : kGf16BsTable)
+        if (t.k == k && t.r == r) return true;
+    return false;
+}
+
+int gf16_bs_syndromes(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint32_t L, uint32_t G,
+                      const uint8_t* rows, uint64_t rgs, uint64_t rs, const uint16_t* smap, uint64_t smap_gs,
+                      const uint16_t* rpos, const uint16_t* rslot, const uint32_t* skip, const uint8_t* zero,
+                      uint8_t* synd, uint64_t synd_gs, uint64_t synd_rs) {
+    const Gf16BsEntry* e = nullptr;
+    for (const auto& t : kGf16BsTable)
+        if (t.k == k && t.r == r) e = &t;
+    if (!e) return kGf16BsNone;
+    Gf16BsArgs a{};
+    a.src = rows;
+    a.rep = synd;
+    a.sgs = rgs;
+    a.srs = rs;
+    a.rgs = synd_gs;
+    a.rrs = synd_rs;
+    a.L = L;
+    a.Lu = (L + 15) / 16;
+    a.Q = (a.Lu + 3) / 4;
+    a.tail = 0;   // syndrome rows are padded: whole units
+    a.total = (uint64_t)G * a.Q;
+    a.smap = smap;
+    a.rpos = rpos;
+    a.rslot = rslot;
+    a.skip = skip;
+    a.zero = zero;
+    a.smap_gs = smap_gs;
+    a.r = r;
+    const uint64_t blocks = (a.total + 255) / 256;
+    const uint64_t grid = (blocks + 7) / 8 * 8 * e->passes;
+    if (grid > 0x7FFFFFFFull) return QF_ERANGE;
+    hipEvent_t ev = ctx_prof_begin(ctx, st);
+    hipLaunchKernelGGL(e->syn, dim3((uint32_t)grid), dim3(256), 0, st, a);
+    if (hipGetLastError() != hipSuccess) return QF_EDEVICE;
+    ctx_prof_end(ctx, st, ev, e->syn_name);
     return QF_OK;
 }
 

@@ -208,38 +208,59 @@ def _acc_stmt(acc: str, ops: list[str], init: bool) -> str:
     return f"{acc} = bs_xor3({acc}, {ops[0]}, {ops[1]});"
 
 
-def kernel_name(k: int, r: int) -> str:
-    return f"qf_gf16bs_k{k}_r{r}"
+def kernel_name(k: int, r: int, mode: str = "enc") -> str:
+    return f"qf_gf16bs_k{k}_r{r}" if mode == "enc" else f"qf_gf16bs_{mode}_k{k}_r{r}"
 
 
-def generate(k: int, r: int) -> str:
+def generate(k: int, r: int, mode: str = "enc") -> str:
     """One kernel per (k, r) holding every pass: block b runs pass
     (b / 8) % P over lane-chunk block ((b / 8) / P) * 8 + b % 8, so the P
     blocks that read the same rows share an XCD (blocks are dealt round-robin
     over the 8 XCDs) and run at about the same time: the re-reads of the
-    later passes hit L2 instead of HBM."""
+    later passes hit L2 instead of HBM.
+
+    mode "syn" (decode syndromes, Decoder16 with Cauchy rows): source row i
+    is gathered through the generation's slot map (a zero row where source i
+    was not received), and repair j's output, if repair k + j was accepted at
+    position a, is XORed with that repair row and stored as syndrome a."""
     P = n_passes(r)
-    lines = [f"// generated by quicfuscate_amd/gf16_codegen.py for k = {k}, r = {r} -- do not edit",
-             f"__global__ void __launch_bounds__(256, 2) {kernel_name(k, r)}(Gf16BsArgs a) {{",
+    syn = mode == "syn"
+    name = kernel_name(k, r, mode)
+    lines = [f"// generated by quicfuscate_amd/gf16_codegen.py for k = {k}, r = {r}, {mode} -- do not edit",
+             f"__global__ void __launch_bounds__(256, 2) {name}(Gf16BsArgs a) {{",
              f"    const uint32_t y = blockIdx.x >> 3, pass = y % {P}u;",
              f"    const uint64_t f = (uint64_t)((y / {P}u) * 8u + (blockIdx.x & 7u)) * 256u + threadIdx.x;",
              "    if (f >= a.total) return;",
-             "    const Gf16BsLane ln = gf16bs_lane(a, f);",
-             "    uint32_t tm[4];",
-             "    gf16bs_masks(tm);"]
+             "    const Gf16BsLane ln = gf16bs_lane(a, f);"]
+    if syn:
+        lines.append("    if (a.skip[ln.g]) return;    // failed, nothing erased, or a repair the kernel has no row for")
+        lines.append("    const uint16_t* sm = a.smap + ln.g * a.smap_gs;")
+    lines += ["    uint32_t tm[4];",
+              "    gf16bs_masks(tm);"]
+
+    def load(i: int, indent: str) -> str:
+        if syn:
+            return f"{indent}gf16bs_load_row_sel(a, ln, sl{i}, nx);"
+        return f"{indent}gf16bs_load_row(a, ln, {i}, nx);"
+
     for p in range(P):
         T = terms(k, r, p)
         nj = len(T[0])
         lines.append(f"    if (pass == {p}u) {{")
         lines.append("        uint32_t " + ", ".join(f"a{jj}_{b}" for jj in range(nj) for b in range(16)) + ";")
         lines.append("        uint32_t x[16], nx[16];")
-        lines.append("        gf16bs_load_row(a, ln, 0, nx);")
+        if syn:
+            lines.append("        uint32_t sl0 = sm[0]" + (", sl1 = sm[1]" if k > 1 else "")
+                         + "".join(f", sl{i}" for i in range(2, k)) + ";")
+        lines.append(load(0, "        "))
         for i in range(k):
             lines.append("        {")
             lines.append("#pragma unroll")
             lines.append("            for (int d = 0; d < 16; ++d) x[d] = nx[d];")
             if i + 1 < k:
-                lines.append(f"            gf16bs_load_row(a, ln, {i + 1}, nx);")
+                if syn and i + 2 < k:
+                    lines.append(f"            sl{i + 2} = sm[{i + 2}];")
+                lines.append(load(i + 1, "            "))
             lines.append("            gf16bs_transpose(x, tm);")
             # groups {0, 1} then {2, 3}: 22 combinations live at a time, one
             # v_xor3 per output plane and group pair
@@ -264,7 +285,8 @@ def generate(k: int, r: int) -> str:
             lines.append("        {")
             lines.append("            uint32_t o[16] = {" + ", ".join(f"a{jj}_{b}" for b in range(16)) + "};")
             lines.append("            gf16bs_transpose(o, tm);")
-            lines.append(f"            gf16bs_store_row(a, ln, {NO * p + jj}u, o);")
+            store = "gf16bs_store_syn" if syn else "gf16bs_store_row"
+            lines.append(f"            {store}(a, ln, {NO * p + jj}u, o);")
             lines.append("        }")
         lines.append("    }")
     lines.append("}")
@@ -274,9 +296,10 @@ def generate(k: int, r: int) -> str:
 
 def generate_all(configs=None) -> str:
     configs = configs or GF16_BS_CONFIGS
-    body = [generate(k, r) for k, r in configs]
+    body = [generate(k, r, m) for k, r in configs for m in ("enc", "syn")]
     table = ["static const Gf16BsEntry kGf16BsTable[] = {"]
     for k, r in configs:
-        table.append(f"    {{{k}u, {r}u, {n_passes(r)}u, {kernel_name(k, r)}, \"{kernel_name(k, r)}\"}},")
+        e, y = kernel_name(k, r), kernel_name(k, r, "syn")
+        table.append(f'    {{{k}u, {r}u, {n_passes(r)}u, {e}, "{e}", {y}, "{y}"}},')
     table.append("};")
     return "\n".join(body + table) + "\n"

@@ -319,3 +319,51 @@ def test_encode16_bitsliced(qf, oracle, gpu_ctx, k, r, L, G):
     qf.set_default_options(gf16_bitsliced=0)
     rep2 = run_encode16(qf, src, r)
     assert np.array_equal(rep, rep2)
+
+
+def test_decode16_bitsliced_syndromes(qf, oracle, gpu_ctx):
+    """Cauchy decode of a (k, r) with a generated bit-sliced kernel: the
+    syndromes come from qf_gf16bs_syn_* (sources gathered through the slot
+    map, the accepted repair row XORed in), the general matvec only for the
+    generation with a repair index past k + r; statuses, recovered bytes and
+    indices equal the oracle's and the general path's (gf16_bitsliced = 0)."""
+    from quicfuscate_amd import gf16_codegen as g16
+
+    k, r, L = 64, 16, 1194
+    rng = np.random.default_rng(1616)
+    src, gens = make_gens(oracle, rng, k, r, L, 8)
+    _, full = make_gens(oracle, rng, k, r, L, 1, erase=16)
+    _, none = make_gens(oracle, rng, k, r, L, 1, erase=0)
+    _, short = make_gens(oracle, rng, k, r, L, 1, erase=5, short=True)
+    _, dup = make_gens(oracle, rng, k, r, L, 1, erase=3, dup=True)
+    src = np.concatenate([src, src[:4]])
+    gens += [full[0], none[0], short[0], dup[0]]
+    # generation 0: one accepted repair row is Cauchy row k + 20 (no row of the kernel)
+    arr, rows, rc = gens[0]
+    far = oracle.encode16(src[0], 21)[20]
+    pos = next(s for s, a in enumerate(arr[:k]) if a < k)
+    gens[0] = ([k + 20] + [a for s, a in enumerate(arr) if s != pos],
+               np.concatenate([far[None], np.delete(rows, pos, 0)]), None)
+    G = len(gens)
+    src_used = np.stack([src[g] for g in range(8)] + [np.zeros((k, L), np.uint8)] * 4)
+    gpu_ctx.profile(True)
+    res = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
+    names = set(gpu_ctx.kernel_times())
+    gpu_ctx.profile(False)
+    assert g16.kernel_name(k, r, "syn") in names and "k_syndromes16_fallback" in names, names
+    rec, ri, nrec, st, rrs, rec_gs = res
+    for g, (a, rw, _) in enumerate(gens):
+        ost, out, mask = oracle.decode16(k, a, rw, None)
+        assert st[g] == ost, (g, st[g], ost)
+        if ost:
+            assert nrec[g] == 0
+            continue
+        erased = [i for i in range(k) if not mask[i]]
+        assert nrec[g] == len(erased) and ri[g, : len(erased)].tolist() == erased, g
+        for b, i in enumerate(erased):
+            o = g * rec_gs + b * rrs
+            assert np.array_equal(rec[o: o + L], out[i]), (g, i)
+    qf.set_default_options(gf16_bitsliced=0)
+    res2 = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
+    for x, y in zip(res[:4], res2[:4]):
+        assert np.array_equal(x, y)
