@@ -124,8 +124,8 @@ enum {
     QF_OPT_GF16_LOGIFY,          /* 1: GF(2^16) inputs in log form for wide matvecs; 0 never [QF_GF16_LOGIFY] */
     QF_OPT_GF16_LOGIFY_MIN_BLOCKS, /* output blocks from which inputs are logified [QF_GF16_LOGIFY_MIN_BLOCKS] */
     QF_OPT_GF16_LDS_GJ,          /* 1: GF(2^16) Gauss-Jordan in LDS for e <= 64 [QF_GF16_LDS_GJ; default 0] */
-    QF_OPT_GF16_BITSLICED,       /* 1: bit-sliced GF(2^16) Cauchy encode where generated; 0 never
-                                    [QF_GF16_BITSLICED; default 1] */
+    QF_OPT_GF16_BITSLICED,       /* 1: bit-sliced GF(2^16) Cauchy encode and decode syndromes where
+                                    generated; 0 never [QF_GF16_BITSLICED; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

@@ -62,3 +62,16 @@ def test_framing_roundtrip_and_errors(qf):
     for bad in (b"", b"\x00\x01", b"\x00\x00\x05ab"):
         with pytest.raises(qf.QfError):
             qf.Packet.from_raw(0, bad)
+
+
+def test_option_enum_matches_binding():
+    """QF_OPT_* of include/qf_fec.h, in enum order, are the Python binding's
+    OPTIONS (the index is the ABI value qf_ctx_set_option takes)."""
+    import re
+
+    from quicfuscate_amd import _lib as L
+
+    txt = L.HEADER.read_text()
+    enum = txt[txt.index("QF_OPT_FFT_KERNELS = 0"): txt.index("QF_OPT_COUNT")]
+    names = [n.lower() for n in re.findall(r"QF_OPT_([A-Z0-9_]+)", enum)]
+    assert names == list(L.OPTIONS) and L.QF_OPT_COUNT == len(names)
