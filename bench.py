@@ -134,9 +134,14 @@ def parse(argv=None):
     ap.add_argument("--host-path-G", type=int, default=16384, help="generations for the pinned-host encode rate (0=skip)")
     ap.add_argument("--overlap", action="store_true",
                     help="run the step's encode and decode (independent batches) on two HIP streams")
-    ap.add_argument("--split", action="store_true",
-                    help="decode acceptance pass on a 2nd stream beside the encode, payload pass after it")
-    return ap.parse_args(argv)
+    ap.add_argument("--split", action="store_true", default=True,
+                    help="(default) decode acceptance pass on a 2nd stream beside the encode, payload pass after it")
+    ap.add_argument("--serial", dest="split", action="store_false",
+                    help="encode, then the whole decode, on one stream")
+    a = ap.parse_args(argv)
+    if a.overlap:
+        a.split = False
+    return a
 
 
 def launch_plan(args, env, argv=None):

@@ -111,7 +111,7 @@ enum {
     QF_OPT_COMBINE_BS,           /* 1: bit-sliced payload pass (qf_combine_bs) at long rows; 0 never [QF_COMBINE_BS] */
     QF_OPT_COMBINE_BS_MIN_Q,     /* its smallest row, in 32-B lane-chunks [QF_COMBINE_BS_MIN_Q; default 64] */
     QF_OPT_COMBINE_SPLIT,        /* 1: slot-split payload pass for <= 1 item per CU; 0 never [QF_COMBINE_SPLIT] */
-    QF_OPT_PREPARE_GRID,         /* split-phase acceptance pass grid, 0 = one block per two CUs [QF_PREPARE_GRID] */
+    QF_OPT_PREPARE_GRID,         /* split-phase acceptance pass grid, 0 = one block per CU [QF_PREPARE_GRID] */
     QF_OPT_ENC_BLOCKS_PER_CU,    /* cap of the bit-sliced encode grid, 0 = none [QF_ENC_BLOCKS_PER_CU] */
     QF_OPT_DEC_BLOCKS_PER_CU,    /* cap of the fused decode grid, 0 = none [QF_DEC_BLOCKS_PER_CU] */
     QF_OPT_SEND_FUSED,           /* 1: one-launch per-packet send (k_send_window); 0 never [QF_SEND_FUSED] */

@@ -530,10 +530,12 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     if (ctx->payload_wait) {
         // split phase: the acceptance pass runs beside the caller's other
         // work, on a capped persistent grid (QF_PREPARE_GRID blocks, default
-        // one per two CUs: beside the C2 encode it then takes ~1 ms, under
-        // the encode, and slows it by ~2 %; 4 blocks per CU slowed it 10 %)
+        // one per CU: beside the C2 encode it then takes ~0.42 ms, under the
+        // encode, and slows it by ~4 %; the step gains ~2 % (DESIGN 3.2,
+        // profiles/r03q_split.jsonl, r03r_split.jsonl); one per two CUs 0.74 ms, 64 blocks
+        // 1.39 ms (longer than the encode), 4 per CU slowed the encode 10 %)
         const int64_t pg = ctx->opt[QF_OPT_PREPARE_GRID];
-        pa.grid_cap = pg ? (uint32_t)pg : std::max<uint32_t>(1, (uint32_t)ctx->num_cus / 2);
+        pa.grid_cap = pg ? (uint32_t)pg : std::max<uint32_t>(1, (uint32_t)ctx->num_cus);
     }
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));

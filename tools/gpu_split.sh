@@ -1,17 +1,17 @@
 #!/bin/bash
-# Split-phase decode: bench serial vs --split at several acceptance-pass grid caps.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# GPU box: split-phase decode (acceptance pass beside the encode; the bench
+# default) vs serial, twice each, alternating.
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_decode.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -k payload_wait > gpurun_out/pytest_split.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_split.log; [ $rc -eq 0 ] || exit $rc
-for cfg in "0 " "64 --split" "128 --split" "256 --split" "512 --split" "1024 --split" "0 "; do
-  set -- $cfg; export QF_PREPARE_GRID=$1; mode=${2:-}
-  timeout -k 10 300 python bench.py --no-cpu --host-path-G 0 $mode > gpurun_out/bench_split.log 2>&1
-  rc=$?; [ $rc -eq 0 ] || { echo "bench $cfg rc=$rc"; tail -5 gpurun_out/bench_split.log; exit $rc; }
-  python - "$cfg" <<'PY'
-import json, sys
-d = json.loads([l for l in open("gpurun_out/bench_split.log") if l.startswith("{")][-1])
-print(sys.argv[1], d["value"], d["ms_per_step"], d["encode_ms"], d["decode_ms"], d["kernel_ms_per_launch"], d["verified"])
-PY
-done
+OUT=gpurun_out/${TAG:-r03}
+mkdir -p $OUT
+ARGS="--no-cpu --host-path-G 0 --c3b-G 0 --c4-G 0 --steps 20"
+run() { local name=$1; shift; env "$@" timeout -k 10 200 python bench.py $ARGS $EXTRA > $OUT/sp_$name.log 2>&1; }
+EXTRA="--serial" run serial
+EXTRA="" run split
+EXTRA="--serial" run serial2
+EXTRA="" run split2
+EXTRA="" run split_g512 QF_PREPARE_GRID=512
+for f in serial split serial2 split2 split_g512; do python3 -c "
+import json; d=json.loads(open('$OUT/sp_$f.log').read().strip().splitlines()[-1]); print('$f', d['value'], d['ms_per_step'], d.get('encode_ms'), d.get('decode_ms'), d['kernel_ms_per_launch'], d['verified'])"; done
