@@ -330,6 +330,20 @@ def main(argv=None):
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
     dec_ms = float(np.mean([(a if args.overlap else b).elapsed_time(c) for a, b, c, _ in ev]))
     step_ms = wall * 1e3 / args.steps
+    # with a second stream the encode shares the GPU with the decode's
+    # acceptance pass (split) or the whole decode (overlap): its own roofline
+    # comes from a few launches alone, after the timed steps (same buffers and
+    # bytes; the repairs are rewritten with the same values)
+    enc_alone_ms = None
+    if ctx_enc is not ctx_dec:
+        ctx_enc.profile(True)
+        for _ in range(5):
+            encode()
+        ctx_enc.sync()
+        ka = ctx_enc.kernel_times()
+        ctx_enc.profile(False)
+        ka = {n: ms / max(1, c) for n, (c, ms) in ka.items() if n.startswith(("qf_cauchy_bs", "k_combine_uniform"))}
+        enc_alone_ms = next(iter(ka.values()), None)
 
     # --- verification (size-independent round trip on the device) ---------
     st_ok = bool((status == 0).all().item())
@@ -467,6 +481,22 @@ def main(argv=None):
 
     enc_kernel = next((n for n in kern_ms if n.startswith(("qf_cauchy_bs", "k_combine_uniform"))), None)
 
+    def roofline_encode():
+        """The encode kernel's roofline: alone (5 launches after the timed
+        steps) when the step runs it beside other work, with its in-step
+        launches under `in_step`; the in-step figures otherwise."""
+        rl = roofline(enc_kernel)
+        if enc_alone_ms is None:
+            return rl
+        in_step = {key: rl[key] for key in ("launch_ms", "achieved", "frac")}
+        rl["launch_ms"] = round(enc_alone_ms, 4)
+        rl["achieved"] = round(alg_bytes(enc_kernel) / (enc_alone_ms / 1e3) / 1e9, 1)
+        rl["frac"] = round(rl["achieved"] / PEAK_HBM_GBPS, 4)
+        rl["valu"] = valu_roof(enc_kernel, enc_alone_ms)
+        rl["timing"] = "the kernel alone: 5 launches on the context stream after the timed steps (HIP events)"
+        rl["in_step"] = dict(in_step, note="its launches inside the timed steps, beside the decode's acceptance pass")
+        return rl
+
     out = {
         "metric": "GF(256) RLNC encode+decode GiB/s device-resident, 1200B pkts gen=64, 1/2/4/8 GPU",
         "value": round(value, 3),
@@ -498,7 +528,7 @@ def main(argv=None):
         # (profiles/ SQ counters)
         "roofline": roofline(dom),
         # the encode kernel BASELINE.json's north star targets (>= 70 % HBM)
-        "roofline_encode": roofline(enc_kernel) if enc_kernel else None,
+        "roofline_encode": roofline_encode() if enc_kernel else None,
         "streams": ("encode || decode (2 HIP streams)" if args.overlap else
                     "encode, then decode payload pass; decode acceptance pass on a 2nd stream beside the encode"
                     if args.split else "encode then decode (1 stream)"),
