@@ -31,6 +31,11 @@ def variant_ops(bs, spec, flags):
     acc_lo, acc_hi = spec.acc0, spec.acc0 + 8 * spec.nacc
     out = []
     for n, op in enumerate(ops):
+        # notables: the prologue's split-table copy into LDS dropped (timing
+        # only: an upper bound on what loading the tables later could save)
+        if "notables" in flags and n < body and (op.name == "ds_write_b128" or
+                                                 (op.name == "load16" and 48 <= op.args[0] < 80)):
+            continue
         if n > body:
             if "noload" in flags and op.name in ("load16", "load16_lds", "s_waitcnt_vm"):
                 continue

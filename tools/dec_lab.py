@@ -36,6 +36,15 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 3u: what the per-wave split-table copy into LDS costs (notables:
+    # dropped, results wrong, timing only)
+    ("t_warm", dict(LIB_DEC), ()),
+    ("t_lib", dict(LIB_DEC), ()),
+    ("t_notables", dict(LIB_DEC), ("notables",)),
+    ("t_lib_2", dict(LIB_DEC), ()),
+    ("t_notables_2", dict(LIB_DEC), ("notables",)),
+]
+VARIANTS_R03K = [
     # round 3k: persistent grids (cap = 2 blocks of 4 waves per CU, every wave
     # loops over items) with the second residency half started late (stagger:
     # workgroups 256..511 sleep iters x 3.4 us), to separate phase alignment
