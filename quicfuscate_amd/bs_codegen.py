@@ -2660,7 +2660,7 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
              total_waves: int, smap: int = 0, map_stride: int = 0, zero: int = 0,
              Lv: Optional[int] = None, zero_tail: bool = False, lu: Optional[tuple[int, int]] = None,
              tables: int = 0, src_offs: int = 0, dst_offs: int = 0, chunked: bool = False,
-             bound: Optional[int] = None, wave_gen: bool = False) -> bytes:
+             bound: Optional[int] = None, wave_gen: bool = False, Q: Optional[int] = None) -> bytes:
     """96-byte kernarg block (layout above; 128 bytes in dec mode).  Syndrome mode: src = received
     rows, dst = syndrome rows, plus slot map and zero row.  zero_tail (enc):
     also write zeros to bytes [L, 16 Lv) of every repair row.  Dec mode
@@ -2668,8 +2668,11 @@ def kernargs(src: int, dst: int, sgs: int, dgs: int, srs: int, drs: int, L: int,
     drs are the recovered rows' base, generation and row strides; 112 bytes."""
     Lv, total, n_items = launch_geometry(L, G, Lv)
     magic, shift = magic_for(Lv)
-    if chunked:   # lane-chunk layout (_prologue_chunked): Lv <- Q = ceil(Lu / 2)
+    if chunked:   # lane-chunk layout (_prologue_chunked): Lv <- Q = ceil(Lu / 2) (Q: a larger one)
         Lv = ((L + 15) // 16 + 1) // 2
+        if Q is not None:
+            assert Lv <= Q < (L + 15) // 16
+            Lv = Q
         total = G * Lv
         n_items = G if wave_gen else (total + 63) // 64
         magic, shift = magic_for(Lv)

@@ -36,6 +36,20 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 3v: line-aligned row segments -- Q = 40 lane-chunks per generation
+    # (a multiple of 8 units: every wave's segment of a row starts on a
+    # 128-B boundary when the rows do, i.e. at 1,280-B row strides)
+    ("q_warm", dict(LIB_DEC), ()),
+    ("q_lib", dict(LIB_DEC), ()),
+    ("q40", {**LIB_DEC, "Q": 40}, ()),
+    ("q40_1280", {**LIB_DEC, "Q": 40, "rs": 1280, "rrs": 1280}, ()),
+    ("q38_1280", {**LIB_DEC, "rs": 1280, "rrs": 1280}, ()),
+    ("q40_1280_nolu", {**LIB_DEC, "Q": 40, "rs": 1280, "rrs": 1280, "lu": False}, ()),
+    ("q_nolu", {**LIB_DEC, "lu": False}, ()),
+    ("q_lib_2", dict(LIB_DEC), ()),
+    ("q40_1280_2", {**LIB_DEC, "Q": 40, "rs": 1280, "rrs": 1280}, ()),
+]
+VARIANTS_R03U = [
     # round 3u: what the per-wave split-table copy into LDS costs (notables:
     # dropped, results wrong, timing only)
     ("t_warm", dict(LIB_DEC), ()),
@@ -213,7 +227,7 @@ def build():
             continue
         kw2 = dict(kw)
         pd = kw2.pop("pd", 3)
-        for key in ("cap", "rs", "rrs"):
+        for key in ("cap", "rs", "rrs", "Q"):
             kw2.pop(key, None)
         spec = bs.KernelSpec(64, 16, pd, "dec", **kw2)
         text = bs.emit_asm(spec, variant_ops(bs, spec, set(flags)))
@@ -274,8 +288,9 @@ def run(G, reps):
         Lv = None
         chunked, wave_gen = m["kw"].get("chunked", False), m["kw"].get("wave_gen", False)
         _, _, n_items = bs.launch_geometry(L, G, Lv)
+        Qv = m["kw"].get("Q")
         if chunked:
-            n_items = G if wave_gen else (G * (((L + 15) // 16 + 1) // 2) + 63) // 64
+            n_items = G if wave_gen else (G * (Qv or (((L + 15) // 16 + 1) // 2)) + 63) // 64
         blocks = (n_items + 3) // 4
         if m["kw"].get("ksplit", 1) > 1:
             blocks = n_items
@@ -285,7 +300,7 @@ def run(G, reps):
         ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * rs, e * rrs, rs, rrs, L, G, blocks * 4,
                          smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
                          lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr(), chunked=chunked,
-                         wave_gen=wave_gen)
+                         wave_gen=wave_gen, Q=Qv)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
