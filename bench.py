@@ -440,7 +440,12 @@ def main(argv=None):
         waves = ent["SQ_WAVES"]
         issue_ms = per_wave * waves * 2 / (n_simd * clk_ghz * 1e9) * 1e3
         peak = n_simd * clk_ghz * 1e9 / 2 / 1e9          # wave-instructions per ns -> G/s
+        # VALU lane-ops per GF byte multiply-add of the launch
+        # (encode r k L G, decode e k L G byte-mult-adds)
+        bm = (e if name.startswith("qf_cauchy_dec") else r) * k * Lb * G
+        per_bm = round(per_wave * waves * 64 / bm, 4) if bm and not name.startswith("k_") else None
         return {"bound": "valu", "achieved": round(per_wave * waves / (ms / 1e3) / 1e9, 2), "peak": round(peak, 2),
+                "lane_ops_per_byte_mult": per_bm,
                 "unit": "G wave64 VALU instr/s", "frac": round(issue_ms / ms, 4),
                 "valu_per_wave": round(per_wave, 1), "waves": int(waves), "issue_ms": round(issue_ms, 4),
                 "source": "profiles/sq_counters.json (SQ_INSTS_VALU / SQ_WAVES, separate --pmc pass of this workload)"}
@@ -505,6 +510,9 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(step_ms_max, 4),
+        # the median of the per-step device times (HIP events
+        # around each step on this rank) beside the wall-clock mean above
+        "ms_per_step_median_rank0": round(float(np.median([a.elapsed_time(d) for a, _, _, d in ev])), 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
