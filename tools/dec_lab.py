@@ -36,6 +36,20 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 3y: the FFT row loop alone with ONE wave per SIMD (cap = 256 blocks
+    # of 4 waves: one per CU), register ring vs deep LDS staging -- the
+    # ceiling of a producer/consumer split (row-loop waves + LU waves)
+    ("y_warm", dict(LIB_DEC), ()),
+    ("y_lib", dict(LIB_DEC), ()),
+    ("y_nolu", {**LIB_DEC, "lu": False}, ()),
+    ("y_nolu_c1", {**LIB_DEC, "lu": False, "cap": 256}, ()),
+    ("y_nolu_l9_c1", {"chunked": True, "fft": 8, "lds_rows": 9, **D, "lu": False, "cap": 256}, ()),
+    ("y_nolu_l12_c1", {"chunked": True, "fft": 8, "lds_rows": 12, **D, "lu": False, "cap": 256}, ()),
+    ("y_nolu_l16_c1", {"chunked": True, "fft": 8, "lds_rows": 16, **D, "lu": False, "cap": 256}, ()),
+    # the LU phase alone (the lane-chunk kernel's LU = the FFT kernel's), one wave per SIMD
+    ("lu_c1", {"chunked": True, "lab_lu_only": True, "cap": 256, **D}, ()),
+]
+VARIANTS_R03V = [
     # round 3v: line-aligned row segments -- Q = 40 lane-chunks per generation
     # (a multiple of 8 units: every wave's segment of a row starts on a
     # 128-B boundary when the rows do, i.e. at 1,280-B row strides)
@@ -209,7 +223,8 @@ VARIANTS_R03 = [
     ("f_l9_norows", {"chunked": True, "fft": 8, "lds_rows": 9, "lab_norows": True}, ()),
     ("f_l8_2", {"chunked": True, "fft": 8, "lds_rows": 8}, ()),
 ]
-PAIRS = [("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]   # need all three built
+PAIRS = [("y_nolu_l12_c1", "lu_c1"), ("y_nolu_c1", "lu_c1"),    # round 3y (need all built)
+         ("rl_pd6_c1", "lu_c1"), ("rl_pd5_c1", "lu_c1"), ("rl_pd3_c1", "lu_c1")]
 
 
 def build():
