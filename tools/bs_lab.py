@@ -51,6 +51,16 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 3z: dense 1,200-B repair rows with the line-aligned item layout
+    # (no zero-tail bytes: 1.3 % less traffic) against the zero-tail default
+    ("z_warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("z_ztail", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("z_dense", 64, 16, 3, ("ld:nt", "st:nt", "pad80", "fft:8"), ALL),
+    ("z_dense_stdef", 64, 16, 3, ("ld:nt", "pad80", "fft:8"), ALL),
+    ("z_ztail_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("z_dense_2", 64, 16, 3, ("ld:nt", "st:nt", "pad80", "fft:8"), ALL),
+]
+VARIANTS_R03B = [
     # round 3b: rows staged in LDS ("lds:<slots per wave>", global_load_lds_dwordx4)
     ("warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
     ("fft_pd3", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
@@ -147,7 +157,9 @@ def run(G: int, reps: int):
         assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
         zt = "ztail" in m["flags"]
-        Lv = bs.padded_units(L) if zt else None
+        # pad80: the padded lane space (items line-aligned) but dense repair rows
+        # of L bytes and no zero tail (the padding lanes store nothing)
+        Lv = bs.padded_units(L) if (zt or "pad80" in m["flags"]) else None
         _, _, n_items = bs.launch_geometry(L, G, Lv)
         blocks = min((n_items + 3) // 4, ncu * m["blocks_per_cu"])
         wide = "dst:wide" in m["flags"]
