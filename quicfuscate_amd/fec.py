@@ -184,6 +184,21 @@ def _ptr(t) -> int:
     return int(t.data_ptr())
 
 
+def _need(t, nbytes: int, what: str) -> None:
+    """A buffer the library will read or write must hold nbytes (the C ABI
+    takes bare pointers: an undersized tensor would be overrun on the device)."""
+    if t is None or nbytes <= 0 or not hasattr(t, "numel"):
+        return
+    have = int(t.numel()) * int(t.element_size())
+    if have < nbytes:
+        raise ValueError(f"{what}: {have} bytes, the call needs {nbytes}")
+
+
+def _span(G: int, gen_stride: int, rows: int, row_stride: int, L: int) -> int:
+    """Bytes from the first byte of generation 0 to the end of the last row."""
+    return 0 if G == 0 or rows == 0 else (G - 1) * gen_stride + (rows - 1) * row_stride + L
+
+
 def gf_mul_slice(a: bytes, b: bytes, ctx: Optional[Context] = None) -> bytes:
     """gf_tables.rs:255 gf_mul_slice: element-wise a[i]*b[i], on the device."""
     import torch
@@ -214,6 +229,8 @@ def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_
     zero_tail: QF_ENCODE_ZERO_TAIL (the library may zero [L, round_up(L, 128))
     of each repair row)."""
     ctx = ctx or default_context()
+    _need(src, _span(G, src_gen_stride, k, src_row_stride, Lb), "src")
+    _need(rep, _span(G, rep_gen_stride, r, rep_row_stride, Lb), "rep")
     sh = L.EncodeShape(k, r, Lb, 1 if zero_tail else 0, src_row_stride, src_gen_stride, rep_row_stride,
                        rep_gen_stride)
     cbuf = None
@@ -290,6 +307,14 @@ def decode_batch(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int,
                  ctx: Optional[Context] = None) -> None:
     """qf_decode_batch: recover erased rows of G generations (decoder.rs:658-791)."""
     ctx = ctx or default_context()
+    em = min(k, r)
+    _need(rows, _span(G, rows_gen_stride, max_rows, row_stride, Lb), "rows")
+    _need(row_index, 2 * G * max_rows, "row_index")
+    _need(rec_index, 2 * G * em, "rec_index (min(k, r) entries per generation)")
+    _need(n_rec, 4 * G, "n_rec")
+    _need(status, 4 * G, "status")
+    if n_rows is not None:
+        _need(n_rows, 4 * G, "n_rows")
     sh = L.DecodeShape(k, r, Lb, max_rows, row_stride, rows_gen_stride, rec_row_stride, rec_gen_stride)
     check(L._lib().qf_decode_batch(
         ctx.handle, ctypes.byref(sh), G, _ptr(rows), _ptr(row_index),

@@ -190,7 +190,7 @@ def main():
                                               rep3[gi, (sel - k).clamp(min=0)])
                 t_idx = torch.from_numpy(ridx.view(np.int16).reshape(-1)).cuda()
                 rec = torch.empty(G * e * RS, dtype=torch.uint8, device="cuda")
-                rec_index = torch.empty(G * e, dtype=torch.int16, device="cuda")
+                rec_index = torch.empty(G * min(k, r), dtype=torch.int16, device="cuda")   # min(k, r) per generation
                 n_rec = torch.empty(G, dtype=torch.int32, device="cuda")
                 status = torch.empty(G, dtype=torch.int32, device="cuda")
 
@@ -200,7 +200,10 @@ def main():
                                     rec_row_stride=RS, rec_gen_stride=e * RS, G=G)
 
                 wall, kt = timed(ctx, dec, a.reps)
-                assert (status == 0).all().item() and (n_rec == e).all().item()
+                if not ((status == 0).all().item() and (n_rec == e).all().item()):
+                    st_np, nr_np = status.cpu().numpy(), n_rec.cpu().numpy()
+                    raise AssertionError(f"k={k} r={r} G={G}: statuses {np.unique(st_np, return_counts=True)}, "
+                                         f"n_rec {np.unique(nr_np, return_counts=True)} (expected {e})")
                 g = G - 1
                 E = sorted(set(range(k)) - set(int(x) for x in ridx[g] if x < k))
                 assert torch.equal(rec.view(G, e, RS)[g, :, :L_JUMBO], src3[g, E, :L_JUMBO])
