@@ -228,9 +228,9 @@ def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_
     """qf_encode_batch: repairs of G generations (decoder.rs:172-275).
     zero_tail: QF_ENCODE_ZERO_TAIL (the library may zero [L, round_up(L, 128))
     of each repair row)."""
-    ctx = ctx or default_context()
     _need(src, _span(G, src_gen_stride, k, src_row_stride, Lb), "src")
     _need(rep, _span(G, rep_gen_stride, r, rep_row_stride, Lb), "rep")
+    ctx = ctx or default_context()
     sh = L.EncodeShape(k, r, Lb, 1 if zero_tail else 0, src_row_stride, src_gen_stride, rep_row_stride,
                        rep_gen_stride)
     cbuf = None
@@ -306,7 +306,6 @@ def decode_batch(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int,
                  rec_gen_stride: int, G: int, n_rows=None, row_coeffs=None,
                  ctx: Optional[Context] = None) -> None:
     """qf_decode_batch: recover erased rows of G generations (decoder.rs:658-791)."""
-    ctx = ctx or default_context()
     em = min(k, r)
     _need(rows, _span(G, rows_gen_stride, max_rows, row_stride, Lb), "rows")
     _need(row_index, 2 * G * max_rows, "row_index")
@@ -315,6 +314,7 @@ def decode_batch(rows, row_index, rec, rec_index, n_rec, status, k: int, r: int,
     _need(status, 4 * G, "status")
     if n_rows is not None:
         _need(n_rows, 4 * G, "n_rows")
+    ctx = ctx or default_context()
     sh = L.DecodeShape(k, r, Lb, max_rows, row_stride, rows_gen_stride, rec_row_stride, rec_gen_stride)
     check(L._lib().qf_decode_batch(
         ctx.handle, ctypes.byref(sh), G, _ptr(rows), _ptr(row_index),

@@ -75,3 +75,34 @@ def test_option_enum_matches_binding():
     enum = txt[txt.index("QF_OPT_FFT_KERNELS = 0"): txt.index("QF_OPT_COUNT")]
     names = [n.lower() for n in re.findall(r"QF_OPT_([A-Z0-9_]+)", enum)]
     assert names == list(L.OPTIONS) and L.QF_OPT_COUNT == len(names)
+
+
+def test_mirror_rejects_undersized_buffers():
+    """fec.encode_batch / decode_batch check every buffer against the shape
+    before the library sees a pointer (rec_index: min(k, r) entries per
+    generation, include/qf_fec.h)."""
+    import pytest
+    import torch
+
+    from quicfuscate_amd import fec
+
+    k, r, L, G = 64, 16, 1200, 3
+    src = torch.zeros(G * k * L, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="rep"):
+        fec.encode_batch(src, torch.zeros(G * r * L - 1, dtype=torch.uint8), k, r, L, src_row_stride=L,
+                         src_gen_stride=k * L, rep_row_stride=L, rep_gen_stride=r * L, G=G)
+    with pytest.raises(ValueError, match="src"):
+        fec.encode_batch(src[:-1], torch.zeros(G * r * L, dtype=torch.uint8), k, r, L, src_row_stride=L,
+                         src_gen_stride=k * L, rep_row_stride=L, rep_gen_stride=r * L, G=G)
+    n = k
+    rows = torch.zeros(G * n * L, dtype=torch.uint8)
+    idx = torch.zeros(G * n, dtype=torch.int16)
+    rec = torch.zeros(G * r * L, dtype=torch.uint8)
+    i32 = torch.zeros(G, dtype=torch.int32)
+    with pytest.raises(ValueError, match="rec_index"):
+        fec.decode_batch(rows, idx, rec, torch.zeros(G * 13, dtype=torch.int16), i32, i32, k, r, L, max_rows=n,
+                         row_stride=L, rows_gen_stride=n * L, rec_row_stride=L, rec_gen_stride=r * L, G=G)
+    with pytest.raises(ValueError, match="status"):
+        fec.decode_batch(rows, idx, rec, torch.zeros(G * r, dtype=torch.int16), i32, i32[:1], k, r, L,
+                         max_rows=n, row_stride=L, rows_gen_stride=n * L, rec_row_stride=L,
+                         rec_gen_stride=r * L, G=G)
