@@ -121,6 +121,10 @@ def parse(argv=None):
     ap.add_argument("--c4-G", type=int, default=156250,
                     help="generations per rank of the separately timed C4 leg (10 M packets/GPU; 0 = skip)")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-split", action="store_true",
+                    help="C4 leg on the split-phase stream plan; default serial: at 156,250 generations the "
+                         "encode's grid holds every CU until it drains, so the acceptance pass runs after it, "
+                         "grid-capped (profiles/r03ab_c4_schedule.json)")
     ap.add_argument("--rank-sample", type=int, default=64,
                     help="seeded generations per rank checked against the CPU oracle (N>1 and --config c4)")
     ap.add_argument("--k", type=int, default=64)
@@ -583,7 +587,7 @@ def main(argv=None):
         del src, rep, rows, rowsv, srcv, repv, rec, rec_index, n_rec, status, aidx_t, row_index, er_t, recv, gi
         torch.cuda.empty_cache()
         out["c4"] = c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, r, Lb, e, args.c4_G,
-                           args.c4_steps, args.warmup, args.rank_sample)
+                           args.c4_steps, args.warmup, args.rank_sample, split=args.c4_split)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -598,7 +602,7 @@ def main(argv=None):
 
 
 def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, r, Lb, e, G, steps, warmup,
-           rank_sample) -> dict:
+           rank_sample, split=False) -> dict:
     """BASELINE C4: 10 M packets = 156,250 generations per rank,
     encoded and then decoded at the C3 loss shape (13 erased sources per
     generation), each rank on its own contiguous generations with distinct
@@ -635,11 +639,27 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
     dec_args = dict(max_rows=n_slots, row_stride=Lb, rows_gen_stride=n_slots * Lb, rec_row_stride=Lb,
                     rec_gen_stride=emax * Lb, G=G, ctx=ctx)
 
+    # split: the headline's stream plan (the decode's acceptance pass on a
+    # second stream beside the encode, its payload pass after the encode)
+    ctx_dec, s_dec = ctx, stream
+    if split:
+        s_dec = torch.cuda.Stream(dev)
+        ctx_dec = fec.Context(dev.index if dev.index is not None else 0, s_dec.cuda_stream)
+        dec_args["ctx"] = ctx_dec
+
     def step(ev):
         ev[0].record(stream)
+        if split:
+            s_dec.wait_event(ev[0])
         fec.encode_batch(src, rep, k, r, Lb, **enc_args)
         ev[1].record(stream)
+        if split:
+            ctx_dec.set_payload_wait(ev[1])
         fec.decode_batch(rows, row_index, rec, rec_index, n_rec, status, k, r, Lb, **dec_args)
+        if split:
+            e_d = torch.cuda.Event()
+            e_d.record(s_dec)
+            stream.wait_event(e_d)
         ev[2].record(stream)
 
     for _ in range(max(1, warmup)):
@@ -650,6 +670,8 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     ctx.profile(True)
+    if split:
+        ctx_dec.profile(True)
     t0 = time.perf_counter()
     for s_ in range(steps):
         step(evs[s_])
@@ -660,6 +682,9 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
     step_ms = (time.perf_counter() - t0) * 1e3 / steps
     kt = ctx.kernel_times()
     ctx.profile(False)
+    if split:
+        kt.update(ctx_dec.kernel_times())
+        ctx_dec.profile(False)
     enc_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
     er_t = torch.from_numpy(erased).to(dev)
@@ -680,6 +705,8 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
     src_total = world * G * k * Lb
     del src, rep, rows, rec, rec_index, n_rec, status, row_index, aidx_t
     torch.cuda.empty_cache()
+    if split:
+        ctx_dec.close()
     return {"workload": f"C4: {G:,} generations = {G * k:,} packets of {Lb} B per rank, encode (r={r}, zero-tail "
                         f"repair rows) then decode with {e} erased sources per generation; independent generations "
                         f"sharded over {world} rank(s), no data-path collective",
@@ -689,6 +716,7 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
             "encode_gibps": round(src_total / (enc_max / 1e3) / 2**30, 3),
             "decode_gibps": round(src_total / (dec_max / 1e3) / 2**30, 3),
             "kernel_ms_per_launch": {n: round(ms / max(1, c), 4) for n, (c, ms) in kt.items()},
+            "schedule": "split" if split else "serial",
             "oracle_sample_generations_per_rank": rank_sample, "verified": bad == 0}
 
 
