@@ -26,7 +26,8 @@ OUT_DIR = PKG / "lib"
 LIB = OUT_DIR / "libqf_fec.so"
 LIB_ROCM = OUT_DIR / "libqf_fec_rocm.so"
 SOURCES = ["qf_kernels.hip", "qf_api.hip", "qf_objects.hip", "qf_bs.hip", "qf_adaptive.hip", "qf_wire.hip",
-           "qf_gf16.hip", "qf_objects16.hip", "qf_wiedemann.hip", "qf_gf16_bs.hip"]
+           "qf_gf16.hip", "qf_objects16.hip", "qf_wiedemann.hip", "qf_gf16_bs.hip",
+           "qf_gf16_fft.hip"]
 # (k, r) Cauchy configurations that get a bit-sliced assembly kernel
 # (bs_codegen.py); every other shape runs the general v_perm kernel.
 BS_CONFIGS = [(64, 16), (64, 10), (32, 16), (16, 16), (16, 1), (32, 5), (48, 8), (96, 15)]

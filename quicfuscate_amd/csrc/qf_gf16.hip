@@ -763,7 +763,7 @@ __global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint
     const uint32_t g = blockIdx.z, tid = threadIdx.x;
     const BigArgs a = view(A, g);
     const uint32_t k = a.k;
-    __shared__ uint32_t cnt[64];
+    __shared__ uint32_t seen[2048];   // repairs k + j seen (j < 65,536)
     __shared__ uint32_t s_bad;
     uint16_t* sm = smap + (uint64_t)g * k;
     uint16_t* rp = rpos + (uint64_t)g * r;
@@ -775,22 +775,19 @@ __global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint
         rp[j] = 0xFFFF;
         rsl[j] = 0;
     }
-    cnt[tid] = 0;
+    for (uint32_t w = tid; w < 2048; w += 64) seen[w] = 0;
     if (tid == 0) s_bad = 0;
     __syncthreads();
     for (uint32_t c = tid; c < nin; c += 64) sm[a.w.Scol[c]] = a.w.Sslot[c];   // columns distinct (else ERANK)
     for (uint32_t q = tid; q < e; q += 64) {
         const uint32_t j = (uint32_t)a.w.J[q] - k;
-        if (j < r) {
-            atomicAdd(&cnt[j], 1u);
+        if (j < r && !(atomicOr(&seen[j >> 5], 1u << (j & 31)) & (1u << (j & 31)))) {
             rp[j] = (uint16_t)q;
             rsl[j] = a.w.Jslot[q];
         } else {
-            s_bad = 1;
+            s_bad = 1;   // no Cauchy row of the kernel, or the same repair twice
         }
     }
-    __syncthreads();
-    if (tid < r && cnt[tid] > 1) s_bad = 1;
     __syncthreads();
     if (tid == 0) {
         skip[g] = (!ok || e == 0 || s_bad) ? 1u : 0u;
@@ -798,8 +795,10 @@ __global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint
     }
 }
 
-// mlog[a][c] = log C[J_a][Scol c] (syndromes: rows_J ^ C[J,S] x_S)
-__global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs A) {
+// mlog[a][c] = log C[J_a][Scol c] (syndromes: rows_J ^ C[J,S] x_S); with
+// nout_fb only for the generations the bit-sliced / FFT kernels leave to the matvec
+__global__ void __launch_bounds__(256) k_dec16_synmat(BigArgs A, const uint32_t* nout_fb) {
+    if (nout_fb && nout_fb[blockIdx.z] == 0) return;
     const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e, ns = a.w.st->nin, k = a.k;
     const uint64_t total = (uint64_t)e * ns;
@@ -1110,6 +1109,23 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
     const uint16_t *glog, *gexp;
     s = qf::ctx_gf16_tables(ctx, &glog, &gexp);
     if (s) return s;
+    // power-of-two windows: the additive FFT (qf_gf16_fft.hip), O(k log k)
+    // products per column instead of k r
+    if (!coeff_rxk && qf::ctx_opt(ctx, QF_OPT_GF16_FFT) && qf::gf16_fft_has(k, r, first)) {
+        const size_t fb = align256(2 * (3ull * k)), mb = coeff_be_dev ? align256((size_t)r * k * 2) : 0;
+        uint8_t* w;
+        s = qf::ctx_work(ctx, fb + mb, &w);
+        if (s) return s;
+        if (coeff_be_dev) {   // the repairs' coefficient blocks (framing)
+            const uint64_t n = (uint64_t)r * k;
+            hipLaunchKernelGGL(k_cauchy16_logs, dim3((uint32_t)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256),
+                               0, st, reinterpret_cast<uint16_t*>(w + fb), k, r, first, rot, glog, gexp, coeff_be_dev);
+            QF_HIP(hipGetLastError());
+        }
+        s = qf::gf16_fft_encode(ctx, st, k, r, first, rot, L, G, src, sh->src_gen_stride, sh->src_row_stride, rep,
+                                sh->rep_gen_stride, sh->rep_row_stride, glog, gexp, w);
+        if (s != qf::kGf16BsNone) return s;
+    }
     const size_t cb = align256((size_t)r * k * 2), ab = matvec_acc_bytes(ctx, G, r, k, L);
     uint8_t* w;
     s = qf::ctx_work(ctx, cb + ab, &w);
@@ -1229,15 +1245,20 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     // from qf_gf16bs_syn_* (maps 13..17, zero row), the general matvec only
     // for the generations it skips
     const bool bs = !row_coeffs && r <= 64 && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED) && qf::gf16_bs_has(k, r);
+    // power-of-two k without one: the additive-FFT syndromes (qf_gf16_fft.hip)
+    // over the same maps, constants in workspace slab 20
+    const bool fft = !bs && !row_coeffs && qf::ctx_opt(ctx, QF_OPT_GF16_FFT) && qf::gf16_fft_has(k, r, 0);
+    const bool maps = bs || fft;
     const size_t per_gen[18] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
                                 row_coeffs ? 4 * em * em : 0, 4 * em, 4 * em, 16 * em, Lp * em,
-                                bs ? 2ull * k : 0, bs ? 2ull * r : 0, bs ? 2ull * r : 0, bs ? 4u : 0u, bs ? 4u : 0u};
+                                maps ? 2ull * k : 0, maps ? 2ull * r : 0, maps ? 2ull * r : 0, maps ? 4u : 0u,
+                                maps ? 4u : 0u};
     size_t gen_bytes = 0;
     for (int q = 0; q < 18; ++q) gen_bytes += per_gen[q];
     // chunk: <= 65535 generations (grid z) and about 1 GiB of workspace
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)G, 65535ull,
                                                                              (1ull << 30) / gen_bytes}));
-    size_t off[20], tot = 0;
+    size_t off[21], tot = 0;
     for (int q = 0; q < 18; ++q) {
         off[q] = tot;
         tot += align256(std::max<size_t>(per_gen[q] * chunk, 1));
@@ -1249,6 +1270,8 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     const size_t zero_bytes = bs ? align256(64 * ((((size_t)L + 15) / 16 + 3) / 4) + 64) : 0;
     off[19] = tot;
     tot += zero_bytes;
+    off[20] = tot;
+    tot += fft ? align256(2 * (3ull * k)) : 0;
     s = qf::ctx_work(ctx, tot, &w);
     if (s) return s;
     if (bs) QF_HIP(hipMemsetAsync(w + off[19], 0, zero_bytes, st));
@@ -1288,7 +1311,16 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         uint32_t acc_threads = 64;
         while (acc_threads * 4 < k) acc_threads <<= 1;
         hipLaunchKernelGGL(k_dec16_accept, dim3(1, 1, gc), dim3(acc_threads), 0, st, b);
-        hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid, 1, gc), dim3(256), 0, st, b);
+        // the maps of the bit-sliced / FFT syndrome kernels; the matvec's
+        // coefficient logs then only for the generations those skip
+        uint16_t* smap = reinterpret_cast<uint16_t*>(w + off[13]);
+        uint16_t* rpos = reinterpret_cast<uint16_t*>(w + off[14]);
+        uint16_t* rslot = reinterpret_cast<uint16_t*>(w + off[15]);
+        uint32_t* skip = reinterpret_cast<uint32_t*>(w + off[16]);
+        uint32_t* nout_fb = maps ? reinterpret_cast<uint32_t*>(w + off[17]) : nullptr;
+        if (maps)
+            hipLaunchKernelGGL(k_dec16_bsmaps, dim3(1, 1, gc), dim3(64), 0, st, b, r, smap, rpos, rslot, skip, nout_fb);
+        hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid, 1, gc), dim3(256), 0, st, b, nout_fb);
         if (!row_coeffs) {
             uint32_t prod_threads = 64;
             while (prod_threads < e_max && prod_threads < 256) prod_threads <<= 1;
@@ -1310,18 +1342,15 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         QF_HIP(hipGetLastError());
         qf::ctx_prof_end(ctx, st, ev, "k_dec16_prepare_large");
         // syndromes s_a = row(J_a) ^ C[J_a, S] x_S
-        uint32_t* nout_fb = nullptr;
         if (bs) {
-            uint16_t* smap = reinterpret_cast<uint16_t*>(w + off[13]);
-            uint16_t* rpos = reinterpret_cast<uint16_t*>(w + off[14]);
-            uint16_t* rslot = reinterpret_cast<uint16_t*>(w + off[15]);
-            uint32_t* skip = reinterpret_cast<uint32_t*>(w + off[16]);
-            nout_fb = reinterpret_cast<uint32_t*>(w + off[17]);
-            hipLaunchKernelGGL(k_dec16_bsmaps, dim3(1, 1, gc), dim3(64), 0, st, b, r, smap, rpos, rslot, skip, nout_fb);
-            QF_HIP(hipGetLastError());
             s = qf::gf16_bs_syndromes(ctx, st, k, r, L, gc, rows + (size_t)g0 * sh->rows_gen_stride,
                                       sh->rows_gen_stride, sh->row_stride, smap, k, rpos, rslot, skip, w + off[19],
                                       b.w.synd, em * Lp, Lp);
+            if (s) return s;
+        } else if (fft) {
+            s = qf::gf16_fft_syndromes(ctx, st, k, r, L, gc, rows + (size_t)g0 * sh->rows_gen_stride,
+                                       sh->rows_gen_stride, sh->row_stride, smap, rpos, rslot, skip, b.w.synd, em * Lp,
+                                       Lp, glog, gexp, w + off[20]);
             if (s) return s;
         }
         Mv16Args sy{};
@@ -1343,7 +1372,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         sy.mrs = k;
         // (bs: only the generations the bit-sliced kernel skipped, rows gathered
         // as symbols: no logify pass over the whole batch)
-        sy.nout_g = bs ? nout_fb : n_rec + g0;
+        sy.nout_g = maps ? nout_fb : n_rec + g0;
         sy.nin_g = &b.w.st->nin;
         sy.nin_gs = sizeof(Dec16State) / 4;
         sy.log = glog;
@@ -1351,7 +1380,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         sy.nout = e_max;
         sy.nin = k;
         sy.L = L;
-        s = launch_matvec(ctx, st, sy, gc, bs ? "k_syndromes16_fallback" : "k_syndromes16", acc, acc_bytes, !bs);
+        s = launch_matvec(ctx, st, sy, gc, maps ? "k_syndromes16_fallback" : "k_syndromes16", acc, acc_bytes, !maps);
         if (s) return s;
         // x_E = C[J,E]^-1 s
         Mv16Args so{};

@@ -1,0 +1,411 @@
+// qf_gf16_fft.hip -- GF(2^16) Cauchy encode for k = 2^a by the additive FFT
+// (Extreme mode's windows, k = 1,024 .. 4,096 in
+// adaptive.rs:131, and every other power-of-two k without a bit-sliced kernel).
+//
+// Encoder16 (decoder.rs:10-88) forms repair j as sum_i C[j][i] x_i with
+// C[j][i] = gf16_inv(i ^ (k + j)) (decoder.rs:77-80): k r products per symbol
+// column, 1,048,576 for a 1,024-source window with 1,024 repairs.  For
+// k = 2^a the source points V = {0 .. k-1} are a GF(2)-subspace of GF(2^16)
+// and the repair points k + j (first + r <= k) lie on its coset k + V, so (the
+// algebra of lch_fft.py, which does the same for GF(2^8)):
+//     p_j = kappa f(k + j),  kappa = Delta / P_V(k),
+// f the degree < k polynomial interpolating the sources over V.  f comes from
+// an inverse Lin-Chung-Han transform over V (a layers of k/2 butterflies), is
+// folded onto the R-point coset k + V_b (R = 2^b >= first + r) with the
+// factors prod_{q in [b, a), bit q of i} xhat(q, k) and kappa, and evaluated
+// there by a forward transform (b layers of R/2 butterflies): about
+// (a k / 2 + k + b R / 2) products per column, 11,264 instead of 1,048,576
+// for k = r = 1,024.
+//
+// Every constant derives from W_q(2^m), W_q the subspace polynomial of
+// {0 .. 2^q - 1} (GF(2)-linear in t):
+//     W_0(t) = t,  W_{q+1}(t) = W_q(t) (W_q(t) + W_q(2^q)),
+//     xhat(q, t) = W_q(t) / W_q(2^q),  Delta = prod_{q<a} W_q(2^q),  P_V(k) = W_a(k),
+// a 16 x 16 table the host builds with ~250 products and passes by value;
+// k_fft16_consts turns it into the log-form butterfly constants.  The numpy
+// restatement in tests/test_gf16_fft_cpu.py runs the same schedule against the
+// oracle.
+//
+// Layout: one workgroup per (generation, strip of S symbol columns); the k x S
+// strip sits in LDS as u16 symbols (row-major), every layer is one pass of
+// butterflies over (butterfly, column) pairs and a barrier; a product is
+// exp[log y + log s] from the device tables (L2-resident, 384 KiB).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "qf_fec.h"
+#include "qf_internal.h"
+
+namespace {
+
+constexpr uint32_t kNoLog16 = 0xFFFF;   // log of 0 (no product)
+constexpr uint32_t kOrd16 = 65535;
+constexpr uint32_t kFftThreads = 256;
+constexpr uint32_t kFftLdsSymbols = 16384;   // 32 KiB strips (k = 32,768: 64 KiB, S = 1)
+constexpr uint32_t kFftMinK = 16;
+
+#define QF_HIP(x)                                 \
+    do {                                          \
+        if ((x) != hipSuccess) return QF_EDEVICE; \
+    } while (0)
+
+struct Fft16Table {
+    uint16_t W[16][16];   // W[q][m] = W_q(2^m), q <= a
+    uint16_t xk[16];      // xhat(q, k), q < a
+    uint16_t kappa;
+};
+
+struct Fft16ConstArgs {
+    Fft16Table t;
+    uint16_t* out;        // [k - 1 inverse][k fold][R - 1 forward], logs
+    const uint16_t* glog;
+    uint32_t k, a, R, b;
+};
+
+struct Fft16Args {
+    const uint8_t* src;
+    uint64_t sgs, srs;
+    uint8_t* rep;
+    uint64_t rgs, rrs;
+    const uint16_t* cst;  // k_fft16_consts output
+    const uint16_t* glog;
+    const uint16_t* gexp;
+    uint32_t k, a, R, b, r, first, rot, nsym, S, lgS;
+    // decode syndromes (syn != 0; qf_gf16.hip k_dec16_bsmaps): src = the
+    // received rows, source i at slot smap[g k + i] (0xFFFF: erased, reads
+    // zero); output row rpos[g r + t] (0xFFFF: none) = coset value t XOR the
+    // accepted row of repair k + t (slot rslot[g r + t]); skip[g]: not ours
+    const uint16_t* smap;
+    const uint16_t* rpos;
+    const uint16_t* rslot;
+    const uint32_t* skip;
+    uint32_t syn;
+};
+
+__device__ __forceinline__ uint32_t wq_at(const Fft16Table& t, uint32_t q, uint32_t x) {
+    uint32_t v = 0;
+    for (uint32_t m = 0; x; ++m, x >>= 1)
+        if (x & 1) v ^= t.W[q][m];
+    return v;
+}
+
+__device__ __forceinline__ uint32_t lg_of(const uint16_t* glog, uint32_t v) { return v ? glog[v] : kNoLog16; }
+
+__device__ __forceinline__ uint32_t lg_mul(uint32_t la, uint32_t lb) {
+    if (la == kNoLog16 || lb == kNoLog16) return kNoLog16;
+    const uint32_t s = la + lb;
+    return s >= kOrd16 ? s - kOrd16 : s;
+}
+
+// log xhat(q, x) = log W_q(x) - log W_q(2^q)
+__device__ __forceinline__ uint32_t lg_xhat(const Fft16ConstArgs& a, uint32_t q, uint32_t x) {
+    const uint32_t lw = lg_of(a.glog, wq_at(a.t, q, x));
+    if (lw == kNoLog16) return kNoLog16;
+    const uint32_t ld = a.glog[a.t.W[q][q]];
+    return lw >= ld ? lw - ld : lw + kOrd16 - ld;
+}
+
+__global__ void __launch_bounds__(256) k_fft16_consts(Fft16ConstArgs a) {
+    const uint32_t n_inv = a.k - 1, n_all = n_inv + a.k + a.R - 1;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n_all; e += gridDim.x * blockDim.x) {
+        uint32_t v;
+        if (e < n_inv) {             // inverse layer q: k >> (q + 1) blocks at k - (k >> q)
+            uint32_t q = 0;
+            while (e >= a.k - (a.k >> (q + 1))) ++q;
+            const uint32_t blk = e - (a.k - (a.k >> q));
+            v = lg_xhat(a, q, blk << (q + 1));
+        } else if (e < n_inv + a.k) {   // fold x kappa of source i
+            const uint32_t i = e - n_inv;
+            v = a.glog[a.t.kappa];
+            for (uint32_t q = a.b; q < a.a; ++q)
+                if (i >> q & 1) v = lg_mul(v, a.glog[a.t.xk[q]]);
+        } else {                     // forward layer q: R >> (q + 1) blocks at R - (R >> q)
+            const uint32_t f = e - n_inv - a.k;
+            uint32_t q = 0;
+            while (f >= a.R - (a.R >> (q + 1))) ++q;
+            const uint32_t blk = f - (a.R - (a.R >> q));
+            v = lg_xhat(a, q, a.k ^ (blk << (q + 1)));
+        }
+        a.out[e] = (uint16_t)v;
+    }
+}
+
+// bytes b0 b1 b2 b3 of two big-endian symbols <-> (b0 b1) | (b2 b3) << 16
+__device__ __forceinline__ uint32_t bswap_sym2(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x02030001u); }
+
+__device__ __forceinline__ uint32_t fmul(const uint16_t* __restrict__ glog, const uint16_t* __restrict__ gexp,
+                                         uint32_t ls, uint32_t y) {
+    // gexp holds 2 x 65,535 entries: no reduction of the sum
+    return (y && ls != kNoLog16) ? gexp[(uint32_t)glog[y] + ls] : 0u;
+}
+
+__global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint32_t g0) {
+    extern __shared__ uint16_t buf[];
+    const uint32_t S = A.S, lgS = A.lgS, k = A.k, tid = threadIdx.x;
+    const uint64_t g = g0 + blockIdx.y;
+    const uint32_t c0 = blockIdx.x << lgS;
+    const uint32_t ncol = min(S, A.nsym - c0);
+    const uint16_t* __restrict__ glog = A.glog;
+    const uint16_t* __restrict__ gexp = A.gexp;
+    if (A.syn && A.skip[g]) return;   // uniform over the block
+    const uint8_t* gsrc = A.src + g * A.sgs;
+    const uint16_t* smap = A.syn ? A.smap + g * k : nullptr;
+    // strip in: window position i reads ring slot (rot + i) mod k (decode:
+    // slot smap[i], none = zero); symbols are big-endian, two per dword
+    // (S >= 2; the rows are 16-byte aligned)
+    if (S >= 2) {
+        const uint32_t lgP = lgS - 1;
+        for (uint32_t p = tid; p < (k << lgP); p += kFftThreads) {
+            const uint32_t i = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
+            const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
+            const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * (c0 + c);
+            uint32_t v = 0;
+            if (slot == 0xFFFFu && smap)
+                v = 0;
+            else if (c + 1 < ncol)
+                v = bswap_sym2(*reinterpret_cast<const uint32_t*>(row));
+            else if (c < ncol)
+                v = ((uint32_t)row[0] << 8) | row[1];
+            reinterpret_cast<uint32_t*>(buf)[p] = v;
+        }
+    } else {
+        for (uint32_t i = tid; i < k; i += kFftThreads) {
+            const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
+            const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * c0;
+            buf[i] = (slot == 0xFFFFu && smap) ? 0 : (uint16_t)(((uint32_t)row[0] << 8) | row[1]);
+        }
+    }
+    __syncthreads();
+    const uint16_t* cinv = A.cst;
+    const uint16_t* cfk = A.cst + (k - 1);
+    const uint16_t* cfwd = cfk + k;
+    // inverse transform over V: y_j ^= y_i; y_i ^= s y_j
+    for (uint32_t q = 0; q < A.a; ++q) {
+        const uint32_t h = 1u << q;
+        const uint16_t* cq = cinv + (k - (k >> q));
+        for (uint32_t p = tid; p < ((k >> 1) << lgS); p += kFftThreads) {
+            const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
+            const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
+            uint32_t yi = buf[(i << lgS) + c];
+            const uint32_t yj = buf[(j << lgS) + c] ^ yi;
+            yi ^= fmul(glog, gexp, cq[blk], yj);
+            buf[(i << lgS) + c] = (uint16_t)yi;
+            buf[(j << lgS) + c] = (uint16_t)yj;
+        }
+        __syncthreads();
+    }
+    // fold onto the R-point coset, times kappa (in place: row t < R is written
+    // only by the thread that reads every row i = t mod R)
+    for (uint32_t p = tid; p < (A.R << lgS); p += kFftThreads) {
+        const uint32_t t = p >> lgS, c = p & (S - 1);
+        uint32_t acc = 0;
+        for (uint32_t i = t; i < k; i += A.R) acc ^= fmul(glog, gexp, cfk[i], buf[(i << lgS) + c]);
+        buf[p] = (uint16_t)acc;
+    }
+    __syncthreads();
+    // forward transform over k + V_b: d_i ^= s d_j; d_j ^= d_i
+    for (uint32_t q = A.b; q-- > 0;) {
+        const uint32_t h = 1u << q;
+        const uint16_t* cq = cfwd + (A.R - (A.R >> q));
+        for (uint32_t p = tid; p < ((A.R >> 1) << lgS); p += kFftThreads) {
+            const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
+            const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
+            const uint32_t dj = buf[(j << lgS) + c];
+            const uint32_t di = buf[(i << lgS) + c] ^ fmul(glog, gexp, cq[blk], dj);
+            buf[(i << lgS) + c] = (uint16_t)di;
+            buf[(j << lgS) + c] = (uint16_t)(dj ^ di);
+        }
+        __syncthreads();
+    }
+    // repairs first .. first + r - 1 = coset points t = first + jj (decode:
+    // the syndrome of the accepted repair k + jj, its received row XORed in)
+    const uint16_t* rpos = A.syn ? A.rpos + g * A.r : nullptr;
+    const uint16_t* rslot = A.syn ? A.rslot + g * A.r : nullptr;
+    if (S >= 2) {
+        const uint32_t lgP = lgS - 1;
+        for (uint32_t p = tid; p < (A.r << lgP); p += kFftThreads) {
+            const uint32_t jj = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
+            if (c >= ncol) continue;
+            uint32_t v = reinterpret_cast<const uint32_t*>(buf)[(((A.first + jj) << lgS) + c) >> 1];
+            uint64_t orow = jj;
+            const uint8_t* base = nullptr;
+            if (rpos) {
+                orow = rpos[jj];
+                if (orow == 0xFFFFu) continue;
+                base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * (c0 + c);
+            }
+            uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * (c0 + c);
+            if (c + 1 < ncol) {
+                if (base) v ^= bswap_sym2(*reinterpret_cast<const uint32_t*>(base));
+                *reinterpret_cast<uint32_t*>(o) = bswap_sym2(v);
+            } else {
+                if (base) v ^= ((uint32_t)base[0] << 8) | base[1];
+                o[0] = (uint8_t)(v >> 8);
+                o[1] = (uint8_t)v;
+            }
+        }
+    } else {
+        for (uint32_t jj = tid; jj < A.r; jj += kFftThreads) {
+            uint32_t v = buf[A.first + jj];
+            uint64_t orow = jj;
+            if (rpos) {
+                orow = rpos[jj];
+                if (orow == 0xFFFFu) continue;
+                const uint8_t* base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * c0;
+                v ^= ((uint32_t)base[0] << 8) | base[1];
+            }
+            uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * c0;
+            o[0] = (uint8_t)(v >> 8);
+            o[1] = (uint8_t)v;
+        }
+    }
+}
+
+uint32_t hmul16(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    while (b) {
+        if (b & 1) r ^= a;
+        b >>= 1;
+        a <<= 1;
+        if (a & 0x10000) a ^= 0x1100B;
+    }
+    return r;
+}
+
+uint32_t hinv16(uint32_t a) {   // a^65534, a != 0
+    uint32_t r = 1, x = a;
+    for (uint32_t p = 0xFFFE; p; p >>= 1) {
+        if (p & 1) r = hmul16(r, x);
+        x = hmul16(x, x);
+    }
+    return r;
+}
+
+}  // namespace
+
+namespace qf {
+
+bool gf16_fft_has(uint32_t k, uint32_t r, uint32_t first) {
+    return k >= kFftMinK && k <= 32768 && (k & (k - 1)) == 0 && r >= 1 && first + r <= k;
+}
+
+namespace {
+
+int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t L, uint8_t* work, const char* name) {
+    const uint32_t k = A.k, r = A.r, first = A.first;
+    uint32_t a = 0, R = 1, b = 0;
+    while ((1u << a) < k) ++a;
+    while (R < first + r) {
+        R <<= 1;
+        ++b;
+    }
+    // the table W_q(2^m), q = 0 .. a
+    Fft16ConstArgs ca{};
+    for (uint32_t m = 0; m < 16; ++m) ca.t.W[0][m] = (uint16_t)(1u << m);
+    for (uint32_t q = 0; q < a; ++q)
+        for (uint32_t m = 0; m < 16; ++m)
+            ca.t.W[q + 1][m] = (uint16_t)hmul16(ca.t.W[q][m], ca.t.W[q][m] ^ ca.t.W[q][q]);
+    auto w_at = [&](uint32_t q, uint32_t x) {
+        uint32_t v = 0;
+        for (uint32_t m = 0; x; ++m, x >>= 1)
+            if (x & 1) v ^= ca.t.W[q][m];
+        return v;
+    };
+    uint32_t delta = 1;
+    for (uint32_t q = 0; q < a; ++q) {
+        delta = hmul16(delta, ca.t.W[q][q]);
+        ca.t.xk[q] = (uint16_t)hmul16(w_at(q, k), hinv16(ca.t.W[q][q]));
+    }
+    ca.t.kappa = (uint16_t)hmul16(delta, hinv16(w_at(a, k)));
+    uint16_t* cst = reinterpret_cast<uint16_t*>(work);
+    ca.out = cst;
+    ca.glog = A.glog;
+    ca.k = k;
+    ca.a = a;
+    ca.R = R;
+    ca.b = b;
+    const uint32_t n_c = 2 * k + R - 2;
+    hipLaunchKernelGGL(k_fft16_consts, dim3(std::min<uint32_t>((n_c + 255) / 256, 1024)), dim3(256), 0, st, ca);
+    QF_HIP(hipGetLastError());
+    // strip width: 32 KiB of LDS, narrowed until the grid covers the CUs
+    const uint32_t nsym = L / 2;
+    uint32_t S = std::max<uint32_t>(1, kFftLdsSymbols / k), lgS = 0;
+    while ((1u << (lgS + 1)) <= S) ++lgS;
+    S = 1u << lgS;
+    const uint64_t want = 4ull * qf::ctx_num_cus(ctx);
+    while (S > 1 && (uint64_t)G * ((nsym + S - 1) / S) < want && S > 1) {
+        S >>= 1;
+        --lgS;
+    }
+    while (S > 1 && S / 2 >= nsym) {   // no strip wider than the row
+        S >>= 1;
+        --lgS;
+    }
+    A.cst = cst;
+    A.a = a;
+    A.R = R;
+    A.b = b;
+    A.nsym = nsym;
+    A.S = S;
+    A.lgS = lgS;
+    const uint32_t strips = (nsym + S - 1) / S;
+    const size_t lds = (size_t)k * S * 2;
+    hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
+    for (uint32_t g0 = 0; g0 < G; g0 += 65535) {
+        const uint32_t gc = std::min<uint32_t>(65535, G - g0);
+        hipLaunchKernelGGL(k_fft16_encode, dim3(strips, gc), dim3(kFftThreads), lds, st, A, g0);
+        QF_HIP(hipGetLastError());
+    }
+    qf::ctx_prof_end(ctx, st, ev, name);
+    return QF_OK;
+}
+
+}  // namespace
+
+int gf16_fft_encode(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint32_t first, uint32_t rot, uint32_t L,
+                    uint32_t G, const uint8_t* src, uint64_t sgs, uint64_t srs, uint8_t* rep, uint64_t rgs,
+                    uint64_t rrs, const uint16_t* glog, const uint16_t* gexp, uint8_t* work) {
+    if (!gf16_fft_has(k, r, first) || (L & 1)) return kGf16BsNone;
+    Fft16Args A{};
+    A.src = src;
+    A.sgs = sgs;
+    A.srs = srs;
+    A.rep = rep;
+    A.rgs = rgs;
+    A.rrs = rrs;
+    A.glog = glog;
+    A.gexp = gexp;
+    A.k = k;
+    A.r = r;
+    A.first = first;
+    A.rot = rot;
+    return fft16_launch(ctx, st, A, G, L, work, "k_fft16_encode");
+}
+
+int gf16_fft_syndromes(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint32_t L, uint32_t G,
+                       const uint8_t* rows, uint64_t rgs, uint64_t rs, const uint16_t* smap, const uint16_t* rpos,
+                       const uint16_t* rslot, const uint32_t* skip, uint8_t* synd, uint64_t synd_gs, uint64_t synd_rs,
+                       const uint16_t* glog, const uint16_t* gexp, uint8_t* work) {
+    if (!gf16_fft_has(k, r, 0) || (L & 1)) return kGf16BsNone;
+    Fft16Args A{};
+    A.src = rows;
+    A.sgs = rgs;
+    A.srs = rs;
+    A.rep = synd;
+    A.rgs = synd_gs;
+    A.rrs = synd_rs;
+    A.glog = glog;
+    A.gexp = gexp;
+    A.k = k;
+    A.r = r;
+    A.smap = smap;
+    A.rpos = rpos;
+    A.rslot = rslot;
+    A.skip = skip;
+    A.syn = 1;
+    return fft16_launch(ctx, st, A, G, L, work, "k_fft16_syndromes");
+}
+
+}  // namespace qf

@@ -1,0 +1,156 @@
+"""The additive-FFT GF(2^16) Cauchy encode (quicfuscate_amd/csrc/qf_gf16_fft.hip)
+restated in numpy and checked against the oracle's Encoder16 (oracle/qf_oracle16.c,
+decoder.rs:10-88 with the intended reduction) on the CPU.
+
+For k = 2^a the sources sit on the subspace V = {0 .. k-1} of GF(2^16) and the
+repair points k + j on its coset, so repair j = kappa * f(k + j) with f the
+polynomial interpolating the sources over V (the GF(2^8) derivation of
+quicfuscate_amd/lch_fft.py, same field-independent algebra).  The model uses
+exactly the constants the library's host code derives from the table
+W_q(2^m) (W_q = the subspace polynomial of {0 .. 2^q - 1}, GF(2)-linear):
+    W_0(t) = t,  W_{q+1}(t) = W_q(t) (W_q(t) + W_q(2^q)),
+    xhat(q, t) = W_q(t) / W_q(2^q),  Delta = prod_q W_q(2^q),  P_V(k) = W_a(k).
+The device kernel runs the same butterflies (tests/test_gpu_gf16.py)."""
+import numpy as np
+import pytest
+
+from quicfuscate_amd import gf16_codegen as g16
+
+POLY = 0x1100B
+
+
+def _tables():
+    exp = np.zeros(2 * 65535, np.int64)
+    log = np.full(65536, -1, np.int64)
+    x = 1
+    for i in range(65535):
+        exp[i] = x
+        log[x] = i
+        x <<= 1
+        if x & 0x10000:
+            x ^= POLY
+    exp[65535:] = exp[:65535]
+    return exp, log
+
+
+EXP, LOG = _tables()
+
+
+def vmul(c: int, y: np.ndarray) -> np.ndarray:
+    """c * y elementwise (y uint16 array)."""
+    if c == 0:
+        return np.zeros_like(y)
+    out = EXP[(LOG[y.astype(np.int64)] + int(LOG[c])) % 65535].astype(np.uint16)
+    out[y == 0] = 0
+    return out
+
+
+def smul(a: int, b: int) -> int:
+    return g16.mul(a, b)
+
+
+def constants(k: int, R: int):
+    """(inv layers, fold * kappa, forward layers) as the host code computes them."""
+    a, b = k.bit_length() - 1, R.bit_length() - 1
+    W = [[1 << m for m in range(16)]]                       # W_0(2^m) = 2^m
+    for q in range(a):
+        wq = W[q][q]
+        W.append([smul(w, w ^ wq) for w in W[q]])
+
+    def w_at(q, t):
+        v, m = 0, 0
+        while t:
+            if t & 1:
+                v ^= W[q][m]
+            t >>= 1
+            m += 1
+        return v
+
+    def xhat(q, t):
+        return smul(w_at(q, t), g16.inv(W[q][q]))
+
+    inv_l = [[xhat(q, o) for o in range(0, k, 2 << q)] for q in range(a)]
+    delta = 1
+    for q in range(a):
+        delta = smul(delta, W[q][q])
+    kappa = smul(delta, g16.inv(w_at(a, k)))
+    fk = []
+    for i in range(k):
+        f = kappa
+        for q in range(b, a):
+            if i >> q & 1:
+                f = smul(f, xhat(q, k))
+        fk.append(f)
+    fwd_l = [[xhat(q, k ^ o) for o in range(0, R, 2 << q)] for q in range(b)]
+    return inv_l, fk, fwd_l
+
+
+def fft_encode(x: np.ndarray, k: int, r: int, first: int = 0) -> np.ndarray:
+    """x: (k, n_sym) uint16 symbols -> repairs first .. first + r - 1, (r, n_sym)."""
+    R = 1
+    while R < first + r:
+        R <<= 1
+    a, b = k.bit_length() - 1, R.bit_length() - 1
+    inv_l, fk, fwd_l = constants(k, R)
+    y = x.astype(np.uint16).copy()
+    for q in range(a):                                      # inverse transform over V
+        h = 1 << q
+        for blk, o in enumerate(range(0, k, 2 * h)):
+            s = inv_l[q][blk]
+            for i in range(o, o + h):
+                y[i + h] ^= y[i]
+                y[i] ^= vmul(s, y[i + h])
+    d = np.zeros((R, x.shape[1]), np.uint16)
+    for i in range(k):                                      # fold onto the coset, times kappa
+        d[i % R] ^= vmul(fk[i], y[i])
+    for q in reversed(range(b)):                            # forward transform over k + V_b
+        h = 1 << q
+        for blk, o in enumerate(range(0, R, 2 * h)):
+            s = fwd_l[q][blk]
+            for i in range(o, o + h):
+                d[i] ^= vmul(s, d[i + h])
+                d[i + h] ^= d[i]
+    return d[first:first + r]
+
+
+def to_sym(rows: np.ndarray) -> np.ndarray:
+    return (rows[:, 0::2].astype(np.uint16) << 8) | rows[:, 1::2]
+
+
+def to_bytes(sym: np.ndarray) -> np.ndarray:
+    out = np.zeros((sym.shape[0], 2 * sym.shape[1]), np.uint8)
+    out[:, 0::2] = sym >> 8
+    out[:, 1::2] = sym & 0xFF
+    return out
+
+
+def test_recurrence_is_the_subspace_polynomial():
+    # W_q(t) = prod_{u < 2^q} (t + u), checked directly for small q
+    for q in range(4):
+        for t in (1, 5, 0x1234, 0xFFFF):
+            want = 1
+            for u in range(1 << q):
+                want = smul(want, t ^ u)
+            inv_l, _, _ = constants(1 << (q + 1), 1)
+            W = [[1 << m for m in range(16)]]
+            for qq in range(q):
+                W.append([smul(w, w ^ W[qq][qq]) for w in W[qq]])
+            got, m, tt = 0, 0, t
+            while tt:
+                if tt & 1:
+                    got ^= W[q][m]
+                tt >>= 1
+                m += 1
+            assert got == want, (q, t)
+
+
+@pytest.mark.parametrize("k,r,first", [(2, 1, 0), (2, 2, 0), (4, 3, 0), (8, 8, 0), (16, 5, 0), (64, 16, 0),
+                                       (64, 64, 0), (128, 96, 0), (256, 3, 100), (32, 7, 20), (512, 512, 0)])
+def test_fft_matches_oracle(oracle, k, r, first):
+    rng = np.random.default_rng(k * 31 + r + first)
+    L = 6
+    rows = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    rows[0, :2] = 0
+    out = to_bytes(fft_encode(to_sym(rows), k, r, first))
+    ref = oracle.encode16(rows, first + r)[first:]
+    assert np.array_equal(out, ref)

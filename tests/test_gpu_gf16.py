@@ -367,3 +367,119 @@ def test_decode16_bitsliced_syndromes(qf, oracle, gpu_ctx):
     res2 = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
     for x, y in zip(res[:4], res2[:4]):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("k,r,L,G", [(16, 5, 100, 3), (32, 32, 2, 4), (128, 96, 200, 2), (256, 1, 34, 5),
+                                     (1024, 1024, 64, 1), (1024, 8, 1200, 2), (4096, 100, 32, 1),
+                                     (32768, 16, 4, 1), (64, 33, 1200, 9)])
+def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G):
+    """Power-of-two windows without a bit-sliced kernel run the additive-FFT
+    kernel (qf_gf16_fft.hip): bit-exact against the oracle's Encoder16 and
+    against the general k_matvec16 path (gf16_fft = 0); guard bytes outside
+    [0, L) of every repair row untouched (run_encode16)."""
+    rng = np.random.default_rng(k * 13 + r + L)
+    src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
+    src[0, 0, :4] = 0
+    src[-1, -1, -2:] = 0
+    gpu_ctx.profile(True)
+    rep = run_encode16(qf, src, r)
+    names = set(gpu_ctx.kernel_times())
+    gpu_ctx.profile(False)
+    assert "k_fft16_encode" in names, names
+    for g in range(G):
+        assert np.array_equal(rep[g], oracle.encode16(src[g], r)), g
+    if k <= 1024:
+        qf.set_default_options(gf16_fft=0)
+        assert np.array_equal(rep, run_encode16(qf, src, r))
+
+
+def test_encode16_fft_many_generations(qf, oracle, gpu_ctx):
+    """More generations than one launch's grid.y (65,535): sampled generations
+    against the oracle."""
+    import torch
+
+    k, r, L, G = 16, 3, 4, 70000
+    rng = np.random.default_rng(70000)
+    src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
+    t_src = torch.from_numpy(src.reshape(-1)).to("cuda")
+    t_rep = torch.zeros(G * r * 16, dtype=torch.uint8, device="cuda")
+    qf.encode16_batch(t_src, t_rep, k, r, L, src_row_stride=L, src_gen_stride=k * L, rep_row_stride=16,
+                      rep_gen_stride=r * 16, G=G)
+    qf.default_context().sync()
+    rep = t_rep.cpu().numpy().reshape(G, r, 16)[:, :, :L]
+    for g in [0, 1, 65534, 65535, 65536, 69999] + rng.integers(0, G, 20).tolist():
+        assert np.array_equal(rep[g], oracle.encode16(src[g], r)), g
+
+
+def test_encoder16_fft_window_slides(qf, oracle, gpu_ctx):
+    """Encoder16 over a power-of-two window (decoder.rs:25-75): after the
+    window slides (ring rotation) and for a repair range starting past 0, the
+    FFT kernel's repairs equal the oracle's Cauchy rows over the window."""
+    k, L = 64, 40
+    rng = np.random.default_rng(64)
+    src = rng.integers(0, 256, (k + 5, L), dtype=np.uint8)
+    enc = qf.Encoder16(k, k + 12)
+    for i in range(k + 5):
+        enc.add_source_packet(qf.Packet(i, bytearray(src[i].tobytes()), L, True))
+    want = oracle.encode16(np.ascontiguousarray(src[5:]), 12)
+    C = oracle.cauchy16(k, 12)
+    gpu_ctx.profile(True)
+    got = [enc.generate_repair_packet(j) for j in (0, 7)] + enc.generate_repairs(3, 9)
+    names = set(gpu_ctx.kernel_times())
+    gpu_ctx.profile(False)
+    assert "k_fft16_encode" in names, names
+    assert got[0].payload() == want[0].tobytes() and got[1].payload() == want[7].tobytes()
+    for n, p in enumerate(got[2:]):
+        assert p.payload() == want[3 + n].tobytes(), n
+        assert p.coeff_len == 2 * k
+        assert bytes(p.coefficients[: 2 * k]) == np.asarray(C[3 + n], dtype=">u2").tobytes(), n
+
+
+@pytest.mark.parametrize("k,r,L", [(128, 40, 100), (256, 256, 34), (32, 16, 2)])
+def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
+    """Cauchy decode of a power-of-two k without a bit-sliced kernel: the
+    syndromes come from the additive FFT (k_fft16_syndromes, sources gathered
+    through the slot map, erased ones as zero rows, the accepted repair row
+    XORed in), the general matvec only for the generation with a repair index
+    past k + r; statuses, recovered bytes and indices equal the oracle's and
+    the general path's (gf16_fft = 0).  Mixed erasure counts, a full-erasure,
+    an erasure-free, a short and a duplicate-row generation."""
+    rng = np.random.default_rng(k + r + L)
+    src, gens = make_gens(oracle, rng, k, r, L, 6)
+    e_full = min(k, r)
+    _, full = make_gens(oracle, rng, k, r, L, 1, erase=e_full)
+    _, none = make_gens(oracle, rng, k, r, L, 1, erase=0)
+    _, short = make_gens(oracle, rng, k, r, L, 1, erase=min(5, e_full), short=True)
+    _, dup = make_gens(oracle, rng, k, r, L, 1, erase=min(3, e_full), dup=True)
+    src = np.concatenate([src, src[:4]])
+    gens += [full[0], none[0], short[0], dup[0]]
+    # generation 0: one accepted repair row is Cauchy row k + r + 3 (past the FFT's coset rows)
+    arr, rows, rc = gens[0]
+    extra = r + 3
+    if k + extra < 65536 and any(a < k for a in arr[:k]):
+        far = oracle.encode16(src[0], extra + 1)[extra]
+        pos = next(s for s, a in enumerate(arr[:k]) if a < k)
+        gens[0] = ([k + extra] + [a for s, a in enumerate(arr) if s != pos],
+                   np.concatenate([far[None], np.delete(rows, pos, 0)]), None)
+    G = len(gens)
+    gpu_ctx.profile(True)
+    res = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
+    names = set(gpu_ctx.kernel_times())
+    gpu_ctx.profile(False)
+    assert "k_fft16_syndromes" in names and "k_syndromes16_fallback" in names, names
+    rec, ri, nrec, st, rrs, rec_gs = res
+    for g, (a, rw, _) in enumerate(gens):
+        ost, out, mask = oracle.decode16(k, a, rw, None)
+        assert st[g] == ost, (g, st[g], ost)
+        if ost:
+            assert nrec[g] == 0
+            continue
+        erased = [i for i in range(k) if not mask[i]]
+        assert nrec[g] == len(erased) and ri[g, : len(erased)].tolist() == erased, g
+        for b, i in enumerate(erased):
+            o = g * rec_gs + b * rrs
+            assert np.array_equal(rec[o: o + L], out[i]), (g, i)
+    qf.set_default_options(gf16_fft=0)
+    res2 = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
+    for x, y in zip(res[:4], res2[:4]):
+        assert np.array_equal(x, y)

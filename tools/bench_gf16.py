@@ -111,6 +111,36 @@ def main():
         print(name, json.dumps({kk: v for kk, v in res.items() if kk.startswith(name)}), flush=True)
         del src, rep, rows, rec
 
+    # encode only: more power-of-two windows (additive FFT), and the general
+    # k_matvec16 kernel on the same inputs (gf16_fft = 0) for comparison
+    for name, k, r, L, G in (("extreme_k1024_x64", 1024, 1024, 1200, 64), ("extreme_k4096_n8192", 4096, 4096, 1200, 1),
+                             ("k128_r32_x2048", 128, 32, 1200, 2048), ("extreme_k1024_x16", 1024, 1024, 1200, 16)):
+        rs = _r16(L)
+        src = torch.randint(0, 256, (G * k * rs,), dtype=torch.uint8, device="cuda")
+        rep = torch.empty(G * r * rs, dtype=torch.uint8, device="cuda")
+
+        def enc():
+            qf.encode16_batch(src, rep, k, r, L, src_row_stride=rs, src_gen_stride=k * rs, rep_row_stride=rs,
+                              rep_gen_stride=r * rs, G=G)
+
+        for mode in ("fft", "matvec"):
+            qf.set_default_options(gf16_fft=1 if mode == "fft" else 0)
+            if mode == "matvec" and k > 1024:
+                continue
+            wall, kt = timed(ctx, enc, a.reps)
+            kms = sum(ms for _, ms in kt.values())
+            res[f"{name}/encode16_{mode}"] = {"k": k, "r": r, "L": L, "G": G, "wall_ms": round(wall, 3),
+                                             "kernels": kt,
+                                             "GiBps_alg": round(G * (k + r) * L / (kms / 1e3) / 2**30, 1)}
+            if mode == "fft":
+                out_fft = rep.clone()
+            else:
+                res[f"{name}/encode16_{mode}"]["same_bytes_as_fft"] = bool(
+                    torch.equal(rep.view(G, r, rs)[:, :, :L], out_fft.view(G, r, rs)[:, :, :L]))
+            print(name, mode, json.dumps(res[f"{name}/encode16_{mode}"]), flush=True)
+        qf.reset_default_options()
+        del src, rep
+
     # oracle single thread, one generation of each shape (CPU reference point)
     for name, k, r, L in (("batched_k64_r16", 64, 16, 1200), ("extreme_k1024_n2048", 1024, 1024, 1200)):
         s = rng.integers(0, 256, (k, L), dtype=np.uint8)
