@@ -969,7 +969,9 @@ int ctx_work(qf_ctx* ctx, size_t bytes, uint8_t** out) {
 }
 int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp) {
     if (!ctx->d_gf16_log) {
-        std::vector<uint16_t> lg(65536, 0xFFFF), ex(2 * 65535);  // log 0: 0xFFFF (no product)
+        // log 0: 0xFFFF (no product); entries 65,536.. hold the Zech logs
+        // Z[d] = log(1 + alpha^d) (Z[0] = log 0) for ctx_gf16_zech
+        std::vector<uint16_t> lg(2 * 65536, 0xFFFF), ex(2 * 65535);
         uint32_t x = 1;
         for (uint32_t i = 0; i < 65535; ++i) {  // generator 2 of GF(2^16) mod 0x1100B
             ex[i] = ex[i + 65535] = (uint16_t)x;
@@ -977,6 +979,7 @@ int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp) {
             x <<= 1;
             if (x & 0x10000u) x ^= 0x1100Bu;
         }
+        for (uint32_t d = 1; d < 65535; ++d) lg[65536 + d] = lg[1u ^ ex[d]];
         uint16_t *dl = nullptr, *de = nullptr;
         if (hipMalloc(&dl, lg.size() * 2) != hipSuccess) return QF_ENOMEM;
         if (hipMalloc(&de, ex.size() * 2) != hipSuccess) {
@@ -990,6 +993,13 @@ int ctx_gf16_tables(qf_ctx* ctx, const uint16_t** log, const uint16_t** exp) {
     }
     *log = ctx->d_gf16_log;
     *exp = ctx->d_gf16_exp;
+    return QF_OK;
+}
+int ctx_gf16_zech(qf_ctx* ctx, const uint16_t** zech) {
+    const uint16_t *lg, *ex;
+    const int s = ctx_gf16_tables(ctx, &lg, &ex);
+    if (s) return s;
+    *zech = lg + 65536;
     return QF_OK;
 }
 hipEvent_t ctx_prof_begin(qf_ctx* ctx, hipStream_t st) { return prof_begin(ctx, st); }

@@ -42,8 +42,8 @@ namespace {
 
 constexpr uint32_t kNoLog16 = 0xFFFF;   // log of 0 (no product)
 constexpr uint32_t kOrd16 = 65535;
-constexpr uint32_t kFftThreads = 256;
-constexpr uint32_t kFftLdsSymbols = 16384;   // 32 KiB strips (k = 32,768: 64 KiB, S = 1)
+constexpr uint32_t kFftThreads = 1024;
+constexpr uint32_t kFftLdsSymbols = 16384;   // 32 KiB strips beside the 128 KiB Zech table
 constexpr uint32_t kFftMinK = 16;
 
 #define QF_HIP(x)                                 \
@@ -72,7 +72,8 @@ struct Fft16Args {
     const uint16_t* cst;  // k_fft16_consts output
     const uint16_t* glog;
     const uint16_t* gexp;
-    uint32_t k, a, R, b, r, first, rot, nsym, S, lgS;
+    const uint16_t* zech;   // Z[d] = log(1 + alpha^d), 65,536 entries
+    uint32_t k, a, R, b, r, first, rot, nsym, S, lgS, strips;
     // decode syndromes (syn != 0; qf_gf16.hip k_dec16_bsmaps): src = the
     // received rows, source i at slot smap[g k + i] (0xFFFF: erased, reads
     // zero); output row rpos[g r + t] (0xFFFF: none) = coset value t XOR the
@@ -135,130 +136,161 @@ __global__ void __launch_bounds__(256) k_fft16_consts(Fft16ConstArgs a) {
 // bytes b0 b1 b2 b3 of two big-endian symbols <-> (b0 b1) | (b2 b3) << 16
 __device__ __forceinline__ uint32_t bswap_sym2(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x02030001u); }
 
-__device__ __forceinline__ uint32_t fmul(const uint16_t* __restrict__ glog, const uint16_t* __restrict__ gexp,
-                                         uint32_t ls, uint32_t y) {
-    // gexp holds 2 x 65,535 entries: no reduction of the sum
-    return (y && ls != kNoLog16) ? gexp[(uint32_t)glog[y] + ls] : 0u;
+// log-domain arithmetic (kNoLog16 = log 0): products add logs, sums go
+// through the Zech table Z[d] = log(1 + alpha^d) (Z[0] = log 0), in LDS
+__device__ __forceinline__ uint32_t lmul(uint32_t a, uint32_t b) {
+    uint32_t s = a + b;
+    s = s >= kOrd16 ? s - kOrd16 : s;
+    return (a == kNoLog16 || b == kNoLog16) ? kNoLog16 : s;
 }
 
-__global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint32_t g0) {
-    extern __shared__ uint16_t buf[];
+__device__ __forceinline__ uint32_t ladd(const uint16_t* Z, uint32_t a, uint32_t b) {
+    // alpha^a + alpha^b = alpha^a (1 + alpha^(b - a)); both indices stay < 65,536
+    uint32_t d = b + kOrd16 - a;
+    d = d >= kOrd16 ? d - kOrd16 : d;
+    const uint32_t z = Z[d];
+    uint32_t s = a + z;
+    s = s >= kOrd16 ? s - kOrd16 : s;
+    s = z == kNoLog16 ? kNoLog16 : s;
+    s = a == kNoLog16 ? b : s;
+    return b == kNoLog16 ? a : s;
+}
+
+// One workgroup per CU (the Zech table fills 128 KiB of LDS, the strip the
+// other 32 KiB), persistent over the (generation, strip) items.  The strip is
+// held as logs: a butterfly is two Zech lookups and a log sum, and only the
+// strip's load and store touch the global log / exp tables.
+__global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint32_t G) {
+    __shared__ uint16_t sz[65536];
+    __shared__ uint16_t buf[kFftLdsSymbols];
     const uint32_t S = A.S, lgS = A.lgS, k = A.k, tid = threadIdx.x;
-    const uint64_t g = g0 + blockIdx.y;
-    const uint32_t c0 = blockIdx.x << lgS;
-    const uint32_t ncol = min(S, A.nsym - c0);
     const uint16_t* __restrict__ glog = A.glog;
     const uint16_t* __restrict__ gexp = A.gexp;
-    if (A.syn && A.skip[g]) return;   // uniform over the block
-    const uint8_t* gsrc = A.src + g * A.sgs;
-    const uint16_t* smap = A.syn ? A.smap + g * k : nullptr;
-    // strip in: window position i reads ring slot (rot + i) mod k (decode:
-    // slot smap[i], none = zero); symbols are big-endian, two per dword
-    // (S >= 2; the rows are 16-byte aligned)
-    if (S >= 2) {
-        const uint32_t lgP = lgS - 1;
-        for (uint32_t p = tid; p < (k << lgP); p += kFftThreads) {
-            const uint32_t i = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
-            const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
-            const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * (c0 + c);
-            uint32_t v = 0;
-            if (slot == 0xFFFFu && smap)
-                v = 0;
-            else if (c + 1 < ncol)
-                v = bswap_sym2(*reinterpret_cast<const uint32_t*>(row));
-            else if (c < ncol)
-                v = ((uint32_t)row[0] << 8) | row[1];
-            reinterpret_cast<uint32_t*>(buf)[p] = v;
-        }
-    } else {
-        for (uint32_t i = tid; i < k; i += kFftThreads) {
-            const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
-            const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * c0;
-            buf[i] = (slot == 0xFFFFu && smap) ? 0 : (uint16_t)(((uint32_t)row[0] << 8) | row[1]);
-        }
+    {
+        const uint4* gz = reinterpret_cast<const uint4*>(A.zech);
+        uint4* lz = reinterpret_cast<uint4*>(sz);
+        for (uint32_t w = tid; w < 65536 / 8; w += kFftThreads) lz[w] = gz[w];
     }
-    __syncthreads();
     const uint16_t* cinv = A.cst;
     const uint16_t* cfk = A.cst + (k - 1);
     const uint16_t* cfwd = cfk + k;
-    // inverse transform over V: y_j ^= y_i; y_i ^= s y_j
-    for (uint32_t q = 0; q < A.a; ++q) {
-        const uint32_t h = 1u << q;
-        const uint16_t* cq = cinv + (k - (k >> q));
-        for (uint32_t p = tid; p < ((k >> 1) << lgS); p += kFftThreads) {
-            const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
-            const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
-            uint32_t yi = buf[(i << lgS) + c];
-            const uint32_t yj = buf[(j << lgS) + c] ^ yi;
-            yi ^= fmul(glog, gexp, cq[blk], yj);
-            buf[(i << lgS) + c] = (uint16_t)yi;
-            buf[(j << lgS) + c] = (uint16_t)yj;
-        }
-        __syncthreads();
-    }
-    // fold onto the R-point coset, times kappa (in place: row t < R is written
-    // only by the thread that reads every row i = t mod R)
-    for (uint32_t p = tid; p < (A.R << lgS); p += kFftThreads) {
-        const uint32_t t = p >> lgS, c = p & (S - 1);
-        uint32_t acc = 0;
-        for (uint32_t i = t; i < k; i += A.R) acc ^= fmul(glog, gexp, cfk[i], buf[(i << lgS) + c]);
-        buf[p] = (uint16_t)acc;
-    }
-    __syncthreads();
-    // forward transform over k + V_b: d_i ^= s d_j; d_j ^= d_i
-    for (uint32_t q = A.b; q-- > 0;) {
-        const uint32_t h = 1u << q;
-        const uint16_t* cq = cfwd + (A.R - (A.R >> q));
-        for (uint32_t p = tid; p < ((A.R >> 1) << lgS); p += kFftThreads) {
-            const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
-            const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
-            const uint32_t dj = buf[(j << lgS) + c];
-            const uint32_t di = buf[(i << lgS) + c] ^ fmul(glog, gexp, cq[blk], dj);
-            buf[(i << lgS) + c] = (uint16_t)di;
-            buf[(j << lgS) + c] = (uint16_t)(dj ^ di);
-        }
-        __syncthreads();
-    }
-    // repairs first .. first + r - 1 = coset points t = first + jj (decode:
-    // the syndrome of the accepted repair k + jj, its received row XORed in)
-    const uint16_t* rpos = A.syn ? A.rpos + g * A.r : nullptr;
-    const uint16_t* rslot = A.syn ? A.rslot + g * A.r : nullptr;
-    if (S >= 2) {
-        const uint32_t lgP = lgS - 1;
-        for (uint32_t p = tid; p < (A.r << lgP); p += kFftThreads) {
-            const uint32_t jj = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
-            if (c >= ncol) continue;
-            uint32_t v = reinterpret_cast<const uint32_t*>(buf)[(((A.first + jj) << lgS) + c) >> 1];
-            uint64_t orow = jj;
-            const uint8_t* base = nullptr;
-            if (rpos) {
-                orow = rpos[jj];
-                if (orow == 0xFFFFu) continue;
-                base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * (c0 + c);
+    const uint64_t items = (uint64_t)G * A.strips;
+    for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint64_t g = it / A.strips;
+        const uint32_t c0 = (uint32_t)(it - g * A.strips) << lgS;
+        const uint32_t ncol = min(S, A.nsym - c0);
+        __syncthreads();   // the table (first item) / the previous item's stores
+        if (A.syn && A.skip[g]) continue;   // uniform over the block
+        const uint8_t* gsrc = A.src + g * A.sgs;
+        const uint16_t* smap = A.syn ? A.smap + g * k : nullptr;
+        // strip in, as logs: window position i reads ring slot (rot + i) mod k
+        // (decode: slot smap[i], none = zero); big-endian symbols, two per
+        // dword (S >= 2; the rows are 16-byte aligned)
+        if (S >= 2) {
+            const uint32_t lgP = lgS - 1;
+            for (uint32_t p = tid; p < (k << lgP); p += kFftThreads) {
+                const uint32_t i = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
+                const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
+                const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * (c0 + c);
+                uint32_t v = 0;
+                if (smap && slot == 0xFFFFu)
+                    v = 0;
+                else if (c + 1 < ncol)
+                    v = bswap_sym2(*reinterpret_cast<const uint32_t*>(row));
+                else if (c < ncol)
+                    v = ((uint32_t)row[0] << 8) | row[1];
+                reinterpret_cast<uint32_t*>(buf)[p] = (uint32_t)glog[v & 0xFFFF] | ((uint32_t)glog[v >> 16] << 16);
             }
-            uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * (c0 + c);
-            if (c + 1 < ncol) {
-                if (base) v ^= bswap_sym2(*reinterpret_cast<const uint32_t*>(base));
-                *reinterpret_cast<uint32_t*>(o) = bswap_sym2(v);
-            } else {
-                if (base) v ^= ((uint32_t)base[0] << 8) | base[1];
+        } else {
+            for (uint32_t i = tid; i < k; i += kFftThreads) {
+                const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
+                const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * c0;
+                const uint32_t v = (smap && slot == 0xFFFFu) ? 0 : (((uint32_t)row[0] << 8) | row[1]);
+                buf[i] = glog[v];
+            }
+        }
+        __syncthreads();
+        // inverse transform over V: y_j += y_i; y_i += s y_j
+        for (uint32_t q = 0; q < A.a; ++q) {
+            const uint32_t h = 1u << q;
+            const uint16_t* cq = cinv + (k - (k >> q));
+            for (uint32_t p = tid; p < ((k >> 1) << lgS); p += kFftThreads) {
+                const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
+                const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
+                const uint32_t yi = buf[(i << lgS) + c];
+                const uint32_t yj = ladd(sz, buf[(j << lgS) + c], yi);
+                buf[(i << lgS) + c] = (uint16_t)ladd(sz, yi, lmul(cq[blk], yj));
+                buf[(j << lgS) + c] = (uint16_t)yj;
+            }
+            __syncthreads();
+        }
+        // fold onto the R-point coset, times kappa (in place: row t < R is
+        // written only by the thread that reads every row i = t mod R)
+        for (uint32_t p = tid; p < (A.R << lgS); p += kFftThreads) {
+            const uint32_t t = p >> lgS, c = p & (S - 1);
+            uint32_t acc = kNoLog16;
+            for (uint32_t i = t; i < k; i += A.R) acc = ladd(sz, acc, lmul(cfk[i], buf[(i << lgS) + c]));
+            buf[p] = (uint16_t)acc;
+        }
+        __syncthreads();
+        // forward transform over k + V_b: d_i += s d_j; d_j += d_i
+        for (uint32_t q = A.b; q-- > 0;) {
+            const uint32_t h = 1u << q;
+            const uint16_t* cq = cfwd + (A.R - (A.R >> q));
+            for (uint32_t p = tid; p < ((A.R >> 1) << lgS); p += kFftThreads) {
+                const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
+                const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
+                const uint32_t dj = buf[(j << lgS) + c];
+                const uint32_t di = ladd(sz, buf[(i << lgS) + c], lmul(cq[blk], dj));
+                buf[(i << lgS) + c] = (uint16_t)di;
+                buf[(j << lgS) + c] = (uint16_t)ladd(sz, dj, di);
+            }
+            __syncthreads();
+        }
+        // repairs first .. first + r - 1 = coset points t = first + jj (decode:
+        // the syndrome of the accepted repair k + jj, its received row XORed in)
+        const uint16_t* rpos = A.syn ? A.rpos + g * A.r : nullptr;
+        const uint16_t* rslot = A.syn ? A.rslot + g * A.r : nullptr;
+        if (S >= 2) {
+            const uint32_t lgP = lgS - 1;
+            for (uint32_t p = tid; p < (A.r << lgP); p += kFftThreads) {
+                const uint32_t jj = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
+                if (c >= ncol) continue;
+                const uint32_t lv = reinterpret_cast<const uint32_t*>(buf)[(((A.first + jj) << lgS) + c) >> 1];
+                const uint32_t l0 = lv & 0xFFFF, l1 = lv >> 16;
+                uint32_t v = (l0 == kNoLog16 ? 0u : (uint32_t)gexp[l0]) | ((l1 == kNoLog16 ? 0u : (uint32_t)gexp[l1]) << 16);
+                uint64_t orow = jj;
+                const uint8_t* base = nullptr;
+                if (rpos) {
+                    orow = rpos[jj];
+                    if (orow == 0xFFFFu) continue;
+                    base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * (c0 + c);
+                }
+                uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * (c0 + c);
+                if (c + 1 < ncol) {
+                    if (base) v ^= bswap_sym2(*reinterpret_cast<const uint32_t*>(base));
+                    *reinterpret_cast<uint32_t*>(o) = bswap_sym2(v);
+                } else {
+                    if (base) v ^= ((uint32_t)base[0] << 8) | base[1];
+                    o[0] = (uint8_t)(v >> 8);
+                    o[1] = (uint8_t)v;
+                }
+            }
+        } else {
+            for (uint32_t jj = tid; jj < A.r; jj += kFftThreads) {
+                const uint32_t l = buf[A.first + jj];
+                uint32_t v = l == kNoLog16 ? 0u : (uint32_t)gexp[l];
+                uint64_t orow = jj;
+                if (rpos) {
+                    orow = rpos[jj];
+                    if (orow == 0xFFFFu) continue;
+                    const uint8_t* base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * c0;
+                    v ^= ((uint32_t)base[0] << 8) | base[1];
+                }
+                uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * c0;
                 o[0] = (uint8_t)(v >> 8);
                 o[1] = (uint8_t)v;
             }
-        }
-    } else {
-        for (uint32_t jj = tid; jj < A.r; jj += kFftThreads) {
-            uint32_t v = buf[A.first + jj];
-            uint64_t orow = jj;
-            if (rpos) {
-                orow = rpos[jj];
-                if (orow == 0xFFFFu) continue;
-                const uint8_t* base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * c0;
-                v ^= ((uint32_t)base[0] << 8) | base[1];
-            }
-            uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * c0;
-            o[0] = (uint8_t)(v >> 8);
-            o[1] = (uint8_t)v;
         }
     }
 }
@@ -288,7 +320,7 @@ uint32_t hinv16(uint32_t a) {   // a^65534, a != 0
 namespace qf {
 
 bool gf16_fft_has(uint32_t k, uint32_t r, uint32_t first) {
-    return k >= kFftMinK && k <= 32768 && (k & (k - 1)) == 0 && r >= 1 && first + r <= k;
+    return k >= kFftMinK && k <= kFftLdsSymbols && (k & (k - 1)) == 0 && r >= 1 && first + r <= k;
 }
 
 namespace {
@@ -329,13 +361,13 @@ int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t 
     const uint32_t n_c = 2 * k + R - 2;
     hipLaunchKernelGGL(k_fft16_consts, dim3(std::min<uint32_t>((n_c + 255) / 256, 1024)), dim3(256), 0, st, ca);
     QF_HIP(hipGetLastError());
-    // strip width: 32 KiB of LDS, narrowed until the grid covers the CUs
+    // strip width: the 32 KiB LDS strip, narrowed until the items cover the CUs
     const uint32_t nsym = L / 2;
-    uint32_t S = std::max<uint32_t>(1, kFftLdsSymbols / k), lgS = 0;
+    uint32_t S = kFftLdsSymbols / k, lgS = 0;
     while ((1u << (lgS + 1)) <= S) ++lgS;
     S = 1u << lgS;
-    const uint64_t want = 4ull * qf::ctx_num_cus(ctx);
-    while (S > 1 && (uint64_t)G * ((nsym + S - 1) / S) < want && S > 1) {
+    const uint32_t cus = (uint32_t)qf::ctx_num_cus(ctx);
+    while (S > 1 && (uint64_t)G * ((nsym + S - 1) / S) < cus) {
         S >>= 1;
         --lgS;
     }
@@ -350,14 +382,11 @@ int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t 
     A.nsym = nsym;
     A.S = S;
     A.lgS = lgS;
-    const uint32_t strips = (nsym + S - 1) / S;
-    const size_t lds = (size_t)k * S * 2;
+    A.strips = (nsym + S - 1) / S;
+    const uint64_t items = (uint64_t)G * A.strips;
     hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-    for (uint32_t g0 = 0; g0 < G; g0 += 65535) {
-        const uint32_t gc = std::min<uint32_t>(65535, G - g0);
-        hipLaunchKernelGGL(k_fft16_encode, dim3(strips, gc), dim3(kFftThreads), lds, st, A, g0);
-        QF_HIP(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_fft16_encode, dim3((uint32_t)std::min<uint64_t>(items, cus)), dim3(kFftThreads), 0, st, A, G);
+    QF_HIP(hipGetLastError());
     qf::ctx_prof_end(ctx, st, ev, name);
     return QF_OK;
 }
@@ -381,6 +410,8 @@ int gf16_fft_encode(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint32_
     A.r = r;
     A.first = first;
     A.rot = rot;
+    const int zs = qf::ctx_gf16_zech(ctx, &A.zech);
+    if (zs) return zs;
     return fft16_launch(ctx, st, A, G, L, work, "k_fft16_encode");
 }
 
@@ -405,6 +436,8 @@ int gf16_fft_syndromes(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint
     A.rslot = rslot;
     A.skip = skip;
     A.syn = 1;
+    const int zs = qf::ctx_gf16_zech(ctx, &A.zech);
+    if (zs) return zs;
     return fft16_launch(ctx, st, A, G, L, work, "k_fft16_syndromes");
 }
 

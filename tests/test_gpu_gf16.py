@@ -371,7 +371,7 @@ def test_decode16_bitsliced_syndromes(qf, oracle, gpu_ctx):
 
 @pytest.mark.parametrize("k,r,L,G", [(16, 5, 100, 3), (32, 32, 2, 4), (128, 96, 200, 2), (256, 1, 34, 5),
                                      (1024, 1024, 64, 1), (1024, 8, 1200, 2), (4096, 100, 32, 1),
-                                     (32768, 16, 4, 1), (64, 33, 1200, 9)])
+                                     (16384, 16, 4, 1), (64, 33, 1200, 9)])
 def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G):
     """Power-of-two windows without a bit-sliced kernel run the additive-FFT
     kernel (qf_gf16_fft.hip): bit-exact against the oracle's Encoder16 and
@@ -398,7 +398,7 @@ def test_encode16_fft_many_generations(qf, oracle, gpu_ctx):
     against the oracle."""
     import torch
 
-    k, r, L, G = 16, 3, 4, 70000
+    k, r, L, G = 16, 3, 16, 70000
     rng = np.random.default_rng(70000)
     src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
     t_src = torch.from_numpy(src.reshape(-1)).to("cuda")
