@@ -126,8 +126,10 @@ enum {
     QF_OPT_GF16_LDS_GJ,          /* 1: GF(2^16) Gauss-Jordan in LDS for e <= 64 [QF_GF16_LDS_GJ; default 0] */
     QF_OPT_GF16_BITSLICED,       /* 1: bit-sliced GF(2^16) Cauchy encode and decode syndromes where
                                     generated; 0 never [QF_GF16_BITSLICED; default 1] */
-    QF_OPT_GF16_FFT,             /* 1: additive-FFT GF(2^16) Cauchy encode for k = 2^a >= 16 (first + r
-                                    <= k) without a bit-sliced kernel; 0 never [QF_GF16_FFT; default 1] */
+    QF_OPT_GF16_FFT,             /* additive-FFT GF(2^16) Cauchy encode / decode syndromes for
+                                    k = 2^a in [16, 8192] (first + r <= k) without a bit-sliced kernel:
+                                    1 where it needs ~9x fewer products than the matvec, 2 always,
+                                    0 never [QF_GF16_FFT; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

@@ -169,7 +169,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* GF16_LOGIFY_MIN_BLOCKS */ {"QF_GF16_LOGIFY_MIN_BLOCKS", 4, 0, 1 << 20, false},
     /* GF16_LDS_GJ */ {"QF_GF16_LDS_GJ", 0, 0, 1, false},
     /* GF16_BITSLICED */ {"QF_GF16_BITSLICED", 1, 0, 1, false},
-    /* GF16_FFT */ {"QF_GF16_FFT", 1, 0, 1, false},
+    /* GF16_FFT */ {"QF_GF16_FFT", 1, 0, 2, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }

@@ -1111,7 +1111,9 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
     if (s) return s;
     // power-of-two windows: the additive FFT (qf_gf16_fft.hip), O(k log k)
     // products per column instead of k r
-    if (!coeff_rxk && qf::ctx_opt(ctx, QF_OPT_GF16_FFT) && qf::gf16_fft_has(k, r, first)) {
+    const int64_t fft_opt = qf::ctx_opt(ctx, QF_OPT_GF16_FFT);
+    if (!coeff_rxk && fft_opt && qf::gf16_fft_has(k, r, first) &&
+        (fft_opt == 2 || qf::gf16_fft_pays(k, r, first + r))) {
         const size_t fb = align256(2 * (3ull * k)), mb = coeff_be_dev ? align256((size_t)r * k * 2) : 0;
         uint8_t* w;
         s = qf::ctx_work(ctx, fb + mb, &w);
@@ -1247,7 +1249,9 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     const bool bs = !row_coeffs && r <= 64 && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED) && qf::gf16_bs_has(k, r);
     // power-of-two k without one: the additive-FFT syndromes (qf_gf16_fft.hip)
     // over the same maps, constants in workspace slab 20
-    const bool fft = !bs && !row_coeffs && qf::ctx_opt(ctx, QF_OPT_GF16_FFT) && qf::gf16_fft_has(k, r, 0);
+    const int64_t fft_opt = qf::ctx_opt(ctx, QF_OPT_GF16_FFT);
+    const bool fft = !bs && !row_coeffs && fft_opt && qf::gf16_fft_has(k, r, 0) &&
+                     (fft_opt == 2 || qf::gf16_fft_pays(k, e_max, r));
     const bool maps = bs || fft;
     const size_t per_gen[18] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
                                 row_coeffs ? 4 * em * em : 0, 4 * em, 4 * em, 16 * em, Lp * em,

@@ -43,7 +43,8 @@ namespace {
 constexpr uint32_t kNoLog16 = 0xFFFF;   // log of 0 (no product)
 constexpr uint32_t kOrd16 = 65535;
 constexpr uint32_t kFftThreads = 1024;
-constexpr uint32_t kFftLdsSymbols = 16384;   // 32 KiB strips beside the 128 KiB Zech table
+constexpr uint32_t kFftLdsSymbols = 8192;    // 16 KiB strips beside the 128 KiB Zech table
+constexpr uint32_t kFftLdsConsts = 8192;     // and 16 KiB of butterfly constants (k <= 2,048)
 constexpr uint32_t kFftMinK = 16;
 
 #define QF_HIP(x)                                 \
@@ -163,6 +164,7 @@ __device__ __forceinline__ uint32_t ladd(const uint16_t* Z, uint32_t a, uint32_t
 __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint32_t G) {
     __shared__ uint16_t sz[65536];
     __shared__ uint16_t buf[kFftLdsSymbols];
+    __shared__ uint16_t scst[kFftLdsConsts];
     const uint32_t S = A.S, lgS = A.lgS, k = A.k, tid = threadIdx.x;
     const uint16_t* __restrict__ glog = A.glog;
     const uint16_t* __restrict__ gexp = A.gexp;
@@ -171,8 +173,15 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
         uint4* lz = reinterpret_cast<uint4*>(sz);
         for (uint32_t w = tid; w < 65536 / 8; w += kFftThreads) lz[w] = gz[w];
     }
-    const uint16_t* cinv = A.cst;
-    const uint16_t* cfk = A.cst + (k - 1);
+    // the butterfly constants of every layer, once per workgroup, when they fit
+    const uint32_t n_cst = 2 * k + A.R - 2;
+    const uint16_t* cst = A.cst;
+    if (n_cst <= kFftLdsConsts) {
+        for (uint32_t e = tid; e < n_cst; e += kFftThreads) scst[e] = A.cst[e];
+        cst = scst;
+    }
+    const uint16_t* cinv = cst;
+    const uint16_t* cfk = cst + (k - 1);
     const uint16_t* cfwd = cfk + k;
     const uint64_t items = (uint64_t)G * A.strips;
     for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
@@ -321,6 +330,20 @@ namespace qf {
 
 bool gf16_fft_has(uint32_t k, uint32_t r, uint32_t first) {
     return k >= kFftMinK && k <= kFftLdsSymbols && (k & (k - 1)) == 0 && r >= 1 && first + r <= k;
+}
+
+bool gf16_fft_pays(uint32_t k, uint32_t nout, uint32_t npoints) {
+    // products per symbol column: nout k direct (k_matvec16, ~4 T/s) against
+    // a k / 2 + k + b R / 2 here (~0.45 T/s, tools/bench_gf16.py r03ae/af):
+    // the FFT where it does ~9x fewer
+    uint32_t a = 0, R = 1, b = 0;
+    while ((1u << a) < k) ++a;
+    while (R < npoints) {
+        R <<= 1;
+        ++b;
+    }
+    const uint64_t fft = (uint64_t)a * k / 2 + k + (uint64_t)b * R / 2;
+    return (uint64_t)nout * k > 9 * fft;
 }
 
 namespace {

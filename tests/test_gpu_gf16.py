@@ -371,7 +371,7 @@ def test_decode16_bitsliced_syndromes(qf, oracle, gpu_ctx):
 
 @pytest.mark.parametrize("k,r,L,G", [(16, 5, 100, 3), (32, 32, 2, 4), (128, 96, 200, 2), (256, 1, 34, 5),
                                      (1024, 1024, 64, 1), (1024, 8, 1200, 2), (4096, 100, 32, 1),
-                                     (16384, 16, 4, 1), (64, 33, 1200, 9)])
+                                     (8192, 16, 4, 1), (2048, 2048, 100, 3), (64, 33, 1200, 9)])
 def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G):
     """Power-of-two windows without a bit-sliced kernel run the additive-FFT
     kernel (qf_gf16_fft.hip): bit-exact against the oracle's Encoder16 and
@@ -381,6 +381,7 @@ def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G):
     src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
     src[0, 0, :4] = 0
     src[-1, -1, -2:] = 0
+    qf.set_default_options(gf16_fft=2)           # the FFT wherever it applies
     gpu_ctx.profile(True)
     rep = run_encode16(qf, src, r)
     names = set(gpu_ctx.kernel_times())
@@ -403,6 +404,7 @@ def test_encode16_fft_many_generations(qf, oracle, gpu_ctx):
     src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
     t_src = torch.from_numpy(src.reshape(-1)).to("cuda")
     t_rep = torch.zeros(G * r * 16, dtype=torch.uint8, device="cuda")
+    qf.set_default_options(gf16_fft=2)
     qf.encode16_batch(t_src, t_rep, k, r, L, src_row_stride=L, src_gen_stride=k * L, rep_row_stride=16,
                       rep_gen_stride=r * 16, G=G)
     qf.default_context().sync()
@@ -423,6 +425,7 @@ def test_encoder16_fft_window_slides(qf, oracle, gpu_ctx):
         enc.add_source_packet(qf.Packet(i, bytearray(src[i].tobytes()), L, True))
     want = oracle.encode16(np.ascontiguousarray(src[5:]), 12)
     C = oracle.cauchy16(k, 12)
+    qf.set_default_options(gf16_fft=2)
     gpu_ctx.profile(True)
     got = [enc.generate_repair_packet(j) for j in (0, 7)] + enc.generate_repairs(3, 9)
     names = set(gpu_ctx.kernel_times())
@@ -462,6 +465,7 @@ def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
         gens[0] = ([k + extra] + [a for s, a in enumerate(arr) if s != pos],
                    np.concatenate([far[None], np.delete(rows, pos, 0)]), None)
     G = len(gens)
+    qf.set_default_options(gf16_fft=2)
     gpu_ctx.profile(True)
     res = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
     names = set(gpu_ctx.kernel_times())
