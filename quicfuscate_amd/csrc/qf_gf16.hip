@@ -759,12 +759,13 @@ __global__ void __launch_bounds__(1024) k_dec16_accept(BigArgs A) {
 // the same repair twice); nout_fb = e for the last kind, which the general
 // syndrome matvec then computes.
 __global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint16_t* smap, uint16_t* rpos,
-                                                     uint16_t* rslot, uint32_t* skip, uint32_t* nout_fb) {
+                                                     uint16_t* rslot, uint32_t* skip, uint32_t* nout_fb,
+                                                     uint32_t* solve_fb) {
     const uint32_t g = blockIdx.z, tid = threadIdx.x;
     const BigArgs a = view(A, g);
     const uint32_t k = a.k;
     __shared__ uint32_t seen[2048];   // repairs k + j seen (j < 65,536)
-    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_bad, s_far;
     uint16_t* sm = smap + (uint64_t)g * k;
     uint16_t* rp = rpos + (uint64_t)g * r;
     uint16_t* rsl = rslot + (uint64_t)g * r;
@@ -776,11 +777,12 @@ __global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint
         rsl[j] = 0;
     }
     for (uint32_t w = tid; w < 2048; w += 64) seen[w] = 0;
-    if (tid == 0) s_bad = 0;
+    if (tid == 0) s_bad = s_far = 0;
     __syncthreads();
     for (uint32_t c = tid; c < nin; c += 64) sm[a.w.Scol[c]] = a.w.Sslot[c];   // columns distinct (else ERANK)
     for (uint32_t q = tid; q < e; q += 64) {
         const uint32_t j = (uint32_t)a.w.J[q] - k;
+        if (j >= k) s_far = 1;   // past the FFT solve's coset (index >= 2k)
         if (j < r && !(atomicOr(&seen[j >> 5], 1u << (j & 31)) & (1u << (j & 31)))) {
             rp[j] = (uint16_t)q;
             rsl[j] = a.w.Jslot[q];
@@ -792,6 +794,7 @@ __global__ void __launch_bounds__(64) k_dec16_bsmaps(BigArgs A, uint32_t r, uint
     if (tid == 0) {
         skip[g] = (!ok || e == 0 || s_bad) ? 1u : 0u;
         nout_fb[g] = (ok && s_bad) ? e : 0u;
+        if (solve_fb) solve_fb[g] = (ok && s_far) ? e : 0u;
     }
 }
 
@@ -858,7 +861,9 @@ __global__ void __launch_bounds__(256) k_dec16_cauchy_prod(BigArgs A) {
     a.w.lprod[(row ? 1 : 3) * a.e_max + q] = (uint32_t)(sp[0] % kOrder);
 }
 
-__global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs A) {
+// (with solve_fb: only for the generations the FFT solve leaves to the matvec)
+__global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs A, const uint32_t* solve_fb) {
+    if (solve_fb && solve_fb[blockIdx.z] == 0) return;
     const BigArgs a = view(A, blockIdx.z);
     const uint32_t e = a.w.st->e;
     if (*a.status != QF_OK) return;
@@ -1253,32 +1258,32 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     const bool fft = !bs && !row_coeffs && fft_opt && qf::gf16_fft_has(k, r, 0) &&
                      (fft_opt == 2 || qf::gf16_fft_pays(k, e_max, r));
     const bool maps = bs || fft;
-    const size_t per_gen[18] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
+    const size_t per_gen[19] = {sizeof(Dec16State), 2 * em, 2 * em, 2 * em, 2ull * k, 2ull * k, 2 * em * k, 2 * em * em,
                                 row_coeffs ? 4 * em * em : 0, 4 * em, 4 * em, 16 * em, Lp * em,
                                 maps ? 2ull * k : 0, maps ? 2ull * r : 0, maps ? 2ull * r : 0, maps ? 4u : 0u,
-                                maps ? 4u : 0u};
+                                maps ? 4u : 0u, fft ? 4u : 0u};
     size_t gen_bytes = 0;
-    for (int q = 0; q < 18; ++q) gen_bytes += per_gen[q];
+    for (int q = 0; q < 19; ++q) gen_bytes += per_gen[q];
     // chunk: <= 65535 generations (grid z) and about 1 GiB of workspace
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)G, 65535ull,
                                                                              (1ull << 30) / gen_bytes}));
-    size_t off[21], tot = 0;
-    for (int q = 0; q < 18; ++q) {
+    size_t off[22], tot = 0;
+    for (int q = 0; q < 19; ++q) {
         off[q] = tot;
         tot += align256(std::max<size_t>(per_gen[q] * chunk, 1));
     }
     const size_t acc_bytes = std::max(matvec_acc_bytes(ctx, chunk, e_max, k, L),
                                       matvec_acc_bytes(ctx, chunk, e_max, e_max, L));
-    off[18] = tot;
+    off[19] = tot;
     tot += align256(std::max<size_t>(acc_bytes, 1));
     const size_t zero_bytes = bs ? align256(64 * ((((size_t)L + 15) / 16 + 3) / 4) + 64) : 0;
-    off[19] = tot;
-    tot += zero_bytes;
     off[20] = tot;
+    tot += zero_bytes;
+    off[21] = tot;
     tot += fft ? align256(2 * (3ull * k)) : 0;
     s = qf::ctx_work(ctx, tot, &w);
     if (s) return s;
-    if (bs) QF_HIP(hipMemsetAsync(w + off[19], 0, zero_bytes, st));
+    if (bs) QF_HIP(hipMemsetAsync(w + off[20], 0, zero_bytes, st));
     BigArgs b{};
     b.w.st = reinterpret_cast<Dec16State*>(w + off[0]);
     b.w.J = reinterpret_cast<uint16_t*>(w + off[1]);
@@ -1299,7 +1304,7 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     b.e_max = e_max;
     b.n_rows = max_rows;
     b.Lp = Lp;
-    uint8_t* acc = acc_bytes ? w + off[18] : nullptr;
+    uint8_t* acc = acc_bytes ? w + off[19] : nullptr;
     const int cus = qf::ctx_num_cus(ctx);
     const uint32_t mgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((em * k + 255) / 256, 8ull * cus / 1));
     const uint32_t dgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((em * em + 255) / 256, 8ull * cus));
@@ -1322,14 +1327,16 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         uint16_t* rslot = reinterpret_cast<uint16_t*>(w + off[15]);
         uint32_t* skip = reinterpret_cast<uint32_t*>(w + off[16]);
         uint32_t* nout_fb = maps ? reinterpret_cast<uint32_t*>(w + off[17]) : nullptr;
+        uint32_t* solve_fb = fft ? reinterpret_cast<uint32_t*>(w + off[18]) : nullptr;
         if (maps)
-            hipLaunchKernelGGL(k_dec16_bsmaps, dim3(1, 1, gc), dim3(64), 0, st, b, r, smap, rpos, rslot, skip, nout_fb);
+            hipLaunchKernelGGL(k_dec16_bsmaps, dim3(1, 1, gc), dim3(64), 0, st, b, r, smap, rpos, rslot, skip, nout_fb,
+                               solve_fb);
         hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid, 1, gc), dim3(256), 0, st, b, nout_fb);
         if (!row_coeffs) {
             uint32_t prod_threads = 64;
             while (prod_threads < e_max && prod_threads < 256) prod_threads <<= 1;
             hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max, 1, gc), dim3(prod_threads), 0, st, b);
-            hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid, 1, gc), dim3(256), 0, st, b);
+            hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid, 1, gc), dim3(256), 0, st, b, solve_fb);
         } else {
             hipLaunchKernelGGL(k_dec16_gj_init,
                                dim3((uint32_t)std::min<uint64_t>((em * 2 * em + 255) / 256, 8ull * cus), 1, gc),
@@ -1348,13 +1355,13 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         // syndromes s_a = row(J_a) ^ C[J_a, S] x_S
         if (bs) {
             s = qf::gf16_bs_syndromes(ctx, st, k, r, L, gc, rows + (size_t)g0 * sh->rows_gen_stride,
-                                      sh->rows_gen_stride, sh->row_stride, smap, k, rpos, rslot, skip, w + off[19],
+                                      sh->rows_gen_stride, sh->row_stride, smap, k, rpos, rslot, skip, w + off[20],
                                       b.w.synd, em * Lp, Lp);
             if (s) return s;
         } else if (fft) {
             s = qf::gf16_fft_syndromes(ctx, st, k, r, L, gc, rows + (size_t)g0 * sh->rows_gen_stride,
                                        sh->rows_gen_stride, sh->row_stride, smap, rpos, rslot, skip, b.w.synd, em * Lp,
-                                       Lp, glog, gexp, w + off[20]);
+                                       Lp, glog, gexp, w + off[21]);
             if (s) return s;
         }
         Mv16Args sy{};
@@ -1397,14 +1404,23 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
         so.m = b.w.dlog;
         so.mgs = em * em;
         so.mrs = e_max;
-        so.nout_g = n_rec + g0;
+        // x_E = D_b (C^T (D_a s))_E by the FFT for the Cauchy generations
+        // (qf_gf16_fft.hip); the matvec for those with a repair index >= 2k
+        if (fft) {
+            s = qf::gf16_fft_solve(ctx, st, k, L, gc, b.w.synd, em * Lp, Lp, rec + (size_t)g0 * sh->rec_gen_stride,
+                                   sh->rec_gen_stride, sh->rec_row_stride, reinterpret_cast<const uint32_t*>(b.w.st),
+                                   sizeof(Dec16State) / 4, status + g0, b.w.J, b.w.E, b.w.lprod, em, solve_fb, glog,
+                                   gexp, w + off[21]);
+            if (s) return s;
+        }
+        so.nout_g = fft ? solve_fb : n_rec + g0;
         so.nin_g = n_rec + g0;
         so.log = glog;
         so.exp = gexp;
         so.nout = e_max;
         so.nin = e_max;
         so.L = L;
-        s = launch_matvec(ctx, st, so, gc, "k_combine16", acc, acc_bytes);
+        s = launch_matvec(ctx, st, so, gc, fft ? "k_combine16_fallback" : "k_combine16", acc, acc_bytes, !fft);
         if (s) return s;
     }
     return QF_OK;

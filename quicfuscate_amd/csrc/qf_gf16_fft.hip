@@ -84,6 +84,19 @@ struct Fft16Args {
     const uint16_t* rslot;
     const uint32_t* skip;
     uint32_t syn;
+    // decode solve (solve != 0): src = the syndrome rows s_a (a < e_g), placed
+    // times D_a = Qx_a / Px_a at source position j_a = J_a - k; output row b
+    // (b < e_g) = D_b' out[E_b], D_b' = Qy_b / Py_b (logs in lprod, the closed
+    // form of k_dec16_cauchy_prod); skipped: status != 0, e_g == 0, solve_fb[g]
+    const uint32_t* st_e;    // e_g at st_e[g * st_stride]
+    uint32_t st_stride;
+    const int32_t* status;
+    const uint16_t* J;
+    const uint16_t* E;
+    const uint32_t* lprod;   // [g][4 em]: log Qx, log Px, log Qy, log Py
+    uint64_t em;
+    const uint32_t* solve_fb;
+    uint32_t solve;
 };
 
 __device__ __forceinline__ uint32_t wq_at(const Fft16Table& t, uint32_t q, uint32_t x) {
@@ -192,10 +205,34 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
         if (A.syn && A.skip[g]) continue;   // uniform over the block
         const uint8_t* gsrc = A.src + g * A.sgs;
         const uint16_t* smap = A.syn ? A.smap + g * k : nullptr;
+        uint32_t e_g = 0;
+        const uint16_t *gJ = nullptr, *gE = nullptr;
+        const uint32_t* lp = nullptr;
+        if (A.solve) {
+            if (A.status[g] != 0 || A.solve_fb[g] != 0) continue;
+            e_g = A.st_e[g * A.st_stride];
+            if (e_g == 0) continue;
+            gJ = A.J + g * A.em;
+            gE = A.E + g * A.em;
+            lp = A.lprod + g * 4 * A.em;
+            // every source position starts at zero; the e_g scaled syndromes go to theirs
+            for (uint32_t p = tid; p < (k << lgS); p += kFftThreads) buf[p] = (uint16_t)kNoLog16;
+            __syncthreads();
+            for (uint32_t p = tid; p < (e_g << lgS); p += kFftThreads) {
+                const uint32_t a = p >> lgS, c = p & (S - 1);
+                if (c >= ncol) continue;
+                const uint8_t* row = gsrc + (uint64_t)a * A.srs + 2ull * (c0 + c);
+                uint32_t da = lp[a] + kOrd16 - lp[A.em + a];
+                da = da >= kOrd16 ? da - kOrd16 : da;
+                buf[(((uint32_t)gJ[a] - k) << lgS) + c] =
+                    (uint16_t)lmul(da, glog[((uint32_t)row[0] << 8) | row[1]]);
+            }
+        }
         // strip in, as logs: window position i reads ring slot (rot + i) mod k
         // (decode: slot smap[i], none = zero); big-endian symbols, two per
         // dword (S >= 2; the rows are 16-byte aligned)
-        if (S >= 2) {
+        if (A.solve) {
+        } else if (S >= 2) {
             const uint32_t lgP = lgS - 1;
             for (uint32_t p = tid; p < (k << lgP); p += kFftThreads) {
                 const uint32_t i = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
@@ -255,6 +292,20 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
                 buf[(j << lgS) + c] = (uint16_t)ladd(sz, dj, di);
             }
             __syncthreads();
+        }
+        if (A.solve) {   // recovered row b = D_b' out[E_b]
+            for (uint32_t p = tid; p < (e_g << lgS); p += kFftThreads) {
+                const uint32_t bb = p >> lgS, c = p & (S - 1);
+                if (c >= ncol) continue;
+                uint32_t db = lp[2 * A.em + bb] + kOrd16 - lp[3 * A.em + bb];
+                db = db >= kOrd16 ? db - kOrd16 : db;
+                const uint32_t l = lmul(db, buf[((uint32_t)gE[bb] << lgS) + c]);
+                const uint32_t v = l == kNoLog16 ? 0u : (uint32_t)gexp[l];
+                uint8_t* o = A.rep + g * A.rgs + (uint64_t)bb * A.rrs + 2ull * (c0 + c);
+                o[0] = (uint8_t)(v >> 8);
+                o[1] = (uint8_t)v;
+            }
+            continue;
         }
         // repairs first .. first + r - 1 = coset points t = first + jj (decode:
         // the syndrome of the accepted repair k + jj, its received row XORed in)
@@ -462,6 +513,37 @@ int gf16_fft_syndromes(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint
     const int zs = qf::ctx_gf16_zech(ctx, &A.zech);
     if (zs) return zs;
     return fft16_launch(ctx, st, A, G, L, work, "k_fft16_syndromes");
+}
+
+int gf16_fft_solve(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t L, uint32_t G, const uint8_t* synd,
+                   uint64_t synd_gs, uint64_t synd_rs, uint8_t* rec, uint64_t rec_gs, uint64_t rec_rs,
+                   const uint32_t* st_e, uint32_t st_stride, const int32_t* status, const uint16_t* J,
+                   const uint16_t* E, const uint32_t* lprod, uint64_t em, const uint32_t* solve_fb,
+                   const uint16_t* glog, const uint16_t* gexp, uint8_t* work) {
+    if (!gf16_fft_has(k, k, 0) || (L & 1)) return kGf16BsNone;
+    Fft16Args A{};
+    A.src = synd;
+    A.sgs = synd_gs;
+    A.srs = synd_rs;
+    A.rep = rec;
+    A.rgs = rec_gs;
+    A.rrs = rec_rs;
+    A.glog = glog;
+    A.gexp = gexp;
+    A.k = k;
+    A.r = k;   // outputs at every point of the coset (E_b < k)
+    A.st_e = st_e;
+    A.st_stride = st_stride;
+    A.status = status;
+    A.J = J;
+    A.E = E;
+    A.lprod = lprod;
+    A.em = em;
+    A.solve_fb = solve_fb;
+    A.solve = 1;
+    const int zs = qf::ctx_gf16_zech(ctx, &A.zech);
+    if (zs) return zs;
+    return fft16_launch(ctx, st, A, G, L, work, "k_fft16_solve");
 }
 
 }  // namespace qf

@@ -444,7 +444,8 @@ def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
     syndromes come from the additive FFT (k_fft16_syndromes, sources gathered
     through the slot map, erased ones as zero rows, the accepted repair row
     XORed in), the general matvec only for the generation with a repair index
-    past k + r; statuses, recovered bytes and indices equal the oracle's and
+    past k + r; the solve x_E = C[J,E]^-1 s is the FFT too (k_fft16_solve),
+    the matvec only for a repair index >= 2k (k = r = 256); statuses, recovered bytes and indices equal the oracle's and
     the general path's (gf16_fft = 0).  Mixed erasure counts, a full-erasure,
     an erasure-free, a short and a duplicate-row generation."""
     rng = np.random.default_rng(k + r + L)
@@ -471,6 +472,7 @@ def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
     names = set(gpu_ctx.kernel_times())
     gpu_ctx.profile(False)
     assert "k_fft16_syndromes" in names and "k_syndromes16_fallback" in names, names
+    assert "k_fft16_solve" in names, names
     rec, ri, nrec, st, rrs, rec_gs = res
     for g, (a, rw, _) in enumerate(gens):
         ost, out, mask = oracle.decode16(k, a, rw, None)
