@@ -10,7 +10,9 @@ exactly the constants the library's host code derives from the table
 W_q(2^m) (W_q = the subspace polynomial of {0 .. 2^q - 1}, GF(2)-linear):
     W_0(t) = t,  W_{q+1}(t) = W_q(t) (W_q(t) + W_q(2^q)),
     xhat(q, t) = W_q(t) / W_q(2^q),  Delta = prod_q W_q(2^q),  P_V(k) = W_a(k).
-The device kernel runs the same butterflies (tests/test_gpu_gf16.py)."""
+The device kernel runs the same butterflies in the log domain (Zech table;
+tests/test_gpu_gf16.py), and the decode's solve reuses the transform
+(test_fft_solve_recovers_erasures)."""
 import numpy as np
 import pytest
 
@@ -131,7 +133,6 @@ def test_recurrence_is_the_subspace_polynomial():
             want = 1
             for u in range(1 << q):
                 want = smul(want, t ^ u)
-            inv_l, _, _ = constants(1 << (q + 1), 1)
             W = [[1 << m for m in range(16)]]
             for qq in range(q):
                 W.append([smul(w, w ^ W[qq][qq]) for w in W[qq]])
@@ -154,3 +155,43 @@ def test_fft_matches_oracle(oracle, k, r, first):
     out = to_bytes(fft_encode(to_sym(rows), k, r, first))
     ref = oracle.encode16(rows, first + r)[first:]
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("k,e", [(16, 5), (64, 33), (128, 128)])
+def test_fft_solve_recovers_erasures(oracle, k, e):
+    """The decode solve of qf_gf16_fft.hip (k_fft16_solve): with accepted
+    repairs J (x_a = k + j_a) and erased sources E (y_b), the closed-form
+    Cauchy inverse (C^-1)_ba = Qx_a Qy_b / ((x_a + y_b) Px_a Py_b) makes
+        x_{E_b} = (Qy_b / Py_b) * FFT(z)[E_b],  z[j_a] = (Qx_a / Px_a) s_a,
+    the same encode FFT with R = k (outputs on the whole coset).  Checked by
+    recovering the erased sources from the oracle's repairs."""
+    rng = np.random.default_rng(k * 7 + e)
+    L = 4
+    rows = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    x = to_sym(rows)
+    E = sorted(rng.choice(k, e, replace=False).tolist())
+    js = rng.choice(k, e, replace=False).tolist()          # accepted repairs k + j, j < k
+    rep = to_sym(oracle.encode16(rows, k))                  # all k Cauchy rows
+    known = np.ones(k, bool)
+    known[E] = False
+    xs = np.where(known[:, None], x, 0).astype(np.uint16)
+    full = fft_encode(xs, k, k)                             # C[J, S] x_S for every repair
+    s = [rep[j] ^ full[j] for j in js]                      # syndromes = C[J, E] x_E
+    X = [k ^ j for j in js]
+
+    def prod(vals):
+        out = 1
+        for v in vals:
+            out = smul(out, v)
+        return out
+
+    z = np.zeros((k, x.shape[1]), np.uint16)
+    for a, j in enumerate(js):
+        qx = prod(X[a] ^ y for y in E)
+        px = prod(X[a] ^ X[c] for c in range(e) if c != a)
+        z[j] = vmul(smul(qx, g16.inv(px)), s[a])
+    out = fft_encode(z, k, k)
+    for b, y in enumerate(E):
+        qy = prod(xa ^ y for xa in X)
+        py = prod(y ^ E[c] for c in range(e) if c != b)
+        assert np.array_equal(vmul(smul(qy, g16.inv(py)), out[y]), x[y]), (b, y)
