@@ -127,7 +127,7 @@ enum {
     QF_OPT_GF16_BITSLICED,       /* 1: bit-sliced GF(2^16) Cauchy encode and decode syndromes where
                                     generated; 0 never [QF_GF16_BITSLICED; default 1] */
     QF_OPT_GF16_FFT,             /* additive-FFT GF(2^16) Cauchy encode / decode syndromes for
-                                    k = 2^a in [16, 8192] (first + r <= k) without a bit-sliced kernel:
+                                    k = 2^a in [16, 4096] (first + r <= k) without a bit-sliced kernel:
                                     1 where it needs ~9x fewer products than the matvec, 2 always,
                                     0 never [QF_GF16_FFT; default 1] */
     QF_OPT_COUNT

@@ -291,7 +291,6 @@ __global__ void __launch_bounds__(kThreads16) k_logify16(Mv16Args a, uint64_t G,
 
 __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
     __shared__ uint16_t sexp[kOrder + 1];  // static: LDS offsets fold into the reads
-    load_exp_lds(sexp, a.exp);
     uint32_t nob = a.nob, nsplit = a.nsplit, kchunk = a.kchunk;
     uint64_t total = a.total_units;
     if (a.shape) {
@@ -301,6 +300,10 @@ __global__ void __launch_bounds__(kThreads16) k_matvec16(Mv16Args a) {
         kchunk = sh.kchunk;
         total = sh.total;
     }
+    // a block without units leaves before the 128 KiB table copy (device-shaped
+    // launches with nothing to do: the FFT paths' fallback matvecs)
+    if ((uint64_t)blockIdx.x * blockDim.x >= total) return;
+    load_exp_lds(sexp, a.exp);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total; f += stride) {
         uint64_t t = f / a.Lu;

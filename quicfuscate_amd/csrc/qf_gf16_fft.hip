@@ -170,6 +170,26 @@ __device__ __forceinline__ uint32_t ladd(const uint16_t* Z, uint32_t a, uint32_t
     return b == kNoLog16 ? a : s;
 }
 
+// two logs per dword (column pairs)
+__device__ __forceinline__ uint32_t ladd2(const uint16_t* Z, uint32_t a, uint32_t b) {
+    return ladd(Z, a & 0xFFFF, b & 0xFFFF) | (ladd(Z, a >> 16, b >> 16) << 16);
+}
+
+__device__ __forceinline__ uint32_t lmul2(uint32_t s, uint32_t y) {
+    return lmul(s, y & 0xFFFF) | (lmul(s, y >> 16) << 16);
+}
+
+// inverse butterfly y_j += y_i; y_i += s y_j / forward d_i += s d_j; d_j += d_i
+__device__ __forceinline__ void ibfly(const uint16_t* Z, uint32_t& yi, uint32_t& yj, uint32_t s) {
+    yj = ladd2(Z, yj, yi);
+    yi = ladd2(Z, yi, lmul2(s, yj));
+}
+
+__device__ __forceinline__ void fbfly(const uint16_t* Z, uint32_t& di, uint32_t& dj, uint32_t s) {
+    di = ladd2(Z, di, lmul2(s, dj));
+    dj = ladd2(Z, dj, di);
+}
+
 // One workgroup per CU (the Zech table fills 128 KiB of LDS, the strip the
 // other 32 KiB), persistent over the (generation, strip) items.  The strip is
 // held as logs: a butterfly is two Zech lookups and a log sum, and only the
@@ -256,40 +276,93 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
             }
         }
         __syncthreads();
-        // inverse transform over V: y_j += y_i; y_i += s y_j
-        for (uint32_t q = 0; q < A.a; ++q) {
+        // inverse transform over V (y_j += y_i; y_i += s y_j), two layers per
+        // pass (radix 4: four rows, three constants, one barrier) on column
+        // pairs (one dword of two logs per LDS access)
+        uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
+        const uint32_t lgP = lgS - 1, P = S >> 1;
+        // (radix 2 throughout when a radix-4 pass would leave threads idle: G = 1)
+        const bool r4 = ((k >> 2) << lgP) >= kFftThreads;
+        uint32_t q = 0;
+        for (; r4 && q + 1 < A.a; q += 2) {
             const uint32_t h = 1u << q;
-            const uint16_t* cq = cinv + (k - (k >> q));
-            for (uint32_t p = tid; p < ((k >> 1) << lgS); p += kFftThreads) {
-                const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
-                const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
-                const uint32_t yi = buf[(i << lgS) + c];
-                const uint32_t yj = ladd(sz, buf[(j << lgS) + c], yi);
-                buf[(i << lgS) + c] = (uint16_t)ladd(sz, yi, lmul(cq[blk], yj));
-                buf[(j << lgS) + c] = (uint16_t)yj;
+            const uint16_t* c0 = cinv + (k - (k >> q));
+            const uint16_t* c1 = cinv + (k - (k >> (q + 1)));
+            for (uint32_t p = tid; p < ((k >> 2) << lgP); p += kFftThreads) {
+                const uint32_t cp = p & (P - 1), qi = p >> lgP, B = qi >> q;
+                uint32_t* w = b32 + ((((B << (q + 2)) + (qi & (h - 1))) << lgP) + cp);
+                const uint32_t st = h << lgP;
+                uint32_t y0 = w[0], y1 = w[st], y2 = w[2 * st], y3 = w[3 * st];
+                ibfly(sz, y0, y1, c0[2 * B]);
+                ibfly(sz, y2, y3, c0[2 * B + 1]);
+                const uint32_t s1 = c1[B];
+                ibfly(sz, y0, y2, s1);
+                ibfly(sz, y1, y3, s1);
+                w[0] = y0;
+                w[st] = y1;
+                w[2 * st] = y2;
+                w[3 * st] = y3;
+            }
+            __syncthreads();
+        }
+        for (; q < A.a; ++q) {   // the rest (an odd layer count: the last layer alone)
+            const uint32_t h = 1u << q;
+            const uint16_t* c0 = cinv + (k - (k >> q));
+            for (uint32_t p = tid; p < ((k >> 1) << lgP); p += kFftThreads) {
+                const uint32_t cp = p & (P - 1), bi = p >> lgP, blk = bi >> q;
+                uint32_t* w = b32 + ((((blk << (q + 1)) | (bi & (h - 1))) << lgP) + cp);
+                const uint32_t st = h << lgP;
+                uint32_t y0 = w[0], y1 = w[st];
+                ibfly(sz, y0, y1, c0[blk]);
+                w[0] = y0;
+                w[st] = y1;
             }
             __syncthreads();
         }
         // fold onto the R-point coset, times kappa (in place: row t < R is
         // written only by the thread that reads every row i = t mod R)
-        for (uint32_t p = tid; p < (A.R << lgS); p += kFftThreads) {
-            const uint32_t t = p >> lgS, c = p & (S - 1);
-            uint32_t acc = kNoLog16;
-            for (uint32_t i = t; i < k; i += A.R) acc = ladd(sz, acc, lmul(cfk[i], buf[(i << lgS) + c]));
-            buf[p] = (uint16_t)acc;
+        for (uint32_t p = tid; p < (A.R << lgP); p += kFftThreads) {
+            const uint32_t t = p >> lgP, cp = p & (P - 1);
+            uint32_t acc = kNoLog16 | (kNoLog16 << 16);
+            for (uint32_t i = t; i < k; i += A.R) acc = ladd2(sz, acc, lmul2(cfk[i], b32[(i << lgP) + cp]));
+            b32[p] = acc;
         }
         __syncthreads();
-        // forward transform over k + V_b: d_i += s d_j; d_j += d_i
-        for (uint32_t q = A.b; q-- > 0;) {
-            const uint32_t h = 1u << q;
-            const uint16_t* cq = cfwd + (A.R - (A.R >> q));
-            for (uint32_t p = tid; p < ((A.R >> 1) << lgS); p += kFftThreads) {
-                const uint32_t c = p & (S - 1), bi = p >> lgS, blk = bi >> q;
-                const uint32_t i = (blk << (q + 1)) | (bi & (h - 1)), j = i + h;
-                const uint32_t dj = buf[(j << lgS) + c];
-                const uint32_t di = ladd(sz, buf[(i << lgS) + c], lmul(cq[blk], dj));
-                buf[(i << lgS) + c] = (uint16_t)di;
-                buf[(j << lgS) + c] = (uint16_t)ladd(sz, dj, di);
+        // forward transform over k + V_b (d_i += s d_j; d_j += d_i), layers
+        // b-1 .. 0, two per pass as above
+        int qq = (int)A.b - 1;
+        for (; ((A.R >> 2) << lgP) >= kFftThreads && qq >= 1; qq -= 2) {
+            const uint32_t ql = (uint32_t)qq - 1, h = 1u << ql;
+            const uint16_t* c0 = cfwd + (A.R - (A.R >> ql));
+            const uint16_t* c1 = cfwd + (A.R - (A.R >> (ql + 1)));
+            for (uint32_t p = tid; p < ((A.R >> 2) << lgP); p += kFftThreads) {
+                const uint32_t cp = p & (P - 1), qi = p >> lgP, B = qi >> ql;
+                uint32_t* w = b32 + ((((B << (ql + 2)) + (qi & (h - 1))) << lgP) + cp);
+                const uint32_t st = h << lgP;
+                uint32_t d0 = w[0], d1 = w[st], d2 = w[2 * st], d3 = w[3 * st];
+                const uint32_t s1 = c1[B];
+                fbfly(sz, d0, d2, s1);
+                fbfly(sz, d1, d3, s1);
+                fbfly(sz, d0, d1, c0[2 * B]);
+                fbfly(sz, d2, d3, c0[2 * B + 1]);
+                w[0] = d0;
+                w[st] = d1;
+                w[2 * st] = d2;
+                w[3 * st] = d3;
+            }
+            __syncthreads();
+        }
+        for (; qq >= 0; --qq) {   // the rest, one layer per pass
+            const uint32_t ql = (uint32_t)qq, h = 1u << ql;
+            const uint16_t* c0 = cfwd + (A.R - (A.R >> ql));
+            for (uint32_t p = tid; p < ((A.R >> 1) << lgP); p += kFftThreads) {
+                const uint32_t cp = p & (P - 1), bi = p >> lgP, blk = bi >> ql;
+                uint32_t* w = b32 + ((((blk << (ql + 1)) | (bi & (h - 1))) << lgP) + cp);
+                const uint32_t st = h << lgP;
+                uint32_t d0 = w[0], d1 = w[st];
+                fbfly(sz, d0, d1, c0[blk]);
+                w[0] = d0;
+                w[st] = d1;
             }
             __syncthreads();
         }
@@ -380,7 +453,7 @@ uint32_t hinv16(uint32_t a) {   // a^65534, a != 0
 namespace qf {
 
 bool gf16_fft_has(uint32_t k, uint32_t r, uint32_t first) {
-    return k >= kFftMinK && k <= kFftLdsSymbols && (k & (k - 1)) == 0 && r >= 1 && first + r <= k;
+    return k >= kFftMinK && k <= kFftLdsSymbols / 2 && (k & (k - 1)) == 0 && r >= 1 && first + r <= k;
 }
 
 bool gf16_fft_pays(uint32_t k, uint32_t nout, uint32_t npoints) {
@@ -441,11 +514,11 @@ int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t 
     while ((1u << (lgS + 1)) <= S) ++lgS;
     S = 1u << lgS;
     const uint32_t cus = (uint32_t)qf::ctx_num_cus(ctx);
-    while (S > 1 && (uint64_t)G * ((nsym + S - 1) / S) < cus) {
+    while (S > 2 && (uint64_t)G * ((nsym + S - 1) / S) < cus) {
         S >>= 1;
         --lgS;
     }
-    while (S > 1 && S / 2 >= nsym) {   // no strip wider than the row
+    while (S > 2 && S / 2 >= nsym) {   // no strip wider than the row (S >= 2: column pairs)
         S >>= 1;
         --lgS;
     }
