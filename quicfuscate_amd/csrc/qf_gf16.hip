@@ -879,6 +879,50 @@ __global__ void __launch_bounds__(256) k_dec16_cauchy_inv(BigArgs A, const uint3
     }
 }
 
+// The same closed form for e_max <= 64 in one block per generation: thread t
+// < 2e forms the log products of row (J) or column (E) value t with a serial
+// loop, then the block writes the e^2 logs of the inverse (one launch of gc
+// blocks instead of 2 e_max gc product blocks and a separate inverse grid).
+__global__ void __launch_bounds__(128) k_dec16_cauchy_small(BigArgs A, const uint32_t* solve_fb) {
+    const BigArgs a = view(A, blockIdx.z);
+    __shared__ uint32_t s_zero;
+    const uint32_t tid = threadIdx.x;
+    if (*a.status != QF_OK) return;   // uniform (accept wrote it)
+    const uint32_t e = a.w.st->e;
+    if (tid == 0) s_zero = 0;
+    __syncthreads();
+    if (tid < 2 * e) {
+        const bool row = tid < e;
+        const uint32_t q = row ? tid : tid - e;
+        const uint32_t v = row ? a.w.J[q] : a.w.E[q];
+        const uint16_t* other = row ? a.w.E : a.w.J;
+        const uint16_t* same = row ? a.w.J : a.w.E;
+        uint64_t lq = 0, lp = 0;
+        bool zero = false;
+        for (uint32_t c = 0; c < e; ++c) {
+            lq += a.log[v ^ other[c]];
+            const uint32_t d = v ^ same[c];
+            zero |= (c != q && d == 0);
+            lp += (c != q && d) ? a.log[d] : 0;
+        }
+        if (zero) s_zero = 1;
+        a.w.lprod[(row ? 0 : 2) * a.e_max + q] = (uint32_t)(lq % kOrder);
+        a.w.lprod[(row ? 1 : 3) * a.e_max + q] = (uint32_t)(lp % kOrder);
+    }
+    __syncthreads();
+    if (s_zero) {
+        if (tid == 0) big_fail(a, QF_ERANK);
+        return;
+    }
+    if (solve_fb && solve_fb[blockIdx.z] == 0) return;   // the FFT solve needs only lprod
+    for (uint32_t t = tid; t < e * e; t += blockDim.x) {
+        const uint32_t b = t / e, r = t % e;
+        const int64_t l = (int64_t)a.w.lprod[r] + a.w.lprod[2 * a.e_max + b] - a.log[a.w.J[r] ^ a.w.E[b]] -
+                          a.w.lprod[a.e_max + r] - a.w.lprod[3 * a.e_max + b];
+        a.w.dlog[(uint64_t)b * a.e_max + r] = (uint16_t)lmod(l);
+    }
+}
+
 // General rows: Gauss-Jordan on [C[J,E] | I] in the workspace, one launch per
 // column.  Rows are not swapped: a column's pivot is the first row not yet
 // used as a pivot with a nonzero entry there (the same pivot as the swap-based
@@ -1336,10 +1380,14 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
                                solve_fb);
         hipLaunchKernelGGL(k_dec16_synmat, dim3(mgrid, 1, gc), dim3(256), 0, st, b, nout_fb);
         if (!row_coeffs) {
-            uint32_t prod_threads = 64;
-            while (prod_threads < e_max && prod_threads < 256) prod_threads <<= 1;
-            hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max, 1, gc), dim3(prod_threads), 0, st, b);
-            hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid, 1, gc), dim3(256), 0, st, b, solve_fb);
+            if (e_max <= 64) {
+                hipLaunchKernelGGL(k_dec16_cauchy_small, dim3(1, 1, gc), dim3(128), 0, st, b, solve_fb);
+            } else {
+                uint32_t prod_threads = 64;
+                while (prod_threads < e_max && prod_threads < 256) prod_threads <<= 1;
+                hipLaunchKernelGGL(k_dec16_cauchy_prod, dim3(2 * e_max, 1, gc), dim3(prod_threads), 0, st, b);
+                hipLaunchKernelGGL(k_dec16_cauchy_inv, dim3(dgrid, 1, gc), dim3(256), 0, st, b, solve_fb);
+            }
         } else {
             hipLaunchKernelGGL(k_dec16_gj_init,
                                dim3((uint32_t)std::min<uint64_t>((em * 2 * em + 255) / 256, 8ull * cus), 1, gc),
