@@ -26,10 +26,12 @@
 // restatement in tests/test_gf16_fft_cpu.py runs the same schedule against the
 // oracle.
 //
-// Layout: one workgroup per (generation, strip of S symbol columns); the k x S
-// strip sits in LDS as u16 symbols (row-major), every layer is one pass of
-// butterflies over (butterfly, column) pairs and a barrier; a product is
-// exp[log y + log s] from the device tables (L2-resident, 384 KiB).
+// Layout (k_fft16): one 1,024-thread workgroup per CU, persistent over the
+// (generation, strip of S symbol columns) items.  The k x S strip sits in LDS
+// as logs beside a 128 KiB Zech table, so a butterfly is two LDS lookups and a
+// log sum; two layers per pass (radix 4) on column pairs, one barrier per
+// pass.  The same kernel computes the decode's syndromes (syn) and its solve
+// x_E = C[J,E]^-1 s (solve), both through this transform.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -194,7 +196,7 @@ __device__ __forceinline__ void fbfly(const uint16_t* Z, uint32_t& di, uint32_t&
 // other 32 KiB), persistent over the (generation, strip) items.  The strip is
 // held as logs: a butterfly is two Zech lookups and a log sum, and only the
 // strip's load and store touch the global log / exp tables.
-__global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint32_t G) {
+__global__ void __launch_bounds__(kFftThreads) k_fft16(Fft16Args A, uint32_t G) {
     __shared__ uint16_t sz[65536];
     __shared__ uint16_t buf[kFftLdsSymbols];
     __shared__ uint16_t scst[kFftLdsConsts];
@@ -250,9 +252,8 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
         }
         // strip in, as logs: window position i reads ring slot (rot + i) mod k
         // (decode: slot smap[i], none = zero); big-endian symbols, two per
-        // dword (S >= 2; the rows are 16-byte aligned)
-        if (A.solve) {
-        } else if (S >= 2) {
+        // dword (S >= 2 column pairs; the rows are 16-byte aligned)
+        if (!A.solve) {
             const uint32_t lgP = lgS - 1;
             for (uint32_t p = tid; p < (k << lgP); p += kFftThreads) {
                 const uint32_t i = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
@@ -266,13 +267,6 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
                 else if (c < ncol)
                     v = ((uint32_t)row[0] << 8) | row[1];
                 reinterpret_cast<uint32_t*>(buf)[p] = (uint32_t)glog[v & 0xFFFF] | ((uint32_t)glog[v >> 16] << 16);
-            }
-        } else {
-            for (uint32_t i = tid; i < k; i += kFftThreads) {
-                const uint32_t slot = smap ? smap[i] : ((A.rot + i) & (k - 1));
-                const uint8_t* row = gsrc + (uint64_t)slot * A.srs + 2ull * c0;
-                const uint32_t v = (smap && slot == 0xFFFFu) ? 0 : (((uint32_t)row[0] << 8) | row[1]);
-                buf[i] = glog[v];
             }
         }
         __syncthreads();
@@ -384,7 +378,7 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
         // the syndrome of the accepted repair k + jj, its received row XORed in)
         const uint16_t* rpos = A.syn ? A.rpos + g * A.r : nullptr;
         const uint16_t* rslot = A.syn ? A.rslot + g * A.r : nullptr;
-        if (S >= 2) {
+        {
             const uint32_t lgP = lgS - 1;
             for (uint32_t p = tid; p < (A.r << lgP); p += kFftThreads) {
                 const uint32_t jj = p >> lgP, c = (p & ((S >> 1) - 1)) << 1;
@@ -408,21 +402,6 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16_encode(Fft16Args A, uint3
                     o[0] = (uint8_t)(v >> 8);
                     o[1] = (uint8_t)v;
                 }
-            }
-        } else {
-            for (uint32_t jj = tid; jj < A.r; jj += kFftThreads) {
-                const uint32_t l = buf[A.first + jj];
-                uint32_t v = l == kNoLog16 ? 0u : (uint32_t)gexp[l];
-                uint64_t orow = jj;
-                if (rpos) {
-                    orow = rpos[jj];
-                    if (orow == 0xFFFFu) continue;
-                    const uint8_t* base = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * c0;
-                    v ^= ((uint32_t)base[0] << 8) | base[1];
-                }
-                uint8_t* o = A.rep + g * A.rgs + orow * A.rrs + 2ull * c0;
-                o[0] = (uint8_t)(v >> 8);
-                o[1] = (uint8_t)v;
             }
         }
     }
@@ -532,7 +511,7 @@ int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t 
     A.strips = (nsym + S - 1) / S;
     const uint64_t items = (uint64_t)G * A.strips;
     hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-    hipLaunchKernelGGL(k_fft16_encode, dim3((uint32_t)std::min<uint64_t>(items, cus)), dim3(kFftThreads), 0, st, A, G);
+    hipLaunchKernelGGL(k_fft16, dim3((uint32_t)std::min<uint64_t>(items, cus)), dim3(kFftThreads), 0, st, A, G);
     QF_HIP(hipGetLastError());
     qf::ctx_prof_end(ctx, st, ev, name);
     return QF_OK;
