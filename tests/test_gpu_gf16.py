@@ -371,7 +371,8 @@ def test_decode16_bitsliced_syndromes(qf, oracle, gpu_ctx):
 
 @pytest.mark.parametrize("k,r,L,G", [(16, 5, 100, 3), (32, 32, 2, 4), (128, 96, 200, 2), (256, 1, 34, 5),
                                      (1024, 1024, 64, 1), (1024, 8, 1200, 2), (4096, 100, 32, 1),
-                                     (4096, 16, 4, 1), (2048, 2048, 100, 3), (64, 33, 1200, 9)])
+                                     (4096, 16, 4, 1), (2048, 2048, 100, 3), (64, 33, 1200, 9),
+                                     (256, 200, 9000, 2)])
 def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G):
     """Power-of-two windows without a bit-sliced kernel run the additive-FFT
     kernel (qf_gf16_fft.hip): bit-exact against the oracle's Encoder16 and
