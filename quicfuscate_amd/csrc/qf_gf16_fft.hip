@@ -172,9 +172,21 @@ __device__ __forceinline__ uint32_t ladd(const uint16_t* Z, uint32_t a, uint32_t
     return b == kNoLog16 ? a : s;
 }
 
-// two logs per dword (column pairs)
+// two logs per dword (column pairs); both Zech lookups issued together
 __device__ __forceinline__ uint32_t ladd2(const uint16_t* Z, uint32_t a, uint32_t b) {
-    return ladd(Z, a & 0xFFFF, b & 0xFFFF) | (ladd(Z, a >> 16, b >> 16) << 16);
+    const uint32_t a0 = a & 0xFFFF, a1 = a >> 16, b0 = b & 0xFFFF, b1 = b >> 16;
+    uint32_t d0 = b0 + kOrd16 - a0, d1 = b1 + kOrd16 - a1;
+    d0 = d0 >= kOrd16 ? d0 - kOrd16 : d0;
+    d1 = d1 >= kOrd16 ? d1 - kOrd16 : d1;
+    const uint32_t z0 = Z[d0], z1 = Z[d1];
+    auto fin = [](uint32_t x, uint32_t y, uint32_t z) {
+        uint32_t t = x + z;
+        t = t >= kOrd16 ? t - kOrd16 : t;
+        t = z == kNoLog16 ? kNoLog16 : t;
+        t = x == kNoLog16 ? y : t;
+        return y == kNoLog16 ? x : t;
+    };
+    return fin(a0, b0, z0) | (fin(a1, b1, z1) << 16);
 }
 
 __device__ __forceinline__ uint32_t lmul2(uint32_t s, uint32_t y) {
@@ -192,10 +204,68 @@ __device__ __forceinline__ void fbfly(const uint16_t* Z, uint32_t& di, uint32_t&
     dj = ladd2(Z, dj, di);
 }
 
+// Four independent log sums a[u] += b[u] with the four Zech lookups issued
+// together (one LDS round trip instead of four)
+__device__ __forceinline__ uint32_t zidx(uint32_t a, uint32_t b) {
+    const uint32_t d = b + kOrd16 - a;
+    return d >= kOrd16 ? d - kOrd16 : d;
+}
+
+__device__ __forceinline__ uint32_t zfin(uint32_t a, uint32_t b, uint32_t z) {
+    uint32_t s = a + z;
+    s = s >= kOrd16 ? s - kOrd16 : s;
+    s = z == kNoLog16 ? kNoLog16 : s;
+    s = a == kNoLog16 ? b : s;
+    return b == kNoLog16 ? a : s;
+}
+
+__device__ __forceinline__ void ladd_x4(const uint16_t* Z, uint32_t (&a)[4], const uint32_t (&b)[4]) {
+    uint32_t z[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) z[u] = Z[zidx(a[u], b[u])];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = zfin(a[u], b[u], z[u]);
+}
+
+// Two butterflies on column pairs in lockstep: (p, q) with constant sp and
+// (r, t) with constant sr.  Inverse: q += p; p += s q.  Forward: p += s q; q += p.
+__device__ __forceinline__ void ibfly_x2(const uint16_t* Z, uint32_t& p, uint32_t& q, uint32_t sp, uint32_t& r,
+                                         uint32_t& t, uint32_t sr) {
+    uint32_t x[4] = {q & 0xFFFF, q >> 16, t & 0xFFFF, t >> 16};
+    const uint32_t y[4] = {p & 0xFFFF, p >> 16, r & 0xFFFF, r >> 16};
+    ladd_x4(Z, x, y);
+    uint32_t w[4] = {y[0], y[1], y[2], y[3]};
+    const uint32_t m[4] = {lmul(sp, x[0]), lmul(sp, x[1]), lmul(sr, x[2]), lmul(sr, x[3])};
+    ladd_x4(Z, w, m);
+    p = w[0] | (w[1] << 16);
+    r = w[2] | (w[3] << 16);
+    q = x[0] | (x[1] << 16);
+    t = x[2] | (x[3] << 16);
+}
+
+__device__ __forceinline__ void fbfly_x2(const uint16_t* Z, uint32_t& p, uint32_t& q, uint32_t sp, uint32_t& r,
+                                         uint32_t& t, uint32_t sr) {
+    uint32_t w[4] = {p & 0xFFFF, p >> 16, r & 0xFFFF, r >> 16};
+    const uint32_t qv[4] = {q & 0xFFFF, q >> 16, t & 0xFFFF, t >> 16};
+    const uint32_t m[4] = {lmul(sp, qv[0]), lmul(sp, qv[1]), lmul(sr, qv[2]), lmul(sr, qv[3])};
+    ladd_x4(Z, w, m);
+    uint32_t x[4] = {qv[0], qv[1], qv[2], qv[3]};
+    ladd_x4(Z, x, w);
+    p = w[0] | (w[1] << 16);
+    r = w[2] | (w[3] << 16);
+    q = x[0] | (x[1] << 16);
+    t = x[2] | (x[3] << 16);
+}
+
 // One workgroup per CU (the Zech table fills 128 KiB of LDS, the strip the
 // other 32 KiB), persistent over the (generation, strip) items.  The strip is
 // held as logs: a butterfly is two Zech lookups and a log sum, and only the
 // strip's load and store touch the global log / exp tables.
+// LC: the constants of every layer in LDS (k <= 2,048), else read from global
+// memory; a template so that every access has a known address space (a
+// pointer that may be either compiles to flat loads, and those make the
+// compiler wait for all LDS and global traffic after each Zech lookup)
+template <bool LC>
 __global__ void __launch_bounds__(kFftThreads) k_fft16(Fft16Args A, uint32_t G) {
     __shared__ uint16_t sz[65536];
     __shared__ uint16_t buf[kFftLdsSymbols];
@@ -210,11 +280,9 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16(Fft16Args A, uint32_t G) 
     }
     // the butterfly constants of every layer, once per workgroup, when they fit
     const uint32_t n_cst = 2 * k + A.R - 2;
-    const uint16_t* cst = A.cst;
-    if (n_cst <= kFftLdsConsts) {
+    if (LC)
         for (uint32_t e = tid; e < n_cst; e += kFftThreads) scst[e] = A.cst[e];
-        cst = scst;
-    }
+    const uint16_t* cst = LC ? scst : A.cst;
     const uint16_t* cinv = cst;
     const uint16_t* cfk = cst + (k - 1);
     const uint16_t* cfwd = cfk + k;
@@ -287,11 +355,9 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16(Fft16Args A, uint32_t G) 
                 uint32_t* w = b32 + ((((B << (q + 2)) + (qi & (h - 1))) << lgP) + cp);
                 const uint32_t st = h << lgP;
                 uint32_t y0 = w[0], y1 = w[st], y2 = w[2 * st], y3 = w[3 * st];
-                ibfly(sz, y0, y1, c0[2 * B]);
-                ibfly(sz, y2, y3, c0[2 * B + 1]);
+                ibfly_x2(sz, y0, y1, c0[2 * B], y2, y3, c0[2 * B + 1]);
                 const uint32_t s1 = c1[B];
-                ibfly(sz, y0, y2, s1);
-                ibfly(sz, y1, y3, s1);
+                ibfly_x2(sz, y0, y2, s1, y1, y3, s1);
                 w[0] = y0;
                 w[st] = y1;
                 w[2 * st] = y2;
@@ -335,10 +401,8 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16(Fft16Args A, uint32_t G) 
                 const uint32_t st = h << lgP;
                 uint32_t d0 = w[0], d1 = w[st], d2 = w[2 * st], d3 = w[3 * st];
                 const uint32_t s1 = c1[B];
-                fbfly(sz, d0, d2, s1);
-                fbfly(sz, d1, d3, s1);
-                fbfly(sz, d0, d1, c0[2 * B]);
-                fbfly(sz, d2, d3, c0[2 * B + 1]);
+                fbfly_x2(sz, d0, d2, s1, d1, d3, s1);
+                fbfly_x2(sz, d0, d1, c0[2 * B], d2, d3, c0[2 * B + 1]);
                 w[0] = d0;
                 w[st] = d1;
                 w[2 * st] = d2;
@@ -511,7 +575,11 @@ int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t 
     A.strips = (nsym + S - 1) / S;
     const uint64_t items = (uint64_t)G * A.strips;
     hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
-    hipLaunchKernelGGL(k_fft16, dim3((uint32_t)std::min<uint64_t>(items, cus)), dim3(kFftThreads), 0, st, A, G);
+    const dim3 grid((uint32_t)std::min<uint64_t>(items, cus));
+    if (n_c <= kFftLdsConsts)
+        hipLaunchKernelGGL(k_fft16<true>, grid, dim3(kFftThreads), 0, st, A, G);
+    else
+        hipLaunchKernelGGL(k_fft16<false>, grid, dim3(kFftThreads), 0, st, A, G);
     QF_HIP(hipGetLastError());
     qf::ctx_prof_end(ctx, st, ev, name);
     return QF_OK;
