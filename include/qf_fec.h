@@ -421,6 +421,14 @@ int qf_adaptive_state(const qf_adaptive *a, int32_t *mode, uint32_t *window, uin
 /* Largest number of packets one on_send can emit (1 + repairs of the
  * current and the cross-fade configuration). */
 uint32_t qf_adaptive_max_send_packets(const qf_adaptive *a);
+/* Largest number of packets one on_receive can recover: the k of the
+ * current decoder plus the k of the cross-fade decoder (both may complete
+ * on the same packet, adaptive.rs:566-599).  A host sizes its reusable
+ * receive buffers from it (INTEGRATION.md AdaptiveFec). */
+uint32_t qf_adaptive_max_receive_packets(const qf_adaptive *a);
+/* Smallest coeff_stride on_send accepts for the current and cross-fade
+ * encoders: k bytes (GF(2^8)) or 2 k bytes (GF(2^16) Extreme windows). */
+uint32_t qf_adaptive_max_coeff_bytes(const qf_adaptive *a);
 /* AdaptiveFec::on_send (adaptive.rs:519-544) + emit_repairs (546-562): the
  * systematic packet, then the cross-fade configuration's repairs (while more
  * than CROSS_FADE_LEN/2 packets of the fade remain), then the current

@@ -165,6 +165,8 @@ _SIGS = {
     "qf_adaptive_free": (_I, [_P]),
     "qf_adaptive_state": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "qf_adaptive_max_send_packets": (_U32, [_P]),
+    "qf_adaptive_max_receive_packets": (_U32, [_P]),
+    "qf_adaptive_max_coeff_bytes": (_U32, [_P]),
     "qf_adaptive_on_send": (_I, [_P, _U64, _P, _U32, _P, _U32, _P, _U32, _P, _U32, _P]),
     "qf_adaptive_on_send_batch": (_I, [_P, _U32, _P, _P, _P, _P, _U32, _P, _U32, _P, _U32, _P, _P]),
     "qf_adaptive_on_receive_batch": (_I, [_P, _U32, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32, _P, _P]),

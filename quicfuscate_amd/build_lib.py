@@ -173,7 +173,11 @@ def _bs_kernels(build_dir: Path) -> Path:
             rp = (rt - j0) // (npass - p)
             specs.append(bs.KernelSpec(k, rp, BS_PD, "synw", r_total=rt, j0=j0))
             j0 += rp
-    specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH) for (k, r) in BS_FFT]
+    # additive-FFT encode ('E'): default cache policy for the row loads (the
+    # boundary line a 1,200-B row shares with the next row / the neighbouring
+    # item stays in L2; non-temporal loads re-fetch it: FETCH_SIZE 1.085x ->
+    # 1.019x the source bytes, 1.133 -> 1.114 ms, profiles/r04a_lab_enc_traffic.json)
+    specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="") for (k, r) in BS_FFT]
     # additive-FFT fused decode ('C'): pd 2 (the ring holds a chunk + pd rows)
     # (default cache policy: neighbouring 1,200-B rows share their boundary
     # lines, and non-temporal loads / stores drop them before the reuse;

@@ -489,6 +489,19 @@ uint32_t qf_adaptive_max_send_packets(const qf_adaptive* a) {
     return m;
 }
 
+// the need on_receive checks against out_cap (both decoders of a cross-fade)
+uint32_t qf_adaptive_max_receive_packets(const qf_adaptive* a) {
+    if (!a) return 0;
+    return a->cur.k + (a->has_fade ? a->fade.k : 0);
+}
+
+uint32_t qf_adaptive_max_coeff_bytes(const qf_adaptive* a) {
+    if (!a) return 0;
+    uint32_t c = a->cur.has_enc() ? a->cur.coeff_bytes() : 0;
+    if (a->has_fade && a->fade.has_enc() && a->fade.coeff_bytes() > c) c = a->fade.coeff_bytes();
+    return c;
+}
+
 int qf_adaptive_on_send(qf_adaptive* a, uint64_t id, const uint8_t* data, uint32_t len, uint8_t* out_data,
                         uint32_t out_stride, uint8_t* out_coeffs, uint32_t coeff_stride, qf_packet_desc* out_desc,
                         uint32_t out_cap, uint32_t* n_out) {

@@ -324,6 +324,104 @@ static void test_adaptive(qf_ctx *ctx) {
     printf("adaptive ok\n");
 }
 
+/* The buffer pattern of INTEGRATION.md's AdaptiveFec: output rows, coefficient
+ * blocks and descriptors are owned by the connection, sized from
+ * qf_adaptive_max_send_packets / _max_coeff_bytes / _max_receive_packets and
+ * grown (never re-allocated per packet), across 16 generations = 1,024
+ * on_receive calls.  After each generation both sides report the loss, which
+ * rebuilds their codecs (adaptive.rs:602-630), as a connection's loss report
+ * would; every recovered payload is checked. */
+typedef struct {
+    uint8_t *data, *coeffs;
+    qf_packet_desc *desc;
+    size_t rows, coeff_bytes, grows;
+} reuse_bufs;
+
+static void reuse_grow(reuse_bufs *b, size_t rows, size_t row_bytes, size_t coeff_bytes) {
+    if (rows <= b->rows && coeff_bytes <= b->coeff_bytes) return;
+    if (rows < b->rows) rows = b->rows;
+    if (coeff_bytes < b->coeff_bytes) coeff_bytes = b->coeff_bytes;
+    b->data = realloc(b->data, rows * row_bytes);
+    b->coeffs = realloc(b->coeffs, rows * (coeff_bytes ? coeff_bytes : 1));
+    b->desc = realloc(b->desc, rows * sizeof(qf_packet_desc));
+    CHECK(b->data && b->coeffs && b->desc, "realloc");
+    b->rows = rows, b->coeff_bytes = coeff_bytes, ++b->grows;
+}
+
+static void test_adaptive_reuse(qf_ctx *ctx) {
+    qf_fec_config cfg;
+    qf_fec_config_default(&cfg);
+    cfg.initial_mode = QF_MODE_NORMAL;
+    cfg.max_len = 1200;
+    qf_adaptive *snd, *rcv;
+    QF(qf_adaptive_new_at(ctx, &cfg, 0.0, &snd));
+    QF(qf_adaptive_new_at(ctx, &cfg, 0.0, &rcv));
+    uint32_t k, n;
+    QF(qf_adaptive_state(snd, NULL, NULL, &k, &n, NULL, NULL, NULL));
+    CHECK(qf_adaptive_max_receive_packets(rcv) == k, "max_receive_packets = k outside a cross-fade");
+    CHECK(qf_adaptive_max_coeff_bytes(snd) == k, "max_coeff_bytes = k (GF(2^8))");
+    const uint32_t L = 1200, gens = 16;
+    reuse_bufs sb = {0}, rb = {0};
+    uint8_t *pk = malloc((size_t)k * L), *rep = malloc((size_t)(n - k) * L), *rco = malloc((size_t)(n - k) * k);
+    uint8_t *got_rows = malloc((size_t)k * L);
+    uint32_t calls = 0;
+    for (uint32_t g = 0; g < gens; ++g) {
+        for (size_t t = 0; t < (size_t)k * L; ++t) pk[t] = rnd8();
+        for (uint32_t i = 0; i < k; ++i) {
+            reuse_grow(&sb, qf_adaptive_max_send_packets(snd), cfg.max_len, qf_adaptive_max_coeff_bytes(snd));
+            uint32_t nout = 0;
+            QF(qf_adaptive_on_send(snd, (uint64_t)g * k + i, pk + (size_t)i * L, L, sb.data, cfg.max_len, sb.coeffs,
+                                   (uint32_t)sb.coeff_bytes, sb.desc, (uint32_t)sb.rows, &nout));
+            CHECK(nout == (i + 1 < k ? 1u : 1 + n - k), "gen %u packet %u: %u out", g, i, nout);
+            for (uint32_t j = 0; j + 1 < nout; ++j) {
+                memcpy(rep + (size_t)j * L, sb.data + (size_t)(1 + j) * cfg.max_len, L);
+                memcpy(rco + (size_t)j * k, sb.coeffs + (size_t)(1 + j) * sb.coeff_bytes, k);
+            }
+        }
+        uint32_t got = 0, m = 0;
+        uint8_t seen[256] = {0};
+        for (uint32_t i = 0; i < k; ++i) {
+            if ((i + g) % 13 == 5) continue;   /* lost */
+            reuse_grow(&rb, qf_adaptive_max_receive_packets(rcv), cfg.max_len, 0);
+            QF(qf_adaptive_on_receive(rcv, i, 1, pk + (size_t)i * L, L, NULL, 0, rb.data, cfg.max_len, rb.desc,
+                                      (uint32_t)rb.rows, &m));
+            ++calls;
+            for (uint32_t q = 0; q < m; ++q) {
+                const qf_packet_desc *d = &rb.desc[q];
+                CHECK(d->id < k && d->len == L && !seen[d->id], "gen %u recovered id %llu", g, (unsigned long long)d->id);
+                seen[d->id] = 1;
+                memcpy(got_rows + (size_t)d->id * L, rb.data + (size_t)q * cfg.max_len, L);
+            }
+            got += m;
+        }
+        for (uint32_t j = 0; j < n - k && got < k; ++j) {
+            reuse_grow(&rb, qf_adaptive_max_receive_packets(rcv), cfg.max_len, 0);
+            QF(qf_adaptive_on_receive(rcv, k + j, 0, rep + (size_t)j * L, L, rco + (size_t)j * k, k, rb.data,
+                                      cfg.max_len, rb.desc, (uint32_t)rb.rows, &m));
+            ++calls;
+            for (uint32_t q = 0; q < m; ++q) {
+                const qf_packet_desc *d = &rb.desc[q];
+                CHECK(d->id < k && d->len == L && !seen[d->id], "gen %u recovered id %llu", g, (unsigned long long)d->id);
+                seen[d->id] = 1;
+                memcpy(got_rows + (size_t)d->id * L, rb.data + (size_t)q * cfg.max_len, L);
+            }
+            got += m;
+        }
+        CHECK(got == k, "gen %u: recovered %u of %u", g, got, k);
+        CHECK(memcmp(got_rows, pk, (size_t)k * L) == 0, "gen %u payloads", g);
+        /* the next generation: a loss report rebuilds both codecs (no mode change in the dwell time) */
+        QF(qf_adaptive_report_loss_at(snd, 0, 100, 0.0));
+        QF(qf_adaptive_report_loss_at(rcv, 0, 100, 0.0));
+    }
+    CHECK(calls >= 1000, "only %u on_receive calls", calls);
+    CHECK(sb.grows == 1 && rb.grows == 1, "buffers grown %zu / %zu times (expected once)", sb.grows, rb.grows);
+    QF(qf_adaptive_free(snd));
+    QF(qf_adaptive_free(rcv));
+    free(sb.data); free(sb.coeffs); free(sb.desc); free(rb.data); free(rb.coeffs); free(rb.desc);
+    free(pk); free(rep); free(rco); free(got_rows);
+    printf("adaptive reuse ok (%u on_receive calls, one allocation per side)\n", calls);
+}
+
 /* qf_adaptive_on_send_batch / on_receive_batch over C connections: every
  * connection's repairs equal the oracle's encode of its window, and every
  * receiver recovers its generation. */
@@ -486,6 +584,7 @@ int main(void) {
     test_objects(ctx);
     test_wiedemann(ctx);
     test_adaptive(ctx);
+    test_adaptive_reuse(ctx);
     test_adaptive_batch(ctx);
     QF(qf_ctx_destroy(ctx));
     printf("ALL OK\n");

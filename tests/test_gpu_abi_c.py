@@ -25,5 +25,5 @@ def test_c_caller_against_oracle():
     p = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.strip().splitlines()[-1] == "ALL OK"
-    for part in ("batch ok", "options ok", "desc ok", "objects ok", "adaptive ok", "framing ok"):
+    for part in ("batch ok", "options ok", "desc ok", "objects ok", "adaptive ok", "adaptive reuse ok", "adaptive batch ok", "framing ok"):
         assert part in p.stdout

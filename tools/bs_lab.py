@@ -51,6 +51,23 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 4: where the encode's 8 % read over-fetch comes from (VERDICT r03
+    # item 2).  Run under rocprofv3 --pmc FETCH_SIZE: every variant has its own
+    # kernel symbol.  Non-temporal loads drop a row's boundary line before the
+    # next row (or the neighbouring item) reads it; the default policy keeps
+    # it in L2.  L:1024 rows are line-aligned (no shared lines at all): the
+    # FETCH_SIZE calibration of this access pattern.
+    ("e_warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("e_nt", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("e_lddef", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("e_nt_reads", 64, 16, 3, ("nostore", "ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("e_lddef_reads", 64, 16, 3, ("nostore", "st:nt", "ztail", "fft:8"), ALL),
+    ("e_nt_1024_reads", 64, 16, 3, ("nostore", "ld:nt", "st:nt", "ztail", "fft:8", "L:1024"), ALL),
+    ("e_lddef_1024_reads", 64, 16, 3, ("nostore", "st:nt", "ztail", "fft:8", "L:1024"), ALL),
+    ("e_nt_2", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
+    ("e_lddef_2", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+]
+VARIANTS_R03Z = [
     # round 3z: dense 1,200-B repair rows with the line-aligned item layout
     # (no zero-tail bytes: 1.3 % less traffic) against the zero-tail default
     ("z_warm", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8"), ALL),
