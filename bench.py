@@ -1090,7 +1090,7 @@ def cpu_gf_mul_loop(target_s=0.3):
 
     res = {"unit": "MB/s (10^6 products/s, one thread)", "published_mb_s": {
         "SSE2 table": 850, "AVX2 bit-sliced": 3000, "AVX-512 bit-sliced": 4800, "scalar fallback": 750}}
-    for kind in ("table", "dispatch", "sse2", "avx512"):
+    for kind in ("table", "dispatch", "sse2", "avx2", "avx512"):
         iters, dt = 64, 0.0
         while True:
             t0 = time.perf_counter()
@@ -1102,7 +1102,8 @@ def cpu_gf_mul_loop(target_s=0.3):
         res[kind] = "not available on this host" if acc < 0 else {
             "mb_s": round(1024 * iters / dt / 1e6, 1), "passes": iters, "seconds": round(dt, 3), "acc": acc}
     res["note"] = ("table = gf_mul_table; dispatch = gf_mul through dispatch_bitslice (the reference's gf_mul); "
-                   "sse2 / avx512 = the CLMUL-fold members called directly (defective fold, SURVEY F3)")
+                   "sse2 / avx2 / avx512 = the CLMUL-fold members called directly, gf_tables.rs:129-141 / 102-118 / "
+                   "76-94 (defective fold, SURVEY F3)")
     return res
 
 

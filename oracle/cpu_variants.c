@@ -220,6 +220,7 @@ typedef struct {
 static feature_map g_features;
 static int g_detector_state; /* Once: 0 new, 2 complete */
 static int g_have_vpclmul;   /* this host can run the 512-bit member (avx512dq + vpclmulqdq) */
+static int g_have_vpclmul256;   /* ... and the 256-bit member (avx2 + vpclmulqdq) */
 
 static void map_insert(feature_map *m, uint8_t f, uint8_t v) {
     const uint64_t h = siphash13_u64(m->k0, m->k1, f);
@@ -248,6 +249,7 @@ static const feature_map *detector_instance(void) {
         map_insert(m, F_AESNI, (uint8_t)!!__builtin_cpu_supports("aes"));
         map_insert(m, F_PCLMULQDQ, (uint8_t)!!__builtin_cpu_supports("pclmul"));
         g_have_vpclmul = __builtin_cpu_supports("avx512dq") && __builtin_cpu_supports("vpclmulqdq");
+        g_have_vpclmul256 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("vpclmulqdq");
         __atomic_store_n(&g_detector_state, 2, __ATOMIC_RELEASE);
     }
     return &g_features;
@@ -272,6 +274,22 @@ __attribute__((target("avx512f,avx512dq,avx512vbmi,vpclmulqdq,pclmul"))) static 
     const __m512i vb = _mm512_broadcast_i64x2(_mm_set_epi64x(0, b));
     const __m512i prod = _mm512_clmulepi64_epi128(va, vb, 0x00);
     uint16_t t = (uint16_t)_mm_extract_epi16(_mm512_castsi512_si128(prod), 0);
+    t ^= t >> 8;
+    t ^= t >> 4;
+    t ^= t >> 2;
+    t ^= t >> 1;
+    return (uint8_t)(t & 0xFF);
+}
+
+/* gf_tables.rs:102-118 gf_mul_bitsliced_avx2: both operands broadcast into a
+ * 256-bit register, one 256-bit VPCLMULQDQ (_mm256_clmulepi64_epi128), the low
+ * 16 bits of lane 0 folded as the other members do (the same defective fold,
+ * SURVEY F3).  Needs avx2 + vpclmulqdq. */
+__attribute__((target("avx2,vpclmulqdq,pclmul"))) static uint8_t clmul_fold_avx2(uint8_t a, uint8_t b) {
+    const __m256i va = _mm256_broadcastsi128_si256(_mm_set_epi64x(0, a));
+    const __m256i vb = _mm256_broadcastsi128_si256(_mm_set_epi64x(0, b));
+    const __m256i prod = _mm256_clmulepi64_epi128(va, vb, 0x00);
+    uint16_t t = (uint16_t)_mm_extract_epi16(_mm256_castsi256_si128(prod), 0);
     t ^= t >> 8;
     t ^= t >> 4;
     t ^= t >> 2;
@@ -445,9 +463,26 @@ int cpu_encode_clmul_dispatch(uint32_t k, uint32_t r, uint32_t L, uint32_t G, co
  *                     then the CLMUL member) -- the reference's own gf_mul
  *   kind 2 "sse2"     gf_mul_bitsliced_sse2 (gf_tables.rs:129-141, one PCLMULQDQ + fold)
  *   kind 3 "avx512"   gf_mul_bitsliced_avx512 (gf_tables.rs:76-94, VPCLMULQDQ)
- * Kinds 1-3 compute the reference's defective fold: timing only.
+ *   kind 4 "avx2"     gf_mul_bitsliced_avx2 (gf_tables.rs:102-118, 256-bit VPCLMULQDQ)
+ * Kinds 1-4 compute the reference's defective fold: timing only.
  * Returns the final acc (>= 0), or -3 when this host lacks the instructions. */
 #define BB(x) __asm__ volatile("" : "+r"(x))
+/* one product of a CLMUL member (2 sse2, 3 avx512, 4 avx2), for the test that
+ * the three members compute the same fold; -3 when the host lacks it */
+int cpu_clmul_fold_pair(int kind, uint8_t a, uint8_t b) {
+#if defined(__x86_64__)
+    (void)detector_instance();
+    if (!cpu_has_pclmul()) return -3;
+    if (kind == 2) return clmul_fold(a, b);
+    if (kind == 3) return g_have_vpclmul ? clmul_fold_avx512(a, b) : -3;
+    if (kind == 4) return g_have_vpclmul256 ? clmul_fold_avx2(a, b) : -3;
+#else
+    (void)a, (void)b;
+#endif
+    (void)kind;
+    return -3;
+}
+
 int cpu_gf_mul_loop(int kind, uint64_t iters) {
     uint8_t a[1024], b[1024];
     for (int i = 0; i < 1024; ++i) {
@@ -503,6 +538,20 @@ int cpu_gf_mul_loop(int kind, uint64_t iters) {
                 BB(x);
                 BB(y);
                 acc ^= clmul_fold_avx512(x, y);
+            }
+            BB(acc);
+        }
+        return acc;
+    }
+    if (kind == 4) {
+        (void)detector_instance();
+        if (!g_have_vpclmul256) return -3;
+        for (uint64_t it = 0; it < iters; ++it) {
+            for (int i = 0; i < 1024; ++i) {
+                uint8_t x = a[i], y = b[i];
+                BB(x);
+                BB(y);
+                acc ^= clmul_fold_avx2(x, y);
             }
             BB(acc);
         }

@@ -279,7 +279,15 @@ def decode16(k: int, row_index, rows: np.ndarray, row_coeffs: np.ndarray | None 
     return s, out[:, :L], mask
 
 
-GF_MUL_LOOP_KINDS = {"table": 0, "dispatch": 1, "sse2": 2, "avx512": 3}
+GF_MUL_LOOP_KINDS = {"table": 0, "dispatch": 1, "sse2": 2, "avx512": 3, "avx2": 4}
+_lib.cpu_clmul_fold_pair.argtypes = [ctypes.c_int, ctypes.c_uint8, ctypes.c_uint8]
+_lib.cpu_clmul_fold_pair.restype = ctypes.c_int
+
+
+def clmul_fold_pair(kind: str, a: int, b: int) -> int:
+    """One product of the reference's CLMUL member `kind` (sse2 / avx512 /
+    avx2, gf_tables.rs:76-141; the defective fold), -3 if absent."""
+    return _lib.cpu_clmul_fold_pair(GF_MUL_LOOP_KINDS[kind], a, b)
 
 
 def gf_mul_loop(kind: str, iters: int) -> int:

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 
-@pytest.mark.parametrize("kind", ["table", "dispatch", "sse2", "avx512"])
+@pytest.mark.parametrize("kind", ["table", "dispatch", "sse2", "avx512", "avx2"])
 def test_gf_mul_micro_loop(oracle, kind):
     """benches/gf_bitslice_bench.rs:17-102: a[i] = i, b[i] = 255 - i over
     1,024 pairs; every product appears four times, so the XOR is 0 for the
@@ -14,6 +14,17 @@ def test_gf_mul_micro_loop(oracle, kind):
     if acc == -3:
         pytest.skip(f"{kind} needs instructions this host lacks")
     assert acc == 0
+
+
+@pytest.mark.parametrize("kind", ["avx512", "avx2"])
+def test_clmul_members_agree_with_sse2(oracle, kind):
+    """gf_mul_bitsliced_avx2 / _avx512 (gf_tables.rs:76-118) compute the same
+    fold as gf_mul_bitsliced_sse2 (:129-141) on every operand pair."""
+    if oracle.clmul_fold_pair(kind, 3, 7) == -3:
+        pytest.skip(f"{kind} needs instructions this host lacks")
+    for a in range(256):
+        for b in range(0, 256, 5):
+            assert oracle.clmul_fold_pair(kind, a, b) == oracle.clmul_fold_pair("sse2", a, b), (a, b)
 
 
 def test_gf_mul_micro_loop_table_matches_products(oracle):

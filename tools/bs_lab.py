@@ -51,6 +51,20 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 4b: source rows as pool blocks of round_up(L, 128) bytes ("srs:1280":
+    # every row starts on a 128-B line; the reference keeps each packet in its
+    # own 4,096-B pool block, optimize.rs:139, 440-530) against dense 1,200-B rows
+    ("s_warm", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("s_dense", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("s_1280", 64, 16, 3, ("st:nt", "ztail", "fft:8", "srs:1280"), ALL),
+    ("s_dense_reads", 64, 16, 3, ("nostore", "st:nt", "ztail", "fft:8"), ALL),
+    ("s_1280_reads", 64, 16, 3, ("nostore", "st:nt", "ztail", "fft:8", "srs:1280"), ALL),
+    ("s_1280_nt", 64, 16, 3, ("ld:nt", "st:nt", "ztail", "fft:8", "srs:1280"), ALL),
+    ("s_1280_pd4", 64, 16, 4, ("st:nt", "ztail", "fft:8", "srs:1280"), ALL),
+    ("s_dense_2", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("s_1280_2", 64, 16, 3, ("st:nt", "ztail", "fft:8", "srs:1280"), ALL),
+]
+VARIANTS_R04A = [
     # round 4: where the encode's 8 % read over-fetch comes from (VERDICT r03
     # item 2).  Run under rocprofv3 --pmc FETCH_SIZE: every variant has its own
     # kernel symbol.  Non-temporal loads drop a row's boundary line before the
@@ -181,7 +195,8 @@ def run(G: int, reps: int):
         blocks = min((n_items + 3) // 4, ncu * m["blocks_per_cu"])
         wide = "dst:wide" in m["flags"]
         drs, dgs = (2048, 32768) if wide else ((16 * Lv, 16 * Lv * r) if zt else (L, r * L))
-        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * L, dgs, L, drs, L, G, blocks * 4, Lv=Lv, zero_tail=zt)
+        srs = next((int(f[4:]) for f in m["flags"] if f.startswith("srs:")), L)
+        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * srs, dgs, srs, drs, L, G, blocks * 4, Lv=Lv, zero_tail=zt)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,

@@ -36,6 +36,19 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 4b: received rows as pool blocks of round_up(L, 128) = 1,280 B
+    # (rs/rrs; every row starts on a 128-B line) with the library's Q = 38
+    # lane-chunks per generation, against dense 1,200-B rows
+    ("d_warm", dict(LIB_DEC), ()),
+    ("d_lib", dict(LIB_DEC), ()),
+    ("d_1280", {**LIB_DEC, "rs": 1280, "rrs": 1280}, ()),
+    ("d_nolu", {**LIB_DEC, "lu": False}, ()),
+    ("d_1280_nolu", {**LIB_DEC, "rs": 1280, "rrs": 1280, "lu": False}, ()),
+    ("d_1280_rrs1200", {**LIB_DEC, "rs": 1280}, ()),
+    ("d_lib_2", dict(LIB_DEC), ()),
+    ("d_1280_2", {**LIB_DEC, "rs": 1280, "rrs": 1280}, ()),
+]
+VARIANTS_R03Y = [
     # round 3y: the FFT row loop alone with ONE wave per SIMD (cap = 256 blocks
     # of 4 waves: one per CU), register ring vs deep LDS staging -- the
     # ceiling of a producer/consumer split (row-loop waves + LU waves)

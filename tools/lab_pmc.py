@@ -36,12 +36,16 @@ def main() -> None:
     ap.add_argument("--manifest", default=str(REPO / "tools" / "lab_build" / "manifest.json"))
     ap.add_argument("--out", default="")
     ap.add_argument("--command", default="")
+    ap.add_argument("--dec", action="store_true", help="decode lab (dec_manifest.json): k = 64 rows read, e = 13 written")
     a = ap.parse_args()
     from quicfuscate_amd import bs_codegen as bs
 
     fetch = per_dispatch(Path(a.fetch_dir), "FETCH_SIZE")
     write = per_dispatch(Path(a.write_dir), "WRITE_SIZE")
-    man = {m["symbol"]: m for m in json.loads(Path(a.manifest).read_text())}
+    mpath = Path(a.manifest)
+    if a.dec and mpath.name == "manifest.json":
+        mpath = mpath.with_name("dec_manifest.json")
+    man = {m["symbol"]: m for m in json.loads(mpath.read_text())}
     out = {"_note": "FETCH_SIZE(KiB)*1024*2 and WRITE_SIZE(KiB)*1024, median over dispatches, per lab kernel; "
                     "known = the bytes the variant must move (source reads G k L; zero-tail repair writes G r 16 Lv)",
            "_command": a.command, "G": a.G}
@@ -50,13 +54,18 @@ def main() -> None:
         w = [v for n, vs in write.items() if sym in n for v in vs]
         if not f:
             continue
-        k, r, L = m["k"], m["r"], m["L"]
-        Lv = bs.padded_units(L)
-        known_r = a.G * k * L
-        known_w = 0 if "nostore" in m["flags"] else a.G * r * 16 * Lv
+        if a.dec:   # C3 shape: 64 received rows read (the 13 zero rows hit L2), 13 rows written
+            L = 1200
+            known_r = a.G * 64 * L
+            known_w = 0 if "nostore" in m["flags"] else a.G * 13 * L
+        else:
+            k, r, L = m["k"], m["r"], m["L"]
+            Lv = bs.padded_units(L)
+            known_r = a.G * k * L
+            known_w = 0 if "nostore" in m["flags"] else a.G * r * 16 * Lv
         fb = statistics.median(f) * 1024 * 2
         wb = statistics.median(w) * 1024 if w else None
-        out[m["name"]] = {"flags": m["flags"], "L": L, "known_read_bytes": known_r, "fetch_bytes_x2": int(fb),
+        out[m["name"]] = {"flags": m["flags"], "kw": m.get("kw"), "L": L, "known_read_bytes": known_r, "fetch_bytes_x2": int(fb),
                           "read_ratio": round(fb / known_r, 4), "known_write_bytes": known_w,
                           "write_bytes": None if wb is None else int(wb),
                           "write_ratio": None if not (wb and known_w) else round(wb / known_w, 4),
