@@ -136,6 +136,9 @@ def parse(argv=None):
     ap.add_argument("--c3b-G", type=int, default=65536,
                     help="generations of the C3 secondary variant (i.i.d. 20 %% loss over all k + r rows; 0 = skip)")
     ap.add_argument("--host-path-G", type=int, default=16384, help="generations for the pinned-host encode rate (0=skip)")
+    ap.add_argument("--c5-mixed-bytes", type=float, default=4e9,
+                    help="C5 (BASELINE configs[4]): source bytes of the heterogeneous batch; 0 skips the c5 leg")
+    ap.add_argument("--c5-shape-bytes", type=float, default=1e9, help="C5: source bytes per shape and mode")
     ap.add_argument("--overlap", action="store_true",
                     help="run the step's encode and decode (independent batches) on two HIP streams")
     ap.add_argument("--split", action="store_true", default=True,
@@ -420,6 +423,18 @@ def main(argv=None):
     dom = max(kern_step_ms, key=kern_step_ms.get)
     tfile = REPO / "profiles" / "traffic.json"
     sqfile = REPO / "profiles" / "sq_counters.json"
+    hfile = REPO / "quicfuscate_amd" / "lib" / "kernel_hashes.json"
+    try:
+        code_sha = json.loads(hfile.read_text())
+    except Exception:
+        code_sha = {}
+
+    def profile_current(name, ent):
+        """A committed counter profile describes this run's kernel only if it
+        recorded the code object it measured and the built kernel still has
+        that hash (no stale counters in the line)."""
+        want = next((v for n_, v in code_sha.items() if name == n_ or name.startswith(n_)), None)
+        return want is not None and ent.get("code_sha16") == want
     props = torch.cuda.get_device_properties(dev)
     n_simd = 4 * props.multi_processor_count
     clk_ghz = (getattr(props, "clock_rate", 0) or 2_400_000) / 1e6   # kHz -> GHz (MI355X engine clock 2.4)
@@ -438,7 +453,7 @@ def main(argv=None):
         except Exception:
             return None
         ent = next((v for n_, v in sq.items() if n_ == name or n_.startswith(name)), None)
-        if not ent or not ent.get("SQ_WAVES"):
+        if not ent or not ent.get("SQ_WAVES") or not profile_current(name, ent):
             return None
         per_wave = ent["SQ_INSTS_VALU"] / ent["SQ_WAVES"]
         waves = ent["SQ_WAVES"]
@@ -452,7 +467,8 @@ def main(argv=None):
                 "lane_ops_per_byte_mult": per_bm,
                 "unit": "G wave64 VALU instr/s", "frac": round(issue_ms / ms, 4),
                 "valu_per_wave": round(per_wave, 1), "waves": int(waves), "issue_ms": round(issue_ms, 4),
-                "source": "profiles/sq_counters.json (SQ_INSTS_VALU / SQ_WAVES, separate --pmc pass of this workload)"}
+                "source": "profiles/sq_counters.json (SQ_INSTS_VALU / SQ_WAVES, separate --pmc pass of this workload; "
+                          "its code_sha16 equals the built kernel's)"}
 
     def roofline(name):
         ms = kern_ms[name]
@@ -461,7 +477,8 @@ def main(argv=None):
         if tfile.exists():
             try:
                 tj = json.loads(tfile.read_text()).get(name, {})
-                if tj.get("k") == k and tj.get("r") == r and tj.get("L") == Lb and tj.get("G") == G:
+                if (tj.get("k") == k and tj.get("r") == r and tj.get("L") == Lb and tj.get("G") == G
+                        and profile_current(name, tj)):
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -485,7 +502,9 @@ def main(argv=None):
                 "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBPS, 4), "valu": vr, "traffic": traffic,
                 "traffic_source": ("profiles/traffic.json: FETCH_SIZE x2 + WRITE_SIZE from separate rocprofv3 --pmc "
-                                   "runs of this workload, not this run" if traffic is not None else None),
+                                   "runs of this workload, not this run; the profile's code_sha16 equals the built "
+                                   "kernel's (quicfuscate_amd/lib/kernel_hashes.json)" if traffic is not None else
+                                   "none: no --pmc pass of the kernel as built (profiles/traffic.json code_sha16)"),
                 "algorithmic_bytes_per_launch": alg_bytes(name)}
 
     enc_kernel = next((n for n in kern_ms if n.startswith(("qf_cauchy_bs", "k_combine_uniform"))), None)
@@ -588,6 +607,9 @@ def main(argv=None):
         torch.cuda.empty_cache()
         out["c4"] = c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, r, Lb, e, args.c4_G,
                            args.c4_steps, args.warmup, args.rank_sample, split=args.c4_split)
+
+    if rank == 0 and world == 1 and args.c5_mixed_bytes > 0:
+        out["c5"] = c5_leg(fec, ctx, args.c5_mixed_bytes, args.c5_shape_bytes)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -718,6 +740,26 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
             "kernel_ms_per_launch": {n: round(ms / max(1, c), 4) for n, (c, ms) in kt.items()},
             "schedule": "split" if split else "serial",
             "oracle_sample_generations_per_rank": rank_sample, "verified": bad == 0}
+
+
+def c5_leg(fec, ctx, mixed_bytes: float, shape_bytes: float, reps: int = 3) -> dict:
+    """BASELINE configs[4] (adaptive.rs:124-153 / 519-562):
+    ASW-RLNC-X windows k = 32..196 at 9,000-B jumbo rows, r = ceil(k ratio) - k.
+    One heterogeneous batch of all seven shapes (qf_encode_batch_desc /
+    qf_decode_batch_desc, >= 4 GB of source, every recovered row verified on
+    the device), then per shape block encode, block decode at 20 % loss and
+    sliding encode (one window per source packet).  Bytes: block (k + r) L,
+    decode (k + e) L, sliding (1 + r) L per window with its VALU fraction
+    (compute-bound by construction).  Outside the headline's timed steps."""
+    import sys
+
+    sys.path.insert(0, str(REPO / "tools"))
+    import bench_c5
+
+    t0 = time.perf_counter()
+    res = bench_c5.c5_bench(fec, ctx, mixed_bytes, shape_bytes, reps)
+    res["seconds"] = round(time.perf_counter() - t0, 1)
+    return res
 
 
 def gather_flags(torch, dist, flag: int, world: int, device) -> list:

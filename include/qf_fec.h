@@ -130,6 +130,11 @@ enum {
                                     k = 2^a in [16, 4096] (first + r <= k) without a bit-sliced kernel:
                                     1 where it needs ~9x fewer products than the matvec, 2 always,
                                     0 never [QF_GF16_FFT; default 1] */
+    QF_OPT_WIEDEMANN_PROJ,       /* k > 256 decoder's projections: 1 = the reference's first init vector
+                                    (decoder.rs:805-807, b = 0), then random vectors drawn per attempt
+                                    from a per-process secret (a packet sender cannot craft a matrix
+                                    that defeats them and forces the exact host fallback); 0 = the
+                                    reference's init vectors b = 0..7 only [QF_WIEDEMANN_PROJ; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);
@@ -332,6 +337,10 @@ int qf_decoder_new(qf_ctx *ctx, uint32_t k, uint32_t max_len, qf_decoder **out);
 #define QF_STRATEGY_GAUSSIAN 0
 #define QF_STRATEGY_WIEDEMANN 1
 int qf_decoder_strategy(const qf_decoder *dec);
+/* Projections the last Wiedemann solve of this decoder tried (1..8; 9 = none
+ * verified and exact elimination decided); 0 before any
+ * Wiedemann solve and for k <= 256 decoders. */
+int qf_decoder_solve_attempts(const qf_decoder *dec);
 int qf_decoder_free(qf_decoder *dec);
 /* replaces decoder.rs:678 Decoder::add_packet.  Returns 1 when the generation
  * is decoded, 0 when more packets are needed, QF_EINVAL for a repair packet

@@ -166,6 +166,7 @@ _SIGS = {
     "qf_adaptive_state": (_I, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "qf_adaptive_max_send_packets": (_U32, [_P]),
     "qf_adaptive_max_receive_packets": (_U32, [_P]),
+    "qf_decoder_solve_attempts": (_I, [_P]),
     "qf_adaptive_max_coeff_bytes": (_U32, [_P]),
     "qf_adaptive_on_send": (_I, [_P, _U64, _P, _U32, _P, _U32, _P, _U32, _P, _U32, _P]),
     "qf_adaptive_on_send_batch": (_I, [_P, _U32, _P, _P, _P, _P, _U32, _P, _U32, _P, _U32, _P, _P]),
@@ -190,7 +191,7 @@ OPTIONS = {n: i for i, n in enumerate([
     "decode_ksplit", "decode_synw", "decode_pd", "decode_chunk", "decode_overlap", "combine_bs",
     "combine_bs_min_q", "combine_split", "prepare_grid", "enc_blocks_per_cu", "dec_blocks_per_cu", "send_fused",
     "send_windows_min_tiles", "send_chunks", "send_profile", "copy_threads", "gf16_dyn", "gf16_logify",
-    "gf16_logify_min_blocks", "gf16_lds_gj", "gf16_bitsliced", "gf16_fft"])}
+    "gf16_logify_min_blocks", "gf16_lds_gj", "gf16_bitsliced", "gf16_fft", "wiedemann_proj"])}
 QF_OPT_COUNT = len(OPTIONS)
 
 

@@ -1071,6 +1071,23 @@ def _epilogue_next_item(E, far: bool = False):
     E(Op("s_endpgm", ()))
 
 
+def valu_per_item(spec: KernelSpec) -> int:
+    """VALU instructions one item (one wave's pass over its 128 lane units)
+    issues: the ops from the item-loop head to its back-edge.  Exact for the
+    encode kernels (straight-line bodies); an upper bound where dec-mode guards
+    skip blocks.  bench.py prices the VALU roof of a kernel from it when no SQ
+    counter pass of that workload exists (C5 sliding windows)."""
+    ops = generate(spec)
+    start = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Litem")
+    n = 0
+    for op in ops[start + 1:]:
+        if op.name in ("s_far_jump", "s_branch") and op.args[0] == ".Litem":
+            break
+        if op.name.startswith("v_"):
+            n += 1
+    return n
+
+
 def generate(spec: KernelSpec) -> list[Op]:
     if spec.mode == "cmb":
         return _generate_cmb(spec)

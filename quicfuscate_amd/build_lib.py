@@ -12,6 +12,7 @@ build fails if any k_combine_* kernel reports scratch usage.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import json
 import os
 import re
 import shutil
@@ -142,12 +143,11 @@ def assemble(name: str, asm_text: str, out_dir: Path) -> Path:
     return hsaco
 
 
-def _bs_kernels(build_dir: Path) -> Path:
-    """Generate + assemble the bit-sliced kernels; emit a C include that
-    embeds the code objects."""
+def kernel_specs() -> list:
+    """Every generated kernel the library embeds (bs_codegen.KernelSpec), in
+    table order."""
     from . import bs_codegen as bs
 
-    entries, blobs = [], []
     specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn", "dec") for (k, r) in BS_CONFIGS]
     # fused decode over the lane-chunk layout (one generation per lane; the
     # default decode, 'c'); the 'd' kernels above stay for QF_DECODE_LEGACY=1
@@ -187,10 +187,26 @@ def _bs_kernels(build_dir: Path) -> Path:
               for (k, r) in BS_FFT]
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
+    return specs
+
+
+def _bs_kernels(build_dir: Path) -> Path:
+    """Generate + assemble the bit-sliced kernels; emit a C include that
+    embeds the code objects, and lib/kernel_hashes.json (sha256 of every code
+    object by kernel name: profiles/ record the hash of the kernel they
+    measured, bench.py uses a profile's counters only while it matches)."""
+    import hashlib
+
+    from . import bs_codegen as bs
+
+    entries, blobs = [], []
+    specs = kernel_specs()
+    hashes = {}
     for n, spec in enumerate(specs):
         k, r = spec.k, spec.r
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
         data = hsaco.read_bytes()
+        hashes[spec.name] = hashlib.sha256(data).hexdigest()[:16]
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         mode = ("C" if spec.fft else "k" if spec.ksplit > 1 else "c") if spec.chunked else \
@@ -203,6 +219,8 @@ def _bs_kernels(build_dir: Path) -> Path:
     kmax = int(re.search(r"kMax = (\d+)", (CSRC / "qf_bs.h").read_text()).group(1))
     if len(specs) > kmax:
         raise RuntimeError(f"{len(specs)} generated kernels > BsCache::kMax = {kmax} (qf_bs.h)")
+    OUT_DIR.mkdir(exist_ok=True)
+    (OUT_DIR / "kernel_hashes.json").write_text(json.dumps(hashes, indent=0, sort_keys=True))
     inc = build_dir / "qf_bs_blobs.inc"
     inc.write_text("// generated by quicfuscate_amd/build_lib.py from bs_codegen.py -- do not edit\n"
                    + "\n".join(blobs) + "\nstatic const QfBsEntry qf_bs_table[] = {\n"

@@ -6,6 +6,7 @@
 // path for encode or decode.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -77,6 +78,7 @@ struct qf_ctx {
     hipEvent_t desc_done = nullptr;
     // send batches: one event per download chunk
     std::vector<hipEvent_t> send_ev;
+    qf::SendProfile send_prof;
     // receive batches: pinned / device staging (rows, row indices, decode outputs)
     uint8_t* h_recv = nullptr;
     uint8_t* d_recv = nullptr;
@@ -170,6 +172,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* GF16_LDS_GJ */ {"QF_GF16_LDS_GJ", 0, 0, 1, false},
     /* GF16_BITSLICED */ {"QF_GF16_BITSLICED", 1, 0, 1, false},
     /* GF16_FFT */ {"QF_GF16_FFT", 1, 0, 2, false},
+    /* WIEDEMANN_PROJ */ {"QF_WIEDEMANN_PROJ", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }
@@ -936,6 +939,8 @@ int ctx_recv_release(qf_ctx* ctx) {
     QF_CHECK_HIP(hipEventRecord(ctx->recv_done, ctx->stream));
     return QF_OK;
 }
+SendProfile* ctx_send_profile(qf_ctx* ctx) { return &ctx->send_prof; }
+
 int ctx_send_events(qf_ctx* ctx, uint32_t n, hipEvent_t** out) {
     while (ctx->send_ev.size() < n) {
         hipEvent_t e = nullptr;
@@ -1115,6 +1120,13 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
 
 int qf_ctx_destroy(qf_ctx* c) {
     if (!c) return QF_OK;
+    if (const uint64_t n = c->send_prof.calls) {   // QF_OPT_SEND_PROFILE (qf_objects.hip encoders_send_batch)
+        const qf::SendProfile& p = c->send_prof;
+        fprintf(stderr, "[qf send batch] ctx %p: %llu calls, us/call: stage %.1f  launch %.1f  wait %.1f  copy-out %.1f\n",
+                (void*)c, (unsigned long long)n, 1e6 * p.t[0] / n, 1e6 * p.t[1] / n, 1e6 * p.t[2] / n, 1e6 * p.t[3] / n);
+        fprintf(stderr, "[qf send batch] ctx %p: stage = host %.1f + buffers %.1f + packets %.1f + upload %.1f\n",
+                (void*)c, 1e6 * p.u[0] / n, 1e6 * p.u[1] / n, 1e6 * p.u[2] / n, 1e6 * p.u[3] / n);
+    }
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (auto& kv : c->cauchy) hipFree(kv.second.dev);

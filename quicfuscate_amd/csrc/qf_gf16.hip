@@ -1154,9 +1154,19 @@ int encode16_window(qf_ctx* ctx, const qf_encode_shape* sh, uint32_t G, const ui
     // the reference's fixed Cauchy rows over an unrotated window: the
     // bit-sliced kernel of (k, r) if one is generated (qf_gf16_bs.hip)
     if (!coeff_rxk && !first && !rot && !coeff_be_dev && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED)) {
-        s = qf::gf16_bs_encode(ctx, st, k, r, L, G, src, sh->src_gen_stride, sh->src_row_stride, rep,
-                               sh->rep_gen_stride, sh->rep_row_stride);
-        if (s != qf::kGf16BsNone) return s;
+        // the bit-sliced kernel reads a partial last unit (L % 16 != 0) as a
+        // whole 16 B: up to 15 bytes past L.  Only the batch's last row can
+        // end its buffer, so the last generation takes the general path below
+        const uint32_t Gb = L % 16 ? G - 1 : G;
+        s = Gb ? qf::gf16_bs_encode(ctx, st, k, r, L, Gb, src, sh->src_gen_stride, sh->src_row_stride, rep,
+                                    sh->rep_gen_stride, sh->rep_row_stride)
+               : (qf::gf16_bs_has(k, r) ? QF_OK : qf::kGf16BsNone);
+        if (s != qf::kGf16BsNone) {
+            if (s != QF_OK || Gb == G) return s;
+            src += (size_t)Gb * sh->src_gen_stride;
+            rep += (size_t)Gb * sh->rep_gen_stride;
+            G = 1;
+        }
     }
     const uint16_t *glog, *gexp;
     s = qf::ctx_gf16_tables(ctx, &glog, &gexp);
@@ -1298,7 +1308,10 @@ int qf_decode16_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
     // Cauchy rows of a (k, r) with a generated bit-sliced kernel: syndromes
     // from qf_gf16bs_syn_* (maps 13..17, zero row), the general matvec only
     // for the generations it skips
-    const bool bs = !row_coeffs && r <= 64 && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED) && qf::gf16_bs_has(k, r);
+    // (L % 16 != 0: the bit-sliced syndrome kernel reads whole 16-B units, up
+    // to 15 bytes past the last row; the other syndrome paths read bytewise)
+    const bool bs = !row_coeffs && r <= 64 && L % 16 == 0 && qf::ctx_opt(ctx, QF_OPT_GF16_BITSLICED) &&
+                    qf::gf16_bs_has(k, r);
     // power-of-two k without one: the additive-FFT syndromes (qf_gf16_fft.hip)
     // over the same maps, constants in workspace slab 20
     const int64_t fft_opt = qf::ctx_opt(ctx, QF_OPT_GF16_FFT);

@@ -17,7 +17,11 @@
 // the lane owns units q, q + Q, q + 2Q, q + 3Q (< Lu) of row i of generation g,
 // so each 16-B load instruction covers consecutive units of a row.  The last
 // unit of a row with L % 16 != 0 is read whole (16-B aligned rows: the bytes
-// past L stay inside the same aligned 16 B) and stored bytewise.
+// past L stay inside the same aligned 16 B) and stored bytewise.  That read
+// can pass the end of the caller's buffer only on the batch's last row, so
+// the host never gives this kernel the last generation of such a batch
+// (qf_encode16_batch: general path for it) and never runs the syndrome
+// kernel at L % 16 != 0 (qf_gf16.hip).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -383,6 +383,11 @@ int qf_decoder_strategy(const qf_decoder* d) {
     return d->k > 256 ? QF_STRATEGY_WIEDEMANN : QF_STRATEGY_GAUSSIAN;
 }
 
+int qf_decoder_solve_attempts(const qf_decoder* d) {
+    if (!d) return QF_EINVAL;
+    return (int)d->w_tries;
+}
+
 // How the k accepted rows decode (decoder.rs:704-783): repair rows that are
 // Cauchy rows of this k (c_i = gf_inv(i ^ y), y = k + j: what Encoder emits
 // for a window aligned with the generation) decode by their repair index on
@@ -636,23 +641,6 @@ int qf_decoder_get_decoded_packets(qf_decoder* d, uint8_t* out_data, uint32_t ou
 namespace qf {
 
 namespace {
-// QF_OPT_SEND_PROFILE: per-phase host wall time of send batches, summed over
-// the calls of every context that has the option on, printed at process exit
-struct SendProfile {
-    bool on = false;      // the current call's context has the option on
-    uint64_t calls = 0, seen = 0;
-    double t[4] = {0, 0, 0, 0};
-    double u[4] = {0, 0, 0, 0};
-    ~SendProfile() {
-        if (on && calls)
-            fprintf(stderr, "[qf send batch] %llu calls, us/call: stage %.1f  launch %.1f  wait %.1f  copy-out %.1f\n",
-                    (unsigned long long)calls, 1e6 * t[0] / calls, 1e6 * t[1] / calls, 1e6 * t[2] / calls,
-                    1e6 * t[3] / calls);
-        if (on && calls)
-            fprintf(stderr, "[qf send batch] stage = host %.1f + buffers %.1f + packets %.1f + upload %.1f\n",
-                    1e6 * u[0] / calls, 1e6 * u[1] / calls, 1e6 * u[2] / calls, 1e6 * u[3] / calls);
-    }
-} g_send_prof;
 double wall() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -735,8 +723,9 @@ class CopyPool {
 int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     if (!ctx || (M && !v)) return QF_EINVAL;
     if (M == 0) return QF_OK;
-    g_send_prof.on = ctx_opt(ctx, QF_OPT_SEND_PROFILE) != 0;
-    const double tp0 = g_send_prof.on ? wall() : 0.0;
+    // QF_OPT_SEND_PROFILE of THIS context (per-context sums, printed at qf_ctx_destroy)
+    const bool prof = ctx_opt(ctx, QF_OPT_SEND_PROFILE) != 0;
+    const double tp0 = prof ? wall() : 0.0;
     for (uint32_t m = 0; m < M; ++m) {
         qf_encoder* e = v[m].e;
         if (!e || e->ctx != ctx || (v[m].len && !v[m].data) || v[m].len > e->max_len) return QF_EINVAL;
@@ -787,9 +776,9 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         rep_bytes += (size_t)(v[wins[w].m].e->n - v[wins[w].m].e->k) * round16(wins[w].L);
     }
     uint8_t *h = nullptr, *d = nullptr;
-    const double tpa = g_send_prof.on ? wall() : 0.0;
+    const double tpa = prof ? wall() : 0.0;
     if ((s = ctx_desc_buffers(ctx, rep_off0 + rep_bytes, &h, &d)) != QF_OK) return s;
-    const double tpb = g_send_prof.on ? wall() : 0.0;
+    const double tpb = prof ? wall() : 0.0;
     for (uint32_t m = 0; m < M; ++m) {
         uint8_t* dst = h + pk_off + slots[m].src_off;
         const uint32_t n = v[m].len, n16 = round16(n);
@@ -798,7 +787,7 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         slots[m].src_off += pk_off;
     }
     memcpy(h + slots_off, slots.data(), sizeof(RingSlot) * M);
-    const double tpc = g_send_prof.on ? wall() : 0.0;
+    const double tpc = prof ? wall() : 0.0;
     RingWin* hw = reinterpret_cast<RingWin*>(h + wins_off);
     for (size_t w = 0; w < wins.size(); ++w) {
         const qf_encoder* e = v[wins[w].m].e;
@@ -810,7 +799,7 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         hw[w].rep_row_stride = round16(wins[w].L);
     }
     if ((s = ctx_desc_upload(ctx, pk_off + pk)) != QF_OK) return s;
-    const double tp1 = g_send_prof.on ? wall() : 0.0;
+    const double tp1 = prof ? wall() : 0.0;
     QF_CHECK_HIP(launch_ring_scatter(d, reinterpret_cast<const RingSlot*>(d + slots_off), M, st));
     for (size_t w0 = 0; w0 < wins.size();) {
         const qf_encoder* e = v[wins[w0].m].e;
@@ -823,7 +812,7 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         if (s != QF_OK) return s;
         w0 = w1;
     }
-    const double tp2 = g_send_prof.on ? wall() : 0.0;
+    const double tp2 = prof ? wall() : 0.0;
     // the repairs out (decoder.rs:172-275): window[0].len bytes, ids after the newest
     auto copy_out = [&](uint32_t w) {
         EncSend& x = v[wins[w].m];
@@ -864,9 +853,9 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     }
     double t_wait = 0.0;
     for (uint32_t c = 0; c < chunks; ++c) {
-        const double tw = g_send_prof.on ? wall() : 0.0;
+        const double tw = prof ? wall() : 0.0;
         QF_CHECK_HIP(hipEventSynchronize(ev[c]));
-        if (g_send_prof.on) t_wait += wall() - tw;
+        if (prof) t_wait += wall() - tw;
         const uint32_t w0 = cw[c], n = cw[c + 1] - cw[c];
         if ((size_t)(chunks > 1 ? rep_bytes / chunks : rep_bytes) >= ((size_t)1 << 20)) {
             CopyPool::get(ctx_opt(ctx, QF_OPT_COPY_THREADS)).run(n, [&](uint32_t i) { copy_out(w0 + i); });
@@ -875,17 +864,18 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         }
     }
     const double tp3 = tp2 + t_wait;
-    if (g_send_prof.on && rep_bytes && ++g_send_prof.seen > 4) {   // steady state: windows full, buffers grown
+    SendProfile* sp = ctx_send_profile(ctx);
+    if (prof && rep_bytes && ++sp->seen > 4) {   // steady state: windows full, buffers grown
         const double tp4 = wall();
-        g_send_prof.calls++;
-        g_send_prof.t[0] += tp1 - tp0;
-        g_send_prof.u[0] += tpa - tp0;
-        g_send_prof.u[1] += tpb - tpa;
-        g_send_prof.u[2] += tpc - tpb;
-        g_send_prof.u[3] += tp1 - tpc;
-        g_send_prof.t[1] += tp2 - tp1;
-        g_send_prof.t[2] += tp3 - tp2;
-        g_send_prof.t[3] += tp4 - tp3;
+        sp->calls++;
+        sp->t[0] += tp1 - tp0;
+        sp->u[0] += tpa - tp0;
+        sp->u[1] += tpb - tpa;
+        sp->u[2] += tpc - tpb;
+        sp->u[3] += tp1 - tpc;
+        sp->t[1] += tp2 - tp1;
+        sp->t[2] += tp3 - tp2;
+        sp->t[3] += tp4 - tp3;
     }
     return QF_OK;
 }

@@ -38,7 +38,10 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <mutex>
+#include <random>
 #include <vector>
 
 #include "gf256_tables.h"
@@ -96,6 +99,7 @@ struct SeqArgs {
     uint8_t* poly;        // f_0..f_L (out)
     int32_t* info;        // [0] L, [1] 0 ok / 1 zero sequence / 2 singular
     uint32_t e, ep, kp, b;
+    uint32_t seed;        // 0: the reference's init vector b; else a random projection (init_u)
     uint32_t lm_lds;      // logs of M in LDS (2 e^2 bytes after the vectors)
     // baby-step / giant-step Krylov (s > 1): a_{i s + j} = w_i . v_j with
     // v_j = M^j u (j < s) and w_i = (M^T)^(s i) u, so 2e / s + s dependent
@@ -113,6 +117,18 @@ constexpr uint32_t kEx2 = 1040;          // exp over [0, 510), zero above
 constexpr uint32_t kRed2Bytes = 4096;
 constexpr uint32_t kBsgsMinE = 64;
 constexpr uint32_t kPsMinE = 16, kPsMaxE = 1024;
+
+// Entry i of the projection / start vector u: the reference's
+// u_i = (i + b + 1) mod 255 (decoder.rs:805-807, 934-941) for seed 0, else a
+// byte of a splitmix-style hash of (seed, i) -- a projection no sender can
+// predict (QF_OPT_WIEDEMANN_PROJ).
+__device__ __forceinline__ uint8_t init_u(const SeqArgs& a, uint32_t i) {
+    if (a.seed == 0) return (uint8_t)((i + a.b + 1) % 255);
+    uint64_t z = ((uint64_t)a.seed << 32 | i) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (uint8_t)((z ^ (z >> 31)) >> 24);
+}
 
 // Log-domain tables: ex2[lg[a] + lg[b]] = a * b for all a, b (lg[0] = kLogZero).
 __device__ void build_log_tables(uint8_t* ex2, uint16_t* lg) {
@@ -165,7 +181,7 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
     }
     if (a.gather_only) return;
     for (uint32_t i = tid; i < e; i += nt) {
-        const uint8_t ui = (uint8_t)((i + a.b + 1) % 255);
+        const uint8_t ui = init_u(a, i);
         lu[i] = lg[ui];
         v[i] = ui;
     }
@@ -219,7 +235,7 @@ __global__ void __launch_bounds__(kSeqThreads) k_w8_sequence(SeqArgs a) {
         }
         // giant steps: x = (M^T)^(s i) u; a_{i s + j} = x . V[j]; thread
         // (j = tid % s, stripe tid / s) sums a stripe, threads j < s fold
-        for (uint32_t i = tid; i < e; i += nt) v[i] = (uint8_t)((i + a.b + 1) % 255);
+        for (uint32_t i = tid; i < e; i += nt) v[i] = init_u(a, i);
         __threadfence_block();
         __syncthreads();
         const uint32_t sp = a.s, nst = nt / sp;
@@ -448,6 +464,22 @@ __attribute__((target("ssse3"))) static void row_axpy(uint8_t* dst, const uint8_
     }
 }
 
+// A nonzero 32-bit seed per random projection: splitmix64 over a per-process
+// secret (std::random_device at first use) and a counter, so the projections
+// of a k > 256 decode cannot be predicted from the packets it receives.
+static uint32_t projection_seed() {
+    static const uint64_t key = [] {
+        std::random_device rd;
+        return ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    }();
+    static std::atomic<uint64_t> ctr{0};
+    uint64_t z = key + 0x9E3779B97F4A7C15ull * (ctr.fetch_add(1, std::memory_order_relaxed) + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    const uint32_t v = (uint32_t)((z ^ (z >> 31)) >> 16);
+    return v ? v : 1;
+}
+
 // The exact fallback when no init vector verifies (every projection missed a
 // factor of M's minimal polynomial -- possible for a nonsingular M, so it is
 // not a rank verdict): Gauss-Jordan on [M | I] on the host, W = M^-1 with row
@@ -556,7 +588,7 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
     uint8_t* W = nullptr;
     const uint32_t ew = (e + 3) / 4;
     SeqArgs sa{w + oA, reinterpret_cast<const uint16_t*>(w + oE), w + oM, w + oP0,
-               reinterpret_cast<uint16_t*>(w + oLM), w + oPoly, info, e, ep, kp, 0, lm_lds};
+               reinterpret_cast<uint16_t*>(w + oLM), w + oPoly, info, e, ep, kp, 0, 0, lm_lds};
     sa.s = sb;
     if (sb > 1) {
         // M^T (gather pass), then (M^T)^s by squaring: out[i] = sum_l X[i][l] X[l]
@@ -576,9 +608,11 @@ int wiedemann_decode(qf_ctx* ctx, uint32_t k, uint32_t e, const uint8_t* A_ek, c
         sa.LMs = reinterpret_cast<uint16_t*>(w + oLMs);
         sa.V = w + oV;
     }
+    const bool random_proj = ctx_opt(ctx, QF_OPT_WIEDEMANN_PROJ) != 0;
     for (uint32_t b = 0; b < kTries; ++b) {
         if (tries_out) *tries_out = b + 1;
         sa.b = b;
+        sa.seed = random_proj && b > 0 ? projection_seed() : 0;
         hipLaunchKernelGGL(k_w8_sequence, dim3(1), dim3(seq_threads), seq_lds, st, sa);
         QF_CHECK_HIP(hipGetLastError());
         int32_t hinfo[2] = {0, 0};

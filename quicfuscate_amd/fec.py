@@ -500,6 +500,12 @@ class Decoder:
         s = check(L._lib().qf_decoder_strategy(self.handle))
         return "Wiedemann" if s == 1 else "GaussianElimination"
 
+    @property
+    def solve_attempts(self) -> int:
+        """Projections the last Wiedemann solve tried (1..8; 9 = exact
+        elimination decided; 0: none yet / k <= 256)."""
+        return check(L._lib().qf_decoder_solve_attempts(self.handle))
+
     def add_packet(self, packet: Packet) -> bool:
         """Returns is_decoded; raises for a repair packet without coefficients."""
         data = packet.payload()

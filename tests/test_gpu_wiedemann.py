@@ -181,14 +181,20 @@ def test_received_ids_kept(qf, gpu_ctx):
     assert [p.id for p in out] == [i if i in lost else ids[i] for i in range(k)]
 
 
+@pytest.mark.parametrize("proj", [0, 1])
 @pytest.mark.parametrize("k,lost_n", [(300, 300), (400, 40)])
-def test_wiedemann_exact_fallback(qf, oracle, gpu_ctx, k, lost_n):
-    """No init vector verifies (qf_wiedemann.hip's exact fallback): M on the
-    erased block is diag(c), c = 7 on positions {0, 1, 16, 17} of E and 11
-    elsewhere -- the init vectors XOR to zero over those positions for every
-    b < 8, so no projection sees the eigenvalue 7.  M is nonsingular, so the
-    generation decodes (exact elimination on the host), as in the oracle; the
-    received columns carry random coefficients."""
+def test_wiedemann_exact_fallback(qf, oracle, gpu_ctx, qf_opts, k, lost_n, proj):
+    """A matrix crafted against the reference's init vectors: M on the erased
+    block is diag(c), c = 7 on positions {0, 1, 16, 17} of E and 11 elsewhere
+    -- the init vectors b < 8 XOR to zero over those positions, so none of
+    them sees the eigenvalue 7.  With the reference's vectors only
+    (QF_OPT_WIEDEMANN_PROJ 0) no projection verifies and exact elimination on
+    the host decides (solve_attempts 9); with the default random projections
+    after the first (a sender must not be able to force the host
+    fallback) a projection verifies.  M is nonsingular, so the generation
+    decodes either way, as in the oracle; the received columns carry random
+    coefficients."""
+    qf_opts(wiedemann_proj=proj)
     rng = np.random.default_rng(k)
     L = 40
     src = rng.integers(0, 256, (k, L), dtype=np.uint8)
@@ -203,6 +209,7 @@ def test_wiedemann_exact_fallback(qf, oracle, gpu_ctx, k, lost_n):
     dec = qf.Decoder(k, max_len=L)
     res, rep = _feed(qf, dec, k, src, lost, coef)
     assert dec.is_decoded and res[-1]
+    assert dec.solve_attempts == 9 if proj == 0 else 2 <= dec.solve_attempts <= 8
     got = np.stack([np.frombuffer(p.payload(), np.uint8) for p in dec.get_decoded_packets()])
     assert (got == src).all()
     idx, rows, rc = _oracle_rows(k, src, lost, coef, rep)
@@ -213,3 +220,34 @@ def test_wiedemann_exact_fallback(qf, oracle, gpu_ctx, k, lost_n):
     dec = qf.Decoder(k, max_len=L)
     _feed(qf, dec, k, src, lost, coef)
     assert not dec.is_decoded
+
+
+def test_wiedemann_exact_fallback_cost_pinned(qf, gpu_ctx, qf_opts):
+    """The host fallback's cost at the largest erased block a test can afford
+    to force (QF_OPT_WIEDEMANN_PROJ 0, e = k = 1,024, the crafted diagonal of
+    test_wiedemann_exact_fallback): O(e^3 / 16) pshufb steps, well under a
+    second here; with the default random projections the same input never
+    reaches it (and e = 4,096 would cost about 64x more)."""
+    import time
+
+    k = 1024
+    L = 16
+    rng = np.random.default_rng(7)
+    src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    coef = np.zeros((k, k), np.uint8)
+    for p in range(k):
+        coef[p, p] = 7 if p in (0, 1, 16, 17) else 11
+    for proj, want in ((0, 9), (1, None)):
+        qf_opts(wiedemann_proj=proj)
+        dec = qf.Decoder(k, max_len=L)
+        t0 = time.perf_counter()
+        _feed(qf, dec, k, src, set(range(k)), coef)
+        dt = time.perf_counter() - t0
+        assert dec.is_decoded
+        got = np.stack([np.frombuffer(p.payload(), np.uint8) for p in dec.get_decoded_packets()])
+        assert (got == src).all()
+        if want is None:
+            assert dec.solve_attempts <= 8
+        else:
+            assert dec.solve_attempts == want
+            assert dt < 10.0, f"exact fallback at e = {k}: {dt:.2f} s"

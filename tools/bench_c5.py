@@ -4,9 +4,13 @@ adaptive sliding-window shapes of SURVEY 8(d) -- k 32..196, r = ceil(k*ratio)-k,
 9000-byte jumbo payloads -- in block mode (independent generations) and
 sliding mode (one window per source packet: generation stride = row stride),
 encode and decode at 20 % source loss, device-resident, HIP-event kernel
-times.  Algorithmic bytes: encode (k + r) L per generation, decode (k + e) L.
+times.  Algorithmic bytes: block encode (k + r) L per generation,
+decode (k + e) L, sliding encode (1 + r) L per window -- compute-bound by
+construction, so its VALU issue fraction is reported beside the HBM one.
 
-    python tools/bench_c5.py [--bytes 2e9] [--out gpurun_out/c5_bench.json] [--mixed-only]
+    python tools/bench_c5.py [--bytes 1e9] [--mixed-bytes 4e9] [--out gpurun_out/c5_bench.json] [--mixed-only]
+
+bench.py runs the same legs (c5_bench) as the `c5` object of its line.
 
 The first leg is one heterogeneous batch of all shapes (qf_encode_batch_desc /
 qf_decode_batch_desc, k drawn per generation).
@@ -123,13 +127,149 @@ def mixed_leg(qf, ctx, nbytes: float, reps: int, seed: int = 5) -> dict:
                        "GiBps_wall": round(dec_b / (wall_d / 1e3) / 2**30, 1)}}
 
 
-def main():
+def _valu_info(kt: dict, G: int, L: int, ms: float) -> dict | None:
+    """VALU issue fraction of the generated encode kernels of a launch set:
+    bs_codegen.valu_per_item (static count of the straight-line item body) x
+    items, at 2 cycles per wave64 instruction on 1,024 SIMDs at 2.4 GHz
+    (MI355X_MICROARCH.md), against the kernels' measured time.  None when a
+    kernel of the set is not a generated one."""
+    from quicfuscate_amd import bs_codegen as bs
+    from quicfuscate_amd.build_lib import kernel_specs
+
+    specs = {sp.name: sp for sp in kernel_specs() if sp.mode == "enc"}
+    Lv = bs.padded_units(L)
+    items = -(-G * Lv // 128)
+    instr = 0
+    for name, (cnt, _) in kt.items():
+        sp = specs.get(name)
+        if sp is None:
+            return None
+        instr += cnt * bs.valu_per_item(sp) * items
+    issue_ms = instr * 2 / (1024 * 2.4e9) * 1e3
+    return {"valu_instr_per_launch_set": int(instr), "issue_ms": round(issue_ms, 4),
+            "frac": round(issue_ms / ms, 4) if ms else None,
+            "model": "static VALU count per item (bs_codegen.valu_per_item) x items, 2 cyc per wave64 instr, "
+                     "1,024 SIMDs at 2.4 GHz"}
+
+
+def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block", "sliding"),
+              exact_rows: bool = False, verify: bool = True) -> dict:
+    """One C5 (k, r) at L = 9,000: block encode ((k + r) L per generation),
+    block decode at 20 % source loss ((k + e) L), sliding encode (one window per
+    source packet, generation stride = row stride; SURVEY 8(d): (1 + r) L per
+    window, compute-bound by construction: its VALU fraction is the roof that
+    matters).  Every decode generation's recovered rows are checked against its
+    erased sources on the device, and a sample of sliding windows against the
+    block encode of the same windows."""
     import torch
 
+    res = {}
+    G = max(1, int(nbytes // (k * L_JUMBO)))
+    drs = RS if exact_rows else REP_RS
+    for mode in modes:
+        if mode == "block":
+            src = torch.randint(0, 256, (G * k * RS,), dtype=torch.uint8, device="cuda")
+            gs = k * RS
+        else:
+            src = torch.randint(0, 256, ((G + k - 1) * RS,), dtype=torch.uint8, device="cuda")
+            gs = RS
+        rep = torch.empty(G * r * drs, dtype=torch.uint8, device="cuda")
+
+        def enc():
+            qf.encode_batch(src, rep, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=drs,
+                            rep_gen_stride=r * drs, G=G, zero_tail=not exact_rows)
+
+        wall, kt = timed(ctx, enc, reps)
+        kms = sum(ms for _, ms in kt.values())
+        alg = G * ((k + r) if mode == "block" else (1 + r)) * L_JUMBO
+        ent = {"G": G, "wall_ms": round(wall, 3), "kernels": kt,
+               "algorithmic_bytes": alg, "bytes_rule": "(k + r) L per generation" if mode == "block" else
+               "(1 + r) L per window (SURVEY 8(d): one new source row read, r repairs written)",
+               "GiBps_alg": round(alg / (kms / 1e3) / 2**30, 1),
+               "hbm_frac_of_8TBps": round(alg / (kms / 1e3) / 8e12, 3),
+               "valu": _valu_info(kt, G, L_JUMBO, kms)}
+        if mode == "sliding" and verify:
+            # windows g = 0, G/2, G-1 re-encoded as a block batch
+            wins = sorted({0, G // 2, G - 1})
+            blk = torch.stack([src.view(-1, RS)[g:g + k] for g in wins]).reshape(-1)
+            rb = torch.empty(len(wins) * r * drs, dtype=torch.uint8, device="cuda")
+            qf.encode_batch(blk, rb, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=k * RS, rep_row_stride=drs,
+                            rep_gen_stride=r * drs, G=len(wins), zero_tail=not exact_rows)
+            ctx.sync()
+            got = rep.view(G, r, drs)[wins, :, :L_JUMBO]
+            ent["verified_windows"] = len(wins)
+            ent["verified"] = bool(torch.equal(got, rb.view(len(wins), r, drs)[:, :, :L_JUMBO]))
+        res[f"{mode}/encode"] = ent
+        if mode == "block":
+            # decode at 20 % source loss (first k rows: survivors then repairs)
+            e = min(r, max(1, round(0.2 * k)))
+            max_rows = k - e + r
+            rng = np.random.default_rng(k)
+            keys = rng.random((G, k))
+            er = np.sort(np.argsort(keys, axis=1)[:, :e], axis=1)
+            keep = np.ones((G, k), bool)
+            np.put_along_axis(keep, er, False, axis=1)
+            ridx = np.zeros((G, max_rows), np.uint16)
+            ridx[:, :k - e] = np.nonzero(keep)[1].reshape(G, k - e)
+            ridx[:, k - e:] = k + np.arange(r)
+            ai = torch.from_numpy(ridx.astype(np.int64)).cuda()
+            src3 = src.view(G, k, RS)
+            rep3 = rep.view(G, r, drs)[:, :, :RS]
+            rows = torch.empty((G, max_rows, RS), dtype=torch.uint8, device="cuda")
+            for g0 in range(0, G, 256):
+                g1 = min(G, g0 + 256)
+                sel = ai[g0:g1]
+                gi = torch.arange(g0, g1, device="cuda")[:, None]
+                rows[g0:g1] = torch.where((sel < k)[..., None], src3[gi, sel.clamp(max=k - 1)],
+                                          rep3[gi, (sel - k).clamp(min=0)])
+            t_idx = torch.from_numpy(ridx.view(np.int16).reshape(-1)).cuda()
+            rec = torch.empty(G * e * RS, dtype=torch.uint8, device="cuda")
+            rec_index = torch.empty(G * min(k, r), dtype=torch.int16, device="cuda")   # min(k, r) per generation
+            n_rec = torch.empty(G, dtype=torch.int32, device="cuda")
+            status = torch.empty(G, dtype=torch.int32, device="cuda")
+
+            def dec():
+                qf.decode_batch(rows.view(-1), t_idx, rec, rec_index, n_rec, status, k, r, L_JUMBO,
+                                max_rows=max_rows, row_stride=RS, rows_gen_stride=max_rows * RS,
+                                rec_row_stride=RS, rec_gen_stride=e * RS, G=G)
+
+            wall, kt = timed(ctx, dec, reps)
+            ok = bool((status == 0).all().item() and (n_rec == e).all().item())
+            if verify and ok:
+                et = torch.from_numpy(er.astype(np.int64)).cuda()
+                gi = torch.arange(G, device="cuda")[:, None].expand(-1, e)
+                ok = bool(torch.equal(rec.view(G, e, RS)[:, :, :L_JUMBO], src3[gi, et][:, :, :L_JUMBO]))
+                ok = ok and bool((rec_index.view(G, min(k, r))[:, :e].long() == et).all().item())
+            kms = sum(ms for _, ms in kt.values())
+            res["block/decode"] = {"G": G, "erased": e, "wall_ms": round(wall, 3), "kernels": kt,
+                                   "GiBps_alg": round(G * (k + e) * L_JUMBO / (kms / 1e3) / 2**30, 1),
+                                   "hbm_frac_of_8TBps": round(G * (k + e) * L_JUMBO / (kms / 1e3) / 8e12, 3),
+                                   "verified": ok}
+            del rows, rec
+        del src, rep
+        torch.cuda.empty_cache()
+    return res
+
+
+def c5_bench(qf, ctx, mixed_bytes: float = 4e9, shape_bytes: float = 1e9, reps: int = 3, shapes=None,
+             modes=("block", "sliding"), mixed: bool = True, exact_rows: bool = False) -> dict:
+    """BASELINE configs[4]: the heterogeneous batch of all
+    seven shapes (>= 4 GB of source) plus block and sliding per shape.  Used by
+    bench.py's `c5` leg and by this tool's command line."""
+    out = {"L": L_JUMBO, "row_stride": RS, "repair_row_stride": REP_RS, "loss": 0.2}
+    if mixed:
+        out["mixed_desc_batch"] = mixed_leg(qf, ctx, mixed_bytes, reps)
+    for k, r in (shapes or SHAPES):
+        out[f"k{k}_r{r}"] = shape_leg(qf, ctx, k, r, shape_bytes, reps, modes, exact_rows)
+    return out
+
+
+def main():
     from quicfuscate_amd import fec as qf
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--bytes", type=float, default=2e9, help="source bytes per shape and mode")
+    ap.add_argument("--bytes", type=float, default=1e9, help="source bytes per shape and mode")
+    ap.add_argument("--mixed-bytes", type=float, default=4e9, help="source bytes of the heterogeneous batch")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="gpurun_out/c5_bench.json")
     ap.add_argument("--exact-rows", action="store_true",
@@ -139,81 +279,15 @@ def main():
     ap.add_argument("--modes", default="block,sliding")
     a = ap.parse_args()
     ctx = qf.default_context()
-    res = {}
     shapes = SHAPES
     if a.shapes:
         shapes = [tuple(int(x) for x in s.split(",")) for s in a.shapes.split(";")]
-    else:
-        res["mixed_desc_batch"] = mixed_leg(qf, ctx, a.bytes, a.reps)
-        print("mixed", {k: v for k, v in res["mixed_desc_batch"].items() if k in ("G", "round_trip_ok")},
-              res["mixed_desc_batch"]["encode"]["GiBps_alg"], res["mixed_desc_batch"]["decode"]["GiBps_alg"],
-              flush=True)
-    for k, r in ([] if a.mixed_only else shapes):
-        G = max(1, int(a.bytes // (k * L_JUMBO)))
-        for mode in a.modes.split(","):
-            if mode == "block":
-                src = torch.randint(0, 256, (G * k * RS,), dtype=torch.uint8, device="cuda")
-                gs = k * RS
-            else:
-                src = torch.randint(0, 256, ((G + k - 1) * RS,), dtype=torch.uint8, device="cuda")
-                gs = RS
-            drs = RS if a.exact_rows else REP_RS
-            rep = torch.empty(G * r * drs, dtype=torch.uint8, device="cuda")
-
-            def enc():
-                qf.encode_batch(src, rep, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=drs,
-                                rep_gen_stride=r * drs, G=G, zero_tail=not a.exact_rows)
-
-            wall, kt = timed(ctx, enc, a.reps)
-            kms = sum(ms for _, ms in kt.values())
-            res[f"k{k}_r{r}/{mode}/encode"] = {"G": G, "wall_ms": round(wall, 3), "kernels": kt,
-                                               "GiBps_alg": round(G * (k + r) * L_JUMBO / (kms / 1e3) / 2**30, 1),
-                                               "frac_of_8TBps": round(G * (k + r) * L_JUMBO / (kms / 1e3) / 8e12, 3)}
-            if mode == "block":
-                # decode at 20 % source loss (first k rows: survivors then repairs)
-                e = min(r, max(1, round(0.2 * k)))
-                max_rows = k - e + r
-                rng = np.random.default_rng(k)
-                ridx = np.zeros((G, max_rows), np.uint16)
-                for g in range(G):
-                    E = set(rng.choice(k, e, replace=False).tolist())
-                    ridx[g] = [i for i in range(k) if i not in E] + [k + j for j in range(r)]
-                ai = torch.from_numpy(ridx.astype(np.int64)).cuda()
-                src3 = src.view(G, k, RS)
-                rep3 = rep.view(G, r, drs)[:, :, :RS]
-                rows = torch.empty((G, max_rows, RS), dtype=torch.uint8, device="cuda")
-                for g0 in range(0, G, 256):
-                    g1 = min(G, g0 + 256)
-                    sel = ai[g0:g1]
-                    gi = torch.arange(g0, g1, device="cuda")[:, None]
-                    rows[g0:g1] = torch.where((sel < k)[..., None], src3[gi, sel.clamp(max=k - 1)],
-                                              rep3[gi, (sel - k).clamp(min=0)])
-                t_idx = torch.from_numpy(ridx.view(np.int16).reshape(-1)).cuda()
-                rec = torch.empty(G * e * RS, dtype=torch.uint8, device="cuda")
-                rec_index = torch.empty(G * min(k, r), dtype=torch.int16, device="cuda")   # min(k, r) per generation
-                n_rec = torch.empty(G, dtype=torch.int32, device="cuda")
-                status = torch.empty(G, dtype=torch.int32, device="cuda")
-
-                def dec():
-                    qf.decode_batch(rows.view(-1), t_idx, rec, rec_index, n_rec, status, k, r, L_JUMBO,
-                                    max_rows=max_rows, row_stride=RS, rows_gen_stride=max_rows * RS,
-                                    rec_row_stride=RS, rec_gen_stride=e * RS, G=G)
-
-                wall, kt = timed(ctx, dec, a.reps)
-                if not ((status == 0).all().item() and (n_rec == e).all().item()):
-                    st_np, nr_np = status.cpu().numpy(), n_rec.cpu().numpy()
-                    raise AssertionError(f"k={k} r={r} G={G}: statuses {np.unique(st_np, return_counts=True)}, "
-                                         f"n_rec {np.unique(nr_np, return_counts=True)} (expected {e})")
-                g = G - 1
-                E = sorted(set(range(k)) - set(int(x) for x in ridx[g] if x < k))
-                assert torch.equal(rec.view(G, e, RS)[g, :, :L_JUMBO], src3[g, E, :L_JUMBO])
-                kms = sum(ms for _, ms in kt.values())
-                res[f"k{k}_r{r}/block/decode"] = {"G": G, "erased": e, "wall_ms": round(wall, 3), "kernels": kt,
-                                                   "GiBps_alg": round(G * (k + e) * L_JUMBO / (kms / 1e3) / 2**30, 1)}
-                del rows, rec
-            del src, rep
-            torch.cuda.empty_cache()
-        print(k, r, {kk: v["GiBps_alg"] for kk, v in res.items() if kk.startswith(f"k{k}_")}, flush=True)
+    res = c5_bench(qf, ctx, a.mixed_bytes, a.bytes, a.reps, [] if a.mixed_only else shapes,
+                   tuple(a.modes.split(",")), mixed=not a.shapes, exact_rows=a.exact_rows)
+    for key, v in res.items():
+        if key.startswith("k"):
+            print(key, {m: (e["GiBps_alg"], e.get("hbm_frac_of_8TBps"), (e.get("valu") or {}).get("frac"))
+                        for m, e in v.items()}, flush=True)
     Path(a.out).parent.mkdir(exist_ok=True)
     Path(a.out).write_text(json.dumps(res, indent=1))
 

@@ -80,6 +80,8 @@ def main() -> None:
     fetch = per_dispatch(Path(a.fetch_dir), "FETCH_SIZE")
     write = per_dispatch(Path(a.write_dir), "WRITE_SIZE")
     res = {}
+    hfile = Path(__file__).resolve().parents[1] / "quicfuscate_amd" / "lib" / "kernel_hashes.json"
+    hashes = json.loads(hfile.read_text()) if hfile.exists() else {}
     for rname in sorted(set(fetch) | set(write)):
         ours = our_name(rname)
         if ours is None:
@@ -95,6 +97,9 @@ def main() -> None:
             "write_bytes_per_launch": round(wb) if wb is not None else None,
             "hbm_bytes_per_launch": round(fb + wb) if fb is not None and wb is not None else None,
             "rocprof_name": rname[:160],
+            # the generated kernel's code object this pass measured
+            # (bench.py uses the counters only while the built kernel matches)
+            "code_sha16": hashes.get(ours),
         }
         print(ours, res[ours]["fetch_bytes_per_launch"], res[ours]["write_bytes_per_launch"])
     out = {"_note": "FETCH_SIZE(KiB)*1024*2 (gfx950 half-count correction) + WRITE_SIZE(KiB)*1024, "

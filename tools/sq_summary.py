@@ -18,6 +18,14 @@ per = defaultdict(lambda: defaultdict(list))
 for (name, disp, ctr), v in acc.items():
     per[name[:60]][ctr].append(v)
 out = {n: {c: sum(v) / len(v) for c, v in sorted(d.items())} for n, d in per.items()}
+# the code object each entry measured (generated kernels; bench.py uses the
+# counters only while the built kernel has the same hash)
+hfile = Path(__file__).resolve().parents[1] / "quicfuscate_amd" / "lib" / "kernel_hashes.json"
+hashes = json.loads(hfile.read_text()) if hfile.exists() else {}
+for n in out:
+    h = next((v for kname, v in hashes.items() if n == kname or n.startswith(kname)), None)
+    if h:
+        out[n]["code_sha16"] = h
 print(json.dumps(out, indent=1))
 if len(sys.argv) > 2:
     Path(sys.argv[2]).write_text(json.dumps(out, indent=1))

@@ -3,7 +3,9 @@
 Times k_combine_uniform (encode) for several output widths R and prefetch
 depths PD, the decode pair for several PD, and a device copy of the same
 byte count as a bandwidth reference.  Variants are selected per call with
-the QF_ENCODE_V / QF_ENCODE_PD / QF_DECODE_PD environment variables."""
+the context's kernel-path options (qf_ctx_set_option: bitsliced, encode_v,
+encode_pd, decode_pd) -- the QF_* environment variables are read only when a
+context is created, so setting them here would not reach the library."""
 import json
 import os
 import sys
@@ -46,6 +48,7 @@ def main():
     ctx = fec.Context(0, s.cuda_stream)
     lib = L._lib()
     res = {}
+    defaults = {n: ctx.option(n) for n in ("bitsliced", "encode_v", "encode_pd", "decode_pd")}
     src = torch.empty(G * k * Lb, dtype=torch.uint8, device=dev)
     L.check(lib.qf_fill_splitmix_dev(ctx.handle, src.data_ptr(), src.numel(), bench.SEED, 0))
     rep = torch.empty(G * 16 * Lb, dtype=torch.uint8, device=dev)
@@ -53,20 +56,20 @@ def main():
     ms, mn = timeit(lambda: dst.copy_(src))
     res["copy_src_GBps"] = round(2 * src.numel() / (mn / 1e3) / 1e9, 1)
     for r in (10, 16):
-        os.environ.pop("QF_DISABLE_BS", None)
+        ctx.set_option("bitsliced", defaults["bitsliced"])
         f = lambda: fec.encode_batch(src, rep, k, r, Lb, src_row_stride=Lb, src_gen_stride=k * Lb,
                                      rep_row_stride=Lb, rep_gen_stride=r * Lb, G=G, ctx=ctx)
         ms, mn = timeit(f)
         byt = G * (k + r) * Lb
         res[f"enc_r{r}_bitsliced"] = {"ms": round(mn, 4), "GBps": round(byt / (mn / 1e3) / 1e9, 1)}
         print(f"enc r={r} bitsliced: {res[f'enc_r{r}_bitsliced']}", flush=True)
-    os.environ["QF_DISABLE_BS"] = "1"
+    ctx.set_option("bitsliced", 0)
     for r in (1, 16):
         for V, PD in ((1, 1), (1, 2)):
             if r >= 9 and V == 2:
                 continue
-            os.environ["QF_ENCODE_V"] = str(V)
-            os.environ["QF_ENCODE_PD"] = str(PD)
+            ctx.set_option("encode_v", V)
+            ctx.set_option("encode_pd", PD)
             f = lambda: fec.encode_batch(src, rep, k, r, Lb, src_row_stride=Lb, src_gen_stride=k * Lb,
                                          rep_row_stride=Lb, rep_gen_stride=r * Lb, G=G, ctx=ctx)
             ms, mn = timeit(f)
@@ -74,9 +77,8 @@ def main():
             res[f"enc_r{r}_V{V}_PD{PD}"] = {"ms": round(mn, 4), "GBps": round(byt / (mn / 1e3) / 1e9, 1),
                                            "src_GiBps": round(G * k * Lb / (mn / 1e3) / 2**30, 1)}
             print(f"enc r={r} V={V} PD={PD}: {res[f'enc_r{r}_V{V}_PD{PD}']}", flush=True)
-    os.environ.pop("QF_ENCODE_V", None)
-    os.environ.pop("QF_ENCODE_PD", None)
-    os.environ.pop("QF_DISABLE_BS", None)
+    for n in ("encode_v", "encode_pd", "bitsliced"):
+        ctx.set_option(n, defaults[n])
     fec.encode_batch(src, rep, k, 16, Lb, src_row_stride=Lb, src_gen_stride=k * Lb, rep_row_stride=Lb,
                      rep_gen_stride=16 * Lb, G=G, ctx=ctx)
     del dst
@@ -98,7 +100,7 @@ def main():
     nrec = torch.empty(G, dtype=torch.int32, device=dev)
     st = torch.empty(G, dtype=torch.int32, device=dev)
     for PD in (1, 2, 3):
-        os.environ["QF_DECODE_PD"] = str(PD)
+        ctx.set_option("decode_pd", PD)
         f = lambda: fec.decode_batch(rows, ridx, rec, reci, nrec, st, k, r, Lb, max_rows=n, row_stride=Lb,
                                      rows_gen_stride=n * Lb, rec_row_stride=Lb, rec_gen_stride=16 * Lb, G=G, ctx=ctx)
         ms, mn = timeit(f)
@@ -106,6 +108,7 @@ def main():
         ok = bool((st == 0).all().item())
         res[f"dec_PD{PD}"] = {"ms": round(mn, 4), "GBps": round(byt / (mn / 1e3) / 1e9, 1), "ok": ok}
         print(f"dec PD={PD}: {res[f'dec_PD{PD}']}", flush=True)
+    ctx.set_option("decode_pd", defaults["decode_pd"])
     print(json.dumps(res))
 
 
