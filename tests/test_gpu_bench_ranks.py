@@ -50,7 +50,7 @@ def test_bench_gpus_without_launcher_spawns_ranks():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(QF_BENCH_BACKEND="gloo", MASTER_PORT="29533")
     cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--G", "1024",
-           "--c4-G", "0", "--no-cpu", "--host-path-G", "0", "--c3b-G", "0"]
+           "--c4-G", "0", "--no-cpu", "--host-path-G", "0", "--c3b-G", "0", "--c5-mixed-bytes", "0"]
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=170)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith('{"metric"')]
@@ -65,7 +65,7 @@ def test_bench_c4_full_size_leg_one_gpu():
     checked on the device, 16 seeded generations against the CPU oracle."""
     cmd = [sys.executable, str(REPO / "bench.py"), "--steps", "2", "--warmup", "1", "--G", "1024",
            "--c4-G", "156250", "--c4-steps", "2", "--rank-sample", "16", "--no-cpu", "--host-path-G", "0",
-           "--c3b-G", "0"]
+           "--c3b-G", "0", "--c5-mixed-bytes", "0"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=170)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -73,3 +73,27 @@ def test_bench_c4_full_size_leg_one_gpu():
     c4 = d["c4"]
     assert c4["generations_per_rank"] == 156250 and c4["packets_per_rank"] == 10_000_000
     assert c4["verified"] and c4["value"] > 0
+
+
+def test_bench_c5_leg_small():
+    """The line's c5 leg (BASELINE configs[4]) at reduced bytes: the
+    heterogeneous batch round-trips, every shape's block decode and sliding
+    windows verify on the device, and no byte accounting exceeds the HBM roof
+    (sliding windows priced at (1 + r) L)."""
+    cmd = [sys.executable, str(REPO / "bench.py"), "--steps", "2", "--warmup", "1", "--G", "1024", "--c4-G", "0",
+           "--no-cpu", "--host-path-G", "0", "--c3b-G", "0", "--c5-mixed-bytes", "2e8", "--c5-shape-bytes", "5e7"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, p.stderr[-2000:]
+    c5 = json.loads([l for l in p.stdout.splitlines() if l.startswith('{"metric"')][0])["c5"]
+    assert c5["mixed_desc_batch"]["round_trip_ok"]
+    shapes = [key for key in c5 if key.startswith("k")]
+    assert len(shapes) == 7
+    for key in shapes:
+        s = c5[key]
+        assert s["block/decode"]["verified"] and s["sliding/encode"]["verified"], key
+        for mode in ("block/encode", "sliding/encode", "block/decode"):
+            assert 0 < s[mode]["hbm_frac_of_8TBps"] < 1.0, (key, mode, s[mode]["hbm_frac_of_8TBps"])
+        assert s["sliding/encode"]["bytes_rule"].startswith("(1 + r) L")
+        v = s["sliding/encode"]["valu"]
+        assert v is None or 0 < v["frac"] <= 1.05, (key, v)

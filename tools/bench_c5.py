@@ -75,7 +75,7 @@ def mixed_leg(qf, ctx, nbytes: float, reps: int, seed: int = 5) -> dict:
                   rep_offset=int(rep_row0[g]) * REP_RS, rep_row_stride=REP_RS) for g in range(G)]
 
     def enc():
-        qf.encode_batch_desc(src, rep, gdesc)
+        qf.encode_batch_desc(src, rep, gdesc, ctx=ctx)
 
     wall_e, kt_e = timed(ctx, enc, reps)
     # received rows: survivors in source order, then every repair; the first
@@ -108,7 +108,7 @@ def mixed_leg(qf, ctx, nbytes: float, reps: int, seed: int = 5) -> dict:
                   rec_index_offset=int(rep_row0[g])) for g in range(G)]
 
     def dec():
-        qf.decode_batch_desc(rows.view(-1), t_idx, rec.view(-1), rec_index, n_rec, status, ddesc)
+        qf.decode_batch_desc(rows.view(-1), t_idx, rec.view(-1), rec_index, n_rec, status, ddesc, ctx=ctx)
 
     wall_d, kt_d = timed(ctx, dec, reps)
     ok = bool((status == 0).all().item() and torch.equal(n_rec.cpu(), torch.from_numpy(es.astype(np.int32))))
@@ -177,7 +177,7 @@ def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block",
 
         def enc():
             qf.encode_batch(src, rep, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=drs,
-                            rep_gen_stride=r * drs, G=G, zero_tail=not exact_rows)
+                            rep_gen_stride=r * drs, G=G, zero_tail=not exact_rows, ctx=ctx)
 
         wall, kt = timed(ctx, enc, reps)
         kms = sum(ms for _, ms in kt.values())
@@ -194,7 +194,7 @@ def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block",
             blk = torch.stack([src.view(-1, RS)[g:g + k] for g in wins]).reshape(-1)
             rb = torch.empty(len(wins) * r * drs, dtype=torch.uint8, device="cuda")
             qf.encode_batch(blk, rb, k, r, L_JUMBO, src_row_stride=RS, src_gen_stride=k * RS, rep_row_stride=drs,
-                            rep_gen_stride=r * drs, G=len(wins), zero_tail=not exact_rows)
+                            rep_gen_stride=r * drs, G=len(wins), zero_tail=not exact_rows, ctx=ctx)
             ctx.sync()
             got = rep.view(G, r, drs)[wins, :, :L_JUMBO]
             ent["verified_windows"] = len(wins)
@@ -231,7 +231,7 @@ def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block",
             def dec():
                 qf.decode_batch(rows.view(-1), t_idx, rec, rec_index, n_rec, status, k, r, L_JUMBO,
                                 max_rows=max_rows, row_stride=RS, rows_gen_stride=max_rows * RS,
-                                rec_row_stride=RS, rec_gen_stride=e * RS, G=G)
+                                rec_row_stride=RS, rec_gen_stride=e * RS, G=G, ctx=ctx)
 
             wall, kt = timed(ctx, dec, reps)
             ok = bool((status == 0).all().item() and (n_rec == e).all().item())
