@@ -1900,6 +1900,8 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
                 E(Op("ds_read_b128", (base + 4, V_LDSA, (n % S) * LDS_ROW_BYTES + 1024)))
                 E(Op("s_waitcnt_lgkm_n", (0,)))
 
+        if spec.prio != (0, 0):
+            E(Op("s_setprio", (spec.prio[0],)))
         _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
         # the accepted repairs, in byte form, onto their syndrome blocks
         for n in range(k, n_all):
@@ -1914,6 +1916,8 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
             for b in range(8):
                 E(Op("v_xor", (blk0 + b, blk0 + b, base + b)))
             E(Op("label", (f".Lrep{j}",)))
+        if spec.prio != (0, 0):
+            E(Op("s_setprio", (spec.prio[1],)))
         _lu_solve_and_store_chunked(E, spec)
         _epilogue_next_item(E, far=True)
         return ops

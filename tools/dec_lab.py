@@ -36,6 +36,23 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 4c: wave priority of the two phases (s_setprio: the row loop's
+    # loads issue first when its partner is in the LU phase, or the reverse)
+    # and the interleaved LU schedule, on the additive-FFT kernel
+    ("p_warm", dict(LIB_DEC), ()),
+    ("p_lib", dict(LIB_DEC), ()),
+    ("p_row1", {**LIB_DEC, "prio": (1, 0)}, ()),
+    ("p_lu1", {**LIB_DEC, "prio": (0, 1)}, ()),
+    ("p_row2", {**LIB_DEC, "prio": (2, 0)}, ()),
+    ("p_ilp", {**LIB_DEC, "lu_ilp": True}, ()),
+    ("p_row1_ilp", {**LIB_DEC, "prio": (1, 0), "lu_ilp": True}, ()),
+    ("p_s64", {**LIB_DEC, "bfi_transpose": "s64"}, ()),
+    ("p_s64_nolu_norows", {**LIB_DEC, "bfi_transpose": "s64", "lu": False, "lab_norows": True}, ()),
+    ("p_nolu_norows", {**LIB_DEC, "lu": False, "lab_norows": True}, ()),
+    ("p_lib_2", dict(LIB_DEC), ()),
+    ("p_row1_2", {**LIB_DEC, "prio": (1, 0)}, ()),
+]
+VARIANTS_R04B = [
     # round 4b: received rows as pool blocks of round_up(L, 128) = 1,280 B
     # (rs/rrs; every row starts on a 128-B line) with the library's Q = 38
     # lane-chunks per generation, against dense 1,200-B rows
