@@ -2121,10 +2121,19 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
         if spec.lu_ilp:   # stage by stage: no op depends on the one before it
             for d in range(8):
                 E(Op("v_andk", (sel + d, 0x07070707, blk(u, d))))
-            for d in range(8):
-                E(Op("v_lshr", (sel + 8 + d, 3, blk(u, d))))
-            for d in range(8):
-                E(Op("v_lshr", (sel + 16 + d, 6, blk(u, d))))
+            if spec.bfi_transpose == "s64":
+                # dword pairs shifted as one 64-bit value: the bits the high
+                # dword carries into the low one land in byte 3's top bits,
+                # which the masks below clear
+                for d in range(0, 8, 2):
+                    E(Op("v_lshr64", (sel + 8 + d, 3, blk(u, d))))
+                for d in range(0, 8, 2):
+                    E(Op("v_lshr64", (sel + 16 + d, 6, blk(u, d))))
+            else:
+                for d in range(8):
+                    E(Op("v_lshr", (sel + 8 + d, 3, blk(u, d))))
+                for d in range(8):
+                    E(Op("v_lshr", (sel + 16 + d, 6, blk(u, d))))
             for d in range(8):
                 E(Op("v_andk", (sel + 8 + d, 0x07070707, sel + 8 + d)))
             for d in range(8):

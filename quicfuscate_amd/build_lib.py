@@ -182,8 +182,10 @@ def kernel_specs() -> list:
     # (default cache policy: neighbouring 1,200-B rows share their boundary
     # lines, and non-temporal loads / stores drop them before the reuse;
     # tools/dec_lab.py, profiles/r03_lab_dec_policy.json: 1.485 -> 1.39 ms)
+    # (round 4: interleaved LU products and 64-bit-shift transposes /
+    # selectors: 1.409 -> 1.358-1.364 ms, profiles/r04d_lab_dec_ilp_s64.json)
     specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="",
-                            early_stores=True)
+                            early_stores=True, lu_ilp=True, bfi_transpose="s64")
               for (k, r) in BS_FFT]
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))

@@ -950,9 +950,35 @@ def test_emulated_fft_encode(oracle, k, r, pd, L, G, zero_tail, defer):
 def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs, es, lds):
     """The additive-FFT fused decode (syndromes through the chunked
     transform, LU in registers): early stores (each recovered row as soon as
-    back-substitution finishes it) and LDS-staged rows included."""
+    back-substitution finishes it) and LDS-staged rows included.  The
+    early-store cases run the library's kernel options since round 4
+    (interleaved LU products, 64-bit-shift transposes and selectors)."""
+    lib4 = {"lu_ilp": True, "bfi_transpose": "s64"} if es and not lds else {}
     assert _dec_case(oracle, k, r, 2, L, G, seed, erase, chunked=True, offs=offs, fft=8, early_stores=es,
-                     lds_rows=lds) == 0
+                     lds_rows=lds, **lib4) == 0
+
+
+def test_library_kernels_register_budget():
+    """Every generated kernel the library embeds (build_lib.kernel_specs):
+    each VGPR it names lies below its descriptor's next_free_vgpr, and every
+    register tuple starts at an even register (gfx950)."""
+    import re
+
+    from quicfuscate_amd.build_lib import kernel_specs
+
+    for spec in kernel_specs():
+        if spec.mode == "cmb":
+            continue
+        text = bs.emit_asm(spec, bs.generate(spec)).split(".amdhsa_kernel", 1)[0]
+        hi = 0
+        for m in re.finditer(r"\bv(\d+)\b|v\[(\d+):(\d+)\]", text):
+            if m.group(1):
+                hi = max(hi, int(m.group(1)))
+            else:
+                lo, top = int(m.group(2)), int(m.group(3))
+                assert lo % 2 == 0, (spec.name, m.group(0))
+                hi = max(hi, top)
+        assert hi < spec.next_free_vgpr <= 256, (spec.name, hi, spec.next_free_vgpr)
 
 
 @pytest.mark.parametrize("k,r,mode", [(64, 16, "enc"), (64, 16, "dec"), (32, 16, "dec"), (16, 16, "enc")])

@@ -51,6 +51,16 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 4d: 64-bit-shift transposes in the (HBM-bound) FFT encode
+    ("t_warm", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("t_lib", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("t_s64", 64, 16, 3, ("st:nt", "ztail", "fft:8", "s64"), ALL),
+    ("t_s64_noload", 64, 16, 3, ("noload", "st:nt", "ztail", "fft:8", "s64"), ALL),
+    ("t_noload", 64, 16, 3, ("noload", "st:nt", "ztail", "fft:8"), ALL),
+    ("t_lib_2", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("t_s64_2", 64, 16, 3, ("st:nt", "ztail", "fft:8", "s64"), ALL),
+]
+VARIANTS_R04B = [
     # round 4b: source rows as pool blocks of round_up(L, 128) bytes ("srs:1280":
     # every row starts on a 128-B line; the reference keeps each packet in its
     # own 4,096-B pool block, optimize.rs:139, 440-530) against dense 1,200-B rows
@@ -153,7 +163,8 @@ def build():
         ld = next((f[3:] for f in flags if f.startswith("ld:")), "")
         st = next((f[3:] for f in flags if f.startswith("st:")), "")
         spec = bs.KernelSpec(k, r, pd, xor3="plain" not in flags, ld_policy=ld, st_policy=st,
-                             bfi_transpose="nobfi" not in flags, xcd_remap="noremap" not in flags,
+                             bfi_transpose="s64" if "s64" in flags else "nobfi" not in flags,
+                             xcd_remap="noremap" not in flags,
                              fft=next((int(f[4:]) for f in flags if f.startswith("fft:")), 0),
                              fft_defer=next((int(f[6:]) for f in flags if f.startswith("defer:")), 0),
                              lds_rows=next((int(f[4:]) for f in flags if f.startswith("lds:")), 0))

@@ -28,7 +28,8 @@ ONLY = None   # --only name,name: build a subset
 
 CANON = ((1, 2, 4, 8, 16, 32, 64, 128), 64)
 D = {"ld_policy": "", "st_policy": ""}
-LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # the library's 'C' kernel
+LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # the library's 'C' kernel (to r04c)
+LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # ... since r04d
 # FETCH_SIZE calibration (tools/traffic_calib.py): the library kernel, and the
 # same kernel with the LU and the stores stripped, which reads a known byte
 # count through the same lane-chunk gather (64 rows + slot map + rank quad
@@ -36,6 +37,18 @@ LIB_DEC = {"chunked": True, "fft": 8, "pd": 2, "early_stores": True, **D}   # th
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 4d: lu_ilp and 64-bit-shift transposes / selectors together
+    ("q_warm", dict(LIB_DEC), ()),
+    ("q_lib", dict(LIB_DEC), ()),
+    ("q_ilp", {**LIB_DEC, "lu_ilp": True}, ()),
+    ("q_s64", {**LIB_DEC, "bfi_transpose": "s64"}, ()),
+    ("q_ilp_s64", {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}, ()),
+    ("q_ilp_s64_nolu", {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64", "lu": False}, ()),
+    ("q_lib_2", dict(LIB_DEC), ()),
+    ("q_ilp_s64_2", {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}, ()),
+    ("q_ilp_2", {**LIB_DEC, "lu_ilp": True}, ()),
+]
+VARIANTS_R04C = [
     # round 4c: wave priority of the two phases (s_setprio: the row loop's
     # loads issue first when its partner is in the LU phase, or the reverse)
     # and the interleaved LU schedule, on the additive-FFT kernel

@@ -13,3 +13,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOK
 tail -1 $OUT/smoke.log
 timeout -k 10 400 python bench.py > $OUT/bench_full.log 2>&1
 tail -1 $OUT/bench_full.log | cut -c1-400
+if [ "${WITH_LAB:-0}" = "1" ]; then
+  timeout -k 10 240 python3 tools/dec_lab.py run --reps 10 --out $OUT/dec_lab.json > $OUT/dec_lab.log 2>&1
+  echo DEC_LAB_OK
+fi
