@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -549,20 +550,24 @@ int qf_adaptive_on_send_batch(qf_adaptive* const* conns, uint32_t M, const uint6
     uint32_t pos = 0;
     std::vector<qf::EncSend> batch;
     std::vector<uint32_t> batch_m, predicted;
-    std::unordered_set<const qf_adaptive*> seen;
-    seen.reserve(M);
+    // packets of a steady connection already in this segment's batch: a
+    // connection may repeat (a burst), its windows then overlap and go to the
+    // device in the same launch (encoders_send_batch)
+    std::unordered_map<const qf_adaptive*, uint32_t> queued;
+    queued.reserve(M);
     for (uint32_t m0 = 0; m0 < M;) {
-        // a segment: each connection at most once (a repeat starts the next)
+        // a segment: normally the whole call (a connection of another
+        // context takes the per-packet path inline, as a cross-fade does)
         batch.clear();
         batch_m.clear();
         predicted.clear();
-        seen.clear();
+        queued.clear();
         qf_ctx* ctx = nullptr;
         uint32_t m = m0;
         for (; m < M; ++m) {
             qf_adaptive* a = conns[m];
-            if (!seen.insert(a).second) break;
             const bool steady = a->ctx && !a->has_fade && a->cur.enc && (!ctx || a->ctx == ctx);
+            if (!steady && queued.count(a)) break;   // its queued packets go first
             if (!steady) {  // cross-fade, GF(2^16), Zero mode, controller only: one on_send
                 uint32_t n = 0;
                 int s = qf_adaptive_on_send(a, ids[m], data[m], lens[m], out_data + (size_t)pos * out_stride,
@@ -576,7 +581,8 @@ int qf_adaptive_on_send_batch(qf_adaptive* const* conns, uint32_t M, const uint6
             }
             ctx = a->ctx;
             const Codec& c = a->cur;
-            const uint32_t cnt = (uint32_t)qf_encoder_window_len(c.enc);
+            uint32_t& q = queued[a];
+            const uint32_t cnt = std::min<uint32_t>((uint32_t)qf_encoder_window_len(c.enc) + q++, c.k);
             const uint32_t n_rep = (cnt + 1 >= c.k && c.n > c.k) ? c.n - c.k : 0;
             put_systematic(ids[m], data[m], lens[m], out_data + (size_t)pos * out_stride, out_desc + pos);
             qf::EncSend x{};

@@ -12,6 +12,7 @@
 #include <condition_variable>
 #include <functional>
 #include <thread>
+#include <unordered_map>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -738,37 +739,100 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     int s = ctx_lock(ctx, lk);
     if (s) return s;
     hipStream_t st = ctx_stream(ctx);
-    // the adds (decoder.rs:164-169) on the host side, and the windows they fill
+    // the adds (decoder.rs:164-169) on the host side, and the windows they fill.
+    // An encoder that takes several packets in this call (one connection's
+    // burst) has its windows overlap: window j of the burst is the k rows
+    // ending at its packet j.  Its rows go to a linear staging area instead
+    // of the ring -- the newest k-1 rows the ring held before the call, then
+    // the burst's packets -- and window j reads rows j' .. j' + k - 1 there
+    // unrotated: one launch for the whole burst, as the sliding-window
+    // encode.  The ring then keeps only the burst's last k packets.
     struct Win {
         uint32_t m, rot, L;
+        uint64_t src_off;   // relative to the staging buffer d; ~0: the encoder's ring
     };
-    std::vector<RingSlot> slots(M);
+    struct Burst {
+        uint32_t B = 0, seen = 0, nold = 0, head0 = 0;
+        size_t ext_off = 0;   // relative to d
+    };
+    std::unordered_map<const qf_encoder*, Burst> bursts;
+    for (uint32_t m = 0; m < M; ++m) bursts[v[m].e].B++;
+    size_t ext_bytes = 0;
+    uint32_t n_old = 0;
+    for (auto& kv : bursts) {
+        Burst& b = kv.second;
+        if (b.B < 2) continue;
+        const qf_encoder* e = kv.first;
+        b.head0 = e->head;
+        b.nold = std::min(e->count, e->k - 1);
+        b.ext_off = ext_bytes;   // relative to the staging area for now
+        ext_bytes += (size_t)(b.nold + b.B) * e->stride;
+        n_old += b.nold;
+    }
+    std::vector<RingSlot> slots;   // packet copies (second launch)
+    std::vector<uint32_t> slot_m;  // their packets
+    std::vector<size_t> slot_ext;  // ~0: dst is a ring slot; else the staging row's offset in the burst area
+    std::vector<RingSlot> olds;    // ring -> staging copies of the bursts' old rows (first launch)
+    slots.reserve(M);
+    slot_m.reserve(M);
+    slot_ext.reserve(M);
+    olds.reserve(n_old);
+    std::vector<size_t> pk_src(M);
     std::vector<Win> wins;
     size_t pk = 0;
+    const uint64_t kRingSrc = ~0ull;
     for (uint32_t m = 0; m < M; ++m) {
         qf_encoder* e = v[m].e;
+        Burst& bu = bursts[e];
         const uint32_t slot = e->head;
-        slots[m].src_off = pk;  // relative to the packet area for now
-        slots[m].dst = e->d_ring + (size_t)slot * e->stride;
-        slots[m].dst2 = e->ring_rot ? nullptr : e->d_ring + (size_t)(slot + e->k) * e->stride;
-        slots[m].len = v[m].len;
-        slots[m].stride = e->stride;
+        pk_src[m] = pk;   // relative to the packet area for now
         pk += round16(v[m].len);
         e->lens[slot] = v[m].len;
         e->ids[slot] = v[m].id;
         e->head = (e->head + 1) % e->k;
         if (e->count < e->k) e->count++;
         v[m].n_rep = 0;
-        if (e->count == e->k && e->n > e->k) wins.push_back({m, e->head, e->lens[e->head]});
+        const uint32_t j = bu.seen++;
+        // the ring copy: every packet of a single add, the last k of a burst
+        if (bu.B < 2 || j + e->k >= bu.B) {
+            RingSlot rs{};
+            rs.dst = e->d_ring + (size_t)slot * e->stride;
+            rs.dst2 = e->ring_rot ? nullptr : e->d_ring + (size_t)(slot + e->k) * e->stride;
+            rs.len = v[m].len;
+            rs.stride = e->stride;
+            slots.push_back(rs);
+            slot_m.push_back(m);
+            slot_ext.push_back(~(size_t)0);
+        }
+        if (bu.B >= 2) {   // and its row of the burst's staging area
+            RingSlot rs{};
+            rs.len = v[m].len;
+            rs.stride = e->stride;
+            slots.push_back(rs);
+            slot_m.push_back(m);
+            slot_ext.push_back(bu.ext_off + (size_t)(bu.nold + j) * e->stride);
+        }
+        if (e->count == e->k && e->n > e->k) {
+            uint64_t so = kRingSrc;
+            uint32_t rot = e->head;
+            if (bu.B >= 2) {   // rows nold + j + 1 - k .. nold + j of the burst's staging area
+                so = bu.ext_off + (size_t)(bu.nold + j + 1 - e->k) * e->stride;
+                rot = 0;
+            }
+            wins.push_back({m, rot, e->lens[e->head], so});
+        }
     }
     // windows grouped by (k, r) class, repairs packed L-rounded per window
     std::sort(wins.begin(), wins.end(), [&](const Win& a, const Win& b) {
         const qf_encoder *x = v[a.m].e, *y = v[b.m].e;
         return x->k != y->k ? x->k < y->k : x->n != y->n ? x->n < y->n : a.m < b.m;
     });
-    const size_t slots_off = 0, wins_off = round16((uint32_t)(sizeof(RingSlot) * M));
+    const uint32_t n_slots = (uint32_t)slots.size(), n_olds = n_old;
+    const size_t slots_off = 0, olds_off = round16((uint32_t)(sizeof(RingSlot) * n_slots));
+    const size_t wins_off = olds_off + round16((uint32_t)(sizeof(RingSlot) * n_olds));
     const size_t pk_off = wins_off + round16((uint32_t)(sizeof(RingWin) * wins.size()));
-    const size_t rep_off0 = (pk_off + pk + 255) & ~(size_t)255;
+    const size_t ext_off0 = (pk_off + pk + 255) & ~(size_t)255;
+    const size_t rep_off0 = (ext_off0 + ext_bytes + 255) & ~(size_t)255;
     std::vector<size_t> rep_off(wins.size());
     size_t rep_bytes = 0;
     for (size_t w = 0; w < wins.size(); ++w) {
@@ -780,18 +844,37 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     if ((s = ctx_desc_buffers(ctx, rep_off0 + rep_bytes, &h, &d)) != QF_OK) return s;
     const double tpb = prof ? wall() : 0.0;
     for (uint32_t m = 0; m < M; ++m) {
-        uint8_t* dst = h + pk_off + slots[m].src_off;
+        uint8_t* dst = h + pk_off + pk_src[m];
         const uint32_t n = v[m].len, n16 = round16(n);
         if (n) memcpy(dst, v[m].data, n);
         if (n16 > n) memset(dst + n, 0, n16 - n);
-        slots[m].src_off += pk_off;
     }
-    memcpy(h + slots_off, slots.data(), sizeof(RingSlot) * M);
+    for (uint32_t i = 0; i < n_slots; ++i) {
+        slots[i].src_off = pk_off + pk_src[slot_m[i]];
+        if (slot_ext[i] != ~(size_t)0) slots[i].dst = d + ext_off0 + slot_ext[i];
+    }
+    for (auto& kv : bursts) {   // old rows, oldest first: ring slots head0 - nold .. head0 - 1
+        const Burst& b = kv.second;
+        if (b.B < 2) continue;
+        const qf_encoder* e = kv.first;
+        for (uint32_t t = 0; t < b.nold; ++t) {
+            const uint32_t slot = (b.head0 + e->k - b.nold + t) % e->k;
+            RingSlot rs{};
+            rs.src_off = (uint64_t)(uintptr_t)(e->d_ring + (size_t)slot * e->stride) - (uint64_t)(uintptr_t)d;   // wraps below d
+            rs.dst = d + ext_off0 + b.ext_off + (size_t)t * e->stride;
+            rs.len = e->stride;
+            rs.stride = e->stride;
+            olds.push_back(rs);
+        }
+    }
+    memcpy(h + slots_off, slots.data(), sizeof(RingSlot) * n_slots);
+    if (n_olds) memcpy(h + olds_off, olds.data(), sizeof(RingSlot) * n_olds);
     const double tpc = prof ? wall() : 0.0;
     RingWin* hw = reinterpret_cast<RingWin*>(h + wins_off);
     for (size_t w = 0; w < wins.size(); ++w) {
         const qf_encoder* e = v[wins[w].m].e;
-        hw[w].src_off = (uint64_t)(uintptr_t)e->d_ring - (uint64_t)(uintptr_t)d;  // wraps when the ring is below d
+        hw[w].src_off = wins[w].src_off == kRingSrc ? (uint64_t)(uintptr_t)e->d_ring - (uint64_t)(uintptr_t)d   // wraps when the ring is below d
+                                                    : ext_off0 + wins[w].src_off;
         hw[w].rep_off = rep_off[w];
         hw[w].rot = wins[w].rot;
         hw[w].L = wins[w].L;
@@ -800,7 +883,9 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
     }
     if ((s = ctx_desc_upload(ctx, pk_off + pk)) != QF_OK) return s;
     const double tp1 = prof ? wall() : 0.0;
-    QF_CHECK_HIP(launch_ring_scatter(d, reinterpret_cast<const RingSlot*>(d + slots_off), M, st));
+    // the bursts' old rows leave the rings before their packets overwrite them
+    if (n_olds) QF_CHECK_HIP(launch_ring_scatter(d, reinterpret_cast<const RingSlot*>(d + olds_off), n_olds, st));
+    QF_CHECK_HIP(launch_ring_scatter(d, reinterpret_cast<const RingSlot*>(d + slots_off), n_slots, st));
     for (size_t w0 = 0; w0 < wins.size();) {
         const qf_encoder* e = v[wins[w0].m].e;
         size_t w1 = w0;
@@ -818,7 +903,7 @@ int encoders_send_batch(qf_ctx* ctx, EncSend* v, uint32_t M) {
         EncSend& x = v[wins[w].m];
         const qf_encoder* e = x.e;
         const uint32_t r = e->n - e->k, L = wins[w].L, Lr = round16(L);
-        const uint64_t newest = e->ids[(e->head + e->k - 1) % e->k];
+        const uint64_t newest = x.id;   // the window's newest packet is the one that filled it
         for (uint32_t q = 0; q < r; ++q) {
             if (L) memcpy(x.rep_data + (size_t)q * x.rep_stride, h + rep_off[w] + (size_t)q * Lr, L);
             if (x.rep_coeffs) memcpy(x.rep_coeffs + (size_t)q * x.coeff_stride, e->win.data() + (size_t)q * e->k, e->k);

@@ -211,3 +211,60 @@ def test_send_batch_after_per_packet_sends(qf, oracle, gpu_ctx):
         reps = [p for p in got if not p.is_systematic]
         if reps:
             _check_oracle(oracle, k, r, hist, reps)
+
+
+@pytest.mark.parametrize("encode_small", [1, 0])
+def test_send_batch_bursts(qf, oracle, gpu_ctx, encode_small):
+    """One connection's burst in one call (the connection repeated B times,
+    B = 1 .. 200, from an empty window and across k): its windows overlap and
+    go to the device in one launch from a staging area holding the ring's
+    newest k - 1 rows and the burst.  Everything equals the per-packet twin,
+    every repair the oracle's encode of its window, and the ring left behind
+    serves the next call (per-packet and batched).  encode_small = 0: the
+    double ring of the bit-sliced per-packet path."""
+    ctx = qf.Context(0)
+    ctx.set_option("encode_small", encode_small)
+    M = qf.FecMode
+    cfgs = {"normal": _cfg(qf, M.Normal, normal_window=20, max_len=700), "light": _cfg(qf, M.Light, max_len=700)}
+    conns = {n: qf.AdaptiveFec(c, now=0.0, ctx=ctx) for n, c in cfgs.items()}
+    twins = {n: qf.AdaptiveFec(c, now=0.0, ctx=ctx) for n, c in cfgs.items()}
+    single, single_twin = qf.AdaptiveFec(cfgs["normal"], now=0.0, ctx=ctx), qf.AdaptiveFec(cfgs["normal"], now=0.0, ctx=ctx)
+    rng = np.random.default_rng(29)
+    hist = {n: [] for n in conns}
+    hist["single"] = []
+    nid = {"normal": 0, "light": 10 ** 6, "single": 2 * 10 ** 6}
+    n_checked = 0
+    for B in (1, 5, 3, 16, 17, 40, 1, 200, 2, 64):
+        order = ["normal"] * B + ["light"] * (B // 2 + 1) + ["single"]
+        order = [order[i] for i in rng.permutation(len(order))]
+        fecs, pkts = [], []
+        for n in order:
+            ln = int(rng.integers(0, 701)) if rng.random() < 0.3 else 700
+            b = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            fecs.append(single if n == "single" else conns[n])
+            pkts.append((n, qf.Packet(nid[n], bytearray(b), ln, True)))
+            nid[n] += 1
+        if B == 2:   # a per-packet send between bursts reads the ring the burst left
+            for n in ("normal", "light"):
+                b = rng.integers(0, 256, 700, dtype=np.uint8).tobytes()
+                got, want = [], []
+                conns[n].on_send(qf.Packet(nid[n], bytearray(b), 700, True), got)
+                twins[n].on_send(qf.Packet(nid[n], bytearray(b), 700, True), want)
+                nid[n] += 1
+                hist[n].append(b)
+                assert len(got) == len(want) and all(_same(a, c) for a, c in zip(got, want))
+        queues, st = qf.on_send_batch(fecs, [p for _, p in pkts])
+        assert st == [L.QF_OK] * len(fecs)
+        for m, (n, p) in enumerate(pkts):
+            want = []
+            tw = single_twin if n == "single" else twins[n]
+            tw.on_send(qf.Packet(p.id, bytearray(p.payload()), p.len, True), want)
+            assert len(queues[m]) == len(want), (B, n, m)
+            assert all(_same(a, c) for a, c in zip(queues[m], want)), (B, n, m)
+            hist[n].append(p.payload())
+            f = single if n == "single" else conns[n]
+            k, nn = f.state()["k"], f.state()["n"]
+            if len(queues[m]) > 1 and (m % 5 == 0 or B < 20):
+                _check_oracle(oracle, k, nn - k, hist[n], queues[m][1:])
+                n_checked += 1
+    assert n_checked > 40
