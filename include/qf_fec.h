@@ -135,6 +135,11 @@ enum {
                                     from a per-process secret (a packet sender cannot craft a matrix
                                     that defeats them and forces the exact host fallback); 0 = the
                                     reference's init vectors b = 0..7 only [QF_WIEDEMANN_PROJ; default 1] */
+    QF_OPT_GF16_FFT_BS,          /* the GF(2^16) additive FFT for k <= 2048 bit-sliced (field elements
+                                    in 16 bit planes, no table lookups): 1 where a batch has items for
+                                    a quarter of the CUs, 2 always, 3 always with two layers per LDS
+                                    pass; 0 the log / Zech-table kernel for every k
+                                    [QF_GF16_FFT_BS; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

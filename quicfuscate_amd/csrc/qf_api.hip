@@ -173,6 +173,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* GF16_BITSLICED */ {"QF_GF16_BITSLICED", 1, 0, 1, false},
     /* GF16_FFT */ {"QF_GF16_FFT", 1, 0, 2, false},
     /* WIEDEMANN_PROJ */ {"QF_WIEDEMANN_PROJ", 1, 0, 1, false},
+    /* GF16_FFT_BS */ {"QF_GF16_FFT_BS", 1, 0, 3, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }

@@ -62,9 +62,11 @@ struct Fft16Table {
 
 struct Fft16ConstArgs {
     Fft16Table t;
-    uint16_t* out;        // [k - 1 inverse][k fold][R - 1 forward], logs
+    uint16_t* out;        // [k - 1 inverse][k fold][R - 1 forward], logs (normal: field elements)
     const uint16_t* glog;
+    const uint16_t* gexp;
     uint32_t k, a, R, b;
+    uint32_t normal;      // 1: the elements themselves (k_fft16_bs), 0: their logs (k_fft16)
 };
 
 struct Fft16Args {
@@ -99,6 +101,7 @@ struct Fft16Args {
     uint64_t em;
     const uint32_t* solve_fb;
     uint32_t solve;
+    uint32_t r4;             // k_fft16_bs: two layers per LDS pass (QF_OPT_GF16_FFT_BS 3), else one
 };
 
 __device__ __forceinline__ uint32_t wq_at(const Fft16Table& t, uint32_t q, uint32_t x) {
@@ -145,7 +148,7 @@ __global__ void __launch_bounds__(256) k_fft16_consts(Fft16ConstArgs a) {
             const uint32_t blk = f - (a.R - (a.R >> q));
             v = lg_xhat(a, q, a.k ^ (blk << (q + 1)));
         }
-        a.out[e] = (uint16_t)v;
+        a.out[e] = (uint16_t)(a.normal ? (v == kNoLog16 ? 0u : (uint32_t)a.gexp[v]) : v);
     }
 }
 
@@ -471,6 +474,395 @@ __global__ void __launch_bounds__(kFftThreads) k_fft16(Fft16Args A, uint32_t G) 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Bit-sliced transform (k_fft16_bs, k <= 2,048): the same schedule on field
+// elements in normal form, 32 symbol columns per lane as 16 bit planes (plane
+// p = bit p of the 32 symbols), so a butterfly is plane XORs and one
+// multiplication by its constant -- no table lookups and no dependent LDS
+// round trips.  s x by Horner over the bits of s, x alpha = the planes
+// shifted up with plane 15 folded into planes 0, 1, 3 and 12 (0x1100B):
+// 16 x 16 masked XORs (v_bitop3) plus 45 for the shifts, ~10 VALU per symbol
+// and butterfly; where the wave's butterflies share their block's constant
+// (layer q >= 6 and each transform's top layer) a scalar branch per bit of s
+// leaves only the set bits' XORs.  The strip lives in LDS plane-major ([16][k cg] dwords, cg
+// column groups of 32 symbols), one butterfly per thread per layer.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBsThreads = 512;          // k <= 1,024: k / 2 x cg butterflies per layer
+constexpr uint32_t kBsRows = 1024;            // strip rows (k cg) of the 512-thread kernel
+constexpr uint32_t kBsConsts = 3072;          // its butterfly constants (2 k + R - 2 <= 3 k)
+constexpr uint32_t kBsMaxK = 2048;            // k = 2,048: 1,024 threads, 128 KiB strip
+
+__device__ __forceinline__ void bs_mulx(uint32_t (&x)[16]) {
+    const uint32_t t = x[15];
+#pragma unroll
+    for (int p = 15; p > 0; --p) x[p] = x[p - 1];
+    x[0] = t;
+    x[1] ^= t;
+    x[3] ^= t;
+    x[12] ^= t;
+}
+
+// y ^= s x: Horner over the bits of s (s per lane), acc = acc alpha ^ (x & m_j)
+// with m_j = bit j of s spread over the dword, one v_bitop3 per plane
+__device__ __forceinline__ void bs_muladd(uint32_t (&y)[16], const uint32_t (&x)[16], uint32_t s) {
+    uint32_t acc[16];
+    {
+        const uint32_t m = 0u - (s >> 15);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) acc[p] = x[p] & m;
+    }
+#pragma unroll
+    for (int j = 14; j >= 0; --j) {
+        bs_mulx(acc);
+        const uint32_t m = 0u - ((s >> j) & 1u);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) acc[p] = __builtin_amdgcn_bitop3_b32(acc[p], x[p], m, 0x78);   // acc ^ (x & m)
+    }
+#pragma unroll
+    for (int p = 0; p < 16; ++p) y[p] ^= acc[p];
+}
+
+// y ^= s x with s uniform over the wave: a scalar branch per bit of s, so only
+// the set bits' 16 XORs issue (45 + 16 popcount(s) VALU against 317)
+__device__ __forceinline__ void bs_muladd_uni(uint32_t (&y)[16], const uint32_t (&x)[16], uint32_t s) {
+    s = __builtin_amdgcn_readfirstlane(s);
+    uint32_t acc[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) acc[p] = 0;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+        bs_mulx(acc);
+        if (__builtin_expect((s >> j) & 1u, 0)) {
+#pragma unroll
+            for (int p = 0; p < 16; ++p) acc[p] ^= x[p];
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 16; ++p) y[p] ^= acc[p];
+}
+
+// uni: every active lane of the wave multiplies by the same s (one block)
+__device__ __forceinline__ void bs_muladd(uint32_t (&y)[16], const uint32_t (&x)[16], uint32_t s, bool uni) {
+    if (uni)
+        bs_muladd_uni(y, x, s);
+    else
+        bs_muladd(y, x, s);
+}
+
+// 16 dwords of one row's 32 big-endian symbols <-> 16 planes.  Dword d holds
+// symbols 2d (low half) and 2d + 1 (high half) after a byte swap; a 16 x 16
+// bit transpose of both halves at once gives plane p: bit i = symbol 2i,
+// bit 16 + i = symbol 2i + 1.  The transpose is its own inverse.
+template <int W, uint32_t M>
+__device__ __forceinline__ void bs_transpose_stage(uint32_t (&d)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i & W) continue;
+        const uint32_t t = ((d[i] >> W) ^ d[i + W]) & M;
+        d[i + W] ^= t;
+        d[i] ^= t << W;
+    }
+}
+
+__device__ __forceinline__ void bs_transpose(uint32_t (&d)[16]) {
+    bs_transpose_stage<8, 0x00FF00FFu>(d);
+    bs_transpose_stage<4, 0x0F0F0F0Fu>(d);
+    bs_transpose_stage<2, 0x33333333u>(d);
+    bs_transpose_stage<1, 0x55555555u>(d);
+}
+
+__device__ __forceinline__ uint32_t bs_swap16x2(uint32_t w) { return __builtin_amdgcn_perm(w, w, 0x02030001u); }
+
+// 2 n bytes (n <= 32 symbols) of a row -> planes; dword loads (rows are 4-byte aligned)
+__device__ __forceinline__ void bs_load_row(const uint8_t* row, uint32_t n, uint32_t (&d)[16]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        uint32_t v = 0;
+        if (2u * q + 1 < n)
+            v = *reinterpret_cast<const uint32_t*>(row + 4 * q);
+        else if (2u * q < n)
+            v = (uint32_t)row[4 * q] | ((uint32_t)row[4 * q + 1] << 8);
+        d[q] = bs_swap16x2(v);
+    }
+    bs_transpose(d);
+}
+
+// planes -> 2 n bytes of a row (xr: XOR the received row's bytes in, decode syndromes)
+__device__ __forceinline__ void bs_store_row(uint8_t* row, uint32_t n, uint32_t (&d)[16], const uint8_t* xr) {
+    bs_transpose(d);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        uint32_t v = bs_swap16x2(d[q]);
+        if (2u * q + 1 < n) {
+            if (xr) v ^= *reinterpret_cast<const uint32_t*>(xr + 4 * q);
+            *reinterpret_cast<uint32_t*>(row + 4 * q) = v;
+        } else if (2u * q < n) {
+            if (xr) v ^= (uint32_t)xr[4 * q] | ((uint32_t)xr[4 * q + 1] << 8);
+            row[4 * q] = (uint8_t)v;
+            row[4 * q + 1] = (uint8_t)(v >> 8);
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void bs_lds_load(const uint32_t* pl, uint32_t row, uint32_t (&y)[16]) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) y[p] = pl[p * N + row];
+}
+
+template <int N>
+__device__ __forceinline__ void bs_lds_store(uint32_t* pl, uint32_t row, const uint32_t (&y)[16]) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) pl[p * N + row] = y[p];
+}
+
+// MODE 0 encode, 1 decode syndromes, 2 decode solve (as k_fft16).  BIG: k =
+// 2,048 (1,024 threads, one column group); else k <= 1,024, 512 threads,
+// cg = A.S column groups (k cg <= 1,024).  A.cst: the constants as elements.
+template <int MODE, bool BIG>
+__global__ void __launch_bounds__(BIG ? 1024 : kBsThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) k_fft16_bs(Fft16Args A, uint32_t G) {
+    constexpr int NT = BIG ? 1024 : (int)kBsThreads;
+    constexpr int N = BIG ? (int)kBsMaxK : (int)kBsRows;   // plane stride (rows)
+    constexpr int NC = BIG ? 2 * (int)kBsMaxK + (int)kBsMaxK : (int)kBsConsts;
+    __shared__ uint32_t pl[16 * N];
+    __shared__ uint16_t scst[NC];
+    const uint32_t k = A.k, cg = A.S, tid = threadIdx.x;
+    const uint32_t lgk = A.a, hk = k >> 1;
+    const uint32_t n_cst = 2 * k + A.R - 2;
+    for (uint32_t e = tid; e < n_cst; e += NT) scst[e] = A.cst[e];
+    const uint16_t* cinv = scst;
+    const uint16_t* cfk = scst + (k - 1);
+    const uint16_t* cfwd = cfk + k;
+    const uint32_t rows = k * cg;   // strip rows: column group c, row i at c k + i
+    // this thread's butterfly slot: column group bc, pair index bp
+    const uint32_t bc = tid >> (lgk - 1), bp = tid & (hk - 1);
+    const bool bact = bc < cg;
+    // radix-4 slot: column group qc, quad index qu (k / 4 per group)
+    const uint32_t qc = tid >> (lgk - 2), qu = tid & ((k >> 2) - 1);
+    const bool qact = qc < cg;
+    const uint64_t items = (uint64_t)G * A.strips;
+    for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint64_t g = it / A.strips;
+        const uint32_t col0 = (uint32_t)(it - g * A.strips) * 32u * cg;   // first symbol column
+        __syncthreads();   // constants (first item) / the previous item's output reads
+        if (MODE == 1 && A.skip[g]) continue;   // uniform over the block
+        const uint8_t* gsrc = A.src + g * A.sgs;
+        uint32_t e_g = 0;
+        const uint16_t *gJ = nullptr, *gE = nullptr;
+        const uint32_t* lp = nullptr;
+        if (MODE == 2) {
+            if (A.status[g] != 0 || A.solve_fb[g] != 0) continue;
+            e_g = A.st_e[g * A.st_stride];
+            if (e_g == 0) continue;
+            gJ = A.J + g * A.em;
+            gE = A.E + g * A.em;
+            lp = A.lprod + g * 4 * A.em;
+            for (uint32_t w = tid; w < 16 * (uint32_t)N; w += NT) pl[w] = 0;
+            __syncthreads();
+            // source position J_a - k gets D_a s_a, D_a = Qx_a / Px_a
+            for (uint32_t q = tid; q < e_g * cg; q += NT) {
+                const uint32_t a = q / cg, c = q - a * cg;
+                const uint32_t cc = col0 + 32u * c;
+                if (cc >= A.nsym) continue;
+                uint32_t y[16], z[16];
+                bs_load_row(gsrc + (uint64_t)a * A.srs + 2ull * cc, min(32u, A.nsym - cc), y);
+                uint32_t da = lp[a] + kOrd16 - lp[A.em + a];
+                da = da >= kOrd16 ? da - kOrd16 : da;
+#pragma unroll
+                for (int p = 0; p < 16; ++p) z[p] = 0;
+                bs_muladd(z, y, A.gexp[da]);
+                bs_lds_store<N>(pl, c * k + ((uint32_t)gJ[a] - k), z);
+            }
+        } else {
+            // strip in: window position i reads ring slot (rot + i) mod k
+            // (decode: slot smap[i], none = zero)
+            const uint16_t* smap = MODE == 1 ? A.smap + g * k : nullptr;
+            for (uint32_t q = tid; q < rows; q += NT) {
+                const uint32_t c = q >> lgk, i = q & (k - 1);
+                const uint32_t cc = col0 + 32u * c;
+                uint32_t y[16];
+                const uint32_t slot = MODE == 1 ? smap[i] : ((A.rot + i) & (k - 1));
+                if (cc >= A.nsym || (MODE == 1 && slot == 0xFFFFu)) {
+#pragma unroll
+                    for (int p = 0; p < 16; ++p) y[p] = 0;
+                } else {
+                    bs_load_row(gsrc + (uint64_t)slot * A.srs + 2ull * cc, min(32u, A.nsym - cc), y);
+                }
+                bs_lds_store<N>(pl, q, y);
+            }
+        }
+        __syncthreads();
+        // inverse transform over V: y_j += y_i; y_i += s y_j, layer q's
+        // pairs (i, i + 2^q) in blocks of 2^(q+1), constant per block.  r4:
+        // layers q and q + 1 in one LDS pass, a thread's four rows i0 + {0, h,
+        // 2h, 3h} (h = 2^q) in registers
+        uint32_t q = 0;
+        for (; !BIG && A.r4 && q + 1 < lgk; q += 2) {   // (k = 2,048: the 128-VGPR budget of 1,024 threads)
+            if (qact) {
+                const uint32_t h = 1u << q, B = qu >> q;
+                const uint32_t i0 = qc * k + (B << (q + 2)) + (qu & (h - 1));
+                const uint16_t* c0 = cinv + (k - (k >> q));
+                const uint16_t* c1 = cinv + (k - (k >> (q + 1)));
+                uint32_t y0[16], y1[16], y2[16], y3[16];
+                bs_lds_load<N>(pl, i0, y0);
+                bs_lds_load<N>(pl, i0 + h, y1);
+                bs_lds_load<N>(pl, i0 + 2 * h, y2);
+                bs_lds_load<N>(pl, i0 + 3 * h, y3);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) {
+                    y1[p] ^= y0[p];
+                    y3[p] ^= y2[p];
+                }
+                const bool uni = q >= 6 || q + 2 == lgk;   // a wave's quads in one block
+                bs_muladd(y0, y1, c0[2 * B], uni);
+                bs_muladd(y2, y3, c0[2 * B + 1], uni);
+                const uint32_t s1 = c1[B];
+                // (rows stored as soon as they are final: the register budget)
+#pragma unroll
+                for (int p = 0; p < 16; ++p) y2[p] ^= y0[p];
+                bs_muladd(y0, y2, s1, uni);
+                bs_lds_store<N>(pl, i0, y0);
+                bs_lds_store<N>(pl, i0 + 2 * h, y2);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) y3[p] ^= y1[p];
+                bs_muladd(y1, y3, s1, uni);
+                bs_lds_store<N>(pl, i0 + h, y1);
+                bs_lds_store<N>(pl, i0 + 3 * h, y3);
+            }
+            __syncthreads();
+        }
+        for (; q < lgk; ++q) {
+            if (bact) {
+                const uint32_t h = 1u << q, blk = bp >> q;
+                const uint32_t i = bc * k + ((blk << (q + 1)) | (bp & (h - 1)));
+                uint32_t yi[16], yj[16];
+                bs_lds_load<N>(pl, i, yi);
+                bs_lds_load<N>(pl, i + h, yj);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) yj[p] ^= yi[p];
+                bs_muladd(yi, yj, cinv[(k - (k >> q)) + blk], q >= 6 || q + 1 == lgk);
+                bs_lds_store<N>(pl, i, yi);
+                bs_lds_store<N>(pl, i + h, yj);
+            }
+            __syncthreads();
+        }
+        // fold onto the R-point coset, times kappa: every row times its
+        // factor, then row t < R = the sum of rows t mod R
+        for (uint32_t q = tid; q < rows; q += NT) {
+            const uint32_t i = q & (k - 1);
+            uint32_t y[16], z[16];
+            bs_lds_load<N>(pl, q, y);
+#pragma unroll
+            for (int p = 0; p < 16; ++p) z[p] = 0;
+            bs_muladd(z, y, cfk[i]);
+            bs_lds_store<N>(pl, q, z);
+        }
+        __syncthreads();
+        if (A.R < k) {
+            for (uint32_t q = tid; q < A.R * cg; q += NT) {
+                const uint32_t c = q / A.R, t = q - c * A.R;
+                uint32_t y[16], z[16];
+                bs_lds_load<N>(pl, c * k + t, y);
+                for (uint32_t i = t + A.R; i < k; i += A.R) {
+                    bs_lds_load<N>(pl, c * k + i, z);
+#pragma unroll
+                    for (int p = 0; p < 16; ++p) y[p] ^= z[p];
+                }
+                bs_lds_store<N>(pl, c * k + t, y);
+            }
+            __syncthreads();
+        }
+        // forward transform over k + V_b: d_i += s d_j; d_j += d_i, layers
+        // b-1 .. 0 (r4: layers ql + 1 and ql in one pass)
+        int qq = (int)A.b - 1;
+        for (; !BIG && A.r4 && qq >= 1; qq -= 2) {
+            const uint32_t ql = (uint32_t)qq - 1, h = 1u << ql;
+            if (qact && qu < (A.R >> 2)) {
+                const uint32_t B = qu >> ql;
+                const uint32_t i0 = qc * k + (B << (ql + 2)) + (qu & (h - 1));
+                const uint16_t* c0 = cfwd + (A.R - (A.R >> ql));
+                const uint16_t* c1 = cfwd + (A.R - (A.R >> (ql + 1)));
+                uint32_t d0[16], d1[16], d2[16], d3[16];
+                bs_lds_load<N>(pl, i0, d0);
+                bs_lds_load<N>(pl, i0 + h, d1);
+                bs_lds_load<N>(pl, i0 + 2 * h, d2);
+                bs_lds_load<N>(pl, i0 + 3 * h, d3);
+                const uint32_t s1 = c1[B];
+                const bool uni = ql >= 6 || ql + 2 == A.b;
+                bs_muladd(d0, d2, s1, uni);
+                bs_muladd(d1, d3, s1, uni);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) {
+                    d2[p] ^= d0[p];
+                    d3[p] ^= d1[p];
+                }
+                bs_muladd(d0, d1, c0[2 * B], uni);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) d1[p] ^= d0[p];
+                bs_lds_store<N>(pl, i0, d0);
+                bs_lds_store<N>(pl, i0 + h, d1);
+                bs_muladd(d2, d3, c0[2 * B + 1], uni);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) d3[p] ^= d2[p];
+                bs_lds_store<N>(pl, i0 + 2 * h, d2);
+                bs_lds_store<N>(pl, i0 + 3 * h, d3);
+            }
+            __syncthreads();
+        }
+        for (; qq >= 0; --qq) {
+            const uint32_t ql = (uint32_t)qq, h = 1u << ql;
+            if (bact && bp < (A.R >> 1)) {
+                const uint32_t blk = bp >> ql;
+                const uint32_t i = bc * k + ((blk << (ql + 1)) | (bp & (h - 1)));
+                uint32_t di[16], dj[16];
+                bs_lds_load<N>(pl, i, di);
+                bs_lds_load<N>(pl, i + h, dj);
+                bs_muladd(di, dj, cfwd[(A.R - (A.R >> ql)) + blk], ql >= 6 || ql + 1 == A.b);
+#pragma unroll
+                for (int p = 0; p < 16; ++p) dj[p] ^= di[p];
+                bs_lds_store<N>(pl, i, di);
+                bs_lds_store<N>(pl, i + h, dj);
+            }
+            __syncthreads();
+        }
+        if (MODE == 2) {   // recovered row b = D_b' out[E_b], D_b' = Qy_b / Py_b
+            for (uint32_t q = tid; q < e_g * cg; q += NT) {
+                const uint32_t bb = q / cg, c = q - bb * cg;
+                const uint32_t cc = col0 + 32u * c;
+                if (cc >= A.nsym) continue;
+                uint32_t y[16], z[16];
+                bs_lds_load<N>(pl, c * k + (uint32_t)gE[bb], y);
+                uint32_t db = lp[2 * A.em + bb] + kOrd16 - lp[3 * A.em + bb];
+                db = db >= kOrd16 ? db - kOrd16 : db;
+#pragma unroll
+                for (int p = 0; p < 16; ++p) z[p] = 0;
+                bs_muladd(z, y, A.gexp[db]);
+                bs_store_row(A.rep + g * A.rgs + (uint64_t)bb * A.rrs + 2ull * cc, min(32u, A.nsym - cc), z, nullptr);
+            }
+            continue;
+        }
+        // repairs first .. first + r - 1 = coset points first + jj (decode:
+        // the syndrome of the accepted repair k + jj, its received row XORed in)
+        const uint16_t* rpos = MODE == 1 ? A.rpos + g * A.r : nullptr;
+        const uint16_t* rslot = MODE == 1 ? A.rslot + g * A.r : nullptr;
+        for (uint32_t q = tid; q < A.r * cg; q += NT) {
+            const uint32_t jj = q / cg, c = q - jj * cg;
+            const uint32_t cc = col0 + 32u * c;
+            if (cc >= A.nsym) continue;
+            uint64_t orow = jj;
+            const uint8_t* xr = nullptr;
+            if (MODE == 1) {
+                orow = rpos[jj];
+                if (orow == 0xFFFFu) continue;
+                xr = gsrc + (uint64_t)rslot[jj] * A.srs + 2ull * cc;
+            }
+            uint32_t y[16];
+            bs_lds_load<N>(pl, c * k + A.first + jj, y);
+            bs_store_row(A.rep + g * A.rgs + orow * A.rrs + 2ull * cc, min(32u, A.nsym - cc), y, xr);
+        }
+    }
+}
+
 uint32_t hmul16(uint32_t a, uint32_t b) {
     uint32_t r = 0;
     while (b) {
@@ -542,17 +934,59 @@ int fft16_launch(qf_ctx* ctx, hipStream_t st, Fft16Args A, uint32_t G, uint32_t 
     }
     ca.t.kappa = (uint16_t)hmul16(delta, hinv16(w_at(a, k)));
     uint16_t* cst = reinterpret_cast<uint16_t*>(work);
+    // the bit-sliced kernel (k <= 2,048) unless QF_OPT_GF16_FFT_BS = 0
+    // the bit-plane kernel (k <= 2,048): an item (generation, 32 symbol
+    // columns) runs its whole transform in one workgroup, so it pays once
+    // the items fill a quarter of the CUs (one Extreme window at L = 1,200
+    // is 19 items: the log kernel's narrower strips spread it wider)
+    const int64_t bs_opt = qf::ctx_opt(ctx, QF_OPT_GF16_FFT_BS);
+    const uint64_t bs_items = (uint64_t)G * ((L / 2 + 31) / 32);
+    const bool bs = k <= kBsMaxK && (bs_opt >= 2 || (bs_opt == 1 && bs_items >= (uint64_t)qf::ctx_num_cus(ctx) / 4));
+    A.r4 = bs_opt == 3 ? 1u : 0u;
     ca.out = cst;
     ca.glog = A.glog;
+    ca.gexp = A.gexp;
     ca.k = k;
     ca.a = a;
     ca.R = R;
     ca.b = b;
+    ca.normal = bs ? 1u : 0u;
     const uint32_t n_c = 2 * k + R - 2;
     hipLaunchKernelGGL(k_fft16_consts, dim3(std::min<uint32_t>((n_c + 255) / 256, 1024)), dim3(256), 0, st, ca);
     QF_HIP(hipGetLastError());
-    // strip width: the 32 KiB LDS strip, narrowed until the items cover the CUs
     const uint32_t nsym = L / 2;
+    if (bs) {
+        // item = (generation, cg column groups of 32 symbols); cg narrowed
+        // until the items cover the workgroup slots (two per CU for k <= 1,024)
+        const bool big = k > kBsRows;
+        const uint32_t slots = (uint32_t)qf::ctx_num_cus(ctx) * (big ? 1u : 2u);
+        const uint32_t groups = (nsym + 31) / 32;
+        uint32_t cg = big ? 1u : kBsRows / k;
+        while (cg > 1 && cg / 2 >= groups) cg >>= 1;
+        while (cg > 1 && (uint64_t)G * ((groups + cg - 1) / cg) < slots) cg >>= 1;
+        A.cst = cst;
+        A.a = a;
+        A.R = R;
+        A.b = b;
+        A.nsym = nsym;
+        A.S = cg;
+        A.strips = (groups + cg - 1) / cg;
+        const uint64_t items = (uint64_t)G * A.strips;
+        const dim3 grid((uint32_t)std::min<uint64_t>(items, slots));
+        const int mode = A.solve ? 2 : A.syn ? 1 : 0;
+        hipEvent_t ev = qf::ctx_prof_begin(ctx, st);
+        auto launch = [&](auto kern, uint32_t nt) { hipLaunchKernelGGL(kern, grid, dim3(nt), 0, st, A, G); };
+        if (big)
+            mode == 0 ? launch(k_fft16_bs<0, true>, 1024) : mode == 1 ? launch(k_fft16_bs<1, true>, 1024)
+                                                           : launch(k_fft16_bs<2, true>, 1024);
+        else
+            mode == 0 ? launch(k_fft16_bs<0, false>, kBsThreads) : mode == 1 ? launch(k_fft16_bs<1, false>, kBsThreads)
+                                                                  : launch(k_fft16_bs<2, false>, kBsThreads);
+        QF_HIP(hipGetLastError());
+        qf::ctx_prof_end(ctx, st, ev, name);
+        return QF_OK;
+    }
+    // strip width: the 32 KiB LDS strip, narrowed until the items cover the CUs
     uint32_t S = kFftLdsSymbols / k, lgS = 0;
     while ((1u << (lgS + 1)) <= S) ++lgS;
     S = 1u << lgS;

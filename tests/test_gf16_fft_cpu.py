@@ -195,3 +195,74 @@ def test_fft_solve_recovers_erasures(oracle, k, e):
         qy = prod(xa ^ y for xa in X)
         py = prod(y ^ E[c] for c in range(e) if c != b)
         assert np.array_equal(vmul(smul(qy, g16.inv(py)), out[y]), x[y]), (b, y)
+
+
+# --- the bit-plane form of k_fft16_bs (qf_gf16_fft.hip) ---------------------
+# A lane holds 32 symbol columns of a row as 16 plane dwords (plane p = bit p of
+# every symbol).  Restated with numpy uint32 arrays: the load (byte swap of the
+# two big-endian symbols of each dword + a 16 x 16 bit transpose of both dword
+# halves), the product s x by Horner over the bits of s with x alpha = the
+# planes shifted up and plane 15 folded into planes 0, 1, 3 and 12 (0x1100B),
+# and the store (the transpose is its own inverse).
+
+_M32 = np.uint32(0xFFFFFFFF)
+
+
+def _bs_transpose(d: np.ndarray) -> np.ndarray:
+    d = d.copy()
+    for w, m in ((8, 0x00FF00FF), (4, 0x0F0F0F0F), (2, 0x33333333), (1, 0x55555555)):
+        for i in range(16):
+            if i & w:
+                continue
+            t = ((d[i] >> np.uint32(w)) ^ d[i + w]) & np.uint32(m)
+            d[i + w] ^= t
+            d[i] ^= (t << np.uint32(w)) & _M32
+    return d
+
+
+def _bs_swap16x2(w: np.ndarray) -> np.ndarray:
+    return ((w & np.uint32(0x00FF00FF)) << np.uint32(8)) | ((w >> np.uint32(8)) & np.uint32(0x00FF00FF))
+
+
+def _bs_load(row64: np.ndarray) -> np.ndarray:
+    """64 bytes (32 big-endian symbols) -> 16 planes."""
+    return _bs_transpose(_bs_swap16x2(row64.view("<u4").astype(np.uint32)))
+
+
+def _bs_store(planes: np.ndarray) -> np.ndarray:
+    return _bs_swap16x2(_bs_transpose(planes)).astype("<u4").view(np.uint8)
+
+
+def _bs_mulx(x: np.ndarray) -> np.ndarray:
+    t = x[15]
+    y = np.concatenate([[t], x[:15]]).astype(np.uint32)
+    y[1] ^= t
+    y[3] ^= t
+    y[12] ^= t
+    return y
+
+
+def _bs_mul(x: np.ndarray, s: int) -> np.ndarray:
+    acc = x & (_M32 if s >> 15 & 1 else np.uint32(0))
+    for j in range(14, -1, -1):
+        acc = _bs_mulx(acc)
+        if s >> j & 1:
+            acc = acc ^ x
+    return acc
+
+
+def test_bitplane_form_matches_field():
+    rng = np.random.default_rng(16)
+    for _ in range(40):
+        row = rng.integers(0, 256, 64, dtype=np.uint8)
+        sym = to_sym(row[None])[0].astype(np.int64)
+        planes = _bs_load(row)
+        for p in range(16):           # plane p: bit i = symbol 2i, bit 16 + i = symbol 2i + 1
+            bits = (sym >> p) & 1
+            want = sum(int(bits[2 * i]) << i for i in range(16)) | sum(int(bits[2 * i + 1]) << (16 + i)
+                                                                       for i in range(16))
+            assert int(planes[p]) == want
+        assert np.array_equal(_bs_store(planes), row)
+        for s in (0, 1, 2, 0x8000, 0xFFFF, int(rng.integers(0, 65536))):
+            got = to_sym(_bs_store(_bs_mul(planes, s))[None])[0]
+            assert np.array_equal(got, vmul(s, sym)), s

@@ -379,16 +379,18 @@ def test_decode16_bitsliced_syndromes(qf, oracle, gpu_ctx, L):
                                      (1024, 1024, 64, 1), (1024, 8, 1200, 2), (4096, 100, 32, 1),
                                      (4096, 16, 4, 1), (2048, 2048, 100, 3), (64, 33, 1200, 9),
                                      (256, 200, 9000, 2)])
-def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G):
+@pytest.mark.parametrize("bs", [2, 3, 0])
+def test_encode16_fft(qf, oracle, gpu_ctx, k, r, L, G, bs):
     """Power-of-two windows without a bit-sliced kernel run the additive-FFT
-    kernel (qf_gf16_fft.hip): bit-exact against the oracle's Encoder16 and
+    kernel (qf_gf16_fft.hip; bs 2 / 3: the bit-plane kernel for k <= 2,048,
+    one / two layers per LDS pass, bs 0: the log / Zech one): bit-exact against the oracle's Encoder16 and
     against the general k_matvec16 path (gf16_fft = 0); guard bytes outside
     [0, L) of every repair row untouched (run_encode16)."""
     rng = np.random.default_rng(k * 13 + r + L)
     src = rng.integers(0, 256, (G, k, L), dtype=np.uint8)
     src[0, 0, :4] = 0
     src[-1, -1, -2:] = 0
-    qf.set_default_options(gf16_fft=2)           # the FFT wherever it applies
+    qf.set_default_options(gf16_fft=2, gf16_fft_bs=bs)   # the FFT wherever it applies
     gpu_ctx.profile(True)
     rep = run_encode16(qf, src, r)
     names = set(gpu_ctx.kernel_times())
@@ -420,7 +422,8 @@ def test_encode16_fft_many_generations(qf, oracle, gpu_ctx):
         assert np.array_equal(rep[g], oracle.encode16(src[g], r)), g
 
 
-def test_encoder16_fft_window_slides(qf, oracle, gpu_ctx):
+@pytest.mark.parametrize("bs", [2, 3, 0])
+def test_encoder16_fft_window_slides(qf, oracle, gpu_ctx, bs):
     """Encoder16 over a power-of-two window (decoder.rs:25-75): after the
     window slides (ring rotation) and for a repair range starting past 0, the
     FFT kernel's repairs equal the oracle's Cauchy rows over the window."""
@@ -432,7 +435,7 @@ def test_encoder16_fft_window_slides(qf, oracle, gpu_ctx):
         enc.add_source_packet(qf.Packet(i, bytearray(src[i].tobytes()), L, True))
     want = oracle.encode16(np.ascontiguousarray(src[5:]), 12)
     C = oracle.cauchy16(k, 12)
-    qf.set_default_options(gf16_fft=2)
+    qf.set_default_options(gf16_fft=2, gf16_fft_bs=bs)
     gpu_ctx.profile(True)
     got = [enc.generate_repair_packet(j) for j in (0, 7)] + enc.generate_repairs(3, 9)
     names = set(gpu_ctx.kernel_times())
@@ -445,8 +448,9 @@ def test_encoder16_fft_window_slides(qf, oracle, gpu_ctx):
         assert bytes(p.coefficients[: 2 * k]) == np.asarray(C[3 + n], dtype=">u2").tobytes(), n
 
 
-@pytest.mark.parametrize("k,r,L", [(128, 40, 100), (256, 256, 34), (32, 16, 2)])
-def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
+@pytest.mark.parametrize("k,r,L", [(128, 40, 100), (256, 256, 34), (32, 16, 2), (1024, 16, 66)])
+@pytest.mark.parametrize("bs", [2, 3, 0])
+def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L, bs):
     """Cauchy decode of a power-of-two k without a bit-sliced kernel: the
     syndromes come from the additive FFT (k_fft16_syndromes, sources gathered
     through the slot map, erased ones as zero rows, the accepted repair row
@@ -473,7 +477,7 @@ def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
         gens[0] = ([k + extra] + [a for s, a in enumerate(arr) if s != pos],
                    np.concatenate([far[None], np.delete(rows, pos, 0)]), None)
     G = len(gens)
-    qf.set_default_options(gf16_fft=2)
+    qf.set_default_options(gf16_fft=2, gf16_fft_bs=bs)
     gpu_ctx.profile(True)
     res = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
     names = set(gpu_ctx.kernel_times())
@@ -496,3 +500,34 @@ def test_decode16_fft_syndromes(qf, oracle, gpu_ctx, k, r, L):
     res2 = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens], False)
     for x, y in zip(res[:4], res2[:4]):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("k,r,L,e", [(2048, 64, 40, 64), (1024, 1024, 34, 700), (2048, 2048, 6, 1500)])
+def test_decode16_fft_large_windows(qf, oracle, gpu_ctx, k, r, L, e):
+    """Extreme-size windows (the oracle's k^3 elimination is too slow here):
+    every erased source comes back equal to the source row, and the bit-plane
+    FFT kernels (k <= 2,048: 1,024-thread variant at k = 2,048) give the same
+    bytes, statuses and indices as the log / Zech kernels."""
+    rng = np.random.default_rng(k + r + L + e)
+    src, gens = make_gens(oracle, rng, k, r, L, 2, erase=e)
+    G = len(gens)
+    out = {}
+    for bs in (2, 3, 0):
+        qf.set_default_options(gf16_fft=2, gf16_fft_bs=bs)
+        gpu_ctx.profile(True)
+        out[bs] = run_decode16(qf, k, r, L, G, [(a, rw, np.zeros((len(a), k), np.uint16)) for a, rw, _ in gens],
+                               False)
+        names = set(gpu_ctx.kernel_times())
+        gpu_ctx.profile(False)
+        assert "k_fft16_syndromes" in names and "k_fft16_solve" in names, names
+    rec, ri, nrec, st, rrs, rec_gs = out[2]
+    for g, (a, rw, _) in enumerate(gens):
+        assert st[g] == 0
+        erased = sorted(set(range(k)) - set(x for x in a[:k] if x < k))
+        assert nrec[g] == len(erased) == e and ri[g, :e].tolist() == erased, g
+        for b, i in enumerate(erased):
+            o = g * rec_gs + b * rrs
+            assert np.array_equal(rec[o: o + L], src[g, i]), (g, i)
+    for bs in (3, 0):
+        for x, y in zip(out[2][:4], out[bs][:4]):
+            assert np.array_equal(x, y), bs

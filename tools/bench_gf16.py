@@ -108,6 +108,19 @@ def main():
         kms = sum(ms for _, ms in kt.values())
         res[name + "/decode16"] = {"k": k, "r": r, "L": L, "G": G, "erasures": e, "wall_ms": round(wall, 3),
                                    "kernels": kt, "GiBps_alg": round(G * (k + e) * L / (kms / 1e3) / 2**30, 1)}
+        if k >= 1024:   # the FFT variants (QF_OPT_GF16_FFT_BS): bit planes always (2), radix 4 (3), log / Zech (0)
+            for v in (2, 3, 0):
+                qf.set_default_options(gf16_fft_bs=v)
+                wall, kt = timed(ctx, enc, a.reps)
+                kms = sum(ms for _, ms in kt.values())
+                res[f"{name}/encode16_bs{v}"] = {"wall_ms": round(wall, 3), "kernels": kt,
+                                                 "GiBps_alg": round(G * (k + r) * L / (kms / 1e3) / 2**30, 1)}
+                wall, kt = timed(ctx, dec, a.reps)
+                assert (st == 0).all().item() and torch.equal(rec.view(G, emax, rs)[g, :e, :L], want)
+                kms = sum(ms for _, ms in kt.values())
+                res[f"{name}/decode16_bs{v}"] = {"wall_ms": round(wall, 3), "kernels": kt,
+                                                 "GiBps_alg": round(G * (k + e) * L / (kms / 1e3) / 2**30, 1)}
+            qf.reset_default_options()
         print(name, json.dumps({kk: v for kk, v in res.items() if kk.startswith(name)}), flush=True)
         del src, rep, rows, rec
 
