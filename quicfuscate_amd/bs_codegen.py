@@ -369,6 +369,10 @@ class KernelSpec:
     stagger: tuple = ()
     # lab only: drop the payload row loads (keeps maps, records, compute)
     lab_norows: bool = False
+    # lab only (chunked dec): absent rows read zero row (g & 63) of a region of
+    # 64 zero rows 2,048 B apart instead of one shared zero row (spreads the
+    # ~20 % of row loads that hit it over 64 x 10 lines)
+    lab_zspread: bool = False
     # lab only (chunked dec): skip the row loop (the LU phase alone, on whatever
     # the accumulator registers hold) -- timing of the LU in isolation
     lab_lu_only: bool = False
@@ -1801,6 +1805,10 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("v_movs", (V_ZA, 22)))
     E(Op("v_movs", (V_ZA + 1, 23)))
     E(Op("v_mad64_k", (V_ZA, V_UA, 16, V_ZA)))
+    if spec.lab_zspread:
+        E(Op("v_andk", (V_SLOT, 63, V_GA)))
+        E(Op("v_lshl", (V_SLOT, 11, V_SLOT)))
+        E(Op("v_mad64_k", (V_ZA, V_SLOT, 1, V_ZA)))
     E(Op("s_nop", (4,)))
     E(Op("label", (".Lbody",)))
 

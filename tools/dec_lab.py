@@ -37,6 +37,17 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 4k: absent rows spread over 64 zero rows (lab_zspread) instead of
+    # one shared zero row that ~20 % of all row loads hit
+    ("z_warm", dict(LIB_DEC4), ()),
+    ("z_lib", dict(LIB_DEC4), ()),
+    ("z_spread", {**LIB_DEC4, "lab_zspread": True}, ()),
+    ("z_nolu", {**LIB_DEC4, "lu": False}, ()),
+    ("z_spread_nolu", {**LIB_DEC4, "lab_zspread": True, "lu": False}, ()),
+    ("z_lib_2", dict(LIB_DEC4), ()),
+    ("z_spread_2", {**LIB_DEC4, "lab_zspread": True}, ()),
+]
+VARIANTS_R04D = [
     # round 4d: lu_ilp and 64-bit-shift transposes / selectors together
     ("q_warm", dict(LIB_DEC), ()),
     ("q_lib", dict(LIB_DEC), ()),
@@ -331,7 +342,7 @@ def run(G, reps):
     d_map = torch.from_numpy(smap.reshape(-1)).to(dev)
     d_lu = torch.from_numpy(lu.reshape(-1)).to(dev)
     d_tab = torch.from_numpy(bs.split_tables()).to(dev)
-    zero = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    zero = torch.zeros(64 * 2048 + 4096, dtype=torch.uint8, device=dev)   # lab_zspread: 64 rows 2,048 B apart
     stream = torch.cuda.current_stream()
     res = {}
     prepared = {}
