@@ -140,6 +140,9 @@ enum {
                                     a quarter of the CUs, 2 always, 3 always with two layers per LDS
                                     pass; 0 the log / Zech-table kernel for every k
                                     [QF_GF16_FFT_BS; default 1] */
+    QF_OPT_PREPARE_LANES,        /* 1: the fused decode's acceptance pass runs one generation per lane
+                                    (k_decode_prepare_lu_lanes); 0: one per wave [QF_PREPARE_LANES;
+                                    default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

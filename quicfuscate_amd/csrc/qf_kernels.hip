@@ -1137,6 +1137,194 @@ __global__ void __launch_bounds__(64 * kPrepWaves) k_decode_prepare_lu(PrepareCa
 }
 
 // ---------------------------------------------------------------------------
+// The same decode control with one generation per LANE (k_decode_prepare_lu
+// runs one per wave): a generation's acceptance is a scalar walk over its row
+// indices, its closed-form LU ~3 e^2 table lookups, so a lane does it with
+// the wave's other 63 generations in lockstep instead of 64 lanes sharing one
+// through ballots, LDS atomics and wave barriers (~15x fewer wave
+// instructions per generation).  The record and slot map of the block's
+// generations are staged in LDS ([word][lane]: a lane's bytes land at
+// data-dependent offsets) and written out coalesced; outputs are byte-equal
+// to k_decode_prepare_lu's (tests/test_gpu_decode.py compares the two).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPrepLanes = 128;      // generations per block
+constexpr uint32_t kPrepRecWords = 68;    // 272-B record
+constexpr uint32_t kPrepMapWords = 64;    // slot map <= 256 B
+constexpr uint32_t kPrepMaskWords = 8;    // accepted-source bits, k <= 256
+
+__global__ void __launch_bounds__(kPrepLanes) k_decode_prepare_lu_lanes(PrepareCauchyArgs a) {
+    __shared__ uint8_t sexp[512];
+    __shared__ uint8_t slog[256];
+    __shared__ __attribute__((aligned(16))) uint32_t srec[kPrepRecWords * kPrepLanes];
+    __shared__ __attribute__((aligned(16))) uint32_t smp[kPrepMapWords * kPrepLanes];
+    __shared__ __attribute__((aligned(16))) uint32_t sam[kPrepMaskWords * kPrepLanes];
+    for (uint32_t i = threadIdx.x; i < 768; i += blockDim.x) {
+        if (i < 512) sexp[i] = a.explog[i];
+        else slog[i - 512] = a.explog[i];
+    }
+    const uint32_t tid = threadIdx.x, k = a.k, r = a.r;
+    const uint32_t mw = a.map_stride / 4;
+    uint8_t* rec8 = reinterpret_cast<uint8_t*>(srec);
+    uint8_t* map8 = reinterpret_cast<uint8_t*>(smp);
+    auto rec_b = [&](uint32_t byte) -> uint8_t& { return rec8[((byte >> 2) * kPrepLanes + tid) * 4 + (byte & 3)]; };
+    auto map_b = [&](uint32_t byte) -> uint8_t& { return map8[((byte >> 2) * kPrepLanes + tid) * 4 + (byte & 3)]; };
+    for (uint64_t g0 = (uint64_t)blockIdx.x * kPrepLanes; g0 < a.G; g0 += (uint64_t)gridDim.x * kPrepLanes) {
+        __syncthreads();   // the tables (first pass) / the previous pass's copy-out
+        const uint64_t g = g0 + tid;
+        const bool live = g < a.G;
+        // record: LU columns zero, rank bytes absent; map all absent (the
+        // block fills them together, 16 bytes per write)
+        {
+            uint4* r4 = reinterpret_cast<uint4*>(srec);
+            const uint32_t zero4 = 64 * kPrepLanes / 4, all4 = kPrepRecWords * kPrepLanes / 4;
+            for (uint32_t i = tid; i < all4; i += kPrepLanes)
+                r4[i] = i < zero4 ? make_uint4(0, 0, 0, 0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+            uint4* m4 = reinterpret_cast<uint4*>(smp);
+            for (uint32_t i = tid; i < mw * kPrepLanes / 4; i += kPrepLanes) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+            uint4* a4 = reinterpret_cast<uint4*>(sam);
+            for (uint32_t i = tid; i < kPrepMaskWords * kPrepLanes / 4; i += kPrepLanes) a4[i] = make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+        int32_t status = 0;
+        uint32_t e = 0;
+        if (live) {
+            // decoder.rs:679-699: rows in arrival order, the first k
+            // candidates accepted; a systematic row only at its index's first
+            // arrival, every valid repair row a candidate (a repeated one:
+            // ERANK); any index >= k + r: EINVAL
+            const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
+            const uint16_t* ridx = a.row_index + g * a.max_rows;
+            uint32_t accepted = 0, rep = 0;
+            uint64_t acc64 = 0;
+            bool bad = false, dup = false;
+            for (uint32_t s0 = 0; s0 < n; s0 += 8) {
+                uint32_t idx[8];
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) idx[q] = s0 + q < n ? ridx[s0 + q] : 0xFFFFu;
+#pragma unroll
+                for (uint32_t q = 0; q < 8; ++q) {
+                    const uint32_t s = s0 + q, x = idx[q];
+                    if (s >= n) break;
+                    if (x >= k) {
+                        const uint32_t j = x - k;
+                        if (j >= r) {
+                            bad = true;
+                            continue;
+                        }
+                        if (accepted < k) {
+                            dup |= (rep >> j) & 1u;
+                            rep |= 1u << j;
+                            map_b(k + j) = (uint8_t)s;
+                            ++accepted;
+                        }
+                    } else if (accepted < k) {
+                        if (k <= 64) {   // the accepted-source bits in registers (no LDS round trip per row)
+                            const uint64_t bit = 1ull << x;
+                            if (!(acc64 & bit)) {
+                                acc64 |= bit;
+                                map_b(x) = (uint8_t)s;
+                                ++accepted;
+                            }
+                        } else {
+                            uint32_t& m = sam[(x >> 5) * kPrepLanes + tid];
+                            const uint32_t bit = 1u << (x & 31);
+                            if (!(m & bit)) {
+                                m |= bit;
+                                map_b(x) = (uint8_t)s;
+                                ++accepted;
+                            }
+                        }
+                    }
+                }
+            }
+            if (k <= 64) {
+                sam[tid] = (uint32_t)acc64;
+                sam[kPrepLanes + tid] = (uint32_t)(acc64 >> 32);
+            }
+            status = bad ? -1 : accepted < k ? -3 : dup ? -4 : 0;
+            e = __popc(rep);
+            if (status != 0) {
+                for (uint32_t w = 0; w < mw; ++w) smp[w * kPrepLanes + tid] = 0xFFFFFFFFu;
+            } else if (e > 0) {
+                // J ascending (x = k + j), E = the erased sources ascending (y)
+                uint32_t X[16], Y[16], J[16];
+                {
+                    uint32_t m = rep;
+#pragma unroll
+                    for (uint32_t q = 0; q < 16; ++q) {
+                        J[q] = m ? (uint32_t)__builtin_ctz(m) : 0u;
+                        X[q] = (k + J[q]) & 0xFF;
+                        m &= m - 1;
+                    }
+                    uint32_t cw = 0, cm = ~sam[tid] & (k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1));
+#pragma unroll
+                    for (uint32_t q = 0; q < 16; ++q) {
+                        while (cm == 0 && cw + 1 < (k + 31) / 32) {
+                            ++cw;
+                            const uint32_t lim = k - 32 * cw;
+                            cm = ~sam[cw * kPrepLanes + tid] & (lim >= 32 ? 0xFFFFFFFFu : ((1u << lim) - 1));
+                        }
+                        Y[q] = cm ? 32 * cw + (uint32_t)__builtin_ctz(cm) : 0u;
+                        cm &= cm - 1;
+                    }
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 16; ++q)
+                    if (q < e) a.rec_index[g * a.e_max + q] = (uint16_t)Y[q];
+                // closed-form LU of C[J, E] (as k_decode_prepare_lu): with
+                //   P0[a][m] = sum_{q<m} log(x_a + x_q) - log(x_a + y_q),
+                //   P1[a][m] = sum_{q<m} log(y_a + x_q) - log(y_a + y_q),
+                //   L  (i > j): log(x_j + y_j) - log(x_i + y_j) + P0[i][j] - P0[j][j]
+                //   U  (i = j): log(x_i + y_i) + P1[i][i] - P0[i][i]
+                //   U' (i < j): log(x_i + y_i) - log(x_i + y_j) + P1[i][i] - P1[j][i]
+                // row a of L and column a of U' come with the prefixes of row a
+                int32_t S[16], D0[16], D1[16];
+#pragma unroll
+                for (uint32_t q = 0; q < 16; ++q) S[q] = slog[X[q] ^ Y[q]];
+                auto put = [&](uint32_t i, uint32_t j, int32_t l0) {   // LU[i][j] -> column J[j], byte J[i]
+                    const uint32_t l = (uint32_t)(l0 + 64 * 255) % 255u;
+                    rec_b(16 * J[j] + J[i]) = sexp[l];
+                };
+#pragma unroll
+                for (uint32_t p = 0; p < 16; ++p) {
+                    if (p >= e) break;
+                    int32_t pp0 = 0, pp1 = 0;
+#pragma unroll
+                    for (uint32_t q = 0; q < p; ++q) {
+                        const int32_t xx = slog[X[p] ^ X[q]], xy = slog[X[p] ^ Y[q]];
+                        const int32_t yx = slog[Y[p] ^ X[q]], yy = slog[Y[p] ^ Y[q]];
+                        put(p, q, S[q] - xy + pp0 - D0[q]);   // L[p][q]
+                        put(q, p, S[q] - yx + D1[q] - pp1);   // U'[q][p]: log(x_q + y_p) = yx
+                        pp0 += xx - xy;
+                        pp1 += yx - yy;
+                    }
+                    D0[p] = pp0;
+                    D1[p] = pp1;
+                    put(p, p, S[p] + pp1 - pp0);
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 16; ++q)
+                    if (q < e) rec_b(256 + J[q]) = (uint8_t)q;   // rank of repair J[q]
+            }
+            a.status[g] = status;
+            a.n_out[g] = status == 0 ? e : 0;
+        }
+        __syncthreads();
+        // copy-out: the block's records and slot maps, contiguous runs
+        const uint32_t ng = (uint32_t)min<uint64_t>(kPrepLanes, a.G - g0);
+        if ((a.lu_stride & 3) == 0)
+            for (uint32_t d = tid; d < ng * kPrepRecWords; d += kPrepLanes) {
+                const uint32_t gl = d / kPrepRecWords, w = d - gl * kPrepRecWords;
+                *reinterpret_cast<uint32_t*>(a.lu_out + (g0 + gl) * a.lu_stride + 4 * w) = srec[w * kPrepLanes + gl];
+            }
+        for (uint32_t d = tid; d < ng * mw; d += kPrepLanes) {
+            const uint32_t gl = d / mw, w = d - gl * mw;
+            *reinterpret_cast<uint32_t*>(a.smap + (g0 + gl) * a.map_stride + 4 * w) = smp[w * kPrepLanes + gl];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Element-wise slice multiply and synthetic fill.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_mul_slice(const uint8_t* __restrict__ a,
@@ -1430,7 +1618,18 @@ hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t 
         // a capped persistent grid when the pass runs beside other work
         // (split-phase decode): fewer CUs taken from the concurrent kernel
         if (a.grid_cap && blocks > a.grid_cap) blocks = a.grid_cap;
-        hipLaunchKernelGGL(k_decode_prepare_lu, dim3(blocks), dim3(64 * kPrepWaves), 0, st, a);
+        if (a.lanes && a.G >= 2048 && a.map_stride <= 4 * kPrepMapWords && a.lu_stride % 4 == 0 &&
+            a.lu_stride >= 4 * kPrepRecWords) {
+            // one generation per lane (the same grid cap, in 128-generation
+            // blocks); small batches keep a wave per generation: a lane's
+            // walk is serial, so one generation alone finishes sooner on 64
+            // lanes (the per-packet decode)
+            uint32_t lb = (a.G + kPrepLanes - 1) / kPrepLanes;
+            if (a.grid_cap && lb > a.grid_cap) lb = a.grid_cap;
+            hipLaunchKernelGGL(k_decode_prepare_lu_lanes, dim3(lb), dim3(kPrepLanes), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(k_decode_prepare_lu, dim3(blocks), dim3(64 * kPrepWaves), 0, st, a);
+        }
     } else {
         hipLaunchKernelGGL(k_decode_prepare_cauchy, dim3(a.G), dim3(64), 0, st, a);
     }

@@ -97,7 +97,7 @@ def check(oracle, k, L, src, gens, out, with_coeffs):
             assert (rec[g * rec_gs + m * rrs + L: g * rec_gs + (m + 1) * rrs] == 0x5A).all()
 
 
-PATHS = ["default", "default_1wave", "default_nofft", "syn", "general", "syn_bs", "general_bs"]
+PATHS = ["default", "default_1wave", "default_nofft", "default_waveprep", "syn", "general", "syn_bs", "general_bs"]
 
 
 def _path(_unused, path):
@@ -112,12 +112,15 @@ def _path(_unused, path):
     # (and the payload pass k_combine_slots_split against k_combine_slots)
     # "default_nofft": the one-wave kernels with one coefficient block per
     # repair instead of the additive-FFT row loop (QF_OPT_FFT_KERNELS = 0)
-    one = path in ("default_1wave", "default_nofft")
+    # "default_waveprep": the one-wave kernels with the acceptance pass one
+    # generation per wave (k_decode_prepare_lu) instead of per lane
+    one = path in ("default_1wave", "default_nofft", "default_waveprep")
     fft = 0 if path == "default_nofft" else 1
+    lanes = 0 if path == "default_waveprep" else 1
     if one:
         path = "default"
     opts = dict(decode_ksplit=0 if one else 1, encode_ksplit=0 if one else 1, combine_split=0 if one else 1,
-                fft_kernels=fft)
+                fft_kernels=fft, prepare_lanes=lanes)
     # "*_bs": the payload pass takes the bit-sliced qf_combine_bs at every row
     # length (by default only rows of >= 64 lane-chunks of 32 B do); "general"
     # keeps k_combine_slots at every length (combine_bs 0)
@@ -372,3 +375,55 @@ def test_decode_batch_host_matches_oracle(qf, oracle, gpu_ctx, path, k, r, L, G,
     out = (t_rec.numpy(), t_recidx.numpy().view(np.uint16).reshape(G, -1), t_nrec.numpy(), t_status.numpy(),
            rs, rec_gs)
     check(oracle, k, L, src, gens, out, False)
+
+
+@pytest.mark.parametrize("k,r,L", [(64, 16, 48), (32, 5, 64), (96, 15, 32)])
+def test_decode_prepare_per_lane_matches_per_wave(qf, oracle, gpu_ctx, k, r, L):
+    """The acceptance pass one generation per lane (k_decode_prepare_lu_lanes,
+    batches of >= 2,048 generations) against one per wave
+    (k_decode_prepare_lu): duplicated sources and repairs, short generations,
+    no erasures, every repair needed, repair indices out of range -- the
+    recovered rows, indices, counts and statuses are identical, and every
+    generation equals the oracle."""
+    rng = np.random.default_rng(k * 7 + r)
+    G = 2600
+    max_rows = k + r + 4
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, dup_prob=0.03, trim_prob=0.05)
+    e_full = min(k, r)
+    for g in range(0, G, 97):            # every repair needed
+        _, full = make_batch(oracle, rng, k, r, L, 1, max_rows, erase=e_full)
+        src[g] = _[0]
+        gens[g] = full[0]
+    for g in range(5, G, 101):           # no erasures
+        _, none = make_batch(oracle, rng, k, r, L, 1, max_rows, erase=0)
+        src[g] = _[0]
+        gens[g] = none[0]
+    bad = set(range(11, G, 211))         # a repair index past k + r: EINVAL
+    for g in bad:
+        arr, rows, rc = gens[g]
+        if arr:
+            arr = list(arr)
+            arr[len(arr) // 2] = k + r + 3
+            gens[g] = (arr, rows, rc)
+    outs = {}
+    for lanes in (1, 0):
+        qf.set_default_options(prepare_lanes=lanes, decode_ksplit=0)
+        outs[lanes] = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    for x, y in zip(outs[1][:4], outs[0][:4]):
+        assert np.array_equal(x, y)
+    status = outs[1][3]
+    assert all(status[g] == -1 for g in bad if gens[g][0])
+    assert {0, -1, -3, -4} <= set(status.tolist())
+    good = [g for g in range(G) if g not in bad]
+    rec, recidx, nrec, st, rrs, rec_gs = outs[1]
+    for g in good:
+        arr, rw, _ = gens[g]
+        ost, sol, mask = oracle.decode(k, arr, rw if len(arr) else np.zeros((0, L), np.uint8), None)
+        assert st[g] == ost, (g, st[g], ost)
+        if ost:
+            assert nrec[g] == 0
+            continue
+        erased = [i for i in range(k) if not mask[i]]
+        assert nrec[g] == len(erased) and list(recidx[g, : nrec[g]]) == erased, g
+        for m, i in enumerate(erased):
+            assert (rec[g * rec_gs + m * rrs: g * rec_gs + m * rrs + L] == sol[i]).all(), (g, i)
