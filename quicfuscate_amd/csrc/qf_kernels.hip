@@ -1197,45 +1197,62 @@ __global__ void __launch_bounds__(kPrepLanes) k_decode_prepare_lu_lanes(PrepareC
             uint32_t accepted = 0, rep = 0;
             uint64_t acc64 = 0;
             bool bad = false, dup = false;
-            for (uint32_t s0 = 0; s0 < n; s0 += 8) {
-                uint32_t idx[8];
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) idx[q] = s0 + q < n ? ridx[s0 + q] : 0xFFFFu;
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q) {
-                    const uint32_t s = s0 + q, x = idx[q];
-                    if (s >= n) break;
-                    if (x >= k) {
-                        const uint32_t j = x - k;
-                        if (j >= r) {
-                            bad = true;
-                            continue;
-                        }
-                        if (accepted < k) {
-                            dup |= (rep >> j) & 1u;
-                            rep |= 1u << j;
-                            map_b(k + j) = (uint8_t)s;
-                            ++accepted;
-                        }
-                    } else if (accepted < k) {
-                        if (k <= 64) {   // the accepted-source bits in registers (no LDS round trip per row)
-                            const uint64_t bit = 1ull << x;
-                            if (!(acc64 & bit)) {
-                                acc64 |= bit;
-                                map_b(x) = (uint8_t)s;
-                                ++accepted;
-                            }
-                        } else {
-                            uint32_t& m = sam[(x >> 5) * kPrepLanes + tid];
-                            const uint32_t bit = 1u << (x & 31);
-                            if (!(m & bit)) {
-                                m |= bit;
-                                map_b(x) = (uint8_t)s;
-                                ++accepted;
-                            }
-                        }
+            auto step = [&](uint32_t s, uint32_t x) {
+                if (k <= 64) {   // branch-free: the accepted-source bits in a register pair, one predicated store
+                    const bool isrep = x >= k;
+                    const uint32_t j = x - k;
+                    const bool vrep = isrep && j < r;
+                    bad |= isrep && !vrep;
+                    const bool open = accepted < k;
+                    const uint64_t bit = isrep ? 0ull : 1ull << (x & 63);
+                    const bool sys_take = !isrep && open && !(acc64 & bit);
+                    const bool rep_take = vrep && open;
+                    acc64 |= sys_take ? bit : 0ull;
+                    dup |= rep_take && ((rep >> (j & 31)) & 1u);
+                    rep |= rep_take ? 1u << (j & 31) : 0u;
+                    const bool take = sys_take || rep_take;
+                    if (take) map_b(isrep ? k + j : x) = (uint8_t)s;
+                    accepted += take ? 1u : 0u;
+                    return;
+                }
+                if (x >= k) {
+                    const uint32_t j = x - k;
+                    if (j >= r) {
+                        bad = true;
+                        return;
+                    }
+                    if (accepted < k) {
+                        dup |= (rep >> j) & 1u;
+                        rep |= 1u << j;
+                        map_b(k + j) = (uint8_t)s;
+                        ++accepted;
+                    }
+                } else if (accepted < k) {
+                    uint32_t& m = sam[(x >> 5) * kPrepLanes + tid];
+                    const uint32_t bit = 1u << (x & 31);
+                    if (!(m & bit)) {
+                        m |= bit;
+                        map_b(x) = (uint8_t)s;
+                        ++accepted;
                     }
                 }
+            };
+            // the row indices in chunks of 32, the next chunk's loads in
+            // flight while this one is walked (one memory latency per chunk
+            // instead of one per 8 rows)
+            constexpr uint32_t kChunk = 32;
+            uint32_t cur[kChunk], nxt[kChunk];
+#pragma unroll
+            for (uint32_t q = 0; q < kChunk; ++q) cur[q] = q < n ? ridx[q] : 0xFFFFu;
+            for (uint32_t s0 = 0; s0 < n; s0 += kChunk) {
+                const bool more = s0 + kChunk < n;
+#pragma unroll
+                for (uint32_t q = 0; q < kChunk; ++q) nxt[q] = more && s0 + kChunk + q < n ? ridx[s0 + kChunk + q] : 0xFFFFu;
+#pragma unroll
+                for (uint32_t q = 0; q < kChunk; ++q)
+                    if (s0 + q < n) step(s0 + q, cur[q]);
+#pragma unroll
+                for (uint32_t q = 0; q < kChunk; ++q) cur[q] = nxt[q];
             }
             if (k <= 64) {
                 sam[tid] = (uint32_t)acc64;
@@ -1285,22 +1302,25 @@ __global__ void __launch_bounds__(kPrepLanes) k_decode_prepare_lu_lanes(PrepareC
                     const uint32_t l = (uint32_t)(l0 + 64 * 255) % 255u;
                     rec_b(16 * J[j] + J[i]) = sexp[l];
                 };
+                // (static trip counts, guarded by e: the loops unroll fully,
+                // so X, Y, J, S, D0 and D1 stay in registers)
 #pragma unroll
                 for (uint32_t p = 0; p < 16; ++p) {
-                    if (p >= e) break;
-                    int32_t pp0 = 0, pp1 = 0;
+                    if (p < e) {
+                        int32_t pp0 = 0, pp1 = 0;
 #pragma unroll
-                    for (uint32_t q = 0; q < p; ++q) {
-                        const int32_t xx = slog[X[p] ^ X[q]], xy = slog[X[p] ^ Y[q]];
-                        const int32_t yx = slog[Y[p] ^ X[q]], yy = slog[Y[p] ^ Y[q]];
-                        put(p, q, S[q] - xy + pp0 - D0[q]);   // L[p][q]
-                        put(q, p, S[q] - yx + D1[q] - pp1);   // U'[q][p]: log(x_q + y_p) = yx
-                        pp0 += xx - xy;
-                        pp1 += yx - yy;
+                        for (uint32_t q = 0; q < p; ++q) {
+                            const int32_t xx = slog[X[p] ^ X[q]], xy = slog[X[p] ^ Y[q]];
+                            const int32_t yx = slog[Y[p] ^ X[q]], yy = slog[Y[p] ^ Y[q]];
+                            put(p, q, S[q] - xy + pp0 - D0[q]);   // L[p][q]
+                            put(q, p, S[q] - yx + D1[q] - pp1);   // U'[q][p]: log(x_q + y_p) = yx
+                            pp0 += xx - xy;
+                            pp1 += yx - yy;
+                        }
+                        D0[p] = pp0;
+                        D1[p] = pp1;
+                        put(p, p, S[p] + pp1 - pp0);
                     }
-                    D0[p] = pp0;
-                    D1[p] = pp1;
-                    put(p, p, S[p] + pp1 - pp0);
                 }
 #pragma unroll
                 for (uint32_t q = 0; q < 16; ++q)
