@@ -385,6 +385,10 @@ class KernelSpec:
     # separate temps) and selectors issued stage by stage, so that dependent
     # VALU ops sit several instructions apart
     lu_ilp: bool = False
+    # chunked fft dec: split-table reads in flight ahead of the LU products
+    # (1: the next coefficient's; 2: the next two, a third table buffer in
+    # the registers the record pointer and the second address held)
+    lu_ahead: int = 1
     # lab only (chunked dec, strided rows): (n_slots, 16 Q) -- during the
     # backward LU phase, touch every row the NEXT item will read (one dword
     # load per half and row into a dummy register), so that its row loop finds
@@ -1664,7 +1668,19 @@ def lu_layout_chunked(spec) -> dict:
         fp = top + 12
         end = fp + 2
         assert spec.lds_rows or end <= spec.ring0 + 8 * spec.nbuf, "LU registers exceed the ring"
-        return {"cols": cols, "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": fp, "end": end}
+        if spec.lu_ahead == 2:
+            # three buffers (b128 base, b32 register): the third one's b128 over
+            # the record pointer (dead once the record loads are issued) and the
+            # next pair, its b32 in the second address register; one address
+            # register for all (a read takes its address at issue)
+            assert not spec.lds_rows and top % 2 == 0
+            tbx = ((top, top + 4), (top + 6, top + 10), (top + 12, top + 11))
+            end = top + 16
+            assert end <= spec.ring0 + 8 * spec.nbuf, "LU registers exceed the ring"
+            return {"cols": cols, "rank": V_SRCA, "sel": sel, "tb": tb, "ta": (top + 5,) * 3, "fp": fp,
+                    "end": end, "tbx": tbx}
+        return {"cols": cols, "rank": V_SRCA, "sel": sel, "tb": tb, "ta": ta, "fp": fp, "end": end,
+                "tbx": ((tb[0], tb[0] + 4), (tb[1], tb[1] + 4))}
     cols = [spec.ring0 + 4 * q for q in range(2 * spec.nbuf)]
     cols += [spec.map_a + 4 * q for q in range(spec.map_quads)]
     top = spec.map_a + 4 * spec.map_quads
@@ -2116,6 +2132,9 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
     r, acc0 = spec.r, spec.acc0
     lay = lu_layout_chunked(spec)
     cols, rank, sel, tbs, tas, fp = lay["cols"], lay["rank"], lay["sel"], lay["tb"], lay["ta"], lay["fp"]
+    tbx = lay.get("tbx", ((tbs[0], tbs[0] + 4), (tbs[1], tbs[1] + 4)))
+    nbufs = len(tbx)
+    ahead = spec.lu_ahead if spec.fft else 1
     lu = spec.lu
     bmap = spec.fplan.out_block if spec.fft else list(range(r))
 
@@ -2156,18 +2175,19 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
             E(Op("v_andk", (sel + 16 + d, 0x03030303, sel + 16 + d)))
 
     def table_read(u, byte, buf):
-        a, tb = tas[buf], tbs[buf]
+        a = tas[buf]
+        tb, t2 = tbx[buf]
         E(Op("v_perm_s", (a, cols[u] + byte // 4, cols[u] + byte // 4, S_PICK + byte % 4)))
         if spec.tab_stride != 256:   # c << 8 -> c * stride
             E(Op("v_lshr", (a, 8 - (spec.tab_stride.bit_length() - 1), a)))
         E(Op("ds_read_b128", (tb, a, 0)))
-        E(Op("ds_read_b32", (tb + 4, a, 16)))
+        E(Op("ds_read_b32", (t2, a, 16)))
 
     def products(d, buf, p=(R_P, R_P + 1, R_P + 2)):
-        tb = tbs[buf]
+        tb, t2 = tbx[buf]
         E(Op("v_perm", (p[0], tb + 1, tb, sel + d)))
         E(Op("v_perm", (p[1], tb + 3, tb + 2, sel + 8 + d)))
-        E(Op("v_perm", (p[2], tb + 4, tb + 4, sel + 16 + d)))
+        E(Op("v_perm", (p[2], t2, t2, sel + 16 + d)))
 
     def mul_acc(t, buf):
         if spec.lu_ilp:
@@ -2197,14 +2217,15 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
             E(Op("v_xor3", (blk(u, d), R_P, R_P + 1, R_P + 2)))
 
     def column(u, steps, end_label, guard_from):
-        table_read(u, steps[0][1], 0)
+        # table reads run `ahead` coefficients ahead of the products, in
+        # nbufs = ahead + 1 rotating buffers (two LDS reads each)
+        for n in range(min(ahead, len(steps))):
+            table_read(u, steps[n][1], n % nbufs)
         for n, (kind, t) in enumerate(steps):
-            buf = n % 2
-            if n + 1 < len(steps):
-                table_read(u, steps[n + 1][1], 1 - buf)
-                E(Op("s_waitcnt_lgkm_n", (2,)))
-            else:
-                E(Op("s_waitcnt_lgkm_n", (0,)))
+            buf = n % nbufs
+            if n + ahead < len(steps):
+                table_read(u, steps[n + ahead][1], (n + ahead) % nbufs)
+            E(Op("s_waitcnt_lgkm_n", (2 * min(ahead, len(steps) - 1 - n),)))
             if kind == "acc":
                 mul_acc(t, buf)
             else:

@@ -958,6 +958,15 @@ def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs, es, ld
                      lds_rows=lds, **lib4) == 0
 
 
+@pytest.mark.parametrize("k,r,L,G,seed,erase", [(64, 16, 1200, 3, 11, 13), (64, 16, 80, 5, 12, 16),
+                                                (64, 10, 320, 4, 13, None), (32, 16, 64, 5, 14, 0)])
+def test_emulated_fft_fused_decode_lu_ahead(oracle, k, r, L, G, seed, erase):
+    """Split-table reads two coefficients ahead of the LU products (three
+    table buffers, lu_ahead = 2) on the library's options."""
+    assert _dec_case(oracle, k, r, 2, L, G, seed, erase, chunked=True, fft=8, early_stores=True, lu_ilp=True,
+                     bfi_transpose="s64", lu_ahead=2) == 0
+
+
 def test_library_kernels_register_budget():
     """Every generated kernel the library embeds (build_lib.kernel_specs):
     each VGPR it names lies below its descriptor's next_free_vgpr, and every

@@ -37,6 +37,16 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 4p: split-table reads two coefficients ahead of the LU products
+    ("a_warm", dict(LIB_DEC4), ()),
+    ("a_lib", dict(LIB_DEC4), ()),
+    ("a_ahead2", {**LIB_DEC4, "lu_ahead": 2}, ()),
+    ("a_lib_2", dict(LIB_DEC4), ()),
+    ("a_ahead2_2", {**LIB_DEC4, "lu_ahead": 2}, ()),
+    ("a_lib_3", dict(LIB_DEC4), ()),
+    ("a_ahead2_3", {**LIB_DEC4, "lu_ahead": 2}, ()),
+]
+VARIANTS_R04K = [
     # round 4k: absent rows spread over 64 zero rows (lab_zspread) instead of
     # one shared zero row that ~20 % of all row loads hit
     ("z_warm", dict(LIB_DEC4), ()),
