@@ -464,7 +464,10 @@ int qf_adaptive_on_send(qf_adaptive *a, uint64_t id, const uint8_t *data, uint32
  * and statuses[m] (nullable) gets that call's status -- but the steady-state
  * GF(2^8) connections of one context share one upload, one small-batch
  * encode launch per (k, n) class and one download.  A connection may appear
- * more than once (its packets are taken in order).  out_cap must cover the
+ * more than once (its packets are taken in order): a burst of one
+ * connection's packets is one launch too, its overlapping windows read from
+ * a staging copy of the ring's newest k - 1 rows and the burst (Normal mode,
+ * 1,200-B packets: 18.5 us per packet alone, 1.2 us at 256 per call).  out_cap must cover the
  * sum of qf_adaptive_max_send_packets; out_stride / coeff_stride follow
  * qf_adaptive_on_send.  An argument error fails the whole call before any
  * state changes (QF_EINVAL / QF_ETOOSMALL); otherwise QF_OK. */
