@@ -65,7 +65,9 @@ int qf_cauchy_coeffs(uint32_t k, uint32_t r, uint8_t *out_rxk);
  * ------------------------------------------------------------------------- */
 typedef struct qf_ctx qf_ctx;
 /* device: HIP device ordinal.  stream: hipStream_t to enqueue on (NULL = the
- * context creates its own non-blocking stream). */
+ * context creates its own non-blocking stream; QF_STREAM_NULL = the device's
+ * null stream, ordered with other work on it, e.g. torch's default stream). */
+#define QF_STREAM_NULL ((void *)1)
 int qf_ctx_create(int device, void *stream, qf_ctx **out);
 int qf_ctx_destroy(qf_ctx *ctx);
 int qf_ctx_set_stream(qf_ctx *ctx, void *stream);
@@ -143,6 +145,10 @@ enum {
     QF_OPT_PREPARE_LANES,        /* 1: the fused decode's acceptance pass runs one generation per lane
                                     (k_decode_prepare_lu_lanes); 0: one per wave [QF_PREPARE_LANES;
                                     default 1] */
+    QF_OPT_ENCODE_MERGED,        /* 1: the encode passes of a code with more repairs than one kernel
+                                    holds (C5 r > 22) run in ONE dispatch, a workgroup's waves
+                                    running the passes on the same item (each source row read from
+                                    HBM once); 0: one launch per pass [QF_ENCODE_MERGED; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

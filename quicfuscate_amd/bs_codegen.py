@@ -32,6 +32,7 @@ and every register read against outstanding loads (a missing vmcnt wait).
 from __future__ import annotations
 
 import dataclasses
+import functools
 from typing import Optional
 
 import numpy as np
@@ -432,6 +433,9 @@ class KernelSpec:
     # fft: plane pairs shared by >= 3 output rows of a constant multiply are
     # XORed once into the transpose scratch registers
     fft_cse: bool = True
+    # enc: this pass is one wave of a MergedSpec dispatch (item = workgroup,
+    # the workgroup's waves run the code's passes on the same item)
+    merged: bool = False
 
     @property
     def ahead(self) -> int:
@@ -449,6 +453,9 @@ class KernelSpec:
         if self.fft_basis:
             from . import lch_fft
             return lch_fft.plan(self.k, self.r, self.fft, basis=self.fft_basis[0], beta_out=self.fft_basis[1])
+        if self.k & (self.k - 1) or self.rt != self.r or self.j0:
+            # a pass of a code the plain plan does not cover (lch_fft.hybrid_plan)
+            return _hybrid_plan(self.k, self.rt, self.j0, self.r, self.fft)
         return _fft_plan(self.k, self.r, self.fft)
 
     @property
@@ -767,6 +774,12 @@ def _fft_plan(k: int, r: int, ch: int):
     return lch_fft.best_plan(k, r, ch)
 
 
+@functools.lru_cache(maxsize=None)
+def _hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int):
+    from . import lch_fft
+    return lch_fft.hybrid_plan(k, rt, j0, r, ch)
+
+
 def _macc_cost(c: int, n_tmp: int = 0) -> int:
     if c == 0:
         return 0
@@ -887,11 +900,26 @@ def _fft_stream(E, ops: list, spec: KernelSpec, load_row, wait_row, acc_block, n
     groups = []      # deferred end-of-chunk work, one group per following row
     for n in range(min(pd, n_rows)):
         load_row(n, slot(n))
+    kA = getattr(P, "kA", 0) or k        # plan rows through the FFT; rows kA .. k - 1 enter directly
+    direct = getattr(P, "direct", {})
+
+    def fold_direct(n):
+        for t, c in direct[n]:
+            _macc(E, acc_block(t), slot(n), c, init=t not in inited, tmp=tmp)
+            inited.add(t)
+
     for n in range(k):
         if n + pd < n_rows:
             load_row(n + pd, slot(n + pd))
         wait_row(n)
         ops.extend(_transpose_ops(slot(n), spec.bfi_transpose, spec.vmask))
+        if n >= kA:
+            work = [(0, lambda n=n: fold_direct(n))]
+            if groups:
+                work = [(0, e) for e in groups.pop(0)] + work
+            for _, emit in work:
+                emit()
+            continue
         hc, m = divmod(n, ch)
         base = hc * ch
         work = []
@@ -944,6 +972,8 @@ def _prologue(E, spec: KernelSpec):
         E(Op("s_load_karg_x2", (SW_BOUND, KERNARG_BYTES)))   # kernarg words 24..25
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
+    if spec.merged:
+        E(Op("label", (".Lhead_end",)))   # _generate_merged: the passes' common head ends here
     if spec.mode == "dec":
         # every wave copies the whole 8 KB split-table set into LDS (no
         # barrier: waves of a workgroup write identical bytes)
@@ -973,7 +1003,10 @@ def _prologue(E, spec: KernelSpec):
     if spec.xcd_remap:
         # w' = base(w % 8) + w / 8 with XCD x owning c_x = q + (x < rem)
         # consecutive workgroups, q = nwg / 8, rem = nwg % 8 (a bijection)
-        E(Op("s_lshrk", (46, 18, 2)))        # nwg = total waves / 4
+        if spec.merged:
+            E(Op("s_mov", (46, 18)))         # nwg = the item stride
+        else:
+            E(Op("s_lshrk", (46, 18, 2)))    # nwg = total waves / 4
         E(Op("s_andk", (47, 2, 7)))          # x
         E(Op("s_lshrk", (30, 46, 3)))        # q
         E(Op("s_mul", (30, 47, 30)))         # x * q
@@ -982,10 +1015,15 @@ def _prologue(E, spec: KernelSpec):
         E(Op("s_add", (30, 30, 46)))
         E(Op("s_lshrk", (46, 2, 3)))         # w / 8
         E(Op("s_add", (30, 30, 46)))
-        E(Op("s_lshl", (30, 30, 2)))         # w' * 4
+        if not spec.merged:
+            E(Op("s_lshl", (30, 30, 2)))     # w' * 4
+    elif spec.merged:
+        E(Op("s_mov", (30, 2)))
     else:
         E(Op("s_lshl", (30, 2, 2)))          # s30 = workgroup_id * 4   (s2 = workgroup id)
-    if spec.ksplit > 1:
+    if spec.merged:
+        E(Op("s_mov", (28, 30)))             # s28 = the workgroup's item (every pass)
+    elif spec.ksplit > 1:
         E(Op("s_lshrk", (28, 30, 2)))        # s28 = the workgroup's item (all its waves)
     else:
         E(Op("s_add", (28, 29, 30)))         # s28 = item = global wave id
@@ -1084,7 +1122,10 @@ def valu_per_item(spec: KernelSpec) -> int:
     issues: the ops from the item-loop head to its back-edge.  Exact for the
     encode kernels (straight-line bodies); an upper bound where dec-mode guards
     skip blocks.  bench.py prices the VALU roof of a kernel from it when no SQ
-    counter pass of that workload exists (C5 sliding windows)."""
+    counter pass of that workload exists (C5 sliding windows).  A merged
+    dispatch: the sum over its passes (one wave each per item)."""
+    if isinstance(spec, MergedSpec):
+        return sum(valu_per_item(p) for p in spec.passes)
     ops = generate(spec)
     start = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Litem")
     n = 0
@@ -1097,6 +1138,8 @@ def valu_per_item(spec: KernelSpec) -> int:
 
 
 def generate(spec: KernelSpec) -> list[Op]:
+    if isinstance(spec, MergedSpec):
+        return _generate_merged(spec)
     if spec.mode == "cmb":
         return _generate_cmb(spec)
     if spec.mode == "enc":
@@ -1106,6 +1149,111 @@ def generate(spec: KernelSpec) -> list[Op]:
     if spec.mode == "dec" and spec.chunked:
         return _generate_dec_chunked(spec)
     return _generate_syn(spec)
+
+
+@dataclasses.dataclass(frozen=True)
+class MergedSpec:
+    """Every encode pass of a code with more repairs than one kernel holds, in
+    ONE dispatch: a workgroup of len(passes) waves per item, wave p running
+    pass p over the item's 128 units.  The passes read the same source rows in
+    the same order at about the same time, so all but the first read of each
+    row hit the CU's L1 / the XCD's L2 instead of HBM (separate pass launches
+    re-read every source row from HBM once per pass)."""
+    passes: tuple
+
+    mode = "enc"
+    chunked = False
+    ksplit = 1
+    j0 = 0
+    map_stride = 0
+    far = True
+
+    @property
+    def k(self) -> int:
+        return self.passes[0].k
+
+    @property
+    def rt(self) -> int:
+        return self.passes[0].rt
+
+    @property
+    def r(self) -> int:
+        return self.rt
+
+    @property
+    def pd(self) -> int:
+        return self.passes[0].pd
+
+    @property
+    def fft(self) -> int:
+        return self.passes[0].fft
+
+    @property
+    def waves(self) -> int:
+        return len(self.passes)
+
+    @property
+    def name(self) -> str:
+        return f"qf_cauchy_bsm{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
+
+    @property
+    def next_free_vgpr(self) -> int:
+        return max(p.next_free_vgpr for p in self.passes)
+
+    @property
+    def next_free_sgpr(self) -> int:
+        return max(p.next_free_sgpr for p in self.passes)
+
+    @property
+    def kernarg_bytes(self) -> int:
+        return self.passes[0].kernarg_bytes
+
+    @property
+    def lds_bytes(self) -> int:
+        return max(p.lds_bytes for p in self.passes)
+
+
+def merged_spec(passes) -> MergedSpec:
+    passes = tuple(dataclasses.replace(p, merged=True) for p in passes)
+    assert 1 < len(passes) <= 4 and all(p.mode == "enc" and p.ksplit == 1 and not p.lds_rows for p in passes)
+    assert all(p.k == passes[0].k and p.rt == passes[0].rt for p in passes)
+    assert sorted((p.j0, p.j0 + p.r) for p in passes) == [(p.j0, p.j0 + p.r) for p in passes]
+    assert passes[0].j0 == 0 and passes[-1].j0 + passes[-1].r == passes[0].rt
+    return MergedSpec(passes)
+
+
+def _generate_merged(ms: MergedSpec) -> list[Op]:
+    """The common head (kernargs, lane / wave ids), a branch on the wave's
+    index in its workgroup (s29) to its pass, and each pass's body (its own
+    item loop, labels and far-jump ids made unique).  A pass's body first
+    moves the repair base s[6:7] to its first row: + j0 * repair row stride."""
+    out: list[Op] = []
+    E = out.append
+    bodies = []
+    for p, sp in enumerate(ms.passes):
+        ops = generate(sp)
+        cut = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Lhead_end")
+        if p == 0:
+            out.extend(ops[:cut])
+        bodies.append(ops[cut + 1:])
+    for p in range(1, ms.waves):
+        E(Op("s_cmp_lg_k_br", (29, p, f".Lnpass{p}")))
+        E(Op("s_far_jump", (f".Lpass{p}", 900 + p)))
+        E(Op("label", (f".Lnpass{p}",)))
+    for p, body in enumerate(bodies):
+        E(Op("label", (f".Lpass{p}",)))
+        j0 = ms.passes[p].j0
+        if j0:
+            E(Op("s_mul_k", (46, 11, j0)))
+            E(Op("s_add", (6, 6, 46)))
+            E(Op("s_addck", (7, 7, 0)))
+        for op in body:
+            args = tuple(a.replace(".L", f".LP{p}", 1) if isinstance(a, str) and a.startswith(".L") else a
+                         for a in op.args)
+            if op.name == "s_far_jump":
+                args = (args[0], args[1] + 1000 * (p + 1))
+            E(Op(op.name, args))
+    return out
 
 
 def _store_pair(E, acc: int, ma: int, mb: int, pol: str = ""):
@@ -1141,7 +1289,7 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         E(Op("v_add64_s", (V_SRCB, V_SRCB, step)))
 
     if spec.fft:
-        assert ks == 1 and spec.rt == r and spec.j0 == 0
+        assert ks == 1
         cur = [0]      # source row the row pointers address
         S = spec.lds_rows
         v_ldsa = spec.next_free_vgpr - 1 if S else None

@@ -40,6 +40,10 @@ BS_PASS = 22   # repairs per pass: 8 r accumulator VGPRs, r <= 22 fits 256 at pd
 # additive-FFT encode ('E', lch_fft.py): power-of-two k where the plan costs
 # fewer plane ops than one coefficient block per repair
 BS_FFT = [(64, 16), (64, 10), (32, 16), (16, 16)]
+# additive-FFT encode passes of the C5 codes with more than 22 repairs
+# (lch_fft.hybrid_plan: one pass per coset of 16 repair points, sources
+# [0, 2^a) through the FFT, the rest folded in directly), merged ('N')
+BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
@@ -147,6 +151,7 @@ def kernel_specs() -> list:
     """Every generated kernel the library embeds (bs_codegen.KernelSpec), in
     table order."""
     from . import bs_codegen as bs
+    from . import lch_fft
 
     specs = [bs.KernelSpec(k, r, BS_PD, mode) for mode in ("enc", "syn", "dec") for (k, r) in BS_CONFIGS]
     # fused decode over the lane-chunk layout (one generation per lane; the
@@ -187,6 +192,24 @@ def kernel_specs() -> list:
     specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="",
                             early_stores=True, lu_ilp=True, bfi_transpose="s64")
               for (k, r) in BS_FFT]
+    # every pass of a C5 code in one dispatch ('M' plain, 'N' additive-FFT
+    # passes; QF_ENCODE_MERGED): one wave per pass on the workgroup's item, so
+    # the source rows come from HBM once.  Plain passes: 4 waves where 3 would
+    # leave a quarter of a CU's 8 wave slots (2 per SIMD at > 128 VGPRs) empty
+    for k, rt in BS_ENC_ONLY:
+        npass = -(-rt // BS_PASS)
+        if npass == 1:
+            continue
+        npass += npass == 3
+        cuts = [rt * p // npass for p in range(npass + 1)]
+        specs.append(bs.merged_spec([bs.KernelSpec(k, cuts[p + 1] - cuts[p], BS_PD, "enc", r_total=rt, j0=cuts[p])
+                                     for p in range(npass)]))
+    # (tools/gpu_r04_c5fft.sh, profiles/r04v_c5_passes.json: 1,508 -> 1,962 GiB/s
+    # at (160, 48), 1,347 -> 1,552 at (196, 59), 2,371 -> 2,600 at (128, 39);
+    # (128, 20) keeps its single plain pass: 4,568 against 3,806 merged FFT)
+    for k, rt in BS_FFT_PASSES:
+        specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
+                                     for j0, rp in lch_fft.coset_passes(k, rt)]))
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
     return specs
@@ -212,11 +235,12 @@ def _bs_kernels(build_dir: Path) -> Path:
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         mode = ("C" if spec.fft else "k" if spec.ksplit > 1 else "c") if spec.chunked else \
+            ("N" if spec.fft else "M") if isinstance(spec, bs.MergedSpec) else \
             "E" if spec.fft else \
             ("f" if spec.mode == "enc" and spec.ksplit > 1 else
              {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode])
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
-                       f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n})}},")
+                       f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n}), {getattr(spec, 'waves', 4)}u}},")
     # the loader caches one module per table entry (qf_bs.h BsCache::kMax)
     kmax = int(re.search(r"kMax = (\d+)", (CSRC / "qf_bs.h").read_text()).group(1))
     if len(specs) > kmax:

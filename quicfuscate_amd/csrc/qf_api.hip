@@ -175,6 +175,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* WIEDEMANN_PROJ */ {"QF_WIEDEMANN_PROJ", 1, 0, 1, false},
     /* GF16_FFT_BS */ {"QF_GF16_FFT_BS", 1, 0, 3, false},
     /* PREPARE_LANES */ {"QF_PREPARE_LANES", 1, 0, 1, false},
+    /* ENCODE_MERGED */ {"QF_ENCODE_MERGED", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }
@@ -1077,7 +1078,9 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
     init_opts(c);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
-    if (stream) {
+    if (stream == QF_STREAM_NULL) {
+        c->stream = nullptr;   // the null stream (not owned)
+    } else if (stream) {
         c->stream = reinterpret_cast<hipStream_t>(stream);
     } else {
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1204,7 +1207,9 @@ int qf_ctx_set_stream(qf_ctx* ctx, void* stream) {
         hipStreamDestroy(ctx->stream);
         ctx->own_stream = false;
     }
-    if (stream) {
+    if (stream == QF_STREAM_NULL) {
+        ctx->stream = nullptr;
+    } else if (stream) {
         ctx->stream = reinterpret_cast<hipStream_t>(stream);
     } else {
         QF_CHECK_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));

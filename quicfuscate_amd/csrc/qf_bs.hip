@@ -19,11 +19,13 @@ struct QfBsEntry {
     uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
     char mode;  // 'e' encode, 'E' additive-FFT encode, 'C' additive-FFT chunked decode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
                 // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves,
-                // 'f' the encode (passes of C5 codes) with an item's sources split the same way
+                // 'f' the encode (passes of C5 codes) with an item's sources split the same way,
+                // 'M' / 'N' every encode pass of a code in one dispatch (plain / additive-FFT passes)
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
     size_t size;
+    uint32_t waves;  // waves per workgroup ('M' / 'N': one per pass, each on the workgroup's item)
 };
 #include "qf_bs_blobs.inc"
 
@@ -84,7 +86,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // the combine never stores); the lane-chunk decode ('c': the lane holding
     // the last unit stores it bytewise); never the item-layout decode ('d')
     const bool chunked = e->mode == 'c' || e->mode == 'k' || e->mode == 'C';
-    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E';
+    const bool merged = e->mode == 'M' || e->mode == 'N';
+    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E' || merged;
     if ((L % 16 && (e->mode == 'd' || (enc && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
@@ -106,8 +109,9 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     uint32_t magic, shift;
     magic_for(Lv, &magic, &shift);
     const uint32_t n_items = (uint32_t)(chunked ? (total + 63) / 64 : (total + 127) / 128);
-    // 'k' / 'f': one workgroup per item
-    uint32_t blocks = (e->mode == 'k' || e->mode == 'f') ? n_items : (n_items + 3) / 4;
+    // 'k' / 'f' / merged passes: one workgroup per item
+    const bool wg_item = e->mode == 'k' || e->mode == 'f' || merged;
+    uint32_t blocks = wg_item ? n_items : (n_items + 3) / 4;
     if (blocks == 0) return hipSuccess;
     // persistent grids (the item loop strides by the grid's wave count):
     // QF_ENC_BLOCKS_PER_CU / QF_DEC_BLOCKS_PER_CU cap the grid at that many
@@ -115,7 +119,9 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // can be resident on every SIMD at once
     {
         const int c = (int)cache.get(enc ? QF_OPT_ENC_BLOCKS_PER_CU : QF_OPT_DEC_BLOCKS_PER_CU);
-        if (c > 0 && num_cus > 0 && blocks > (uint32_t)(c * num_cus)) blocks = (uint32_t)(c * num_cus);
+        // (a block of the merged kernels is one item's passes: up to 4 per CU fill it)
+        const uint32_t cap = (uint32_t)(c * num_cus) * (merged ? 4u / e->waves : 1u);
+        if (c > 0 && num_cus > 0 && blocks > cap) blocks = cap;
     }
     uint32_t a[32] = {};
     a[0] = (uint32_t)(uintptr_t)src;
@@ -132,7 +138,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[11] = magic;
     a[12] = shift;
     a[13] = n_items;
-    a[14] = blocks * 4;
+    a[14] = merged ? blocks : blocks * 4;   // item stride: workgroups (merged) or waves
     a[15] = s19;
     if (enc) {
         // byte masks of the last unit's dwords (bs_codegen.tail_masks)
@@ -167,7 +173,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     }
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+    return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 64 * e->waves, 1, 1, 0, st, nullptr, cfg);
 }
 
 uint32_t bs_padded_units(uint32_t L) { return ((L + 15) / 16 + 7) / 8 * 8; }
@@ -199,8 +205,11 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     char mode = 'e';
     {
         const uint64_t items = ((uint64_t)G * Lv + 127) / 128;
+        const bool fft = cache.get(QF_OPT_FFT_KERNELS);
         if (cache.get(QF_OPT_ENCODE_KSPLIT) && find('f', k, r) && num_cus > 0 && items <= (uint64_t)num_cus) mode = 'f';
-        else if (cache.get(QF_OPT_FFT_KERNELS) && find('E', k, r)) mode = 'E';
+        else if (cache.get(QF_OPT_ENCODE_MERGED) && fft && find('N', k, r)) mode = 'N';
+        else if (cache.get(QF_OPT_ENCODE_MERGED) && find('M', k, r)) mode = 'M';
+        else if (fft && find('E', k, r)) mode = 'E';
     }
     // one launch per pass of repairs (codes with more repairs than a kernel
     // holds): pass j0 writes repair rows j0 .. j0 + r_pass - 1

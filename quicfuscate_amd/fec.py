@@ -78,6 +78,9 @@ def cauchy_coefficients(k: int, r: int) -> bytes:
 # ---------------------------------------------------------------------------
 # Device context
 # ---------------------------------------------------------------------------
+QF_STREAM_NULL = 1   # qf_fec.h: the device's null stream
+
+
 class Context:
     """A qf_ctx bound to a device and a HIP stream (default: torch's current)."""
 
@@ -89,6 +92,12 @@ class Context:
         self.device = torch.cuda.current_device() if device is None else int(device)
         if stream is None:
             stream = torch.cuda.current_stream(self.device).cuda_stream
+        if not stream:
+            # torch's default stream is the null stream: QF_STREAM_NULL binds
+            # the library to it, so its work is ordered with torch's (a NULL
+            # stream makes qf_ctx_create allocate its own non-blocking stream,
+            # which a torch fill / randint on the default stream does not wait for)
+            stream = QF_STREAM_NULL
         h = ctypes.c_void_p()
         check(L._lib().qf_ctx_create(self.device, ctypes.c_void_p(stream), ctypes.byref(h)), "ctx")
         self.handle = h

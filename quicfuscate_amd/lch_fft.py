@@ -252,3 +252,167 @@ def best_plan(k: int, r: int, ch: int = 8) -> Plan:
     if b is None:
         return plan(k, r, ch)
     return plan(k, r, ch, basis=b[0], beta_out=b[1])
+
+
+# --------------------------------------------------------------------------
+# Passes of codes the plain plan does not cover: k not a power of two, or
+# repair points beyond the coset k + V (r > k or a pass j0 > 0).  The
+# reference's points are x_j = k + j (integer sum, decoder.rs:280-298).  A
+# pass takes the repairs whose points share one aligned coset beta + V_b
+# (beta = x & ~(R - 1)); sources [0, kA), kA = 2^a the largest power of two
+# <= k, go through the additive FFT evaluated on that coset (kappa and the
+# fold factors taken at beta, which lies outside V_a since x >= k >= kA); the
+# rows [kA, k) enter directly: each one's Cauchy column over the pass,
+# pulled back through the final butterflies (an invertible linear map), is a
+# set of accumulator constants like a chunk output's.
+# --------------------------------------------------------------------------
+def coset_passes(k: int, rt: int, R: int = 16) -> list[tuple[int, int]]:
+    """(j0, r) of every pass: repairs whose points k + j share x // R."""
+    out = []
+    j = 0
+    while j < rt:
+        x = k + j
+        end = min(rt, (x // R + 1) * R - k)
+        out.append((j, end - j))
+        j = end
+    return out
+
+
+@dataclasses.dataclass
+class HybridPlan(Plan):
+    kA: int = 0                   # rows through the FFT (plan rows 0 .. kA - 1)
+    direct: dict = dataclasses.field(default_factory=dict)   # plan row n >= kA -> [(t, c)]
+
+    def cost(self) -> int:
+        n = 0
+        for bf in self.chunk_bfly:
+            n += sum(8 + macc_cost(s) for _, _, s in bf)
+        for hc in range(self.kA // self.ch):
+            for m in range(self.ch):
+                n += sum(macc_cost(c) for _, c in self.acc[(hc, m)])
+        for lst in self.direct.values():
+            n += sum(macc_cost(c) for _, c in lst)
+        n += sum(8 + macc_cost(s) for _, _, s in self.final_bfly)
+        return n
+
+    def evaluate(self, xs: list[int]) -> list[int]:
+        e = [0] * self.R
+        for hc in range(self.kA // self.ch):
+            y = [xs[self.order[hc * self.ch + m]] for m in range(self.ch)]
+            for i, j, s in self.chunk_bfly[hc]:
+                y[j] ^= y[i]
+                y[i] ^= mul(s, y[j])
+            for m in range(self.ch):
+                for t, c in self.acc[(hc, m)]:
+                    e[t] ^= mul(c, y[m])
+        for n, lst in self.direct.items():
+            for t, c in lst:
+                e[t] ^= mul(c, xs[self.order[n]])
+        for i, j, s in self.final_bfly:
+            e[i] ^= mul(s, e[j])
+            e[j] ^= e[i]
+        return [e[self.out_block[j]] for j in range(self.r)]
+
+
+def hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int = 8, R: int = 16, check: int = 8) -> HybridPlan:
+    """The pass j0 .. j0 + r - 1 of the (k, rt) code (module note above)."""
+    a = k.bit_length() - 1
+    kA = 1 << a
+    b, c = _log2(R), _log2(ch)
+    x0 = k + j0
+    beta = x0 & ~(R - 1)
+    if not (1 <= r and j0 + r <= rt and k + rt <= 256 and (k + j0 + r - 1) & ~(R - 1) == beta and
+            kA >= R and kA % ch == 0 and beta >= kA and c <= b):
+        raise ValueError(f"no hybrid additive-FFT pass for k={k}, rt={rt}, j0={j0}, r={r}")
+    basis = tuple(1 << q for q in range(8))
+    order = list(range(k))                      # canonical basis: span_point(n) = n
+
+    chunk_bfly = []
+    for hc in range(kA // ch):
+        bf = []
+        for q in range(c):
+            h = 1 << q
+            for o in range(0, ch, 2 * h):
+                s = xhat(q, hc * ch + o, basis)
+                bf += [(o + i, o + i + h, s) for i in range(h)]
+        chunk_bfly.append(bf)
+
+    delta = 1
+    for u in range(1, kA):
+        delta = mul(delta, u)
+    kappa = mul(delta, inv(_subspace_poly(a, beta, basis)))
+    fold = [1] * kA
+    for i in range(kA):
+        for q in range(b, a):
+            if i >> q & 1:
+                fold[i] = mul(fold[i], xhat(q, beta, basis))
+
+    def rest(y: list[int]) -> list[int]:
+        y = list(y)
+        for q in range(c, a):
+            h = 1 << q
+            for o in range(0, kA, 2 * h):
+                s = xhat(q, o, basis)
+                for i in range(o, o + h):
+                    y[i + h] ^= y[i]
+                    y[i] ^= mul(s, y[i + h])
+        d = [0] * R
+        for i in range(kA):
+            d[i % R] ^= mul(mul(y[i], fold[i]), kappa)
+        for q in reversed(range(c, b)):
+            h = 1 << q
+            for o in range(0, R, 2 * h):
+                s = xhat(q, beta ^ o, basis)
+                for i in range(o, o + h):
+                    d[i] ^= mul(s, d[i + h])
+                    d[i + h] ^= d[i]
+        return d
+
+    acc = {}
+    for hc in range(kA // ch):
+        for m in range(ch):
+            y = [0] * kA
+            y[hc * ch + m] = 1
+            d = rest(y)
+            acc[(hc, m)] = [(t, d[t]) for t in range(R) if d[t]]
+
+    final_bfly = []
+    for blk in range(0, R, ch):
+        for q in reversed(range(c)):
+            h = 1 << q
+            for o in range(blk, blk + ch, 2 * h):
+                s = xhat(q, beta ^ o, basis)
+                final_bfly += [(o + i, o + i + h, s) for i in range(h)]
+    out_block = [0] * r
+    for t in range(R):
+        j = (beta ^ t) - x0
+        if 0 <= j < r:
+            out_block[j] = t
+
+    def final_inverse(v: list[int]) -> list[int]:
+        v = list(v)
+        for i, j, s in reversed(final_bfly):     # forward: v_i ^= s v_j; v_j ^= v_i
+            v[j] ^= v[i]
+            v[i] ^= mul(s, v[j])
+        return v
+
+    direct = {}
+    for i in range(kA, k):
+        w = [0] * R
+        for j in range(r):
+            w[out_block[j]] = inv(i ^ (x0 + j))
+        d = final_inverse(w)
+        direct[i] = [(t, d[t]) for t in range(R) if d[t]]
+
+    p = HybridPlan(k, r, ch, R, basis, beta, order, chunk_bfly, acc, final_bfly, out_block, kA=kA, direct=direct)
+    rng = random.Random(0x51464543 + j0)
+    C = [[inv(i ^ (x0 + j)) for i in range(k)] for j in range(r)]
+    for _ in range(check):
+        xs = [rng.randrange(256) for _ in range(k)]
+        ref = [0] * r
+        for j in range(r):
+            for i in range(k):
+                ref[j] ^= mul(C[j][i], xs[i])
+        if p.evaluate(xs) != ref:
+            raise AssertionError(f"hybrid additive-FFT pass disagrees with the Cauchy matrix (k={k}, j0={j0})")
+    return p

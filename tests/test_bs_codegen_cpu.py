@@ -958,6 +958,88 @@ def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs, es, ld
                      lds_rows=lds, **lib4) == 0
 
 
+@pytest.mark.parametrize("k,rt,L,G", [(24, 10, 200, 3), (20, 20, 72, 2), (48, 21, 64, 2), (160, 48, 40, 1)])
+def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
+    """Codes the plain additive-FFT plan does not cover (k not a power of
+    two, repairs past the first coset): one kernel per coset pass
+    (lch_fft.coset_passes), sources [0, 2^a) through the FFT at the pass's
+    coset, the rest folded in directly; every pass writes its own repairs."""
+    from quicfuscate_amd import lch_fft
+
+    Lv = bs.padded_units(L)
+    rng = np.random.default_rng(k * 13 + rt + L)
+    srs = (L + 15) // 16 * 16 + 16 * (k % 2)
+    sgs = k * srs
+    drs = 16 * Lv + 64
+    dgs = rt * drs
+    src = rng.integers(0, 256, G * sgs + 64, dtype=np.uint8)
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    SRC, DST = 0x10000000, 0x40000000
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    waves = (items + 3) // 4
+    for j0, rp in lch_fft.coset_passes(k, rt):
+        spec = bs.KernelSpec(k, rp, 2, r_total=rt, j0=j0, fft=8)
+        emu = bs.Emulator(bs.generate(spec))
+        emu.add_buffer(SRC, src)
+        emu.add_buffer(DST, dst)
+        ka = bs.kernargs(SRC, DST + j0 * drs, sgs, dgs, srs, drs, L, G, waves * 4, Lv=Lv, zero_tail=True)
+        for wg in range(waves):
+            for w in range(4):
+                emu.run_wave(ka, wg, w)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, rt)
+        for j in range(rt):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            assert (dst[off + L: off + 16 * Lv] == 0).all(), (g, j)
+            assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
+
+
+@pytest.mark.parametrize("k,rt,L,G,fft,blocks", [(24, 10, 200, 3, 8, 0), (20, 20, 72, 2, 0, 0), (48, 21, 4000, 2, 8, 3),
+                                                  (40, 30, 40, 1, 0, 0), (160, 48, 40, 1, 8, 0)])
+def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks):
+    """All passes of a code in one dispatch (MergedSpec): wave p of each
+    workgroup runs pass p on the workgroup's item; a persistent grid (fewer
+    workgroups than items, item stride = workgroups) included."""
+    from quicfuscate_amd import lch_fft
+
+    Lv = bs.padded_units(L)
+    rng = np.random.default_rng(k * 17 + rt + L)
+    srs = (L + 15) // 16 * 16 + 16 * (k % 2)
+    sgs = k * srs
+    drs = 16 * Lv + 64
+    dgs = rt * drs
+    src = rng.integers(0, 256, G * sgs + 64, dtype=np.uint8)
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    if fft:
+        passes = [bs.KernelSpec(k, rp, 2, r_total=rt, j0=j0, fft=fft) for j0, rp in lch_fft.coset_passes(k, rt)]
+    else:
+        n = -(-rt // 12)
+        cuts = [rt * p // n for p in range(n + 1)]
+        passes = [bs.KernelSpec(k, cuts[p + 1] - cuts[p], 2, r_total=rt, j0=cuts[p]) for p in range(n)]
+    ms = bs.merged_spec(passes)
+    assert ms.waves == len(passes) > 1
+    emu = bs.Emulator(bs.generate(ms))
+    SRC, DST = 0x10000000, 0x40000000
+    emu.add_buffer(SRC, src)
+    emu.add_buffer(DST, dst)
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    wgs = blocks or items
+    ka = bs.kernargs(SRC, DST, sgs, dgs, srs, drs, L, G, wgs, Lv=Lv, zero_tail=True)
+    for wg in range(wgs):
+        for w in range(ms.waves):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, rt)
+        for j in range(rt):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            assert (dst[off + L: off + 16 * Lv] == 0).all(), (g, j)
+            assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
+
+
 @pytest.mark.parametrize("k,r,L,G,seed,erase", [(64, 16, 1200, 3, 11, 13), (64, 16, 80, 5, 12, 16),
                                                 (64, 10, 320, 4, 13, None), (32, 16, 64, 5, 14, 0)])
 def test_emulated_fft_fused_decode_lu_ahead(oracle, k, r, L, G, seed, erase):

@@ -233,6 +233,53 @@ def test_bit_sliced_partial_last_unit_random_lengths(qf, oracle, gpu_ctx, k, r):
                 assert (rep[off + tail: off + rrs] == 0xA5).all(), (L, g, j)
 
 
+@pytest.mark.parametrize("k,r", [(128, 20), (128, 39), (160, 48), (196, 59)])
+def test_c5_passes_large_batch(qf, oracle, gpu_ctx, k, r):
+    """C5 codes at jumbo rows with more items than CUs (the multi-item
+    kernels, not the row-split 'f' ones): one launch per pass, every pass in
+    one dispatch (QF_ENCODE_MERGED) and the additive-FFT coset passes
+    (lch_fft.hybrid_plan) give the same repairs, block and sliding layouts;
+    generations of the block batch against the oracle."""
+    import torch
+
+    L, RS = 9000, 9008
+    drs = 9088
+    G = 72                       # 72 x 568 units / 128 = 320 items
+    gen = torch.Generator(device="cuda").manual_seed(k + r)
+    src = torch.randint(0, 256, ((G + 1) * k * RS,), dtype=torch.uint8, device="cuda", generator=gen)
+    out = {}
+    for merged in (0, 1):
+        for fft in (0, 1):
+            qf.set_default_options(encode_merged=merged, fft_kernels=fft)
+            for mode, gs in (("block", k * RS), ("sliding", RS)):
+                rep = torch.full((G * r * drs,), 0xA5, dtype=torch.uint8, device="cuda")
+                qf.encode_batch(src, rep, k, r, L, src_row_stride=RS, src_gen_stride=gs, rep_row_stride=drs,
+                                rep_gen_stride=r * drs, G=G, zero_tail=True, ctx=gpu_ctx)
+                gpu_ctx.sync()
+                out[(merged, fft, mode)] = rep.view(G, r, drs)
+    base = out[(0, 0, "block")].cpu().numpy()
+    s = src.cpu().numpy()
+    for key, rep in out.items():
+        if not torch.equal(rep, out[(0, 0, key[2])]):
+            d = np.argwhere(rep.cpu().numpy() != out[(0, 0, key[2])].cpu().numpy())
+            g = int(d[0, 0])
+            msg = f"{key}: {len(d)} bytes differ, gens {sorted(set(d[:, 0].tolist()))[:10]}, " \
+                  f"rows {sorted(set(d[:, 1].tolist()))[:20]}, bytes {d[:3, 2].tolist()}"
+            if key[2] == "block":
+                w = oracle.encode(s[g * k * RS:(g + 1) * k * RS].reshape(k, RS)[:, :L], r)
+                msg += f"; gen {g}: variant == oracle {bool((rep[g, :, :L].cpu().numpy() == w).all())}, " \
+                       f"base == oracle {bool((base[g, :, :L] == w).all())}"
+            raise AssertionError(msg)
+    assert (base[:, :, L:] == 0).all()
+    for g in (0, 37, G - 1):
+        rows = s[g * k * RS:(g + 1) * k * RS].reshape(k, RS)[:, :L]
+        assert (base[g, :, :L] == oracle.encode(rows, r)).all(), g
+    sl = out[(0, 0, "sliding")].cpu().numpy()
+    for g in (1, G - 1):
+        rows = s[g * RS:(g + k) * RS].reshape(k, RS)[:, :L]
+        assert (sl[g, :, :L] == oracle.encode(rows, r)).all(), g
+
+
 def test_gf_mul_slice_large_table_kernel(qf, oracle, gpu_ctx):
     """Slices from 16 MiB use the 64 KiB product-table kernel: every byte
     (and the n % 16 tail) equals gf_mul_table (gf_tables.rs:47-57)."""
