@@ -1161,12 +1161,18 @@ class MergedSpec:
     re-read every source row from HBM once per pass)."""
     passes: tuple
 
-    mode = "enc"
     chunked = False
     ksplit = 1
     j0 = 0
-    map_stride = 0
     far = True
+
+    @property
+    def mode(self) -> str:
+        return self.passes[0].mode       # "enc" or "synw"
+
+    @property
+    def map_stride(self) -> int:
+        return self.passes[0].map_stride
 
     @property
     def k(self) -> int:
@@ -1194,6 +1200,8 @@ class MergedSpec:
 
     @property
     def name(self) -> str:
+        if self.mode == "synw":
+            return f"qf_cauchy_synwm_k{self.k}_r{self.rt}"
         return f"qf_cauchy_bsm{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
 
     @property
@@ -1210,12 +1218,15 @@ class MergedSpec:
 
     @property
     def lds_bytes(self) -> int:
-        return max(p.lds_bytes for p in self.passes)
+        # lds_rows: each wave's row slots at s29 (its pass) x the slots' bytes
+        return self.waves * self.passes[0].lds_rows * LDS_ROW_BYTES
 
 
 def merged_spec(passes) -> MergedSpec:
     passes = tuple(dataclasses.replace(p, merged=True) for p in passes)
-    assert 1 < len(passes) <= 4 and all(p.mode == "enc" and p.ksplit == 1 and not p.lds_rows for p in passes)
+    assert 1 < len(passes) <= 4 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
+                                        for p in passes)
+    assert len({p.lds_rows for p in passes}) == 1 and (not passes[0].lds_rows or passes[0].fft)
     assert all(p.k == passes[0].k and p.rt == passes[0].rt for p in passes)
     assert sorted((p.j0, p.j0 + p.r) for p in passes) == [(p.j0, p.j0 + p.r) for p in passes]
     assert passes[0].j0 == 0 and passes[-1].j0 + passes[-1].r == passes[0].rt
@@ -1226,7 +1237,8 @@ def _generate_merged(ms: MergedSpec) -> list[Op]:
     """The common head (kernargs, lane / wave ids), a branch on the wave's
     index in its workgroup (s29) to its pass, and each pass's body (its own
     item loop, labels and far-jump ids made unique).  A pass's body first
-    moves the repair base s[6:7] to its first row: + j0 * repair row stride."""
+    moves the output base s[6:7] to its first row: + j0 * output row stride
+    (repair rows for enc, syndrome rows for synw)."""
     out: list[Op] = []
     E = out.append
     bodies = []

@@ -210,6 +210,10 @@ def kernel_specs() -> list:
     for k, rt in BS_FFT_PASSES:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
                                      for j0, rp in lch_fft.coset_passes(k, rt)]))
+    # (the synw passes merged the same way -- bs_codegen.merged_spec takes
+    # them -- measured no faster: 0.479 / 0.546 / 0.467 ms against 0.485 /
+    # 0.529 / 0.482 at (160, 48) / (196, 59) / (128, 39), profiles/r04z_c5_merged.json;
+    # those passes are not bound by their row reads)
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
     return specs

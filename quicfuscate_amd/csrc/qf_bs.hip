@@ -8,6 +8,7 @@
 // hipModuleLoadData and launches them with a packed kernarg buffer.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -30,6 +31,13 @@ struct QfBsEntry {
 #include "qf_bs_blobs.inc"
 
 namespace qf {
+
+// QF_BS_DEBUG=1: name the check behind a hipErrorInvalidValue on stderr
+static hipError_t bs_invalid(int line) {
+    static const bool on = getenv("QF_BS_DEBUG") != nullptr;
+    if (on) fprintf(stderr, "qf_bs.hip:%d: launch refused\n", line);
+    return hipErrorInvalidValue;
+}
 
 // the kernel (first pass, j0 = 0) of the (k, r) code
 static const QfBsEntry* find(char mode, uint32_t k, uint32_t r) {
@@ -78,9 +86,9 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
                          uint32_t lu_stride = 0, const uint32_t* tab256 = nullptr,
                          const uint64_t* src_offs = nullptr, const uint64_t* dst_offs = nullptr,
                          const uint32_t* bound = nullptr) {
-    if (!e) return hipErrorInvalidValue;
+    if (!e) return bs_invalid(__LINE__);
     int idx = (int)(e - qf_bs_table);
-    if (idx >= BsCache::kMax) return hipErrorInvalidValue;
+    if (idx >= BsCache::kMax) return bs_invalid(__LINE__);
     // a partial last unit: enc in the zero-tail lane space (its bytes >= L are
     // masked to zero before the store); syn (the syndrome rows' tail is junk
     // the combine never stores); the lane-chunk decode ('c': the lane holding
@@ -91,21 +99,23 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     if ((L % 16 && (e->mode == 'd' || (enc && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
-        return hipErrorInvalidValue;
+        return bs_invalid(__LINE__);
     if (!cache.fn[idx]) {
         hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
-        if (err != hipSuccess) return err;
-        err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
-        if (err != hipSuccess) return err;
+        if (err == hipSuccess) err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
+        if (err != hipSuccess) {
+            if (getenv("QF_BS_DEBUG")) fprintf(stderr, "%s: module load %d\n", e->name, (int)err);
+            return err;
+        }
     }
     const uint32_t Lu = (L + 15) / 16;
     // lane-chunk layout of the chunked fused decode ('c'): lane-chunk = units
     // q and q + Q of one generation, Q = ceil(Lu / 2), 64 lane-chunks per item
     if (chunked) Lv = (Lu + 1) / 2;
-    else if (Lv < Lu) return hipErrorInvalidValue;
-    if (Lv < 2) return hipErrorInvalidValue;
+    else if (Lv < Lu) return bs_invalid(__LINE__);
+    if (Lv < 2) return bs_invalid(__LINE__);
     const uint64_t total = (uint64_t)G * Lv;
-    if (total >= (1ull << 31)) return hipErrorInvalidValue;
+    if (total >= (1ull << 31)) return bs_invalid(__LINE__);
     uint32_t magic, shift;
     magic_for(Lv, &magic, &shift);
     const uint32_t n_items = (uint32_t)(chunked ? (total + 63) / 64 : (total + 127) / 128);
@@ -173,7 +183,10 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     }
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 64 * e->waves, 1, 1, 0, st, nullptr, cfg);
+    const hipError_t err = hipModuleLaunchKernel(cache.fn[idx], blocks, 1, 1, 64 * e->waves, 1, 1, 0, st, nullptr, cfg);
+    if (err != hipSuccess && getenv("QF_BS_DEBUG"))
+        fprintf(stderr, "%s: hipModuleLaunchKernel %d (%u blocks x %u)\n", e->name, (int)err, blocks, 64 * e->waves);
+    return err;
 }
 
 uint32_t bs_padded_units(uint32_t L) { return ((L + 15) / 16 + 7) / 8 * 8; }
@@ -196,9 +209,9 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
     // (with a destination offset table each generation's repair block is the
     // caller's: only the row stride is checked here)
     if (zero_tail && !(dst_offs ? (r == 1 || drs >= 16ull * bs_padded_units(L)) : bs_zero_tail_fits(r, L, drs, dgs)))
-        return hipErrorInvalidValue;
-    if (!zero_tail && L % 16) return hipErrorInvalidValue;
-    if (!find('e', k, r)) return hipErrorInvalidValue;
+        return bs_invalid(__LINE__);
+    if (!zero_tail && L % 16) return bs_invalid(__LINE__);
+    if (!find('e', k, r)) return bs_invalid(__LINE__);
     // batches of at most one item (128 units) per CU take the 'f' kernels
     // (the sources of an item split over its workgroup's four waves) where
     // they exist, unless QF_ENCODE_KSPLIT=0
@@ -228,11 +241,11 @@ hipError_t syn_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                       const uint8_t* zero, const uint64_t* rows_offs) {
     const QfBsEntry* e = find('s', k, r);
-    if (!e || map_stride != e->map_stride || !zero) return hipErrorInvalidValue;
+    if (!e || map_stride != e->map_stride || !zero) return bs_invalid(__LINE__);
     // syndrome rows live in the library's workspace: always the padded lane
     // space (srs >= 16 * bs_padded_units(L); the tail holds junk)
     const uint32_t Lv = bs_padded_units(L);
-    if (srs < 16ull * Lv) return hipErrorInvalidValue;
+    if (srs < 16ull * Lv) return bs_invalid(__LINE__);
     return launch(cache, e, num_cus, st, rows, syn, rgs, sgs, rs, srs, L, G, Lv, map_stride, smap, zero, nullptr, 0,
                   nullptr, rows_offs, nullptr);
 }
@@ -242,10 +255,10 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
                        uint64_t srs, uint32_t L, uint32_t G, const uint8_t* smap, uint32_t map_stride,
                        const uint8_t* zero, const uint32_t* bound, const uint64_t* rows_offs) {
     const QfBsEntry* first = find('w', k, r);
-    if (!first || map_stride != first->map_stride || !zero) return hipErrorInvalidValue;
+    if (!first || map_stride != first->map_stride || !zero) return bs_invalid(__LINE__);
     // an item (128 units) must lie in at most two generations
     const uint32_t Lv = bs_padded_units(L);
-    if (Lv < 128 || srs < 16ull * Lv) return hipErrorInvalidValue;
+    if (Lv < 128 || srs < 16ull * Lv) return bs_invalid(__LINE__);
     for (const auto& e : qf_bs_table) {
         if (e.mode != 'w' || e.k != k || e.rt != r) continue;
         hipError_t err = launch(cache, &e, num_cus, st, rows, syn + (uint64_t)e.j0 * srs, rgs, sgs, rs, srs, L, G, Lv,
@@ -295,12 +308,12 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
                       const uint64_t* rows_offs, const uint64_t* rec_offs) {
     const QfBsEntry* e = find_dec(&cache, k, r, L, G, num_cus);
     if (!e || map_stride != e->map_stride || !zero || !lu || !tab256 || (lu_stride & 15) || lu_stride < 272)
-        return hipErrorInvalidValue;
+        return bs_invalid(__LINE__);
     // the LU record pointer is computed with a 32-bit stride multiply
-    if ((uint64_t)G * lu_stride >= (1ull << 40)) return hipErrorInvalidValue;
+    if ((uint64_t)G * lu_stride >= (1ull << 40)) return bs_invalid(__LINE__);
     // unpadded lane space: the kernel is VALU-bound, padding lanes would be
     // pure extra work (and the recovered rows are caller memory, payload only)
-    if (L % 16 && e->mode != 'c' && e->mode != 'k' && e->mode != 'C') return hipErrorInvalidValue;
+    if (L % 16 && e->mode != 'c' && e->mode != 'k' && e->mode != 'C') return bs_invalid(__LINE__);
     return launch(cache, e, num_cus, st, rows, rec, rgs, rec_gs, rs, rec_rs, L, G, (L + 15) / 16, map_stride, smap, zero,
                   lu, lu_stride, tab256, rows_offs, rec_offs);
 }
@@ -314,9 +327,9 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     const QfBsEntry* e = find('m', 0, 16);
     if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || a.dst_row_stride >= (1ull << 32) ||
         a.coef_gen_stride >= (1ull << 32))
-        return hipErrorInvalidValue;
+        return bs_invalid(__LINE__);
     const int idx = (int)(e - qf_bs_table);
-    if (idx >= BsCache::kMax) return hipErrorInvalidValue;
+    if (idx >= BsCache::kMax) return bs_invalid(__LINE__);
     if (!cache.fn[idx]) {
         hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
         if (err != hipSuccess) return err;
@@ -327,7 +340,7 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     const uint64_t G = a.total_units / Lu;
     const uint64_t n_items = G * ipg;
     if (n_items == 0) return hipSuccess;
-    if (n_items >= (1ull << 31)) return hipErrorInvalidValue;
+    if (n_items >= (1ull << 31)) return bs_invalid(__LINE__);
     uint32_t magic = 0, shift = 0;
     if (ipg >= 2) magic_for(ipg, &magic, &shift);
     // persistent grid: two 4-wave blocks per CU (192 VGPRs: two waves per SIMD)

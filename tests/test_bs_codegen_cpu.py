@@ -616,7 +616,7 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
         assert nv <= 256
 
 
-def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True):
+def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False):
     """The wave-uniform syndrome kernel (mode "synw") on the emulator for
     every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
     generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
@@ -654,7 +654,9 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True):
         plans.append((src, rep, E, J))
     emu_bufs = {}
     ROWS, SYN, MAP, ZERO, OFFS, BOUND = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
-    for spec in specs:
+    # merged: every pass in one dispatch (MergedSpec), wave p of workgroup w
+    # running pass p on item w
+    for spec in ([bs.merged_spec(specs)] if merged else specs):
         emu = bs.Emulator(bs.generate(spec))
         emu.add_buffer(ROWS, rows)
         emu.add_buffer(SYN, syn)
@@ -666,6 +668,14 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True):
                          map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
                          bound=BOUND if use_bound else 0)
         n_items = bs.launch_geometry(L, G, Lv)[2]
+        if merged:
+            ka = bs.kernargs(ROWS, SYN, 0 if offs else rgs, sgs, rs, srs, L, G, n_items, smap=MAP,
+                             map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
+                             bound=BOUND if use_bound else 0)
+            for wg in range(n_items):
+                for w in range(spec.waves):
+                    emu.run_wave(ka, wg, w)
+            break
         for wv in range(n_items):
             emu.run_wave(ka, wv // 4, wv % 4)
         emu_bufs[spec.j0] = emu
@@ -701,6 +711,14 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True):
 ])
 def test_emulated_synw_kernel(oracle, k, rt, rp, L, G, offs):
     assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L, offs=offs) > 0
+
+
+@pytest.mark.parametrize("k,rt,rp,L,G,offs", [(8, 6, 3, 2048, 5, False), (12, 7, 4, 2064, 4, True),
+                                               (5, 3, 1, 2200, 3, False)])
+def test_emulated_synw_merged(oracle, k, rt, rp, L, G, offs):
+    """All synw passes in one dispatch ('W'): the same syndromes, and the
+    same skips, as one launch per pass."""
+    assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L + 1, offs=offs, merged=True) > 0
 
 
 def test_emulated_synw_without_bound(oracle):
@@ -996,9 +1014,10 @@ def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
             assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
 
 
-@pytest.mark.parametrize("k,rt,L,G,fft,blocks", [(24, 10, 200, 3, 8, 0), (20, 20, 72, 2, 0, 0), (48, 21, 4000, 2, 8, 3),
-                                                  (40, 30, 40, 1, 0, 0), (160, 48, 40, 1, 8, 0)])
-def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks):
+@pytest.mark.parametrize("k,rt,L,G,fft,blocks,lds", [(24, 10, 200, 3, 8, 0, 0), (20, 20, 72, 2, 0, 0, 0),
+                                                      (48, 21, 4000, 2, 8, 3, 0), (40, 30, 40, 1, 0, 0, 0),
+                                                      (160, 48, 40, 1, 8, 0, 0), (48, 21, 2100, 2, 8, 0, 6)])
+def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks, lds):
     """All passes of a code in one dispatch (MergedSpec): wave p of each
     workgroup runs pass p on the workgroup's item; a persistent grid (fewer
     workgroups than items, item stride = workgroups) included."""
@@ -1013,7 +1032,8 @@ def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks):
     src = rng.integers(0, 256, G * sgs + 64, dtype=np.uint8)
     dst = np.full(G * dgs, 0xEE, np.uint8)
     if fft:
-        passes = [bs.KernelSpec(k, rp, 2, r_total=rt, j0=j0, fft=fft) for j0, rp in lch_fft.coset_passes(k, rt)]
+        passes = [bs.KernelSpec(k, rp, 2, r_total=rt, j0=j0, fft=fft, lds_rows=lds)
+                  for j0, rp in lch_fft.coset_passes(k, rt)]
     else:
         n = -(-rt // 12)
         cuts = [rt * p // n for p in range(n + 1)]
@@ -1028,8 +1048,11 @@ def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks):
     wgs = blocks or items
     ka = bs.kernargs(SRC, DST, sgs, dgs, srs, drs, L, G, wgs, Lv=Lv, zero_tail=True)
     for wg in range(wgs):
-        for w in range(ms.waves):
-            emu.run_wave(ka, wg, w)
+        if lds:   # the waves of a workgroup share its LDS (row slots at s29)
+            emu.run_workgroup(ka, wg, ms.waves, ms.lds_bytes)
+        else:
+            for w in range(ms.waves):
+                emu.run_wave(ka, wg, w)
     for g in range(G):
         rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
         want = oracle.encode(rows, rt)

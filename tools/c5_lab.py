@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""C5 pass-kernel lab: variants of the merged multi-pass encode (MergedSpec)
+at the C5 jumbo shapes, timed on the GPU and checked against the library's
+encode of the same batch.
+
+    python tools/c5_lab.py build                      # here: generate + assemble -> tools/lab_build/c5_*
+    python tools/c5_lab.py run [--bytes 1e9]          # GPU box
+
+Variant kinds: "N" additive-FFT coset passes (lch_fft.coset_passes), "M"
+plain passes split into `npass` balanced ranges.  Diagnostic only.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+OUT = REPO / "tools" / "lab_build"
+L_JUMBO, RS, DRS = 9000, 9008, 9088
+
+# (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
+VARIANTS = [
+    ("n160_lib", 160, 48, "N", 0, {}),
+    ("n160_lds6", 160, 48, "N", 0, {"lds_rows": 6}),
+    ("n160_lds8", 160, 48, "N", 0, {"lds_rows": 8}),
+    ("n160_lds10", 160, 48, "N", 0, {"lds_rows": 10}),
+    ("m160_lib", 160, 48, "M", 4, {}),
+    ("m160_pd2", 160, 48, "M", 4, {"pd": 2}),
+    ("m160_p3", 160, 48, "M", 3, {}),
+    ("n160_noload", 160, 48, "N", 0, {"flags": ("noload",)}),
+    ("n160_novalu", 160, 48, "N", 0, {"flags": ("novalu",)}),
+    ("n160_same", 160, 48, "N", 0, {"flags": ("same",)}),
+    ("n160_same_noload", 160, 48, "N", 0, {"flags": ("same", "noload")}),
+    ("n196_lib", 196, 59, "N", 0, {}),
+    ("n196_lds8", 196, 59, "N", 0, {"lds_rows": 8}),
+    ("m196_lib", 196, 59, "M", 4, {}),
+    ("n128_lib", 128, 39, "N", 0, {}),
+    ("n128_lds8", 128, 39, "N", 0, {"lds_rows": 8}),
+    ("m128_lib", 128, 39, "M", 2, {}),
+    ("m128_p3pd2", 128, 39, "M", 3, {"pd": 2}),
+]
+
+
+def make_spec(bs, k, rt, kind, npass, kw):
+    from quicfuscate_amd import lch_fft
+
+    pd = kw.get("pd", 3)
+    extra = {x: v for x, v in kw.items() if x not in ("pd", "flags")}
+    if kind == "N":
+        passes = [bs.KernelSpec(k, rp, pd, "enc", fft=8, ld_policy="", r_total=rt, j0=j0, **extra)
+                  for j0, rp in lch_fft.coset_passes(k, rt)]
+    else:
+        cuts = [rt * p // npass for p in range(npass + 1)]
+        passes = [bs.KernelSpec(k, cuts[p + 1] - cuts[p], pd, "enc", r_total=rt, j0=cuts[p], **extra)
+                  for p in range(npass)]
+    return bs.merged_spec(passes)
+
+
+VALU = {"v_xor", "v_xor3", "v_mov", "v_movk", "v_bitsel_s", "v_bitop3", "v_lshl64", "v_lshr64", "v_bfi", "v_and_s",
+        "v_perm"}
+
+
+def variant_ops(bs, ms, flags):
+    """noload: no row loads / load waits in the pass bodies; novalu: no
+    XOR / move / select work in them (loads, addresses, stores kept); same:
+    every wave runs pass 0 (no dispatch: one body's code for all waves)."""
+    ops = bs.generate(ms)
+    out, in_body = [], False
+    for n, op in enumerate(ops):
+        if op.name == "label" and op.args[0].startswith(".LP") and op.args[0].endswith("body"):
+            in_body = True
+        if op.name == "label" and op.args[0].startswith(".Lpass"):
+            in_body = False
+        if "same" in flags and op.name in ("s_cmp_lg_k_br", "s_far_jump") and str(op.args[0]).startswith((".Lnpass", ".Lpass")):
+            continue
+        if in_body and "noload" in flags and op.name in ("load16", "load16_lds", "s_waitcnt_vm"):
+            continue
+        if in_body and "novalu" in flags and (op.name in VALU or (op.name.startswith("v_") and op.name not in
+                                                                   ("v_add64_s", "v_add64_v", "v_mad64_k",
+                                                                    "v_mad64_s", "v_movs", "v_readfirstlane",
+                                                                    "v_add_s", "v_addk", "v_cmp_eq_s", "v_cmp_gt_s"))):
+            continue
+        out.append(op)
+    return out
+
+
+def build():
+    from quicfuscate_amd import bs_codegen as bs
+    from quicfuscate_amd.build_lib import assemble
+
+    OUT.mkdir(parents=True, exist_ok=True)
+    for old in OUT.glob("c5_*"):
+        old.unlink()
+    manifest = []
+    for name, k, rt, kind, npass, kw in VARIANTS:
+        ms = make_spec(bs, k, rt, kind, npass, kw)
+        text = bs.emit_asm(ms, variant_ops(bs, ms, set(kw.get("flags", ()))))
+        h = assemble(f"c5_{name}", text.replace(ms.name, f"c5_{name}"), OUT)
+        manifest.append({"name": name, "k": k, "rt": rt, "kind": kind, "npass": npass, "kw": kw, "waves": ms.waves,
+                         "hsaco": h.name, "symbol": f"c5_{name}", "vgprs": ms.next_free_vgpr, "lds": ms.lds_bytes})
+        print(name, ms.waves, ms.next_free_vgpr, ms.lds_bytes, h.stat().st_size, flush=True)
+    (OUT / "c5_manifest.json").write_text(json.dumps(manifest, indent=1))
+
+
+def run(nbytes: float, reps: int):
+    import torch
+
+    from quicfuscate_amd import bs_codegen as bs
+    from quicfuscate_amd import fec as qf
+
+    hip = ctypes.CDLL(str(Path(torch.__file__).parent / "lib" / "libamdhip64.so"))
+    manifest = json.loads((OUT / "c5_manifest.json").read_text())
+    ctx = qf.default_context()
+    stream = torch.cuda.current_stream()
+    res = {}
+    cur = None
+    for m in manifest:
+        k, rt = m["k"], m["rt"]
+        G = max(1, int(nbytes // (k * L_JUMBO)))
+        if cur != (k, rt):
+            src = torch.randint(0, 256, (G * k * RS,), dtype=torch.uint8, device="cuda")
+            ref = torch.empty(G * rt * DRS, dtype=torch.uint8, device="cuda")
+            qf.encode_batch(src, ref, k, rt, L_JUMBO, src_row_stride=RS, src_gen_stride=k * RS, rep_row_stride=DRS,
+                            rep_gen_stride=rt * DRS, G=G, zero_tail=True, ctx=ctx)
+            ctx.sync()
+            dst = torch.empty_like(ref)
+            cur = (k, rt)
+        mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        data = (OUT / m["hsaco"]).read_bytes()
+        buf = ctypes.create_string_buffer(data, len(data))
+        assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
+        Lv = bs.padded_units(L_JUMBO)
+        _, _, n_items = bs.launch_geometry(L_JUMBO, G, Lv)
+        blocks = n_items
+        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * RS, rt * DRS, RS, DRS, L_JUMBO, G, blocks, Lv=Lv,
+                         zero_tail=True)
+        kbuf = ctypes.create_string_buffer(ka, len(ka))
+        size = ctypes.c_size_t(len(ka))
+        extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
+                                     ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+
+        def launch():
+            e = hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 64 * m["waves"], 1, 1, 0,
+                                          ctypes.c_void_p(stream.cuda_stream), None, extra)
+            assert e == 0, e
+
+        dst.fill_(0xA5)
+        launch()
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(dst, ref))
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record(stream)
+        for _ in range(reps):
+            launch()
+        t1.record(stream)
+        torch.cuda.synchronize()
+        ms = t0.elapsed_time(t1) / reps
+        gib = G * (k + rt) * L_JUMBO / (ms / 1e3) / 2**30
+        res[m["name"]] = {"ms": round(ms, 4), "GiBps_alg": round(gib, 1), "G": G, "matches_library": ok,
+                          "waves": m["waves"], "vgprs": m["vgprs"], "lds": m["lds"], "kw": m["kw"]}
+        print(m["name"], res[m["name"]], flush=True)
+        hip.hipModuleUnload(mod)
+    return res
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--bytes", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default="gpurun_out/c5_lab.json")
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build()
+    else:
+        r = run(a.bytes, a.reps)
+        Path(a.out).parent.mkdir(exist_ok=True)
+        Path(a.out).write_text(json.dumps(r, indent=1))

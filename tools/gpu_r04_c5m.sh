@@ -1,0 +1,20 @@
+#!/bin/bash
+# GPU box, round 4: C5 tests, then the C5 shapes with every pass in one
+# dispatch (encode 'N' + decode syndromes 'W') against one launch per pass.
+#   TAG=r04z tools/gpu_r04_c5m.sh
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+TAG=${TAG:-r04}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_gpu_c5_mixed.py tests/test_gpu_desc.py tests/test_gpu_decode.py \
+    tests/test_gpu_encode.py -x -q --timeout 170 --timeout-method thread > $OUT/c5m_tests.log 2>&1 || { tail -30 $OUT/c5m_tests.log; exit 1; }
+tail -2 $OUT/c5m_tests.log
+SH="128,20;128,39;160,48;196,59"
+for M in 0 1; do
+    QF_ENCODE_MERGED=$M timeout -k 10 300 python3 tools/bench_c5.py --shapes "$SH" --modes block,sliding \
+        --reps 5 --out $OUT/c5_m$M.json > $OUT/c5_m$M.log 2>&1
+    echo "merged=$M"
+    grep "^k" $OUT/c5_m$M.log
+done
