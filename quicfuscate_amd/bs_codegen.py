@@ -433,6 +433,10 @@ class KernelSpec:
     # fft: plane pairs shared by >= 3 output rows of a constant multiply are
     # XORed once into the transpose scratch registers
     fft_cse: bool = True
+    # fft passes of codes the plain plan does not cover (lch_fft.hybrid_plan):
+    # repair points per coset, i.e. accumulator blocks (16, or 8: half the
+    # accumulator VGPRs, twice the passes)
+    fft_coset: int = 16
     # enc: this pass is one wave of a MergedSpec dispatch (item = workgroup,
     # the workgroup's waves run the code's passes on the same item)
     merged: bool = False
@@ -455,7 +459,7 @@ class KernelSpec:
             return lch_fft.plan(self.k, self.r, self.fft, basis=self.fft_basis[0], beta_out=self.fft_basis[1])
         if self.k & (self.k - 1) or self.rt != self.r or self.j0:
             # a pass of a code the plain plan does not cover (lch_fft.hybrid_plan)
-            return _hybrid_plan(self.k, self.rt, self.j0, self.r, self.fft)
+            return _hybrid_plan(self.k, self.rt, self.j0, self.r, self.fft, self.fft_coset)
         return _fft_plan(self.k, self.r, self.fft)
 
     @property
@@ -775,9 +779,9 @@ def _fft_plan(k: int, r: int, ch: int):
 
 
 @functools.lru_cache(maxsize=None)
-def _hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int):
+def _hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int, R: int = 16):
     from . import lch_fft
-    return lch_fft.hybrid_plan(k, rt, j0, r, ch)
+    return lch_fft.hybrid_plan(k, rt, j0, r, ch, R)
 
 
 def _macc_cost(c: int, n_tmp: int = 0) -> int:
@@ -1224,7 +1228,7 @@ class MergedSpec:
 
 def merged_spec(passes) -> MergedSpec:
     passes = tuple(dataclasses.replace(p, merged=True) for p in passes)
-    assert 1 < len(passes) <= 4 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
+    assert 1 < len(passes) <= 16 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
                                         for p in passes)
     assert len({p.lds_rows for p in passes}) == 1 and (not passes[0].lds_rows or passes[0].fft)
     assert all(p.k == passes[0].k and p.rt == passes[0].rt for p in passes)
@@ -2817,7 +2821,7 @@ amdhsa.kernels:
     .group_segment_fixed_size: {spec.lds_bytes}
     .kernarg_segment_align: 8
     .kernarg_segment_size: {spec.kernarg_bytes}
-    .max_flat_workgroup_size: 256
+    .max_flat_workgroup_size: {64 * getattr(spec, "waves", 4)}
     .name:           {name}
     .private_segment_fixed_size: 0
     .sgpr_count:     {spec.next_free_sgpr + 6}

@@ -25,6 +25,11 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
     ("n160_lib", 160, 48, "N", 0, {}),
+    ("n160_c8pd2", 160, 48, "N", 0, {"fft_coset": 8, "pd": 2}),
+    ("n160_c8pd3", 160, 48, "N", 0, {"fft_coset": 8, "pd": 3}),
+    ("n160_c8lds6", 160, 48, "N", 0, {"fft_coset": 8, "lds_rows": 6}),
+    ("n128_c8pd2", 128, 39, "N", 0, {"fft_coset": 8, "pd": 2}),
+    ("n196_c8lds4", 196, 59, "N", 0, {"fft_coset": 8, "lds_rows": 4}),
     ("n160_lds6", 160, 48, "N", 0, {"lds_rows": 6}),
     ("n160_lds8", 160, 48, "N", 0, {"lds_rows": 8}),
     ("n160_lds10", 160, 48, "N", 0, {"lds_rows": 10}),
@@ -51,8 +56,9 @@ def make_spec(bs, k, rt, kind, npass, kw):
     pd = kw.get("pd", 3)
     extra = {x: v for x, v in kw.items() if x not in ("pd", "flags")}
     if kind == "N":
+        R = extra.get("fft_coset", 16)
         passes = [bs.KernelSpec(k, rp, pd, "enc", fft=8, ld_policy="", r_total=rt, j0=j0, **extra)
-                  for j0, rp in lch_fft.coset_passes(k, rt)]
+                  for j0, rp in lch_fft.coset_passes(k, rt, R)]
     else:
         cuts = [rt * p // npass for p in range(npass + 1)]
         passes = [bs.KernelSpec(k, cuts[p + 1] - cuts[p], pd, "enc", r_total=rt, j0=cuts[p], **extra)
