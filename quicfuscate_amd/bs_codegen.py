@@ -1754,8 +1754,8 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
     _synw_item_setup(E, spec)
     quad = [None]
 
-    def load_row(n: int):
-        kind, idx = seq[n]
+    def load_row(n: int, b: Optional[int] = None, order=seq):
+        kind, idx = order[n]
         pos = k + spec.j0 + idx if kind == "rep" else idx
         q = pos // 16
         if quad[0] != q:
@@ -1772,7 +1772,8 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
             E(Op("s_addc", (base + 1, base + 1, R + 1)))
             E(Op("s_cmp_eq_k", (t, ABSENT)))
             E(Op("s_cselect64", (base, 22, base)))
-        b = ring0 + 8 * (n % nbuf)
+        if b is None:
+            b = ring0 + 8 * (n % nbuf)
         for mask, voff, d, sb in ((SW_A0, V_SRCA, b, SW_BASE0), (SW_A1, V_SRCA, b, SW_BASE1),
                                   (SW_B0, V_SRCB, b + 4, SW_BASE0), (SW_B1, V_SRCB, b + 4, SW_BASE1)):
             E(Op("s_exec", (mask,)))
@@ -1782,6 +1783,36 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
 
     n_seq = len(seq)
     per_row = 0 if spec.lab_norows else 4
+    if spec.fft:
+        # additive-FFT syndromes (lch_fft plan of the pass, as the 'N' encode):
+        # sources (the zero row when absent) through the chunked transform,
+        # then each repair row, in byte form, onto its transposed block
+        P = spec.fplan
+        fseq = [("src", i) for i in P.order] + [("rep", j) for j in range(r)]
+        n_all = len(fseq)
+
+        def load_fft(n: int, base: int):
+            load_row(n, base, fseq)
+
+        def wait_fft(n: int):
+            E(Op("s_waitcnt_vm", (per_row * min(pd, n_all - 1 - n),)))
+
+        _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
+        for n in range(k, n_all):
+            if n + pd < n_all:
+                load_fft(n + pd, ring0 + 8 * ((n + pd) % nbuf))
+            wait_fft(n)
+            blk0 = acc0 + 8 * P.out_block[fseq[n][1]]
+            ops.extend(_transpose_ops(blk0, spec.bfi_transpose, spec.vmask))
+            base = ring0 + 8 * (n % nbuf)
+            for b in range(8):
+                E(Op("v_xor", (blk0 + b, blk0 + b, base + b)))
+        E(Op("s_nop", (4,)))
+        for j in range(r):
+            _store_pair(E, acc0 + 8 * P.out_block[j], S_STA, S_STB, spec.st_policy)
+        E(Op("label", (".Lskip",)))
+        _epilogue_next_item(E, far=spec.far)
+        return ops
     for n in range(min(pd, n_seq)):
         load_row(n)
     for n, (kind, idx) in enumerate(seq):

@@ -44,6 +44,7 @@ BS_FFT = [(64, 16), (64, 10), (32, 16), (16, 16)]
 # (lch_fft.hybrid_plan: one pass per coset of 16 repair points, sources
 # [0, 2^a) through the FFT, the rest folded in directly), merged ('N')
 BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
+BS_FFT_SYNW = [(128, 39)]
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
@@ -210,6 +211,14 @@ def kernel_specs() -> list:
     for k, rt in BS_FFT_PASSES:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
                                      for j0, rp in lch_fft.coset_passes(k, rt)]))
+    # additive-FFT synw passes ('V', QF_FFT_KERNELS): one per coset of 16
+    # repair points, as the 'N' encode; where they cut the time of the passes
+    # that run at 20 % loss: (128, 39) 0.506 -> 0.388 ms; (160, 48) 0.489 ms
+    # either way; (196, 59) would run 3 FFT passes against 2 plain
+    # (tools/gpu_r04_c5v.sh, profiles/r04ac_c5_synw_fft.json)
+    for k, rt in BS_FFT_SYNW:
+        specs += [bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
+                  for j0, rp in lch_fft.coset_passes(k, rt)]
     # (the synw passes merged the same way -- bs_codegen.merged_spec takes
     # them -- measured no faster: 0.479 / 0.546 / 0.467 ms against 0.485 /
     # 0.529 / 0.482 at (160, 48) / (196, 59) / (128, 39), profiles/r04z_c5_merged.json;
@@ -239,6 +248,7 @@ def _bs_kernels(build_dir: Path) -> Path:
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         mode = ("C" if spec.fft else "k" if spec.ksplit > 1 else "c") if spec.chunked else \
+            "V" if spec.mode == "synw" and spec.fft else \
             ("N" if spec.fft else "M") if isinstance(spec, bs.MergedSpec) else \
             "E" if spec.fft else \
             ("f" if spec.mode == "enc" and spec.ksplit > 1 else

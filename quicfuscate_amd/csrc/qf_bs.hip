@@ -21,7 +21,8 @@ struct QfBsEntry {
     char mode;  // 'e' encode, 'E' additive-FFT encode, 'C' additive-FFT chunked decode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
                 // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves,
                 // 'f' the encode (passes of C5 codes) with an item's sources split the same way,
-                // 'M' / 'N' every encode pass of a code in one dispatch (plain / additive-FFT passes)
+                // 'M' / 'N' every encode pass of a code in one dispatch (plain / additive-FFT passes),
+                // 'V' the 'w' syndrome passes through the additive FFT
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -176,7 +177,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
     a[ot + 3] = (uint32_t)((uintptr_t)dst_offs >> 32);
     size_t sz = (size_t)(ot + 4) * 4;
-    if (e->mode == 'w') {   // per-generation pass bound (bs_codegen KERNARG_BYTES_SYNW)
+    if (e->mode == 'w' || e->mode == 'V') {   // per-generation pass bound (bs_codegen KERNARG_BYTES_SYNW)
         a[24] = (uint32_t)(uintptr_t)bound;
         a[25] = (uint32_t)((uintptr_t)bound >> 32);
         sz = 26 * 4;
@@ -259,8 +260,10 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
     // an item (128 units) must lie in at most two generations
     const uint32_t Lv = bs_padded_units(L);
     if (Lv < 128 || srs < 16ull * Lv) return bs_invalid(__LINE__);
+    // the additive-FFT passes ('V') where generated, unless QF_FFT_KERNELS=0
+    const char mode = cache.get(QF_OPT_FFT_KERNELS) && find('V', k, r) ? 'V' : 'w';
     for (const auto& e : qf_bs_table) {
-        if (e.mode != 'w' || e.k != k || e.rt != r) continue;
+        if (e.mode != mode || e.k != k || e.rt != r) continue;
         hipError_t err = launch(cache, &e, num_cus, st, rows, syn + (uint64_t)e.j0 * srs, rgs, sgs, rs, srs, L, G, Lv,
                                 map_stride, smap, zero, nullptr, 0, nullptr, rows_offs, nullptr, bound);
         if (err != hipSuccess) return err;

@@ -616,7 +616,7 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
         assert nv <= 256
 
 
-def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False):
+def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0):
     """The wave-uniform syndrome kernel (mode "synw") on the emulator for
     every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
     generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
@@ -628,7 +628,13 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
     Lv = bs.padded_units(L)
     srs = 16 * Lv + 16
     sgs = rt * srs
-    specs = [bs.KernelSpec(k, min(rp, rt - j0), 2, mode="synw", r_total=rt, j0=j0) for j0 in range(0, rt, rp)]
+    if fft:   # additive-FFT passes: one per coset of 16 repair points (lch_fft.coset_passes)
+        from quicfuscate_amd import lch_fft
+
+        specs = [bs.KernelSpec(k, n, 2, mode="synw", r_total=rt, j0=j0, fft=fft)
+                 for j0, n in lch_fft.coset_passes(k, rt)]
+    else:
+        specs = [bs.KernelSpec(k, min(rp, rt - j0), 2, mode="synw", r_total=rt, j0=j0) for j0 in range(0, rt, rp)]
     ms = specs[0].map_stride
     rows = rng.integers(0, 256, G * rgs + 4096, dtype=np.uint8)
     smap = np.full(G * ms, 0xFF, np.uint8)
@@ -719,6 +725,14 @@ def test_emulated_synw_merged(oracle, k, rt, rp, L, G, offs):
     """All synw passes in one dispatch ('W'): the same syndromes, and the
     same skips, as one launch per pass."""
     assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L + 1, offs=offs, merged=True) > 0
+
+
+@pytest.mark.parametrize("k,rt,L,G,offs", [(24, 10, 2048, 3, False), (20, 20, 2100, 2, True), (48, 21, 2064, 2, False)])
+def test_emulated_synw_fft(oracle, k, rt, L, G, offs):
+    """synw passes through the hybrid additive FFT (lch_fft.hybrid_plan;
+    absent sources read the zero row, accepted repairs XOR onto their
+    transposed blocks): the same syndromes and skips as the plain passes."""
+    assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 7 + rt + L, offs=offs, fft=8) > 0
 
 
 def test_emulated_synw_without_bound(oracle):
