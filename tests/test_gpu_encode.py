@@ -280,6 +280,30 @@ def test_c5_passes_large_batch(qf, oracle, gpu_ctx, k, r):
         assert (sl[g, :, :L] == oracle.encode(rows, r)).all(), g
 
 
+def test_default_context_orders_with_torch_default_stream(qf, oracle, gpu_ctx):
+    """fec.Context() on torch's default stream binds the library to the null
+    stream (QF_STREAM_NULL): an encode enqueued right after torch work on that
+    stream, with no synchronize in between, sees its results, and torch work
+    enqueued after the encode sees the repairs."""
+    import torch
+
+    k, r, L, G = 64, 16, 1200, 4096          # large enough that an unordered read races
+    assert torch.cuda.default_stream().cuda_stream == 0
+    for trial in range(3):
+        gen = torch.Generator(device="cuda").manual_seed(100 + trial)
+        src = torch.empty(G * k * L, dtype=torch.uint8, device="cuda")
+        src.copy_(torch.randint(0, 256, src.shape, dtype=torch.uint8, device="cuda", generator=gen))
+        rep = torch.full((G * r * L,), 0xA5, dtype=torch.uint8, device="cuda")
+        qf.encode_batch(src, rep, k, r, L, src_row_stride=L, src_gen_stride=k * L, rep_row_stride=L,
+                        rep_gen_stride=r * L, G=G, ctx=gpu_ctx)
+        folded = rep.view(G, r * L).to(torch.int64).sum(dim=1)    # torch, after the encode, same stream
+        s = src.cpu().numpy()
+        for g in (0, G // 2, G - 1):
+            want = oracle.encode(s[g * k * L:(g + 1) * k * L].reshape(k, L), r)
+            assert (rep[g * r * L:(g + 1) * r * L].cpu().numpy().reshape(r, L) == want).all(), (trial, g)
+            assert int(folded[g]) == int(want.astype(np.int64).sum()), (trial, g)
+
+
 def test_gf_mul_slice_large_table_kernel(qf, oracle, gpu_ctx):
     """Slices from 16 MiB use the 64 KiB product-table kernel: every byte
     (and the n % 16 tail) equals gf_mul_table (gf_tables.rs:47-57)."""
