@@ -440,6 +440,9 @@ class KernelSpec:
     # enc: this pass is one wave of a MergedSpec dispatch (item = workgroup,
     # the workgroup's waves run the code's passes on the same item)
     merged: bool = False
+    # this pass is one block range of a pass-major MergedSpec (concat): the
+    # usual prologue, with the end of the common head marked
+    head_mark: bool = False
 
     @property
     def ahead(self) -> int:
@@ -976,7 +979,7 @@ def _prologue(E, spec: KernelSpec):
         E(Op("s_load_karg_x2", (SW_BOUND, KERNARG_BYTES)))   # kernarg words 24..25
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
-    if spec.merged:
+    if spec.merged or spec.head_mark:
         E(Op("label", (".Lhead_end",)))   # _generate_merged: the passes' common head ends here
     if spec.mode == "dec":
         # every wave copies the whole 8 KB split-table set into LDS (no
@@ -1164,6 +1167,10 @@ class MergedSpec:
     row hit the CU's L1 / the XCD's L2 instead of HBM (separate pass launches
     re-read every source row from HBM once per pass)."""
     passes: tuple
+    # pass-major: workgroups [p n, (p + 1) n) run pass p over the items as a
+    # separate launch of n 4-wave workgroups would (n = s18 / 4), so one pass's
+    # last, partly filled round of workgroups overlaps the next pass's first
+    concat: bool = False
 
     chunked = False
     ksplit = 1
@@ -1200,12 +1207,16 @@ class MergedSpec:
 
     @property
     def waves(self) -> int:
+        return 4 if self.concat else len(self.passes)
+
+    @property
+    def n_passes(self) -> int:
         return len(self.passes)
 
     @property
     def name(self) -> str:
         if self.mode == "synw":
-            return f"qf_cauchy_synwm_k{self.k}_r{self.rt}"
+            return f"qf_cauchy_synw{'c' if self.concat else 'm'}_k{self.k}_r{self.rt}"
         return f"qf_cauchy_bsm{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
 
     @property
@@ -1223,18 +1234,20 @@ class MergedSpec:
     @property
     def lds_bytes(self) -> int:
         # lds_rows: each wave's row slots at s29 (its pass) x the slots' bytes
+        if self.concat:
+            return max(p.lds_bytes for p in self.passes)
         return self.waves * self.passes[0].lds_rows * LDS_ROW_BYTES
 
 
-def merged_spec(passes) -> MergedSpec:
-    passes = tuple(dataclasses.replace(p, merged=True) for p in passes)
+def merged_spec(passes, concat: bool = False) -> MergedSpec:
+    passes = tuple(dataclasses.replace(p, merged=not concat, head_mark=concat) for p in passes)
     assert 1 < len(passes) <= 16 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
                                         for p in passes)
     assert len({p.lds_rows for p in passes}) == 1 and (not passes[0].lds_rows or passes[0].fft)
     assert all(p.k == passes[0].k and p.rt == passes[0].rt for p in passes)
     assert sorted((p.j0, p.j0 + p.r) for p in passes) == [(p.j0, p.j0 + p.r) for p in passes]
     assert passes[0].j0 == 0 and passes[-1].j0 + passes[-1].r == passes[0].rt
-    return MergedSpec(passes)
+    return MergedSpec(passes, concat)
 
 
 def _generate_merged(ms: MergedSpec) -> list[Op]:
@@ -1252,10 +1265,21 @@ def _generate_merged(ms: MergedSpec) -> list[Op]:
         if p == 0:
             out.extend(ops[:cut])
         bodies.append(ops[cut + 1:])
-    for p in range(1, ms.waves):
-        E(Op("s_cmp_lg_k_br", (29, p, f".Lnpass{p}")))
-        E(Op("s_far_jump", (f".Lpass{p}", 900 + p)))
-        E(Op("label", (f".Lnpass{p}",)))
+    if ms.concat:
+        # pass p = the workgroup id's range; s2 becomes the id within it
+        E(Op("s_lshrk", (46, 18, 2)))            # n = workgroups per pass
+        for p in range(ms.n_passes - 1):
+            E(Op("s_cmp_lt_br", (2, 46, f".Lsel{p}")))
+            E(Op("s_sub", (2, 2, 46)))
+        E(Op("s_far_jump", (f".Lpass{ms.n_passes - 1}", 900)))
+        for p in range(ms.n_passes - 1):
+            E(Op("label", (f".Lsel{p}",)))
+            E(Op("s_far_jump", (f".Lpass{p}", 901 + p)))
+    else:
+        for p in range(1, ms.waves):
+            E(Op("s_cmp_lg_k_br", (29, p, f".Lnpass{p}")))
+            E(Op("s_far_jump", (f".Lpass{p}", 900 + p)))
+            E(Op("label", (f".Lnpass{p}",)))
     for p, body in enumerate(bodies):
         E(Op("label", (f".Lpass{p}",)))
         j0 = ms.passes[p].j0

@@ -219,7 +219,20 @@ def kernel_specs() -> list:
     for k, rt in BS_FFT_SYNW:
         specs += [bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
                   for j0, rp in lch_fft.coset_passes(k, rt)]
-    # (the synw passes merged the same way -- bs_codegen.merged_spec takes
+    # the plain synw passes of the other C5 codes in one pass-major dispatch
+    # ('X'): one launch of P x n workgroups instead of P launches of n, so a
+    # pass's last, partly filled round overlaps the next pass's first
+    for k, rt in BS_ENC_ONLY:
+        npass = -(-rt // BS_PASS)
+        if npass == 1 or (k, rt) in BS_FFT_SYNW:
+            continue
+        j0, passes = 0, []
+        for p in range(npass):
+            rp = (rt - j0) // (npass - p)
+            passes.append(bs.KernelSpec(k, rp, BS_PD, "synw", r_total=rt, j0=j0))
+            j0 += rp
+        specs.append(bs.merged_spec(passes, concat=True))
+    # (the synw passes merged item-major -- bs_codegen.merged_spec takes
     # them -- measured no faster: 0.479 / 0.546 / 0.467 ms against 0.485 /
     # 0.529 / 0.482 at (160, 48) / (196, 59) / (128, 39), profiles/r04z_c5_merged.json;
     # those passes are not bound by their row reads)
@@ -249,12 +262,13 @@ def _bs_kernels(build_dir: Path) -> Path:
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         mode = ("C" if spec.fft else "k" if spec.ksplit > 1 else "c") if spec.chunked else \
             "V" if spec.mode == "synw" and spec.fft else \
-            ("N" if spec.fft else "M") if isinstance(spec, bs.MergedSpec) else \
+            ("X" if spec.mode == "synw" else "N" if spec.fft else "M") if isinstance(spec, bs.MergedSpec) else \
             "E" if spec.fft else \
             ("f" if spec.mode == "enc" and spec.ksplit > 1 else
              {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode])
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
-                       f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n}), {getattr(spec, 'waves', 4)}u}},")
+                       f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n}), {getattr(spec, 'waves', 4)}u, "
+                       f"{getattr(spec, 'n_passes', 1)}u}},")
     # the loader caches one module per table entry (qf_bs.h BsCache::kMax)
     kmax = int(re.search(r"kMax = (\d+)", (CSRC / "qf_bs.h").read_text()).group(1))
     if len(specs) > kmax:

@@ -616,7 +616,7 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
         assert nv <= 256
 
 
-def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0):
+def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0, concat=False):
     """The wave-uniform syndrome kernel (mode "synw") on the emulator for
     every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
     generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
@@ -662,7 +662,7 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
     ROWS, SYN, MAP, ZERO, OFFS, BOUND = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     # merged: every pass in one dispatch (MergedSpec), wave p of workgroup w
     # running pass p on item w
-    for spec in ([bs.merged_spec(specs)] if merged else specs):
+    for spec in ([bs.merged_spec(specs, concat)] if merged else specs):
         emu = bs.Emulator(bs.generate(spec))
         emu.add_buffer(ROWS, rows)
         emu.add_buffer(SYN, syn)
@@ -674,6 +674,15 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
                          map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
                          bound=BOUND if use_bound else 0)
         n_items = bs.launch_geometry(L, G, Lv)[2]
+        if merged and concat:   # pass-major: n 4-wave workgroups per pass
+            n = (n_items + 3) // 4
+            ka = bs.kernargs(ROWS, SYN, 0 if offs else rgs, sgs, rs, srs, L, G, 4 * n, smap=MAP,
+                             map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
+                             bound=BOUND if use_bound else 0)
+            for wg in range(spec.n_passes * n):
+                for w in range(4):
+                    emu.run_wave(ka, wg, w)
+            break
         if merged:
             ka = bs.kernargs(ROWS, SYN, 0 if offs else rgs, sgs, rs, srs, L, G, n_items, smap=MAP,
                              map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
@@ -719,12 +728,15 @@ def test_emulated_synw_kernel(oracle, k, rt, rp, L, G, offs):
     assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L, offs=offs) > 0
 
 
+@pytest.mark.parametrize("concat", [False, True])
 @pytest.mark.parametrize("k,rt,rp,L,G,offs", [(8, 6, 3, 2048, 5, False), (12, 7, 4, 2064, 4, True),
-                                               (5, 3, 1, 2200, 3, False)])
-def test_emulated_synw_merged(oracle, k, rt, rp, L, G, offs):
-    """All synw passes in one dispatch ('W'): the same syndromes, and the
-    same skips, as one launch per pass."""
-    assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L + 1, offs=offs, merged=True) > 0
+                                               (5, 3, 1, 2200, 3, False), (8, 6, 2, 4100, 9, False)])
+def test_emulated_synw_merged(oracle, k, rt, rp, L, G, offs, concat):
+    """All synw passes in one dispatch, item-major (a workgroup's waves run
+    the passes on one item) or pass-major (concat: workgroup ranges per
+    pass): the same syndromes, and the same skips, as one launch per pass."""
+    assert _synw_case(oracle, k, rt, rp, L, G, seed=k * 100 + rt + L + 1, offs=offs, merged=True,
+                      concat=concat) > 0
 
 
 @pytest.mark.parametrize("k,rt,L,G,offs", [(24, 10, 2048, 3, False), (20, 20, 2100, 2, True), (48, 21, 2064, 2, False)])
