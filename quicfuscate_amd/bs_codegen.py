@@ -443,6 +443,10 @@ class KernelSpec:
     # this pass is one block range of a pass-major MergedSpec (concat): the
     # usual prologue, with the end of the common head marked
     head_mark: bool = False
+    # cmb: every pass of the payload in one pass-major launch (the grid holds
+    # the passes' workgroup ranges; kernarg word 32 = the coefficient records'
+    # pass stride)
+    pass_major: bool = False
 
     @property
     def ahead(self) -> int:
@@ -491,7 +495,7 @@ class KernelSpec:
     @property
     def name(self) -> str:
         if self.mode == "cmb":
-            return f"qf_combine_bs_r{self.r}"
+            return f"qf_combine_bs_r{self.r}" + ("_pm" if self.pass_major else "")
         tag = {"enc": "bss" if self.ksplit > 1 else "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
             tag = "decs" if self.ksplit > 1 else "decc"
@@ -590,7 +594,7 @@ class KernelSpec:
     @property
     def kernarg_bytes(self) -> int:
         if self.mode == "cmb":
-            return KERNARG_BYTES_CMB
+            return KERNARG_BYTES_CMB + (8 if self.pass_major else 0)
         if self.mode == "synw":
             return KERNARG_BYTES_SYNW
         return KERNARG_BYTES_DEC if self.mode == "dec" else KERNARG_BYTES
@@ -2691,7 +2695,26 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
         E(Op("v_movs", (C_VM + q, CS_MASKS + q)))
     E(Op("v_movk", (C_LO, 0)))
     E(Op("v_movk", (C_HI, 0)))
+    if spec.pass_major:
+        E(Op("s_load_n", (CS_T1, 0, 1, None, KERNARG_BYTES_CMB)))   # records' pass stride
     E(Op("s_waitcnt_lgkm", ()))
+    if spec.pass_major:
+        # workgroups [p n, (p + 1) n) run pass p (n = grid waves / 4): the
+        # pass, its records and its 16 output rows, and the workgroup id in
+        # the pass's range (at most 4 passes: e <= 64)
+        # (CS_T0 holds the wave's index in its workgroup: n goes to s95)
+        E(Op("s_lshrk", (CS_TMP64 + 1, 33, 2)))
+        E(Op("s_movk", (17, 0)))
+        for _ in range(3):
+            E(Op("s_cmp_lt_br", (2, CS_TMP64 + 1, ".Lpm_done")))
+            E(Op("s_sub", (2, 2, CS_TMP64 + 1)))
+            E(Op("s_addk", (17, 17, 1)))
+            E(Op("s_add", (14, 14, CS_T1)))
+            E(Op("s_addck", (15, 15, 0)))
+            E(Op("s_lshl", (CS_TMP64, 13, 4)))
+            E(Op("s_add", (6, 6, CS_TMP64)))
+            E(Op("s_addck", (7, 7, 0)))
+        E(Op("label", (".Lpm_done",)))
     E(Op("s_lshl", (CS_ITEM, 2, 2)))
     E(Op("s_add", (CS_ITEM, CS_ITEM, CS_T0)))
     E(Op("s_andk", (CS_TBYTES, 28, 15)))            # L % 16: bytes of a partial last unit
@@ -2796,8 +2819,10 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
 
 def cmb_kernargs(rows: int, dst: int, rgs: int, dgs: int, rs: int, drs: int, coef: int, cgs: int, pas: int,
                  n_out: int, bound: int, idxtab: int, L: int, G: int, total_waves: int,
-                 rows_offs: int = 0, dst_offs: int = 0) -> tuple[bytes, int]:
-    """Kernarg block of qf_combine_bs (layout above) and the item count."""
+                 rows_offs: int = 0, dst_offs: int = 0, pass_stride: Optional[int] = None) -> tuple[bytes, int]:
+    """Kernarg block of qf_combine_bs (layout above) and the item count;
+    pass_stride: the pass-major kernel's word 32 (records of pass p at
+    coef + p pass_stride, its outputs at dst + 16 p drs)."""
     Lu = (L + 15) // 16
     Q = (Lu + 1) // 2
     ipg = (Q + 63) // 64
@@ -2807,6 +2832,8 @@ def cmb_kernargs(rows: int, dst: int, rgs: int, dgs: int, rs: int, drs: int, coe
              rs, drs, coef & MASK32, coef >> 32, cgs, pas, n_out & MASK32, n_out >> 32, bound & MASK32,
              bound >> 32, idxtab & MASK32, idxtab >> 32, rows_offs & MASK32, rows_offs >> 32,
              dst_offs & MASK32, dst_offs >> 32, L, Lu, Q, ipg, n_items, total_waves, magic, shift]
+    if pass_stride is not None:
+        words += [pass_stride, 0]
     for w in words:
         assert 0 <= w < 1 << 32, words
     return np.array(words, np.uint32).tobytes(), n_items

@@ -238,6 +238,8 @@ def kernel_specs() -> list:
     # those passes are not bound by their row reads)
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
+    # ... and every pass of it in one pass-major launch ('P', QF_ENCODE_MERGED)
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True))
     return specs
 
 
@@ -265,7 +267,7 @@ def _bs_kernels(build_dir: Path) -> Path:
             ("X" if spec.mode == "synw" else "N" if spec.fft else "M") if isinstance(spec, bs.MergedSpec) else \
             "E" if spec.fft else \
             ("f" if spec.mode == "enc" and spec.ksplit > 1 else
-             {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "m"}[spec.mode])
+             {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "P" if spec.pass_major else "m"}[spec.mode])
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n}), {getattr(spec, 'waves', 4)}u, "
                        f"{getattr(spec, 'n_passes', 1)}u}},")

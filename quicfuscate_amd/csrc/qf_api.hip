@@ -683,7 +683,11 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
             QF_CHECK_HIP(qf::launch_xor_repairs(ga, ctx->num_cus, st));
             prof_end(ctx, st, ev, "k_xor_repairs");
         }
-        for (uint32_t p = 0; p < passes; ++p) {
+        // every pass in one pass-major launch (QF_ENCODE_MERGED, the
+        // bit-sliced payload kernel): one pass's last, partly filled round of
+        // workgroups overlaps the next pass's first
+        bool pm = false;
+        for (uint32_t p = 0; p < passes && !pm; ++p) {
             qf::CombineSlotsArgs a{};
             a.rows = w + off_syn;
             a.rows_gen_stride = (uint64_t)r * Lp;
@@ -704,7 +708,14 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
             a.total_units = (uint64_t)Gc * Lu;
             ev = prof_begin(ctx, st);
             std::string cname;
-            QF_CHECK_HIP(combine_payload(ctx, a, PD, st, &cname));
+            pm = p == 0 && passes > 1 && ctx->opt[QF_OPT_ENCODE_MERGED] && qf::cmb_pass_major_available() &&
+                 (uint64_t)G * cgs < (1ull << 32) && combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
+            if (pm) {
+                cname = "qf_combine_bs_r16_pm";
+                QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx, passes, (uint64_t)G * cgs));
+            } else {
+                QF_CHECK_HIP(combine_payload(ctx, a, PD, st, &cname));
+            }
             prof_end(ctx, st, ev, cname);
         }
     }
@@ -1538,7 +1549,8 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
     prof_end(ctx, ctx->stream, ev, "k_decode_prepare");
     if (int gs = payload_gate(ctx, ctx->stream)) return gs;
     const uint32_t Lu = (L + 15) / 16;
-    for (uint32_t p = 0; p < passes; ++p) {
+    bool pm = false;   // every pass in one pass-major launch, as in decode_cauchy_syn
+    for (uint32_t p = 0; p < passes && !pm; ++p) {
         qf::CombineSlotsArgs a{};
         a.rows = rows;
         a.rows_gen_stride = sh->rows_gen_stride;
@@ -1561,7 +1573,16 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         const int PD = pick_PD(ctx, QF_OPT_DECODE_PD, 1);
         hipEvent_t ev2 = prof_begin(ctx, ctx->stream);
         std::string cname;
-        QF_CHECK_HIP(combine_payload(ctx, a, PD, ctx->stream, &cname));
+        pm = p == 0 && passes > 1 && ctx->opt[QF_OPT_ENCODE_MERGED] && qf::cmb_pass_major_available() &&
+             (uint64_t)G * coef_gen_stride < (1ull << 32) &&
+             combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
+        if (pm) {
+            cname = "qf_combine_bs_r16_pm";
+            QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, ctx->stream, a, ctx->d_cmbidx, passes,
+                                        (uint64_t)G * coef_gen_stride));
+        } else {
+            QF_CHECK_HIP(combine_payload(ctx, a, PD, ctx->stream, &cname));
+        }
         prof_end(ctx, ctx->stream, ev2, cname);
     }
     return QF_OK;

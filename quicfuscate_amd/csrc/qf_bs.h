@@ -76,9 +76,13 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // 256 x 64-byte plane-index table (bs_codegen.cmb_index_table).  Rows are
 // read in whole 16-byte units (the unit holding byte L - 1 too); only bytes
 // [0, L) of the output rows are written.
+// passes > 1: every pass in one pass-major launch (qf_combine_bs_r16_pm):
+// pass p takes the records at a.coef + p * pass_stride and writes output rows
+// 16 p .. of each generation (a.pass must be 0).
 bool cmb_available();
+bool cmb_pass_major_available();
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
-                      const uint32_t* idxtab);
+                      const uint32_t* idxtab, uint32_t passes = 1, uint64_t pass_stride = 0);
 void bs_unload(BsCache& cache);
 
 }  // namespace qf

@@ -330,12 +330,14 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // Bit-sliced payload pass (bs_codegen.py "cmb", mode 'm'): one generation
 // per item, wave-uniform coefficients (kernarg layout: bs_codegen.cmb_kernargs)
 bool cmb_available() { return find('m', 0, 16) != nullptr; }
+bool cmb_pass_major_available() { return find('P', 0, 16) != nullptr; }
 
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
-                      const uint32_t* idxtab) {
-    const QfBsEntry* e = find('m', 0, 16);
+                      const uint32_t* idxtab, uint32_t passes, uint64_t pass_stride) {
+    const QfBsEntry* e = find(passes > 1 ? 'P' : 'm', 0, 16);
     if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || a.dst_row_stride >= (1ull << 32) ||
-        a.coef_gen_stride >= (1ull << 32))
+        a.coef_gen_stride >= (1ull << 32) || passes == 0 || passes > 4 || pass_stride >= (1ull << 32) ||
+        (passes > 1 && a.pass != 0))
         return bs_invalid(__LINE__);
     const int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return bs_invalid(__LINE__);
@@ -358,16 +360,19 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     if (blocks > cap) blocks = cap;
     auto lo = [](const void* p) { return (uint32_t)(uintptr_t)p; };
     auto hi = [](const void* p) { return (uint32_t)((uintptr_t)p >> 32); };
-    uint32_t w[32] = {lo(a.rows), hi(a.rows), lo(a.dst), hi(a.dst),
+    uint32_t w[34] = {lo(a.rows), hi(a.rows), lo(a.dst), hi(a.dst),
                       (uint32_t)a.rows_gen_stride, (uint32_t)(a.rows_gen_stride >> 32),
                       (uint32_t)a.dst_gen_stride, (uint32_t)(a.dst_gen_stride >> 32),
                       (uint32_t)a.row_stride, (uint32_t)a.dst_row_stride, lo(a.coef), hi(a.coef),
                       (uint32_t)a.coef_gen_stride, a.pass, lo(a.n_out), hi(a.n_out), lo(a.bound), hi(a.bound),
                       lo(idxtab), hi(idxtab), lo(a.rows_offs), hi(a.rows_offs), lo(a.dst_offs), hi(a.dst_offs),
-                      a.L, Lu, Q, ipg, (uint32_t)n_items, (uint32_t)blocks * 4, magic, shift};
-    size_t sz = sizeof(w);
+                      a.L, Lu, Q, ipg, (uint32_t)n_items, (uint32_t)blocks * 4, magic, shift,
+                      (uint32_t)pass_stride, 0};
+    // (pass-major: words 32..33 = the records' pass stride; the grid holds
+    // every pass's `blocks` workgroups, pass p's at [p blocks, (p + 1) blocks))
+    size_t sz = passes > 1 ? sizeof(w) : 32 * sizeof(uint32_t);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, w, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks * passes, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
 void bs_unload(BsCache& cache) {

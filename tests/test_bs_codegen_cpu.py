@@ -908,6 +908,64 @@ def test_emulated_combine_bs(L, G, seed, pas, offs):
     assert _cmb_case(L, G, seed, pas, offs) == 0
 
 
+@pytest.mark.parametrize("L,G,P,offs", [(1200, 5, 3, False), (4100, 3, 2, True), (100, 9, 4, False)])
+def test_emulated_combine_bs_pass_major(L, G, P, offs):
+    """Every payload pass in one launch (qf_combine_bs_r16_pm): workgroup
+    range p runs pass p with its records at coef + p * pass_stride and its
+    outputs at rows 16 p ..; generations with fewer outputs leave the later
+    passes' rows untouched."""
+    global _GFT
+    if _GFT is None:
+        _GFT = _gf_table()
+    rng = np.random.default_rng(L + G + P)
+    spec = bs.KernelSpec(0, 16, mode="cmb", pass_major=True)
+    Lp = (L + 15) // 16 * 16
+    rs, drs = Lp + 32, Lp + 48
+    nslot = 16 * P + 4
+    rgs, dgs = nslot * rs + 16, 16 * P * drs + 32
+    cgs = (nslot + 1) * 16
+    PS = G * cgs + 64                       # the records' pass stride
+    rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
+    rec = rng.integers(0, 256, P * PS, dtype=np.uint8)
+    e = rng.integers(1, 16 * P + 1, G).astype(np.uint32)
+    bound = rng.integers(1, nslot + 1, G).astype(np.uint32)
+    e[0] = 16 * P
+    out = np.full(G * dgs, 0xEE, np.uint8)
+    ROWS, OUT, REC, NO, BD, TAB, T1, T2 = (0x10000000, 0x40000000, 0x50000000, 0x60000000, 0x61000000,
+                                           0x62000000, 0x63000000, 0x64000000)
+    emu = bs.Emulator(bs.generate(spec))
+    so = do = 0
+    rgs_k, dgs_k = rgs, dgs
+    if offs:
+        emu.add_buffer(T1, np.array([(G - 1 - g) * rgs for g in range(G)], np.uint64).view(np.uint8))
+        emu.add_buffer(T2, np.array([(G - 1 - g) * dgs for g in range(G)], np.uint64).view(np.uint8))
+        so, do, rgs_k, dgs_k = T1, T2, 0, 0
+    for base, buf in ((ROWS, rows), (OUT, out), (REC, rec), (NO, e), (BD, bound),
+                      (TAB, bs.cmb_index_table().reshape(-1).view(np.uint8))):
+        emu.add_buffer(base, buf.view(np.uint8))
+    n = 2                                   # workgroups per pass (persistent: items stride 8 waves)
+    ka, n_items = bs.cmb_kernargs(ROWS, OUT, rgs_k, dgs_k, rs, drs, REC, cgs, 0, NO, BD, TAB, L, G, 4 * n,
+                                  rows_offs=so, dst_offs=do, pass_stride=PS)
+    for wg in range(P * n):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        gr = (G - 1 - g) if offs else g
+        blk = out[gr * dgs:(gr + 1) * dgs]
+        for j in range(16 * P):
+            row = blk[j * drs:(j + 1) * drs]
+            if j < e[g]:
+                p, jj = divmod(j, 16)
+                want = np.zeros(L, np.uint8)
+                for sl in range(int(bound[g])):
+                    c = rec[p * PS + g * cgs + 16 * sl + jj]
+                    want ^= _GFT[c][rows[gr * rgs + sl * rs: gr * rgs + sl * rs + L]]
+                assert (row[:L] == want).all(), (g, j)
+                assert (row[L:] == 0xEE).all(), (g, j)
+            else:
+                assert (row == 0xEE).all(), (g, j)
+
+
 # --------------------------------------------------------------------------
 # Additive-FFT row loop (lch_fft.py, KernelSpec.fft)
 # --------------------------------------------------------------------------
