@@ -145,10 +145,12 @@ enum {
     QF_OPT_PREPARE_LANES,        /* 1: the fused decode's acceptance pass runs one generation per lane
                                     (k_decode_prepare_lu_lanes); 0: one per wave [QF_PREPARE_LANES;
                                     default 1] */
-    QF_OPT_ENCODE_MERGED,        /* 1: the encode passes of a code with more repairs than one kernel
-                                    holds (C5 r > 22) run in ONE dispatch, a workgroup's waves
-                                    running the passes on the same item (each source row read from
-                                    HBM once); 0: one launch per pass [QF_ENCODE_MERGED; default 1] */
+    QF_OPT_ENCODE_MERGED,        /* 1: multi-pass work in ONE dispatch each: the encode passes of a
+                                    code with more repairs than one kernel holds (C5 r > 22; a
+                                    workgroup's waves run the passes on one item, so each source row
+                                    is read from HBM once), and the decode's syndrome and payload
+                                    passes (pass-major workgroup ranges); 0: one launch per pass
+                                    [QF_ENCODE_MERGED; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);
