@@ -145,6 +145,9 @@ def parse(argv=None):
                     help="(default) decode acceptance pass on a 2nd stream beside the encode, payload pass after it")
     ap.add_argument("--serial", dest="split", action="store_false",
                     help="encode, then the whole decode, on one stream")
+    ap.add_argument("--payload-stream", action="store_true",
+                    help="split, with the decode's payload pass enqueued on the encode's stream "
+                         "(qf_ctx_set_payload_stream) instead of waiting for it across streams")
     a = ap.parse_args(argv)
     if a.overlap:
         a.split = False
@@ -294,14 +297,16 @@ def main(argv=None):
             s_dec.wait_event(e0)
         encode()
         e_enc.record(s_enc)
-        if args.split:
+        if args.split and args.payload_stream:
+            ctx_dec.set_payload_stream(stream)     # payload pass after the encode, same stream
+        elif args.split:
             ctx_dec.set_payload_wait(e_enc)
         decode()
-        e_dec.record(s_dec)
+        e_dec.record(stream if args.payload_stream else s_dec)
         if args.overlap:
             stream.wait_event(e_enc)
             stream.wait_event(e_dec)
-        if args.split:
+        if args.split and not args.payload_stream:
             stream.wait_event(e_dec)
         e1.record(stream)
 
@@ -561,7 +566,9 @@ def main(argv=None):
         # the encode kernel BASELINE.json's north star targets (>= 70 % HBM)
         "roofline_encode": roofline_encode() if enc_kernel else None,
         "streams": ("encode || decode (2 HIP streams)" if args.overlap else
-                    "encode, then decode payload pass; decode acceptance pass on a 2nd stream beside the encode"
+                    ("encode, then decode payload pass on the same stream (qf_ctx_set_payload_stream); decode "
+                     "acceptance pass on a 2nd stream beside the encode" if args.payload_stream else
+                     "encode, then decode payload pass; decode acceptance pass on a 2nd stream beside the encode")
                     if args.split else "encode then decode (1 stream)"),
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,

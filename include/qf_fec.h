@@ -82,6 +82,16 @@ void *qf_ctx_stream(qf_ctx *ctx);
  * NULL clears it.  No reference counterpart beyond the add_packet /
  * try_decode split. */
 int qf_ctx_set_payload_wait(qf_ctx *ctx, void *event);
+/* Split-phase decode on two streams.  The next qf_decode_batch on ctx keeps
+ * its acceptance pass on the context's stream and enqueues its payload pass
+ * on `stream` (a hipStream_t; QF_STREAM_NULL = the null stream) after it, so
+ * a caller whose rows are produced on `stream` needs no cross-stream wait
+ * before the payload and none after it: the call's work is complete when
+ * `stream` reaches that point.  Combines with qf_ctx_set_payload_wait.  The
+ * fused decode runs its payload kernel on `stream`; the other decode paths
+ * finish on the context's stream and `stream` waits for them.  Cleared when
+ * that qf_decode_batch returns; NULL clears it. */
+int qf_ctx_set_payload_stream(qf_ctx *ctx, void *stream);
 int qf_sync(qf_ctx *ctx);
 
 /* Kernel-path options of a context.  No reference counterpart: the

@@ -106,6 +106,7 @@ _SIGS = {
     "qf_ctx_set_stream": (_I, [_P, _P]),
     "qf_ctx_stream": (_P, [_P]),
     "qf_ctx_set_payload_wait": (_I, [_P, _P]),
+    "qf_ctx_set_payload_stream": (_I, [_P, _P]),
     "qf_sync": (_I, [_P]),
     "qf_ctx_profile": (_I, [_P, _I]),
     "qf_ctx_set_option": (_I, [_P, _I, ctypes.c_int64]),

@@ -65,6 +65,13 @@ struct qf_ctx {
     std::map<std::pair<uint32_t, uint32_t>, uint8_t*> small_coef;
     // qf_ctx_set_payload_wait: event the next decode's payload pass waits for
     hipEvent_t payload_wait = nullptr;
+    // qf_ctx_set_payload_stream: the stream the next decode's payload pass
+    // runs on (has_payload_stream), the acceptance pass's completion event,
+    // and whether the decode path launched its payload there itself
+    hipStream_t payload_stream = nullptr;
+    bool has_payload_stream = false;
+    bool payload_on_stream = false;
+    hipEvent_t ev_accept = nullptr;
     // heterogeneous batch API (qf_*_batch_desc): the generation offset tables
     // of the class being launched (nullptr: strided generations) and the
     // device / pinned buffers holding a call's per-generation metadata
@@ -548,12 +555,20 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     hipEvent_t ev = prof_begin(ctx, st);
     QF_CHECK_HIP(qf::launch_decode_prepare_cauchy(pa, st));
     prof_end(ctx, st, ev, "k_decode_prepare_lu");
-    if (int gs = payload_gate(ctx, st)) return gs;
-    ev = prof_begin(ctx, st);
-    QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, st, k, r, rows, rec, sh->rows_gen_stride,
+    hipStream_t ps = st;
+    if (ctx->has_payload_stream) {   // qf_ctx_set_payload_stream: the payload pass on the caller's stream
+        if (!ctx->ev_accept) QF_CHECK_HIP(hipEventCreateWithFlags(&ctx->ev_accept, hipEventDisableTiming));
+        QF_CHECK_HIP(hipEventRecord(ctx->ev_accept, st));
+        ps = ctx->payload_stream;
+        QF_CHECK_HIP(hipStreamWaitEvent(ps, ctx->ev_accept, 0));
+        ctx->payload_on_stream = true;
+    }
+    if (int gs = payload_gate(ctx, ps)) return gs;
+    ev = prof_begin(ctx, ps);
+    QF_CHECK_HIP(qf::dec_launch(ctx->bs, ctx->num_cus, ps, k, r, rows, rec, sh->rows_gen_stride,
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
                                 ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
-    prof_end(ctx, st, ev, qf::dec_name(&ctx->bs, k, r, L, G, ctx->num_cus));
+    prof_end(ctx, ps, ev, qf::dec_name(&ctx->bs, k, r, L, G, ctx->num_cus));
     return QF_OK;
 }
 
@@ -1159,6 +1174,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->d_desc) hipFree(c->d_desc);
     if (c->h_desc) hipHostFree(c->h_desc);
     if (c->desc_done) hipEventDestroy(c->desc_done);
+    if (c->ev_accept) hipEventDestroy(c->ev_accept);
     for (hipEvent_t e : c->send_ev) hipEventDestroy(e);
     if (c->recv_done) {
         hipEventSynchronize(c->recv_done);
@@ -1353,10 +1369,28 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
                     const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
                     uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
     if (!ctx) return QF_EINVAL;
-    const int s = decode_batch_impl(ctx, sh, G, rows, row_index, n_rows, row_coeffs, rec, rec_index, n_rec, status);
+    int s = decode_batch_impl(ctx, sh, G, rows, row_index, n_rows, row_coeffs, rec, rec_index, n_rec, status);
     std::lock_guard<std::mutex> g(ctx->mu);
+    if (ctx->has_payload_stream && !ctx->payload_on_stream) {
+        // a path that finished on the context's stream: the caller's stream waits for it
+        hipError_t e = hipSuccess;
+        if (!ctx->ev_accept) e = hipEventCreateWithFlags(&ctx->ev_accept, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(ctx->ev_accept, ctx->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->payload_stream, ctx->ev_accept, 0);
+        if (e != hipSuccess && s == QF_OK) s = QF_EDEVICE;
+    }
     ctx->payload_wait = nullptr;  // one decode call only, whatever its outcome
+    ctx->has_payload_stream = ctx->payload_on_stream = false;
     return s;
+}
+
+int qf_ctx_set_payload_stream(qf_ctx* ctx, void* stream) {
+    if (!ctx) return QF_EINVAL;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->has_payload_stream = stream != nullptr;
+    ctx->payload_stream = stream == QF_STREAM_NULL ? nullptr : reinterpret_cast<hipStream_t>(stream);
+    ctx->payload_on_stream = false;
+    return QF_OK;
 }
 
 int qf_ctx_set_payload_wait(qf_ctx* ctx, void* event) {

@@ -125,6 +125,18 @@ class Context:
         h = event if (event is None or isinstance(event, int)) else event.cuda_event
         check(L._lib().qf_ctx_set_payload_wait(self.handle, ctypes.c_void_p(h)), "payload_wait")
 
+    def set_payload_stream(self, stream) -> None:
+        """qf_ctx_set_payload_stream: the next decode_batch keeps its
+        acceptance pass on this context's stream and runs its payload pass on
+        `stream` (a torch.cuda.Stream or a raw hipStream_t; torch's default
+        stream maps to the null stream; None clears)."""
+        if stream is None:
+            h = None
+        else:
+            h = stream if isinstance(stream, int) else stream.cuda_stream
+            h = h or QF_STREAM_NULL
+        check(L._lib().qf_ctx_set_payload_stream(self.handle, ctypes.c_void_p(h)), "payload_stream")
+
     def sync(self) -> None:
         check(L._lib().qf_sync(self.handle), "sync")
 

@@ -339,6 +339,55 @@ def test_decode_payload_wait_orders_the_rows_copy(qf, oracle, gpu_ctx, path, mon
     del big_a, big_b
 
 
+@pytest.mark.parametrize("k,r,L,G", [(64, 16, 1200, 3000), (20, 9, 200, 50), (128, 39, 9000, 24)])
+def test_decode_payload_stream(qf, oracle, gpu_ctx, k, r, L, G):
+    """qf_ctx_set_payload_stream: the acceptance pass stays on the context's
+    stream, the payload pass (or, for paths that finish on the context's
+    stream, a wait for them) is enqueued on the caller's stream, so work
+    queued on that stream afterwards sees the recovered rows with no other
+    synchronisation.  The setting holds for one decode call."""
+    import torch
+
+    max_rows = k + r
+    rng = np.random.default_rng(k + r + L)
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, erase=min(r, max(1, k // 5)))
+    rs, emax = _r16(L), min(k, r)
+    rgs, rec_gs = max_rows * rs, emax * rs
+    rows = np.zeros(G * rgs, np.uint8)
+    ridx = np.zeros((G, max_rows), np.uint16)
+    nrows = np.zeros(G, np.uint32)
+    for g, (arr, rw, _) in enumerate(gens):
+        nrows[g] = len(arr)
+        ridx[g, : len(arr)] = arr
+        for s in range(len(arr)):
+            rows[g * rgs + s * rs: g * rgs + s * rs + L] = rw[s]
+    t_rows = torch.from_numpy(rows).cuda()
+    t_idx = torch.from_numpy(ridx.view(np.int16)).cuda()
+    t_n = torch.from_numpy(nrows.view(np.int32)).cuda()
+    t_rec = torch.zeros(G * rec_gs, dtype=torch.uint8, device="cuda")
+    t_recidx = torch.zeros(G * emax, dtype=torch.int16, device="cuda")
+    t_nrec = torch.zeros(G, dtype=torch.int32, device="cuda")
+    t_status = torch.full((G,), 77, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    ctx = qf.Context(0, torch.cuda.Stream().cuda_stream)     # the acceptance pass's own stream
+    try:
+        ctx.set_payload_stream(side)
+        qf.decode_batch(t_rows, t_idx, t_rec, t_recidx, t_nrec, t_status, k, r, L, max_rows=max_rows,
+                        row_stride=rs, rows_gen_stride=rgs, rec_row_stride=rs, rec_gen_stride=rec_gs,
+                        G=G, n_rows=t_n, ctx=ctx)
+        with torch.cuda.stream(side):      # ordered after the decode by the library alone
+            snap = [t.clone() for t in (t_rec, t_recidx, t_nrec, t_status)]
+        side.synchronize()
+        out = (snap[0].cpu().numpy(), snap[1].cpu().numpy().view(np.uint16).reshape(G, -1),
+               snap[2].cpu().numpy(), snap[3].cpu().numpy(), rs, rec_gs)
+        assert (out[3] == 0).all()
+        check(oracle, k, L, src, gens, out, False)
+        ctx.sync()
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("k,r,L,G,pin", [(64, 16, 1200, 2000, True), (16, 16, 100, 37, False),
                                          (96, 15, 9000, 120, True)])
