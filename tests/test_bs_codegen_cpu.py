@@ -1060,6 +1060,32 @@ def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs, es, ld
                      lds_rows=lds, **lib4) == 0
 
 
+@pytest.mark.parametrize("k,rt,R", [(128, 39, 16), (160, 48, 16), (196, 59, 16), (128, 20, 16), (24, 10, 16),
+                                    (255, 1, 16), (17, 200, 16), (160, 48, 8), (100, 30, 8)])
+def test_hybrid_plans_equal_cauchy(k, rt, R):
+    """Every coset pass of a (k, r) code (lch_fft.coset_passes / hybrid_plan:
+    sources [0, 2^a) through the FFT at the pass's coset, the rest direct)
+    evaluates to the reference's repairs p_j = sum_i inv(i ^ (k + j)) x_i
+    (decoder.rs:280-298) on random bytes; the passes tile 0 .. r - 1."""
+    import random
+
+    from quicfuscate_amd import lch_fft
+
+    passes = lch_fft.coset_passes(k, rt, R)
+    assert passes[0][0] == 0 and sum(n for _, n in passes) == rt
+    assert all(j0 + n == j1 for (j0, n), (j1, _) in zip(passes, passes[1:]))
+    rng = random.Random(k * 1000 + rt)
+    for j0, n in passes:
+        p = lch_fft.hybrid_plan(k, rt, j0, n, 8, R, check=0)
+        for _ in range(3):
+            xs = [rng.randrange(256) for _ in range(k)]
+            want = [0] * n
+            for j in range(n):
+                for i in range(k):
+                    want[j] ^= bs.gf_mul(bs.gf_inv(i ^ (k + j0 + j)), xs[i])
+            assert p.evaluate(xs) == want, (j0, n)
+
+
 @pytest.mark.parametrize("k,rt,L,G", [(24, 10, 200, 3), (20, 20, 72, 2), (48, 21, 64, 2), (160, 48, 40, 1)])
 def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
     """Codes the plain additive-FFT plan does not cover (k not a power of
