@@ -90,7 +90,8 @@ int qf_ctx_set_payload_wait(qf_ctx *ctx, void *event);
  * `stream` reaches that point.  Combines with qf_ctx_set_payload_wait.  The
  * fused decode runs its payload kernel on `stream`; the other decode paths
  * finish on the context's stream and `stream` waits for them.  Cleared when
- * that qf_decode_batch returns; NULL clears it. */
+ * that qf_decode_batch returns; NULL clears it.  qf_decode_batch_host and
+ * qf_decode_batch_desc clear it and run on the context's stream. */
 int qf_ctx_set_payload_stream(qf_ctx *ctx, void *stream);
 int qf_sync(qf_ctx *ctx);
 

@@ -1417,6 +1417,10 @@ int qf_decode_batch_host(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, con
                          const uint16_t* row_index, const uint32_t* n_rows, const uint8_t* row_coeffs,
                          uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec, int32_t* status) {
     if (!ctx || !sh) return QF_EINVAL;
+    {   // qf_ctx_set_payload_stream applies to qf_decode_batch only
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->has_payload_stream = ctx->payload_on_stream = false;
+    }
     const uint32_t k = sh->k, r = sh->r, L = sh->L, mr = sh->max_rows;
     if (k == 0 || k > 256 || mr == 0 || mr > 4096 || L == 0) return QF_EINVAL;
     if (G == 0) return QF_OK;
@@ -1767,6 +1771,10 @@ int qf_decode_batch_desc(qf_ctx* ctx, const qf_dec_desc* gens, uint32_t G, const
                          const uint16_t* row_index, uint8_t* rec, uint16_t* rec_index, uint32_t* n_rec,
                          int32_t* status) {
     if (!ctx) return QF_EINVAL;
+    {   // qf_ctx_set_payload_stream applies to qf_decode_batch only
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->has_payload_stream = ctx->payload_on_stream = false;
+    }
     if (G == 0) return QF_OK;
     if (!gens || !rows || !row_index || !n_rec || !status || !aligned16(rows)) return QF_EINVAL;
     typedef std::tuple<uint32_t, uint32_t, uint32_t, uint64_t, uint64_t> Key;
