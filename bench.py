@@ -145,9 +145,11 @@ def parse(argv=None):
                     help="(default) decode acceptance pass on a 2nd stream beside the encode, payload pass after it")
     ap.add_argument("--serial", dest="split", action="store_false",
                     help="encode, then the whole decode, on one stream")
-    ap.add_argument("--payload-stream", action="store_true",
-                    help="split, with the decode's payload pass enqueued on the encode's stream "
+    ap.add_argument("--payload-stream", action="store_true", default=True,
+                    help="(default) split, with the decode's payload pass enqueued on the encode's stream "
                          "(qf_ctx_set_payload_stream) instead of waiting for it across streams")
+    ap.add_argument("--cross-stream", dest="payload_stream", action="store_false",
+                    help="split, with the payload pass on the decode's stream waiting for the encode's event")
     a = ap.parse_args(argv)
     if a.overlap:
         a.split = False
@@ -302,7 +304,7 @@ def main(argv=None):
         elif args.split:
             ctx_dec.set_payload_wait(e_enc)
         decode()
-        e_dec.record(stream if args.payload_stream else s_dec)
+        e_dec.record(stream if (args.split and args.payload_stream) else s_dec)
         if args.overlap:
             stream.wait_event(e_enc)
             stream.wait_event(e_dec)

@@ -364,7 +364,7 @@ def test_decode_payload_stream(qf, oracle, gpu_ctx, k, r, L, G):
     t_rows = torch.from_numpy(rows).cuda()
     t_idx = torch.from_numpy(ridx.view(np.int16)).cuda()
     t_n = torch.from_numpy(nrows.view(np.int32)).cuda()
-    t_rec = torch.zeros(G * rec_gs, dtype=torch.uint8, device="cuda")
+    t_rec = torch.full((G * rec_gs,), 0x5A, dtype=torch.uint8, device="cuda")   # check(): bytes past L stay 0x5A
     t_recidx = torch.zeros(G * emax, dtype=torch.int16, device="cuda")
     t_nrec = torch.zeros(G, dtype=torch.int32, device="cuda")
     t_status = torch.full((G,), 77, dtype=torch.int32, device="cuda")
