@@ -1220,7 +1220,7 @@ class MergedSpec:
     @property
     def name(self) -> str:
         if self.mode == "synw":
-            return f"qf_cauchy_synw{'c' if self.concat else 'm'}_k{self.k}_r{self.rt}"
+            return f"qf_cauchy_synw{'c' if self.concat else 'm'}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
         return f"qf_cauchy_bsm{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
 
     @property

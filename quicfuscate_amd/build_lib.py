@@ -44,7 +44,11 @@ BS_FFT = [(64, 16), (64, 10), (32, 16), (16, 16)]
 # (lch_fft.hybrid_plan: one pass per coset of 16 repair points, sources
 # [0, 2^a) through the FFT, the rest folded in directly), merged ('N')
 BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
-BS_FFT_SYNW = [(128, 39)]
+# pass-major FFT synw ('Y') where its passes that run at 20 % loss cost less
+# than the plain ones (tools/gpu_r04_c5y.sh, profiles/r04al_c5_hybrid_chunks.json:
+# block decode (128, 39) 1,470 -> 1,784 GiB/s, (160, 48) 1,536 -> 1,700;
+# (196, 59) 1,383 -> 1,262: three FFT passes run against two plain ones)
+BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
@@ -211,20 +215,17 @@ def kernel_specs() -> list:
     for k, rt in BS_FFT_PASSES:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
                                      for j0, rp in lch_fft.coset_passes(k, rt)]))
-    # additive-FFT synw passes ('V', QF_FFT_KERNELS): one per coset of 16
-    # repair points, as the 'N' encode; where they cut the time of the passes
-    # that run at 20 % loss: (128, 39) 0.506 -> 0.388 ms; (160, 48) 0.489 ms
-    # either way; (196, 59) would run 3 FFT passes against 2 plain
-    # (tools/gpu_r04_c5v.sh, profiles/r04ac_c5_synw_fft.json)
+    # the synw passes of the C5 codes in one pass-major dispatch: one launch
+    # of P x n workgroups instead of P launches of n, so a pass's last, partly
+    # filled round overlaps the next pass's first; 'Y' the additive-FFT passes
+    # (one per coset of 16 repair points, as the 'N' encode; QF_FFT_KERNELS),
+    # 'X' the plain ones
     for k, rt in BS_FFT_SYNW:
-        specs += [bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
-                  for j0, rp in lch_fft.coset_passes(k, rt)]
-    # the plain synw passes of the other C5 codes in one pass-major dispatch
-    # ('X'): one launch of P x n workgroups instead of P launches of n, so a
-    # pass's last, partly filled round overlaps the next pass's first
+        specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt,
+                                                   j0=j0) for j0, rp in lch_fft.coset_passes(k, rt)], concat=True))
     for k, rt in BS_ENC_ONLY:
         npass = -(-rt // BS_PASS)
-        if npass == 1 or (k, rt) in BS_FFT_SYNW:
+        if npass == 1:
             continue
         j0, passes = 0, []
         for p in range(npass):
@@ -262,12 +263,16 @@ def _bs_kernels(build_dir: Path) -> Path:
         hashes[spec.name] = hashlib.sha256(data).hexdigest()[:16]
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
-        mode = ("C" if spec.fft else "k" if spec.ksplit > 1 else "c") if spec.chunked else \
-            "V" if spec.mode == "synw" and spec.fft else \
-            ("X" if spec.mode == "synw" else "N" if spec.fft else "M") if isinstance(spec, bs.MergedSpec) else \
-            "E" if spec.fft else \
-            ("f" if spec.mode == "enc" and spec.ksplit > 1 else
-             {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "P" if spec.pass_major else "m"}[spec.mode])
+        if isinstance(spec, bs.MergedSpec):
+            mode = ("Y" if spec.fft else "X") if spec.mode == "synw" else ("N" if spec.fft else "M")
+        elif spec.chunked:
+            mode = "C" if spec.fft else "k" if spec.ksplit > 1 else "c"
+        elif spec.fft:
+            mode = "E"
+        elif spec.mode == "enc" and spec.ksplit > 1:
+            mode = "f"
+        else:
+            mode = {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "P" if spec.pass_major else "m"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n}), {getattr(spec, 'waves', 4)}u, "
                        f"{getattr(spec, 'n_passes', 1)}u}},")

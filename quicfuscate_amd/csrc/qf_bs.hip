@@ -22,8 +22,7 @@ struct QfBsEntry {
                 // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves,
                 // 'f' the encode (passes of C5 codes) with an item's sources split the same way,
                 // 'M' / 'N' every encode pass of a code in one dispatch (plain / additive-FFT passes),
-                // 'V' the 'w' syndrome passes through the additive FFT,
-                // 'X' every 'w' pass in one pass-major dispatch
+                // 'X' / 'Y' every 'w' pass in one pass-major dispatch (plain / additive-FFT passes)
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -179,7 +178,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
     a[ot + 3] = (uint32_t)((uintptr_t)dst_offs >> 32);
     size_t sz = (size_t)(ot + 4) * 4;
-    if (e->mode == 'w' || e->mode == 'V' || e->mode == 'X') {   // per-generation pass bound (KERNARG_BYTES_SYNW)
+    if (e->mode == 'w' || e->mode == 'X' || e->mode == 'Y') {   // per-generation pass bound (KERNARG_BYTES_SYNW)
         a[24] = (uint32_t)(uintptr_t)bound;
         a[25] = (uint32_t)((uintptr_t)bound >> 32);
         sz = 26 * 4;
@@ -187,7 +186,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                    HIP_LAUNCH_PARAM_END};
     // 'X': the grid holds every pass's `blocks` workgroups, pass-major
-    const uint32_t grid = blocks * (e->mode == 'X' ? e->passes : 1u);
+    const uint32_t grid = blocks * (e->mode == 'X' || e->mode == 'Y' ? e->passes : 1u);
     const hipError_t err = hipModuleLaunchKernel(cache.fn[idx], grid, 1, 1, 64 * e->waves, 1, 1, 0, st, nullptr, cfg);
     if (err != hipSuccess && getenv("QF_BS_DEBUG"))
         fprintf(stderr, "%s: hipModuleLaunchKernel %d (%u blocks x %u)\n", e->name, (int)err, blocks, 64 * e->waves);
@@ -264,10 +263,11 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
     // an item (128 units) must lie in at most two generations
     const uint32_t Lv = bs_padded_units(L);
     if (Lv < 128 || srs < 16ull * Lv) return bs_invalid(__LINE__);
-    // the additive-FFT passes ('V') where generated, unless QF_FFT_KERNELS=0;
-    // else the passes in one pass-major dispatch ('X') unless QF_ENCODE_MERGED=0
-    const char mode = cache.get(QF_OPT_FFT_KERNELS) && find('V', k, r) ? 'V'
-                      : cache.get(QF_OPT_ENCODE_MERGED) && find('X', k, r) ? 'X' : 'w';
+    // the passes in one pass-major dispatch unless QF_ENCODE_MERGED=0: the
+    // additive-FFT ones ('Y') unless QF_FFT_KERNELS=0, else the plain ones ('X')
+    const bool merged = cache.get(QF_OPT_ENCODE_MERGED);
+    const char mode = merged && cache.get(QF_OPT_FFT_KERNELS) && find('Y', k, r) ? 'Y'
+                      : merged && find('X', k, r) ? 'X' : 'w';
     for (const auto& e : qf_bs_table) {
         if (e.mode != mode || e.k != k || e.rt != r) continue;
         hipError_t err = launch(cache, &e, num_cus, st, rows, syn + (uint64_t)e.j0 * srs, rgs, sgs, rs, srs, L, G, Lv,

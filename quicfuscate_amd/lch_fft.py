@@ -314,8 +314,17 @@ class HybridPlan(Plan):
         return [e[self.out_block[j]] for j in range(self.r)]
 
 
-def hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int = 8, R: int = 16, check: int = 8) -> HybridPlan:
-    """The pass j0 .. j0 + r - 1 of the (k, rt) code (module note above)."""
+def hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int = 8, R: int = 16, check: int = 8,
+                extra_chunks: bool = True) -> HybridPlan:
+    """The pass j0 .. j0 + r - 1 of the (k, rt) code (module note above).
+
+    extra_chunks: rows [2^a, k) in whole chunks also go through a chunk
+    transform, at their own points (twiddles xhat(q, i)); a chunk output's
+    accumulator constants are the chunk rows' direct columns pulled through
+    the chunk's inverse (computed numerically, so any invertible chunk map is
+    exact; at the translated points 2^a + V_c they are as sparse as the first
+    block's: 2 accumulators per output instead of 16 per direct row).  Each
+    chunk is taken only where it costs fewer plane ops than its direct rows."""
     a = k.bit_length() - 1
     kA = 1 << a
     b, c = _log2(R), _log2(ch)
@@ -404,7 +413,40 @@ def hybrid_plan(k: int, rt: int, j0: int, r: int, ch: int = 8, R: int = 16, chec
         d = final_inverse(w)
         direct[i] = [(t, d[t]) for t in range(R) if d[t]]
 
-    p = HybridPlan(k, r, ch, R, basis, beta, order, chunk_bfly, acc, final_bfly, out_block, kA=kA, direct=direct)
+    nA = kA
+    while extra_chunks and nA + ch <= k:
+        bf = []
+        for q in range(c):
+            h = 1 << q
+            for o in range(0, ch, 2 * h):
+                s = xhat(q, nA + o, basis)
+                bf += [(o + i, o + i + h, s) for i in range(h)]
+        cost_chunk = sum(8 + macc_cost(s) for _, _, s in bf)
+        cols = {}
+        for m in range(ch):
+            y = [0] * ch
+            y[m] = 1
+            for i, j, s in reversed(bf):        # the chunk op's inverse: chunk output m -> rows
+                y[i] ^= mul(s, y[j])
+                y[j] ^= y[i]
+            vec = [0] * R
+            for ii in range(ch):
+                if y[ii]:
+                    for t, cc in direct[nA + ii]:
+                        vec[t] ^= mul(cc, y[ii])
+            cols[m] = [(t, vec[t]) for t in range(R) if vec[t]]
+            cost_chunk += sum(macc_cost(cc) for _, cc in cols[m])
+        if cost_chunk >= sum(macc_cost(cc) for ii in range(ch) for _, cc in direct[nA + ii]):
+            break
+        hc = nA // ch
+        chunk_bfly.append(bf)
+        for m in range(ch):
+            acc[(hc, m)] = cols[m]
+        for ii in range(ch):
+            del direct[nA + ii]
+        nA += ch
+
+    p = HybridPlan(k, r, ch, R, basis, beta, order, chunk_bfly, acc, final_bfly, out_block, kA=nA, direct=direct)
     rng = random.Random(0x51464543 + j0)
     C = [[inv(i ^ (x0 + j)) for i in range(k)] for j in range(r)]
     for _ in range(check):
