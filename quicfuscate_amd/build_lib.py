@@ -188,6 +188,10 @@ def kernel_specs() -> list:
     # item stays in L2; non-temporal loads re-fetch it: FETCH_SIZE 1.085x ->
     # 1.019x the source bytes, 1.133 -> 1.114 ms, profiles/r04a_lab_enc_traffic.json)
     specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="") for (k, r) in BS_FFT]
+    # (one hybrid pass for (96, 15) / (48, 8), whose repair points share one
+    # coset of 16: 19.5 k -> 16.2 k VALU per item at (96, 15), but block encode
+    # 4,703 -> 4,450 / 5,024 -> 4,841 GiB/s against sliding 758 -> 831 /
+    # 1,232 -> 1,325; not in the library, profiles/r04an_c5_single_hybrid.json)
     # additive-FFT fused decode ('C'): pd 2 (the ring holds a chunk + pd rows)
     # (default cache policy: neighbouring 1,200-B rows share their boundary
     # lines, and non-temporal loads / stores drop them before the reuse;

@@ -1086,7 +1086,8 @@ def test_hybrid_plans_equal_cauchy(k, rt, R):
             assert p.evaluate(xs) == want, (j0, n)
 
 
-@pytest.mark.parametrize("k,rt,L,G", [(24, 10, 200, 3), (20, 20, 72, 2), (48, 21, 64, 2), (160, 48, 40, 1)])
+@pytest.mark.parametrize("k,rt,L,G", [(24, 10, 200, 3), (20, 20, 72, 2), (48, 21, 64, 2), (160, 48, 40, 1),
+                                     (40, 8, 100, 2), (96, 15, 40, 1)])
 def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
     """Codes the plain additive-FFT plan does not cover (k not a power of
     two, repairs past the first coset): one kernel per coset pass
