@@ -61,11 +61,17 @@ def payload_word_offset(rank: int, G: int, k: int, L: int) -> int:
     return (rank * G * k * L) // 8
 
 
+def _pg(dist, world: int) -> bool:
+    """Collectives run when a process group exists: every N > 1 run, and the
+    one-rank rehearsal of the RCCL branch (--force-pg)."""
+    return world > 1 or (dist is not None and dist.is_available() and dist.is_initialized())
+
+
 def reduce_max(torch, dist, values, world: int, device) -> list:
     """Max over ranks of [step_ms, enc_ms, dec_ms, failed] (the bench
     contract: the slowest rank defines the step time; any failure fails)."""
     t = torch.tensor(values, dtype=torch.float64, device=device)
-    if world > 1:
+    if _pg(dist, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.tolist()
 
@@ -91,7 +97,7 @@ def broadcast_descriptor(torch, dist, lib, k: int, r: int, Lb: int, G: int, e: i
         return False
     d = torch.tensor([k, r, Lb, G, e, SEED], dtype=torch.int64, device=device)
     c = torch.from_numpy(mine.copy()).to(device)
-    if world > 1:
+    if _pg(dist, world):
         dist.broadcast(d, src=0)
         dist.broadcast(c, src=0)
     return d.tolist() == [k, r, Lb, G, e, SEED] and bool((c.cpu().numpy() == mine).all())
@@ -100,7 +106,7 @@ def broadcast_descriptor(torch, dist, lib, k: int, r: int, Lb: int, G: int, e: i
 def gather_folds(torch, dist, fold: int, world: int, device) -> list:
     """Every rank's repair XOR-fold (RCCL all_gather: XOR is not a reduction op)."""
     t = torch.tensor([fold - (1 << 64) if fold >= 1 << 63 else fold], dtype=torch.int64, device=device)
-    if world == 1:
+    if not _pg(dist, world):
         return [fold]
     out = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(out, t)
@@ -150,6 +156,11 @@ def parse(argv=None):
                          "(qf_ctx_set_payload_stream) instead of waiting for it across streams")
     ap.add_argument("--cross-stream", dest="payload_stream", action="store_false",
                     help="split, with the payload pass on the decode's stream waiting for the encode's event")
+    ap.add_argument("--detail", default="gpurun_out/bench_detail.json",
+                    help="file for the full per-leg record (the stdout line is the compact form, <= LINE_MAX bytes); "
+                         "'' = do not write it")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="initialise the process group even at world size 1 (rehearses the RCCL branch on one GPU)")
     a = ap.parse_args(argv)
     if a.overlap:
         a.split = False
@@ -202,7 +213,8 @@ def main(argv=None):
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:
+    pg = world > 1 or args.force_pg
+    if pg:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -318,7 +330,7 @@ def main(argv=None):
     for _ in range(args.warmup):
         step(*events())
     torch.cuda.synchronize()
-    if world > 1:
+    if _pg(dist, world):
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -329,7 +341,7 @@ def main(argv=None):
     for s in range(args.steps):
         step(*ev[s])
     torch.cuda.synchronize()
-    if world > 1:
+    if _pg(dist, world):
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -575,10 +587,10 @@ def main(argv=None):
         "verified": bool(fails == 0),
         "repair_checksum_rank0": checksum,
         "repair_xor_fold_by_rank": [f"{f:016x}" for f in folds],
-        "process_group": {"backend": dist.get_backend() if world > 1 else None,
-                          "world_size": dist.get_world_size() if world > 1 else 1,
+        "process_group": {"backend": dist.get_backend() if pg else None,
+                          "world_size": dist.get_world_size() if pg else 1,
                           "env_world_size": world},
-        "run_descriptor": {"broadcast_from_rank0": world > 1, "fields": ["k", "r", "L", "G", "erased", "seed"],
+        "run_descriptor": {"broadcast_from_rank0": pg, "fields": ["k", "r", "L", "G", "erased", "seed"],
                            "cauchy_matrix_bytes": r * k, "matches_by_rank": [bool(f == 1) for f in desc_flags]},
     }
     if c4:
@@ -587,7 +599,7 @@ def main(argv=None):
                                      f"{e} erased sources/generation")
         out["rank_oracle_sample"] = {"generations_per_rank": args.rank_sample,
                                      "pass_by_rank": [None if f < 0 else bool(f) for f in sample_flags]}
-    if world > 1:
+    if pg:
         out["sliding_halo"] = sliding_halo_leg(torch, dist, ctx, lib, L, rank, world, dev, backend)
 
     if rank == 0 and world == 1:
@@ -621,8 +633,9 @@ def main(argv=None):
         out["c5"] = c5_leg(fec, ctx, args.c5_mixed_bytes, args.c5_shape_bytes)
 
     if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        detail = emit_detail(out, args.detail)
+        print(json.dumps(compact_line(out, detail)), flush=True)
+    if pg:
         dist.destroy_process_group()
     if args.split:
         ctx_dec.close()
@@ -696,7 +709,7 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
     for _ in range(max(1, warmup)):
         step([torch.cuda.Event(enable_timing=True) for _ in range(3)])
     torch.cuda.synchronize()
-    if world > 1:
+    if _pg(dist, world):
         dist.barrier()
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
@@ -707,7 +720,7 @@ def c4_leg(torch, dist, fec, L, lib, ctx, stream, dev, rank, world, backend, k, 
     for s_ in range(steps):
         step(evs[s_])
     torch.cuda.synchronize()
-    if world > 1:
+    if _pg(dist, world):
         dist.barrier()
     torch.cuda.synchronize()
     step_ms = (time.perf_counter() - t0) * 1e3 / steps
@@ -774,7 +787,7 @@ def c5_leg(fec, ctx, mixed_bytes: float, shape_bytes: float, reps: int = 3) -> d
 def gather_flags(torch, dist, flag: int, world: int, device) -> list:
     """Every rank's small integer flag (RCCL all_gather)."""
     t = torch.tensor([flag], dtype=torch.int64, device=device)
-    if world == 1:
+    if not _pg(dist, world):
         return [flag]
     out = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(out, t)
@@ -1230,6 +1243,160 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
         "seconds": round(t_enc + t_dec, 2),
         "sample_parity_vs_gpu": bool(parity),
     }
+
+
+# ---------------------------------------------------------------------------
+# The stdout line.  The driver parses ONE JSON line; round 4's full record
+# (20.8 KB, c5 / cpu legs verbatim) was not parsed.  The
+# line carries the contract keys first, then one compact figure per leg; the
+# full record goes to --detail (a file, kept under profiles/ by the builder).
+# ---------------------------------------------------------------------------
+LINE_MAX = 6000   # bytes; the driver's stdout tail holds ~8 KB
+
+
+def emit_detail(full: dict, path: str) -> str | None:
+    """Write the full per-leg record; returns the path written (or None)."""
+    if not path:
+        return None
+    try:
+        p = Path(path)
+        if not p.is_absolute():
+            p = REPO / p
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(json.dumps(full, indent=1))
+        return str(Path(path))
+    except OSError:
+        return None
+
+
+def _r(x, nd=1):
+    return None if x is None else round(float(x), nd)
+
+
+def _roof_compact(rl: dict | None) -> dict | None:
+    if not rl:
+        return None
+    out = {k: rl.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "launch_ms",
+                                  "algorithmic_bytes_per_launch", "limiter")}
+    if rl.get("traffic") is not None and rl.get("algorithmic_bytes_per_launch"):
+        out["traffic_over_alg"] = round(rl["traffic"] / rl["algorithmic_bytes_per_launch"], 3)
+    v = rl.get("valu")
+    if v:
+        out["valu_frac"] = v.get("frac")
+        out["valu_per_wave"] = v.get("valu_per_wave")
+    if rl.get("in_step"):
+        out["in_step"] = {k: rl["in_step"].get(k) for k in ("launch_ms", "frac")}
+    out["timing"] = "HIP events on the launch stream, per launch, inside bench.py"
+    if rl.get("timing"):
+        out["timing"] = "alone: 5 launches after the timed steps (HIP events); in_step: inside the timed steps"
+    out["traffic_src"] = "profiles/traffic.json (rocprofv3 --pmc, same code hash)" if rl.get("traffic") else None
+    return out
+
+
+def _c5_compact(c5: dict | None) -> dict | None:
+    """Per shape [block encode, block decode, sliding encode] GiB/s (kernel
+    time), the mixed batch's device span beside its kernel sum."""
+    if not c5:
+        return None
+    out = {"L": c5.get("L"), "unit": "GiB/s algorithmic bytes",
+           "cols": ["block_enc", "block_dec", "sliding_enc", "block_enc_hbm_frac", "block_dec_hbm_frac"]}
+    shapes, ok = {}, True
+    for key, v in c5.items():
+        if not (key.startswith("k") and isinstance(v, dict)):
+            continue
+        be, bd, sl = v.get("block/encode", {}), v.get("block/decode", {}), v.get("sliding/encode", {})
+        shapes[key] = [be.get("GiBps_alg"), bd.get("GiBps_alg"), sl.get("GiBps_alg"),
+                       be.get("hbm_frac_of_8TBps"), bd.get("hbm_frac_of_8TBps")]
+        ok &= bd.get("verified", True) is not False and sl.get("verified", True) is not False
+    out["shapes"] = shapes
+    m = c5.get("mixed_desc_batch")
+    if m:
+        mx = {"G": m.get("G"), "round_trip_ok": m.get("round_trip_ok")}
+        for leg in ("encode", "decode"):
+            e = m.get(leg, {})
+            mx[leg] = {k: e.get(k) for k in ("span_gibps", "kernel_gibps", "span_ms", "kernel_ms", "span_over_kernel",
+                                             "host_call_ms") if k in e}
+        out["mixed"] = mx
+        ok &= m.get("round_trip_ok") is not False
+    out["verified"] = ok
+    return out
+
+
+def compact_line(full: dict, detail: str | None = None) -> dict:
+    """The stdout JSON line: contract keys first (metric .. config, roofline,
+    cpu_baseline), then one compact figure per leg.  Size-checked by
+    tests/test_bench_cpu.py against LINE_MAX on a recorded full run."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config")
+    line = {k: full.get(k) for k in keys}
+    line["roofline"] = _roof_compact(full.get("roofline"))
+    cb = full.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "encode_gibps",
+                                                       "decode_gibps", "sample_parity_vs_gpu")}
+    line["roofline_encode"] = _roof_compact(full.get("roofline_encode"))
+    for k in ("encode_gibps", "decode_gibps", "encode_ms", "decode_ms", "ms_per_step_median_rank0",
+              "kernel_ms_per_launch", "verified", "process_group"):
+        if k in full:
+            line[k] = full[k]
+    line["streams"] = "split" if "2nd stream" in (full.get("streams") or "") else full.get("streams")
+    rd = full.get("run_descriptor")
+    if rd:
+        line["descriptor_matches_by_rank"] = rd.get("matches_by_rank")
+    if full.get("repair_xor_fold_by_rank") and len(full["repair_xor_fold_by_rank"]) <= 8:
+        line["repair_xor_fold_by_rank"] = full["repair_xor_fold_by_rank"]
+    c4 = full.get("c4")
+    if c4:
+        line["c4"] = {k: c4.get(k) for k in ("generations_per_rank", "ranks", "value", "unit", "ms_per_step",
+                                             "encode_gibps", "decode_gibps", "schedule", "verified")}
+    if "rank_oracle_sample" in full:
+        line["rank_oracle_sample"] = full["rank_oracle_sample"]
+    if full.get("sliding_halo"):
+        sh = full["sliding_halo"]
+        line["sliding_halo"] = {k: sh.get(k) for k in ("backend", "ms_per_step_max", "windows_per_s",
+                                                       "first_window_matches")}
+    if full.get("c5"):
+        line["c5"] = _c5_compact(full["c5"])
+    b = full.get("c3_bernoulli")
+    if b:
+        line["c3_bernoulli"] = {k: b.get(k) for k in ("success_rate", "expected_success_rate", "verified",
+                                                      "decode_gibps_source_of_decoded_generations")}
+    hp = full.get("host_path")
+    if hp:
+        line["host_path_gibps_incl_pcie"] = {
+            "encode": hp.get("encode_src_gibps_incl_pcie"),
+            "decode": (hp.get("decode") or {}).get("decode_src_gibps_incl_pcie"),
+            "match": bool(hp.get("matches_device_encode")) and bool((hp.get("decode") or {}).get(
+                "matches_device_decode", True))}
+    if full.get("hbm_copy_context"):
+        line["hbm_copy_gbps"] = full["hbm_copy_context"].get("gbps_read_plus_write")
+    cv = full.get("cpu_variants")
+    if cv:
+        line["cpu_variants_gibps"] = {k: (v.get("gibps") if isinstance(v, dict) else None) for k, v in cv.items()
+                                      if k.endswith("t") and k.split("_")[-1][:-1].isdigit()}
+        # the clmul kinds restate the reference's defective fold (SURVEY F3): timing only
+        line["cpu_variants_match_gpu"] = all(v.get("matches_gpu", True) for k, v in cv.items()
+                                             if isinstance(v, dict) and not k.startswith("clmul"))
+    c1 = full.get("cpu_c1")
+    if c1:
+        line["cpu_c1_gibps"] = {k: (v.get("gibps") if isinstance(v, dict) else None) for k, v in c1.items()
+                                if k.endswith("t") and k.split("_")[-1][:-1].isdigit()}
+    gl = full.get("cpu_gf_mul_loop")
+    if gl:
+        line["cpu_gf_mul_loop_mb_s"] = {k: (v.get("mb_s") if isinstance(v, dict) else None) for k, v in gl.items()
+                                        if k in ("table", "dispatch", "sse2", "avx2", "avx512")}
+    ch = full.get("cpu_host")
+    if ch:
+        line["cpu_host"] = {"model": ch.get("cpu_model"), "usable_cpus": ch.get("usable_cpus")}
+    line["detail"] = detail
+    s = json.dumps(line)
+    if len(s) > LINE_MAX:   # never again an unparsed line: drop optional legs, largest first
+        for k in sorted((k for k in line if k not in keys + ("roofline", "cpu_baseline", "roofline_encode", "verified")),
+                        key=lambda k: -len(json.dumps(line[k]))):
+            line.pop(k)
+            if len(json.dumps(line)) <= LINE_MAX:
+                break
+    return line
 
 
 if __name__ == "__main__":

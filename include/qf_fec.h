@@ -89,7 +89,10 @@ int qf_ctx_set_payload_wait(qf_ctx *ctx, void *event);
  * before the payload and none after it: the call's work is complete when
  * `stream` reaches that point.  Combines with qf_ctx_set_payload_wait.  The
  * fused decode runs its payload kernel on `stream`; the other decode paths
- * finish on the context's stream and `stream` waits for them.  Cleared when
+ * finish on the context's stream and `stream` waits for them.  The context's
+ * own stream also waits for the payload pass (an event, no host block), so a
+ * later call on ctx -- the next decode rewriting the context's workspace,
+ * qf_sync, qf_ctx_destroy -- is ordered after it.  Cleared when
  * that qf_decode_batch returns; NULL clears it.  qf_decode_batch_host and
  * qf_decode_batch_desc clear it and run on the context's stream. */
 int qf_ctx_set_payload_stream(qf_ctx *ctx, void *stream);

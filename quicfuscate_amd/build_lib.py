@@ -52,7 +52,12 @@ BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
+# gfx950 (CDNA4) only: the generated kernels are gfx950 assembly, and the
+# HIP kernels assume its 160 KB of LDS per CU (k_decode_prepare_lu_lanes
+# stages 72 KB statically, above the 64 KiB of gfx942 / gfx90a)
 ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
+if ARCH != "gfx950":
+    raise RuntimeError(f"QF_OFFLOAD_ARCH={ARCH}: this library targets gfx950 (MI355X) only")
 
 
 def _hipcc() -> str:

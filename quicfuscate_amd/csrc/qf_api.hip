@@ -72,6 +72,11 @@ struct qf_ctx {
     bool has_payload_stream = false;
     bool payload_on_stream = false;
     hipEvent_t ev_accept = nullptr;
+    // recorded after a payload pass on the caller's stream; the context's
+    // stream waits for it, so later context work (the next acceptance pass
+    // rewriting d_work, qf_sync, workspace growth, destroy) is ordered after
+    // that pass's reads of d_work / d_zero
+    hipEvent_t ev_payload = nullptr;
     // heterogeneous batch API (qf_*_batch_desc): the generation offset tables
     // of the class being launched (nullptr: strided generations) and the
     // device / pinned buffers holding a call's per-generation metadata
@@ -569,6 +574,11 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
                                 sh->rec_gen_stride, sh->row_stride, sh->rec_row_stride, L, G, w + off_map, ms,
                                 ctx->d_zero, w, lu_stride, ctx->d_tab256, ctx->offs_in, ctx->offs_out));
     prof_end(ctx, ps, ev, qf::dec_name(&ctx->bs, k, r, L, G, ctx->num_cus));
+    if (ps != st) {
+        if (!ctx->ev_payload) QF_CHECK_HIP(hipEventCreateWithFlags(&ctx->ev_payload, hipEventDisableTiming));
+        QF_CHECK_HIP(hipEventRecord(ctx->ev_payload, ps));
+        QF_CHECK_HIP(hipStreamWaitEvent(st, ctx->ev_payload, 0));
+    }
     return QF_OK;
 }
 
@@ -723,8 +733,9 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
             a.total_units = (uint64_t)Gc * Lu;
             ev = prof_begin(ctx, st);
             std::string cname;
-            pm = p == 0 && passes > 1 && ctx->opt[QF_OPT_ENCODE_MERGED] && qf::cmb_pass_major_available() &&
-                 (uint64_t)G * cgs < (1ull << 32) && combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
+            pm = p == 0 && ctx->opt[QF_OPT_ENCODE_MERGED] &&
+                 qf::cmb_pass_major_ok(passes, sh->rec_row_stride, (uint64_t)G * cgs) &&
+                 combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
             if (pm) {
                 cname = "qf_combine_bs_r16_pm";
                 QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx, passes, (uint64_t)G * cgs));
@@ -1160,7 +1171,9 @@ int qf_ctx_destroy(qf_ctx* c) {
                 (void*)c, 1e6 * p.u[0] / n, 1e6 * p.u[1] / n, 1e6 * p.u[2] / n, 1e6 * p.u[3] / n);
     }
     hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    // (a null stream is QF_STREAM_NULL's: synchronising it is valid and
+    // needed before the buffers below are freed)
+    hipStreamSynchronize(c->stream);
     for (auto& kv : c->cauchy) hipFree(kv.second.dev);
     for (auto& kv : c->small_coef) hipFree(kv.second);
     if (c->d_tab256) hipFree(c->d_tab256);
@@ -1175,6 +1188,7 @@ int qf_ctx_destroy(qf_ctx* c) {
     if (c->h_desc) hipHostFree(c->h_desc);
     if (c->desc_done) hipEventDestroy(c->desc_done);
     if (c->ev_accept) hipEventDestroy(c->ev_accept);
+    if (c->ev_payload) hipEventDestroy(c->ev_payload);
     for (hipEvent_t e : c->send_ev) hipEventDestroy(e);
     if (c->recv_done) {
         hipEventSynchronize(c->recv_done);
@@ -1611,8 +1625,10 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
         const int PD = pick_PD(ctx, QF_OPT_DECODE_PD, 1);
         hipEvent_t ev2 = prof_begin(ctx, ctx->stream);
         std::string cname;
-        pm = p == 0 && passes > 1 && ctx->opt[QF_OPT_ENCODE_MERGED] && qf::cmb_pass_major_available() &&
-             (uint64_t)G * coef_gen_stride < (1ull << 32) &&
+        // (at most kCmbMaxPasses passes per launch: e_max reaches 128 on this
+        // path, i.e. up to 8 passes, which then run one launch per pass)
+        pm = p == 0 && ctx->opt[QF_OPT_ENCODE_MERGED] &&
+             qf::cmb_pass_major_ok(passes, sh->rec_row_stride, (uint64_t)G * coef_gen_stride) &&
              combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
         if (pm) {
             cname = "qf_combine_bs_r16_pm";

@@ -81,6 +81,11 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // 16 p .. of each generation (a.pass must be 0).
 bool cmb_available();
 bool cmb_pass_major_available();
+// The pass-major launch covers at most kCmbMaxPasses passes (the generated
+// loop), and advances dst by 16 rows per pass in a 32-bit SGPR: callers fall
+// back to one launch per pass when this is false.
+constexpr uint32_t kCmbMaxPasses = 4;
+bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_stride);
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
                       const uint32_t* idxtab, uint32_t passes = 1, uint64_t pass_stride = 0);
 void bs_unload(BsCache& cache);

@@ -332,12 +332,17 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 bool cmb_available() { return find('m', 0, 16) != nullptr; }
 bool cmb_pass_major_available() { return find('P', 0, 16) != nullptr; }
 
+bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_stride) {
+    return passes > 1 && passes <= kCmbMaxPasses && pass_stride < (1ull << 32) &&
+           16ull * (passes - 1) * dst_row_stride < (1ull << 32) && cmb_pass_major_available();
+}
+
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
                       const uint32_t* idxtab, uint32_t passes, uint64_t pass_stride) {
     const QfBsEntry* e = find(passes > 1 ? 'P' : 'm', 0, 16);
     if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || a.dst_row_stride >= (1ull << 32) ||
-        a.coef_gen_stride >= (1ull << 32) || passes == 0 || passes > 4 || pass_stride >= (1ull << 32) ||
-        (passes > 1 && a.pass != 0))
+        a.coef_gen_stride >= (1ull << 32) || passes == 0 || (passes > 1 && a.pass != 0) ||
+        (passes > 1 && !cmb_pass_major_ok(passes, a.dst_row_stride, pass_stride)))
         return bs_invalid(__LINE__);
     const int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return bs_invalid(__LINE__);

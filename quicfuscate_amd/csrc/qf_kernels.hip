@@ -1151,6 +1151,10 @@ constexpr uint32_t kPrepLanes = 128;      // generations per block
 constexpr uint32_t kPrepRecWords = 68;    // 272-B record
 constexpr uint32_t kPrepMapWords = 64;    // slot map <= 256 B
 constexpr uint32_t kPrepMaskWords = 8;    // accepted-source bits, k <= 256
+// 768 B of tables + 72 KB of staging: fits gfx950's 160 KB LDS per CU (the
+// library is built for gfx950 only, build_lib.ARCH)
+static_assert(768 + 4 * (kPrepRecWords + kPrepMapWords + kPrepMaskWords) * kPrepLanes <= 160 * 1024,
+              "k_decode_prepare_lu_lanes LDS exceeds the gfx950 CU");
 
 __global__ void __launch_bounds__(kPrepLanes) k_decode_prepare_lu_lanes(PrepareCauchyArgs a) {
     __shared__ uint8_t sexp[512];

@@ -264,15 +264,33 @@ def encode_batch(src, rep, k: int, r: int, Lb: int, *, src_row_stride: int, src_
           "encode_batch")
 
 
+def pack_gen_descs(descs):
+    """A ctypes qf_gen_desc array from dicts / tuples: build it once and pass it
+    to encode_batch_desc on every call (a per-call rebuild of thousands of
+    descriptors costs milliseconds of host time)."""
+    arr = (L.GenDesc * max(1, len(descs)))()
+    for i, d in enumerate(descs):
+        arr[i] = L.GenDesc(**d) if isinstance(d, dict) else L.GenDesc(*d)
+    arr.qf_n = len(descs)
+    return arr
+
+
+def pack_dec_descs(descs):
+    """A ctypes qf_dec_desc array (see pack_gen_descs)."""
+    arr = (L.DecDesc * max(1, len(descs)))()
+    for i, d in enumerate(descs):
+        arr[i] = L.DecDesc(**d) if isinstance(d, dict) else L.DecDesc(*d)
+    arr.qf_n = len(descs)
+    return arr
+
+
 def encode_batch_desc(src, rep, descs, ctx: Optional[Context] = None) -> None:
     """qf_encode_batch_desc: one call over generations of different (k, r, L)
     at arbitrary offsets.  descs: sequence of dicts or tuples
     (k, r, L, flags, src_offset, src_row_stride, rep_offset, rep_row_stride)."""
     ctx = ctx or default_context()
-    arr = (L.GenDesc * max(1, len(descs)))()
-    for i, d in enumerate(descs):
-        arr[i] = L.GenDesc(**d) if isinstance(d, dict) else L.GenDesc(*d)
-    check(L._lib().qf_encode_batch_desc(ctx.handle, arr, len(descs), _ptr(src), _ptr(rep)), "encode_batch_desc")
+    arr = descs if isinstance(descs, ctypes.Array) else pack_gen_descs(descs)
+    check(L._lib().qf_encode_batch_desc(ctx.handle, arr, getattr(arr, "qf_n", len(arr)), _ptr(src), _ptr(rep)), "encode_batch_desc")
 
 
 def decode_batch_desc(rows, row_index, rec, rec_index, n_rec, status, descs, ctx: Optional[Context] = None) -> None:
@@ -280,10 +298,8 @@ def decode_batch_desc(rows, row_index, rec, rec_index, n_rec, status, descs, ctx
     n_rows, rows_offset, row_stride, row_index_offset, rec_offset,
     rec_row_stride, rec_index_offset); n_rec / status: one entry per descriptor."""
     ctx = ctx or default_context()
-    arr = (L.DecDesc * max(1, len(descs)))()
-    for i, d in enumerate(descs):
-        arr[i] = L.DecDesc(**d) if isinstance(d, dict) else L.DecDesc(*d)
-    check(L._lib().qf_decode_batch_desc(ctx.handle, arr, len(descs), _ptr(rows), _ptr(row_index),
+    arr = descs if isinstance(descs, ctypes.Array) else pack_dec_descs(descs)
+    check(L._lib().qf_decode_batch_desc(ctx.handle, arr, getattr(arr, "qf_n", len(arr)), _ptr(rows), _ptr(row_index),
                                          _ptr(rec) if rec is not None else None,
                                          _ptr(rec_index) if rec_index is not None else None, _ptr(n_rec),
                                          _ptr(status)), "decode_batch_desc")

@@ -40,3 +40,52 @@ def test_headline_workload_is_per_gpu_constant():
     """Every N runs the same generations per GPU (weak scaling); C4 is its own leg."""
     a = bench.parse([])
     assert a.G is None and a.config == "auto" and a.c4_G == 156250
+
+
+def _recorded_full(name="r04am_bench_full.json"):
+    import json
+    lines = [l for l in (REPO / "profiles" / name).read_text().splitlines() if l.startswith("{")]
+    return json.loads(lines[-1])
+
+
+def test_line_fits_driver_parse():
+    """the 20.8 KB round-4 line was not parsed by the
+    driver.  The compact line of a recorded full run (every leg present) must
+    stay under LINE_MAX and carry the contract keys first."""
+    import json
+    full = _recorded_full()
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) <= bench.LINE_MAX <= 8000, len(s)
+    keys = list(line)
+    assert keys[:13] == ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                         "scaling", "vs_baseline", "dtype", "data", "config"]
+    for k in ("roofline", "cpu_baseline", "roofline_encode", "c5", "c4", "cpu_variants_gibps"):
+        assert line.get(k), k
+    rl = line["roofline"]
+    assert rl["bound"] == "hbm" and rl["unit"] == "GB/s" and 0 < rl["frac"] < 1
+    assert abs(rl["achieved"] / rl["peak"] - rl["frac"]) < 1e-3
+    cb = line["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1 and cb["value"] > 0
+    assert len(line["c5"]["shapes"]) == 7
+    assert json.loads(s) == line
+
+
+def test_line_trims_oversized_legs():
+    """Whatever a leg grows into, the line keeps the contract keys and fits."""
+    import json
+    full = _recorded_full()
+    full["cpu_gf_mul_loop"] = {f"k{i}": {"mb_s": i} for i in range(2000)}
+    full["cpu_gf_mul_loop"].update({"table": {"mb_s": 1.0}})
+    full["c5"]["k32_r5"]["block/encode"]["GiBps_alg"] = "x" * 9000
+    line = bench.compact_line(full)
+    assert len(json.dumps(line)) <= bench.LINE_MAX
+    assert line["roofline"] and line["cpu_baseline"] and line["value"] == full["value"]
+
+
+def test_detail_written(tmp_path):
+    import json
+    full = _recorded_full()
+    p = bench.emit_detail(full, str(tmp_path / "d.json"))
+    assert p and json.loads(open(p).read())["value"] == full["value"]
+    assert bench.emit_detail(full, "") is None

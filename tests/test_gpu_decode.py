@@ -476,3 +476,71 @@ def test_decode_prepare_per_lane_matches_per_wave(qf, oracle, gpu_ctx, k, r, L):
         assert nrec[g] == len(erased) and list(recidx[g, : nrec[g]]) == erased, g
         for m, i in enumerate(erased):
             assert (rec[g * rec_gs + m * rrs: g * rec_gs + m * rrs + L] == sol[i]).all(), (g, i)
+
+
+def test_decode_payload_stream_back_to_back(qf, oracle, gpu_ctx):
+    """two payload-stream decodes on one context, different rows,
+    no join between them.  The first payload pass is held back on the caller's
+    stream (HBM copies queued ahead of it); the second call's acceptance pass,
+    on the context's stream, must not rewrite the context's LU records / slot
+    map before that pass has read them."""
+    import torch
+
+    k, r, L, G = 64, 16, 1200, 3000
+    max_rows = k + r
+    rs, emax = _r16(L), min(k, r)
+    rgs, rec_gs = max_rows * rs, emax * rs
+    batches = []
+    for seed in (21, 22):
+        rng = np.random.default_rng(seed)
+        src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, erase=13)
+        rows = np.zeros(G * rgs, np.uint8)
+        ridx = np.zeros((G, max_rows), np.uint16)
+        for g, (arr, rw, _) in enumerate(gens):
+            ridx[g, : len(arr)] = arr
+            for s in range(len(arr)):
+                rows[g * rgs + s * rs: g * rgs + s * rs + L] = rw[s]
+        t = dict(rows=torch.from_numpy(rows).cuda(), idx=torch.from_numpy(ridx.view(np.int16)).cuda(),
+                 rec=torch.full((G * rec_gs,), 0x5A, dtype=torch.uint8, device="cuda"),
+                 recidx=torch.zeros(G * emax, dtype=torch.int16, device="cuda"),
+                 nrec=torch.zeros(G, dtype=torch.int32, device="cuda"),
+                 status=torch.full((G,), 77, dtype=torch.int32, device="cuda"))
+        batches.append((src, gens, t))
+    big_a = torch.ones(1 << 30, dtype=torch.uint8, device="cuda")
+    big_b = torch.empty_like(big_a)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    ctx = qf.Context(0, torch.cuda.Stream().cuda_stream)
+    try:
+        with torch.cuda.stream(side):
+            for _ in range(6):          # ~3 ms of HBM traffic ahead of the first payload pass
+                big_b.copy_(big_a)
+        for _, _, t in batches:
+            ctx.set_payload_stream(side)
+            qf.decode_batch(t["rows"], t["idx"], t["rec"], t["recidx"], t["nrec"], t["status"], k, r, L,
+                            max_rows=max_rows, row_stride=rs, rows_gen_stride=rgs, rec_row_stride=rs,
+                            rec_gen_stride=rec_gs, G=G, ctx=ctx)
+        ctx.sync()          # the context's stream now also covers the payload passes
+        for src, gens, t in batches:
+            out = (t["rec"].cpu().numpy(), t["recidx"].cpu().numpy().view(np.uint16).reshape(G, -1),
+                   t["nrec"].cpu().numpy(), t["status"].cpu().numpy(), rs, rec_gs)
+            assert (out[3] == 0).all()
+            check(oracle, k, L, src, gens, out, False)
+    finally:
+        ctx.close()
+        del big_a, big_b
+
+
+@pytest.mark.parametrize("path", ["default", "general"])
+def test_decode_general_path_more_than_four_passes(qf, oracle, gpu_ctx, path, monkeypatch):
+    """Cauchy k=128, r=96 (r > 64: no syndrome kernel) with 2 KiB
+    rows takes the general path with the bit-sliced payload pass; e up to 96
+    means up to 6 passes of 16 outputs, more than one pass-major launch holds,
+    so the passes run one launch each instead of failing with QF_EDEVICE."""
+    _path(monkeypatch, path)
+    rng = np.random.default_rng(96)
+    k, r, L, G = 128, 96, 2048, 4
+    src, gens = make_batch(oracle, rng, k, r, L, G, k + r, erase=90)
+    out = run_decode(qf, k, r, L, G, k + r, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+    assert max(out[2]) > 64

@@ -1,0 +1,77 @@
+#!/bin/bash
+# The one GPU-box launcher (replaces the per-round tools/gpu_r0*_*.sh; those
+# are in git history before round 5).  Every GPU step has its own time limit
+# and any failure ends the script (set -e, steps chained).
+#
+#   TAG=r05a tools/gpu.sh tests [pytest args...]   -m gpu suite (or the files given)
+#   TAG=r05a tools/gpu.sh full                     -m gpu suite, smoke, one default bench line
+#   TAG=r05a tools/gpu.sh bench [bench args...]    one bench line (+ detail record)
+#   TAG=r05a tools/gpu.sh prof                     bench line, kernel trace, SQ counters, FETCH / WRITE passes
+#   TAG=r05a tools/gpu.sh run <command...>         any command, under a 600 s limit
+#
+# Outputs: gpurun_out/$TAG/ (merged back by gpurun; copy what is judged into profiles/).
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+TAG=${TAG:-r05}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+what=${1:-full}
+shift || true
+PYT="python -u -m pytest -x -q --timeout 170 --timeout-method thread"
+ARGS="--steps 3 --warmup 1 --no-cpu --host-path-G 0 --c3b-G 0 --c4-G 0 --c5-mixed-bytes 0"
+
+bench_line() {   # $1 log name, rest: bench args
+  local name=$1
+  shift
+  timeout -k 10 400 python3 bench.py --detail "$OUT/${name}_detail.json" "$@" > "$OUT/$name.log" 2>&1
+  grep '^{"metric"' "$OUT/$name.log" > "$OUT/$name.json"
+  echo "$name: $(wc -c < "$OUT/$name.json") bytes"
+  cut -c1-300 "$OUT/$name.json"
+}
+
+case "$what" in
+  tests)
+    if [ $# -eq 0 ]; then set -- tests -m gpu; fi
+    timeout -k 10 1000 $PYT "$@" > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+    tail -3 "$OUT/gpu_tests.log"
+    ;;
+  full)
+    timeout -k 10 1000 $PYT tests -m gpu > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
+    tail -3 "$OUT/gpu_tests.log"
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > "$OUT/smoke.log" 2>&1
+    tail -1 "$OUT/smoke.log"
+    bench_line bench_full
+    ;;
+  bench)
+    bench_line bench_full "$@"
+    ;;
+  prof)
+    bench_line bench_full
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
+      python3 bench.py --detail "$OUT/kt_detail.json" $ARGS > "$OUT/kt.log" 2>&1
+    grep '^{"metric"' "$OUT/kt.log" > "$OUT/kt.bench.json"
+    python3 tools/prof_summary.py "$OUT/kt" "$OUT/kernel_stats.json" \
+      --command "rocprofv3 --kernel-trace --stats --output-format csv -- python3 bench.py $ARGS"
+    echo KT_OK
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_LDS \
+      SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY --output-format csv -d "$OUT/sq" -o run -- \
+      python3 bench.py --detail "" $ARGS > "$OUT/sq.log" 2>&1
+    python3 tools/sq_summary.py "$OUT/sq" "$OUT/sq_counters.json" > /dev/null
+    echo SQ_OK
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
+      python3 bench.py --detail "" $ARGS > "$OUT/fetch.log" 2>&1
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
+      python3 bench.py --detail "" $ARGS > "$OUT/write.log" 2>&1
+    python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" --k 64 --r 16 --L 1200 --G 65536 --out "$OUT/traffic.json" \
+      --command "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate runs) -- python3 bench.py $ARGS"
+    echo PMC_OK
+    ;;
+  run)
+    timeout -k 10 600 "$@"
+    ;;
+  *)
+    echo "unknown: $what" >&2
+    exit 2
+    ;;
+esac
