@@ -377,6 +377,13 @@ class KernelSpec:
     # lab only (chunked dec): skip the row loop (the LU phase alone, on whatever
     # the accumulator registers hold) -- timing of the LU in isolation
     lab_lu_only: bool = False
+    # lab only (chunked fft dec): row n of the loop reads slot n % 64 of the
+    # generation (no slot map: the generation's rows in address order; the
+    # results are wrong, timing of the access pattern only)
+    lab_slot_order: bool = False
+    # lab only (chunked fft dec): absent rows are not loaded at all (their
+    # lanes masked off) instead of reading the shared zero row
+    lab_skip_absent: bool = False
     # chunked dec, small batches: the four waves of a workgroup share ONE item,
     # each running every ksplit-th row of it; waves 1..3 hand their partial
     # syndromes to wave 0 through LDS, which solves and stores (kernel
@@ -2123,13 +2130,21 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
 
         def load_fft(n: int, base: int):
             kind, idx = fseq[n]
-            present(idx if kind == "src" else k + idx, S_TMP)
+            if spec.lab_slot_order:
+                E(Op("v_movk", (V_SLOT, n % 64)))
+            else:
+                present(idx if kind == "src" else k + idx, S_TMP)
             E(Op("v_mad64_s", (V_ADDR, V_SLOT, 10, V_SRCA)))
-            E(Op("v_cndmask", (V_ADDR, V_ZA, V_ADDR, S_TMP)))
-            E(Op("v_cndmask", (V_ADDR + 1, V_ZA + 1, V_ADDR + 1, S_TMP)))
+            if not (spec.lab_slot_order or spec.lab_skip_absent):
+                E(Op("v_cndmask", (V_ADDR, V_ZA, V_ADDR, S_TMP)))
+                E(Op("v_cndmask", (V_ADDR + 1, V_ZA + 1, V_ADDR + 1, S_TMP)))
             E(Op("v_add64_s", (V_SRCB, V_ADDR, S_QB)))
             for h, (vm, va) in enumerate(((26, V_ADDR), (24, V_SRCB))):
-                E(Op("s_exec", (vm,)))
+                if spec.lab_skip_absent and not spec.lab_slot_order:
+                    E(Op("s_and64", (S_TMP2, vm, S_TMP)))
+                    E(Op("s_exec", (S_TMP2,)))
+                else:
+                    E(Op("s_exec", (vm,)))
                 if spec.lab_norows:
                     continue
                 if S:   # -> LDS slot n % S of this wave (no VGPR destination)

@@ -1223,3 +1223,40 @@ def test_fft_register_budget_covers_code(k, r, mode):
             assert lo % 2 == 0, m.group(0)
             hi = max(hi, top)
     assert hi < spec.next_free_vgpr <= 256
+
+
+def test_dec_lab_variants_stay_in_bounds():
+    """tools/dec_lab.py's round-5 access-pattern variants (nodata, slot order,
+    masked absent rows) are timing-only kernels, but they run on the GPU box:
+    every load and store must stay inside the lab's buffers (the emulator
+    raises on any access outside them).  C3 geometry, a few generations."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import dec_lab
+    from bs_lab import variant_ops
+
+    k, r, L, e, G = 64, 16, 1200, 13, 6
+    n_slots = k - e + r
+    erased, smap = dec_lab.c3_inputs(G, k, r, L, e)
+    recs = np.stack([bs.lu_record(k, r, list(range(e)), erased[g].tolist()) for g in range(G)])
+    rows = np.random.default_rng(1).integers(0, 256, G * n_slots * L, dtype=np.uint8)
+    ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
+    Q = ((L + 15) // 16 + 1) // 2
+    items = (G * Q + 63) // 64
+    waves = (items + 3) // 4
+    for name, kw, flags in dec_lab.VARIANTS:
+        if not name.startswith("m_") or name.endswith("_2") or name == "m_warm":
+            continue
+        kw2 = {a: b for a, b in kw.items() if a not in ("pd", "cap", "rs", "rrs", "Q")}
+        spec = bs.KernelSpec(k, r, kw.get("pd", 3), "dec", **kw2)
+        emu = bs.Emulator(variant_ops(bs, spec, set(flags)))
+        out = np.zeros(G * e * L, np.uint8)
+        for base, buf in ((ROWS, rows), (OUT, out), (MAP, smap.reshape(-1)), (ZERO, np.zeros(1216, np.uint8)),
+                          (REC, recs.reshape(-1)), (TAB, bs.split_tables())):
+            emu.add_buffer(base, buf)
+        ka = bs.kernargs(ROWS, OUT, n_slots * L, e * L, L, L, L, G, waves * 4, smap=MAP, map_stride=smap.shape[1],
+                         zero=ZERO, lu=(REC, bs.LU_REC_BYTES), tables=TAB, chunked=True)
+        for wg in range(waves):
+            for w in range(4):
+                emu.run_wave(ka, wg, w)

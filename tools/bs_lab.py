@@ -23,12 +23,16 @@ sys.path.insert(0, str(REPO))
 OUT = REPO / "tools" / "lab_build"
 
 VALU = {"v_xor", "v_andk", "v_lshl", "v_lshr", "v_mov", "v_movk", "v_xor3", "v_bitsel_s"}
+# address arithmetic (kept by "nodata" even where the register is reused:
+# the LU record pointer lives in the accumulator range after the row loop)
+ADDR_OPS = {"v_movs", "v_mad64_s", "v_mad64_k", "v_add64_s", "v_cndmask", "v_bfe", "v_readfirstlane"}
 
 
 def variant_ops(bs, spec, flags):
     ops = bs.generate(spec)
     body = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Lbody")
     acc_lo, acc_hi = spec.acc0, spec.acc0 + 8 * spec.nacc
+    ring_lo, ring_hi = spec.ring0, spec.ring0 + 8 * spec.nbuf
     out = []
     for n, op in enumerate(ops):
         # notables: the prologue's split-table copy into LDS dropped (timing
@@ -44,6 +48,13 @@ def variant_ops(bs, spec, flags):
             if "nocoeff" in flags and op.name in ("v_xor", "v_xor3", "v_mov", "v_movk") and acc_lo <= op.args[0] < acc_hi:
                 continue
             if "nocompute" in flags and op.name in VALU:
+                continue
+            # nodata: every VALU op writing a row-ring or accumulator register
+            # dropped (the row loop's transposes, butterflies, folds): the
+            # loads and their addressing stay -- the access pattern alone
+            if ("nodata" in flags and op.name.startswith("v_") and op.name not in ADDR_OPS and op.args
+                    and isinstance(op.args[0], int)
+                    and (acc_lo <= op.args[0] < acc_hi or ring_lo <= op.args[0] < ring_hi)):
                 continue
         out.append(op)
     return out

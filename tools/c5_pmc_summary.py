@@ -21,7 +21,7 @@ for d in a.dirs:
         with fp.open() as f:
             for row in csv.DictReader(f):
                 name = row.get("Kernel_Name", "?")
-                if "qf_cauchy" not in name and "k_" not in name:
+                if "qf_" not in name and "k_" not in name:
                     continue
                 acc[(name.split("(")[0].strip(), row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
 per = defaultdict(lambda: defaultdict(list))

@@ -37,6 +37,23 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5: what bounds the row loop's gather -- the access pattern alone
+    # (nodata: loads + addressing, no transposes / butterflies / LU / stores),
+    # in slot-map FFT order with the zero row, with absent rows masked off,
+    # and in address order (slot n % 64, no map); the encode's reads-only
+    # pass runs 0.829 ms for 5.03 GB (profiles/r04a_lab_enc_traffic.json)
+    ("m_warm", dict(LIB_DEC4), ()),
+    ("m_lib", dict(LIB_DEC4), ()),
+    ("m_rowloop", {**LIB_DEC4, "lu": False}, ("nostore",)),
+    ("m_loads", {**LIB_DEC4, "lu": False}, ("nostore", "nodata")),
+    ("m_loads_skip", {**LIB_DEC4, "lu": False, "lab_skip_absent": True}, ("nostore", "nodata")),
+    ("m_loads_addr", {**LIB_DEC4, "lu": False, "lab_slot_order": True}, ("nostore", "nodata")),
+    ("m_rowloop_skip", {**LIB_DEC4, "lu": False, "lab_skip_absent": True}, ("nostore",)),
+    ("m_lib_skip", {**LIB_DEC4, "lab_skip_absent": True}, ()),
+    ("m_lib_2", dict(LIB_DEC4), ()),
+    ("m_loads_2", {**LIB_DEC4, "lu": False}, ("nostore", "nodata")),
+]
+VARIANTS_R04P = [
     # round 4p: split-table reads two coefficients ahead of the LU products
     ("a_warm", dict(LIB_DEC4), ()),
     ("a_lib", dict(LIB_DEC4), ()),

@@ -67,6 +67,28 @@ case "$what" in
       --command "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate runs) -- python3 bench.py $ARGS"
     echo PMC_OK
     ;;
+  declab)   # tools/dec_lab.py run (build the variants here first: python tools/dec_lab.py build)
+    timeout -k 10 300 python3 tools/dec_lab.py run --reps 10 --out "$OUT/dec_lab.json" "$@" > "$OUT/dec_lab.log" 2>&1
+    tail -20 "$OUT/dec_lab.log"
+    ;;
+  c5pmc)    # counters of the C5 kernels of one shape (C5_SHAPES, default 196,59): block encode + decode
+    SH="${C5_SHAPES:-196,59}"
+    BC="python3 tools/bench_c5.py --shapes $SH --modes block --reps 3 --bytes 2e9"
+    timeout -k 10 200 $BC --out "$OUT/c5_plain.json" > "$OUT/c5_plain.log" 2>&1
+    tail -2 "$OUT/c5_plain.log"
+    timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5kt" -o kt -- \
+      $BC --out /tmp/c5x.json > "$OUT/c5kt.log" 2>&1
+    timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES \
+      SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_ANY --output-format csv -d "$OUT/c5sq" -o sq -- \
+      $BC --out /tmp/c5x.json > "$OUT/c5sq.log" 2>&1
+    timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c5fetch" -o f -- \
+      $BC --out /tmp/c5x.json > "$OUT/c5fetch.log" 2>&1
+    timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c5write" -o w -- \
+      $BC --out /tmp/c5x.json > "$OUT/c5write.log" 2>&1
+    python3 tools/c5_pmc_summary.py "$OUT/c5sq" "$OUT/c5fetch" "$OUT/c5write" --out "$OUT/c5_pmc.json"
+    python3 tools/prof_summary.py "$OUT/c5kt" "$OUT/c5_kernel_stats.json" --command "rocprofv3 --kernel-trace --stats -- $BC"
+    echo C5PMC_OK
+    ;;
   run)
     timeout -k 10 600 "$@"
     ;;
