@@ -1243,20 +1243,21 @@ def test_dec_lab_variants_stay_in_bounds():
     rows = np.random.default_rng(1).integers(0, 256, G * n_slots * L, dtype=np.uint8)
     ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     Q = ((L + 15) // 16 + 1) // 2
-    items = (G * Q + 63) // 64
-    waves = (items + 3) // 4
-    for name, kw, flags in dec_lab.VARIANTS:
-        if not name.startswith("m_") or name.endswith("_2") or name == "m_warm":
+    for name, kw, flags in dec_lab.VARIANTS + dec_lab.VARIANTS_R05A:
+        if name.endswith("_2") or name.endswith("_warm") or kw.get("rs"):
             continue
         kw2 = {a: b for a, b in kw.items() if a not in ("pd", "cap", "rs", "rrs", "Q")}
         spec = bs.KernelSpec(k, r, kw.get("pd", 3), "dec", **kw2)
         emu = bs.Emulator(variant_ops(bs, spec, set(flags)))
-        out = np.zeros(G * e * L, np.uint8)
+        rrs, Qv = kw.get("rrs", L), kw.get("Q")
+        waves = ((G * (Qv or Q) + 63) // 64 + 3) // 4
+        out = np.zeros(G * e * rrs, np.uint8)
         for base, buf in ((ROWS, rows), (OUT, out), (MAP, smap.reshape(-1)), (ZERO, np.zeros(1216, np.uint8)),
                           (REC, recs.reshape(-1)), (TAB, bs.split_tables())):
             emu.add_buffer(base, buf)
-        ka = bs.kernargs(ROWS, OUT, n_slots * L, e * L, L, L, L, G, waves * 4, smap=MAP, map_stride=smap.shape[1],
-                         zero=ZERO, lu=(REC, bs.LU_REC_BYTES), tables=TAB, chunked=True)
+        ka = bs.kernargs(ROWS, OUT, n_slots * L, e * rrs, L, rrs, L, G, waves * 4, smap=MAP,
+                         map_stride=smap.shape[1], zero=ZERO, lu=(REC, bs.LU_REC_BYTES), tables=TAB, chunked=True,
+                         Q=Qv)
         for wg in range(waves):
             for w in range(4):
                 emu.run_wave(ka, wg, w)

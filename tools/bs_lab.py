@@ -43,6 +43,10 @@ def variant_ops(bs, spec, flags):
         if n > body:
             if "noload" in flags and op.name in ("load16", "load16_lds", "s_waitcnt_vm"):
                 continue
+            # norowload: only the payload row loads (into the row ring) dropped;
+            # slot maps, LU records and rank quads still load
+            if "norowload" in flags and op.name in ("load16", "load16_lds") and ring_lo <= op.args[0] < ring_hi:
+                continue
             if "nostore" in flags and op.name in ("store16", "store_byte"):
                 continue
             if "nocoeff" in flags and op.name in ("v_xor", "v_xor3", "v_mov", "v_movk") and acc_lo <= op.args[0] < acc_hi:

@@ -37,6 +37,28 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5b: what the recovered-row stores cost (r05a: the row loop alone,
+    # no LU and no stores, runs 0.83 ms; the loads alone 0.80 ms): dense
+    # 1,200-B recovered rows against pool-block rows (rrs 1,280: every row
+    # starts on a 128-B line) with Q = 38 and Q = 40 lane-chunks (Q = 40: both
+    # of a lane's store segments start on a line), received rows dense
+    ("s_warm", dict(LIB_DEC4), ()),
+    ("s_lib", dict(LIB_DEC4), ()),
+    ("s_nolu", {**LIB_DEC4, "lu": False}, ()),
+    ("s_nolu_r1280", {**LIB_DEC4, "lu": False, "rrs": 1280}, ()),
+    ("s_nolu_q40_r1280", {**LIB_DEC4, "lu": False, "rrs": 1280, "Q": 40}, ()),
+    ("s_lib_r1280", {**LIB_DEC4, "rrs": 1280}, ()),
+    ("s_lib_q40_r1280", {**LIB_DEC4, "rrs": 1280, "Q": 40}, ()),
+    ("s_lib_q40", {**LIB_DEC4, "Q": 40}, ()),
+    ("s_nolu_noload", {**LIB_DEC4, "lu": False}, ("norowload",)),
+    ("s_nolu_noload_nostore", {**LIB_DEC4, "lu": False}, ("norowload", "nostore")),
+    ("s_noload", dict(LIB_DEC4), ("norowload",)),
+    ("s_nostore", dict(LIB_DEC4), ("nostore",)),
+    ("s_lib_2", dict(LIB_DEC4), ()),
+    ("s_nolu_2", {**LIB_DEC4, "lu": False}, ()),
+    ("s_lib_q40_r1280_2", {**LIB_DEC4, "rrs": 1280, "Q": 40}, ()),
+]
+VARIANTS_R05A = [
     # round 5: what bounds the row loop's gather -- the access pattern alone
     # (nodata: loads + addressing, no transposes / butterflies / LU / stores),
     # in slot-map FFT order with the zero row, with absent rows masked off,
