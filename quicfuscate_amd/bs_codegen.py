@@ -384,6 +384,10 @@ class KernelSpec:
     # lab only (chunked fft dec): absent rows are not loaded at all (their
     # lanes masked off) instead of reading the shared zero row
     lab_skip_absent: bool = False
+    # lab only (chunked dec, Q = 2^m lane-chunks, recovered rows >= 32 Q bytes
+    # apart): every lane of a generation stores its B half, the lanes past the
+    # last unit included (the zero tail of pool-block rows: whole 128-B lines)
+    lab_full_b_store: bool = False
     # chunked dec, small batches: the four waves of a workgroup share ONE item,
     # each running every ksplit-th row of it; waves 1..3 hand their partial
     # syndromes to wave 0 through LDS, which solves and stores (kernel
@@ -2543,7 +2547,7 @@ def _store_recovered_chunked(E, spec: KernelSpec, blk, rank: int, t: int, a: int
     E(Op("s_and64", (S_TMP2, S_TMP, S_STA)))
     E(Op("s_exec", (S_TMP2,)))
     E(Op("store16", (a, blk(t, 0), 0, spec.st_policy)))
-    E(Op("s_and64", (S_TMP2, S_TMP, S_STB)))
+    E(Op("s_and64", (S_TMP2, S_TMP, S_STA if spec.lab_full_b_store else S_STB)))
     E(Op("s_exec", (S_TMP2,)))
     E(Op("store16", (a + 2, blk(t, 4), 0, spec.st_policy)))
     # the partial last unit: bytes [0, L % 16) of the tail lane's unit B

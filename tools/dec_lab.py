@@ -37,6 +37,21 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5c: recovered rows as pool blocks with whole-line stores -- Q = 40
+    # lane-chunks, 1,280-B recovered rows, every lane storing its B half (the
+    # 80-B zero tail included), received rows dense
+    ("z_warm", dict(LIB_DEC4), ()),
+    ("z_lib", dict(LIB_DEC4), ()),
+    ("z_q40_zt", {**LIB_DEC4, "rrs": 1280, "Q": 40, "lab_full_b_store": True}, ()),
+    ("z_q40", {**LIB_DEC4, "rrs": 1280, "Q": 40}, ()),
+    ("z_nolu", {**LIB_DEC4, "lu": False}, ()),
+    ("z_nolu_q40_zt", {**LIB_DEC4, "lu": False, "rrs": 1280, "Q": 40, "lab_full_b_store": True}, ()),
+    ("z_lib_2", dict(LIB_DEC4), ()),
+    ("z_q40_zt_2", {**LIB_DEC4, "rrs": 1280, "Q": 40, "lab_full_b_store": True}, ()),
+    ("z_lib_3", dict(LIB_DEC4), ()),
+    ("z_q40_zt_3", {**LIB_DEC4, "rrs": 1280, "Q": 40, "lab_full_b_store": True}, ()),
+]
+VARIANTS_R05B = [
     # round 5b: what the recovered-row stores cost (r05a: the row loop alone,
     # no LU and no stores, runs 0.83 ms; the loads alone 0.80 ms): dense
     # 1,200-B recovered rows against pool-block rows (rrs 1,280: every row
