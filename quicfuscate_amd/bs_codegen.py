@@ -388,6 +388,10 @@ class KernelSpec:
     # apart): every lane of a generation stores its B half, the lanes past the
     # last unit included (the zero tail of pool-block rows: whole 128-B lines)
     lab_full_b_store: bool = False
+    # lab only (chunked dec): "fwd" / "bwd" -- only the forward (L, diagonal)
+    # or only the backward (U') products of the LU run (results wrong; the
+    # marginal time of ~half the per-lane products)
+    lab_lu_part: str = ""
     # chunked dec, small batches: the four waves of a workgroup share ONE item,
     # each running every ksplit-th row of it; waves 1..3 hand their partial
     # syndromes to wave 0 through LDS, which solves and stores (kernel
@@ -2489,6 +2493,8 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
         for u in range(r):
             E(Op("s_cmp_le_k_br", (S_JMAX, u, ".Lfwd_end")))
             E(Op("s_waitcnt_vm", (r - u,)))
+            if spec.lab_lu_part == "bwd":
+                continue
             selectors(u)
             column(u, [("scale", u)] + [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}", 1)
         E(Op("label", (".Lfwd_end",)))
@@ -2501,8 +2507,11 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
             pf_rows = [list(range(n_slots))[c::chunks] for c in range(chunks)]
         for n_u, u in enumerate(reversed(range(1, r))):
             E(Op("s_cmp_le_k_br", (S_JMAX, u, f".Lbwd{u}")))
-            selectors(u)
-            column(u, [("acc", t) for t in range(u)], f".Lbwd{u}", r + 1)
+            if spec.lab_lu_part != "fwd":
+                selectors(u)
+                column(u, [("acc", t) for t in range(u)], f".Lbwd{u}", r + 1)
+            else:
+                E(Op("label", (f".Lbwd{u}",)))
             if pf_rows:
                 _prefetch_rows(E, spec, len(pf_rows[n_u]))
             if spec.early_stores:

@@ -37,6 +37,18 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5d: the marginal time of the LU's per-lane products (forward only:
+    # 91 products; backward only: 78; none: stores only)
+    ("h_warm", dict(LIB_DEC4), ()),
+    ("h_lib", dict(LIB_DEC4), ()),
+    ("h_fwd", {**LIB_DEC4, "lab_lu_part": "fwd"}, ()),
+    ("h_bwd", {**LIB_DEC4, "lab_lu_part": "bwd"}, ()),
+    ("h_nolu", {**LIB_DEC4, "lu": False}, ()),
+    ("h_lib_2", dict(LIB_DEC4), ()),
+    ("h_fwd_2", {**LIB_DEC4, "lab_lu_part": "fwd"}, ()),
+    ("h_bwd_2", {**LIB_DEC4, "lab_lu_part": "bwd"}, ()),
+]
+VARIANTS_R05C = [
     # round 5c: recovered rows as pool blocks with whole-line stores -- Q = 40
     # lane-chunks, 1,280-B recovered rows, every lane storing its B half (the
     # 80-B zero tail included), received rows dense
