@@ -139,6 +139,55 @@ class Plan:
         return [e[self.out_block[j]] for j in range(self.r)]
 
 
+def transposed_evaluate(p: "Plan", t: list[int]) -> list[int]:
+    """The plan run backwards with every elementary op transposed (a ^= c b
+    -> b ^= c a): r repair-point values t -> the k values u_i = sum_j t_j /
+    ((k + j) + i), i.e. C^T t at the plan's own op count (transposition
+    principle).  The middle factor of the closed-form Cauchy inverse
+    C[J,E]^-1 = diag(alpha) K diag(beta) is a sub-block of C^T; DESIGN.md 3.2
+    (round 5) costs a decode solve built on it."""
+    e = [0] * p.R
+    for j in range(p.r):
+        e[p.out_block[j]] ^= t[j]
+    for i, j, s in reversed(p.final_bfly):
+        e[i] ^= e[j]
+        e[j] ^= mul(s, e[i])
+    u = [0] * p.k
+    for hc in range(p.k // p.ch):
+        y = [0] * p.ch
+        for m in range(p.ch):
+            for tt, c in p.acc[(hc, m)]:
+                y[m] ^= mul(c, e[tt])
+        for i, j, s in reversed(p.chunk_bfly[hc]):
+            y[j] ^= mul(s, y[i])
+            y[i] ^= y[j]
+        for m in range(p.ch):
+            u[p.order[hc * p.ch + m]] = y[m]
+    return u
+
+
+def cauchy_inverse_factors(k: int, J: list[int], E: list[int]) -> tuple[list[int], list[int]]:
+    """(alpha, beta) of C[J,E]^-1 = diag(alpha) K diag(beta), K[b][a] =
+    1 / (x_a + y_b), x = k + J, y = E (characteristic 2: no signs)."""
+    xs, e = [k + j for j in J], len(E)
+    alpha, beta = [], []
+    for b in range(e):
+        num = den = 1
+        for c in range(e):
+            num = mul(num, xs[c] ^ E[b])
+            if c != b:
+                den = mul(den, E[b] ^ E[c])
+        alpha.append(mul(num, inv(den)))
+    for a in range(e):
+        num = den = 1
+        for c in range(e):
+            num = mul(num, xs[a] ^ E[c])
+            if c != a:
+                den = mul(den, xs[a] ^ xs[c])
+        beta.append(mul(num, inv(den)))
+    return alpha, beta
+
+
 def _log2(n: int) -> int:
     assert n > 0 and n & (n - 1) == 0, n
     return n.bit_length() - 1

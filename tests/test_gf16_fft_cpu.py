@@ -266,3 +266,4 @@ def test_bitplane_form_matches_field():
         for s in (0, 1, 2, 0x8000, 0xFFFF, int(rng.integers(0, 65536))):
             got = to_sym(_bs_store(_bs_mul(planes, s))[None])[0]
             assert np.array_equal(got, vmul(s, sym)), s
+
