@@ -159,6 +159,8 @@ def parse(argv=None):
     ap.add_argument("--detail", default="gpurun_out/bench_detail.json",
                     help="file for the full per-leg record (the stdout line is the compact form, <= LINE_MAX bytes); "
                          "'' = do not write it")
+    ap.add_argument("--stream-priority", action="store_true",
+                    help="encode / payload stream at high HIP stream priority (split schedule)")
     ap.add_argument("--force-pg", action="store_true",
                     help="initialise the process group even at world size 1 (rehearses the RCCL branch on one GPU)")
     a = ap.parse_args(argv)
@@ -236,7 +238,10 @@ def main(argv=None):
     # A dedicated stream for the library AND torch: torch's default stream is
     # handle 0, which the C ABI would replace by a private stream, and the
     # timing events must be recorded on the stream the kernels run on.
-    stream = torch.cuda.Stream(dev)
+    # --stream-priority: the step's main stream (encode, then the payload pass)
+    # at high priority, so the split acceptance pass on the decode's stream
+    # only takes wave slots the encode leaves free
+    stream = torch.cuda.Stream(dev, priority=-1 if args.stream_priority else 0)
     torch.cuda.set_stream(stream)
     ctx = fec.Context(local, stream.cuda_stream)
 
