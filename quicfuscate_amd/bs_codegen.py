@@ -392,6 +392,9 @@ class KernelSpec:
     # or only the backward (U') products of the LU run (results wrong; the
     # marginal time of ~half the per-lane products)
     lab_lu_part: str = ""
+    # lab only (fft row loop): the first n chunks' transposes, butterflies and
+    # folds dropped (their rows still load): the marginal time of row-loop VALU
+    lab_skip_chunks: int = 0
     # chunked dec, small batches: the four waves of a workgroup share ONE item,
     # each running every ksplit-th row of it; waves 1..3 hand their partial
     # syndromes to wave 0 through LDS, which solves and stores (kernel
@@ -938,6 +941,8 @@ def _fft_stream(E, ops: list, spec: KernelSpec, load_row, wait_row, acc_block, n
         if n + pd < n_rows:
             load_row(n + pd, slot(n + pd))
         wait_row(n)
+        if n < spec.lab_skip_chunks * ch:
+            continue
         ops.extend(_transpose_ops(slot(n), spec.bfi_transpose, spec.vmask))
         if n >= kA:
             work = [(0, lambda n=n: fold_direct(n))]

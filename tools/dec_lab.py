@@ -37,6 +37,18 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5e: the marginal time of row-loop VALU (the first 1 / 2 / 4 of the
+    # 8 source chunks without transposes / butterflies / folds; rows still load)
+    ("k_warm", dict(LIB_DEC4), ()),
+    ("k_lib", dict(LIB_DEC4), ()),
+    ("k_skip1", {**LIB_DEC4, "lab_skip_chunks": 1}, ()),
+    ("k_skip2", {**LIB_DEC4, "lab_skip_chunks": 2}, ()),
+    ("k_skip4", {**LIB_DEC4, "lab_skip_chunks": 4}, ()),
+    ("k_nolu_skip2", {**LIB_DEC4, "lab_skip_chunks": 2, "lu": False}, ()),
+    ("k_lib_2", dict(LIB_DEC4), ()),
+    ("k_skip2_2", {**LIB_DEC4, "lab_skip_chunks": 2}, ()),
+]
+VARIANTS_R05D = [
     # round 5d: the marginal time of the LU's per-lane products (forward only:
     # 91 products; backward only: 78; none: stores only)
     ("h_warm", dict(LIB_DEC4), ()),
