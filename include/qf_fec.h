@@ -42,6 +42,13 @@ extern "C" {
 #define QF_ABI_VERSION 1
 int qf_abi_version(void);
 const char *qf_strerror(int status);
+/* The cause of the calling thread's most recent QF_EDEVICE: the failing HIP
+ * call's source file:line and error name, and, when a generated kernel's
+ * launch checks refused the call, which check ("... (qf_bs.hip:339 launch
+ * refused)").  Thread-local, like errno: kept until the next device failure on
+ * this thread; "" if there was none.  No reference counterpart (the
+ * reference's codec has no device). */
+const char *qf_last_error(void);
 
 /* ---------------------------------------------------------------------------
  * GF(2^8) scalar helpers (host).  These mirror the reference's public GF API

@@ -38,6 +38,10 @@ class QfError(RuntimeError):
     def __init__(self, status: int, what: str = ""):
         self.status = status
         msg = _lib().qf_strerror(status).decode() if _LIB is not None else str(status)
+        # QF_EDEVICE: the failing HIP call and any refused launch check (qf_last_error)
+        self.detail = _lib().qf_last_error().decode() if (_LIB is not None and status == -5) else ""
+        if self.detail:
+            msg = f"{msg} [{self.detail}]"
         super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
 
 
@@ -96,6 +100,7 @@ _D = ctypes.c_double
 _SIGS = {
     "qf_abi_version": (_I, []),
     "qf_strerror": (ctypes.c_char_p, [_I]),
+    "qf_last_error": (ctypes.c_char_p, []),
     "qf_gf256_init": (_I, []),
     "qf_gf256_mul": (_U8, [_U8, _U8]),
     "qf_gf256_mul_add": (_U8, [_U8, _U8, _U8]),

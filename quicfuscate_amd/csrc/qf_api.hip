@@ -32,11 +32,28 @@ const Gf256& gf() {
 
 using qf::gf;
 
-#define QF_CHECK_HIP(expr)                         \
-    do {                                           \
-        hipError_t _e = (expr);                    \
-        if (_e != hipSuccess) return QF_EDEVICE;   \
-    } while (0)
+namespace qf {
+namespace {
+thread_local char t_last_error[256];
+thread_local char t_refused[96];
+}  // namespace
+
+int device_fail(const char* file, int line, hipError_t e) {
+    const char* base = strrchr(file, '/');
+    base = base ? base + 1 : file;
+    snprintf(t_last_error, sizeof t_last_error, "%s:%d: %s%s%s%s", base, line, hipGetErrorName(e),
+             t_refused[0] ? " (" : "", t_refused, t_refused[0] ? ")" : "");
+    t_refused[0] = 0;
+    return QF_EDEVICE;
+}
+
+void note_launch_refused(const char* what, int line) {
+    snprintf(t_refused, sizeof t_refused, "%s:%d launch refused", what, line);
+}
+
+const char* last_error_text() { return t_last_error; }
+}  // namespace qf
+
 
 static inline uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
@@ -210,8 +227,8 @@ void init_opts(qf_ctx* c) {
 
 int ensure_device(qf_ctx* ctx) {
     int cur = -1;
-    if (hipGetDevice(&cur) != hipSuccess) return QF_EDEVICE;
-    if (cur != ctx->device && hipSetDevice(ctx->device) != hipSuccess) return QF_EDEVICE;
+    QF_CHECK_HIP(hipGetDevice(&cur));
+    if (cur != ctx->device) QF_CHECK_HIP(hipSetDevice(ctx->device));
     return QF_OK;
 }
 
@@ -1067,6 +1084,9 @@ extern "C" {
 
 int qf_abi_version(void) { return QF_ABI_VERSION; }
 
+
+const char* qf_last_error(void) { return qf::last_error_text(); }
+
 const char* qf_strerror(int s) {
     switch (s) {
         case QF_OK: return "ok";
@@ -1108,7 +1128,8 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
     if (!out) return QF_EINVAL;
     *out = nullptr;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return QF_EDEVICE;
+    QF_CHECK_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return qf::device_fail(__FILE__, __LINE__, hipErrorInvalidDevice);
     QF_CHECK_HIP(hipSetDevice(device));
     qf_ctx* c = new qf_ctx();
     c->device = device;
@@ -1120,9 +1141,9 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
     } else if (stream) {
         c->stream = reinterpret_cast<hipStream_t>(stream);
     } else {
-        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        if (hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) {
             delete c;
-            return QF_EDEVICE;
+            return qf::device_fail(__FILE__, __LINE__, e);
         }
         c->own_stream = true;
     }
@@ -1154,8 +1175,9 @@ int qf_ctx_create(int device, void* stream, qf_ctx** out) {
               hipMemcpy(c->d_explog, el.data(), 768, hipMemcpyHostToDevice) == hipSuccess &&
               hipEventCreateWithFlags(&c->custom_done, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
+        const hipError_t e = hipGetLastError();
         qf_ctx_destroy(c);
-        return QF_EDEVICE;
+        return qf::device_fail(__FILE__, __LINE__, e != hipSuccess ? e : hipErrorOutOfMemory);
     }
     *out = c;
     return QF_OK;

@@ -14,6 +14,7 @@
 
 #include "qf_bs.h"
 #include "qf_fec.h"
+#include "qf_internal.h"
 
 struct QfBsEntry {
     uint32_t k, r, pd;
@@ -35,9 +36,11 @@ struct QfBsEntry {
 namespace qf {
 
 // QF_BS_DEBUG=1: name the check behind a hipErrorInvalidValue on stderr
+// (qf_last_error carries the refusal's line whether or not it is set)
 static hipError_t bs_invalid(int line) {
     static const bool on = getenv("QF_BS_DEBUG") != nullptr;
     if (on) fprintf(stderr, "qf_bs.hip:%d: launch refused\n", line);
+    note_launch_refused("qf_bs.hip", line);
     return hipErrorInvalidValue;
 }
 

@@ -1005,10 +1005,7 @@ int grid16(qf_ctx* ctx, uint64_t units) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)qf::ctx_num_cus(ctx)));
 }
 
-#define QF_HIP(x)                                 \
-    do {                                          \
-        if ((x) != hipSuccess) return QF_EDEVICE; \
-    } while (0)
+#define QF_HIP(x) QF_CHECK_HIP(x)
 
 }  // namespace
 

@@ -244,7 +244,7 @@ int gf16_bs_encode(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint32_t
     if (grid > 0x7FFFFFFFull) return QF_ERANGE;
     hipEvent_t ev = ctx_prof_begin(ctx, st);
     hipLaunchKernelGGL(e->fn, dim3((uint32_t)grid), dim3(256), 0, st, a);
-    if (hipGetLastError() != hipSuccess) return QF_EDEVICE;
+    QF_CHECK_HIP(hipGetLastError());
     ctx_prof_end(ctx, st, ev, e->name);
     return QF_OK;
 }
@@ -287,7 +287,7 @@ int gf16_bs_syndromes(qf_ctx* ctx, hipStream_t st, uint32_t k, uint32_t r, uint3
     if (grid > 0x7FFFFFFFull) return QF_ERANGE;
     hipEvent_t ev = ctx_prof_begin(ctx, st);
     hipLaunchKernelGGL(e->syn, dim3((uint32_t)grid), dim3(256), 0, st, a);
-    if (hipGetLastError() != hipSuccess) return QF_EDEVICE;
+    QF_CHECK_HIP(hipGetLastError());
     ctx_prof_end(ctx, st, ev, e->syn_name);
     return QF_OK;
 }

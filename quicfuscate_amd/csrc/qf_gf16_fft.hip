@@ -49,10 +49,7 @@ constexpr uint32_t kFftLdsSymbols = 8192;    // 16 KiB strips beside the 128 KiB
 constexpr uint32_t kFftLdsConsts = 8192;     // and 16 KiB of butterfly constants (k <= 2,048)
 constexpr uint32_t kFftMinK = 16;
 
-#define QF_HIP(x)                                 \
-    do {                                          \
-        if ((x) != hipSuccess) return QF_EDEVICE; \
-    } while (0)
+#define QF_HIP(x) QF_CHECK_HIP(x)
 
 struct Fft16Table {
     uint16_t W[16][16];   // W[q][m] = W_q(2^m), q <= a

@@ -23,11 +23,6 @@
 #include "qf_internal.h"
 #include "qf_kernels.h"
 
-#define QF_CHECK_HIP(expr)                         \
-    do {                                           \
-        hipError_t _e = (expr);                    \
-        if (_e != hipSuccess) return QF_EDEVICE;   \
-    } while (0)
 
 static inline uint32_t round16(uint32_t x) { return (x + 15) & ~15u; }
 

@@ -11,11 +11,6 @@
 #include "qf_fec.h"
 #include "qf_internal.h"
 
-#define QF_CHECK_HIP(expr)                       \
-    do {                                         \
-        hipError_t _e = (expr);                  \
-        if (_e != hipSuccess) return QF_EDEVICE; \
-    } while (0)
 
 namespace {
 

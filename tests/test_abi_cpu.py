@@ -106,3 +106,20 @@ def test_mirror_rejects_undersized_buffers():
         fec.decode_batch(rows, idx, rec, torch.zeros(G * r, dtype=torch.int16), i32, i32[:1], k, r, L,
                          max_rows=n, row_stride=L, rows_gen_stride=n * L, rec_row_stride=L,
                          rec_gen_stride=r * L, G=G)
+
+
+def test_last_error_names_the_failing_hip_call():
+    """qf_last_error: a QF_EDEVICE carries the failing HIP call's file:line and
+    error name.  Here (no GPU, or an out-of-range
+    device ordinal on a GPU host) qf_ctx_create fails in the library."""
+    import ctypes
+    from quicfuscate_amd import _lib as L
+
+    lib = L._lib()
+    h = ctypes.c_void_p()
+    s = lib.qf_ctx_create(1 << 20, None, ctypes.byref(h))
+    assert s == L.QF_EDEVICE
+    why = lib.qf_last_error().decode()
+    assert why.startswith("qf_api.hip:") and "hipError" in why, why
+    err = L.QfError(s, "ctx")
+    assert why in str(err) and err.detail == why

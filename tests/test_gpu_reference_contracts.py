@@ -251,3 +251,19 @@ def test_fused_send_window(qf, oracle, gpu_ctx, monkeypatch, fused, k, max_len):
             rp = enc.generate_repair_packet(j, pool)
             assert rp.len == L and bytes(rp.data[:L]) == want[j].tobytes(), (t, j)
             assert rp.id == t + 1 + j
+
+
+def test_last_error_on_the_device(qf):
+    """On a GPU host: an out-of-range device ordinal names hipErrorInvalidDevice;
+    a decode that succeeds afterwards does not clear it (errno semantics)."""
+    import ctypes
+    from quicfuscate_amd import _lib as L
+
+    lib = L._lib()
+    h = ctypes.c_void_p()
+    assert lib.qf_ctx_create(1 << 20, None, ctypes.byref(h)) == L.QF_EDEVICE
+    why = lib.qf_last_error().decode()
+    assert why.startswith("qf_api.hip:") and "hipErrorInvalidDevice" in why, why
+    with pytest.raises(L.QfError) as ei:
+        qf.check(lib.qf_ctx_create(1 << 20, None, ctypes.byref(h)), "ctx")
+    assert "hipErrorInvalidDevice" in str(ei.value)
