@@ -19,7 +19,7 @@ mkdir -p "$OUT"
 what=${1:-full}
 shift || true
 PYT="python -u -m pytest -x -q --timeout 170 --timeout-method thread"
-ARGS="--steps 3 --warmup 1 --no-cpu --host-path-G 0 --c3b-G 0 --c4-G 0 --c5-mixed-bytes 0"
+ARGS="--steps 20 --warmup 5 --no-cpu --host-path-G 0 --c3b-G 0 --c4-G 0 --c5-mixed-bytes 0"
 
 bench_line() {   # $1 log name, rest: bench args
   local name=$1

@@ -52,6 +52,9 @@ def main() -> None:
             "name": short(name),
             "calls": len(v),
             "avg_ms": round(statistics.mean(v) / 1e6, 4),
+            "median_ms": round(statistics.median(v) / 1e6, 4),
+            # the first launch of a kernel (code-object load, cold caches) aside
+            "avg_after_first_ms": round(statistics.mean(v[1:]) / 1e6, 4) if len(v) > 1 else None,
             "min_ms": round(min(v) / 1e6, 4),
             "max_ms": round(max(v) / 1e6, 4),
             "total_ms": round(sum(v) / 1e6, 4),
