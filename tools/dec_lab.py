@@ -37,6 +37,19 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5f: store cache policy -- non-temporal recovered-row stores with
+    # default-policy loads (the library: default policy for both since round 3)
+    ("p_warm", dict(LIB_DEC4), ()),
+    ("p_lib", dict(LIB_DEC4), ()),
+    ("p_stnt", {**LIB_DEC4, "st_policy": "nt"}, ()),
+    ("p_nolu", {**LIB_DEC4, "lu": False}, ()),
+    ("p_nolu_stnt", {**LIB_DEC4, "lu": False, "st_policy": "nt"}, ()),
+    ("p_lib_2", dict(LIB_DEC4), ()),
+    ("p_stnt_2", {**LIB_DEC4, "st_policy": "nt"}, ()),
+    ("p_lib_3", dict(LIB_DEC4), ()),
+    ("p_stnt_3", {**LIB_DEC4, "st_policy": "nt"}, ()),
+]
+VARIANTS_R05E = [
     # round 5e: the marginal time of row-loop VALU (the first 1 / 2 / 4 of the
     # 8 source chunks without transposes / butterflies / folds; rows still load)
     ("k_warm", dict(LIB_DEC4), ()),
