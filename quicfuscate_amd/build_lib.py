@@ -203,7 +203,9 @@ def kernel_specs() -> list:
     # tools/dec_lab.py, profiles/r03_lab_dec_policy.json: 1.485 -> 1.39 ms)
     # (round 4: interleaved LU products and 64-bit-shift transposes /
     # selectors: 1.409 -> 1.358-1.364 ms, profiles/r04d_lab_dec_ilp_s64.json)
-    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="",
+    # (round 5: non-temporal recovered-row stores, loads still at the default
+    # policy: 1.357-1.387 -> 1.345-1.352 ms, profiles/r05_lab_dec.json r05k)
+    specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="nt",
                             early_stores=True, lu_ilp=True, bfi_transpose="s64")
               for (k, r) in BS_FFT]
     # every pass of a C5 code in one dispatch ('M' plain, 'N' additive-FFT
