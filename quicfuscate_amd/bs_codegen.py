@@ -395,6 +395,10 @@ class KernelSpec:
     # lab only (fft row loop): the first n chunks' transposes, butterflies and
     # folds dropped (their rows still load): the marginal time of row-loop VALU
     lab_skip_chunks: int = 0
+    # VALU list scheduling (bs_sched.schedule): runs of plain VALU ops between
+    # non-VALU ops reordered so a producer sits >= sched ops before its
+    # consumers where the run allows it (0: program order)
+    sched: int = 0
     # chunked dec, small batches: the four waves of a workgroup share ONE item,
     # each running every ksplit-th row of it; waves 1..3 hand their partial
     # syndromes to wave 0 through LDS, which solves and stores (kernel
@@ -1172,14 +1176,25 @@ def generate(spec: KernelSpec) -> list[Op]:
     if isinstance(spec, MergedSpec):
         return _generate_merged(spec)
     if spec.mode == "cmb":
-        return _generate_cmb(spec)
-    if spec.mode == "enc":
-        return _generate_enc(spec)
-    if spec.mode == "synw":
-        return _generate_synw(spec)
-    if spec.mode == "dec" and spec.chunked:
-        return _generate_dec_chunked(spec)
-    return _generate_syn(spec)
+        ops = _generate_cmb(spec)
+    elif spec.mode == "enc":
+        ops = _generate_enc(spec)
+    elif spec.mode == "synw":
+        ops = _generate_synw(spec)
+    elif spec.mode == "dec" and spec.chunked:
+        ops = _generate_dec_chunked(spec)
+    else:
+        ops = _generate_syn(spec)
+    lat = spec.sched or _SCHED_ALL
+    if lat:
+        from . import bs_sched
+        ops = bs_sched.schedule(ops, lat)
+    return ops
+
+
+# tests only: schedule every generated kernel (BS_SCHED_ALL=<slots>), so the
+# whole emulator suite checks the scheduler on every kernel family
+_SCHED_ALL = int(__import__("os").environ.get("BS_SCHED_ALL", "0") or 0)
 
 
 @dataclasses.dataclass(frozen=True)

@@ -61,11 +61,25 @@ def variant_ops(bs, spec, flags):
                     and (acc_lo <= op.args[0] < acc_hi or ring_lo <= op.args[0] < ring_hi)):
                 continue
         out.append(op)
+    for f in flags:   # sched:N -- bs_sched list scheduling, N slots producer -> consumer
+        if f.startswith("sched:"):
+            from quicfuscate_amd import bs_sched
+            out = bs_sched.schedule(out, int(f.split(":")[1]))
     return out
 
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 5g: VALU list scheduling (bs_sched, "sched:N") of the FFT encode
+    ("u_warm", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("u_lib", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("u_s2", 64, 16, 3, ("st:nt", "ztail", "fft:8", "sched:2"), ALL),
+    ("u_s3", 64, 16, 3, ("st:nt", "ztail", "fft:8", "sched:3"), ALL),
+    ("u_s4", 64, 16, 3, ("st:nt", "ztail", "fft:8", "sched:4"), ALL),
+    ("u_lib_2", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("u_s3_2", 64, 16, 3, ("st:nt", "ztail", "fft:8", "sched:3"), ALL),
+]
+VARIANTS_R04D = [
     # round 4d: 64-bit-shift transposes in the (HBM-bound) FFT encode
     ("t_warm", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
     ("t_lib", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),

@@ -24,6 +24,20 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5g: VALU list scheduling of the merged FFT passes (bs_sched)
+    ("s196_warm", 196, 59, "N", 0, {}),
+    ("s196_lib", 196, 59, "N", 0, {}),
+    ("s196_s2", 196, 59, "N", 0, {"sched": 2}),
+    ("s196_s3", 196, 59, "N", 0, {"sched": 3}),
+    ("s196_s4", 196, 59, "N", 0, {"sched": 4}),
+    ("s160_lib", 160, 48, "N", 0, {}),
+    ("s160_s3", 160, 48, "N", 0, {"sched": 3}),
+    ("s128_lib", 128, 39, "N", 0, {}),
+    ("s128_s3", 128, 39, "N", 0, {"sched": 3}),
+    ("s196_lib_2", 196, 59, "N", 0, {}),
+    ("s196_s3_2", 196, 59, "N", 0, {"sched": 3}),
+]
+VARIANTS_R04 = [
     ("n160_lib", 160, 48, "N", 0, {}),
     ("n160_c8pd2", 160, 48, "N", 0, {"fft_coset": 8, "pd": 2}),
     ("n160_c8pd3", 160, 48, "N", 0, {"fft_coset": 8, "pd": 3}),

@@ -37,6 +37,20 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5g: VALU list scheduling (quicfuscate_amd/bs_sched.py): runs of
+    # plain VALU ops reordered so producers sit >= N ops before consumers
+    ("q_warm", dict(LIB_DEC4), ()),
+    ("q_lib", dict(LIB_DEC4), ()),
+    ("q_sched2", dict(LIB_DEC4), ("sched:2",)),
+    ("q_sched3", dict(LIB_DEC4), ("sched:3",)),
+    ("q_sched4", dict(LIB_DEC4), ("sched:4",)),
+    ("q_lib_2", dict(LIB_DEC4), ()),
+    ("q_sched2_2", dict(LIB_DEC4), ("sched:2",)),
+    ("q_sched4_2", dict(LIB_DEC4), ("sched:4",)),
+    ("q_nolu_sched4", {**LIB_DEC4, "lu": False}, ("sched:4",)),
+    ("q_nolu", {**LIB_DEC4, "lu": False}, ()),
+]
+VARIANTS_R05F = [
     # round 5f: store cache policy -- non-temporal recovered-row stores with
     # default-policy loads (the library: default policy for both since round 3)
     ("p_warm", dict(LIB_DEC4), ()),
