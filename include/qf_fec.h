@@ -164,8 +164,7 @@ enum {
                                     pass; 0 the log / Zech-table kernel for every k
                                     [QF_GF16_FFT_BS; default 1] */
     QF_OPT_PREPARE_LANES,        /* 1: the fused decode's acceptance pass runs one generation per lane
-                                    (k_decode_prepare_lu_lanes); 2: four lanes per generation
-                                    (k_decode_prepare_lu_quad); 0: one per wave [QF_PREPARE_LANES;
+                                    (k_decode_prepare_lu_lanes); 0: one per wave [QF_PREPARE_LANES;
                                     default 1] */
     QF_OPT_ENCODE_MERGED,        /* 1: multi-pass work in ONE dispatch each: the encode passes of a
                                     code with more repairs than one kernel holds (C5 r > 22; a

@@ -203,7 +203,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* GF16_FFT */ {"QF_GF16_FFT", 1, 0, 2, false},
     /* WIEDEMANN_PROJ */ {"QF_WIEDEMANN_PROJ", 1, 0, 1, false},
     /* GF16_FFT_BS */ {"QF_GF16_FFT_BS", 1, 0, 3, false},
-    /* PREPARE_LANES */ {"QF_PREPARE_LANES", 1, 0, 2, false},
+    /* PREPARE_LANES */ {"QF_PREPARE_LANES", 1, 0, 1, false},
     /* ENCODE_MERGED */ {"QF_ENCODE_MERGED", 1, 0, 1, false},
 };
 
@@ -563,7 +563,7 @@ int decode_fused(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const uint8
     pa.G = G;
     pa.lu_out = w;
     pa.lu_stride = lu_stride;
-    pa.lanes = (uint32_t)ctx->opt[QF_OPT_PREPARE_LANES];
+    pa.lanes = ctx->opt[QF_OPT_PREPARE_LANES] != 0 ? 1u : 0u;
     if (ctx->payload_wait) {
         // split phase: the acceptance pass runs beside the caller's other
         // work, on a capped persistent grid (QF_PREPARE_GRID blocks, default

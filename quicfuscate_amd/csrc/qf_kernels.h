@@ -102,7 +102,7 @@ struct PrepareCauchyArgs {
     uint8_t* lu_out;
     uint32_t lu_stride;
     uint32_t grid_cap;   // k_decode_prepare_lu: max blocks (0 = one generation per wave)
-    uint32_t lanes;      // 1: k_decode_prepare_lu_lanes (one generation per lane); 2: _quad (four lanes each)
+    uint32_t lanes;      // 1: k_decode_prepare_lu_lanes (one generation per lane)
 };
 hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t st);
 

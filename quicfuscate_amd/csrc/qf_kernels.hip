@@ -1349,198 +1349,6 @@ __global__ void __launch_bounds__(kPrepLanes) k_decode_prepare_lu_lanes(PrepareC
 }
 
 // ---------------------------------------------------------------------------
-// The same with FOUR lanes per generation (32 generations per 128-thread
-// block): lane 0 of each quad walks the row indices (the first-k-rows rule
-// is a serial scan), then the quad shares the closed-form LU: rows p = sub,
-// sub + 4, ... first compute their full log prefixes D0[p] / D1[p] (they
-// depend on row p alone), the quad exchanges them through LDS, and each
-// lane emits the L entries of its rows and the U' entries of its columns.
-// 4x the waves of the per-lane kernel (4 per SIMD at G = 65,536 instead of
-// one) and a quarter of the LU per lane: the pass is latency-bound
-// (DESIGN.md 9).  Outputs are byte-equal to k_decode_prepare_lu_lanes'
-// (tests/test_gpu_decode.py::test_decode_prepare_per_lane_matches_per_wave).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kQuadGens = 32;   // generations per 128-thread block
-
-__global__ void __launch_bounds__(4 * kQuadGens) k_decode_prepare_lu_quad(PrepareCauchyArgs a) {
-    __shared__ uint8_t sexp[512];
-    __shared__ uint8_t slog[256];
-    __shared__ __attribute__((aligned(16))) uint32_t srec[kPrepRecWords * kQuadGens];
-    __shared__ __attribute__((aligned(16))) uint32_t smp[kPrepMapWords * kQuadGens];
-    __shared__ __attribute__((aligned(16))) uint32_t sam[kPrepMaskWords * kQuadGens];
-    __shared__ uint8_t sX[16 * kQuadGens], sY[16 * kQuadGens], sJ[16 * kQuadGens];
-    __shared__ int32_t sD0[16 * kQuadGens], sD1[16 * kQuadGens];
-    __shared__ uint32_t sE[kQuadGens];
-    constexpr uint32_t T = 4 * kQuadGens;
-    for (uint32_t i = threadIdx.x; i < 768; i += T) {
-        if (i < 512) sexp[i] = a.explog[i];
-        else slog[i - 512] = a.explog[i];
-    }
-    const uint32_t tid = threadIdx.x, gl = tid >> 2, sub = tid & 3, k = a.k, r = a.r;
-    const uint32_t mw = a.map_stride / 4;
-    uint8_t* rec8 = reinterpret_cast<uint8_t*>(srec);
-    uint8_t* map8 = reinterpret_cast<uint8_t*>(smp);
-    auto rec_b = [&](uint32_t byte) -> uint8_t& { return rec8[((byte >> 2) * kQuadGens + gl) * 4 + (byte & 3)]; };
-    auto map_b = [&](uint32_t byte) -> uint8_t& { return map8[((byte >> 2) * kQuadGens + gl) * 4 + (byte & 3)]; };
-    for (uint64_t g0 = (uint64_t)blockIdx.x * kQuadGens; g0 < a.G; g0 += (uint64_t)gridDim.x * kQuadGens) {
-        __syncthreads();   // the tables (first pass) / the previous pass's copy-out
-        const uint64_t g = g0 + gl;
-        const bool live = g < a.G;
-        {
-            uint4* r4 = reinterpret_cast<uint4*>(srec);
-            const uint32_t zero4 = 64 * kQuadGens / 4, all4 = kPrepRecWords * kQuadGens / 4;
-            for (uint32_t i = tid; i < all4; i += T)
-                r4[i] = i < zero4 ? make_uint4(0, 0, 0, 0) : make_uint4(~0u, ~0u, ~0u, ~0u);
-            uint4* m4 = reinterpret_cast<uint4*>(smp);
-            for (uint32_t i = tid; i < mw * kQuadGens / 4; i += T) m4[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
-            uint4* a4 = reinterpret_cast<uint4*>(sam);
-            for (uint32_t i = tid; i < kPrepMaskWords * kQuadGens / 4; i += T) a4[i] = make_uint4(0, 0, 0, 0);
-        }
-        __syncthreads();
-        if (live && sub == 0) {
-            // decoder.rs:679-699, as k_decode_prepare_lu_lanes
-            const uint32_t n = a.n_rows ? min(a.n_rows[g], a.max_rows) : a.max_rows;
-            const uint16_t* ridx = a.row_index + g * a.max_rows;
-            uint32_t accepted = 0, rep = 0;
-            uint64_t acc64 = 0;
-            bool bad = false, dup = false;
-            auto step = [&](uint32_t s, uint32_t x) {
-                if (k <= 64) {
-                    const bool isrep = x >= k;
-                    const uint32_t j = x - k;
-                    const bool vrep = isrep && j < r;
-                    bad |= isrep && !vrep;
-                    const bool open = accepted < k;
-                    const uint64_t bit = isrep ? 0ull : 1ull << (x & 63);
-                    const bool sys_take = !isrep && open && !(acc64 & bit);
-                    const bool rep_take = vrep && open;
-                    acc64 |= sys_take ? bit : 0ull;
-                    dup |= rep_take && ((rep >> (j & 31)) & 1u);
-                    rep |= rep_take ? 1u << (j & 31) : 0u;
-                    const bool take = sys_take || rep_take;
-                    if (take) map_b(isrep ? k + j : x) = (uint8_t)s;
-                    accepted += take ? 1u : 0u;
-                    return;
-                }
-                if (x >= k) {
-                    const uint32_t j = x - k;
-                    if (j >= r) {
-                        bad = true;
-                        return;
-                    }
-                    if (accepted < k) {
-                        dup |= (rep >> j) & 1u;
-                        rep |= 1u << j;
-                        map_b(k + j) = (uint8_t)s;
-                        ++accepted;
-                    }
-                } else if (accepted < k) {
-                    uint32_t& m = sam[(x >> 5) * kQuadGens + gl];
-                    const uint32_t bit = 1u << (x & 31);
-                    if (!(m & bit)) {
-                        m |= bit;
-                        map_b(x) = (uint8_t)s;
-                        ++accepted;
-                    }
-                }
-            };
-            constexpr uint32_t kChunk = 32;
-            uint32_t cur[kChunk], nxt[kChunk];
-#pragma unroll
-            for (uint32_t q = 0; q < kChunk; ++q) cur[q] = q < n ? ridx[q] : 0xFFFFu;
-            for (uint32_t s0 = 0; s0 < n; s0 += kChunk) {
-                const bool more = s0 + kChunk < n;
-#pragma unroll
-                for (uint32_t q = 0; q < kChunk; ++q) nxt[q] = more && s0 + kChunk + q < n ? ridx[s0 + kChunk + q] : 0xFFFFu;
-#pragma unroll
-                for (uint32_t q = 0; q < kChunk; ++q)
-                    if (s0 + q < n) step(s0 + q, cur[q]);
-#pragma unroll
-                for (uint32_t q = 0; q < kChunk; ++q) cur[q] = nxt[q];
-            }
-            if (k <= 64) {
-                sam[gl] = (uint32_t)acc64;
-                sam[kQuadGens + gl] = (uint32_t)(acc64 >> 32);
-            }
-            const int32_t status = bad ? -1 : accepted < k ? -3 : dup ? -4 : 0;
-            uint32_t e = __popc(rep);
-            if (status != 0) {
-                for (uint32_t w = 0; w < mw; ++w) smp[w * kQuadGens + gl] = 0xFFFFFFFFu;
-                e = 0;
-            } else if (e > 0) {
-                uint32_t m = rep;
-                for (uint32_t q = 0; q < 16; ++q) {
-                    const uint32_t j = m ? (uint32_t)__builtin_ctz(m) : 0u;
-                    sJ[16 * gl + q] = (uint8_t)j;
-                    sX[16 * gl + q] = (uint8_t)((k + j) & 0xFF);
-                    m &= m - 1;
-                }
-                uint32_t cw = 0, cm = ~sam[gl] & (k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1));
-                for (uint32_t q = 0; q < 16; ++q) {
-                    while (cm == 0 && cw + 1 < (k + 31) / 32) {
-                        ++cw;
-                        const uint32_t lim = k - 32 * cw;
-                        cm = ~sam[cw * kQuadGens + gl] & (lim >= 32 ? 0xFFFFFFFFu : ((1u << lim) - 1));
-                    }
-                    const uint32_t y = cm ? 32 * cw + (uint32_t)__builtin_ctz(cm) : 0u;
-                    sY[16 * gl + q] = (uint8_t)y;
-                    if (q < e) a.rec_index[g * a.e_max + q] = (uint16_t)y;
-                    cm &= cm - 1;
-                }
-                for (uint32_t q = 0; q < e; ++q) rec_b(256 + sJ[16 * gl + q]) = (uint8_t)q;   // rank of repair J[q]
-            }
-            sE[gl] = e;
-            a.status[g] = status;
-            a.n_out[g] = status == 0 ? e : 0;
-        }
-        __syncthreads();
-        // the closed-form LU (k_decode_prepare_lu_lanes), rows p = sub, sub + 4, ...
-        const uint32_t e = live ? sE[gl] : 0;
-        const uint8_t* X = sX + 16 * gl;
-        const uint8_t* Y = sY + 16 * gl;
-        const uint8_t* J = sJ + 16 * gl;
-        auto put = [&](uint32_t i, uint32_t j, int32_t l0) {   // LU[i][j] -> column J[j], byte J[i]
-            const uint32_t l = (uint32_t)(l0 + 64 * 255) % 255u;
-            rec_b(16 * J[j] + J[i]) = sexp[l];
-        };
-        for (uint32_t p = sub; p < e; p += 4) {   // full prefixes of row p
-            int32_t pp0 = 0, pp1 = 0;
-            for (uint32_t q = 0; q < p; ++q) {
-                pp0 += slog[X[p] ^ X[q]] - slog[X[p] ^ Y[q]];
-                pp1 += slog[Y[p] ^ X[q]] - slog[Y[p] ^ Y[q]];
-            }
-            sD0[16 * gl + p] = pp0;
-            sD1[16 * gl + p] = pp1;
-        }
-        __syncthreads();
-        for (uint32_t p = sub; p < e; p += 4) {
-            int32_t pp0 = 0, pp1 = 0;
-            for (uint32_t q = 0; q < p; ++q) {
-                const int32_t xx = slog[X[p] ^ X[q]], xy = slog[X[p] ^ Y[q]];
-                const int32_t yx = slog[Y[p] ^ X[q]], yy = slog[Y[p] ^ Y[q]];
-                const int32_t sq = slog[X[q] ^ Y[q]];
-                put(p, q, sq - xy + pp0 - sD0[16 * gl + q]);      // L[p][q]
-                put(q, p, sq - yx + sD1[16 * gl + q] - pp1);      // U'[q][p]
-                pp0 += xx - xy;
-                pp1 += yx - yy;
-            }
-            put(p, p, slog[X[p] ^ Y[p]] + pp1 - pp0);
-        }
-        __syncthreads();
-        const uint32_t ng = (uint32_t)min<uint64_t>(kQuadGens, a.G - g0);
-        if ((a.lu_stride & 3) == 0)
-            for (uint32_t d = tid; d < ng * kPrepRecWords; d += T) {
-                const uint32_t gg = d / kPrepRecWords, w = d - gg * kPrepRecWords;
-                *reinterpret_cast<uint32_t*>(a.lu_out + (g0 + gg) * a.lu_stride + 4 * w) = srec[w * kQuadGens + gg];
-            }
-        for (uint32_t d = tid; d < ng * mw; d += T) {
-            const uint32_t gg = d / mw, w = d - gg * mw;
-            *reinterpret_cast<uint32_t*>(a.smap + (g0 + gg) * a.map_stride + 4 * w) = smp[w * kQuadGens + gg];
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Element-wise slice multiply and synthetic fill.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_mul_slice(const uint8_t* __restrict__ a,
@@ -1840,12 +1648,6 @@ hipError_t launch_decode_prepare_cauchy(const PrepareCauchyArgs& a, hipStream_t 
             // blocks); small batches keep a wave per generation: a lane's
             // walk is serial, so one generation alone finishes sooner on 64
             // lanes (the per-packet decode)
-            if (a.lanes == 2) {   // four lanes per generation (32 per block; the cap in 128-generation units)
-                uint32_t qb = (a.G + kQuadGens - 1) / kQuadGens;
-                if (a.grid_cap && qb > 4 * a.grid_cap) qb = 4 * a.grid_cap;
-                hipLaunchKernelGGL(k_decode_prepare_lu_quad, dim3(qb), dim3(4 * kQuadGens), 0, st, a);
-                return hipGetLastError();
-            }
             uint32_t lb = (a.G + kPrepLanes - 1) / kPrepLanes;
             if (a.grid_cap && lb > a.grid_cap) lb = a.grid_cap;
             hipLaunchKernelGGL(k_decode_prepare_lu_lanes, dim3(lb), dim3(kPrepLanes), 0, st, a);
