@@ -24,6 +24,18 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5h: what bounds the (196, 59) merged encode: no row loads (compute
+    # and stores only) / no VALU data work (loads, addresses, stores only)
+    ("b196_warm", 196, 59, "N", 0, {}),
+    ("b196_lib", 196, 59, "N", 0, {}),
+    ("b196_noload", 196, 59, "N", 0, {"flags": ("noload",)}),
+    ("b196_novalu", 196, 59, "N", 0, {"flags": ("novalu",)}),
+    ("b196_same", 196, 59, "N", 0, {"flags": ("same",)}),
+    ("b196_lib_2", 196, 59, "N", 0, {}),
+    ("b196_noload_2", 196, 59, "N", 0, {"flags": ("noload",)}),
+    ("b196_novalu_2", 196, 59, "N", 0, {"flags": ("novalu",)}),
+]
+VARIANTS_R05G = [
     # round 5g: VALU list scheduling of the merged FFT passes (bs_sched)
     ("s196_warm", 196, 59, "N", 0, {}),
     ("s196_lib", 196, 59, "N", 0, {}),
