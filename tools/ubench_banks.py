@@ -58,6 +58,12 @@ def _ops(kind: str) -> list[str]:
 
 KINDS = ["xor_diff", "xor_same", "bop_diff", "bop_2same", "bop_3same", "bop_dsame", "bsel_s_diff", "perm_diff",
          "perm_same"]
+# straight-line code (no loop): LINE x 64 ops unrolled, ITERS // LINE passes of
+# an outer loop -- the same op count as the looped kinds, but the code of one
+# pass is LINE times larger (instruction fetch beyond the instruction cache)
+LINES = {"bop_diff_line64": ("bop_diff", 64), "bop_diff_line512": ("bop_diff", 512),
+         "bop_diff_line2048": ("bop_diff", 2048), "xor_diff_line2048": ("xor_diff", 2048)}
+KINDS += list(LINES)
 
 
 class _Spec:
@@ -74,11 +80,13 @@ def _asm(kind: str) -> tuple[str, str]:
     from quicfuscate_amd import bs_codegen as bs
 
     name = f"ub_{kind}"
-    body = [f"s_mov_b32 s20, {ITERS}", "s_mov_b32 s40, 0x0f0f0f0f"]
+    base, line = LINES.get(kind, (kind, 1))
+    body = [f"s_mov_b32 s20, {ITERS // line}", "s_mov_b32 s40, 0x0f0f0f0f"]
     for r in range(16, 72):
         body.append(f"v_mov_b32_e32 v{r}, {r * 2654435761 & 0xFFFF}")
     body.append(".Lloop:")
-    body += _ops(kind)
+    for _ in range(line):
+        body += _ops(base)
     body += ["s_sub_u32 s20, s20, 1", "s_cmp_lg_u32 s20, 0", "s_cbranch_scc1 .Lloop", "s_endpgm"]
 
     class Op:
