@@ -61,8 +61,10 @@ KINDS = ["xor_diff", "xor_same", "bop_diff", "bop_2same", "bop_3same", "bop_dsam
 # straight-line code (no loop): LINE x 64 ops unrolled, ITERS // LINE passes of
 # an outer loop -- the same op count as the looped kinds, but the code of one
 # pass is LINE times larger (instruction fetch beyond the instruction cache)
-LINES = {"bop_diff_line64": ("bop_diff", 64), "bop_diff_line512": ("bop_diff", 512),
-         "bop_diff_line2048": ("bop_diff", 2048), "xor_diff_line2048": ("xor_diff", 2048)}
+# (s_cbranch reaches +-128 KiB: at most ~240 x 64 eight-byte ops per pass)
+LINES = {"bop_diff_line16": ("bop_diff", 16), "bop_diff_line64": ("bop_diff", 64),
+         "bop_diff_line128": ("bop_diff", 128), "bop_diff_line240": ("bop_diff", 240),
+         "xor_diff_line240": ("xor_diff", 240)}
 KINDS += list(LINES)
 
 
@@ -81,7 +83,7 @@ def _asm(kind: str) -> tuple[str, str]:
 
     name = f"ub_{kind}"
     base, line = LINES.get(kind, (kind, 1))
-    body = [f"s_mov_b32 s20, {ITERS // line}", "s_mov_b32 s40, 0x0f0f0f0f"]
+    body = [f"s_mov_b32 s20, {max(1, ITERS // line)}", "s_mov_b32 s40, 0x0f0f0f0f"]
     for r in range(16, 72):
         body.append(f"v_mov_b32_e32 v{r}, {r * 2654435761 & 0xFFFF}")
     body.append(".Lloop:")
@@ -142,7 +144,8 @@ def run():
             t1.record(stream)
             torch.cuda.synchronize()
             ms = t0.elapsed_time(t1) / 5
-            per_simd = blocks * 4 * OPS * ITERS / (cus * 4) / (ms * 1e6)
+            base, line = LINES.get(m["kind"], (m["kind"], 1))
+            per_simd = blocks * 4 * OPS * line * max(1, ITERS // line) / (cus * 4) / (ms * 1e6)
             res[f"{m['kind']}_w{w}"] = round(per_simd, 4)
             print(m["kind"], w, res[f"{m['kind']}_w{w}"], flush=True)
         hip.hipModuleUnload(mod)
