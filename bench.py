@@ -507,14 +507,13 @@ def main(argv=None):
             except Exception:
                 traffic = None
         # the roof priced is HBM (byte work, no MFMA); what actually limits the
-        # kernel comes from its SQ counters and the decode lab (DESIGN 3.2,
-        # profiles/r03_lab_dec_policy.json): the fused decode's row loop alone
-        # runs 1.20 ms, its compute alone (no row loads) 1.01 ms, and at two
-        # waves per SIMD the per-lane LU phase (v_perm products, no loads) is
-        # not hidden behind the other wave's row loads: neither the VALU nor
-        # HBM is saturated (latency of the phase alternation)
+        # kernel comes from its SQ counters and the decode lab (DESIGN 3.2
+        # "Round 5", profiles/r05_lab_dec.json): the fused decode's row loop
+        # alone (no solve, no stores) reads at 6.06 TB/s in 0.83 ms; the
+        # per-lane solve (half-rate v_perm products) and the recovered-row
+        # stores add 0.55 ms, only partly hidden behind the partner wave's loads
         if name.startswith("qf_cauchy_dec"):
-            limiter = "lu_phase_not_hidden"
+            limiter = "solve_issue_not_hidden"
         elif name.startswith(("k_combine", "k_decode_prepare")):
             limiter = "valu_issue"
         else:
