@@ -1127,7 +1127,8 @@ def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
 
 @pytest.mark.parametrize("k,rt,L,G,fft,blocks,lds", [(24, 10, 200, 3, 8, 0, 0), (20, 20, 72, 2, 0, 0, 0),
                                                       (48, 21, 4000, 2, 8, 3, 0), (40, 30, 40, 1, 0, 0, 0),
-                                                      (160, 48, 40, 1, 8, 0, 0), (48, 21, 2100, 2, 8, 0, 6)])
+                                                      (160, 48, 40, 1, 8, 0, 0), (48, 21, 2100, 2, 8, 0, 6),
+                                                      (196, 59, 40, 1, 8, 0, 0)])
 def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks, lds):
     """All passes of a code in one dispatch (MergedSpec): wave p of each
     workgroup runs pass p on the workgroup's item; a persistent grid (fewer

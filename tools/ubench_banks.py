@@ -66,6 +66,13 @@ LINES = {"bop_diff_line16": ("bop_diff", 16), "bop_diff_line64": ("bop_diff", 64
          "bop_diff_line128": ("bop_diff", 128), "bop_diff_line240": ("bop_diff", 240),
          "xor_diff_line240": ("xor_diff", 240)}
 KINDS += list(LINES)
+# the same straight-line loop copied to NB addresses: wave w of workgroup g runs
+# copy (w + 4 (g & 1)) % NB, so the CU's waves fetch NB different code streams
+# (the merged C5 encode runs 4 pass bodies of ~200 KB on every CU)
+DISTINCT = {"bop_diff_line16_d4": ("bop_diff", 16, 4), "bop_diff_line64_d4": ("bop_diff", 64, 4),
+            "bop_diff_line240_d4": ("bop_diff", 240, 4), "bop_diff_line64_d8": ("bop_diff", 64, 8),
+            "bop_diff_line240_d8": ("bop_diff", 240, 8), "xor_diff_line240_d4": ("xor_diff", 240, 4)}
+KINDS += list(DISTINCT)
 
 
 class _Spec:
@@ -82,14 +89,24 @@ def _asm(kind: str) -> tuple[str, str]:
     from quicfuscate_amd import bs_codegen as bs
 
     name = f"ub_{kind}"
-    base, line = LINES.get(kind, (kind, 1))
+    base, line, nb = DISTINCT.get(kind, LINES.get(kind, (kind, 1)) + (1,))
     body = [f"s_mov_b32 s20, {max(1, ITERS // line)}", "s_mov_b32 s40, 0x0f0f0f0f"]
     for r in range(16, 72):
         body.append(f"v_mov_b32_e32 v{r}, {r * 2654435761 & 0xFFFF}")
-    body.append(".Lloop:")
-    for _ in range(line):
-        body += _ops(base)
-    body += ["s_sub_u32 s20, s20, 1", "s_cmp_lg_u32 s20, 0", "s_cbranch_scc1 .Lloop", "s_endpgm"]
+    if nb > 1:
+        # copy index (wave + 4 (workgroup & 1)) % nb; far jumps (copies > 128 KiB apart)
+        body += ["v_lshrrev_b32_e32 v1, 6, v0", "v_readfirstlane_b32 s21, v1", "s_and_b32 s22, s2, 1",
+                 "s_lshl_b32 s22, s22, 2", "s_add_u32 s21, s21, s22", f"s_and_b32 s21, s21, {nb - 1}"]
+        for c in range(1, nb):
+            body += [f"s_cmp_lg_u32 s21, {c}", f"s_cbranch_scc1 .Lnc{c}", "s_getpc_b64 s[24:25]", f".Lfar{c}:",
+                     f"s_add_u32 s24, s24, (.Lcopy{c}-.Lfar{c})&4294967295",
+                     f"s_addc_u32 s25, s25, (.Lcopy{c}-.Lfar{c})>>32", "s_setpc_b64 s[24:25]", f".Lnc{c}:"]
+    for c in range(nb):
+        body.append(f".Lcopy{c}:")
+        body.append(f".Lloop{c}:")
+        for _ in range(line):
+            body += _ops(base)
+        body += ["s_sub_u32 s20, s20, 1", "s_cmp_lg_u32 s20, 0", f"s_cbranch_scc1 .Lloop{c}", "s_endpgm"]
 
     class Op:
         def __init__(self, s):
@@ -144,7 +161,7 @@ def run():
             t1.record(stream)
             torch.cuda.synchronize()
             ms = t0.elapsed_time(t1) / 5
-            base, line = LINES.get(m["kind"], (m["kind"], 1))
+            base, line, _ = DISTINCT.get(m["kind"], LINES.get(m["kind"], (m["kind"], 1)) + (1,))
             per_simd = blocks * 4 * OPS * line * max(1, ITERS // line) / (cus * 4) / (ms * 1e6)
             res[f"{m['kind']}_w{w}"] = round(per_simd, 4)
             print(m["kind"], w, res[f"{m['kind']}_w{w}"], flush=True)
