@@ -469,6 +469,12 @@ class KernelSpec:
     # the passes' workgroup ranges; kernarg word 32 = the coefficient records'
     # pass stride)
     pass_major: bool = False
+    # enc fft, one pass of a MergedSpec built with xchg: (waves, this wave).
+    # The pass-independent row work (loads, transposes, the chunks' inverse
+    # butterflies) is split over the workgroup's waves by chunk and handed
+    # over in LDS; each wave folds every chunk into its own pass's
+    # accumulators (_generate_enc_xchg)
+    xchg: tuple = ()
 
     @property
     def ahead(self) -> int:
@@ -533,6 +539,8 @@ class KernelSpec:
         # next chunk's first pd rows land
         if self.fft and self.lds_rows:
             return self.fft          # only the chunk itself lives in registers
+        if self.xchg:
+            return self.fft + 2      # the chunk being produced + two rows read back from LDS
         return self.pd + (self.fft + self.fft_defer if self.fft else 1)
 
     @property
@@ -588,7 +596,7 @@ class KernelSpec:
         n = self._base_free_vgpr()
         if self.vmask is not None and not (self.mode == "dec" and self.chunked):
             n += 3
-        if self.lds_rows and self.mode == "enc":
+        if (self.lds_rows or self.xchg) and self.mode == "enc":
             n += 1          # the ds_read address of the row slots
         n = (n + 7) // 8 * 8
         if n > 256:
@@ -636,6 +644,8 @@ class KernelSpec:
             return 256 * self.tab_stride + 4 * self.lds_rows * LDS_ROW_BYTES
         if self.mode == "enc" and self.lds_rows:
             return 4 * self.lds_rows * LDS_ROW_BYTES
+        if self.mode == "enc" and self.xchg:
+            return self.xchg[0] * self.fft * LDS_ROW_BYTES
         return LDS_TAB_BYTES if self.mode == "dec" else 0
 
 
@@ -1256,7 +1266,7 @@ class MergedSpec:
     def name(self) -> str:
         if self.mode == "synw":
             return f"qf_cauchy_synw{'c' if self.concat else 'm'}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
-        return f"qf_cauchy_bsm{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
+        return f"qf_cauchy_bsm{'x' if self.passes[0].xchg else ''}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
 
     @property
     def next_free_vgpr(self) -> int:
@@ -1273,13 +1283,15 @@ class MergedSpec:
     @property
     def lds_bytes(self) -> int:
         # lds_rows: each wave's row slots at s29 (its pass) x the slots' bytes
-        if self.concat:
+        if self.concat or self.passes[0].xchg:
             return max(p.lds_bytes for p in self.passes)
         return self.waves * self.passes[0].lds_rows * LDS_ROW_BYTES
 
 
-def merged_spec(passes, concat: bool = False) -> MergedSpec:
-    passes = tuple(dataclasses.replace(p, merged=not concat, head_mark=concat) for p in passes)
+def merged_spec(passes, concat: bool = False, xchg: bool = False) -> MergedSpec:
+    assert not (xchg and (concat or passes[0].mode != "enc" or not passes[0].fft or passes[0].lds_rows))
+    passes = tuple(dataclasses.replace(p, merged=not concat, head_mark=concat,
+                                       xchg=(len(passes), n) if xchg else ()) for n, p in enumerate(passes))
     assert 1 < len(passes) <= 16 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
                                         for p in passes)
     assert len({p.lds_rows for p in passes}) == 1 and (not passes[0].lds_rows or passes[0].fft)
@@ -1346,6 +1358,8 @@ def _store_pair(E, acc: int, ma: int, mb: int, pol: str = ""):
 
 
 def _generate_enc(spec: KernelSpec) -> list[Op]:
+    if spec.xchg:
+        return _generate_enc_xchg(spec)
     k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
     assert spec.j0 + r <= spec.rt
     C = cauchy(k, spec.rt)[spec.j0: spec.j0 + r]
@@ -1444,6 +1458,156 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
         ops.extend(_transpose_ops(blk(j), spec.bfi_transpose, spec.vmask))
     if ks > 1:   # partial repairs of waves 1.. into wave 0 (temps: the ring, dead now)
         _ksplit_reduce(E, ks, r, acc0, ring0, ring0 + 8, 0, jmax_guard=False)
+    _enc_store_repairs(E, spec, blk)
+    if ks > 1:
+        _ksplit_epilogue(E)
+    else:
+        _epilogue_next_item(E, far=spec.far)
+    return ops
+
+
+def xchg_groups(P) -> list[tuple[list[int], list, list]]:
+    """The row groups of an additive-FFT pass plan, in fold order: every
+    chunk (plan rows hc*ch .. hc*ch + ch - 1, its inverse butterflies, each
+    row's accumulator constants) and then the rows that enter directly (no
+    butterflies).  The groups depend on the plan's source side only, the
+    constants on the pass."""
+    ch = P.ch
+    kA = getattr(P, "kA", 0) or P.k
+    groups = [(list(range(hc * ch, hc * ch + ch)), P.chunk_bfly[hc], [P.acc[(hc, m)] for m in range(ch)])
+              for hc in range(kA // ch)]
+    direct = sorted(getattr(P, "direct", {}))
+    for q in range(0, len(direct), ch):
+        rows = direct[q: q + ch]
+        groups.append((rows, [], [P.direct[n] for n in rows]))
+    return groups
+
+
+def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
+    """One wave's stream of a merged additive-FFT encode whose waves share
+    the row work (MergedSpec with xchg).  Every pass of a code streams the
+    same source rows through the same chunk transforms (xchg_groups: only the
+    fold constants and the final butterflies depend on the pass), so wave w of
+    the workgroup loads, transposes and inverse-transforms only the groups
+    n * W + w (round n, W waves) and writes their planes to its LDS slot;
+    after a barrier every wave folds the round's W groups from LDS into its
+    own pass's accumulators, and a second barrier frees the slots.  Per wave
+    that is 1/W of the loads, transposes and chunk butterflies (58 % of a
+    (196, 59) pass's VALU before) and 1/W of the code they take.  The loads of
+    a wave's next group are issued as soon as its planes are in LDS, so they
+    fly during the fold phase.  Every stream has the same barrier sequence
+    and item loop, so the workgroup's waves meet at every barrier."""
+    nw, me = spec.xchg
+    P = spec.fplan
+    ch = P.ch
+    ring0, acc0 = spec.ring0, spec.acc0
+    rowbuf = (ring0 + 8 * ch, ring0 + 8 * ch + 8)
+    v_ldsa = spec.next_free_vgpr - 1
+    tmp = tuple(range(V_T, V_T + 4)) if spec.fft_cse else ()
+    groups = xchg_groups(P)
+    G = len(groups)
+    nrounds = -(-G // nw)
+    slot_bytes = ch * LDS_ROW_BYTES
+    assert nw * slot_bytes <= 65536 and all(len(g[0]) <= ch for g in groups)
+    ops: list[Op] = []
+    E = ops.append
+    _prologue(E, spec)
+    E(Op("v_lshl", (v_ldsa, 4, V_LANE)))      # LDS byte offset of the lane's 16-B unit A
+    cur = [0]            # source row the row pointers address (row 0 after the item setup)
+
+    def load_group(gi: int):
+        for m, n in enumerate(groups[gi][0]):
+            i = P.order[n]
+            if i != cur[0]:
+                E(Op("s_mul_k", (46, 10, i - cur[0])))     # (i - cur) * row stride, signed
+                E(Op("s_ashr31", (47, 46)))
+                E(Op("v_add64_s", (V_SRCA, V_SRCA, 46)))
+                E(Op("v_add64_s", (V_SRCB, V_SRCB, 46)))
+                cur[0] = i
+            base = ring0 + 8 * m
+            for h, (vm, va) in enumerate(((26, V_SRCA), (24, V_SRCB))):
+                E(Op("s_exec", (vm,)))
+                E(Op("load16", (base + 4 * h, va, 0, spec.ld_policy)))
+            E(Op("s_exec", (None,)))
+
+    def produce(gi: int):
+        rows, bfly, _ = groups[gi]
+        E(Op("s_waitcnt_vm", (0,)))
+        for m in range(len(rows)):
+            ops.extend(_transpose_ops(ring0 + 8 * m, spec.bfi_transpose, spec.vmask))
+        for i, j, c in bfly:           # y_j ^= y_i; y_i ^= c y_j (lch_fft.Plan.chunk_bfly)
+            yi, yj = ring0 + 8 * i, ring0 + 8 * j
+            for b in range(8):
+                E(Op("v_xor", (yj + b, yj + b, yi + b)))
+            if c:
+                _macc(E, yi, yj, c, init=False, tmp=tmp)
+        for m in range(len(rows)):
+            off = me * slot_bytes + m * LDS_ROW_BYTES
+            E(Op("ds_write_b128", (v_ldsa, ring0 + 8 * m, off)))
+            E(Op("ds_write_b128", (v_ldsa, ring0 + 8 * m + 4, off + 1024)))
+        E(Op("s_waitcnt_lgkm_n", (0,)))      # planes in LDS; the chunk registers are free
+
+    inited: set = set()
+
+    def consume(rnd: int):
+        seq = [(q, m) for q in range(nw) if rnd * nw + q < G for m in range(len(groups[rnd * nw + q][0]))]
+
+        def read(x: int):
+            q, m = seq[x]
+            buf = rowbuf[x % 2]
+            off = q * slot_bytes + m * LDS_ROW_BYTES
+            E(Op("ds_read_b128", (buf, v_ldsa, off)))
+            E(Op("ds_read_b128", (buf + 4, v_ldsa, off + 1024)))
+        read(0)
+        for x, (q, m) in enumerate(seq):
+            if x + 1 < len(seq):
+                read(x + 1)
+                E(Op("s_waitcnt_lgkm_n", (2,)))
+            else:
+                E(Op("s_waitcnt_lgkm_n", (0,)))
+            for t, c in groups[rnd * nw + q][2][m]:
+                _macc(E, acc0 + 8 * t, rowbuf[x % 2], c, init=t not in inited, tmp=tmp)
+                inited.add(t)
+
+    def mine(rnd: int):
+        gi = rnd * nw + me
+        return gi if gi < G else None
+
+    if mine(0) is not None:
+        load_group(mine(0))
+    for rnd in range(nrounds):
+        gi = mine(rnd)
+        if gi is not None:
+            produce(gi)
+            if mine(rnd + 1) is not None:
+                load_group(mine(rnd + 1))
+        E(Op("s_barrier", ()))
+        consume(rnd)
+        E(Op("s_barrier", ()))
+    for t in range(P.R):
+        if t not in inited:
+            for b in range(8):
+                E(Op("v_movk", (acc0 + 8 * t + b, 0)))
+    for i, j, c in P.final_bfly:
+        ei, ej = acc0 + 8 * i, acc0 + 8 * j
+        if c:
+            _macc(E, ei, ej, c, init=False, tmp=tmp)
+        for b in range(8):
+            E(Op("v_xor", (ej + b, ej + b, ei + b)))
+
+    def blk(j):
+        return acc0 + 8 * P.out_block[j]
+    for j in range(spec.r):
+        ops.extend(_transpose_ops(blk(j), spec.bfi_transpose, spec.vmask))
+    _enc_store_repairs(E, spec, blk)
+    _epilogue_next_item(E, far=spec.far)
+    return ops
+
+
+def _enc_store_repairs(E, spec: KernelSpec, blk):
+    """The repairs (byte form in the accumulator blocks blk(j)) to memory:
+    padding lanes zeroed, the partial last unit masked, 2 x 16 B per lane."""
+    r = spec.r
     # padding lanes (stored, not loaded: the zero tail) hold garbage, since
     # masked loads leave stale planes in their half of the ring; byte
     # positions are independent, so clearing their half of the repairs here
@@ -1476,11 +1640,6 @@ def _generate_enc(spec: KernelSpec) -> list[Op]:
     E(Op("s_nop", (4,)))
     for j in range(r):
         _store_pair(E, blk(j), S_STA, S_STB, spec.st_policy)
-    if ks > 1:
-        _ksplit_epilogue(E)
-    else:
-        _epilogue_next_item(E, far=spec.far)
-    return ops
 
 
 def _jmax(E, k: int, r: int, present):

@@ -223,9 +223,13 @@ def kernel_specs() -> list:
     # (tools/gpu_r04_c5fft.sh, profiles/r04v_c5_passes.json: 1,508 -> 1,962 GiB/s
     # at (160, 48), 1,347 -> 1,552 at (196, 59), 2,371 -> 2,600 at (128, 39);
     # (128, 20) keeps its single plain pass: 4,568 against 3,806 merged FFT)
+    # (round 5: the passes' waves share loads, transposes and chunk butterflies
+    # through LDS, xchg: 0.506-0.541 -> 0.323-0.325 ms at (196, 59), 0.446 ->
+    # 0.320 at (160, 48), 0.438 -> 0.304 at (128, 39), bit-exact,
+    # tools/c5_lab.py, profiles/r05u_c5_xchg.json)
     for k, rt in BS_FFT_PASSES:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
-                                     for j0, rp in lch_fft.coset_passes(k, rt)]))
+                                     for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))
     # the synw passes of the C5 codes in one pass-major dispatch: one launch
     # of P x n workgroups instead of P launches of n, so a pass's last, partly
     # filled round overlaps the next pass's first; 'Y' the additive-FFT passes

@@ -1125,6 +1125,46 @@ def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
             assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
 
 
+@pytest.mark.parametrize("k,rt,L,G,blocks", [(24, 10, 200, 3, 0), (48, 21, 2100, 2, 3), (20, 20, 72, 2, 0),
+                                            (196, 59, 40, 1, 0), (160, 48, 40, 1, 0), (128, 39, 100, 2, 1)])
+def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks):
+    """The merged additive-FFT encode whose waves share the row work through
+    LDS (merged_spec(xchg=True), _generate_enc_xchg): wave w produces groups
+    w, w + W, ... into its LDS slot, every wave folds every group; the
+    workgroup's waves run together (shared LDS, s_barrier), persistent grids
+    included; every repair byte equals the oracle's."""
+    from quicfuscate_amd import lch_fft
+
+    Lv = bs.padded_units(L)
+    rng = np.random.default_rng(k * 19 + rt + L)
+    srs = (L + 15) // 16 * 16 + 16 * (k % 2)
+    sgs = k * srs
+    drs = 16 * Lv + 64
+    dgs = rt * drs
+    src = rng.integers(0, 256, G * sgs + 64, dtype=np.uint8)
+    dst = np.full(G * dgs, 0xEE, np.uint8)
+    passes = [bs.KernelSpec(k, rp, 3, r_total=rt, j0=j0, fft=8, ld_policy="") for j0, rp in lch_fft.coset_passes(k, rt)]
+    ms = bs.merged_spec(passes, xchg=True)
+    assert ms.waves == len(passes) > 1 and ms.lds_bytes == ms.waves * 8 * bs.LDS_ROW_BYTES
+    emu = bs.Emulator(bs.generate(ms))
+    SRC, DST = 0x10000000, 0x40000000
+    emu.add_buffer(SRC, src)
+    emu.add_buffer(DST, dst)
+    _, _, items = bs.launch_geometry(L, G, Lv)
+    wgs = blocks or items
+    ka = bs.kernargs(SRC, DST, sgs, dgs, srs, drs, L, G, wgs, Lv=Lv, zero_tail=True)
+    for wg in range(wgs):
+        emu.run_workgroup(ka, wg, ms.waves, ms.lds_bytes)
+    for g in range(G):
+        rows = np.stack([src[g * sgs + i * srs: g * sgs + i * srs + L] for i in range(k)])
+        want = oracle.encode(rows, rt)
+        for j in range(rt):
+            off = g * dgs + j * drs
+            assert (dst[off: off + L] == want[j]).all(), (g, j)
+            assert (dst[off + L: off + 16 * Lv] == 0).all(), (g, j)
+            assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
+
+
 @pytest.mark.parametrize("k,rt,L,G,fft,blocks,lds", [(24, 10, 200, 3, 8, 0, 0), (20, 20, 72, 2, 0, 0, 0),
                                                       (48, 21, 4000, 2, 8, 3, 0), (40, 30, 40, 1, 0, 0, 0),
                                                       (160, 48, 40, 1, 8, 0, 0), (48, 21, 2100, 2, 8, 0, 6),

@@ -24,6 +24,19 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5u: the waves of a merged FFT encode share loads, transposes and
+    # chunk butterflies through LDS (merged_spec(xchg=True))
+    ("x196_warm", 196, 59, "N", 0, {}),
+    ("x196_lib", 196, 59, "N", 0, {}),
+    ("x196_xchg", 196, 59, "N", 0, {"xchg": True}),
+    ("x160_lib", 160, 48, "N", 0, {}),
+    ("x160_xchg", 160, 48, "N", 0, {"xchg": True}),
+    ("x128_lib", 128, 39, "N", 0, {}),
+    ("x128_xchg", 128, 39, "N", 0, {"xchg": True}),
+    ("x196_lib_2", 196, 59, "N", 0, {}),
+    ("x196_xchg_2", 196, 59, "N", 0, {"xchg": True}),
+]
+VARIANTS_R05H = [
     # round 5h: what bounds the (196, 59) merged encode: no row loads (compute
     # and stores only) / no VALU data work (loads, addresses, stores only)
     ("b196_warm", 196, 59, "N", 0, {}),
@@ -80,11 +93,12 @@ def make_spec(bs, k, rt, kind, npass, kw):
     from quicfuscate_amd import lch_fft
 
     pd = kw.get("pd", 3)
-    extra = {x: v for x, v in kw.items() if x not in ("pd", "flags")}
+    extra = {x: v for x, v in kw.items() if x not in ("pd", "flags", "xchg")}
     if kind == "N":
         R = extra.get("fft_coset", 16)
         passes = [bs.KernelSpec(k, rp, pd, "enc", fft=8, ld_policy="", r_total=rt, j0=j0, **extra)
                   for j0, rp in lch_fft.coset_passes(k, rt, R)]
+        return bs.merged_spec(passes, xchg=bool(kw.get("xchg")))
     else:
         cuts = [rt * p // npass for p in range(npass + 1)]
         passes = [bs.KernelSpec(k, cuts[p + 1] - cuts[p], pd, "enc", r_total=rt, j0=cuts[p], **extra)
