@@ -172,6 +172,10 @@ enum {
                                     is read from HBM once), and the decode's syndrome and payload
                                     passes (pass-major workgroup ranges); 0: one launch per pass
                                     [QF_ENCODE_MERGED; default 1] */
+    QF_OPT_SYNW_SHARED,          /* 1: the additive-FFT syndrome passes of the C5 decode item-major in
+                                    one dispatch, the passes' waves sharing the source rows' gather,
+                                    transposes and chunk butterflies through LDS; 0: pass-major
+                                    (each pass re-reads the sources) [QF_SYNW_SHARED; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

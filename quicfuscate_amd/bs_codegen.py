@@ -596,7 +596,7 @@ class KernelSpec:
         n = self._base_free_vgpr()
         if self.vmask is not None and not (self.mode == "dec" and self.chunked):
             n += 3
-        if (self.lds_rows or self.xchg) and self.mode == "enc":
+        if (self.lds_rows and self.mode == "enc") or self.xchg:
             n += 1          # the ds_read address of the row slots
         n = (n + 7) // 8 * 8
         if n > 256:
@@ -644,7 +644,7 @@ class KernelSpec:
             return 256 * self.tab_stride + 4 * self.lds_rows * LDS_ROW_BYTES
         if self.mode == "enc" and self.lds_rows:
             return 4 * self.lds_rows * LDS_ROW_BYTES
-        if self.mode == "enc" and self.xchg:
+        if self.xchg:
             return self.xchg[0] * self.fft * LDS_ROW_BYTES
         return LDS_TAB_BYTES if self.mode == "dec" else 0
 
@@ -1265,7 +1265,8 @@ class MergedSpec:
     @property
     def name(self) -> str:
         if self.mode == "synw":
-            return f"qf_cauchy_synw{'c' if self.concat else 'm'}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
+            return (f"qf_cauchy_synw{'c' if self.concat else 'm'}{'x' if self.passes[0].xchg else ''}"
+                    f"{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}")
         return f"qf_cauchy_bsm{'x' if self.passes[0].xchg else ''}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
 
     @property
@@ -1289,7 +1290,7 @@ class MergedSpec:
 
 
 def merged_spec(passes, concat: bool = False, xchg: bool = False) -> MergedSpec:
-    assert not (xchg and (concat or passes[0].mode != "enc" or not passes[0].fft or passes[0].lds_rows))
+    assert not (xchg and (concat or passes[0].mode not in ("enc", "synw") or not passes[0].fft or passes[0].lds_rows))
     passes = tuple(dataclasses.replace(p, merged=not concat, head_mark=concat,
                                        xchg=(len(passes), n) if xchg else ()) for n, p in enumerate(passes))
     assert 1 < len(passes) <= 16 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
@@ -1359,7 +1360,7 @@ def _store_pair(E, acc: int, ma: int, mb: int, pol: str = ""):
 
 def _generate_enc(spec: KernelSpec) -> list[Op]:
     if spec.xchg:
-        return _generate_enc_xchg(spec)
+        return _generate_xchg(spec)
     k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
     assert spec.j0 + r <= spec.rt
     C = cauchy(k, spec.rt)[spec.j0: spec.j0 + r]
@@ -1483,8 +1484,8 @@ def xchg_groups(P) -> list[tuple[list[int], list, list]]:
     return groups
 
 
-def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
-    """One wave's stream of a merged additive-FFT encode whose waves share
+def _generate_xchg(spec: KernelSpec) -> list[Op]:
+    """One wave's stream of a merged additive-FFT encode (or synw) whose waves share
     the row work (MergedSpec with xchg).  Every pass of a code streams the
     same source rows through the same chunk transforms (xchg_groups: only the
     fold constants and the final butterflies depend on the pass), so wave w of
@@ -1496,7 +1497,15 @@ def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
     (196, 59) pass's VALU before) and 1/W of the code they take.  The loads of
     a wave's next group are issued as soon as its planes are in LDS, so they
     fly during the fold phase.  Every stream has the same barrier sequence
-    and item loop, so the workgroup's waves meet at every barrier."""
+    and item loop, so the workgroup's waves meet at every barrier.
+
+    synw (decode syndromes, slot-map gather): the groups' rows are the
+    received sources (the zero row where absent), the pass's accepted repairs
+    are XORed onto its syndromes in byte form at the end (their loads issued
+    once the wave's last group is in LDS), and a wave whose pass no
+    generation of the item needs (s[SW_SKIP]) still produces its groups but
+    skips its folds and stores."""
+    synw = spec.mode == "synw"
     nw, me = spec.xchg
     P = spec.fplan
     ch = P.ch
@@ -1512,11 +1521,17 @@ def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
     ops: list[Op] = []
     E = ops.append
     _prologue(E, spec)
+    if synw:
+        _synw_item_setup(E, spec)
     E(Op("v_lshl", (v_ldsa, 4, V_LANE)))      # LDS byte offset of the lane's 16-B unit A
     cur = [0]            # source row the row pointers address (row 0 after the item setup)
+    quad = [None]        # synw: the slot-map quad in s[SW_Q0..] / s[SW_Q1..]
 
     def load_group(gi: int):
         for m, n in enumerate(groups[gi][0]):
+            if synw:
+                _synw_load_row(E, spec, quad, "src", P.order[n], ring0 + 8 * m)
+                continue
             i = P.order[n]
             if i != cur[0]:
                 E(Op("s_mul_k", (46, 10, i - cur[0])))     # (i - cur) * row stride, signed
@@ -1551,6 +1566,8 @@ def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
 
     def consume(rnd: int):
         seq = [(q, m) for q in range(nw) if rnd * nw + q < G for m in range(len(groups[rnd * nw + q][0]))]
+        if synw:
+            E(Op("s_cmp_lg_k_br", (SW_SKIP, 0, f".Lnofold{rnd}")))
 
         def read(x: int):
             q, m = seq[x]
@@ -1568,6 +1585,15 @@ def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
             for t, c in groups[rnd * nw + q][2][m]:
                 _macc(E, acc0 + 8 * t, rowbuf[x % 2], c, init=t not in inited, tmp=tmp)
                 inited.add(t)
+        if synw:
+            E(Op("label", (f".Lnofold{rnd}",)))
+
+    per_row = 0 if spec.lab_norows else 4
+    issued: list = []     # synw: repair rows in load order (per_row loads each)
+
+    def load_repair(j: int):
+        _synw_load_row(E, spec, quad, "rep", j, ring0 + 8 * (j % ch))
+        issued.append(j)
 
     def mine(rnd: int):
         gi = rnd * nw + me
@@ -1575,15 +1601,26 @@ def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
 
     if mine(0) is not None:
         load_group(mine(0))
+    elif synw:
+        for j in range(min(ch, spec.r)):
+            load_repair(j)
     for rnd in range(nrounds):
         gi = mine(rnd)
         if gi is not None:
             produce(gi)
             if mine(rnd + 1) is not None:
                 load_group(mine(rnd + 1))
+            elif synw:        # the wave's last group: its chunk registers take the first repairs
+                for j in range(min(ch, spec.r)):
+                    load_repair(j)
         E(Op("s_barrier", ()))
         consume(rnd)
         E(Op("s_barrier", ()))
+    if synw:
+        E(Op("s_cmp_eq_k_br", (SW_SKIP, 0, ".Lfold_all")))
+        E(Op("s_waitcnt_vm", (0,)))
+        E(Op("s_far_jump", (".Lskip", 3)))
+        E(Op("label", (".Lfold_all",)))
     for t in range(P.R):
         if t not in inited:
             for b in range(8):
@@ -1599,7 +1636,20 @@ def _generate_enc_xchg(spec: KernelSpec) -> list[Op]:
         return acc0 + 8 * P.out_block[j]
     for j in range(spec.r):
         ops.extend(_transpose_ops(blk(j), spec.bfi_transpose, spec.vmask))
-    _enc_store_repairs(E, spec, blk)
+        if synw:      # + the accepted repair (byte form); its registers then take repair j + ch
+            E(Op("s_waitcnt_vm", (per_row * (len(issued) - 1 - issued.index(j)),)))
+            base = ring0 + 8 * (j % ch)
+            for b in range(8):
+                E(Op("v_xor", (blk(j) + b, blk(j) + b, base + b)))
+            if j + ch < spec.r:
+                load_repair(j + ch)
+    if synw:
+        E(Op("s_nop", (4,)))
+        for j in range(spec.r):
+            _store_pair(E, blk(j), S_STA, S_STB, spec.st_policy)
+        E(Op("label", (".Lskip",)))
+    else:
+        _enc_store_repairs(E, spec, blk)
     _epilogue_next_item(E, far=spec.far)
     return ops
 
@@ -1917,10 +1967,14 @@ def _scalar_gen_base(E, dst: int, base_s: int, gs_s: int, tab_s: int, g: int, ta
     E(Op("label", (f".Lsgd{tag}",)))
 
 
+SW_SKIP = 81   # xchg synw: 1 when the item's generations accepted no repair of this pass
+
+
 def _synw_item_setup(E, spec: KernelSpec):
     """Per item: g0 / g1, the four load-lane masks, both generations' row
     bases and slot-map pointers; items whose generations accepted no repair
-    of this pass (bound <= j0 for both) skip to the next item."""
+    of this pass (bound <= j0 for both) skip to the next item (xchg: set
+    s[SW_SKIP] instead -- the wave still produces its share of the rows)."""
     E(Op("s_exec", (None,)))
     E(Op("v_readfirstlane", (SW_G0, V_GA)))          # lane 0, unit A: the item's first unit
     E(Op("s_addk", (SW_G1, SW_G0, 1)))
@@ -1948,8 +2002,45 @@ def _synw_item_setup(E, spec: KernelSpec):
     E(Op("s_cmp_le_k_br", (SW_T0, spec.j0, ".Lskipnear")))
     E(Op("s_branch", (".Lnobound",)))
     E(Op("label", (".Lskipnear",)))
-    E(Op("s_far_jump", (".Lskip", 2)) if spec.far else Op("s_branch", (".Lskip",)))
+    if spec.xchg:
+        E(Op("s_movk", (SW_SKIP, 1)))
+        E(Op("s_branch", (".Lsetup_end",)))
+    else:
+        E(Op("s_far_jump", (".Lskip", 2)) if spec.far else Op("s_branch", (".Lskip",)))
     E(Op("label", (".Lnobound",)))
+    if spec.xchg:
+        E(Op("s_movk", (SW_SKIP, 0)))
+        E(Op("label", (".Lsetup_end",)))
+
+
+def _synw_load_row(E, spec: KernelSpec, quad: list, kind: str, idx: int, b: int):
+    """Loads of source row idx ("src") or pass repair idx ("rep") of both of
+    the item's generations into b .. b + 7 (the zero row where the slot map
+    says absent): the slot byte from the scalar map quad (re-read when the
+    row's quad changes, quad[0] tracks it), four masked saddr loads."""
+    k = spec.k
+    pos = k + spec.j0 + idx if kind == "rep" else idx
+    q = pos // 16
+    if quad[0] != q:
+        E(Op("s_load_x4", (SW_Q0, SW_M0, 16 * q)))
+        E(Op("s_load_x4", (SW_Q1, SW_M1, 16 * q)))
+        E(Op("s_waitcnt_lgkm", ()))
+        quad[0] = q
+    w, sh = (pos % 16) // 4, 8 * (pos % 4)
+    for qb, base, R, t in ((SW_Q0, SW_BASE0, SW_R0, SW_T0), (SW_Q1, SW_BASE1, SW_R1, SW_T1)):
+        E(Op("s_bfe_k", (t, qb + w, sh, 8)))
+        E(Op("s_mul", (base, t, 10)))
+        E(Op("s_mul_hi", (base + 1, t, 10)))
+        E(Op("s_add_cc", (base, base, R)))
+        E(Op("s_addc", (base + 1, base + 1, R + 1)))
+        E(Op("s_cmp_eq_k", (t, ABSENT)))
+        E(Op("s_cselect64", (base, 22, base)))
+    for mask, voff, d, sb in ((SW_A0, V_SRCA, b, SW_BASE0), (SW_A1, V_SRCA, b, SW_BASE1),
+                              (SW_B0, V_SRCB, b + 4, SW_BASE0), (SW_B1, V_SRCB, b + 4, SW_BASE1)):
+        E(Op("s_exec", (mask,)))
+        if not spec.lab_norows:
+            E(Op("load16_saddr", (d, voff, sb, spec.ld_policy)))
+    E(Op("s_exec", (None,)))
 
 
 def _generate_synw(spec: KernelSpec) -> list[Op]:
@@ -1966,6 +2057,8 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
     Rows stream as in _generate_syn (repairs initialise the accumulators);
     syndromes of all r repairs are stored, the unaccepted ones are junk the
     combine never reads."""
+    if spec.xchg:
+        return _generate_xchg(spec)
     k, r, pd, nbuf = spec.k, spec.r, spec.pd, spec.nbuf
     C = cauchy(k, spec.rt)[spec.j0: spec.j0 + r]
     acc0, ring0 = spec.acc0, spec.ring0
@@ -1977,31 +2070,9 @@ def _generate_synw(spec: KernelSpec) -> list[Op]:
     quad = [None]
 
     def load_row(n: int, b: Optional[int] = None, order=seq):
-        kind, idx = order[n]
-        pos = k + spec.j0 + idx if kind == "rep" else idx
-        q = pos // 16
-        if quad[0] != q:
-            E(Op("s_load_x4", (SW_Q0, SW_M0, 16 * q)))
-            E(Op("s_load_x4", (SW_Q1, SW_M1, 16 * q)))
-            E(Op("s_waitcnt_lgkm", ()))
-            quad[0] = q
-        w, sh = (pos % 16) // 4, 8 * (pos % 4)
-        for qb, base, R, t in ((SW_Q0, SW_BASE0, SW_R0, SW_T0), (SW_Q1, SW_BASE1, SW_R1, SW_T1)):
-            E(Op("s_bfe_k", (t, qb + w, sh, 8)))
-            E(Op("s_mul", (base, t, 10)))
-            E(Op("s_mul_hi", (base + 1, t, 10)))
-            E(Op("s_add_cc", (base, base, R)))
-            E(Op("s_addc", (base + 1, base + 1, R + 1)))
-            E(Op("s_cmp_eq_k", (t, ABSENT)))
-            E(Op("s_cselect64", (base, 22, base)))
         if b is None:
             b = ring0 + 8 * (n % nbuf)
-        for mask, voff, d, sb in ((SW_A0, V_SRCA, b, SW_BASE0), (SW_A1, V_SRCA, b, SW_BASE1),
-                                  (SW_B0, V_SRCB, b + 4, SW_BASE0), (SW_B1, V_SRCB, b + 4, SW_BASE1)):
-            E(Op("s_exec", (mask,)))
-            if not spec.lab_norows:
-                E(Op("load16_saddr", (d, voff, sb, spec.ld_policy)))
-        E(Op("s_exec", (None,)))
+        _synw_load_row(E, spec, quad, *order[n], b)
 
     n_seq = len(seq)
     per_row = 0 if spec.lab_norows else 4

@@ -49,6 +49,7 @@ BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
 # block decode (128, 39) 1,470 -> 1,784 GiB/s, (160, 48) 1,536 -> 1,700;
 # (196, 59) 1,383 -> 1,262: three FFT passes run against two plain ones)
 BS_FFT_SYNW = [(128, 39), (160, 48)]
+BS_FFT_SYNW_SHARED = [(128, 39), (160, 48), (196, 59)]
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
@@ -238,6 +239,12 @@ def kernel_specs() -> list:
     for k, rt in BS_FFT_SYNW:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt,
                                                    j0=j0) for j0, rp in lch_fft.coset_passes(k, rt)], concat=True))
+    # the FFT synw passes item-major, their waves sharing the row gather,
+    # transposes and chunk butterflies through LDS ('Z', QF_SYNW_SHARED; the
+    # sources are read once instead of once per pass)
+    for k, rt in BS_FFT_SYNW_SHARED:
+        specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt,
+                                                   j0=j0) for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))
     for k, rt in BS_ENC_ONLY:
         npass = -(-rt // BS_PASS)
         if npass == 1:
@@ -279,7 +286,10 @@ def _bs_kernels(build_dir: Path) -> Path:
         hexs = ",".join(str(b) for b in data)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         if isinstance(spec, bs.MergedSpec):
-            mode = ("Y" if spec.fft else "X") if spec.mode == "synw" else ("N" if spec.fft else "M")
+            if spec.mode == "synw":
+                mode = ("Z" if spec.passes[0].xchg else "Y") if spec.fft else "X"
+            else:
+                mode = "N" if spec.fft else "M"
         elif spec.chunked:
             mode = "C" if spec.fft else "k" if spec.ksplit > 1 else "c"
         elif spec.fft:

@@ -205,6 +205,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* GF16_FFT_BS */ {"QF_GF16_FFT_BS", 1, 0, 3, false},
     /* PREPARE_LANES */ {"QF_PREPARE_LANES", 1, 0, 1, false},
     /* ENCODE_MERGED */ {"QF_ENCODE_MERGED", 1, 0, 1, false},
+    /* SYNW_SHARED */ {"QF_SYNW_SHARED", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }

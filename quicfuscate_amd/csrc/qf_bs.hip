@@ -24,6 +24,7 @@ struct QfBsEntry {
                 // 'f' the encode (passes of C5 codes) with an item's sources split the same way,
                 // 'M' / 'N' every encode pass of a code in one dispatch (plain / additive-FFT passes),
                 // 'X' / 'Y' every 'w' pass in one pass-major dispatch (plain / additive-FFT passes)
+                // 'Z' the additive-FFT 'w' passes item-major, one wave per pass, row work shared in LDS
     uint32_t map_stride;
     const char* name;
     const unsigned char* data;
@@ -99,8 +100,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // the combine never stores); the lane-chunk decode ('c': the lane holding
     // the last unit stores it bytewise); never the item-layout decode ('d')
     const bool chunked = e->mode == 'c' || e->mode == 'k' || e->mode == 'C';
-    const bool merged = e->mode == 'M' || e->mode == 'N';
-    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E' || merged;
+    const bool merged = e->mode == 'M' || e->mode == 'N' || e->mode == 'Z';
+    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E' || e->mode == 'M' || e->mode == 'N';
     if ((L % 16 && (e->mode == 'd' || (enc && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
@@ -181,7 +182,7 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     a[ot + 2] = (uint32_t)(uintptr_t)dst_offs;
     a[ot + 3] = (uint32_t)((uintptr_t)dst_offs >> 32);
     size_t sz = (size_t)(ot + 4) * 4;
-    if (e->mode == 'w' || e->mode == 'X' || e->mode == 'Y') {   // per-generation pass bound (KERNARG_BYTES_SYNW)
+    if (e->mode == 'w' || e->mode == 'X' || e->mode == 'Y' || e->mode == 'Z') {   // per-generation pass bound (KERNARG_BYTES_SYNW)
         a[24] = (uint32_t)(uintptr_t)bound;
         a[25] = (uint32_t)((uintptr_t)bound >> 32);
         sz = 26 * 4;
@@ -266,10 +267,13 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
     // an item (128 units) must lie in at most two generations
     const uint32_t Lv = bs_padded_units(L);
     if (Lv < 128 || srs < 16ull * Lv) return bs_invalid(__LINE__);
-    // the passes in one pass-major dispatch unless QF_ENCODE_MERGED=0: the
-    // additive-FFT ones ('Y') unless QF_FFT_KERNELS=0, else the plain ones ('X')
+    // the passes in one dispatch unless QF_ENCODE_MERGED=0: the additive-FFT
+    // ones item-major with the row work shared in LDS ('Z', QF_SYNW_SHARED) or
+    // pass-major ('Y') unless QF_FFT_KERNELS=0, else the plain ones ('X')
     const bool merged = cache.get(QF_OPT_ENCODE_MERGED);
-    const char mode = merged && cache.get(QF_OPT_FFT_KERNELS) && find('Y', k, r) ? 'Y'
+    const bool fft = merged && cache.get(QF_OPT_FFT_KERNELS);
+    const char mode = fft && cache.get(QF_OPT_SYNW_SHARED) && find('Z', k, r) ? 'Z'
+                      : fft && find('Y', k, r) ? 'Y'
                       : merged && find('X', k, r) ? 'X' : 'w';
     for (const auto& e : qf_bs_table) {
         if (e.mode != mode || e.k != k || e.rt != r) continue;

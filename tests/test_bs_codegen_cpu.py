@@ -616,7 +616,8 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
         assert nv <= 256
 
 
-def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0, concat=False):
+def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0, concat=False,
+               xchg=False):
     """The wave-uniform syndrome kernel (mode "synw") on the emulator for
     every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
     generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
@@ -662,7 +663,7 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
     ROWS, SYN, MAP, ZERO, OFFS, BOUND = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     # merged: every pass in one dispatch (MergedSpec), wave p of workgroup w
     # running pass p on item w
-    for spec in ([bs.merged_spec(specs, concat)] if merged else specs):
+    for spec in ([bs.merged_spec(specs, concat, xchg=xchg)] if merged else specs):
         emu = bs.Emulator(bs.generate(spec))
         emu.add_buffer(ROWS, rows)
         emu.add_buffer(SYN, syn)
@@ -688,6 +689,9 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
                              map_stride=ms, zero=ZERO, Lv=Lv, src_offs=OFFS if offs else 0,
                              bound=BOUND if use_bound else 0)
             for wg in range(n_items):
+                if xchg:    # the waves share LDS and meet at barriers
+                    emu.run_workgroup(ka, wg, spec.waves, spec.lds_bytes)
+                    continue
                 for w in range(spec.waves):
                     emu.run_wave(ka, wg, w)
             break
@@ -745,6 +749,16 @@ def test_emulated_synw_fft(oracle, k, rt, L, G, offs):
     absent sources read the zero row, accepted repairs XOR onto their
     transposed blocks): the same syndromes and skips as the plain passes."""
     assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 7 + rt + L, offs=offs, fft=8) > 0
+
+
+@pytest.mark.parametrize("k,rt,L,G,offs", [(24, 10, 2048, 3, False), (20, 20, 2100, 4, True), (48, 21, 2064, 3, False),
+                                           (196, 59, 2048, 2, False)])
+def test_emulated_synw_xchg(oracle, k, rt, L, G, offs):
+    """Item-major merged FFT synw whose waves share the source rows' gather,
+    transposes and chunk butterflies through LDS (merged_spec(xchg=True)):
+    the same syndromes and skips as the per-pass kernels; a skipped pass's
+    wave still produces its groups (the barriers stay matched)."""
+    assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 11 + rt + L, offs=offs, fft=8, merged=True, xchg=True) > 0
 
 
 def test_emulated_synw_without_bound(oracle):
