@@ -61,6 +61,26 @@ def variant_ops(bs, spec, flags):
                     and (acc_lo <= op.args[0] < acc_hi or ring_lo <= op.args[0] < ring_hi)):
                 continue
         out.append(op)
+    # sync:N / synclu: s_barrier after every N-th row wait of the body and
+    # (both) after every drained LDS wait (the LU columns' ends), so the
+    # workgroup's waves run the same code at about the same time and share
+    # its instruction fetches (timing only: the decode's waves exchange no
+    # data, so a barrier pairs any two positions safely)
+    syncn = next((int(f.split(":")[1]) for f in flags if f.startswith("sync:")), 0)
+    if syncn or "synclu" in flags:
+        body_at = next(n for n, op in enumerate(out) if op.name == "label" and op.args[0] == ".Lbody")
+        synced, nvm = [], 0
+        for n, op in enumerate(out):
+            synced.append(op)
+            if n <= body_at:
+                continue
+            if op.name == "s_waitcnt_vm" and syncn:
+                nvm += 1
+                if nvm % syncn == 0:
+                    synced.append(bs.Op("s_barrier", ()))
+            elif op.name == "s_waitcnt_lgkm_n" and op.args == (0,):
+                synced.append(bs.Op("s_barrier", ()))
+        out = synced
     for f in flags:   # sched:N -- bs_sched list scheduling, N slots producer -> consumer
         if f.startswith("sched:"):
             from quicfuscate_amd import bs_sched

@@ -37,6 +37,19 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5y: barriers keep a workgroup's four waves (four items) at the
+    # same code position, so they share instruction fetches (the merged C5
+    # encode lost ~35 % issue rate to distinct 8-byte code streams)
+    ("y_warm", dict(LIB_DEC4), ()),
+    ("y_lib", dict(LIB_DEC4), ()),
+    ("y_synclu", dict(LIB_DEC4), ("synclu",)),
+    ("y_sync8", dict(LIB_DEC4), ("sync:8",)),
+    ("y_sync2", dict(LIB_DEC4), ("sync:2",)),
+    ("y_lib_2", dict(LIB_DEC4), ()),
+    ("y_synclu_2", dict(LIB_DEC4), ("synclu",)),
+    ("y_sync8_2", dict(LIB_DEC4), ("sync:8",)),
+]
+VARIANTS_R05G = [
     # round 5g: VALU list scheduling (quicfuscate_amd/bs_sched.py): runs of
     # plain VALU ops reordered so producers sit >= N ops before consumers
     ("q_warm", dict(LIB_DEC4), ()),
