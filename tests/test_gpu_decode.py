@@ -544,3 +544,22 @@ def test_decode_general_path_more_than_four_passes(qf, oracle, gpu_ctx, path, mo
     out = run_decode(qf, k, r, L, G, k + r, gens, False)
     check(oracle, k, L, src, gens, out, False)
     assert max(out[2]) > 64
+
+
+@pytest.mark.parametrize("shared", [1, 0])
+@pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 6, None), (196, 59, 9000, 6, 3), (160, 48, 4100, 9, 40),
+                                           (128, 39, 2100, 12, None)])
+def test_decode_c5_synw_shared(qf, oracle, gpu_ctx, k, r, L, G, erase, shared, monkeypatch):
+    """Long-row C5 decode with the FFT syndrome passes item-major, their waves
+    sharing the row gather through LDS ('Z', QF_OPT_SYNW_SHARED = 1), and
+    pass-major ('Y' / plain 'X', 0): bit-exact either way, with few erasures
+    (most items then skip the upper passes but still produce their share of
+    the rows) and with many, and a partial last unit (L % 16 != 0)."""
+    _path(monkeypatch, "default_1wave")
+    qf.set_default_options(synw_shared=shared)
+    rng = np.random.default_rng(k * 31 + L + (erase or 0))
+    kw = {"erase": erase, "shuffle": False} if erase is not None else {}
+    max_rows = k + r
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, **kw)
+    out = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    check(oracle, k, L, src, gens, out, False)
