@@ -1220,6 +1220,10 @@ class MergedSpec:
     # separate launch of n 4-wave workgroups would (n = s18 / 4), so one pass's
     # last, partly filled round of workgroups overlaps the next pass's first
     concat: bool = False
+    # xchg: producer-only waves beside the pass waves (a 3-pass code's
+    # workgroup gets a 4th wave that only loads, transposes and transforms
+    # row groups, so two workgroups fill a CU's 8 wave slots)
+    helpers: int = 0
 
     chunked = False
     ksplit = 1
@@ -1256,7 +1260,7 @@ class MergedSpec:
 
     @property
     def waves(self) -> int:
-        return 4 if self.concat else len(self.passes)
+        return 4 if self.concat else len(self.passes) + self.helpers
 
     @property
     def n_passes(self) -> int:
@@ -1265,9 +1269,14 @@ class MergedSpec:
     @property
     def name(self) -> str:
         if self.mode == "synw":
-            return (f"qf_cauchy_synw{'c' if self.concat else 'm'}{'x' if self.passes[0].xchg else ''}"
+            return (f"qf_cauchy_synw{'c' if self.concat else 'm'}{self._xtag}"
                     f"{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}")
-        return f"qf_cauchy_bsm{'x' if self.passes[0].xchg else ''}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
+        return f"qf_cauchy_bsm{self._xtag}{f'f{self.fft}' if self.fft else ''}_k{self.k}_r{self.rt}"
+
+    @property
+    def _xtag(self) -> str:
+        """'x' for shared row work, 'xh' with producer-only waves."""
+        return ("x" + "h" * bool(self.helpers)) if self.passes[0].xchg else ""
 
     @property
     def next_free_vgpr(self) -> int:
@@ -1289,17 +1298,19 @@ class MergedSpec:
         return self.waves * self.passes[0].lds_rows * LDS_ROW_BYTES
 
 
-def merged_spec(passes, concat: bool = False, xchg: bool = False) -> MergedSpec:
+def merged_spec(passes, concat: bool = False, xchg: bool = False, helpers: int = 0) -> MergedSpec:
     assert not (xchg and (concat or passes[0].mode not in ("enc", "synw") or not passes[0].fft or passes[0].lds_rows))
+    assert not helpers or xchg
+    nw = len(passes) + helpers
     passes = tuple(dataclasses.replace(p, merged=not concat, head_mark=concat,
-                                       xchg=(len(passes), n) if xchg else ()) for n, p in enumerate(passes))
+                                       xchg=(nw, n) if xchg else ()) for n, p in enumerate(passes))
     assert 1 < len(passes) <= 16 and all(p.mode == passes[0].mode in ("enc", "synw") and p.ksplit == 1
                                         for p in passes)
     assert len({p.lds_rows for p in passes}) == 1 and (not passes[0].lds_rows or passes[0].fft)
     assert all(p.k == passes[0].k and p.rt == passes[0].rt for p in passes)
     assert sorted((p.j0, p.j0 + p.r) for p in passes) == [(p.j0, p.j0 + p.r) for p in passes]
     assert passes[0].j0 == 0 and passes[-1].j0 + passes[-1].r == passes[0].rt
-    return MergedSpec(passes, concat)
+    return MergedSpec(passes, concat, helpers)
 
 
 def _generate_merged(ms: MergedSpec) -> list[Op]:
@@ -1311,7 +1322,9 @@ def _generate_merged(ms: MergedSpec) -> list[Op]:
     out: list[Op] = []
     E = out.append
     bodies = []
-    for p, sp in enumerate(ms.passes):
+    streams = list(ms.passes) + [dataclasses.replace(ms.passes[0], xchg=(ms.waves, len(ms.passes) + h, True))
+                                 for h in range(ms.helpers)]
+    for p, sp in enumerate(streams):
         ops = generate(sp)
         cut = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Lhead_end")
         if p == 0:
@@ -1334,7 +1347,7 @@ def _generate_merged(ms: MergedSpec) -> list[Op]:
             E(Op("label", (f".Lnpass{p}",)))
     for p, body in enumerate(bodies):
         E(Op("label", (f".Lpass{p}",)))
-        j0 = ms.passes[p].j0
+        j0 = ms.passes[p].j0 if p < len(ms.passes) else 0
         if j0:
             E(Op("s_mul_k", (46, 11, j0)))
             E(Op("s_add", (6, 6, 46)))
@@ -1506,7 +1519,8 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
     generation of the item needs (s[SW_SKIP]) still produces its groups but
     skips its folds and stores."""
     synw = spec.mode == "synw"
-    nw, me = spec.xchg
+    nw, me = spec.xchg[:2]
+    helper = len(spec.xchg) > 2 and spec.xchg[2]   # a producer-only wave (no pass of its own)
     P = spec.fplan
     ch = P.ch
     ring0, acc0 = spec.ring0, spec.acc0
@@ -1601,7 +1615,7 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
 
     if mine(0) is not None:
         load_group(mine(0))
-    elif synw:
+    elif synw and not helper:
         for j in range(min(ch, spec.r)):
             load_repair(j)
     for rnd in range(nrounds):
@@ -1610,12 +1624,18 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
             produce(gi)
             if mine(rnd + 1) is not None:
                 load_group(mine(rnd + 1))
-            elif synw:        # the wave's last group: its chunk registers take the first repairs
+            elif synw and not helper:    # the wave's last group: its chunk registers take the first repairs
                 for j in range(min(ch, spec.r)):
                     load_repair(j)
         E(Op("s_barrier", ()))
-        consume(rnd)
+        if not helper:
+            consume(rnd)
         E(Op("s_barrier", ()))
+    if helper:
+        if synw:
+            E(Op("label", (".Lskip",)))
+        _epilogue_next_item(E, far=spec.far)
+        return ops
     if synw:
         E(Op("s_cmp_eq_k_br", (SW_SKIP, 0, ".Lfold_all")))
         E(Op("s_waitcnt_vm", (0,)))

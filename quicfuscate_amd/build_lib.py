@@ -228,9 +228,13 @@ def kernel_specs() -> list:
     # through LDS, xchg: 0.506-0.541 -> 0.323-0.325 ms at (196, 59), 0.446 ->
     # 0.320 at (160, 48), 0.438 -> 0.304 at (128, 39), bit-exact,
     # tools/c5_lab.py, profiles/r05u_c5_xchg.json)
+    # (a code of 3 passes gets a producer-only 4th wave, so two workgroups fill a
+    # CU's 8 wave slots and a round holds 4 groups: 0.322-0.333 -> 0.305 ms at
+    # (160, 48), 0.309-0.316 -> 0.299-0.302 at (128, 39), profiles/r05ae_c5_helper.json)
     for k, rt in BS_FFT_PASSES:
+        cps = lch_fft.coset_passes(k, rt)
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
-                                     for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))
+                                     for j0, rp in cps], xchg=True, helpers=max(0, 4 - len(cps))))
     # the synw passes of the C5 codes in one pass-major dispatch: one launch
     # of P x n workgroups instead of P launches of n, so a pass's last, partly
     # filled round overlaps the next pass's first; 'Y' the additive-FFT passes
@@ -242,6 +246,8 @@ def kernel_specs() -> list:
     # the FFT synw passes item-major, their waves sharing the row gather,
     # transposes and chunk butterflies through LDS ('Z', QF_SYNW_SHARED; the
     # sources are read once instead of once per pass)
+    # (a producer-only 4th wave, as the encode's, measured no faster here: (160, 48) block
+    # decode 2,007-2,019 against 2,025-2,031 GiB/s, profiles/r05af_c5_helper_decode.json)
     for k, rt in BS_FFT_SYNW_SHARED:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt,
                                                    j0=j0) for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))

@@ -617,7 +617,7 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
 
 
 def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0, concat=False,
-               xchg=False):
+               xchg=False, helpers=0):
     """The wave-uniform syndrome kernel (mode "synw") on the emulator for
     every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
     generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
@@ -663,7 +663,7 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
     ROWS, SYN, MAP, ZERO, OFFS, BOUND = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     # merged: every pass in one dispatch (MergedSpec), wave p of workgroup w
     # running pass p on item w
-    for spec in ([bs.merged_spec(specs, concat, xchg=xchg)] if merged else specs):
+    for spec in ([bs.merged_spec(specs, concat, xchg=xchg, helpers=helpers)] if merged else specs):
         emu = bs.Emulator(bs.generate(spec))
         emu.add_buffer(ROWS, rows)
         emu.add_buffer(SYN, syn)
@@ -751,14 +751,16 @@ def test_emulated_synw_fft(oracle, k, rt, L, G, offs):
     assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 7 + rt + L, offs=offs, fft=8) > 0
 
 
-@pytest.mark.parametrize("k,rt,L,G,offs", [(24, 10, 2048, 3, False), (20, 20, 2100, 4, True), (48, 21, 2064, 3, False),
-                                           (196, 59, 2048, 2, False)])
-def test_emulated_synw_xchg(oracle, k, rt, L, G, offs):
+@pytest.mark.parametrize("k,rt,L,G,offs,helpers", [(24, 10, 2048, 3, False, 0), (20, 20, 2100, 4, True, 0),
+                                                   (48, 21, 2064, 3, False, 0), (196, 59, 2048, 2, False, 0),
+                                                   (48, 21, 2064, 3, True, 1), (20, 20, 2100, 4, False, 2)])
+def test_emulated_synw_xchg(oracle, k, rt, L, G, offs, helpers):
     """Item-major merged FFT synw whose waves share the source rows' gather,
     transposes and chunk butterflies through LDS (merged_spec(xchg=True)):
     the same syndromes and skips as the per-pass kernels; a skipped pass's
     wave still produces its groups (the barriers stay matched)."""
-    assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 11 + rt + L, offs=offs, fft=8, merged=True, xchg=True) > 0
+    assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 11 + rt + L, offs=offs, fft=8, merged=True, xchg=True,
+                      helpers=helpers) > 0
 
 
 def test_emulated_synw_without_bound(oracle):
@@ -1139,9 +1141,11 @@ def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
             assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
 
 
-@pytest.mark.parametrize("k,rt,L,G,blocks", [(24, 10, 200, 3, 0), (48, 21, 2100, 2, 3), (20, 20, 72, 2, 0),
-                                            (196, 59, 40, 1, 0), (160, 48, 40, 1, 0), (128, 39, 100, 2, 1)])
-def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks):
+@pytest.mark.parametrize("k,rt,L,G,blocks,helpers", [(24, 10, 200, 3, 0, 0), (48, 21, 2100, 2, 3, 0),
+                                                    (20, 20, 72, 2, 0, 0), (196, 59, 40, 1, 0, 0),
+                                                    (160, 48, 40, 1, 0, 0), (128, 39, 100, 2, 1, 0),
+                                                    (160, 48, 40, 1, 0, 1), (20, 20, 72, 2, 1, 2)])
+def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks, helpers):
     """The merged additive-FFT encode whose waves share the row work through
     LDS (merged_spec(xchg=True), _generate_enc_xchg): wave w produces groups
     w, w + W, ... into its LDS slot, every wave folds every group; the
@@ -1158,8 +1162,8 @@ def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks):
     src = rng.integers(0, 256, G * sgs + 64, dtype=np.uint8)
     dst = np.full(G * dgs, 0xEE, np.uint8)
     passes = [bs.KernelSpec(k, rp, 3, r_total=rt, j0=j0, fft=8, ld_policy="") for j0, rp in lch_fft.coset_passes(k, rt)]
-    ms = bs.merged_spec(passes, xchg=True)
-    assert ms.waves == len(passes) > 1 and ms.lds_bytes == ms.waves * 8 * bs.LDS_ROW_BYTES
+    ms = bs.merged_spec(passes, xchg=True, helpers=helpers)
+    assert ms.waves == len(passes) + helpers and len(passes) > 1 and ms.lds_bytes == ms.waves * 8 * bs.LDS_ROW_BYTES
     emu = bs.Emulator(bs.generate(ms))
     SRC, DST = 0x10000000, 0x40000000
     emu.add_buffer(SRC, src)

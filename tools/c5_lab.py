@@ -24,6 +24,20 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5ae: a producer-only 4th wave in the 3-pass codes' workgroups
+    # (merged_spec(xchg=True, helpers=1)): two workgroups then fill a CU's 8
+    # wave slots
+    ("h160_warm", 160, 48, "N", 0, {"xchg": True}),
+    ("h160_x", 160, 48, "N", 0, {"xchg": True}),
+    ("h160_xh", 160, 48, "N", 0, {"xchg": True, "helpers": 1}),
+    ("h128_x", 128, 39, "N", 0, {"xchg": True}),
+    ("h128_xh", 128, 39, "N", 0, {"xchg": True, "helpers": 1}),
+    ("h160_x_2", 160, 48, "N", 0, {"xchg": True}),
+    ("h160_xh_2", 160, 48, "N", 0, {"xchg": True, "helpers": 1}),
+    ("h128_x_2", 128, 39, "N", 0, {"xchg": True}),
+    ("h128_xh_2", 128, 39, "N", 0, {"xchg": True, "helpers": 1}),
+]
+VARIANTS_R05U = [
     # round 5u: the waves of a merged FFT encode share loads, transposes and
     # chunk butterflies through LDS (merged_spec(xchg=True))
     ("x196_warm", 196, 59, "N", 0, {}),
@@ -93,12 +107,12 @@ def make_spec(bs, k, rt, kind, npass, kw):
     from quicfuscate_amd import lch_fft
 
     pd = kw.get("pd", 3)
-    extra = {x: v for x, v in kw.items() if x not in ("pd", "flags", "xchg")}
+    extra = {x: v for x, v in kw.items() if x not in ("pd", "flags", "xchg", "helpers")}
     if kind == "N":
         R = extra.get("fft_coset", 16)
         passes = [bs.KernelSpec(k, rp, pd, "enc", fft=8, ld_policy="", r_total=rt, j0=j0, **extra)
                   for j0, rp in lch_fft.coset_passes(k, rt, R)]
-        return bs.merged_spec(passes, xchg=bool(kw.get("xchg")))
+        return bs.merged_spec(passes, xchg=bool(kw.get("xchg")), helpers=kw.get("helpers", 0))
     else:
         cuts = [rt * p // npass for p in range(npass + 1)]
         passes = [bs.KernelSpec(k, cuts[p + 1] - cuts[p], pd, "enc", r_total=rt, j0=cuts[p], **extra)
