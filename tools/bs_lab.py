@@ -90,6 +90,18 @@ def variant_ops(bs, spec, flags):
 
 ALL = 1 << 20  # blocks per CU beyond residency: one item per wave
 VARIANTS = [
+    # round 5ai: prefetch depth of the FFT encode (pd 3 = 240 VGPRs, 2 = 232,
+    # 1 = 224: at <= 224 two encode waves leave a 64-VGPR wave slot on the SIMD
+    # for the decode's acceptance pass running beside it)
+    ("v_warm", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("v_pd3", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("v_pd2", 64, 16, 2, ("st:nt", "ztail", "fft:8"), ALL),
+    ("v_pd1", 64, 16, 1, ("st:nt", "ztail", "fft:8"), ALL),
+    ("v_pd3_2", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
+    ("v_pd2_2", 64, 16, 2, ("st:nt", "ztail", "fft:8"), ALL),
+    ("v_pd1_2", 64, 16, 1, ("st:nt", "ztail", "fft:8"), ALL),
+]
+VARIANTS_R05G = [
     # round 5g: VALU list scheduling (bs_sched, "sched:N") of the FFT encode
     ("u_warm", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
     ("u_lib", 64, 16, 3, ("st:nt", "ztail", "fft:8"), ALL),
