@@ -1321,3 +1321,37 @@ def test_dec_lab_variants_stay_in_bounds():
         for wg in range(waves):
             for w in range(4):
                 emu.run_wave(ka, wg, w)
+
+
+def test_xchg_streams_meet_at_every_barrier():
+    """Every library kernel whose waves share row work through LDS (xchg,
+    helper waves included): each wave's stream, from its pass label to the
+    item loop's back-edge, holds the same number of s_barrier ops with no
+    branch that could skip one (a skipped barrier would leave the other waves
+    of the workgroup waiting on the GPU)."""
+    from quicfuscate_amd import build_lib
+
+    specs = [s for s in build_lib.kernel_specs() if isinstance(s, bs.MergedSpec) and s.passes[0].xchg]
+    assert len(specs) >= 6
+    for ms in specs:
+        ops = bs.generate(ms)
+        labels = {op.args[0]: n for n, op in enumerate(ops) if op.name == "label"}
+        counts = []
+        for p in range(ms.waves):
+            start = labels[f".Lpass{p}"]
+            end = labels.get(f".Lpass{p + 1}", len(ops))
+            body = ops[start:end]
+            counts.append(sum(op.name == "s_barrier" for op in body))
+            # barriers sit outside every conditional region: the only forward
+            # branches between the first and last barrier are the fold skips
+            # (synw), whose targets lie before the next barrier
+            bars = [n for n, op in enumerate(body) if op.name == "s_barrier"]
+            blabels = {op.args[0]: n for n, op in enumerate(body) if op.name == "label"}
+            for n in range(bars[0], bars[-1]):
+                op = body[n]
+                tgt = next((a for a in op.args if isinstance(a, str) and a.startswith(".L")), None)
+                if tgt is None or op.name == "label":
+                    continue
+                t = blabels[tgt]
+                assert t > n and not any(n < b < t for b in bars), (ms.name, p, op.name, tgt)
+        assert len(set(counts)) == 1 and counts[0] > 0, (ms.name, counts)
