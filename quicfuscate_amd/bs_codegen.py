@@ -1301,6 +1301,9 @@ class MergedSpec:
 def merged_spec(passes, concat: bool = False, xchg: bool = False, helpers: int = 0) -> MergedSpec:
     assert not (xchg and (concat or passes[0].mode not in ("enc", "synw") or not passes[0].fft or passes[0].lds_rows))
     assert not helpers or xchg
+    if xchg:   # the waves share the groups: every pass streams the same rows through the same chunk transforms
+        g0 = [(rows, bf) for rows, bf, _ in xchg_groups(passes[0].fplan)]
+        assert all([(rows, bf) for rows, bf, _ in xchg_groups(p.fplan)] == g0 for p in passes[1:])
     nw = len(passes) + helpers
     passes = tuple(dataclasses.replace(p, merged=not concat, head_mark=concat,
                                        xchg=(nw, n) if xchg else ()) for n, p in enumerate(passes))
@@ -1517,7 +1520,8 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
     are XORed onto its syndromes in byte form at the end (their loads issued
     once the wave's last group is in LDS), and a wave whose pass no
     generation of the item needs (s[SW_SKIP]) still produces its groups but
-    skips its folds and stores."""
+    skips its folds and stores.  A producer-only wave (spec.xchg[2],
+    MergedSpec.helpers) produces its share of the groups and folds nothing."""
     synw = spec.mode == "synw"
     nw, me = spec.xchg[:2]
     helper = len(spec.xchg) > 2 and spec.xchg[2]   # a producer-only wave (no pass of its own)
