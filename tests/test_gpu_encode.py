@@ -345,3 +345,38 @@ def test_encode_small_batch_kernel(qf, oracle, gpu_ctx, k, r, L, G, monkeypatch)
         for j in range(r):
             assert (rep[g * rgs + j * rrs: g * rgs + j * rrs + L] == want[j]).all(), (g, j)
             assert (rep[g * rgs + j * rrs + L: g * rgs + (j + 1) * rrs] == 0xA5).all(), (g, j)  # nothing past L
+
+
+@pytest.mark.parametrize("k,r,L", [(196, 59, 2001), (160, 48, 2047), (128, 39, 4099)])
+def test_c5_shared_row_encode_odd_lengths(qf, oracle, gpu_ctx, k, r, L):
+    """The merged passes whose waves share their row work through LDS
+    (kernels qf_cauchy_bsmx*, a producer-only wave at 3 passes) at odd row
+    lengths and more items than CUs: repairs bit-exact against the oracle on
+    a sample of generations, the zero tail written, nothing beyond it."""
+    import torch
+
+    rs = _r16(L)
+    tail = (L + 127) // 128 * 128
+    rrs = tail + 64
+    items_per_gen = tail // 16 // 128 or 1
+    G = 300 // items_per_gen + 8
+    gs, rgs = k * rs, r * rrs
+    gen = torch.Generator(device="cuda").manual_seed(k * L)
+    src = torch.randint(0, 256, (G * gs,), dtype=torch.uint8, device="cuda", generator=gen)
+    rep = torch.full((G * rgs,), 0xA5, dtype=torch.uint8, device="cuda")
+    gpu_ctx.profile(True)
+    qf.encode_batch(src, rep, k, r, L, src_row_stride=rs, src_gen_stride=gs, rep_row_stride=rrs,
+                    rep_gen_stride=rgs, G=G, zero_tail=True, ctx=gpu_ctx)
+    gpu_ctx.sync()
+    names = set(gpu_ctx.kernel_times())
+    gpu_ctx.profile(False)
+    assert any(n.startswith("qf_cauchy_bsmx") for n in names), names
+    s, out = src.cpu().numpy(), rep.cpu().numpy()
+    for g in (0, 1, G // 2, G - 1):
+        rows = s[g * gs: (g + 1) * gs].reshape(k, rs)[:, :L]
+        want = oracle.encode(rows, r)
+        for j in range(r):
+            off = g * rgs + j * rrs
+            assert (out[off: off + L] == want[j]).all(), (g, j)
+            assert (out[off + L: off + tail] == 0).all(), (g, j)
+            assert (out[off + tail: off + rrs] == 0xA5).all(), (g, j)
