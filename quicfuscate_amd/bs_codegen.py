@@ -1170,7 +1170,9 @@ def valu_per_item(spec: KernelSpec) -> int:
     counter pass of that workload exists (C5 sliding windows).  A merged
     dispatch: the sum over its passes (one wave each per item)."""
     if isinstance(spec, MergedSpec):
-        return sum(valu_per_item(p) for p in spec.passes)
+        helpers = [dataclasses.replace(spec.passes[0], xchg=(spec.waves, len(spec.passes) + h, True))
+                   for h in range(spec.helpers)]
+        return sum(valu_per_item(p) for p in list(spec.passes) + helpers)
     ops = generate(spec)
     start = next(n for n, op in enumerate(ops) if op.name == "label" and op.args[0] == ".Litem")
     n = 0
