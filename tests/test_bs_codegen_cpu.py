@@ -1302,7 +1302,7 @@ def test_dec_lab_variants_stay_in_bounds():
     rows = np.random.default_rng(1).integers(0, 256, G * n_slots * L, dtype=np.uint8)
     ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     Q = ((L + 15) // 16 + 1) // 2
-    for name, kw, flags in (dec_lab.VARIANTS + dec_lab.VARIANTS_R05G + dec_lab.VARIANTS_R05F + dec_lab.VARIANTS_R05E + dec_lab.VARIANTS_R05D + dec_lab.VARIANTS_R05C + dec_lab.VARIANTS_R05B
+    for name, kw, flags in (dec_lab.VARIANTS + dec_lab.VARIANTS_R05Y + dec_lab.VARIANTS_R05G + dec_lab.VARIANTS_R05F + dec_lab.VARIANTS_R05E + dec_lab.VARIANTS_R05D + dec_lab.VARIANTS_R05C + dec_lab.VARIANTS_R05B
                              + dec_lab.VARIANTS_R05A):
         if name.endswith("_2") or name.endswith("_warm") or kw.get("rs"):
             continue

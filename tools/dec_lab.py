@@ -37,6 +37,17 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5al: the item -> workgroup remap that keeps neighbouring items on
+    # one XCD (xcd_remap, the library's) against dispatch order
+    ("x_warm", dict(LIB_DEC4), ()),
+    ("x_lib", dict(LIB_DEC4), ()),
+    ("x_noremap", {**LIB_DEC4, "xcd_remap": False}, ()),
+    ("x_lib_2", dict(LIB_DEC4), ()),
+    ("x_noremap_2", {**LIB_DEC4, "xcd_remap": False}, ()),
+    ("x_lib_3", dict(LIB_DEC4), ()),
+    ("x_noremap_3", {**LIB_DEC4, "xcd_remap": False}, ()),
+]
+VARIANTS_R05Y = [
     # round 5y: barriers keep a workgroup's four waves (four items) at the
     # same code position, so they share instruction fetches (the merged C5
     # encode lost ~35 % issue rate to distinct 8-byte code streams)
