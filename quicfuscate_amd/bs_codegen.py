@@ -806,6 +806,7 @@ def _source_row(ops: list[Op], C, i: int, r: int, base: int, acc0: int, init: bo
 FFT_RING0_ENC = 18     # the ring starts where the plane combinations lived
 FFT_RING0_DEC = 48     # chunked dec keeps its low registers (V_ZA .. v47)
 FFT_MAP_DEC = 18       # chunked dec: slot map quads v18..v37 (dead in the LU phase)
+FFT_MAP_DEC_QUADS = 5  # ... k + r <= 80 slots; larger maps run a window of 5 quads there
 LDS_ROW_BYTES = 2048   # lds_rows: one row of a wave (64 lanes x 2 units x 16 B) per LDS slot
 S_ROWLDS = 80          # lds_rows: the wave's first LDS row slot (byte address)
 S_ROWLDS_ENC = 76      # the same in the encode kernels
@@ -2356,18 +2357,39 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
     E = ops.append
     _prologue_chunked(E, spec)
     # the generation's slot map (payload lanes; padding-free: every lane with a chunk)
-    E(Op("v_movs", (V_ADDR, 20)))
-    E(Op("v_movs", (V_ADDR + 1, 21)))
-    E(Op("v_mad64_s", (V_ADDR, V_GA, 19, V_ADDR)))
-    E(Op("s_exec", (S_STA,)))
-    for q in range(spec.map_quads):
-        E(Op("load16", (mp + 4 * q, V_ADDR, 16 * q)))
-    E(Op("s_exec", (None,)))
-    E(Op("s_waitcnt_vm", (0,)))
+    # (additive FFT with more than FFT_MAP_DEC_QUADS map quads, k + r > 80: a
+    # window of FFT_MAP_DEC_QUADS quads in v18..; the quads past it sit in the
+    # free ring for the jmax scan, and once the row loop reaches them they are
+    # reloaded over the window's first quads, whose rows have all been issued)
+    W = FFT_MAP_DEC_QUADS if spec.fft and spec.map_quads > FFT_MAP_DEC_QUADS else spec.map_quads
+    win = {"phase": 0}
+
+    def map_load(quads, reg):
+        E(Op("v_movs", (V_ADDR, 20)))
+        E(Op("v_movs", (V_ADDR + 1, 21)))
+        E(Op("v_mad64_s", (V_ADDR, V_GA, 19, V_ADDR)))
+        E(Op("s_exec", (S_STA,)))
+        for q in quads:
+            E(Op("load16", (reg(q), V_ADDR, 16 * q)))
+        E(Op("s_exec", (None,)))
+        E(Op("s_waitcnt_vm", (0,)))
+    map_load(range(spec.map_quads), lambda q: mp + 4 * q if q < W else ring0 + 4 * (q - W))
     seq = [("src", i) for i in range(k)] + [("rep", j) for j in range(r)]
 
+    def map_reg(pos: int) -> int:
+        q = pos // 16
+        if q < W:
+            assert win["phase"] < 2, "map quad reloaded over"
+            return mp + pos // 4
+        if win["phase"] == 0:
+            return ring0 + 4 * (q - W) + (pos % 16) // 4
+        if win["phase"] == 1:    # the row loop reaches the quads past the window
+            map_load(range(W, spec.map_quads), lambda qq: mp + 4 * (qq - W))
+            win["phase"] = 2
+        return mp + 4 * (q - W) + (pos % 16) // 4
+
     def present(pos: int, sm: int):
-        E(Op("v_bfe", (V_SLOT, mp + pos // 4, 8 * (pos % 4), 8)))
+        E(Op("v_bfe", (V_SLOT, map_reg(pos), 8 * (pos % 4), 8)))
         E(Op("v_cmp_ne_s", (sm, S_ABSENT, V_SLOT)))
         E(Op("s_nop", (4,)))
 
@@ -2379,6 +2401,7 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         E(Op("s_cmp_lg64_br", (S_TMP, ".Ljdone")))
     E(Op("s_movk", (S_JMAX, 0)))
     E(Op("label", (".Ljdone",)))
+    win["phase"] = 1
     if spec.wave_gen:   # any source row may be skipped, so no row initialises
         for a in range(acc0, acc0 + 8 * r):
             E(Op("v_movk", (a, 0)))

@@ -50,6 +50,7 @@ BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
 # (196, 59) 1,383 -> 1,262: three FFT passes run against two plain ones)
 BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_SYNW_SHARED = [(128, 39), (160, 48), (196, 59)]
+BS_FFT_DEC_HYBRID = [(96, 15), (48, 8)]   # fused FFT decode ('C') of C5 shapes with k not a power of two
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
@@ -206,9 +207,12 @@ def kernel_specs() -> list:
     # selectors: 1.409 -> 1.358-1.364 ms, profiles/r04d_lab_dec_ilp_s64.json)
     # (round 5: non-temporal recovered-row stores, loads still at the default
     # policy: 1.357-1.387 -> 1.345-1.352 ms, profiles/r05_lab_dec.json r05k)
+    # (round 5: also the C5 shapes whose k is not a power of two, through the
+    # hybrid plan: (96, 15) 30.4 k -> 22.4 k VALU per item, its 7-quad slot map
+    # run as a window; (48, 8) 10.6 k -> 9.4 k)
     specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="nt",
                             early_stores=True, lu_ilp=True, bfi_transpose="s64")
-              for (k, r) in BS_FFT]
+              for (k, r) in BS_FFT + BS_FFT_DEC_HYBRID]
     # every pass of a C5 code in one dispatch ('M' plain, 'N' additive-FFT
     # passes; QF_ENCODE_MERGED): one wave per pass on the workgroup's item, so
     # the source rows come from HBM once.  Plain passes: 4 waves where 3 would

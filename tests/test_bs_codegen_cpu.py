@@ -1064,6 +1064,10 @@ def test_emulated_fft_encode(oracle, k, r, pd, L, G, zero_tail, defer):
     (64, 10, 320, 4, 5, None, False, False, 0),  # r < R
     (16, 16, 96, 4, 6, 16, False, True, 0),
     (32, 16, 64, 5, 7, 0, False, True, 0),      # nothing erased
+    # hybrid plans (k not a power of two: sources past 2^a in extra chunks / direct rows)
+    (96, 15, 1200, 2, 9, 12, False, True, 0),
+    (96, 15, 9000, 1, 10, None, True, True, 0),  # C5 row length, partial last unit
+    (48, 8, 1200, 3, 11, None, False, True, 0),
 ])
 def test_emulated_fft_fused_decode(oracle, k, r, L, G, seed, erase, offs, es, lds):
     """The additive-FFT fused decode (syndromes through the chunked
