@@ -213,6 +213,9 @@ def kernel_specs() -> list:
     specs += [bs.KernelSpec(k, r, BS_FFT_DEC_PD, "dec", chunked=True, fft=BS_FFT_CH, ld_policy="", st_policy="nt",
                             early_stores=True, lu_ilp=True, bfi_transpose="s64")
               for (k, r) in BS_FFT + BS_FFT_DEC_HYBRID]
+    # ((32, 5) with chunks of 4 rows, 160 VGPRs and 5.1 k VALU per item against
+    # the plain kernel's 152 and 5.5 k, measured 2-4 % slower: block decode
+    # 4,227-4,242 against 4,305-4,402 GiB/s, profiles/r05ap_c5_fft_decode_ch4.json)
     # every pass of a C5 code in one dispatch ('M' plain, 'N' additive-FFT
     # passes; QF_ENCODE_MERGED): one wave per pass on the workgroup's item, so
     # the source rows come from HBM once.  Plain passes: 4 waves where 3 would

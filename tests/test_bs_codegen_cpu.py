@@ -1237,6 +1237,15 @@ def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks, lds):
             assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
 
 
+@pytest.mark.parametrize("k,r,L,G,seed,erase", [(32, 5, 1200, 3, 12, None), (32, 5, 9000, 1, 13, 5), (16, 4, 96, 4, 14, 3)])
+def test_emulated_fft_fused_decode_chunk4(oracle, k, r, L, G, seed, erase):
+    """The additive-FFT fused decode with chunks of 4 rows (fft=4: a ring of 6
+    rows, 160 VGPRs at (32, 5), so three waves per SIMD; the LU's r column
+    quads must fit that ring, r <= 8)."""
+    assert _dec_case(oracle, k, r, 2, L, G, seed, erase, chunked=True, fft=4, early_stores=True, lu_ilp=True,
+                     bfi_transpose="s64") == 0
+
+
 @pytest.mark.parametrize("k,r,L,G,seed,erase", [(64, 16, 1200, 3, 11, 13), (64, 16, 80, 5, 12, 16),
                                                 (64, 10, 320, 4, 13, None), (32, 16, 64, 5, 14, 0)])
 def test_emulated_fft_fused_decode_lu_ahead(oracle, k, r, L, G, seed, erase):
