@@ -8,6 +8,10 @@
 #   TAG=r05a tools/gpu.sh bench [bench args...]    one bench line (+ detail record)
 #   TAG=r05a tools/gpu.sh prof                     bench line, kernel trace, SQ counters, FETCH / WRITE passes
 #   TAG=r05a tools/gpu.sh run <command...>         any command, under a 600 s limit
+#   TAG=r05a C5_SHAPES="196,59;160,48" AB_ENV=QF_SYNW_SHARED=0 [C5_TESTK="..."] tools/gpu.sh c5ab
+#        C5 GPU tests, then block GiB/s of the shapes: library (a) against AB_ENV (b), alternating twice
+#   TAG=r05a VARIANTS="lib g128:QF_PREPARE_GRID=128" tools/gpu.sh benchab
+#        the headline step under environment variants, alternating twice (value, encode in-step, kernel ms)
 #
 # Outputs: gpurun_out/$TAG/ (merged back by gpurun; copy what is judged into profiles/).
 set -euo pipefail
@@ -88,6 +92,34 @@ case "$what" in
     python3 tools/c5_pmc_summary.py "$OUT/c5sq" "$OUT/c5fetch" "$OUT/c5write" --out "$OUT/c5_pmc.json"
     python3 tools/prof_summary.py "$OUT/c5kt" "$OUT/c5_kernel_stats.json" --command "rocprofv3 --kernel-trace --stats -- $BC"
     echo C5PMC_OK
+    ;;
+  c5ab)
+    SH="${C5_SHAPES:-196,59;160,48;128,39}"
+    TK="${C5_TESTK:-c5 or passes or merged or 196 or synw or large or 96 or 48}"
+    timeout -k 10 600 $PYT tests/test_gpu_c5_mixed.py tests/test_gpu_encode.py tests/test_gpu_decode.py -k "$TK" \
+      > "$OUT/tests.log" 2>&1 || { tail -30 "$OUT/tests.log"; exit 1; }
+    tail -2 "$OUT/tests.log"
+    for i in 1 2; do
+      timeout -k 10 200 python3 tools/bench_c5.py --shapes "$SH" --modes block --reps 5 --out "$OUT/c5_a$i.json" \
+        > "$OUT/c5_a$i.log" 2>&1
+      env ${AB_ENV:-QF_SYNW_SHARED=0} timeout -k 10 200 python3 tools/bench_c5.py --shapes "$SH" --modes block \
+        --reps 5 --out "$OUT/c5_b$i.json" > "$OUT/c5_b$i.log" 2>&1
+    done
+    for f in a1 b1 a2 b2; do echo "== $f"; grep "^k" "$OUT/c5_$f.log"; done
+    ;;
+  benchab)
+    AB_ARGS="$ARGS --c5-shape-bytes 0"
+    for i in 1 2; do
+      for v in ${VARIANTS:-lib}; do
+        name=${v%%:*}; envs=${v#*:}; [ "$envs" = "$v" ] && envs=""
+        env $envs timeout -k 10 300 python3 bench.py --detail "" $AB_ARGS > "$OUT/${name}_$i.log" 2>&1
+        python3 - "$OUT/${name}_$i.log" "$name" <<'PY'
+import json, sys
+d = json.loads(next(l for l in open(sys.argv[1]) if l.startswith('{"metric"')))
+print(sys.argv[2], d["value"], d["ms_per_step"], d["roofline_encode"]["in_step"], d["kernel_ms_per_launch"], flush=True)
+PY
+      done
+    done
     ;;
   run)
     timeout -k 10 600 "$@"
