@@ -395,6 +395,10 @@ class KernelSpec:
     # lab only (fft row loop): the first n chunks' transposes, butterflies and
     # folds dropped (their rows still load): the marginal time of row-loop VALU
     lab_skip_chunks: int = 0
+    # lab only (chunked dec): the split tables at a 32-B record stride (8 KB,
+    # records start on 8 different LDS banks) instead of 256 B (64 KB, every
+    # record on the same bank)
+    lab_tab32: bool = False
     # VALU list scheduling (bs_sched.schedule): runs of plain VALU ops between
     # non-VALU ops reordered so a producer sits >= sched ops before its
     # consumers where the run allows it (0: program order)
@@ -483,7 +487,7 @@ class KernelSpec:
 
     @property
     def tab_stride(self) -> int:
-        return 32 if self.lds_rows else LDS_TAB_STRIDE
+        return 32 if self.lds_rows or self.lab_tab32 else LDS_TAB_STRIDE
 
     @property
     def fplan(self):
@@ -642,6 +646,8 @@ class KernelSpec:
             return (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
         if self.mode == "dec" and self.lds_rows:
             return 256 * self.tab_stride + 4 * self.lds_rows * LDS_ROW_BYTES
+        if self.mode == "dec" and self.lab_tab32 and self.ksplit == 1:
+            return 256 * self.tab_stride
         if self.mode == "enc" and self.lds_rows:
             return 4 * self.lds_rows * LDS_ROW_BYTES
         if self.xchg:

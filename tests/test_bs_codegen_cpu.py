@@ -1237,6 +1237,13 @@ def test_emulated_merged_passes(oracle, k, rt, L, G, fft, blocks, lds):
             assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
 
 
+def test_emulated_fft_fused_decode_tab32(oracle):
+    """Lab option lab_tab32: the split tables at a 32-B record stride in LDS
+    (the table copy and the LU's address scaling follow spec.tab_stride)."""
+    assert _dec_case(oracle, 64, 16, 2, 1200, 2, 21, 13, chunked=True, fft=8, early_stores=True, lu_ilp=True,
+                     bfi_transpose="s64", lab_tab32=True) == 0
+
+
 @pytest.mark.parametrize("k,r,L,G,seed,erase", [(32, 5, 1200, 3, 12, None), (32, 5, 9000, 1, 13, 5), (16, 4, 96, 4, 14, 3)])
 def test_emulated_fft_fused_decode_chunk4(oracle, k, r, L, G, seed, erase):
     """The additive-FFT fused decode with chunks of 4 rows (fft=4: a ring of 6
@@ -1315,7 +1322,7 @@ def test_dec_lab_variants_stay_in_bounds():
     rows = np.random.default_rng(1).integers(0, 256, G * n_slots * L, dtype=np.uint8)
     ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     Q = ((L + 15) // 16 + 1) // 2
-    for name, kw, flags in (dec_lab.VARIANTS + dec_lab.VARIANTS_R05Y + dec_lab.VARIANTS_R05G + dec_lab.VARIANTS_R05F + dec_lab.VARIANTS_R05E + dec_lab.VARIANTS_R05D + dec_lab.VARIANTS_R05C + dec_lab.VARIANTS_R05B
+    for name, kw, flags in (dec_lab.VARIANTS + dec_lab.VARIANTS_R05AL + dec_lab.VARIANTS_R05Y + dec_lab.VARIANTS_R05G + dec_lab.VARIANTS_R05F + dec_lab.VARIANTS_R05E + dec_lab.VARIANTS_R05D + dec_lab.VARIANTS_R05C + dec_lab.VARIANTS_R05B
                              + dec_lab.VARIANTS_R05A):
         if name.endswith("_2") or name.endswith("_warm") or kw.get("rs"):
             continue

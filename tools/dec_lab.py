@@ -37,6 +37,16 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
 VARIANTS = [
+    # round 5as: split tables at a 32-B record stride (LDS banks) against 256 B
+    ("t_warm", dict(LIB_DEC4), ()),
+    ("t_lib", dict(LIB_DEC4), ()),
+    ("t_tab32", {**LIB_DEC4, "lab_tab32": True}, ()),
+    ("t_lib_2", dict(LIB_DEC4), ()),
+    ("t_tab32_2", {**LIB_DEC4, "lab_tab32": True}, ()),
+    ("t_lib_3", dict(LIB_DEC4), ()),
+    ("t_tab32_3", {**LIB_DEC4, "lab_tab32": True}, ()),
+]
+VARIANTS_R05AL = [
     # round 5al: the item -> workgroup remap that keeps neighbouring items on
     # one XCD (xcd_remap, the library's) against dispatch order
     ("x_warm", dict(LIB_DEC4), ()),
