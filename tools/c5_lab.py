@@ -24,6 +24,18 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5at: what the shared-row (196, 59) encode waits on: no row loads
+    # (compute, LDS exchange and barriers only) / no VALU data work (loads,
+    # LDS exchange, barriers, stores)
+    ("z196_warm", 196, 59, "N", 0, {"xchg": True}),
+    ("z196_x", 196, 59, "N", 0, {"xchg": True}),
+    ("z196_noload", 196, 59, "N", 0, {"xchg": True, "flags": ("noload",)}),
+    ("z196_novalu", 196, 59, "N", 0, {"xchg": True, "flags": ("novalu",)}),
+    ("z196_x_2", 196, 59, "N", 0, {"xchg": True}),
+    ("z196_noload_2", 196, 59, "N", 0, {"xchg": True, "flags": ("noload",)}),
+    ("z196_novalu_2", 196, 59, "N", 0, {"xchg": True, "flags": ("novalu",)}),
+]
+VARIANTS_R05AE = [
     # round 5ae: a producer-only 4th wave in the 3-pass codes' workgroups
     # (merged_spec(xchg=True, helpers=1)): two workgroups then fill a CU's 8
     # wave slots
