@@ -479,6 +479,11 @@ class KernelSpec:
     # over in LDS; each wave folds every chunk into its own pass's
     # accumulators (_generate_enc_xchg)
     xchg: tuple = ()
+    # xchg: rows of a wave's next group whose loads are issued before it
+    # transforms its current group (the rest after, as its registers free up):
+    # the row slots grow from ch + 2 to ch + early, so a load has a produce and
+    # a fold phase to land in instead of a fold phase
+    xchg_early: int = 0
 
     @property
     def ahead(self) -> int:
@@ -544,7 +549,9 @@ class KernelSpec:
         if self.fft and self.lds_rows:
             return self.fft          # only the chunk itself lives in registers
         if self.xchg:
-            return self.fft + 2      # the chunk being produced + two rows read back from LDS
+            # the chunk being produced + two rows read back from LDS (+ the
+            # next group's early rows beyond those two)
+            return self.fft + max(2, self.xchg_early)
         return self.pd + (self.fft + self.fft_defer if self.fft else 1)
 
     @property
@@ -1537,7 +1544,8 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
     P = spec.fplan
     ch = P.ch
     ring0, acc0 = spec.ring0, spec.acc0
-    rowbuf = (ring0 + 8 * ch, ring0 + 8 * ch + 8)
+    nslot = spec.nbuf                    # 8-VGPR row slots from ring0 (rotating roles)
+    early = spec.xchg_early
     v_ldsa = spec.next_free_vgpr - 1
     tmp = tuple(range(V_T, V_T + 4)) if spec.fft_cse else ()
     groups = xchg_groups(P)
@@ -1554,10 +1562,17 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
     cur = [0]            # source row the row pointers address (row 0 after the item setup)
     quad = [None]        # synw: the slot-map quad in s[SW_Q0..] / s[SW_Q1..]
 
-    def load_group(gi: int):
-        for m, n in enumerate(groups[gi][0]):
+    def slot(x: int) -> int:
+        return ring0 + 8 * x
+
+    def load_group(gi: int, ms=None, slots=None):
+        rows = groups[gi][0]
+        ms = range(len(rows)) if ms is None else ms
+        for m in ms:
+            n = rows[m]
+            base = slot(slots[m]) if slots is not None else ring0 + 8 * m
             if synw:
-                _synw_load_row(E, spec, quad, "src", P.order[n], ring0 + 8 * m)
+                _synw_load_row(E, spec, quad, "src", P.order[n], base)
                 continue
             i = P.order[n]
             if i != cur[0]:
@@ -1566,32 +1581,54 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
                 E(Op("v_add64_s", (V_SRCA, V_SRCA, 46)))
                 E(Op("v_add64_s", (V_SRCB, V_SRCB, 46)))
                 cur[0] = i
-            base = ring0 + 8 * m
             for h, (vm, va) in enumerate(((26, V_SRCA), (24, V_SRCB))):
                 E(Op("s_exec", (vm,)))
                 E(Op("load16", (base + 4 * h, va, 0, spec.ld_policy)))
             E(Op("s_exec", (None,)))
 
-    def produce(gi: int):
+    per_row = (0 if spec.lab_norows else 4) if synw else 2    # loads per row
+
+    def produce(gi: int, rs: list, nxt):
+        """Transform group gi, whose row m sits in slot rs[m], and write it to
+        LDS; nxt = (group, slots) of the wave's next group: its first `early`
+        rows load before the transform (into slots rs does not hold), the rest
+        after it.  Returns the next group's slots by row."""
         rows, bfly, _ = groups[gi]
-        E(Op("s_waitcnt_vm", (0,)))
+        ne = min(early, len(groups[nxt][0])) if nxt is not None else 0
+        nslots = None
+        if nxt is not None:
+            nslots = [None] * len(groups[nxt][0])
+            free = [x for x in range(nslot) if x not in rs]
+            for m in range(ne):
+                nslots[m] = free[m]
+            load_group(nxt, range(ne), nslots)
+        E(Op("s_waitcnt_vm", (per_row * ne,)))
         for m in range(len(rows)):
-            ops.extend(_transpose_ops(ring0 + 8 * m, spec.bfi_transpose, spec.vmask))
+            ops.extend(_transpose_ops(slot(rs[m]), spec.bfi_transpose, spec.vmask))
         for i, j, c in bfly:           # y_j ^= y_i; y_i ^= c y_j (lch_fft.Plan.chunk_bfly)
-            yi, yj = ring0 + 8 * i, ring0 + 8 * j
+            yi, yj = slot(rs[i]), slot(rs[j])
             for b in range(8):
                 E(Op("v_xor", (yj + b, yj + b, yi + b)))
             if c:
                 _macc(E, yi, yj, c, init=False, tmp=tmp)
         for m in range(len(rows)):
             off = me * slot_bytes + m * LDS_ROW_BYTES
-            E(Op("ds_write_b128", (v_ldsa, ring0 + 8 * m, off)))
-            E(Op("ds_write_b128", (v_ldsa, ring0 + 8 * m + 4, off + 1024)))
-        E(Op("s_waitcnt_lgkm_n", (0,)))      # planes in LDS; the chunk registers are free
+            E(Op("ds_write_b128", (v_ldsa, slot(rs[m]), off)))
+            E(Op("ds_write_b128", (v_ldsa, slot(rs[m]) + 4, off + 1024)))
+        E(Op("s_waitcnt_lgkm_n", (0,)))      # planes in LDS; their slots are free
+        if nxt is not None and ne < len(nslots):
+            free = [x for x in range(nslot) if x not in nslots[:ne]]
+            for m in range(ne, len(nslots)):
+                nslots[m] = free[m - ne]
+            load_group(nxt, range(ne, len(nslots)), nslots)
+        return nslots
 
     inited: set = set()
 
-    def consume(rnd: int):
+    def consume(rnd: int, busy: list):
+        # the two read-back buffers: slots no pending load targets
+        bufs = [x for x in reversed(range(nslot)) if x not in busy][:2]
+        rowbuf = (slot(bufs[0]), slot(bufs[1]))
         seq = [(q, m) for q in range(nw) if rnd * nw + q < G for m in range(len(groups[rnd * nw + q][0]))]
         if synw:
             E(Op("s_cmp_lg_k_br", (SW_SKIP, 0, f".Lnofold{rnd}")))
@@ -1615,7 +1652,6 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
         if synw:
             E(Op("label", (f".Lnofold{rnd}",)))
 
-    per_row = 0 if spec.lab_norows else 4
     issued: list = []     # synw: repair rows in load order (per_row loads each)
 
     def load_repair(j: int):
@@ -1626,23 +1662,26 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
         gi = rnd * nw + me
         return gi if gi < G else None
 
+    rs = None           # slots of the wave's current group, by row
     if mine(0) is not None:
-        load_group(mine(0))
+        rs = list(range(len(groups[mine(0)][0])))
+        load_group(mine(0), None, rs)
     elif synw and not helper:
         for j in range(min(ch, spec.r)):
             load_repair(j)
+    busy = list(rs or []) + (list(range(min(ch, spec.r))) if issued else [])
     for rnd in range(nrounds):
         gi = mine(rnd)
         if gi is not None:
-            produce(gi)
-            if mine(rnd + 1) is not None:
-                load_group(mine(rnd + 1))
-            elif synw and not helper:    # the wave's last group: its chunk registers take the first repairs
+            rs = produce(gi, rs, mine(rnd + 1))
+            busy = list(rs or [])
+            if rs is None and synw and not helper:    # the wave's last group: slots 0.. take the first repairs
                 for j in range(min(ch, spec.r)):
                     load_repair(j)
+                busy = list(range(min(ch, spec.r)))
         E(Op("s_barrier", ()))
         if not helper:
-            consume(rnd)
+            consume(rnd, busy)
         E(Op("s_barrier", ()))
     if helper:
         if synw:

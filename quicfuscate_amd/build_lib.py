@@ -50,6 +50,7 @@ BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
 # (196, 59) 1,383 -> 1,262: three FFT passes run against two plain ones)
 BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_SYNW_SHARED = [(128, 39), (160, 48), (196, 59)]
+BS_XCHG_EARLY = 3     # rows of the next group a shared-row wave loads before its transform
 BS_FFT_DEC_HYBRID = [(96, 15), (48, 8)]   # fused FFT decode ('C') of C5 shapes with k not a power of two
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
@@ -238,9 +239,13 @@ def kernel_specs() -> list:
     # (a code of 3 passes gets a producer-only 4th wave, so two workgroups fill a
     # CU's 8 wave slots and a round holds 4 groups: 0.322-0.333 -> 0.305 ms at
     # (160, 48), 0.309-0.316 -> 0.299-0.302 at (128, 39), profiles/r05ae_c5_helper.json)
+    # (each wave issues the loads of its next group's first 3 rows before
+    # transforming the current group, xchg_early: 0.315-0.329 -> 0.305-0.316 ms
+    # at (196, 59), tools/c5_lab.py, profiles/r05au_c5_xchg_early.json)
     for k, rt in BS_FFT_PASSES:
         cps = lch_fft.coset_passes(k, rt)
-        specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0)
+        specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0,
+                                                   xchg_early=BS_XCHG_EARLY)
                                      for j0, rp in cps], xchg=True, helpers=max(0, 4 - len(cps))))
     # the synw passes of the C5 codes in one pass-major dispatch: one launch
     # of P x n workgroups instead of P launches of n, so a pass's last, partly
@@ -257,7 +262,8 @@ def kernel_specs() -> list:
     # decode 2,007-2,019 against 2,025-2,031 GiB/s, profiles/r05af_c5_helper_decode.json)
     for k, rt in BS_FFT_SYNW_SHARED:
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt,
-                                                   j0=j0) for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))
+                                                   j0=j0, xchg_early=BS_XCHG_EARLY)
+                                     for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))
     for k, rt in BS_ENC_ONLY:
         npass = -(-rt // BS_PASS)
         if npass == 1:

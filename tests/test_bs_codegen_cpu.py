@@ -617,7 +617,7 @@ def test_register_tuples_even_aligned(k, r, mode, chunked):
 
 
 def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged=False, fft=0, concat=False,
-               xchg=False, helpers=0):
+               xchg=False, helpers=0, xchg_early=0):
     """The wave-uniform syndrome kernel (mode "synw") on the emulator for
     every pass j0 of (k, rt) in steps of rp: accepted repairs' syndromes of
     generations with a repair >= j0 equal p_j ^ C[j, S] x_S; items whose
@@ -632,7 +632,7 @@ def _synw_case(oracle, k, rt, rp, L, G, seed, offs=False, use_bound=True, merged
     if fft:   # additive-FFT passes: one per coset of 16 repair points (lch_fft.coset_passes)
         from quicfuscate_amd import lch_fft
 
-        specs = [bs.KernelSpec(k, n, 2, mode="synw", r_total=rt, j0=j0, fft=fft)
+        specs = [bs.KernelSpec(k, n, 2, mode="synw", r_total=rt, j0=j0, fft=fft, xchg_early=xchg_early)
                  for j0, n in lch_fft.coset_passes(k, rt)]
     else:
         specs = [bs.KernelSpec(k, min(rp, rt - j0), 2, mode="synw", r_total=rt, j0=j0) for j0 in range(0, rt, rp)]
@@ -751,16 +751,17 @@ def test_emulated_synw_fft(oracle, k, rt, L, G, offs):
     assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 7 + rt + L, offs=offs, fft=8) > 0
 
 
+@pytest.mark.parametrize("early", [0, 5])
 @pytest.mark.parametrize("k,rt,L,G,offs,helpers", [(24, 10, 2048, 3, False, 0), (20, 20, 2100, 4, True, 0),
                                                    (48, 21, 2064, 3, False, 0), (196, 59, 2048, 2, False, 0),
                                                    (48, 21, 2064, 3, True, 1), (20, 20, 2100, 4, False, 2)])
-def test_emulated_synw_xchg(oracle, k, rt, L, G, offs, helpers):
+def test_emulated_synw_xchg(oracle, k, rt, L, G, offs, helpers, early):
     """Item-major merged FFT synw whose waves share the source rows' gather,
     transposes and chunk butterflies through LDS (merged_spec(xchg=True)):
     the same syndromes and skips as the per-pass kernels; a skipped pass's
     wave still produces its groups (the barriers stay matched)."""
     assert _synw_case(oracle, k, rt, 0, L, G, seed=k * 11 + rt + L, offs=offs, fft=8, merged=True, xchg=True,
-                      helpers=helpers) > 0
+                      helpers=helpers, xchg_early=early) > 0
 
 
 def test_emulated_synw_without_bound(oracle):
@@ -1145,11 +1146,12 @@ def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
             assert (dst[off + 16 * Lv: off + drs] == 0xEE).all()
 
 
+@pytest.mark.parametrize("early", [0, 5])
 @pytest.mark.parametrize("k,rt,L,G,blocks,helpers", [(24, 10, 200, 3, 0, 0), (48, 21, 2100, 2, 3, 0),
                                                     (20, 20, 72, 2, 0, 0), (196, 59, 40, 1, 0, 0),
                                                     (160, 48, 40, 1, 0, 0), (128, 39, 100, 2, 1, 0),
                                                     (160, 48, 40, 1, 0, 1), (20, 20, 72, 2, 1, 2)])
-def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks, helpers):
+def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks, helpers, early):
     """The merged additive-FFT encode whose waves share the row work through
     LDS (merged_spec(xchg=True), _generate_enc_xchg): wave w produces groups
     w, w + W, ... into its LDS slot, every wave folds every group; the
@@ -1165,7 +1167,8 @@ def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks, helpers):
     dgs = rt * drs
     src = rng.integers(0, 256, G * sgs + 64, dtype=np.uint8)
     dst = np.full(G * dgs, 0xEE, np.uint8)
-    passes = [bs.KernelSpec(k, rp, 3, r_total=rt, j0=j0, fft=8, ld_policy="") for j0, rp in lch_fft.coset_passes(k, rt)]
+    passes = [bs.KernelSpec(k, rp, 3, r_total=rt, j0=j0, fft=8, ld_policy="", xchg_early=early)
+              for j0, rp in lch_fft.coset_passes(k, rt)]
     ms = bs.merged_spec(passes, xchg=True, helpers=helpers)
     assert ms.waves == len(passes) + helpers and len(passes) > 1 and ms.lds_bytes == ms.waves * 8 * bs.LDS_ROW_BYTES
     emu = bs.Emulator(bs.generate(ms))

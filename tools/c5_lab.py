@@ -24,6 +24,21 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5au: each wave issues the loads of its next group's first rows
+    # before transforming the current group (KernelSpec.xchg_early rotating slots)
+    ("e196_warm", 196, 59, "N", 0, {"xchg": True}),
+    ("e196_x", 196, 59, "N", 0, {"xchg": True}),
+    ("e196_e3", 196, 59, "N", 0, {"xchg": True, "xchg_early": 3}),
+    ("e196_e5", 196, 59, "N", 0, {"xchg": True, "xchg_early": 5}),
+    ("e160_x", 160, 48, "N", 0, {"xchg": True}),
+    ("e160_e5", 160, 48, "N", 0, {"xchg": True, "xchg_early": 5}),
+    ("e196_x_2", 196, 59, "N", 0, {"xchg": True}),
+    ("e196_e3_2", 196, 59, "N", 0, {"xchg": True, "xchg_early": 3}),
+    ("e196_e5_2", 196, 59, "N", 0, {"xchg": True, "xchg_early": 5}),
+    ("e160_x_2", 160, 48, "N", 0, {"xchg": True}),
+    ("e160_e5_2", 160, 48, "N", 0, {"xchg": True, "xchg_early": 5}),
+]
+VARIANTS_R05AT = [
     # round 5at: what the shared-row (196, 59) encode waits on: no row loads
     # (compute, LDS exchange and barriers only) / no VALU data work (loads,
     # LDS exchange, barriers, stores)
