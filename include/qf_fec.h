@@ -176,6 +176,9 @@ enum {
                                     one dispatch, the passes' waves sharing the source rows' gather,
                                     transposes and chunk butterflies through LDS; 0: pass-major
                                     (each pass re-reads the sources) [QF_SYNW_SHARED; default 1] */
+    QF_OPT_COMBINE_WIDE,         /* 1: a bit-sliced payload pass with 17-24 outputs (e_max) runs as one
+                                    24-output pass reading two coefficient records per row; 0: two
+                                    16-output passes (pass-major) [QF_COMBINE_WIDE; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

@@ -603,7 +603,7 @@ class KernelSpec:
     @property
     def next_free_vgpr(self) -> int:
         if self.mode == "cmb":
-            return CMB_NEXT_FREE_VGPR
+            return _cmb_regs(self.r)["end"]
         n = self._base_free_vgpr()
         if self.vmask is not None and not (self.mode == "dec" and self.chunked):
             n += 3
@@ -635,7 +635,7 @@ class KernelSpec:
     @property
     def kernarg_bytes(self) -> int:
         if self.mode == "cmb":
-            return KERNARG_BYTES_CMB + (8 if self.pass_major else 0)
+            return KERNARG_BYTES_CMB + (8 if self.pass_major or self.r > 16 else 0)
         if self.mode == "synw":
             return KERNARG_BYTES_SYNW
         return KERNARG_BYTES_DEC if self.mode == "dec" else KERNARG_BYTES
@@ -2950,6 +2950,17 @@ C_LO, C_HI = 24, 40               # LO[0..15], HI[0..15]
 C_ACC = 56                        # 16 x 8 accumulators v56..v183
 C_QV, C_QC, C_UB, C_UBC, C_TB = 184, 185, 186, 187, 188
 C_VM = 189                        # v189..v191 transpose masks (full-rate all-VGPR v_bitop3)
+CMB_WIDE_R = 24                   # the wide single pass: outputs 16..23 from the pass-1 record
+
+
+def _cmb_regs(R: int) -> dict:
+    """VGPRs past the accumulators: the fixed layout above for R <= 16; the
+    wide pass (R = 24, 192 accumulators) moves them above its accumulators
+    (256 VGPRs: still two waves per SIMD)."""
+    if R <= 16:
+        return {"qv": C_QV, "qc": C_QC, "ub": C_UB, "ubc": C_UBC, "tb": C_TB, "vm": C_VM, "end": CMB_NEXT_FREE_VGPR}
+    b = C_ACC + 8 * R
+    return {"qv": b, "qc": b + 1, "ub": b + 2, "ubc": b + 3, "tb": b + 4, "vm": b + 5, "end": b + 8}
 # SGPRs
 CS_ITEM, CS_G, CS_T, CS_EW, CS_BOUND, CS_SLOT = 36, 37, 38, 39, 40, 41
 CS_ROWG, CS_CUR, CS_NEXT, CS_COEFG, CS_DSTG = 42, 44, 46, 48, 50
@@ -2958,6 +2969,10 @@ CS_IDX = (56, 72)                 # two 16-SGPR index buffers (4-aligned)
 CS_VALID, CS_FULLB, CS_TAIL, CS_TMP64 = 88, 90, 92, 94
 CS_MASKS = 96                     # s96..s98 transpose masks
 CS_T0, CS_T1, CS_TBYTES = 99, 100, 3
+# wide pass (R > 16): s[0:1] the pass-1 record's first 8 bytes (outputs 16..23),
+# s2 its offset (free once the kernarg is loaded and the workgroup id read),
+# s101 the records' pass stride (kernarg word 32)
+CS_REC2, CS_REC2_OFF, CS_PSTRIDE = 0, 2, 101
 
 
 def cmb_index_table() -> np.ndarray:
@@ -2971,11 +2986,11 @@ def cmb_index_table() -> np.ndarray:
     return t
 
 
-def _cmb_transpose(E, base: int, last_dst: Optional[list] = None):
+def _cmb_transpose(E, base: int, last_dst: Optional[list] = None, vm0: int = C_VM):
     """bfi delta-swap network on 8 registers (plane p <- bit p of every byte);
     the last stage writes plane p to last_dst[p] (default: in place)."""
     for stage, (sh, _mask, pairs) in enumerate(_TRANSPOSE):
-        vm = C_VM + stage
+        vm = vm0 + stage
         for q, (a, b) in enumerate(pairs):
             t, u = C_T + 2 * (q & 1), C_T + 2 * (q & 1) + 1
             da, db = base + a, base + b
@@ -3010,6 +3025,9 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     `other`, bit-slice, combinations, then the ew products."""
     E(Op("s_lshl", (CS_T0, CS_SLOT, 4)))
     E(Op("s_load_n", (CS_REC, CS_COEFG, 4, CS_T0, 0)))
+    if spec.r > 16:   # outputs 16.. from the pass-1 record of the row
+        E(Op("s_add", (CS_REC2_OFF, CS_T0, CS_PSTRIDE)))
+        E(Op("s_load_n", (CS_REC2, CS_COEFG, 2, CS_REC2_OFF, 0)))
     E(Op("s_addk", (CS_T0, CS_SLOT, 1)))
     E(Op("s_cmp_ge_br", (CS_T0, CS_BOUND, f".Lnopf{tag}")))
     E(Op("s_add_cc", (CS_NEXT, CS_CUR, 12)))
@@ -3022,7 +3040,7 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     E(Op("s_waitcnt_vm", (0,)))
     E(Op("label", (f".Lrow{tag}",)))
     singles = [C_LO + 1, C_LO + 2, C_LO + 4, C_LO + 8, C_HI + 1, C_HI + 2, C_HI + 4, C_HI + 8]
-    _cmb_transpose(E, buf, singles)
+    _cmb_transpose(E, buf, singles, _cmb_regs(spec.r)["vm"])
     for tab in (C_LO, C_HI):
         for m in sorted(_COMBO_BUILD):
             a, b = _COMBO_BUILD[m]
@@ -3032,12 +3050,15 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     E(Op("s_bfe_k", (CS_T0, CS_REC, 0, 8)))
     E(Op("s_lshl", (CS_T0, CS_T0, 6)))
     E(Op("s_load_n", (CS_IDX[0], 22, 16, CS_T0, 0)))
+    def rec_sgpr(j: int) -> int:   # the SGPR holding output j's coefficient byte
+        return CS_REC + j // 4 if j < 16 else CS_REC2 + (j - 16) // 4
+
     for j in range(spec.r):
         if j:
             E(Op("s_cmp_le_k_br", (CS_EW, j, f".Lpe{tag}")))
         E(Op("s_waitcnt_lgkm", ()))
         if j + 1 < spec.r:   # the next output's indices load during this product
-            E(Op("s_bfe_k", (CS_T0, CS_REC + (j + 1) // 4, 8 * ((j + 1) % 4), 8)))
+            E(Op("s_bfe_k", (CS_T0, rec_sgpr(j + 1), 8 * ((j + 1) % 4), 8)))
             E(Op("s_lshl", (CS_T0, CS_T0, 6)))
             E(Op("s_load_n", (CS_IDX[(j + 1) % 2], 22, 16, CS_T0, 0)))
         ix = CS_IDX[j % 2]
@@ -3056,7 +3077,10 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     ops: list[Op] = []
     E = ops.append
     R = spec.r
-    assert R <= 16 and C_ACC + 8 * R <= C_QV
+    assert R <= 16 or (R == CMB_WIDE_R and not spec.pass_major)
+    rg = _cmb_regs(R)
+    C_QV, C_QC, C_UB, C_UBC, C_TB, C_VM = (rg[x] for x in ("qv", "qc", "ub", "ubc", "tb", "vm"))
+    assert C_ACC + 8 * R <= C_QV and rg["end"] <= 256
     E(Op("s_load_n", (4, 0, 16, None, 0)))
     E(Op("s_load_n", (20, 0, 16, None, 64)))
     E(Op("v_lshr", (1, 6, 0)))
@@ -3069,6 +3093,8 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     E(Op("v_movk", (C_HI, 0)))
     if spec.pass_major:
         E(Op("s_load_n", (CS_T1, 0, 1, None, KERNARG_BYTES_CMB)))   # records' pass stride
+    if R > 16:
+        E(Op("s_load_n", (CS_PSTRIDE, 0, 1, None, KERNARG_BYTES_CMB)))
     E(Op("s_waitcnt_lgkm", ()))
     if spec.pass_major:
         # workgroups [p n, (p + 1) n) run pass p (n = grid waves / 4): the
@@ -3160,7 +3186,7 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     for j in range(R):
         acc = C_ACC + 8 * j
         E(Op("s_cmp_le_k_br", (CS_EW, j, ".Lst_end")))
-        _cmb_transpose(E, acc)
+        _cmb_transpose(E, acc, None, C_VM)
         E(Op("s_movk", (CS_T0, j)))
         E(Op("s_mul", (CS_T0, CS_T0, 13)))
         E(Op("s_add_cc", (CS_TMP64, CS_DSTG, CS_T0)))

@@ -282,6 +282,9 @@ def kernel_specs() -> list:
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
     # ... and every pass of it in one pass-major launch ('P', QF_ENCODE_MERGED)
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True))
+    # ... and the wide single pass for 17-24 outputs (QF_COMBINE_WIDE): each
+    # input row read and transposed once instead of once per pass
+    specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb"))
     return specs
 
 

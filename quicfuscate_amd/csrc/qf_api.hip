@@ -206,6 +206,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* PREPARE_LANES */ {"QF_PREPARE_LANES", 1, 0, 1, false},
     /* ENCODE_MERGED */ {"QF_ENCODE_MERGED", 1, 0, 1, false},
     /* SYNW_SHARED */ {"QF_SYNW_SHARED", 1, 0, 1, false},
+    /* COMBINE_WIDE */ {"QF_COMBINE_WIDE", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }
@@ -611,6 +612,9 @@ static bool combine_bs_ok(qf_ctx* ctx, const qf::CombineSlotsArgs& a, bool offs_
     const uint32_t min_q = (uint32_t)ctx->opt[QF_OPT_COMBINE_BS_MIN_Q];
     // (Lu >= 2: the partial last unit is then always some lane's unit B)
     if (a.Lu < 2 || (a.Lu + 1) / 2 < min_q) return false;
+    // (32-bit strides in the kernel: row j of the 16 outputs at j * dst stride)
+    if (a.row_stride >= (1ull << 32) || 16ull * a.dst_row_stride >= (1ull << 32) || a.coef_gen_stride >= (1ull << 32))
+        return false;
     if (a.L % 16 && ((a.rows_offs && !offs_al16) ||
                      ((uintptr_t)a.rows | a.row_stride | (a.rows_offs ? 0 : a.rows_gen_stride)) % 16))
         return false;
@@ -755,8 +759,10 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
                  qf::cmb_pass_major_ok(passes, sh->rec_row_stride, (uint64_t)G * cgs) &&
                  combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
             if (pm) {
-                cname = "qf_combine_bs_r16_pm";
-                QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx, passes, (uint64_t)G * cgs));
+                cname = qf::cmb_wide_ok(ctx->bs, a, passes, (uint64_t)G * cgs, e_max) ? "qf_combine_bs_r24"
+                                                                                      : "qf_combine_bs_r16_pm";
+                QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx, passes, (uint64_t)G * cgs,
+                                            e_max));
             } else {
                 QF_CHECK_HIP(combine_payload(ctx, a, PD, st, &cname));
             }
@@ -1654,9 +1660,10 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
              qf::cmb_pass_major_ok(passes, sh->rec_row_stride, (uint64_t)G * coef_gen_stride) &&
              combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
         if (pm) {
-            cname = "qf_combine_bs_r16_pm";
+            cname = qf::cmb_wide_ok(ctx->bs, a, passes, (uint64_t)G * coef_gen_stride, e_max) ? "qf_combine_bs_r24"
+                                                                                              : "qf_combine_bs_r16_pm";
             QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, ctx->stream, a, ctx->d_cmbidx, passes,
-                                        (uint64_t)G * coef_gen_stride));
+                                        (uint64_t)G * coef_gen_stride, e_max));
         } else {
             QF_CHECK_HIP(combine_payload(ctx, a, PD, ctx->stream, &cname));
         }

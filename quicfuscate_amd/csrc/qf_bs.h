@@ -86,8 +86,13 @@ bool cmb_pass_major_available();
 // back to one launch per pass when this is false.
 constexpr uint32_t kCmbMaxPasses = 4;
 bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_stride);
+// e_max: the largest n_out of the batch; 16 < e_max <= 24 over two passes
+// runs the wide single pass (QF_COMBINE_WIDE) when the library holds it and
+// cmb_wide_ok says so
+bool cmb_wide_ok(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride, uint32_t e_max);
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
-                      const uint32_t* idxtab, uint32_t passes = 1, uint64_t pass_stride = 0);
+                      const uint32_t* idxtab, uint32_t passes = 1, uint64_t pass_stride = 0,
+                      uint32_t e_max = 0);
 void bs_unload(BsCache& cache);
 
 }  // namespace qf

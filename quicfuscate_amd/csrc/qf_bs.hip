@@ -344,12 +344,24 @@ bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_s
            16ull * (passes - 1) * dst_row_stride < (1ull << 32) && cmb_pass_major_available();
 }
 
+bool cmb_wide_ok(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride,
+                 uint32_t e_max) {
+    return passes == 2 && e_max > 16 && e_max <= 24 && a.pass == 0 && pass_stride < (1ull << 32) &&
+           24ull * a.dst_row_stride < (1ull << 32) && cache.get(QF_OPT_COMBINE_WIDE) && find('m', 0, 24) != nullptr;
+}
+
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
-                      const uint32_t* idxtab, uint32_t passes, uint64_t pass_stride) {
-    const QfBsEntry* e = find(passes > 1 ? 'P' : 'm', 0, 16);
-    if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || a.dst_row_stride >= (1ull << 32) ||
+                      const uint32_t* idxtab, uint32_t passes, uint64_t pass_stride, uint32_t e_max) {
+    // the wide pass: 24 outputs per item (192 accumulator VGPRs, still two
+    // waves per SIMD), outputs 16..23 from the row's pass-1 record, so a
+    // batch of 17-24 outputs reads and transposes each input row once
+    // instead of once per 16-output pass (output j's row at j * dst stride:
+    // a 32-bit product in the kernel)
+    const bool wide = cmb_wide_ok(cache, a, passes, pass_stride, e_max);
+    const QfBsEntry* e = wide ? find('m', 0, 24) : find(passes > 1 ? 'P' : 'm', 0, 16);
+    if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || 16ull * a.dst_row_stride >= (1ull << 32) ||
         a.coef_gen_stride >= (1ull << 32) || passes == 0 || (passes > 1 && a.pass != 0) ||
-        (passes > 1 && !cmb_pass_major_ok(passes, a.dst_row_stride, pass_stride)))
+        (passes > 1 && !wide && !cmb_pass_major_ok(passes, a.dst_row_stride, pass_stride)))
         return bs_invalid(__LINE__);
     const int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return bs_invalid(__LINE__);
@@ -382,9 +394,11 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
                       (uint32_t)pass_stride, 0};
     // (pass-major: words 32..33 = the records' pass stride; the grid holds
     // every pass's `blocks` workgroups, pass p's at [p blocks, (p + 1) blocks))
+    // (the wide pass: word 32 too, one pass's grid)
     size_t sz = passes > 1 ? sizeof(w) : 32 * sizeof(uint32_t);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, w, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks * passes, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks * (wide ? 1 : passes), 1, 1, 256, 1, 1, 0, st,
+                                 nullptr, cfg);
 }
 
 void bs_unload(BsCache& cache) {

@@ -983,6 +983,67 @@ def test_emulated_combine_bs_pass_major(L, G, P, offs):
                 assert (row == 0xEE).all(), (g, j)
 
 
+@pytest.mark.parametrize("L,G,offs", [(1200, 6, False), (4100, 3, True), (100, 9, False), (33, 4, True)])
+def test_emulated_combine_bs_wide(L, G, offs):
+    """The wide single pass (qf_combine_bs_r24, QF_COMBINE_WIDE): 24 outputs
+    per item, outputs 16..23 from the row's pass-1 record at coef +
+    pass_stride; byte-equal to the two 16-output passes it replaces, and rows
+    past a generation's e untouched."""
+    global _GFT
+    if _GFT is None:
+        _GFT = _gf_table()
+    rng = np.random.default_rng(L + 7 * G)
+    spec = bs.KernelSpec(0, bs.CMB_WIDE_R, mode="cmb")
+    assert spec.next_free_vgpr <= 256
+    Lp = (L + 15) // 16 * 16
+    rs, drs = Lp + 32, Lp + 48
+    nslot = 28
+    rgs, dgs = nslot * rs + 16, 24 * drs + 32
+    cgs = (nslot + 1) * 16
+    PS = G * cgs + 64
+    rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
+    rec = rng.integers(0, 256, 2 * PS, dtype=np.uint8)
+    e = rng.integers(1, 25, G).astype(np.uint32)
+    bound = rng.integers(1, nslot + 1, G).astype(np.uint32)
+    e[0], e[1 % G] = 24, 17
+    if G > 3:
+        e[2], bound[3] = 16, 0
+    out = np.full(G * dgs, 0xEE, np.uint8)
+    ROWS, OUT, REC, NO, BD, TAB, T1, T2 = (0x10000000, 0x40000000, 0x50000000, 0x60000000, 0x61000000,
+                                           0x62000000, 0x63000000, 0x64000000)
+    emu = bs.Emulator(bs.generate(spec))
+    so = do = 0
+    rgs_k, dgs_k = rgs, dgs
+    if offs:
+        emu.add_buffer(T1, np.array([(G - 1 - g) * rgs for g in range(G)], np.uint64).view(np.uint8))
+        emu.add_buffer(T2, np.array([(G - 1 - g) * dgs for g in range(G)], np.uint64).view(np.uint8))
+        so, do, rgs_k, dgs_k = T1, T2, 0, 0
+    for base, buf in ((ROWS, rows), (OUT, out), (REC, rec), (NO, e), (BD, bound),
+                      (TAB, bs.cmb_index_table().reshape(-1).view(np.uint8))):
+        emu.add_buffer(base, buf.view(np.uint8))
+    n = 2
+    ka, n_items = bs.cmb_kernargs(ROWS, OUT, rgs_k, dgs_k, rs, drs, REC, cgs, 0, NO, BD, TAB, L, G, 4 * n,
+                                  rows_offs=so, dst_offs=do, pass_stride=PS)
+    for wg in range(n):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        gr = (G - 1 - g) if offs else g
+        blk = out[gr * dgs:(gr + 1) * dgs]
+        for j in range(24):
+            row = blk[j * drs:(j + 1) * drs]
+            if j < e[g]:
+                p, jj = divmod(j, 16)
+                want = np.zeros(L, np.uint8)
+                for sl in range(int(bound[g])):
+                    c = rec[p * PS + g * cgs + 16 * sl + jj]
+                    want ^= _GFT[c][rows[gr * rgs + sl * rs: gr * rgs + sl * rs + L]]
+                assert (row[:L] == want).all(), (g, j)
+                assert (row[L:] == 0xEE).all(), (g, j)
+            else:
+                assert (row == 0xEE).all(), (g, j)
+
+
 # --------------------------------------------------------------------------
 # Additive-FFT row loop (lch_fft.py, KernelSpec.fft)
 # --------------------------------------------------------------------------

@@ -546,6 +546,26 @@ def test_decode_general_path_more_than_four_passes(qf, oracle, gpu_ctx, path, mo
     assert max(out[2]) > 64
 
 
+@pytest.mark.parametrize("wide", [1, 0])
+@pytest.mark.parametrize("path", ["default_1wave", "general_bs"])
+@pytest.mark.parametrize("k,r,L,G,erase", [(128, 20, 9000, 5, None), (128, 20, 4100, 7, 20), (64, 24, 2048, 6, 24),
+                                           (40, 20, 3000, 5, 17), (64, 24, 2100, 9, None)])
+def test_decode_combine_wide(qf, oracle, gpu_ctx, k, r, L, G, erase, path, wide, monkeypatch):
+    """A payload pass of 17-24 outputs (e_max = min(k, r)) as one 24-output
+    pass reading two coefficient records per row (qf_combine_bs_r24,
+    QF_OPT_COMBINE_WIDE = 1) or as two 16-output passes (0): bit-exact either
+    way, on the C5 syndrome path and the general (Gauss-Jordan) path, with
+    generations of e <= 16 (no pass-1 outputs) among them when e is random."""
+    _path(monkeypatch, path)
+    qf.set_default_options(combine_wide=wide)
+    rng = np.random.default_rng(k * 7 + r + L + (erase or 0))
+    kw = {"erase": erase, "shuffle": False} if erase is not None else {}
+    max_rows = k + r
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, **kw)
+    out = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+
+
 @pytest.mark.parametrize("shared", [1, 0])
 @pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 6, None), (196, 59, 9000, 6, 3), (160, 48, 4100, 9, 40),
                                            (128, 39, 2100, 12, None)])
