@@ -399,6 +399,9 @@ class KernelSpec:
     # records start on 8 different LDS banks) instead of 256 B (64 KB, every
     # record on the same bank)
     lab_tab32: bool = False
+    # lab only (cmb): "idx_once" -- one index row per input row, reused by every
+    # output (no per-product scalar load); "noload" -- no input-row loads
+    lab_cmb: tuple = ()
     # VALU list scheduling (bs_sched.schedule): runs of plain VALU ops between
     # non-VALU ops reordered so a producer sits >= sched ops before its
     # consumers where the run allows it (0: program order)
@@ -3032,8 +3035,9 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     E(Op("s_cmp_ge_br", (CS_T0, CS_BOUND, f".Lnopf{tag}")))
     E(Op("s_add_cc", (CS_NEXT, CS_CUR, 12)))
     E(Op("s_addck", (CS_NEXT + 1, CS_CUR + 1, 0)))
-    E(Op("load16_saddr", (other, C_OA, CS_NEXT, spec.ld_policy)))
-    E(Op("load16_saddr", (other + 4, C_OB, CS_NEXT, spec.ld_policy)))
+    if "noload" not in spec.lab_cmb:
+        E(Op("load16_saddr", (other, C_OA, CS_NEXT, spec.ld_policy)))
+        E(Op("load16_saddr", (other + 4, C_OB, CS_NEXT, spec.ld_policy)))
     E(Op("s_waitcnt_vm", (2,)))
     E(Op("s_branch", (f".Lrow{tag}",)))
     E(Op("label", (f".Lnopf{tag}",)))
@@ -3057,11 +3061,11 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
         if j:
             E(Op("s_cmp_le_k_br", (CS_EW, j, f".Lpe{tag}")))
         E(Op("s_waitcnt_lgkm", ()))
-        if j + 1 < spec.r:   # the next output's indices load during this product
+        if j + 1 < spec.r and "idx_once" not in spec.lab_cmb:   # the next output's indices load during this product
             E(Op("s_bfe_k", (CS_T0, rec_sgpr(j + 1), 8 * ((j + 1) % 4), 8)))
             E(Op("s_lshl", (CS_T0, CS_T0, 6)))
             E(Op("s_load_n", (CS_IDX[(j + 1) % 2], 22, 16, CS_T0, 0)))
-        ix = CS_IDX[j % 2]
+        ix = CS_IDX[0] if "idx_once" in spec.lab_cmb else CS_IDX[j % 2]
         for p in range(8):
             acc = C_ACC + 8 * j + p
             E(Op("s_idx_on" if p == 0 else "s_idx", (ix + 2 * p,)))
