@@ -402,6 +402,13 @@ class KernelSpec:
     # lab only (cmb): "idx_once" -- one index row per input row, reused by every
     # output (no per-product scalar load); "noload" -- no input-row loads
     lab_cmb: tuple = ()
+    # cmb: the gpr_idx mode on for a row's whole product run (not per product)
+    # and the early exit tested every 4 outputs (products past a generation's
+    # outputs go to accumulators that are never stored)
+    cmb_lean: bool = False
+    # cmb (R <= 16): input rows prefetched two ahead (a third row buffer at
+    # v192..v199: 200 VGPRs, still two waves per SIMD)
+    cmb_pf2: bool = False
     # VALU list scheduling (bs_sched.schedule): runs of plain VALU ops between
     # non-VALU ops reordered so a producer sits >= sched ops before its
     # consumers where the run allows it (0: program order)
@@ -606,7 +613,7 @@ class KernelSpec:
     @property
     def next_free_vgpr(self) -> int:
         if self.mode == "cmb":
-            return _cmb_regs(self.r)["end"]
+            return _cmb_regs(self.r)["end"] + (8 if self.cmb_pf2 else 0)
         n = self._base_free_vgpr()
         if self.vmask is not None and not (self.mode == "dec" and self.chunked):
             n += 3
@@ -3031,14 +3038,19 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     if spec.r > 16:   # outputs 16.. from the pass-1 record of the row
         E(Op("s_add", (CS_REC2_OFF, CS_T0, CS_PSTRIDE)))
         E(Op("s_load_n", (CS_REC2, CS_COEFG, 2, CS_REC2_OFF, 0)))
-    E(Op("s_addk", (CS_T0, CS_SLOT, 1)))
+    ahead = 2 if spec.cmb_pf2 else 1
+    E(Op("s_addk", (CS_T0, CS_SLOT, ahead)))
     E(Op("s_cmp_ge_br", (CS_T0, CS_BOUND, f".Lnopf{tag}")))
-    E(Op("s_add_cc", (CS_NEXT, CS_CUR, 12)))
-    E(Op("s_addck", (CS_NEXT + 1, CS_CUR + 1, 0)))
+    if spec.cmb_pf2:   # CS_NEXT: the last row issued
+        E(Op("s_add_cc", (CS_NEXT, CS_NEXT, 12)))
+        E(Op("s_addck", (CS_NEXT + 1, CS_NEXT + 1, 0)))
+    else:
+        E(Op("s_add_cc", (CS_NEXT, CS_CUR, 12)))
+        E(Op("s_addck", (CS_NEXT + 1, CS_CUR + 1, 0)))
     if "noload" not in spec.lab_cmb:
         E(Op("load16_saddr", (other, C_OA, CS_NEXT, spec.ld_policy)))
         E(Op("load16_saddr", (other + 4, C_OB, CS_NEXT, spec.ld_policy)))
-    E(Op("s_waitcnt_vm", (2,)))
+    E(Op("s_waitcnt_vm", (2 * ahead,)))
     E(Op("s_branch", (f".Lrow{tag}",)))
     E(Op("label", (f".Lnopf{tag}",)))
     E(Op("s_waitcnt_vm", (0,)))
@@ -3057,8 +3069,9 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     def rec_sgpr(j: int) -> int:   # the SGPR holding output j's coefficient byte
         return CS_REC + j // 4 if j < 16 else CS_REC2 + (j - 16) // 4
 
+    lean = spec.cmb_lean
     for j in range(spec.r):
-        if j:
+        if j and (not lean or j % 4 == 0):
             E(Op("s_cmp_le_k_br", (CS_EW, j, f".Lpe{tag}")))
         E(Op("s_waitcnt_lgkm", ()))
         if j + 1 < spec.r and "idx_once" not in spec.lab_cmb:   # the next output's indices load during this product
@@ -3068,12 +3081,15 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
         ix = CS_IDX[0] if "idx_once" in spec.lab_cmb else CS_IDX[j % 2]
         for p in range(8):
             acc = C_ACC + 8 * j + p
-            E(Op("s_idx_on" if p == 0 else "s_idx", (ix + 2 * p,)))
+            E(Op("s_idx_on" if p == 0 and (j == 0 or not lean) else "s_idx", (ix + 2 * p,)))
             E(Op("v_xor_rel", (acc, C_LO, acc)))
             E(Op("s_idx", (ix + 2 * p + 1,)))
             E(Op("v_xor_rel", (acc, C_HI, acc)))
-        E(Op("s_idx_off", ()))
+        if not lean:
+            E(Op("s_idx_off", ()))
     E(Op("label", (f".Lpe{tag}",)))
+    if lean:   # every exit leaves after product 0, with the mode on
+        E(Op("s_idx_off", ()))
     E(Op("s_waitcnt_lgkm", ()))
 
 
@@ -3176,13 +3192,28 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     E(Op("s_cmp_le_k_br", (CS_BOUND, 0, ".Lstores")))
     E(Op("load16_saddr", (C_BUF[0], C_OA, CS_CUR, spec.ld_policy)))
     E(Op("load16_saddr", (C_BUF[0] + 4, C_OB, CS_CUR, spec.ld_policy)))
+    bufs = list(C_BUF)
+    if spec.cmb_pf2:   # row 1 in flight too; CS_NEXT tracks the last row issued
+        assert R <= 16
+        bufs.append(rg["end"])
+        E(Op("s_mov", (CS_NEXT, CS_CUR)))
+        E(Op("s_mov", (CS_NEXT + 1, CS_CUR + 1)))
+        E(Op("s_cmp_le_k_br", (CS_BOUND, 1, ".Lpf1")))
+        E(Op("s_add_cc", (CS_NEXT, CS_NEXT, 12)))
+        E(Op("s_addck", (CS_NEXT + 1, CS_NEXT + 1, 0)))
+        E(Op("load16_saddr", (bufs[1], C_OA, CS_NEXT, spec.ld_policy)))
+        E(Op("load16_saddr", (bufs[1] + 4, C_OB, CS_NEXT, spec.ld_policy)))
+        E(Op("label", (".Lpf1",)))
+    nb = len(bufs)
+    ahead = 2 if spec.cmb_pf2 else 1
     E(Op("label", (".Lslot",)))
-    for h in range(2):
-        _cmb_row(E, spec, C_BUF[h], C_BUF[1 - h], f"{h}")
+    for h in range(nb):
+        _cmb_row(E, spec, bufs[h], bufs[(h + ahead) % nb], f"{h}")
         E(Op("s_addk", (CS_SLOT, CS_SLOT, 1)))
         E(Op("s_cmp_ge_br", (CS_SLOT, CS_BOUND, ".Lstores")))
-        E(Op("s_mov", (CS_CUR, CS_NEXT)))
-        E(Op("s_mov", (CS_CUR + 1, CS_NEXT + 1)))
+        if not spec.cmb_pf2:
+            E(Op("s_mov", (CS_CUR, CS_NEXT)))
+            E(Op("s_mov", (CS_CUR + 1, CS_NEXT + 1)))
     E(Op("s_branch", (".Lslot",)))
     # recovered rows: bytes back (inverse transpose), unit A on valid lanes,
     # unit B where it is a whole unit, and the partial last unit bytewise

@@ -279,12 +279,17 @@ def kernel_specs() -> list:
     # 0.529 / 0.482 at (160, 48) / (196, 59) / (128, 39), profiles/r04z_c5_merged.json;
     # those passes are not bound by their row reads)
     # bit-sliced payload pass with wave-uniform runtime coefficients ('m')
-    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb"))
+    # (cmb_lean: the gpr_idx mode on for a row's whole product run, the early
+    # exit every 4 outputs: 2.47 -> 2.40 ms at e = 39, 1.34 -> 1.27-1.29 for the
+    # wide pass at e = 20, tools/cmb_lab.py, profiles/r05az_cmb_lab.json; rows
+    # two ahead (cmb_pf2) measured neutral, profiles/r05ba_cmb_lab.json)
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", cmb_lean=True))
     # ... and every pass of it in one pass-major launch ('P', QF_ENCODE_MERGED)
-    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True))
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True))
     # ... and the wide single pass for 17-24 outputs (QF_COMBINE_WIDE): each
     # input row read and transposed once instead of once per pass
-    specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb"))
+    # (e = 20: 1.60 -> 1.34 ms, tools/cmb_lab.py, profiles/r05ay_cmb_lab.json)
+    specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb", cmb_lean=True))
     return specs
 
 

@@ -857,14 +857,14 @@ def _gf_table():
 _GFT = None
 
 
-def _cmb_case(L, G, seed, pas=0, offs=False, R=16):
+def _cmb_case(L, G, seed, pas=0, offs=False, R=16, lean=False, pf2=False):
     """qf_combine_bs on the emulator: out[j] = sum_{s < bound[g]} rec[g][s][j] *
     rows[g][s] for j < min(e[g] - 16 pass, R), bytes [0, L) only."""
     global _GFT
     if _GFT is None:
         _GFT = _gf_table()
     rng = np.random.default_rng(seed)
-    spec = bs.KernelSpec(0, R, mode="cmb")
+    spec = bs.KernelSpec(0, R, mode="cmb", cmb_lean=lean, cmb_pf2=pf2)
     Lp = (L + 15) // 16 * 16
     rs, drs = Lp + 32, Lp + 48
     nslot = 24
@@ -914,19 +914,22 @@ def _cmb_case(L, G, seed, pas=0, offs=False, R=16):
     return bad
 
 
+@pytest.mark.parametrize("lean,pf2", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("L,G,seed,pas,offs", [
     (64, 5, 1, 0, False),       # Lu = 4, Q = 2: one item per generation
     (100, 4, 2, 0, False),      # partial last unit (4 bytes)
     (1200, 2, 3, 1, True),      # second pass (outputs 16..), offset tables
     (4100, 2, 4, 0, False),     # Q = 129: three items per generation, tail of 4 bytes
     (33, 3, 5, 0, True),        # Lu = 3: unit B of lane 0 is the partial last unit
+    (200, 9, 6, 0, False),      # e of every residue mod 4 (lean: products past e, never stored)
 ])
-def test_emulated_combine_bs(L, G, seed, pas, offs):
-    assert _cmb_case(L, G, seed, pas, offs) == 0
+def test_emulated_combine_bs(L, G, seed, pas, offs, lean, pf2):
+    assert _cmb_case(L, G, seed, pas, offs, lean=lean, pf2=pf2) == 0
 
 
+@pytest.mark.parametrize("lean,pf2", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("L,G,P,offs", [(1200, 5, 3, False), (4100, 3, 2, True), (100, 9, 4, False)])
-def test_emulated_combine_bs_pass_major(L, G, P, offs):
+def test_emulated_combine_bs_pass_major(L, G, P, offs, lean, pf2):
     """Every payload pass in one launch (qf_combine_bs_r16_pm): workgroup
     range p runs pass p with its records at coef + p * pass_stride and its
     outputs at rows 16 p ..; generations with fewer outputs leave the later
@@ -935,7 +938,7 @@ def test_emulated_combine_bs_pass_major(L, G, P, offs):
     if _GFT is None:
         _GFT = _gf_table()
     rng = np.random.default_rng(L + G + P)
-    spec = bs.KernelSpec(0, 16, mode="cmb", pass_major=True)
+    spec = bs.KernelSpec(0, 16, mode="cmb", pass_major=True, cmb_lean=lean, cmb_pf2=pf2)
     Lp = (L + 15) // 16 * 16
     rs, drs = Lp + 32, Lp + 48
     nslot = 16 * P + 4
@@ -983,8 +986,9 @@ def test_emulated_combine_bs_pass_major(L, G, P, offs):
                 assert (row == 0xEE).all(), (g, j)
 
 
+@pytest.mark.parametrize("lean", [False, True])
 @pytest.mark.parametrize("L,G,offs", [(1200, 6, False), (4100, 3, True), (100, 9, False), (33, 4, True)])
-def test_emulated_combine_bs_wide(L, G, offs):
+def test_emulated_combine_bs_wide(L, G, offs, lean):
     """The wide single pass (qf_combine_bs_r24, QF_COMBINE_WIDE): 24 outputs
     per item, outputs 16..23 from the row's pass-1 record at coef +
     pass_stride; byte-equal to the two 16-output passes it replaces, and rows
@@ -993,7 +997,7 @@ def test_emulated_combine_bs_wide(L, G, offs):
     if _GFT is None:
         _GFT = _gf_table()
     rng = np.random.default_rng(L + 7 * G)
-    spec = bs.KernelSpec(0, bs.CMB_WIDE_R, mode="cmb")
+    spec = bs.KernelSpec(0, bs.CMB_WIDE_R, mode="cmb", cmb_lean=lean)
     assert spec.next_free_vgpr <= 256
     Lp = (L + 15) // 16 * 16
     rs, drs = Lp + 32, Lp + 48

@@ -27,18 +27,15 @@ RS = 9008
 # (name, e, R, pass_major, KernelSpec keyword overrides); the first variant of
 # each e is the reference the others' outputs are compared with
 VARIANTS = [
-    ("e39_pm", 39, 16, True, {}),
-    ("e39_pm_idx_once", 39, 16, True, {"lab_cmb": ("idx_once",)}),
-    ("e39_pm_noload", 39, 16, True, {"lab_cmb": ("noload",)}),
-    ("e39_pm_both", 39, 16, True, {"lab_cmb": ("idx_once", "noload")}),
-    ("e20_pm", 20, 16, True, {}),
-    ("e20_wide", 20, 24, False, {}),
-    ("e20_wide_idx_once", 20, 24, False, {"lab_cmb": ("idx_once",)}),
-    ("e20_wide_noload", 20, 24, False, {"lab_cmb": ("noload",)}),
-    ("e39_pm_2", 39, 16, True, {}),
-    ("e39_pm_idx_once_2", 39, 16, True, {"lab_cmb": ("idx_once",)}),
-    ("e20_wide_2", 20, 24, False, {}),
-    ("e20_pm_2", 20, 16, True, {}),
+    # round 5ba: input rows two ahead (KernelSpec.cmb_pf2, a third row buffer)
+    ("e39_lean", 39, 16, True, {"cmb_lean": True}),
+    ("e39_lean_pf2", 39, 16, True, {"cmb_lean": True, "cmb_pf2": True}),
+    ("e20_wide_lean", 20, 24, False, {"cmb_lean": True}),
+    ("e20_pm_lean_pf2", 20, 16, True, {"cmb_lean": True, "cmb_pf2": True}),
+    ("e39_lean_2", 39, 16, True, {"cmb_lean": True}),
+    ("e39_lean_pf2_2", 39, 16, True, {"cmb_lean": True, "cmb_pf2": True}),
+    ("e39_lean_idx_once", 39, 16, True, {"cmb_lean": True, "lab_cmb": ("idx_once",)}),
+    ("e39_lean_pf2_idx_once", 39, 16, True, {"cmb_lean": True, "cmb_pf2": True, "lab_cmb": ("idx_once",)}),
 ]
 
 
@@ -58,7 +55,7 @@ def build():
         spec = make_spec(bs, R, pm, kw)
         text = bs.emit_asm(spec, bs.generate(spec))
         h = assemble(f"cmb_{name}", text.replace(spec.name, f"cmb_{name}"), OUT)
-        manifest.append({"name": name, "e": e, "R": R, "pm": pm, "kw": {k: list(v) for k, v in kw.items()},
+        manifest.append({"name": name, "e": e, "R": R, "pm": pm, "kw": {k: (list(v) if isinstance(v, tuple) else v) for k, v in kw.items()},
                          "hsaco": h.name, "symbol": f"cmb_{name}", "vgprs": spec.next_free_vgpr})
         print(name, spec.next_free_vgpr, h.stat().st_size, flush=True)
     (OUT / "cmb_manifest.json").write_text(json.dumps(manifest, indent=1))
