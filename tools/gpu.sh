@@ -71,6 +71,16 @@ case "$what" in
       --command "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate runs) -- python3 bench.py $ARGS"
     echo PMC_OK
     ;;
+  schedab)  # the headline step, default (split) schedule against --overlap, twice each
+    for i in 1 2; do
+      for m in split overlap; do
+        X=""; [ "$m" = overlap ] && X="--overlap"
+        timeout -k 10 200 python3 bench.py --no-cpu --c3b-G 0 --host-path-G 0 --c5-mixed-bytes 0 --steps 20 \
+          --warmup 5 --detail "" $X > "$OUT/$m$i.log" 2>&1
+      done
+    done
+    for f in split1 overlap1 split2 overlap2; do echo "== $f"; grep '^{"metric"' "$OUT/$f.log" | cut -c1-200; done
+    ;;
   declab)   # tools/dec_lab.py run (build the variants here first: python tools/dec_lab.py build)
     timeout -k 10 300 python3 tools/dec_lab.py run --reps 10 --out "$OUT/dec_lab.json" "$@" > "$OUT/dec_lab.log" 2>&1
     tail -20 "$OUT/dec_lab.log"
