@@ -1538,7 +1538,9 @@ def _generate_xchg(spec: KernelSpec) -> list[Op]:
     that is 1/W of the loads, transposes and chunk butterflies (58 % of a
     (196, 59) pass's VALU before) and 1/W of the code they take.  The loads of
     a wave's next group are issued as soon as its planes are in LDS, so they
-    fly during the fold phase.  Every stream has the same barrier sequence
+    fly during the fold phase; with spec.xchg_early its first rows already
+    before the transform, into 8-VGPR row slots the current group does not
+    hold (the slots rotate roles).  Every stream has the same barrier sequence
     and item loop, so the workgroup's waves meet at every barrier.
 
     synw (decode syndromes, slot-map gather): the groups' rows are the
