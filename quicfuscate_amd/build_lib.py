@@ -43,13 +43,13 @@ BS_FFT = [(64, 16), (64, 10), (32, 16), (16, 16)]
 # additive-FFT encode passes of the C5 codes with more than 22 repairs
 # (lch_fft.hybrid_plan: one pass per coset of 16 repair points, sources
 # [0, 2^a) through the FFT, the rest folded in directly), merged ('N')
-BS_FFT_PASSES = [(128, 39), (160, 48), (196, 59)]
+BS_FFT_PASSES = [(128, 20), (128, 39), (160, 48), (196, 59)]
 # pass-major FFT synw ('Y') where its passes that run at 20 % loss cost less
 # than the plain ones (tools/gpu_r04_c5y.sh, profiles/r04al_c5_hybrid_chunks.json:
 # block decode (128, 39) 1,470 -> 1,784 GiB/s, (160, 48) 1,536 -> 1,700;
 # (196, 59) 1,383 -> 1,262: three FFT passes run against two plain ones)
 BS_FFT_SYNW = [(128, 39), (160, 48)]
-BS_FFT_SYNW_SHARED = [(128, 39), (160, 48), (196, 59)]
+BS_FFT_SYNW_SHARED = [(128, 20), (128, 39), (160, 48), (196, 59)]
 BS_XCHG_EARLY = 3     # rows of the next group a shared-row wave loads before its transform
 BS_FFT_DEC_HYBRID = [(96, 15), (48, 8)]   # fused FFT decode ('C') of C5 shapes with k not a power of two
 BS_FFT_CH = 8
@@ -242,11 +242,16 @@ def kernel_specs() -> list:
     # (each wave issues the loads of its next group's first 3 rows before
     # transforming the current group, xchg_early: 0.315-0.329 -> 0.305-0.316 ms
     # at (196, 59), tools/c5_lab.py, profiles/r05au_c5_xchg_early.json)
+    # ((128, 20), two coset passes of 16 + 4: shared-row FFT passes 0.231-0.235
+    # ms against 0.241-0.250 for its single plain pass on the same box; with
+    # two producer-only waves 0.272-0.278, so none; tools/c5_lab.py,
+    # profiles/r05bg_c5_128_20.json)
     for k, rt in BS_FFT_PASSES:
         cps = lch_fft.coset_passes(k, rt)
+        three = len(cps) >= 3
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", r_total=rt, j0=j0,
-                                                   xchg_early=BS_XCHG_EARLY)
-                                     for j0, rp in cps], xchg=True, helpers=max(0, 4 - len(cps))))
+                                                   xchg_early=BS_XCHG_EARLY if three else 0)
+                                     for j0, rp in cps], xchg=True, helpers=1 if len(cps) == 3 else 0))
     # the synw passes of the C5 codes in one pass-major dispatch: one launch
     # of P x n workgroups instead of P launches of n, so a pass's last, partly
     # filled round overlaps the next pass's first; 'Y' the additive-FFT passes
@@ -261,9 +266,10 @@ def kernel_specs() -> list:
     # (a producer-only 4th wave, as the encode's, measured no faster here: (160, 48) block
     # decode 2,007-2,019 against 2,025-2,031 GiB/s, profiles/r05af_c5_helper_decode.json)
     for k, rt in BS_FFT_SYNW_SHARED:
+        cps = lch_fft.coset_passes(k, rt)
         specs.append(bs.merged_spec([bs.KernelSpec(k, rp, BS_PD, "synw", fft=BS_FFT_CH, ld_policy="", r_total=rt,
-                                                   j0=j0, xchg_early=BS_XCHG_EARLY)
-                                     for j0, rp in lch_fft.coset_passes(k, rt)], xchg=True))
+                                                   j0=j0, xchg_early=BS_XCHG_EARLY if len(cps) >= 3 else 0)
+                                     for j0, rp in cps], xchg=True))
     for k, rt in BS_ENC_ONLY:
         npass = -(-rt // BS_PASS)
         if npass == 1:

@@ -754,7 +754,8 @@ def test_emulated_synw_fft(oracle, k, rt, L, G, offs):
 @pytest.mark.parametrize("early", [0, 5])
 @pytest.mark.parametrize("k,rt,L,G,offs,helpers", [(24, 10, 2048, 3, False, 0), (20, 20, 2100, 4, True, 0),
                                                    (48, 21, 2064, 3, False, 0), (196, 59, 2048, 2, False, 0),
-                                                   (48, 21, 2064, 3, True, 1), (20, 20, 2100, 4, False, 2)])
+                                                   (48, 21, 2064, 3, True, 1), (20, 20, 2100, 4, False, 2),
+                                                   (128, 20, 2048, 2, False, 0)])
 def test_emulated_synw_xchg(oracle, k, rt, L, G, offs, helpers, early):
     """Item-major merged FFT synw whose waves share the source rows' gather,
     transposes and chunk butterflies through LDS (merged_spec(xchg=True)):
@@ -1215,7 +1216,8 @@ def test_emulated_fft_encode_hybrid_passes(oracle, k, rt, L, G):
 @pytest.mark.parametrize("k,rt,L,G,blocks,helpers", [(24, 10, 200, 3, 0, 0), (48, 21, 2100, 2, 3, 0),
                                                     (20, 20, 72, 2, 0, 0), (196, 59, 40, 1, 0, 0),
                                                     (160, 48, 40, 1, 0, 0), (128, 39, 100, 2, 1, 0),
-                                                    (160, 48, 40, 1, 0, 1), (20, 20, 72, 2, 1, 2)])
+                                                    (160, 48, 40, 1, 0, 1), (20, 20, 72, 2, 1, 2),
+                                                    (128, 20, 40, 1, 0, 0)])
 def test_emulated_merged_passes_xchg(oracle, k, rt, L, G, blocks, helpers, early):
     """The merged additive-FFT encode whose waves share the row work through
     LDS (merged_spec(xchg=True), _generate_enc_xchg): wave w produces groups

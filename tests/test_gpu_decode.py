@@ -568,7 +568,7 @@ def test_decode_combine_wide(qf, oracle, gpu_ctx, k, r, L, G, erase, path, wide,
 
 @pytest.mark.parametrize("shared", [1, 0])
 @pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 6, None), (196, 59, 9000, 6, 3), (160, 48, 4100, 9, 40),
-                                           (128, 39, 2100, 12, None)])
+                                           (128, 39, 2100, 12, None), (128, 20, 9000, 6, None), (128, 20, 2100, 9, 20)])
 def test_decode_c5_synw_shared(qf, oracle, gpu_ctx, k, r, L, G, erase, shared, monkeypatch):
     """Long-row C5 decode with the FFT syndrome passes item-major, their waves
     sharing the row gather through LDS ('Z', QF_OPT_SYNW_SHARED = 1), and

@@ -24,6 +24,18 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5bf: (128, 20) -- the library's single plain pass against the
+    # additive-FFT coset passes sharing their row work (xchg, with helpers)
+    # (the plain pass is not a merged kernel: its time is the bench's block
+    # encode, 0.238-0.242 ms at this size, profiles/r05bc_bench_detail.json)
+    ("q128_warm", 128, 20, "N", 0, {"xchg": True}),
+    ("q128_x", 128, 20, "N", 0, {"xchg": True}),
+    ("q128_xh2", 128, 20, "N", 0, {"xchg": True, "helpers": 2, "xchg_early": 3}),
+    ("q128_xh2e0", 128, 20, "N", 0, {"xchg": True, "helpers": 2}),
+    ("q128_x_2", 128, 20, "N", 0, {"xchg": True}),
+    ("q128_xh2_2", 128, 20, "N", 0, {"xchg": True, "helpers": 2, "xchg_early": 3}),
+]
+VARIANTS_R05AU = [
     # round 5au: each wave issues the loads of its next group's first rows
     # before transforming the current group (KernelSpec.xchg_early rotating slots)
     ("e196_warm", 196, 59, "N", 0, {"xchg": True}),
