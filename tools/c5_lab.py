@@ -24,6 +24,21 @@ L_JUMBO, RS, DRS = 9000, 9008, 9088
 
 # (name, k, rt, kind, npass (M), KernelSpec keyword overrides)
 VARIANTS = [
+    # round 5bi: single-pass C5 codes -- the library's plain pass ("S") against
+    # the hybrid additive-FFT pass (fft=8: sources past 2^a folded in directly)
+    ("s96_warm", 96, 15, "S", 0, {}),
+    ("s96_plain", 96, 15, "S", 0, {}),
+    ("s96_fft", 96, 15, "S", 0, {"fft": 8, "ld_policy": ""}),
+    ("s48_plain", 48, 8, "S", 0, {}),
+    ("s48_fft", 48, 8, "S", 0, {"fft": 8, "ld_policy": ""}),
+    ("s32_plain", 32, 5, "S", 0, {}),
+    ("s32_fft", 32, 5, "S", 0, {"fft": 8, "ld_policy": ""}),
+    ("s96_plain_2", 96, 15, "S", 0, {}),
+    ("s96_fft_2", 96, 15, "S", 0, {"fft": 8, "ld_policy": ""}),
+    ("s48_plain_2", 48, 8, "S", 0, {}),
+    ("s48_fft_2", 48, 8, "S", 0, {"fft": 8, "ld_policy": ""}),
+]
+VARIANTS_R05BF = [
     # round 5bf: (128, 20) -- the library's single plain pass against the
     # additive-FFT coset passes sharing their row work (xchg, with helpers)
     # (the plain pass is not a merged kernel: its time is the bench's block
@@ -147,6 +162,8 @@ def make_spec(bs, k, rt, kind, npass, kw):
 
     pd = kw.get("pd", 3)
     extra = {x: v for x, v in kw.items() if x not in ("pd", "flags", "xchg", "helpers")}
+    if kind == "S":   # one plain / hybrid-FFT pass (4 one-item waves per workgroup, as the library)
+        return bs.KernelSpec(k, rt, pd, "enc", **extra)
     if kind == "N":
         R = extra.get("fft_coset", 16)
         passes = [bs.KernelSpec(k, rp, pd, "enc", fft=8, ld_policy="", r_total=rt, j0=j0, **extra)
@@ -199,9 +216,9 @@ def build():
         ms = make_spec(bs, k, rt, kind, npass, kw)
         text = bs.emit_asm(ms, variant_ops(bs, ms, set(kw.get("flags", ()))))
         h = assemble(f"c5_{name}", text.replace(ms.name, f"c5_{name}"), OUT)
-        manifest.append({"name": name, "k": k, "rt": rt, "kind": kind, "npass": npass, "kw": kw, "waves": ms.waves,
+        manifest.append({"name": name, "k": k, "rt": rt, "kind": kind, "npass": npass, "kw": kw, "waves": getattr(ms, "waves", 4),
                          "hsaco": h.name, "symbol": f"c5_{name}", "vgprs": ms.next_free_vgpr, "lds": ms.lds_bytes})
-        print(name, ms.waves, ms.next_free_vgpr, ms.lds_bytes, h.stat().st_size, flush=True)
+        print(name, getattr(ms, "waves", 4), ms.next_free_vgpr, ms.lds_bytes, h.stat().st_size, flush=True)
     (OUT / "c5_manifest.json").write_text(json.dumps(manifest, indent=1))
 
 
@@ -236,7 +253,11 @@ def run(nbytes: float, reps: int):
         Lv = bs.padded_units(L_JUMBO)
         _, _, n_items = bs.launch_geometry(L_JUMBO, G, Lv)
         blocks = n_items
-        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * RS, rt * DRS, RS, DRS, L_JUMBO, G, blocks, Lv=Lv,
+        stride = blocks
+        if m["kind"] == "S":   # one item per wave, 4-wave workgroups, item stride in waves
+            blocks = (n_items + 3) // 4
+            stride = 4 * blocks
+        ka = bs.kernargs(src.data_ptr(), dst.data_ptr(), k * RS, rt * DRS, RS, DRS, L_JUMBO, G, stride, Lv=Lv,
                          zero_tail=True)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
