@@ -52,6 +52,7 @@ BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_SYNW_SHARED = [(128, 20), (128, 39), (160, 48), (196, 59)]
 BS_XCHG_EARLY = 3     # rows of the next group a shared-row wave loads before its transform
 BS_FFT_DEC_HYBRID = [(96, 15), (48, 8)]   # fused FFT decode ('C') of C5 shapes with k not a power of two
+BS_FFT_ENC_HYBRID = [(96, 15)]   # hybrid-plan FFT encode ('E'): sliding windows +35 %, block equal
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
 BS_PD = 3
@@ -200,6 +201,13 @@ def kernel_specs() -> list:
     # coset of 16: 19.5 k -> 16.2 k VALU per item at (96, 15), but block encode
     # 4,703 -> 4,450 / 5,024 -> 4,841 GiB/s against sliding 758 -> 831 /
     # 1,232 -> 1,325; not in the library, profiles/r04an_c5_single_hybrid.json)
+    # (round 5, natural coset fill: 12.6 k VALU per item at (96, 15), and the
+    # block encode no slower, profiles/r05bi_c5_single_pass_fft.json; in the
+    # library block 4,807-4,844 against 4,799-4,819 GiB/s, sliding windows, whose
+    # overlapping rows come from cache, 1,023-1,033 against 754-764; (48, 8):
+    # block 4,862-4,868 against 4,994-5,007, sliding 1,273 against 1,179-1,223,
+    # a wash, so it stays plain; profiles/r05bk_c5_hybrid_encode.json)
+    specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="") for (k, r) in BS_FFT_ENC_HYBRID]
     # additive-FFT fused decode ('C'): pd 2 (the ring holds a chunk + pd rows)
     # (default cache policy: neighbouring 1,200-B rows share their boundary
     # lines, and non-temporal loads / stores drop them before the reuse;
