@@ -453,6 +453,133 @@ int cpu_encode_clmul_dispatch(uint32_t k, uint32_t r, uint32_t L, uint32_t G, co
     return run(k, r, L, G, src, rep, threads, 4);
 }
 
+/* ---- decode on host threads (bench.py cpu_baseline) --------
+ * The reference decodes one generation per Decoder (decoder.rs:658-791) and
+ * fans its row operations out on rayon (decoder.rs:410-433, 479-489); here
+ * the host cores each take whole generations (one generation per pinned
+ * thread at a time), which is at least as parallel.
+ *   kind 0 "table"     oracle_decode_generation: decoder.rs:720-783 with table
+ *                      gf_mul (gf_tables.rs:47-57), F4 fixed -- its output is
+ *                      compared with the GPU's recovered rows
+ *   kind 4 "dispatch"  the same elimination with every product through the
+ *                      reference's gf_mul -> dispatch_bitslice (optimize.rs:
+ *                      385-408) -> CLMUL fold: the as-written per-byte cost,
+ *                      timing only (the fold is not a field product)
+ * rows: G generations of n_rows received rows (arrival order, row_index
+ * G x n_rows), L bytes each, dense; out: G x k x L (every source row). */
+typedef struct {
+    uint32_t k, L, n_rows, g0, g1;
+    const uint16_t *row_index;
+    const uint8_t *rows;
+    uint8_t *out;
+    int kind;
+    int status;
+} dec_job_t;
+
+#if defined(__x86_64__)
+/* decoder.rs:720-783 (pivot search, swap, scale_row, add_scaled_row on every
+ * other row, early exit at rank k) over dense rows, products dispatched */
+static int decode_dispatch_gen(uint32_t k, uint32_t L, uint32_t n_rows, const uint16_t *ri, const uint8_t *rows,
+                               uint8_t *out) {
+    uint8_t *m = (uint8_t *)calloc((size_t)k, (size_t)k + L);
+    uint8_t **row = (uint8_t **)malloc(sizeof(uint8_t *) * k);
+    uint8_t present[256] = {0};
+    if (!m || !row) { free(m); free(row); return -1; }
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < n_rows && n < k; ++s) {
+        const uint32_t idx = ri[s];
+        uint8_t *c = m + (size_t)n * (k + L);
+        if (idx < k) {
+            if (present[idx]) continue;
+            present[idx] = 1;
+            c[idx] = 1;
+        } else {
+            const uint8_t y = (uint8_t)idx;
+            for (uint32_t i = 0; i < k; ++i) oracle_gf_inv((uint8_t)((uint8_t)i ^ y), &c[i]);
+        }
+        memcpy(c + k, rows + (size_t)s * L, L);
+        row[n++] = c;
+    }
+    int st = n < k ? -2 : 0;
+    for (uint32_t i = 0; i < k && !st; ++i) {
+        uint32_t p = k;
+        for (uint32_t r = i; r < k; ++r)
+            if (row[r][i]) { p = r; break; }
+        if (p == k) { st = -3; break; }
+        uint8_t *t = row[i]; row[i] = row[p]; row[p] = t;
+        uint8_t inv;
+        oracle_gf_inv(row[i][i], &inv);
+        for (uint32_t c = 0; c < k + L; ++c) row[i][c] = gf_mul_dispatched(row[i][c], inv);
+        for (uint32_t r = 0; r < k; ++r) {
+            const uint8_t f = row[r][i];
+            if (r == i || f == 0) continue;
+            for (uint32_t c = 0; c < k + L; ++c) row[r][c] ^= gf_mul_dispatched(f, row[i][c]);
+        }
+    }
+    for (uint32_t i = 0; i < k && !st; ++i) memcpy(out + (size_t)i * L, row[i] + k, L);
+    free(m);
+    free(row);
+    return st;
+}
+#endif
+
+static void *dec_worker(void *arg) {
+    dec_job_t *j = (dec_job_t *)arg;
+    for (uint32_t g = j->g0; g < j->g1; ++g) {
+        const uint16_t *ri = j->row_index + (size_t)g * j->n_rows;
+        const uint8_t *rows = j->rows + (size_t)g * j->n_rows * j->L;
+        uint8_t *out = j->out + (size_t)g * j->k * j->L;
+        int st = -1;
+#if defined(__x86_64__)
+        if (j->kind == 4) st = decode_dispatch_gen(j->k, j->L, j->n_rows, ri, rows, out);
+#endif
+        if (j->kind == 0)
+            st = oracle_decode_generation(j->k, j->L, j->n_rows, ri, rows, j->L, NULL, out, j->L, NULL);
+        if (st != 0 && j->status == 0) j->status = st;
+    }
+    return NULL;
+}
+
+int cpu_decode(int kind, uint32_t k, uint32_t L, uint32_t G, uint32_t n_rows, const uint16_t *row_index,
+               const uint8_t *rows, uint8_t *out, uint32_t threads) {
+    if (k == 0 || k > 256 || threads == 0 || (kind != 0 && kind != 4)) return -1;
+    if (kind == 4 && !cpu_has_pclmul()) return -3;
+#if defined(__x86_64__)
+    if (kind == 4) (void)detector_instance();
+#endif
+    if (threads > G) threads = G ? G : 1;
+    pthread_t *th = (pthread_t *)calloc(threads, sizeof(pthread_t));
+    dec_job_t *jobs = (dec_job_t *)calloc(threads, sizeof(dec_job_t));
+    if (!th || !jobs) { free(th); free(jobs); return -1; }
+    cpu_set_t allowed;
+    int ncpu = 0, cpus[1024];
+    if (g_pin && sched_getaffinity(0, sizeof allowed, &allowed) == 0)
+        for (int c = 0; c < CPU_SETSIZE && ncpu < 1024; ++c)
+            if (CPU_ISSET(c, &allowed)) cpus[ncpu++] = c;
+    for (uint32_t w = 0; w < threads; ++w) {
+        jobs[w] = (dec_job_t){k, L, n_rows, (uint32_t)((uint64_t)G * w / threads),
+                              (uint32_t)((uint64_t)G * (w + 1) / threads), row_index, rows, out, kind, 0};
+        pthread_attr_t at;
+        pthread_attr_init(&at);
+        if (ncpu) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus[w % (uint32_t)ncpu], &one);
+            pthread_attr_setaffinity_np(&at, sizeof one, &one);
+        }
+        pthread_create(&th[w], &at, dec_worker, &jobs[w]);
+        pthread_attr_destroy(&at);
+    }
+    int st = 0;
+    for (uint32_t w = 0; w < threads; ++w) {
+        pthread_join(th[w], NULL);
+        if (jobs[w].status && !st) st = jobs[w].status;
+    }
+    free(th);
+    free(jobs);
+    return st;
+}
+
 /* benches/gf_bitslice_bench.rs:17-102 restated (the
  * only published numbers of the path): a[i] = i, b[i] = 255 - i for i < 1024
  * (as u8), acc ^= mul(a[i], b[i]), `iters` passes; every operand goes

@@ -229,6 +229,21 @@ _ASM = {
     "store_byte_saddr": lambda voff, d, sb, off: f"global_store_byte {V(voff)}, {V(d)}, {SP(sb)}"
                         + (f" offset:{off}" if off else ""),
     "store_byte": lambda a, d, off: f"global_store_byte {VP(a)}, {V(d)}, off" + (f" offset:{off}" if off else ""),
+    # lab (lab_stamps): the real-time counter (100 MHz, chip-wide) into s[80 + 2p : 81 + 2p]
+    "stamp": lambda p: f"s_memrealtime s[{STAMP_S0 + 2 * p}:{STAMP_S0 + 2 * p + 1}]",
+    # lab (lab_stamps): the item's stores drained, stamp 7, then lane 0 writes
+    # the 8 stamps and the wave's HW_ID / XCC_ID to stamps[item] (128 B each;
+    # kernarg bytes 128..135) with vector stores; v14..v17 are dead there
+    "stamp_flush": lambda: "\n\t".join(
+        ["s_waitcnt vmcnt(0)", f"s_memrealtime s[{STAMP_S0 + 14}:{STAMP_S0 + 15}]",
+         f"s_load_dwordx2 s[{STAMP_S0 + 16}:{STAMP_S0 + 17}], s[0:1], 0x{KERNARG_BYTES_DEC:x}",
+         f"s_getreg_b32 s{STAMP_S0 + 18}, hwreg(HW_REG_HW_ID)",
+         f"s_getreg_b32 s{STAMP_S0 + 19}, hwreg(HW_REG_XCC_ID)",
+         "s_waitcnt lgkmcnt(0)", "s_lshl_b32 s66, s28, 7", "v_mov_b32_e32 v16, s66", "s_mov_b64 exec, 1"]
+        + [f"v_mov_b32_e32 v14, s{STAMP_S0 + q}\n\tv_mov_b32_e32 v15, s{STAMP_S0 + q + 1}\n\t"
+           f"global_store_dwordx2 v16, v[14:15], s[{STAMP_S0 + 16}:{STAMP_S0 + 17}] offset:{4 * q}"
+           for q in (0, 2, 4, 6, 8, 10, 12, 14, 18)]
+        + ["s_mov_b64 exec, -1"]),
     # lab: a cache-warming load (the destination is a dummy register)
     "load4": lambda d, a, off: f"global_load_dword {V(d)}, {VP(a)}, off" + (f" offset:{off}" if off else ""),
 }
@@ -333,6 +348,7 @@ SW_Q0, SW_Q1 = 84, 88                         # the current map quad of g0 / g1 
 SW_BASE0, SW_BASE1 = 92, 94                   # this row's address in g0 / g1
 SW_T0, SW_T1 = 96, 97                         # slot bytes / temps
 SW_NEXT_FREE = 98
+STAMP_S0 = 80    # lab_stamps: s80..s95 stamps, s[96:97] buffer, s98 / s99 HW_ID / XCC_ID
 S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
@@ -431,6 +447,11 @@ class KernelSpec:
     # load per half and row into a dummy register), so that its row loop finds
     # them in L2 / the Infinity Cache while HBM would otherwise idle
     lab_prefetch: tuple = ()
+    # lab only (chunked fft dec): per-item phase timestamps (s_memrealtime)
+    # written to a buffer named by kernarg bytes 128..135 (tools/dec_lab.py
+    # --stamps): entry, item start, map read, source rows done, repairs done,
+    # forward LU done, backward LU + stores issued, stores drained
+    lab_stamps: bool = False
     # enc mode, one pass of a code with more repairs than a kernel holds:
     # repairs j0 .. j0 + r - 1 of the Cauchy matrix of (k, r_total)
     r_total: int = 0
@@ -630,6 +651,8 @@ class KernelSpec:
             return CMB_NEXT_FREE_SGPR
         if self.mode == "synw":
             return SW_NEXT_FREE
+        if self.mode == "dec" and self.lab_stamps:
+            return STAMP_S0 + 20
         if self.mode == "dec":
             # chunked: s[76:77] = {16 Q, 0}, s[78:79] the partial-last-unit lane
             return SGPR_NEXT_FREE_DEC + (4 if self.chunked else 0) + (2 if self.lds_rows else 0)
@@ -648,6 +671,8 @@ class KernelSpec:
             return KERNARG_BYTES_CMB + (8 if self.pass_major or self.r > 16 else 0)
         if self.mode == "synw":
             return KERNARG_BYTES_SYNW
+        if self.mode == "dec" and self.lab_stamps:
+            return KERNARG_BYTES_DEC + 16
         return KERNARG_BYTES_DEC if self.mode == "dec" else KERNARG_BYTES
 
     @property
@@ -2276,6 +2301,8 @@ def _prologue_chunked(E, spec: KernelSpec):
     """Prologue of the chunked dec kernel: lane-chunk f = 64 item + lane,
     g = f / Q, q = f % Q; A unit q, B unit q + Q (loaded iff q + Q < Lu).
     kernarg s12 = Lu, s13 = Q, s14 = G * Q, s15 / s16 = magic / shift of Q."""
+    if spec.lab_stamps:
+        E(Op("stamp", (0,)))
     E(Op("s_load_args", ()))
     E(Op("v_lshr", (V_T, 6, V_LANE)))
     E(Op("v_andk", (V_LANE, 63, V_LANE)))
@@ -2352,6 +2379,8 @@ def _prologue_chunked(E, spec: KernelSpec):
     E(Op("s_cmp_lt_br", (28, 17, ".Lgo")))
     E(Op("s_far_jump", (".Lend", 0)))
     E(Op("label", (".Lgo",)))
+    if spec.lab_stamps:
+        E(Op("stamp", (1,)))
     if spec.wave_gen:
         # f = Q item + (lane < Q ? lane : 0): lanes past Q alias lane 0 and store nothing
         E(Op("v_cmp_gt_s", (26, 13, V_LANE)))
@@ -2459,6 +2488,8 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
     E(Op("s_movk", (S_JMAX, 0)))
     E(Op("label", (".Ljdone",)))
     win["phase"] = 1
+    if spec.lab_stamps:
+        E(Op("stamp", (2,)))
     if spec.wave_gen:   # any source row may be skipped, so no row initialises
         for a in range(acc0, acc0 + 8 * r):
             E(Op("v_movk", (a, 0)))
@@ -2529,6 +2560,8 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         if spec.prio != (0, 0):
             E(Op("s_setprio", (spec.prio[0],)))
         _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
+        if spec.lab_stamps:
+            E(Op("stamp", (3,)))
         # the accepted repairs, in byte form, onto their syndrome blocks
         for n in range(k, n_all):
             if n + ahead < n_all:
@@ -2544,7 +2577,12 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
             E(Op("label", (f".Lrep{j}",)))
         if spec.prio != (0, 0):
             E(Op("s_setprio", (spec.prio[1],)))
+        if spec.lab_stamps:
+            E(Op("stamp", (4,)))
         _lu_solve_and_store_chunked(E, spec)
+        if spec.lab_stamps:
+            E(Op("stamp", (6,)))
+            E(Op("stamp_flush", ()))
         _epilogue_next_item(E, far=True)
         return ops
     for n in range(min(pd, n_seq)):
@@ -2854,6 +2892,8 @@ def _lu_solve_and_store_chunked(E, spec: KernelSpec):
             selectors(u)
             column(u, [("scale", u)] + [("acc", t) for t in range(u + 1, r)], f".Lfwd{u}", 1)
         E(Op("label", (".Lfwd_end",)))
+        if spec.lab_stamps:
+            E(Op("stamp", (5,)))
         E(Op("s_waitcnt_vm", (0,)))
         pf_rows = []
         if spec.lab_prefetch:
@@ -3637,7 +3677,7 @@ class Emulator:
                 raise EmuError(f"{n} while the gpr_idx mode is on")
             if n == "s_waitcnt_lgkm" or (n == "s_waitcnt_lgkm_n" and a[0] == 0):
                 retire_s()
-            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger"):
+            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger", "stamp", "stamp_flush"):
                 continue
             if n == "s_load_args":
                 for q in range(20):

@@ -18,6 +18,7 @@ import re
 import shutil
 import subprocess
 import sys
+import zlib
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -59,9 +60,16 @@ BS_PD = 3
 # gfx950 (CDNA4) only: the generated kernels are gfx950 assembly, and the
 # HIP kernels assume its 160 KB of LDS per CU (k_decode_prepare_lu_lanes
 # stages 72 KB statically, above the 64 KiB of gfx942 / gfx90a)
-ARCH = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
-if ARCH != "gfx950":
-    raise RuntimeError(f"QF_OFFLOAD_ARCH={ARCH}: this library targets gfx950 (MI355X) only")
+ARCH = "gfx950"
+
+
+def _check_arch() -> None:
+    """QF_OFFLOAD_ARCH may only name gfx950: checked where code is compiled or
+    assembled, so importing this module (kernel_specs() in the CPU emulator
+    tests) works whatever another project set that variable to."""
+    arch = os.environ.get("QF_OFFLOAD_ARCH", "gfx950")
+    if arch != "gfx950":
+        raise RuntimeError(f"QF_OFFLOAD_ARCH={arch}: this library targets gfx950 (MI355X) only")
 
 
 def _hipcc() -> str:
@@ -99,6 +107,7 @@ def _rocm_hip_runtime() -> Path:
 
 
 def _compile(src: str, build_dir: Path, extra: list[str]) -> tuple[Path, str]:
+    _check_arch()
     obj = build_dir / (Path(src).stem + ".o")
     cmd = [
         _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
@@ -145,6 +154,7 @@ def _check_gf16_bs(remarks: str) -> None:
 
 def assemble(name: str, asm_text: str, out_dir: Path) -> Path:
     """gfx950 assembly text -> code object (.hsaco) via clang + ld.lld."""
+    _check_arch()
     clang = _clangxx().replace("clang++", "clang")
     lld = str(Path(clang).parent / "ld.lld")
     asm = out_dir / f"{name}.s"
@@ -324,7 +334,11 @@ def _bs_kernels(build_dir: Path) -> Path:
         hsaco = assemble(spec.name, bs.emit_asm(spec, bs.generate(spec)), build_dir)
         data = hsaco.read_bytes()
         hashes[spec.name] = hashlib.sha256(data).hexdigest()[:16]
-        hexs = ",".join(str(b) for b in data)
+        # zlib-compressed (about 3x smaller; qf_bs.hip inflates a code object
+        # once, on its first load): the library is pushed to the GPU box on
+        # every call, and these objects are most of its bytes
+        z = zlib.compress(data, 9)
+        hexs = ",".join(str(b) for b in z)
         blobs.append(f"static const unsigned char qf_bs_blob_{n}[] = {{{hexs}}};")
         if isinstance(spec, bs.MergedSpec):
             if spec.mode == "synw":
@@ -340,8 +354,8 @@ def _bs_kernels(build_dir: Path) -> Path:
         else:
             mode = {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "P" if spec.pass_major else "m"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
-                       f"qf_bs_blob_{n}, sizeof(qf_bs_blob_{n}), {getattr(spec, 'waves', 4)}u, "
-                       f"{getattr(spec, 'n_passes', 1)}u}},")
+                       f"qf_bs_blob_{n}, {len(data)}u, {getattr(spec, 'waves', 4)}u, "
+                       f"{getattr(spec, 'n_passes', 1)}u, sizeof(qf_bs_blob_{n})}},")
     # the loader caches one module per table entry (qf_bs.h BsCache::kMax)
     kmax = int(re.search(r"kMax = (\d+)", (CSRC / "qf_bs.h").read_text()).group(1))
     if len(specs) > kmax:
@@ -391,7 +405,7 @@ def build(verbose: bool = False) -> Path:
     for lib, hip in ((LIB, _torch_hip_runtime()), (LIB_ROCM, _rocm_hip_runtime())):
         tmp = lib.with_suffix(".so.tmp")
         cmd = [_clangxx(), "-shared", "-o", str(tmp)] + [str(o) for o in objs] + [
-            str(hip), f"-Wl,-rpath,{hip.parent}", "-Wl,--no-undefined", "-lstdc++",
+            str(hip), f"-Wl,-rpath,{hip.parent}", "-Wl,--no-undefined", "-lstdc++", "-lz",
         ]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:

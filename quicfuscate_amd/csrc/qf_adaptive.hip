@@ -611,13 +611,13 @@ int qf_adaptive_on_send_batch(qf_adaptive* const* conns, uint32_t M, const uint6
                                         out_stride, out_coeffs ? out_coeffs + (size_t)p0 * coeff_stride : nullptr,
                                         coeff_stride, out_desc + p0, out_cap - p0, &n);
             if (s < 0 && s != QF_ERANGE) return s;
-            if (n != predicted[0] + 1) return QF_EDEVICE;  // internal inconsistency
+            if (n != predicted[0] + 1) return qf::device_fail(__FILE__, __LINE__, hipErrorIllegalState);  // internal inconsistency
             if (statuses) statuses[mm] = s;
         } else if (!batch.empty()) {
             int s = qf::encoders_send_batch(ctx, batch.data(), (uint32_t)batch.size());
             if (s != QF_OK) return s;
             for (size_t b = 0; b < batch.size(); ++b) {
-                if (batch[b].n_rep != predicted[b]) return QF_EDEVICE;  // internal inconsistency
+                if (batch[b].n_rep != predicted[b]) return qf::device_fail(__FILE__, __LINE__, hipErrorIllegalState);  // internal inconsistency
                 finish_send(conns[batch_m[b]]);
             }
         }

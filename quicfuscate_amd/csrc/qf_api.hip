@@ -41,8 +41,13 @@ thread_local char t_refused[96];
 int device_fail(const char* file, int line, hipError_t e) {
     const char* base = strrchr(file, '/');
     base = base ? base + 1 : file;
+    // a refused generated-kernel launch returns hipErrorInvalidValue: only
+    // then is the refusal noted by note_launch_refused the cause (a refusal a
+    // caller recovered from, e.g. by another kernel, is never attached to a
+    // later, unrelated failure)
+    const bool refused = e == hipErrorInvalidValue && t_refused[0];
     snprintf(t_last_error, sizeof t_last_error, "%s:%d: %s%s%s%s", base, line, hipGetErrorName(e),
-             t_refused[0] ? " (" : "", t_refused, t_refused[0] ? ")" : "");
+             refused ? " (" : "", refused ? t_refused : "", refused ? ")" : "");
     t_refused[0] = 0;
     return QF_EDEVICE;
 }
@@ -1420,7 +1425,7 @@ int qf_decode_batch(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const ui
         if (!ctx->ev_accept) e = hipEventCreateWithFlags(&ctx->ev_accept, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventRecord(ctx->ev_accept, ctx->stream);
         if (e == hipSuccess) e = hipStreamWaitEvent(ctx->payload_stream, ctx->ev_accept, 0);
-        if (e != hipSuccess && s == QF_OK) s = QF_EDEVICE;
+        if (e != hipSuccess && s == QF_OK) s = qf::device_fail(__FILE__, __LINE__, e);
     }
     ctx->payload_wait = nullptr;  // one decode call only, whatever its outcome
     ctx->has_payload_stream = ctx->payload_on_stream = false;

@@ -11,6 +11,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <zlib.h>
+
+#include <mutex>
 
 #include "qf_bs.h"
 #include "qf_fec.h"
@@ -27,14 +30,47 @@ struct QfBsEntry {
                 // 'Z' the additive-FFT 'w' passes item-major, one wave per pass, row work shared in LDS
     uint32_t map_stride;
     const char* name;
-    const unsigned char* data;
-    size_t size;
+    const unsigned char* data;  // the code object, zlib-compressed (build_lib.py)
+    size_t size;                // its size inflated
     uint32_t waves;  // waves per workgroup ('M' / 'N': one per pass, each on the workgroup's item)
     uint32_t passes; // 'X': passes laid out pass-major over the grid (workgroup ranges of equal size)
+    size_t zsize;    // bytes at data
 };
 #include "qf_bs_blobs.inc"
 
 namespace qf {
+
+// The inflated code object of a table entry: inflated once per process and
+// kept (contexts on several devices load the same image).
+static const void* blob_image(const QfBsEntry* e) {
+    static std::mutex mu;
+    static unsigned char* images[sizeof(qf_bs_table) / sizeof(qf_bs_table[0])] = {};
+    const size_t idx = (size_t)(e - qf_bs_table);
+    std::lock_guard<std::mutex> g(mu);
+    if (!images[idx]) {
+        unsigned char* buf = static_cast<unsigned char*>(malloc(e->size));
+        uLongf n = (uLongf)e->size;
+        if (!buf) return nullptr;
+        if (uncompress(buf, &n, e->data, (uLong)e->zsize) != Z_OK || n != e->size) {
+            free(buf);
+            return nullptr;
+        }
+        images[idx] = buf;
+    }
+    return images[idx];
+}
+
+static hipError_t load_module(BsCache& cache, int idx, const QfBsEntry* e) {
+    const void* image = blob_image(e);
+    if (!image) {
+        note_launch_refused("qf_bs.hip code object inflate", __LINE__);
+        return hipErrorInvalidImage;
+    }
+    hipError_t err = hipModuleLoadData(&cache.mod[idx], image);
+    if (err == hipSuccess) err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
+    if (err != hipSuccess && getenv("QF_BS_DEBUG")) fprintf(stderr, "%s: module load %d\n", e->name, (int)err);
+    return err;
+}
 
 // QF_BS_DEBUG=1: name the check behind a hipErrorInvalidValue on stderr
 // (qf_last_error carries the refusal's line whether or not it is set)
@@ -107,12 +143,8 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
         srs >= (1ull << 32) || drs >= (1ull << 32))
         return bs_invalid(__LINE__);
     if (!cache.fn[idx]) {
-        hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
-        if (err == hipSuccess) err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
-        if (err != hipSuccess) {
-            if (getenv("QF_BS_DEBUG")) fprintf(stderr, "%s: module load %d\n", e->name, (int)err);
-            return err;
-        }
+        hipError_t err = load_module(cache, idx, e);
+        if (err != hipSuccess) return err;
     }
     const uint32_t Lu = (L + 15) / 16;
     // lane-chunk layout of the chunked fused decode ('c'): lane-chunk = units
@@ -277,6 +309,9 @@ hipError_t synw_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, 
                       : merged && find('X', k, r) ? 'X' : 'w';
     for (const auto& e : qf_bs_table) {
         if (e.mode != mode || e.k != k || e.rt != r) continue;
+        // every pass of the chosen mode reads the slot map at the caller's
+        // stride (checked per entry: 'X' / 'Y' / 'Z' are separate specs)
+        if (e.map_stride != map_stride) return bs_invalid(__LINE__);
         hipError_t err = launch(cache, &e, num_cus, st, rows, syn + (uint64_t)e.j0 * srs, rgs, sgs, rs, srs, L, G, Lv,
                                 map_stride, smap, zero, nullptr, 0, nullptr, rows_offs, nullptr, bound);
         if (err != hipSuccess) return err;
@@ -366,9 +401,7 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     const int idx = (int)(e - qf_bs_table);
     if (idx >= BsCache::kMax) return bs_invalid(__LINE__);
     if (!cache.fn[idx]) {
-        hipError_t err = hipModuleLoadData(&cache.mod[idx], e->data);
-        if (err != hipSuccess) return err;
-        err = hipModuleGetFunction(&cache.fn[idx], cache.mod[idx], e->name);
+        hipError_t err = load_module(cache, idx, e);
         if (err != hipSuccess) return err;
     }
     const uint32_t Lu = (a.L + 15) / 16, Q = (Lu + 1) / 2, ipg = (Q + 63) / 64;

@@ -553,7 +553,7 @@ static int decoder_try_decode(qf_decoder* d) {
     const int32_t status = *reinterpret_cast<const int32_t*>(d->h_out);
     const uint32_t nrec = *reinterpret_cast<const uint32_t*>(d->h_out + 4);
     if (status != QF_OK) return status;  // singular: stays undecoded (decoder.rs:756-758)
-    if (nrec > nmax) return QF_EDEVICE;
+    if (nrec > nmax) return qf::device_fail(__FILE__, __LINE__, hipErrorIllegalState);  // internal inconsistency
     decoder_assemble(d, L, nrec, reinterpret_cast<const uint16_t*>(d->h_out + 16), d->h_rec, d->stride);
     return QF_OK;
 }
@@ -1112,11 +1112,15 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
         ci_o += std::min(d->k, pl.rc);
         rr_o += (size_t)std::min(d->k, pl.rc) * d->stride;
     }
-    if ((o_pk + pk && hipMemcpyAsync(dv, h, o_pk + pk, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        launch_ring_scatter(dv, reinterpret_cast<const RingSlot*>(dv + o_slots), (uint32_t)n_up, st) != hipSuccess) {
-        abandon(QF_EDEVICE);
-        ctx_recv_release(ctx);
-        return QF_EDEVICE;
+    {
+        hipError_t e = o_pk + pk ? hipMemcpyAsync(dv, h, o_pk + pk, hipMemcpyHostToDevice, st) : hipSuccess;
+        if (e == hipSuccess) e = launch_ring_scatter(dv, reinterpret_cast<const RingSlot*>(dv + o_slots), (uint32_t)n_up, st);
+        if (e != hipSuccess) {
+            const int err = qf::device_fail(__FILE__, __LINE__, e);
+            abandon(err);
+            ctx_recv_release(ctx);
+            return err;
+        }
     }
     // a failed batch decode: every connection whose generation was in it gets
     // the error as its status, and its decoder retries on its next packet
@@ -1135,9 +1139,11 @@ int decoders_add_batch(qf_ctx* ctx, DecAdd* v, uint32_t M) {
         s = qf_decode_batch_desc(ctx, descs.data(), (uint32_t)G, rows_base, reinterpret_cast<const uint16_t*>(dv + o_ri),
                                  dv + o_rec, reinterpret_cast<uint16_t*>(dv + o_ci),
                                  reinterpret_cast<uint32_t*>(dv + o_nrec), reinterpret_cast<int32_t*>(dv + o_st));
-        if (s == QF_OK && (hipMemcpyAsync(h + o_out, dv + o_out, total - o_out, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                           hipStreamSynchronize(st) != hipSuccess))
-            s = QF_EDEVICE;
+        if (s == QF_OK) {
+            hipError_t e = hipMemcpyAsync(h + o_out, dv + o_out, total - o_out, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) s = qf::device_fail(__FILE__, __LINE__, e);
+        }
         if (s != QF_OK) {
             fail_cauchy(s);
             failed = true;

@@ -124,6 +124,26 @@ def has_avx2() -> bool:
     return bool(_lib.cpu_has_avx2())
 
 
+_lib.cpu_decode.argtypes = [ctypes.c_int] + [ctypes.c_uint32] * 4 + [_P, _P, _P, ctypes.c_uint32]
+
+
+def cpu_decode(kind: str, k: int, row_index: np.ndarray, rows: np.ndarray, threads: int = 1) -> np.ndarray:
+    """Host decode of oracle/cpu_variants.c over G generations on `threads`
+    threads: row_index (G, n) and rows (G, n, L) in arrival order -> every
+    source row (G, k, L).  kind "table" = the oracle's Gauss-Jordan
+    (decoder.rs:720-783, table gf_mul); "clmul_dispatch" = the same
+    elimination with the reference's per-byte dispatched CLMUL-fold product
+    (timing only)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint8)
+    ri = np.ascontiguousarray(row_index, dtype=np.uint16)
+    G, n, L = rows.shape
+    out = np.zeros((G, k, L), np.uint8)
+    s = _lib.cpu_decode({"table": 0, "clmul_dispatch": 4}[kind], k, L, G, n, _p(ri), _p(rows), _p(out), threads)
+    if s != 0 and kind == "table":
+        raise ValueError(f"cpu_decode({kind}) status {s}")
+    return out
+
+
 def has_cpu_kind(kind: str) -> bool:
     """Whether this host can run cpu_encode(kind)."""
     return {"table": lambda: True, "avx2": _lib.cpu_has_avx2, "gfni": _lib.cpu_has_gfni,

@@ -36,6 +36,15 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 # per generation from HBM; the 13 zero-row reads hit L2)
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
+VARIANTS_STAMPS = [
+    # round 6: per-item phase timestamps (lab_stamps) of the library kernel and
+    # of the no-LU variant, one wave per item; and a persistent grid (2 blocks
+    # per CU, every wave loops over 19 items)
+    ("st_warm", {**LIB_DEC4, "lab_stamps": True}, ()),
+    ("st_lib", {**LIB_DEC4, "lab_stamps": True}, ()),
+    ("st_nolu", {**LIB_DEC4, "lab_stamps": True, "lu": False}, ()),
+    ("st_cap2", {**LIB_DEC4, "lab_stamps": True, "cap": 512}, ()),
+]
 VARIANTS = [
     # round 5as: split tables at a 32-B record stride (LDS banks) against 256 B
     ("t_warm", dict(LIB_DEC4), ()),
@@ -470,6 +479,59 @@ def c3_inputs(G, k, r, L, e, seed=0x51464543):
     return erased, smap
 
 
+STAMP_PHASES = ("entry", "item", "map", "rows", "repairs", "fwd", "bwd_stores", "drained")
+
+
+def stamp_report(raw: np.ndarray, n_items: int) -> dict:
+    """Per-item phase stamps (lab_stamps, 100 MHz real-time counter) -> phase
+    durations and how many items are in each phase over the launch."""
+    a = raw[: n_items * 32].reshape(n_items, 32).view(np.uint32).astype(np.uint64)
+    t = (a[:, 0:16:2] | (a[:, 1:16:2] << np.uint64(32))).astype(np.int64)   # 8 stamps
+    hw = a[:, 18].astype(np.int64)
+    ok = (t > 0).all(axis=1)
+    t, hw = t[ok], hw[ok]
+    t0 = t.min()
+    t = (t - t0) * 10                      # ns
+    names = ["prologue", "map", "rows", "repairs", "lu_fwd", "lu_bwd_stores", "drain"]
+    d = np.diff(t, axis=1)
+    out = {"items": int(ok.sum()), "span_us": round(float(t.max()) / 1e3, 2),
+           "phase_us_mean": {n: round(float(d[:, q].mean()) / 1e3, 3) for q, n in enumerate(names)},
+           "phase_us_p90": {n: round(float(np.percentile(d[:, q], 90)) / 1e3, 3) for q, n in enumerate(names)},
+           "item_us_mean": round(float((t[:, 7] - t[:, 0]).mean()) / 1e3, 3)}
+    # occupancy over time: items between stamps (entry..map: startup, map..repairs:
+    # row loop, repairs..bwd_stores: solve, bwd_stores..drained: drain)
+    grid = np.linspace(0, t.max(), 400)
+    spans = {"startup": (0, 2), "rowloop": (2, 4), "solve": (4, 6), "drain": (6, 7)}
+    occ = {}
+    for nm, (i, j) in spans.items():
+        st, en = np.sort(t[:, i]), np.sort(t[:, j])
+        cnt = np.searchsorted(st, grid, "right") - np.searchsorted(en, grid, "right")
+        occ[nm] = cnt
+    mid = (grid > 0.1 * t.max()) & (grid < 0.85 * t.max())
+    out["mean_waves_in_phase_steady"] = {nm: round(float(c[mid].mean()), 1) for nm, c in occ.items()}
+    # co-resident waves of one SIMD (same XCC, SE, CU, SIMD): the fraction of a
+    # wave's solve phase during which its SIMD partner is also in its solve phase
+    simd = (hw >> 4) & 0x3
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    key = (a[ok][:, 19].astype(np.int64) << 12) | (se << 8) | (cu << 4) | (simd << 2)
+    both, tot = 0.0, 0.0
+    order = np.argsort(key, kind="stable")
+    ks, ts = key[order], t[order]
+    bounds = np.nonzero(np.diff(ks))[0] + 1
+    for grp in np.split(np.arange(len(ks)), bounds):
+        s4, s6 = ts[grp, 4], ts[grp, 6]
+        for x in range(len(grp)):
+            lo, hi = s4[x], s6[x]
+            ov = np.clip(np.minimum(hi, s6) - np.maximum(lo, s4), 0, None)
+            ov[x] = 0
+            both += float(ov.sum())
+            tot += float(hi - lo)
+    out["solve_overlap_with_simd_partner"] = round(both / max(tot, 1.0), 3)
+    out["occupancy_trace"] = {nm: c[::10].tolist() for nm, c in occ.items()}
+    return out
+
+
 def run(G, reps):
     import torch
 
@@ -493,6 +555,7 @@ def run(G, reps):
     d_tab = torch.from_numpy(bs.split_tables()).to(dev)
     zero = torch.zeros(64 * 2048 + 4096, dtype=torch.uint8, device=dev)   # lab_zspread: 64 rows 2,048 B apart
     stream = torch.cuda.current_stream()
+    stamps = torch.zeros(((G * 38 + 63) // 64 + 64) * 32, dtype=torch.int32, device=dev)
     res = {}
     prepared = {}
     s2 = torch.cuda.Stream()
@@ -519,6 +582,8 @@ def run(G, reps):
                          smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
                          lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr(), chunked=chunked,
                          wave_gen=wave_gen, Q=Qv)
+        if m["kw"].get("lab_stamps"):
+            ka += np.array([stamps.data_ptr() & 0xFFFFFFFF, stamps.data_ptr() >> 32, 0, 0], np.uint32).tobytes()
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
@@ -547,6 +612,11 @@ def run(G, reps):
         res[m["name"]] = {"ms": round(ms, 4), "GBps_alg": round(alg / (ms / 1e3) / 1e9, 1), "items": n_items,
                           "kw": m["kw"],
                           "flags": m["flags"], "vgprs": m["vgprs"]}
+        if m["kw"].get("lab_stamps"):
+            stamps.zero_()
+            launch()
+            torch.cuda.synchronize()
+            res[m["name"]]["stamps"] = stamp_report(stamps.cpu().numpy(), n_items)
         print(m["name"], res[m["name"]], flush=True)
     for a, b in PAIRS:
         if a not in prepared or b not in prepared:
@@ -579,12 +649,15 @@ if __name__ == "__main__":
     ap.add_argument("--out", default="gpurun_out/dec_lab.json")
     ap.add_argument("--only", default="", help="comma-separated variant names (build)")
     ap.add_argument("--calib", action="store_true", help="build only the FETCH_SIZE calibration pair")
+    ap.add_argument("--stamps", action="store_true", help="build the per-item phase-stamp variants")
     ap.add_argument("--small", default="", help="comma-separated G values: run every variant at each")
     a = ap.parse_args()
     if a.only:
         ONLY = set(a.only.split(","))
     if a.calib:
         VARIANTS = CALIB
+    if a.stamps:
+        VARIANTS = VARIANTS_STAMPS
     if a.cmd == "build":
         build()
     else:

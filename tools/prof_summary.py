@@ -44,7 +44,10 @@ def main() -> None:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name") or row.get("KernelName") or "?"
             t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
-            dur[name].append(t1 - t0)
+            dur[name].append((t0, t1 - t0))
+    # rows of kernels on several streams are not in dispatch order: sort each
+    # kernel's launches by start time, so "first" below is the earliest launch
+    dur = {n: [d for _, d in sorted(v)] for n, v in dur.items()}
     total = sum(sum(v) for v in dur.values())
     kernels = []
     for name, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
