@@ -1209,8 +1209,22 @@ def _cpu_model():
 
 
 def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
-    """The CPU oracle (scalar port of decoder.rs loops) on the first S generations,
-    one core; its outputs are also compared with the GPU's for that sample."""
+    """The CPU oracle (port of the reference's loops) on the first S benchmark
+    generations, and its outputs checked against the GPU's on that sample:
+      single core  the scalar port: encode decoder.rs:172-275 (table gf_mul),
+                   Gauss-Jordan decode decoder.rs:720-783 (F4 fixed), one thread;
+      all cores    the same encode and decode (oracle/cpu_variants.c) with the
+                   generations split over every CPU this process may use, one
+                   generation per pinned thread at a time (the reference fans a
+                   decode's row operations out on rayon, decoder.rs:410-433,
+                   479-489: one generation per core is at least as parallel);
+                   also at the 16 CPUs the box allots per GPU;
+      as written   encode + decode with every product through the reference's
+                   gf_mul -> dispatch_bitslice -> CLMUL fold (optimize.rs:385-408,
+                   gf_tables.rs:76-141) on all cores: its per-byte cost; its
+                   output is the defective fold, timing only.
+    `value` / `cores` are the all-core table figure (encode + decode of the
+    sample's source bytes); the single-core figure stays beside it."""
     import sys
 
     sys.path.insert(0, str(REPO))
@@ -1220,8 +1234,10 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
     rep_h = rep[: S * r * Lb].cpu().numpy().reshape(S, r, Lb)
     n_slots = aidx.shape[1]
     rows_h = rows[: S * n_slots * Lb].cpu().numpy().reshape(S, n_slots, Lb)
+    ri_h = np.ascontiguousarray(np.asarray(aidx[:S]), dtype=np.uint16)
     emax = min(k, r)
     rec_h = rec[: S * emax * Lb].cpu().numpy().reshape(S, emax, Lb)
+    erased = []   # per generation: the source rows the decode recovers (the oracle's received mask)
     parity = True
     t0 = time.perf_counter()
     for g in range(S):
@@ -1232,20 +1248,66 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
     for g in range(S):
         st, sol, mask = oracle.decode(k, aidx[g], rows_h[g])
         er = np.nonzero(mask == 0)[0]
+        erased.append(er)
         parity &= st == 0 and bool((sol[er] == rec_h[g, : len(er)]).all())
     t_dec = time.perf_counter() - t0
     src_bytes = S * k * Lb
+    try:
+        n_all = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n_all = os.cpu_count() or 1
+
+    def timed(fn, min_s=1.0):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            out = fn()
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= min_s:
+                return out, dt / reps
+
+    oracle.set_pinning(True)
+    legs = {}
+    for nt in sorted({min(16, n_all), n_all}):
+        got_rep, te = timed(lambda: oracle.cpu_encode("table", src_h, r, nt))
+        got_dec, td = timed(lambda: oracle.cpu_decode("table", k, ri_h, rows_h, nt))
+        ok = bool((got_rep == rep_h).all())
+        for g in range(S):
+            ok &= bool((got_dec[g][erased[g]] == rec_h[g, : len(erased[g])]).all())
+        legs[nt] = {"value": round(src_bytes / (te + td) / (1 << 30), 4), "cores": nt,
+                    "encode_gibps": round(src_bytes / te / (1 << 30), 4),
+                    "decode_gibps": round(src_bytes / td / (1 << 30), 4), "sample_parity_vs_gpu": ok}
+    as_written = None
+    if oracle.has_cpu_kind("clmul_dispatch"):
+        n = min(S, max(n_all, 4 * n_all))   # about 1 s per leg on a 64-core host
+        _, te = timed(lambda: oracle.cpu_encode("clmul_dispatch", src_h[:n], r, n_all), 0.5)
+        _, td = timed(lambda: oracle.cpu_decode("clmul_dispatch", k, ri_h[:n], rows_h[:n], n_all), 0.5)
+        b = n * k * Lb
+        as_written = {"value": round(b / (te + td) / (1 << 30), 4), "cores": n_all, "generations": n,
+                      "encode_gibps": round(b / te / (1 << 30), 4), "decode_gibps": round(b / td / (1 << 30), 4),
+                      "note": "per-byte dispatched CLMUL-fold products (the reference as written): timing only, "
+                              "SURVEY F3"}
+    oracle.set_pinning(False)
+    allc = legs[n_all]
+    single = {"value": round(src_bytes / (t_enc + t_dec) / (1 << 30), 5), "cores": 1,
+              "encode_gibps": round(src_bytes / t_enc / (1 << 30), 5),
+              "decode_gibps": round(src_bytes / t_dec / (1 << 30), 5), "seconds": round(t_enc + t_dec, 2),
+              "sample_parity_vs_gpu": bool(parity)}
     return {
-        "value": round(src_bytes / (t_enc + t_dec) / (1 << 30), 5),
+        "value": allc["value"],
         "unit": "GiB/s",
-        "cores": 1,
+        "cores": n_all,
         "kind": "port",
         "sample": f"first {S} of the benchmark generations: oracle encode (decoder.rs:172-275 loop, table gf_mul) "
-                  f"+ oracle Gauss-Jordan decode (decoder.rs:720-783, F4 fixed), single thread",
-        "encode_gibps": round(src_bytes / t_enc / (1 << 30), 5),
-        "decode_gibps": round(src_bytes / t_dec / (1 << 30), 5),
-        "seconds": round(t_enc + t_dec, 2),
-        "sample_parity_vs_gpu": bool(parity),
+                  f"+ oracle Gauss-Jordan decode (decoder.rs:720-783, F4 fixed); all {n_all} usable CPUs, "
+                  f"generations split over pinned threads (single-core figure beside)",
+        "encode_gibps": allc["encode_gibps"],
+        "decode_gibps": allc["decode_gibps"],
+        "sample_parity_vs_gpu": bool(parity) and all(v["sample_parity_vs_gpu"] for v in legs.values()),
+        "single_core": single,
+        "all_cores": allc,
+        "share_16": legs[min(16, n_all)],
+        "as_written_all_cores": as_written,
     }
 
 
@@ -1338,6 +1400,10 @@ def compact_line(full: dict, detail: str | None = None) -> dict:
     if cb:
         line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "encode_gibps",
                                                        "decode_gibps", "sample_parity_vs_gpu")}
+        for leg in ("single_core", "share_16", "as_written_all_cores"):
+            if cb.get(leg):
+                line["cpu_baseline"][leg] = {k: cb[leg].get(k) for k in ("value", "cores", "encode_gibps",
+                                                                         "decode_gibps")}
     line["roofline_encode"] = _roof_compact(full.get("roofline_encode"))
     for k in ("encode_gibps", "decode_gibps", "encode_ms", "decode_ms", "ms_per_step_median_rank0",
               "kernel_ms_per_launch", "verified", "process_group"):
