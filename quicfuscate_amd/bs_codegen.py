@@ -229,6 +229,14 @@ _ASM = {
     "store_byte_saddr": lambda voff, d, sb, off: f"global_store_byte {V(voff)}, {V(d)}, {SP(sb)}"
                         + (f" offset:{off}" if off else ""),
     "store_byte": lambda a, d, off: f"global_store_byte {VP(a)}, {V(d)}, off" + (f" offset:{off}" if off else ""),
+    # closed-form solve (cx): per-lane masked products on bit-planes
+    "v_bfe_i": lambda d, a, off, w: f"v_bfe_i32 {V(d)}, {V(a)}, {off}, {w}",
+    "v_and": lambda d, a, b: f"v_and_b32_e32 {V(d)}, {V(a)}, {V(b)}",
+    # d = a ^ (b & c) (truth table index a*4 + b*2 + c)
+    "v_xor_and": lambda d, a, b, c: f"v_bitop3_b32 {V(d)}, {V(a)}, {V(b)}, {V(c)} bitop3:0x78",
+    "v_bcnt0": lambda d, a: f"v_bcnt_u32_b32 {V(d)}, {V(a)}, 0",
+    "v_bcnt": lambda d, a, b: f"v_bcnt_u32_b32 {V(d)}, {V(a)}, {V(b)}",
+    "v_cmp_ne0": lambda sd, a: f"v_cmp_ne_u32_e64 {SP(sd)}, 0, {V(a)}",
     # lab (lab_stamps): the real-time counter (100 MHz, chip-wide) into s[80 + 2p : 81 + 2p]
     "stamp": lambda p: f"s_memrealtime s[{STAMP_S0 + 2 * p}:{STAMP_S0 + 2 * p + 1}]",
     # lab (lab_stamps): the item's stores drained, stamp 7, then lane 0 writes
@@ -447,6 +455,12 @@ class KernelSpec:
     # load per half and row into a dummy register), so that its row loop finds
     # them in L2 / the Infinity Cache while HBM would otherwise idle
     lab_prefetch: tuple = ()
+    # chunked fft dec: the closed-form Cauchy solve (round 6): x_E = alpha *
+    # (C^T (beta * s))|_E, C^T through the additive-FFT plan run backwards
+    # with every op transposed, alpha / beta per-lane masked products on the
+    # bit-planes (no LU, no split tables); cx records (cx_record) instead of
+    # LU records
+    cx: bool = False
     # lab only (chunked fft dec): per-item phase timestamps (s_memrealtime)
     # written to a buffer named by kernarg bytes 128..135 (tools/dec_lab.py
     # --stamps): entry, item start, map read, source rows done, repairs done,
@@ -566,7 +580,7 @@ class KernelSpec:
             return f"qf_combine_bs_r{self.r}" + ("_pm" if self.pass_major else "")
         tag = {"enc": "bss" if self.ksplit > 1 else "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
-            tag = "decs" if self.ksplit > 1 else "decc"
+            tag = "decs" if self.ksplit > 1 else ("decx" if self.cx else "decc")
         if self.fft:
             tag += f"f{self.fft}" + (f"l{self.lds_rows}" if self.lds_rows else "")
         if self.rt != self.r or self.j0:
@@ -677,7 +691,10 @@ class KernelSpec:
 
     @property
     def offs_kernarg(self) -> int:
-        """Byte offset of the generation offset tables in the kernarg block."""
+        """Byte offset of the generation offset tables in the kernarg block
+        (lab_stamps: the stamp buffer pointer follows them)."""
+        if self.mode == "dec" and self.lab_stamps:
+            return KERNARG_BYTES_DEC - 16
         return KERNARG_BYTES - 16 if self.mode == "synw" else self.kernarg_bytes - 16
 
     @property
@@ -686,6 +703,8 @@ class KernelSpec:
             return LDS_TAB_BYTES + (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
         if self.mode == "enc" and self.ksplit > 1:
             return (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
+        if self.mode == "dec" and self.cx:
+            return 0
         if self.mode == "dec" and self.lds_rows:
             return 256 * self.tab_stride + 4 * self.lds_rows * LDS_ROW_BYTES
         if self.mode == "dec" and self.lab_tab32 and self.ksplit == 1:
@@ -2313,29 +2332,30 @@ def _prologue_chunked(E, spec: KernelSpec):
         E(Op("s_load_karg_x2", (SW_BOUND, KERNARG_BYTES)))   # kernarg words 24..25
     E(Op("s_nop", (4,)))
     E(Op("s_waitcnt_lgkm", ()))
-    # split tables -> LDS (as _prologue)
-    E(Op("s_movk", (62, 4096)))
-    E(Op("s_movk", (63, 0)))
-    E(Op("v_movs", (V_ADDR, 60)))
-    E(Op("v_movs", (V_ADDR + 1, 61)))
-    E(Op("v_mad64_k", (V_ADDR, V_LANE, 16, V_ADDR)))
-    E(Op("v_add64_s", (V_SRCA, V_ADDR, 62)))
-    for q in range(8):
-        E(Op("load16", (48 + 4 * q, V_ADDR if q < 4 else V_SRCA, 1024 * (q % 4))))
+    # split tables -> LDS (as _prologue; the closed-form solve has no tables)
     ts = spec.tab_stride
-    # global bytes q*1024 + 16 l = record 32 q + l/2, half l % 2 -> LDS
-    # (32 q + l/2) * stride + 16 (l % 2)
-    E(Op("v_lshr", (V_T, 1, V_LANE)))
-    E(Op("v_lshl", (V_T, ts.bit_length() - 1, V_T)))
-    E(Op("v_andk", (V_T + 1, 1, V_LANE)))
-    E(Op("v_lshl", (V_T + 1, 4, V_T + 1)))
-    E(Op("v_xor", (V_T, V_T, V_T + 1)))
-    for b in range(4):
-        E(Op("s_movk", (S_PICK + b, 0x0C0C000C | (b << 8))))
-    E(Op("s_waitcnt_vm", (0,)))
-    for q in range(8):
-        E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * ts * q)))
-    E(Op("s_waitcnt_lgkm_n", (0,)))
+    if not spec.cx:
+        E(Op("s_movk", (62, 4096)))
+        E(Op("s_movk", (63, 0)))
+        E(Op("v_movs", (V_ADDR, 60)))
+        E(Op("v_movs", (V_ADDR + 1, 61)))
+        E(Op("v_mad64_k", (V_ADDR, V_LANE, 16, V_ADDR)))
+        E(Op("v_add64_s", (V_SRCA, V_ADDR, 62)))
+        for q in range(8):
+            E(Op("load16", (48 + 4 * q, V_ADDR if q < 4 else V_SRCA, 1024 * (q % 4))))
+        # global bytes q*1024 + 16 l = record 32 q + l/2, half l % 2 -> LDS
+        # (32 q + l/2) * stride + 16 (l % 2)
+        E(Op("v_lshr", (V_T, 1, V_LANE)))
+        E(Op("v_lshl", (V_T, ts.bit_length() - 1, V_T)))
+        E(Op("v_andk", (V_T + 1, 1, V_LANE)))
+        E(Op("v_lshl", (V_T + 1, 4, V_T + 1)))
+        E(Op("v_xor", (V_T, V_T, V_T + 1)))
+        for b in range(4):
+            E(Op("s_movk", (S_PICK + b, 0x0C0C000C | (b << 8))))
+        E(Op("s_waitcnt_vm", (0,)))
+        for q in range(8):
+            E(Op("ds_write_b128", (V_T, 48 + 4 * q, 32 * ts * q)))
+        E(Op("s_waitcnt_lgkm_n", (0,)))
     if spec.lds_rows:   # this wave's row slots: after the tables, lds_rows x 2 KiB per wave
         E(Op("s_movk", (S_ROWLDS, spec.lds_rows * LDS_ROW_BYTES)))
         E(Op("s_mul", (S_ROWLDS, S_ROWLDS, 29)))
@@ -2559,6 +2579,20 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
 
         if spec.prio != (0, 0):
             E(Op("s_setprio", (spec.prio[0],)))
+        if spec.cx:
+            # repair rows past the first `ahead` (loaded inside _fft_stream into
+            # slots k % nbuf ..) rotate through three ring slots, so the record
+            # can land in slots that stay free (_cx_solve)
+            assert ahead == 2 and nbuf == 10 and k % nbuf == 4 and P.ch == 8
+
+            def cx_slot(n):
+                return ring0 + 8 * (n % nbuf if n < k else 4 + (n - k) % 3)
+            _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
+            if spec.lab_stamps:
+                E(Op("stamp", (3,)))
+            _cx_solve(E, ops, spec, P, fseq, load_fft, cx_slot)
+            _epilogue_next_item(E, far=True)
+            return ops
         _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
         if spec.lab_stamps:
             E(Op("stamp", (3,)))
@@ -2764,6 +2798,194 @@ def _ksplit_epilogue(E):
     E(Op("s_far_jump", (".Litem", 1)))
     E(Op("label", (".Lend",)))
     E(Op("s_endpgm", ()))
+
+
+# --------------------------------------------------------------------------
+# Closed-form Cauchy solve (spec.cx, round 6)
+# --------------------------------------------------------------------------
+# C[J,E]^-1 = diag(alpha) K diag(beta), K[b][a] = 1 / (x_a + y_b), x = k + J,
+# y = E (lch_fft.cauchy_inverse_factors), and K is a sub-block of the fixed
+# C^T: x_E = alpha * u|_E with u = C^T t, t_j = beta_j s_j (t_j = 0 for a
+# repair the lane's generation did not accept).  u comes from the encode's
+# additive-FFT plan run backwards with every op transposed
+# (lch_fft.transposed_evaluate): the 16 syndrome blocks stay in registers and
+# each chunk of 8 source rows is produced from them, then every row some lane
+# of the wave recovers is scaled by its alpha, transposed back to bytes and
+# stored.  The per-lane products are masked plane XORs (no v_perm, no LDS):
+# c * y = XOR over the set bits a of c of y * 2^a, y * 2^a by in-place
+# doubling (3 XORs a step, the planes renamed).
+# Record (cx_record, CX_REC_BYTES): [0, 16) beta by repair index, [16, 24)
+# the lane generation's erased-source mask, [32, 32 + k) alpha by source.
+CX_REC_BYTES = 96
+CX_BETA, CX_MASK, CX_FREE, CX_ADDR, CX_MT = 18, 22, 26, 34, 38   # v18..21, v22..23, v26..33, v34..37, v38..39
+CX_ALPHA_SLOT = 8                                                 # ring slots 8, 9: alpha (v112..v127)
+
+
+def _cx_mul(E, x: list, c_reg: int, c_off: int, res: int, mt: tuple = (CX_MT, CX_MT + 1)) -> None:
+    """res (8 planes) = c * x for the per-lane byte c at bits c_off.. of
+    c_reg; x (8 plane registers, list by plane) is doubled in place and left
+    destroyed.  8 mask extractions + 64 masked XORs + 21 doubling XORs."""
+    x = list(x)
+    for a in range(8):
+        m = mt[a & 1]
+        E(Op("v_bfe_i", (m, c_reg, c_off + a, 1)))   # all ones where bit a of c is set
+        for b in range(8):
+            if a == 0:
+                E(Op("v_and", (res + b, x[b], m)))
+            else:
+                E(Op("v_xor_and", (res + b, res + b, x[b], m)))
+        if a < 7:   # x <- x * 2 (poly 0x11D): bits 2, 3, 4 take bit 7; the others move up one
+            for b in (1, 2, 3):
+                E(Op("v_xor", (x[b], x[b], x[7])))
+            x = [x[7], x[0], x[1], x[2], x[3], x[4], x[5], x[6]]
+
+
+def _cx_solve(E, ops: list, spec: KernelSpec, P, fseq, load_fft, cx_slot) -> None:
+    k, r, R, ch = spec.k, spec.r, P.R, P.ch
+    acc0, ring0, ahead = spec.acc0, spec.ring0, spec.ahead
+    n_all = len(fseq)
+    planes = lambda base: [base + b for b in range(8)]
+    # the record: beta / mask quads in the map registers the source rows no
+    # longer need, alpha in ring slots 8 and 9 (free until the solve)
+    E(Op("v_movs", (V_ADDR, 56)))
+    E(Op("v_movs", (V_ADDR + 1, 57)))
+    E(Op("v_mad64_s", (V_ADDR, V_GA, 58, V_ADDR)))
+    E(Op("s_exec", (S_STA,)))
+    E(Op("load16", (CX_BETA, V_ADDR, 0)))
+    E(Op("load16", (CX_MASK, V_ADDR, 16)))
+    alpha0 = ring0 + 8 * CX_ALPHA_SLOT
+    n_alpha = (k + 15) // 16
+    for q in range(n_alpha):
+        E(Op("load16", (alpha0 + 4 * q, V_ADDR, 32 + 16 * q)))
+    E(Op("s_exec", (None,)))
+    n_rec = 2 + n_alpha
+    # loads in issue order (per-row counts), for the counted waits below
+    issued = [("row", k, 2)] + ([("row", k + 1, 2)] if ahead > 1 else []) + [("rec", None, n_rec)]
+
+    def younger(tag):
+        i = next(q for q, x in enumerate(issued) if x[:2] == tag)
+        return sum(x[2] for x in issued[i + 1:])
+    # accepted repairs, transposed to planes, onto their syndrome blocks
+    for n in range(k, n_all):
+        if n + ahead < n_all:
+            load_fft(n + ahead, cx_slot(n + ahead))
+            issued.append(("row", n + ahead, 2))
+        E(Op("s_waitcnt_vm", (younger(("row", n)),)))
+        j = fseq[n][1]
+        blk0 = acc0 + 8 * P.out_block[j]
+        E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lcxrep{j}")))
+        base = cx_slot(n)
+        ops.extend(_transpose_ops(base, spec.bfi_transpose, spec.vmask))
+        for b in range(8):
+            E(Op("v_xor", (blk0 + b, blk0 + b, base + b)))
+        E(Op("label", (f".Lcxrep{j}",)))
+    E(Op("s_waitcnt_vm", (0,)))
+    if spec.lab_stamps:
+        E(Op("stamp", (4,)))
+    # t_j = beta_j s_j; blocks of repairs no lane accepted (and of coset
+    # points past r) are zero.  The products rotate through one free block:
+    # block t ends in home[t]
+    home = {t: acc0 + 8 * t for t in range(R)}
+    free = CX_FREE
+    used = set(P.out_block)
+    for t in range(R):
+        if t not in used:
+            for b in range(8):
+                E(Op("v_movk", (home[t] + b, 0)))
+    for j in range(r):
+        t = P.out_block[j]
+        E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lcxz{j}")))
+        _cx_mul(E, planes(home[t]), CX_BETA + j // 4, 8 * (j % 4), free)
+        E(Op("s_branch", (f".Lcxb{j}",)))
+        E(Op("label", (f".Lcxz{j}",)))
+        for b in range(8):
+            E(Op("v_movk", (free + b, 0)))
+        E(Op("label", (f".Lcxb{j}",)))
+        home[t], free = free, home[t]
+    # u = C^T t: the final butterflies transposed, in reverse
+    tmp = tuple(range(V_T, V_T + 4)) if spec.fft_cse else ()
+    for i, j, sc in reversed(P.final_bfly):
+        for b in range(8):
+            E(Op("v_xor", (home[i] + b, home[i] + b, home[j] + b)))
+        if sc:
+            _macc(E, home[j], home[i], sc, init=False, tmp=tmp)
+    if spec.lab_stamps:
+        E(Op("stamp", (5,)))
+    y = [ring0 + 8 * m for m in range(ch)]
+    for hc in range(k // ch):
+        for m in range(ch):
+            terms = P.acc[(hc, m)]
+            if not terms:
+                for b in range(8):
+                    E(Op("v_movk", (y[m] + b, 0)))
+            for q, (t, c) in enumerate(terms):
+                _macc(E, y[m], home[t], c, init=q == 0, tmp=tmp)
+        for i, j, sc in reversed(P.chunk_bfly[hc]):
+            if sc:
+                _macc(E, y[j], y[i], sc, init=False, tmp=tmp)
+            for b in range(8):
+                E(Op("v_xor", (y[i] + b, y[i] + b, y[j] + b)))
+        for m in range(ch):
+            _cx_store_row(E, ops, spec, P.order[hc * ch + m], y[m], free, alpha0)
+
+
+def _cx_store_row(E, ops: list, spec: KernelSpec, v: int, yreg: int, res: int, alpha0: int) -> None:
+    """Source row v of u (planes at yreg): where a lane's generation erased
+    it, x_v = alpha_v u_v to recovered row rank(v) = the erased sources
+    below v; skipped when no lane of the wave erased it."""
+    mw = CX_MASK + v // 32
+    skip = f".Lcxs{v}"
+    E(Op("v_bfe", (V_SLOT, mw, v % 32, 1)))
+    E(Op("v_cmp_ne0", (S_TMP, V_SLOT)))
+    E(Op("s_nop", (4,)))
+    E(Op("s_and64", (S_TMP, S_TMP, S_STA)))
+    E(Op("s_cmp_eq64_0_br", (S_TMP, skip)))
+    _cx_mul(E, [yreg + b for b in range(8)], alpha0 + v // 4, 8 * (v % 4), res)
+    ops.extend(_transpose_ops(res, spec.bfi_transpose, spec.vmask))
+    lo = v % 32
+    E(Op("v_andk", (V_SLOT, (1 << lo) - 1, mw)))
+    E(Op("v_bcnt0", (V_SLOT, V_SLOT)))
+    if v >= 32:
+        E(Op("v_bcnt", (V_SLOT, CX_MASK, V_SLOT)))
+    a = CX_ADDR
+    E(Op("v_mad64_s", (a, V_SLOT, 11, V_DSTA)))
+    E(Op("v_add64_s", (a + 2, a, S_QB)))
+    E(Op("s_and64", (S_TMP2, S_TMP, S_STA)))
+    E(Op("s_exec", (S_TMP2,)))
+    E(Op("store16", (a, res, 0, spec.st_policy)))
+    E(Op("s_and64", (S_TMP2, S_TMP, S_STB)))
+    E(Op("s_exec", (S_TMP2,)))
+    E(Op("store16", (a + 2, res + 4, 0, spec.st_policy)))
+    # the partial last unit: bytes [0, L % 16) of the tail lane's unit B
+    E(Op("s_and64", (S_TMP2, S_TMP, S_TAIL)))
+    E(Op("s_exec", (S_TMP2,)))
+    E(Op("s_cbranch_execz", (f".Lcxt{v}",)))
+    for b in range(15):
+        E(Op("s_cmp_le_k_br", (59, b, f".Lcxt{v}")))
+        E(Op("v_lshr", (V_T, 8 * (b % 4), res + 4 + b // 4)))
+        E(Op("store_byte", (a + 2, V_T, b)))
+        E(Op("s_nop", (0,)))
+    E(Op("label", (f".Lcxt{v}",)))
+    E(Op("s_exec", (None,)))
+    E(Op("label", (skip,)))
+
+
+def cx_record(k: int, r: int, J: list[int], E_: list[int]) -> np.ndarray:
+    """The cx record of one generation (CX_REC_BYTES): beta by repair index,
+    the erased-source mask, alpha by source index (zero elsewhere)."""
+    from . import lch_fft
+    rec = np.zeros(CX_REC_BYTES, np.uint8)
+    if not E_:
+        return rec
+    alpha, beta = lch_fft.cauchy_inverse_factors(k, list(J), sorted(E_))
+    for a, j in enumerate(J):
+        rec[j] = beta[a]
+    m = 0
+    for b, v in enumerate(sorted(E_)):
+        m |= 1 << v
+        rec[32 + v] = alpha[b]
+    rec[16:24] = np.frombuffer(m.to_bytes(8, "little"), np.uint8)
+    return rec
 
 
 def _lu_solve_and_store_chunked(E, spec: KernelSpec):
@@ -3565,6 +3787,7 @@ class Emulator:
         self.labels = {op.args[0]: n for n, op in enumerate(ops) if op.name == "label"}
         self.buffers: list[tuple[int, int]] = []
         self.mem = {}
+        self.executed = {}   # op name -> times executed (over every wave run): dynamic instruction counts
 
     def add_buffer(self, base: int, data: np.ndarray):
         self.buffers.append((base, len(data)))
@@ -3673,11 +3896,12 @@ class Emulator:
             pc += 1
             steps += 1
             n, a = op.name, op.args
+            self.executed[n] = self.executed.get(n, 0) + 1
             if idx_mode and n.startswith("v_") and n != "v_xor_rel":
                 raise EmuError(f"{n} while the gpr_idx mode is on")
             if n == "s_waitcnt_lgkm" or (n == "s_waitcnt_lgkm_n" and a[0] == 0):
                 retire_s()
-            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger", "stamp", "stamp_flush"):
+            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger", "stamp"):
                 continue
             if n == "s_load_args":
                 for q in range(20):
@@ -3830,6 +4054,20 @@ class Emulator:
                 s[a[0]] = int(rv(a[1])[lane])
             elif n == "v_bfe":
                 wv(a[0], (rv(a[1]) >> np.uint64(a[2])) & np.uint64((1 << a[3]) - 1))
+            elif n == "v_bfe_i":
+                f = (rv(a[1]) >> np.uint64(a[2])) & np.uint64((1 << a[3]) - 1)
+                sign = (f >> np.uint64(a[3] - 1)) & np.uint64(1)
+                wv(a[0], np.where(sign == 1, f | (np.uint64(MASK32) ^ np.uint64((1 << a[3]) - 1)), f))
+            elif n == "v_and":
+                wv(a[0], rv(a[1]) & rv(a[2]))
+            elif n == "v_xor_and":
+                wv(a[0], rv(a[1]) ^ (rv(a[2]) & rv(a[3])))
+            elif n in ("v_bcnt0", "v_bcnt"):
+                x = rv(a[1]).astype(np.uint64)
+                cnt = np.array([bin(int(q)).count("1") for q in x], np.uint64)
+                wv(a[0], (cnt + (rv(a[2]) if n == "v_bcnt" else np.uint64(0))) & np.uint64(MASK32))
+            elif n == "v_cmp_ne0":
+                set_smask(a[0], (rv(a[1]) != 0) & exec_)
             elif n == "v_cmp_ne_s":
                 set_smask(a[0], (rv(a[2]) != np.uint64(s[a[1]])) & exec_)
             elif n == "v_cmp_eq_s":
@@ -4006,6 +4244,10 @@ class Emulator:
                                    np.array([rv(d + q)[l] for q in range(4)], np.uint32).tobytes())
                     else:
                         self.write(base + int(off[l]) + a[3], bytes([int(rv(d)[l]) & 0xFF]))
+            elif n == "stamp_flush":   # lab_stamps: 72 B at stamps + 128 item (pointer: kernarg bytes 128..135)
+                pending.clear()
+                base = int(ka[KERNARG_BYTES_DEC // 4]) | (int(ka[KERNARG_BYTES_DEC // 4 + 1]) << 32)
+                self.write(base + 128 * s[28], bytes(72))
             elif n == "s_barrier":
                 if pend_lgkm:
                     raise EmuError("s_barrier with LDS operations outstanding")

@@ -1392,7 +1392,11 @@ def test_dec_lab_variants_stay_in_bounds():
     rows = np.random.default_rng(1).integers(0, 256, G * n_slots * L, dtype=np.uint8)
     ROWS, OUT, MAP, ZERO, REC, TAB = 0x10000000, 0x40000000, 0x70000000, 0x78000000, 0x7C000000, 0x7E000000
     Q = ((L + 15) // 16 + 1) // 2
-    for name, kw, flags in (dec_lab.VARIANTS + dec_lab.VARIANTS_R05AL + dec_lab.VARIANTS_R05Y + dec_lab.VARIANTS_R05G + dec_lab.VARIANTS_R05F + dec_lab.VARIANTS_R05E + dec_lab.VARIANTS_R05D + dec_lab.VARIANTS_R05C + dec_lab.VARIANTS_R05B
+    STAMPS = 0x7F000000
+    outs = {}
+    cxrecs = np.stack([bs.cx_record(k, r, list(range(e)), erased[g].tolist()) for g in range(G)])
+    for name, kw, flags in (dec_lab.VARIANTS_STAMPS + [("lib_ref", dict(dec_lab.LIB_DEC4), ())] + dec_lab.VARIANTS_CX
+                            + dec_lab.VARIANTS + dec_lab.VARIANTS_R05AL + dec_lab.VARIANTS_R05Y + dec_lab.VARIANTS_R05G + dec_lab.VARIANTS_R05F + dec_lab.VARIANTS_R05E + dec_lab.VARIANTS_R05D + dec_lab.VARIANTS_R05C + dec_lab.VARIANTS_R05B
                              + dec_lab.VARIANTS_R05A):
         if name.endswith("_2") or name.endswith("_warm") or kw.get("rs"):
             continue
@@ -1402,15 +1406,24 @@ def test_dec_lab_variants_stay_in_bounds():
         rrs, Qv = kw.get("rrs", L), kw.get("Q")
         waves = ((G * (Qv or Q) + 63) // 64 + 3) // 4
         out = np.zeros(G * e * rrs, np.uint8)
+        cx = kw.get("cx", False)
         for base, buf in ((ROWS, rows), (OUT, out), (MAP, smap.reshape(-1)), (ZERO, np.zeros(1216, np.uint8)),
-                          (REC, recs.reshape(-1)), (TAB, bs.split_tables())):
+                          (REC, (cxrecs if cx else recs).reshape(-1)), (TAB, bs.split_tables())):
             emu.add_buffer(base, buf)
         ka = bs.kernargs(ROWS, OUT, n_slots * L, e * rrs, L, rrs, L, G, waves * 4, smap=MAP,
-                         map_stride=smap.shape[1], zero=ZERO, lu=(REC, bs.LU_REC_BYTES), tables=TAB, chunked=True,
-                         Q=Qv)
+                         map_stride=smap.shape[1], zero=ZERO, lu=(REC, bs.CX_REC_BYTES if cx else bs.LU_REC_BYTES),
+                         tables=TAB, chunked=True, Q=Qv)
+        if kw.get("lab_stamps"):   # the stamp buffer pointer follows the 128 kernarg bytes
+            emu.add_buffer(STAMPS, np.zeros(128 * 4 * waves, np.uint8))
+            ka += np.array([STAMPS, 0, 0, 0], np.uint32).tobytes()
+            assert spec.offs_kernarg == bs.KERNARG_BYTES_DEC - 16 and len(ka) == spec.kernarg_bytes
         for wg in range(waves):
             for w in range(4):
                 emu.run_wave(ka, wg, w)
+        outs[name] = out
+    # the stamps change nothing the kernel computes, nor does the closed-form solve
+    assert (outs["st_lib"] == outs["lib_ref"]).all() and outs["lib_ref"].any()
+    assert (outs["c_cx"] == outs["lib_ref"]).all() and (outs["c_cx_st"] == outs["lib_ref"]).all()
 
 
 def test_xchg_streams_meet_at_every_barrier():

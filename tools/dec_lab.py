@@ -36,14 +36,33 @@ LIB_DEC4 = {**LIB_DEC, "lu_ilp": True, "bfi_transpose": "s64"}                # 
 # per generation from HBM; the 13 zero-row reads hit L2)
 CALIB = [("calib_reads", {**LIB_DEC, "lu": False}, ("nostore",)),
          ("calib_full", dict(LIB_DEC), ())]
+LIB_CX = {"chunked": True, "fft": 8, "pd": 2, "ld_policy": "", "st_policy": "nt", "bfi_transpose": "s64", "cx": True}
+VARIANTS_CX = [
+    # round 6: the closed-form Cauchy solve (cx: alpha * C^T (beta * s) through
+    # the transposed additive FFT, masked plane products, no LU / split tables)
+    # against the library kernel, alternating; and both with phase stamps
+    ("c_warm", dict(LIB_DEC4), ()),
+    ("c_lib", {**LIB_DEC4, "st_policy": "nt"}, ()),
+    ("c_cx", dict(LIB_CX), ()),
+    ("c_lib_2", {**LIB_DEC4, "st_policy": "nt"}, ()),
+    ("c_cx_2", dict(LIB_CX), ()),
+    ("c_cx_st", {**LIB_CX, "lab_stamps": True}, ()),
+    ("c_lib_st", {**LIB_DEC4, "st_policy": "nt", "lab_stamps": True}, ()),
+    ("c_cx_nostore", dict(LIB_CX), ("nostore",)),
+    ("c_lib_3", {**LIB_DEC4, "st_policy": "nt"}, ()),
+    ("c_cx_3", dict(LIB_CX), ()),
+]
 VARIANTS_STAMPS = [
-    # round 6: per-item phase timestamps (lab_stamps) of the library kernel and
-    # of the no-LU variant, one wave per item; and a persistent grid (2 blocks
-    # per CU, every wave loops over 19 items)
+    # round 6: per-item phase timestamps (lab_stamps) of the library kernel,
+    # with deeper row prefetch (rows staged in LDS: 8 / 5 rows ahead instead
+    # of 2), split tables two coefficients ahead, and a persistent grid
     ("st_warm", {**LIB_DEC4, "lab_stamps": True}, ()),
     ("st_lib", {**LIB_DEC4, "lab_stamps": True}, ()),
-    ("st_nolu", {**LIB_DEC4, "lab_stamps": True, "lu": False}, ()),
-    ("st_cap2", {**LIB_DEC4, "lab_stamps": True, "cap": 512}, ()),
+    ("st_l9", {**LIB_DEC4, "lab_stamps": True, "lds_rows": 9}, ()),
+    ("st_l6", {**LIB_DEC4, "lab_stamps": True, "lds_rows": 6}, ()),
+    ("st_ahead2", {**LIB_DEC4, "lab_stamps": True, "lu_ahead": 2}, ()),
+    ("st_lib_2", {**LIB_DEC4, "lab_stamps": True}, ()),
+    ("lib_plain", dict(LIB_DEC4), ()),
 ]
 VARIANTS = [
     # round 5as: split tables at a 32-B record stride (LDS banks) against 256 B
@@ -492,6 +511,8 @@ def stamp_report(raw: np.ndarray, n_items: int) -> dict:
     t, hw = t[ok], hw[ok]
     t0 = t.min()
     t = (t - t0) * 10                      # ns
+    if not (t[:, 5] >= t[:, 4]).all():     # no LU (lu=False): no forward stamp
+        t[:, 5] = t[:, 4]
     names = ["prologue", "map", "rows", "repairs", "lu_fwd", "lu_bwd_stores", "drain"]
     d = np.diff(t, axis=1)
     out = {"items": int(ok.sum()), "span_us": round(float(t.max()) / 1e3, 2),
@@ -544,9 +565,12 @@ def run(G, reps):
     erased, smap = c3_inputs(G, k, r, L, e)
     nr = min(256, G)
     recs = np.zeros((nr, bs.LU_REC_BYTES), np.uint8)
+    cxr = np.zeros((nr, bs.CX_REC_BYTES), np.uint8)
     for q in range(nr):
         recs[q] = bs.lu_record(k, r, list(range(e)), erased[q].tolist())
+        cxr[q] = bs.cx_record(k, r, list(range(e)), erased[q].tolist())
     lu = np.tile(recs, (G // nr + 1, 1))[:G]
+    d_cx = torch.from_numpy(np.tile(cxr, (G // nr + 1, 1))[:G].reshape(-1)).to(dev)
     RS = 1280
     rows = torch.randint(0, 256, (G * n_slots * RS,), dtype=torch.uint8, device=dev)
     rec = torch.empty(G * e * RS, dtype=torch.uint8, device=dev)
@@ -580,7 +604,8 @@ def run(G, reps):
         rs, rrs = m["kw"].get("rs", L), m["kw"].get("rrs", L)
         ka = bs.kernargs(rows.data_ptr(), rec.data_ptr(), n_slots * rs, e * rrs, rs, rrs, L, G, blocks * 4,
                          smap=d_map.data_ptr(), map_stride=smap.shape[1], zero=zero.data_ptr(), Lv=Lv,
-                         lu=(d_lu.data_ptr(), bs.LU_REC_BYTES), tables=d_tab.data_ptr(), chunked=chunked,
+                         lu=(d_cx.data_ptr(), bs.CX_REC_BYTES) if m["kw"].get("cx") else (d_lu.data_ptr(), bs.LU_REC_BYTES),
+                         tables=d_tab.data_ptr(), chunked=chunked,
                          wave_gen=wave_gen, Q=Qv)
         if m["kw"].get("lab_stamps"):
             ka += np.array([stamps.data_ptr() & 0xFFFFFFFF, stamps.data_ptr() >> 32, 0, 0], np.uint32).tobytes()
@@ -650,6 +675,7 @@ if __name__ == "__main__":
     ap.add_argument("--only", default="", help="comma-separated variant names (build)")
     ap.add_argument("--calib", action="store_true", help="build only the FETCH_SIZE calibration pair")
     ap.add_argument("--stamps", action="store_true", help="build the per-item phase-stamp variants")
+    ap.add_argument("--cx", action="store_true", help="build the closed-form solve variants")
     ap.add_argument("--small", default="", help="comma-separated G values: run every variant at each")
     a = ap.parse_args()
     if a.only:
@@ -658,6 +684,8 @@ if __name__ == "__main__":
         VARIANTS = CALIB
     if a.stamps:
         VARIANTS = VARIANTS_STAMPS
+    if a.cx:
+        VARIANTS = VARIANTS_CX
     if a.cmd == "build":
         build()
     else:
