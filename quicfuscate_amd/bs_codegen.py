@@ -356,7 +356,7 @@ SW_Q0, SW_Q1 = 84, 88                         # the current map quad of g0 / g1 
 SW_BASE0, SW_BASE1 = 92, 94                   # this row's address in g0 / g1
 SW_T0, SW_T1 = 96, 97                         # slot bytes / temps
 SW_NEXT_FREE = 98
-STAMP_S0 = 80    # lab_stamps: s80..s95 stamps, s[96:97] buffer, s98 / s99 HW_ID / XCC_ID
+STAMP_S0 = 82    # lab_stamps: s82..s97 stamps, s[98:99] buffer, s100 / s101 HW_ID / XCC_ID (above S_ROWLDS)
 S_TMASK = 42     # s42..s44: the transpose masks 0x0F0F0F0F, 0x33333333, 0x55555555
 S_ABSENT = 31    # holds ABSENT (VOP3 takes no literal)
 ABSENT = 0xFF    # slot-map value of a row that was not accepted
@@ -639,7 +639,9 @@ class KernelSpec:
         n = self.map_b + 4 * self.map_quads
         if self.fft:
             n = max(n, self.acc0 + 8 * self.nacc)
-        if self.mode == "dec" and self.chunked:
+        if self.mode == "dec" and self.chunked and self.cx:
+            n = max(n, cx_alpha0(self) + 4 * ((self.k + 15) // 16))
+        elif self.mode == "dec" and self.chunked:
             n = max(n, lu_layout_chunked(self)["end"])
         elif self.mode == "dec":
             n = max(n, max(lu_layout(self)[0]) + 4)
@@ -703,10 +705,10 @@ class KernelSpec:
             return LDS_TAB_BYTES + (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
         if self.mode == "enc" and self.ksplit > 1:
             return (self.ksplit - 1) * self.r * KSPLIT_BLOCK_BYTES
-        if self.mode == "dec" and self.cx:
+        if self.mode == "dec" and self.cx and not self.lds_rows:
             return 0
         if self.mode == "dec" and self.lds_rows:
-            return 256 * self.tab_stride + 4 * self.lds_rows * LDS_ROW_BYTES
+            return (0 if self.cx else 256 * self.tab_stride) + 4 * self.lds_rows * LDS_ROW_BYTES
         if self.mode == "dec" and self.lab_tab32 and self.ksplit == 1:
             return 256 * self.tab_stride
         if self.mode == "enc" and self.lds_rows:
@@ -2359,7 +2361,8 @@ def _prologue_chunked(E, spec: KernelSpec):
     if spec.lds_rows:   # this wave's row slots: after the tables, lds_rows x 2 KiB per wave
         E(Op("s_movk", (S_ROWLDS, spec.lds_rows * LDS_ROW_BYTES)))
         E(Op("s_mul", (S_ROWLDS, S_ROWLDS, 29)))
-        E(Op("s_addk", (S_ROWLDS, S_ROWLDS, 256 * ts)))
+        if not spec.cx:   # after the split tables (the closed-form solve has none)
+            E(Op("s_addk", (S_ROWLDS, S_ROWLDS, 256 * ts)))
         E(Op("v_lshl", (V_LDSA, 4, V_LANE)))
         E(Op("v_add_s", (V_LDSA, S_ROWLDS, V_LDSA)))
     if spec.xcd_remap:
@@ -2580,17 +2583,22 @@ def _generate_dec_chunked(spec: KernelSpec) -> list[Op]:
         if spec.prio != (0, 0):
             E(Op("s_setprio", (spec.prio[0],)))
         if spec.cx:
-            # repair rows past the first `ahead` (loaded inside _fft_stream into
-            # slots k % nbuf ..) rotate through three ring slots, so the record
-            # can land in slots that stay free (_cx_solve)
-            assert ahead == 2 and nbuf == 10 and k % nbuf == 4 and P.ch == 8
+            # repair rows rotate through three ring slots (the first two are
+            # where _fft_stream loaded rows k and k + 1), away from slots 8
+            # and 9, which take the record's alpha quads (_cx_solve)
+            rot = cx_repair_slots(spec)
 
             def cx_slot(n):
-                return ring0 + 8 * (n % nbuf if n < k else 4 + (n - k) % 3)
+                if spec.lds_rows and n >= k:
+                    return ring0 + 8 * rot[(n - k) % 3]
+                return ring0 + 8 * (n % nbuf if n < k else rot[(n - k) % 3])
             _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
             if spec.lab_stamps:
                 E(Op("stamp", (3,)))
             _cx_solve(E, ops, spec, P, fseq, load_fft, cx_slot)
+            if spec.lab_stamps:
+                E(Op("stamp", (6,)))
+                E(Op("stamp_flush", ()))
             _epilogue_next_item(E, far=True)
             return ops
         _fft_stream(E, ops, spec, load_fft, wait_fft, lambda t: acc0 + 8 * t, n_rows=n_all)
@@ -2817,8 +2825,49 @@ def _ksplit_epilogue(E):
 # Record (cx_record, CX_REC_BYTES): [0, 16) beta by repair index, [16, 24)
 # the lane generation's erased-source mask, [32, 32 + k) alpha by source.
 CX_REC_BYTES = 96
-CX_BETA, CX_MASK, CX_FREE, CX_ADDR, CX_MT = 18, 22, 26, 34, 38   # v18..21, v22..23, v26..33, v34..37, v38..39
-CX_ALPHA_SLOT = 8                                                 # ring slots 8, 9: alpha (v112..v127)
+CX_MT = 38            # v38, v39: mask temps of the products
+CX_ALPHA_SLOT = 8     # ring slots 8, 9: alpha (v112..v127)
+
+
+def cx_regs(spec: KernelSpec) -> dict:
+    """The cx solve's registers in the five slot-map quads v18..v37: beta,
+    the erased mask, the product block `free` (two quads) and the store
+    address pairs, around the quad holding the repair slots (k .. k + 15),
+    which the repair loop still reads while the record lands."""
+    repq = spec.k // 16
+    q = [x for x in range(FFT_MAP_DEC_QUADS) if x != repq]
+    beta, mask = q[0], q[1]
+    rest = [x for x in range(FFT_MAP_DEC_QUADS) if x not in (beta, mask)]
+    free = next(x for x in rest if x + 1 in rest)
+    addr = next(x for x in rest if x not in (free, free + 1))
+    return {n: FFT_MAP_DEC + 4 * x for n, x in (("beta", beta), ("mask", mask), ("free", free), ("addr", addr))}
+
+
+def cx_alpha0(spec: KernelSpec) -> int:
+    """First VGPR of the cx record's alpha quads: ring slots 8 and 9 (free
+    from the last source chunk on), or with lds_rows (the ring is the chunk
+    alone) the registers past the accumulators."""
+    if spec.lds_rows:
+        return spec.acc0 + 8 * spec.nacc
+    return spec.ring0 + 8 * CX_ALPHA_SLOT
+
+
+def cx_repair_slots(spec: KernelSpec) -> list:
+    """The three ring slots the cx kernel's repair rows rotate through (the
+    first two are where _fft_stream loaded rows k and k + 1; with lds_rows,
+    the slots their LDS copies are read into)."""
+    k, nbuf = spec.k, spec.nbuf
+    ok = spec.fplan.ch == 8 and spec.k <= 64 and not getattr(spec.fplan, "direct", None) and \
+        (getattr(spec.fplan, "kA", 0) or k) == k
+    if spec.lds_rows:
+        if not ok or nbuf != 8 or spec.ahead + 1 != spec.lds_rows:
+            raise ValueError(f"{spec.name}: no cx layout")
+        return [0, 1, 2]
+    first = [k % nbuf, (k + 1) % nbuf]
+    if not (ok and spec.ahead == 2 and nbuf == 10 and not set(first) & {CX_ALPHA_SLOT, CX_ALPHA_SLOT + 1}):
+        raise ValueError(f"{spec.name}: no cx layout (power-of-two k <= 64, pd 2, chunks of 8)")
+    third = next(q for q in range(nbuf) if q not in first + [CX_ALPHA_SLOT, CX_ALPHA_SLOT + 1])
+    return first + [third]
 
 
 def _cx_mul(E, x: list, c_reg: int, c_off: int, res: int, mt: tuple = (CX_MT, CX_MT + 1)) -> None:
@@ -2845,22 +2894,23 @@ def _cx_solve(E, ops: list, spec: KernelSpec, P, fseq, load_fft, cx_slot) -> Non
     acc0, ring0, ahead = spec.acc0, spec.ring0, spec.ahead
     n_all = len(fseq)
     planes = lambda base: [base + b for b in range(8)]
+    cr = cx_regs(spec)
     # the record: beta / mask quads in the map registers the source rows no
     # longer need, alpha in ring slots 8 and 9 (free until the solve)
     E(Op("v_movs", (V_ADDR, 56)))
     E(Op("v_movs", (V_ADDR + 1, 57)))
     E(Op("v_mad64_s", (V_ADDR, V_GA, 58, V_ADDR)))
     E(Op("s_exec", (S_STA,)))
-    E(Op("load16", (CX_BETA, V_ADDR, 0)))
-    E(Op("load16", (CX_MASK, V_ADDR, 16)))
-    alpha0 = ring0 + 8 * CX_ALPHA_SLOT
+    E(Op("load16", (cr["beta"], V_ADDR, 0)))
+    E(Op("load16", (cr["mask"], V_ADDR, 16)))
+    alpha0 = cx_alpha0(spec)
     n_alpha = (k + 15) // 16
     for q in range(n_alpha):
         E(Op("load16", (alpha0 + 4 * q, V_ADDR, 32 + 16 * q)))
     E(Op("s_exec", (None,)))
     n_rec = 2 + n_alpha
     # loads in issue order (per-row counts), for the counted waits below
-    issued = [("row", k, 2)] + ([("row", k + 1, 2)] if ahead > 1 else []) + [("rec", None, n_rec)]
+    issued = [("row", k + q, 2) for q in range(min(ahead, n_all - k))] + [("rec", None, n_rec)]
 
     def younger(tag):
         i = next(q for q, x in enumerate(issued) if x[:2] == tag)
@@ -2875,6 +2925,11 @@ def _cx_solve(E, ops: list, spec: KernelSpec, P, fseq, load_fft, cx_slot) -> Non
         blk0 = acc0 + 8 * P.out_block[j]
         E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lcxrep{j}")))
         base = cx_slot(n)
+        if spec.lds_rows:   # the row from its LDS slot
+            S = spec.lds_rows
+            E(Op("ds_read_b128", (base, V_LDSA, (n % S) * LDS_ROW_BYTES)))
+            E(Op("ds_read_b128", (base + 4, V_LDSA, (n % S) * LDS_ROW_BYTES + 1024)))
+            E(Op("s_waitcnt_lgkm_n", (0,)))
         ops.extend(_transpose_ops(base, spec.bfi_transpose, spec.vmask))
         for b in range(8):
             E(Op("v_xor", (blk0 + b, blk0 + b, base + b)))
@@ -2886,7 +2941,7 @@ def _cx_solve(E, ops: list, spec: KernelSpec, P, fseq, load_fft, cx_slot) -> Non
     # points past r) are zero.  The products rotate through one free block:
     # block t ends in home[t]
     home = {t: acc0 + 8 * t for t in range(R)}
-    free = CX_FREE
+    free = cr["free"]
     used = set(P.out_block)
     for t in range(R):
         if t not in used:
@@ -2895,7 +2950,7 @@ def _cx_solve(E, ops: list, spec: KernelSpec, P, fseq, load_fft, cx_slot) -> Non
     for j in range(r):
         t = P.out_block[j]
         E(Op("s_cmp_le_k_br", (S_JMAX, j, f".Lcxz{j}")))
-        _cx_mul(E, planes(home[t]), CX_BETA + j // 4, 8 * (j % 4), free)
+        _cx_mul(E, planes(home[t]), cr["beta"] + j // 4, 8 * (j % 4), free)
         E(Op("s_branch", (f".Lcxb{j}",)))
         E(Op("label", (f".Lcxz{j}",)))
         for b in range(8):
@@ -2926,14 +2981,14 @@ def _cx_solve(E, ops: list, spec: KernelSpec, P, fseq, load_fft, cx_slot) -> Non
             for b in range(8):
                 E(Op("v_xor", (y[i] + b, y[i] + b, y[j] + b)))
         for m in range(ch):
-            _cx_store_row(E, ops, spec, P.order[hc * ch + m], y[m], free, alpha0)
+            _cx_store_row(E, ops, spec, P.order[hc * ch + m], y[m], free, alpha0, cr)
 
 
-def _cx_store_row(E, ops: list, spec: KernelSpec, v: int, yreg: int, res: int, alpha0: int) -> None:
+def _cx_store_row(E, ops: list, spec: KernelSpec, v: int, yreg: int, res: int, alpha0: int, cr: dict) -> None:
     """Source row v of u (planes at yreg): where a lane's generation erased
     it, x_v = alpha_v u_v to recovered row rank(v) = the erased sources
     below v; skipped when no lane of the wave erased it."""
-    mw = CX_MASK + v // 32
+    mw = cr["mask"] + v // 32
     skip = f".Lcxs{v}"
     E(Op("v_bfe", (V_SLOT, mw, v % 32, 1)))
     E(Op("v_cmp_ne0", (S_TMP, V_SLOT)))
@@ -2946,8 +3001,8 @@ def _cx_store_row(E, ops: list, spec: KernelSpec, v: int, yreg: int, res: int, a
     E(Op("v_andk", (V_SLOT, (1 << lo) - 1, mw)))
     E(Op("v_bcnt0", (V_SLOT, V_SLOT)))
     if v >= 32:
-        E(Op("v_bcnt", (V_SLOT, CX_MASK, V_SLOT)))
-    a = CX_ADDR
+        E(Op("v_bcnt", (V_SLOT, cr["mask"], V_SLOT)))
+    a = cr["addr"]
     E(Op("v_mad64_s", (a, V_SLOT, 11, V_DSTA)))
     E(Op("v_add64_s", (a + 2, a, S_QB)))
     E(Op("s_and64", (S_TMP2, S_TMP, S_STA)))

@@ -41,16 +41,24 @@ VARIANTS_CX = [
     # round 6: the closed-form Cauchy solve (cx: alpha * C^T (beta * s) through
     # the transposed additive FFT, masked plane products, no LU / split tables)
     # against the library kernel, alternating; and both with phase stamps
+    # (r06d: lib 1.379 / 1.352 ms, cx 1.399 / 1.412)
+    # (r06e: lib 1.387 / 1.523, cx 1.400 / 1.418; without row loads cx 1.089
+    # against 1.479: the cx solve issues far faster, its row loop then waits
+    # on memory -- so cx with rows staged in LDS, 8 / 9 rows ahead (no split
+    # tables: 72 / 80 KB per workgroup, two workgroups per CU))
     ("c_warm", dict(LIB_DEC4), ()),
     ("c_lib", {**LIB_DEC4, "st_policy": "nt"}, ()),
     ("c_cx", dict(LIB_CX), ()),
+    ("c_cx_l9", {**LIB_CX, "lds_rows": 9}, ()),
+    ("c_cx_l10", {**LIB_CX, "lds_rows": 10}, ()),
+    ("c_cx_l9_st", {**LIB_CX, "lds_rows": 9, "lab_stamps": True}, ()),
     ("c_lib_2", {**LIB_DEC4, "st_policy": "nt"}, ()),
+    ("c_cx_l9_2", {**LIB_CX, "lds_rows": 9}, ()),
+    ("c_cx_l10_2", {**LIB_CX, "lds_rows": 10}, ()),
     ("c_cx_2", dict(LIB_CX), ()),
-    ("c_cx_st", {**LIB_CX, "lab_stamps": True}, ()),
-    ("c_lib_st", {**LIB_DEC4, "st_policy": "nt", "lab_stamps": True}, ()),
-    ("c_cx_nostore", dict(LIB_CX), ("nostore",)),
+    ("c_cx_l9_norowload", {**LIB_CX, "lds_rows": 9}, ("norowload",)),
     ("c_lib_3", {**LIB_DEC4, "st_policy": "nt"}, ()),
-    ("c_cx_3", dict(LIB_CX), ()),
+    ("c_cx_l10_3", {**LIB_CX, "lds_rows": 10}, ()),
 ]
 VARIANTS_STAMPS = [
     # round 6: per-item phase timestamps (lab_stamps) of the library kernel,
@@ -509,6 +517,8 @@ def stamp_report(raw: np.ndarray, n_items: int) -> dict:
     hw = a[:, 18].astype(np.int64)
     ok = (t > 0).all(axis=1)
     t, hw = t[ok], hw[ok]
+    if not len(t):
+        return {"items": 0}
     t0 = t.min()
     t = (t - t0) * 10                      # ns
     if not (t[:, 5] >= t[:, 4]).all():     # no LU (lu=False): no forward stamp
