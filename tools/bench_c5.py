@@ -162,29 +162,57 @@ def mixed_leg(qf, ctx, nbytes: float, reps: int, seed: int = 5) -> dict:
                        "GiBps_alg": round(dec_b / (kms_d / 1e3) / 2**30, 1)}}
 
 
-def _valu_info(kt: dict, G: int, L: int, ms: float) -> dict | None:
-    """VALU issue fraction of the generated encode kernels of a launch set:
-    bs_codegen.valu_per_item (static count of the straight-line item body) x
-    items, at 2 cycles per wave64 instruction on 1,024 SIMDs at 2.4 GHz
-    (MI355X_MICROARCH.md), against the kernels' measured time.  None when a
-    kernel of the set is not a generated one."""
+# SQ counters of the sliding-window launches (tools/gpu.sh c5sq: rocprofv3
+# --pmc over `--modes sliding` of every shape at the G below), keyed by
+# kernel name and G, each with the code hash of the kernel it measured
+C5_SQ = REPO / "profiles" / "c5_sq_counters.json"
+# residency: at least this many generations per leg, so every launch runs
+# several rounds of workgroups (>= 4 per CU for the one-wave-per-item
+# kernels: G x 568 units / 128 per item / 4 items per workgroup >= 1,024)
+G_MIN = 1024
+
+
+def _valu_info(kt: dict, G: int, L: int, ms: float, mode: str = "block") -> dict | None:
+    """VALU issue fraction of the generated encode kernels of a launch set,
+    against the kernels' measured time, at 2 cycles per wave64 instruction on
+    1,024 SIMDs at 2.4 GHz (MI355X_MICROARCH.md).  The instruction count is
+    SQ_INSTS_VALU of a counter pass of the same launches (C5_SQ) where one
+    exists for this mode, kernel, G and code hash; otherwise the static model
+    (bs_codegen.valu_per_item x items), labelled as such.  None when a kernel
+    of the set is not a generated one."""
     from quicfuscate_amd import bs_codegen as bs
     from quicfuscate_amd.build_lib import kernel_specs
 
     specs = {sp.name: sp for sp in kernel_specs() if sp.mode == "enc"}
+    try:
+        sq = json.loads(C5_SQ.read_text())
+        hashes = json.loads((REPO / "quicfuscate_amd" / "lib" / "kernel_hashes.json").read_text())
+    except Exception:
+        sq, hashes = {}, {}
     Lv = bs.padded_units(L)
     items = -(-G * Lv // 128)
-    instr = 0
+    instr, counted, cycles = 0, True, 0.0
     for name, (cnt, _) in kt.items():
         sp = specs.get(name)
         if sp is None:
             return None
-        instr += cnt * bs.valu_per_item(sp) * items
+        ent = sq.get(f"{mode}/{name}/G{G}")
+        if ent and ent.get("code_sha16") == hashes.get(name):
+            instr += cnt * ent["SQ_INSTS_VALU"]
+            cycles += cnt * ent.get("SQ_BUSY_CYCLES", 0.0)
+        else:
+            counted = False
+            instr += cnt * bs.valu_per_item(sp) * items
     issue_ms = instr * 2 / (1024 * 2.4e9) * 1e3
-    return {"valu_instr_per_launch_set": int(instr), "issue_ms": round(issue_ms, 4),
-            "frac": round(issue_ms / ms, 4) if ms else None,
-            "model": "static VALU count per item (bs_codegen.valu_per_item) x items, 2 cyc per wave64 instr, "
-                     "1,024 SIMDs at 2.4 GHz"}
+    out = {"valu_instr_per_launch_set": int(instr), "issue_ms": round(issue_ms, 4),
+           "frac": round(issue_ms / ms, 4) if ms else None,
+           "source": "counters" if counted else "model",
+           "model": ("SQ_INSTS_VALU of the same launches (profiles/c5_sq_counters.json, code hash checked)"
+                     if counted else "static VALU count per item (bs_codegen.valu_per_item) x items")
+           + ", 2 cyc per wave64 instr, 1,024 SIMDs at 2.4 GHz"}
+    if counted and cycles:
+        out["sq_busy_cycles"] = int(cycles)
+    return out
 
 
 def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block", "sliding"),
@@ -199,7 +227,7 @@ def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block",
     import torch
 
     res = {}
-    G = max(1, int(nbytes // (k * L_JUMBO)))
+    G = max(G_MIN, int(nbytes // (k * L_JUMBO)))
     drs = RS if exact_rows else REP_RS
     for mode in modes:
         if mode == "block":
@@ -222,7 +250,7 @@ def shape_leg(qf, ctx, k: int, r: int, nbytes: float, reps: int, modes=("block",
                "(1 + r) L per window (SURVEY 8(d): one new source row read, r repairs written)",
                "GiBps_alg": round(alg / (kms / 1e3) / 2**30, 1),
                "hbm_frac_of_8TBps": round(alg / (kms / 1e3) / 8e12, 3),
-               "valu": _valu_info(kt, G, L_JUMBO, kms)}
+               "valu": _valu_info(kt, G, L_JUMBO, kms, mode)}
         if mode == "sliding" and verify:
             # windows g = 0, G/2, G-1 re-encoded as a block batch
             wins = sorted({0, G // 2, G - 1})

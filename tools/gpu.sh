@@ -103,6 +103,19 @@ case "$what" in
     python3 tools/prof_summary.py "$OUT/c5kt" "$OUT/c5_kernel_stats.json" --command "rocprofv3 --kernel-trace --stats -- $BC"
     echo C5PMC_OK
     ;;
+  c5sq)     # SQ counters of the C5 sliding-window encodes, all seven shapes -> profiles/c5_sq_counters.json
+    SH="32,5;48,8;64,10;96,15;128,20;160,48;196,59"
+    BC="python3 tools/bench_c5.py --shapes $SH --modes sliding --reps 3 --bytes 1e9"
+    timeout -k 10 300 $BC --out "$OUT/c5sl_plain.json" > "$OUT/c5sl_plain.log" 2>&1
+    grep "^k" "$OUT/c5sl_plain.log"
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
+      SQ_WAIT_INST_ANY SQ_INSTS_LDS --output-format csv -d "$OUT/c5slsq" -o sq -- \
+      $BC --out "$OUT/c5sl_sq.json" > "$OUT/c5slsq.log" 2>&1
+    cp profiles/c5_sq_counters.json "$OUT/c5_sq_counters.json" 2>/dev/null || true
+    python3 tools/c5_sq_summary.py "$OUT/c5slsq" "$OUT/c5sl_sq.json" --mode sliding --out "$OUT/c5_sq_counters.json" \
+      --command "rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS -- $BC"
+    echo C5SQ_OK
+    ;;
   c5ab)
     SH="${C5_SHAPES:-196,59;160,48;128,39}"
     TK="${C5_TESTK:-c5 or passes or merged or 196 or synw or large or 96 or 48}"
