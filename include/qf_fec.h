@@ -179,6 +179,10 @@ enum {
     QF_OPT_COMBINE_WIDE,         /* 1: a bit-sliced payload pass with 17-24 outputs (e_max) runs as one
                                     24-output pass reading two coefficient records per row; 0: two
                                     16-output passes (pass-major) [QF_COMBINE_WIDE; default 1] */
+    QF_OPT_COMBINE_XCD,          /* 1: the pass-major payload pass item-major: the passes of one
+                                    generation's lane-chunk run together on one XCD, so the later
+                                    passes read the syndrome rows from its L2 instead of HBM; 0: pass
+                                    p's workgroups after pass p - 1's [QF_COMBINE_XCD; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

@@ -222,6 +222,17 @@ _ASM = {
     "s_idx_on": lambda s_: f"s_set_gpr_idx_on s{s_}, gpr_idx(SRC0)",
     "s_idx": lambda s_: f"s_set_gpr_idx_idx s{s_}",
     "s_idx_off": lambda: "s_set_gpr_idx_off",
+    # jump-table products (KernelSpec.cmb_jump): the table's address, the call
+    # and return, the block alignment and the destination-indexed XORs
+    "s_getpc_rel": lambda d, lbl: (f"s_getpc_b64 s[{d}:{d + 1}]\n{lbl}_pc:\n\ts_add_u32 s{d}, s{d}, {lbl}-{lbl}_pc\n"
+                                   f"\ts_addc_u32 s{d + 1}, s{d + 1}, 0"),
+    "s_call": lambda ret, tgt: f"s_swappc_b64 s[{ret}:{ret + 1}], s[{tgt}:{tgt + 1}]",
+    "s_ret": lambda ret: f"s_setpc_b64 s[{ret}:{ret + 1}]",
+    "align7": lambda: ".p2align 7",
+    "s_idx_on_d3": lambda s_: f"s_set_gpr_idx_on s{s_}, gpr_idx(SRC0,DST)",
+    "s_idx_on_d2": lambda s_: f"s_set_gpr_idx_on s{s_}, gpr_idx(SRC1,DST)",
+    "v_xor3_reld": lambda d, a, b: f"v_bitop3_b32 {V(d)}, {V(d)}, {V(a)}, {V(b)} bitop3:0x96",
+    "v_xor_reld": lambda d, a: f"v_xor_b32_e32 {V(d)}, {V(a)}, {V(d)}",
     # d = v[base + M0] ^ b: src0 indexed while the gpr_idx mode is on
     "v_xor_rel": lambda d, base, b: f"v_xor_b32_e32 {V(d)}, {V(base)}, {V(b)}",
     "store16_saddr": lambda voff, d, sb, pol="": f"global_store_dwordx4 {V(voff)}, {VQ(d)}, {SP(sb)}"
@@ -433,6 +444,13 @@ class KernelSpec:
     # cmb (R <= 16): input rows prefetched two ahead (a third row buffer at
     # v192..v199: 200 VGPRs, still two waves per SIMD)
     cmb_pf2: bool = False
+    # cmb (R <= 16): the product of a row by output j's runtime coefficient c
+    # as a call into c's code block (256 blocks of 128 B after the kernel's
+    # end, built from cmb_index_table), accumulator set j chosen by the gpr_idx
+    # index 8 j on the destination: 3 = 8 VOP3 xor3 (acc ^= LO[a] ^ HI[b]) per
+    # block; 2 = 16 VOP2 xors; 0 = M0-indexed sources (an s_set_gpr_idx_idx per
+    # XOR). 6 SALU per product instead of 16 + the index-row load
+    cmb_jump: int = 0
     # VALU list scheduling (bs_sched.schedule): runs of plain VALU ops between
     # non-VALU ops reordered so a producer sits >= sched ops before its
     # consumers where the run allows it (0: program order)
@@ -518,6 +536,12 @@ class KernelSpec:
     # the passes' workgroup ranges; kernarg word 32 = the coefficient records'
     # pass stride)
     pass_major: bool = False
+    # cmb pass-major, item-major interleave: the P passes of one persistent
+    # slot are neighbouring workgroups on one XCD (workgroup w: XCD w % 8, pass
+    # (w >> 3) mod P, slot 8 ((w >> 3) div P) + w % 8), so they walk the same
+    # items together and the later passes' syndrome reads hit that XCD's L2;
+    # kernarg word 33 = (ceil(2^16 / P) << 3) | P, the grid a multiple of 8 P
+    pm_xcd: bool = False
     # enc fft, one pass of a MergedSpec built with xchg: (waves, this wave).
     # The pass-independent row work (loads, transposes, the chunks' inverse
     # butterflies) is split over the workgroup's waves by chunk and handed
@@ -577,7 +601,8 @@ class KernelSpec:
     @property
     def name(self) -> str:
         if self.mode == "cmb":
-            return f"qf_combine_bs_r{self.r}" + ("_pm" if self.pass_major else "")
+            return (f"qf_combine_bs_r{self.r}" + ("_pmx" if self.pm_xcd else "_pm" if self.pass_major else "")
+                    + (f"_j{self.cmb_jump}" if self.cmb_jump else ""))
         tag = {"enc": "bss" if self.ksplit > 1 else "bs", "syn": "syn", "dec": "dec", "synw": "synw"}[self.mode]
         if self.chunked:
             tag = "decs" if self.ksplit > 1 else ("decx" if self.cx else "decc")
@@ -3381,14 +3406,17 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
             a, b = _COMBO_BUILD[m]
             E(Op("v_xor", (tab + m, tab + a, tab + b)))
     E(Op("s_waitcnt_lgkm", ()))
-    # index rows of output 0's coefficient
-    E(Op("s_bfe_k", (CS_T0, CS_REC, 0, 8)))
-    E(Op("s_lshl", (CS_T0, CS_T0, 6)))
-    E(Op("s_load_n", (CS_IDX[0], 22, 16, CS_T0, 0)))
+    if not spec.cmb_jump:   # index rows of output 0's coefficient
+        E(Op("s_bfe_k", (CS_T0, CS_REC, 0, 8)))
+        E(Op("s_lshl", (CS_T0, CS_T0, 6)))
+        E(Op("s_load_n", (CS_IDX[0], 22, 16, CS_T0, 0)))
     def rec_sgpr(j: int) -> int:   # the SGPR holding output j's coefficient byte
         return CS_REC + j // 4 if j < 16 else CS_REC2 + (j - 16) // 4
 
     lean = spec.cmb_lean
+    if spec.cmb_jump:
+        _cmb_jump_products(E, spec, rec_sgpr, tag)
+        return
     for j in range(spec.r):
         if j and (not lean or j % 4 == 0):
             E(Op("s_cmp_le_k_br", (CS_EW, j, f".Lpe{tag}")))
@@ -3412,6 +3440,50 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     E(Op("s_waitcnt_lgkm", ()))
 
 
+CJ_J8, CJ_TGT, CJ_RET, CJ_TAB = 56, 72, 74, 76   # jump products: 8 j by output (s56..s71), call pair, table
+CJ_BLOCK = 128                                   # bytes per coefficient block (a power of two)
+CJ_FAKE_TAB = 0x7F0000000000                     # the emulator's table address
+
+
+def _cmb_jump_products(E, spec: KernelSpec, rec_sgpr, tag: str):
+    """Row products as calls into the coefficient blocks (KernelSpec.cmb_jump):
+    index 8 j on the destination (and the accumulator source), block c =
+    output j's record byte; every 4 outputs the early exit (lean)."""
+    assert spec.r <= 16 and spec.cmb_lean
+    E(Op("s_idx_on_d3" if spec.cmb_jump == 3 else "s_idx_on_d2", (CJ_J8,)))
+    for j in range(spec.r):
+        if j and j % 4 == 0:
+            E(Op("s_cmp_le_k_br", (CS_EW, j, f".Lpe{tag}")))
+        if j:
+            E(Op("s_idx", (CJ_J8 + j,)))
+        E(Op("s_bfe_k", (CS_T0, rec_sgpr(j), 8 * (j % 4), 8)))
+        E(Op("s_lshl", (CS_T0, CS_T0, CJ_BLOCK.bit_length() - 1)))
+        E(Op("s_add_cc", (CJ_TGT, CJ_TAB, CS_T0)))
+        E(Op("s_addck", (CJ_TGT + 1, CJ_TAB + 1, 0)))
+        E(Op("s_call", (CJ_RET, CJ_TGT)))
+    E(Op("label", (f".Lpe{tag}",)))
+    E(Op("s_idx_off", ()))
+
+
+def _cmb_jump_table(E, spec: KernelSpec):
+    """After s_endpgm: the 256 coefficient blocks, CJ_BLOCK bytes apart from
+    .Ltab (acc_j[p] ^= LO[row p of M_c & 15] ^ HI[row p >> 4], j by gpr_idx)."""
+    tab = cmb_index_table()
+    E(Op("align7", ()))
+    E(Op("label", (".Ltab",)))
+    for c in range(256):
+        E(Op("label", (f".Lblk{c}",)))
+        for p in range(8):
+            a, b = int(tab[c, 2 * p]), int(tab[c, 2 * p + 1])
+            if spec.cmb_jump == 3:
+                E(Op("v_xor3_reld", (C_ACC + p, C_LO + a, C_HI + b)))
+            else:
+                E(Op("v_xor_reld", (C_ACC + p, C_LO + a)))
+                E(Op("v_xor_reld", (C_ACC + p, C_HI + b)))
+        E(Op("s_ret", (CJ_RET,)))
+        E(Op("align7", ()))
+
+
 def _generate_cmb(spec: KernelSpec) -> list[Op]:
     ops: list[Op] = []
     E = ops.append
@@ -3430,12 +3502,43 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
         E(Op("v_movs", (C_VM + q, CS_MASKS + q)))
     E(Op("v_movk", (C_LO, 0)))
     E(Op("v_movk", (C_HI, 0)))
-    if spec.pass_major:
+    if spec.cmb_jump:
+        assert spec.cmb_jump in (2, 3) and 8 * 8 + 4 <= CJ_BLOCK   # 8 VOP3 or 16 VOP2 + the return
+        E(Op("s_getpc_rel", (CJ_TAB, ".Ltab")))
+        for j in range(R):
+            E(Op("s_movk", (CJ_J8 + j, 8 * j)))
+    assert not spec.pm_xcd or spec.pass_major
+    if spec.pm_xcd:   # records' pass stride; word 33: (magic << 3) | passes
+        E(Op("s_load_n", (CS_T1, 0, 2, None, KERNARG_BYTES_CMB)))
+    elif spec.pass_major:
         E(Op("s_load_n", (CS_T1, 0, 1, None, KERNARG_BYTES_CMB)))   # records' pass stride
     if R > 16:
         E(Op("s_load_n", (CS_PSTRIDE, 0, 1, None, KERNARG_BYTES_CMB)))
     E(Op("s_waitcnt_lgkm", ()))
-    if spec.pass_major:
+    if spec.pm_xcd:
+        # workgroup w = 8 h + x: pass p = h mod P, slot 8 (h div P) + x, with
+        # h div P = (h * ceil(2^16 / P)) >> 16 (exact for h < 2^15, P <= 4)
+        E(Op("s_andk", (36, 2, 7)))                  # x
+        E(Op("s_lshrk", (37, 2, 3)))                 # h
+        E(Op("s_lshrk", (38, CS_T1 + 1, 3)))         # magic
+        E(Op("s_andk", (39, CS_T1 + 1, 7)))          # P
+        E(Op("s_mul", (40, 37, 38)))
+        E(Op("s_lshrk", (40, 40, 16)))               # q = h div P
+        E(Op("s_mul", (41, 40, 39)))
+        E(Op("s_sub", (41, 37, 41)))                 # p = h - q P
+        E(Op("s_lshl", (2, 40, 3)))
+        E(Op("s_add", (2, 2, 36)))                   # the slot
+        E(Op("s_movk", (17, 0)))
+        for _ in range(3):
+            E(Op("s_cmp_ge_br", (17, 41, ".Lpm_done")))
+            E(Op("s_addk", (17, 17, 1)))
+            E(Op("s_add", (14, 14, CS_T1)))
+            E(Op("s_addck", (15, 15, 0)))
+            E(Op("s_lshl", (CS_TMP64, 13, 4)))
+            E(Op("s_add", (6, 6, CS_TMP64)))
+            E(Op("s_addck", (7, 7, 0)))
+        E(Op("label", (".Lpm_done",)))
+    elif spec.pass_major:
         # workgroups [p n, (p + 1) n) run pass p (n = grid waves / 4): the
         # pass, its records and its 16 output rows, and the workgroup id in
         # the pass's range (at most 4 passes: e <= 64)
@@ -3566,15 +3669,26 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     E(Op("s_branch", (".Litem",)))
     E(Op("label", (".Lend",)))
     E(Op("s_endpgm", ()))
+    if spec.cmb_jump:
+        _cmb_jump_table(E, spec)
     return ops
+
+
+def pm_xcd_word(passes: int) -> int:
+    """Kernarg word 33 of the interleaved pass-major payload kernel
+    (KernelSpec.pm_xcd): (ceil(2^16 / P) << 3) | P."""
+    assert 2 <= passes <= 4
+    return (-(-65536 // passes) << 3) | passes
 
 
 def cmb_kernargs(rows: int, dst: int, rgs: int, dgs: int, rs: int, drs: int, coef: int, cgs: int, pas: int,
                  n_out: int, bound: int, idxtab: int, L: int, G: int, total_waves: int,
-                 rows_offs: int = 0, dst_offs: int = 0, pass_stride: Optional[int] = None) -> tuple[bytes, int]:
+                 rows_offs: int = 0, dst_offs: int = 0, pass_stride: Optional[int] = None,
+                 pm_xcd_passes: int = 0) -> tuple[bytes, int]:
     """Kernarg block of qf_combine_bs (layout above) and the item count;
     pass_stride: the pass-major kernel's word 32 (records of pass p at
-    coef + p pass_stride, its outputs at dst + 16 p drs)."""
+    coef + p pass_stride, its outputs at dst + 16 p drs); pm_xcd_passes: the
+    interleaved pass-major kernel's pass count (word 33, pm_xcd_word)."""
     Lu = (L + 15) // 16
     Q = (Lu + 1) // 2
     ipg = (Q + 63) // 64
@@ -3585,7 +3699,7 @@ def cmb_kernargs(rows: int, dst: int, rgs: int, dgs: int, rs: int, drs: int, coe
              bound >> 32, idxtab & MASK32, idxtab >> 32, rows_offs & MASK32, rows_offs >> 32,
              dst_offs & MASK32, dst_offs >> 32, L, Lu, Q, ipg, n_items, total_waves, magic, shift]
     if pass_stride is not None:
-        words += [pass_stride, 0]
+        words += [pass_stride, pm_xcd_word(pm_xcd_passes) if pm_xcd_passes else 0]
     for w in words:
         assert 0 <= w < 1 << 32, words
     return np.array(words, np.uint32).tobytes(), n_items
@@ -3939,6 +4053,7 @@ class Emulator:
         steps = 0
         pend_s = []        # s_load_n: (first SGPR, values) written at the next lgkmcnt(0)
         idx_mode, m0 = False, 0
+        idx_dst, call_ret = False, None   # gpr_idx on the destination (jump products); the open call
 
         def retire_s():
             for d0, w in pend_s:
@@ -3952,11 +4067,11 @@ class Emulator:
             steps += 1
             n, a = op.name, op.args
             self.executed[n] = self.executed.get(n, 0) + 1
-            if idx_mode and n.startswith("v_") and n != "v_xor_rel":
+            if idx_mode and n.startswith("v_") and n not in ("v_xor_rel", "v_xor3_reld", "v_xor_reld"):
                 raise EmuError(f"{n} while the gpr_idx mode is on")
             if n == "s_waitcnt_lgkm" or (n == "s_waitcnt_lgkm_n" and a[0] == 0):
                 retire_s()
-            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger", "stamp"):
+            if n in ("label", "s_nop", "s_waitcnt_lgkm", "s_setprio", "s_stagger", "stamp", "align7"):
                 continue
             if n == "s_load_args":
                 for q in range(20):
@@ -4274,14 +4389,38 @@ class Emulator:
                 s[a[0]] = s[a[1]] if scc else s[a[2]]
             elif n == "v_min_s":
                 wv(a[0], np.minimum(rv(a[2]), np.uint64(s[a[1]])))
-            elif n in ("s_idx_on", "s_idx"):
+            elif n in ("s_idx_on", "s_idx", "s_idx_on_d3", "s_idx_on_d2"):
                 if n == "s_idx" and not idx_mode:
                     raise EmuError("s_set_gpr_idx_idx outside the gpr_idx mode")
+                if n != "s_idx":
+                    idx_dst = n != "s_idx_on"
                 idx_mode, m0 = True, s[a[0]] & 0xFF
+            elif n == "s_getpc_rel":
+                s[a[0]], s[a[0] + 1] = CJ_FAKE_TAB & MASK32, CJ_FAKE_TAB >> 32
+            elif n == "s_call":
+                if call_ret is not None:
+                    raise EmuError("nested s_swappc")
+                off = (s[a[1]] | (s[a[1] + 1] << 32)) - CJ_FAKE_TAB
+                if off % CJ_BLOCK or not 0 <= off < 256 * CJ_BLOCK:
+                    raise EmuError(f"call outside the coefficient table (offset {off})")
+                s[a[0]], s[a[0] + 1] = 0xC0DE, 0
+                call_ret, pc = pc, self.labels[f".Lblk{off // CJ_BLOCK}"]
+            elif n == "s_ret":
+                if call_ret is None or s[a[0]] != 0xC0DE:
+                    raise EmuError("s_setpc without a call")
+                pc, call_ret = call_ret, None
+            elif n in ("v_xor3_reld", "v_xor_reld"):
+                if not (idx_mode and idx_dst):
+                    raise EmuError(f"{n} outside the destination gpr_idx mode")
+                d = a[0] + m0
+                if d >= 256:
+                    raise EmuError(f"indexed destination v{d}")
+                x = rv(d) ^ rv(a[1])
+                wv(d, x ^ rv(a[2]) if n == "v_xor3_reld" else x)
             elif n == "s_idx_off":
                 idx_mode = False
             elif n == "v_xor_rel":
-                if not idx_mode:
+                if not idx_mode or idx_dst:
                     raise EmuError("v_xor_rel outside the gpr_idx mode")
                 wv(a[0], rv(a[1] + m0) ^ rv(a[2]))
             elif n == "store_byte":

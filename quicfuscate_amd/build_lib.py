@@ -310,6 +310,9 @@ def kernel_specs() -> list:
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", cmb_lean=True))
     # ... and every pass of it in one pass-major launch ('P', QF_ENCODE_MERGED)
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True))
+    # ... and its item-major interleave ('Q', QF_COMBINE_XCD): the passes of
+    # one slot on one XCD at once, the later passes' syndrome reads from L2
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True, pm_xcd=True))
     # ... and the wide single pass for 17-24 outputs (QF_COMBINE_WIDE): each
     # input row read and transposed once instead of once per pass
     # (e = 20: 1.60 -> 1.34 ms, tools/cmb_lab.py, profiles/r05ay_cmb_lab.json)
@@ -352,7 +355,7 @@ def _bs_kernels(build_dir: Path) -> Path:
         elif spec.mode == "enc" and spec.ksplit > 1:
             mode = "f"
         else:
-            mode = {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": "P" if spec.pass_major else "m"}[spec.mode]
+            mode = {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": ("Q" if spec.pm_xcd else "P") if spec.pass_major else "m"}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, {len(data)}u, {getattr(spec, 'waves', 4)}u, "
                        f"{getattr(spec, 'n_passes', 1)}u, sizeof(qf_bs_blob_{n})}},")

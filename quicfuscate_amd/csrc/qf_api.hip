@@ -212,6 +212,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* ENCODE_MERGED */ {"QF_ENCODE_MERGED", 1, 0, 1, false},
     /* SYNW_SHARED */ {"QF_SYNW_SHARED", 1, 0, 1, false},
     /* COMBINE_WIDE */ {"QF_COMBINE_WIDE", 1, 0, 1, false},
+    /* COMBINE_XCD */ {"QF_COMBINE_XCD", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }

@@ -373,6 +373,14 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // per item, wave-uniform coefficients (kernarg layout: bs_codegen.cmb_kernargs)
 bool cmb_available() { return find('m', 0, 16) != nullptr; }
 bool cmb_pass_major_available() { return find('P', 0, 16) != nullptr; }
+// the pass-major payload pass item-major ('Q', QF_COMBINE_XCD): workgroup w
+// runs pass (w >> 3) mod P for slot 8 ((w >> 3) div P) + w % 8, so the P
+// passes of a slot are neighbours on one XCD (dispatch w -> XCD w % 8) and
+// their syndrome reads after the first come from that XCD's L2
+static const QfBsEntry* cmb_pm_entry(BsCache& cache, uint32_t passes) {
+    const QfBsEntry* q = cache.get(QF_OPT_COMBINE_XCD) ? find('Q', 0, 16) : nullptr;
+    return q && passes >= 2 && passes <= 4 ? q : find('P', 0, 16);
+}
 
 bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_stride) {
     return passes > 1 && passes <= kCmbMaxPasses && pass_stride < (1ull << 32) &&
@@ -385,6 +393,10 @@ bool cmb_wide_ok(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uin
            24ull * a.dst_row_stride < (1ull << 32) && cache.get(QF_OPT_COMBINE_WIDE) && find('m', 0, 24) != nullptr;
 }
 
+// kernarg word 33 of the interleaved pass-major kernel (bs_codegen.pm_xcd_word):
+// (ceil(2^16 / P) << 3) | P, the kernel's h div P by multiply and shift
+static uint32_t pm_xcd_word(uint32_t passes) { return ((65536u + passes - 1) / passes) << 3 | passes; }
+
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
                       const uint32_t* idxtab, uint32_t passes, uint64_t pass_stride, uint32_t e_max) {
     // the wide pass: 24 outputs per item (192 accumulator VGPRs, still two
@@ -393,7 +405,8 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     // instead of once per 16-output pass (output j's row at j * dst stride:
     // a 32-bit product in the kernel)
     const bool wide = cmb_wide_ok(cache, a, passes, pass_stride, e_max);
-    const QfBsEntry* e = wide ? find('m', 0, 24) : find(passes > 1 ? 'P' : 'm', 0, 16);
+    const QfBsEntry* e = wide ? find('m', 0, 24) : passes > 1 ? cmb_pm_entry(cache, passes) : find('m', 0, 16);
+    const bool xcd = e && e->mode == 'Q';
     if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || 16ull * a.dst_row_stride >= (1ull << 32) ||
         a.coef_gen_stride >= (1ull << 32) || passes == 0 || (passes > 1 && a.pass != 0) ||
         (passes > 1 && !wide && !cmb_pass_major_ok(passes, a.dst_row_stride, pass_stride)))
@@ -415,6 +428,7 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     uint64_t blocks = (n_items + 3) / 4;
     const uint64_t cap = (uint64_t)(num_cus > 0 ? num_cus : 256) * 2;
     if (blocks > cap) blocks = cap;
+    if (xcd) blocks = (blocks + 7) / 8 * 8;   // slots in groups of 8, one per XCD: a grid of 8 P-blocks
     auto lo = [](const void* p) { return (uint32_t)(uintptr_t)p; };
     auto hi = [](const void* p) { return (uint32_t)((uintptr_t)p >> 32); };
     uint32_t w[34] = {lo(a.rows), hi(a.rows), lo(a.dst), hi(a.dst),
@@ -424,9 +438,10 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
                       (uint32_t)a.coef_gen_stride, a.pass, lo(a.n_out), hi(a.n_out), lo(a.bound), hi(a.bound),
                       lo(idxtab), hi(idxtab), lo(a.rows_offs), hi(a.rows_offs), lo(a.dst_offs), hi(a.dst_offs),
                       a.L, Lu, Q, ipg, (uint32_t)n_items, (uint32_t)blocks * 4, magic, shift,
-                      (uint32_t)pass_stride, 0};
-    // (pass-major: words 32..33 = the records' pass stride; the grid holds
-    // every pass's `blocks` workgroups, pass p's at [p blocks, (p + 1) blocks))
+                      (uint32_t)pass_stride, xcd ? pm_xcd_word(passes) : 0u};
+    // (pass-major: word 32 = the records' pass stride; the grid holds every
+    // pass's `blocks` workgroups, pass p's at [p blocks, (p + 1) blocks), or
+    // interleaved ('Q': word 33 = pm_xcd_word(passes)))
     // (the wide pass: word 32 too, one pass's grid)
     size_t sz = passes > 1 ? sizeof(w) : 32 * sizeof(uint32_t);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, w, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};

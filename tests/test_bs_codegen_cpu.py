@@ -858,14 +858,14 @@ def _gf_table():
 _GFT = None
 
 
-def _cmb_case(L, G, seed, pas=0, offs=False, R=16, lean=False, pf2=False):
+def _cmb_case(L, G, seed, pas=0, offs=False, R=16, lean=False, pf2=False, jump=0):
     """qf_combine_bs on the emulator: out[j] = sum_{s < bound[g]} rec[g][s][j] *
     rows[g][s] for j < min(e[g] - 16 pass, R), bytes [0, L) only."""
     global _GFT
     if _GFT is None:
         _GFT = _gf_table()
     rng = np.random.default_rng(seed)
-    spec = bs.KernelSpec(0, R, mode="cmb", cmb_lean=lean, cmb_pf2=pf2)
+    spec = bs.KernelSpec(0, R, mode="cmb", cmb_lean=lean, cmb_pf2=pf2, cmb_jump=jump)
     Lp = (L + 15) // 16 * 16
     rs, drs = Lp + 32, Lp + 48
     nslot = 24
@@ -915,7 +915,7 @@ def _cmb_case(L, G, seed, pas=0, offs=False, R=16, lean=False, pf2=False):
     return bad
 
 
-@pytest.mark.parametrize("lean,pf2", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("lean,pf2,jump", [(False, False, 0), (True, False, 0), (True, True, 0), (True, False, 3)])
 @pytest.mark.parametrize("L,G,seed,pas,offs", [
     (64, 5, 1, 0, False),       # Lu = 4, Q = 2: one item per generation
     (100, 4, 2, 0, False),      # partial last unit (4 bytes)
@@ -924,22 +924,25 @@ def _cmb_case(L, G, seed, pas=0, offs=False, R=16, lean=False, pf2=False):
     (33, 3, 5, 0, True),        # Lu = 3: unit B of lane 0 is the partial last unit
     (200, 9, 6, 0, False),      # e of every residue mod 4 (lean: products past e, never stored)
 ])
-def test_emulated_combine_bs(L, G, seed, pas, offs, lean, pf2):
-    assert _cmb_case(L, G, seed, pas, offs, lean=lean, pf2=pf2) == 0
+def test_emulated_combine_bs(L, G, seed, pas, offs, lean, pf2, jump):
+    assert _cmb_case(L, G, seed, pas, offs, lean=lean, pf2=pf2, jump=jump) == 0
 
 
-@pytest.mark.parametrize("lean,pf2", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("lean,pf2,xcd,jump", [(False, False, False, 0), (True, False, False, 0), (True, True, False, 0),
+                                               (True, False, True, 0), (True, False, True, 3), (True, False, False, 2)])
 @pytest.mark.parametrize("L,G,P,offs", [(1200, 5, 3, False), (4100, 3, 2, True), (100, 9, 4, False)])
-def test_emulated_combine_bs_pass_major(L, G, P, offs, lean, pf2):
+def test_emulated_combine_bs_pass_major(L, G, P, offs, lean, pf2, xcd, jump):
     """Every payload pass in one launch (qf_combine_bs_r16_pm): workgroup
     range p runs pass p with its records at coef + p * pass_stride and its
     outputs at rows 16 p ..; generations with fewer outputs leave the later
-    passes' rows untouched."""
+    passes' rows untouched. xcd: the interleaved form (qf_combine_bs_r16_pmx),
+    pass (w >> 3) mod P of workgroup w, on a grid of 8 slots per pass; jump:
+    the products as calls into the coefficient blocks (KernelSpec.cmb_jump)."""
     global _GFT
     if _GFT is None:
         _GFT = _gf_table()
     rng = np.random.default_rng(L + G + P)
-    spec = bs.KernelSpec(0, 16, mode="cmb", pass_major=True, cmb_lean=lean, cmb_pf2=pf2)
+    spec = bs.KernelSpec(0, 16, mode="cmb", pass_major=True, cmb_lean=lean, cmb_pf2=pf2, pm_xcd=xcd, cmb_jump=jump)
     Lp = (L + 15) // 16 * 16
     rs, drs = Lp + 32, Lp + 48
     nslot = 16 * P + 4
@@ -964,9 +967,9 @@ def test_emulated_combine_bs_pass_major(L, G, P, offs, lean, pf2):
     for base, buf in ((ROWS, rows), (OUT, out), (REC, rec), (NO, e), (BD, bound),
                       (TAB, bs.cmb_index_table().reshape(-1).view(np.uint8))):
         emu.add_buffer(base, buf.view(np.uint8))
-    n = 2                                   # workgroups per pass (persistent: items stride 8 waves)
+    n = 8 if xcd else 2                     # workgroups per pass (persistent: items stride 4 n waves)
     ka, n_items = bs.cmb_kernargs(ROWS, OUT, rgs_k, dgs_k, rs, drs, REC, cgs, 0, NO, BD, TAB, L, G, 4 * n,
-                                  rows_offs=so, dst_offs=do, pass_stride=PS)
+                                  rows_offs=so, dst_offs=do, pass_stride=PS, pm_xcd_passes=P if xcd else 0)
     for wg in range(P * n):
         for w in range(4):
             emu.run_wave(ka, wg, w)

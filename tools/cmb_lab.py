@@ -27,15 +27,23 @@ RS = 9008
 # (name, e, R, pass_major, KernelSpec keyword overrides); the first variant of
 # each e is the reference the others' outputs are compared with
 VARIANTS = [
-    # round 5ba: input rows two ahead (KernelSpec.cmb_pf2, a third row buffer)
+    # round 6: the passes of one slot interleaved on one XCD (KernelSpec.pm_xcd);
+    # the products as calls into per-coefficient code blocks (cmb_jump 3 / 2)
     ("e39_lean", 39, 16, True, {"cmb_lean": True}),
-    ("e39_lean_pf2", 39, 16, True, {"cmb_lean": True, "cmb_pf2": True}),
-    ("e20_wide_lean", 20, 24, False, {"cmb_lean": True}),
-    ("e20_pm_lean_pf2", 20, 16, True, {"cmb_lean": True, "cmb_pf2": True}),
+    ("e39_lean_xcd", 39, 16, True, {"cmb_lean": True, "pm_xcd": True}),
+    ("e39_xcd_j3", 39, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
+    ("e39_xcd_j2", 39, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 2}),
     ("e39_lean_2", 39, 16, True, {"cmb_lean": True}),
-    ("e39_lean_pf2_2", 39, 16, True, {"cmb_lean": True, "cmb_pf2": True}),
-    ("e39_lean_idx_once", 39, 16, True, {"cmb_lean": True, "lab_cmb": ("idx_once",)}),
-    ("e39_lean_pf2_idx_once", 39, 16, True, {"cmb_lean": True, "cmb_pf2": True, "lab_cmb": ("idx_once",)}),
+    ("e39_lean_xcd_2", 39, 16, True, {"cmb_lean": True, "pm_xcd": True}),
+    ("e39_xcd_j3_2", 39, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
+    ("e59_lean", 59, 16, True, {"cmb_lean": True}),
+    ("e59_lean_xcd", 59, 16, True, {"cmb_lean": True, "pm_xcd": True}),
+    ("e59_xcd_j3", 59, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
+    ("e48_lean", 48, 16, True, {"cmb_lean": True}),
+    ("e48_lean_xcd", 48, 16, True, {"cmb_lean": True, "pm_xcd": True}),
+    ("e48_xcd_j3", 48, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
+    ("e16_m", 16, 16, False, {"cmb_lean": True}),
+    ("e16_m_j3", 16, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
 ]
 
 
@@ -95,9 +103,12 @@ def run(nbytes: float, reps: int):
         ipg = ((Lu + 1) // 2 + 63) // 64
         blocks = min((G * ipg + 3) // 4, 2 * 256)
         passes = P if m["pm"] else 1
+        xcd = bool(m["kw"].get("pm_xcd"))
+        if xcd:   # slots in groups of 8 (one per XCD)
+            blocks = (blocks + 7) // 8 * 8
         ka, _ = bs.cmb_kernargs(rows.data_ptr(), dst.data_ptr(), e * RS, e * RS, RS, RS, rec.data_ptr(), cgs, 0,
                                 n_out.data_ptr(), bound.data_ptr(), idxtab.data_ptr(), L, G, 4 * blocks,
-                                pass_stride=PS)
+                                pass_stride=PS, pm_xcd_passes=passes if xcd else 0)
         kbuf = ctypes.create_string_buffer(ka, len(ka))
         size = ctypes.c_size_t(len(ka))
         extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,

@@ -7,6 +7,7 @@
 #   TAG=r05a tools/gpu.sh full                     -m gpu suite, smoke, one default bench line
 #   TAG=r05a tools/gpu.sh bench [bench args...]    one bench line (+ detail record)
 #   TAG=r05a tools/gpu.sh prof                     bench line, kernel trace, SQ counters, FETCH / WRITE passes
+#   TAG=r06a tools/gpu.sh cmblab                   payload-pass lab (tools/cmb_lab.py) + FETCH / WRITE per variant
 #   TAG=r05a tools/gpu.sh run <command...>         any command, under a 600 s limit
 #   TAG=r05a C5_SHAPES="196,59;160,48" AB_ENV=QF_SYNW_SHARED=0 [C5_TESTK="..."] tools/gpu.sh c5ab
 #        C5 GPU tests, then block GiB/s of the shapes: library (a) against AB_ENV (b), alternating twice
@@ -84,6 +85,17 @@ case "$what" in
   declab)   # tools/dec_lab.py run (build the variants here first: python tools/dec_lab.py build)
     timeout -k 10 300 python3 tools/dec_lab.py run --reps 10 --out "$OUT/dec_lab.json" "$@" > "$OUT/dec_lab.log" 2>&1
     tail -20 "$OUT/dec_lab.log"
+    ;;
+  cmblab)   # tools/cmb_lab.py run + FETCH / WRITE passes per variant (build here first: python tools/cmb_lab.py build)
+    CL="python3 tools/cmb_lab.py run --reps 10"
+    timeout -k 10 300 $CL --out "$OUT/cmb_lab.json" > "$OUT/cmb_lab.log" 2>&1
+    tail -12 "$OUT/cmb_lab.log"
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/cmbfetch" -o f -- \
+      $CL --reps 2 --out /tmp/cmbx.json > "$OUT/cmbfetch.log" 2>&1
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/cmbwrite" -o w -- \
+      $CL --reps 2 --out /tmp/cmbx.json > "$OUT/cmbwrite.log" 2>&1
+    python3 tools/c5_pmc_summary.py "$OUT/cmbfetch" "$OUT/cmbwrite" --match cmb_ --out "$OUT/cmb_pmc.json"
+    echo CMBLAB_OK
     ;;
   c5pmc)    # counters of the C5 kernels of one shape (C5_SHAPES, default 196,59): block encode + decode
     SH="${C5_SHAPES:-196,59}"

@@ -71,6 +71,16 @@ def body(kind: str) -> list[str]:
         for p in range(8):
             ops.append(f"v_bitop3_b32 v{ACC + 4 * p}, v{LO + 1 + 4 * (p % 4)}, v{HI + 2 + 4 * (p % 3)}, v63 bitop3:0xd8")
             ops.append(f"v_bitop3_b32 v{ACC + 4 * p + 1}, v{LO + 2 + 4 * (p % 3)}, v{HI + 3 + 4 * (p % 3)}, v63 bitop3:0xd8")
+    elif kind in ("jump_xor3", "jump_xor3_noidx"):
+        # one product per call: acc_j[p] ^= LO[a_p(c)] ^ HI[b_p(c)] for p < 8 in
+        # the coefficient's code block (JUMP_BLOCK bytes at .Ltab + c * 128),
+        # acc_j chosen by gpr_idx (DST, SRC0) = 8 j; 8 products per body
+        for i, c in enumerate(JUMP_CS):
+            if kind == "jump_xor3":
+                ops.append(f"s_set_gpr_idx_idx s{24 + (i % 2)}")
+            ops.append(f"s_add_u32 s42, s40, s{8 + i}")
+            ops.append("s_addc_u32 s43, s41, 0")
+            ops.append("s_swappc_b64 s[44:45], s[42:43]")
     elif kind == "plain_salu":   # same SALU count as idx, no indexing
         for p in range(8):
             ops.append(f"s_mov_b32 s{40 + 2 * p}, s{8 + 2 * p}")
@@ -78,6 +88,27 @@ def body(kind: str) -> list[str]:
             ops.append(f"s_mov_b32 s{41 + 2 * p}, s{9 + 2 * p}")
             ops.append(f"v_xor_b32_e32 v{ACC + p}, v{HI + 15 - p}, v{ACC + p}")
     return ops
+
+
+JUMP_CS = (3, 77, 140, 201, 18, 255, 96, 5)    # the body's coefficients, in order
+
+
+def jump_ab(c: int, p: int) -> tuple[int, int]:
+    """The LO / HI table entries plane p of coefficient c's block reads
+    (arbitrary but distinct per plane: the check recomputes them)."""
+    return (c + 5 * p) & 15, (3 * c + p) & 15
+
+
+def jump_table(kind: str) -> list[str]:
+    """256 blocks of 128 B: 8 v_bitop3 (xor3) and the return."""
+    lines = ["s_endpgm", ".p2align 7", ".Ltab:"]
+    for c in range(256):
+        for p in range(8):
+            a, b = jump_ab(c, p)
+            lines.append(f"v_bitop3_b32 v{ACC + p}, v{ACC + p}, v{LO + a}, v{HI + b} bitop3:0x96")
+        lines.append("s_setpc_b64 s[44:45]")
+        lines.append(".p2align 7")
+    return lines
 
 
 def kernel(name: str, kind: str, unroll: int = 4) -> str:
@@ -94,22 +125,41 @@ def kernel(name: str, kind: str, unroll: int = 4) -> str:
         lines.append(f"v_lshlrev_b32_e32 v{HI + i}, 16, v{LO + i}")
     lines.append("s_mov_b32 s30, 0x0f0f0f0f")
     lines.append("v_mov_b32_e32 v63, s30")
-    for p in range(8):
-        lines.append(f"s_mov_b32 s{8 + 2 * p}, {p}")
-        lines.append(f"s_mov_b32 s{9 + 2 * p}, {15 - p}")
+    jump = kind.startswith("jump")
+    if jump:   # block offsets of the body's coefficients; the table's address; gpr_idx 0 / 8
+        for i, c in enumerate(JUMP_CS):
+            lines.append(f"s_mov_b32 s{8 + i}, {c * 128}")
+        lines += ["s_getpc_b64 s[40:41]", ".Lpc:", "s_add_u32 s40, s40, .Ltab-.Lpc", "s_addc_u32 s41, s41, 0",
+                  "s_mov_b32 s24, 0", "s_mov_b32 s25, 8"]
+        if kind == "jump_xor3":
+            lines.append("s_set_gpr_idx_on s24, gpr_idx(SRC0,DST)")
+    else:
+        for p in range(8):
+            lines.append(f"s_mov_b32 s{8 + 2 * p}, {p}")
+            lines.append(f"s_mov_b32 s{9 + 2 * p}, {15 - p}")
     lines.append("s_waitcnt lgkmcnt(0)")
     lines.append(".Lloop:")
     for _ in range(unroll):
         lines += body(kind)
     lines += ["s_sub_u32 s6, s6, 1", "s_cmp_lg_u32 s6, 0", "s_cbranch_scc1 .Lloop"]
-    # out + (workgroup * 256 + tid) * 32
-    lines += ["s_lshl_b32 s7, s2, 13", "v_lshlrev_b32_e32 v4, 5, v0", "v_add_u32_e32 v4, s7, v4",
+    if kind == "jump_xor3":
+        lines.append("s_set_gpr_idx_off")
+    # out + (workgroup * 256 + tid) * 32 (jump kinds: * 64, two accumulator sets)
+    sh = 6 if jump else 5
+    lines += [f"s_lshl_b32 s7, s2, {sh + 8}", f"v_lshlrev_b32_e32 v4, {sh}, v0", "v_add_u32_e32 v4, s7, v4",
               "v_mov_b32_e32 v5, 0",
               "v_lshl_add_u64 v[10:11], v[4:5], 0, s[4:5]",
               f"global_store_dwordx4 v[10:11], v[{ACC}:{ACC + 3}], off",
-              f"global_store_dwordx4 v[10:11], v[{ACC + 4}:{ACC + 7}], off offset:16",
-              "s_endpgm"]
-    body_s = "\n".join("\t" + x if not x.endswith(":") else x for x in lines).replace(".Lloop", f".L{name}_loop")
+              f"global_store_dwordx4 v[10:11], v[{ACC + 4}:{ACC + 7}], off offset:16"]
+    if jump:   # the second accumulator set (gpr_idx 8) after the first
+        lines += [f"global_store_dwordx4 v[10:11], v[{ACC + 8}:{ACC + 11}], off offset:32",
+                  f"global_store_dwordx4 v[10:11], v[{ACC + 12}:{ACC + 15}], off offset:48"]
+        lines += jump_table(kind)
+    else:
+        lines.append("s_endpgm")
+    body_s = "\n".join("\t" + x if not x.endswith(":") else x for x in lines)
+    for lbl in (".Lloop", ".Ltab", ".Lpc"):
+        body_s = body_s.replace(lbl, f".L{name}_{lbl[2:]}")
     return f"""\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"
 \t.amdhsa_code_object_version 6
 \t.text
@@ -170,7 +220,22 @@ amdhsa.version:
 
 
 KINDS = ["idx", "plain", "plain_salu", "bitop3_banks", "bitop3_same", "xor_banks", "perm_banks", "bitsel_sgpr",
-         "bitsel_vgpr", "xor3_sgpr", "bitsel_vgpr_last"]
+         "bitsel_vgpr", "xor3_sgpr", "bitsel_vgpr_last", "jump_xor3", "jump_xor3_noidx"]
+
+
+def valu_per_body(kind: str) -> int:
+    return 8 * len(JUMP_CS) if kind.startswith("jump") else len([o for o in body(kind) if o.startswith("v_")])
+
+
+def jump_expected(kind: str, lanes: np.ndarray) -> np.ndarray:
+    """(lanes, 16) accumulators after one body of a jump kind."""
+    want = np.zeros((len(lanes), 16), np.uint32)
+    for i, c in enumerate(JUMP_CS):
+        j = (i % 2) if kind == "jump_xor3" else 0
+        for p in range(8):
+            a, b = jump_ab(c, p)
+            want[:, 8 * j + p] ^= ((lanes * 16 + a) ^ ((lanes * 16 + b) << 16)).astype(np.uint32)
+    return want
 
 
 def build():
@@ -193,7 +258,7 @@ def run(out):
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, f"idx_{k}".encode()) == 0
         for waves_per_simd in (1, 2, 4):
             blocks = 256 * waves_per_simd
-            o = torch.zeros(blocks * 256 * 8, dtype=torch.int32, device="cuda")
+            o = torch.zeros(blocks * 256 * (16 if k.startswith("jump") else 8), dtype=torch.int32, device="cuda")
 
             def launch(iters):
                 ka = np.zeros(4, np.uint32)
@@ -214,7 +279,7 @@ def run(out):
             torch.cuda.synchronize()
             ms = t0.elapsed_time(t1)
             waves = blocks * 4
-            xors = waves * iters * 4 * len([o for o in body(k) if o.startswith("v_")])
+            xors = waves * iters * 4 * valu_per_body(k)
             res[f"{k}@{waves_per_simd}w"] = {"ms": round(ms, 3),
                                              "xor_per_simd_per_ns": round(xors / 1024 / (ms * 1e6), 3)}
             print(k, waves_per_simd, res[f"{k}@{waves_per_simd}w"], flush=True)
@@ -241,6 +306,25 @@ def run(out):
     want = np.stack([(lane * 16 + p) ^ ((lane * 16 + 15 - p) << 16) for p in range(8)], axis=1).astype(np.uint32)
     res["idx_correct"] = bool((got == want).all())
     print("idx correct:", res["idx_correct"], flush=True)
+    hip.hipModuleUnload(mod)
+    for k in ("jump_xor3", "jump_xor3_noidx"):   # one body, one iteration
+        mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        data = (OUT / f"idx_check_{k}.hsaco").read_bytes()
+        buf = ctypes.create_string_buffer(data, len(data))
+        assert hip.hipModuleLoadData(ctypes.byref(mod), buf) == 0
+        assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, f"idx_check_{k}".encode()) == 0
+        o = torch.zeros(256 * 16, dtype=torch.int32, device="cuda")
+        ka[0], ka[1], ka[2] = o.data_ptr() & 0xFFFFFFFF, o.data_ptr() >> 32, 1
+        kb = ctypes.create_string_buffer(ka.tobytes(), 16)
+        extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kb, ctypes.c_void_p), 2,
+                                     ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+        assert hip.hipModuleLaunchKernel(fn, 1, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(stream.cuda_stream), None,
+                                         extra) == 0
+        torch.cuda.synchronize()
+        got = o.cpu().numpy().view(np.uint32).reshape(256, 16)
+        res[f"{k}_correct"] = bool((got == jump_expected(k, lane)).all())
+        print(k, "correct:", res[f"{k}_correct"], flush=True)
+        hip.hipModuleUnload(mod)
     Path(out).parent.mkdir(exist_ok=True)
     Path(out).write_text(json.dumps(res, indent=1))
 
@@ -254,5 +338,7 @@ if __name__ == "__main__":
         build()
         from quicfuscate_amd.build_lib import assemble
         print(assemble("idx_check", kernel("idx_check", "idx", unroll=1), OUT))
+        for k in ("jump_xor3", "jump_xor3_noidx"):
+            print(assemble(f"idx_check_{k}", kernel(f"idx_check_{k}", k, unroll=1), OUT))
     else:
         run(a.out)
