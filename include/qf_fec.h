@@ -182,7 +182,13 @@ enum {
     QF_OPT_COMBINE_XCD,          /* 1: the pass-major payload pass item-major: the passes of one
                                     generation's lane-chunk run together on one XCD, so the later
                                     passes read the syndrome rows from its L2 instead of HBM; 0: pass
-                                    p's workgroups after pass p - 1's [QF_COMBINE_XCD; default 1] */
+                                    p's workgroups after pass p - 1's [QF_COMBINE_XCD; default 0:
+                                    where the last pass is short it runs ahead of the others and the
+                                    reuse is lost, 5 % slower at e = 39 / 59, DESIGN 3.7] */
+    QF_OPT_COMBINE_JUMP,         /* 1: the bit-sliced payload pass multiplies by a runtime coefficient c
+                                    with a call into c's code block (8 destination-indexed 3-input
+                                    XORs); 0: M0-indexed XORs, one index write per XOR
+                                    [QF_COMBINE_JUMP; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

@@ -3440,7 +3440,9 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     E(Op("s_waitcnt_lgkm", ()))
 
 
-CJ_J8, CJ_TGT, CJ_RET, CJ_TAB = 56, 72, 74, 76   # jump products: 8 j by output (s56..s71), call pair, table
+# jump products: 8 j by output (s56..s79, the index-row buffers' SGPRs), the
+# call target, the return address, the table's address
+CJ_J8, CJ_TGT, CJ_RET, CJ_TAB = 56, 80, 82, 84
 CJ_BLOCK = 128                                   # bytes per coefficient block (a power of two)
 CJ_FAKE_TAB = 0x7F0000000000                     # the emulator's table address
 
@@ -3449,7 +3451,7 @@ def _cmb_jump_products(E, spec: KernelSpec, rec_sgpr, tag: str):
     """Row products as calls into the coefficient blocks (KernelSpec.cmb_jump):
     index 8 j on the destination (and the accumulator source), block c =
     output j's record byte; every 4 outputs the early exit (lean)."""
-    assert spec.r <= 16 and spec.cmb_lean
+    assert spec.r <= 24 and spec.cmb_lean and CJ_J8 + spec.r <= CJ_TGT
     E(Op("s_idx_on_d3" if spec.cmb_jump == 3 else "s_idx_on_d2", (CJ_J8,)))
     for j in range(spec.r):
         if j and j % 4 == 0:

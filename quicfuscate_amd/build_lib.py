@@ -317,7 +317,24 @@ def kernel_specs() -> list:
     # input row read and transposed once instead of once per pass
     # (e = 20: 1.60 -> 1.34 ms, tools/cmb_lab.py, profiles/r05ay_cmb_lab.json)
     specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb", cmb_lean=True))
+    # ... and all four with the products as calls into per-coefficient code
+    # blocks (QF_COMBINE_JUMP: 'j' single / wide, 'J' pass-major, 'V'
+    # interleaved): e = 39, 3 passes 2.41-2.53 -> 2.17 ms, e = 16 1.14 -> 1.00
+    # (tools/cmb_lab.py, profiles/r06j_cmb_lab.json)
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", cmb_lean=True, cmb_jump=3))
+    specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb", cmb_lean=True, cmb_jump=3))
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True, cmb_jump=3))
+    specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True, pm_xcd=True, cmb_jump=3))
     return specs
+
+
+def _cmb_mode(spec) -> str:
+    """Table letter of a payload-pass kernel (qf_bs.hip cmb_entry): 'm' / 'P' /
+    'Q' (single or wide / pass-major / interleaved), 'j' / 'J' / 'V' the same
+    with jump-table products."""
+    if spec.pass_major:
+        return ("V" if spec.cmb_jump else "Q") if spec.pm_xcd else ("J" if spec.cmb_jump else "P")
+    return "j" if spec.cmb_jump else "m"
 
 
 def _bs_kernels(build_dir: Path) -> Path:
@@ -355,7 +372,7 @@ def _bs_kernels(build_dir: Path) -> Path:
         elif spec.mode == "enc" and spec.ksplit > 1:
             mode = "f"
         else:
-            mode = {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": ("Q" if spec.pm_xcd else "P") if spec.pass_major else "m"}[spec.mode]
+            mode = {"enc": "e", "syn": "s", "dec": "d", "synw": "w", "cmb": _cmb_mode(spec)}[spec.mode]
         entries.append(f"    {{{k}u, {r}u, {spec.pd}u, {spec.rt}u, {spec.j0}u, '{mode}', {spec.map_stride}u, \"{spec.name}\", "
                        f"qf_bs_blob_{n}, {len(data)}u, {getattr(spec, 'waves', 4)}u, "
                        f"{getattr(spec, 'n_passes', 1)}u, sizeof(qf_bs_blob_{n})}},")

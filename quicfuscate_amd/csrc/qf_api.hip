@@ -212,7 +212,8 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* ENCODE_MERGED */ {"QF_ENCODE_MERGED", 1, 0, 1, false},
     /* SYNW_SHARED */ {"QF_SYNW_SHARED", 1, 0, 1, false},
     /* COMBINE_WIDE */ {"QF_COMBINE_WIDE", 1, 0, 1, false},
-    /* COMBINE_XCD */ {"QF_COMBINE_XCD", 1, 0, 1, false},
+    /* COMBINE_XCD */ {"QF_COMBINE_XCD", 0, 0, 1, false},
+    /* COMBINE_JUMP */ {"QF_COMBINE_JUMP", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }
@@ -631,7 +632,7 @@ static hipError_t combine_payload(qf_ctx* ctx, const qf::CombineSlotsArgs& a, in
                                   std::string* name) {
     // (rows_offs is the context's input table on the general path only)
     if (combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16)) {
-        if (name) *name = "qf_combine_bs_r16";
+        if (name) *name = qf::cmb_kernel_name(ctx->bs, a);
         return qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx);
     }
     const bool split_ok = ctx->opt[QF_OPT_COMBINE_SPLIT] != 0;
@@ -765,8 +766,7 @@ int decode_cauchy_enc(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G, const 
                  qf::cmb_pass_major_ok(passes, sh->rec_row_stride, (uint64_t)G * cgs) &&
                  combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
             if (pm) {
-                cname = qf::cmb_wide_ok(ctx->bs, a, passes, (uint64_t)G * cgs, e_max) ? "qf_combine_bs_r24"
-                                                                                      : "qf_combine_bs_r16_pm";
+                cname = qf::cmb_kernel_name(ctx->bs, a, passes, (uint64_t)G * cgs, e_max);
                 QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, st, a, ctx->d_cmbidx, passes, (uint64_t)G * cgs,
                                             e_max));
             } else {
@@ -1666,8 +1666,7 @@ static int decode_batch_impl(qf_ctx* ctx, const qf_decode_shape* sh, uint32_t G,
              qf::cmb_pass_major_ok(passes, sh->rec_row_stride, (uint64_t)G * coef_gen_stride) &&
              combine_bs_ok(ctx, a, a.rows_offs == ctx->offs_in && ctx->offs_in_al16);
         if (pm) {
-            cname = qf::cmb_wide_ok(ctx->bs, a, passes, (uint64_t)G * coef_gen_stride, e_max) ? "qf_combine_bs_r24"
-                                                                                              : "qf_combine_bs_r16_pm";
+            cname = qf::cmb_kernel_name(ctx->bs, a, passes, (uint64_t)G * coef_gen_stride, e_max);
             QF_CHECK_HIP(qf::cmb_launch(ctx->bs, ctx->num_cus, ctx->stream, a, ctx->d_cmbidx, passes,
                                         (uint64_t)G * coef_gen_stride, e_max));
         } else {

@@ -90,6 +90,9 @@ bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_s
 // runs the wide single pass (QF_COMBINE_WIDE) when the library holds it and
 // cmb_wide_ok says so
 bool cmb_wide_ok(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride, uint32_t e_max);
+// the kernel cmb_launch would run for these arguments (profiling labels)
+const char* cmb_kernel_name(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes = 1, uint64_t pass_stride = 0,
+                            uint32_t e_max = 0);
 hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const CombineSlotsArgs& a,
                       const uint32_t* idxtab, uint32_t passes = 1, uint64_t pass_stride = 0,
                       uint32_t e_max = 0);

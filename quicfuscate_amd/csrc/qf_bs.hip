@@ -373,13 +373,31 @@ hipError_t dec_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, u
 // per item, wave-uniform coefficients (kernarg layout: bs_codegen.cmb_kernargs)
 bool cmb_available() { return find('m', 0, 16) != nullptr; }
 bool cmb_pass_major_available() { return find('P', 0, 16) != nullptr; }
-// the pass-major payload pass item-major ('Q', QF_COMBINE_XCD): workgroup w
-// runs pass (w >> 3) mod P for slot 8 ((w >> 3) div P) + w % 8, so the P
-// passes of a slot are neighbours on one XCD (dispatch w -> XCD w % 8) and
-// their syndrome reads after the first come from that XCD's L2
-static const QfBsEntry* cmb_pm_entry(BsCache& cache, uint32_t passes) {
-    const QfBsEntry* q = cache.get(QF_OPT_COMBINE_XCD) ? find('Q', 0, 16) : nullptr;
-    return q && passes >= 2 && passes <= 4 ? q : find('P', 0, 16);
+// the payload kernel of a launch: single (16 outputs, 'm'), wide (24, 'm'
+// r = 24), pass-major ('P') or the pass-major item-major interleave ('Q',
+// QF_COMBINE_XCD: workgroup w runs pass (w >> 3) mod P for slot
+// 8 ((w >> 3) div P) + w % 8, so the P passes of a slot are neighbours on one
+// XCD); each with its products as calls into per-coefficient code blocks
+// ('j' / 'j' / 'J' / 'V', QF_COMBINE_JUMP) where built
+static const QfBsEntry* cmb_pick(BsCache& cache, char plain, char jump, uint32_t r) {
+    const QfBsEntry* j = cache.get(QF_OPT_COMBINE_JUMP) ? find(jump, 0, r) : nullptr;
+    return j ? j : find(plain, 0, r);
+}
+
+static const QfBsEntry* cmb_entry(BsCache& cache, bool wide, uint32_t passes) {
+    if (wide) return cmb_pick(cache, 'm', 'j', 24);
+    if (passes <= 1) return cmb_pick(cache, 'm', 'j', 16);
+    if (cache.get(QF_OPT_COMBINE_XCD) && passes <= 4) {
+        const QfBsEntry* q = cmb_pick(cache, 'Q', 'V', 16);
+        if (q) return q;
+    }
+    return cmb_pick(cache, 'P', 'J', 16);
+}
+
+const char* cmb_kernel_name(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride,
+                            uint32_t e_max) {
+    const QfBsEntry* e = cmb_entry(cache, cmb_wide_ok(cache, a, passes, pass_stride, e_max), passes);
+    return e ? e->name : "qf_combine_bs?";
 }
 
 bool cmb_pass_major_ok(uint32_t passes, uint64_t dst_row_stride, uint64_t pass_stride) {
@@ -405,8 +423,8 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     // instead of once per 16-output pass (output j's row at j * dst stride:
     // a 32-bit product in the kernel)
     const bool wide = cmb_wide_ok(cache, a, passes, pass_stride, e_max);
-    const QfBsEntry* e = wide ? find('m', 0, 24) : passes > 1 ? cmb_pm_entry(cache, passes) : find('m', 0, 16);
-    const bool xcd = e && e->mode == 'Q';
+    const QfBsEntry* e = cmb_entry(cache, wide, passes);
+    const bool xcd = e && (e->mode == 'Q' || e->mode == 'V');
     if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || 16ull * a.dst_row_stride >= (1ull << 32) ||
         a.coef_gen_stride >= (1ull << 32) || passes == 0 || (passes > 1 && a.pass != 0) ||
         (passes > 1 && !wide && !cmb_pass_major_ok(passes, a.dst_row_stride, pass_stride)))

@@ -990,9 +990,9 @@ def test_emulated_combine_bs_pass_major(L, G, P, offs, lean, pf2, xcd, jump):
                 assert (row == 0xEE).all(), (g, j)
 
 
-@pytest.mark.parametrize("lean", [False, True])
+@pytest.mark.parametrize("lean,jump", [(False, 0), (True, 0), (True, 3), (True, 2)])
 @pytest.mark.parametrize("L,G,offs", [(1200, 6, False), (4100, 3, True), (100, 9, False), (33, 4, True)])
-def test_emulated_combine_bs_wide(L, G, offs, lean):
+def test_emulated_combine_bs_wide(L, G, offs, lean, jump):
     """The wide single pass (qf_combine_bs_r24, QF_COMBINE_WIDE): 24 outputs
     per item, outputs 16..23 from the row's pass-1 record at coef +
     pass_stride; byte-equal to the two 16-output passes it replaces, and rows
@@ -1001,7 +1001,7 @@ def test_emulated_combine_bs_wide(L, G, offs, lean):
     if _GFT is None:
         _GFT = _gf_table()
     rng = np.random.default_rng(L + 7 * G)
-    spec = bs.KernelSpec(0, bs.CMB_WIDE_R, mode="cmb", cmb_lean=lean)
+    spec = bs.KernelSpec(0, bs.CMB_WIDE_R, mode="cmb", cmb_lean=lean, cmb_jump=jump)
     assert spec.next_free_vgpr <= 256
     Lp = (L + 15) // 16 * 16
     rs, drs = Lp + 32, Lp + 48

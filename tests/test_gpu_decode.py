@@ -566,6 +566,27 @@ def test_decode_combine_wide(qf, oracle, gpu_ctx, k, r, L, G, erase, path, wide,
     check(oracle, k, L, src, gens, out, False)
 
 
+@pytest.mark.parametrize("jump,xcd", [(1, 0), (0, 0), (1, 1), (0, 1)])
+@pytest.mark.parametrize("path", ["default_1wave", "general_bs"])
+@pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 5, None), (160, 48, 4100, 7, 40), (128, 39, 2100, 9, 30),
+                                           (128, 20, 9000, 5, None), (64, 16, 3000, 6, 12)])
+def test_decode_combine_jump_xcd(qf, oracle, gpu_ctx, k, r, L, G, erase, path, jump, xcd, monkeypatch):
+    """The bit-sliced payload pass with its runtime-coefficient products as
+    calls into per-coefficient code blocks (QF_OPT_COMBINE_JUMP = 1) or as
+    M0-indexed XORs (0), pass-major or with the passes of a slot interleaved
+    on one XCD (QF_OPT_COMBINE_XCD = 1): bit-exact in every combination, for
+    one, two (wide), three and four passes, on the C5 syndrome path and the
+    general (Gauss-Jordan) path."""
+    _path(monkeypatch, path)
+    qf.set_default_options(combine_jump=jump, combine_xcd=xcd)
+    rng = np.random.default_rng(k * 11 + r + L + (erase or 0))
+    kw = {"erase": erase, "shuffle": False} if erase is not None else {}
+    max_rows = k + r
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, **kw)
+    out = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+
+
 @pytest.mark.parametrize("shared", [1, 0])
 @pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 6, None), (196, 59, 9000, 6, 3), (160, 48, 4100, 9, 40),
                                            (128, 39, 2100, 12, None), (128, 20, 9000, 6, None), (128, 20, 2100, 9, 20)])

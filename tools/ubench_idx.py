@@ -228,13 +228,15 @@ def valu_per_body(kind: str) -> int:
 
 
 def jump_expected(kind: str, lanes: np.ndarray) -> np.ndarray:
-    """(lanes, 16) accumulators after one body of a jump kind."""
+    """(lanes, 16) accumulators after one body of a jump kind (HI[7] is v63,
+    which the prologue sets to the 0x0f0f0f0f mask after the tables)."""
     want = np.zeros((len(lanes), 16), np.uint32)
     for i, c in enumerate(JUMP_CS):
         j = (i % 2) if kind == "jump_xor3" else 0
         for p in range(8):
             a, b = jump_ab(c, p)
-            want[:, 8 * j + p] ^= ((lanes * 16 + a) ^ ((lanes * 16 + b) << 16)).astype(np.uint32)
+            hi = np.full(len(lanes), 0x0F0F0F0F, np.int64) if HI + b == 63 else (lanes * 16 + b) << 16
+            want[:, 8 * j + p] ^= ((lanes * 16 + a) ^ hi).astype(np.uint32)
     return want
 
 
