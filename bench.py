@@ -169,6 +169,24 @@ def parse(argv=None):
     return a
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of the cgroup's CPU quota (v2 cpu.max, else v1 cfs quota /
+    period, floored, at least 1); None without a quota."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            return max(1, int(q) // int(per))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return max(1, q // per) if q > 0 and per > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def launch_plan(args, env, argv=None):
     """--gpus N > 1 with no launcher in the environment (WORLD_SIZE unset): the
     command that starts N rank processes (torch.distributed.run on 127.0.0.1,
@@ -1083,6 +1101,7 @@ def cpu_host() -> dict:
     except AttributeError:
         usable = os.cpu_count() or 1
     return {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "usable_cpus": usable,
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
             "isa_flags": [f for f in ISA_FLAGS if f in flags],
             "pinning": "worker w pinned to the w-th CPU of this process's affinity mask (pthread_attr_setaffinity_np) "
                        "for the cpu_c1 rows; cpu_variants unpinned; cpu_baseline single-threaded"}
@@ -1256,6 +1275,11 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
         n_all = len(os.sched_getaffinity(0))
     except AttributeError:
         n_all = os.cpu_count() or 1
+    # the CPUs this process may actually keep busy: the affinity mask, capped by
+    # the cgroup's CPU quota (the GPU box's mask shows the whole host, 256 CPUs,
+    # under a quota of 16 per GPU)
+    quota = cgroup_cpu_quota()
+    usable = min(n_all, quota) if quota else n_all
 
     def timed(fn, min_s=1.0):
         reps, t0 = 0, time.perf_counter()
@@ -1268,7 +1292,7 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
 
     oracle.set_pinning(True)
     legs = {}
-    for nt in sorted({min(16, n_all), n_all}):
+    for nt in sorted({min(16, n_all), usable, n_all}):
         got_rep, te = timed(lambda: oracle.cpu_encode("table", src_h, r, nt))
         got_dec, td = timed(lambda: oracle.cpu_decode("table", k, ri_h, rows_h, nt))
         ok = bool((got_rep == rep_h).all())
@@ -1288,7 +1312,7 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
                       "note": "per-byte dispatched CLMUL-fold products (the reference as written): timing only, "
                               "SURVEY F3"}
     oracle.set_pinning(False)
-    allc = legs[n_all]
+    allc = legs[usable]
     single = {"value": round(src_bytes / (t_enc + t_dec) / (1 << 30), 5), "cores": 1,
               "encode_gibps": round(src_bytes / t_enc / (1 << 30), 5),
               "decode_gibps": round(src_bytes / t_dec / (1 << 30), 5), "seconds": round(t_enc + t_dec, 2),
@@ -1296,16 +1320,20 @@ def cpu_baseline(src, rep, rows, aidx, rec, n_rec, rec_index, k, r, Lb, e, S):
     return {
         "value": allc["value"],
         "unit": "GiB/s",
-        "cores": n_all,
+        "cores": usable,
         "kind": "port",
         "sample": f"first {S} of the benchmark generations: oracle encode (decoder.rs:172-275 loop, table gf_mul) "
-                  f"+ oracle Gauss-Jordan decode (decoder.rs:720-783, F4 fixed); all {n_all} usable CPUs, "
-                  f"generations split over pinned threads (single-core figure beside)",
+                  f"+ oracle Gauss-Jordan decode (decoder.rs:720-783, F4 fixed); all {usable} usable CPUs "
+                  f"({n_all} in the affinity mask, cgroup CPU quota {quota or 'none'}), generations split over "
+                  f"pinned threads (single-core and whole-mask figures beside)",
+        "affinity_cpus": n_all,
+        "cgroup_cpu_quota": quota,
         "encode_gibps": allc["encode_gibps"],
         "decode_gibps": allc["decode_gibps"],
         "sample_parity_vs_gpu": bool(parity) and all(v["sample_parity_vs_gpu"] for v in legs.values()),
         "single_core": single,
         "all_cores": allc,
+        "affinity_all": legs[n_all],
         "share_16": legs[min(16, n_all)],
         "as_written_all_cores": as_written,
     }
@@ -1399,8 +1427,9 @@ def compact_line(full: dict, detail: str | None = None) -> dict:
     cb = full.get("cpu_baseline")
     if cb:
         line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "encode_gibps",
-                                                       "decode_gibps", "sample_parity_vs_gpu")}
-        for leg in ("single_core", "share_16", "as_written_all_cores"):
+                                                       "decode_gibps", "sample_parity_vs_gpu", "affinity_cpus",
+                                                       "cgroup_cpu_quota")}
+        for leg in ("single_core", "share_16", "affinity_all", "as_written_all_cores"):
             if cb.get(leg):
                 line["cpu_baseline"][leg] = {k: cb[leg].get(k) for k in ("value", "cores", "encode_gibps",
                                                                          "decode_gibps")}
