@@ -1393,16 +1393,23 @@ def _c5_compact(c5: dict | None) -> dict | None:
     if not c5:
         return None
     out = {"L": c5.get("L"), "unit": "GiB/s algorithmic bytes",
-           "cols": ["block_enc", "block_dec", "sliding_enc", "block_enc_hbm_frac", "block_dec_hbm_frac"]}
-    shapes, ok = {}, True
+           "cols": ["block_enc", "block_dec", "sliding_enc", "block_enc_hbm_frac", "block_dec_hbm_frac",
+                    "sliding_valu_frac"]}
+    shapes, ok, sources = {}, True, set()
     for key, v in c5.items():
         if not (key.startswith("k") and isinstance(v, dict)):
             continue
         be, bd, sl = v.get("block/encode", {}), v.get("block/decode", {}), v.get("sliding/encode", {})
+        sv = sl.get("valu") or {}
+        if sv.get("source"):
+            sources.add(sv["source"])
         shapes[key] = [be.get("GiBps_alg"), bd.get("GiBps_alg"), sl.get("GiBps_alg"),
-                       be.get("hbm_frac_of_8TBps"), bd.get("hbm_frac_of_8TBps")]
+                       be.get("hbm_frac_of_8TBps"), bd.get("hbm_frac_of_8TBps"), sv.get("frac")]
         ok &= bd.get("verified", True) is not False and sl.get("verified", True) is not False
     out["shapes"] = shapes
+    # where the sliding VALU issue fractions come from: SQ counters of the same
+    # kernels (profiles/c5_sq_counters.json, code hash checked) or the static model
+    out["sliding_valu_source"] = "/".join(sorted(sources)) or None
     m = c5.get("mixed_desc_batch")
     if m:
         mx = {"G": m.get("G"), "round_trip_ok": m.get("round_trip_ok")}

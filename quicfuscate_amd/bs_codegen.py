@@ -3311,8 +3311,9 @@ def _cmb_regs(R: int) -> dict:
     """VGPRs past the accumulators: the fixed layout above for R <= 16; the
     wide pass (R = 24, 192 accumulators) moves them above its accumulators
     (256 VGPRs: still two waves per SIMD)."""
-    if R <= 16:
+    if 8 < R <= 16:
         return {"qv": C_QV, "qc": C_QC, "ub": C_UB, "ubc": C_UBC, "tb": C_TB, "vm": C_VM, "end": CMB_NEXT_FREE_VGPR}
+    # R <= 8: 128 VGPRs (four waves per SIMD); R = 24: 256 (two)
     b = C_ACC + 8 * R
     return {"qv": b, "qc": b + 1, "ub": b + 2, "ubc": b + 3, "tb": b + 4, "vm": b + 5, "end": b + 8}
 # SGPRs

@@ -27,28 +27,31 @@ RS = 9008
 # (name, e, R, pass_major, KernelSpec keyword overrides); the first variant of
 # each e is the reference the others' outputs are compared with
 VARIANTS = [
-    # round 6: the passes of one slot interleaved on one XCD (KernelSpec.pm_xcd);
-    # the products as calls into per-coefficient code blocks (cmb_jump 3 / 2)
-    ("e39_lean", 39, 16, True, {"cmb_lean": True}),
-    ("e39_lean_xcd", 39, 16, True, {"cmb_lean": True, "pm_xcd": True}),
-    ("e39_xcd_j3", 39, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
-    ("e39_xcd_j2", 39, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 2}),
-    ("e39_lean_2", 39, 16, True, {"cmb_lean": True}),
-    ("e39_lean_xcd_2", 39, 16, True, {"cmb_lean": True, "pm_xcd": True}),
-    ("e39_xcd_j3_2", 39, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
-    ("e59_lean", 59, 16, True, {"cmb_lean": True}),
-    ("e59_lean_xcd", 59, 16, True, {"cmb_lean": True, "pm_xcd": True}),
-    ("e59_xcd_j3", 59, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
-    ("e48_lean", 48, 16, True, {"cmb_lean": True}),
-    ("e48_lean_xcd", 48, 16, True, {"cmb_lean": True, "pm_xcd": True}),
-    ("e48_xcd_j3", 48, 16, True, {"cmb_lean": True, "pm_xcd": True, "cmb_jump": 3}),
-    ("e16_m", 16, 16, False, {"cmb_lean": True}),
-    ("e16_m_j3", 16, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
+    # round 6b: occupancy -- R = 8 accumulators (128 VGPRs, four waves per SIMD,
+    # "bpc" 4 blocks per CU) against R = 16 (192, two) at equal work (e = 8:
+    # the R = 16 kernel stops after 8 outputs); e = 16 as two R = 8 launches
+    # ("split": launch i reads record bytes 8 i.. and writes rows 8 i..)
+    ("e8_r16_j3", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e8_r8_j3", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4}),
+    ("e8_r8_j3_bpc2", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e8_r16", 8, 16, False, {"cmb_lean": True}),
+    ("e8_r8", 8, 8, False, {"cmb_lean": True, "bpc": 4}),
+    ("e16_r16_j3", 16, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e16_r8x2_j3", 16, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "split": 2}),
+    ("e16_r16", 16, 16, False, {"cmb_lean": True}),
+    ("e16_r8x2", 16, 8, False, {"cmb_lean": True, "bpc": 4, "split": 2}),
+    ("e8_r16_j3_2", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e8_r8_j3_2", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4}),
+    ("e16_r16_j3_2", 16, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e16_r8x2_j3_2", 16, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "split": 2}),
 ]
 
 
+LAB_KEYS = ("bpc", "split")
+
+
 def make_spec(bs, R, pm, kw):
-    return bs.KernelSpec(0, R, 3, "cmb", pass_major=pm, **kw)
+    return bs.KernelSpec(0, R, 3, "cmb", pass_major=pm, **{a: b for a, b in kw.items() if a not in LAB_KEYS})
 
 
 def build():
@@ -101,23 +104,32 @@ def run(nbytes: float, reps: int):
         assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, m["symbol"].encode()) == 0
         Lu = (L + 15) // 16
         ipg = ((Lu + 1) // 2 + 63) // 64
-        blocks = min((G * ipg + 3) // 4, 2 * 256)
+        blocks = min((G * ipg + 3) // 4, m["kw"].get("bpc", 2) * 256)
         passes = P if m["pm"] else 1
         xcd = bool(m["kw"].get("pm_xcd"))
         if xcd:   # slots in groups of 8 (one per XCD)
             blocks = (blocks + 7) // 8 * 8
-        ka, _ = bs.cmb_kernargs(rows.data_ptr(), dst.data_ptr(), e * RS, e * RS, RS, RS, rec.data_ptr(), cgs, 0,
-                                n_out.data_ptr(), bound.data_ptr(), idxtab.data_ptr(), L, G, 4 * blocks,
-                                pass_stride=PS, pm_xcd_passes=passes if xcd else 0)
-        kbuf = ctypes.create_string_buffer(ka, len(ka))
-        size = ctypes.c_size_t(len(ka))
-        extra = (ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
-                                     ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3)
+        split = m["kw"].get("split", 1)
+        R = m["R"]
+        n_outs = [n_out] if split == 1 else [torch.full((G,), max(0, e - R * i), dtype=torch.int32, device="cuda")
+                                             for i in range(split)]
+        extras, keep = [], []
+        for i in range(split):   # launch i: record bytes R i.., output rows R i..
+            ka, _ = bs.cmb_kernargs(rows.data_ptr(), dst.data_ptr() + R * i * RS, e * RS, e * RS, RS, RS,
+                                    rec.data_ptr() + R * i, cgs, 0, n_outs[i].data_ptr(), bound.data_ptr(),
+                                    idxtab.data_ptr(), L, G, 4 * blocks, pass_stride=PS,
+                                    pm_xcd_passes=passes if xcd else 0)
+            kbuf = ctypes.create_string_buffer(ka, len(ka))
+            size = ctypes.c_size_t(len(ka))
+            keep += [kbuf, size]
+            extras.append((ctypes.c_void_p * 5)(1, ctypes.cast(kbuf, ctypes.c_void_p), 2,
+                                                ctypes.cast(ctypes.pointer(size), ctypes.c_void_p), 3))
 
         def launch():
-            err = hip.hipModuleLaunchKernel(fn, blocks * passes, 1, 1, 256, 1, 1, 0,
-                                            ctypes.c_void_p(stream.cuda_stream), None, extra)
-            assert err == 0, err
+            for extra in extras:
+                err = hip.hipModuleLaunchKernel(fn, blocks * passes, 1, 1, 256, 1, 1, 0,
+                                                ctypes.c_void_p(stream.cuda_stream), None, extra)
+                assert err == 0, err
 
         dst.fill_(0xA5)
         launch()
