@@ -169,19 +169,20 @@ def parse(argv=None):
     return a
 
 
-def cgroup_cpu_quota():
+def cgroup_cpu_quota(root: str = "/sys/fs/cgroup"):
     """CPUs' worth of the cgroup's CPU quota (v2 cpu.max, else v1 cfs quota /
     period, floored, at least 1); None without a quota."""
+    root = Path(root)
     try:
-        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        q, per = (root / "cpu.max").read_text().split()[:2]
         if q != "max":
             return max(1, int(q) // int(per))
         return None
     except (OSError, ValueError):
         pass
     try:
-        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
-        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        q = int((root / "cpu" / "cpu.cfs_quota_us").read_text())
+        per = int((root / "cpu" / "cpu.cfs_period_us").read_text())
         return max(1, q // per) if q > 0 and per > 0 else None
     except (OSError, ValueError):
         return None

@@ -89,3 +89,20 @@ def test_detail_written(tmp_path):
     p = bench.emit_detail(full, str(tmp_path / "d.json"))
     assert p and json.loads(open(p).read())["value"] == full["value"]
     assert bench.emit_detail(full, "") is None
+
+
+def test_cgroup_cpu_quota(tmp_path):
+    """The usable-CPU count of cpu_baseline: cgroup v2 cpu.max, else v1 cfs
+    quota / period, floored; None without a quota."""
+    assert bench.cgroup_cpu_quota(str(tmp_path)) is None
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) == 16
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) is None
+    (tmp_path / "cpu.max").unlink()
+    (tmp_path / "cpu").mkdir()
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("250000")
+    (tmp_path / "cpu" / "cpu.cfs_period_us").write_text("100000")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) == 2
+    (tmp_path / "cpu" / "cpu.cfs_quota_us").write_text("-1")
+    assert bench.cgroup_cpu_quota(str(tmp_path)) is None

@@ -1461,3 +1461,14 @@ def test_xchg_streams_meet_at_every_barrier():
                 t = blabels[tgt]
                 assert t > n and not any(n < b < t for b in bars), (ms.name, p, op.name, tgt)
         assert len(set(counts)) == 1 and counts[0] > 0, (ms.name, counts)
+
+
+def test_pm_xcd_word_divides_exactly():
+    """The interleaved pass-major payload kernel's h div P = (h * magic) >> 16
+    (kernarg word 33, bs_codegen.pm_xcd_word; qf_bs.hip computes the same
+    word) is exact over every workgroup index the launch can produce."""
+    for P in (2, 3, 4):
+        w = bs.pm_xcd_word(P)
+        assert w & 7 == P
+        M = w >> 3
+        assert all((h * M) >> 16 == h // P and h * M < 1 << 32 for h in range(1 << 15))

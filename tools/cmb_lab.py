@@ -27,27 +27,22 @@ RS = 9008
 # (name, e, R, pass_major, KernelSpec keyword overrides); the first variant of
 # each e is the reference the others' outputs are compared with
 VARIANTS = [
-    # round 6b: occupancy -- R = 8 accumulators (128 VGPRs, four waves per SIMD,
-    # "bpc" 4 blocks per CU) against R = 16 (192, two) at equal work (e = 8:
-    # the R = 16 kernel stops after 8 outputs); e = 16 as two R = 8 launches
-    # ("split": launch i reads record bytes 8 i.. and writes rows 8 i..)
-    ("e8_r16_j3", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
-    ("e8_r8_j3", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4}),
-    ("e8_r8_j3_bpc2", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3}),
-    ("e8_r16", 8, 16, False, {"cmb_lean": True}),
-    ("e8_r8", 8, 8, False, {"cmb_lean": True, "bpc": 4}),
-    ("e16_r16_j3", 16, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
-    ("e16_r8x2_j3", 16, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "split": 2}),
-    ("e16_r16", 16, 16, False, {"cmb_lean": True}),
-    ("e16_r8x2", 16, 8, False, {"cmb_lean": True, "bpc": 4, "split": 2}),
-    ("e8_r16_j3_2", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
-    ("e8_r8_j3_2", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4}),
-    ("e16_r16_j3_2", 16, 16, False, {"cmb_lean": True, "cmb_jump": 3}),
-    ("e16_r8x2_j3_2", 16, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "split": 2}),
+    # round 6c: occupancy at equal, compute-bound work -- 39 input rows ("rows"),
+    # 8 outputs: R = 8 (128 VGPRs, four waves per SIMD with "bpc" 4) against
+    # R = 16 (192 VGPRs, two waves; it stops after 8 outputs)
+    ("e8x39_r16_j3", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3, "rows": 39}),
+    ("e8x39_r8_j3", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "rows": 39}),
+    ("e8x39_r8_j3_bpc3", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 3, "rows": 39}),
+    ("e8x39_r16", 8, 16, False, {"cmb_lean": True, "rows": 39}),
+    ("e8x39_r8", 8, 8, False, {"cmb_lean": True, "bpc": 4, "rows": 39}),
+    ("e8x39_r16_j3_2", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3, "rows": 39}),
+    ("e8x39_r8_j3_2", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "rows": 39}),
+    ("e8x39_r16_2", 8, 16, False, {"cmb_lean": True, "rows": 39}),
+    ("e8x39_r8_2", 8, 8, False, {"cmb_lean": True, "bpc": 4, "rows": 39}),
 ]
 
 
-LAB_KEYS = ("bpc", "split")
+LAB_KEYS = ("bpc", "split", "rows")
 
 
 def make_spec(bs, R, pm, kw):
@@ -85,18 +80,19 @@ def run(nbytes: float, reps: int):
     res, cur, base_out = {}, None, {}
     for m in manifest:
         e = m["e"]
-        G = max(1, int(nbytes // (e * L)))
+        nr = m["kw"].get("rows", e)   # input rows per generation (default: e syndromes)
+        G = max(1, int(nbytes // (nr * L)))
         P = (e + 15) // 16
-        cgs = (e + 1) * 16
+        cgs = (nr + 1) * 16
         PS = G * cgs
-        if cur != e:
+        if cur != (e, nr):
             g = torch.Generator(device="cuda").manual_seed(e)
-            rows = torch.randint(0, 256, (G * e * RS,), dtype=torch.uint8, device="cuda", generator=g)
+            rows = torch.randint(0, 256, (G * nr * RS,), dtype=torch.uint8, device="cuda", generator=g)
             rec = torch.randint(0, 256, (P * PS,), dtype=torch.uint8, device="cuda", generator=g)
             n_out = torch.full((G,), e, dtype=torch.int32, device="cuda")
-            bound = torch.full((G,), e, dtype=torch.int32, device="cuda")
+            bound = torch.full((G,), nr, dtype=torch.int32, device="cuda")
             dst = torch.empty(G * e * RS, dtype=torch.uint8, device="cuda")
-            cur = e
+            cur = (e, nr)
         mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
         data = (OUT / m["hsaco"]).read_bytes()
         buf = ctypes.create_string_buffer(data, len(data))
@@ -115,7 +111,7 @@ def run(nbytes: float, reps: int):
                                              for i in range(split)]
         extras, keep = [], []
         for i in range(split):   # launch i: record bytes R i.., output rows R i..
-            ka, _ = bs.cmb_kernargs(rows.data_ptr(), dst.data_ptr() + R * i * RS, e * RS, e * RS, RS, RS,
+            ka, _ = bs.cmb_kernargs(rows.data_ptr(), dst.data_ptr() + R * i * RS, nr * RS, e * RS, RS, RS,
                                     rec.data_ptr() + R * i, cgs, 0, n_outs[i].data_ptr(), bound.data_ptr(),
                                     idxtab.data_ptr(), L, G, 4 * blocks, pass_stride=PS,
                                     pm_xcd_passes=passes if xcd else 0)
@@ -134,9 +130,9 @@ def run(nbytes: float, reps: int):
         dst.fill_(0xA5)
         launch()
         torch.cuda.synchronize()
-        if e not in base_out:
-            base_out[e] = dst.clone()
-        ok = bool(torch.equal(dst, base_out[e]))
+        if (e, nr) not in base_out:
+            base_out[(e, nr)] = dst.clone()
+        ok = bool(torch.equal(dst, base_out[(e, nr)]))
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record(stream)
         for _ in range(reps):
@@ -146,7 +142,7 @@ def run(nbytes: float, reps: int):
         ms = t0.elapsed_time(t1) / reps
         res[m["name"]] = {"ms": round(ms, 4), "G": G, "e": e, "passes": passes, "matches_base": ok,
                           "vgprs": m["vgprs"], "kw": m["kw"],
-                          "indexed_xor_per_simd_per_ns": round(G * ipg * e * e * 16 / (ms * 1e6) / 1024, 3)}
+                          "indexed_xor_per_simd_per_ns": round(G * ipg * nr * e * 16 / (ms * 1e6) / 1024, 3)}
         print(m["name"], res[m["name"]], flush=True)
         hip.hipModuleUnload(mod)
     return res
