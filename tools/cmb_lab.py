@@ -27,18 +27,20 @@ RS = 9008
 # (name, e, R, pass_major, KernelSpec keyword overrides); the first variant of
 # each e is the reference the others' outputs are compared with
 VARIANTS = [
-    # round 6c: occupancy at equal, compute-bound work -- 39 input rows ("rows"),
-    # 8 outputs: R = 8 (128 VGPRs, four waves per SIMD with "bpc" 4) against
-    # R = 16 (192 VGPRs, two waves; it stops after 8 outputs)
-    ("e8x39_r16_j3", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3, "rows": 39}),
-    ("e8x39_r8_j3", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "rows": 39}),
-    ("e8x39_r8_j3_bpc3", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 3, "rows": 39}),
-    ("e8x39_r16", 8, 16, False, {"cmb_lean": True, "rows": 39}),
-    ("e8x39_r8", 8, 8, False, {"cmb_lean": True, "bpc": 4, "rows": 39}),
-    ("e8x39_r16_j3_2", 8, 16, False, {"cmb_lean": True, "cmb_jump": 3, "rows": 39}),
-    ("e8x39_r8_j3_2", 8, 8, False, {"cmb_lean": True, "cmb_jump": 3, "bpc": 4, "rows": 39}),
-    ("e8x39_r16_2", 8, 16, False, {"cmb_lean": True, "rows": 39}),
-    ("e8x39_r8_2", 8, 8, False, {"cmb_lean": True, "bpc": 4, "rows": 39}),
+    # round 6d: with the jump products, does the syndrome re-read bound the
+    # pass-major pass? pass-major against the XCD interleave, both jump
+    ("e39_pm_j3", 39, 16, True, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e39_xcd_j3", 39, 16, True, {"cmb_lean": True, "cmb_jump": 3, "pm_xcd": True}),
+    ("e48_pm_j3", 48, 16, True, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e48_xcd_j3", 48, 16, True, {"cmb_lean": True, "cmb_jump": 3, "pm_xcd": True}),
+    ("e59_pm_j3", 59, 16, True, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e59_xcd_j3", 59, 16, True, {"cmb_lean": True, "cmb_jump": 3, "pm_xcd": True}),
+    ("e32_pm_j3", 32, 16, True, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e32_xcd_j3", 32, 16, True, {"cmb_lean": True, "cmb_jump": 3, "pm_xcd": True}),
+    ("e39_pm_j3_2", 39, 16, True, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e39_xcd_j3_2", 39, 16, True, {"cmb_lean": True, "cmb_jump": 3, "pm_xcd": True}),
+    ("e48_pm_j3_2", 48, 16, True, {"cmb_lean": True, "cmb_jump": 3}),
+    ("e48_xcd_j3_2", 48, 16, True, {"cmb_lean": True, "cmb_jump": 3, "pm_xcd": True}),
 ]
 
 
