@@ -3379,8 +3379,16 @@ def _cmb_row(E, spec, buf: int, other: int, tag: str):
     """One input row (slot CS_SLOT, data in `buf`): prefetch the next row into
     `other`, bit-slice, combinations, then the ew products."""
     E(Op("s_lshl", (CS_T0, CS_SLOT, 4)))
-    E(Op("s_load_n", (CS_REC, CS_COEFG, 4, CS_T0, 0)))
-    if spec.r > 16:   # outputs 16.. from the pass-1 record of the row
+    if spec.pass_major and spec.r == CMB_WIDE_R:
+        # pm24: outputs 8t..8t+7 of the pass from the record byte offset D_t
+        # (s22 / s23 / s101, _cmb_pm24_prologue), three 8-byte pieces
+        for dst, d, tmp in ((CS_REC, PM24_D[0], CS_REC2_OFF), (CS_REC + 2, PM24_D[1], PM24_T[0]),
+                            (CS_REC2, PM24_D[2], PM24_T[1])):
+            E(Op("s_add", (tmp, CS_T0, d)))
+            E(Op("s_load_n", (dst, CS_COEFG, 2, tmp, 0)))
+    else:
+        E(Op("s_load_n", (CS_REC, CS_COEFG, 4, CS_T0, 0)))
+    if spec.r > 16 and not spec.pass_major:   # outputs 16.. from the pass-1 record of the row
         E(Op("s_add", (CS_REC2_OFF, CS_T0, CS_PSTRIDE)))
         E(Op("s_load_n", (CS_REC2, CS_COEFG, 2, CS_REC2_OFF, 0)))
     ahead = 2 if spec.cmb_pf2 else 1
@@ -3487,11 +3495,69 @@ def _cmb_jump_table(E, spec: KernelSpec):
         E(Op("align7", ()))
 
 
+# pm24 (24-output pass-major, jump products only): the three record pieces'
+# byte offsets (the index-row SGPRs s22:23, dead in jump mode, and s101) and
+# the address temps (free in jump mode)
+PM24_D = (22, 23, 101)
+PM24_T = (86, 87)
+
+
+def _cmb_pm24_prologue(E):
+    """Pass p' of a 24-output pass-major launch (workgroups [p' n, (p' + 1) n),
+    at most 3 passes): outputs 24 p' .. 24 p' + 23 are the 16-output record
+    passes' bytes [24 p', 24 p' + 24), i.e. record pass q0 = (3 p') >> 1 from
+    byte 8 (p' & 1), in three 8-byte pieces at D_t = 8 (p' & 1) + 8 t past
+    pass q0 (a piece past 15 is the next record pass's, D - 16 + pass
+    stride). Pieces in a record pass that was not written (q0 + 1 >= word 33)
+    read piece 0 instead: their outputs lie past e_max and are never stored.
+    The coefficient base advances by q0 record passes, the output rows by
+    24 p' rows."""
+    E(Op("s_lshrk", (CS_TMP64 + 1, 33, 2)))            # n = workgroups per pass
+    E(Op("s_movk", (17, 0)))
+    for _ in range(2):
+        E(Op("s_cmp_lt_br", (2, CS_TMP64 + 1, ".Lpm_done")))
+        E(Op("s_sub", (2, 2, CS_TMP64 + 1)))
+        E(Op("s_addk", (17, 17, 1)))
+        E(Op("s_mul_k", (CS_TMP64, 13, CMB_WIDE_R)))   # dst += 24 rows
+        E(Op("s_add_cc", (6, 6, CS_TMP64)))
+        E(Op("s_addck", (7, 7, 0)))
+    E(Op("label", (".Lpm_done",)))
+    # q0 = (3 p') >> 1 record passes: p' = 1 -> 1, p' = 2 -> 3
+    E(Op("s_mul_k", (36, 17, 3)))
+    E(Op("s_lshrk", (36, 36, 1)))
+    E(Op("s_movk", (37, 0)))
+    E(Op("label", (".Lpm_q",)))
+    E(Op("s_cmp_ge_br", (37, 36, ".Lpm_qd")))
+    E(Op("s_addk", (37, 37, 1)))
+    E(Op("s_add_cc", (14, 14, CS_T1)))
+    E(Op("s_addck", (15, 15, 0)))
+    E(Op("s_branch", (".Lpm_q",)))
+    E(Op("label", (".Lpm_qd",)))
+    # D0 = 8 (p' & 1); D1 = p' odd ? stride : 8; D2 = p' odd ? stride + 8 : stride
+    # (D2 takes s101, word 33: the record-pass count moves to s41 first)
+    E(Op("s_mov", (41, CS_T1 + 1)))
+    E(Op("s_andk", (38, 17, 1)))
+    E(Op("s_lshl", (PM24_D[0], 38, 3)))
+    E(Op("s_movk", (39, 8)))
+    E(Op("s_add", (40, CS_T1, 39)))                    # stride + 8
+    E(Op("s_cmp_eq_k", (38, 1)))
+    E(Op("s_cselect32", (PM24_D[1], CS_T1, 39)))
+    E(Op("s_cselect32", (PM24_D[2], 40, CS_T1)))
+    # record pass q0 + 1 not written: its pieces read piece 0
+    E(Op("s_addk", (36, 36, 1)))
+    E(Op("s_cmp_lt_br", (36, 41, ".Lpm_dok")))
+    E(Op("s_mov", (PM24_D[2], PM24_D[0])))
+    E(Op("s_cmp_eq_k", (38, 1)))
+    E(Op("s_cselect32", (PM24_D[1], PM24_D[0], PM24_D[1])))
+    E(Op("label", (".Lpm_dok",)))
+
+
 def _generate_cmb(spec: KernelSpec) -> list[Op]:
     ops: list[Op] = []
     E = ops.append
     R = spec.r
-    assert R <= 16 or (R == CMB_WIDE_R and not spec.pass_major)
+    assert R <= 16 or (R == CMB_WIDE_R and (not spec.pass_major or (spec.cmb_jump and not spec.pm_xcd)))
+    pm24 = spec.pass_major and R == CMB_WIDE_R
     rg = _cmb_regs(R)
     C_QV, C_QC, C_UB, C_UBC, C_TB, C_VM = (rg[x] for x in ("qv", "qc", "ub", "ubc", "tb", "vm"))
     assert C_ACC + 8 * R <= C_QV and rg["end"] <= 256
@@ -3513,9 +3579,11 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     assert not spec.pm_xcd or spec.pass_major
     if spec.pm_xcd:   # records' pass stride; word 33: (magic << 3) | passes
         E(Op("s_load_n", (CS_T1, 0, 2, None, KERNARG_BYTES_CMB)))
+    elif pm24:        # records' pass stride; word 33: the record passes written
+        E(Op("s_load_n", (CS_T1, 0, 2, None, KERNARG_BYTES_CMB)))
     elif spec.pass_major:
         E(Op("s_load_n", (CS_T1, 0, 1, None, KERNARG_BYTES_CMB)))   # records' pass stride
-    if R > 16:
+    if R > 16 and not pm24:
         E(Op("s_load_n", (CS_PSTRIDE, 0, 1, None, KERNARG_BYTES_CMB)))
     E(Op("s_waitcnt_lgkm", ()))
     if spec.pm_xcd:
@@ -3541,6 +3609,8 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
             E(Op("s_add", (6, 6, CS_TMP64)))
             E(Op("s_addck", (7, 7, 0)))
         E(Op("label", (".Lpm_done",)))
+    elif pm24:
+        _cmb_pm24_prologue(E)
     elif spec.pass_major:
         # workgroups [p n, (p + 1) n) run pass p (n = grid waves / 4): the
         # pass, its records and its 16 output rows, and the workgroup id in
@@ -3576,8 +3646,11 @@ def _generate_cmb(spec: KernelSpec) -> list[Op]:
     E(Op("s_load_n", (CS_T1, 18, 1, CS_T0, 0)))      # e = n_out[g]
     E(Op("s_load_n", (CS_BOUND, 20, 1, CS_T0, 0)))   # bound[g]
     E(Op("s_waitcnt_lgkm", ()))
-    # outputs of this pass: ew = min(e - 16 pass, R); none -> next item
-    E(Op("s_lshl", (CS_T0, 17, 4)))
+    # outputs of this pass: ew = min(e - 16 pass, R) (24 pass for pm24); none -> next item
+    if pm24:
+        E(Op("s_mul_k", (CS_T0, 17, CMB_WIDE_R)))
+    else:
+        E(Op("s_lshl", (CS_T0, 17, 4)))
     E(Op("s_cmp_ge_br", (CS_T0, CS_T1, ".Lnext")))
     E(Op("s_sub", (CS_EW, CS_T1, CS_T0)))
     E(Op("s_movk", (CS_T0, R)))

@@ -325,13 +325,23 @@ def kernel_specs() -> list:
     specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb", cmb_lean=True, cmb_jump=3))
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True, cmb_jump=3))
     specs.append(bs.KernelSpec(0, 16, BS_PD, "cmb", pass_major=True, cmb_lean=True, pm_xcd=True, cmb_jump=3))
+    # ... and 24-output passes in one pass-major launch ('W', QF_COMBINE_PM24):
+    # e_max 33-48 in 2 passes instead of 3, 49-72 in 3 instead of 4
+    specs.append(bs.KernelSpec(0, bs.CMB_WIDE_R, BS_PD, "cmb", pass_major=True, cmb_lean=True, cmb_jump=3))
     return specs
+
+
+def bs_codegen_wide() -> int:
+    from . import bs_codegen as bs
+    return bs.CMB_WIDE_R
 
 
 def _cmb_mode(spec) -> str:
     """Table letter of a payload-pass kernel (qf_bs.hip cmb_entry): 'm' / 'P' /
     'Q' (single or wide / pass-major / interleaved), 'j' / 'J' / 'V' the same
-    with jump-table products."""
+    with jump-table products; 'W' the 24-output pass-major passes (jump)."""
+    if spec.pass_major and spec.r == bs_codegen_wide():
+        return "W"
     if spec.pass_major:
         return ("V" if spec.cmb_jump else "Q") if spec.pm_xcd else ("J" if spec.cmb_jump else "P")
     return "j" if spec.cmb_jump else "m"

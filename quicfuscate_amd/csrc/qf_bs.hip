@@ -384,7 +384,18 @@ static const QfBsEntry* cmb_pick(BsCache& cache, char plain, char jump, uint32_t
     return j ? j : find(plain, 0, r);
 }
 
-static const QfBsEntry* cmb_entry(BsCache& cache, bool wide, uint32_t passes) {
+// the 24-output pass-major launch ('W', jump products, QF_COMBINE_PM24) for
+// 3-4 record passes (e_max 33-64): ceil(e_max / 24) passes, the records'
+// pass stride plus one piece (8 B) in 32 bits
+static bool cmb_pm24_ok(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride,
+                        uint32_t e_max) {
+    return passes >= 3 && passes <= kCmbMaxPasses && e_max > 32 && e_max <= 72 && a.pass == 0 &&
+           pass_stride + 8 < (1ull << 32) && 72ull * a.dst_row_stride < (1ull << 32) &&
+           cache.get(QF_OPT_COMBINE_JUMP) && cache.get(QF_OPT_COMBINE_PM24) && find('W', 0, 24) != nullptr;
+}
+
+static const QfBsEntry* cmb_entry(BsCache& cache, bool wide, uint32_t passes, bool pm24 = false) {
+    if (pm24) return find('W', 0, 24);
     if (wide) return cmb_pick(cache, 'm', 'j', 24);
     if (passes <= 1) return cmb_pick(cache, 'm', 'j', 16);
     if (cache.get(QF_OPT_COMBINE_XCD) && passes <= 4) {
@@ -396,7 +407,8 @@ static const QfBsEntry* cmb_entry(BsCache& cache, bool wide, uint32_t passes) {
 
 const char* cmb_kernel_name(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride,
                             uint32_t e_max) {
-    const QfBsEntry* e = cmb_entry(cache, cmb_wide_ok(cache, a, passes, pass_stride, e_max), passes);
+    const QfBsEntry* e = cmb_entry(cache, cmb_wide_ok(cache, a, passes, pass_stride, e_max), passes,
+                                   cmb_pm24_ok(cache, a, passes, pass_stride, e_max));
     return e ? e->name : "qf_combine_bs?";
 }
 
@@ -423,8 +435,10 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
     // instead of once per 16-output pass (output j's row at j * dst stride:
     // a 32-bit product in the kernel)
     const bool wide = cmb_wide_ok(cache, a, passes, pass_stride, e_max);
-    const QfBsEntry* e = cmb_entry(cache, wide, passes);
+    const bool pm24 = !wide && cmb_pm24_ok(cache, a, passes, pass_stride, e_max);
+    const QfBsEntry* e = cmb_entry(cache, wide, passes, pm24);
     const bool xcd = e && (e->mode == 'Q' || e->mode == 'V');
+    const uint32_t launch_passes = pm24 ? (e_max + 23) / 24 : wide ? 1 : passes;
     if (!e || !idxtab || a.L == 0 || a.row_stride >= (1ull << 32) || 16ull * a.dst_row_stride >= (1ull << 32) ||
         a.coef_gen_stride >= (1ull << 32) || passes == 0 || (passes > 1 && a.pass != 0) ||
         (passes > 1 && !wide && !cmb_pass_major_ok(passes, a.dst_row_stride, pass_stride)))
@@ -456,14 +470,14 @@ hipError_t cmb_launch(BsCache& cache, int num_cus, hipStream_t st, const Combine
                       (uint32_t)a.coef_gen_stride, a.pass, lo(a.n_out), hi(a.n_out), lo(a.bound), hi(a.bound),
                       lo(idxtab), hi(idxtab), lo(a.rows_offs), hi(a.rows_offs), lo(a.dst_offs), hi(a.dst_offs),
                       a.L, Lu, Q, ipg, (uint32_t)n_items, (uint32_t)blocks * 4, magic, shift,
-                      (uint32_t)pass_stride, xcd ? pm_xcd_word(passes) : 0u};
+                      (uint32_t)pass_stride, xcd ? pm_xcd_word(passes) : pm24 ? passes : 0u};
     // (pass-major: word 32 = the records' pass stride; the grid holds every
     // pass's `blocks` workgroups, pass p's at [p blocks, (p + 1) blocks), or
     // interleaved ('Q': word 33 = pm_xcd_word(passes)))
     // (the wide pass: word 32 too, one pass's grid)
     size_t sz = passes > 1 ? sizeof(w) : 32 * sizeof(uint32_t);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, w, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks * (wide ? 1 : passes), 1, 1, 256, 1, 1, 0, st,
+    return hipModuleLaunchKernel(cache.fn[idx], (uint32_t)blocks * launch_passes, 1, 1, 256, 1, 1, 0, st,
                                  nullptr, cfg);
 }
 

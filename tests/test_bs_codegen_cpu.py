@@ -1472,3 +1472,70 @@ def test_pm_xcd_word_divides_exactly():
         assert w & 7 == P
         M = w >> 3
         assert all((h * M) >> 16 == h // P and h * M < 1 << 32 for h in range(1 << 15))
+
+
+@pytest.mark.parametrize("L,G,P16,offs", [(1200, 5, 3, False), (4100, 3, 4, True), (100, 9, 4, False),
+                                          (33, 6, 3, False), (2000, 7, 2, False)])
+def test_emulated_combine_bs_pm24(L, G, P16, offs):
+    """The 24-output pass-major payload pass with jump-table products
+    (qf_combine_bs_r24_pm_j3): pass p' takes outputs 24 p' .. 24 p' + 23 from
+    the 16-output record passes' bytes (three 8-byte pieces, a piece in an
+    unwritten record pass redirected: its outputs lie past e_max); every
+    generation's e outputs equal the 16-output passes' products, rows past e
+    untouched."""
+    global _GFT
+    if _GFT is None:
+        _GFT = _gf_table()
+    rng = np.random.default_rng(L + 3 * G + P16)
+    spec = bs.KernelSpec(0, bs.CMB_WIDE_R, mode="cmb", pass_major=True, cmb_lean=True, cmb_jump=3)
+    assert spec.next_free_vgpr <= 256
+    e_max = 16 * P16
+    P24 = -(-e_max // 24)
+    Lp = (L + 15) // 16 * 16
+    rs, drs = Lp + 32, Lp + 48
+    nslot = e_max + 4
+    rgs, dgs = nslot * rs + 16, 24 * P24 * drs + 32
+    cgs = (nslot + 1) * 16
+    PS = G * cgs + 64
+    rows = rng.integers(0, 256, G * rgs, dtype=np.uint8)
+    rec = rng.integers(0, 256, P16 * PS, dtype=np.uint8)      # exactly the record passes written
+    e = rng.integers(0, e_max + 1, G).astype(np.uint32)
+    bound = rng.integers(1, nslot + 1, G).astype(np.uint32)
+    e[0] = e_max
+    if G > 2:
+        e[1], e[2] = 24, 25
+    out = np.full(G * dgs, 0xEE, np.uint8)
+    ROWS, OUT, REC, NO, BD, TAB, T1, T2 = (0x10000000, 0x40000000, 0x50000000, 0x60000000, 0x61000000,
+                                           0x62000000, 0x63000000, 0x64000000)
+    emu = bs.Emulator(bs.generate(spec))
+    so = do = 0
+    rgs_k, dgs_k = rgs, dgs
+    if offs:
+        emu.add_buffer(T1, np.array([(G - 1 - g) * rgs for g in range(G)], np.uint64).view(np.uint8))
+        emu.add_buffer(T2, np.array([(G - 1 - g) * dgs for g in range(G)], np.uint64).view(np.uint8))
+        so, do, rgs_k, dgs_k = T1, T2, 0, 0
+    for base, buf in ((ROWS, rows), (OUT, out), (REC, rec), (NO, e), (BD, bound),
+                      (TAB, bs.cmb_index_table().reshape(-1).view(np.uint8))):
+        emu.add_buffer(base, buf.view(np.uint8))
+    n = 2
+    ka, _ = bs.cmb_kernargs(ROWS, OUT, rgs_k, dgs_k, rs, drs, REC, cgs, 0, NO, BD, TAB, L, G, 4 * n,
+                            rows_offs=so, dst_offs=do, pass_stride=PS)
+    ka = ka[:-4] + np.uint32(P16).tobytes()                 # word 33: the record passes written
+    for wg in range(P24 * n):
+        for w in range(4):
+            emu.run_wave(ka, wg, w)
+    for g in range(G):
+        gr = (G - 1 - g) if offs else g
+        blk = out[gr * dgs:(gr + 1) * dgs]
+        for j in range(24 * P24):
+            row = blk[j * drs:(j + 1) * drs]
+            if j < e[g]:
+                p, jj = divmod(j, 16)
+                want = np.zeros(L, np.uint8)
+                for sl in range(int(bound[g])):
+                    c = rec[p * PS + g * cgs + 16 * sl + jj]
+                    want ^= _GFT[c][rows[gr * rgs + sl * rs: gr * rgs + sl * rs + L]]
+                assert (row[:L] == want).all(), (g, j)
+                assert (row[L:] == 0xEE).all(), (g, j)
+            else:
+                assert (row == 0xEE).all(), (g, j)

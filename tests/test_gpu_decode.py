@@ -587,6 +587,26 @@ def test_decode_combine_jump_xcd(qf, oracle, gpu_ctx, k, r, L, G, erase, path, j
     check(oracle, k, L, src, gens, out, False)
 
 
+@pytest.mark.parametrize("pm24", [1, 0])
+@pytest.mark.parametrize("path", ["default_1wave", "general_bs"])
+@pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 5, None), (196, 59, 4100, 6, 39), (160, 48, 4100, 7, 40),
+                                           (128, 39, 2100, 9, 36), (100, 64, 3000, 5, None), (80, 40, 2500, 6, 33)])
+def test_decode_combine_pm24(qf, oracle, gpu_ctx, k, r, L, G, erase, path, pm24, monkeypatch):
+    """A payload pass of 33-64 outputs (e_max) as 24-output passes in one
+    launch (qf_combine_bs_r24_pm_j3, QF_OPT_COMBINE_PM24 = 1; the last pass's
+    pieces past the written records redirected) or as 16-output passes (0):
+    bit-exact either way, random or fixed erasure counts, C5 and general
+    paths, rows that end mid-unit."""
+    _path(monkeypatch, path)
+    qf.set_default_options(combine_pm24=pm24)
+    rng = np.random.default_rng(k * 13 + r + L + (erase or 0))
+    kw = {"erase": erase, "shuffle": False} if erase is not None else {}
+    max_rows = k + r
+    src, gens = make_batch(oracle, rng, k, r, L, G, max_rows, **kw)
+    out = run_decode(qf, k, r, L, G, max_rows, gens, False)
+    check(oracle, k, L, src, gens, out, False)
+
+
 @pytest.mark.parametrize("shared", [1, 0])
 @pytest.mark.parametrize("k,r,L,G,erase", [(196, 59, 9000, 6, None), (196, 59, 9000, 6, 3), (160, 48, 4100, 9, 40),
                                            (128, 39, 2100, 12, None), (128, 20, 9000, 6, None), (128, 20, 2100, 9, 20)])
