@@ -189,9 +189,9 @@ enum {
                                     with a call into c's code block (8 destination-indexed 3-input
                                     XORs); 0: M0-indexed XORs, one index write per XOR
                                     [QF_COMBINE_JUMP; default 1] */
-    QF_OPT_COMBINE_PM24,         /* 1: with QF_COMBINE_JUMP, a payload pass of 33-72 outputs (e_max) runs
-                                    as 24-output passes in one launch (2 or 3 passes instead of 3 or 4
-                                    16-output ones: the syndrome rows read and transposed once less);
+    QF_OPT_COMBINE_PM24,         /* 1: with QF_COMBINE_JUMP, a payload pass of 49-64 outputs (e_max) runs
+                                    as 3 24-output passes in one launch instead of 4 16-output ones
+                                    (the syndrome rows read and transposed once less);
                                     0: 16-output passes [QF_COMBINE_PM24; default 1] */
     QF_OPT_COUNT
 };

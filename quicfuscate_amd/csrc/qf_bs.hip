@@ -385,11 +385,13 @@ static const QfBsEntry* cmb_pick(BsCache& cache, char plain, char jump, uint32_t
 }
 
 // the 24-output pass-major launch ('W', jump products, QF_COMBINE_PM24) for
-// 3-4 record passes (e_max 33-64): ceil(e_max / 24) passes, the records'
-// pass stride plus one piece (8 B) in 32 bits
+// 4 record passes (e_max 49-64): 3 passes of 24 instead of 4 of 16, the
+// records' pass stride plus one piece (8 B) in 32 bits.  At e_max 33-48 the
+// generations' own e usually needs two passes either way, and there the
+// 24-output form measured 2-3 % slower (DESIGN 3.7 "Round 6")
 static bool cmb_pm24_ok(BsCache& cache, const CombineSlotsArgs& a, uint32_t passes, uint64_t pass_stride,
                         uint32_t e_max) {
-    return passes >= 3 && passes <= kCmbMaxPasses && e_max > 32 && e_max <= 72 && a.pass == 0 &&
+    return passes == 4 && passes <= kCmbMaxPasses && e_max > 48 && e_max <= 64 && a.pass == 0 &&
            pass_stride + 8 < (1ull << 32) && 72ull * a.dst_row_stride < (1ull << 32) &&
            cache.get(QF_OPT_COMBINE_JUMP) && cache.get(QF_OPT_COMBINE_PM24) && find('W', 0, 24) != nullptr;
 }
