@@ -193,6 +193,10 @@ enum {
                                     as 3 24-output passes in one launch instead of 4 16-output ones
                                     (the syndrome rows read and transposed once less);
                                     0: 16-output passes [QF_COMBINE_PM24; default 1] */
+    QF_OPT_SLIDING_KERNELS,      /* 1: an encode batch whose generations overlap (generation stride
+                                    below k row strides: sliding windows) runs the shape's sliding-window
+                                    kernel where one is built (cached row loads; (48, 8) as the hybrid
+                                    FFT pass); 0: the block kernels [QF_SLIDING_KERNELS; default 1] */
     QF_OPT_COUNT
 };
 int qf_ctx_set_option(qf_ctx *ctx, int option, int64_t value);

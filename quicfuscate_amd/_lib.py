@@ -198,7 +198,7 @@ OPTIONS = {n: i for i, n in enumerate([
     "combine_bs_min_q", "combine_split", "prepare_grid", "enc_blocks_per_cu", "dec_blocks_per_cu", "send_fused",
     "send_windows_min_tiles", "send_chunks", "send_profile", "copy_threads", "gf16_dyn", "gf16_logify",
     "gf16_logify_min_blocks", "gf16_lds_gj", "gf16_bitsliced", "gf16_fft", "wiedemann_proj", "gf16_fft_bs", "prepare_lanes", "encode_merged",
-    "synw_shared", "combine_wide", "combine_xcd", "combine_jump", "combine_pm24"])}
+    "synw_shared", "combine_wide", "combine_xcd", "combine_jump", "combine_pm24", "sliding_kernels"])}
 QF_OPT_COUNT = len(OPTIONS)
 
 

@@ -451,6 +451,9 @@ class KernelSpec:
     # block; 2 = 16 VOP2 xors; 0 = M0-indexed sources (an s_set_gpr_idx_idx per
     # XOR). 6 SALU per product instead of 16 + the index-row load
     cmb_jump: int = 0
+    # enc: the library's sliding-window variant of a shape ('g', chosen when a
+    # batch's generations overlap): "_sl" appended to the name
+    sliding: bool = False
     # VALU list scheduling (bs_sched.schedule): runs of plain VALU ops between
     # non-VALU ops reordered so a producer sits >= sched ops before its
     # consumers where the run allows it (0: program order)
@@ -608,9 +611,10 @@ class KernelSpec:
             tag = "decs" if self.ksplit > 1 else ("decx" if self.cx else "decc")
         if self.fft:
             tag += f"f{self.fft}" + (f"l{self.lds_rows}" if self.lds_rows else "")
+        sl = "_sl" if self.sliding else ""
         if self.rt != self.r or self.j0:
-            return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}"
-        return f"qf_cauchy_{tag}_k{self.k}_r{self.r}"
+            return f"qf_cauchy_{tag}_k{self.k}_r{self.rt}_j{self.j0}{sl}"
+        return f"qf_cauchy_{tag}_k{self.k}_r{self.r}{sl}"
 
     @property
     def nbuf(self) -> int:

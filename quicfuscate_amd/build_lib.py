@@ -53,6 +53,8 @@ BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_SYNW_SHARED = [(128, 20), (128, 39), (160, 48), (196, 59)]
 BS_XCHG_EARLY = 3     # rows of the next group a shared-row wave loads before its transform
 BS_FFT_DEC_HYBRID = [(96, 15), (48, 8)]   # fused FFT decode ('C') of C5 shapes with k not a power of two
+BS_SLIDING_PLAIN = [(32, 5), (16, 1)]   # sliding-window encoders ('g'): plain pass, cached row loads
+BS_SLIDING_FFT = [(48, 8)]              # ... hybrid FFT pass, cached row loads
 BS_FFT_ENC_HYBRID = [(96, 15)]   # hybrid-plan FFT encode ('E'): sliding windows +35 %, block equal
 BS_FFT_CH = 8
 BS_FFT_DEC_PD = 2
@@ -218,6 +220,15 @@ def kernel_specs() -> list:
     # block 4,862-4,868 against 4,994-5,007, sliding 1,273 against 1,179-1,223,
     # a wash, so it stays plain; profiles/r05bk_c5_hybrid_encode.json)
     specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="") for (k, r) in BS_FFT_ENC_HYBRID]
+    # sliding windows ('g', QF_SLIDING_KERNELS: chosen when the generations of a
+    # batch overlap, generation stride < k row strides): consecutive windows
+    # share k - 1 rows, so the row loads keep the default cache policy (the
+    # block encoders' non-temporal loads drop the rows the next window reads),
+    # and (48, 8) takes the hybrid FFT pass that was a wash for block encode
+    # but not for windows (1,273 against 1,179-1,223 GiB/s, round 5)
+    specs += [bs.KernelSpec(k, r, BS_PD, "enc", ld_policy="", sliding=True) for (k, r) in BS_SLIDING_PLAIN]
+    specs += [bs.KernelSpec(k, r, BS_PD, "enc", fft=BS_FFT_CH, ld_policy="", sliding=True)
+              for (k, r) in BS_SLIDING_FFT]
     # additive-FFT fused decode ('C'): pd 2 (the ring holds a chunk + pd rows)
     # (default cache policy: neighbouring 1,200-B rows share their boundary
     # lines, and non-temporal loads / stores drop them before the reuse;
@@ -375,6 +386,8 @@ def _bs_kernels(build_dir: Path) -> Path:
                 mode = ("Z" if spec.passes[0].xchg else "Y") if spec.fft else "X"
             else:
                 mode = "N" if spec.fft else "M"
+        elif getattr(spec, "sliding", False):
+            mode = "g"
         elif spec.chunked:
             mode = "C" if spec.fft else "k" if spec.ksplit > 1 else "c"
         elif spec.fft:

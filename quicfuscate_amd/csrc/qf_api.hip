@@ -215,6 +215,7 @@ const OptDef kOpts[QF_OPT_COUNT] = {
     /* COMBINE_XCD */ {"QF_COMBINE_XCD", 0, 0, 1, false},
     /* COMBINE_JUMP */ {"QF_COMBINE_JUMP", 1, 0, 1, false},
     /* COMBINE_PM24 */ {"QF_COMBINE_PM24", 1, 0, 1, false},
+    /* SLIDING_KERNELS */ {"QF_SLIDING_KERNELS", 1, 0, 1, false},
 };
 
 int64_t clamp_opt(int o, int64_t v) { return std::min(kOpts[o].hi, std::max(kOpts[o].lo, v)); }

@@ -263,6 +263,13 @@ hipError_t bs_launch(BsCache& cache, int num_cus, hipStream_t st, uint32_t k, ui
         else if (cache.get(QF_OPT_ENCODE_MERGED) && fft && find('N', k, r)) mode = 'N';
         else if (cache.get(QF_OPT_ENCODE_MERGED) && find('M', k, r)) mode = 'M';
         else if (fft && find('E', k, r)) mode = 'E';
+        // overlapping generations (sliding windows: generation stride below k
+        // row strides) take the shape's 'g' kernel where one is built
+        // (QF_SLIDING_KERNELS): cached row loads, since the next windows read
+        // the same rows, and for (48, 8) the hybrid FFT pass
+        if (mode != 'f' && cache.get(QF_OPT_SLIDING_KERNELS) && !src_offs && sgs < (uint64_t)k * srs &&
+            find('g', k, r))
+            mode = 'g';
     }
     // one launch per pass of repairs (codes with more repairs than a kernel
     // holds): pass j0 writes repair rows j0 .. j0 + r_pass - 1

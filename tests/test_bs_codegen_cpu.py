@@ -1539,3 +1539,40 @@ def test_emulated_combine_bs_pm24(L, G, P16, offs):
                 assert (row[L:] == 0xEE).all(), (g, j)
             else:
                 assert (row == 0xEE).all(), (g, j)
+
+
+@pytest.mark.parametrize("L,G,zero_tail", [(320, 7, True), (1201, 4, True), (96, 9, False)])
+def test_emulated_sliding_window_encoders(oracle, L, G, zero_tail):
+    """The library's sliding-window encoders ('g', build_lib BS_SLIDING_*:
+    cached row loads, (48, 8) as the hybrid FFT pass) on overlapping windows,
+    generation stride = row stride (window g = rows g .. g + k - 1), every
+    window's repairs equal the oracle's encode of its rows."""
+    from quicfuscate_amd.build_lib import kernel_specs
+    specs = [s for s in kernel_specs() if getattr(s, "sliding", False)]
+    assert {(s.k, s.r) for s in specs} >= {(32, 5), (48, 8), (16, 1)}
+    for spec in specs:
+        k, r = spec.k, spec.r
+        Lv = bs.padded_units(L) if zero_tail else None
+        rng = np.random.default_rng(k + L + G)
+        srs = (L + 15) // 16 * 16 + 16
+        drs = 16 * (Lv or L // 16) + 128
+        dgs = r * drs
+        src = rng.integers(0, 256, (G + k - 1) * srs + 64, dtype=np.uint8)
+        dst = np.full(G * dgs, 0xEE, np.uint8)
+        emu = bs.Emulator(bs.generate(spec))
+        emu.add_buffer(0x10000000, src)
+        emu.add_buffer(0x40000000, dst)
+        _, _, items = bs.launch_geometry(L, G, Lv)
+        waves = (items + 3) // 4
+        ka = bs.kernargs(0x10000000, 0x40000000, srs, dgs, srs, drs, L, G, waves * 4, Lv=Lv, zero_tail=zero_tail)
+        for wg in range(waves):
+            for w in range(4):
+                emu.run_wave(ka, wg, w)
+        for g in range(G):
+            rows = np.stack([src[(g + i) * srs: (g + i) * srs + L] for i in range(k)])
+            want = oracle.encode(rows, r)
+            for j in range(r):
+                off = g * dgs + j * drs
+                assert (dst[off: off + L] == want[j]).all(), (spec.name, g, j)
+                tail = 16 * Lv if zero_tail else L
+                assert (dst[off + L: off + tail] == 0).all(), spec.name

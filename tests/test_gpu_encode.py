@@ -380,3 +380,37 @@ def test_c5_shared_row_encode_odd_lengths(qf, oracle, gpu_ctx, k, r, L):
             assert (out[off: off + L] == want[j]).all(), (g, j)
             assert (out[off + L: off + tail] == 0).all(), (g, j)
             assert (out[off + tail: off + rrs] == 0xA5).all(), (g, j)
+
+
+@pytest.mark.parametrize("sliding", [1, 0])
+@pytest.mark.parametrize("k,r,L", [(32, 5, 9000), (48, 8, 9000), (16, 1, 1200), (48, 8, 1200), (32, 5, 1201)])
+def test_encode_sliding_kernels(qf, oracle, gpu_ctx, k, r, L, sliding):
+    """Overlapping generations (adaptive.rs:519-562: a window per source
+    packet, generation stride = row stride) through the shapes' sliding-window
+    kernels (QF_OPT_SLIDING_KERNELS = 1: cached row loads, (48, 8) as the
+    hybrid FFT pass) or the block kernels (0): every checked window equals the
+    oracle's encode of its k rows, and the batch equals the block layout's
+    encode of the same windows."""
+    import torch
+
+    qf.set_default_options(sliding_kernels=sliding)
+    RS = (L + 15) // 16 * 16 + 16
+    drs = (L + 127) // 128 * 128 + 128
+    G = 300
+    gen = torch.Generator(device="cuda").manual_seed(k * 7 + L)
+    src = torch.randint(0, 256, ((G + k - 1) * RS,), dtype=torch.uint8, device="cuda", generator=gen)
+    rep = torch.full((G * r * drs,), 0xA5, dtype=torch.uint8, device="cuda")
+    qf.encode_batch(src, rep, k, r, L, src_row_stride=RS, src_gen_stride=RS, rep_row_stride=drs,
+                    rep_gen_stride=r * drs, G=G, zero_tail=True, ctx=gpu_ctx)
+    wins = [0, 1, 77, G - 1]
+    blk = torch.stack([src.view(-1, RS)[g:g + k] for g in wins]).reshape(-1)
+    rb = torch.full((len(wins) * r * drs,), 0x5A, dtype=torch.uint8, device="cuda")
+    qf.encode_batch(blk, rb, k, r, L, src_row_stride=RS, src_gen_stride=k * RS, rep_row_stride=drs,
+                    rep_gen_stride=r * drs, G=len(wins), zero_tail=True, ctx=gpu_ctx)
+    gpu_ctx.sync()
+    got = rep.view(G, r, drs)
+    assert torch.equal(got[wins], rb.view(len(wins), r, drs))
+    s = src.cpu().numpy()
+    for g in wins:
+        rows = s[g * RS:(g + k) * RS].reshape(k, RS)[:, :L]
+        assert (got[g, :, :L].cpu().numpy() == oracle.encode(rows, r)).all(), g
