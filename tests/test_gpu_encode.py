@@ -404,7 +404,7 @@ def test_encode_sliding_kernels(qf, oracle, gpu_ctx, k, r, L, sliding):
                     rep_gen_stride=r * drs, G=G, zero_tail=True, ctx=gpu_ctx)
     wins = [0, 1, 77, G - 1]
     blk = torch.stack([src.view(-1, RS)[g:g + k] for g in wins]).reshape(-1)
-    rb = torch.full((len(wins) * r * drs,), 0x5A, dtype=torch.uint8, device="cuda")
+    rb = torch.full((len(wins) * r * drs,), 0xA5, dtype=torch.uint8, device="cuda")   # same fill: bytes past the tail untouched
     qf.encode_batch(blk, rb, k, r, L, src_row_stride=RS, src_gen_stride=k * RS, rep_row_stride=drs,
                     rep_gen_stride=r * drs, G=len(wins), zero_tail=True, ctx=gpu_ctx)
     gpu_ctx.sync()
