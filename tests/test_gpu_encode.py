@@ -408,9 +408,12 @@ def test_encode_sliding_kernels(qf, oracle, gpu_ctx, k, r, L, sliding):
     qf.encode_batch(blk, rb, k, r, L, src_row_stride=RS, src_gen_stride=k * RS, rep_row_stride=drs,
                     rep_gen_stride=r * drs, G=len(wins), zero_tail=True, ctx=gpu_ctx)
     gpu_ctx.sync()
-    got = rep.view(G, r, drs)
-    assert torch.equal(got[wins], rb.view(len(wins), r, drs))
+    got = rep.view(G, r, drs).cpu().numpy()
+    blk_rep = rb.view(len(wins), r, drs).cpu().numpy()
     s = src.cpu().numpy()
-    for g in wins:
+    for n, g in enumerate(wins):
         rows = s[g * RS:(g + k) * RS].reshape(k, RS)[:, :L]
-        assert (got[g, :, :L].cpu().numpy() == oracle.encode(rows, r)).all(), g
+        want = oracle.encode(rows, r)
+        ok_s, ok_b = bool((got[g, :, :L] == want).all()), bool((blk_rep[n, :, :L] == want).all())
+        assert ok_s and ok_b, (g, "sliding batch == oracle", ok_s, "block batch == oracle", ok_b)
+    assert (got[wins] == blk_rep).all()   # tails and untouched bytes too
