@@ -22,7 +22,7 @@
 struct QfBsEntry {
     uint32_t k, r, pd;
     uint32_t rt, j0;  // enc passes: repairs j0 .. j0 + r - 1 of the (k, rt) code
-    char mode;  // 'e' encode, 'E' additive-FFT encode, 'C' additive-FFT chunked decode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
+    char mode;  // 'e' encode, 'E' additive-FFT encode, 'g' sliding-window encode, 'C' additive-FFT chunked decode, 's' decode syndromes, 'w' syndromes (scalar slot map), 'd'/'c' fused decode,
                 // 'k' the chunked fused decode with an item's rows split over its workgroup's 4 waves,
                 // 'f' the encode (passes of C5 codes) with an item's sources split the same way,
                 // 'M' / 'N' every encode pass of a code in one dispatch (plain / additive-FFT passes),
@@ -137,7 +137,9 @@ static hipError_t launch(BsCache& cache, const QfBsEntry* e, int num_cus, hipStr
     // the last unit stores it bytewise); never the item-layout decode ('d')
     const bool chunked = e->mode == 'c' || e->mode == 'k' || e->mode == 'C';
     const bool merged = e->mode == 'M' || e->mode == 'N' || e->mode == 'Z';
-    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E' || e->mode == 'M' || e->mode == 'N';
+    // (every encoder letter: the kernarg words 16..19 are its tail byte masks)
+    const bool enc = e->mode == 'e' || e->mode == 'f' || e->mode == 'E' || e->mode == 'M' || e->mode == 'N' ||
+                     e->mode == 'g';
     if ((L % 16 && (e->mode == 'd' || (enc && Lv != s19))) || L < 32 ||
         sgs >= (1ull << 32) || dgs >= (1ull << 32) ||
         srs >= (1ull << 32) || drs >= (1ull << 32))
