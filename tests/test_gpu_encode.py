@@ -383,7 +383,8 @@ def test_c5_shared_row_encode_odd_lengths(qf, oracle, gpu_ctx, k, r, L):
 
 
 @pytest.mark.parametrize("sliding", [1, 0])
-@pytest.mark.parametrize("k,r,L", [(32, 5, 9000), (48, 8, 9000), (16, 1, 1200), (48, 8, 1200), (32, 5, 1201)])
+@pytest.mark.parametrize("k,r,L", [(32, 5, 9000), (48, 8, 9000), (16, 1, 1200), (48, 8, 1200), (32, 5, 1201),
+                                   (64, 10, 9000), (96, 15, 9000), (128, 20, 9000), (64, 10, 1201)])
 def test_encode_sliding_kernels(qf, oracle, gpu_ctx, k, r, L, sliding):
     """Overlapping generations (adaptive.rs:519-562: a window per source
     packet, generation stride = row stride) through the shapes' sliding-window
