@@ -53,7 +53,7 @@ BS_FFT_SYNW = [(128, 39), (160, 48)]
 BS_FFT_SYNW_SHARED = [(128, 20), (128, 39), (160, 48), (196, 59)]
 BS_XCHG_EARLY = 3     # rows of the next group a shared-row wave loads before its transform
 BS_FFT_DEC_HYBRID = [(96, 15), (48, 8)]   # fused FFT decode ('C') of C5 shapes with k not a power of two
-BS_SLIDING_PLAIN = [(32, 5), (16, 1), (64, 10), (96, 15), (128, 20)]   # sliding-window encoders ('g'): plain pass, cached row loads
+BS_SLIDING_PLAIN = [(32, 5), (16, 1)]   # sliding-window encoders ('g'): plain pass, cached row loads
 BS_SLIDING_FFT = [(48, 8)]              # ... hybrid FFT pass, cached row loads
 BS_FFT_ENC_HYBRID = [(96, 15)]   # hybrid-plan FFT encode ('E'): sliding windows +35 %, block equal
 BS_FFT_CH = 8
